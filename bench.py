@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Headline benchmark: AROW classifier training throughput (samples/s) +
+p50/p99 classify latency on MI355X, 1..N GPUs (one rank per GPU, RCCL MIX).
+
+Metric/config: BASELINE.json - "samples/sec (train) + p50 classify latency,
+AROW classifier at 1/2/4/8 MI355X", config/classifier/arow.json
+(AROW, regularization_weight 1.0, converter str bin/bin + num).
+
+One timed step on every rank =
+  * R concurrent ``train`` request bodies (msgpack list<labeled_datum>, as
+    received by the RPC layer) of S samples each: native scan + label
+    resolution + pinned staging (host), H2D, GPU msgpack parse + feature
+    hashing (fv_hash kernel), GPU AROW update (R lock-free update streams,
+    each exact-sequential) - i.e. the complete train path minus the socket;
+  * one MIX: label-set agreement + RCCL all-reduce mean of W and S
+    (hash_max_size x labels x 2 tables, fp32) over xGMI (N > 1).
+Per-GPU work is fixed as N grows (weak scaling). Data: synthetic datums
+(8 string + 8 numeric features, 16 labels), random-init (zero) model.
+
+Usage: python bench.py --gpus N --steps K --warmup W
+       (N > 1: launched by torch.distributed.run, one process per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+import time
+
+import msgpack
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+AROW_CONFIG = {
+    "converter": {
+        "string_filter_types": {}, "string_filter_rules": [],
+        "num_filter_types": {}, "num_filter_rules": [],
+        "string_types": {},
+        "string_rules": [{"key": "*", "type": "str", "sample_weight": "bin",
+                          "global_weight": "bin"}],
+        "num_types": {},
+        "num_rules": [{"key": "*", "type": "num"}],
+    },
+    "parameter": {"regularization_weight": 1.0},
+    "method": "AROW",
+}
+
+
+def make_requests(rng: random.Random, nreq: int, per_req: int, nlabels: int, n_str: int,
+                  n_num: int, vocab: int) -> list[bytes]:
+    """Synthetic, label-correlated datums, msgpack-encoded per request."""
+    bodies = []
+    for _ in range(nreq):
+        items = []
+        for _ in range(per_req):
+            y = rng.randrange(nlabels)
+            sv = []
+            for j in range(n_str):
+                tok = (y * 131 + rng.randrange(16)) if rng.random() < 0.6 else rng.randrange(vocab)
+                sv.append([f"s{j}", f"t{tok}"])
+            nv = [[f"n{j}", (y - nlabels / 2) * 0.05 + rng.gauss(0.0, 1.0)] for j in range(n_num)]
+            items.append([f"label{y}", [sv, nv, []]])
+        bodies.append(msgpack.packb(items, use_bin_type=False))
+    return bodies
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--requests", type=int, default=1024, help="concurrent train requests per step per GPU")
+    ap.add_argument("--per-request", type=int, default=128, help="samples per train request")
+    ap.add_argument("--labels", type=int, default=16)
+    ap.add_argument("--str-features", type=int, default=8)
+    ap.add_argument("--num-features", type=int, default=8)
+    ap.add_argument("--vocab", type=int, default=100000)
+    ap.add_argument("--hash-bits", type=int, default=20)
+    ap.add_argument("--pools", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--mix-every", type=int, default=1)
+    ap.add_argument("--latency-iters", type=int, default=300)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    cfg = json.loads(json.dumps(AROW_CONFIG))
+    cfg["converter"]["hash_max_size"] = 1 << args.hash_bits
+    conv = DatumToFvConverter(cfg["converter"])
+    clf = LinearClassifier(cfg["method"], cfg["parameter"], conv, device=device)
+    for y in range(args.labels):  # same label order on every rank (set_label, as a client would)
+        clf.set_label(f"label{y}")
+
+    rng = random.Random(1234 + rank)
+    pools = [make_requests(rng, args.requests, args.per_request, args.labels, args.str_features,
+                           args.num_features, args.vocab) for _ in range(args.pools)]
+    samples_per_step = args.requests * args.per_request
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def step(i: int) -> None:
+        n = clf.train_requests(pools[i % len(pools)])
+        assert n == samples_per_step
+        if world > 1 and (i + 1) % args.mix_every == 0:
+            clf.mix()
+
+    for i in range(args.warmup):
+        step(i)
+    clf.pipe.check_errors()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    clf.pipe.check_errors()
+
+    # accuracy on a held-out synthetic request (sanity: the model learns)
+    test = make_requests(random.Random(99), 1, 2048, args.labels, args.str_features,
+                         args.num_features, args.vocab)[0]
+    items = msgpack.unpackb(test, raw=False)
+    res = clf.classify_requests([msgpack.packb([d for _, d in items], use_bin_type=False)])
+    acc = float(np.mean([max(r, key=lambda t: t[1])[0] == lab for r, (lab, _) in zip(res, items)]))
+
+    # classify latency: one datum per request, full round trip incl. D2H
+    one = msgpack.packb([items[0][1]], use_bin_type=False)
+    lat = []
+    for i in range(args.latency_iters + 20):
+        t1 = time.perf_counter()
+        clf.classify_requests([one])
+        dt = time.perf_counter() - t1
+        if i >= 20:
+            lat.append(dt * 1e6)
+    lat.sort()
+    p50 = statistics.median(lat)
+    p99 = lat[min(len(lat) - 1, int(0.99 * len(lat)))]
+
+    total = samples_per_step * args.steps * world
+    value = total / elapsed
+    if rank == 0:
+        out = {
+            "metric": "train_samples_per_sec",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (label-correlated datums, 8 str + 8 num features), random-init model",
+            "config": {
+                "model": "jubaclassifier AROW (config/classifier/arow.json: regularization_weight 1.0, "
+                         "str bin/bin + num)",
+                "global_batch": samples_per_step * world,
+                "seq_len": None,
+                "parallelism": f"dp{world}",
+                "requests_per_step_per_gpu": args.requests,
+                "samples_per_request": args.per_request,
+                "hash_max_size": 1 << args.hash_bits,
+                "labels": args.labels,
+                "mix": "linear (RCCL all-reduce mean) every step" if world > 1 else "standalone",
+            },
+            "classify_latency_us_p50": round(p50, 1),
+            "classify_latency_us_p99": round(p99, 1),
+            "heldout_accuracy": round(acc, 4),
+            "baseline_note": "reference publishes no numbers (BASELINE.md)",
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+"""In-tree build of the native components.
+
+* ``jubatus_amd/_jubatus_native*.so`` - host C++17 runtime (pybind11):
+  request scanner, label table, hashing, CRC32, MD5, msgpack codec, RPC core.
+* ``jubatus_amd/libjubatus_hip.so`` - every HIP kernel, compiled for gfx950
+  only (``hipcc --offload-arch=gfx950``), exported through a C ABI and
+  loaded with ctypes (jubatus_amd/ops/hip.py).
+
+Both are built in-tree so they travel with the repository snapshot to the
+GPU box. Incremental: a target is rebuilt only if a source is newer.
+
+Usage: ``python -m jubatus_amd.build_ext [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "csrc", "build")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+
+NATIVE_SO = os.path.join(PKG, "_jubatus_native" + sysconfig.get_config_var("EXT_SUFFIX"))
+HIP_SO = os.path.join(PKG, "libjubatus_hip.so")
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout)
+        raise RuntimeError(f"build failed: {cmd[0]} (exit {r.returncode})")
+
+
+def _compile_all(jobs: list[tuple[str, list[str]]], nproc: int) -> None:
+    with cf.ThreadPoolExecutor(max_workers=max(1, nproc)) as ex:
+        futs = [ex.submit(_run, cmd) for _, cmd in jobs]
+        for f in futs:
+            f.result()
+
+
+def build_native(force: bool = False, nproc: int = 8) -> str:
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(CSRC, "native", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "native", "*.hpp")))
+    if not force and not _newer(NATIVE_SO, srcs + hdrs):
+        return NATIVE_SO
+    os.makedirs(BUILD, exist_ok=True)
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}",
+           f"-I{os.path.join(CSRC, 'native')}"]
+    flags = ["-O3", "-std=c++17", "-fPIC", "-pthread", "-fvisibility=hidden", "-Wall",
+             "-Wno-unused-function"]
+    objs, jobs = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, "native_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            jobs.append((o, ["g++", *flags, *inc, "-c", s, "-o", o]))
+    _compile_all(jobs, nproc)
+    _run(["g++", "-shared", "-pthread", "-o", NATIVE_SO, *objs, "-ldl"])
+    return NATIVE_SO
+
+
+def build_hip(force: bool = False, nproc: int = 8) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hip")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "hip", "*.hpp")))
+    if not force and not _newer(HIP_SO, srcs + hdrs):
+        return HIP_SO
+    os.makedirs(BUILD, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
+             f"-I{os.path.join(CSRC, 'hip')}"]
+    objs, jobs = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, "hip_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + hdrs):
+            jobs.append((o, [HIPCC, *flags, "-c", s, "-o", o]))
+    _compile_all(jobs, nproc)
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", HIP_SO, *objs])
+    return HIP_SO
+
+
+def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, str]:
+    nproc = nproc or min(8, os.cpu_count() or 4)
+    return build_native(force, nproc), build_hip(force, nproc)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    a = ap.parse_args()
+    for p in build_all(a.force, a.j):
+        print(p)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+// Python bindings of the host-native runtime (_jubatus_native).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "jb_hash.hpp"
+#include "jb_pack.hpp"
+
+namespace py = pybind11;
+
+namespace {
+
+py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* table,
+               uintptr_t staging, uint64_t staging_cap, uintptr_t datum_off, uintptr_t labels,
+               uintptr_t row_ptr, uintptr_t stream_ptr, int64_t max_samples, int nthreads) {
+  std::vector<jb::RequestView> views;
+  std::vector<py::buffer_info> keep;
+  views.reserve(reqs.size());
+  keep.reserve(reqs.size());
+  for (auto item : reqs) {
+    py::buffer b = py::reinterpret_borrow<py::buffer>(item);
+    keep.emplace_back(b.request());
+    const py::buffer_info& bi = keep.back();
+    views.push_back({(const uint8_t*)bi.ptr, (uint64_t)(bi.size * bi.itemsize)});
+  }
+  jb::PackOut out{(uint8_t*)staging, staging_cap, (int64_t*)datum_off, (int32_t*)labels,
+                  (int64_t*)row_ptr, (int64_t*)stream_ptr, max_samples};
+  jb::PackResult r;
+  {
+    py::gil_scoped_release nogil;
+    r = jb::pack_requests(views, labeled, sps, spn, table, out, nthreads);
+  }
+  return py::make_tuple(r.n_samples, r.n_bytes, r.n_slots, r.error, r.error_request);
+}
+
+uint32_t crc32(py::buffer b, uint32_t init) {
+  py::buffer_info bi = b.request();
+  return jb::crc32_update(init, (const uint8_t*)bi.ptr, (size_t)(bi.size * bi.itemsize));
+}
+
+std::string md5_hex(const std::string& s) { return jb::Md5::hex(s); }
+
+int64_t feature_index(py::bytes name, uint64_t H) {
+  std::string s = name;
+  return jb::hash_to_index(jb::fnv_bytes(jb::kFnvOffset, (const uint8_t*)s.data(), s.size()), H);
+}
+
+uint64_t fnv1a64(py::bytes name) {
+  std::string s = name;
+  return jb::fnv_bytes(jb::kFnvOffset, (const uint8_t*)s.data(), s.size());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_jubatus_native, m) {
+  m.doc() = "jubatus_amd host-native runtime: request scanning, hashing, CRC32, MD5";
+  py::class_<jb::LabelTable>(m, "LabelTable")
+      .def(py::init<>())
+      .def("get_or_add", [](jb::LabelTable& t, const std::string& s) { return t.get_or_add(s.data(), s.size()); })
+      .def("lookup", &jb::LabelTable::lookup)
+      .def("remove", &jb::LabelTable::remove)
+      .def("clear", &jb::LabelTable::clear)
+      .def("size", &jb::LabelTable::size)
+      .def("names", &jb::LabelTable::names)
+      .def("alive", &jb::LabelTable::alive)
+      .def("version", &jb::LabelTable::version)
+      .def("count", &jb::LabelTable::count)
+      .def("set_count", &jb::LabelTable::set_count)
+      .def("add_count", &jb::LabelTable::add_count);
+  m.def("pack_requests", &pack, "scan msgpack request bodies into a device-ready batch");
+  m.def("crc32", &crc32, py::arg("data"), py::arg("init") = 0u);
+  m.def("md5_hex", &md5_hex);
+  m.def("feature_index", &feature_index);
+  m.def("fnv1a64", &fnv1a64);
+}

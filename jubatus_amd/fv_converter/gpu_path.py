@@ -1,0 +1,70 @@
+"""GPU fv_converter fast path (host half).
+
+Decides whether a converter config can run entirely in
+csrc/hip/fv_hash.hip and packs its rules into the device rule table.
+
+Eligible configs (the common ones: config/classifier/*.json, anomaly,
+clustering, nearest_neighbor defaults): no filters, no binary or combination
+rules; every string rule is of built-in type ``str`` with sample weight
+bin/tf/log_tf and global weight ``bin``; every num rule is ``num`` or
+``log``; key matchers are ``*``, prefix, suffix or exact (regex needs the
+host path).
+"""
+from __future__ import annotations
+
+import math
+import struct
+
+import numpy as np
+
+from .converter import DatumToFvConverter
+
+_RULE = struct.Struct("<iiiiiifi")  # mirrors jb::GpuRule
+_KIND = {"all": 0, "prefix": 1, "suffix": 2, "exact": 3}
+
+
+def gpu_eligible(conv: DatumToFvConverter) -> bool:
+    if conv.string_filters or conv.num_filters or conv.binary_rules or conv.combination_rules:
+        return False
+    for r in conv.string_rules:
+        if r.type_name != "str" or r.splitter is not None or r.gw != "bin":
+            return False
+        if r.matcher.kind not in _KIND:
+            return False
+    for r in conv.num_rules:
+        if r.type_name not in ("num", "log") or r.matcher.kind not in _KIND:
+            return False
+    return True
+
+
+class GpuRuleTable:
+    """Packed rule tables: (string rules, num rules, byte blob)."""
+
+    def __init__(self, conv: DatumToFvConverter):
+        if not gpu_eligible(conv):
+            raise ValueError("converter config is not eligible for the GPU fast path")
+        blob = bytearray()
+
+        def put(b: bytes) -> tuple[int, int]:
+            off = len(blob)
+            blob.extend(b)
+            return off, len(b)
+
+        srows = []
+        for r in conv.string_rules:
+            mo, ml = put(r.matcher.arg.encode())
+            so, sl = put(r.suffix.encode())
+            w = {"bin": 1.0, "tf": 1.0, "log_tf": math.log(2.0)}[r.sw]
+            srows.append(_RULE.pack(_KIND[r.matcher.kind], mo, ml, so, sl, 0, w, 0))
+        nrows = []
+        for r in conv.num_rules:
+            mo, ml = put(r.matcher.arg.encode())
+            so, sl = put(f"@{r.type_name}".encode())
+            nrows.append(_RULE.pack(_KIND[r.matcher.kind], mo, ml, so, sl,
+                                    1 if r.type_name == "log" else 0, 0.0, 0))
+        self.n_srules = len(srows)
+        self.n_nrules = len(nrows)
+        self.srules = np.frombuffer(b"".join(srows) or b"\0" * _RULE.size, dtype=np.uint8).copy()
+        self.nrules = np.frombuffer(b"".join(nrows) or b"\0" * _RULE.size, dtype=np.uint8).copy()
+        self.blob = np.frombuffer(bytes(blob) or b"\0", dtype=np.uint8).copy()
+        self.H = conv.hash_max_size

@@ -1,0 +1,404 @@
+"""Linear online classifier driver (perceptron, PA, PA1, PA2, CW, AROW, NHERD).
+
+Reference surface: jubatus/server/server/classifier_serv.cpp:91-225 (train,
+classify, get_labels, set_label, delete_label, clear) on top of jubatus_core's
+linear classifiers (EXTERNAL).
+
+Model: hashed tables W[H][LC] (+ S[H][LC] for CW/AROW/NHERD, init 1.0) with
+H = converter ``hash_max_size`` and LC = label capacity (power of two, grown
+on demand). On a GPU the tables live in HBM and every update/score runs in
+csrc/hip/linear.hip; without a GPU the NumPy oracle (linear_oracle.py) runs
+the same semantics on the host.
+
+Update semantics: a request's samples are applied in order (exact online
+learning). Several requests submitted together (``train_requests``) run as
+concurrent lock-free streams, like concurrent train RPCs on the reference's
+giant-lock-free classifier (ChangeLog.rst:152).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Any, Sequence
+
+import msgpack
+import numpy as np
+
+from .._native import native
+from ..fv_converter.converter import DatumToFvConverter
+from ..fv_converter.datum import as_datum
+from . import linear_oracle as lo
+
+LINEAR_METHODS = ("perceptron", "PA", "PA1", "PA2", "CW", "AROW", "NHERD")
+LABEL_CAPS = (8, 16, 32, 64, 128, 256, 512, 1024)
+
+
+class ClassifierConfigError(ValueError):
+    pass
+
+
+def _pack_body(items: Sequence[Any]) -> bytes:
+    return msgpack.packb(items, use_bin_type=False)
+
+
+def _label_cap(n: int) -> int:
+    for c in LABEL_CAPS:
+        if c >= n:
+            return c
+    raise ClassifierConfigError(f"at most {LABEL_CAPS[-1]} labels are supported")
+
+
+class LinearClassifier:
+    def __init__(self, method: str, parameter: dict | None, converter: DatumToFvConverter,
+                 device: Any = None):
+        if method not in LINEAR_METHODS:
+            raise ClassifierConfigError(f"unknown linear method: {method}")
+        parameter = dict(parameter or {})
+        self.method = method
+        self.mid = lo.METHOD_IDS[method]
+        if method != "perceptron" and method != "PA":
+            if "regularization_weight" not in parameter:
+                raise ClassifierConfigError("parameter.regularization_weight is required")
+        self.C = float(parameter.get("regularization_weight", 1.0))
+        if method not in ("perceptron", "PA") and not self.C > 0:
+            raise ClassifierConfigError("regularization_weight must be positive")
+        self.conv = converter
+        self.H = converter.hash_max_size
+        self.use_s = self.mid in lo.USES_COVARIANCE
+        self.labels = native().LabelTable()
+        self._lock = threading.RLock()
+        self.device = device
+        self.gpu = device is not None
+        self.LC = 0
+        self._label_version = -1
+        if self.gpu:
+            import torch
+            from ..ops.feature_pipeline import FeaturePipeline
+            self.torch = torch
+            self.pipe = FeaturePipeline(converter, device)
+        self._alloc(LABEL_CAPS[0])
+
+    # ------------------------------------------------------------ storage
+    def _alloc(self, LC: int) -> None:
+        H = self.H
+        if self.gpu:
+            t = self.torch
+            W = t.zeros((H, LC), dtype=t.float32, device=self.device)
+            S = t.ones((H, LC), dtype=t.float32, device=self.device) if self.use_s else None
+            if self.LC:
+                W[:, :self.LC].copy_(self.W)
+                if S is not None:
+                    S[:, :self.LC].copy_(self.S)
+            self.W, self.S = W, S
+            self.active = t.zeros(LC, dtype=t.int32, device=self.device)
+        else:
+            W = np.zeros((H, LC), dtype=np.float32)
+            S = np.ones((H, LC), dtype=np.float32) if self.use_s else None
+            if self.LC:
+                W[:, :self.LC] = self.W
+                if S is not None:
+                    S[:, :self.LC] = self.S
+            self.W, self.S = W, S
+            self.active = np.zeros(LC, dtype=np.int32)
+        self.LC = LC
+        self._label_version = -1
+
+    def _sync_labels(self) -> None:
+        """grow the tables and refresh the active-column mask after label changes"""
+        v = self.labels.version()
+        if v == self._label_version:
+            return
+        n = self.labels.size()
+        if n > self.LC:
+            self._alloc(_label_cap(n))
+        alive = self.labels.alive()
+        mask = np.zeros(self.LC, dtype=np.int32)
+        mask[:len(alive)] = np.asarray(alive, dtype=np.int32)
+        if self.gpu:
+            self.active.copy_(self.torch.from_numpy(mask))
+        else:
+            self.active[:] = mask
+        self._label_version = v
+
+    # -------------------------------------------------------------- train
+    def train_requests(self, bodies: Sequence[Any]) -> int:
+        """Train on raw msgpack ``list<labeled_datum>`` bodies (one stream each)."""
+        with self._lock:
+            if self.gpu and self.pipe.fast:
+                from ..ops import hip
+                b = self.pipe.from_requests(list(bodies), True, self.labels)
+                self._sync_labels()
+                if b.n:
+                    hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr,
+                                     b.nstreams, self.W, self.S, self.active, self.mid, self.C,
+                                     concurrent=b.nstreams > 1)
+                return b.n
+            total = 0
+            streams = [msgpack.unpackb(bytes(x), raw=False) for x in bodies]
+            rows, labs, sizes = [], [], []
+            for items in streams:
+                for lab, d in items:
+                    idx, val = self.conv.hashed(self.conv.convert_and_update_weight(as_datum(d)))
+                    rows.append((idx, val))
+                    labs.append(self.labels.get_or_add(_s(lab)))
+                    self.labels.add_count(labs[-1], 1)
+                sizes.append(len(items))
+                total += len(items)
+            self._train_rows(rows, labs, sizes)
+            return total
+
+    def train(self, data: Sequence[tuple[str, Any]]) -> int:
+        data = list(data)
+        if not data:
+            return 0
+        if self.gpu and self.pipe.fast:
+            body = _pack_body([[lab, as_datum(d).to_msgpack()] for lab, d in data])
+            return self.train_requests([body])
+        with self._lock:
+            rows, labs = [], []
+            for lab, d in data:
+                rows.append(self.conv.hashed(self.conv.convert_and_update_weight(as_datum(d))))
+                labs.append(self.labels.get_or_add(_s(lab)))
+                self.labels.add_count(labs[-1], 1)
+            self._train_rows(rows, labs, [len(rows)])
+        return len(data)
+
+    def _train_rows(self, rows, labs, sizes) -> None:
+        self._sync_labels()
+        if self.gpu:
+            from ..ops import hip
+            b = self.pipe.from_rows(rows, labs, sizes)
+            hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
+                             self.W, self.S, self.active, self.mid, self.C,
+                             concurrent=b.nstreams > 1)
+            return
+        for (idx, val), y in zip(rows, labs):
+            lo.train_one(self.W, self.S, np.asarray(idx, np.int64), np.asarray(val, np.float32),
+                         y, self.active, self.mid, self.C)
+
+    # ----------------------------------------------------------- classify
+    def _results(self, scores: np.ndarray) -> list[list[tuple[str, float]]]:
+        names = self.labels.names()
+        alive = self.labels.alive()
+        cols = [i for i, a in enumerate(alive) if a]
+        return [[(names[c], float(row[c])) for c in cols] for row in scores]
+
+    def classify_requests(self, bodies: Sequence[Any]) -> list[list[tuple[str, float]]]:
+        with self._lock:
+            if self.gpu and self.pipe.fast:
+                from ..ops import hip
+                b = self.pipe.from_requests(list(bodies), False, None)
+                self._sync_labels()
+                if b.n == 0:
+                    return []
+                out = self.pipe._dev.get("scores", b.n * self.LC, self.torch.float32)
+                hip.linear_classify(b.row_ptr, b.fidx, b.fval, b.n, self.W, out)
+                scores = out[:b.n * self.LC].view(b.n, self.LC).cpu().numpy()
+                return self._results(scores)
+        ds = [d for x in bodies for d in msgpack.unpackb(bytes(x), raw=False)]
+        return self.classify(ds)
+
+    def classify(self, data: Sequence[Any]) -> list[list[tuple[str, float]]]:
+        data = list(data)
+        if not data:
+            return []
+        if self.gpu and self.pipe.fast:
+            return self.classify_requests([_pack_body([as_datum(d).to_msgpack() for d in data])])
+        rows = [self.conv.hashed(self.conv.convert(as_datum(d))) for d in data]
+        with self._lock:
+            self._sync_labels()
+            if self.gpu:
+                from ..ops import hip
+                b = self.pipe.from_rows(rows, None)
+                out = self.torch.empty(b.n * self.LC, dtype=self.torch.float32, device=self.device)
+                hip.linear_classify(b.row_ptr, b.fidx, b.fval, b.n, self.W, out)
+                scores = out.view(b.n, self.LC).cpu().numpy()
+            else:
+                scores = np.stack([lo.scores(self.W, np.asarray(i, np.int64),
+                                             np.asarray(v, np.float32)) for i, v in rows])
+        return self._results(scores)
+
+    # ------------------------------------------------------------- labels
+    def get_labels(self) -> dict[str, int]:
+        names = self.labels.names()
+        alive = self.labels.alive()
+        return {n: int(self.labels.count(i)) for i, n in enumerate(names) if alive[i]}
+
+    def set_label(self, label: str) -> bool:
+        with self._lock:
+            if self.labels.lookup(label) >= 0:
+                return False
+            self.labels.get_or_add(label)
+            self._sync_labels()
+            return True
+
+    def delete_label(self, label: str) -> bool:
+        with self._lock:
+            i = self.labels.lookup(label)
+            if i < 0:
+                return False
+            self.labels.remove(label)
+            self.W[:, i] = 0.0
+            if self.S is not None:
+                self.S[:, i] = 1.0
+            self._sync_labels()
+            return True
+
+    def clear(self) -> None:
+        with self._lock:
+            self.labels.clear()
+            self.LC = 0
+            self._alloc(LABEL_CAPS[0])
+            self.conv.weights.clear()
+
+    # ------------------------------------------------------------ persist
+    def synchronize(self) -> None:
+        if self.gpu:
+            self.torch.cuda.synchronize(self.device)
+
+    def _host_tables(self) -> tuple[np.ndarray, np.ndarray | None]:
+        if self.gpu:
+            W = self.W.cpu().numpy()
+            S = self.S.cpu().numpy() if self.S is not None else None
+            return W, S
+        return self.W, self.S
+
+    def pack(self) -> dict:
+        """Model payload (user_data of the model file).
+
+        Sparse: only feature rows that differ from the initial state are
+        stored, as (row indices, W rows, S rows) over the live label columns.
+        """
+        with self._lock:
+            self.synchronize()
+            W, S = self._host_tables()
+            names = self.labels.names()
+            alive = self.labels.alive()
+            cols = [i for i, a in enumerate(alive) if a]
+            Wc = W[:, cols]
+            touched = np.any(Wc != 0.0, axis=1)
+            if S is not None:
+                Sc = S[:, cols]
+                touched |= np.any(Sc != 1.0, axis=1)
+            rows = np.nonzero(touched)[0].astype(np.int64)
+            out = {
+                "method": self.method, "H": self.H,
+                "labels": [names[c] for c in cols],
+                "counts": [int(self.labels.count(c)) for c in cols],
+                "rows": rows.tobytes(),
+                "W": np.ascontiguousarray(Wc[rows]).astype(np.float32).tobytes(),
+                "S": (np.ascontiguousarray(S[:, cols][rows]).astype(np.float32).tobytes()
+                      if S is not None else b""),
+                "weights": self.conv.weights.pack(),
+            }
+            return out
+
+    def unpack(self, obj: dict) -> None:
+        obj = {(k.decode() if isinstance(k, bytes) else k): v for k, v in obj.items()}
+        with self._lock:
+            if int(obj["H"]) != self.H:
+                raise ValueError("model hash_max_size differs from the configuration")
+            labels = [(x.decode() if isinstance(x, bytes) else x) for x in obj["labels"]]
+            self.labels.clear()
+            self.LC = 0
+            self._alloc(_label_cap(max(1, len(labels))))
+            for i, (name, cnt) in enumerate(zip(labels, obj["counts"])):
+                self.labels.get_or_add(name)
+                self.labels.set_count(i, int(cnt))
+            self._sync_labels()
+            rows = np.frombuffer(obj["rows"], dtype=np.int64)
+            L = len(labels)
+            Wr = np.frombuffer(obj["W"], dtype=np.float32).reshape(len(rows), L)
+            W = np.zeros((self.H, self.LC), dtype=np.float32)
+            W[rows, :L] = Wr
+            S = None
+            if self.use_s:
+                S = np.ones((self.H, self.LC), dtype=np.float32)
+                if len(obj["S"]):
+                    S[rows, :L] = np.frombuffer(obj["S"], dtype=np.float32).reshape(len(rows), L)
+            if self.gpu:
+                self.W.copy_(self.torch.from_numpy(W))
+                if S is not None:
+                    self.S.copy_(self.torch.from_numpy(S))
+            else:
+                self.W, self.S = W, S
+            if obj.get("weights"):
+                self.conv.weights.unpack(obj["weights"])
+
+    # ----------------------------------------------------------------- MIX
+    def _live_labels(self) -> list[str]:
+        names, alive = self.labels.names(), self.labels.alive()
+        return [n for n, a in zip(names, alive) if a]
+
+    def _reorder_labels(self, order: list[str]) -> None:
+        """Re-lay the label columns in ``order`` (labels missing locally get
+        fresh columns)."""
+        old = {n: i for i, n in enumerate(self.labels.names()) if self.labels.lookup(n) == i}
+        counts = {n: int(self.labels.count(i)) for n, i in old.items()}
+        LC = _label_cap(max(1, len(order)))
+        if self.gpu:
+            t = self.torch
+            perm = t.tensor([old.get(n, -1) for n in order], dtype=t.int64, device=self.device)
+            have = perm >= 0
+            W = t.zeros((self.H, LC), dtype=t.float32, device=self.device)
+            S = t.ones((self.H, LC), dtype=t.float32, device=self.device) if self.use_s else None
+            src = perm.clamp(min=0)
+            W[:, :len(order)] = t.where(have, self.W.index_select(1, src), W[:, :len(order)])
+            if S is not None:
+                S[:, :len(order)] = t.where(have, self.S.index_select(1, src), S[:, :len(order)])
+        else:
+            W = np.zeros((self.H, LC), dtype=np.float32)
+            S = np.ones((self.H, LC), dtype=np.float32) if self.use_s else None
+            for c, n in enumerate(order):
+                if n in old:
+                    W[:, c] = self.W[:, old[n]]
+                    if S is not None:
+                        S[:, c] = self.S[:, old[n]]
+        self.labels.clear()
+        for c, n in enumerate(order):
+            self.labels.get_or_add(n)
+            self.labels.set_count(c, counts.get(n, 0))
+        self.W, self.S, self.LC = W, S, LC
+        self.active = (self.torch.zeros(LC, dtype=self.torch.int32, device=self.device)
+                       if self.gpu else np.zeros(LC, dtype=np.int32))
+        self._label_version = -1
+        self._sync_labels()
+
+    def mix(self, group=None) -> int:
+        """Collective model averaging across the ranks of ``group`` (RCCL).
+        Returns the number of bytes all-reduced per rank."""
+        from ..parallel import collective as coll
+        with self._lock:
+            names = self.labels.names()
+            alive = self.labels.alive()
+            fp = coll.fingerprint([n + ("+" if a else "-") for n, a in zip(names, alive)])
+            if not coll.all_equal(fp, self.device if self.gpu else None, group):
+                lists = coll.all_gather_object(self._live_labels(), group)
+                order: list[str] = []
+                seen = set()
+                for lst in lists:
+                    for n in lst:
+                        if n not in seen:
+                            seen.add(n)
+                            order.append(n)
+                self._reorder_labels(order)
+            tables = [self.W] + ([self.S] if self.S is not None else [])
+            if self.gpu:
+                coll.allreduce_mean_(tables, group)
+                nbytes = sum(t.numel() * 4 for t in tables)
+            else:
+                import torch
+                ts = [torch.from_numpy(t) for t in tables]
+                coll.allreduce_mean_(ts, group)
+                nbytes = sum(t.nbytes for t in tables)
+            return nbytes
+
+    def get_status(self) -> dict[str, str]:
+        st = {"num_classes": str(len(self.get_labels())), "num_features": str(self.H),
+              "label_capacity": str(self.LC), "method": self.method,
+              "storage": "hbm" if self.gpu else "host",
+              "fv_path": "gpu" if (self.gpu and self.pipe.fast) else "host"}
+        return st
+
+
+def _s(x: Any) -> str:
+    return x.decode() if isinstance(x, (bytes, bytearray)) else str(x)

@@ -1,0 +1,185 @@
+"""Host -> HBM feature pipeline.
+
+Turns train/classify request bodies into device CSR batches:
+
+* fast path (config eligible, see fv_converter/gpu_path.py): the native
+  scanner validates the msgpack bodies, resolves labels and copies the raw
+  bytes into a pinned staging buffer (multi-threaded over requests); one
+  async H2D copy moves bytes + descriptors; ``fv_hash`` parses and hashes on
+  the GPU into CSR (row_ptr, idx, val).
+* host path (any other config): the host converter produces feature names,
+  which are hashed on the host and shipped as CSR.
+
+Pinned staging sets are double-buffered: the scan of batch k+1 fills one set
+while the H2D copy of batch k drains the other (an event guards reuse).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .._native import native
+from ..fv_converter.gpu_path import GpuRuleTable, gpu_eligible
+from . import hip
+
+
+def _grow(cap: int, need: int) -> int:
+    c = max(cap, 1)
+    while c < need:
+        c *= 2
+    return c
+
+
+@dataclass
+class DeviceBatch:
+    n: int
+    nnz: int
+    nstreams: int
+    row_ptr: torch.Tensor     # int64 [n+1]
+    fidx: torch.Tensor        # int32 [nnz]
+    fval: torch.Tensor        # float32 [nnz]
+    labels: torch.Tensor | None   # int32 [n]
+    stream_ptr: torch.Tensor  # int64 [nstreams+1]
+
+
+class _Pinned:
+    def __init__(self):
+        self.cap_bytes = 0
+        self.cap_samples = 0
+        self.cap_streams = 0
+        self.staging = self.datum_off = self.labels = self.row_ptr = self.stream_ptr = None
+        self.event: torch.cuda.Event | None = None
+
+    def ensure(self, nbytes: int, nsamples: int, nstreams: int) -> None:
+        if nbytes > self.cap_bytes:
+            self.cap_bytes = _grow(self.cap_bytes or (1 << 16), nbytes)
+            self.staging = torch.empty(self.cap_bytes, dtype=torch.uint8, pin_memory=True)
+        if nsamples > self.cap_samples:
+            self.cap_samples = _grow(self.cap_samples or 1024, nsamples)
+            self.datum_off = torch.empty(self.cap_samples, dtype=torch.int64, pin_memory=True)
+            self.labels = torch.empty(self.cap_samples, dtype=torch.int32, pin_memory=True)
+            self.row_ptr = torch.empty(self.cap_samples + 1, dtype=torch.int64, pin_memory=True)
+        if nstreams + 1 > self.cap_streams:
+            self.cap_streams = _grow(self.cap_streams or 64, nstreams + 1)
+            self.stream_ptr = torch.empty(self.cap_streams, dtype=torch.int64, pin_memory=True)
+
+    def wait(self) -> None:
+        if self.event is not None:
+            self.event.synchronize()
+            self.event = None
+
+
+class _DeviceBufs:
+    def __init__(self, device):
+        self.device = device
+        self.cap = {}
+        self.t = {}
+
+    def get(self, name: str, n: int, dtype) -> torch.Tensor:
+        if self.cap.get(name, -1) < n:
+            c = _grow(self.cap.get(name, 0) or 1024, n)
+            self.t[name] = torch.empty(c, dtype=dtype, device=self.device)
+            self.cap[name] = c
+        return self.t[name]
+
+
+class FeaturePipeline:
+    def __init__(self, converter, device, nthreads: int | None = None):
+        self.conv = converter
+        self.device = torch.device(device)
+        self.H = converter.hash_max_size
+        self.fast = gpu_eligible(converter)
+        self.nthreads = nthreads or max(1, min(16, (os.cpu_count() or 4)))
+        self._pinned = [_Pinned(), _Pinned()]
+        self._turn = 0
+        self._dev = _DeviceBufs(self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if self.fast:
+            rt = GpuRuleTable(converter)
+            self.rules = rt
+            self.d_srules = torch.from_numpy(rt.srules).to(self.device)
+            self.d_nrules = torch.from_numpy(rt.nrules).to(self.device)
+            self.d_blob = torch.from_numpy(rt.blob).to(self.device)
+
+    # ------------------------------------------------------------ fast path
+    def from_requests(self, bodies: list, labeled: bool, table=None) -> DeviceBatch:
+        """bodies: buffer-protocol objects, each a msgpack list<labeled_datum>
+        (labeled) or list<datum>; every body is one update stream."""
+        if not self.fast:
+            raise RuntimeError("converter config is not eligible for the GPU fast path")
+        nat = native()
+        pin = self._pinned[self._turn]
+        self._turn ^= 1
+        pin.wait()
+        R = len(bodies)
+        need_bytes = sum(memoryview(b).nbytes for b in bodies) + 16 * R + 16
+        pin.ensure(need_bytes, max(1024, pin.cap_samples), R)
+        while True:
+            n, nbytes, nslots, err, err_req = nat.pack_requests(
+                bodies, labeled, self.rules.n_srules, self.rules.n_nrules, table,
+                pin.staging.data_ptr(), pin.cap_bytes, pin.datum_off.data_ptr(),
+                pin.labels.data_ptr() if labeled else 0, pin.row_ptr.data_ptr(),
+                pin.stream_ptr.data_ptr(), pin.cap_samples, self.nthreads)
+            if err == 2:
+                pin.ensure(nbytes, n, R)
+                continue
+            if err == 1:
+                raise TypeError(f"malformed datum list in request {err_req}")
+            if err == 3:
+                raise RuntimeError("label table full")
+            break
+        dev = self._dev
+        d_buf = dev.get("buf", max(nbytes, 1), torch.uint8)
+        d_off = dev.get("datum_off", max(n, 1), torch.int64)
+        d_row = dev.get("row_ptr", n + 1, torch.int64)
+        d_sp = dev.get("stream_ptr", R + 1, torch.int64)
+        d_idx = dev.get("fidx", max(nslots, 1), torch.int32)
+        d_val = dev.get("fval", max(nslots, 1), torch.float32)
+        d_buf[:nbytes].copy_(pin.staging[:nbytes], non_blocking=True)
+        d_off[:n].copy_(pin.datum_off[:n], non_blocking=True)
+        d_row[:n + 1].copy_(pin.row_ptr[:n + 1], non_blocking=True)
+        d_sp[:R + 1].copy_(pin.stream_ptr[:R + 1], non_blocking=True)
+        d_lab = None
+        if labeled:
+            d_lab = dev.get("labels", max(n, 1), torch.int32)
+            d_lab[:n].copy_(pin.labels[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        pin.event = ev
+        if n > 0:
+            hip.fv_hash(d_buf, nbytes, d_off, d_row, n, self.d_srules, self.rules.n_srules,
+                        self.d_nrules, self.rules.n_nrules, self.d_blob, self.H, d_idx, d_val,
+                        self.err)
+        return DeviceBatch(n, nslots, R, d_row, d_idx, d_val, d_lab, d_sp)
+
+    # ------------------------------------------------------------ host path
+    def from_rows(self, rows: list[tuple[list[int], list[float]]], labels: list[int] | None,
+                  stream_sizes: list[int] | None = None) -> DeviceBatch:
+        n = len(rows)
+        lens = np.fromiter((len(r[0]) for r in rows), dtype=np.int64, count=n)
+        row_ptr = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=row_ptr[1:])
+        nnz = int(row_ptr[-1])
+        idx = np.fromiter((i for r in rows for i in r[0]), dtype=np.int32, count=nnz)
+        val = np.fromiter((v for r in rows for v in r[1]), dtype=np.float32, count=nnz)
+        sizes = stream_sizes if stream_sizes is not None else [n]
+        sp = np.zeros(len(sizes) + 1, dtype=np.int64)
+        np.cumsum(np.asarray(sizes, dtype=np.int64), out=sp[1:])
+        dev = self.device
+        d_row = torch.from_numpy(row_ptr).to(dev, non_blocking=False)
+        d_idx = torch.from_numpy(idx if nnz else np.zeros(1, np.int32)).to(dev)
+        d_val = torch.from_numpy(val if nnz else np.zeros(1, np.float32)).to(dev)
+        d_lab = None
+        if labels is not None:
+            d_lab = torch.from_numpy(np.asarray(labels, dtype=np.int32).reshape(-1)).to(dev)
+        d_sp = torch.from_numpy(sp).to(dev)
+        return DeviceBatch(n, nnz, len(sizes), d_row, d_idx, d_val, d_lab, d_sp)
+
+    def check_errors(self) -> None:
+        e = int(self.err.item())
+        if e:
+            self.err.zero_()
+            raise RuntimeError(f"GPU datum parser reported error mask {e}")

@@ -1,0 +1,127 @@
+"""ctypes bindings of the HIP kernel library (csrc/hip/*.hip).
+
+Every wrapper takes torch tensors that already live on the current HIP
+device, checks shapes/dtypes on the host (a kernel never sees an operand it
+was not written for), and launches on the current torch stream so kernels
+order naturally with torch ops and RCCL collectives.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .._native import hip_lib
+
+_c_void_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+_f32 = ctypes.c_float
+
+_SIGS = {
+    "jb_fv_hash": [_c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i32,
+                   _c_void_p, _u64, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_linear_train": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
+                        _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p],
+    "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
+                           _c_void_p],
+    "jb_scale": [_c_void_p, _i64, _f32, _c_void_p],
+}
+
+_fns: dict = {}
+
+LABEL_CAPS = (8, 16, 32, 64, 128, 256, 512, 1024)
+METHODS = {"perceptron": 0, "PA": 1, "PA1": 2, "PA2": 3, "CW": 4, "AROW": 5, "NHERD": 6}
+
+
+def _fn(name: str):
+    f = _fns.get(name)
+    if f is None:
+        lib = hip_lib()
+        f = getattr(lib, name)
+        f.argtypes = _SIGS[name]
+        f.restype = ctypes.c_int
+        _fns[name] = f
+    return f
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{name}: HIP launch failed (code {rc})")
+
+
+def _dev(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if not t.is_cuda or t.dtype != dtype or not t.is_contiguous():
+        raise TypeError(f"{name}: expected contiguous {dtype} device tensor, got {t.dtype} "
+                        f"on {t.device}")
+
+
+def fv_hash(buf: torch.Tensor, buf_len: int, datum_off: torch.Tensor, row_ptr: torch.Tensor,
+            n: int, srules: torch.Tensor, n_srules: int, nrules: torch.Tensor, n_nrules: int,
+            blob: torch.Tensor, H: int, out_idx: torch.Tensor, out_val: torch.Tensor,
+            err: torch.Tensor) -> None:
+    _dev(buf, torch.uint8, "buf")
+    _dev(datum_off, torch.int64, "datum_off")
+    _dev(row_ptr, torch.int64, "row_ptr")
+    _dev(out_idx, torch.int32, "out_idx")
+    _dev(out_val, torch.float32, "out_val")
+    if datum_off.numel() < n or row_ptr.numel() < n + 1:
+        raise ValueError("fv_hash: descriptor arrays shorter than n")
+    if buf.numel() < buf_len:
+        raise ValueError("fv_hash: staging buffer shorter than buf_len")
+    rc = _fn("jb_fv_hash")(_p(buf), buf_len, _p(datum_off), _p(row_ptr), n, _p(srules), n_srules,
+                           _p(nrules), n_nrules, _p(blob), H, _p(out_idx), _p(out_val), _p(err),
+                           _stream())
+    _check(rc, "jb_fv_hash")
+
+
+def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
+                 labels: torch.Tensor, stream_ptr: torch.Tensor, nstreams: int, W: torch.Tensor,
+                 S: torch.Tensor | None, active: torch.Tensor, method: int, C: float,
+                 concurrent: bool) -> None:
+    LC = W.shape[1]
+    if LC not in LABEL_CAPS:
+        raise ValueError(f"label capacity {LC} not supported")
+    _dev(W, torch.float32, "W")
+    _dev(active, torch.int32, "active")
+    if active.numel() < LC:
+        raise ValueError("active mask shorter than label capacity")
+    if method >= METHODS["CW"]:
+        if S is None or S.shape != W.shape:
+            raise ValueError("CW/AROW/NHERD need a covariance table shaped like W")
+        _dev(S, torch.float32, "S")
+    if stream_ptr.numel() < nstreams + 1:
+        raise ValueError("stream_ptr shorter than nstreams+1")
+    rc = _fn("jb_linear_train")(_p(row_ptr), _p(fidx), _p(fval), _p(labels), _p(stream_ptr),
+                                nstreams, _p(W), _p(S) if S is not None else None, _p(active), LC,
+                                method, float(C), 1 if concurrent else 0, _stream())
+    _check(rc, "jb_linear_train")
+
+
+def linear_classify(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor, n: int,
+                    W: torch.Tensor, out: torch.Tensor) -> None:
+    LC = W.shape[1]
+    if LC not in LABEL_CAPS:
+        raise ValueError(f"label capacity {LC} not supported")
+    _dev(W, torch.float32, "W")
+    _dev(out, torch.float32, "out")
+    if out.numel() < n * LC or row_ptr.numel() < n + 1:
+        raise ValueError("linear_classify: output / row_ptr too small")
+    rc = _fn("jb_linear_classify")(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), LC, _p(out),
+                                   _stream())
+    _check(rc, "jb_linear_classify")
+
+
+def scale_(t: torch.Tensor, a: float) -> None:
+    _dev(t, torch.float32, "t")
+    rc = _fn("jb_scale")(_p(t), t.numel(), float(a), _stream())
+    _check(rc, "jb_scale")

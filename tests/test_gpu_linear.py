@@ -1,0 +1,146 @@
+"""GPU numerics of the fv_hash and linear classifier kernels vs the host
+reference (fv_converter + linear_oracle, fp32 NumPy)."""
+import random
+
+import msgpack
+import numpy as np
+import pytest
+
+from jubatus_amd.fv_converter.converter import DatumToFvConverter
+from jubatus_amd.models import linear_oracle as lo
+
+pytestmark = pytest.mark.gpu
+
+CONV = {
+    "string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"},
+                     {"key": "s1*", "type": "str", "sample_weight": "log_tf", "global_weight": "bin"}],
+    "num_rules": [{"key": "*", "type": "num"}, {"key": "*1", "type": "log"}],
+    "hash_max_size": 1 << 18,
+}
+
+
+def _data(n, nlabels=5, seed=0):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        y = rng.randrange(nlabels)
+        d = {f"s{j}": f"v{(y * 7 + rng.randrange(4)) if rng.random() < 0.7 else rng.randrange(500)}"
+             for j in range(3)}
+        for j in range(3):
+            d[f"n{j}"] = (y - 2) * 0.5 + rng.gauss(0, 1)
+        d["big"] = rng.randrange(1 << 20)  # integer msgpack encodings
+        d["neg"] = -rng.randrange(200)
+        out.append((f"L{y}", d))
+    return out
+
+
+def _device():
+    import torch
+    return torch.device("cuda", 0)
+
+
+def test_fv_hash_matches_host_converter():
+    import torch
+    from jubatus_amd.fv_converter.datum import Datum
+    from jubatus_amd.ops.feature_pipeline import FeaturePipeline
+
+    conv = DatumToFvConverter(CONV)
+    pipe = FeaturePipeline(conv, _device())
+    data = _data(300)
+    bodies = [msgpack.packb([[l, Datum(d).to_msgpack()] for l, d in data[i:i + 37]],
+                            use_bin_type=False) for i in range(0, len(data), 37)]
+    from jubatus_amd._native import native
+    table = native().LabelTable()
+    b = pipe.from_requests(bodies, True, table)
+    torch.cuda.synchronize()
+    pipe.check_errors()
+    row_ptr = b.row_ptr[:b.n + 1].cpu().numpy()
+    idx = b.fidx[:b.nnz].cpu().numpy()
+    val = b.fval[:b.nnz].cpu().numpy()
+    for s, (lab, d) in enumerate(data):
+        hi, hv = conv.hashed(conv.convert(d))
+        gi = idx[row_ptr[s]:row_ptr[s + 1]]
+        gv = val[row_ptr[s]:row_ptr[s + 1]]
+        m = gi >= 0
+        assert sorted(zip(gi[m].tolist(), np.round(gv[m], 4).tolist())) == \
+            sorted(zip(hi, np.round(np.asarray(hv, np.float32), 4).tolist())), s
+    assert b.labels[:b.n].cpu().tolist() == [table.lookup(l) for l, _ in data]
+
+
+@pytest.mark.parametrize("method", ["perceptron", "PA", "PA1", "PA2", "CW", "AROW", "NHERD"])
+def test_single_stream_train_matches_oracle(method):
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    conv_g = DatumToFvConverter(CONV)
+    conv_c = DatumToFvConverter(CONV)
+    param = {"regularization_weight": 0.7}
+    g = LinearClassifier(method, param, conv_g, device=_device())
+    c = LinearClassifier(method, param, conv_c, device=None)
+    data = _data(400, seed=3)
+    for i in range(0, len(data), 100):
+        g.train(data[i:i + 100])
+        c.train(data[i:i + 100])
+    g.synchronize()
+    Wg = g.W.cpu().numpy()
+    np.testing.assert_allclose(Wg[:, :c.LC], c.W, rtol=2e-3, atol=2e-4)
+    if c.S is not None:
+        np.testing.assert_allclose(g.S.cpu().numpy()[:, :c.LC], c.S, rtol=2e-3, atol=2e-4)
+    q = [d for _, d in data[:64]]
+    rg, rc = g.classify(q), c.classify(q)
+    for a, b in zip(rg, rc):
+        assert [x[0] for x in a] == [x[0] for x in b]
+        np.testing.assert_allclose([x[1] for x in a], [x[1] for x in b], rtol=2e-3, atol=2e-3)
+    assert g.get_labels() == c.get_labels()
+
+
+def test_many_labels_capacity_growth():
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    conv_g, conv_c = DatumToFvConverter(CONV), DatumToFvConverter(CONV)
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, conv_g, device=_device())
+    c = LinearClassifier("AROW", {"regularization_weight": 1.0}, conv_c)
+    data = _data(300, nlabels=150, seed=5)
+    g.train(data)
+    c.train(data)
+    g.synchronize()
+    assert g.LC == 256
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=3e-3, atol=3e-4)
+
+
+def test_concurrent_streams_learn():
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    conv = DatumToFvConverter(CONV)
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, conv, device=_device())
+    data = _data(4096, seed=7)
+    from jubatus_amd.fv_converter.datum import Datum
+    bodies = [msgpack.packb([[l, Datum(d).to_msgpack()] for l, d in data[i:i + 32]],
+                            use_bin_type=False) for i in range(0, len(data), 32)]
+    assert g.train_requests(bodies) == len(data)
+    test = _data(500, seed=8)
+    res = g.classify([d for _, d in test])
+    acc = np.mean([max(r, key=lambda t: t[1])[0] == l for r, (l, _) in zip(res, test)])
+    assert acc > 0.8, acc
+    g.pipe.check_errors()
+
+
+def test_delete_label_and_pack_roundtrip():
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    g = LinearClassifier("PA1", {"regularization_weight": 1.0}, DatumToFvConverter(CONV),
+                         device=_device())
+    data = _data(200, seed=9)
+    g.train(data)
+    assert g.delete_label("L0")
+    assert "L0" not in g.get_labels()
+    res = g.classify([data[0][1]])
+    assert all(l != "L0" for l, _ in res[0])
+    blob = g.pack()
+    h = LinearClassifier("PA1", {"regularization_weight": 1.0}, DatumToFvConverter(CONV),
+                         device=_device())
+    h.unpack(blob)
+    a, b = g.classify([d for _, d in data[:20]]), h.classify([d for _, d in data[:20]])
+    for x, y in zip(a, b):
+        assert dict(x).keys() == dict(y).keys()
+        for k in dict(x):
+            assert abs(dict(x)[k] - dict(y)[k]) < 1e-4
