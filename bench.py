@@ -109,9 +109,20 @@ def main() -> None:
     for y in range(args.labels):  # same label order on every rank (set_label, as a client would)
         clf.set_label(f"label{y}")
 
+    from jubatus_amd.ops.feature_pipeline import RequestArena
+
     rng = random.Random(1234 + rank)
-    pools = [make_requests(rng, args.requests, args.per_request, args.labels, args.str_features,
-                           args.num_features, args.vocab) for _ in range(args.pools)]
+    pools = []
+    for _ in range(args.pools):
+        bodies = make_requests(rng, args.requests, args.per_request, args.labels,
+                               args.str_features, args.num_features, args.vocab)
+        # the synthetic client "sends" the step's requests into a pinned
+        # receive arena, as the RPC reader does for real connections
+        arena = RequestArena(sum(len(b) for b in bodies) + 16 * len(bodies) + 64)
+        for b in bodies:
+            arena.append(b)
+        offs, lens = arena.spans()
+        pools.append((arena, offs, lens))
     samples_per_step = args.requests * args.per_request
 
     def barrier():
@@ -119,7 +130,8 @@ def main() -> None:
             dist.barrier()
 
     def step(i: int) -> None:
-        n = clf.train_requests(pools[i % len(pools)])
+        arena, offs, lens = pools[i % len(pools)]
+        n = clf.train_arena(arena, offs, lens)
         assert n == samples_per_step
         if world > 1 and (i + 1) % args.mix_every == 0:
             clf.mix()

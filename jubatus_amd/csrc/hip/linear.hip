@@ -10,9 +10,15 @@
 // jubatus_amd/models/linear_oracle.py, which is the numerical oracle for this
 // file.
 //
-// Storage: W[H][LC] and S[H][LC] (fp32), LC = label capacity (power of two).
-// One feature row of W is LC*4 contiguous bytes, so the score gather of one
-// feature is one coalesced segment.
+// Storage: W[H][LC] and P[H][LC] (fp32), LC = label capacity (power of two).
+// P is the diagonal *precision* 1/S of the confidence methods (init 1). Every
+// covariance update of CW/AROW/NHERD is an additive precision update
+//     CW:         P += beta x^2
+//     AROW/NHERD: P += beta x^2 / (1 - beta s x^2)   (s = 1/P)
+// which is algebraically the reference form S -= beta S^2 x^2 but stays
+// positive and commutes, so concurrent streams can apply it with float
+// atomics. One feature row of W is LC*4 contiguous bytes, so the score gather
+// of one feature is one coalesced segment.
 //
 // Execution model (MI355X): one wave64 owns one *stream* (a contiguous run of
 // samples that must be applied in order, e.g. one train RPC). Inside a sample
@@ -124,8 +130,8 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
           nrm += x * x;
           float a = 1.f, b = 1.f;
           if (use_s) {
-            a = ld_agent(S + row + y);
-            b = lstar >= 0 ? ld_agent(S + row + lstar) : 0.f;
+            a = 1.f / ld_agent(S + row + y);
+            b = lstar >= 0 ? 1.f / ld_agent(S + row + lstar) : 0.f;
             var += x * x * (a + b);
           }
           if (base == 0) {
@@ -190,22 +196,24 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
           idx = fidx[beg + j]; x = fval[beg + j];
           if (idx < 0) continue;
           const int64_t row = (int64_t)idx * LC;
-          a = use_s ? ld_agent(S + row + y) : 1.f;
-          b = (use_s && lstar >= 0) ? ld_agent(S + row + lstar) : 1.f;
+          a = use_s ? 1.f / ld_agent(S + row + y) : 1.f;
+          b = (use_s && lstar >= 0) ? 1.f / ld_agent(S + row + lstar) : 1.f;
           if (!CONC) { wy = ld_agent(W + row + y); wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f; }
         }
         if (idx < 0) continue;
         const int64_t row = (int64_t)idx * LC;
         const float dwy = use_s ? tau * a * x : tau * x;
         const float dwl = use_s ? -tau * b * x : -tau * x;
+        // precision increments (see header)
         float dsy = 0.f, dsl = 0.f;
         if (use_s) {
+          const float bx2 = beta * x * x;
           if (method == CW) {
-            dsy = 1.f / (1.f / a + beta * x * x) - a;
-            dsl = 1.f / (1.f / b + beta * x * x) - b;
+            dsy = bx2;
+            dsl = bx2;
           } else {
-            dsy = -beta * a * a * x * x;
-            dsl = -beta * b * b * x * x;
+            dsy = bx2 / (1.f - bx2 * a);
+            dsl = bx2 / (1.f - bx2 * b);
           }
         }
         if (CONC) {
@@ -219,8 +227,8 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
           W[row + y] = wy + dwy;
           if (lstar >= 0) W[row + lstar] = wl + dwl;
           if (use_s) {
-            S[row + y] = a + dsy;
-            if (lstar >= 0) S[row + lstar] = b + dsl;
+            S[row + y] = 1.f / a + dsy;
+            if (lstar >= 0) S[row + lstar] = 1.f / b + dsl;
           }
         }
       }

@@ -22,7 +22,27 @@ py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* ta
     const py::buffer_info& bi = keep.back();
     views.push_back({(const uint8_t*)bi.ptr, (uint64_t)(bi.size * bi.itemsize)});
   }
-  jb::PackOut out{(uint8_t*)staging, staging_cap, (int64_t*)datum_off, (int32_t*)labels,
+  jb::PackOut out{(uint8_t*)staging, nullptr, staging_cap, (int64_t*)datum_off, (int32_t*)labels,
+                  (int64_t*)row_ptr, (int64_t*)stream_ptr, max_samples};
+  jb::PackResult r;
+  {
+    py::gil_scoped_release nogil;
+    r = jb::pack_requests(views, labeled, sps, spn, table, out, nthreads);
+  }
+  return py::make_tuple(r.n_samples, r.n_bytes, r.n_slots, r.error, r.error_request);
+}
+
+// zero-copy variant: requests are spans [offs[k], offs[k]+lens[k]) of one
+// pinned arena at `base` (e.g. the RPC receive arena); nothing is copied.
+py::tuple pack_spans(uintptr_t base, uintptr_t offs, uintptr_t lens, int64_t nreq, bool labeled,
+                     int sps, int spn, jb::LabelTable* table, uintptr_t datum_off,
+                     uintptr_t labels, uintptr_t row_ptr, uintptr_t stream_ptr,
+                     int64_t max_samples, int nthreads) {
+  std::vector<jb::RequestView> views((size_t)nreq);
+  const int64_t* o = (const int64_t*)offs;
+  const int64_t* l = (const int64_t*)lens;
+  for (int64_t k = 0; k < nreq; ++k) views[k] = {(const uint8_t*)base + o[k], (uint64_t)l[k]};
+  jb::PackOut out{nullptr, (const uint8_t*)base, 0, (int64_t*)datum_off, (int32_t*)labels,
                   (int64_t*)row_ptr, (int64_t*)stream_ptr, max_samples};
   jb::PackResult r;
   {
@@ -67,6 +87,7 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("set_count", &jb::LabelTable::set_count)
       .def("add_count", &jb::LabelTable::add_count);
   m.def("pack_requests", &pack, "scan msgpack request bodies into a device-ready batch");
+  m.def("pack_spans", &pack_spans, "zero-copy scan of request spans inside one pinned arena");
   m.def("crc32", &crc32, py::arg("data"), py::arg("init") = 0u);
   m.def("md5_hex", &md5_hex);
   m.def("feature_index", &feature_index);

@@ -3,6 +3,8 @@
 
 #include <string.h>
 
+#include "jb_hash.hpp"
+
 #include <algorithm>
 #include <string>
 #include <thread>
@@ -20,28 +22,60 @@ struct ReqScan {
   bool table_full = false;
 };
 
-void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelTable* table,
-              std::unordered_map<std::string, int>* cache, ReqScan* out) {
+// Per-thread label cache: open addressing on FNV-1a of the label bytes,
+// verified by a byte compare (labels are few and repeat on every sample).
+class LabelCache {
+ public:
+  explicit LabelCache(LabelTable* t) : table_(t), slots_(256) {}
+  int get(const uint8_t* s, uint32_t n) {
+    const uint64_t h = fnv_bytes(kFnvOffset, s, n);
+    size_t mask = slots_.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      Slot& sl = slots_[i];
+      if (sl.id < 0) {
+        int id = table_->get_or_add((const char*)s, n);
+        if (id < 0) return -1;
+        sl.h = h; sl.key.assign((const char*)s, n); sl.id = id;
+        if (++used_ * 2 > slots_.size()) rehash();
+        return id;
+      }
+      if (sl.h == h && sl.key.size() == n && memcmp(sl.key.data(), s, n) == 0) return sl.id;
+    }
+  }
+
+ private:
+  struct Slot { uint64_t h = 0; std::string key; int id = -1; };
+  void rehash() {
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.resize(old.size() * 2);
+    size_t mask = slots_.size() - 1;
+    for (auto& o : old) {
+      if (o.id < 0) continue;
+      size_t i = o.h & mask;
+      while (slots_[i].id >= 0) i = (i + 1) & mask;
+      slots_[i] = std::move(o);
+    }
+  }
+  LabelTable* table_;
+  std::vector<Slot> slots_;
+  size_t used_ = 0;
+};
+
+void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelCache* cache,
+              ReqScan* out) {
   Cursor c{r.data, r.data + r.len};
   uint32_t n;
   if (!c.array(&n)) { out->ok = false; return; }
   out->off.reserve(n);
   out->slots.reserve(n);
   if (labeled) out->label.reserve(n);
-  std::string key;
   for (uint32_t i = 0; i < n; ++i) {
     if (labeled) {
       uint32_t two; const uint8_t* ls; uint32_t ln;
       if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { out->ok = false; return; }
-      key.assign((const char*)ls, ln);
-      auto it = cache->find(key);
-      int id;
-      if (it != cache->end()) id = it->second;
-      else {
-        id = table->get_or_add(key.data(), key.size());
-        if (id < 0) { out->table_full = true; out->ok = false; return; }
-        cache->emplace(key, id);
-      }
+      int id = cache->get(ls, ln);
+      if (id < 0) { out->table_full = true; out->ok = false; return; }
       out->label.push_back(id);
     }
     uint64_t doff = (uint64_t)(c.p - r.data);
@@ -63,8 +97,8 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
   if ((size_t)nthreads > R) nthreads = (int)std::max<size_t>(R, 1);
 
   auto worker = [&](int t) {
-    std::unordered_map<std::string, int> cache;  // per-thread label cache
-    for (size_t k = t; k < R; k += nthreads) scan_one(reqs[k], labeled, sps, spn, table, &cache, &scans[k]);
+    LabelCache cache(table);
+    for (size_t k = t; k < R; k += nthreads) scan_one(reqs[k], labeled, sps, spn, &cache, &scans[k]);
   };
   if (nthreads == 1) worker(0);
   else {
@@ -74,6 +108,9 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
   }
 
   // serial prefix over requests
+  // staging == nullptr: zero-copy mode, the requests already live in one
+  // pinned arena starting at out.base; offsets are taken relative to it.
+  const bool copy = out.staging != nullptr;
   std::vector<uint64_t> byte_base(R);
   std::vector<int64_t> sample_base(R), slot_base(R);
   uint64_t bytes = 0; int64_t samples = 0, slots = 0;
@@ -83,13 +120,20 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
       res.error_request = (int64_t)k;
       return res;
     }
-    byte_base[k] = bytes; sample_base[k] = samples; slot_base[k] = slots;
-    bytes += reqs[k].len;
-    bytes = (bytes + 15) & ~(uint64_t)15;  // keep every request 16-B aligned in staging
+    sample_base[k] = samples; slot_base[k] = slots;
+    if (copy) {
+      byte_base[k] = bytes;
+      bytes += reqs[k].len;
+      bytes = (bytes + 15) & ~(uint64_t)15;  // keep every request 16-B aligned in staging
+    } else {
+      if (reqs[k].data < out.base) { res.error = 1; res.error_request = (int64_t)k; return res; }
+      byte_base[k] = (uint64_t)(reqs[k].data - out.base);
+      bytes = std::max<uint64_t>(bytes, byte_base[k] + reqs[k].len);
+    }
     samples += (int64_t)scans[k].off.size();
     for (int64_t s : scans[k].slots) slots += s;
   }
-  if (bytes > out.staging_cap || samples > out.max_samples) {
+  if ((copy && bytes > out.staging_cap) || samples > out.max_samples) {
     // report the sizes needed so the caller can grow its buffers and retry
     res.error = 2; res.n_samples = samples; res.n_bytes = bytes; res.n_slots = slots;
     return res;
@@ -97,7 +141,7 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
 
   auto writer = [&](int t) {
     for (size_t k = t; k < R; k += nthreads) {
-      memcpy(out.staging + byte_base[k], reqs[k].data, reqs[k].len);
+      if (copy) memcpy(out.staging + byte_base[k], reqs[k].data, reqs[k].len);
       const ReqScan& sc = scans[k];
       int64_t s0 = sample_base[k], slot = slot_base[k];
       for (size_t i = 0; i < sc.off.size(); ++i) {

@@ -124,7 +124,9 @@ struct RequestView {
 };
 
 struct PackOut {
-  uint8_t* staging;         // pinned host buffer receiving the raw request bytes
+  uint8_t* staging;         // pinned host buffer receiving the raw request bytes,
+                            // or null: zero-copy, requests already in an arena at `base`
+  const uint8_t* base;
   uint64_t staging_cap;
   int64_t* datum_off;       // [max_samples]
   int32_t* labels;          // [max_samples] (train only, may be null)

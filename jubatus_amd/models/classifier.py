@@ -4,7 +4,8 @@ Reference surface: jubatus/server/server/classifier_serv.cpp:91-225 (train,
 classify, get_labels, set_label, delete_label, clear) on top of jubatus_core's
 linear classifiers (EXTERNAL).
 
-Model: hashed tables W[H][LC] (+ S[H][LC] for CW/AROW/NHERD, init 1.0) with
+Model: hashed tables W[H][LC] (+ P[H][LC] = diagonal precision 1/S for
+CW/AROW/NHERD, init 1.0; see linear_oracle.py) with
 H = converter ``hash_max_size`` and LC = label capacity (power of two, grown
 on demand). On a GPU the tables live in HBM and every update/score runs in
 csrc/hip/linear.hip; without a GPU the NumPy oracle (linear_oracle.py) runs
@@ -83,21 +84,21 @@ class LinearClassifier:
         if self.gpu:
             t = self.torch
             W = t.zeros((H, LC), dtype=t.float32, device=self.device)
-            S = t.ones((H, LC), dtype=t.float32, device=self.device) if self.use_s else None
+            P = t.ones((H, LC), dtype=t.float32, device=self.device) if self.use_s else None
             if self.LC:
                 W[:, :self.LC].copy_(self.W)
-                if S is not None:
-                    S[:, :self.LC].copy_(self.S)
-            self.W, self.S = W, S
+                if P is not None:
+                    P[:, :self.LC].copy_(self.P)
+            self.W, self.P = W, P
             self.active = t.zeros(LC, dtype=t.int32, device=self.device)
         else:
             W = np.zeros((H, LC), dtype=np.float32)
-            S = np.ones((H, LC), dtype=np.float32) if self.use_s else None
+            P = np.ones((H, LC), dtype=np.float32) if self.use_s else None
             if self.LC:
                 W[:, :self.LC] = self.W
-                if S is not None:
-                    S[:, :self.LC] = self.S
-            self.W, self.S = W, S
+                if P is not None:
+                    P[:, :self.LC] = self.P
+            self.W, self.P = W, P
             self.active = np.zeros(LC, dtype=np.int32)
         self.LC = LC
         self._label_version = -1
@@ -120,18 +121,29 @@ class LinearClassifier:
         self._label_version = v
 
     # -------------------------------------------------------------- train
+    def _train_batch(self, b) -> int:
+        from ..ops import hip
+        self._sync_labels()
+        if b.n:
+            hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
+                             self.W, self.P, self.active, self.mid, self.C,
+                             concurrent=b.nstreams > 1)
+        return b.n
+
+    def train_arena(self, arena, offs, lens) -> int:
+        """Train on request bodies that already sit in a pinned RequestArena
+        (zero-copy receive path; one stream per span)."""
+        with self._lock:
+            if not (self.gpu and self.pipe.fast):
+                bodies = [bytes(arena.np[o:o + n]) for o, n in zip(offs, lens)]
+                return self.train_requests(bodies)
+            return self._train_batch(self.pipe.from_arena(arena, offs, lens, True, self.labels))
+
     def train_requests(self, bodies: Sequence[Any]) -> int:
         """Train on raw msgpack ``list<labeled_datum>`` bodies (one stream each)."""
         with self._lock:
             if self.gpu and self.pipe.fast:
-                from ..ops import hip
-                b = self.pipe.from_requests(list(bodies), True, self.labels)
-                self._sync_labels()
-                if b.n:
-                    hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr,
-                                     b.nstreams, self.W, self.S, self.active, self.mid, self.C,
-                                     concurrent=b.nstreams > 1)
-                return b.n
+                return self._train_batch(self.pipe.from_requests(list(bodies), True, self.labels))
             total = 0
             streams = [msgpack.unpackb(bytes(x), raw=False) for x in bodies]
             rows, labs, sizes = [], [], []
@@ -168,11 +180,11 @@ class LinearClassifier:
             from ..ops import hip
             b = self.pipe.from_rows(rows, labs, sizes)
             hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
-                             self.W, self.S, self.active, self.mid, self.C,
+                             self.W, self.P, self.active, self.mid, self.C,
                              concurrent=b.nstreams > 1)
             return
         for (idx, val), y in zip(rows, labs):
-            lo.train_one(self.W, self.S, np.asarray(idx, np.int64), np.asarray(val, np.float32),
+            lo.train_one(self.W, self.P, np.asarray(idx, np.int64), np.asarray(val, np.float32),
                          y, self.active, self.mid, self.C)
 
     # ----------------------------------------------------------- classify
@@ -238,8 +250,8 @@ class LinearClassifier:
                 return False
             self.labels.remove(label)
             self.W[:, i] = 0.0
-            if self.S is not None:
-                self.S[:, i] = 1.0
+            if self.P is not None:
+                self.P[:, i] = 1.0
             self._sync_labels()
             return True
 
@@ -258,15 +270,16 @@ class LinearClassifier:
     def _host_tables(self) -> tuple[np.ndarray, np.ndarray | None]:
         if self.gpu:
             W = self.W.cpu().numpy()
-            S = self.S.cpu().numpy() if self.S is not None else None
+            S = self.P.cpu().numpy() if self.P is not None else None
             return W, S
-        return self.W, self.S
+        return self.W, self.P
 
     def pack(self) -> dict:
         """Model payload (user_data of the model file).
 
         Sparse: only feature rows that differ from the initial state are
-        stored, as (row indices, W rows, S rows) over the live label columns.
+        stored, as (row indices, W rows, P rows) over the live label columns
+        (P = diagonal precision of CW/AROW/NHERD).
         """
         with self._lock:
             self.synchronize()
@@ -286,7 +299,7 @@ class LinearClassifier:
                 "counts": [int(self.labels.count(c)) for c in cols],
                 "rows": rows.tobytes(),
                 "W": np.ascontiguousarray(Wc[rows]).astype(np.float32).tobytes(),
-                "S": (np.ascontiguousarray(S[:, cols][rows]).astype(np.float32).tobytes()
+                "P": (np.ascontiguousarray(S[:, cols][rows]).astype(np.float32).tobytes()
                       if S is not None else b""),
                 "weights": self.conv.weights.pack(),
             }
@@ -310,17 +323,17 @@ class LinearClassifier:
             Wr = np.frombuffer(obj["W"], dtype=np.float32).reshape(len(rows), L)
             W = np.zeros((self.H, self.LC), dtype=np.float32)
             W[rows, :L] = Wr
-            S = None
+            P = None
             if self.use_s:
-                S = np.ones((self.H, self.LC), dtype=np.float32)
-                if len(obj["S"]):
-                    S[rows, :L] = np.frombuffer(obj["S"], dtype=np.float32).reshape(len(rows), L)
+                P = np.ones((self.H, self.LC), dtype=np.float32)
+                if len(obj["P"]):
+                    P[rows, :L] = np.frombuffer(obj["P"], dtype=np.float32).reshape(len(rows), L)
             if self.gpu:
                 self.W.copy_(self.torch.from_numpy(W))
-                if S is not None:
-                    self.S.copy_(self.torch.from_numpy(S))
+                if P is not None:
+                    self.P.copy_(self.torch.from_numpy(P))
             else:
-                self.W, self.S = W, S
+                self.W, self.P = W, P
             if obj.get("weights"):
                 self.conv.weights.unpack(obj["weights"])
 
@@ -340,24 +353,24 @@ class LinearClassifier:
             perm = t.tensor([old.get(n, -1) for n in order], dtype=t.int64, device=self.device)
             have = perm >= 0
             W = t.zeros((self.H, LC), dtype=t.float32, device=self.device)
-            S = t.ones((self.H, LC), dtype=t.float32, device=self.device) if self.use_s else None
+            P = t.ones((self.H, LC), dtype=t.float32, device=self.device) if self.use_s else None
             src = perm.clamp(min=0)
             W[:, :len(order)] = t.where(have, self.W.index_select(1, src), W[:, :len(order)])
             if S is not None:
-                S[:, :len(order)] = t.where(have, self.S.index_select(1, src), S[:, :len(order)])
+                S[:, :len(order)] = t.where(have, self.P.index_select(1, src), S[:, :len(order)])
         else:
             W = np.zeros((self.H, LC), dtype=np.float32)
-            S = np.ones((self.H, LC), dtype=np.float32) if self.use_s else None
+            P = np.ones((self.H, LC), dtype=np.float32) if self.use_s else None
             for c, n in enumerate(order):
                 if n in old:
                     W[:, c] = self.W[:, old[n]]
                     if S is not None:
-                        S[:, c] = self.S[:, old[n]]
+                        S[:, c] = self.P[:, old[n]]
         self.labels.clear()
         for c, n in enumerate(order):
             self.labels.get_or_add(n)
             self.labels.set_count(c, counts.get(n, 0))
-        self.W, self.S, self.LC = W, S, LC
+        self.W, self.P, self.LC = W, S, LC
         self.active = (self.torch.zeros(LC, dtype=self.torch.int32, device=self.device)
                        if self.gpu else np.zeros(LC, dtype=np.int32))
         self._label_version = -1
@@ -381,7 +394,7 @@ class LinearClassifier:
                             seen.add(n)
                             order.append(n)
                 self._reorder_labels(order)
-            tables = [self.W] + ([self.S] if self.S is not None else [])
+            tables = [self.W] + ([self.P] if self.P is not None else [])
             if self.gpu:
                 coll.allreduce_mean_(tables, group)
                 nbytes = sum(t.numel() * 4 for t in tables)

@@ -24,6 +24,12 @@ v = sum_i x_i^2 (S[i,y] + S[i,l*]).
   NHERD       m < 1: alpha = (1 - m) / (v + 1/C)
               W as AROW; S -= S^2 x^2 (C^2 v + 2C) / (1 + C v)^2
 
+The diagonal covariance S is *stored as its precision* P = 1/S (init 1):
+the updates above become additive, P += beta x^2 (CW) and
+P += beta x^2 / (1 - beta S x^2) (AROW, NHERD) - algebraically identical,
+always positive, and commutative (what lets concurrent GPU streams apply
+them with float atomics).
+
 Coordinates with idx < 0 are ignored. Every update reads the table before
 the sample and then writes (gather-compute-scatter), like the kernel.
 """
@@ -44,7 +50,7 @@ def scores(W: np.ndarray, idx: np.ndarray, val: np.ndarray) -> np.ndarray:
     return (val[m, None].astype(np.float32) * W[idx[m]]).sum(axis=0, dtype=np.float32)
 
 
-def train_one(W: np.ndarray, S: np.ndarray | None, idx: np.ndarray, val: np.ndarray, y: int,
+def train_one(W: np.ndarray, P: np.ndarray | None, idx: np.ndarray, val: np.ndarray, y: int,
               active: np.ndarray, method: int, C: float) -> bool:
     m = idx >= 0
     idx = idx[m]
@@ -60,8 +66,9 @@ def train_one(W: np.ndarray, S: np.ndarray | None, idx: np.ndarray, val: np.ndar
     nrm = float((x * x).sum())
     use_s = method in USES_COVARIANCE
     if use_s:
-        a = S[idx, y].copy()
-        b = S[idx, lstar].copy() if lstar >= 0 else np.zeros_like(a)
+        a = (np.float32(1.0) / P[idx, y]).astype(np.float32)
+        b = ((np.float32(1.0) / P[idx, lstar]).astype(np.float32) if lstar >= 0
+             else np.zeros_like(a))
         var = float((x * x * (a + b)).sum())
     else:
         a = b = None
@@ -107,14 +114,15 @@ def train_one(W: np.ndarray, S: np.ndarray | None, idx: np.ndarray, val: np.ndar
         W[idx, y] = wy + np.float32(tau) * a * x
         if lstar >= 0:
             W[idx, lstar] = wl - np.float32(tau) * b * x
+        bx2 = np.float32(beta) * x * x
         if method == CW:
-            S[idx, y] = 1.0 / (1.0 / a + np.float32(beta) * x * x)
-            if lstar >= 0:
-                S[idx, lstar] = 1.0 / (1.0 / b + np.float32(beta) * x * x)
+            dy = dl = bx2
         else:
-            S[idx, y] = a - np.float32(beta) * a * a * x * x
-            if lstar >= 0:
-                S[idx, lstar] = b - np.float32(beta) * b * b * x * x
+            dy = bx2 / (np.float32(1.0) - bx2 * a)
+            dl = bx2 / (np.float32(1.0) - bx2 * b)
+        P[idx, y] = np.float32(1.0) / a + dy
+        if lstar >= 0:
+            P[idx, lstar] = np.float32(1.0) / b + dl
     else:
         W[idx, y] = wy + np.float32(tau) * x
         if lstar >= 0:

@@ -72,6 +72,40 @@ class _Pinned:
             self.event = None
 
 
+class RequestArena:
+    """Pinned receive arena: request bodies are written here once (by the
+    RPC reader, or by the benchmark's synthetic client) and DMA'd to HBM
+    straight from it - no host-side copy on the train path."""
+
+    def __init__(self, capacity: int):
+        import torch
+        self.buf = torch.empty(max(16, capacity), dtype=torch.uint8, pin_memory=True)
+        self.np = self.buf.numpy()
+        self.used = 0
+        self.offs: list[int] = []
+        self.lens: list[int] = []
+
+    def append(self, body) -> tuple[int, int]:
+        mv = memoryview(body).cast("B")
+        n = mv.nbytes
+        off = (self.used + 15) & ~15
+        if off + n > self.np.size:
+            raise MemoryError("request arena full")
+        self.np[off:off + n] = np.frombuffer(mv, dtype=np.uint8)
+        self.used = off + n
+        self.offs.append(off)
+        self.lens.append(n)
+        return off, n
+
+    def reset(self) -> None:
+        self.used = 0
+        self.offs.clear()
+        self.lens.clear()
+
+    def spans(self) -> tuple[np.ndarray, np.ndarray]:
+        return np.asarray(self.offs, dtype=np.int64), np.asarray(self.lens, dtype=np.int64)
+
+
 class _DeviceBufs:
     def __init__(self, device):
         self.device = device
@@ -131,6 +165,41 @@ class FeaturePipeline:
             if err == 3:
                 raise RuntimeError("label table full")
             break
+        return self._launch(pin, pin.staging, n, nbytes, nslots, R, labeled)
+
+    def from_arena(self, arena: RequestArena, offs: np.ndarray, lens: np.ndarray, labeled: bool,
+                   table=None) -> DeviceBatch:
+        """Zero-copy variant of from_requests: bodies are spans of a pinned
+        RequestArena; the scanner reads them in place and one H2D copy moves
+        the arena prefix to HBM."""
+        if not self.fast:
+            raise RuntimeError("converter config is not eligible for the GPU fast path")
+        nat = native()
+        pin = self._pinned[self._turn]
+        self._turn ^= 1
+        pin.wait()
+        R = int(offs.size)
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int64)
+        pin.ensure(0, max(1024, pin.cap_samples), R)
+        while True:
+            n, nbytes, nslots, err, err_req = nat.pack_spans(
+                arena.buf.data_ptr(), offs.ctypes.data, lens.ctypes.data, R, labeled,
+                self.rules.n_srules, self.rules.n_nrules, table, pin.datum_off.data_ptr(),
+                pin.labels.data_ptr() if labeled else 0, pin.row_ptr.data_ptr(),
+                pin.stream_ptr.data_ptr(), pin.cap_samples, self.nthreads)
+            if err == 2:
+                pin.ensure(0, n, R)
+                continue
+            if err == 1:
+                raise TypeError(f"malformed datum list in request {err_req}")
+            if err == 3:
+                raise RuntimeError("label table full")
+            break
+        return self._launch(pin, arena.buf, n, nbytes, nslots, R, labeled)
+
+    def _launch(self, pin: "_Pinned", src: torch.Tensor, n: int, nbytes: int, nslots: int,
+                R: int, labeled: bool) -> DeviceBatch:
         dev = self._dev
         d_buf = dev.get("buf", max(nbytes, 1), torch.uint8)
         d_off = dev.get("datum_off", max(n, 1), torch.int64)
@@ -138,7 +207,7 @@ class FeaturePipeline:
         d_sp = dev.get("stream_ptr", R + 1, torch.int64)
         d_idx = dev.get("fidx", max(nslots, 1), torch.int32)
         d_val = dev.get("fval", max(nslots, 1), torch.float32)
-        d_buf[:nbytes].copy_(pin.staging[:nbytes], non_blocking=True)
+        d_buf[:nbytes].copy_(src[:nbytes], non_blocking=True)
         d_off[:n].copy_(pin.datum_off[:n], non_blocking=True)
         d_row[:n + 1].copy_(pin.row_ptr[:n + 1], non_blocking=True)
         d_sp[:R + 1].copy_(pin.stream_ptr[:R + 1], non_blocking=True)

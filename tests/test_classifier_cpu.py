@@ -61,7 +61,7 @@ def test_pack_unpack_roundtrip():
     c2.unpack(blob)
     assert c2.get_labels() == c.get_labels()
     np.testing.assert_array_equal(c2.W[:, :3], c.W[:, :3])
-    np.testing.assert_array_equal(c2.S[:, :3], c.S[:, :3])
+    np.testing.assert_array_equal(c2.P[:, :3], c.P[:, :3])
 
 
 def test_sequential_semantics_order_matters():
