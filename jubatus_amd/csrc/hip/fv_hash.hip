@@ -45,35 +45,30 @@ __device__ __forceinline__ bool key_matches(const GpuRule& r, const uint8_t* blo
   return true;
 }
 
-__global__ __launch_bounds__(256) void fv_hash_kernel(
-    const uint8_t* __restrict__ buf, int64_t buf_len,
-    const int64_t* __restrict__ datum_off, const int64_t* __restrict__ row_ptr, int n,
-    const GpuRule* __restrict__ srules, int n_srules,
-    const GpuRule* __restrict__ nrules, int n_nrules,
-    const uint8_t* __restrict__ blob, uint64_t H,
-    int32_t* __restrict__ out_idx, float* __restrict__ out_val, int32_t* __restrict__ err) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  Reader rd{buf + datum_off[s], buf + buf_len, true};
-  int64_t slot = row_ptr[s];
-  const int64_t slot_end = row_ptr[s + 1];
-
+// Walk one datum and emit its feature slots; returns false on a structural
+// error (the host scanner validated the bytes already, so this is defensive).
+__device__ __forceinline__ bool emit_datum(Reader& rd, int64_t slot, const int64_t slot_end,
+                                           const GpuRule* __restrict__ srules, int n_srules,
+                                           const GpuRule* __restrict__ nrules, int n_nrules,
+                                           const uint8_t* blob, uint64_t H,
+                                           int32_t* __restrict__ out_idx,
+                                           float* __restrict__ out_val) {
   int64_t top = rd.array_len();
-  if (top < 2) { atomicOr(err, 1); return; }
+  if (top < 2) return false;
   // ---- string_values: [[key, value], ...]
   int64_t ns = rd.array_len();
   for (int64_t i = 0; i < ns && rd.ok; ++i) {
-    if (rd.array_len() != 2) { rd.ok = false; break; }
+    if (rd.array_len() != 2) return false;
     const uint8_t *k, *v; int kn, vn;
-    if (!rd.raw(&k, &kn) || !rd.raw(&v, &vn)) break;
+    if (!rd.raw(&k, &kn) || !rd.raw(&v, &vn)) return false;
     uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
     hk = fnv_byte(hk, '$');
     hk = fnv_bytes(hk, v, vn);
     for (int r = 0; r < n_srules; ++r) {
       const GpuRule rule = srules[r];
-      if (slot >= slot_end) { rd.ok = false; break; }
+      if (slot >= slot_end) return false;
       if (key_matches(rule, blob, k, kn)) {
-        uint64_t h = fnv_bytes(hk, blob + rule.suffix_off, rule.suffix_len);
+        const uint64_t h = fnv_bytes(hk, blob + rule.suffix_off, rule.suffix_len);
         out_idx[slot] = (int32_t)hash_to_index(h, H);
         out_val[slot] = rule.weight;
       } else {
@@ -86,18 +81,17 @@ __global__ __launch_bounds__(256) void fv_hash_kernel(
   // ---- num_values: [[key, number], ...]
   int64_t nn = rd.ok ? rd.array_len() : -1;
   for (int64_t i = 0; i < nn && rd.ok; ++i) {
-    if (rd.array_len() != 2) { rd.ok = false; break; }
+    if (rd.array_len() != 2) return false;
     const uint8_t* k; int kn; double x;
-    if (!rd.raw(&k, &kn) || !rd.number(&x)) break;
-    uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
+    if (!rd.raw(&k, &kn) || !rd.number(&x)) return false;
+    const uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
     for (int r = 0; r < n_nrules; ++r) {
       const GpuRule rule = nrules[r];
-      if (slot >= slot_end) { rd.ok = false; break; }
+      if (slot >= slot_end) return false;
       if (key_matches(rule, blob, k, kn)) {
-        uint64_t h = fnv_bytes(hk, blob + rule.suffix_off, rule.suffix_len);
-        float val = (rule.value_kind == 1) ? logf(fmaxf(1.f, (float)x)) : (float)x;
+        const uint64_t h = fnv_bytes(hk, blob + rule.suffix_off, rule.suffix_len);
         out_idx[slot] = (int32_t)hash_to_index(h, H);
-        out_val[slot] = val;
+        out_val[slot] = (rule.value_kind == 1) ? logf(fmaxf(1.f, (float)x)) : (float)x;
       } else {
         out_idx[slot] = -1;
         out_val[slot] = 0.f;
@@ -105,20 +99,86 @@ __global__ __launch_bounds__(256) void fv_hash_kernel(
       ++slot;
     }
   }
-  if (!rd.ok || slot != slot_end) atomicOr(err, 2);
+  return rd.ok && slot == slot_end;
+}
+
+constexpr int kBlobCap = 1024;   // rule blob staged in LDS when it fits
+constexpr int kWin = 16384;      // per-wave LDS window of datum bytes
+
+// One lane per datum. The 64 datums of a wave are consecutive samples, so
+// their bytes form one contiguous window of the request arena: the wave
+// stages that window into LDS with 16-B loads (coalesced), then every lane
+// parses its datum out of LDS instead of issuing ~200 dependent byte loads
+// to global memory. Windows larger than kWin fall back to global parsing.
+__global__ __launch_bounds__(256) void fv_hash_kernel(
+    const uint8_t* __restrict__ buf, int64_t buf_len, int64_t buf_cap,
+    const int64_t* __restrict__ datum_off, const int32_t* __restrict__ datum_len,
+    const int64_t* __restrict__ row_ptr, int n,
+    const GpuRule* __restrict__ srules, int n_srules,
+    const GpuRule* __restrict__ nrules, int n_nrules,
+    const uint8_t* __restrict__ blob, int blob_len, uint64_t H,
+    int32_t* __restrict__ out_idx, float* __restrict__ out_val, int32_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_blob[kBlobCap];
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[4][kWin];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const bool blob_lds = blob_len <= kBlobCap;
+  if (blob_lds)
+    for (int i = threadIdx.x; i < blob_len; i += blockDim.x) s_blob[i] = blob[i];
+  __syncthreads();
+  const uint8_t* bl = blob_lds ? (const uint8_t*)s_blob : blob;
+
+  const int s0 = (blockIdx.x * blockDim.x) + wv * 64;
+  if (s0 >= n) return;
+  const int s = s0 + lane;
+  const bool live = s < n;
+  const int64_t off = live ? datum_off[s] : datum_off[s0];
+  const int64_t dend = live ? off + datum_len[s] : off;
+  // window [lo, hi) covering every datum of the wave
+  int64_t lo = off, hi = dend;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t olo = __shfl_xor(lo, o, 64);
+    const int64_t ohi = __shfl_xor(hi, o, 64);
+    lo = olo < lo ? olo : lo;
+    hi = ohi > hi ? ohi : hi;
+  }
+  const int64_t lo16 = lo & ~(int64_t)15;
+  const int64_t span = ((hi + 15) & ~(int64_t)15) - lo16;
+  bool ok = true;
+  if (span <= kWin && lo16 + span <= buf_cap) {
+    for (int64_t b = (int64_t)lane * 16; b < span; b += 64 * 16)
+      *reinterpret_cast<uint4*>(&s_win[wv][b]) = *reinterpret_cast<const uint4*>(buf + lo16 + b);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (live) {
+      const uint8_t* base = &s_win[wv][off - lo16];
+      Reader rd{base, base + (dend - off), true};
+      ok = emit_datum(rd, row_ptr[s], row_ptr[s + 1], srules, n_srules, nrules, n_nrules, bl, H,
+                      out_idx, out_val);
+    }
+  } else if (live) {
+    Reader rd{buf + off, buf + (dend < buf_len ? dend : buf_len), true};
+    ok = emit_datum(rd, row_ptr[s], row_ptr[s + 1], srules, n_srules, nrules, n_nrules, bl, H,
+                    out_idx, out_val);
+  }
+  if (!ok) atomicOr(err, 2);
 }
 
 }  // namespace jb
 
-extern "C" int jb_fv_hash(const uint8_t* buf, int64_t buf_len, const int64_t* datum_off,
+extern "C" int jb_fv_hash(const uint8_t* buf, int64_t buf_len, int64_t buf_cap,
+                          const int64_t* datum_off, const int32_t* datum_len,
                           const int64_t* row_ptr, int n, const void* srules, int n_srules,
-                          const void* nrules, int n_nrules, const uint8_t* blob, uint64_t H,
-                          int32_t* out_idx, float* out_val, int32_t* err, hipStream_t stream) {
+                          const void* nrules, int n_nrules, const uint8_t* blob, int blob_len,
+                          uint64_t H, int32_t* out_idx, float* out_val, int32_t* err,
+                          hipStream_t stream) {
   if (n <= 0) return 0;
   const int threads = 256;
   const int blocks = (n + threads - 1) / threads;
   hipLaunchKernelGGL(jb::fv_hash_kernel, dim3(blocks), dim3(threads), 0, stream, buf, buf_len,
-                     datum_off, row_ptr, n, (const jb::GpuRule*)srules, n_srules,
-                     (const jb::GpuRule*)nrules, n_nrules, blob, H, out_idx, out_val, err);
+                     buf_cap, datum_off, datum_len, row_ptr, n, (const jb::GpuRule*)srules,
+                     n_srules, (const jb::GpuRule*)nrules, n_nrules, blob, blob_len, H, out_idx,
+                     out_val, err);
   return (int)hipGetLastError();
 }

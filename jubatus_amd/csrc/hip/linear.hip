@@ -73,16 +73,114 @@ __device__ __forceinline__ void sample_scores(const int32_t* __restrict__ fidx,
   }
 }
 
+// step sizes of one update; returns false when the sample causes no update.
+// W += tau * (S) * x ; precision increments use beta (see header).
+__device__ __forceinline__ bool step_coeffs(int method, float margin, float var, float nrm,
+                                            bool has_l, float C, float* tau, float* beta) {
+  switch (method) {
+    case PERCEPTRON:
+      if (margin <= 0.f) { *tau = 1.f; *beta = 0.f; return true; }
+      return false;
+    case PA: case PA1: case PA2: {
+      const float loss = 1.f - margin;
+      if (!(loss > 0.f && nrm > 0.f)) return false;
+      const float sq = (has_l ? 2.f : 1.f) * nrm;
+      if (method == PA) *tau = loss / sq;
+      else if (method == PA1) *tau = fminf(C, loss / sq);
+      else *tau = loss / (sq + 0.5f / C);
+      *beta = 0.f;
+      return true;
+    }
+    case CW: {
+      if (!(var > 0.f)) return false;
+      const float phi = C;
+      const float b = 1.f + 2.f * phi * margin;
+      const float disc = b * b - 8.f * phi * (margin - phi * var);
+      const float gamma = (-b + sqrtf(fmaxf(disc, 0.f))) / (4.f * phi * var);
+      if (!(gamma > 0.f)) return false;
+      *tau = gamma; *beta = 2.f * gamma * phi;
+      return true;
+    }
+    case AROW:
+      if (!(margin < 1.f)) return false;
+      *beta = 1.f / (var + 1.f / C);
+      *tau = (1.f - margin) * *beta;
+      return true;
+    case NHERD: {
+      if (!(margin < 1.f)) return false;
+      *tau = (1.f - margin) / (var + 1.f / C);
+      const float cv = 1.f + C * var;
+      *beta = (C * C * var + 2.f * C) / (cv * cv);
+      return true;
+    }
+    default: return false;
+  }
+}
+
+// precision increment for one (feature, label): s = 1/P before the update
+__device__ __forceinline__ float dprec(int method, float beta, float x, float s) {
+  const float bx2 = beta * x * x;
+  return method == CW ? bx2 : bx2 / (1.f - bx2 * s);
+}
+
+// apply the update of one feature (lane-per-feature form)
+template <int LC, bool CONC>
+__device__ __forceinline__ void apply_feature(float* W, float* P, int32_t idx, float x, int y,
+                                              int lstar, bool use_s, int method, float tau,
+                                              float beta, float a, float b, float wy, float wl) {
+  const int64_t row = (int64_t)idx * LC;
+  const float dwy = use_s ? tau * a * x : tau * x;
+  const float dwl = use_s ? -tau * b * x : -tau * x;
+  if (CONC) {
+    atomicAdd(W + row + y, dwy);
+    if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+    if (use_s) {
+      atomicAdd(P + row + y, dprec(method, beta, x, a));
+      if (lstar >= 0) atomicAdd(P + row + lstar, dprec(method, beta, x, b));
+    }
+  } else {
+    W[row + y] = wy + dwy;
+    if (lstar >= 0) W[row + lstar] = wl + dwl;
+    if (use_s) {
+      P[row + y] = 1.f / a + dprec(method, beta, x, a);
+      if (lstar >= 0) P[row + lstar] = 1.f / b + dprec(method, beta, x, b);
+    }
+  }
+}
+
+// best wrong label among the lanes of one feature group (lowest index on ties)
+template <int LW>
+__device__ __forceinline__ void argmax_wrong(float& best, int& bl) {
+#pragma unroll
+  for (int off = 1; off < LW; off <<= 1) {
+    const float ob = __shfl_xor(best, off, 64);
+    const int ol = __shfl_xor(bl, off, 64);
+    if (ol >= 0 && (bl < 0 || ob > best || (ob == best && ol < bl))) { best = ob; bl = ol; }
+  }
+}
+
+// Staged-row capacity of the fast path: NMAX features x LC labels per wave.
+template <int LC>
+struct Stage {
+  static constexpr int NMAX = LC <= 64 ? 1024 / LC : 0;
+};
+
 template <int LC, bool CONC>
 __global__ __launch_bounds__(256) void linear_train_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
-    const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* S,
+    const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
     const int32_t* __restrict__ active, int method, float C) {
   using L = Lanes<LC>;
+  constexpr int NMAX = Stage<LC>::NMAX;
+  // per-wave LDS image of the gathered W / P rows of the current sample
+  __shared__ float sW[4][NMAX > 0 ? NMAX * LC : 1];
+  __shared__ float sP[4][NMAX > 0 ? NMAX * LC : 1];
   const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (wid >= nstreams) return;
+  const int g = lane / L::LW;
   const int l0 = lane % L::LW;
   bool act[L::K];
 #pragma unroll
@@ -90,15 +188,89 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
   const bool use_s = method >= CW;
 
   const int64_t s_beg = stream_ptr[wid], s_end = stream_ptr[wid + 1];
+  // software prefetch of the next sample's (idx, x) for lane j = feature j
+  int64_t nb = s_beg < s_end ? row_ptr[s_beg] : 0;
+  int nn = s_beg < s_end ? (int)(row_ptr[s_beg + 1] - nb) : 0;
+  int32_t pidx = (lane < nn) ? fidx[nb + lane] : -1;
+  float px = (lane < nn) ? fval[nb + lane] : 0.f;
+  int py = s_beg < s_end ? labels[s_beg] : -1;
+
   for (int64_t s = s_beg; s < s_end; ++s) {
-    const int64_t beg = row_ptr[s];
-    const int n = (int)(row_ptr[s + 1] - beg);
-    const int y = labels[s];
+    const int64_t beg = nb;
+    const int n = nn;
+    const int y = py;
+    const int32_t my_idx = pidx;
+    const float my_x = px;
+    if (s + 1 < s_end) {  // issue next sample's descriptor loads now
+      nb = row_ptr[s + 1];
+      nn = (int)(row_ptr[s + 2] - nb);
+      pidx = (lane < nn) ? fidx[nb + lane] : -1;
+      px = (lane < nn) ? fval[nb + lane] : 0.f;
+      py = labels[s + 1];
+    }
     if (y < 0 || y >= LC) continue;
+
+    if (NMAX > 0 && n <= NMAX && n <= 64) {
+      // ---------------- fast path: one gather round trip, rows staged in LDS
+      float acc = 0.f;
+      // wave-uniform trip count: every lane takes part in each shuffle
+      for (int j0 = 0; j0 < n; j0 += L::G) {
+        const int j = j0 + g;
+        const int src = j < 64 ? j : 63;
+        const int32_t idx = __shfl(my_idx, src, 64);
+        const float x = __shfl(my_x, src, 64);
+        if (j < n) {
+          float w = 0.f, pr = 1.f;
+          if (idx >= 0) {
+            const int64_t row = (int64_t)idx * LC + l0;
+            w = ld_agent(W + row);
+            if (use_s) pr = ld_agent(P + row);
+            acc += x * w;
+          }
+          sW[wv][j * LC + l0] = w;
+          if (use_s) sP[wv][j * LC + l0] = pr;
+        }
+      }
+#pragma unroll
+      for (int off = L::LW; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
+      const float sy = __shfl(acc, y % L::LW, 64);
+      float best = (act[0] && l0 != y) ? acc : -INFINITY;
+      int bl = (act[0] && l0 != y) ? l0 : -1;
+      argmax_wrong<L::LW>(best, bl);
+      const int lstar = bl;
+      const float margin = sy - (lstar >= 0 ? best : 0.f);
+      __builtin_amdgcn_wave_barrier();
+      // lane-per-feature: staged values of feature `lane`
+      float a = 1.f, b = 1.f, wy = 0.f, wl = 0.f, x2 = 0.f;
+      const bool mine = lane < n && my_idx >= 0;
+      if (mine) {
+        x2 = my_x * my_x;
+        if (use_s) {
+          a = 1.f / sP[wv][lane * LC + y];
+          b = lstar >= 0 ? 1.f / sP[wv][lane * LC + lstar] : 0.f;
+        }
+        if (!CONC) {
+          wy = sW[wv][lane * LC + y];
+          wl = lstar >= 0 ? sW[wv][lane * LC + lstar] : 0.f;
+        }
+      }
+      const float var = wave_sum(use_s ? x2 * (a + b) : 0.f);
+      const float nrm = wave_sum(x2);
+      float tau = 0.f, beta = 0.f;
+      if (step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) {
+        if (mine)
+          apply_feature<LC, CONC>(W, P, my_idx, my_x, y, lstar, use_s, method, tau, beta, a, b,
+                                  wy, wl);
+        // the next sample of this stream must observe these stores
+        if (!CONC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
+
+    // ---------------- general path (many features or > 64 labels)
     float acc[L::K];
     sample_scores<LC>(fidx, fval, beg, n, W, lane, acc);
-
-    // correct-label score and best wrong label (lowest index wins ties)
     float sy = 0.f, best = -INFINITY;
     int bl = -1;
 #pragma unroll
@@ -108,17 +280,9 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
       if (act[k] && l != y && acc[k] > best) { best = acc[k]; bl = l; }
     }
     sy = __shfl(sy, y % L::LW, 64);
-#pragma unroll
-    for (int off = 1; off < L::LW; off <<= 1) {
-      const float ob = __shfl_xor(best, off, 64);
-      const int ol = __shfl_xor(bl, off, 64);
-      if (ol >= 0 && (bl < 0 || ob > best || (ob == best && ol < bl))) { best = ob; bl = ol; }
-    }
+    argmax_wrong<L::LW>(best, bl);
     const int lstar = bl;
     const float margin = sy - (lstar >= 0 ? best : 0.f);
-
-    // pass 2: lane-per-feature variance / squared norm (first 64 features kept in registers)
-    int32_t idx0 = -1; float x0 = 0.f, sy0 = 1.f, sl0 = 1.f, wy0 = 0.f, wl0 = 0.f;
     float var = 0.f, nrm = 0.f;
     for (int base = 0; base < n; base += 64) {
       const int j = base + lane;
@@ -128,113 +292,32 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
         if (idx >= 0) {
           const int64_t row = (int64_t)idx * LC;
           nrm += x * x;
-          float a = 1.f, b = 1.f;
           if (use_s) {
-            a = 1.f / ld_agent(S + row + y);
-            b = lstar >= 0 ? 1.f / ld_agent(S + row + lstar) : 0.f;
+            const float a = 1.f / ld_agent(P + row + y);
+            const float b = lstar >= 0 ? 1.f / ld_agent(P + row + lstar) : 0.f;
             var += x * x * (a + b);
-          }
-          if (base == 0) {
-            idx0 = idx; x0 = x; sy0 = a; sl0 = b;
-            if (!CONC) { wy0 = ld_agent(W + row + y); wl0 = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f; }
           }
         }
       }
     }
     var = wave_sum(var);
     nrm = wave_sum(nrm);
-
-    // step sizes
-    float tau = 0.f, beta = 0.f;  // W += tau*(S)*x ; S update uses beta
-    bool upd = false;
-    switch (method) {
-      case PERCEPTRON: if (margin <= 0.f) { tau = 1.f; upd = true; } break;
-      case PA: case PA1: case PA2: {
-        const float loss = 1.f - margin;
-        if (loss > 0.f && nrm > 0.f) {
-          const float sq = (lstar >= 0 ? 2.f : 1.f) * nrm;
-          if (method == PA) tau = loss / sq;
-          else if (method == PA1) tau = fminf(C, loss / sq);
-          else tau = loss / (sq + 0.5f / C);
-          upd = true;
-        }
-      } break;
-      case CW: {
-        if (var > 0.f) {
-          const float phi = C;
-          const float b = 1.f + 2.f * phi * margin;
-          const float disc = b * b - 8.f * phi * (margin - phi * var);
-          const float gamma = (-b + sqrtf(fmaxf(disc, 0.f))) / (4.f * phi * var);
-          if (gamma > 0.f) { tau = gamma; beta = 2.f * gamma * phi; upd = true; }
-        }
-      } break;
-      case AROW: {
-        if (margin < 1.f) {
-          beta = 1.f / (var + 1.f / C);
-          tau = (1.f - margin) * beta;
-          upd = true;
-        }
-      } break;
-      case NHERD: {
-        if (margin < 1.f) {
-          tau = (1.f - margin) / (var + 1.f / C);
-          const float cv = 1.f + C * var;
-          beta = (C * C * var + 2.f * C) / (cv * cv);
-          upd = true;
-        }
-      } break;
-      default: break;
+    float tau = 0.f, beta = 0.f;
+    if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) continue;
+    for (int base = 0; base < n; base += 64) {
+      const int j = base + lane;
+      if (j >= n) continue;
+      const int32_t idx = fidx[beg + j];
+      if (idx < 0) continue;
+      const float x = fval[beg + j];
+      const int64_t row = (int64_t)idx * LC;
+      const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
+      const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
+      float wy = 0.f, wl = 0.f;
+      if (!CONC) { wy = ld_agent(W + row + y); wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f; }
+      apply_feature<LC, CONC>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, wy, wl);
     }
-
-    if (upd) {
-      for (int base = 0; base < n; base += 64) {
-        const int j = base + lane;
-        if (j >= n) continue;
-        int32_t idx; float x, a, b, wy, wl;
-        if (base == 0) { idx = idx0; x = x0; a = sy0; b = sl0; wy = wy0; wl = wl0; }
-        else {
-          idx = fidx[beg + j]; x = fval[beg + j];
-          if (idx < 0) continue;
-          const int64_t row = (int64_t)idx * LC;
-          a = use_s ? 1.f / ld_agent(S + row + y) : 1.f;
-          b = (use_s && lstar >= 0) ? 1.f / ld_agent(S + row + lstar) : 1.f;
-          if (!CONC) { wy = ld_agent(W + row + y); wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f; }
-        }
-        if (idx < 0) continue;
-        const int64_t row = (int64_t)idx * LC;
-        const float dwy = use_s ? tau * a * x : tau * x;
-        const float dwl = use_s ? -tau * b * x : -tau * x;
-        // precision increments (see header)
-        float dsy = 0.f, dsl = 0.f;
-        if (use_s) {
-          const float bx2 = beta * x * x;
-          if (method == CW) {
-            dsy = bx2;
-            dsl = bx2;
-          } else {
-            dsy = bx2 / (1.f - bx2 * a);
-            dsl = bx2 / (1.f - bx2 * b);
-          }
-        }
-        if (CONC) {
-          atomicAdd(W + row + y, dwy);
-          if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
-          if (use_s) {
-            atomicAdd(S + row + y, dsy);
-            if (lstar >= 0) atomicAdd(S + row + lstar, dsl);
-          }
-        } else {
-          W[row + y] = wy + dwy;
-          if (lstar >= 0) W[row + lstar] = wl + dwl;
-          if (use_s) {
-            S[row + y] = 1.f / a + dsy;
-            if (lstar >= 0) S[row + lstar] = 1.f / b + dsl;
-          }
-        }
-      }
-      // the next sample of this stream must observe these stores
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (!CONC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 

@@ -10,8 +10,9 @@ namespace py = pybind11;
 namespace {
 
 py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* table,
-               uintptr_t staging, uint64_t staging_cap, uintptr_t datum_off, uintptr_t labels,
-               uintptr_t row_ptr, uintptr_t stream_ptr, int64_t max_samples, int nthreads) {
+               uintptr_t staging, uint64_t staging_cap, uintptr_t datum_off, uintptr_t datum_len,
+               uintptr_t labels, uintptr_t row_ptr, uintptr_t stream_ptr, int64_t max_samples,
+               int nthreads) {
   std::vector<jb::RequestView> views;
   std::vector<py::buffer_info> keep;
   views.reserve(reqs.size());
@@ -22,7 +23,8 @@ py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* ta
     const py::buffer_info& bi = keep.back();
     views.push_back({(const uint8_t*)bi.ptr, (uint64_t)(bi.size * bi.itemsize)});
   }
-  jb::PackOut out{(uint8_t*)staging, nullptr, staging_cap, (int64_t*)datum_off, (int32_t*)labels,
+  jb::PackOut out{(uint8_t*)staging, nullptr, staging_cap, (int64_t*)datum_off,
+                  (int32_t*)datum_len, (int32_t*)labels,
                   (int64_t*)row_ptr, (int64_t*)stream_ptr, max_samples};
   jb::PackResult r;
   {
@@ -36,13 +38,14 @@ py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* ta
 // pinned arena at `base` (e.g. the RPC receive arena); nothing is copied.
 py::tuple pack_spans(uintptr_t base, uintptr_t offs, uintptr_t lens, int64_t nreq, bool labeled,
                      int sps, int spn, jb::LabelTable* table, uintptr_t datum_off,
-                     uintptr_t labels, uintptr_t row_ptr, uintptr_t stream_ptr,
+                     uintptr_t datum_len, uintptr_t labels, uintptr_t row_ptr, uintptr_t stream_ptr,
                      int64_t max_samples, int nthreads) {
   std::vector<jb::RequestView> views((size_t)nreq);
   const int64_t* o = (const int64_t*)offs;
   const int64_t* l = (const int64_t*)lens;
   for (int64_t k = 0; k < nreq; ++k) views[k] = {(const uint8_t*)base + o[k], (uint64_t)l[k]};
-  jb::PackOut out{nullptr, (const uint8_t*)base, 0, (int64_t*)datum_off, (int32_t*)labels,
+  jb::PackOut out{nullptr, (const uint8_t*)base, 0, (int64_t*)datum_off, (int32_t*)datum_len,
+                  (int32_t*)labels,
                   (int64_t*)row_ptr, (int64_t*)stream_ptr, max_samples};
   jb::PackResult r;
   {

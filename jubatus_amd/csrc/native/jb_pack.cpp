@@ -4,6 +4,7 @@
 #include <string.h>
 
 #include "jb_hash.hpp"
+#include "jb_pool.hpp"
 
 #include <algorithm>
 #include <string>
@@ -16,6 +17,7 @@ namespace {
 
 struct ReqScan {
   std::vector<uint64_t> off;     // datum offset inside the request
+  std::vector<uint32_t> len;     // datum byte length
   std::vector<int32_t> label;
   std::vector<int64_t> slots;
   bool ok = true;
@@ -68,6 +70,7 @@ void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelCache* 
   uint32_t n;
   if (!c.array(&n)) { out->ok = false; return; }
   out->off.reserve(n);
+  out->len.reserve(n);
   out->slots.reserve(n);
   if (labeled) out->label.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
@@ -82,6 +85,7 @@ void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelCache* 
     DatumShape d;
     if (!scan_datum(c, &d)) { out->ok = false; return; }
     out->off.push_back(doff);
+    out->len.push_back((uint32_t)((uint64_t)(c.p - r.data) - doff));
     out->slots.push_back((int64_t)d.n_str * sps + (int64_t)d.n_num * spn);
   }
 }
@@ -93,19 +97,24 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
   PackResult res;
   const size_t R = reqs.size();
   std::vector<ReqScan> scans(R);
-  if (nthreads < 1) nthreads = 1;
-  if ((size_t)nthreads > R) nthreads = (int)std::max<size_t>(R, 1);
-
-  auto worker = [&](int t) {
-    LabelCache cache(table);
-    for (size_t k = t; k < R; k += nthreads) scan_one(reqs[k], labeled, sps, spn, &cache, &scans[k]);
-  };
-  if (nthreads == 1) worker(0);
-  else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
-    for (auto& x : th) x.join();
+  if (R == 0) {
+    if (out.row_ptr) out.row_ptr[0] = 0;
+    if (out.stream_ptr) out.stream_ptr[0] = 0;
+    return res;
   }
+
+  WorkerPool& pool = global_pool(nthreads);
+  const int64_t nchunks = std::min<int64_t>((int64_t)R, (int64_t)pool.size() * 4);
+  auto chunk = [&](int64_t c, int64_t* b, int64_t* e) {
+    *b = c * (int64_t)R / nchunks;
+    *e = (c + 1) * (int64_t)R / nchunks;
+  };
+  pool.parallel_for(nchunks, [&](int64_t c) {
+    LabelCache cache(table);
+    int64_t b, e;
+    chunk(c, &b, &e);
+    for (int64_t k = b; k < e; ++k) scan_one(reqs[k], labeled, sps, spn, &cache, &scans[k]);
+  });
 
   // serial prefix over requests
   // staging == nullptr: zero-copy mode, the requests already live in one
@@ -139,36 +148,55 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
     return res;
   }
 
-  auto writer = [&](int t) {
-    for (size_t k = t; k < R; k += nthreads) {
+  pool.parallel_for(nchunks, [&](int64_t c) {
+    int64_t b, e;
+    chunk(c, &b, &e);
+    for (int64_t k = b; k < e; ++k) {
       if (copy) memcpy(out.staging + byte_base[k], reqs[k].data, reqs[k].len);
       const ReqScan& sc = scans[k];
       int64_t s0 = sample_base[k], slot = slot_base[k];
       for (size_t i = 0; i < sc.off.size(); ++i) {
         out.datum_off[s0 + i] = (int64_t)(byte_base[k] + sc.off[i]);
+        if (out.datum_len) out.datum_len[s0 + i] = (int32_t)sc.len[i];
         out.row_ptr[s0 + i] = slot;
         slot += sc.slots[i];
         if (labeled && out.labels) out.labels[s0 + i] = sc.label[i];
       }
     }
-  };
-  if (nthreads == 1) writer(0);
-  else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthreads; ++t) th.emplace_back(writer, t);
-    for (auto& x : th) x.join();
-  }
+  });
   out.row_ptr[samples] = slots;
   if (out.stream_ptr) {
     for (size_t k = 0; k < R; ++k) out.stream_ptr[k] = sample_base[k];
     out.stream_ptr[R] = samples;
   }
   if (labeled && table) {
-    for (size_t k = 0; k < R; ++k)
-      for (int32_t id : scans[k].label) table->add_count(id, 1);
+    // per-chunk histograms, then one atomic add per (chunk, label)
+    pool.parallel_for(nchunks, [&](int64_t c) {
+      int64_t b, e;
+      chunk(c, &b, &e);
+      std::vector<uint64_t> hist;
+      for (int64_t k = b; k < e; ++k)
+        for (int32_t id : scans[k].label) {
+          if ((size_t)id >= hist.size()) hist.resize((size_t)id + 1, 0);
+          ++hist[id];
+        }
+      for (size_t id = 0; id < hist.size(); ++id)
+        if (hist[id]) table->add_count((int)id, hist[id]);
+    });
   }
   res.n_samples = samples; res.n_bytes = bytes; res.n_slots = slots;
   return res;
+}
+
+WorkerPool& global_pool(int nthreads) {
+  static std::mutex mu;
+  static WorkerPool* pool = nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (pool == nullptr || (nthreads > pool->size() && pool->size() < 64)) {
+    // grown pools are leaked on purpose: a concurrent caller may still hold the old one
+    pool = new WorkerPool(std::max(1, std::min(nthreads, 64)));
+  }
+  return *pool;
 }
 
 }  // namespace jb

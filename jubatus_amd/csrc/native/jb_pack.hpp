@@ -129,6 +129,7 @@ struct PackOut {
   const uint8_t* base;
   uint64_t staging_cap;
   int64_t* datum_off;       // [max_samples]
+  int32_t* datum_len;       // [max_samples] (may be null)
   int32_t* labels;          // [max_samples] (train only, may be null)
   int64_t* row_ptr;         // [max_samples + 1]
   int64_t* stream_ptr;      // [n_requests + 1]

@@ -10,8 +10,13 @@ Turns train/classify request bodies into device CSR batches:
 * host path (any other config): the host converter produces feature names,
   which are hashed on the host and shipped as CSR.
 
-Pinned staging sets are double-buffered: the scan of batch k+1 fills one set
-while the H2D copy of batch k drains the other (an event guards reuse).
+Pinned staging sets and device input sets are double-buffered and the H2D
+copies run on a dedicated copy stream: the host scan of batch k+1 and its
+DMA overlap the kernels of batch k. Events order everything:
+  copy(k)      waits for the compute work that last read device set k%2
+               (the train of batch k-2), recorded when batch k-1 was launched
+  fv_hash(k)   waits for copy(k)
+  host reuse of pinned set k%2 waits for copy(k).
 """
 from __future__ import annotations
 
@@ -60,6 +65,7 @@ class _Pinned:
         if nsamples > self.cap_samples:
             self.cap_samples = _grow(self.cap_samples or 1024, nsamples)
             self.datum_off = torch.empty(self.cap_samples, dtype=torch.int64, pin_memory=True)
+            self.datum_len = torch.empty(self.cap_samples, dtype=torch.int32, pin_memory=True)
             self.labels = torch.empty(self.cap_samples, dtype=torch.int32, pin_memory=True)
             self.row_ptr = torch.empty(self.cap_samples + 1, dtype=torch.int64, pin_memory=True)
         if nstreams + 1 > self.cap_streams:
@@ -129,7 +135,10 @@ class FeaturePipeline:
         self.nthreads = nthreads or max(1, min(16, (os.cpu_count() or 4)))
         self._pinned = [_Pinned(), _Pinned()]
         self._turn = 0
-        self._dev = _DeviceBufs(self.device)
+        self._devsets = [_DeviceBufs(self.device), _DeviceBufs(self.device)]
+        self._dev = self._devsets[0]      # scratch for single-shot users (classify)
+        self._copy_stream = torch.cuda.Stream(device=self.device)
+        self._last_mark: torch.cuda.Event | None = None
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         if self.fast:
             rt = GpuRuleTable(converter)
@@ -155,7 +164,7 @@ class FeaturePipeline:
             n, nbytes, nslots, err, err_req = nat.pack_requests(
                 bodies, labeled, self.rules.n_srules, self.rules.n_nrules, table,
                 pin.staging.data_ptr(), pin.cap_bytes, pin.datum_off.data_ptr(),
-                pin.labels.data_ptr() if labeled else 0, pin.row_ptr.data_ptr(),
+                pin.datum_len.data_ptr(), pin.labels.data_ptr() if labeled else 0, pin.row_ptr.data_ptr(),
                 pin.stream_ptr.data_ptr(), pin.cap_samples, self.nthreads)
             if err == 2:
                 pin.ensure(nbytes, n, R)
@@ -186,7 +195,7 @@ class FeaturePipeline:
             n, nbytes, nslots, err, err_req = nat.pack_spans(
                 arena.buf.data_ptr(), offs.ctypes.data, lens.ctypes.data, R, labeled,
                 self.rules.n_srules, self.rules.n_nrules, table, pin.datum_off.data_ptr(),
-                pin.labels.data_ptr() if labeled else 0, pin.row_ptr.data_ptr(),
+                pin.datum_len.data_ptr(), pin.labels.data_ptr() if labeled else 0, pin.row_ptr.data_ptr(),
                 pin.stream_ptr.data_ptr(), pin.cap_samples, self.nthreads)
             if err == 2:
                 pin.ensure(0, n, R)
@@ -200,26 +209,39 @@ class FeaturePipeline:
 
     def _launch(self, pin: "_Pinned", src: torch.Tensor, n: int, nbytes: int, nslots: int,
                 R: int, labeled: bool) -> DeviceBatch:
-        dev = self._dev
+        compute = torch.cuda.current_stream(self.device)
+        dev = self._devsets[self._turn]   # the set not used by the previous batch
+        prev_mark = self._last_mark
+        mark = torch.cuda.Event()
+        mark.record(compute)
+        self._last_mark = mark
         d_buf = dev.get("buf", max(nbytes, 1), torch.uint8)
         d_off = dev.get("datum_off", max(n, 1), torch.int64)
+        d_len = dev.get("datum_len", max(n, 1), torch.int32)
         d_row = dev.get("row_ptr", n + 1, torch.int64)
         d_sp = dev.get("stream_ptr", R + 1, torch.int64)
         d_idx = dev.get("fidx", max(nslots, 1), torch.int32)
         d_val = dev.get("fval", max(nslots, 1), torch.float32)
-        d_buf[:nbytes].copy_(src[:nbytes], non_blocking=True)
-        d_off[:n].copy_(pin.datum_off[:n], non_blocking=True)
-        d_row[:n + 1].copy_(pin.row_ptr[:n + 1], non_blocking=True)
-        d_sp[:R + 1].copy_(pin.stream_ptr[:R + 1], non_blocking=True)
-        d_lab = None
-        if labeled:
-            d_lab = dev.get("labels", max(n, 1), torch.int32)
-            d_lab[:n].copy_(pin.labels[:n], non_blocking=True)
+        d_lab = dev.get("labels", max(n, 1), torch.int32) if labeled else None
+        cs = self._copy_stream
+        if prev_mark is not None:
+            cs.wait_event(prev_mark)
+        else:
+            cs.wait_stream(compute)
+        with torch.cuda.stream(cs):
+            d_buf[:nbytes].copy_(src[:nbytes], non_blocking=True)
+            d_off[:n].copy_(pin.datum_off[:n], non_blocking=True)
+            d_len[:n].copy_(pin.datum_len[:n], non_blocking=True)
+            d_row[:n + 1].copy_(pin.row_ptr[:n + 1], non_blocking=True)
+            d_sp[:R + 1].copy_(pin.stream_ptr[:R + 1], non_blocking=True)
+            if labeled:
+                d_lab[:n].copy_(pin.labels[:n], non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(cs)
+        compute.wait_event(ev)
         pin.event = ev
         if n > 0:
-            hip.fv_hash(d_buf, nbytes, d_off, d_row, n, self.d_srules, self.rules.n_srules,
+            hip.fv_hash(d_buf, nbytes, d_off, d_len, d_row, n, self.d_srules, self.rules.n_srules,
                         self.d_nrules, self.rules.n_nrules, self.d_blob, self.H, d_idx, d_val,
                         self.err)
         return DeviceBatch(n, nslots, R, d_row, d_idx, d_val, d_lab, d_sp)

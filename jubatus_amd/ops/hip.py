@@ -20,8 +20,9 @@ _u64 = ctypes.c_uint64
 _f32 = ctypes.c_float
 
 _SIGS = {
-    "jb_fv_hash": [_c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i32,
-                   _c_void_p, _u64, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_fv_hash": [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32,
+                   _c_void_p, _i32, _c_void_p, _i32, _u64, _c_void_p, _c_void_p, _c_void_p,
+                   _c_void_p],
     "jb_linear_train": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
                         _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p],
     "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
@@ -65,22 +66,23 @@ def _dev(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
                         f"on {t.device}")
 
 
-def fv_hash(buf: torch.Tensor, buf_len: int, datum_off: torch.Tensor, row_ptr: torch.Tensor,
-            n: int, srules: torch.Tensor, n_srules: int, nrules: torch.Tensor, n_nrules: int,
-            blob: torch.Tensor, H: int, out_idx: torch.Tensor, out_val: torch.Tensor,
-            err: torch.Tensor) -> None:
+def fv_hash(buf: torch.Tensor, buf_len: int, datum_off: torch.Tensor, datum_len: torch.Tensor,
+            row_ptr: torch.Tensor, n: int, srules: torch.Tensor, n_srules: int,
+            nrules: torch.Tensor, n_nrules: int, blob: torch.Tensor, H: int,
+            out_idx: torch.Tensor, out_val: torch.Tensor, err: torch.Tensor) -> None:
     _dev(buf, torch.uint8, "buf")
     _dev(datum_off, torch.int64, "datum_off")
+    _dev(datum_len, torch.int32, "datum_len")
     _dev(row_ptr, torch.int64, "row_ptr")
     _dev(out_idx, torch.int32, "out_idx")
     _dev(out_val, torch.float32, "out_val")
-    if datum_off.numel() < n or row_ptr.numel() < n + 1:
+    if datum_off.numel() < n or datum_len.numel() < n or row_ptr.numel() < n + 1:
         raise ValueError("fv_hash: descriptor arrays shorter than n")
     if buf.numel() < buf_len:
         raise ValueError("fv_hash: staging buffer shorter than buf_len")
-    rc = _fn("jb_fv_hash")(_p(buf), buf_len, _p(datum_off), _p(row_ptr), n, _p(srules), n_srules,
-                           _p(nrules), n_nrules, _p(blob), H, _p(out_idx), _p(out_val), _p(err),
-                           _stream())
+    rc = _fn("jb_fv_hash")(_p(buf), buf_len, buf.numel(), _p(datum_off), _p(datum_len),
+                           _p(row_ptr), n, _p(srules), n_srules, _p(nrules), n_nrules, _p(blob),
+                           blob.numel(), H, _p(out_idx), _p(out_val), _p(err), _stream())
     _check(rc, "jb_fv_hash")
 
 

@@ -148,3 +148,28 @@ def test_delete_label_and_pack_roundtrip():
         assert dict(x).keys() == dict(y).keys()
         for k in dict(x):
             assert abs(dict(x)[k] - dict(y)[k]) < 1e-4
+
+
+def test_wide_datums_general_path_and_global_parse():
+    """>64 features per datum (general train path) and >16 KiB per 64 datums
+    (fv_hash falls back from the LDS window to global parsing)."""
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    rng = random.Random(11)
+    data = []
+    for _ in range(150):
+        y = rng.randrange(3)
+        d = {f"k{j}": f"v{y}_{rng.randrange(6)}" + "x" * rng.randrange(40) for j in range(70)}
+        d["num"] = rng.random()
+        data.append((f"c{y}", d))
+    conv = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+            "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 16}
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv), device=_device())
+    c = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv))
+    g.train(data)
+    c.train(data)
+    g.synchronize()
+    g.pipe.check_errors()
+    scale = float(np.abs(c.W).max()) or 1.0
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+    np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3, atol=2e-3 * float(c.P.max()))

@@ -40,9 +40,10 @@ def _pack_call(bodies, labeled, table, rs=1, rn=1):
     lab = np.zeros(4096, np.int32)
     row = np.zeros(4097, np.int64)
     sp = np.zeros(len(bodies) + 1, np.int64)
+    ln = np.zeros(4096, np.int32)
     r = n.pack_requests(bodies, labeled, rs, rn, table, staging.ctypes.data, staging.nbytes,
-                        off.ctypes.data, lab.ctypes.data if labeled else 0, row.ctypes.data,
-                        sp.ctypes.data, 4096, 2)
+                        off.ctypes.data, ln.ctypes.data, lab.ctypes.data if labeled else 0,
+                        row.ctypes.data, sp.ctypes.data, 4096, 2)
     return r, staging, off, lab, row, sp
 
 
