@@ -84,6 +84,8 @@ def main() -> None:
     ap.add_argument("--pools", type=int, default=4, help="distinct synthetic batches cycled")
     ap.add_argument("--mix-every", type=int, default=1)
     ap.add_argument("--latency-iters", type=int, default=300)
+    ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
+                    help="how concurrent request streams update shared rows")
     args = ap.parse_args()
 
     import torch
@@ -105,7 +107,8 @@ def main() -> None:
     cfg = json.loads(json.dumps(AROW_CONFIG))
     cfg["converter"]["hash_max_size"] = 1 << args.hash_bits
     conv = DatumToFvConverter(cfg["converter"])
-    clf = LinearClassifier(cfg["method"], cfg["parameter"], conv, device=device)
+    clf = LinearClassifier(cfg["method"], cfg["parameter"], conv, device=device,
+                           concurrent_update=args.update_mode)
     for y in range(args.labels):  # same label order on every rank (set_label, as a client would)
         clf.set_label(f"label{y}")
 
@@ -202,6 +205,7 @@ def main() -> None:
                 "hash_max_size": 1 << args.hash_bits,
                 "labels": args.labels,
                 "mix": "linear (RCCL all-reduce mean) every step" if world > 1 else "standalone",
+                "concurrent_update": args.update_mode,
             },
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),

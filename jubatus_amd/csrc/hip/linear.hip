@@ -27,14 +27,20 @@
 // result of a single stream is exactly the sequential online update.
 // Different streams (concurrent train requests) update the shared table
 // lock-free - the GPU analogue of the reference's giant-lock-free classifier
-// (ChangeLog.rst:152) - using memory-side float atomics so that no update is
-// lost. Loads use the agent-scope (sc1) path so a stream always sees the
-// latest L2 contents instead of a stale L1 line.
+// (ChangeLog.rst:152). Update modes (template MODE):
+//   kExact   one stream: plain stores, drained before the next sample
+//   kAtomic  concurrent streams, memory-side float atomics: no update is lost
+//   kHogwild concurrent streams, plain stores of (read value + increment):
+//            racing updates of a hot row may be lost (Hogwild), but the
+//            precision form keeps every P positive
+// Loads use the agent-scope (sc1) path so a stream sees the latest L2
+// contents instead of a stale L1 line.
 #include "jb_device.hpp"
 
 namespace jb {
 
 enum Method : int { PERCEPTRON = 0, PA = 1, PA1 = 2, PA2 = 3, CW = 4, AROW = 5, NHERD = 6 };
+enum UpdateMode : int { kExact = 0, kAtomic = 1, kHogwild = 2 };
 
 __device__ __forceinline__ float ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -124,14 +130,14 @@ __device__ __forceinline__ float dprec(int method, float beta, float x, float s)
 }
 
 // apply the update of one feature (lane-per-feature form)
-template <int LC, bool CONC>
+template <int LC, int MODE>
 __device__ __forceinline__ void apply_feature(float* W, float* P, int32_t idx, float x, int y,
                                               int lstar, bool use_s, int method, float tau,
                                               float beta, float a, float b, float wy, float wl) {
   const int64_t row = (int64_t)idx * LC;
   const float dwy = use_s ? tau * a * x : tau * x;
   const float dwl = use_s ? -tau * b * x : -tau * x;
-  if (CONC) {
+  if (MODE == kAtomic) {
     atomicAdd(W + row + y, dwy);
     if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
     if (use_s) {
@@ -165,7 +171,7 @@ struct Stage {
   static constexpr int NMAX = LC <= 64 ? 1024 / LC : 0;
 };
 
-template <int LC, bool CONC>
+template <int LC, int MODE>
 __global__ __launch_bounds__(256) void linear_train_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
           a = 1.f / sP[wv][lane * LC + y];
           b = lstar >= 0 ? 1.f / sP[wv][lane * LC + lstar] : 0.f;
         }
-        if (!CONC) {
+        if (MODE != kAtomic) {
           wy = sW[wv][lane * LC + y];
           wl = lstar >= 0 ? sW[wv][lane * LC + lstar] : 0.f;
         }
@@ -259,10 +265,10 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
       float tau = 0.f, beta = 0.f;
       if (step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) {
         if (mine)
-          apply_feature<LC, CONC>(W, P, my_idx, my_x, y, lstar, use_s, method, tau, beta, a, b,
+          apply_feature<LC, MODE>(W, P, my_idx, my_x, y, lstar, use_s, method, tau, beta, a, b,
                                   wy, wl);
         // the next sample of this stream must observe these stores
-        if (!CONC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_wave_barrier();
       continue;
@@ -314,10 +320,13 @@ __global__ __launch_bounds__(256) void linear_train_kernel(
       const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
       const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
       float wy = 0.f, wl = 0.f;
-      if (!CONC) { wy = ld_agent(W + row + y); wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f; }
-      apply_feature<LC, CONC>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, wy, wl);
+      if (MODE != kAtomic) {
+        wy = ld_agent(W + row + y);
+        wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f;
+      }
+      apply_feature<LC, MODE>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, wy, wl);
     }
-    if (!CONC) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 
@@ -370,21 +379,20 @@ __global__ void scale_kernel(float* __restrict__ p, int64_t n, float a) {
 extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                float* W, float* S, const int32_t* active, int LC, int method,
-                               float C, int concurrent, hipStream_t stream) {
+                               float C, int mode, hipStream_t stream) {
   if (nstreams <= 0) return 0;
   const int threads = 256;
   const int blocks = (nstreams * 64 + threads - 1) / threads;
-#define JB_TRAIN(L)                                                                            \
-  if (concurrent)                                                                              \
-    hipLaunchKernelGGL((jb::linear_train_kernel<L, true>), dim3(blocks), dim3(threads), 0,    \
-                       stream, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,       \
-                       active, method, C);                                                    \
-  else                                                                                         \
-    hipLaunchKernelGGL((jb::linear_train_kernel<L, false>), dim3(blocks), dim3(threads), 0,   \
-                       stream, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,       \
-                       active, method, C);
+#define JB_TRAIN_M(L, M)                                                                     \
+  hipLaunchKernelGGL((jb::linear_train_kernel<L, M>), dim3(blocks), dim3(threads), 0, stream,  \
+                     row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active, method, C);
+#define JB_TRAIN(L)                                        \
+  if (mode == jb::kAtomic) { JB_TRAIN_M(L, jb::kAtomic) }  \
+  else if (mode == jb::kHogwild) { JB_TRAIN_M(L, jb::kHogwild) } \
+  else { JB_TRAIN_M(L, jb::kExact) }
   JB_LC_DISPATCH(LC, JB_TRAIN)
 #undef JB_TRAIN
+#undef JB_TRAIN_M
   return (int)hipGetLastError();
 }
 

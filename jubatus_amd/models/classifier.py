@@ -50,7 +50,7 @@ def _label_cap(n: int) -> int:
 
 class LinearClassifier:
     def __init__(self, method: str, parameter: dict | None, converter: DatumToFvConverter,
-                 device: Any = None):
+                 device: Any = None, concurrent_update: str = "atomic"):
         if method not in LINEAR_METHODS:
             raise ClassifierConfigError(f"unknown linear method: {method}")
         parameter = dict(parameter or {})
@@ -62,6 +62,9 @@ class LinearClassifier:
         self.C = float(parameter.get("regularization_weight", 1.0))
         if method not in ("perceptron", "PA") and not self.C > 0:
             raise ClassifierConfigError("regularization_weight must be positive")
+        if concurrent_update not in ("atomic", "hogwild"):
+            raise ClassifierConfigError("concurrent_update must be 'atomic' or 'hogwild'")
+        self.concurrent_update = concurrent_update
         self.conv = converter
         self.H = converter.hash_max_size
         self.use_s = self.mid in lo.USES_COVARIANCE
@@ -121,13 +124,19 @@ class LinearClassifier:
         self._label_version = v
 
     # -------------------------------------------------------------- train
+    def _mode(self, nstreams: int) -> int:
+        from ..ops import hip
+        if nstreams <= 1:
+            return hip.UPDATE_EXACT
+        return hip.UPDATE_MODES[self.concurrent_update]
+
     def _train_batch(self, b) -> int:
         from ..ops import hip
         self._sync_labels()
         if b.n:
             hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
                              self.W, self.P, self.active, self.mid, self.C,
-                             concurrent=b.nstreams > 1)
+                             mode=self._mode(b.nstreams))
         return b.n
 
     def train_arena(self, arena, offs, lens) -> int:
@@ -181,7 +190,7 @@ class LinearClassifier:
             b = self.pipe.from_rows(rows, labs, sizes)
             hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
                              self.W, self.P, self.active, self.mid, self.C,
-                             concurrent=b.nstreams > 1)
+                             mode=self._mode(b.nstreams))
             return
         for (idx, val), y in zip(rows, labs):
             lo.train_one(self.W, self.P, np.asarray(idx, np.int64), np.asarray(val, np.float32),

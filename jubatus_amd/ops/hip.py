@@ -33,6 +33,8 @@ _SIGS = {
 _fns: dict = {}
 
 LABEL_CAPS = (8, 16, 32, 64, 128, 256, 512, 1024)
+UPDATE_EXACT, UPDATE_ATOMIC, UPDATE_HOGWILD = 0, 1, 2
+UPDATE_MODES = {"exact": UPDATE_EXACT, "atomic": UPDATE_ATOMIC, "hogwild": UPDATE_HOGWILD}
 METHODS = {"perceptron": 0, "PA": 1, "PA1": 2, "PA2": 3, "CW": 4, "AROW": 5, "NHERD": 6}
 
 
@@ -89,7 +91,8 @@ def fv_hash(buf: torch.Tensor, buf_len: int, datum_off: torch.Tensor, datum_len:
 def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
                  labels: torch.Tensor, stream_ptr: torch.Tensor, nstreams: int, W: torch.Tensor,
                  S: torch.Tensor | None, active: torch.Tensor, method: int, C: float,
-                 concurrent: bool) -> None:
+                 mode: int) -> None:
+    """mode: UPDATE_EXACT (single stream), UPDATE_ATOMIC or UPDATE_HOGWILD."""
     LC = W.shape[1]
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
@@ -105,7 +108,7 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
         raise ValueError("stream_ptr shorter than nstreams+1")
     rc = _fn("jb_linear_train")(_p(row_ptr), _p(fidx), _p(fval), _p(labels), _p(stream_ptr),
                                 nstreams, _p(W), _p(S) if S is not None else None, _p(active), LC,
-                                method, float(C), 1 if concurrent else 0, _stream())
+                                method, float(C), int(mode), _stream())
     _check(rc, "jb_linear_train")
 
 

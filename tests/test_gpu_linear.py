@@ -111,11 +111,13 @@ def test_many_labels_capacity_growth():
     np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=3e-3, atol=3e-4)
 
 
-def test_concurrent_streams_learn():
+@pytest.mark.parametrize("mode", ["atomic", "hogwild"])
+def test_concurrent_streams_learn(mode):
     from jubatus_amd.models.classifier import LinearClassifier
 
     conv = DatumToFvConverter(CONV)
-    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, conv, device=_device())
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, conv, device=_device(),
+                         concurrent_update=mode)
     data = _data(4096, seed=7)
     from jubatus_amd.fv_converter.datum import Datum
     bodies = [msgpack.packb([[l, Datum(d).to_msgpack()] for l, d in data[i:i + 32]],
@@ -163,7 +165,7 @@ def test_wide_datums_general_path_and_global_parse():
         d["num"] = rng.random()
         data.append((f"c{y}", d))
     conv = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
-            "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 16}
+            "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 22}  # collision-free
     g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv), device=_device())
     c = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv))
     g.train(data)
