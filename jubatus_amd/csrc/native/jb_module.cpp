@@ -4,6 +4,7 @@
 
 #include "jb_hash.hpp"
 #include "jb_pack.hpp"
+#include "jb_rpc.hpp"
 
 namespace py = pybind11;
 
@@ -72,6 +73,61 @@ uint64_t fnv1a64(py::bytes name) {
   return jb::fnv_bytes(jb::kFnvOffset, (const uint8_t*)s.data(), s.size());
 }
 
+// Python face of jb::RpcServer. handler(method: str, params: bytes,
+// msgid: int, notify: bool) -> bytes | None (the complete encoded response).
+class PyRpcServer {
+ public:
+  PyRpcServer(py::object handler, int nworkers, double idle_timeout)
+      : handler_(std::move(handler)) {
+    srv_.reset(new jb::RpcServer(
+        [this](const jb::RpcRequest& r) -> std::string {
+          py::gil_scoped_acquire gil;
+          try {
+            py::object res = handler_(py::str(r.method), py::bytes(r.params), r.msgid, r.notify);
+            if (res.is_none()) return std::string();
+            return res.cast<std::string>();
+          } catch (py::error_already_set& e) {
+            // last-resort error response: [1, msgid, "<error>", nil] (fixarray 4)
+            std::string what = e.what();
+            if (what.size() > 255) what.resize(255);
+            std::string out;
+            out.push_back((char)0x94);
+            out.push_back((char)0x01);
+            out.push_back((char)0xce);
+            for (int i = 3; i >= 0; --i) out.push_back((char)((r.msgid >> (8 * i)) & 0xff));
+            out.push_back((char)0xd9);
+            out.push_back((char)what.size());
+            out += what;
+            out.push_back((char)0xc0);
+            return r.notify ? std::string() : out;
+          }
+        },
+        nworkers, idle_timeout));
+  }
+  ~PyRpcServer() {
+    py::gil_scoped_release nogil;
+    srv_.reset();
+  }
+  int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
+  void start() { srv_->start(); }
+  void stop() {
+    py::gil_scoped_release nogil;
+    srv_->stop();
+  }
+  bool running() const { return srv_->running(); }
+  uint64_t served() const { return srv_->requests_served(); }
+  uint64_t connections() const { return srv_->connections(); }
+
+ private:
+  py::object handler_;
+  std::unique_ptr<jb::RpcServer> srv_;
+};
+
+int64_t frame(py::buffer b) {
+  py::buffer_info bi = b.request();
+  return jb::msgpack_frame((const uint8_t*)bi.ptr, (size_t)(bi.size * bi.itemsize));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_jubatus_native, m) {
@@ -91,6 +147,16 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("add_count", &jb::LabelTable::add_count);
   m.def("pack_requests", &pack, "scan msgpack request bodies into a device-ready batch");
   m.def("pack_spans", &pack_spans, "zero-copy scan of request spans inside one pinned arena");
+  py::class_<PyRpcServer>(m, "RpcServer")
+      .def(py::init<py::object, int, double>(), py::arg("handler"), py::arg("nworkers") = 2,
+           py::arg("idle_timeout") = 0.0)
+      .def("listen", &PyRpcServer::listen)
+      .def("start", &PyRpcServer::start)
+      .def("stop", &PyRpcServer::stop)
+      .def("running", &PyRpcServer::running)
+      .def("served", &PyRpcServer::served)
+      .def("connections", &PyRpcServer::connections);
+  m.def("msgpack_frame", &frame, "length of the first complete msgpack object (0: incomplete, -1: bad)");
   m.def("crc32", &crc32, py::arg("data"), py::arg("init") = 0u);
   m.def("md5_hex", &md5_hex);
   m.def("feature_index", &feature_index);

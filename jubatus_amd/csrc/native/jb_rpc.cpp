@@ -1,0 +1,385 @@
+// See jb_rpc.hpp.
+#include "jb_rpc.hpp"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <signal.h>
+#include <string.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <stdexcept>
+
+#include "jb_msgpack.hpp"
+
+namespace jb {
+
+namespace {
+
+double now_sec() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+// skip one object: 1 ok, 0 incomplete, -1 malformed
+int skip_status(Cursor& c, int depth) {
+  if (depth > 128) return -1;
+  if (!c.need(1)) return 0;
+  const uint8_t t = *c.p;
+  auto take = [&](uint64_t n) -> int {
+    if (!c.need(n)) return 0;
+    c.p += n;
+    return 1;
+  };
+  auto be = [&](int off, int nb) -> uint64_t {
+    uint64_t v = 0;
+    for (int i = 0; i < nb; ++i) v = (v << 8) | c.p[off + i];
+    return v;
+  };
+  if (t <= 0x7f || t >= 0xe0 || t == 0xc0 || t == 0xc2 || t == 0xc3) return take(1);
+  if ((t & 0xe0) == 0xa0) return take(1 + (t & 0x1f));
+  if ((t & 0xf0) == 0x90 || (t & 0xf0) == 0x80) {
+    uint64_t n = (t & 0x0f) * (((t & 0xf0) == 0x80) ? 2 : 1);
+    c.p += 1;
+    for (uint64_t i = 0; i < n; ++i) {
+      int r = skip_status(c, depth + 1);
+      if (r <= 0) return r;
+    }
+    return 1;
+  }
+  switch (t) {
+    case 0xcc: case 0xd0: return take(2);
+    case 0xcd: case 0xd1: return take(3);
+    case 0xce: case 0xd2: case 0xca: return take(5);
+    case 0xcf: case 0xd3: case 0xcb: return take(9);
+    case 0xd9: case 0xc4: if (!c.need(2)) return 0; return take(2 + be(1, 1));
+    case 0xda: case 0xc5: if (!c.need(3)) return 0; return take(3 + be(1, 2));
+    case 0xdb: case 0xc6: if (!c.need(5)) return 0; return take(5 + be(1, 4));
+    case 0xd4: return take(3); case 0xd5: return take(4); case 0xd6: return take(6);
+    case 0xd7: return take(10); case 0xd8: return take(18);
+    case 0xc7: if (!c.need(2)) return 0; return take(3 + be(1, 1));
+    case 0xc8: if (!c.need(3)) return 0; return take(4 + be(1, 2));
+    case 0xc9: if (!c.need(5)) return 0; return take(6 + be(1, 4));
+    case 0xdc: case 0xdd: case 0xde: case 0xdf: {
+      const int nb = (t == 0xdc || t == 0xde) ? 2 : 4;
+      if (!c.need(1 + nb)) return 0;
+      uint64_t n = be(1, nb) * ((t == 0xde || t == 0xdf) ? 2 : 1);
+      c.p += 1 + nb;
+      for (uint64_t i = 0; i < n; ++i) {
+        int r = skip_status(c, depth + 1);
+        if (r <= 0) return r;
+      }
+      return 1;
+    }
+    default: return -1;
+  }
+}
+
+void set_nonblock(int fd) {
+  int fl = fcntl(fd, F_GETFL, 0);
+  fcntl(fd, F_SETFL, fl | O_NONBLOCK);
+}
+
+}  // namespace
+
+int64_t msgpack_frame(const uint8_t* p, size_t n) {
+  Cursor c{p, p + n};
+  int r = skip_status(c, 0);
+  if (r == 0) return 0;
+  if (r < 0) return -1;
+  return (int64_t)(c.p - p);
+}
+
+RpcServer::RpcServer(Handler h, int nworkers, double idle_timeout_sec)
+    : handler_(std::move(h)), nworkers_(nworkers < 1 ? 1 : nworkers),
+      idle_timeout_(idle_timeout_sec) {
+  signal(SIGPIPE, SIG_IGN);
+}
+
+RpcServer::~RpcServer() { stop(); }
+
+int RpcServer::listen(const std::string& addr, int port) {
+  listen_fd_ = socket(AF_INET, SOCK_STREAM, 0);
+  if (listen_fd_ < 0) throw std::runtime_error("socket() failed");
+  int one = 1;
+  setsockopt(listen_fd_, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_port = htons((uint16_t)port);
+  if (addr.empty() || addr == "0.0.0.0") sa.sin_addr.s_addr = htonl(INADDR_ANY);
+  else if (inet_pton(AF_INET, addr.c_str(), &sa.sin_addr) != 1)
+    throw std::runtime_error("bad bind address: " + addr);
+  if (::bind(listen_fd_, (sockaddr*)&sa, sizeof(sa)) != 0) {
+    int e = errno;
+    ::close(listen_fd_);
+    listen_fd_ = -1;
+    throw std::runtime_error(std::string("bind failed: ") + strerror(e));
+  }
+  if (::listen(listen_fd_, 1024) != 0) throw std::runtime_error("listen failed");
+  set_nonblock(listen_fd_);
+  socklen_t len = sizeof(sa);
+  getsockname(listen_fd_, (sockaddr*)&sa, &len);
+  return ntohs(sa.sin_port);
+}
+
+void RpcServer::start() {
+  if (listen_fd_ < 0) throw std::runtime_error("listen() first");
+  epfd_ = epoll_create1(0);
+  wake_fd_ = eventfd(0, EFD_NONBLOCK);
+  epoll_event ev{};
+  ev.events = EPOLLIN;
+  ev.data.u64 = 0;  // listen socket
+  epoll_ctl(epfd_, EPOLL_CTL_ADD, listen_fd_, &ev);
+  ev.data.u64 = UINT64_MAX;  // wakeup
+  epoll_ctl(epfd_, EPOLL_CTL_ADD, wake_fd_, &ev);
+  running_.store(true);
+  io_ = std::thread([this] { io_loop(); });
+  for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker_loop(); });
+}
+
+void RpcServer::stop() {
+  if (!running_.exchange(false)) return;
+  uint64_t one = 1;
+  if (wake_fd_ >= 0) { ssize_t r = write(wake_fd_, &one, 8); (void)r; }
+  qcv_.notify_all();
+  if (io_.joinable()) io_.join();
+  for (auto& w : workers_) if (w.joinable()) w.join();
+  workers_.clear();
+  {
+    std::lock_guard<std::mutex> g(cmu_);
+    for (auto& kv : conns_) ::close(kv.second->fd);
+    conns_.clear();
+  }
+  if (listen_fd_ >= 0) ::close(listen_fd_);
+  if (epfd_ >= 0) ::close(epfd_);
+  if (wake_fd_ >= 0) ::close(wake_fd_);
+  listen_fd_ = epfd_ = wake_fd_ = -1;
+}
+
+void RpcServer::close_conn(uint64_t id) {
+  std::shared_ptr<Conn> c;
+  {
+    std::lock_guard<std::mutex> g(cmu_);
+    auto it = conns_.find(id);
+    if (it == conns_.end()) return;
+    c = it->second;
+    conns_.erase(it);
+  }
+  {
+    std::lock_guard<std::mutex> g(c->wmu);
+    c->closed = true;
+  }
+  epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
+  ::close(c->fd);
+  nconn_.fetch_sub(1);
+}
+
+void RpcServer::io_loop() {
+  epoll_event evs[256];
+  double last_sweep = now_sec();
+  while (running_.load()) {
+    int n = epoll_wait(epfd_, evs, 256, 100);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t key = evs[i].data.u64;
+      if (key == UINT64_MAX) {
+        uint64_t v;
+        ssize_t r = read(wake_fd_, &v, 8);
+        (void)r;
+        std::vector<uint64_t> ids;
+        {
+          std::lock_guard<std::mutex> g(wq_mu_);
+          ids.swap(want_write_);
+        }
+        for (uint64_t id : ids) {
+          std::shared_ptr<Conn> c;
+          {
+            std::lock_guard<std::mutex> g(cmu_);
+            auto it = conns_.find(id);
+            if (it != conns_.end()) c = it->second;
+          }
+          if (!c) continue;
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLOUT;
+          ev.data.u64 = id;
+          epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+        }
+        continue;
+      }
+      if (key == 0) {  // accept
+        for (;;) {
+          int fd = accept(listen_fd_, nullptr, nullptr);
+          if (fd < 0) break;
+          set_nonblock(fd);
+          int one = 1;
+          setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+          auto c = std::make_shared<Conn>();
+          c->fd = fd;
+          c->last_active = now_sec();
+          {
+            std::lock_guard<std::mutex> g(cmu_);
+            c->id = next_id_++;
+            conns_[c->id] = c;
+          }
+          nconn_.fetch_add(1);
+          epoll_event ev{};
+          ev.events = EPOLLIN;
+          ev.data.u64 = c->id;
+          epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
+        }
+        continue;
+      }
+      std::shared_ptr<Conn> c;
+      {
+        std::lock_guard<std::mutex> g(cmu_);
+        auto it = conns_.find(key);
+        if (it != conns_.end()) c = it->second;
+      }
+      if (!c) continue;
+      if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+        // drain what is readable first (a peer may send then close)
+        on_readable(c);
+        close_conn(key);
+        continue;
+      }
+      if (evs[i].events & EPOLLIN) on_readable(c);
+      if (evs[i].events & EPOLLOUT) {
+        flush(c);
+        std::lock_guard<std::mutex> g(c->wmu);
+        if (c->wbuf.empty() && !c->closed) {
+          epoll_event ev{};
+          ev.events = EPOLLIN;
+          ev.data.u64 = c->id;
+          epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+          c->want_write = false;
+        }
+      }
+    }
+    const double t = now_sec();
+    if (idle_timeout_ > 0 && t - last_sweep > 1.0) {
+      last_sweep = t;
+      std::vector<uint64_t> idle;
+      {
+        std::lock_guard<std::mutex> g(cmu_);
+        for (auto& kv : conns_)
+          if (t - kv.second->last_active > idle_timeout_) idle.push_back(kv.first);
+      }
+      for (uint64_t id : idle) close_conn(id);
+    }
+  }
+}
+
+void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
+  char tmp[65536];
+  bool eof = false;
+  for (;;) {
+    ssize_t r = ::read(c->fd, tmp, sizeof(tmp));
+    if (r > 0) { c->rbuf.append(tmp, (size_t)r); continue; }
+    if (r == 0) eof = true;
+    else if (errno == EINTR) continue;
+    else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+    break;
+  }
+  c->last_active = now_sec();
+  size_t pos = 0;
+  while (pos < c->rbuf.size()) {
+    const uint8_t* p = (const uint8_t*)c->rbuf.data() + pos;
+    const size_t avail = c->rbuf.size() - pos;
+    int64_t len = msgpack_frame(p, avail);
+    if (len == 0) break;
+    if (len < 0) { eof = true; break; }
+    Cursor cur{p, p + len};
+    uint32_t n;
+    double type = -1, msgid = 0;
+    const uint8_t* m = nullptr;
+    uint32_t mlen = 0;
+    bool ok = cur.array(&n) && (n == 4 || n == 3) && cur.number(&type);
+    if (ok && n == 4 && type == 0) {
+      ok = cur.number(&msgid) && cur.raw(&m, &mlen);
+      if (ok) {
+        RpcRequest req{c->id, (uint32_t)msgid, false, std::string((const char*)m, mlen),
+                       std::string((const char*)cur.p, (size_t)(p + len - cur.p))};
+        std::lock_guard<std::mutex> g(qmu_);
+        queue_.push_back(std::move(req));
+        qcv_.notify_one();
+      }
+    } else if (ok && n == 3 && type == 2) {
+      ok = cur.raw(&m, &mlen);
+      if (ok) {
+        RpcRequest req{c->id, 0, true, std::string((const char*)m, mlen),
+                       std::string((const char*)cur.p, (size_t)(p + len - cur.p))};
+        std::lock_guard<std::mutex> g(qmu_);
+        queue_.push_back(std::move(req));
+        qcv_.notify_one();
+      }
+    }
+    // responses (type 1) sent to a server are ignored
+    pos += (size_t)len;
+  }
+  if (pos) c->rbuf.erase(0, pos);
+  if (eof) close_conn(c->id);
+}
+
+void RpcServer::flush(const std::shared_ptr<Conn>& c) {
+  std::lock_guard<std::mutex> g(c->wmu);
+  while (!c->wbuf.empty() && !c->closed) {
+    ssize_t w = ::send(c->fd, c->wbuf.data(), c->wbuf.size(), MSG_NOSIGNAL);
+    if (w > 0) { c->wbuf.erase(0, (size_t)w); continue; }
+    if (w < 0 && errno == EINTR) continue;
+    break;  // EAGAIN or error: the IO thread retries on EPOLLOUT / HUP
+  }
+}
+
+void RpcServer::send_response(uint64_t conn_id, const std::string& bytes) {
+  std::shared_ptr<Conn> c;
+  {
+    std::lock_guard<std::mutex> g(cmu_);
+    auto it = conns_.find(conn_id);
+    if (it == conns_.end()) return;  // client went away
+    c = it->second;
+  }
+  bool arm = false;
+  {
+    std::lock_guard<std::mutex> g(c->wmu);
+    if (c->closed) return;
+    c->wbuf.append(bytes);
+  }
+  flush(c);
+  {
+    std::lock_guard<std::mutex> g(c->wmu);
+    if (!c->wbuf.empty() && !c->want_write) { c->want_write = true; arm = true; }
+  }
+  if (arm) {
+    {
+      std::lock_guard<std::mutex> g(wq_mu_);
+      want_write_.push_back(conn_id);
+    }
+    uint64_t one = 1;
+    ssize_t r = write(wake_fd_, &one, 8);
+    (void)r;
+  }
+}
+
+void RpcServer::worker_loop() {
+  for (;;) {
+    RpcRequest req;
+    {
+      std::unique_lock<std::mutex> g(qmu_);
+      qcv_.wait(g, [this] { return !queue_.empty() || !running_.load(); });
+      if (!running_.load()) return;
+      req = std::move(queue_.front());
+      queue_.pop_front();
+    }
+    std::string resp = handler_(req);
+    served_.fetch_add(1);
+    if (!req.notify && !resp.empty()) send_response(req.conn_id, resp);
+  }
+}
+
+}  // namespace jb

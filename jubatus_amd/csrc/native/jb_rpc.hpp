@@ -1,0 +1,98 @@
+// msgpack-RPC transport (server side), native C++17.
+//
+// Reference: jubatus/server/common/mprpc/rpc_server.{hpp,cpp} (dispatcher
+// over msgpack-rpc/mpio). Wire protocol (msgpack-RPC):
+//   request      [0, msgid, method, params]
+//   response     [1, msgid, error, result]
+//   notification [2, method, params]
+//
+// Design: one epoll IO thread owns every socket (accept, non-blocking reads,
+// message framing by a validating skip-walk, deferred writes); complete
+// requests go to a queue served by `nworkers` threads that call the
+// dispatcher callback (Python, with the GIL) and hand back the encoded
+// response. Request parameter bytes are copied once out of the socket buffer
+// into an owned string (or, for the train fast path, into a pinned arena by
+// the callback) - never decoded in C++ unless the callback asks for it.
+#pragma once
+#include <stdint.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace jb {
+
+struct RpcRequest {
+  uint64_t conn_id;
+  uint32_t msgid;
+  bool notify;
+  std::string method;
+  std::string params;  // msgpack array bytes
+};
+
+class RpcServer {
+ public:
+  // handler(request) -> encoded response bytes (empty for notifications)
+  using Handler = std::function<std::string(const RpcRequest&)>;
+
+  RpcServer(Handler h, int nworkers, double idle_timeout_sec);
+  ~RpcServer();
+  // returns the bound port (useful with port 0)
+  int listen(const std::string& addr, int port);
+  void start();
+  void stop();
+  bool running() const { return running_.load(); }
+  uint64_t requests_served() const { return served_.load(); }
+  uint64_t connections() const { return nconn_.load(); }
+
+ private:
+  struct Conn {
+    int fd;
+    uint64_t id;
+    std::string rbuf;
+    std::mutex wmu;
+    std::string wbuf;  // pending output
+    bool want_write = false;
+    bool closed = false;
+    double last_active = 0;
+  };
+  void io_loop();
+  void worker_loop();
+  void on_readable(const std::shared_ptr<Conn>& c);
+  void flush(const std::shared_ptr<Conn>& c);
+  void close_conn(uint64_t id);
+  void send_response(uint64_t conn_id, const std::string& bytes);
+
+  Handler handler_;
+  int nworkers_;
+  double idle_timeout_;
+  int listen_fd_ = -1;
+  int epfd_ = -1;
+  int wake_fd_ = -1;
+  std::atomic<bool> running_{false};
+  std::atomic<uint64_t> served_{0};
+  std::atomic<uint64_t> nconn_{0};
+  std::thread io_;
+  std::vector<std::thread> workers_;
+  std::mutex cmu_;
+  std::unordered_map<uint64_t, std::shared_ptr<Conn>> conns_;
+  uint64_t next_id_ = 1;
+  std::mutex qmu_;
+  std::condition_variable qcv_;
+  std::deque<RpcRequest> queue_;
+  std::mutex wq_mu_;
+  std::vector<uint64_t> want_write_;  // conns the IO thread must arm for EPOLLOUT
+};
+
+// Frame one complete msgpack object at the head of [p, p+n): returns its
+// length, 0 if incomplete, -1 if malformed.
+int64_t msgpack_frame(const uint8_t* p, size_t n);
+
+}  // namespace jb
