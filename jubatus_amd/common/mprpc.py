@@ -85,8 +85,7 @@ class RpcTypeError(RpcError):
     pass
 
 
-class ArgumentError(TypeError):
-    """Raised by server-side handlers for bad arguments -> ARGUMENT_ERROR."""
+from .exceptions import ArgumentError  # noqa: E402  (re-export)
 
 
 def error_from_wire(err: Any, host=None, port=None) -> RpcError:

@@ -8,6 +8,8 @@ from __future__ import annotations
 
 from typing import Any, Iterable
 
+from ..common.exceptions import ArgumentError
+
 
 class Datum:
     __slots__ = ("string_values", "num_values", "binary_values")
@@ -31,7 +33,7 @@ class Datum:
         elif isinstance(value, (int, float)):
             self.num_values.append((key, float(value)))
         else:
-            raise TypeError(f"unsupported datum value type {type(value)!r} for key {key!r}")
+            raise ArgumentError(f"unsupported datum value type {type(value)!r} for key {key!r}")
         return self
 
     add_string = add
@@ -49,14 +51,21 @@ class Datum:
         if isinstance(obj, Datum):
             return obj
         if not isinstance(obj, (list, tuple)) or len(obj) < 2:
-            raise TypeError("datum must be an array [string_values, num_values, binary_values]")
+            raise ArgumentError("datum must be an array [string_values, num_values, binary_values]")
+        try:
+            return cls._parse(obj, d)
+        except (ValueError, TypeError) as e:
+            raise ArgumentError(f"malformed datum: {e}") from e
+
+    @classmethod
+    def _parse(cls, obj: Any, d: "Datum") -> "Datum":
         for kv in obj[0]:
             k, v = kv
             d.string_values.append((_s(k), _s(v)))
         for kv in obj[1]:
             k, v = kv
             if isinstance(v, bool) or not isinstance(v, (int, float)):
-                raise TypeError("num_values value must be a number")
+                raise ArgumentError("num_values value must be a number")
             d.num_values.append((_s(k), float(v)))
         if len(obj) >= 3:
             for kv in obj[2]:
@@ -77,7 +86,7 @@ def _s(x: Any) -> str:
         return x
     if isinstance(x, (bytes, bytearray)):
         return bytes(x).decode("utf-8", errors="surrogateescape")
-    raise TypeError(f"expected string, got {type(x)!r}")
+    raise ArgumentError(f"expected string, got {type(x)!r}")
 
 
 def _b(x: Any) -> bytes:
@@ -85,7 +94,7 @@ def _b(x: Any) -> bytes:
         return bytes(x)
     if isinstance(x, str):
         return x.encode("utf-8", errors="surrogateescape")
-    raise TypeError(f"expected raw, got {type(x)!r}")
+    raise ArgumentError(f"expected raw, got {type(x)!r}")
 
 
 def as_datum(x: Any) -> Datum:

@@ -1,0 +1,155 @@
+"""jubaclassifier server glue (reference C28: jubatus/server/server/classifier_serv.cpp).
+
+Config: {"method", "parameter", "converter"} (classifier_serv.cpp:56-65,91-117).
+Linear methods (perceptron, PA, PA1, PA2, CW, AROW, NHERD) run on the
+hashed-table driver (models/classifier.py); NN / cosine / euclidean run on
+the nearest-neighbor classifier (models/nn_classifier.py).
+
+RPC methods (classifier.idl): train, classify, get_labels, set_label, clear,
+delete_label; all NOLOCK at the dispatcher with a brief write lock to bump
+the update counter (classifier_serv.cpp:131-134).
+"""
+from __future__ import annotations
+
+import json
+import math
+
+from ..common.exceptions import ArgumentError, ConfigNotSet
+from ..common.mprpc import split_params
+from ..framework.device import select_device
+from ..framework.server_base import ServerBase
+from ..fv_converter.converter import DatumToFvConverter
+from ..fv_converter.datum import Datum
+from ..models.classifier import LINEAR_METHODS, LinearClassifier
+from ..utils import logger
+
+log = logger.get_logger("classifier")
+
+NN_METHODS = ("NN", "nearest_neighbor", "cosine", "euclidean")
+
+
+def build_classifier(cfg: dict, device):
+    method = cfg.get("method")
+    if not isinstance(method, str):
+        raise ValueError("config: 'method' is required")
+    conv = DatumToFvConverter(cfg.get("converter") or {})
+    param = cfg.get("parameter")
+    if method in LINEAR_METHODS:
+        return LinearClassifier(method, param, conv, device=device)
+    if method in NN_METHODS:
+        from ..models.nn_classifier import NNClassifier
+        return NNClassifier(method, param or {}, conv, device=device)
+    raise ValueError(f"unsupported classifier method: {method}")
+
+
+def labeled_data(data) -> list[tuple[str, Datum]]:
+    if not isinstance(data, list):
+        raise ArgumentError("train: data must be a list")
+    out = []
+    for item in data:
+        if not isinstance(item, (list, tuple)) or len(item) != 2 or not isinstance(item[0], str):
+            raise ArgumentError("labeled_datum must be [label, datum]")
+        out.append((item[0], Datum.from_msgpack(item[1])))
+    return out
+
+
+class ClassifierServ(ServerBase):
+    type_name = "classifier"
+
+    def __init__(self, argv, coord=None):
+        super().__init__(argv, coord)
+        self.clf = None
+        self.config = None
+        self.device = select_device(argv)
+
+    def check_set_config(self) -> None:
+        if self.clf is None:
+            raise ConfigNotSet()
+
+    # ------------------------------------------------------------- config
+    def set_config(self, config: str) -> None:
+        cfg = json.loads(config)
+        self.clf = build_classifier(cfg, self.device)
+        self.config = config
+        if self.mixer is not None:
+            self.mixer.set_driver(self.clf)
+        log.info("config loaded: %s", cfg.get("method"))
+
+    def get_config(self) -> str:
+        self.check_set_config()
+        return self.config
+
+    def get_driver(self):
+        self.check_set_config()
+        return self.clf
+
+    # ---------------------------------------------------------------- RPC
+    def _bump(self) -> None:
+        with self.rw_mutex.write():
+            self.event_model_updated()
+
+    def train(self, data) -> int:
+        self.check_set_config()
+        items = labeled_data(data)
+        self._bump()
+        return self.clf.train(items)
+
+    def raw_train(self, params: bytes) -> int:
+        """zero-copy path: the list<labeled_datum> bytes go straight to the
+        GPU pipeline (native scan -> pinned staging -> fv_hash -> update)."""
+        self.check_set_config()
+        parts = split_params(params)
+        if len(parts) != 2:
+            raise ArgumentError("train: expected 2 arguments")
+        self._bump()
+        if hasattr(self.clf, "train_requests"):
+            try:
+                return self.clf.train_requests([parts[1]])
+            except TypeError as e:
+                raise ArgumentError(str(e)) from e
+        from ..common.mprpc import unpackb
+        return self.clf.train(labeled_data(unpackb(bytes(parts[1]))))
+
+    def classify(self, data) -> list:
+        self.check_set_config()
+        if not isinstance(data, list):
+            raise ArgumentError("classify: data must be a list")
+        res = self.clf.classify([Datum.from_msgpack(d) for d in data])
+        out = []
+        for row in res:
+            r = []
+            for label, score in row:
+                if not math.isfinite(score):
+                    log.warning("score is infinite: %s = %s", label, score)
+                r.append([label, float(score)])
+            out.append(r)
+        return out
+
+    def get_labels(self) -> dict:
+        self.check_set_config()
+        return self.clf.get_labels()
+
+    def set_label(self, label: str) -> bool:
+        self.check_set_config()
+        self._bump()
+        return self.clf.set_label(label)
+
+    def clear(self) -> bool:
+        self.check_set_config()
+        self._bump()
+        self.clf.clear()
+        log.info("model cleared: %s", self.argv().name)
+        return True
+
+    def delete_label(self, label: str) -> bool:
+        self.check_set_config()
+        self._bump()
+        return self.clf.delete_label(label)
+
+    def get_status(self, status: dict) -> None:
+        if self.clf is not None:
+            status.update(self.clf.get_status())
+        if self.device is not None:
+            import torch
+            status["device"] = str(self.device)
+            status["hbm_allocated_bytes"] = str(torch.cuda.memory_allocated(self.device))
