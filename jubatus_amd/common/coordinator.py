@@ -1,0 +1,79 @@
+"""jubacoordinator: the cluster coordination server (replaces ZooKeeper for
+the reference's lock_service usage; see lock_service.py for the data model).
+
+Serves a ZNodeStore over msgpack-RPC (native transport) and expires
+sessions whose heartbeat is older than their timeout (ephemeral nodes go
+with them - the liveness mechanism of membership, CHT and mixer masters,
+SURVEY §5.3).
+"""
+from __future__ import annotations
+
+import threading
+
+from ..utils import logger
+from .lock_service import ZNodeStore
+from .mprpc import RpcServer
+
+log = logger.get_logger("coordinator")
+
+
+class CoordinatorServer:
+    def __init__(self, port: int = 2181, bind: str = "0.0.0.0", nthreads: int = 4,
+                 store: ZNodeStore | None = None):
+        self.store = store or ZNodeStore()
+        self.rpc = RpcServer(nthreads=nthreads)
+        st = self.store
+        self.rpc.add("open_session", st.open_session, 1)
+        self.rpc.add("heartbeat", st.heartbeat, 1)
+        self.rpc.add("close_session", st.close_session, 1)
+        self.rpc.add("create", st.create, 4)
+        self.rpc.add("create_seq", lambda sid, p: list(st.create_seq(sid, p)), 2)
+        self.rpc.add("set", lambda p, d: list(st.set(p, d)), 2)
+        self.rpc.add("remove", st.remove, 1)
+        self.rpc.add("exists", st.exists, 1)
+        self.rpc.add("list", lambda p: list(st.list(p)), 1)
+        self.rpc.add("read", lambda p: list(st.read(p)), 1)
+        self.rpc.add("stat_many", st.stat_many, 1)
+        self.rpc.add("dump", st.dump, 0)
+        self.port = self.rpc.listen(port, bind)
+        self._stop = threading.Event()
+        self._sweeper = threading.Thread(target=self._sweep, name="coord-sweeper", daemon=True)
+
+    def _sweep(self) -> None:
+        while not self._stop.wait(0.1):
+            self.store.expire_sessions()
+
+    def start(self) -> "CoordinatorServer":
+        self.rpc.start()
+        self._sweeper.start()
+        log.info("coordinator listening on %d", self.port)
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.rpc.stop()
+
+    def join(self) -> None:
+        while not self._stop.wait(0.5):
+            pass
+
+
+def main(argv: list[str] | None = None) -> int:
+    import argparse
+    import sys
+
+    from ..utils import signals
+    p = argparse.ArgumentParser(prog="jubacoordinator")
+    p.add_argument("-p", "--port", type=int, default=2181)
+    p.add_argument("-b", "--listen_addr", default="0.0.0.0")
+    p.add_argument("-c", "--thread", type=int, default=4)
+    a = p.parse_args(sys.argv[1:] if argv is None else argv)
+    srv = CoordinatorServer(a.port, a.listen_addr, a.thread).start()
+    signals.prepare_signal_handling()
+    signals.set_action_on_term(srv.stop)
+    srv.join()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
