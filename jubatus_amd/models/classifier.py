@@ -403,16 +403,94 @@ class LinearClassifier:
                             seen.add(n)
                             order.append(n)
                 self._reorder_labels(order)
-            tables = [self.W] + ([self.P] if self.P is not None else [])
-            if self.gpu:
-                coll.allreduce_mean_(tables, group)
-                nbytes = sum(t.numel() * 4 for t in tables)
+            tables = self._tables()
+            coll.allreduce_mean_(tables, group)
+            self._mix_counts(group)
+            return sum(t.numel() * t.element_size() for t in tables)
+
+    def _tables(self) -> list:
+        """the mixable tensors (torch views of the host arrays on the CPU backend)"""
+        tables = [self.W] + ([self.P] if self.P is not None else [])
+        if self.gpu:
+            return tables
+        import torch
+        return [torch.from_numpy(t) for t in tables]
+
+    def _mix_counts(self, group=None) -> None:
+        """label counts: base + cluster-wide sum of the per-rank deltas since
+        the last MIX (the local_mixture semantics of get_labels)."""
+        import torch
+        from ..parallel import collective as coll
+        names = self.labels.names()
+        base = getattr(self, "_count_base", {})
+        cur = np.array([self.labels.count(i) for i in range(len(names))], dtype=np.int64)
+        b = np.array([base.get(n, 0) for n in names], dtype=np.int64)
+        delta = torch.from_numpy(cur - b)
+        if self.gpu and coll.is_dist() and __import__("torch.distributed").distributed.get_backend(group) == "nccl":
+            d = delta.to(self.device)
+            coll.allreduce_sum_([d], group)
+            delta = d.cpu()
+        else:
+            coll.allreduce_sum_([delta], group)
+        new = b + delta.numpy()
+        for i, n in enumerate(names):
+            self.labels.set_count(i, int(max(0, new[i])))
+        self._count_base = {n: int(max(0, new[i])) for i, n in enumerate(names)}
+
+    def broadcast_from(self, src: int) -> None:
+        """hand the whole model to a newly joined member (obsolete protocol)"""
+        import torch.distributed as dist
+        with self._lock:
+            names = self.labels.names()
+            meta = [[names, [int(self.labels.count(i)) for i in range(len(names))],
+                     self.labels.alive()]]
+            dist.broadcast_object_list(meta, src=src)
+            names, counts, alive = meta[0]
+            if dist.get_rank() != src:
+                self.labels.clear()
+                self.LC = 0
+                self._alloc(_label_cap(max(1, len(names))))
+                for i, (n, c) in enumerate(zip(names, counts)):
+                    self.labels.get_or_add(n)
+                    self.labels.set_count(i, int(c))
+                for n, a in zip(names, alive):
+                    if not a:
+                        self.labels.remove(n)
+                self._sync_labels()
+            for t in self._tables():
+                dist.broadcast(t, src=src)
+            self._count_base = {n: int(c) for n, c in zip(names, counts)}
+
+    def pair_mix(self, peer: int) -> None:
+        """push_mixer exchange with one peer: agree on the label layout, then
+        swap the tables point-to-point and keep the pairwise mean."""
+        import torch
+        import torch.distributed as dist
+        with self._lock:
+            me = dist.get_rank()
+            mine = [self._live_labels()]
+            theirs = [None]
+            if me < peer:
+                dist.send_object_list(mine, dst=peer)
+                dist.recv_object_list(theirs, src=peer)
+                lists = [mine[0], theirs[0]]
             else:
-                import torch
-                ts = [torch.from_numpy(t) for t in tables]
-                coll.allreduce_mean_(ts, group)
-                nbytes = sum(t.nbytes for t in tables)
-            return nbytes
+                dist.recv_object_list(theirs, src=peer)
+                dist.send_object_list(mine, dst=peer)
+                lists = [theirs[0], mine[0]]
+            order: list[str] = []
+            for lst in lists:
+                for n in lst:
+                    if n not in order:
+                        order.append(n)
+            if order != self.labels.names() or not all(self.labels.alive()):
+                self._reorder_labels(order)
+            for t in self._tables():
+                buf = torch.empty_like(t)
+                ops = [dist.P2POp(dist.isend, t, peer), dist.P2POp(dist.irecv, buf, peer)]
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+                t.add_(buf).mul_(0.5)
 
     def get_status(self) -> dict[str, str]:
         st = {"num_classes": str(len(self.get_labels())), "num_features": str(self.H),

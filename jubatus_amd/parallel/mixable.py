@@ -1,0 +1,96 @@
+"""How a driver takes part in a MIX (the reference's linear_mixable /
+push_mixable, jubatus_core EXTERNAL; used at linear_mixer.cpp:438-480 and
+push_mixer.cpp:410-472).
+
+A driver supports one of:
+
+* ``mix()`` - a collective over the current process group (dense models on
+  the GPU: label/row reconciliation + RCCL all-reduce mean of the HBM
+  tables; models/classifier.py);
+* ``get_diff() / mix_diff(a, b) / put_diff(m)`` - the reference's
+  linear_mixable protocol, run as an all-gather of diffs, a fold in rank
+  order (the reference folds in arrival order, linear_mixer.cpp:455-485;
+  rank order makes it deterministic) and a local put_diff.
+
+Model hand-over to an obsolete (newly joined) member: ``broadcast_from(src)``
+if the driver has it, else ``pack()`` / ``unpack()`` through a broadcast of
+the packed object.
+"""
+from __future__ import annotations
+
+import time
+from typing import Any
+
+from ..framework.mixer import UnsupportedMixables
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist
+
+
+def linear_mix(driver: Any) -> dict:
+    """Run one MIX on the current process group; returns stats."""
+    t0 = time.perf_counter()
+    nbytes = 0
+    if hasattr(driver, "mix"):
+        nbytes = int(driver.mix() or 0)
+    elif hasattr(driver, "get_diff"):
+        dist = _dist()
+        diff = driver.get_diff()
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        diffs = [None] * world
+        if world > 1:
+            dist.all_gather_object(diffs, diff)
+        else:
+            diffs = [diff]
+        mixed = diffs[0]
+        for d in diffs[1:]:
+            mixed = driver.mix_diff(mixed, d)
+        driver.put_diff(mixed)
+        try:
+            import pickle
+            nbytes = sum(len(pickle.dumps(d)) for d in diffs)
+        except Exception:  # noqa: BLE001
+            nbytes = 0
+    else:
+        raise UnsupportedMixables(f"{type(driver).__name__} is not mixable")
+    return {"bytes": nbytes, "seconds": time.perf_counter() - t0}
+
+
+def broadcast_model(driver: Any, src: int) -> None:
+    dist = _dist()
+    if hasattr(driver, "broadcast_from"):
+        driver.broadcast_from(src)
+        return
+    box = [driver.pack() if dist.get_rank() == src else None]
+    dist.broadcast_object_list(box, src=src)
+    if dist.get_rank() != src:
+        driver.unpack(box[0])
+
+
+def pair_exchange(driver: Any, peer: int) -> None:
+    """Symmetric pairwise MIX with one peer (push_mixer's pull/push in both
+    directions, push_mixer.cpp:354-388): both sides end with the same model
+    (the mean of the two for tensor drivers, mix_diff of the two diffs
+    otherwise)."""
+    dist = _dist()
+    me = dist.get_rank()
+    if hasattr(driver, "pair_mix"):
+        driver.pair_mix(peer)
+        return
+    if not hasattr(driver, "get_diff"):
+        raise UnsupportedMixables(f"{type(driver).__name__} is not push-mixable")
+    mine = driver.get_diff()
+    out = [mine]
+    inb = [None]
+    # lower rank sends first: matched send/recv order on both sides
+    if me < peer:
+        dist.send_object_list(out, dst=peer)
+        dist.recv_object_list(inb, src=peer)
+    else:
+        dist.recv_object_list(inb, src=peer)
+        dist.send_object_list(out, dst=peer)
+    theirs = inb[0]
+    mixed = driver.mix_diff(mine, theirs) if me < peer else driver.mix_diff(theirs, mine)
+    driver.put_diff(mixed)

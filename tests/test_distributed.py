@@ -1,0 +1,118 @@
+"""Multi-process cluster on one host (reference strategy: several servers on
+localhost ports + a local coordinator, client_test/envdef.sample.py:13-18).
+
+Two jubaclassifier processes (host backend, gloo process group) join a
+cluster through our coordinator; training lands on one server only and a
+MIX makes the other one learn it: linear_mixer (all-reduce mean) and the
+push mixers (pairwise send/recv)."""
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+from jubatus_amd.client import Classifier, Datum
+from jubatus_amd.common import config as zkconfig
+from jubatus_amd.common import membership as mb
+from jubatus_amd.common.coordinator import CoordinatorServer
+from jubatus_amd.common.lock_service import CoordinatorClient
+from jubatus_amd.common.mprpc import wait_server
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def coord():
+    srv = CoordinatorServer(0, "127.0.0.1").start()
+    yield srv
+    srv.stop()
+
+
+def spawn(engine, zport, name, port, mixer="linear_mixer", extra=()):
+    env = dict(os.environ, PYTHONPATH=ROOT, JUBATUS_FORCE_CPU="1")
+    cmd = [sys.executable, "-m", "jubatus_amd.cmd.server", engine, "-z", f"127.0.0.1:{zport}",
+           "-n", name, "-p", str(port), "-b", "127.0.0.1", "-x", mixer, "-s", "0", "-i", "0",
+           "-I", "5", "--cpu", *extra]
+    return subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+
+
+def wait_actives(ls, engine, name, n, timeout=60):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        if len(mb.get_all_actives(ls, engine, name)) >= n:
+            return True
+        time.sleep(0.2)
+    return False
+
+
+@pytest.mark.parametrize("mixer", ["linear_mixer", "skip_mixer", "random_mixer", "broadcast_mixer"])
+def test_two_server_mix(coord, mixer):
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    name = f"dist_{mixer}"
+    zkconfig.config_tozk(ls, "classifier", name, open(os.path.join(ROOT, "config/classifier/arow.json")).read())
+    ports = [free_port(), free_port()]
+    procs = [spawn("classifier", coord.port, name, p, mixer) for p in ports]
+    try:
+        for p in ports:
+            assert wait_server("127.0.0.1", p, 60), "server did not start"
+        assert wait_actives(ls, "classifier", name, 2), "servers did not become active"
+        a = Classifier("127.0.0.1", ports[0], name)
+        b = Classifier("127.0.0.1", ports[1], name)
+        a.train([("pos", Datum({"w": "good"})), ("neg", Datum({"w": "bad"}))] * 3)
+        assert b.get_labels() == {}
+        assert a.do_mix() is True
+        deadline = time.time() + 20
+        key = f"{mixer}.mix_count"
+        while int(list(b.get_status().values())[0][key]) < 1 and time.time() < deadline:
+            time.sleep(0.2)
+        assert set(b.get_labels()) == {"pos", "neg"}
+        top = max(b.classify([Datum({"w": "good"})])[0], key=lambda e: e.score)
+        assert top.label == "pos"
+        if mixer == "linear_mixer":
+            # model averaging: both servers hold the same model after the MIX
+            sa = {e.label: e.score for e in a.classify([Datum({"w": "good"})])[0]}
+            sb = {e.label: e.score for e in b.classify([Datum({"w": "good"})])[0]}
+            assert sa.keys() == sb.keys()
+            assert all(abs(sa[k] - sb[k]) < 1e-5 for k in sa)
+            assert b.get_labels() == {"pos": 3, "neg": 3}  # counts mixed (sum of deltas)
+        st = list(b.get_status().values())[0]
+        assert st["mixer"] == mixer and st["is_standalone"] == "0"
+        assert int(st[f"{mixer}.mix_count"]) >= 1
+        a.close()
+        b.close()
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        ls.close()
+
+
+def test_server_self_fences_when_actor_deleted(coord):
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    zkconfig.config_tozk(ls, "classifier", "fence", open(os.path.join(ROOT, "config/classifier/pa.json")).read())
+    port = free_port()
+    p = spawn("classifier", coord.port, "fence", port)
+    try:
+        assert wait_server("127.0.0.1", port, 60)
+        assert wait_actives(ls, "classifier", "fence", 1)
+        ls.remove(f"/jubatus/actors/classifier/fence/nodes/127.0.0.1_{port}")
+        p.wait(timeout=30)   # stops itself (server_helper.cpp:91-94)
+        assert p.returncode == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+        ls.close()
