@@ -116,3 +116,50 @@ def test_server_self_fences_when_actor_deleted(coord):
         if p.poll() is None:
             p.kill()
         ls.close()
+
+
+def test_proxy_routing(coord):
+    from jubatus_amd.framework.proxy import Proxy
+    from jubatus_amd.framework.server_util import ProxyArgv
+
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    name = "viaproxy"
+    zkconfig.config_tozk(ls, "classifier", name, open(os.path.join(ROOT, "config/classifier/pa.json")).read())
+    ports = [free_port(), free_port()]
+    procs = [spawn("classifier", coord.port, name, p) for p in ports]
+    pa = ProxyArgv(type="classifier", port=0, bind_address="127.0.0.1", eth="127.0.0.1",
+                   z=f"127.0.0.1:{coord.port}", program_name="jubaclassifier_proxy")
+    proxy = Proxy(pa)
+    proxy.start(block=False)
+    try:
+        for p in ports:
+            assert wait_server("127.0.0.1", p, 60)
+        assert wait_actives(ls, "classifier", name, 2)
+        c = Classifier("127.0.0.1", pa.port, name)
+        for _ in range(10):  # random routing spreads the requests
+            assert c.train([("a", Datum({"k": "x"})), ("b", Datum({"k": "y"}))]) == 2
+        st = c.get_status()                      # broadcast + merge
+        assert len(st) == 2
+        assert sum(int(s["update_count"]) for s in st.values()) == 10
+        assert c.set_label("z") is True          # broadcast + all_and
+        assert all("z" in Classifier("127.0.0.1", p, name).get_labels() for p in ports)
+        saved = c.save("px")                     # broadcast + merge
+        assert len(saved) == 2
+        assert c.load("px") is True
+        ps = c.get_proxy_status()
+        (k, v), = ps.items()
+        assert int(v["request_count"]) >= 14 and int(v["forward_count"]) >= 16
+        from jubatus_amd.common.mprpc import RpcCallError
+        with pytest.raises(RpcCallError):
+            Classifier("127.0.0.1", pa.port, "no_such_cluster").get_config()
+        c.close()
+    finally:
+        proxy.stop()
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        ls.close()
