@@ -10,7 +10,7 @@ namespace py = pybind11;
 
 namespace {
 
-py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* table,
+py::tuple pack(py::list reqs, int labeled, int sps, int spn, jb::LabelTable* table,
                uintptr_t staging, uint64_t staging_cap, uintptr_t datum_off, uintptr_t datum_len,
                uintptr_t labels, uintptr_t row_ptr, uintptr_t stream_ptr, int64_t max_samples,
                int nthreads) {
@@ -37,7 +37,7 @@ py::tuple pack(py::list reqs, bool labeled, int sps, int spn, jb::LabelTable* ta
 
 // zero-copy variant: requests are spans [offs[k], offs[k]+lens[k]) of one
 // pinned arena at `base` (e.g. the RPC receive arena); nothing is copied.
-py::tuple pack_spans(uintptr_t base, uintptr_t offs, uintptr_t lens, int64_t nreq, bool labeled,
+py::tuple pack_spans(uintptr_t base, uintptr_t offs, uintptr_t lens, int64_t nreq, int labeled,
                      int sps, int spn, jb::LabelTable* table, uintptr_t datum_off,
                      uintptr_t datum_len, uintptr_t labels, uintptr_t row_ptr, uintptr_t stream_ptr,
                      int64_t max_samples, int nthreads) {

@@ -64,7 +64,7 @@ class LabelCache {
   size_t used_ = 0;
 };
 
-void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelCache* cache,
+void scan_one(const RequestView& r, int kind, int sps, int spn, LabelCache* cache,
               ReqScan* out) {
   Cursor c{r.data, r.data + r.len};
   uint32_t n;
@@ -72,14 +72,21 @@ void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelCache* 
   out->off.reserve(n);
   out->len.reserve(n);
   out->slots.reserve(n);
-  if (labeled) out->label.reserve(n);
+  if (kind) out->label.reserve(n);
   for (uint32_t i = 0; i < n; ++i) {
-    if (labeled) {
+    if (kind == 1) {
       uint32_t two; const uint8_t* ls; uint32_t ln;
       if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { out->ok = false; return; }
       int id = cache->get(ls, ln);
       if (id < 0) { out->table_full = true; out->ok = false; return; }
       out->label.push_back(id);
+    } else if (kind == 2) {  // scored_datum [score, datum]
+      uint32_t two; double score;
+      if (!c.array(&two) || two != 2 || !c.number(&score)) { out->ok = false; return; }
+      const float f = (float)score;
+      int32_t bits;
+      memcpy(&bits, &f, 4);
+      out->label.push_back(bits);
     }
     uint64_t doff = (uint64_t)(c.p - r.data);
     DatumShape d;
@@ -92,7 +99,7 @@ void scan_one(const RequestView& r, bool labeled, int sps, int spn, LabelCache* 
 
 }  // namespace
 
-PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int sps, int spn,
+PackResult pack_requests(const std::vector<RequestView>& reqs, int kind, int sps, int spn,
                          LabelTable* table, const PackOut& out, int nthreads) {
   PackResult res;
   const size_t R = reqs.size();
@@ -113,7 +120,7 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
     LabelCache cache(table);
     int64_t b, e;
     chunk(c, &b, &e);
-    for (int64_t k = b; k < e; ++k) scan_one(reqs[k], labeled, sps, spn, &cache, &scans[k]);
+    for (int64_t k = b; k < e; ++k) scan_one(reqs[k], kind, sps, spn, &cache, &scans[k]);
   });
 
   // serial prefix over requests
@@ -160,7 +167,7 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
         if (out.datum_len) out.datum_len[s0 + i] = (int32_t)sc.len[i];
         out.row_ptr[s0 + i] = slot;
         slot += sc.slots[i];
-        if (labeled && out.labels) out.labels[s0 + i] = sc.label[i];
+        if (kind && out.labels) out.labels[s0 + i] = sc.label[i];
       }
     }
   });
@@ -169,7 +176,7 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int
     for (size_t k = 0; k < R; ++k) out.stream_ptr[k] = sample_base[k];
     out.stream_ptr[R] = samples;
   }
-  if (labeled && table) {
+  if (kind == 1 && table) {
     // per-chunk histograms, then one atomic add per (chunk, label)
     pool.parallel_for(nchunks, [&](int64_t c) {
       int64_t b, e;

@@ -144,8 +144,9 @@ struct PackResult {
   int64_t error_request = -1;
 };
 
-// labeled: request body is list<[label, datum]>; otherwise list<datum>
-PackResult pack_requests(const std::vector<RequestView>& reqs, bool labeled, int slots_per_str,
+// kind 0: list<datum>; 1: list<[label, datum]> (labels -> ids); 2: list<[score, datum]>
+// (scored; the float targets are written, bit-cast, into out.labels)
+PackResult pack_requests(const std::vector<RequestView>& reqs, int kind, int slots_per_str,
                          int slots_per_num, LabelTable* table, const PackOut& out, int nthreads);
 
 }  // namespace jb

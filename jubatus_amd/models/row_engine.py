@@ -1,0 +1,168 @@
+"""Common driver of the row-oriented engines: a RowStore + a similarity
+index (LSH family on the GPU, or the exact inverted index) + the converter.
+
+MIX (the reference's versioned column table, mixed by linear_mixer): the
+diff is every row changed or removed since the last MIX with its version;
+diffs are folded newest-version-wins and applied everywhere, so every
+server can answer random-routed queries over all rows.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Any
+
+from ..fv_converter.converter import DatumToFvConverter
+from ..fv_converter.datum import Datum, as_datum
+from .rows import RowStore, Unlearner, datum_to_dicts, dicts_to_datum
+from .similarity import InvertedIndex, LshIndex
+
+LSH_METHODS = ("lsh", "euclid_lsh", "minhash")
+INDEX_METHODS = LSH_METHODS + ("inverted_index", "inverted_index_euclid")
+
+
+def make_index(method: str, parameter: dict, device: Any):
+    if method in LSH_METHODS:
+        return LshIndex(method, int(parameter.get("hash_num", 64)),
+                        int(parameter.get("seed", 1091)), device)
+    if method == "inverted_index":
+        return InvertedIndex(False, device)
+    if method == "inverted_index_euclid":
+        return InvertedIndex(True, device)
+    raise ValueError(f"unknown similarity method: {method}")
+
+
+class RowEngine:
+    def __init__(self, method: str, parameter: dict | None, converter: DatumToFvConverter,
+                 device: Any = None, unlearner: str | None = None,
+                 unlearner_parameter: dict | None = None):
+        self.method = method
+        self.parameter = dict(parameter or {})
+        self.conv = converter
+        self.device = device
+        self.gpu = device is not None
+        self.index = make_index(method, self.parameter, device)
+        self.rows = RowStore()
+        self.unlearner = Unlearner(unlearner, unlearner_parameter)
+        self._lock = threading.RLock()
+
+    # ------------------------------------------------------------ rows
+    def fv_of(self, d: Datum, update_weight: bool = False):
+        f = self.conv.convert_and_update_weight(d) if update_weight else self.conv.convert(d)
+        return self.conv.hashed(f)
+
+    def _set(self, rid: str, dicts, bump: bool = True, update_weight: bool = True) -> None:
+        fv = self.fv_of(dicts_to_datum(*dicts), update_weight)
+        slot = self.rows.put(rid, dicts, fv, bump)
+        self.index.set_rows([slot], [fv])
+        for victim in self.unlearner.touch(rid):
+            if victim != rid:
+                self._remove(victim)
+
+    def _remove(self, rid: str, record: bool = True) -> bool:
+        s = self.rows.remove(rid, record)
+        if s is None:
+            return False
+        self.index.remove(s)
+        self.unlearner.remove(rid)
+        return True
+
+    def set_row(self, rid: str, d: Any) -> bool:
+        with self._lock:
+            self._set(rid, datum_to_dicts(as_datum(d)))
+            return True
+
+    def update_row(self, rid: str, d: Any) -> bool:
+        """merge the datum into the existing row (recommender update_row)"""
+        with self._lock:
+            new = datum_to_dicts(as_datum(d))
+            s = self.rows.slot(rid)
+            if s is not None:
+                sv, nv, bv = (dict(x) for x in self.rows.datum[s])
+                sv.update(new[0]); nv.update(new[1]); bv.update(new[2])
+                new = (sv, nv, bv)
+            self._set(rid, new)
+            return True
+
+    def clear_row(self, rid: str) -> bool:
+        with self._lock:
+            return self._remove(rid)
+
+    def clear(self) -> None:
+        with self._lock:
+            self.rows.clear()
+            self.index.clear()
+            self.unlearner.clear()
+            self.conv.weights.clear()
+
+    def get_all_rows(self) -> list[str]:
+        with self._lock:
+            return self.rows.all_ids()
+
+    # ------------------------------------------------------------ queries
+    def _results(self, res: list[tuple[int, float]]) -> list[tuple[str, float]]:
+        out = []
+        for slot, score in res:
+            rid = self.rows.id_of(slot)
+            if rid is not None:
+                out.append((rid, float(score)))
+        return out
+
+    def query_fv(self, fv, k: int, similar: bool) -> list[tuple[str, float]]:
+        with self._lock:
+            n = self.rows.nslots
+            if n == 0 or k <= 0:
+                return []
+            (r,) = self.index.query([fv], n, k, similar)
+            return self._results(r)
+
+    def query_datum(self, d: Any, k: int, similar: bool) -> list[tuple[str, float]]:
+        return self.query_fv(self.fv_of(as_datum(d)), k, similar)
+
+    def query_id(self, rid: str, k: int, similar: bool) -> list[tuple[str, float]]:
+        with self._lock:
+            s = self.rows.slot(rid)
+            if s is None:
+                raise KeyError(f"row not found: {rid}")
+            return self.query_fv(self.rows.fv[s], k, similar)
+
+    # ------------------------------------------------------------ MIX
+    def get_diff(self) -> dict:
+        return self.rows.get_diff()
+
+    @staticmethod
+    def mix_diff(a: dict, b: dict) -> dict:
+        return RowStore.mix_diff(a, b)
+
+    def put_diff(self, mixed: dict) -> bool:
+        with self._lock:
+            for rid, (v, d) in mixed["rows"].items():
+                if self.rows.version.get(rid, -1) < v or rid not in self.rows.slot_of:
+                    self._set(rid, tuple(dict(x) for x in d), bump=False, update_weight=False)
+                    self.rows.version[rid] = v
+            for rid, v in mixed["removed"].items():
+                if self.rows.version.get(rid, -1) <= v:
+                    self._remove(rid, record=False)
+                    self.rows.version[rid] = v
+            self.rows.dirty.clear()
+            self.rows.removed.clear()
+            return True
+
+    # ------------------------------------------------------------ persist
+    def pack(self) -> dict:
+        with self._lock:
+            return {"method": self.method, "rows": self.rows.pack()["rows"],
+                    "weights": self.conv.weights.pack()}
+
+    def unpack(self, obj: dict) -> None:
+        with self._lock:
+            self.clear()
+            if obj.get("weights"):
+                self.conv.weights.unpack(obj["weights"])
+            for rid, (v, d) in obj["rows"].items():
+                self._set(rid, tuple(dict(x) for x in d), bump=False, update_weight=False)
+                self.rows.version[rid] = v
+
+    def get_status(self) -> dict[str, str]:
+        return {"method": self.method, "num_rows": str(len(self.rows.slot_of)),
+                "storage": "hbm" if self.gpu else "host",
+                "unlearner": self.unlearner.kind or "none"}

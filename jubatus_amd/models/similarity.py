@@ -1,0 +1,377 @@
+"""Row indexes for similarity search (nearest_neighbor, recommender, anomaly).
+
+* ``LshIndex``       lsh / euclid_lsh / minhash signatures in a table
+                     (HBM on a GPU: csrc/hip/lsh.hip), XOR-popcount scans
+* ``InvertedIndex``  exact cosine (inverted_index) or euclidean
+                     (inverted_index_euclid) over the sparse rows
+
+Both map a row *slot* (int) to its representation; the id <-> slot mapping
+lives in RowStore (models/rows.py). ``query(rows, k)`` returns, per query,
+``[(slot, distance)]`` ascending; similarity views are derived by the
+engines. The NumPy paths below are the oracles of the HIP kernels (same
+splitmix64 hyperplane coefficients, same distance formulas).
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Sequence
+
+import numpy as np
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _splitmix(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = (x + np.uint64(0x9E3779B97F4A7C15))
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def feat_hash(seed: int, idx: np.ndarray, j: np.ndarray) -> np.ndarray:
+    idx = np.asarray(idx, dtype=np.uint64)
+    j = np.asarray(j, dtype=np.uint64)
+    return _splitmix(np.uint64(seed) ^ _splitmix((idx << np.uint64(20)) ^ j))
+
+
+def gauss(h: np.ndarray) -> np.ndarray:
+    u1 = ((h >> np.uint64(40)).astype(np.float64) + 1.0) / 16777217.0
+    u2 = (h & np.uint64(0xFFFFFF)).astype(np.float64) / 16777216.0
+    return (np.sqrt(-2.0 * np.log(u1)) * np.cos(6.2831853 * u2)).astype(np.float32)
+
+
+def signature_host(idx: Sequence[int], val: Sequence[float], hash_num: int, seed: int,
+                   mode: int) -> tuple[np.ndarray, float]:
+    """(bits uint64[words], norm) of one sparse vector."""
+    idx = np.asarray(idx, dtype=np.int64)
+    val = np.asarray(val, dtype=np.float32)
+    m = idx >= 0
+    idx, val = idx[m], val[m]
+    words = (hash_num + 63) // 64
+    j = np.arange(words * 64, dtype=np.uint64)
+    if len(idx) == 0:
+        bits = np.zeros(words * 64, dtype=bool)
+    else:
+        h = feat_hash(seed, idx[:, None].astype(np.uint64), j[None, :])
+        if mode == 0:
+            acc = (val[:, None] * gauss(h)).sum(axis=0)
+            bits = acc > 0
+        else:
+            keep = val != 0
+            if not keep.any():
+                bits = np.ones(words * 64, dtype=bool)  # min of nothing = all ones
+            else:
+                bits = (h[keep].min(axis=0) & np.uint64(1)) != 0
+    bits[hash_num:] = False
+    packed = np.zeros(words, dtype=np.uint64)
+    for w in range(words):
+        chunk = bits[w * 64:(w + 1) * 64]
+        packed[w] = np.uint64(sum(1 << i for i, b in enumerate(chunk) if b))
+    return packed, float(np.sqrt((val.astype(np.float64) ** 2).sum()))
+
+
+def _popcount(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint64)
+    c = np.zeros(x.shape, dtype=np.int64)
+    while np.any(x):
+        c += (x & np.uint64(1)).astype(np.int64)
+        x >>= np.uint64(1)
+    return c
+
+
+METRIC = {"lsh": 0, "euclid_lsh": 1, "minhash": 2}
+
+
+class LshIndex:
+    def __init__(self, method: str, hash_num: int = 64, seed: int = 1091, device: Any = None):
+        if method not in METRIC:
+            raise ValueError(f"unknown lsh method {method}")
+        if hash_num <= 0:
+            raise ValueError("hash_num must be positive")
+        self.method, self.hash_num, self.seed = method, int(hash_num), int(seed)
+        self.metric = METRIC[method]
+        self.mode = 1 if method == "minhash" else 0
+        self.words = (self.hash_num + 63) // 64
+        self.device = device
+        self.gpu = device is not None
+        self.cap = 0
+        self._alloc(1024)
+
+    def _alloc(self, cap: int) -> None:
+        if self.gpu:
+            import torch
+            bits = torch.zeros((cap, self.words), dtype=torch.int64, device=self.device)
+            norms = torch.zeros(cap, dtype=torch.float32, device=self.device)
+            valid = torch.zeros(cap, dtype=torch.uint8, device=self.device)
+            if self.cap:
+                bits[:self.cap] = self.bits
+                norms[:self.cap] = self.norms
+                valid[:self.cap] = self.valid
+        else:
+            bits = np.zeros((cap, self.words), dtype=np.uint64)
+            norms = np.zeros(cap, dtype=np.float32)
+            valid = np.zeros(cap, dtype=np.uint8)
+            if self.cap:
+                bits[:self.cap] = self.bits
+                norms[:self.cap] = self.norms
+                valid[:self.cap] = self.valid
+        self.bits, self.norms, self.valid, self.cap = bits, norms, valid, cap
+
+    def clear(self) -> None:
+        self.cap = 0
+        self._alloc(1024)
+
+    def _signatures(self, rows: list[tuple[Sequence[int], Sequence[float]]]):
+        """-> (bits [n, words], norms [n]) on the index's device."""
+        if self.gpu:
+            import torch
+            from ..ops import hip
+            from ..ops.feature_pipeline import FeaturePipeline  # noqa: F401 (CSR helper below)
+            row_ptr, fidx, fval = _csr_device(rows, self.device)
+            n = len(rows)
+            bits = torch.empty((max(n, 1), self.words), dtype=torch.int64, device=self.device)
+            norms = torch.empty(max(n, 1), dtype=torch.float32, device=self.device)
+            hip.signature(row_ptr, fidx, fval, n, self.hash_num, self.seed, self.mode, bits, norms)
+            return bits[:n], norms[:n]
+        out = [signature_host(i, v, self.hash_num, self.seed, self.mode) for i, v in rows]
+        bits = np.stack([b for b, _ in out]) if out else np.zeros((0, self.words), np.uint64)
+        norms = np.asarray([n for _, n in out], dtype=np.float32)
+        return bits, norms
+
+    def set_rows(self, slots: Sequence[int], rows: list[tuple[Sequence[int], Sequence[float]]]) -> None:
+        if not slots:
+            return
+        need = max(slots) + 1
+        if need > self.cap:
+            c = self.cap
+            while c < need:
+                c *= 2
+            self._alloc(c)
+        bits, norms = self._signatures(rows)
+        if self.gpu:
+            import torch
+            s = torch.as_tensor(list(slots), dtype=torch.int64, device=self.device)
+            self.bits[s] = bits
+            self.norms[s] = norms
+            self.valid[s] = 1
+        else:
+            s = np.asarray(slots, dtype=np.int64)
+            self.bits[s] = bits
+            self.norms[s] = norms
+            self.valid[s] = 1
+
+    def remove(self, slot: int) -> None:
+        if slot < self.cap:
+            self.valid[slot] = 0
+
+    def distances(self, rows: list, nrows: int):
+        """distance matrix [nq, nrows] (device tensor or ndarray)"""
+        nq = len(rows)
+        qb, qn = self._signatures(rows)
+        if self.gpu:
+            import torch
+            from ..ops import hip
+            out = torch.empty((nq, max(nrows, 1)), dtype=torch.float32, device=self.device)
+            if nrows:
+                hip.hamming_scan(qb.contiguous(), qn.contiguous(), nq, self.bits, self.norms,
+                                 self.valid, nrows, self.hash_num, self.metric, out)
+            return out[:, :nrows]
+        tb = self.bits[:nrows]
+        ham = np.zeros((nq, nrows), dtype=np.int64)
+        for w in range(self.words):
+            ham += _popcount(qb[:, w][:, None] ^ tb[:, w][None, :])
+        frac = ham.astype(np.float32) / self.hash_num
+        if self.metric == 1:
+            a = qn[:, None].astype(np.float32)
+            b = self.norms[:nrows][None, :]
+            d = np.sqrt(np.maximum(0.0, a * a + b * b - 2 * a * b * np.cos(np.float32(math.pi) * frac)))
+        else:
+            d = frac
+        d = d.astype(np.float32)
+        d[:, self.valid[:nrows] == 0] = np.inf
+        return d
+
+    def similarity_of(self, d):
+        """distance -> similarity as reported by similar_row_* (lsh / minhash:
+        1 - d; euclid_lsh: -d)"""
+        return -d if self.metric == 1 else 1.0 - d
+
+    def query(self, rows: list, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
+        return topk(self.distances(rows, nrows), k, self.similarity_of if similar else None)
+
+    def state(self, nrows: int) -> dict:
+        if self.gpu:
+            bits = self.bits[:nrows].cpu().numpy().view(np.uint64)
+            norms = self.norms[:nrows].cpu().numpy()
+            valid = self.valid[:nrows].cpu().numpy()
+        else:
+            bits, norms, valid = self.bits[:nrows], self.norms[:nrows], self.valid[:nrows]
+        return {"bits": np.ascontiguousarray(bits).tobytes(), "norms": norms.tobytes(),
+                "valid": valid.tobytes(), "n": nrows}
+
+    def load_state(self, st: dict) -> None:
+        n = int(st["n"])
+        self.clear()
+        c = 1024
+        while c < n:
+            c *= 2
+        self.cap = 0
+        self._alloc(c)
+        bits = np.frombuffer(st["bits"], dtype=np.uint64).reshape(n, self.words)
+        norms = np.frombuffer(st["norms"], dtype=np.float32)
+        valid = np.frombuffer(st["valid"], dtype=np.uint8)
+        if self.gpu:
+            import torch
+            self.bits[:n] = torch.from_numpy(bits.view(np.int64).copy()).to(self.device)
+            self.norms[:n] = torch.from_numpy(norms.copy()).to(self.device)
+            self.valid[:n] = torch.from_numpy(valid.copy()).to(self.device)
+        else:
+            self.bits[:n], self.norms[:n], self.valid[:n] = bits, norms, valid
+
+
+def topk(d, k: int, to_sim=None) -> list[list[tuple[int, float]]]:
+    """smallest-k distances per query row (inf = absent), optionally mapped to
+    similarities."""
+    out = []
+    if hasattr(d, "is_cuda"):
+        import torch
+        n = d.shape[1]
+        kk = min(k, n)
+        if kk <= 0:
+            return [[] for _ in range(d.shape[0])]
+        vals, idx = torch.topk(d, kk, dim=1, largest=False)
+        vals, idx = vals.cpu().numpy(), idx.cpu().numpy()
+    else:
+        n = d.shape[1]
+        kk = min(k, n)
+        if kk <= 0:
+            return [[] for _ in range(d.shape[0])]
+        idx = np.argsort(d, axis=1, kind="stable")[:, :kk]
+        vals = np.take_along_axis(d, idx, axis=1)
+    for vr, ir in zip(vals, idx):
+        row = []
+        for v, i in zip(vr, ir):
+            if not np.isfinite(v):
+                continue
+            row.append((int(i), float(to_sim(np.float32(v)) if to_sim else v)))
+        out.append(row)
+    return out
+
+
+def _csr_device(rows, device):
+    import torch
+    n = len(rows)
+    lens = np.fromiter((len(r[0]) for r in rows), dtype=np.int64, count=n)
+    rp = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(lens, out=rp[1:])
+    nnz = int(rp[-1])
+    idx = np.fromiter((i for r in rows for i in r[0]), dtype=np.int32, count=nnz)
+    val = np.fromiter((v for r in rows for v in r[1]), dtype=np.float32, count=nnz)
+    if nnz == 0:
+        idx, val = np.zeros(1, np.int32), np.zeros(1, np.float32)
+    return (torch.from_numpy(rp).to(device), torch.from_numpy(idx).to(device),
+            torch.from_numpy(val).to(device))
+
+
+class InvertedIndex:
+    """Exact sparse similarity (inverted_index: cosine; inverted_index_euclid:
+    euclidean distance). Rows kept as sorted sparse vectors on the host; on a
+    GPU a CSR mirror is rebuilt lazily after changes and scanned by
+    ``sparse_scan`` (csrc/hip/lsh.hip)."""
+
+    def __init__(self, euclid: bool = False, device: Any = None):
+        self.euclid = euclid
+        self.device = device
+        self.gpu = device is not None
+        self.rows: dict[int, tuple[np.ndarray, np.ndarray]] = {}
+        self._dirty = True
+        self._dev = None
+
+    def clear(self) -> None:
+        self.rows.clear()
+        self._dirty = True
+
+    @staticmethod
+    def _norm_row(idx, val) -> tuple[np.ndarray, np.ndarray]:
+        d: dict[int, float] = {}
+        for i, v in zip(idx, val):
+            if i >= 0:
+                d[int(i)] = d.get(int(i), 0.0) + float(v)
+        ks = np.asarray(sorted(d), dtype=np.int32)
+        return ks, np.asarray([d[int(k)] for k in ks], dtype=np.float32)
+
+    def set_rows(self, slots, rows) -> None:
+        for s, (i, v) in zip(slots, rows):
+            self.rows[int(s)] = self._norm_row(i, v)
+        self._dirty = True
+
+    def remove(self, slot: int) -> None:
+        self.rows.pop(int(slot), None)
+        self._dirty = True
+
+    def _mirror(self, nrows: int):
+        import torch
+        if not self._dirty and self._dev is not None and self._dev[0] == nrows:
+            return self._dev
+        lens = np.zeros(nrows, dtype=np.int64)
+        valid = np.zeros(nrows, dtype=np.uint8)
+        for s, (i, _) in self.rows.items():
+            if s < nrows:
+                lens[s] = len(i)
+                valid[s] = 1
+        rp = np.zeros(nrows + 1, dtype=np.int64)
+        np.cumsum(lens, out=rp[1:])
+        nnz = int(rp[-1])
+        idx = np.zeros(max(nnz, 1), dtype=np.int32)
+        val = np.zeros(max(nnz, 1), dtype=np.float32)
+        n2 = np.zeros(nrows, dtype=np.float32)
+        for s, (i, v) in self.rows.items():
+            if s < nrows:
+                idx[rp[s]:rp[s + 1]] = i
+                val[rp[s]:rp[s + 1]] = v
+                n2[s] = float((v.astype(np.float64) ** 2).sum())
+        d = self.device
+        self._dev = (nrows, torch.from_numpy(rp).to(d), torch.from_numpy(idx).to(d),
+                     torch.from_numpy(val).to(d), torch.from_numpy(n2).to(d),
+                     torch.from_numpy(valid).to(d))
+        self._dirty = False
+        return self._dev
+
+    def scores(self, row, nrows: int) -> np.ndarray:
+        """similarity (cosine) or distance (euclid) of one query vs every slot"""
+        qi, qv = self._norm_row(*row)
+        q2 = float((qv.astype(np.float64) ** 2).sum())
+        if self.gpu and nrows:
+            import torch
+            from ..ops import hip
+            _, rp, ridx, rval, rn2, valid = self._mirror(nrows)
+            out = torch.empty(nrows, dtype=torch.float32, device=self.device)
+            hip.sparse_scan(torch.from_numpy(qi).to(self.device), torch.from_numpy(qv).to(self.device),
+                            q2, rp, ridx, rval, rn2, valid, nrows, 1 if self.euclid else 0, out)
+            return out.cpu().numpy()
+        out = np.full(nrows, np.inf if self.euclid else -np.inf, dtype=np.float32)
+        qd = dict(zip(qi.tolist(), qv.tolist()))
+        for s, (i, v) in self.rows.items():
+            if s >= nrows:
+                continue
+            dot = sum(float(x) * qd.get(int(k), 0.0) for k, x in zip(i, v))
+            r2 = float((v.astype(np.float64) ** 2).sum())
+            if self.euclid:
+                out[s] = math.sqrt(max(0.0, q2 + r2 - 2 * dot))
+            else:
+                den = math.sqrt(q2) * math.sqrt(r2)
+                out[s] = dot / den if den > 0 else 0.0
+        return out
+
+    def query(self, rows: list, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
+        res = []
+        for row in rows:
+            s = self.scores(row, nrows)
+            d = s if self.euclid else (1.0 - s)        # distance view
+            d = np.where(np.isfinite(s), d, np.inf).astype(np.float32)
+            (r,) = topk(d[None, :], k, None)
+            if similar:
+                r = [(i, float(-dd if self.euclid else 1.0 - dd)) for i, dd in r]
+            res.append(r)
+        return res

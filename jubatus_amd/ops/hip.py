@@ -28,7 +28,53 @@ _SIGS = {
     "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
                            _c_void_p],
     "jb_scale": [_c_void_p, _i64, _f32, _c_void_p],
+    "jb_regression_train": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
+                            _c_void_p, _c_void_p, _f32, _f32, _i32, _c_void_p],
+    "jb_regression_estimate": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                               _c_void_p],
+    "jb_signature": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _u64, _i32, _c_void_p,
+                     _c_void_p, _c_void_p],
+    "jb_hamming_scan": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
+                        _i32, _i32, _c_void_p, _c_void_p],
+    "jb_sparse_scan": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _c_void_p,
+                       _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
 }
+
+
+def signature(row_ptr, fidx, fval, n: int, hash_num: int, seed: int, mode: int, bits, norms) -> None:
+    words = (hash_num + 63) // 64
+    _dev(bits, torch.int64, "bits")
+    _dev(norms, torch.float32, "norms")
+    if bits.numel() < n * words or norms.numel() < n or row_ptr.numel() < n + 1:
+        raise ValueError("signature: bad operand shapes")
+    rc = _fn("jb_signature")(_p(row_ptr), _p(fidx), _p(fval), n, hash_num, seed & (2**64 - 1),
+                             mode, _p(bits), _p(norms), _stream())
+    _check(rc, "jb_signature")
+
+
+def hamming_scan(qbits, qnorm, nq: int, tbits, tnorm, valid, nrows: int, hash_num: int,
+                 metric: int, out) -> None:
+    words = (hash_num + 63) // 64
+    _dev(out, torch.float32, "out")
+    _dev(valid, torch.uint8, "valid")
+    if (qbits.numel() < nq * words or tbits.numel() < nrows * words or out.numel() < nq * nrows
+            or valid.numel() < nrows or tnorm.numel() < nrows or qnorm.numel() < nq):
+        raise ValueError("hamming_scan: bad operand shapes")
+    rc = _fn("jb_hamming_scan")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid), nrows,
+                                words, hash_num, metric, _p(out), _stream())
+    _check(rc, "jb_hamming_scan")
+
+
+def sparse_scan(qidx, qval, qnorm2: float, row_ptr, ridx, rval, rnorm2, valid, nrows: int,
+                metric: int, out) -> None:
+    qn = qidx.numel()
+    if qn > 4096:
+        raise ValueError("sparse_scan: query has more than 4096 features")
+    if out.numel() < nrows or row_ptr.numel() < nrows + 1 or valid.numel() < nrows:
+        raise ValueError("sparse_scan: bad operand shapes")
+    rc = _fn("jb_sparse_scan")(_p(qidx), _p(qval), qn, float(qnorm2), _p(row_ptr), _p(ridx),
+                               _p(rval), _p(rnorm2), _p(valid), nrows, metric, _p(out), _stream())
+    _check(rc, "jb_sparse_scan")
 
 _fns: dict = {}
 
@@ -130,3 +176,26 @@ def scale_(t: torch.Tensor, a: float) -> None:
     _dev(t, torch.float32, "t")
     rc = _fn("jb_scale")(_p(t), t.numel(), float(a), _stream())
     _check(rc, "jb_scale")
+
+
+def regression_train(row_ptr, fidx, fval, targets, stream_ptr, nstreams: int, W, stats,
+                     C: float, eps: float, concurrent: bool) -> None:
+    _dev(W, torch.float32, "W")
+    _dev(stats, torch.float32, "stats")
+    _dev(targets, torch.float32, "targets")
+    if W.dim() != 1 or stats.numel() < 3 or stream_ptr.numel() < nstreams + 1:
+        raise ValueError("regression_train: bad operand shapes")
+    rc = _fn("jb_regression_train")(_p(row_ptr), _p(fidx), _p(fval), _p(targets), _p(stream_ptr),
+                                    nstreams, _p(W), _p(stats), float(C), float(eps),
+                                    1 if concurrent else 0, _stream())
+    _check(rc, "jb_regression_train")
+
+
+def regression_estimate(row_ptr, fidx, fval, n: int, W, out) -> None:
+    _dev(W, torch.float32, "W")
+    _dev(out, torch.float32, "out")
+    if out.numel() < n or row_ptr.numel() < n + 1:
+        raise ValueError("regression_estimate: bad operand shapes")
+    rc = _fn("jb_regression_estimate")(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), _p(out),
+                                       _stream())
+    _check(rc, "jb_regression_estimate")
