@@ -38,7 +38,25 @@ _SIGS = {
                         _i32, _i32, _c_void_p, _c_void_p],
     "jb_sparse_scan": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
+    "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
+                       _c_void_p],
 }
+
+
+def sqdist(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+    """[n, k] squared euclidean distances on the matrix cores (fp32 MFMA)."""
+    _dev(X, torch.float32, "X")
+    _dev(C, torch.float32, "C")
+    n, d = X.shape
+    k, d2 = C.shape
+    if d != d2:
+        raise ValueError("sqdist: dimension mismatch")
+    xn2 = (X * X).sum(1).contiguous()
+    cn2 = (C * C).sum(1).contiguous()
+    out = torch.empty((n, k), dtype=torch.float32, device=X.device)
+    rc = _fn("jb_sqdist_mfma")(_p(X), n, _p(C), k, d, _p(xn2), _p(cn2), _p(out), _stream())
+    _check(rc, "jb_sqdist_mfma")
+    return out
 
 
 def signature(row_ptr, fidx, fval, n: int, hash_num: int, seed: int, mode: int, bits, norms) -> None:

@@ -117,3 +117,29 @@ def test_engines_on_gpu():
     for i in range(60):
         lof.add(str(i), {"x": float(i % 6) * 0.1, "y": float(i % 4) * 0.1})
     assert lof.calc_score({"x": 40.0, "y": -30.0}) > lof.calc_score({"x": 0.2, "y": 0.1})
+
+
+@pytest.mark.parametrize("n,k,d", [(1, 1, 1), (100, 3, 2), (777, 37, 130), (4096, 64, 33)])
+def test_sqdist_mfma_matches_fp32(n, k, d):
+    import torch
+    from jubatus_amd.ops import hip
+    g = torch.Generator().manual_seed(n + k + d)
+    X = torch.randn(n, d, generator=g)
+    C = torch.randn(k, d, generator=g)
+    ref = ((X[:, None, :] - C[None, :, :]) ** 2).sum(-1)
+    out = hip.sqdist(X.to(dev()), C.to(dev())).cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4 * d)
+
+
+def test_clustering_on_gpu_matches_cpu():
+    from jubatus_amd.models.clustering import Clustering
+    p = {"k": 3, "compressor_method": "compressive_kmeans", "bucket_size": 90,
+         "compressed_bucket_size": 30, "seed": 0}
+    conv = {"num_rules": [{"key": "*", "type": "num"}]}
+    r = random.Random(0)
+    pts = [{"x": cx + r.gauss(0, 0.3), "y": cy + r.gauss(0, 0.3)}
+           for i in range(180) for cx, cy in [[(0, 0), (8, 8), (-8, 8)][i % 3]]]
+    g = Clustering("kmeans", p, DatumToFvConverter(conv), dev())
+    g.push(pts)
+    cs = sorted(tuple(round(v) for _, v in sorted(c.num_values)) for c in g.get_k_center())
+    assert cs == sorted([(0, 0), (8, 8), (-8, 8)])
