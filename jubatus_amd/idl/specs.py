@@ -34,9 +34,23 @@ class Method:
         return len(self.args) + 1  # + cluster name
 
 
+def split_args(spec: str) -> tuple[str, ...]:
+    """split "a:t1, b:map<string,string>" on top-level commas only"""
+    out, depth, cur = [], 0, ""
+    for ch in spec:
+        depth += (ch == "<") - (ch == ">")
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    out.append(cur.strip())
+    return tuple(a for a in out if a)
+
+
 def M(name, args, ret, routing, lock, agg="pass", cht_n=2, doc=""):
     if isinstance(args, str):
-        args = tuple(a.strip() for a in args.split(",") if a.strip())
+        args = split_args(args)
     return Method(name, tuple(args), ret, routing, lock, agg, cht_n, doc)
 
 

@@ -365,21 +365,21 @@ class LinearClassifier:
             P = t.ones((self.H, LC), dtype=t.float32, device=self.device) if self.use_s else None
             src = perm.clamp(min=0)
             W[:, :len(order)] = t.where(have, self.W.index_select(1, src), W[:, :len(order)])
-            if S is not None:
-                S[:, :len(order)] = t.where(have, self.P.index_select(1, src), S[:, :len(order)])
+            if P is not None:
+                P[:, :len(order)] = t.where(have, self.P.index_select(1, src), P[:, :len(order)])
         else:
             W = np.zeros((self.H, LC), dtype=np.float32)
             P = np.ones((self.H, LC), dtype=np.float32) if self.use_s else None
             for c, n in enumerate(order):
                 if n in old:
                     W[:, c] = self.W[:, old[n]]
-                    if S is not None:
-                        S[:, c] = self.P[:, old[n]]
+                    if P is not None:
+                        P[:, c] = self.P[:, old[n]]
         self.labels.clear()
         for c, n in enumerate(order):
             self.labels.get_or_add(n)
             self.labels.set_count(c, counts.get(n, 0))
-        self.W, self.P, self.LC = W, S, LC
+        self.W, self.P, self.LC = W, P, LC
         self.active = (self.torch.zeros(LC, dtype=self.torch.int32, device=self.device)
                        if self.gpu else np.zeros(LC, dtype=np.int32))
         self._label_version = -1
@@ -426,7 +426,7 @@ class LinearClassifier:
         cur = np.array([self.labels.count(i) for i in range(len(names))], dtype=np.int64)
         b = np.array([base.get(n, 0) for n in names], dtype=np.int64)
         delta = torch.from_numpy(cur - b)
-        if self.gpu and coll.is_dist() and __import__("torch.distributed").distributed.get_backend(group) == "nccl":
+        if self.gpu and coll.is_dist() and coll.backend(group) == "nccl":
             d = delta.to(self.device)
             coll.allreduce_sum_([d], group)
             delta = d.cpu()

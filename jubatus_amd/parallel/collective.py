@@ -26,6 +26,10 @@ def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
+def backend(group=None) -> str:
+    return str(dist.get_backend(group))
+
+
 def world() -> int:
     return dist.get_world_size() if is_dist() else 1
 

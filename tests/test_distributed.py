@@ -8,6 +8,7 @@ push mixers (pairwise send/recv)."""
 import os
 import socket
 import subprocess
+import tempfile
 import sys
 import time
 
@@ -38,12 +39,16 @@ def coord():
     srv.stop()
 
 
+LOGDIR = os.environ.get("JUBATUS_TEST_LOGDIR", tempfile.gettempdir())
+
+
 def spawn(engine, zport, name, port, mixer="linear_mixer", extra=()):
     env = dict(os.environ, PYTHONPATH=ROOT, JUBATUS_FORCE_CPU="1")
     cmd = [sys.executable, "-m", "jubatus_amd.cmd.server", engine, "-z", f"127.0.0.1:{zport}",
            "-n", name, "-p", str(port), "-b", "127.0.0.1", "-x", mixer, "-s", "0", "-i", "0",
            "-I", "5", "--cpu", *extra]
-    return subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    log = open(os.path.join(LOGDIR, f"{engine}_{name}_{port}.log"), "wb")
+    return subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=log)
 
 
 def wait_actives(ls, engine, name, n, timeout=60):

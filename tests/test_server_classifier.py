@@ -125,3 +125,34 @@ def test_concurrent_train_and_classify(server):
     assert not errs
     with Classifier("127.0.0.1", port, "") as c:
         assert sum(c.get_labels().values()) == 80
+
+
+@pytest.mark.parametrize("cfg", ["nn.json", "cosine.json", "euclidean.json"])
+def test_nn_classifiers(tmp_path, cfg):
+    """NN / cosine / euclidean classifiers (models/nn_classifier.py)"""
+    from helpers import config_path, start_standalone
+    from jubatus_amd.client import Classifier, Datum, EstimateResult
+    h = start_standalone("classifier", config_path(f"classifier/{cfg}"), tmp_path)
+    try:
+        with Classifier("127.0.0.1", h.argv.port, "") as c:
+            data = []
+            for i in range(30):
+                lab = "pos" if i % 2 else "neg"
+                x = 3.0 if lab == "pos" else -3.0
+                data.append([lab, Datum({"x": x + 0.1 * (i % 5), "y": 1.0, "t": lab + "w"})])
+            assert c.train(data) == 30
+            assert c.get_labels() == {"pos": 15, "neg": 15}
+            res = c.classify([Datum({"x": 3.2, "y": 1.0, "t": "posw"}), Datum({"x": -2.9, "y": 1.0, "t": "negw"})])
+            assert all(isinstance(r, EstimateResult) for row in res for r in row)
+            best = [max(row, key=lambda r: r.score).label for row in res]
+            assert best == ["pos", "neg"]
+            assert c.set_label("other") is True and c.set_label("other") is False
+            assert c.get_labels()["other"] == 0
+            c.save("nn")
+            assert c.delete_label("pos") is True
+            assert set(c.get_labels()) == {"neg", "other"}
+            assert all(r.label != "pos" for r in c.classify([Datum({"x": 3.0})])[0])
+            assert c.load("nn") is True and c.get_labels()["pos"] == 15
+            assert c.clear() is True and c.get_labels() == {}
+    finally:
+        h.stop()
