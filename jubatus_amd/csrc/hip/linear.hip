@@ -165,169 +165,509 @@ __device__ __forceinline__ void argmax_wrong(float& best, int& bl) {
   }
 }
 
-// Staged-row capacity of the fast path: NMAX features x LC labels per wave.
-template <int LC>
-struct Stage {
-  static constexpr int NMAX = LC <= 64 ? 1024 / LC : 0;
-};
-
+// One sample on the direct path: gathers straight from W / P (any feature
+// count, any label capacity) and applies the update. Used for samples wider
+// than the pipelined window and for label capacities above 64.
 template <int LC, int MODE>
-__global__ __launch_bounds__(256) void linear_train_kernel(
+__device__ __forceinline__ void general_sample(const int32_t* __restrict__ fidx,
+                                               const float* __restrict__ fval, int64_t beg, int n,
+                                               int y, float* W, float* P, const bool (&act)[Lanes<LC>::K],
+                                               int lane, int method, float C) {
+  using L = Lanes<LC>;
+  const int l0 = lane % L::LW;
+  const bool use_s = method >= CW;
+  float acc[L::K];
+  sample_scores<LC>(fidx, fval, beg, n, W, lane, acc);
+  float sy = 0.f, best = -INFINITY;
+  int bl = -1;
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) {
+    const int l = l0 + 64 * k;
+    if (l == y) sy = acc[k];
+    if (act[k] && l != y && acc[k] > best) { best = acc[k]; bl = l; }
+  }
+  sy = __shfl(sy, y % L::LW, 64);
+  argmax_wrong<L::LW>(best, bl);
+  const int lstar = bl;
+  const float margin = sy - (lstar >= 0 ? best : 0.f);
+  float var = 0.f, nrm = 0.f;
+  for (int base = 0; base < n; base += 64) {
+    const int j = base + lane;
+    if (j < n) {
+      const int32_t idx = fidx[beg + j];
+      const float x = fval[beg + j];
+      if (idx >= 0) {
+        const int64_t row = (int64_t)idx * LC;
+        nrm += x * x;
+        if (use_s) {
+          const float a = 1.f / ld_agent(P + row + y);
+          const float b = lstar >= 0 ? 1.f / ld_agent(P + row + lstar) : 0.f;
+          var += x * x * (a + b);
+        }
+      }
+    }
+  }
+  var = wave_sum(var);
+  nrm = wave_sum(nrm);
+  float tau = 0.f, beta = 0.f;
+  if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return;
+  for (int base = 0; base < n; base += 64) {
+    const int j = base + lane;
+    if (j >= n) continue;
+    const int32_t idx = fidx[beg + j];
+    if (idx < 0) continue;
+    const float x = fval[beg + j];
+    const int64_t row = (int64_t)idx * LC;
+    const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
+    const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
+    float wy = 0.f, wl = 0.f;
+    if (MODE != kAtomic) {
+      wy = ld_agent(W + row + y);
+      wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f;
+    }
+    apply_feature<LC, MODE>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, wy, wl);
+  }
+}
+
+// Label capacities above 64: every sample on the direct path.
+template <int LC, int MODE>
+__global__ __launch_bounds__(256) void linear_train_wide_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
     const int32_t* __restrict__ active, int method, float C) {
   using L = Lanes<LC>;
-  constexpr int NMAX = Stage<LC>::NMAX;
-  // per-wave LDS image of the gathered W / P rows of the current sample
-  __shared__ float sW[4][NMAX > 0 ? NMAX * LC : 1];
-  __shared__ float sP[4][NMAX > 0 ? NMAX * LC : 1];
+  const int lane = threadIdx.x & 63;
+  const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (wid >= nstreams) return;
+  bool act[L::K];
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
+  for (int64_t s = stream_ptr[wid]; s < stream_ptr[wid + 1]; ++s) {
+    const int y = labels[s];
+    if (y < 0 || y >= LC) continue;
+    const int64_t beg = row_ptr[s];
+    general_sample<LC, MODE>(fidx, fval, beg, (int)(row_ptr[s + 1] - beg), y, W, P, act, lane,
+                             method, C);
+    if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined path (LC <= 64). A sample's W / P rows are gathered with every
+// load of the sample in flight at once (U unrolled passes of G features),
+// staged in LDS, and the gather of sample s+1 is issued *before* sample s is
+// reduced and applied, so its latency hides behind s's arithmetic and the
+// in-order vmcnt never makes s+1's data wait for s's atomics. Sample s's own
+// increments are forwarded into the staged rows of s+1 (an LDS add wherever
+// s+1 reuses one of s's features), so one stream still sees exactly its own
+// sequential updates; other streams' updates arrive as the loads observe
+// them (the same lock-free semantics as before). Per-sample descriptors
+// (row offsets, labels) come from a 64-entry register window refreshed every
+// ~60 samples; feature descriptors of s+2 are prefetched during s.
+template <int LC>
+struct Pipe {
+  static_assert(LC <= 64, "pipelined path covers label capacities up to 64");
+  static constexpr int G = 64 / LC;              // features per pass
+  static constexpr int F = LC <= 32 ? 32 : 16;   // max features of a staged sample
+  static constexpr int U = F / G;                // unrolled passes per gather
+};
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int i) {
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, i);
+  const int hi = __builtin_amdgcn_readlane((int)((uint64_t)v >> 32), i);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Issue the gather of one staged sample: lane (g, l0) loads W / P of
+// features u*G + g, label l0. Every load is unconditional (invalid slots read
+// row 0) and nothing reads the results here, so the whole gather is U (or 2U)
+// loads in flight; ``vmask`` bit u marks the valid slots for the commit.
+template <int LC>
+__device__ __forceinline__ uint32_t gather_issue(const float* W, const float* P, bool use_s,
+                                                 const int32_t* sI, int n, int g, int l0,
+                                                 float (&gw)[Pipe<LC>::U],
+                                                 float (&gp)[Pipe<LC>::U]) {
+  using Q = Pipe<LC>;
+  int64_t rows[Q::U];
+  uint32_t vmask = 0;
+#pragma unroll
+  for (int u = 0; u < Q::U; ++u) {
+    const int j = u * Q::G + g;
+    const int32_t idx = sI[j];
+    const bool v = j < n && idx >= 0;
+    vmask |= (v ? 1u : 0u) << u;
+    rows[u] = (int64_t)(v ? idx : 0) * LC + l0;
+  }
+  if (use_s) {
+#pragma unroll
+    for (int u = 0; u < Q::U; ++u) {
+      gw[u] = ld_agent(W + rows[u]);
+      gp[u] = ld_agent(P + rows[u]);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < Q::U; ++u) {
+      gw[u] = ld_agent(W + rows[u]);
+      gp[u] = 1.f;
+    }
+  }
+  return vmask;
+}
+
+template <int LC>
+__device__ __forceinline__ void gather_commit(float* sW, float* sP, bool use_s, int n, int g,
+                                              int l0, uint32_t vmask,
+                                              const float (&gw)[Pipe<LC>::U],
+                                              const float (&gp)[Pipe<LC>::U]) {
+  using Q = Pipe<LC>;
+#pragma unroll
+  for (int u = 0; u < Q::U; ++u) {
+    const int j = u * Q::G + g;
+    const bool v = (vmask >> u) & 1u;
+    if (j < n) {
+      sW[j * LC + l0] = v ? gw[u] : 0.f;
+      if (use_s) sP[j * LC + l0] = v ? gp[u] : 1.f;
+    }
+  }
+}
+
+// feature list of a sample into its LDS slot (lane j = feature j)
+template <int LC>
+__device__ __forceinline__ void put_features(int32_t* sI, float* sX, int32_t idx, float x, int n,
+                                             int lane) {
+  if (lane < Pipe<LC>::F) {
+    const bool v = lane < n && idx >= 0;
+    sI[lane] = v ? idx : -1;
+    sX[lane] = v ? x : 0.f;
+  }
+}
+
+// Per-wave write-combining cache of a stream's own increments (atomic mode).
+// Hot rows (features nearly every sample carries: numeric keys, frequent
+// tokens) would otherwise take one float atomic per sample from every
+// stream and serialise at their L2 line; instead a stream accumulates its
+// increments in LDS (direct-mapped, CE rows) and flushes a row when another
+// row claims its slot or when the stream ends. Gathered rows are folded with
+// the cached increments, so the stream still sees all of its own updates.
+template <int LC>
+struct DCache {
+  static constexpr int CE = 1024 / LC;  // entries (power of two)
+};
+
+template <int LC>
+__device__ __forceinline__ void cache_init(int32_t* cT, float* cW, float* cP, int lane) {
+  constexpr int CE = DCache<LC>::CE;
+  for (int i = lane; i < CE; i += 64) cT[i] = -1;
+  for (int i = lane; i < CE * LC; i += 64) {
+    cW[i] = 0.f;
+    cP[i] = 0.f;
+  }
+}
+
+// flush every cached row (all lanes cooperate: lane i -> (entry, label))
+template <int LC>
+__device__ __forceinline__ void cache_flush_all(int32_t* cT, float* cW, float* cP, float* W,
+                                                float* P, bool use_s, int lane) {
+  constexpr int CE = DCache<LC>::CE;
+  for (int i = lane; i < CE * LC; i += 64) {
+    const int32_t tag = cT[i / LC];
+    if (tag >= 0) {
+      const int64_t a = (int64_t)tag * LC + (i % LC);
+      const float dw = cW[i];
+      if (dw != 0.f) atomicAdd(W + a, dw);
+      if (use_s) {
+        const float dp = cP[i];
+        if (dp != 0.f) atomicAdd(P + a, dp);
+      }
+    }
+    cW[i] = 0.f;
+    cP[i] = 0.f;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < CE; i += 64) cT[i] = -1;
+  __builtin_amdgcn_wave_barrier();
+}
+
+// staged rows of a sample += the stream's cached increments of those rows
+template <int LC>
+__device__ __forceinline__ void cache_fold(float* sW, float* sP, const int32_t* sI, int n, int g,
+                                           int l0, const int32_t* cT, const float* cW,
+                                           const float* cP, bool use_s) {
+  using Q = Pipe<LC>;
+  constexpr int CE = DCache<LC>::CE;
+#pragma unroll
+  for (int u = 0; u < Q::U; ++u) {
+    const int j = u * Q::G + g;
+    if (j < n) {
+      const int32_t idx = sI[j];
+      if (idx >= 0) {
+        const int slot = idx & (CE - 1);
+        if (cT[slot] == idx) {
+          sW[j * LC + l0] += cW[slot * LC + l0];
+          if (use_s) sP[j * LC + l0] += cP[slot * LC + l0];
+        }
+      }
+    }
+  }
+}
+
+// make the compiler wait for these registers here (before later atomics
+// enter the in-order vmcnt queue) instead of at their first use
+#define JB_CONSUME(r) asm volatile("" ::"v"(r))
+
+template <int LC, int MODE>
+__global__ __launch_bounds__(256) void linear_train_pipe_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
+    const float* __restrict__ fval, const int32_t* __restrict__ labels,
+    const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
+    const int32_t* __restrict__ active, int method, float C) {
+  using Q = Pipe<LC>;
+  constexpr int F = Q::F;
+  __shared__ float sW[4][2][F * LC];
+  __shared__ float sP[4][2][F * LC];
+  __shared__ int32_t sI[4][2][F];
+  __shared__ float sX[4][2][F];
+  constexpr bool CACHE = MODE == kAtomic;
+  constexpr int CE = CACHE ? DCache<LC>::CE : 1;
+  __shared__ int32_t cT[4][CE];
+  __shared__ int32_t cClaim[4][CE];
+  __shared__ float cW[4][CE * (CACHE ? LC : 1)];
+  __shared__ float cP[4][CE * (CACHE ? LC : 1)];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (wid >= nstreams) return;
-  const int g = lane / L::LW;
-  const int l0 = lane % L::LW;
-  bool act[L::K];
-#pragma unroll
-  for (int k = 0; k < L::K; ++k) act[k] = active[l0 + 64 * k] != 0;
+  const int g = lane / LC;
+  const int l0 = lane % LC;
+  bool act[1] = {active[l0] != 0};
   const bool use_s = method >= CW;
+  if (CACHE) cache_init<LC>(cT[wv], cW[wv], cP[wv], lane);
 
   const int64_t s_beg = stream_ptr[wid], s_end = stream_ptr[wid + 1];
-  // software prefetch of the next sample's (idx, x) for lane j = feature j
-  int64_t nb = s_beg < s_end ? row_ptr[s_beg] : 0;
-  int nn = s_beg < s_end ? (int)(row_ptr[s_beg + 1] - nb) : 0;
-  int32_t pidx = (lane < nn) ? fidx[nb + lane] : -1;
-  float px = (lane < nn) ? fval[nb + lane] : 0.f;
-  int py = s_beg < s_end ? labels[s_beg] : -1;
+  if (s_beg >= s_end) return;
+  // descriptor window: lane i holds row_ptr[wb + i] and labels[wb + i]
+  int64_t wb = s_beg;
+  int64_t rp = (wb + lane <= s_end) ? row_ptr[wb + lane] : 0;
+  int lab = (wb + lane < s_end) ? labels[wb + lane] : -1;
+
+  // feature descriptors of sample s (current) and s+1, lane j = feature j
+  const int64_t beg0 = readlane64(rp, 0);
+  int n_s = (int)(readlane64(rp, 1) - beg0);
+  int y_s = __builtin_amdgcn_readlane(lab, 0);
+  int32_t idx_s = lane < n_s ? fidx[beg0 + lane] : -1;
+  float x_s = lane < n_s ? fval[beg0 + lane] : 0.f;
+  int n1 = 0, y1 = -1;
+  int32_t idx1 = -1;
+  float x1 = 0.f;
+  if (s_beg + 1 < s_end) {
+    const int64_t b1 = readlane64(rp, 1);
+    n1 = (int)(readlane64(rp, 2) - b1);
+    y1 = __builtin_amdgcn_readlane(lab, 1);
+    idx1 = lane < n1 ? fidx[b1 + lane] : -1;
+    x1 = lane < n1 ? fval[b1 + lane] : 0.f;
+  }
+  JB_CONSUME(idx_s);
+  JB_CONSUME(x_s);
+  JB_CONSUME(idx1);
+  JB_CONSUME(x1);
+  put_features<LC>(sI[wv][0], sX[wv][0], idx_s, x_s, n_s, lane);
+  put_features<LC>(sI[wv][1], sX[wv][1], idx1, x1, n1, lane);
+  float gw[Q::U], gp[Q::U];
+  uint32_t vmask = 0;
+  bool staged = n_s <= F;
+  if (staged) {
+    vmask = gather_issue<LC>(W, P, use_s, sI[wv][0], n_s, g, l0, gw, gp);
+    gather_commit<LC>(sW[wv][0], sP[wv][0], use_s, n_s, g, l0, vmask, gw, gp);
+  }
 
   for (int64_t s = s_beg; s < s_end; ++s) {
-    const int64_t beg = nb;
-    const int n = nn;
-    const int y = py;
-    const int32_t my_idx = pidx;
-    const float my_x = px;
-    if (s + 1 < s_end) {  // issue next sample's descriptor loads now
-      nb = row_ptr[s + 1];
-      nn = (int)(row_ptr[s + 2] - nb);
-      pidx = (lane < nn) ? fidx[nb + lane] : -1;
-      px = (lane < nn) ? fval[nb + lane] : 0.f;
-      py = labels[s + 1];
+    const int c = (int)((s - s_beg) & 1);
+    const int c1 = c ^ 1;
+    if (s + 3 - wb > 63) {  // slide the descriptor window (every ~60 samples)
+      wb = s;
+      rp = (wb + lane <= s_end) ? row_ptr[wb + lane] : 0;
+      lab = (wb + lane < s_end) ? labels[wb + lane] : -1;
+      JB_CONSUME(rp);
+      JB_CONSUME(lab);
     }
-    if (y < 0 || y >= LC) continue;
-
-    if (NMAX > 0 && n <= NMAX && n <= 64) {
-      // ---------------- fast path: one gather round trip, rows staged in LDS
+    const bool valid_s = y_s >= 0 && y_s < LC;
+    const bool general_s = valid_s && !staged;
+    const bool pipe1 = s + 1 < s_end && n1 <= F;
+    const bool early = pipe1 && !general_s;
+    // 1. the gather of s+1 goes in flight first
+    if (early) vmask = gather_issue<LC>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
+    // 2. feature descriptors of s+2
+    int n2 = 0, y2 = -1;
+    int32_t idx2 = -1;
+    float x2 = 0.f;
+    if (s + 2 < s_end) {
+      const int i2 = (int)(s + 2 - wb);
+      const int64_t b2 = readlane64(rp, i2);
+      n2 = (int)(readlane64(rp, i2 + 1) - b2);
+      y2 = __builtin_amdgcn_readlane(lab, i2);
+      idx2 = lane < n2 ? fidx[b2 + lane] : -1;
+      x2 = lane < n2 ? fval[b2 + lane] : 0.f;
+    }
+    // 3. sample s (from LDS while the loads above are in flight)
+    bool upd = false;
+    int lstar = -1;
+    float dwy = 0.f, dwl = 0.f, dpy = 0.f, dpl = 0.f, py = 1.f, pl = 1.f, wy = 0.f, wl = 0.f;
+    const bool mine = lane < n_s && idx_s >= 0;
+    if (general_s) {
+      if (CACHE) {  // the direct path reads the table: hand it our pending increments first
+        cache_flush_all<LC>(cT[wv], cW[wv], cP[wv], W, P, use_s, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      const int i = (int)(s - wb);
+      const int64_t b0 = readlane64(rp, i);
+      general_sample<LC, MODE>(fidx, fval, b0, (int)(readlane64(rp, i + 1) - b0), y_s, W, P, act,
+                               lane, method, C);
+    } else if (valid_s) {
+      const float* cw = sW[wv][c];
+      const float* cp = sP[wv][c];
+      const float* cx = sX[wv][c];
       float acc = 0.f;
-      // wave-uniform trip count: every lane takes part in each shuffle
-      for (int j0 = 0; j0 < n; j0 += L::G) {
-        const int j = j0 + g;
-        const int src = j < 64 ? j : 63;
-        const int32_t idx = __shfl(my_idx, src, 64);
-        const float x = __shfl(my_x, src, 64);
-        if (j < n) {
-          float w = 0.f, pr = 1.f;
-          if (idx >= 0) {
-            const int64_t row = (int64_t)idx * LC + l0;
-            w = ld_agent(W + row);
-            if (use_s) pr = ld_agent(P + row);
-            acc += x * w;
-          }
-          sW[wv][j * LC + l0] = w;
-          if (use_s) sP[wv][j * LC + l0] = pr;
-        }
-      }
+      for (int j = g; j < n_s; j += Q::G) acc += cx[j] * cw[j * LC + l0];
 #pragma unroll
-      for (int off = L::LW; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
-      const float sy = __shfl(acc, y % L::LW, 64);
-      float best = (act[0] && l0 != y) ? acc : -INFINITY;
-      int bl = (act[0] && l0 != y) ? l0 : -1;
-      argmax_wrong<L::LW>(best, bl);
-      const int lstar = bl;
+      for (int off = LC; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
+      const float sy = __shfl(acc, y_s, 64);
+      float best = (act[0] && l0 != y_s) ? acc : -INFINITY;
+      int bl = (act[0] && l0 != y_s) ? l0 : -1;
+      argmax_wrong<LC>(best, bl);
+      lstar = bl;
       const float margin = sy - (lstar >= 0 ? best : 0.f);
-      __builtin_amdgcn_wave_barrier();
-      // lane-per-feature: staged values of feature `lane`
-      float a = 1.f, b = 1.f, wy = 0.f, wl = 0.f, x2 = 0.f;
-      const bool mine = lane < n && my_idx >= 0;
+      float a = 1.f, b = 1.f, x2s = 0.f;
       if (mine) {
-        x2 = my_x * my_x;
+        x2s = x_s * x_s;
         if (use_s) {
-          a = 1.f / sP[wv][lane * LC + y];
-          b = lstar >= 0 ? 1.f / sP[wv][lane * LC + lstar] : 0.f;
+          py = cp[lane * LC + y_s];
+          pl = lstar >= 0 ? cp[lane * LC + lstar] : 1.f;
+          a = 1.f / py;
+          b = lstar >= 0 ? 1.f / pl : 0.f;
         }
-        if (MODE != kAtomic) {
-          wy = sW[wv][lane * LC + y];
-          wl = lstar >= 0 ? sW[wv][lane * LC + lstar] : 0.f;
-        }
+        wy = cw[lane * LC + y_s];
+        wl = lstar >= 0 ? cw[lane * LC + lstar] : 0.f;
       }
-      const float var = wave_sum(use_s ? x2 * (a + b) : 0.f);
-      const float nrm = wave_sum(x2);
+      const float var = wave_sum(use_s ? x2s * (a + b) : 0.f);
+      const float nrm = wave_sum(x2s);
       float tau = 0.f, beta = 0.f;
-      if (step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) {
-        if (mine)
-          apply_feature<LC, MODE>(W, P, my_idx, my_x, y, lstar, use_s, method, tau, beta, a, b,
-                                  wy, wl);
-        // the next sample of this stream must observe these stores
-        if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      upd = step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta);
+      if (upd && mine) {
+        dwy = use_s ? tau * a * x_s : tau * x_s;
+        dwl = use_s ? -tau * b * x_s : -tau * x_s;
+        if (use_s) {
+          dpy = dprec(method, beta, x_s, a);
+          dpl = lstar >= 0 ? dprec(method, beta, x_s, b) : 0.f;
+        }
       }
+    }
+    // 4. stage s+1 and forward s's own increments into it
+    if (early) {
+      gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
+      if (CACHE)
+        cache_fold<LC>(sW[wv][c1], sP[wv][c1], sI[wv][c1], n1, g, l0, cT[wv], cW[wv], cP[wv], use_s);
       __builtin_amdgcn_wave_barrier();
-      continue;
-    }
-
-    // ---------------- general path (many features or > 64 labels)
-    float acc[L::K];
-    sample_scores<LC>(fidx, fval, beg, n, W, lane, acc);
-    float sy = 0.f, best = -INFINITY;
-    int bl = -1;
-#pragma unroll
-    for (int k = 0; k < L::K; ++k) {
-      const int l = l0 + 64 * k;
-      if (l == y) sy = acc[k];
-      if (act[k] && l != y && acc[k] > best) { best = acc[k]; bl = l; }
-    }
-    sy = __shfl(sy, y % L::LW, 64);
-    argmax_wrong<L::LW>(best, bl);
-    const int lstar = bl;
-    const float margin = sy - (lstar >= 0 ? best : 0.f);
-    float var = 0.f, nrm = 0.f;
-    for (int base = 0; base < n; base += 64) {
-      const int j = base + lane;
-      if (j < n) {
-        const int32_t idx = fidx[beg + j];
-        const float x = fval[beg + j];
-        if (idx >= 0) {
-          const int64_t row = (int64_t)idx * LC;
-          nrm += x * x;
-          if (use_s) {
-            const float a = 1.f / ld_agent(P + row + y);
-            const float b = lstar >= 0 ? 1.f / ld_agent(P + row + lstar) : 0.f;
-            var += x * x * (a + b);
+      if (upd && mine) {
+        const int32_t* ni = sI[wv][c1];
+        float* nw = sW[wv][c1];
+        float* np = sP[wv][c1];
+        for (int k = 0; k < n1; ++k) {
+          if (ni[k] == idx_s) {
+            atomicAdd(nw + k * LC + y_s, dwy);
+            if (lstar >= 0) atomicAdd(nw + k * LC + lstar, dwl);
+            if (use_s) {
+              atomicAdd(np + k * LC + y_s, dpy);
+              if (lstar >= 0) atomicAdd(np + k * LC + lstar, dpl);
+            }
           }
         }
       }
+      __builtin_amdgcn_wave_barrier();
     }
-    var = wave_sum(var);
-    nrm = wave_sum(nrm);
-    float tau = 0.f, beta = 0.f;
-    if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) continue;
-    for (int base = 0; base < n; base += 64) {
-      const int j = base + lane;
-      if (j >= n) continue;
-      const int32_t idx = fidx[beg + j];
-      if (idx < 0) continue;
-      const float x = fval[beg + j];
-      const int64_t row = (int64_t)idx * LC;
-      const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
-      const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
-      float wy = 0.f, wl = 0.f;
-      if (MODE != kAtomic) {
-        wy = ld_agent(W + row + y);
-        wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f;
+    JB_CONSUME(idx2);
+    JB_CONSUME(x2);
+    // 5. apply s: into the stream's cache (atomic mode) or the table
+    if (CACHE) {
+      const int slot = idx_s & (CE - 1);
+      if (upd && mine) cClaim[wv][slot] = lane;
+      __builtin_amdgcn_wave_barrier();
+      if (upd && mine && cClaim[wv][slot] == lane) {
+        const int32_t old = cT[wv][slot];
+        if (old != idx_s) {  // evict the previous row of this slot
+          if (old >= 0) {
+            const int64_t orow = (int64_t)old * LC;
+            for (int l = 0; l < LC; ++l) {
+              const float dw = cW[wv][slot * LC + l];
+              if (dw != 0.f) atomicAdd(W + orow + l, dw);
+              cW[wv][slot * LC + l] = 0.f;
+              if (use_s) {
+                const float dp = cP[wv][slot * LC + l];
+                if (dp != 0.f) atomicAdd(P + orow + l, dp);
+                cP[wv][slot * LC + l] = 0.f;
+              }
+            }
+          }
+          cT[wv][slot] = idx_s;
+        }
       }
-      apply_feature<LC, MODE>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, wy, wl);
+      __builtin_amdgcn_wave_barrier();
+      if (upd && mine) {
+        if (cT[wv][slot] == idx_s) {
+          float* ew = cW[wv] + slot * LC;
+          float* ep = cP[wv] + slot * LC;
+          atomicAdd(ew + y_s, dwy);
+          if (lstar >= 0) atomicAdd(ew + lstar, dwl);
+          if (use_s) {
+            atomicAdd(ep + y_s, dpy);
+            if (lstar >= 0) atomicAdd(ep + lstar, dpl);
+          }
+        } else {  // lost the slot to another row of this sample: straight to the table
+          const int64_t row = (int64_t)idx_s * LC;
+          atomicAdd(W + row + y_s, dwy);
+          if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+          if (use_s) {
+            atomicAdd(P + row + y_s, dpy);
+            if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else if (upd && mine) {
+      const int64_t row = (int64_t)idx_s * LC;
+      if (MODE == kAtomic) {
+        atomicAdd(W + row + y_s, dwy);
+        if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+        if (use_s) {
+          atomicAdd(P + row + y_s, dpy);
+          if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
+        }
+      } else {
+        W[row + y_s] = wy + dwy;
+        if (lstar >= 0) W[row + lstar] = wl + dwl;
+        if (use_s) {
+          P[row + y_s] = py + dpy;
+          if (lstar >= 0) P[row + lstar] = pl + dpl;
+        }
+      }
     }
-    if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (MODE == kExact && (upd || general_s)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // 6. s+1 not prefetched (s took the direct path): stage it now that s landed
+    if (pipe1 && !early) {
+      if (MODE != kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      vmask = gather_issue<LC>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
+      gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
+      if (CACHE)
+        cache_fold<LC>(sW[wv][c1], sP[wv][c1], sI[wv][c1], n1, g, l0, cT[wv], cW[wv], cP[wv], use_s);
+    }
+    // slot c is free again: it receives the features of s+2
+    put_features<LC>(sI[wv][c], sX[wv][c], idx2, x2, n2, lane);
+    __builtin_amdgcn_wave_barrier();
+    staged = pipe1;
+    idx_s = idx1; x_s = x1; n_s = n1; y_s = y1;
+    idx1 = idx2; x1 = x2; n1 = n2; y1 = y2;
   }
+  if (CACHE) cache_flush_all<LC>(cT[wv], cW[wv], cP[wv], W, P, use_s, lane);
 }
 
 template <int LC>
@@ -383,9 +723,15 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
   if (nstreams <= 0) return 0;
   const int threads = 256;
   const int blocks = (nstreams * 64 + threads - 1) / threads;
-#define JB_TRAIN_M(L, M)                                                                     \
-  hipLaunchKernelGGL((jb::linear_train_kernel<L, M>), dim3(blocks), dim3(threads), 0, stream,  \
-                     row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active, method, C);
+#define JB_TRAIN_M(L, M)                                                                      \
+  if (L <= 64)                                                                                \
+    hipLaunchKernelGGL((jb::linear_train_pipe_kernel<(L <= 64 ? L : 64), M>), dim3(blocks),    \
+                       dim3(threads), 0, stream, row_ptr, fidx, fval, labels, stream_ptr,      \
+                       nstreams, W, S, active, method, C);                                    \
+  else                                                                                        \
+    hipLaunchKernelGGL((jb::linear_train_wide_kernel<L, M>), dim3(blocks), dim3(threads), 0,  \
+                       stream, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,       \
+                       active, method, C);
 #define JB_TRAIN(L)                                        \
   if (mode == jb::kAtomic) { JB_TRAIN_M(L, jb::kAtomic) }  \
   else if (mode == jb::kHogwild) { JB_TRAIN_M(L, jb::kHogwild) } \

@@ -178,3 +178,38 @@ def test_wide_datums_general_path_and_global_parse():
     scale = float(np.abs(c.W).max()) or 1.0
     np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
     np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3, atol=2e-3 * float(c.P.max()))
+
+
+@pytest.mark.parametrize("mode", ["exact", "atomic"])
+@pytest.mark.parametrize("nlabels", [5, 12, 40])
+def test_mixed_width_stream_matches_oracle(nlabels, mode):
+    """one stream whose samples alternate between the pipelined window
+    (<= 16 / 32 features) and the direct path (wider), with features shared
+    between consecutive samples (forwarding of a sample's own increments);
+    the atomic kernel (LDS write-combining cache) must be exact for one stream."""
+    from jubatus_amd.models.classifier import LinearClassifier
+    from jubatus_amd.ops import hip
+
+    rng = random.Random(nlabels)
+    data = []
+    for i in range(240):
+        y = rng.randrange(nlabels)
+        width = rng.choice([2, 5, 15, 16, 17, 31, 32, 33, 45])
+        d = {f"k{j}": f"v{(y + j) % 7 if rng.random() < 0.8 else rng.randrange(30)}" for j in range(width)}
+        d["shared"] = "always"                      # every sample reuses this feature
+        data.append((f"L{y}", d))
+    conv = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+            "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 20}
+    for method in ("AROW", "PA1"):
+        g = LinearClassifier(method, {"regularization_weight": 0.5}, DatumToFvConverter(conv), device=_device())
+        c = LinearClassifier(method, {"regularization_weight": 0.5}, DatumToFvConverter(conv))
+        g._mode = lambda n: hip.UPDATE_MODES[mode] if n > 1 or mode == "atomic" else hip.UPDATE_EXACT
+        for i in range(0, len(data), 80):
+            g.train(data[i:i + 80])
+            c.train(data[i:i + 80])
+        g.synchronize()
+        scale = float(np.abs(c.W).max()) or 1.0
+        np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+        if c.P is not None:
+            np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3,
+                                       atol=2e-3 * float(c.P.max()))
