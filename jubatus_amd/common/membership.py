@@ -120,7 +120,10 @@ def register_proxy(ls: LockService, type_: str, ip: str, port: int) -> None:
 
 
 def register_supervisor(ls: LockService, ip: str, port: int) -> None:
-    ls.create(JUBAVISOR_BASE_PATH)
+    # jubavisor.cpp:70-72 creates the base paths before registering
+    for p in (JUBATUS_BASE_PATH, JUBAVISOR_BASE_PATH, ACTOR_BASE_PATH):
+        if not ls.exists(p):
+            ls.create(p)
     if not ls.create(build_existence_path(JUBAVISOR_BASE_PATH, ip, port), "", True):
         raise RuntimeError("Failed to register_supervisor")
 

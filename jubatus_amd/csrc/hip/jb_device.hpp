@@ -105,4 +105,59 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Register-only cross-lane moves (no LDS round trip): DPP inside a 16-lane
+// row, v_permlane16/32_swap (gfx950) across rows. A ds_bpermute costs an LDS
+// latency (~50+ cycles) per step of a dependent chain; these are VALU ops.
+enum : int {
+  kDppXor1 = 0xB1,        // quad_perm [1,0,3,2]
+  kDppXor2 = 0x4E,        // quad_perm [2,3,0,1]
+  kDppRowRor8 = 0x128,    // lane i <- lane (i+8) mod 16 within the row
+  kDppHalfMirror = 0x141, // lane i <- lane 7-i within each half row
+  kDppMirror = 0x140,     // lane i <- lane 15-i within the row
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+
+// value of lane ^ 16 / lane ^ 32
+__device__ __forceinline__ float partner16_f(float v, int lane) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(((lane >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ int partner16_i(int v, int lane) {
+  auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)(((lane >> 4) & 1) ? r[0] : r[1]);
+}
+__device__ __forceinline__ float partner32_f(float v, int lane) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(lane >= 32 ? r[0] : r[1]);
+}
+__device__ __forceinline__ int partner32_i(int v, int lane) {
+  auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  return (int)(lane >= 32 ? r[0] : r[1]);
+}
+
+// sum over the 16 lanes of each row (every lane gets its row's sum)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<kDppXor1>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppHalfMirror>(v);
+  v += dpp_f<kDppMirror>(v);
+  return v;
+}
+
+// full-wave sum, every lane gets it, no LDS
+__device__ __forceinline__ float wave_sum_fast(float v, int lane) {
+  v = row16_sum(v);
+  v += partner16_f(v, lane);
+  v += partner32_f(v, lane);
+  return v;
+}
+
 }  // namespace jb

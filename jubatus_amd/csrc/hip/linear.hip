@@ -343,78 +343,34 @@ __device__ __forceinline__ void put_features(int32_t* sI, float* sX, int32_t idx
   }
 }
 
-// Per-wave write-combining cache of a stream's own increments (atomic mode).
-// Hot rows (features nearly every sample carries: numeric keys, frequent
-// tokens) would otherwise take one float atomic per sample from every
-// stream and serialise at their L2 line; instead a stream accumulates its
-// increments in LDS (direct-mapped, CE rows) and flushes a row when another
-// row claims its slot or when the stream ends. Gathered rows are folded with
-// the cached increments, so the stream still sees all of its own updates.
-template <int LC>
-struct DCache {
-  static constexpr int CE = 1024 / LC;  // entries (power of two)
-};
-
-template <int LC>
-__device__ __forceinline__ void cache_init(int32_t* cT, float* cW, float* cP, int lane) {
-  constexpr int CE = DCache<LC>::CE;
-  for (int i = lane; i < CE; i += 64) cT[i] = -1;
-  for (int i = lane; i < CE * LC; i += 64) {
-    cW[i] = 0.f;
-    cP[i] = 0.f;
-  }
-}
-
-// flush every cached row (all lanes cooperate: lane i -> (entry, label))
-template <int LC>
-__device__ __forceinline__ void cache_flush_all(int32_t* cT, float* cW, float* cP, float* W,
-                                                float* P, bool use_s, int lane) {
-  constexpr int CE = DCache<LC>::CE;
-  for (int i = lane; i < CE * LC; i += 64) {
-    const int32_t tag = cT[i / LC];
-    if (tag >= 0) {
-      const int64_t a = (int64_t)tag * LC + (i % LC);
-      const float dw = cW[i];
-      if (dw != 0.f) atomicAdd(W + a, dw);
-      if (use_s) {
-        const float dp = cP[i];
-        if (dp != 0.f) atomicAdd(P + a, dp);
-      }
-    }
-    cW[i] = 0.f;
-    cP[i] = 0.f;
-  }
-  __builtin_amdgcn_wave_barrier();
-  for (int i = lane; i < CE; i += 64) cT[i] = -1;
-  __builtin_amdgcn_wave_barrier();
-}
-
-// staged rows of a sample += the stream's cached increments of those rows
-template <int LC>
-__device__ __forceinline__ void cache_fold(float* sW, float* sP, const int32_t* sI, int n, int g,
-                                           int l0, const int32_t* cT, const float* cW,
-                                           const float* cP, bool use_s) {
-  using Q = Pipe<LC>;
-  constexpr int CE = DCache<LC>::CE;
-#pragma unroll
-  for (int u = 0; u < Q::U; ++u) {
-    const int j = u * Q::G + g;
-    if (j < n) {
-      const int32_t idx = sI[j];
-      if (idx >= 0) {
-        const int slot = idx & (CE - 1);
-        if (cT[slot] == idx) {
-          sW[j * LC + l0] += cW[slot * LC + l0];
-          if (use_s) sP[j * LC + l0] += cP[slot * LC + l0];
-        }
-      }
-    }
-  }
-}
-
 // make the compiler wait for these registers here (before later atomics
 // enter the in-order vmcnt queue) instead of at their first use
 #define JB_CONSUME(r) asm volatile("" ::"v"(r))
+
+// sum of the G lane groups of one label (lanes l0, l0+LC, ...): every lane
+// ends with the full score of its label
+template <int LC>
+__device__ __forceinline__ float group_sum(float v, int lane) {
+  if (LC <= 8) v += dpp_f<kDppRowRor8>(v);
+  if (LC <= 16) v += partner16_f(v, lane);
+  if (LC <= 32) v += partner32_f(v, lane);
+  return v;
+}
+
+// arg-max over the LC lanes of a label group (ties -> lowest label); every
+// group holds the same scores, so every lane ends with the answer
+template <int LC>
+__device__ __forceinline__ void group_argmax(float& best, int& bl, int lane) {
+  auto step = [&](float ob, int ol) {
+    if (ol >= 0 && (bl < 0 || ob > best || (ob == best && ol < bl))) { best = ob; bl = ol; }
+  };
+  step(dpp_f<kDppXor1>(best), dpp_i<kDppXor1>(bl));
+  step(dpp_f<kDppXor2>(best), dpp_i<kDppXor2>(bl));
+  step(dpp_f<kDppHalfMirror>(best), dpp_i<kDppHalfMirror>(bl));
+  if (LC >= 16) step(dpp_f<kDppMirror>(best), dpp_i<kDppMirror>(bl));
+  if (LC >= 32) step(partner16_f(best, lane), partner16_i(bl, lane));
+  if (LC >= 64) step(partner32_f(best, lane), partner32_i(bl, lane));
+}
 
 template <int LC, int MODE>
 __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
@@ -428,12 +384,6 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
   __shared__ float sP[4][2][F * LC];
   __shared__ int32_t sI[4][2][F];
   __shared__ float sX[4][2][F];
-  constexpr bool CACHE = MODE == kAtomic;
-  constexpr int CE = CACHE ? DCache<LC>::CE : 1;
-  __shared__ int32_t cT[4][CE];
-  __shared__ int32_t cClaim[4][CE];
-  __shared__ float cW[4][CE * (CACHE ? LC : 1)];
-  __shared__ float cP[4][CE * (CACHE ? LC : 1)];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -442,7 +392,6 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
   const int l0 = lane % LC;
   bool act[1] = {active[l0] != 0};
   const bool use_s = method >= CW;
-  if (CACHE) cache_init<LC>(cT[wv], cW[wv], cP[wv], lane);
 
   const int64_t s_beg = stream_ptr[wid], s_end = stream_ptr[wid + 1];
   if (s_beg >= s_end) return;
@@ -509,16 +458,12 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       idx2 = lane < n2 ? fidx[b2 + lane] : -1;
       x2 = lane < n2 ? fval[b2 + lane] : 0.f;
     }
-    // 3. sample s (from LDS while the loads above are in flight)
+    // 3. sample s (LDS + registers only while the loads above are in flight)
     bool upd = false;
     int lstar = -1;
     float dwy = 0.f, dwl = 0.f, dpy = 0.f, dpl = 0.f, py = 1.f, pl = 1.f, wy = 0.f, wl = 0.f;
     const bool mine = lane < n_s && idx_s >= 0;
     if (general_s) {
-      if (CACHE) {  // the direct path reads the table: hand it our pending increments first
-        cache_flush_all<LC>(cT[wv], cW[wv], cP[wv], W, P, use_s, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
       const int i = (int)(s - wb);
       const int64_t b0 = readlane64(rp, i);
       general_sample<LC, MODE>(fidx, fval, b0, (int)(readlane64(rp, i + 1) - b0), y_s, W, P, act,
@@ -528,14 +473,18 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       const float* cp = sP[wv][c];
       const float* cx = sX[wv][c];
       float acc = 0.f;
-      for (int j = g; j < n_s; j += Q::G) acc += cx[j] * cw[j * LC + l0];
 #pragma unroll
-      for (int off = LC; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
-      const float sy = __shfl(acc, y_s, 64);
+      for (int u = 0; u < Q::U; ++u) {
+        const int j = u * Q::G + g;
+        if (j < n_s) acc += cx[j] * cw[j * LC + l0];
+      }
+      acc = group_sum<LC>(acc, lane);
+      const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), y_s));
       float best = (act[0] && l0 != y_s) ? acc : -INFINITY;
       int bl = (act[0] && l0 != y_s) ? l0 : -1;
-      argmax_wrong<LC>(best, bl);
-      lstar = bl;
+      group_argmax<LC>(best, bl, lane);
+      lstar = __builtin_amdgcn_readfirstlane(bl);
+      best = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(best)));
       const float margin = sy - (lstar >= 0 ? best : 0.f);
       float a = 1.f, b = 1.f, x2s = 0.f;
       if (mine) {
@@ -549,8 +498,8 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
         wy = cw[lane * LC + y_s];
         wl = lstar >= 0 ? cw[lane * LC + lstar] : 0.f;
       }
-      const float var = wave_sum(use_s ? x2s * (a + b) : 0.f);
-      const float nrm = wave_sum(x2s);
+      const float var = use_s ? wave_sum_fast(x2s * (a + b), lane) : 0.f;
+      const float nrm = wave_sum_fast(x2s, lane);
       float tau = 0.f, beta = 0.f;
       upd = step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta);
       if (upd && mine) {
@@ -562,24 +511,33 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
         }
       }
     }
-    // 4. stage s+1 and forward s's own increments into it
+    // 4. stage s+1 and forward s's own increments into it: lane k (feature k
+    //    of s+1) scans s's features through readlane (registers only)
     if (early) {
       gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
-      if (CACHE)
-        cache_fold<LC>(sW[wv][c1], sP[wv][c1], sI[wv][c1], n1, g, l0, cT[wv], cW[wv], cP[wv], use_s);
-      __builtin_amdgcn_wave_barrier();
-      if (upd && mine) {
-        const int32_t* ni = sI[wv][c1];
-        float* nw = sW[wv][c1];
-        float* np = sP[wv][c1];
-        for (int k = 0; k < n1; ++k) {
-          if (ni[k] == idx_s) {
-            atomicAdd(nw + k * LC + y_s, dwy);
-            if (lstar >= 0) atomicAdd(nw + k * LC + lstar, dwl);
-            if (use_s) {
-              atomicAdd(np + k * LC + y_s, dpy);
-              if (lstar >= 0) atomicAdd(np + k * LC + lstar, dpl);
-            }
+      if (upd) {
+        float fwy = 0.f, fwl = 0.f, fpy = 0.f, fpl = 0.f;
+        const bool kv = lane < n1 && idx1 >= 0;
+        for (int j = 0; j < n_s; ++j) {
+          const int32_t ij = __builtin_amdgcn_readlane(idx_s, j);
+          const bool hit = kv && ij == idx1;
+          if (__builtin_amdgcn_ballot_w64(hit)) {
+            const float ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dwy), j));
+            const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dwl), j));
+            const float by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dpy), j));
+            const float bq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dpl), j));
+            if (hit) { fwy += ay; fwl += al; fpy += by; fpl += bq; }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (kv && (fwy != 0.f || fwl != 0.f || fpy != 0.f || fpl != 0.f)) {
+          float* nw = sW[wv][c1] + lane * LC;
+          float* np = sP[wv][c1] + lane * LC;
+          nw[y_s] += fwy;
+          if (lstar >= 0) nw[lstar] += fwl;
+          if (use_s) {
+            np[y_s] += fpy;
+            if (lstar >= 0) np[lstar] += fpl;
           }
         }
       }
@@ -587,53 +545,8 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
     }
     JB_CONSUME(idx2);
     JB_CONSUME(x2);
-    // 5. apply s: into the stream's cache (atomic mode) or the table
-    if (CACHE) {
-      const int slot = idx_s & (CE - 1);
-      if (upd && mine) cClaim[wv][slot] = lane;
-      __builtin_amdgcn_wave_barrier();
-      if (upd && mine && cClaim[wv][slot] == lane) {
-        const int32_t old = cT[wv][slot];
-        if (old != idx_s) {  // evict the previous row of this slot
-          if (old >= 0) {
-            const int64_t orow = (int64_t)old * LC;
-            for (int l = 0; l < LC; ++l) {
-              const float dw = cW[wv][slot * LC + l];
-              if (dw != 0.f) atomicAdd(W + orow + l, dw);
-              cW[wv][slot * LC + l] = 0.f;
-              if (use_s) {
-                const float dp = cP[wv][slot * LC + l];
-                if (dp != 0.f) atomicAdd(P + orow + l, dp);
-                cP[wv][slot * LC + l] = 0.f;
-              }
-            }
-          }
-          cT[wv][slot] = idx_s;
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (upd && mine) {
-        if (cT[wv][slot] == idx_s) {
-          float* ew = cW[wv] + slot * LC;
-          float* ep = cP[wv] + slot * LC;
-          atomicAdd(ew + y_s, dwy);
-          if (lstar >= 0) atomicAdd(ew + lstar, dwl);
-          if (use_s) {
-            atomicAdd(ep + y_s, dpy);
-            if (lstar >= 0) atomicAdd(ep + lstar, dpl);
-          }
-        } else {  // lost the slot to another row of this sample: straight to the table
-          const int64_t row = (int64_t)idx_s * LC;
-          atomicAdd(W + row + y_s, dwy);
-          if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
-          if (use_s) {
-            atomicAdd(P + row + y_s, dpy);
-            if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-    } else if (upd && mine) {
+    // 5. apply s to the table
+    if (upd && mine) {
       const int64_t row = (int64_t)idx_s * LC;
       if (MODE == kAtomic) {
         atomicAdd(W + row + y_s, dwy);
@@ -657,8 +570,6 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       if (MODE != kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       vmask = gather_issue<LC>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
       gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
-      if (CACHE)
-        cache_fold<LC>(sW[wv][c1], sP[wv][c1], sI[wv][c1], n1, g, l0, cT[wv], cW[wv], cP[wv], use_s);
     }
     // slot c is free again: it receives the features of s+2
     put_features<LC>(sI[wv][c], sX[wv][c], idx2, x2, n2, lane);
@@ -667,7 +578,6 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
     idx_s = idx1; x_s = x1; n_s = n1; y_s = y1;
     idx1 = idx2; x1 = x2; n1 = n2; y1 = y2;
   }
-  if (CACHE) cache_flush_all<LC>(cT[wv], cW[wv], cP[wv], W, P, use_s, lane);
 }
 
 template <int LC>
