@@ -5,6 +5,8 @@
 * ``jubatus_amd/libjubatus_hip.so`` - every HIP kernel, compiled for gfx950
   only (``hipcc --offload-arch=gfx950``), exported through a C ABI and
   loaded with ctypes (jubatus_amd/ops/hip.py).
+* ``jubatus_amd/plugins/libjubatus_sample_plugins.so`` - sample fv_converter
+  plug-ins (C ABI csrc/plugins/jb_plugin.h), the in-tree plug-in directory.
 
 Both are built in-tree so they travel with the repository snapshot to the
 GPU box. Incremental: a target is rebuilt only if a source is newer.
@@ -94,9 +96,24 @@ def build_hip(force: bool = False, nproc: int = 8) -> str:
     return HIP_SO
 
 
-def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, str]:
+PLUGIN_DIR = os.path.join(PKG, "plugins")
+PLUGIN_SO = os.path.join(PLUGIN_DIR, "libjubatus_sample_plugins.so")
+
+
+def build_plugins(force: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "plugins", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "plugins", "*.h")))
+    if not force and not _newer(PLUGIN_SO, srcs + hdrs):
+        return PLUGIN_SO
+    os.makedirs(PLUGIN_DIR, exist_ok=True)
+    _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+          f"-I{os.path.join(CSRC, 'plugins')}", "-o", PLUGIN_SO, *srcs])
+    return PLUGIN_SO
+
+
+def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, str, str]:
     nproc = nproc or min(8, os.cpu_count() or 4)
-    return build_native(force, nproc), build_hip(force, nproc)
+    return build_native(force, nproc), build_hip(force, nproc), build_plugins(force)
 
 
 def main() -> None:

@@ -1,0 +1,80 @@
+"""fv_converter dynamic plug-ins through the C ABI (reference
+server/fv_converter/{dynamic_loader,so_factory}_test.cpp strategy: real
+sample plug-ins built by the same build, every extension point, path search
+and error paths)."""
+import os
+
+import pytest
+
+from jubatus_amd.fv_converter.converter import DatumToFvConverter
+from jubatus_amd.fv_converter.datum import Datum
+from jubatus_amd.fv_converter.plugin import PLUGIN_DIR, PluginError, PluginLoader, resolve_path
+
+LIB = "libjubatus_sample_plugins.so"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    from jubatus_amd import build_ext
+    build_ext.build_plugins()
+
+
+def dyn(fn, **kw):
+    return {"method": "dynamic", "path": LIB, "function": fn, **kw}
+
+
+def test_all_extension_points():
+    conf = {
+        "string_filter_types": {"up": dyn("create_upper_filter")},
+        "string_filter_rules": [{"key": "t", "type": "up", "suffix": "-up"}],
+        "num_filter_types": {"aff": dyn("create_affine_filter", scale="2", shift="1")},
+        "num_filter_rules": [{"key": "x", "type": "aff", "suffix": "-aff"}],
+        "string_types": {"comma": dyn("create_splitter", delimiter=",", min_length="2")},
+        "string_rules": [{"key": "t*", "type": "comma", "sample_weight": "tf", "global_weight": "bin"}],
+        "num_types": {"bk": dyn("create_bucket_feature", width="10")},
+        "num_rules": [{"key": "x*", "type": "bk"}],
+        "binary_types": {"hist": dyn("create_byte_histogram")},
+        "binary_rules": [{"key": "*", "type": "hist"}],
+        "combination_types": {"mx": dyn("create_max_combination")},
+        "combination_rules": [{"key_left": "x@raw", "key_right": "x-aff@raw", "type": "mx"}],
+    }
+    conv = DatumToFvConverter(conf)
+    d = Datum({"t": "ab,c,ab,de", "x": 25.0})
+    d.binary_values.append(("bin", b"\x01\x01\x02"))
+    fv = dict(conv.convert(d))
+    assert fv["t$ab@comma#tf/bin"] == 2.0 and fv["t$de@comma#tf/bin"] == 1.0
+    assert "t$c@comma#tf/bin" not in fv                         # min_length 2
+    assert fv["t-up$AB@comma#tf/bin"] == 2.0                     # string filter + splitter
+    assert fv["x@bucket2"] == 1.0 and fv["x@raw"] == 25.0
+    assert fv["x-aff@bucket5"] == 1.0 and fv["x-aff@raw"] == 51.0  # 25 * 2 + 1
+    assert fv["bin$b1@hist"] == 2.0 and fv["bin$b2@hist"] == 1.0
+    assert fv["x@raw&x-aff@raw/mx"] == 51.0
+
+
+def test_path_search(monkeypatch, tmp_path):
+    assert resolve_path(LIB) == os.path.join(PLUGIN_DIR, LIB)
+    assert resolve_path(os.path.join(PLUGIN_DIR, LIB)) == os.path.join(PLUGIN_DIR, LIB)
+    os.symlink(os.path.join(PLUGIN_DIR, LIB), tmp_path / "mine.so")
+    monkeypatch.setenv("JUBATUS_PLUGIN_PATH", str(tmp_path))
+    assert resolve_path("mine.so") == str(tmp_path / "mine.so")
+    with pytest.raises(PluginError):
+        resolve_path("nope.so")
+
+
+def test_errors():
+    ld = PluginLoader()
+    with pytest.raises(PluginError):
+        ld.create("string_feature", {"path": LIB})                       # no function
+    with pytest.raises(PluginError):
+        ld.create("string_feature", {"path": LIB, "function": "missing"})
+    with pytest.raises(PluginError):
+        ld.create("num_filter", {"path": LIB, "function": "create_splitter"})  # wrong kind
+    with pytest.raises(PluginError):
+        ld.create("string_feature", {"path": "/nonexistent/x.so", "function": "f"})
+
+
+def test_gpu_path_falls_back_for_plugins():
+    from jubatus_amd.fv_converter.gpu_path import gpu_eligible
+    conv = DatumToFvConverter({"string_types": {"c": dyn("create_splitter")},
+                               "string_rules": [{"key": "*", "type": "c"}]})
+    assert not gpu_eligible(conv)
