@@ -54,6 +54,32 @@ def M(name, args, ret, routing, lock, agg="pass", cht_n=2, doc=""):
     return Method(name, tuple(args), ret, routing, lock, agg, cht_n, doc)
 
 
+# message types per engine (the reference IDLs' ``message`` blocks; field
+# order is the wire order). ``datum`` is built in.
+MESSAGES: dict[str, tuple[tuple[str, tuple[str, ...]], ...]] = {
+    "classifier": (("estimate_result", ("label:string", "score:double")),
+                   ("labeled_datum", ("label:string", "data:datum"))),
+    "regression": (("scored_datum", ("score:float", "data:datum")),),
+    "recommender": (("id_with_score", ("id:string", "score:float")),),
+    "nearest_neighbor": (("id_with_score", ("id:string", "score:float")),),
+    "anomaly": (("id_with_score", ("id:string", "score:float")),),
+    "clustering": (("weighted_datum", ("weight:double", "point:datum")),),
+    "graph": (("node", ("property:map<string,string>", "in_edges:list<ulong>", "out_edges:list<ulong>")),
+              ("query", ("from_id:string", "to_id:string")),
+              ("preset_query", ("edge_query:list<query>", "node_query:list<query>")),
+              ("edge", ("property:map<string,string>", "source:string", "target:string")),
+              ("shortest_path_query", ("source:string", "target:string", "max_hop:uint",
+                                       "query:preset_query"))),
+    "bandit": (("arm_info", ("trial_count:int", "weight:double")),),
+    "burst": (("keyword_with_params", ("keyword:string", "scaling_param:double", "gamma:double")),
+              ("batch", ("all_data_count:int", "relevant_data_count:int", "burst_weight:double")),
+              ("window", ("start_pos:double", "batches:list<batch>")),
+              ("document", ("pos:double", "text:string"))),
+    "stat": (),
+    "weight": (("feature", ("key:string", "value:float")),),
+}
+
+
 # methods every engine has (framework + generated impl; proxy.cpp:43-66)
 COMMON = (
     M("get_config", "", "string", "random", "analysis"),
@@ -98,8 +124,8 @@ SERVICES: dict[str, tuple[Method, ...]] = {
         M("set_row", "id:string, d:datum", "bool", "cht", "update", "pass", cht_n=1),
         M("neighbor_row_from_id", "id:string, size:uint", "list<id_with_score>", "random", "nolock"),
         M("neighbor_row_from_datum", "query:datum, size:uint", "list<id_with_score>", "random", "nolock"),
-        M("similar_row_from_id", "id:string, ret_num:int", "list<id_with_score>", "random", "nolock"),
-        M("similar_row_from_datum", "query:datum, ret_num:int", "list<id_with_score>", "random", "nolock"),
+        M("similar_row_from_id", "id:string, ret_num:uint", "list<id_with_score>", "random", "nolock"),
+        M("similar_row_from_datum", "query:datum, ret_num:uint", "list<id_with_score>", "random", "nolock"),
         M("get_all_rows", "", "list<string>", "random", "nolock"),
     ),
     # anomaly.idl:26-49
@@ -141,9 +167,9 @@ SERVICES: dict[str, tuple[Method, ...]] = {
         M("clear", "", "bool", "broadcast", "update", "all_and"),
         M("get_node", "node_id:string", "node", "cht", "analysis"),
         M("get_edge", "node_id:string, edge_id:ulong", "edge", "cht", "analysis"),
-        M("create_node_here", "node_id:string", "bool", "internal", "update", "all_and"),
-        M("remove_global_node", "node_id:string", "bool", "internal", "update", "all_and"),
-        M("create_edge_here", "edge_id:ulong, e:edge", "bool", "internal", "update", "all_and"),
+        M("create_node_here", "node_id:string", "bool", "internal", "update"),
+        M("remove_global_node", "node_id:string", "bool", "internal", "update"),
+        M("create_edge_here", "edge_id:ulong, e:edge", "bool", "internal", "update"),
     ),
     # bandit.idl:17-91
     "bandit": (
