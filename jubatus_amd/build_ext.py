@@ -5,8 +5,9 @@
 * ``jubatus_amd/libjubatus_hip.so`` - every HIP kernel, compiled for gfx950
   only (``hipcc --offload-arch=gfx950``), exported through a C ABI and
   loaded with ctypes (jubatus_amd/ops/hip.py).
-* ``jubatus_amd/plugins/libjubatus_sample_plugins.so`` - sample fv_converter
-  plug-ins (C ABI csrc/plugins/jb_plugin.h), the in-tree plug-in directory.
+* ``jubatus_amd/plugins/libjubatus_{sample_plugins,ux_splitter}.so`` -
+  fv_converter plug-ins (C ABI csrc/plugins/jb_plugin.h) in the in-tree
+  plug-in directory.
 
 Both are built in-tree so they travel with the repository snapshot to the
 GPU box. Incremental: a target is rebuilt only if a source is newer.
@@ -98,17 +99,21 @@ def build_hip(force: bool = False, nproc: int = 8) -> str:
 
 PLUGIN_DIR = os.path.join(PKG, "plugins")
 PLUGIN_SO = os.path.join(PLUGIN_DIR, "libjubatus_sample_plugins.so")
+# one shared object per plug-in source
+PLUGINS = {"sample_plugins.cpp": "libjubatus_sample_plugins.so",
+           "ux_splitter.cpp": "libjubatus_ux_splitter.so"}
 
 
 def build_plugins(force: bool = False) -> str:
-    srcs = sorted(glob.glob(os.path.join(CSRC, "plugins", "*.cpp")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "plugins", "*.h")))
-    if not force and not _newer(PLUGIN_SO, srcs + hdrs):
-        return PLUGIN_SO
     os.makedirs(PLUGIN_DIR, exist_ok=True)
-    _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
-          f"-I{os.path.join(CSRC, 'plugins')}", "-o", PLUGIN_SO, *srcs])
-    return PLUGIN_SO
+    for src, lib in PLUGINS.items():
+        s = os.path.join(CSRC, "plugins", src)
+        target = os.path.join(PLUGIN_DIR, lib)
+        if force or _newer(target, [s] + hdrs):
+            _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+                  f"-I{os.path.join(CSRC, 'plugins')}", "-o", target, s])
+    return PLUGIN_DIR
 
 
 def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, str, str]:

@@ -78,3 +78,18 @@ def test_gpu_path_falls_back_for_plugins():
     conv = DatumToFvConverter({"string_types": {"c": dyn("create_splitter")},
                                "string_rules": [{"key": "*", "type": "c"}]})
     assert not gpu_eligible(conv)
+
+
+def test_ux_splitter_longest_prefix(tmp_path):
+    d = tmp_path / "dict.txt"
+    d.write_text("tokyo\ntokyo tower\nto\nkyoto\n\n")
+    conv = DatumToFvConverter({
+        "string_types": {"ux": {"method": "dynamic", "path": "libjubatus_ux_splitter.so",
+                                "function": "create", "dict_path": str(d)}},
+        "string_rules": [{"key": "*", "type": "ux", "sample_weight": "tf", "global_weight": "bin"}]})
+    fv = dict(conv.convert(Datum({"t": "tokyo towerxkyoto to tokyo"})))
+    # longest match wins ("tokyo tower" over "tokyo"); unmatched bytes are skipped
+    assert fv == {"t$tokyo tower@ux#tf/bin": 1.0, "t$kyoto@ux#tf/bin": 1.0,
+                  "t$to@ux#tf/bin": 1.0, "t$tokyo@ux#tf/bin": 1.0}
+    with pytest.raises(PluginError):
+        PluginLoader().create("string_feature", {"path": "libjubatus_ux_splitter.so", "function": "create"})
