@@ -31,6 +31,7 @@ from typing import Any, Callable, Sequence
 import msgpack
 
 from .._native import native
+from ..utils import fault, trace
 
 NO_METHOD_ERROR = 1
 ARGUMENT_ERROR = 2
@@ -154,7 +155,10 @@ class RpcServer:
         if m is None:
             err = NO_METHOD_ERROR
         else:
+            t0 = time.perf_counter_ns()
             try:
+                if fault.on_rpc(method) == "drop":
+                    return None
                 if m.raw:
                     result = m.fn(params)
                 else:
@@ -168,6 +172,7 @@ class RpcServer:
                 err = ARGUMENT_ERROR
             except Exception as e:  # application error -> message string
                 err = str(e) or type(e).__name__
+            trace.record("rpc." + method, time.perf_counter_ns() - t0)
         if notify:
             return None
         try:

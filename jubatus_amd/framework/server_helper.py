@@ -24,7 +24,7 @@ from typing import Any, Callable
 from .. import __version__
 from ..common import mprpc
 from ..idl import specs
-from ..utils import logger, signals, system
+from ..utils import logger, signals, system, trace
 from .mixer import create_mixer
 from .server_util import ArgvError, ServerArgv, get_conf, get_server_identifier
 
@@ -173,6 +173,7 @@ class ServerHelper:
                 "mixer": a.mixer,
             })
             s.mixer.get_status(data)
+        data.update(trace.stats())
         return {get_server_identifier(a): data}
 
     # ----------------------------------------------------------- lifecycle

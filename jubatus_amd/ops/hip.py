@@ -8,10 +8,12 @@ order naturally with torch ops and RCCL collectives.
 from __future__ import annotations
 
 import ctypes
+import time
 
 import torch
 
 from .._native import hip_lib
+from ..utils import trace
 
 _c_void_p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -106,9 +108,16 @@ def _fn(name: str):
     f = _fns.get(name)
     if f is None:
         lib = hip_lib()
-        f = getattr(lib, name)
-        f.argtypes = _SIGS[name]
-        f.restype = ctypes.c_int
+        raw = getattr(lib, name)
+        raw.argtypes = _SIGS[name]
+        raw.restype = ctypes.c_int
+        tag = "hip." + name[3:]
+
+        def f(*args, _raw=raw, _tag=tag):
+            t0 = time.perf_counter_ns()
+            rc = _raw(*args)
+            trace.record(_tag, time.perf_counter_ns() - t0)
+            return rc
         _fns[name] = f
     return f
 

@@ -13,7 +13,11 @@ rank set, so membership changes become *group epochs*:
 * every member polls the epoch each mixer tick; when a new epoch lists it,
   it tears down the old group and joins the new one
   (``init_process_group(tcp://addr:port, rank=index)``);
-* a member missing from the epoch waits (it is obsolete until it joins).
+* a member missing from the epoch waits (it is obsolete until it joins);
+* an epoch that lists a member whose node is gone is not joined (the leader
+  publishes its successor once the dead member's session expires), and an
+  epoch whose group failed is re-joined only after a back-off, so a
+  survivor does not burn rendezvous timeouts waiting for a dead rank.
 
 One group per server process (= per GPU). The group carries the mixer's
 trigger agreement (a 2-int all-reduce) and the MIX collectives.
@@ -52,6 +56,8 @@ class ProcessGroupManager:
         self.members: list[str] = []
         self.rank = -1
         self.world = 0
+        self.failed: dict[int, float] = {}   # epoch -> time its group failed
+        self.retry_after = timeout
         self.path = mb.build_actor_path(type_, name) + "/mix_epoch"
         coord.create(self.path, "")
 
@@ -89,6 +95,11 @@ class ProcessGroupManager:
             return False
         if self.ident not in cur["members"]:
             return False
+        t = self.failed.get(cur["epoch"])
+        if t is not None and time.time() - t < self.retry_after:
+            return False
+        if any(m not in self._live() for m in cur["members"]):
+            return False  # a member is gone: wait for the next epoch
         self._destroy()
         rank = cur["members"].index(self.ident)
         world = len(cur["members"])
@@ -124,6 +135,10 @@ class ProcessGroupManager:
         self.rank, self.world = -1, 0
 
     def close(self) -> None:
+        """tear down after a failed collective; the epoch is not re-joined
+        before ``retry_after`` seconds unless a new one is published"""
+        if self.epoch >= 0:
+            self.failed[self.epoch] = time.time()
         self._destroy()
         self.epoch = -1
 

@@ -29,7 +29,7 @@ import time
 
 from ..common import membership as mb
 from ..framework.mixer import Mixer
-from ..utils import logger
+from ..utils import fault, logger, trace
 from .group import ProcessGroupManager
 from .mixable import broadcast_model, linear_mix
 
@@ -170,7 +170,9 @@ class CollectiveMixer(Mixer):
                     self._mixed({"bytes": 0, "seconds": 0.0})
             return
         if formed:
-            self._hand_over()
+            fault.on_mix("handover")
+            with trace.span("mix.handover"):
+                self._hand_over()
         with self._lock:
             want = 1 if self._want() else 0
             force = 1 if self._force else 0
@@ -210,7 +212,9 @@ class CollectiveMixer(Mixer):
         self._register_active()
 
     def mix_once(self) -> dict:
-        return linear_mix(self.driver)
+        fault.on_mix("allreduce")
+        with trace.span("mix.linear"):
+            return linear_mix(self.driver)
 
 
 class LinearMixer(CollectiveMixer):

@@ -22,6 +22,7 @@ import random
 
 from .linear_mixer import CollectiveMixer
 from .mixable import pair_exchange
+from ..utils import fault, trace
 
 
 def skip_strides(n: int) -> list[int]:
@@ -101,5 +102,7 @@ class PushMixer(CollectiveMixer):
         t0 = time.perf_counter()
         g = self.group
         for peer in self.schedule(g.rank, g.world, self.mix_count):
-            pair_exchange(self.driver, peer)
+            fault.on_mix("pair")
+            with trace.span("mix.pair"):
+                pair_exchange(self.driver, peer)
         return {"bytes": 0, "seconds": time.perf_counter() - t0}

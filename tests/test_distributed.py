@@ -42,8 +42,8 @@ def coord():
 LOGDIR = os.environ.get("JUBATUS_TEST_LOGDIR", tempfile.gettempdir())
 
 
-def spawn(engine, zport, name, port, mixer="linear_mixer", extra=()):
-    env = dict(os.environ, PYTHONPATH=ROOT, JUBATUS_FORCE_CPU="1")
+def spawn(engine, zport, name, port, mixer="linear_mixer", extra=(), env_extra=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, JUBATUS_FORCE_CPU="1", **(env_extra or {}))
     cmd = [sys.executable, "-m", "jubatus_amd.cmd.server", engine, "-z", f"127.0.0.1:{zport}",
            "-n", name, "-p", str(port), "-b", "127.0.0.1", "-x", mixer, "-s", "0", "-i", "0",
            "-I", "5", "--cpu", *extra]
@@ -167,4 +167,53 @@ def test_proxy_routing(coord):
                 p.wait(timeout=15)
             except subprocess.TimeoutExpired:
                 p.kill()
+        ls.close()
+
+
+def test_rank_killed_mid_mix_survivor_recovers(coord):
+    """fault injection kills one server when its first MIX reaches the
+    all-reduce; the survivor re-forms the group alone, keeps serving and
+    keeps its model (SURVEY §5.3 elastic recovery)."""
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    name = "faulty"
+    zkconfig.config_tozk(ls, "classifier", name, open(os.path.join(ROOT, "config/classifier/pa.json")).read())
+    ports = [free_port(), free_port()]
+    fast = ("-Z", "2")   # short coordinator session: the dead rank's nodes expire quickly
+    good = spawn("classifier", coord.port, name, ports[0], extra=fast)
+    bad = spawn("classifier", coord.port, name, ports[1], extra=fast,
+                env_extra={"JUBATUS_FAULT": "mix_kill:phase=allreduce,at=1"})
+    try:
+        for p in ports:
+            assert wait_server("127.0.0.1", p, 60)
+        assert wait_actives(ls, "classifier", name, 2)
+        a = Classifier("127.0.0.1", ports[0], name, timeout=90.0)
+        a.train([("pos", Datum({"w": "good"})), ("neg", Datum({"w": "bad"}))] * 3)
+        try:
+            a.do_mix()                  # the faulty rank dies inside this MIX
+        except Exception:
+            pass
+        bad.wait(timeout=60)
+        assert bad.returncode == 17
+        deadline = time.time() + 120
+        ok = False
+        while time.time() < deadline:
+            try:
+                if a.do_mix():          # alone again: the mixer runs and reports success
+                    ok = True
+                    break
+            except Exception:
+                pass
+            time.sleep(0.5)
+        assert ok
+        top = max(a.classify([Datum({"w": "good"})])[0], key=lambda e: e.score)
+        assert top.label == "pos"
+        a.close()
+    finally:
+        for p in (good, bad):
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
         ls.close()
