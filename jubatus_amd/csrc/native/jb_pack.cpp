@@ -7,6 +7,7 @@
 #include "jb_pool.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -14,15 +15,6 @@
 namespace jb {
 
 namespace {
-
-struct ReqScan {
-  std::vector<uint64_t> off;     // datum offset inside the request
-  std::vector<uint32_t> len;     // datum byte length
-  std::vector<int32_t> label;
-  std::vector<int64_t> slots;
-  bool ok = true;
-  bool table_full = false;
-};
 
 // Per-thread label cache: open addressing on FNV-1a of the label bytes,
 // verified by a byte compare (labels are few and repeat on every sample).
@@ -64,79 +56,81 @@ class LabelCache {
   size_t used_ = 0;
 };
 
-void scan_one(const RequestView& r, int kind, int sps, int spn, LabelCache* cache,
-              ReqScan* out) {
+// Number of elements of a request body (its top-level array header).
+bool body_count(const RequestView& r, uint32_t* n) {
+  Cursor c{r.data, r.data + r.len};
+  return c.array(n);
+}
+
+// Scan request k straight into the final output slots [s0, s0 + n): datum
+// offsets / lengths / labels, and row_ptr relative to the request (the
+// request's slot base is added afterwards). Returns the request's slot total
+// or -1 (malformed) / -2 (label table full).
+int64_t scan_into(const RequestView& r, int kind, int sps, int spn, LabelCache* cache,
+                  const PackOut& out, uint64_t byte_base, int64_t s0, uint64_t* hist,
+                  size_t hist_cap) {
   Cursor c{r.data, r.data + r.len};
   uint32_t n;
-  if (!c.array(&n)) { out->ok = false; return; }
-  out->off.reserve(n);
-  out->len.reserve(n);
-  out->slots.reserve(n);
-  if (kind) out->label.reserve(n);
+  if (!c.array(&n)) return -1;
+  int64_t slot = 0;
   for (uint32_t i = 0; i < n; ++i) {
+    const int64_t s = s0 + i;
     if (kind == 1) {
       uint32_t two; const uint8_t* ls; uint32_t ln;
-      if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { out->ok = false; return; }
-      int id = cache->get(ls, ln);
-      if (id < 0) { out->table_full = true; out->ok = false; return; }
-      out->label.push_back(id);
+      if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) return -1;
+      const int id = cache->get(ls, ln);
+      if (id < 0) return -2;
+      if (out.labels) out.labels[s] = id;
+      if ((size_t)id < hist_cap) ++hist[id];
     } else if (kind == 2) {  // scored_datum [score, datum]
       uint32_t two; double score;
-      if (!c.array(&two) || two != 2 || !c.number(&score)) { out->ok = false; return; }
+      if (!c.array(&two) || two != 2 || !c.number(&score)) return -1;
       const float f = (float)score;
       int32_t bits;
       memcpy(&bits, &f, 4);
-      out->label.push_back(bits);
+      if (out.labels) out.labels[s] = bits;
     }
-    uint64_t doff = (uint64_t)(c.p - r.data);
+    const uint64_t doff = (uint64_t)(c.p - r.data);
     DatumShape d;
-    if (!scan_datum(c, &d)) { out->ok = false; return; }
-    out->off.push_back(doff);
-    out->len.push_back((uint32_t)((uint64_t)(c.p - r.data) - doff));
-    out->slots.push_back((int64_t)d.n_str * sps + (int64_t)d.n_num * spn);
+    if (!scan_datum(c, &d)) return -1;
+    out.datum_off[s] = (int64_t)(byte_base + doff);
+    if (out.datum_len) out.datum_len[s] = (int32_t)((uint64_t)(c.p - r.data) - doff);
+    out.row_ptr[s] = slot;
+    slot += (int64_t)d.n_str * sps + (int64_t)d.n_num * spn;
   }
+  return slot;
 }
 
 }  // namespace
 
+// Three passes, one of them over the bytes:
+//   1. serial: each body's top-level array length -> sample base per request
+//      (a few bytes per request);
+//   2. parallel over requests: one scan writes every per-sample output at its
+//      final index (row_ptr relative to the request) and counts labels into a
+//      per-chunk histogram;
+//   3. serial prefix of the per-request slot totals, then a parallel pass adds
+//      each request's slot base to its row_ptr entries.
 PackResult pack_requests(const std::vector<RequestView>& reqs, int kind, int sps, int spn,
                          LabelTable* table, const PackOut& out, int nthreads) {
   PackResult res;
   const size_t R = reqs.size();
-  std::vector<ReqScan> scans(R);
   if (R == 0) {
     if (out.row_ptr) out.row_ptr[0] = 0;
     if (out.stream_ptr) out.stream_ptr[0] = 0;
     return res;
   }
-
-  WorkerPool& pool = global_pool(nthreads);
-  const int64_t nchunks = std::min<int64_t>((int64_t)R, (int64_t)pool.size() * 4);
-  auto chunk = [&](int64_t c, int64_t* b, int64_t* e) {
-    *b = c * (int64_t)R / nchunks;
-    *e = (c + 1) * (int64_t)R / nchunks;
-  };
-  pool.parallel_for(nchunks, [&](int64_t c) {
-    LabelCache cache(table);
-    int64_t b, e;
-    chunk(c, &b, &e);
-    for (int64_t k = b; k < e; ++k) scan_one(reqs[k], kind, sps, spn, &cache, &scans[k]);
-  });
-
-  // serial prefix over requests
-  // staging == nullptr: zero-copy mode, the requests already live in one
-  // pinned arena starting at out.base; offsets are taken relative to it.
+  // ---- pass 1: sample and byte bases
   const bool copy = out.staging != nullptr;
   std::vector<uint64_t> byte_base(R);
-  std::vector<int64_t> sample_base(R), slot_base(R);
-  uint64_t bytes = 0; int64_t samples = 0, slots = 0;
+  std::vector<int64_t> sample_base(R + 1);
+  uint64_t bytes = 0;
+  int64_t samples = 0;
   for (size_t k = 0; k < R; ++k) {
-    if (!scans[k].ok) {
-      res.error = scans[k].table_full ? 3 : 1;
-      res.error_request = (int64_t)k;
-      return res;
-    }
-    sample_base[k] = samples; slot_base[k] = slots;
+    uint32_t n;
+    if (!body_count(reqs[k], &n)) { res.error = 1; res.error_request = (int64_t)k; return res; }
+    sample_base[k] = samples;
+    samples += n;
     if (copy) {
       byte_base[k] = bytes;
       bytes += reqs[k].len;
@@ -146,51 +140,77 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, int kind, int sps
       byte_base[k] = (uint64_t)(reqs[k].data - out.base);
       bytes = std::max<uint64_t>(bytes, byte_base[k] + reqs[k].len);
     }
-    samples += (int64_t)scans[k].off.size();
-    for (int64_t s : scans[k].slots) slots += s;
   }
+  sample_base[R] = samples;
   if ((copy && bytes > out.staging_cap) || samples > out.max_samples) {
     // report the sizes needed so the caller can grow its buffers and retry
-    res.error = 2; res.n_samples = samples; res.n_bytes = bytes; res.n_slots = slots;
+    res.error = 2; res.n_samples = samples; res.n_bytes = bytes;
     return res;
   }
 
+  // ---- pass 2: the scan
+  WorkerPool& pool = global_pool(nthreads);
+  const int64_t nchunks = std::min<int64_t>((int64_t)R, (int64_t)pool.size() * 4);
+  auto chunk = [&](int64_t c, int64_t* b, int64_t* e) {
+    *b = c * (int64_t)R / nchunks;
+    *e = (c + 1) * (int64_t)R / nchunks;
+  };
+  std::vector<int64_t> req_slots(R, 0);
+  std::atomic<int64_t> bad{-1};
+  std::atomic<int> bad_kind{0};
+  constexpr size_t kHist = 4096;  // labels beyond this are counted one by one
   pool.parallel_for(nchunks, [&](int64_t c) {
+    LabelCache cache(table);
+    std::vector<uint64_t> hist(kind == 1 && table ? kHist : 0, 0);
     int64_t b, e;
     chunk(c, &b, &e);
     for (int64_t k = b; k < e; ++k) {
       if (copy) memcpy(out.staging + byte_base[k], reqs[k].data, reqs[k].len);
-      const ReqScan& sc = scans[k];
-      int64_t s0 = sample_base[k], slot = slot_base[k];
-      for (size_t i = 0; i < sc.off.size(); ++i) {
-        out.datum_off[s0 + i] = (int64_t)(byte_base[k] + sc.off[i]);
-        if (out.datum_len) out.datum_len[s0 + i] = (int32_t)sc.len[i];
-        out.row_ptr[s0 + i] = slot;
-        slot += sc.slots[i];
-        if (kind && out.labels) out.labels[s0 + i] = sc.label[i];
+      const int64_t sl = scan_into(reqs[k], kind, sps, spn, &cache, out, byte_base[k],
+                                   sample_base[k], hist.data(), hist.size());
+      if (sl < 0) {
+        int64_t expect = -1;
+        bad.compare_exchange_strong(expect, k);
+        bad_kind.store(sl == -2 ? 3 : 1);
+        return;
       }
+      req_slots[k] = sl;
+      if (kind == 1 && table && hist.empty() == false) {
+        // labels past the histogram range
+        const int64_t s0 = sample_base[k], s1 = sample_base[k + 1];
+        if (out.labels)
+          for (int64_t s = s0; s < s1; ++s)
+            if ((size_t)out.labels[s] >= kHist) table->add_count(out.labels[s], 1);
+      }
+    }
+    for (size_t id = 0; id < hist.size(); ++id)
+      if (hist[id]) table->add_count((int)id, hist[id]);
+  });
+  if (bad.load() >= 0) {
+    res.error = bad_kind.load();
+    res.error_request = bad.load();
+    return res;
+  }
+
+  // ---- pass 3: slot bases
+  std::vector<int64_t> slot_base(R);
+  int64_t slots = 0;
+  for (size_t k = 0; k < R; ++k) {
+    slot_base[k] = slots;
+    slots += req_slots[k];
+  }
+  pool.parallel_for(nchunks, [&](int64_t c) {
+    int64_t b, e;
+    chunk(c, &b, &e);
+    for (int64_t k = b; k < e; ++k) {
+      const int64_t base = slot_base[k];
+      if (base == 0) continue;
+      for (int64_t s = sample_base[k]; s < sample_base[k + 1]; ++s) out.row_ptr[s] += base;
     }
   });
   out.row_ptr[samples] = slots;
-  if (out.stream_ptr) {
-    for (size_t k = 0; k < R; ++k) out.stream_ptr[k] = sample_base[k];
-    out.stream_ptr[R] = samples;
-  }
-  if (kind == 1 && table) {
-    // per-chunk histograms, then one atomic add per (chunk, label)
-    pool.parallel_for(nchunks, [&](int64_t c) {
-      int64_t b, e;
-      chunk(c, &b, &e);
-      std::vector<uint64_t> hist;
-      for (int64_t k = b; k < e; ++k)
-        for (int32_t id : scans[k].label) {
-          if ((size_t)id >= hist.size()) hist.resize((size_t)id + 1, 0);
-          ++hist[id];
-        }
-      for (size_t id = 0; id < hist.size(); ++id)
-        if (hist[id]) table->add_count((int)id, hist[id]);
-    });
-  }
+  if (out.stream_ptr)
+    for (size_t k = 0; k <= R; ++k) out.stream_ptr[k] = sample_base[k];
   res.n_samples = samples; res.n_bytes = bytes; res.n_slots = slots;
   return res;
 }

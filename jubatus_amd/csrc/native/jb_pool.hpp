@@ -1,8 +1,13 @@
 // Persistent worker pool for the host runtime (request scanning, host-side
 // conversion). Threads are created once; parallel_for() hands out task
 // indices through an atomic counter and blocks until every task finished.
+// Idle workers spin briefly (~kSpinIters pause loops, a few hundred us)
+// before sleeping on the condition variable: the train path calls
+// parallel_for every millisecond or so, and a futex wake-up per worker per
+// call would add tens of microseconds to every batch.
 #pragma once
 #include <atomic>
+#include <immintrin.h>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -63,10 +68,12 @@ class WorkerPool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      for (int i = 0; i < kSpinIters && gen_.load(std::memory_order_acquire) == seen; ++i)
+        _mm_pause();
       {
         std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return gen_ != seen; });
-        seen = gen_;
+        cv_.wait(g, [&] { return gen_.load() != seen; });
+        seen = gen_.load();
         if (stop_) return;
       }
       work();
@@ -84,7 +91,8 @@ class WorkerPool {
   int64_t n_ = 0;
   std::atomic<int64_t> next_{0};
   std::atomic<int> pending_{0};
-  uint64_t gen_ = 0;
+  static constexpr int kSpinIters = 20000;
+  std::atomic<uint64_t> gen_{0};
   bool stop_ = false;
 };
 
