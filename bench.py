@@ -12,8 +12,11 @@ One timed step on every rank =
     resolution + pinned staging (host), H2D, GPU msgpack parse + feature
     hashing (fv_hash kernel), GPU AROW update (R lock-free update streams,
     each exact-sequential) - i.e. the complete train path minus the socket;
-  * one MIX: label-set agreement + RCCL all-reduce mean of W and S
-    (hash_max_size x labels x 2 tables, fp32) over xGMI (N > 1).
+  * one MIX: label-set agreement (host gloo group) + RCCL all-reduce mean
+    of W and P (hash_max_size x labels x 2 tables, fp32) over xGMI (N > 1).
+    Default ``--mix-mode overlap``: the all-reduce of step k's snapshot runs
+    on the communicator stream during step k+1 and is folded in as
+    W += mean(snapshot) - snapshot, so no update is lost; ``sync`` blocks.
 Per-GPU work is fixed as N grows (weak scaling). Data: synthetic datums
 (8 string + 8 numeric features, 16 labels), random-init (zero) model.
 
@@ -86,6 +89,13 @@ def main() -> None:
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
                     help="how concurrent request streams update shared rows")
+    ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                    help="cpu: host engine + gloo, for rehearsing the multi-rank path without a GPU "
+                         "(not a benchmark configuration)")
+    ap.add_argument("--mix-mode", choices=("overlap", "sync"), default="overlap",
+                    help="overlap: the RCCL all-reduce of step k runs during step k+1 and its "
+                         "mean is folded in afterwards (updates made meanwhile are kept); "
+                         "sync: blocking MIX at the end of every step")
     args = ap.parse_args()
 
     import torch
@@ -96,10 +106,19 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    if args.device == "gpu":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+        if world > 1:
+            dist.init_process_group("nccl", device_id=device)
+    else:
+        device = None
+        if world > 1:
+            dist.init_process_group("gloo")
+
+    def sync():
+        if device is not None:
+            torch.cuda.synchronize()
 
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.classifier import LinearClassifier
@@ -128,35 +147,53 @@ def main() -> None:
         pools.append((arena, offs, lens))
     samples_per_step = args.requests * args.per_request
 
+    # host-side metadata (label agreement, count deltas) rides on a gloo group
+    # so the MIX never forces a GPU synchronisation
+    meta = dist.new_group(backend="gloo") if world > 1 else None
+    pending = [None]
+
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def finish_mix():
+        if pending[0] is not None:
+            clf.mix_end(pending[0])
+            pending[0] = None
 
     def step(i: int) -> None:
         arena, offs, lens = pools[i % len(pools)]
         n = clf.train_arena(arena, offs, lens)
         assert n == samples_per_step
         if world > 1 and (i + 1) % args.mix_every == 0:
-            clf.mix()
+            if args.mix_mode == "sync":
+                clf.mix()
+            else:
+                finish_mix()
+                pending[0] = clf.mix_begin(meta_group=meta)
 
     for i in range(args.warmup):
         step(i)
-    clf.pipe.check_errors()
-    torch.cuda.synchronize()
+    finish_mix()
+    if device is not None:
+        clf.pipe.check_errors()
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
-    torch.cuda.synchronize()
+    finish_mix()          # the last MIX completes inside the timed region
+    sync()
     barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if device is not None else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    clf.pipe.check_errors()
+    if device is not None:
+        clf.pipe.check_errors()
 
     # accuracy on a held-out synthetic request (sanity: the model learns)
     test = make_requests(random.Random(99), 1, 2048, args.labels, args.str_features,
@@ -204,7 +241,8 @@ def main() -> None:
                 "samples_per_request": args.per_request,
                 "hash_max_size": 1 << args.hash_bits,
                 "labels": args.labels,
-                "mix": "linear (RCCL all-reduce mean) every step" if world > 1 else "standalone",
+                "mix": (f"linear, RCCL all-reduce mean of W and P every {args.mix_every} step(s), "
+                        f"{args.mix_mode}") if world > 1 else "standalone",
                 "concurrent_update": args.update_mode,
             },
             "classify_latency_us_p50": round(p50, 1),

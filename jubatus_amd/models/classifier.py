@@ -41,6 +41,15 @@ def _pack_body(items: Sequence[Any]) -> bytes:
     return msgpack.packb(items, use_bin_type=False)
 
 
+def dist_all_reduce(t, op: str, group):
+    """async all-reduce helper for the MIX metadata (None when not distributed)"""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    o = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
+    return dist.all_reduce(t, op=o, group=group, async_op=True)
+
+
 def _label_cap(n: int) -> int:
     for c in LABEL_CAPS:
         if c >= n:
@@ -407,6 +416,75 @@ class LinearClassifier:
             coll.allreduce_mean_(tables, group)
             self._mix_counts(group)
             return sum(t.numel() * t.element_size() for t in tables)
+
+    # ------------------------------------------------ overlapped MIX
+    def mix_begin(self, group=None, meta_group=None) -> dict:
+        """Start an overlapped MIX: snapshot W / P, launch the cluster SUM
+        all-reduce of the snapshot on the communicator stream and return;
+        training continues meanwhile. ``mix_end`` folds the cluster mean in
+        with W += mean(snapshot) - own snapshot, so updates made during the
+        collective are kept. Label agreement and count deltas ride on
+        ``meta_group`` (a host/gloo group: no GPU synchronisation). If the
+        label layouts disagree the synchronous ``mix`` runs instead (it
+        re-lays the label columns first)."""
+        import torch
+        from ..parallel import collective as coll
+        with self._lock:
+            names = self.labels.names()
+            alive = self.labels.alive()
+            fp = coll.fingerprint([n + ("+" if a else "-") for n, a in zip(names, alive)])
+            cur = np.array([self.labels.count(i) for i in range(len(names))], dtype=np.int64)
+            base = getattr(self, "_count_base", {})
+            b = np.array([base.get(n, 0) for n in names], dtype=np.int64)
+            mg = meta_group if meta_group is not None else group
+            on_dev = self.gpu and coll.is_dist() and coll.backend(mg) == "nccl"
+            mdev = self.device if on_dev else "cpu"
+            # the label-layout check is blocking (a host collective on the
+            # meta group); everything after it is asynchronous
+            if not coll.all_equal(fp, mdev if on_dev else torch.device("cpu"), mg):
+                return {"sync": self.mix(group)}
+            meta_cnt = torch.from_numpy(cur - b).to(mdev)
+            works = [dist_all_reduce(meta_cnt, "sum", mg)]
+            tables = self._tables()
+            snap = getattr(self, "_mix_bufs", None)
+            if snap is None or any(a.shape != t.shape for a, t in zip(snap[0], tables)):
+                snap = ([torch.empty_like(t) for t in tables], [torch.empty_like(t) for t in tables])
+                self._mix_bufs = snap
+            loc, red = snap
+            for l, r, t in zip(loc, red, tables):
+                l.copy_(t)
+                r.copy_(t)
+            twork = coll.allreduce_sum_async(red, group)
+            return {"group": group, "names": names, "cur": cur, "base": b,
+                    "meta": works, "meta_cnt": meta_cnt, "twork": twork,
+                    "nbytes": sum(t.numel() * t.element_size() for t in tables)}
+
+    def mix_end(self, h: dict) -> int:
+        """Finish a ``mix_begin``; returns the bytes all-reduced per rank."""
+        from ..parallel import collective as coll
+        if "sync" in h:
+            return h["sync"]
+        for w in h["meta"]:
+            if w is not None:
+                w.wait()
+        for w in h["twork"]:
+            w.wait()
+        n = coll.world() if coll.is_dist() else 1
+        with self._lock:
+            loc, red = self._mix_bufs
+            for t, r, l in zip(self._tables(), red, loc):
+                if self.gpu:
+                    from ..ops import hip
+                    hip.mix_apply_(t, r, l, 1.0 / n)
+                else:
+                    t.add_(r, alpha=1.0 / n).sub_(l)
+            names, cur, b = h["names"], h["cur"], h["base"]
+            new_base = b + h["meta_cnt"].cpu().numpy()
+            for i, nm in enumerate(names):
+                since = int(self.labels.count(i)) - int(cur[i])
+                self.labels.set_count(i, int(max(0, new_base[i] + since)))
+            self._count_base = {nm: int(max(0, new_base[i])) for i, nm in enumerate(names)}
+            return h["nbytes"]
 
     def _tables(self) -> list:
         """the mixable tensors (torch views of the host arrays on the CPU backend)"""

@@ -85,7 +85,8 @@ class RequestArena:
 
     def __init__(self, capacity: int):
         import torch
-        self.buf = torch.empty(max(16, capacity), dtype=torch.uint8, pin_memory=True)
+        self.buf = torch.empty(max(16, capacity), dtype=torch.uint8,
+                               pin_memory=torch.cuda.is_available())
         self.np = self.buf.numpy()
         self.used = 0
         self.offs: list[int] = []

@@ -40,6 +40,7 @@ _SIGS = {
                         _i32, _i32, _c_void_p, _c_void_p],
     "jb_sparse_scan": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
+    "jb_mix_apply": [_c_void_p, _c_void_p, _c_void_p, _i64, _f32, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -197,6 +198,16 @@ def linear_classify(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tenso
     rc = _fn("jb_linear_classify")(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), LC, _p(out),
                                    _stream())
     _check(rc, "jb_linear_classify")
+
+
+def mix_apply_(w: torch.Tensor, red: torch.Tensor, loc: torch.Tensor, inv_n: float) -> None:
+    """w += red * inv_n - loc (overlapped MIX finish)"""
+    for name, t in (("w", w), ("red", red), ("loc", loc)):
+        _dev(t, torch.float32, name)
+    if not (w.numel() == red.numel() == loc.numel()):
+        raise ValueError("mix_apply_: size mismatch")
+    rc = _fn("jb_mix_apply")(_p(w), _p(red), _p(loc), w.numel(), float(inv_n), _stream())
+    _check(rc, "jb_mix_apply")
 
 
 def scale_(t: torch.Tensor, a: float) -> None:

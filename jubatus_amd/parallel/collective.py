@@ -74,6 +74,22 @@ def allreduce_sum_(tensors: Sequence[torch.Tensor], group=None,
             dist.all_reduce(c, op=dist.ReduceOp.SUM, group=group)
 
 
+def allreduce_sum_async(tensors: Sequence[torch.Tensor], group=None,
+                        bucket_bytes: int = DEFAULT_BUCKET_BYTES) -> list:
+    """Launch in-place SUM all-reduces without blocking; returns the work
+    handles. On RCCL the collective runs on the communicator's stream after
+    the work already queued on the current stream; ``work.wait()`` makes the
+    current stream (not the host) wait for it."""
+    if not is_dist():
+        return []
+    works = []
+    for t in tensors:
+        elems = max(1, bucket_bytes // t.element_size())
+        for c in _chunks(t, elems):
+            works.append(dist.all_reduce(c, op=dist.ReduceOp.SUM, group=group, async_op=True))
+    return works
+
+
 def fingerprint(strings: Sequence[str]) -> int:
     h = hashlib.blake2b("\x00".join(strings).encode(), digest_size=7).digest()
     return int.from_bytes(h, "little")

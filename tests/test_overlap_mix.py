@@ -1,0 +1,74 @@
+"""Overlapped MIX (LinearClassifier.mix_begin / mix_end) on a 2-rank gloo
+group: the cluster mean of the snapshot is folded in while updates made
+during the collective survive; a label-layout disagreement falls back to the
+synchronous MIX. Compared against a numpy recomputation."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+CONV = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+        "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 12}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, q, mismatch):
+    import torch.distributed as dist
+    os.environ.setdefault("JUBATUS_FORCE_CPU", "1")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.classifier import LinearClassifier
+    clf = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV))
+    for lab in ("a", "b"):
+        clf.set_label(lab)
+    if mismatch and rank == 0:
+        clf.set_label("extra")
+    data = [(("a" if (i + rank) % 2 else "b"), {"x": f"v{i % 5}", "n": float(i + rank)}) for i in range(20)]
+    clf.train(data)
+    snapW, snapP = clf.W.copy(), clf.P.copy()
+    h = clf.mix_begin()
+    late = [("a", {"x": "late", "n": 1.0})] if rank == 1 and not mismatch else []
+    clf.train(late)                      # keeps going while the collective runs
+    W_after, P_after = clf.W.copy(), clf.P.copy()
+    clf.mix_end(h)
+    # every rank's snapshot, for the reference computation
+    out = [None, None]
+    dist.all_gather_object(out, (snapW, snapP, W_after, P_after, clf.W.copy(), clf.P.copy(),
+                                 clf.get_labels()))
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mismatch", [False, True])
+def test_overlapped_mix(mismatch):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q, mismatch)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (s0W, s0P, a0W, a0P, f0W, f0P, l0), (s1W, s1P, a1W, a1P, f1W, f1P, l1) = res
+    if not mismatch:
+        meanW, meanP = (s0W + s1W) / 2, (s0P + s1P) / 2
+        np.testing.assert_allclose(f0W, meanW + (a0W - s0W), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(f1W, meanW + (a1W - s1W), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(f1P, meanP + (a1P - s1P), rtol=1e-5, atol=1e-6)
+        assert l0 == {"a": 20, "b": 20} and l1 == {"a": 21, "b": 20}   # + rank 1's late sample
+    else:
+        # fell back to the synchronous MIX: one label layout, identical tables
+        assert set(l0) == set(l1) == {"a", "b", "extra"}
+        np.testing.assert_allclose(f0W, f1W, rtol=1e-6, atol=1e-7)
