@@ -81,6 +81,7 @@ class LinearClassifier:
         self._lock = threading.RLock()
         self.device = device
         self.gpu = device is not None
+        self.direct = True        # fused single-launch path for small classify requests
         self.LC = 0
         self._label_version = -1
         if self.gpu:
@@ -216,6 +217,10 @@ class LinearClassifier:
         with self._lock:
             if self.gpu and self.pipe.fast:
                 from ..ops import hip
+                self._sync_labels()
+                scores = self.pipe.classify_direct(list(bodies), self.W) if self.direct else None
+                if scores is not None:
+                    return self._results(scores)
                 b = self.pipe.from_requests(list(bodies), False, None)
                 self._sync_labels()
                 if b.n == 0:

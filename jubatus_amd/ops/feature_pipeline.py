@@ -141,6 +141,7 @@ class FeaturePipeline:
         self._copy_stream = torch.cuda.Stream(device=self.device)
         self._last_mark: torch.cuda.Event | None = None
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._direct = None
         if self.fast:
             rt = GpuRuleTable(converter)
             self.rules = rt
@@ -246,6 +247,55 @@ class FeaturePipeline:
                         self.d_nrules, self.rules.n_nrules, self.d_blob, self.H, d_idx, d_val,
                         self.err)
         return DeviceBatch(n, nslots, R, d_row, d_idx, d_val, d_lab, d_sp)
+
+    # ------------------------------------------------------ direct classify
+    def classify_direct(self, bodies: list, W: torch.Tensor) -> np.ndarray | None:
+        """Latency path for small classify requests: host scan into pinned
+        descriptors, then ONE fused kernel (csrc/hip/classify_direct.hip)
+        whose arguments carry the request bytes and whose scores land in
+        pinned host memory. Returns [n, LC] scores, or None when the request
+        is too large for the direct path."""
+        if not self.fast:
+            return None
+        total = sum(memoryview(b).nbytes for b in bodies)
+        if total > hip.DIRECT_MAX_BYTES:
+            return None
+        LC = W.shape[1]
+        d = self._direct
+        if d is None or d["LC"] < LC:
+            cap = hip.DIRECT_MAX_SAMPLES
+            d = self._direct = {
+                "LC": LC,
+                "staging": torch.empty(hip.DIRECT_MAX_BYTES + 64, dtype=torch.uint8, pin_memory=True),
+                "datum_off": torch.empty(cap + 1, dtype=torch.int64, pin_memory=True),
+                "datum_len": torch.empty(cap + 1, dtype=torch.int32, pin_memory=True),
+                "row_ptr": torch.empty(cap + 2, dtype=torch.int64, pin_memory=True),
+                "stream_ptr": torch.empty(len(bodies) + 64, dtype=torch.int64, pin_memory=True),
+                "out": hip.HostBuffer(cap * LC * 4),
+                "err": hip.HostBuffer(64),
+            }
+        if d["stream_ptr"].numel() < len(bodies) + 1:
+            d["stream_ptr"] = torch.empty(len(bodies) + 64, dtype=torch.int64, pin_memory=True)
+        n, nbytes, _, err, err_req = native().pack_requests(
+            bodies, False, self.rules.n_srules, self.rules.n_nrules, None,
+            d["staging"].data_ptr(), d["staging"].numel(), d["datum_off"].data_ptr(),
+            d["datum_len"].data_ptr(), 0, d["row_ptr"].data_ptr(), d["stream_ptr"].data_ptr(),
+            hip.DIRECT_MAX_SAMPLES, 1)
+        if err == 2:
+            return None
+        if err == 1:
+            raise TypeError(f"malformed datum list in request {err_req}")
+        if n == 0:
+            return np.zeros((0, LC), dtype=np.float32)
+        ok = hip.classify_direct(d["staging"].data_ptr(), nbytes, d["datum_off"].data_ptr(),
+                                 d["datum_len"].data_ptr(), d["row_ptr"].data_ptr(), n,
+                                 self.d_srules, self.rules.n_srules, self.d_nrules,
+                                 self.rules.n_nrules, self.d_blob, self.H, W, d["out"], d["err"])
+        if not ok:
+            return None
+        if int(d["err"].view(np.int32, 1)[0]):
+            raise RuntimeError("GPU datum parser reported a malformed datum")
+        return d["out"].view(np.float32, n * LC).reshape(n, LC).copy()
 
     # ------------------------------------------------------------ host path
     def from_rows(self, rows: list[tuple[list[int], list[float]]], labels: list[int] | None,

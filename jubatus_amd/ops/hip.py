@@ -41,6 +41,9 @@ _SIGS = {
     "jb_sparse_scan": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
     "jb_mix_apply": [_c_void_p, _c_void_p, _c_void_p, _i64, _f32, _c_void_p],
+    "jb_classify_direct": [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
+                           _i32, _c_void_p, _i32, _c_void_p, _u64, _c_void_p, _i32, _c_void_p,
+                           _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -237,3 +240,59 @@ def regression_estimate(row_ptr, fidx, fval, n: int, W, out) -> None:
     rc = _fn("jb_regression_estimate")(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), _p(out),
                                        _stream())
     _check(rc, "jb_regression_estimate")
+
+
+# ------------------------------------------------------------ direct classify
+DIRECT_MAX_SAMPLES = 32     # csrc/hip/classify_direct.hip kDirectMaxSamples
+DIRECT_MAX_BYTES = 2816     # kDirectArgBytes
+
+
+class HostBuffer:
+    """Fine-grained pinned host memory (hipHostMallocCoherent) that kernels
+    write into directly; exposed to the host as a numpy array."""
+
+    def __init__(self, nbytes: int):
+        lib = hip_lib()
+        lib.jb_host_alloc.restype = ctypes.c_void_p
+        lib.jb_host_alloc.argtypes = [_i64]
+        lib.jb_host_free.argtypes = [_c_void_p]
+        self._lib = lib
+        self.nbytes = int(nbytes)
+        self.ptr = lib.jb_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"hipHostMalloc({nbytes}) failed")
+
+    def view(self, dtype, count: int, offset: int = 0):
+        import numpy as np
+        dt = np.dtype(dtype)
+        if offset + count * dt.itemsize > self.nbytes:
+            raise ValueError("HostBuffer view out of range")
+        buf = (ctypes.c_uint8 * (count * dt.itemsize)).from_address(self.ptr + offset)
+        return np.frombuffer(buf, dtype=dt, count=count)
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            self._lib.jb_host_free(self.ptr)
+            self.ptr = None
+
+
+def classify_direct(bytes_ptr: int, nbytes: int, datum_off_ptr: int, datum_len_ptr: int,
+                    row_ptr_ptr: int, n: int, srules, n_srules: int, nrules, n_nrules: int, blob,
+                    H: int, W: torch.Tensor, out: HostBuffer, err: HostBuffer) -> bool:
+    """One fused parse+hash+score launch for a small classify request; the
+    host arrays (bytes, datum_off/len, row_ptr) are host pointers, the scores
+    land in ``out`` (n x LC fp32). Returns False when the request does not fit
+    the direct path (the caller uses the batch path)."""
+    LC = W.shape[1]
+    if LC not in LABEL_CAPS:
+        raise ValueError(f"label capacity {LC} not supported")
+    _dev(W, torch.float32, "W")
+    if out.nbytes < n * LC * 4 or err.nbytes < 4:
+        raise ValueError("classify_direct: output buffer too small")
+    rc = _fn("jb_classify_direct")(bytes_ptr, nbytes, datum_off_ptr, datum_len_ptr, row_ptr_ptr, n,
+                                   _p(srules), n_srules, _p(nrules), n_nrules, _p(blob),
+                                   H, _p(W), LC, out.ptr, err.ptr, _stream())
+    if rc == 1:
+        return False
+    _check(rc, "jb_classify_direct")
+    return True

@@ -213,3 +213,43 @@ def test_mixed_width_stream_matches_oracle(nlabels, mode):
         if c.P is not None:
             np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3,
                                        atol=2e-3 * float(c.P.max()))
+
+
+@pytest.mark.parametrize("nq", [1, 7, 32, 33])
+def test_direct_classify_matches_batch_path(nq):
+    """classify_direct.hip (request bytes in the kernel arguments, scores
+    written into pinned host memory) == batch path == host oracle."""
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    param = {"regularization_weight": 1.0}
+    g = LinearClassifier("AROW", param, DatumToFvConverter(CONV), device=_device())
+    c = LinearClassifier("AROW", param, DatumToFvConverter(CONV))
+    data = _data(300, seed=11, nlabels=9)
+    g.train(data)
+    c.train(data)
+    q = [d for _, d in data[:nq]]
+    g.direct = True
+    a = g.classify(q)
+    g.direct = False
+    b = g.classify(q)
+    r = c.classify(q)
+    assert len(a) == len(b) == len(r) == nq
+    for x, y, z in zip(a, b, r):
+        assert [t[0] for t in x] == [t[0] for t in y] == [t[0] for t in z]
+        np.testing.assert_allclose([t[1] for t in x], [t[1] for t in y], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose([t[1] for t in x], [t[1] for t in z], rtol=2e-3, atol=2e-3)
+
+
+def test_direct_classify_used_for_small_requests():
+    import msgpack as mp
+    from jubatus_amd.fv_converter.datum import Datum
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    g = LinearClassifier("PA", {}, DatumToFvConverter(CONV), device=_device())
+    data = _data(50, seed=12)
+    g.train(data)
+    body = mp.packb([Datum(data[0][1]).to_msgpack()], use_bin_type=False)
+    scores = g.pipe.classify_direct([body], g.W)
+    assert scores is not None and scores.shape == (1, g.LC)
+    big = mp.packb([Datum(d).to_msgpack() for _, d in data], use_bin_type=False)
+    assert g.pipe.classify_direct([big], g.W) is None   # > kernarg block: batch path
