@@ -13,12 +13,15 @@
 // datum stages its bytes into LDS, lane 0 parses and hashes the features into
 // LDS, then the wave gathers the W rows of those features (HBM) and writes
 // the LC scores straight into fine-grained pinned host memory. The host waits
-// for that single dispatch. No copy engine, no second launch.
+// for that single dispatch by spinning on per-datum completion flags the
+// kernel publishes after its scores. No copy engine, no second launch.
 //
 // Requests that do not fit the kernarg block take the batch path.
 #include "jb_fv.hpp"
 #include "jb_linear.hpp"
 
+#include <atomic>
+#include <chrono>
 #include <cstring>
 
 namespace jb {
@@ -43,7 +46,8 @@ template <int LC>
 __global__ __launch_bounds__(64) void classify_direct_kernel(
     const DirectArgs a, const GpuRule* __restrict__ srules, int n_srules,
     const GpuRule* __restrict__ nrules, int n_nrules, const uint8_t* __restrict__ blob, uint64_t H,
-    const float* W, float* __restrict__ out, int32_t* __restrict__ err) {
+    const float* W, float* __restrict__ out, int32_t* __restrict__ err,
+    volatile uint32_t* __restrict__ done, uint32_t seq) {
   using L = Lanes<LC>;
   __shared__ __attribute__((aligned(16))) uint8_t s_bytes[kDirectArgBytes];
   __shared__ int32_t s_idx[kDirectMaxSlots];
@@ -65,16 +69,20 @@ __global__ __launch_bounds__(64) void classify_direct_kernel(
     s_ok = emit_datum(rd, 0, nslots, srules, n_srules, nrules, n_nrules, blob, H, s_idx, s_val);
   }
   __syncthreads();
-  if (!s_ok) {
-    if (lane == 0) *err = 2;
-    return;
-  }
-  float acc[L::K];
-  sample_scores<LC>(s_idx, s_val, 0, nslots, W, lane, acc);
-  if (lane < L::LW) {
+  if (s_ok) {
+    float acc[L::K];
+    sample_scores<LC>(s_idx, s_val, 0, nslots, W, lane, acc);
+    if (lane < L::LW) {
 #pragma unroll
-    for (int k = 0; k < L::K; ++k) out[(int64_t)s * LC + lane + 64 * k] = acc[k];
+      for (int k = 0; k < L::K; ++k) out[(int64_t)s * LC + lane + 64 * k] = acc[k];
+    }
+  } else if (lane == 0) {
+    *err = 2;
   }
+  // completion flag of this datum, published after the scores at system
+  // scope: the host spins on it instead of a stream synchronisation
+  __threadfence_system();
+  if (lane == 0) done[s] = seq;
 }
 
 }  // namespace jb
@@ -87,7 +95,7 @@ extern "C" int jb_classify_direct(const uint8_t* bytes, int64_t nbytes, const in
                                   const void* srules, int n_srules, const void* nrules,
                                   int n_nrules, const uint8_t* blob, uint64_t H, const float* W,
                                   int LC, float* out_host, int32_t* err_host,
-                                  hipStream_t stream) {
+                                  uint32_t* done_host, hipStream_t stream) {
   if (n <= 0) return 0;
   if (n > jb::kDirectMaxSamples || nbytes > jb::kDirectArgBytes) return 1;
   jb::DirectArgs a;
@@ -104,15 +112,29 @@ extern "C" int jb_classify_direct(const uint8_t* bytes, int64_t nbytes, const in
   }
   std::memcpy(a.bytes, bytes, (size_t)nbytes);
   *err_host = 0;
+  static std::atomic<uint32_t> g_seq{0};
+  const uint32_t seq = g_seq.fetch_add(1, std::memory_order_relaxed) + 1;
 #define JB_DIRECT(L)                                                                       \
   hipLaunchKernelGGL((jb::classify_direct_kernel<L>), dim3(n), dim3(64), 0, stream, a,    \
                      (const jb::GpuRule*)srules, n_srules, (const jb::GpuRule*)nrules,     \
-                     n_nrules, blob, H, W, out_host, err_host);
+                     n_nrules, blob, H, W, out_host, err_host, done_host, seq);
   JB_LC_DISPATCH(LC, JB_DIRECT)
 #undef JB_DIRECT
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  return (int)hipStreamSynchronize(stream);
+  // spin on the per-datum completion flags (a blocking stream sync costs an
+  // interrupt + wakeup); after ~2 ms of spinning fall back to the sync,
+  // which also surfaces any asynchronous launch error
+  volatile uint32_t* done = done_host;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n;) {
+    if (done[i] == seq) { ++i; continue; }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+      return (int)hipStreamSynchronize(stream);
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return 0;
 }
 
 // Fine-grained (coherent) pinned host memory the GPU writes into directly.

@@ -273,6 +273,7 @@ class FeaturePipeline:
                 "stream_ptr": torch.empty(len(bodies) + 64, dtype=torch.int64, pin_memory=True),
                 "out": hip.HostBuffer(cap * LC * 4),
                 "err": hip.HostBuffer(64),
+                "done": hip.HostBuffer(4 * cap),
             }
         if d["stream_ptr"].numel() < len(bodies) + 1:
             d["stream_ptr"] = torch.empty(len(bodies) + 64, dtype=torch.int64, pin_memory=True)
@@ -290,7 +291,8 @@ class FeaturePipeline:
         ok = hip.classify_direct(d["staging"].data_ptr(), nbytes, d["datum_off"].data_ptr(),
                                  d["datum_len"].data_ptr(), d["row_ptr"].data_ptr(), n,
                                  self.d_srules, self.rules.n_srules, self.d_nrules,
-                                 self.rules.n_nrules, self.d_blob, self.H, W, d["out"], d["err"])
+                                 self.rules.n_nrules, self.d_blob, self.H, W, d["out"], d["err"],
+                                 d["done"])
         if not ok:
             return None
         if int(d["err"].view(np.int32, 1)[0]):

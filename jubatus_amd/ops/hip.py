@@ -43,7 +43,7 @@ _SIGS = {
     "jb_mix_apply": [_c_void_p, _c_void_p, _c_void_p, _i64, _f32, _c_void_p],
     "jb_classify_direct": [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
                            _i32, _c_void_p, _i32, _c_void_p, _u64, _c_void_p, _i32, _c_void_p,
-                           _c_void_p, _c_void_p],
+                           _c_void_p, _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -261,6 +261,7 @@ class HostBuffer:
         self.ptr = lib.jb_host_alloc(self.nbytes)
         if not self.ptr:
             raise MemoryError(f"hipHostMalloc({nbytes}) failed")
+        ctypes.memset(self.ptr, 0, self.nbytes)
 
     def view(self, dtype, count: int, offset: int = 0):
         import numpy as np
@@ -278,7 +279,8 @@ class HostBuffer:
 
 def classify_direct(bytes_ptr: int, nbytes: int, datum_off_ptr: int, datum_len_ptr: int,
                     row_ptr_ptr: int, n: int, srules, n_srules: int, nrules, n_nrules: int, blob,
-                    H: int, W: torch.Tensor, out: HostBuffer, err: HostBuffer) -> bool:
+                    H: int, W: torch.Tensor, out: HostBuffer, err: HostBuffer,
+                    done: HostBuffer) -> bool:
     """One fused parse+hash+score launch for a small classify request; the
     host arrays (bytes, datum_off/len, row_ptr) are host pointers, the scores
     land in ``out`` (n x LC fp32). Returns False when the request does not fit
@@ -287,11 +289,11 @@ def classify_direct(bytes_ptr: int, nbytes: int, datum_off_ptr: int, datum_len_p
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
     _dev(W, torch.float32, "W")
-    if out.nbytes < n * LC * 4 or err.nbytes < 4:
+    if out.nbytes < n * LC * 4 or err.nbytes < 4 or done.nbytes < 4 * n:
         raise ValueError("classify_direct: output buffer too small")
     rc = _fn("jb_classify_direct")(bytes_ptr, nbytes, datum_off_ptr, datum_len_ptr, row_ptr_ptr, n,
                                    _p(srules), n_srules, _p(nrules), n_nrules, _p(blob),
-                                   H, _p(W), LC, out.ptr, err.ptr, _stream())
+                                   H, _p(W), LC, out.ptr, err.ptr, done.ptr, _stream())
     if rc == 1:
         return False
     _check(rc, "jb_classify_direct")
