@@ -3,6 +3,7 @@
 #include <pybind11/stl.h>
 
 #include "jb_hash.hpp"
+#include "jb_hostfv.hpp"
 #include "jb_pack.hpp"
 #include "jb_rpc.hpp"
 
@@ -123,6 +124,32 @@ class PyRpcServer {
   std::unique_ptr<jb::RpcServer> srv_;
 };
 
+jb::HostFvHasher* make_hasher(py::buffer srules, int n_srules, py::buffer nrules, int n_nrules,
+                              py::buffer blob, uint64_t H) {
+  py::buffer_info s = srules.request(), n = nrules.request(), b = blob.request();
+  if ((size_t)s.size * s.itemsize < sizeof(jb::HostRule) * (size_t)n_srules ||
+      (size_t)n.size * n.itemsize < sizeof(jb::HostRule) * (size_t)n_nrules)
+    throw std::invalid_argument("rule table shorter than its rule count");
+  return new jb::HostFvHasher((const uint8_t*)s.ptr, n_srules, (const uint8_t*)n.ptr, n_nrules,
+                              (const uint8_t*)b.ptr, (size_t)(b.size * b.itemsize), H);
+}
+
+// -> (n_samples, n_slots, error): 0 ok, 1 malformed request, 2 capacity
+py::tuple hasher_hash(const jb::HostFvHasher& h, py::list reqs, uintptr_t idx, uintptr_t val,
+                      uintptr_t row_ptr, int64_t max_samples, int64_t max_slots) {
+  int64_t n = 0, slots = 0;
+  int64_t* rp = (int64_t*)row_ptr;
+  rp[0] = 0;
+  for (auto item : reqs) {
+    py::buffer b = py::reinterpret_borrow<py::buffer>(item);
+    py::buffer_info bi = b.request();
+    int rc = h.hash_body((const uint8_t*)bi.ptr, (size_t)(bi.size * bi.itemsize), (int32_t*)idx,
+                         (float*)val, rp, max_samples, max_slots, &n, &slots);
+    if (rc) return py::make_tuple(n, slots, rc);
+  }
+  return py::make_tuple(n, slots, 0);
+}
+
 int64_t frame(py::buffer b) {
   py::buffer_info bi = b.request();
   return jb::msgpack_frame((const uint8_t*)bi.ptr, (size_t)(bi.size * bi.itemsize));
@@ -145,6 +172,9 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("count", &jb::LabelTable::count)
       .def("set_count", &jb::LabelTable::set_count)
       .def("add_count", &jb::LabelTable::add_count);
+  py::class_<jb::HostFvHasher>(m, "HostFvHasher")
+      .def(py::init(&make_hasher))
+      .def("hash", &hasher_hash, "hash msgpack list<datum> bodies into CSR (idx, val, row_ptr)");
   m.def("pack_requests", &pack, "scan msgpack request bodies into a device-ready batch");
   m.def("pack_spans", &pack_spans, "zero-copy scan of request spans inside one pinned arena");
   py::class_<PyRpcServer>(m, "RpcServer")

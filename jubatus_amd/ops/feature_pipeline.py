@@ -250,53 +250,41 @@ class FeaturePipeline:
 
     # ------------------------------------------------------ direct classify
     def classify_direct(self, bodies: list, W: torch.Tensor) -> np.ndarray | None:
-        """Latency path for small classify requests: host scan into pinned
-        descriptors, then ONE fused kernel (csrc/hip/classify_direct.hip)
-        whose arguments carry the request bytes and whose scores land in
-        pinned host memory. Returns [n, LC] scores, or None when the request
-        is too large for the direct path."""
+        """Latency path for small classify requests: the native host hasher
+        (csrc/native/jb_hostfv.hpp, bit-identical to fv_hash) turns the
+        bodies into CSR, then ONE kernel (csrc/hip/classify_direct.hip)
+        whose arguments carry the (idx, val) pairs scores them against the
+        HBM-resident W and writes into pinned host memory. Returns [n, LC]
+        scores, or None when the request is too large for the direct path."""
         if not self.fast:
-            return None
-        total = sum(memoryview(b).nbytes for b in bodies)
-        if total > hip.DIRECT_MAX_BYTES:
             return None
         LC = W.shape[1]
         d = self._direct
         if d is None or d["LC"] < LC:
-            cap = hip.DIRECT_MAX_SAMPLES
+            cap, slots = hip.DIRECT_MAX_SAMPLES, hip.DIRECT_MAX_SLOTS
+            r = self.rules
             d = self._direct = {
                 "LC": LC,
-                "staging": torch.empty(hip.DIRECT_MAX_BYTES + 64, dtype=torch.uint8, pin_memory=True),
-                "datum_off": torch.empty(cap + 1, dtype=torch.int64, pin_memory=True),
-                "datum_len": torch.empty(cap + 1, dtype=torch.int32, pin_memory=True),
-                "row_ptr": torch.empty(cap + 2, dtype=torch.int64, pin_memory=True),
-                "stream_ptr": torch.empty(len(bodies) + 64, dtype=torch.int64, pin_memory=True),
+                "hasher": native().HostFvHasher(r.srules, r.n_srules, r.nrules, r.n_nrules, r.blob,
+                                                self.H),
+                "idx": np.zeros(slots, np.int32),
+                "val": np.zeros(slots, np.float32),
+                "row_ptr": np.zeros(cap + 1, np.int64),
                 "out": hip.HostBuffer(cap * LC * 4),
-                "err": hip.HostBuffer(64),
                 "done": hip.HostBuffer(4 * cap),
             }
-        if d["stream_ptr"].numel() < len(bodies) + 1:
-            d["stream_ptr"] = torch.empty(len(bodies) + 64, dtype=torch.int64, pin_memory=True)
-        n, nbytes, _, err, err_req = native().pack_requests(
-            bodies, False, self.rules.n_srules, self.rules.n_nrules, None,
-            d["staging"].data_ptr(), d["staging"].numel(), d["datum_off"].data_ptr(),
-            d["datum_len"].data_ptr(), 0, d["row_ptr"].data_ptr(), d["stream_ptr"].data_ptr(),
-            hip.DIRECT_MAX_SAMPLES, 1)
+        n, _, err = d["hasher"].hash(bodies, d["idx"].ctypes.data, d["val"].ctypes.data,
+                                     d["row_ptr"].ctypes.data, hip.DIRECT_MAX_SAMPLES,
+                                     hip.DIRECT_MAX_SLOTS)
         if err == 2:
             return None
         if err == 1:
-            raise TypeError(f"malformed datum list in request {err_req}")
+            raise TypeError("malformed datum list in classify request")
         if n == 0:
             return np.zeros((0, LC), dtype=np.float32)
-        ok = hip.classify_direct(d["staging"].data_ptr(), nbytes, d["datum_off"].data_ptr(),
-                                 d["datum_len"].data_ptr(), d["row_ptr"].data_ptr(), n,
-                                 self.d_srules, self.rules.n_srules, self.d_nrules,
-                                 self.rules.n_nrules, self.d_blob, self.H, W, d["out"], d["err"],
-                                 d["done"])
-        if not ok:
+        if not hip.classify_direct(d["idx"].ctypes.data, d["val"].ctypes.data,
+                                   d["row_ptr"].ctypes.data, n, W, d["out"], d["done"]):
             return None
-        if int(d["err"].view(np.int32, 1)[0]):
-            raise RuntimeError("GPU datum parser reported a malformed datum")
         return d["out"].view(np.float32, n * LC).reshape(n, LC).copy()
 
     # ------------------------------------------------------------ host path

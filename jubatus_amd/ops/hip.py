@@ -41,9 +41,9 @@ _SIGS = {
     "jb_sparse_scan": [_c_void_p, _c_void_p, _i32, _f32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p],
     "jb_mix_apply": [_c_void_p, _c_void_p, _c_void_p, _i64, _f32, _c_void_p],
-    "jb_classify_direct": [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
-                           _i32, _c_void_p, _i32, _c_void_p, _u64, _c_void_p, _i32, _c_void_p,
-                           _c_void_p, _c_void_p, _c_void_p],
+    "jb_classify_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
+                           _c_void_p, _c_void_p],
+    "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -244,7 +244,7 @@ def regression_estimate(row_ptr, fidx, fval, n: int, W, out) -> None:
 
 # ------------------------------------------------------------ direct classify
 DIRECT_MAX_SAMPLES = 32     # csrc/hip/classify_direct.hip kDirectMaxSamples
-DIRECT_MAX_BYTES = 2816     # kDirectArgBytes
+DIRECT_MAX_SLOTS = 320      # kDirectMaxSlots
 
 
 class HostBuffer:
@@ -277,24 +277,26 @@ class HostBuffer:
             self.ptr = None
 
 
-def classify_direct(bytes_ptr: int, nbytes: int, datum_off_ptr: int, datum_len_ptr: int,
-                    row_ptr_ptr: int, n: int, srules, n_srules: int, nrules, n_nrules: int, blob,
-                    H: int, W: torch.Tensor, out: HostBuffer, err: HostBuffer,
-                    done: HostBuffer) -> bool:
-    """One fused parse+hash+score launch for a small classify request; the
-    host arrays (bytes, datum_off/len, row_ptr) are host pointers, the scores
-    land in ``out`` (n x LC fp32). Returns False when the request does not fit
-    the direct path (the caller uses the batch path)."""
+def classify_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, n: int, W: torch.Tensor,
+                    out: HostBuffer, done: HostBuffer, stream: int | None = None) -> bool:
+    """Scores of n host-hashed datums (host CSR pointers) computed by ONE
+    launch whose kernel arguments carry the (idx, val) pairs; the scores land
+    in ``out`` (n x LC fp32). Returns False when the request does not fit the
+    direct path (the caller uses the batch path)."""
     LC = W.shape[1]
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
     _dev(W, torch.float32, "W")
-    if out.nbytes < n * LC * 4 or err.nbytes < 4 or done.nbytes < 4 * n:
+    if out.nbytes < n * LC * 4 or done.nbytes < 4 * n:
         raise ValueError("classify_direct: output buffer too small")
-    rc = _fn("jb_classify_direct")(bytes_ptr, nbytes, datum_off_ptr, datum_len_ptr, row_ptr_ptr, n,
-                                   _p(srules), n_srules, _p(nrules), n_nrules, _p(blob),
-                                   H, _p(W), LC, out.ptr, err.ptr, done.ptr, _stream())
+    rc = _fn("jb_classify_direct")(idx_ptr, val_ptr, row_ptr_ptr, n, _p(W), LC, out.ptr, done.ptr,
+                                   _stream() if stream is None else stream)
     if rc == 1:
         return False
     _check(rc, "jb_classify_direct")
     return True
+
+
+def diag_empty(done: HostBuffer, spin: bool, stream: int | None = None) -> None:
+    rc = _fn("jb_diag_empty")(done.ptr, 1 if spin else 0, _stream() if stream is None else stream)
+    _check(rc, "jb_diag_empty")

@@ -70,3 +70,43 @@ def test_gpu_eligibility():
     ng = dict(base, string_types={"u": {"method": "ngram", "char_num": "1"}},
               string_rules=[{"key": "*", "type": "u", "sample_weight": "tf", "global_weight": "idf"}])
     assert not gpu_eligible(DatumToFvConverter(ng))
+
+
+def test_native_host_hasher_matches_converter():
+    """csrc/native/jb_hostfv.hpp (low-latency classify path) == host converter."""
+    import random
+
+    import msgpack
+    import numpy as np
+
+    from jubatus_amd._native import native
+    from jubatus_amd.fv_converter.gpu_path import GpuRuleTable
+
+    conf = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"},
+                             {"key": "s1*", "type": "str", "sample_weight": "log_tf",
+                              "global_weight": "bin"}],
+            "num_rules": [{"key": "*", "type": "num"}, {"key": "*1", "type": "log"}],
+            "hash_max_size": 1 << 18}
+    conv = DatumToFvConverter(conf)
+    rt = GpuRuleTable(conv)
+    h = native().HostFvHasher(rt.srules, rt.n_srules, rt.nrules, rt.n_nrules, rt.blob, rt.H)
+    rng = random.Random(4)
+    data = [{**{f"s{j}": f"v{rng.randrange(50)}" for j in range(3)},
+             **{f"n{j}": rng.gauss(0, 5) for j in range(3)}, "big": rng.randrange(1 << 20)}
+            for _ in range(20)]
+    body = msgpack.packb([Datum(d).to_msgpack() for d in data], use_bin_type=False)
+    idx = np.zeros(4096, np.int32)
+    val = np.zeros(4096, np.float32)
+    rp = np.zeros(64, np.int64)
+    n, slots, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 63, 4096)
+    assert (n, err) == (20, 0)
+    for s, d in enumerate(data):
+        hi, hv = conv.hashed(conv.convert(d))
+        gi, gv = idx[rp[s]:rp[s + 1]], val[rp[s]:rp[s + 1]]
+        m = gi >= 0
+        assert sorted(zip(gi[m].tolist(), np.round(gv[m], 4).tolist())) == \
+            sorted(zip(hi, np.round(np.asarray(hv, np.float32), 4).tolist()))
+    # capacity: too few slots / samples -> 2 (caller falls back)
+    assert h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 63, 10)[2] == 2
+    assert h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 5, 4096)[2] == 2
+    assert h.hash([b"\x93\x01"], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 5, 4096)[2] == 1

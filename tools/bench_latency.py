@@ -37,7 +37,6 @@ def timeit(fn, iters):
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 500
     import torch
-    from jubatus_amd._native import native
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.classifier import LinearClassifier
     from jubatus_amd.ops import hip
@@ -58,16 +57,20 @@ def main():
     pipe = clf.pipe
     res["direct_1"] = timeit(lambda: pipe.classify_direct([one], clf.W), iters)
     d = pipe._direct
-    nat = native()
-    res["scan_1"] = timeit(lambda: nat.pack_requests(
-        [one], False, pipe.rules.n_srules, pipe.rules.n_nrules, None, d["staging"].data_ptr(),
-        d["staging"].numel(), d["datum_off"].data_ptr(), d["datum_len"].data_ptr(), 0,
-        d["row_ptr"].data_ptr(), d["stream_ptr"].data_ptr(), hip.DIRECT_MAX_SAMPLES, 1), iters)
-    n, nbytes = 1, len(one)
-    res["kernel_roundtrip_1"] = timeit(lambda: hip.classify_direct(
-        d["staging"].data_ptr(), nbytes, d["datum_off"].data_ptr(), d["datum_len"].data_ptr(),
-        d["row_ptr"].data_ptr(), n, pipe.d_srules, pipe.rules.n_srules, pipe.d_nrules,
-        pipe.rules.n_nrules, pipe.d_blob, pipe.H, clf.W, d["out"], d["err"], d["done"]), iters)
+    hasher = d["hasher"]
+    res["host_hash_1"] = timeit(lambda: hasher.hash([one], d["idx"].ctypes.data, d["val"].ctypes.data,
+                                                    d["row_ptr"].ctypes.data, 32, 320), iters)
+
+    def kr(stream=None):
+        return lambda: hip.classify_direct(d["idx"].ctypes.data, d["val"].ctypes.data,
+                                           d["row_ptr"].ctypes.data, 1, clf.W, d["out"], d["done"],
+                                           stream=stream)
+    ns = torch.cuda.Stream(device=dev)
+    hs = torch.cuda.Stream(device=dev, priority=-1)
+    for name, st in (("cur", None), ("new", ns.cuda_stream), ("hiprio", hs.cuda_stream)):
+        res[f"kernel_roundtrip_{name}"] = timeit(kr(st), iters)
+        res[f"empty_{name}_spin"] = timeit(lambda: hip.diag_empty(d["done"], True, st), iters)
+        res[f"empty_{name}_sync"] = timeit(lambda: hip.diag_empty(d["done"], False, st), iters)
     sc = np.zeros((1, clf.LC), np.float32)
     res["format_1"] = timeit(lambda: clf._results(sc), iters)
     s = torch.cuda.current_stream()
