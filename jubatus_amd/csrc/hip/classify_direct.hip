@@ -46,8 +46,38 @@ __global__ __launch_bounds__(64) void classify_direct_kernel(const DirectArgs a,
   if (s >= a.n) return;
   const int beg = a.slot[s];
   const int n = a.slot[s + 1] - beg;
+  const int g = lane / L::LW;
+  const int l0 = lane % L::LW;
   float acc[L::K];
-  sample_scores<LC>(a.idx, a.val, beg, n, W, lane, acc);
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) acc[k] = 0.f;
+  // 4 features per lane group in flight: the W row loads of one datum are
+  // independent HBM round trips, issue them together
+  for (int j0 = g; j0 < n; j0 += 4 * L::G) {
+    int32_t id[4];
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u * L::G;
+      id[u] = j < n ? a.idx[beg + j] : -1;
+      x[u] = j < n ? a.val[beg + j] : 0.f;
+    }
+    float w[4][L::K];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < L::K; ++k)
+        w[u][k] = id[u] >= 0 ? ld_agent(W + (int64_t)id[u] * LC + l0 + 64 * k) : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < L::K; ++k) acc[k] += x[u] * w[u][k];
+  }
+#pragma unroll
+  for (int off = L::LW; off < 64; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < L::K; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
+  }
   if (lane < L::LW) {
 #pragma unroll
     for (int k = 0; k < L::K; ++k) out[(int64_t)s * LC + lane + 64 * k] = acc[k];

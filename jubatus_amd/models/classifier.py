@@ -81,7 +81,8 @@ class LinearClassifier:
         self._lock = threading.RLock()
         self.device = device
         self.gpu = device is not None
-        self.direct = True        # fused single-launch path for small classify requests
+        self.direct = True        # single-launch path for small classify requests
+        self._result_cols = None
         self.LC = 0
         self._label_version = -1
         if self.gpu:
@@ -208,10 +209,16 @@ class LinearClassifier:
 
     # ----------------------------------------------------------- classify
     def _results(self, scores: np.ndarray) -> list[list[tuple[str, float]]]:
-        names = self.labels.names()
-        alive = self.labels.alive()
-        cols = [i for i, a in enumerate(alive) if a]
-        return [[(names[c], float(row[c])) for c in cols] for row in scores]
+        v = self.labels.version()
+        cache = self._result_cols
+        if cache is None or cache[0] != v:
+            names = self.labels.names()
+            alive = self.labels.alive()
+            cols = [i for i, a in enumerate(alive) if a]
+            cache = self._result_cols = (v, cols, [names[c] for c in cols])
+        _, cols, names = cache
+        sub = scores[:, cols].tolist()
+        return [list(zip(names, row)) for row in sub]
 
     def classify_requests(self, bodies: Sequence[Any]) -> list[list[tuple[str, float]]]:
         with self._lock:

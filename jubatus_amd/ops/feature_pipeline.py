@@ -272,6 +272,9 @@ class FeaturePipeline:
                 "row_ptr": np.zeros(cap + 1, np.int64),
                 "out": hip.HostBuffer(cap * LC * 4),
                 "done": hip.HostBuffer(4 * cap),
+                # high-priority stream: used when the compute stream is idle
+                # (a launch on the busy compute stream keeps train -> classify order)
+                "stream": torch.cuda.Stream(device=self.device, priority=-1),
             }
         n, _, err = d["hasher"].hash(bodies, d["idx"].ctypes.data, d["val"].ctypes.data,
                                      d["row_ptr"].ctypes.data, hip.DIRECT_MAX_SAMPLES,
@@ -282,8 +285,10 @@ class FeaturePipeline:
             raise TypeError("malformed datum list in classify request")
         if n == 0:
             return np.zeros((0, LC), dtype=np.float32)
+        compute = torch.cuda.current_stream(self.device)
+        st = d["stream"].cuda_stream if compute.query() else compute.cuda_stream
         if not hip.classify_direct(d["idx"].ctypes.data, d["val"].ctypes.data,
-                                   d["row_ptr"].ctypes.data, n, W, d["out"], d["done"]):
+                                   d["row_ptr"].ctypes.data, n, W, d["out"], d["done"], stream=st):
             return None
         return d["out"].view(np.float32, n * LC).reshape(n, LC).copy()
 
