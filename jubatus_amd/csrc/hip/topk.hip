@@ -1,0 +1,240 @@
+// Exact top-k (smallest distances) for the similarity engines, fused with
+// the signature scan.
+//
+// Reference: similar_row_* / neighbor_row_* / LOF kNN (recommender_serv.cpp:170-200,
+// nearest_neighbor_serv.cpp:138-172, anomaly_serv.cpp:157-244; the search
+// itself is jubatus_core, EXTERNAL). Replaces "write an nq x N distance
+// matrix, then a radix-select top-k over it" with:
+//
+//   K1  grid (blocks, nq): every block scans tiles of 2048 rows (8 per
+//       thread, coalesced), computes the distance in registers (fused
+//       XOR+popcount over the signature table for lsh / minhash /
+//       euclid_lsh, or a read of a precomputed score vector), drops rows
+//       worse than the block's running k-th best, and merges the survivors
+//       into the block's top-k. Per wave the selection is a "pop" loop over
+//       per-lane sorted register lists: each round is one wave64 butterfly
+//       arg-min (64-wide, 6 shuffle steps) and the winning lane shifts its
+//       list; it stops as soon as the wave minimum is +inf, so after the
+//       first tile the pops cost almost nothing (few rows beat the
+//       threshold). Output: k candidates per block.
+//   K2  one block per query merges the blocks' candidates (same code).
+//
+// Ties are broken by the lower row index (the CPU oracle's stable order).
+// Distances: metric 0 lsh (hamming / hash_num), 2 minhash (mismatch
+// fraction), 1 euclid_lsh (law of cosines on the norms). Invalid rows: +inf.
+#include <limits.h>
+
+#include "jb_device.hpp"
+
+namespace jb {
+
+constexpr int kTopThreads = 256;
+constexpr int kTopR = 8;                          // rows per thread per tile
+constexpr int kTopTile = kTopThreads * kTopR;     // 2048
+constexpr int kTopMaxK = 128;
+constexpr int kTopMaxWords = 16;                  // hash_num <= 1024
+
+__device__ __forceinline__ bool lt_pair(float a, int ia, float b, int ib) {
+  return a < b || (a == b && ia < ib);
+}
+
+// ascending insertion network over N register values (compile-time indices)
+template <int N>
+__device__ __forceinline__ void sort_regs(float (&d)[N], int (&ix)[N]) {
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+#pragma unroll
+    for (int j = i; j > 0; --j) {
+      const bool sw = lt_pair(d[j], ix[j], d[j - 1], ix[j - 1]);
+      const float a = d[j - 1], b = d[j];
+      const int ia = ix[j - 1], ib = ix[j];
+      d[j - 1] = sw ? b : a; d[j] = sw ? a : b;
+      ix[j - 1] = sw ? ib : ia; ix[j] = sw ? ia : ib;
+    }
+  }
+}
+
+__device__ __forceinline__ void wave_argmin(float& v, int& id) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(v, off, 64);
+    const int oid = __shfl_xor(id, off, 64);
+    if (lt_pair(ov, oid, v, id)) { v = ov; id = oid; }
+  }
+}
+
+// Pops the k smallest (d, ix) of the wave's per-lane sorted lists into
+// od/oi[0..k); stops early at +inf and pads with (+inf, INT_MAX). Returns
+// the k-th value (or +inf when fewer than k finite values exist).
+template <int N>
+__device__ __forceinline__ float wave_pop(float (&d)[N], int (&ix)[N], int k,
+                                          float* od, int* oi, int lane) {
+  int r = 0;
+  float last = INFINITY;
+  for (; r < k; ++r) {
+    float v = d[0];
+    int id = ix[0];
+    wave_argmin(v, id);
+    if (!(v < INFINITY)) break;                 // uniform across the wave
+    const bool win = (ix[0] == id) && (d[0] == v);
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) {
+      d[j] = win ? d[j + 1] : d[j];
+      ix[j] = win ? ix[j + 1] : ix[j];
+    }
+    if (win) { d[N - 1] = INFINITY; ix[N - 1] = INT_MAX; }
+    if (lane == 0) { od[r] = v; oi[r] = id; }
+    last = v;
+  }
+  for (int j = r + lane; j < k; j += 64) { od[j] = INFINITY; oi[j] = INT_MAX; }
+  return r == k ? last : INFINITY;
+}
+
+struct TopkSrc {
+  // MODE 0: fused signature scan
+  const uint64_t* qbits;
+  const float* qnorm;
+  const uint64_t* tbits;
+  const float* tnorm;
+  const uint8_t* valid;
+  int words, hash_num, metric;
+  // MODE 1: score vector [nq][n] (flip: distance = 1 - score)
+  // MODE 2: candidate pairs [nq][n]
+  const float* src_d;
+  const int32_t* src_i;
+  int flip;
+};
+
+template <int MODE>
+__device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, int64_t r,
+                                          const uint64_t* qb, float qn, float& d, int& id) {
+  if (r >= n) { d = INFINITY; id = INT_MAX; return; }
+  if (MODE == 0) {
+    id = (int)r;
+    if (!s.valid[r]) { d = INFINITY; return; }
+    int ham = 0;
+#pragma unroll
+    for (int w = 0; w < kTopMaxWords; ++w)
+      if (w < s.words) ham += __popcll(qb[w] ^ s.tbits[r * s.words + w]);
+    const float frac = (float)ham / (float)s.hash_num;
+    if (s.metric == 1) {
+      const float b = s.tnorm[r];
+      d = sqrtf(fmaxf(0.f, qn * qn + b * b - 2.f * qn * b * __cosf(3.14159265f * frac)));
+    } else {
+      d = frac;
+    }
+  } else if (MODE == 1) {
+    id = (int)r;
+    const float v = s.src_d[(int64_t)q * n + r];
+    d = s.flip ? 1.f - v : v;
+    if (!(d < INFINITY) || d != d) d = INFINITY;   // -inf scores / NaN -> absent
+  } else {
+    d = s.src_d[(int64_t)q * n + r];
+    id = s.src_i[(int64_t)q * n + r];
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int64_t n,
+                                                           int64_t per_block, int k,
+                                                           float* __restrict__ out_d,
+                                                           int32_t* __restrict__ out_i) {
+  __shared__ float s_wd[4][kTopMaxK];
+  __shared__ int s_wi[4][kTopMaxK];
+  __shared__ float s_cd[kTopMaxK];
+  __shared__ int s_ci[kTopMaxK];
+  __shared__ float s_thr;
+  __shared__ uint64_t s_q[kTopMaxWords];
+  const int q = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int j = t; j < k; j += kTopThreads) { s_cd[j] = INFINITY; s_ci[j] = INT_MAX; }
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += kTopThreads) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  if (t == 0) s_thr = INFINITY;
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  for (int64_t base = b0; base < b1; base += kTopTile) {
+    const float thr = s_thr;
+    float d[kTopR];
+    int ix[kTopR];
+#pragma unroll
+    for (int r = 0; r < kTopR; ++r) {
+      const int64_t row = base + (int64_t)r * kTopThreads + t;
+      load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
+      if (d[r] > thr) { d[r] = INFINITY; ix[r] = INT_MAX; }
+    }
+    sort_regs<kTopR>(d, ix);
+    wave_pop<kTopR>(d, ix, k, s_wd[wv], s_wi[wv], lane);
+    __syncthreads();
+    if (wv == 0) {
+      // merge carry (k) + 4 wave lists (4k) <= 640 -> 10 per lane
+      constexpr int M = 10;
+      float m[M];
+      int mi[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const int c = lane + 64 * j;
+        if (c < k) { m[j] = s_cd[c]; mi[j] = s_ci[c]; }
+        else if (c < 5 * k) { const int w = (c - k) / k, o = (c - k) % k; m[j] = s_wd[w][o]; mi[j] = s_wi[w][o]; }
+        else { m[j] = INFINITY; mi[j] = INT_MAX; }
+      }
+      __builtin_amdgcn_wave_barrier();
+      sort_regs<M>(m, mi);
+      const float kth = wave_pop<M>(m, mi, k, s_cd, s_ci, lane);
+      if (lane == 0) s_thr = kth;
+    }
+    __syncthreads();
+  }
+  const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
+  for (int j = t; j < k; j += kTopThreads) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
+}
+
+}  // namespace jb
+
+// Top-k smallest distances of nq queries.
+//   mode 0: fused signature scan (qbits [nq][words], tbits [nrows][words],
+//           norms, valid, metric 0 lsh / 1 euclid_lsh / 2 minhash)
+//   mode 1: score vector src_d [nq][nrows] (flip: distance = 1 - score)
+// out_d / out_i: [nq][k] (+inf / INT_MAX padding). scratch_d / scratch_i:
+// >= nq * jb_topk_blocks(nrows, k) * k entries each. k <= 128.
+extern "C" int jb_topk_blocks(int64_t nrows, int k) {
+  if (k <= 0 || nrows <= 0) return 0;
+  const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
+  int64_t max_blocks = 8192 / k;              // bound the candidates K2 merges
+  if (max_blocks < 1) max_blocks = 1;
+  const int64_t tiles_per_block = (tiles + max_blocks - 1) / max_blocks;
+  return (int)((tiles + tiles_per_block - 1) / tiles_per_block);
+}
+
+extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int nq,
+                       const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
+                       int64_t nrows, int words, int hash_num, int metric, const float* src_d,
+                       int flip, int k, float* scratch_d, int32_t* scratch_i, float* out_d,
+                       int32_t* out_i, hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  if (k > jb::kTopMaxK || words > jb::kTopMaxWords || (mode != 0 && mode != 1)) return -2;
+  const int blocks = jb_topk_blocks(nrows, k);
+  const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
+  const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
+  jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
+  if (mode == 0)
+    hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
+                       nrows, per_block, k, scratch_d, scratch_i);
+  else
+    hipLaunchKernelGGL(jb::topk_kernel<1>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
+                       nrows, per_block, k, scratch_d, scratch_i);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int64_t nc = (int64_t)blocks * k;   // candidates per query
+  jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
+  hipLaunchKernelGGL(jb::topk_kernel<2>, dim3(1, nq), dim3(jb::kTopThreads), 0, stream, m, nc,
+                     ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d, out_i);
+  return (int)hipGetLastError();
+}

@@ -84,9 +84,31 @@ class LOF(RowEngine):
             self._lrd[rid] = v
         return v
 
+    def _knn_many(self, rids: list[str], k: int) -> dict[str, list[tuple[str, float]]]:
+        res = self.query_ids(rids, k + 1, similar=False)
+        return {rid: [(o, d) for o, d in nb if o != rid][:k] for rid, nb in res.items()}
+
+    def _prefetch(self, nb: list[tuple[str, float]]) -> None:
+        """warm the lrd/kdist caches _score(nb) needs with two batched kNN
+        launches (neighbours of the neighbours, then the kdist of theirs)
+        instead of one query per row"""
+        need = [o for o, _ in nb if o not in self._lrd]
+        if not need:
+            return
+        lists = self._knn_many(need, self.k)
+        for o, lo in lists.items():
+            self._kdist.setdefault(o, self._kth(lo))
+        need_k = sorted({x for lo in lists.values() for x, _ in lo if x not in self._kdist})
+        if need_k:
+            for x, lx in self._knn_many(need_k, self.k).items():
+                self._kdist[x] = self._kth(lx)
+        for o, lo in lists.items():
+            self._lrd[o] = self._lrd_of(lo)
+
     def _score(self, nb: list[tuple[str, float]]) -> float:
         if not nb:
             return 1.0
+        self._prefetch(nb)
         lp = self._lrd_of(nb)
         lo = [self.lrd(o) for o, _ in nb]
         mean_lo = sum(lo) / len(lo)

@@ -44,6 +44,7 @@ class RowEngine:
         self.rows = RowStore()
         self.unlearner = Unlearner(unlearner, unlearner_parameter)
         self._lock = threading.RLock()
+        self._host_hasher = None
 
     # ------------------------------------------------------------ rows
     def fv_of(self, d: Datum, update_weight: bool = False):
@@ -57,6 +58,76 @@ class RowEngine:
         for victim in self.unlearner.touch(rid):
             if victim != rid:
                 self._remove(victim)
+
+    def _hasher(self):
+        """native host hasher (csrc/native/jb_hostfv.hpp) when the converter
+        config is eligible (no filters / global weights / plug-ins), else None"""
+        if self._host_hasher is None:
+            from ..fv_converter.gpu_path import GpuRuleTable, gpu_eligible
+            if gpu_eligible(self.conv):
+                from .._native import native
+                rt = GpuRuleTable(self.conv)
+                self._host_hasher = native().HostFvHasher(rt.srules, rt.n_srules, rt.nrules,
+                                                          rt.n_nrules, rt.blob, rt.H)
+            else:
+                self._host_hasher = False
+        return self._host_hasher or None
+
+    def _set_many(self, items: list, bump: bool = True, update_weight: bool = True) -> None:
+        """set many rows at once: one native hashing pass over all datums and
+        one bulk index insert (signatures of every row in one launch)."""
+        h = self._hasher()
+        if h is None or len(items) < 2 or self.unlearner.kind:
+            # (the lru unlearner interleaves evictions with inserts: sequential)
+            for rid, dicts in items:
+                self._set(rid, dicts, bump, update_weight)
+            return
+        import msgpack
+        import numpy as np
+        body = msgpack.packb([dicts_to_datum(*d).to_msgpack() for _, d in items], use_bin_type=False)
+        n = len(items)
+        cap = max(1024, 64 * n)
+        while True:
+            idx = np.empty(cap, np.int32)
+            val = np.empty(cap, np.float32)
+            rp = np.zeros(n + 1, np.int64)
+            got, _, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, n, cap)
+            if err == 2:
+                cap *= 4
+                continue
+            if err:
+                raise ValueError("malformed datum in bulk row update")
+            break
+        slots = np.empty(n, np.int64)
+        for i, (rid, dicts) in enumerate(items):
+            a, b = rp[i], rp[i + 1]
+            keep = idx[a:b] >= 0
+            fv = (idx[a:b][keep].tolist(), val[a:b][keep].tolist())
+            slots[i] = self.rows.put(rid, dicts, fv, bump)
+        # a row set twice in one batch: the last write wins (same as sequential)
+        last = {}
+        for i, (rid, _) in enumerate(items):
+            last[rid] = i
+        if len(last) != n:
+            sel = np.asarray(sorted(last.values()), np.int64)
+        else:
+            sel = np.arange(n, dtype=np.int64)
+        lens = rp[sel + 1] - rp[sel]
+        rp2 = np.zeros(sel.size + 1, np.int64)
+        np.cumsum(lens, out=rp2[1:])
+        gather = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in sel]) if sel.size else \
+            np.zeros(0, np.int64)
+        self.index.set_rows_csr(slots[sel], rp2, idx[gather], val[gather])
+        for rid, _ in items:
+            for victim in self.unlearner.touch(rid):
+                if victim != rid:
+                    self._remove(victim)
+
+    def set_rows(self, items: list) -> int:
+        """bulk set_row: [(id, datum)] -> number of rows written"""
+        with self._lock:
+            self._set_many([(rid, datum_to_dicts(as_datum(d))) for rid, d in items])
+            return len(items)
 
     def _remove(self, rid: str, record: bool = True) -> bool:
         s = self.rows.remove(rid, record)
@@ -125,6 +196,21 @@ class RowEngine:
                 raise KeyError(f"row not found: {rid}")
             return self.query_fv(self.rows.fv[s], k, similar)
 
+    def query_ids(self, rids: list[str], k: int, similar: bool) -> dict[str, list[tuple[str, float]]]:
+        """batched query_id (every row's neighbours, itself included): one
+        launch for the LSH family (stored signatures), per-row otherwise"""
+        with self._lock:
+            n = self.rows.nslots
+            slots = [self.rows.slot(r) for r in rids]
+            if any(s is None for s in slots):
+                raise KeyError("row not found")
+            res = None
+            if hasattr(self.index, "query_slots"):
+                res = self.index.query_slots(slots, n, k, similar)
+            if res is None:
+                res = self.index.query([self.rows.fv[s] for s in slots], n, k, similar)
+            return {rid: self._results(r) for rid, r in zip(rids, res)}
+
     # ------------------------------------------------------------ MIX
     def get_diff(self) -> dict:
         return self.rows.get_diff()
@@ -135,10 +221,12 @@ class RowEngine:
 
     def put_diff(self, mixed: dict) -> bool:
         with self._lock:
-            for rid, (v, d) in mixed["rows"].items():
-                if self.rows.version.get(rid, -1) < v or rid not in self.rows.slot_of:
-                    self._set(rid, tuple(dict(x) for x in d), bump=False, update_weight=False)
-                    self.rows.version[rid] = v
+            todo = [(rid, v, d) for rid, (v, d) in mixed["rows"].items()
+                    if self.rows.version.get(rid, -1) < v or rid not in self.rows.slot_of]
+            self._set_many([(rid, tuple(dict(x) for x in d)) for rid, _, d in todo], bump=False,
+                           update_weight=False)
+            for rid, v, _ in todo:
+                self.rows.version[rid] = v
             for rid, v in mixed["removed"].items():
                 if self.rows.version.get(rid, -1) <= v:
                     self._remove(rid, record=False)
@@ -158,8 +246,10 @@ class RowEngine:
             self.clear()
             if obj.get("weights"):
                 self.conv.weights.unpack(obj["weights"])
-            for rid, (v, d) in obj["rows"].items():
-                self._set(rid, tuple(dict(x) for x in d), bump=False, update_weight=False)
+            items = list(obj["rows"].items())
+            self._set_many([(rid, tuple(dict(x) for x in d)) for rid, (_, d) in items], bump=False,
+                           update_weight=False)
+            for rid, (v, _) in items:
                 self.rows.version[rid] = v
 
     def get_status(self) -> dict[str, str]:

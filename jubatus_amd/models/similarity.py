@@ -161,6 +161,39 @@ class LshIndex:
             self.norms[s] = norms
             self.valid[s] = 1
 
+    def set_rows_csr(self, slots: np.ndarray, row_ptr: np.ndarray, idx: np.ndarray,
+                     val: np.ndarray) -> None:
+        """bulk insert: host CSR of n rows -> one H2D copy + one signature
+        launch + one scatter into the HBM table (MIX put_diff, load, bulk
+        ingest)."""
+        n = int(slots.size)
+        if n == 0:
+            return
+        need = int(slots.max()) + 1
+        if need > self.cap:
+            c = self.cap
+            while c < need:
+                c *= 2
+            self._alloc(c)
+        if not self.gpu:
+            rows = [(idx[row_ptr[i]:row_ptr[i + 1]], val[row_ptr[i]:row_ptr[i + 1]]) for i in range(n)]
+            self.set_rows(slots.tolist(), rows)
+            return
+        import torch
+        from ..ops import hip
+        nnz = int(row_ptr[n])
+        d = self.device
+        rp = torch.from_numpy(np.ascontiguousarray(row_ptr[:n + 1], dtype=np.int64)).to(d)
+        fi = torch.from_numpy(np.ascontiguousarray(idx[:max(nnz, 1)], dtype=np.int32)).to(d)
+        fv = torch.from_numpy(np.ascontiguousarray(val[:max(nnz, 1)], dtype=np.float32)).to(d)
+        bits = torch.empty((n, self.words), dtype=torch.int64, device=d)
+        norms = torch.empty(n, dtype=torch.float32, device=d)
+        hip.signature(rp, fi, fv, n, self.hash_num, self.seed, self.mode, bits, norms)
+        st = torch.from_numpy(np.ascontiguousarray(slots, dtype=np.int64)).to(d)
+        self.bits.index_copy_(0, st, bits)
+        self.norms.index_copy_(0, st, norms)
+        self.valid.index_fill_(0, st, 1)
+
     def remove(self, slot: int) -> None:
         if slot < self.cap:
             self.valid[slot] = 0
@@ -198,7 +231,35 @@ class LshIndex:
         return -d if self.metric == 1 else 1.0 - d
 
     def query(self, rows: list, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
+        if self.gpu and nrows > 0 and rows:
+            from ..ops import hip
+            if 0 < k <= hip.TOPK_MAX_K and self.words <= hip.TOPK_MAX_WORDS:
+                # fused scan + exact top-k (csrc/hip/topk.hip): no nq x N matrix
+                qb, qn = self._signatures(rows)
+                d, i = hip.topk_hamming(qb.contiguous(), qn.contiguous(), len(rows), self.bits,
+                                        self.norms, self.valid, nrows, self.hash_num,
+                                        self.metric, k)
+                return _pairs(d.cpu().numpy(), i.cpu().numpy(),
+                              self.similarity_of if similar else None)
         return topk(self.distances(rows, nrows), k, self.similarity_of if similar else None)
+
+    def query_slots(self, slots: Sequence[int], nrows: int, k: int,
+                    similar: bool) -> list[list[tuple[int, float]]] | None:
+        """queries by stored rows (their own signatures, no re-hashing); one
+        fused scan + top-k launch for all of them. None: not supported here
+        (the caller queries by feature vector)."""
+        if not (self.gpu and nrows > 0 and slots):
+            return None
+        from ..ops import hip
+        if not (0 < k <= hip.TOPK_MAX_K and self.words <= hip.TOPK_MAX_WORDS):
+            return None
+        import torch
+        st = torch.as_tensor(list(slots), dtype=torch.int64).to(self.device)
+        qb = self.bits.index_select(0, st).contiguous()
+        qn = self.norms.index_select(0, st).contiguous()
+        d, i = hip.topk_hamming(qb, qn, len(slots), self.bits, self.norms, self.valid, nrows,
+                                self.hash_num, self.metric, k)
+        return _pairs(d.cpu().numpy(), i.cpu().numpy(), self.similarity_of if similar else None)
 
     def state(self, nrows: int) -> dict:
         if self.gpu:
@@ -259,6 +320,18 @@ def topk(d, k: int, to_sim=None) -> list[list[tuple[int, float]]]:
     return out
 
 
+def _pairs(vals: np.ndarray, idx: np.ndarray, to_sim=None) -> list[list[tuple[int, float]]]:
+    out = []
+    for vr, ir in zip(vals, idx):
+        row = []
+        for v, i in zip(vr.tolist(), ir.tolist()):
+            if not math.isfinite(v):
+                break
+            row.append((int(i), float(to_sim(np.float32(v)) if to_sim else v)))
+        out.append(row)
+    return out
+
+
 def _csr_device(rows, device):
     import torch
     n = len(rows)
@@ -306,6 +379,12 @@ class InvertedIndex:
             self.rows[int(s)] = self._norm_row(i, v)
         self._dirty = True
 
+    def set_rows_csr(self, slots: np.ndarray, row_ptr: np.ndarray, idx: np.ndarray,
+                     val: np.ndarray) -> None:
+        rows = [(idx[row_ptr[i]:row_ptr[i + 1]], val[row_ptr[i]:row_ptr[i + 1]])
+                for i in range(int(slots.size))]
+        self.set_rows(slots.tolist(), rows)
+
     def remove(self, slot: int) -> None:
         self.rows.pop(int(slot), None)
         self._dirty = True
@@ -338,18 +417,24 @@ class InvertedIndex:
         self._dirty = False
         return self._dev
 
-    def scores(self, row, nrows: int) -> np.ndarray:
-        """similarity (cosine) or distance (euclid) of one query vs every slot"""
+    def scores_device(self, row, nrows: int):
+        """device score vector (cosine similarity / euclidean distance)"""
+        import torch
+        from ..ops import hip
         qi, qv = self._norm_row(*row)
         q2 = float((qv.astype(np.float64) ** 2).sum())
+        _, rp, ridx, rval, rn2, valid = self._mirror(nrows)
+        out = torch.empty(nrows, dtype=torch.float32, device=self.device)
+        hip.sparse_scan(torch.from_numpy(qi).to(self.device), torch.from_numpy(qv).to(self.device),
+                        q2, rp, ridx, rval, rn2, valid, nrows, 1 if self.euclid else 0, out)
+        return out
+
+    def scores(self, row, nrows: int) -> np.ndarray:
+        """similarity (cosine) or distance (euclid) of one query vs every slot"""
         if self.gpu and nrows:
-            import torch
-            from ..ops import hip
-            _, rp, ridx, rval, rn2, valid = self._mirror(nrows)
-            out = torch.empty(nrows, dtype=torch.float32, device=self.device)
-            hip.sparse_scan(torch.from_numpy(qi).to(self.device), torch.from_numpy(qv).to(self.device),
-                            q2, rp, ridx, rval, rn2, valid, nrows, 1 if self.euclid else 0, out)
-            return out.cpu().numpy()
+            return self.scores_device(row, nrows).cpu().numpy()
+        qi, qv = self._norm_row(*row)
+        q2 = float((qv.astype(np.float64) ** 2).sum())
         out = np.full(nrows, np.inf if self.euclid else -np.inf, dtype=np.float32)
         qd = dict(zip(qi.tolist(), qv.tolist()))
         for s, (i, v) in self.rows.items():
@@ -366,6 +451,17 @@ class InvertedIndex:
 
     def query(self, rows: list, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
         res = []
+        if self.gpu and nrows > 0:
+            from ..ops import hip
+            if 0 < k <= hip.TOPK_MAX_K:
+                for row in rows:
+                    sc = self.scores_device(row, nrows)
+                    d, i = hip.topk_scores(sc, 1, nrows, k, flip=not self.euclid)
+                    (r,) = _pairs(d.cpu().numpy(), i.cpu().numpy())
+                    if similar:
+                        r = [(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in r]
+                    res.append(r)
+                return res
         for row in rows:
             s = self.scores(row, nrows)
             d = s if self.euclid else (1.0 - s)        # distance view

@@ -43,6 +43,9 @@ _SIGS = {
     "jb_mix_apply": [_c_void_p, _c_void_p, _c_void_p, _i64, _f32, _c_void_p],
     "jb_classify_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
                            _c_void_p, _c_void_p],
+    "jb_topk": [_i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
+                _i32, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_topk_blocks": [_i64, _i32],
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
@@ -87,6 +90,66 @@ def hamming_scan(qbits, qnorm, nq: int, tbits, tnorm, valid, nrows: int, hash_nu
     rc = _fn("jb_hamming_scan")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid), nrows,
                                 words, hash_num, metric, _p(out), _stream())
     _check(rc, "jb_hamming_scan")
+
+
+TOPK_MAX_K = 128            # csrc/hip/topk.hip kTopMaxK
+TOPK_MAX_WORDS = 16
+
+
+def _topk_scratch(device, n: int):
+    key = (str(device), "topk")
+    buf = _scratch.get(key)
+    if buf is None or buf[0].numel() < n:
+        c = max(n, 1 << 16)
+        buf = (torch.empty(c, dtype=torch.float32, device=device),
+               torch.empty(c, dtype=torch.int32, device=device))
+        _scratch[key] = buf
+    return buf
+
+
+_scratch: dict = {}
+
+
+def topk_hamming(qbits, qnorm, nq: int, tbits, tnorm, valid, nrows: int, hash_num: int,
+                 metric: int, k: int):
+    """Fused signature scan + exact top-k (csrc/hip/topk.hip): -> (dist [nq, k],
+    row [nq, k]) device tensors, +inf / INT_MAX padded."""
+    words = (hash_num + 63) // 64
+    if not 0 < k <= TOPK_MAX_K or words > TOPK_MAX_WORDS:
+        raise ValueError("topk_hamming: k or hash_num out of range")
+    _dev(valid, torch.uint8, "valid")
+    _dev(tnorm, torch.float32, "tnorm")
+    _dev(qnorm, torch.float32, "qnorm")
+    if (qbits.numel() < nq * words or tbits.numel() < nrows * words or valid.numel() < nrows
+            or tnorm.numel() < nrows or qnorm.numel() < nq):
+        raise ValueError("topk_hamming: bad operand shapes")
+    return _topk(0, qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, None, 0,
+                 k, qbits.device)
+
+
+def topk_scores(scores, nq: int, nrows: int, k: int, flip: bool):
+    """Exact top-k smallest of a [nq, nrows] fp32 distance (flip: 1 - score)
+    matrix -> (dist [nq, k], row [nq, k])."""
+    if not 0 < k <= TOPK_MAX_K:
+        raise ValueError("topk_scores: k out of range")
+    _dev(scores, torch.float32, "scores")
+    if scores.numel() < nq * nrows:
+        raise ValueError("topk_scores: bad operand shapes")
+    return _topk(1, None, None, nq, None, None, None, nrows, 0, 0, 0, scores, 1 if flip else 0, k,
+                 scores.device)
+
+
+def _topk(mode, qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, src, flip,
+          k, device):
+    blocks = _fn("jb_topk_blocks")(nrows, k)
+    sd, si = _topk_scratch(device, nq * blocks * k)
+    out_d = torch.empty((nq, k), dtype=torch.float32, device=device)
+    out_i = torch.empty((nq, k), dtype=torch.int32, device=device)
+    rc = _fn("jb_topk")(mode, _p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid), nrows,
+                        words, hash_num, metric, _p(src), flip, k, _p(sd), _p(si), _p(out_d),
+                        _p(out_i), _stream())
+    _check(rc, "jb_topk")
+    return out_d, out_i
 
 
 def sparse_scan(qidx, qval, qnorm2: float, row_ptr, ridx, rval, rnorm2, valid, nrows: int,

@@ -143,3 +143,46 @@ def test_clustering_on_gpu_matches_cpu():
     g.push(pts)
     cs = sorted(tuple(round(v) for _, v in sorted(c.num_values)) for c in g.get_k_center())
     assert cs == sorted([(0, 0), (8, 8), (-8, 8)])
+
+
+@pytest.mark.parametrize("metric,k,nrows,nq", [(0, 10, 100_000, 3), (1, 10, 250_000, 2),
+                                               (2, 1, 5000, 4), (1, 128, 70_000, 2),
+                                               (0, 37, 3000, 5), (1, 100, 50, 1)])
+def test_topk_hamming_matches_full_sort(metric, k, nrows, nq):
+    """csrc/hip/topk.hip (fused scan + exact top-k) == full distance matrix
+    + stable argsort, including ties (lsh/minhash distances are multiples of
+    1/hash_num) and invalid rows."""
+    import torch
+    from jubatus_amd.ops import hip
+    g = torch.Generator().manual_seed(nrows + k)
+    words = 1
+    tb = torch.randint(-2**62, 2**62, (nrows, words), generator=g, dtype=torch.int64)
+    tn = torch.rand(nrows, generator=g) * 3
+    valid = (torch.rand(nrows, generator=g) > 0.1).to(torch.uint8)
+    qb = torch.randint(-2**62, 2**62, (nq, words), generator=g, dtype=torch.int64)
+    qn = torch.rand(nq, generator=g) * 3
+    d = dev()
+    tbd, tnd, vd, qbd, qnd = (x.to(d) for x in (tb, tn, valid, qb, qn))
+    full = torch.empty((nq, nrows), dtype=torch.float32, device=d)
+    hip.hamming_scan(qbd, qnd, nq, tbd, tnd, vd, nrows, 64, metric, full)
+    od, oi = hip.topk_hamming(qbd, qnd, nq, tbd, tnd, vd, nrows, 64, metric, k)
+    full = full.cpu().numpy()
+    od, oi = od.cpu().numpy(), oi.cpu().numpy()
+    for q in range(nq):
+        order = np.argsort(full[q], kind="stable")[:k]
+        ref = full[q][order]
+        fin = np.isfinite(ref)
+        np.testing.assert_array_equal(oi[q][:fin.sum()], order[fin])
+        np.testing.assert_allclose(od[q][:fin.sum()], ref[fin], rtol=1e-6)
+        assert np.all(np.isinf(od[q][fin.sum():]))
+
+
+def test_topk_scores_flip():
+    import torch
+    from jubatus_amd.ops import hip
+    s = torch.rand((2, 9000), generator=torch.Generator().manual_seed(1))
+    s[0, 5] = float("-inf")
+    od, oi = hip.topk_scores(s.to(dev()), 2, 9000, 20, flip=True)
+    for q in range(2):
+        ref = np.argsort(1.0 - s[q].numpy(), kind="stable")[:20]
+        np.testing.assert_array_equal(oi[q].cpu().numpy(), ref)
