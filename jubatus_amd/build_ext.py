@@ -8,8 +8,10 @@
 * ``jubatus_amd/plugins/libjubatus_{sample_plugins,ux_splitter}.so`` -
   fv_converter plug-ins (C ABI csrc/plugins/jb_plugin.h) in the in-tree
   plug-in directory.
+* ``jubatus_amd/native_bin/jubacoordinator`` - the Python-free coordination
+  server (csrc/coord).
 
-Both are built in-tree so they travel with the repository snapshot to the
+All are built in-tree so they travel with the repository snapshot to the
 GPU box. Incremental: a target is rebuilt only if a source is newer.
 
 Usage: ``python -m jubatus_amd.build_ext [--force] [-j N]``
@@ -116,9 +118,35 @@ def build_plugins(force: bool = False) -> str:
     return PLUGIN_DIR
 
 
-def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, str, str]:
+NATIVE_BIN = os.path.join(PKG, "native_bin")
+# native executables: name -> (sources, extra include dirs)
+TOOLS = {
+    "jubacoordinator": (["coord/jubacoordinator.cpp", "native/jb_rpc.cpp"],
+                        ["coord", "native", "../client_cpp/include"]),
+}
+
+
+def build_tools(force: bool = False, nproc: int = 8) -> str:
+    """Python-free native executables (the coordinator)."""
+    os.makedirs(NATIVE_BIN, exist_ok=True)
+    jobs = []
+    for name, (srcs, incs) in TOOLS.items():
+        target = os.path.join(NATIVE_BIN, name)
+        paths = [os.path.join(CSRC, x) for x in srcs]
+        deps = paths + [h for d in incs for h in glob.glob(os.path.join(CSRC, d, "**", "*.h*"),
+                                                            recursive=True)]
+        if force or _newer(target, deps):
+            jobs.append((target, ["g++", "-O2", "-std=c++17", "-pthread", "-Wall",
+                                  *[f"-I{os.path.join(CSRC, d)}" for d in incs], *paths,
+                                  "-o", target]))
+    _compile_all(jobs, nproc)
+    return NATIVE_BIN
+
+
+def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, ...]:
     nproc = nproc or min(8, os.cpu_count() or 4)
-    return build_native(force, nproc), build_hip(force, nproc), build_plugins(force)
+    return (build_native(force, nproc), build_hip(force, nproc), build_plugins(force),
+            build_tools(force, nproc))
 
 
 def main() -> None:

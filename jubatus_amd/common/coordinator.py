@@ -8,6 +8,8 @@ SURVEY §5.3).
 """
 from __future__ import annotations
 
+import os
+import subprocess
 import threading
 
 from ..utils import logger
@@ -56,6 +58,43 @@ class CoordinatorServer:
     def join(self) -> None:
         while not self._stop.wait(0.5):
             pass
+
+
+NATIVE_BIN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                          "native_bin", "jubacoordinator")
+
+
+def native_available() -> bool:
+    return os.access(NATIVE_BIN, os.X_OK)
+
+
+class NativeCoordinator:
+    """The native coordinator (csrc/coord/jubacoordinator.cpp) as a child
+    process: same RPC surface as CoordinatorServer, no Python in the server."""
+
+    def __init__(self, port: int = 0, bind: str = "127.0.0.1", nthreads: int = 4):
+        if not native_available():
+            from .. import build_ext
+            build_ext.build_tools()
+        self.proc = subprocess.Popen([NATIVE_BIN, "-p", str(port), "-b", bind, "-c", str(nthreads)],
+                                     stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        line = self.proc.stdout.readline()
+        if not line.startswith("jubacoordinator ready"):
+            self.proc.kill()
+            raise RuntimeError(f"native coordinator failed to start: {line!r}")
+        self.port = int(line.split()[-1])
+
+    def start(self) -> "NativeCoordinator":
+        return self
+
+    def stop(self) -> None:
+        if self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
 
 
 def main(argv: list[str] | None = None) -> int:

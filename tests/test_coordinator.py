@@ -9,7 +9,7 @@ import pytest
 from jubatus_amd.common import cht as chtmod
 from jubatus_amd.common import config as zkconfig
 from jubatus_amd.common import membership as mb
-from jubatus_amd.common.coordinator import CoordinatorServer
+from jubatus_amd.common.coordinator import CoordinatorServer, NativeCoordinator
 from jubatus_amd.common.idgen import CoordinatorIdGenerator, StandaloneIdGenerator
 from jubatus_amd.common.lock_service import (CachedLockService, CoordinatorClient, LocalLockService,
                                              LockServiceMutex, ZNodeStore)
@@ -22,14 +22,54 @@ def coord():
     srv.stop()
 
 
-@pytest.fixture(params=["local", "remote"])
-def ls(request, coord):
+@pytest.fixture(scope="module")
+def native_coord():
+    srv = NativeCoordinator(0, "127.0.0.1")
+    yield srv
+    srv.stop()
+
+
+@pytest.fixture(params=["local", "remote", "native"])
+def ls(request, coord, native_coord):
     if request.param == "local":
         s = LocalLockService(ZNodeStore())
-    else:
+    elif request.param == "remote":
         s = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=2.0)
+    else:
+        s = CoordinatorClient(f"127.0.0.1:{native_coord.port}", timeout=2.0)
+        for top in s.list("/"):              # module-scoped server: start from an empty tree
+            _rm_tree(s, "/" + top)
     yield s
     s.close()
+
+
+def _rm_tree(s, path):
+    for c in s.list(path):
+        _rm_tree(s, f"{path}/{c}")
+    s.remove(path)
+
+
+def test_native_coordinator_sessions_and_errors(native_coord):
+    """native server: ephemerals die with the session (close and TTL expiry),
+    NO_METHOD / ARGUMENT errors like the reference rpc_server"""
+    from jubatus_amd.common.mprpc import RpcClient, RpcMethodNotFound, RpcTypeError
+    a = CoordinatorClient(f"127.0.0.1:{native_coord.port}", timeout=0.6)
+    b = CoordinatorClient(f"127.0.0.1:{native_coord.port}", timeout=2.0)
+    b.create("/nat")
+    assert a.create("/nat/e", "x", True) and b.exists("/nat/e")
+    assert not a.create("/nat/e/child")                 # no children under ephemerals
+    a._stop.set()                                       # stop heartbeating: TTL expiry
+    deadline = time.time() + 5
+    while b.exists("/nat/e") and time.time() < deadline:
+        time.sleep(0.05)
+    assert not b.exists("/nat/e")
+    c = RpcClient("127.0.0.1", native_coord.port, timeout=2.0)
+    with pytest.raises(RpcMethodNotFound):
+        c.call("no_such_method")
+    with pytest.raises(RpcTypeError):
+        c.call("create", "not-a-sid", "/p", "", False)
+    assert c.call("dump")["/nat"] == ""
+    b.close()
 
 
 def test_create_exists_remove(ls):

@@ -17,7 +17,7 @@ import pytest
 from jubatus_amd.client import Classifier, Datum
 from jubatus_amd.common import config as zkconfig
 from jubatus_amd.common import membership as mb
-from jubatus_amd.common.coordinator import CoordinatorServer
+from jubatus_amd.common.coordinator import CoordinatorServer, NativeCoordinator, native_available
 from jubatus_amd.common.lock_service import CoordinatorClient
 from jubatus_amd.common.mprpc import wait_server
 
@@ -32,9 +32,11 @@ def free_port():
     return p
 
 
-@pytest.fixture
-def coord():
-    srv = CoordinatorServer(0, "127.0.0.1").start()
+@pytest.fixture(params=["native"])
+def coord(request):
+    # the production coordinator: native C++ server (csrc/coord), no Python
+    srv = NativeCoordinator(0, "127.0.0.1") if native_available() else \
+        CoordinatorServer(0, "127.0.0.1").start()
     yield srv
     srv.stop()
 
