@@ -8,8 +8,8 @@
 * ``jubatus_amd/plugins/libjubatus_{sample_plugins,ux_splitter}.so`` -
   fv_converter plug-ins (C ABI csrc/plugins/jb_plugin.h) in the in-tree
   plug-in directory.
-* ``jubatus_amd/native_bin/jubacoordinator`` - the Python-free coordination
-  server (csrc/coord).
+* ``jubatus_amd/native_bin/{jubacoordinator,jubaproxy}`` - the Python-free
+  coordination server (csrc/coord) and request router (csrc/proxy).
 
 All are built in-tree so they travel with the repository snapshot to the
 GPU box. Incremental: a target is rebuilt only if a source is newer.
@@ -123,6 +123,8 @@ NATIVE_BIN = os.path.join(PKG, "native_bin")
 TOOLS = {
     "jubacoordinator": (["coord/jubacoordinator.cpp", "native/jb_rpc.cpp"],
                         ["coord", "native", "../client_cpp/include"]),
+    "jubaproxy": (["proxy/jubaproxy.cpp", "native/jb_rpc.cpp"],
+                  ["proxy", "native", "../client_cpp/include"]),
 }
 
 

@@ -125,19 +125,50 @@ def test_server_self_fences_when_actor_deleted(coord):
         ls.close()
 
 
-def test_proxy_routing(coord):
+class _NativeProxy:
+    """csrc/proxy/jubaproxy.cpp as a child process"""
+
+    def __init__(self, engine, zport):
+        from jubatus_amd import build_ext
+        exe = os.path.join(build_ext.NATIVE_BIN, "jubaproxy")
+        if not os.access(exe, os.X_OK):
+            build_ext.build_tools()
+        self.port = free_port()
+        self.proc = subprocess.Popen([exe, engine, "-p", str(self.port), "-b", "127.0.0.1",
+                                      "-z", f"127.0.0.1:{zport}", "-I", "5"],
+                                     stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        line = self.proc.stdout.readline()
+        assert line.startswith("jubaproxy ready"), line
+
+    def stop(self):
+        self.proc.terminate()
+        self.proc.wait(10)
+
+
+def _start_proxy(impl, engine, zport):
+    if impl == "native":
+        return _NativeProxy(engine, zport)
     from jubatus_amd.framework.proxy import Proxy
     from jubatus_amd.framework.server_util import ProxyArgv
+    pa = ProxyArgv(type=engine, port=0, bind_address="127.0.0.1", eth="127.0.0.1",
+                   z=f"127.0.0.1:{zport}", program_name=f"juba{engine}_proxy")
+    proxy = Proxy(pa)
+    proxy.start(block=False)
+    proxy.port = pa.port
+    return proxy
 
+
+@pytest.mark.parametrize("impl", ["python", "native"])
+def test_proxy_routing(coord, impl):
     ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
     name = "viaproxy"
     zkconfig.config_tozk(ls, "classifier", name, open(os.path.join(ROOT, "config/classifier/pa.json")).read())
     ports = [free_port(), free_port()]
     procs = [spawn("classifier", coord.port, name, p) for p in ports]
-    pa = ProxyArgv(type="classifier", port=0, bind_address="127.0.0.1", eth="127.0.0.1",
-                   z=f"127.0.0.1:{coord.port}", program_name="jubaclassifier_proxy")
-    proxy = Proxy(pa)
-    proxy.start(block=False)
+    proxy = _start_proxy(impl, "classifier", coord.port)
+
+    class pa:  # noqa: N801
+        port = proxy.port
     try:
         for p in ports:
             assert wait_server("127.0.0.1", p, 60)
@@ -160,6 +191,50 @@ def test_proxy_routing(coord):
         with pytest.raises(RpcCallError):
             Classifier("127.0.0.1", pa.port, "no_such_cluster").get_config()
         c.close()
+    finally:
+        proxy.stop()
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        ls.close()
+
+
+def test_native_proxy_cht_routing(coord):
+    """cht(2) methods reach the two CHT owners of the row id; random analysis
+    methods see the row (recommender, native proxy)"""
+    from jubatus_amd.client import Recommender
+    from jubatus_amd.common.cht import CHT
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    name = "chtproxy"
+    zkconfig.config_tozk(ls, "recommender", name,
+                         open(os.path.join(ROOT, "config/recommender/inverted_index.json")).read())
+    ports = []
+    while len(ports) < 3:
+        p = free_port()
+        if p not in ports:
+            ports.append(p)
+    procs = [spawn("recommender", coord.port, name, p) for p in ports]
+    proxy = _NativeProxy("recommender", coord.port)
+    try:
+        for p in ports:
+            assert wait_server("127.0.0.1", p, 60)
+        assert wait_actives(ls, "recommender", name, 3)
+        r = Recommender("127.0.0.1", proxy.port, name)
+        for i in range(12):
+            assert r.update_row(f"row{i}", Datum({"a": float(i), "b": 1.0})) is True
+        cht = CHT(ls, "recommender", name)
+        for i in range(12):
+            owners = {p for _, p in cht.find(f"row{i}", 2)}
+            for p in ports:
+                rows = Recommender("127.0.0.1", p, name).get_all_rows()
+                assert (f"row{i}" in rows) == (p in owners), (i, p, owners)
+        assert r.decode_row("row3").num_values                    # cht analysis
+        assert r.clear() is True                                   # broadcast all_and
+        r.close()
     finally:
         proxy.stop()
         for p in procs:

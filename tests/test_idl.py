@@ -89,3 +89,12 @@ def test_generated_sources_compile(engine):
     rst = jenerator.emit_rst(f)
     assert all(f".. mdef:: {m.name}(" in rst for m in specs.SERVICES[engine])
     compile("SERVICES = {\n" + jenerator.emit_spec(f) + "}\n", "spec.py", "exec")
+
+
+def test_native_proxy_tables_up_to_date():
+    """csrc/proxy/jb_proxy_tables.hpp (compiled into the native proxy) is the
+    jenerator output of the current specs"""
+    from jubatus_amd.idl import jenerator
+    with open(jenerator.PROXY_TABLES) as f:
+        assert f.read() == jenerator.emit_proxy_tables(), \
+            "regenerate: python -m jubatus_amd.idl.jenerator --proxy-tables"
