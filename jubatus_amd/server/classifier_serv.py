@@ -125,6 +125,30 @@ class ClassifierServ(ServerBase):
             out.append(r)
         return out
 
+    def raw_classify(self, params: bytes) -> list:
+        """zero-copy classify: the list<datum> bytes go straight to the
+        latency path (native hashing + one kernel launch) or the GPU batch
+        pipeline, without building Python datums"""
+        self.check_set_config()
+        if not (hasattr(self.clf, "classify_requests") and getattr(self.clf, "gpu", False)):
+            from ..common.mprpc import unpackb
+            parts = split_params(params)
+            if len(parts) != 2:
+                raise ArgumentError("classify: expected 2 arguments")
+            return self.classify(unpackb(bytes(parts[1])))
+        parts = split_params(params)
+        if len(parts) != 2:
+            raise ArgumentError("classify: expected 2 arguments")
+        try:
+            res = self.clf.classify_requests([parts[1]])
+        except TypeError as e:
+            raise ArgumentError(str(e)) from e
+        for row in res:
+            for label, score in row:
+                if not math.isfinite(score):
+                    log.warning("score is infinite: %s = %s", label, score)
+        return res
+
     def get_labels(self) -> dict:
         self.check_set_config()
         return self.clf.get_labels()

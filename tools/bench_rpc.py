@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""End-to-end RPC latency of the flagship server (1 GPU): msgpack-RPC client
+-> jubaclassifier (AROW, GPU) directly, and through the native coordinator
++ native proxy (distributed mode, one server) - the reference's
+client -> proxy -> server path.
+
+Prints one JSON line: classify / train p50/p99 per path, and
+get_proxy_status of the native proxy.
+
+Usage: python tools/bench_rpc.py [iters]   (needs the native binaries:
+python -m jubatus_amd.build_ext)
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import socket
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def lat(fn, iters):
+    for _ in range(20):
+        fn()
+    xs = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        fn()
+        xs.append((time.perf_counter() - t) * 1e6)
+    xs.sort()
+    return {"p50_us": round(statistics.median(xs), 1), "p99_us": round(xs[int(0.99 * (len(xs) - 1))], 1)}
+
+
+def wait_port(port, timeout=120):
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        try:
+            socket.create_connection(("127.0.0.1", port), 0.5).close()
+            return True
+        except OSError:
+            time.sleep(0.2)
+    return False
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 500
+    from jubatus_amd import build_ext
+    from jubatus_amd.client import Classifier, Datum
+    from jubatus_amd.common import config as zkconfig
+    from jubatus_amd.common import membership as mb
+    from jubatus_amd.common.coordinator import NativeCoordinator
+    from jubatus_amd.common.lock_service import CoordinatorClient
+
+    build_ext.build_tools()
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cfg = os.path.join(ROOT, "config", "classifier", "arow.json")
+    tmp = tempfile.mkdtemp()
+    rng = random.Random(0)
+
+    def datum(y):
+        return Datum({**{f"s{j}": f"t{y * 7 + rng.randrange(4)}" for j in range(8)},
+                      **{f"n{j}": y + rng.gauss(0, 1) for j in range(8)}})
+
+    train = [(f"l{y}", datum(y)) for y in [rng.randrange(16) for _ in range(128)]]
+    one = [datum(3)]
+    out = {"model": "jubaclassifier AROW (config/classifier/arow.json)", "device": "MI355X"}
+    procs = []
+    coord = None
+    try:
+        # standalone server, client -> server
+        sp = free_port()
+        procs.append(subprocess.Popen([sys.executable, "-m", "jubatus_amd.cmd.server", "classifier",
+                                       "-p", str(sp), "-b", "127.0.0.1", "-f", cfg, "-d", tmp],
+                                      env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+        assert wait_port(sp), "server did not start"
+        c = Classifier("127.0.0.1", sp, "", timeout=30)
+        for _ in range(20):
+            c.train(train)
+        out["direct_train_128"] = lat(lambda: c.train(train), iters // 5)
+        out["direct_classify_1"] = lat(lambda: c.classify(one), iters)
+        c.close()
+        # distributed: native coordinator + server + native proxy
+        coord = NativeCoordinator(0, "127.0.0.1")
+        ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
+        zkconfig.config_tozk(ls, "classifier", "bench", open(cfg).read())
+        dp = free_port()
+        procs.append(subprocess.Popen([sys.executable, "-m", "jubatus_amd.cmd.server", "classifier",
+                                       "-p", str(dp), "-b", "127.0.0.1", "-z", f"127.0.0.1:{coord.port}",
+                                       "-n", "bench", "-d", tmp], env=env,
+                                      stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
+        deadline = time.time() + 120
+        while time.time() < deadline and not mb.get_all_actives(ls, "classifier", "bench"):
+            time.sleep(0.2)
+        pp = free_port()
+        px = subprocess.Popen([os.path.join(build_ext.NATIVE_BIN, "jubaproxy"), "classifier",
+                               "-p", str(pp), "-b", "127.0.0.1", "-z", f"127.0.0.1:{coord.port}"],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        procs.append(px)
+        assert px.stdout.readline().startswith("jubaproxy ready")
+        c = Classifier("127.0.0.1", pp, "bench", timeout=30)
+        for _ in range(20):
+            c.train(train)
+        out["proxy_train_128"] = lat(lambda: c.train(train), iters // 5)
+        out["proxy_classify_1"] = lat(lambda: c.classify(one), iters)
+        (_, st), = c.get_proxy_status().items()
+        out["proxy_status"] = {k: st[k] for k in ("request_count", "forward_count", "implementation")}
+        c.close()
+        ls.close()
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        if coord is not None:
+            coord.stop()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
