@@ -307,6 +307,7 @@ void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
                        std::string((const char*)cur.p, (size_t)(p + len - cur.p))};
         std::lock_guard<std::mutex> g(qmu_);
         queue_.push_back(std::move(req));
+        qlen_.store(queue_.size(), std::memory_order_relaxed);
         qcv_.notify_one();
       }
     } else if (ok && n == 3 && type == 2) {
@@ -316,6 +317,7 @@ void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
                        std::string((const char*)cur.p, (size_t)(p + len - cur.p))};
         std::lock_guard<std::mutex> g(qmu_);
         queue_.push_back(std::move(req));
+        qlen_.store(queue_.size(), std::memory_order_relaxed);
         qcv_.notify_one();
       }
     }
@@ -367,15 +369,26 @@ void RpcServer::send_response(uint64_t conn_id, const std::string& bytes) {
 }
 
 void RpcServer::worker_loop() {
+  bool busy = false;
   for (;;) {
     RpcRequest req;
+    if (busy) {
+      // spin briefly after a request before parking on the condition
+      // variable: back-to-back requests skip the futex wakeup (~10-20 us)
+      const double t0 = now_sec();
+      while (qlen_.load(std::memory_order_relaxed) == 0 && running_.load(std::memory_order_relaxed) &&
+             now_sec() - t0 < 50e-6)
+        __builtin_ia32_pause();
+    }
     {
       std::unique_lock<std::mutex> g(qmu_);
       qcv_.wait(g, [this] { return !queue_.empty() || !running_.load(); });
       if (!running_.load()) return;
       req = std::move(queue_.front());
       queue_.pop_front();
+      qlen_.store(queue_.size(), std::memory_order_relaxed);
     }
+    busy = true;
     std::string resp = handler_(req);
     served_.fetch_add(1);
     if (!req.notify && !resp.empty()) send_response(req.conn_id, resp);

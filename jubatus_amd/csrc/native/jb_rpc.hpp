@@ -87,6 +87,7 @@ class RpcServer {
   std::mutex qmu_;
   std::condition_variable qcv_;
   std::deque<RpcRequest> queue_;
+  std::atomic<size_t> qlen_{0};   // queue_.size(), readable without qmu_
   std::mutex wq_mu_;
   std::vector<uint64_t> want_write_;  // conns the IO thread must arm for EPOLLOUT
 };

@@ -75,6 +75,25 @@ def main():
     res["format_1"] = timeit(lambda: clf._results(sc), iters)
     s = torch.cuda.current_stream()
     res["empty_sync"] = timeit(lambda: s.synchronize(), iters)
+    # one train request (one update stream, exact sequential semantics)
+    for nsamp in (1, 16, 128):
+        body = msgpack.packb([[lab, d] for lab, d in items[:nsamp]], use_bin_type=False)
+
+        def tr():
+            clf.train_requests([body])
+            torch.cuda.synchronize()
+        res[f"train_1x{nsamp}_sync"] = timeit(tr, max(50, iters // 5))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    b = clf.pipe.from_requests([body], True, clf.labels)
+    torch.cuda.synchronize()
+    ks = []
+    for _ in range(30):
+        ev0.record()
+        clf._train_batch(b)
+        ev1.record()
+        torch.cuda.synchronize()
+        ks.append(ev0.elapsed_time(ev1) * 1e3)
+    res["train_kernel_1x128_us"] = round(statistics.median(ks), 1)
     clf.direct = False
     res["classify_1_batch_path"] = timeit(lambda: clf.classify_requests([one]), iters)
     print(json.dumps(res), flush=True)

