@@ -103,7 +103,8 @@ PLUGIN_DIR = os.path.join(PKG, "plugins")
 PLUGIN_SO = os.path.join(PLUGIN_DIR, "libjubatus_sample_plugins.so")
 # one shared object per plug-in source
 PLUGINS = {"sample_plugins.cpp": "libjubatus_sample_plugins.so",
-           "ux_splitter.cpp": "libjubatus_ux_splitter.so"}
+           "ux_splitter.cpp": "libjubatus_ux_splitter.so",
+           "mecab_splitter.cpp": "libjubatus_mecab_splitter.so"}
 
 
 def build_plugins(force: bool = False) -> str:
@@ -114,7 +115,7 @@ def build_plugins(force: bool = False) -> str:
         target = os.path.join(PLUGIN_DIR, lib)
         if force or _newer(target, [s] + hdrs):
             _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
-                  f"-I{os.path.join(CSRC, 'plugins')}", "-o", target, s])
+                  f"-I{os.path.join(CSRC, 'plugins')}", "-o", target, s, "-ldl"])
     return PLUGIN_DIR
 
 

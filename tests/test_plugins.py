@@ -93,3 +93,56 @@ def test_ux_splitter_longest_prefix(tmp_path):
                   "t$to@ux#tf/bin": 1.0, "t$tokyo@ux#tf/bin": 1.0}
     with pytest.raises(PluginError):
         PluginLoader().create("string_feature", {"path": "libjubatus_ux_splitter.so", "function": "create"})
+
+
+@pytest.fixture(scope="module")
+def fake_mecab(tmp_path_factory):
+    """a test double of libmecab (tests/fixtures/fake_mecab.cpp): MeCab is not
+    installed here, so parity with real MeCab dictionaries is unpinned"""
+    import subprocess
+    out = tmp_path_factory.mktemp("mecab") / "libfakemecab.so"
+    src = os.path.join(os.path.dirname(__file__), "fixtures", "fake_mecab.cpp")
+    subprocess.run(["g++", "-O1", "-std=c++17", "-shared", "-fPIC", "-o", str(out), src], check=True)
+    return str(out)
+
+
+def _mecab_conv(lib, **params):
+    p = {"method": "dynamic", "path": "libjubatus_mecab_splitter.so", "function": "create",
+         "libmecab": lib, **params}
+    return DatumToFvConverter({"string_types": {"mecab": p},
+                               "string_rules": [{"key": "*", "type": "mecab", "sample_weight": "tf",
+                                                 "global_weight": "bin"}]})
+
+
+def test_mecab_splitter_surface_base_ngram_filters(fake_mecab):
+    text = "Tokyo is  running fast !"
+    fv = dict(_mecab_conv(fake_mecab).convert(Datum({"t": text})))
+    assert fv == {f"t${w}@mecab#tf/bin": 1.0 for w in ("Tokyo", "is", "running", "fast", "!")}
+    # base form (7th CSV field; the surface where it is "*"), bigrams
+    fv = dict(_mecab_conv(fake_mecab, base="true", ngram="2").convert(Datum({"t": text})))
+    assert fv == {f"t${w}@mecab#tf/bin": 1.0 for w in ("tokyo,is", "is,runn", "runn,fast", "fast,!")}
+    # include nouns and verbs, exclude a feature by regex
+    conv = _mecab_conv(fake_mecab, include_features="名詞*|動詞*", exclude_features="/,fast$/")
+    fv = dict(conv.convert(Datum({"t": text})))
+    assert fv == {f"t${w}@mecab#tf/bin": 1.0 for w in ("Tokyo", "is", "running")}
+    # fewer words than n: no feature
+    assert dict(_mecab_conv(fake_mecab, ngram="9").convert(Datum({"t": text}))) == {}
+
+
+def test_mecab_splitter_token_spans(fake_mecab):
+    from jubatus_amd.fv_converter.plugin import PluginLoader
+    split = PluginLoader().create("string_feature", {
+        "path": "libjubatus_mecab_splitter.so", "function": "create", "libmecab": fake_mecab,
+        "ngram": "2"})
+    assert split("a  bb ccc") == ["a,bb", "bb,ccc"]
+
+
+def test_mecab_splitter_errors(fake_mecab):
+    from jubatus_amd.fv_converter.plugin import PluginLoader
+    base = {"path": "libjubatus_mecab_splitter.so", "function": "create"}
+    for bad in ({"ngram": "0", "libmecab": fake_mecab}, {"base": "yes", "libmecab": fake_mecab},
+                {"include_features": "", "libmecab": fake_mecab},
+                {"arg": "--fail", "libmecab": fake_mecab},        # tagger creation fails
+                {"libmecab": "/nonexistent/libmecab.so.2"}):      # MeCab not installed
+        with pytest.raises(PluginError):
+            PluginLoader().create("string_feature", {**base, **bad})
