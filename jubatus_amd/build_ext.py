@@ -129,21 +129,26 @@ TOOLS = {
 }
 
 
-def build_tools(force: bool = False, nproc: int = 8) -> str:
-    """Python-free native executables (the coordinator)."""
-    os.makedirs(NATIVE_BIN, exist_ok=True)
+def build_tools(force: bool = False, nproc: int = 8, sanitize: str | None = None) -> str:
+    """Python-free native executables (coordinator, proxy). ``sanitize``
+    ("address", "thread", "undefined") builds instrumented copies into
+    native_bin/<sanitizer>/ (the reference's --fsanitize build option,
+    wscript:55-57,143-146; host code only)."""
+    out = os.path.join(NATIVE_BIN, sanitize) if sanitize else NATIVE_BIN
+    os.makedirs(out, exist_ok=True)
+    opt = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={sanitize}"] if sanitize else ["-O2"]
     jobs = []
     for name, (srcs, incs) in TOOLS.items():
-        target = os.path.join(NATIVE_BIN, name)
+        target = os.path.join(out, name)
         paths = [os.path.join(CSRC, x) for x in srcs]
         deps = paths + [h for d in incs for h in glob.glob(os.path.join(CSRC, d, "**", "*.h*"),
                                                             recursive=True)]
         if force or _newer(target, deps):
-            jobs.append((target, ["g++", "-O2", "-std=c++17", "-pthread", "-Wall",
+            jobs.append((target, ["g++", *opt, "-std=c++17", "-pthread", "-Wall",
                                   *[f"-I{os.path.join(CSRC, d)}" for d in incs], *paths,
                                   "-o", target]))
     _compile_all(jobs, nproc)
-    return NATIVE_BIN
+    return out
 
 
 def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, ...]:
@@ -156,7 +161,11 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--sanitize", choices=("address", "thread", "undefined"), default=None,
+                    help="also build sanitizer-instrumented native executables")
     a = ap.parse_args()
+    if a.sanitize:
+        print(build_tools(a.force, a.j or 8, a.sanitize))
     for p in build_all(a.force, a.j):
         print(p)
 

@@ -72,12 +72,15 @@ class NativeCoordinator:
     """The native coordinator (csrc/coord/jubacoordinator.cpp) as a child
     process: same RPC surface as CoordinatorServer, no Python in the server."""
 
-    def __init__(self, port: int = 0, bind: str = "127.0.0.1", nthreads: int = 4):
-        if not native_available():
+    def __init__(self, port: int = 0, bind: str = "127.0.0.1", nthreads: int = 4,
+                 exe: str | None = None, env: dict | None = None, stderr=None):
+        if exe is None and not native_available():
             from .. import build_ext
             build_ext.build_tools()
-        self.proc = subprocess.Popen([NATIVE_BIN, "-p", str(port), "-b", bind, "-c", str(nthreads)],
-                                     stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        self.proc = subprocess.Popen([exe or NATIVE_BIN, "-p", str(port), "-b", bind, "-c",
+                                      str(nthreads)], stdout=subprocess.PIPE,
+                                     stderr=stderr if stderr is not None else subprocess.DEVNULL,
+                                     text=True, env=env)
         line = self.proc.stdout.readline()
         if not line.startswith("jubacoordinator ready"):
             self.proc.kill()
@@ -87,14 +90,15 @@ class NativeCoordinator:
     def start(self) -> "NativeCoordinator":
         return self
 
-    def stop(self) -> None:
+    def stop(self) -> int:
         if self.proc.poll() is None:
             self.proc.terminate()
             try:
-                self.proc.wait(5)
+                self.proc.wait(15)
             except subprocess.TimeoutExpired:
                 self.proc.kill()
                 self.proc.wait()
+        return self.proc.returncode
 
 
 def main(argv: list[str] | None = None) -> int:

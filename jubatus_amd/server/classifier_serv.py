@@ -17,6 +17,7 @@ import math
 from ..common.exceptions import ArgumentError, ConfigNotSet
 from ..common.mprpc import split_params
 from ..framework.device import select_device
+from ..framework.batching import MicroBatcher, msgpack_array_len
 from ..framework.server_base import ServerBase
 from ..fv_converter.converter import DatumToFvConverter
 from ..fv_converter.datum import Datum
@@ -60,6 +61,7 @@ class ClassifierServ(ServerBase):
         super().__init__(argv, coord)
         self.clf = None
         self.config = None
+        self._train_batcher = self._classify_batcher = None
         self.device = select_device(argv)
 
     def check_set_config(self) -> None:
@@ -70,6 +72,24 @@ class ClassifierServ(ServerBase):
     def set_config(self, config: str) -> None:
         cfg = json.loads(config)
         self.clf = build_classifier(cfg, self.device)
+        self._train_batcher = self._classify_batcher = None
+        if getattr(self.clf, "gpu", False) and hasattr(self.clf, "train_requests"):
+            clf = self.clf
+
+            def train_many(bodies):
+                clf.train_requests(list(bodies))       # one launch, one stream per request
+                return [max(0, msgpack_array_len(b)) for b in bodies]
+
+            def classify_many(bodies):
+                flat = clf.classify_requests(list(bodies))
+                out, k = [], 0
+                for b in bodies:
+                    n = max(0, msgpack_array_len(b))
+                    out.append(flat[k:k + n])
+                    k += n
+                return out
+            self._train_batcher = MicroBatcher(train_many)
+            self._classify_batcher = MicroBatcher(classify_many)
         self.config = config
         if self.mixer is not None:
             self.mixer.set_driver(self.clf)
@@ -102,6 +122,11 @@ class ClassifierServ(ServerBase):
         if len(parts) != 2:
             raise ArgumentError("train: expected 2 arguments")
         self._bump()
+        if self._train_batcher is not None:
+            try:
+                return self._train_batcher.submit(parts[1])
+            except TypeError as e:
+                raise ArgumentError(str(e)) from e
         if hasattr(self.clf, "train_requests"):
             try:
                 return self.clf.train_requests([parts[1]])
@@ -140,7 +165,8 @@ class ClassifierServ(ServerBase):
         if len(parts) != 2:
             raise ArgumentError("classify: expected 2 arguments")
         try:
-            res = self.clf.classify_requests([parts[1]])
+            res = self._classify_batcher.submit(parts[1]) if self._classify_batcher is not None \
+                else self.clf.classify_requests([parts[1]])
         except TypeError as e:
             raise ArgumentError(str(e)) from e
         for row in res:
@@ -177,3 +203,7 @@ class ClassifierServ(ServerBase):
             import torch
             status["device"] = str(self.device)
             status["hbm_allocated_bytes"] = str(torch.cuda.memory_allocated(self.device))
+        for k, b in (("train", self._train_batcher), ("classify", self._classify_batcher)):
+            if b is not None:
+                status[f"batching.{k}.calls"] = str(b.calls)
+                status[f"batching.{k}.launches"] = str(b.batches)
