@@ -57,6 +57,34 @@ def wait_port(port, timeout=120):
     return False
 
 
+def _client_proc(args):
+    """one load-generating client process: pre-encoded train RPCs for `secs`"""
+    port, name, body, secs, per = args
+    sys.path.insert(0, ROOT)
+    from jubatus_amd.common.mprpc import RpcClient
+    c = RpcClient("127.0.0.1", port, 60)
+    n = 0
+    t_end = time.time() + secs
+    while time.time() < t_end:
+        assert c.call_raw("train", body) == per
+        n += per
+    c.close()
+    return n
+
+
+def concurrent_train(port, name, enc_train, nproc=16, secs=4.0):
+    """samples/s of the server under nproc concurrent clients (the server's
+    micro-batcher merges their train RPCs into shared launches)"""
+    import multiprocessing as mp
+    from jubatus_amd.common.mprpc import packb
+    body = packb([name, enc_train])
+    with mp.get_context("spawn").Pool(nproc) as pool:
+        t0 = time.time()
+        counts = pool.map(_client_proc, [(port, name, body, secs, len(enc_train))] * nproc)
+        dt = time.time() - t0
+    return round(sum(counts) / dt, 1)
+
+
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 500
     from jubatus_amd import build_ext
@@ -96,7 +124,7 @@ def main():
         # standalone server, client -> server
         sp = free_port()
         procs.append(subprocess.Popen([sys.executable, "-m", "jubatus_amd.cmd.server", "classifier",
-                                       "-p", str(sp), "-b", "127.0.0.1", "-f", cfg, "-d", tmp],
+                                       "-p", str(sp), "-b", "127.0.0.1", "-f", cfg, "-d", tmp, "-c", "16"],
                                       env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
         assert wait_port(sp), "server did not start"
         c = Classifier("127.0.0.1", sp, "", timeout=30)
@@ -110,6 +138,7 @@ def main():
         out["direct_train_128"] = lat(lambda: rc.call_raw("train", p_train("")), iters // 5)
         out["direct_classify_1"] = lat(lambda: rc.call_raw("classify", p_one("")), iters)
         rc.close()
+        out["direct_concurrent_train_samples_per_s"] = concurrent_train(sp, "", enc_train)
         # distributed: native coordinator + server + native proxy
         coord = NativeCoordinator(0, "127.0.0.1")
         ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
