@@ -126,6 +126,7 @@ TOOLS = {
                         ["coord", "native", "../client_cpp/include"]),
     "jubaproxy": (["proxy/jubaproxy.cpp", "native/jb_rpc.cpp"],
                   ["proxy", "native", "../client_cpp/include"]),
+    "jubaloadgen": (["tools/jubaloadgen.cpp", "native/jb_rpc.cpp"], ["native"]),
 }
 
 

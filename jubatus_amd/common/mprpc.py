@@ -114,12 +114,71 @@ class RpcServer:
 
     def __init__(self, nthreads: int = 2, idle_timeout: float = 0.0):
         self._methods: dict[str, _Method] = {}
+        self._batch: dict[str, Callable] = {}
         self._srv = native().RpcServer(self._dispatch, nthreads, idle_timeout)
         self.port: int | None = None
         self.on_request: Callable[[str], None] | None = None
 
     def add(self, name: str, fn: Callable, arity: int | None = None, raw: bool = False) -> None:
         self._methods[name] = _Method(fn, arity, raw)
+
+    def add_batch(self, name: str, fn: Callable[[list], list]) -> None:
+        """Transport-level batching: every queued request of ``name`` is
+        served by ONE call ``fn(list of params bytes) -> list of results``
+        (a result may be an Exception: ArgumentError -> ARGUMENT_ERROR,
+        others -> message string). Register before start()."""
+        self._batch[name] = fn
+        self._srv.set_batch(sorted(self._batch), self._dispatch_batch)
+
+    def batches(self) -> int:
+        return self._srv.batches()
+
+    def _dispatch_batch(self, method: str, params: list, msgids: list) -> list:
+        fn = self._batch[method]
+        if self.on_request is not None:
+            for _ in params:
+                try:
+                    self.on_request(method)
+                except Exception:  # noqa: BLE001
+                    pass
+        # per-request fault injection (utils/fault.py): drop -> no reply,
+        # error -> that request fails; the others are served
+        keep, pre = [], {}
+        for i in range(len(params)):
+            try:
+                if fault.on_rpc(method) == "drop":
+                    pre[i] = None
+                    continue
+            except Exception as e:  # noqa: BLE001
+                pre[i] = e
+                continue
+            keep.append(i)
+        t0 = time.perf_counter_ns()
+        try:
+            got = list(fn([params[i] for i in keep])) if keep else []
+        except Exception as e:  # noqa: BLE001 - the whole batch failed
+            got = [e] * len(keep)
+        trace.record("rpc." + method, time.perf_counter_ns() - t0)
+        results = [None] * len(params)
+        for i, r in zip(keep, got):
+            results[i] = r
+        out = []
+        for i, (mid, r) in enumerate(zip(msgids, results)):
+            if i in pre:
+                r = pre[i]
+                if r is None:
+                    out.append(None)
+                    continue
+            if isinstance(r, ArgumentError):
+                out.append(packb([RESPONSE, mid, ARGUMENT_ERROR, None]))
+            elif isinstance(r, Exception):
+                out.append(packb([RESPONSE, mid, str(r) or type(r).__name__, None]))
+            else:
+                try:
+                    out.append(packb([RESPONSE, mid, None, r]))
+                except Exception as e:  # noqa: BLE001
+                    out.append(packb([RESPONSE, mid, f"failed to encode result: {e}", None]))
+        return out
 
     def remove(self, name: str) -> None:
         self._methods.pop(name, None)

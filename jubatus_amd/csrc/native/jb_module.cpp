@@ -109,6 +109,44 @@ class PyRpcServer {
     py::gil_scoped_release nogil;
     srv_.reset();
   }
+  // fn(method: str, params: list[bytes], msgids: list[int]) -> list[bytes | None]
+  void set_batch(std::vector<std::string> methods, py::object fn, size_t max_batch) {
+    batch_fn_ = std::move(fn);
+    srv_->set_batch(
+        methods,
+        [this](const std::string& method, std::vector<jb::RpcRequest>& reqs) {
+          std::vector<std::string> out(reqs.size());
+          py::gil_scoped_acquire gil;
+          try {
+            py::list params, ids;
+            for (auto& r : reqs) {
+              params.append(py::bytes(r.params));
+              ids.append(r.msgid);
+            }
+            py::list res = batch_fn_(py::str(method), params, ids);
+            for (size_t i = 0; i < reqs.size() && i < (size_t)py::len(res); ++i)
+              if (!res[i].is_none()) out[i] = res[i].cast<std::string>();
+          } catch (py::error_already_set& e) {
+            // every request of the batch gets the error string
+            std::string what = e.what();
+            if (what.size() > 255) what.resize(255);
+            for (size_t i = 0; i < reqs.size(); ++i) {
+              std::string& o = out[i];
+              o.push_back((char)0x94);
+              o.push_back((char)0x01);
+              o.push_back((char)0xce);
+              for (int k = 3; k >= 0; --k) o.push_back((char)((reqs[i].msgid >> (8 * k)) & 0xff));
+              o.push_back((char)0xd9);
+              o.push_back((char)what.size());
+              o += what;
+              o.push_back((char)0xc0);
+            }
+          }
+          return out;
+        },
+        max_batch);
+  }
+  uint64_t batches() const { return srv_->batches(); }
   int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
   void start() { srv_->start(); }
   void stop() {
@@ -121,6 +159,7 @@ class PyRpcServer {
 
  private:
   py::object handler_;
+  py::object batch_fn_;
   std::unique_ptr<jb::RpcServer> srv_;
 };
 
@@ -180,6 +219,9 @@ PYBIND11_MODULE(_jubatus_native, m) {
   py::class_<PyRpcServer>(m, "RpcServer")
       .def(py::init<py::object, int, double>(), py::arg("handler"), py::arg("nworkers") = 2,
            py::arg("idle_timeout") = 0.0)
+      .def("set_batch", &PyRpcServer::set_batch, py::arg("methods"), py::arg("fn"),
+           py::arg("max_batch") = 4096)
+      .def("batches", &PyRpcServer::batches)
       .def("listen", &PyRpcServer::listen)
       .def("start", &PyRpcServer::start)
       .def("stop", &PyRpcServer::stop)

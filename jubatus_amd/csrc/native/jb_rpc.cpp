@@ -105,6 +105,55 @@ RpcServer::RpcServer(Handler h, int nworkers, double idle_timeout_sec)
 
 RpcServer::~RpcServer() { stop(); }
 
+void RpcServer::set_batch(const std::vector<std::string>& methods, BatchHandler h,
+                          size_t max_batch) {
+  batch_methods_ = methods;
+  batch_handler_ = std::move(h);
+  max_batch_ = max_batch ? max_batch : 1;
+}
+
+void RpcServer::enqueue(RpcRequest&& req) {
+  for (const auto& m : batch_methods_)
+    if (m == req.method) {
+      std::lock_guard<std::mutex> g(bmu_);
+      bqueue_.push_back(std::move(req));
+      bcv_.notify_one();
+      return;
+    }
+  std::lock_guard<std::mutex> g(qmu_);
+  queue_.push_back(std::move(req));
+  qlen_.store(queue_.size(), std::memory_order_relaxed);
+  qcv_.notify_one();
+}
+
+// Drain every queued request of the method at the head of the batch queue
+// and serve them with one handler call; requests arriving meanwhile form
+// the next (larger) batch - adaptive batching without a timer.
+void RpcServer::batch_loop() {
+  for (;;) {
+    std::vector<RpcRequest> batch;
+    {
+      std::unique_lock<std::mutex> g(bmu_);
+      bcv_.wait(g, [this] { return !bqueue_.empty() || !running_.load(); });
+      if (!running_.load()) return;
+      const std::string method = bqueue_.front().method;
+      for (auto it = bqueue_.begin(); it != bqueue_.end() && batch.size() < max_batch_;) {
+        if (it->method == method) {
+          batch.push_back(std::move(*it));
+          it = bqueue_.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    std::vector<std::string> resp = batch_handler_(batch[0].method, batch);
+    batches_.fetch_add(1);
+    served_.fetch_add(batch.size());
+    for (size_t i = 0; i < batch.size() && i < resp.size(); ++i)
+      if (!batch[i].notify && !resp[i].empty()) send_response(batch[i].conn_id, resp[i]);
+  }
+}
+
 int RpcServer::listen(const std::string& addr, int port) {
   listen_fd_ = socket(AF_INET, SOCK_STREAM, 0);
   if (listen_fd_ < 0) throw std::runtime_error("socket() failed");
@@ -142,6 +191,7 @@ void RpcServer::start() {
   running_.store(true);
   io_ = std::thread([this] { io_loop(); });
   for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker_loop(); });
+  if (batch_handler_) batcher_ = std::thread([this] { batch_loop(); });
 }
 
 void RpcServer::stop() {
@@ -149,7 +199,12 @@ void RpcServer::stop() {
   uint64_t one = 1;
   if (wake_fd_ >= 0) { ssize_t r = write(wake_fd_, &one, 8); (void)r; }
   qcv_.notify_all();
+  {
+    std::lock_guard<std::mutex> g(bmu_);
+    bcv_.notify_all();
+  }
   if (io_.joinable()) io_.join();
+  if (batcher_.joinable()) batcher_.join();
   for (auto& w : workers_) if (w.joinable()) w.join();
   workers_.clear();
   {
@@ -303,22 +358,14 @@ void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
     if (ok && n == 4 && type == 0) {
       ok = cur.number(&msgid) && cur.raw(&m, &mlen);
       if (ok) {
-        RpcRequest req{c->id, (uint32_t)msgid, false, std::string((const char*)m, mlen),
-                       std::string((const char*)cur.p, (size_t)(p + len - cur.p))};
-        std::lock_guard<std::mutex> g(qmu_);
-        queue_.push_back(std::move(req));
-        qlen_.store(queue_.size(), std::memory_order_relaxed);
-        qcv_.notify_one();
+        enqueue(RpcRequest{c->id, (uint32_t)msgid, false, std::string((const char*)m, mlen),
+                           std::string((const char*)cur.p, (size_t)(p + len - cur.p))});
       }
     } else if (ok && n == 3 && type == 2) {
       ok = cur.raw(&m, &mlen);
       if (ok) {
-        RpcRequest req{c->id, 0, true, std::string((const char*)m, mlen),
-                       std::string((const char*)cur.p, (size_t)(p + len - cur.p))};
-        std::lock_guard<std::mutex> g(qmu_);
-        queue_.push_back(std::move(req));
-        qlen_.store(queue_.size(), std::memory_order_relaxed);
-        qcv_.notify_one();
+        enqueue(RpcRequest{c->id, 0, true, std::string((const char*)m, mlen),
+                           std::string((const char*)cur.p, (size_t)(p + len - cur.p))});
       }
     }
     // responses (type 1) sent to a server are ignored

@@ -42,7 +42,17 @@ class RpcServer {
   // handler(request) -> encoded response bytes (empty for notifications)
   using Handler = std::function<std::string(const RpcRequest&)>;
 
+  // batch handler(method, requests) -> one encoded response per request
+  // (empty string: no response, e.g. a notification)
+  using BatchHandler =
+      std::function<std::vector<std::string>(const std::string&, std::vector<RpcRequest>&)>;
+
   RpcServer(Handler h, int nworkers, double idle_timeout_sec);
+  // Requests of `methods` bypass the per-request workers: one batch thread
+  // drains everything queued for a method and calls `h` once for all of it
+  // (concurrent train / classify RPCs become one GPU launch). Call before start().
+  void set_batch(const std::vector<std::string>& methods, BatchHandler h, size_t max_batch);
+  uint64_t batches() const { return batches_.load(); }
   ~RpcServer();
   // returns the bound port (useful with port 0)
   int listen(const std::string& addr, int port);
@@ -69,6 +79,8 @@ class RpcServer {
   void flush(const std::shared_ptr<Conn>& c);
   void close_conn(uint64_t id);
   void send_response(uint64_t conn_id, const std::string& bytes);
+  void batch_loop();
+  void enqueue(RpcRequest&& req);
 
   Handler handler_;
   int nworkers_;
@@ -88,6 +100,15 @@ class RpcServer {
   std::condition_variable qcv_;
   std::deque<RpcRequest> queue_;
   std::atomic<size_t> qlen_{0};   // queue_.size(), readable without qmu_
+  // batched methods
+  std::vector<std::string> batch_methods_;
+  BatchHandler batch_handler_;
+  size_t max_batch_ = 4096;
+  std::mutex bmu_;
+  std::condition_variable bcv_;
+  std::deque<RpcRequest> bqueue_;
+  std::thread batcher_;
+  std::atomic<uint64_t> batches_{0};
   std::mutex wq_mu_;
   std::vector<uint64_t> want_write_;  // conns the IO thread must arm for EPOLLOUT
 };

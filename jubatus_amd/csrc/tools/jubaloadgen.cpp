@@ -1,0 +1,166 @@
+// jubaloadgen: native msgpack-RPC load generator (benchmarks of the servers'
+// request path without a Python client in the way).
+//
+// Sends one pre-encoded request (params = a msgpack array read from a file,
+// e.g. ["", [[label, datum]...]] for train) on C connections, each keeping
+// D requests in flight, for T seconds; prints one JSON line with the request
+// rate and the per-request latency distribution. Any error response aborts.
+//
+// Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/tcp.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "jb_msgpack.hpp"
+#include "jb_rpc.hpp"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+std::string request_bytes(uint32_t msgid, const std::string& method, const std::string& params) {
+  std::string o;
+  o.push_back((char)0x94);
+  o.push_back((char)0x00);
+  o.push_back((char)0xce);
+  for (int k = 3; k >= 0; --k) o.push_back((char)((msgid >> (8 * k)) & 0xff));
+  const size_t n = method.size();
+  if (n < 32) o.push_back((char)(0xa0 | n));
+  else { o.push_back((char)0xda); o.push_back((char)(n >> 8)); o.push_back((char)n); }
+  o += method;
+  o += params;
+  return o;
+}
+
+int connect_to(const std::string& host, int port) {
+  addrinfo hints{}, *ai = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &ai) != 0) return -1;
+  int fd = socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0 || connect(fd, ai->ai_addr, ai->ai_addrlen) != 0) {
+    freeaddrinfo(ai);
+    if (fd >= 0) close(fd);
+    return -1;
+  }
+  freeaddrinfo(ai);
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  return fd;
+}
+
+struct Result {
+  uint64_t done = 0;
+  std::vector<double> lat_us;
+  std::string error;
+};
+
+void run_conn(const std::string& host, int port, const std::string& method, const std::string& params,
+              int depth, double secs, Result* r) {
+  const int fd = connect_to(host, port);
+  if (fd < 0) { r->error = "connect failed"; return; }
+  std::vector<Clock::time_point> sent(1 << 16);
+  uint32_t next = 1;
+  int inflight = 0;
+  std::string rbuf;
+  const auto t_end = Clock::now() + std::chrono::duration<double>(secs);
+  bool sending = true;
+  char buf[1 << 16];
+  while (sending || inflight > 0) {
+    while (sending && inflight < depth) {
+      if (Clock::now() >= t_end) { sending = false; break; }
+      const std::string req = request_bytes(next, method, params);
+      sent[next & 0xffff] = Clock::now();
+      size_t off = 0;
+      while (off < req.size()) {
+        ssize_t w = send(fd, req.data() + off, req.size() - off, MSG_NOSIGNAL);
+        if (w <= 0) { r->error = "send failed"; close(fd); return; }
+        off += (size_t)w;
+      }
+      ++next;
+      ++inflight;
+    }
+    if (inflight == 0) break;
+    ssize_t k = recv(fd, buf, sizeof buf, 0);
+    if (k <= 0) { r->error = "connection closed"; close(fd); return; }
+    rbuf.append(buf, (size_t)k);
+    for (;;) {
+      const int64_t f = jb::msgpack_frame((const uint8_t*)rbuf.data(), rbuf.size());
+      if (f < 0) { r->error = "malformed response"; close(fd); return; }
+      if (f == 0) break;
+      jb::Cursor c{(const uint8_t*)rbuf.data(), (const uint8_t*)rbuf.data() + f};
+      uint32_t n;
+      double type, id;
+      if (!c.array(&n) || n != 4 || !c.number(&type) || !c.number(&id)) { r->error = "bad response"; close(fd); return; }
+      if (*c.p != 0xc0) { r->error = "error response from server"; close(fd); return; }
+      const auto now = Clock::now();
+      r->lat_us.push_back(std::chrono::duration<double, std::micro>(now - sent[(uint32_t)id & 0xffff]).count());
+      ++r->done;
+      --inflight;
+      rbuf.erase(0, (size_t)f);
+    }
+  }
+  close(fd);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  std::string host = "127.0.0.1", method, file;
+  int port = 0, conns = 8, depth = 4;
+  double secs = 3.0;
+  for (int i = 1; i + 1 < argc; i += 2) {
+    const std::string a = argv[i], v = argv[i + 1];
+    if (a == "-H") host = v;
+    else if (a == "-p") port = atoi(v.c_str());
+    else if (a == "-m") method = v;
+    else if (a == "-f") file = v;
+    else if (a == "-c") conns = atoi(v.c_str());
+    else if (a == "-d") depth = atoi(v.c_str());
+    else if (a == "-t") secs = atof(v.c_str());
+    else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
+  }
+  if (!port || method.empty() || file.empty() || conns < 1 || depth < 1) {
+    fprintf(stderr, "usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]\n");
+    return 1;
+  }
+  std::ifstream ifs(file, std::ios::binary);
+  std::stringstream ss;
+  ss << ifs.rdbuf();
+  const std::string params = ss.str();
+  if (params.empty()) { fprintf(stderr, "empty params file\n"); return 1; }
+  std::vector<Result> res(conns);
+  std::vector<std::thread> ts;
+  const auto t0 = Clock::now();
+  for (int i = 0; i < conns; ++i)
+    ts.emplace_back(run_conn, host, port, method, params, depth, secs, &res[i]);
+  for (auto& t : ts) t.join();
+  const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
+  uint64_t done = 0;
+  std::vector<double> lat;
+  for (auto& r : res) {
+    if (!r.error.empty()) { fprintf(stderr, "jubaloadgen: %s\n", r.error.c_str()); return 2; }
+    done += r.done;
+    lat.insert(lat.end(), r.lat_us.begin(), r.lat_us.end());
+  }
+  std::sort(lat.begin(), lat.end());
+  auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[(size_t)(q * (lat.size() - 1))]; };
+  printf("{\"requests\": %llu, \"seconds\": %.3f, \"requests_per_s\": %.1f, \"connections\": %d, "
+         "\"depth\": %d, \"p50_us\": %.1f, \"p99_us\": %.1f}\n",
+         (unsigned long long)done, dt, done / dt, conns, depth, pct(0.5), pct(0.99));
+  return 0;
+}

@@ -106,6 +106,11 @@ class ServerHelper:
             raw = getattr(self.server, "raw_" + m.name, None)
             if raw is not None:  # zero-copy fast path (e.g. classifier train)
                 self.rpc.add(m.name, self._wrap_raw(m, raw), raw=True)
+        # transport-level batching: every queued request of a method, one call
+        batched = getattr(self.server, "batched_methods", lambda: {})()
+        for m in specs.methods(self.type):
+            if m.name in batched:
+                self.rpc.add_batch(m.name, self._wrap_batch(m, batched[m.name]))
 
     def _wrap_raw(self, m: specs.Method, fn: Callable) -> Callable:
         rw = self.server.rw_mutex
@@ -120,6 +125,22 @@ class ServerHelper:
                 with rw.read():
                     return fn(params)
             return fn(params)
+        return call
+
+    def _wrap_batch(self, m: specs.Method, fn: Callable) -> Callable:
+        rw = self.server.rw_mutex
+        srv = self.server
+
+        def call(params_list: list) -> list:
+            if m.lock == "update":
+                with rw.write():
+                    for _ in params_list:
+                        srv.event_model_updated()
+                    return fn(params_list)
+            if m.lock == "analysis":
+                with rw.read():
+                    return fn(params_list)
+            return fn(params_list)
         return call
 
     # -------------------------------------------------------- common RPCs

@@ -62,6 +62,7 @@ class ClassifierServ(ServerBase):
         self.clf = None
         self.config = None
         self._train_batcher = self._classify_batcher = None
+        self._batch_stats = {"train": [0, 0], "classify": [0, 0]}
         self.device = select_device(argv)
 
     def check_set_config(self) -> None:
@@ -175,6 +176,69 @@ class ClassifierServ(ServerBase):
                     log.warning("score is infinite: %s = %s", label, score)
         return res
 
+    # ------------------------------------------------ transport batching
+    def batched_methods(self) -> dict:
+        """GPU engines: concurrent train / classify RPCs are served in
+        batches by the transport (one GPU launch per batch)"""
+        if not (getattr(self.clf, "gpu", False) and hasattr(self.clf, "train_requests")):
+            return {}
+        return {"train": self.batch_train, "classify": self.batch_classify}
+
+    def _split_bodies(self, params_list: list, what: str):
+        bodies, idx, out = [], [], [None] * len(params_list)
+        for i, p in enumerate(params_list):
+            try:
+                parts = split_params(p)
+            except ArgumentError as e:
+                out[i] = e
+                continue
+            if len(parts) != 2:
+                out[i] = ArgumentError(f"{what}: expected 2 arguments")
+                continue
+            bodies.append(parts[1])
+            idx.append(i)
+        return bodies, idx, out
+
+    def batch_train(self, params_list: list) -> list:
+        self.check_set_config()
+        bodies, idx, out = self._split_bodies(params_list, "train")
+        with self.rw_mutex.write():
+            for _ in bodies:
+                self.event_model_updated()
+        self._batch_stats["train"][0] += len(bodies)
+        self._batch_stats["train"][1] += 1
+        try:
+            self.clf.train_requests(bodies)          # one launch, one stream per request
+            for i, b in zip(idx, bodies):
+                out[i] = max(0, msgpack_array_len(b))
+        except TypeError:
+            for i, b in zip(idx, bodies):            # isolate the malformed request(s)
+                try:
+                    out[i] = self.clf.train_requests([b])
+                except TypeError as e:
+                    out[i] = ArgumentError(str(e))
+        return out
+
+    def batch_classify(self, params_list: list) -> list:
+        self.check_set_config()
+        bodies, idx, out = self._split_bodies(params_list, "classify")
+        self._batch_stats["classify"][0] += len(bodies)
+        self._batch_stats["classify"][1] += 1
+        try:
+            flat = self.clf.classify_requests(bodies)
+            k = 0
+            for i, b in zip(idx, bodies):
+                n = max(0, msgpack_array_len(b))
+                out[i] = flat[k:k + n]
+                k += n
+        except TypeError:
+            for i, b in zip(idx, bodies):
+                try:
+                    out[i] = self.clf.classify_requests([b])
+                except TypeError as e:
+                    out[i] = ArgumentError(str(e))
+        return out
+
     def get_labels(self) -> dict:
         self.check_set_config()
         return self.clf.get_labels()
@@ -204,6 +268,9 @@ class ClassifierServ(ServerBase):
             status["device"] = str(self.device)
             status["hbm_allocated_bytes"] = str(torch.cuda.memory_allocated(self.device))
         for k, b in (("train", self._train_batcher), ("classify", self._classify_batcher)):
+            calls, launches = self._batch_stats[k]
             if b is not None:
-                status[f"batching.{k}.calls"] = str(b.calls)
-                status[f"batching.{k}.launches"] = str(b.batches)
+                calls, launches = calls + b.calls, launches + b.batches
+            if calls:
+                status[f"batching.{k}.calls"] = str(calls)
+                status[f"batching.{k}.launches"] = str(launches)

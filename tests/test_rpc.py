@@ -137,3 +137,56 @@ def test_split_params():
     b = msgpack.packb(["name", [[1, 2], "x"], 3.5])
     parts = mprpc.split_params(b)
     assert [msgpack.unpackb(bytes(p)) for p in parts] == ["name", [[1, 2], "x"], 3.5]
+
+
+def test_transport_batching_merges_concurrent_requests():
+    """RpcServer.add_batch: queued requests of a method are served by one
+    call; per-request results / ArgumentError / exceptions are routed back"""
+    import threading
+    import time as _t
+
+    from jubatus_amd.common.mprpc import ArgumentError, RpcCallError, RpcClient, RpcServer, RpcTypeError
+
+    sizes = []
+
+    def batch(params_list):
+        sizes.append(len(params_list))
+        _t.sleep(0.005)
+        out = []
+        for p in params_list:
+            (x,) = msgpack.unpackb(p)
+            out.append(ArgumentError("neg") if x < 0 else (RuntimeError("boom") if x == 13 else x * 2))
+        return out
+
+    srv = RpcServer(nthreads=2)
+    srv.add("double", lambda x: x * 2, 1)        # per-request path is shadowed by the batch
+    srv.add_batch("double", batch)
+    port = srv.listen(0, "127.0.0.1")
+    srv.start()
+    try:
+        res, errs = {}, {}
+
+        def client(i):
+            c = RpcClient("127.0.0.1", port, 10)
+            for j in range(10):
+                x = i * 100 + j
+                try:
+                    res[x] = c.call("double", x)
+                except Exception as e:  # noqa: BLE001
+                    errs[x] = e
+            c.close()
+        ts = [threading.Thread(target=client, args=(i,)) for i in range(12)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs and res == {x: 2 * x for x in res} and len(res) == 120
+        assert sum(sizes) == 120 and srv.batches() < 120
+        c = RpcClient("127.0.0.1", port, 10)
+        with pytest.raises(RpcTypeError):
+            c.call("double", -1)
+        with pytest.raises(RpcCallError):
+            c.call("double", 13)
+        c.close()
+    finally:
+        srv.stop()

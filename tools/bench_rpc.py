@@ -85,6 +85,24 @@ def concurrent_train(port, name, enc_train, nproc=16, secs=4.0):
     return round(sum(counts) / dt, 1)
 
 
+def loadgen(port, method, params, per, conns=16, depth=4, secs=4.0):
+    """native load generator (csrc/tools/jubaloadgen.cpp): `conns` connections
+    x `depth` requests in flight; the server batches them per launch"""
+    from jubatus_amd import build_ext
+    f = tempfile.NamedTemporaryFile(delete=False, suffix=".bin")
+    f.write(params)
+    f.close()
+    r = subprocess.run([os.path.join(build_ext.NATIVE_BIN, "jubaloadgen"), "-p", str(port), "-m", method,
+                        "-f", f.name, "-c", str(conns), "-d", str(depth), "-t", str(secs)],
+                       capture_output=True, text=True, timeout=secs + 60)
+    os.unlink(f.name)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()}
+    d = json.loads(r.stdout)
+    d["samples_per_s"] = round(d["requests_per_s"] * per, 1)
+    return d
+
+
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 500
     from jubatus_amd import build_ext
@@ -138,7 +156,9 @@ def main():
         out["direct_train_128"] = lat(lambda: rc.call_raw("train", p_train("")), iters // 5)
         out["direct_classify_1"] = lat(lambda: rc.call_raw("classify", p_one("")), iters)
         rc.close()
-        out["direct_concurrent_train_samples_per_s"] = concurrent_train(sp, "", enc_train)
+        out["direct_concurrent_train_samples_per_s_py_clients"] = concurrent_train(sp, "", enc_train)
+        out["direct_loadgen_train"] = loadgen(sp, "train", p_train(""), len(enc_train))
+        out["direct_loadgen_classify_1"] = loadgen(sp, "classify", p_one(""), 1, conns=8, depth=1)
         # distributed: native coordinator + server + native proxy
         coord = NativeCoordinator(0, "127.0.0.1")
         ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
