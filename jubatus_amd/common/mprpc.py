@@ -112,10 +112,12 @@ class RpcServer:
     (csrc/native/jb_rpc.cpp). ``raw`` methods receive the undecoded params
     bytes (the train/classify fast path hands them to the GPU scanner)."""
 
-    def __init__(self, nthreads: int = 2, idle_timeout: float = 0.0):
+    def __init__(self, nthreads: int = 2, idle_timeout: float = 0.0, io_threads: int | None = None):
         self._methods: dict[str, _Method] = {}
         self._batch: dict[str, Callable] = {}
         self._srv = native().RpcServer(self._dispatch, nthreads, idle_timeout)
+        # epoll IO threads (request framing): one per 4 workers
+        self._srv.set_io_threads(io_threads or max(1, nthreads // 4))
         self.port: int | None = None
         self.on_request: Callable[[str], None] | None = None
 

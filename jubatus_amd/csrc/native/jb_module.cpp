@@ -147,6 +147,7 @@ class PyRpcServer {
         max_batch);
   }
   uint64_t batches() const { return srv_->batches(); }
+  void set_io_threads(int n) { srv_->set_io_threads(n); }
   int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
   void start() { srv_->start(); }
   void stop() {
@@ -222,6 +223,7 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("set_batch", &PyRpcServer::set_batch, py::arg("methods"), py::arg("fn"),
            py::arg("max_batch") = 4096)
       .def("batches", &PyRpcServer::batches)
+      .def("set_io_threads", &PyRpcServer::set_io_threads)
       .def("listen", &PyRpcServer::listen)
       .def("start", &PyRpcServer::start)
       .def("stop", &PyRpcServer::stop)

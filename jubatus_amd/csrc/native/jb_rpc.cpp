@@ -180,16 +180,22 @@ int RpcServer::listen(const std::string& addr, int port) {
 
 void RpcServer::start() {
   if (listen_fd_ < 0) throw std::runtime_error("listen() first");
-  epfd_ = epoll_create1(0);
-  wake_fd_ = eventfd(0, EFD_NONBLOCK);
-  epoll_event ev{};
-  ev.events = EPOLLIN;
-  ev.data.u64 = 0;  // listen socket
-  epoll_ctl(epfd_, EPOLL_CTL_ADD, listen_fd_, &ev);
-  ev.data.u64 = UINT64_MAX;  // wakeup
-  epoll_ctl(epfd_, EPOLL_CTL_ADD, wake_fd_, &ev);
   running_.store(true);
-  io_ = std::thread([this] { io_loop(); });
+  for (int i = 0; i < nio_; ++i) {
+    std::unique_ptr<Loop> L(new Loop());
+    L->epfd = epoll_create1(0);
+    L->wake_fd = eventfd(0, EFD_NONBLOCK);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.u64 = UINT64_MAX;  // wakeup
+    epoll_ctl(L->epfd, EPOLL_CTL_ADD, L->wake_fd, &ev);
+    if (i == 0) {
+      ev.data.u64 = 0;  // listen socket lives in loop 0
+      epoll_ctl(L->epfd, EPOLL_CTL_ADD, listen_fd_, &ev);
+    }
+    loops_.push_back(std::move(L));
+  }
+  for (int i = 0; i < nio_; ++i) loops_[i]->th = std::thread([this, i] { io_loop(i); });
   for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker_loop(); });
   if (batch_handler_) batcher_ = std::thread([this] { batch_loop(); });
 }
@@ -197,13 +203,15 @@ void RpcServer::start() {
 void RpcServer::stop() {
   if (!running_.exchange(false)) return;
   uint64_t one = 1;
-  if (wake_fd_ >= 0) { ssize_t r = write(wake_fd_, &one, 8); (void)r; }
+  for (auto& L : loops_)
+    if (L->wake_fd >= 0) { ssize_t r = write(L->wake_fd, &one, 8); (void)r; }
   qcv_.notify_all();
   {
     std::lock_guard<std::mutex> g(bmu_);
     bcv_.notify_all();
   }
-  if (io_.joinable()) io_.join();
+  for (auto& L : loops_)
+    if (L->th.joinable()) L->th.join();
   if (batcher_.joinable()) batcher_.join();
   for (auto& w : workers_) if (w.joinable()) w.join();
   workers_.clear();
@@ -213,9 +221,12 @@ void RpcServer::stop() {
     conns_.clear();
   }
   if (listen_fd_ >= 0) ::close(listen_fd_);
-  if (epfd_ >= 0) ::close(epfd_);
-  if (wake_fd_ >= 0) ::close(wake_fd_);
-  listen_fd_ = epfd_ = wake_fd_ = -1;
+  for (auto& L : loops_) {
+    if (L->epfd >= 0) ::close(L->epfd);
+    if (L->wake_fd >= 0) ::close(L->wake_fd);
+  }
+  loops_.clear();
+  listen_fd_ = -1;
 }
 
 void RpcServer::close_conn(uint64_t id) {
@@ -231,26 +242,27 @@ void RpcServer::close_conn(uint64_t id) {
     std::lock_guard<std::mutex> g(c->wmu);
     c->closed = true;
   }
-  epoll_ctl(epfd_, EPOLL_CTL_DEL, c->fd, nullptr);
+  epoll_ctl(loops_[c->loop]->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
   ::close(c->fd);
   nconn_.fetch_sub(1);
 }
 
-void RpcServer::io_loop() {
+void RpcServer::io_loop(int li) {
+  Loop& L = *loops_[li];
   epoll_event evs[256];
   double last_sweep = now_sec();
   while (running_.load()) {
-    int n = epoll_wait(epfd_, evs, 256, 100);
+    int n = epoll_wait(L.epfd, evs, 256, 100);
     for (int i = 0; i < n; ++i) {
       const uint64_t key = evs[i].data.u64;
       if (key == UINT64_MAX) {
         uint64_t v;
-        ssize_t r = read(wake_fd_, &v, 8);
+        ssize_t r = read(L.wake_fd, &v, 8);
         (void)r;
         std::vector<uint64_t> ids;
         {
-          std::lock_guard<std::mutex> g(wq_mu_);
-          ids.swap(want_write_);
+          std::lock_guard<std::mutex> g(L.wq_mu);
+          ids.swap(L.want_write);
         }
         for (uint64_t id : ids) {
           std::shared_ptr<Conn> c;
@@ -263,7 +275,7 @@ void RpcServer::io_loop() {
           epoll_event ev{};
           ev.events = EPOLLIN | EPOLLOUT;
           ev.data.u64 = id;
-          epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+          epoll_ctl(L.epfd, EPOLL_CTL_MOD, c->fd, &ev);
         }
         continue;
       }
@@ -277,6 +289,7 @@ void RpcServer::io_loop() {
           auto c = std::make_shared<Conn>();
           c->fd = fd;
           c->last_active = now_sec();
+          c->loop = (int)(next_loop_.fetch_add(1) % (uint64_t)nio_);
           {
             std::lock_guard<std::mutex> g(cmu_);
             c->id = next_id_++;
@@ -286,7 +299,7 @@ void RpcServer::io_loop() {
           epoll_event ev{};
           ev.events = EPOLLIN;
           ev.data.u64 = c->id;
-          epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev);
+          epoll_ctl(loops_[c->loop]->epfd, EPOLL_CTL_ADD, fd, &ev);
         }
         continue;
       }
@@ -311,7 +324,7 @@ void RpcServer::io_loop() {
           epoll_event ev{};
           ev.events = EPOLLIN;
           ev.data.u64 = c->id;
-          epoll_ctl(epfd_, EPOLL_CTL_MOD, c->fd, &ev);
+          epoll_ctl(L.epfd, EPOLL_CTL_MOD, c->fd, &ev);
           c->want_write = false;
         }
       }
@@ -323,7 +336,8 @@ void RpcServer::io_loop() {
       {
         std::lock_guard<std::mutex> g(cmu_);
         for (auto& kv : conns_)
-          if (t - kv.second->last_active > idle_timeout_) idle.push_back(kv.first);
+          if (kv.second->loop == li && t - kv.second->last_active > idle_timeout_)
+            idle.push_back(kv.first);
       }
       for (uint64_t id : idle) close_conn(id);
     }
@@ -405,12 +419,13 @@ void RpcServer::send_response(uint64_t conn_id, const std::string& bytes) {
     if (!c->wbuf.empty() && !c->want_write) { c->want_write = true; arm = true; }
   }
   if (arm) {
+    Loop& L = *loops_[c->loop];
     {
-      std::lock_guard<std::mutex> g(wq_mu_);
-      want_write_.push_back(conn_id);
+      std::lock_guard<std::mutex> g(L.wq_mu);
+      L.want_write.push_back(conn_id);
     }
     uint64_t one = 1;
-    ssize_t r = write(wake_fd_, &one, 8);
+    ssize_t r = write(L.wake_fd, &one, 8);
     (void)r;
   }
 }

@@ -58,6 +58,9 @@ class RpcServer {
   int listen(const std::string& addr, int port);
   void start();
   void stop();
+  // number of epoll IO threads (connections are spread round-robin); call
+  // before start(). One thread frames ~1 GB/s of request bytes.
+  void set_io_threads(int n) { nio_ = n < 1 ? 1 : n; }
   bool running() const { return running_.load(); }
   uint64_t requests_served() const { return served_.load(); }
   uint64_t connections() const { return nconn_.load(); }
@@ -66,6 +69,7 @@ class RpcServer {
   struct Conn {
     int fd;
     uint64_t id;
+    int loop = 0;
     std::string rbuf;
     std::mutex wmu;
     std::string wbuf;  // pending output
@@ -73,7 +77,14 @@ class RpcServer {
     bool closed = false;
     double last_active = 0;
   };
-  void io_loop();
+  struct Loop {
+    int epfd = -1;
+    int wake_fd = -1;
+    std::thread th;
+    std::mutex wq_mu;
+    std::vector<uint64_t> want_write;  // conns this loop must arm for EPOLLOUT
+  };
+  void io_loop(int li);
   void worker_loop();
   void on_readable(const std::shared_ptr<Conn>& c);
   void flush(const std::shared_ptr<Conn>& c);
@@ -86,12 +97,12 @@ class RpcServer {
   int nworkers_;
   double idle_timeout_;
   int listen_fd_ = -1;
-  int epfd_ = -1;
-  int wake_fd_ = -1;
+  int nio_ = 1;
+  std::vector<std::unique_ptr<Loop>> loops_;
+  std::atomic<uint64_t> next_loop_{0};
   std::atomic<bool> running_{false};
   std::atomic<uint64_t> served_{0};
   std::atomic<uint64_t> nconn_{0};
-  std::thread io_;
   std::vector<std::thread> workers_;
   std::mutex cmu_;
   std::unordered_map<uint64_t, std::shared_ptr<Conn>> conns_;
@@ -109,8 +120,6 @@ class RpcServer {
   std::deque<RpcRequest> bqueue_;
   std::thread batcher_;
   std::atomic<uint64_t> batches_{0};
-  std::mutex wq_mu_;
-  std::vector<uint64_t> want_write_;  // conns the IO thread must arm for EPOLLOUT
 };
 
 // Frame one complete msgpack object at the head of [p, p+n): returns its

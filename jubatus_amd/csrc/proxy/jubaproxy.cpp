@@ -783,6 +783,7 @@ int main(int argc, char** argv) {
   }
   Proxy* px = proxy.get();
   jb::RpcServer srv([px](const jb::RpcRequest& r) { return px->handle(r); }, a.threads, 0.0);
+  srv.set_io_threads(a.threads >= 8 ? a.threads / 4 : 1);
   try {
     const int bound = srv.listen(a.bind_addr, a.port);
     a.port = bound;
