@@ -83,6 +83,13 @@ def main():
             clf.train_requests([body])
             torch.cuda.synchronize()
         res[f"train_1x{nsamp}_sync"] = timeit(tr, max(50, iters // 5))
+    for nreq in (16, 64):
+        bodies64 = [msgpack.packb([[lab, d] for lab, d in items[:128]], use_bin_type=False)] * nreq
+
+        def trn():
+            clf.train_requests(bodies64)
+            torch.cuda.synchronize()
+        res[f"train_{nreq}x128_sync"] = timeit(trn, 50)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     b = clf.pipe.from_requests([body], True, clf.labels)
     torch.cuda.synchronize()

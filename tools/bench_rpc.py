@@ -159,6 +159,12 @@ def main():
         out["direct_concurrent_train_samples_per_s_py_clients"] = concurrent_train(sp, "", enc_train)
         out["direct_loadgen_train"] = loadgen(sp, "train", p_train(""), len(enc_train))
         out["direct_loadgen_classify_1"] = loadgen(sp, "classify", p_one(""), 1, conns=8, depth=1)
+        rc = RpcClient("127.0.0.1", sp, 30)
+        (_, st), = rc.call("get_status", "").items()
+        out["server_spans"] = {k: v for k, v in st.items()
+                               if k.startswith(("trace.rpc.train", "trace.rpc.classify", "trace.hip.",
+                                                "batching."))}
+        rc.close()
         # distributed: native coordinator + server + native proxy
         coord = NativeCoordinator(0, "127.0.0.1")
         ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
