@@ -158,6 +158,9 @@ def main():
         rc.close()
         out["direct_concurrent_train_samples_per_s_py_clients"] = concurrent_train(sp, "", enc_train)
         out["direct_loadgen_train"] = loadgen(sp, "train", p_train(""), len(enc_train))
+        # 1024 requests in flight (the in-process bench's concurrency)
+        out["direct_loadgen_train_1024_inflight"] = loadgen(sp, "train", p_train(""), len(enc_train),
+                                                            conns=64, depth=16)
         out["direct_loadgen_classify_1"] = loadgen(sp, "classify", p_one(""), 1, conns=8, depth=1)
         rc = RpcClient("127.0.0.1", sp, 30)
         (_, st), = rc.call("get_status", "").items()
