@@ -21,6 +21,7 @@ DMA overlap the kernels of batch k. Events order everything:
 from __future__ import annotations
 
 import os
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -28,6 +29,7 @@ import torch
 
 from .._native import native
 from ..fv_converter.gpu_path import GpuRuleTable, gpu_eligible
+from ..utils import trace
 from . import hip
 
 
@@ -158,7 +160,9 @@ class FeaturePipeline:
         nat = native()
         pin = self._pinned[self._turn]
         self._turn ^= 1
+        t0 = time.perf_counter_ns()
         pin.wait()
+        trace.record("pipe.wait_pinned", time.perf_counter_ns() - t0)
         R = len(bodies)
         need_bytes = sum(memoryview(b).nbytes for b in bodies) + 16 * R + 16
         pin.ensure(need_bytes, max(1024, pin.cap_samples), R)

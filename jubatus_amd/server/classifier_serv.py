@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import json
 import math
+import time
 
 from ..common.exceptions import ArgumentError, ConfigNotSet
 from ..common.mprpc import split_params
@@ -22,7 +23,7 @@ from ..framework.server_base import ServerBase
 from ..fv_converter.converter import DatumToFvConverter
 from ..fv_converter.datum import Datum
 from ..models.classifier import LINEAR_METHODS, LinearClassifier
-from ..utils import logger
+from ..utils import logger, trace
 
 log = logger.get_logger("classifier")
 
@@ -201,14 +202,18 @@ class ClassifierServ(ServerBase):
 
     def batch_train(self, params_list: list) -> list:
         self.check_set_config()
+        t0 = time.perf_counter_ns()
         bodies, idx, out = self._split_bodies(params_list, "train")
         with self.rw_mutex.write():
             for _ in bodies:
                 self.event_model_updated()
+        trace.record("batch.train.split", time.perf_counter_ns() - t0)
         self._batch_stats["train"][0] += len(bodies)
         self._batch_stats["train"][1] += 1
         try:
+            t1 = time.perf_counter_ns()
             self.clf.train_requests(bodies)          # one launch, one stream per request
+            trace.record("batch.train.submit", time.perf_counter_ns() - t1)
             for i, b in zip(idx, bodies):
                 out[i] = max(0, msgpack_array_len(b))
         except TypeError:

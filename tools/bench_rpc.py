@@ -165,7 +165,8 @@ def main():
         rc = RpcClient("127.0.0.1", sp, 30)
         (_, st), = rc.call("get_status", "").items()
         out["server_spans"] = {k: v for k, v in st.items()
-                               if k.startswith(("trace.rpc.train", "trace.rpc.classify", "trace.hip.",
+                               if k.startswith(("trace.rpc.train", "trace.rpc.classify", "trace.hip.", "trace.batch.",
+                                                "trace.pipe.",
                                                 "batching."))}
         rc.close()
         # distributed: native coordinator + server + native proxy
