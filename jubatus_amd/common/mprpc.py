@@ -242,6 +242,30 @@ class RpcServer:
             return packb([RESPONSE, msgid, f"failed to encode result: {e}", None])
 
 
+def name_and_rest(params) -> memoryview:
+    """O(1) split of a 2-element params array [name: raw, data]: returns a
+    view of ``data`` (unvalidated - the consumer's native scanner validates
+    it). Raises ArgumentError unless params is a 2-array led by a raw."""
+    mv = memoryview(params).cast("B")
+    n = len(mv)
+    if n < 2 or mv[0] != 0x92:
+        raise ArgumentError("expected a 2-element params array")
+    t = mv[1]
+    if 0xA0 <= t <= 0xBF:
+        pos = 2 + (t & 0x1F)
+    elif t in (0xD9, 0xC4) and n >= 3:
+        pos = 3 + mv[2]
+    elif t in (0xDA, 0xC5) and n >= 4:
+        pos = 4 + ((mv[2] << 8) | mv[3])
+    elif t in (0xDB, 0xC6) and n >= 6:
+        pos = 6 + ((mv[2] << 24) | (mv[3] << 16) | (mv[4] << 8) | mv[5])
+    else:
+        raise ArgumentError("cluster name must be a string")
+    if pos >= n:
+        raise ArgumentError("truncated params")
+    return mv[pos:]
+
+
 def split_params(params: bytes) -> list[memoryview]:
     """Top-level elements of a params array as zero-copy views."""
     mv = memoryview(params)

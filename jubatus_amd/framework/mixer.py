@@ -22,7 +22,7 @@ class Mixer:
     def set_driver(self, driver) -> None: ...
     def start(self) -> None: ...
     def stop(self) -> None: ...
-    def updated(self) -> None: ...
+    def updated(self, n: int = 1) -> None: ...
     def get_status(self, status: dict[str, str]) -> None: ...
     def type(self) -> str: return "mixer"
     def do_mix(self) -> bool: return False
@@ -36,8 +36,8 @@ class DummyMixer(Mixer):
     def set_driver(self, driver) -> None:
         self.driver = driver
 
-    def updated(self) -> None:
-        self.count += 1
+    def updated(self, n: int = 1) -> None:
+        self.count += n
 
     def type(self) -> str:
         return "dummy_mixer"

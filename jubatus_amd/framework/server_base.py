@@ -121,10 +121,11 @@ class ServerBase:
         self.get_driver().clear()
         return True
 
-    def event_model_updated(self) -> None:
-        self.update_count += 1
+    def event_model_updated(self, n: int = 1) -> None:
+        """n updates (a batch of update RPCs counts each of them)"""
+        self.update_count += n
         if self.mixer is not None:
-            self.mixer.updated()
+            self.mixer.updated(n)
 
     def _local_path(self, model_id: str) -> str:
         a = self._argv

@@ -134,8 +134,7 @@ class ServerHelper:
         def call(params_list: list) -> list:
             if m.lock == "update":
                 with rw.write():
-                    for _ in params_list:
-                        srv.event_model_updated()
+                    srv.event_model_updated(len(params_list))
                     return fn(params_list)
             if m.lock == "analysis":
                 with rw.read():

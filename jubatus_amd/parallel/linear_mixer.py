@@ -98,9 +98,9 @@ class CollectiveMixer(Mixer):
         if self.group is not None:
             self.group.close()
 
-    def updated(self) -> None:
+    def updated(self, n: int = 1) -> None:
         with self._lock:
-            self.counter += 1
+            self.counter += n
             if 0 < self.argv.interval_count <= self.counter:
                 self._lock.notify_all()
 

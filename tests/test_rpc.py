@@ -190,3 +190,13 @@ def test_transport_batching_merges_concurrent_requests():
         c.close()
     finally:
         srv.stop()
+
+
+@pytest.mark.parametrize("name", ["", "c", "x" * 40, "y" * 300])
+def test_name_and_rest(name):
+    from jubatus_amd.common.mprpc import ArgumentError, name_and_rest
+    body = msgpack.packb([name, [[1, 2], "abc"]], use_bin_type=False)
+    assert msgpack.unpackb(bytes(name_and_rest(body))) == [[1, 2], "abc"]
+    for bad in (msgpack.packb([name]), msgpack.packb([1, 2]), msgpack.packb([name, 1, 2]), b""):
+        with pytest.raises(ArgumentError):
+            name_and_rest(bad)
