@@ -15,6 +15,7 @@
 // completion flag; the host spins on the flags (an empty launch + spin is
 // ~7 us on MI355X, a blocking stream sync adds ~5 us of interrupt wakeup).
 // Requests that do not fit take the batch path.
+#include "jb_host_wait.hpp"
 #include "jb_linear.hpp"
 
 #include <atomic>
@@ -90,25 +91,6 @@ __global__ __launch_bounds__(64) void classify_direct_kernel(const DirectArgs a,
 __global__ void empty_flag_kernel(volatile uint32_t* done, uint32_t seq) {
   __threadfence_system();
   if (threadIdx.x == 0) done[0] = seq;
-}
-
-// Spin on the per-datum completion flags; after ~2 ms fall back to a stream
-// sync, which also surfaces an asynchronous launch error.
-inline int wait_flags(volatile uint32_t* done, int n, uint32_t seq, hipStream_t stream) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < n;) {
-    if (done[i] == seq) { ++i; continue; }
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
-      return (int)hipStreamSynchronize(stream);
-    __builtin_ia32_pause();
-  }
-  std::atomic_thread_fence(std::memory_order_acquire);
-  return 0;
-}
-
-inline uint32_t next_seq() {
-  static std::atomic<uint32_t> g_seq{0};
-  return g_seq.fetch_add(1, std::memory_order_relaxed) + 1;
 }
 
 }  // namespace jb

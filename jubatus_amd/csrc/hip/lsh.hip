@@ -17,6 +17,9 @@
 // and over CSR rows (exact cosine / euclid for inverted_index), writing a
 // score per row; top-k selection then runs on the score vector.
 #include "jb_device.hpp"
+#include "jb_host_wait.hpp"
+
+#include <cstring>
 
 namespace jb {
 
@@ -38,16 +41,11 @@ __device__ __forceinline__ float gauss(uint64_t h) {
   return sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853f * u2);
 }
 
-// mode 0: sign-of-projection bits (lsh, euclid_lsh); 1: minhash bits
-__global__ __launch_bounds__(256) void signature_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
-    const float* __restrict__ fval, int n, int hash_num, uint64_t seed, int mode,
-    uint64_t* __restrict__ bits, float* __restrict__ norms) {
-  const int lane = threadIdx.x & 63;
-  const int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (s >= n) return;
-  const int64_t beg = row_ptr[s];
-  const int nf = (int)(row_ptr[s + 1] - beg);
+// Signature of one sample (one wave): mode 0 sign-of-projection bits (lsh,
+// euclid_lsh), 1 minhash bits; lane j owns bit j of each 64-bit word.
+__device__ __forceinline__ void signature_one(const int32_t* fidx, const float* fval, int64_t beg,
+                                              int nf, int hash_num, uint64_t seed, int mode,
+                                              uint64_t* __restrict__ bits, float* norm, int lane) {
   const int words = (hash_num + 63) / 64;
   float nrm = 0.f;
   for (int j = lane; j < nf; j += 64) {
@@ -78,10 +76,65 @@ __global__ __launch_bounds__(256) void signature_kernel(
     }
     if (j >= hash_num) bit = false;
     const uint64_t word = __ballot(bit);
-    if (lane == 0) bits[(int64_t)s * words + w] = word;
+    if (lane == 0) bits[w] = word;
   }
-  if (lane == 0 && norms != nullptr) norms[s] = sqrtf(nrm);
+  if (lane == 0 && norm != nullptr) *norm = sqrtf(nrm);
 }
+
+__global__ __launch_bounds__(256) void signature_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
+    const float* __restrict__ fval, int n, int hash_num, uint64_t seed, int mode,
+    uint64_t* __restrict__ bits, float* __restrict__ norms) {
+  const int lane = threadIdx.x & 63;
+  const int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (s >= n) return;
+  const int64_t beg = row_ptr[s];
+  const int words = (hash_num + 63) / 64;
+  signature_one(fidx, fval, beg, (int)(row_ptr[s + 1] - beg), hash_num, seed, mode,
+                bits + (int64_t)s * words, norms != nullptr ? norms + s : nullptr, lane);
+}
+
+// Query signatures from the kernel arguments (latency path: no H2D copy).
+constexpr int kQueryMax = 8;
+constexpr int kQuerySlots = 256;
+struct alignas(16) QueryArgs {
+  int32_t n;
+  int32_t slot[kQueryMax + 1];
+  int32_t pad[2];
+  int64_t dst[kQueryMax];   // destination row of each signature (-1: row q of the output)
+  int32_t idx[kQuerySlots];
+  float val[kQuerySlots];
+};
+
+// valid != nullptr: the rows are table slots (set_row) and become valid
+__global__ __launch_bounds__(64) void signature_query_kernel(const QueryArgs a, int hash_num,
+                                                             uint64_t seed, int mode,
+                                                             uint64_t* __restrict__ bits,
+                                                             float* __restrict__ norms,
+                                                             uint8_t* __restrict__ valid) {
+  const int q = blockIdx.x;
+  if (q >= a.n) return;
+  const int words = (hash_num + 63) / 64;
+  const int64_t row = a.dst[q] >= 0 ? a.dst[q] : q;
+  signature_one(a.idx, a.val, a.slot[q], a.slot[q + 1] - a.slot[q], hash_num, seed, mode,
+                bits + row * words, norms + row, threadIdx.x);
+  if (valid != nullptr && threadIdx.x == 0) valid[row] = 1;
+}
+
+namespace {
+int fill_query_args(QueryArgs* a, const int32_t* idx, const float* val, const int64_t* row_ptr,
+                    int n, const int64_t* dst) {
+  if (n > kQueryMax || row_ptr[n] - row_ptr[0] > kQuerySlots) return 1;
+  a->n = n;
+  const int64_t base = row_ptr[0];
+  for (int i = 0; i <= n; ++i) a->slot[i] = (int32_t)(row_ptr[i] - base);
+  for (int i = 0; i < n; ++i) a->dst[i] = dst ? dst[i] : -1;
+  const int ns = a->slot[n];
+  std::memcpy(a->idx, idx + base, sizeof(int32_t) * (size_t)ns);
+  std::memcpy(a->val, val + base, sizeof(float) * (size_t)ns);
+  return 0;
+}
+}  // namespace
 
 // metric: 0 lsh (distance = hamming / hash_num), 1 euclid_lsh (approximate
 // euclidean distance from norms + angle), 2 minhash (distance = 1 - matching
@@ -184,5 +237,55 @@ extern "C" int jb_sparse_scan(const int32_t* qidx, const float* qval, int qn, fl
   const unsigned blocks = (unsigned)((nrows + threads - 1) / threads);
   hipLaunchKernelGGL(jb::sparse_scan_kernel, dim3(blocks), dim3(threads), 0, stream, qidx, qval, qn,
                      qnorm2, row_ptr, ridx, rval, rnorm2, valid, nrows, metric, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq,
+                               const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
+                               int64_t nrows, int words, int hash_num, int metric, int k,
+                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                               hipStream_t stream);
+
+// Latency path of similar_row / neighbor_row (lsh family): the host-hashed
+// query CSR (row_ptr[nq+1] host, idx / val host) rides in the kernel
+// arguments of the signature kernel; the fused scan + top-k follows and its
+// merge writes (distance, row) straight into pinned host memory. Three
+// back-to-back launches, no copy, one host spin. Returns 1 when the query
+// does not fit (nq > 8 or > 256 feature slots): the caller uses the batch path.
+extern "C" int jb_lsh_query_direct(const int32_t* idx, const float* val, const int64_t* row_ptr,
+                                   int nq, int hash_num, uint64_t seed, int mode, int metric,
+                                   const uint64_t* tbits, const float* tnorm,
+                                   const uint8_t* valid, int64_t nrows, int k,
+                                   uint64_t* qbits_scratch, float* qnorm_scratch,
+                                   float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                                   int32_t* out_i_host, uint32_t* done_host, hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  jb::QueryArgs a;
+  if (jb::fill_query_args(&a, idx, val, row_ptr, nq, nullptr)) return 1;
+  hipLaunchKernelGGL(jb::signature_query_kernel, dim3(nq), dim3(64), 0, stream, a, hash_num,
+                     seed, mode, qbits_scratch, qnorm_scratch, (uint8_t*)nullptr);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const uint32_t seq = jb::next_seq();
+  const int rc = jb_topk_to_host(qbits_scratch, qnorm_scratch, nq, tbits, tnorm, valid, nrows,
+                                 (hash_num + 63) / 64, hash_num, metric, k, scratch_d, scratch_i,
+                                 out_d_host, out_i_host, done_host, seq, stream);
+  if (rc != 0) return rc;
+  return jb::wait_flags(done_host, nq, seq, stream);
+}
+
+// set_row latency path: signatures of n host-hashed rows computed from the
+// kernel arguments straight into their table slots (bits / norms / valid);
+// asynchronous, no copy. Returns 1 when the rows do not fit (caller: bulk path).
+extern "C" int jb_lsh_set_rows_direct(const int32_t* idx, const float* val, const int64_t* row_ptr,
+                                      int n, const int64_t* slots, int hash_num, uint64_t seed,
+                                      int mode, uint64_t* tbits, float* tnorm, uint8_t* valid,
+                                      hipStream_t stream) {
+  if (n <= 0) return 0;
+  jb::QueryArgs a;
+  if (jb::fill_query_args(&a, idx, val, row_ptr, n, slots)) return 1;
+  hipLaunchKernelGGL(jb::signature_query_kernel, dim3(n), dim3(64), 0, stream, a, hash_num, seed,
+                     mode, tbits, tnorm, valid);
   return (int)hipGetLastError();
 }

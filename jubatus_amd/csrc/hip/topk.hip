@@ -138,7 +138,9 @@ template <int MODE>
 __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int64_t n,
                                                            int64_t per_block, int k,
                                                            float* __restrict__ out_d,
-                                                           int32_t* __restrict__ out_i) {
+                                                           int32_t* __restrict__ out_i,
+                                                           volatile uint32_t* done = nullptr,
+                                                           uint32_t seq = 0) {
   __shared__ float s_wd[4][kTopMaxK];
   __shared__ int s_wi[4][kTopMaxK];
   __shared__ float s_cd[kTopMaxK];
@@ -194,6 +196,11 @@ __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int6
   }
   const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
   for (int j = t; j < k; j += kTopThreads) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
+  if (done != nullptr) {   // latency path: results went to pinned host memory
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) done[q] = seq;
+  }
 }
 
 }  // namespace jb
@@ -226,15 +233,42 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
   if (mode == 0)
     hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                       nrows, per_block, k, scratch_d, scratch_i);
+                       nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
   else
     hipLaunchKernelGGL(jb::topk_kernel<1>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                       nrows, per_block, k, scratch_d, scratch_i);
+                       nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;   // candidates per query
   jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
   hipLaunchKernelGGL(jb::topk_kernel<2>, dim3(1, nq), dim3(jb::kTopThreads), 0, stream, m, nc,
-                     ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d, out_i);
+                     ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d, out_i,
+                     nullptr, 0u);
+  return (int)hipGetLastError();
+}
+
+// Latency path (mode 0): as jb_topk, but the final merge writes straight into
+// fine-grained pinned host memory and publishes done[q] = seq per query.
+extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq,
+                               const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
+                               int64_t nrows, int words, int hash_num, int metric, int k,
+                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                               hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  if (k > jb::kTopMaxK || words > jb::kTopMaxWords) return -2;
+  const int blocks = jb_topk_blocks(nrows, k);
+  const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
+  const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
+  jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
+  hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
+                     nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  const int64_t nc = (int64_t)blocks * k;
+  jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
+  hipLaunchKernelGGL(jb::topk_kernel<2>, dim3(1, nq), dim3(jb::kTopThreads), 0, stream, m, nc,
+                     ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d_host,
+                     out_i_host, (volatile uint32_t*)done_host, seq);
   return (int)hipGetLastError();
 }

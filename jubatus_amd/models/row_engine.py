@@ -52,9 +52,12 @@ class RowEngine:
         return self.conv.hashed(f)
 
     def _set(self, rid: str, dicts, bump: bool = True, update_weight: bool = True) -> None:
-        fv = self.fv_of(dicts_to_datum(*dicts), update_weight)
-        slot = self.rows.put(rid, dicts, fv, bump)
-        self.index.set_rows([slot], [fv])
+        if self.gpu and hasattr(self.index, "set_rows_direct") and self._set_direct(rid, dicts, bump):
+            pass
+        else:
+            fv = self.fv_of(dicts_to_datum(*dicts), update_weight)
+            slot = self.rows.put(rid, dicts, fv, bump)
+            self.index.set_rows([slot], [fv])
         for victim in self.unlearner.touch(rid):
             if victim != rid:
                 self._remove(victim)
@@ -123,6 +126,29 @@ class RowEngine:
                 if victim != rid:
                     self._remove(victim)
 
+    def _set_direct(self, rid: str, dicts, bump: bool) -> bool:
+        """native hashing + one signature launch into the row's slot"""
+        h = self._hasher()
+        if h is None:
+            return False
+        import msgpack
+        import numpy as np
+        from ..ops import hip
+        body = msgpack.packb([dicts_to_datum(*dicts).to_msgpack()], use_bin_type=False)
+        idx = np.empty(hip.QUERY_SLOTS, np.int32)
+        val = np.empty(hip.QUERY_SLOTS, np.float32)
+        rp = np.zeros(2, np.int64)
+        n, _, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 1,
+                           hip.QUERY_SLOTS)
+        if err or n != 1:
+            return False
+        keep = idx[:rp[1]] >= 0
+        fv = (idx[:rp[1]][keep].tolist(), val[:rp[1]][keep].tolist())
+        slot = self.rows.put(rid, dicts, fv, bump)
+        if not self.index.set_rows_direct(np.asarray([slot], np.int64), rp, idx, val):
+            self.index.set_rows([slot], [fv])
+        return True
+
     def set_rows(self, items: list) -> int:
         """bulk set_row: [(id, datum)] -> number of rows written"""
         with self._lock:
@@ -187,7 +213,37 @@ class RowEngine:
             return self._results(r)
 
     def query_datum(self, d: Any, k: int, similar: bool) -> list[tuple[str, float]]:
-        return self.query_fv(self.fv_of(as_datum(d)), k, similar)
+        d = as_datum(d)
+        if self.gpu and hasattr(self.index, "query_direct") and k > 0:
+            r = self._query_datum_direct(d, k, similar)
+            if r is not None:
+                return r
+        return self.query_fv(self.fv_of(d), k, similar)
+
+    def _query_datum_direct(self, d, k: int, similar: bool):
+        """native hashing of the datum + the single-shot LSH query kernel"""
+        h = self._hasher()
+        if h is None:
+            return None
+        import msgpack
+        import numpy as np
+        body = msgpack.packb([d.to_msgpack()], use_bin_type=False)
+        from ..ops import hip
+        idx = np.empty(hip.QUERY_SLOTS, np.int32)
+        val = np.empty(hip.QUERY_SLOTS, np.float32)
+        rp = np.zeros(2, np.int64)
+        n, _, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 1,
+                           hip.QUERY_SLOTS)
+        if err or n != 1:
+            return None
+        with self._lock:
+            nrows = self.rows.nslots
+            if nrows == 0:
+                return []
+            r = self.index.query_direct(idx, val, rp, 1, nrows, k, similar)
+            if r is None:
+                return None
+            return self._results(r[0])
 
     def query_id(self, rid: str, k: int, similar: bool) -> list[tuple[str, float]]:
         with self._lock:

@@ -96,6 +96,7 @@ class LshIndex:
         self.device = device
         self.gpu = device is not None
         self.cap = 0
+        self._direct = None
         self._alloc(1024)
 
     def _alloc(self, cap: int) -> None:
@@ -194,6 +195,23 @@ class LshIndex:
         self.norms.index_copy_(0, st, norms)
         self.valid.index_fill_(0, st, 1)
 
+    def set_rows_direct(self, slots: np.ndarray, row_ptr: np.ndarray, idx: np.ndarray,
+                        val: np.ndarray) -> bool:
+        """latency path of set_row / update_row: one launch, the rows in the
+        kernel arguments, signatures written straight into their slots"""
+        if not self.gpu:
+            return False
+        need = int(slots.max()) + 1
+        if need > self.cap:
+            c = self.cap
+            while c < need:
+                c *= 2
+            self._alloc(c)
+        from ..ops import hip
+        return hip.lsh_set_rows_direct(idx.ctypes.data, val.ctypes.data, row_ptr.ctypes.data,
+                                       int(slots.size), slots.ctypes.data, self.hash_num,
+                                       self.seed, self.mode, self.bits, self.norms, self.valid)
+
     def remove(self, slot: int) -> None:
         if slot < self.cap:
             self.valid[slot] = 0
@@ -242,6 +260,27 @@ class LshIndex:
                 return _pairs(d.cpu().numpy(), i.cpu().numpy(),
                               self.similarity_of if similar else None)
         return topk(self.distances(rows, nrows), k, self.similarity_of if similar else None)
+
+    def query_direct(self, idx, val, row_ptr, nq: int, nrows: int, k: int,
+                     similar: bool) -> list[list[tuple[int, float]]] | None:
+        """latency path: host-hashed query CSR (numpy int32 / float32 / int64)
+        -> one signature launch from kernel arguments + fused scan/top-k whose
+        result lands in pinned host memory (csrc/hip/lsh.hip). None when not
+        applicable (CPU index, large query / k)."""
+        if not (self.gpu and nrows > 0):
+            return None
+        from ..ops import hip
+        if self._direct is None:
+            self._direct = hip.DirectQueryBuffers(self.device, self.words)
+        import torch
+        stream = torch.cuda.current_stream(self.device)
+        r = hip.lsh_query_direct(idx.ctypes.data, val.ctypes.data, row_ptr.ctypes.data, nq,
+                                 self.hash_num, self.seed, self.mode, self.metric, self.bits,
+                                 self.norms, self.valid, nrows, k, self._direct,
+                                 stream.cuda_stream)
+        if r is None:
+            return None
+        return _pairs(r[0], r[1], self.similarity_of if similar else None)
 
     def query_slots(self, slots: Sequence[int], nrows: int, k: int,
                     similar: bool) -> list[list[tuple[int, float]]] | None:

@@ -46,6 +46,11 @@ _SIGS = {
     "jb_topk": [_i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
                 _i32, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_topk_blocks": [_i64, _i32],
+    "jb_lsh_query_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _u64, _i32, _i32, _c_void_p,
+                            _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
+                            _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_lsh_set_rows_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _u64, _i32,
+                               _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
@@ -363,3 +368,61 @@ def classify_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, n: int, W: tor
 def diag_empty(done: HostBuffer, spin: bool, stream: int | None = None) -> None:
     rc = _fn("jb_diag_empty")(done.ptr, 1 if spin else 0, _stream() if stream is None else stream)
     _check(rc, "jb_diag_empty")
+
+
+QUERY_MAX = 8          # csrc/hip/lsh.hip kQueryMax
+QUERY_SLOTS = 256      # kQuerySlots
+
+
+class DirectQueryBuffers:
+    """pinned host outputs + device scratch of the LSH latency path"""
+
+    def __init__(self, device, words: int):
+        self.out_d = HostBuffer(QUERY_MAX * TOPK_MAX_K * 4)
+        self.out_i = HostBuffer(QUERY_MAX * TOPK_MAX_K * 4)
+        self.done = HostBuffer(QUERY_MAX * 4)
+        self.qbits = torch.empty(QUERY_MAX * max(words, 1), dtype=torch.int64, device=device)
+        self.qnorm = torch.empty(QUERY_MAX, dtype=torch.float32, device=device)
+
+
+def lsh_query_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, nq: int, hash_num: int, seed: int,
+                     mode: int, metric: int, tbits, tnorm, valid, nrows: int, k: int,
+                     bufs: DirectQueryBuffers, stream: int | None = None):
+    """-> (dist [nq, k], row [nq, k]) numpy (copies), or None when the query
+    does not fit the direct path"""
+    import numpy as np
+    words = (hash_num + 63) // 64
+    if not (0 < k <= TOPK_MAX_K and words <= TOPK_MAX_WORDS and 0 < nq <= QUERY_MAX):
+        return None
+    _dev(valid, torch.uint8, "valid")
+    _dev(tnorm, torch.float32, "tnorm")
+    if tbits.numel() < nrows * words or valid.numel() < nrows or tnorm.numel() < nrows:
+        raise ValueError("lsh_query_direct: bad table shapes")
+    blocks = _fn("jb_topk_blocks")(nrows, k)
+    sd, si = _topk_scratch(tbits.device, nq * blocks * k)
+    rc = _fn("jb_lsh_query_direct")(idx_ptr, val_ptr, row_ptr_ptr, nq, hash_num, seed & (2**64 - 1),
+                                    mode, metric, _p(tbits), _p(tnorm), _p(valid), nrows, k,
+                                    _p(bufs.qbits), _p(bufs.qnorm), _p(sd), _p(si), bufs.out_d.ptr,
+                                    bufs.out_i.ptr, bufs.done.ptr,
+                                    _stream() if stream is None else stream)
+    if rc == 1:
+        return None
+    _check(rc, "jb_lsh_query_direct")
+    d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
+    i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
+    return d, i
+
+
+def lsh_set_rows_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, n: int, slots_ptr: int,
+                        hash_num: int, seed: int, mode: int, tbits, tnorm, valid) -> bool:
+    """signatures of n host-hashed rows written into their table slots by one
+    launch whose arguments carry the rows (async). False: does not fit."""
+    _dev(valid, torch.uint8, "valid")
+    _dev(tnorm, torch.float32, "tnorm")
+    rc = _fn("jb_lsh_set_rows_direct")(idx_ptr, val_ptr, row_ptr_ptr, n, slots_ptr, hash_num,
+                                       seed & (2**64 - 1), mode, _p(tbits), _p(tnorm), _p(valid),
+                                       _stream())
+    if rc == 1:
+        return False
+    _check(rc, "jb_lsh_set_rows_direct")
+    return True

@@ -186,3 +186,36 @@ def test_topk_scores_flip():
     for q in range(2):
         ref = np.argsort(1.0 - s[q].numpy(), kind="stable")[:20]
         np.testing.assert_array_equal(oi[q].cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("method", ["lsh", "euclid_lsh", "minhash"])
+def test_direct_set_row_and_query_match_batch_paths(method):
+    """latency paths (csrc/hip/lsh.hip: signatures from kernel arguments into
+    table slots; query signature + fused top-k into pinned host memory) ==
+    the batch paths on the same data"""
+    from jubatus_amd.models.recommender import NearestNeighbor
+    conv = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin",
+                              "global_weight": "bin"}],
+            "num_rules": [{"key": "*", "type": "num"}]}
+    a = NearestNeighbor(method, {"hash_num": 128}, DatumToFvConverter(conv), dev())
+    b = NearestNeighbor(method, {"hash_num": 128}, DatumToFvConverter(conv), dev())
+    import random as _r
+    rng = _r.Random(3)
+    rows_ = [(f"r{i}", {"s": f"t{rng.randrange(30)}", "x": rng.gauss(0, 1), "y": float(i % 7)})
+             for i in range(400)]
+    for rid, d in rows_:
+        a.set_row(rid, d)                       # direct path, one launch per row
+    b.set_rows(rows_)                           # bulk path
+    na = a.rows.nslots
+    assert na == b.rows.nslots
+    ba = a.index.bits[:na].cpu().numpy()
+    bb = b.index.bits[:na].cpu().numpy()
+    sa = [a.rows.slot(r) for r, _ in rows_]
+    sb = [b.rows.slot(r) for r, _ in rows_]
+    assert (ba[sa] == bb[sb]).all()
+    for q in ({"s": "t3", "x": 0.1, "y": 2.0}, {"x": -1.0}):
+        ra = a.similar_row_from_datum(q, 10)    # direct query
+        fv = a.fv_of(__import__("jubatus_amd.fv_converter.datum", fromlist=["as_datum"]).as_datum(q))
+        rb = a.query_fv(fv, 10, True)           # batch query path
+        assert [s for _, s in ra] == pytest.approx([s for _, s in rb], rel=1e-5, abs=1e-6)
+        assert [r for r, _ in ra] == [r for r, _ in rb]
