@@ -25,6 +25,7 @@
 #include <limits.h>
 
 #include "jb_device.hpp"
+#include "jb_host_wait.hpp"
 
 namespace jb {
 
@@ -271,4 +272,22 @@ extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq
                      ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d_host,
                      out_i_host, (volatile uint32_t*)done_host, seq);
   return (int)hipGetLastError();
+}
+
+// Latency path by stored rows: query signatures already on the device
+// (e.g. gathered table rows); launch the fused scan/top-k into pinned host
+// memory and wait for it.
+extern "C" int jb_topk_direct_wait(const uint64_t* qbits, const float* qnorm, int nq,
+                                   const uint64_t* tbits, const float* tnorm,
+                                   const uint8_t* valid, int64_t nrows, int words, int hash_num,
+                                   int metric, int k, float* scratch_d, int32_t* scratch_i,
+                                   float* out_d_host, int32_t* out_i_host, uint32_t* done_host,
+                                   hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  const uint32_t seq = jb::next_seq();
+  const int rc = jb_topk_to_host(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num,
+                                 metric, k, scratch_d, scratch_i, out_d_host, out_i_host,
+                                 done_host, seq, stream);
+  if (rc != 0) return rc;
+  return jb::wait_flags(done_host, nq, seq, stream);
 }

@@ -209,6 +209,14 @@ class RowEngine:
             n = self.rows.nslots
             if n == 0 or k <= 0:
                 return []
+            if self.gpu and hasattr(self.index, "query_direct") and len(fv[0]) <= 256:
+                import numpy as np
+                idx = np.asarray(fv[0], np.int32)
+                val = np.asarray(fv[1], np.float32)
+                rp = np.asarray([0, idx.size], np.int64)
+                r = self.index.query_direct(idx, val, rp, 1, n, k, similar)
+                if r is not None:
+                    return self._results(r[0])
             (r,) = self.index.query([fv], n, k, similar)
             return self._results(r)
 
@@ -250,6 +258,10 @@ class RowEngine:
             s = self.rows.slot(rid)
             if s is None:
                 raise KeyError(f"row not found: {rid}")
+            if hasattr(self.index, "query_slots") and k > 0:
+                r = self.index.query_slots([s], self.rows.nslots, k, similar)
+                if r is not None:
+                    return self._results(r[0])
             return self.query_fv(self.rows.fv[s], k, similar)
 
     def query_ids(self, rids: list[str], k: int, similar: bool) -> dict[str, list[tuple[str, float]]]:
@@ -262,7 +274,17 @@ class RowEngine:
                 raise KeyError("row not found")
             res = None
             if hasattr(self.index, "query_slots"):
-                res = self.index.query_slots(slots, n, k, similar)
+                from ..ops import hip
+                if len(slots) > hip.QUERY_MAX and self.gpu:
+                    res = []
+                    for i in range(0, len(slots), hip.QUERY_MAX):
+                        part = self.index.query_slots(slots[i:i + hip.QUERY_MAX], n, k, similar)
+                        if part is None:
+                            res = None
+                            break
+                        res.extend(part)
+                else:
+                    res = self.index.query_slots(slots, n, k, similar)
             if res is None:
                 res = self.index.query([self.rows.fv[s] for s in slots], n, k, similar)
             return {rid: self._results(r) for rid, r in zip(rids, res)}

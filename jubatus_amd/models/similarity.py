@@ -293,7 +293,22 @@ class LshIndex:
         if not (0 < k <= hip.TOPK_MAX_K and self.words <= hip.TOPK_MAX_WORDS):
             return None
         import torch
-        st = torch.as_tensor(list(slots), dtype=torch.int64).to(self.device)
+        slots = list(slots)
+        if len(slots) <= hip.QUERY_MAX:
+            # latency path: rows gathered on the device, result in pinned host memory
+            if self._direct is None:
+                self._direct = hip.DirectQueryBuffers(self.device, self.words)
+            if len(slots) == 1:
+                s0 = int(slots[0])
+                qb, qn = self.bits[s0:s0 + 1], self.norms[s0:s0 + 1]
+            else:
+                st = torch.as_tensor(slots, dtype=torch.int64).to(self.device, non_blocking=True)
+                qb = self.bits.index_select(0, st)
+                qn = self.norms.index_select(0, st)
+            r = hip.topk_rows_direct(qb, qn, len(slots), self.bits, self.norms, self.valid, nrows,
+                                     self.hash_num, self.metric, k, self._direct)
+            return _pairs(r[0], r[1], self.similarity_of if similar else None)
+        st = torch.as_tensor(slots, dtype=torch.int64).to(self.device)
         qb = self.bits.index_select(0, st).contiguous()
         qn = self.norms.index_select(0, st).contiguous()
         d, i = hip.topk_hamming(qb, qn, len(slots), self.bits, self.norms, self.valid, nrows,

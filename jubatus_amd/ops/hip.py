@@ -51,6 +51,9 @@ _SIGS = {
                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_lsh_set_rows_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _u64, _i32,
                                _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_topk_direct_wait": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
+                            _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                            _c_void_p, _c_void_p],
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
@@ -426,3 +429,22 @@ def lsh_set_rows_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, n: int, sl
         return False
     _check(rc, "jb_lsh_set_rows_direct")
     return True
+
+
+def topk_rows_direct(qbits, qnorm, nq: int, tbits, tnorm, valid, nrows: int, hash_num: int,
+                     metric: int, k: int, bufs: DirectQueryBuffers):
+    """queries whose signatures are device rows (gathered table rows): fused
+    scan/top-k straight into pinned host memory -> numpy (dist, row) or None"""
+    import numpy as np
+    words = (hash_num + 63) // 64
+    if not (0 < k <= TOPK_MAX_K and words <= TOPK_MAX_WORDS and 0 < nq <= QUERY_MAX):
+        return None
+    blocks = _fn("jb_topk_blocks")(nrows, k)
+    sd, si = _topk_scratch(tbits.device, nq * blocks * k)
+    rc = _fn("jb_topk_direct_wait")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid),
+                                    nrows, words, hash_num, metric, k, _p(sd), _p(si),
+                                    bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
+    _check(rc, "jb_topk_direct_wait")
+    d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
+    i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
+    return d, i
