@@ -55,11 +55,29 @@ __device__ __forceinline__ void sort_regs(float (&d)[N], int (&ix)[N]) {
   }
 }
 
-__device__ __forceinline__ void wave_argmin(float& v, int& id) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const float ov = __shfl_xor(v, off, 64);
-    const int oid = __shfl_xor(id, off, 64);
+// wave64 arg-min of (v, id) with every lane getting the result, in
+// registers only: DPP quad / half-row / row mirrors, then permlane16/32
+// swaps (gfx950). A ds_bpermute butterfly costs an LDS round trip per step.
+template <int CTRL>
+__device__ __forceinline__ void argmin_step_dpp(float& v, int& id) {
+  const float ov = dpp_f<CTRL>(v);
+  const int oid = dpp_i<CTRL>(id);
+  if (lt_pair(ov, oid, v, id)) { v = ov; id = oid; }
+}
+
+__device__ __forceinline__ void wave_argmin(float& v, int& id, int lane) {
+  argmin_step_dpp<kDppXor1>(v, id);
+  argmin_step_dpp<kDppXor2>(v, id);
+  argmin_step_dpp<kDppHalfMirror>(v, id);
+  argmin_step_dpp<kDppMirror>(v, id);
+  {
+    const float ov = partner16_f(v, lane);
+    const int oid = partner16_i(id, lane);
+    if (lt_pair(ov, oid, v, id)) { v = ov; id = oid; }
+  }
+  {
+    const float ov = partner32_f(v, lane);
+    const int oid = partner32_i(id, lane);
     if (lt_pair(ov, oid, v, id)) { v = ov; id = oid; }
   }
 }
@@ -75,7 +93,7 @@ __device__ __forceinline__ float wave_pop(float (&d)[N], int (&ix)[N], int k,
   for (; r < k; ++r) {
     float v = d[0];
     int id = ix[0];
-    wave_argmin(v, id);
+    wave_argmin(v, id, lane);
     if (!(v < INFINITY)) break;                 // uniform across the wave
     const bool win = (ix[0] == id) && (d[0] == v);
 #pragma unroll
