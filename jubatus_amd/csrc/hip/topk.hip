@@ -130,18 +130,20 @@ __device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, in
   if (r >= n) { d = INFINITY; id = INT_MAX; return; }
   if (MODE == 0) {
     id = (int)r;
-    if (!s.valid[r]) { d = INFINITY; return; }
+    // every load issued unconditionally (no branch between them): the rows
+    // of a tile are in flight together instead of valid -> bits -> norm
+    const uint8_t ok = s.valid[r];
+    const float b = s.metric == 1 ? s.tnorm[r] : 0.f;
     int ham = 0;
 #pragma unroll
     for (int w = 0; w < kTopMaxWords; ++w)
       if (w < s.words) ham += __popcll(qb[w] ^ s.tbits[r * s.words + w]);
     const float frac = (float)ham / (float)s.hash_num;
-    if (s.metric == 1) {
-      const float b = s.tnorm[r];
+    if (s.metric == 1)
       d = sqrtf(fmaxf(0.f, qn * qn + b * b - 2.f * qn * b * __cosf(3.14159265f * frac)));
-    } else {
+    else
       d = frac;
-    }
+    if (!ok) d = INFINITY;
   } else if (MODE == 1) {
     id = (int)r;
     const float v = s.src_d[(int64_t)q * n + r];
@@ -233,7 +235,9 @@ __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int6
 extern "C" int jb_topk_blocks(int64_t nrows, int k) {
   if (k <= 0 || nrows <= 0) return 0;
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
-  int64_t max_blocks = 8192 / k;              // bound the candidates K2 merges
+  // bound the candidates K2 merges; one block per CU is enough to stream
+  // the table (the scan is a few bytes per row)
+  int64_t max_blocks = 8192 / k < 256 ? 8192 / k : 256;
   if (max_blocks < 1) max_blocks = 1;
   const int64_t tiles_per_block = (tiles + max_blocks - 1) / max_blocks;
   return (int)((tiles + tiles_per_block - 1) / tiles_per_block);
