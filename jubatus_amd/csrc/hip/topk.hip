@@ -155,25 +155,29 @@ __device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, in
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int64_t n,
+// NW waves per block; the merge of (NW + 1) * k candidates in wave 0 must fit
+// 10 per lane: NW = 4 for k <= 128, NW = 16 (the final merge) for k <= 37.
+template <int MODE, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t n,
                                                            int64_t per_block, int k,
                                                            float* __restrict__ out_d,
                                                            int32_t* __restrict__ out_i,
                                                            volatile uint32_t* done = nullptr,
                                                            uint32_t seq = 0) {
-  __shared__ float s_wd[4][kTopMaxK];
-  __shared__ int s_wi[4][kTopMaxK];
+  constexpr int T = NW * 64;
+  constexpr int TILE = T * kTopR;
+  __shared__ float s_wd[NW][kTopMaxK];
+  __shared__ int s_wi[NW][kTopMaxK];
   __shared__ float s_cd[kTopMaxK];
   __shared__ int s_ci[kTopMaxK];
   __shared__ float s_thr;
   __shared__ uint64_t s_q[kTopMaxWords];
   const int q = blockIdx.y;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int j = t; j < k; j += kTopThreads) { s_cd[j] = INFINITY; s_ci[j] = INT_MAX; }
+  for (int j = t; j < k; j += T) { s_cd[j] = INFINITY; s_ci[j] = INT_MAX; }
   float qn = 0.f;
   if (MODE == 0) {
-    for (int w = t; w < s.words; w += kTopThreads) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    for (int w = t; w < s.words; w += T) s_q[w] = s.qbits[(int64_t)q * s.words + w];
     qn = s.qnorm[q];
   }
   if (t == 0) s_thr = INFINITY;
@@ -183,13 +187,13 @@ __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int6
   for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
   const int64_t b0 = (int64_t)blockIdx.x * per_block;
   const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
-  for (int64_t base = b0; base < b1; base += kTopTile) {
+  for (int64_t base = b0; base < b1; base += TILE) {
     const float thr = s_thr;
     float d[kTopR];
     int ix[kTopR];
 #pragma unroll
     for (int r = 0; r < kTopR; ++r) {
-      const int64_t row = base + (int64_t)r * kTopThreads + t;
+      const int64_t row = base + (int64_t)r * T + t;
       load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
       if (d[r] > thr) { d[r] = INFINITY; ix[r] = INT_MAX; }
     }
@@ -197,7 +201,7 @@ __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int6
     wave_pop<kTopR>(d, ix, k, s_wd[wv], s_wi[wv], lane);
     __syncthreads();
     if (wv == 0) {
-      // merge carry (k) + 4 wave lists (4k) <= 640 -> 10 per lane
+      // merge carry (k) + NW wave lists (NW k) <= 640 -> 10 per lane
       constexpr int M = 10;
       float m[M];
       int mi[M];
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int6
       for (int j = 0; j < M; ++j) {
         const int c = lane + 64 * j;
         if (c < k) { m[j] = s_cd[c]; mi[j] = s_ci[c]; }
-        else if (c < 5 * k) { const int w = (c - k) / k, o = (c - k) % k; m[j] = s_wd[w][o]; mi[j] = s_wi[w][o]; }
+        else if (c < (NW + 1) * k) { const int w = (c - k) / k, o = (c - k) % k; m[j] = s_wd[w][o]; mi[j] = s_wi[w][o]; }
         else { m[j] = INFINITY; mi[j] = INT_MAX; }
       }
       __builtin_amdgcn_wave_barrier();
@@ -216,11 +220,26 @@ __global__ __launch_bounds__(kTopThreads) void topk_kernel(const TopkSrc s, int6
     __syncthreads();
   }
   const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
-  for (int j = t; j < k; j += kTopThreads) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
+  for (int j = t; j < k; j += T) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
   if (done != nullptr) {   // latency path: results went to pinned host memory
     __threadfence_system();
     __syncthreads();
     if (t == 0) done[q] = seq;
+  }
+}
+
+// the final merge: one block per query; 16 waves when the (17 k) candidates
+// of the merge stage fit (k <= 37), else 4
+inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out_d,
+                         int32_t* out_i, volatile uint32_t* done, uint32_t seq,
+                         hipStream_t stream) {
+  if (k <= 37) {
+    const int64_t tile = 16 * 64 * kTopR;
+    hipLaunchKernelGGL((topk_kernel<2, 16>), dim3(1, nq), dim3(16 * 64), 0, stream, m, nc,
+                       ((nc + tile - 1) / tile) * tile, k, out_d, out_i, done, seq);
+  } else {
+    hipLaunchKernelGGL((topk_kernel<2, 4>), dim3(1, nq), dim3(4 * 64), 0, stream, m, nc,
+                       ((nc + kTopTile - 1) / kTopTile) * kTopTile, k, out_d, out_i, done, seq);
   }
 }
 
@@ -264,9 +283,7 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;   // candidates per query
   jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
-  hipLaunchKernelGGL(jb::topk_kernel<2>, dim3(1, nq), dim3(jb::kTopThreads), 0, stream, m, nc,
-                     ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d, out_i,
-                     nullptr, 0u);
+  jb::launch_merge(m, nq, nc, k, out_d, out_i, nullptr, 0u, stream);
   return (int)hipGetLastError();
 }
 
@@ -290,9 +307,8 @@ extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;
   jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
-  hipLaunchKernelGGL(jb::topk_kernel<2>, dim3(1, nq), dim3(jb::kTopThreads), 0, stream, m, nc,
-                     ((nc + jb::kTopTile - 1) / jb::kTopTile) * jb::kTopTile, k, out_d_host,
-                     out_i_host, (volatile uint32_t*)done_host, seq);
+  jb::launch_merge(m, nq, nc, k, out_d_host, out_i_host, (volatile uint32_t*)done_host, seq,
+                   stream);
   return (int)hipGetLastError();
 }
 
