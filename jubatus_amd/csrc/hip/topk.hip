@@ -87,7 +87,7 @@ __device__ __forceinline__ void wave_argmin(float& v, int& id, int lane) {
 // the k-th value (or +inf when fewer than k finite values exist).
 template <int N>
 __device__ __forceinline__ float wave_pop(float (&d)[N], int (&ix)[N], int k,
-                                          float* od, int* oi, int lane) {
+                                          float* od, int* oi, int lane, int* popped = nullptr) {
   int r = 0;
   float last = INFINITY;
   for (; r < k; ++r) {
@@ -106,6 +106,7 @@ __device__ __forceinline__ float wave_pop(float (&d)[N], int (&ix)[N], int k,
     last = v;
   }
   for (int j = r + lane; j < k; j += 64) { od[j] = INFINITY; oi[j] = INT_MAX; }
+  if (popped != nullptr) *popped = r;
   return r == k ? last : INFINITY;
 }
 
@@ -166,8 +167,9 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
                                                            uint32_t seq = 0) {
   constexpr int T = NW * 64;
   constexpr int TILE = T * kTopR;
-  __shared__ float s_wd[NW][kTopMaxK];
-  __shared__ int s_wi[NW][kTopMaxK];
+  __shared__ float s_wd[NW * kTopMaxK];   // wave w's list at [w k, w k + k)
+  __shared__ int s_wi[NW * kTopMaxK];
+  __shared__ int s_cnt[NW];
   __shared__ float s_cd[kTopMaxK];
   __shared__ int s_ci[kTopMaxK];
   __shared__ float s_thr;
@@ -187,35 +189,52 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
   const int64_t b0 = (int64_t)blockIdx.x * per_block;
   const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  float* wd = &s_wd[wv * k];
+  int* wi = &s_wi[wv * k];
   for (int64_t base = b0; base < b1; base += TILE) {
     const float thr = s_thr;
     float d[kTopR];
     int ix[kTopR];
+    bool any = false;
 #pragma unroll
     for (int r = 0; r < kTopR; ++r) {
       const int64_t row = base + (int64_t)r * T + t;
       load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
       if (d[r] > thr) { d[r] = INFINITY; ix[r] = INT_MAX; }
+      any |= d[r] < INFINITY;
     }
-    sort_regs<kTopR>(d, ix);
-    wave_pop<kTopR>(d, ix, k, s_wd[wv], s_wi[wv], lane);
+    // once the block's k-th best is known almost every row fails the
+    // threshold: a wave with no survivor skips the sort and the selection
+    int cnt = 0;
+    if (__ballot(any)) {
+      sort_regs<kTopR>(d, ix);
+      wave_pop<kTopR>(d, ix, k, wd, wi, lane, &cnt);
+    } else {
+      for (int j = lane; j < k; j += 64) { wd[j] = INFINITY; wi[j] = INT_MAX; }
+    }
+    if (lane == 0) s_cnt[wv] = cnt;
     __syncthreads();
     if (wv == 0) {
-      // merge carry (k) + NW wave lists (NW k) <= 640 -> 10 per lane
-      constexpr int M = 10;
-      float m[M];
-      int mi[M];
+      int total = 0;
 #pragma unroll
-      for (int j = 0; j < M; ++j) {
-        const int c = lane + 64 * j;
-        if (c < k) { m[j] = s_cd[c]; mi[j] = s_ci[c]; }
-        else if (c < (NW + 1) * k) { const int w = (c - k) / k, o = (c - k) % k; m[j] = s_wd[w][o]; mi[j] = s_wi[w][o]; }
-        else { m[j] = INFINITY; mi[j] = INT_MAX; }
+      for (int w = 0; w < NW; ++w) total += s_cnt[w];
+      if (total > 0) {
+        // merge carry (k) + NW wave lists (NW k) <= 640 -> 10 per lane
+        constexpr int M = 10;
+        float m[M];
+        int mi[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+          const int c = lane + 64 * j;
+          if (c < k) { m[j] = s_cd[c]; mi[j] = s_ci[c]; }
+          else if (c < (NW + 1) * k) { m[j] = s_wd[c - k]; mi[j] = s_wi[c - k]; }
+          else { m[j] = INFINITY; mi[j] = INT_MAX; }
+        }
+        __builtin_amdgcn_wave_barrier();
+        sort_regs<M>(m, mi);
+        const float kth = wave_pop<M>(m, mi, k, s_cd, s_ci, lane);
+        if (lane == 0) s_thr = kth;
       }
-      __builtin_amdgcn_wave_barrier();
-      sort_regs<M>(m, mi);
-      const float kth = wave_pop<M>(m, mi, k, s_cd, s_ci, lane);
-      if (lane == 0) s_thr = kth;
     }
     __syncthreads();
   }
