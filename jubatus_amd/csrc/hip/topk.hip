@@ -247,12 +247,102 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   }
 }
 
+// Small k (<= KL): every thread keeps its own sorted top-KL of the rows it
+// scans (strided across the block's range) in registers - no per-tile block
+// synchronisation; a row costs one compare with the thread's KL-th value
+// and, rarely, an insertion. The block merges once at the end (per-wave
+// pops, then wave 0).
+template <int MODE, int KL, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void topk_lists_kernel(const TopkSrc s, int64_t n,
+                                                             int64_t per_block, int k,
+                                                             float* __restrict__ out_d,
+                                                             int32_t* __restrict__ out_i,
+                                                             volatile uint32_t* done = nullptr,
+                                                             uint32_t seq = 0) {
+  constexpr int T = NW * 64;
+  __shared__ float s_wd[NW * KL];
+  __shared__ int s_wi[NW * KL];
+  __shared__ float s_cd[KL];
+  __shared__ int s_ci[KL];
+  __shared__ uint64_t s_q[kTopMaxWords];
+  const int q = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += T) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  float ld[KL];
+  int li[KL];
+#pragma unroll
+  for (int j = 0; j < KL; ++j) { ld[j] = INFINITY; li[j] = INT_MAX; }
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  for (int64_t base = b0; base < b1; base += (int64_t)T * 4) {
+    float d[4];
+    int ix[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // 4 rows in flight per thread
+      const int64_t row = base + (int64_t)r * T + t;
+      load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = d[r];
+      const int id = ix[r];
+      if (lt_pair(v, id, ld[KL - 1], li[KL - 1])) {
+#pragma unroll
+        for (int j = KL - 1; j > 0; --j) {
+          const bool up = lt_pair(v, id, ld[j - 1], li[j - 1]);
+          const bool here = !up && lt_pair(v, id, ld[j], li[j]);
+          ld[j] = up ? ld[j - 1] : (here ? v : ld[j]);
+          li[j] = up ? li[j - 1] : (here ? id : li[j]);
+        }
+        if (lt_pair(v, id, ld[0], li[0])) { ld[0] = v; li[0] = id; }
+      }
+    }
+  }
+  wave_pop<KL>(ld, li, k, &s_wd[wv * k], &s_wi[wv * k], lane);
+  __syncthreads();
+  if (wv == 0) {
+    constexpr int M = (NW * KL + 63) / 64;
+    float m[M];
+    int mi[M];
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      const int c = lane + 64 * j;
+      if (c < NW * k) { m[j] = s_wd[c]; mi[j] = s_wi[c]; }
+      else { m[j] = INFINITY; mi[j] = INT_MAX; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    sort_regs<M>(m, mi);
+    wave_pop<M>(m, mi, k, s_cd, s_ci, lane);
+  }
+  __syncthreads();
+  const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
+  for (int j = t; j < k; j += T) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
+  if (done != nullptr) {
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) done[q] = seq;
+  }
+}
+
+constexpr int kListK = 16;   // k up to this uses topk_lists_kernel
+
 // the final merge: one block per query; 16 waves when the (17 k) candidates
 // of the merge stage fit (k <= 37), else 4
 inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out_d,
                          int32_t* out_i, volatile uint32_t* done, uint32_t seq,
                          hipStream_t stream) {
-  if (k <= 37) {
+  if (k <= kListK) {
+    hipLaunchKernelGGL((topk_lists_kernel<2, kListK, 16>), dim3(1, nq), dim3(16 * 64), 0, stream,
+                       m, nc, nc, k, out_d, out_i, done, seq);
+  } else if (k <= 37) {
     const int64_t tile = 16 * 64 * kTopR;
     hipLaunchKernelGGL((topk_kernel<2, 16>), dim3(1, nq), dim3(16 * 64), 0, stream, m, nc,
                        ((nc + tile - 1) / tile) * tile, k, out_d, out_i, done, seq);
@@ -292,12 +382,22 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
-  if (mode == 0)
+  if (k <= jb::kListK) {
+    if (mode == 0)
+      hipLaunchKernelGGL((jb::topk_lists_kernel<0, jb::kListK>), dim3(blocks, nq),
+                         dim3(jb::kTopThreads), 0, stream, s, nrows, per_block, k, scratch_d,
+                         scratch_i, nullptr, 0u);
+    else
+      hipLaunchKernelGGL((jb::topk_lists_kernel<1, jb::kListK>), dim3(blocks, nq),
+                         dim3(jb::kTopThreads), 0, stream, s, nrows, per_block, k, scratch_d,
+                         scratch_i, nullptr, 0u);
+  } else if (mode == 0) {
     hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
                        nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
-  else
+  } else {
     hipLaunchKernelGGL(jb::topk_kernel<1>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
                        nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;   // candidates per query
@@ -320,8 +420,13 @@ extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
-  hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                     nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
+  if (k <= jb::kListK)
+    hipLaunchKernelGGL((jb::topk_lists_kernel<0, jb::kListK>), dim3(blocks, nq),
+                       dim3(jb::kTopThreads), 0, stream, s, nrows, per_block, k, scratch_d,
+                       scratch_i, nullptr, 0u);
+  else
+    hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
+                       nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;
