@@ -247,11 +247,12 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   }
 }
 
-// Small k (<= KL): every thread keeps its own sorted top-KL of the rows it
-// scans (strided across the block's range) in registers - no per-tile block
-// synchronisation; a row costs one compare with the thread's KL-th value
-// and, rarely, an insertion. The block merges once at the end (per-wave
-// pops, then wave 0).
+// Small k (<= KL): every thread keeps its own sorted top-KL of the items it
+// reads (strided across the block's range) in registers and the block merges
+// once at the end (per-wave pops, then wave 0). Used for the final merge of
+// the blocks' candidates (a few items per thread); on a long scan with random
+// distances the per-thread insertions cost more than the tile kernel's
+// threshold-pruned selection (measured, tools/bench_topk.py).
 template <int MODE, int KL, int NW = 4>
 __global__ __launch_bounds__(NW * 64) void topk_lists_kernel(const TopkSrc s, int64_t n,
                                                              int64_t per_block, int k,
@@ -382,16 +383,7 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
-  if (k <= jb::kListK) {
-    if (mode == 0)
-      hipLaunchKernelGGL((jb::topk_lists_kernel<0, jb::kListK>), dim3(blocks, nq),
-                         dim3(jb::kTopThreads), 0, stream, s, nrows, per_block, k, scratch_d,
-                         scratch_i, nullptr, 0u);
-    else
-      hipLaunchKernelGGL((jb::topk_lists_kernel<1, jb::kListK>), dim3(blocks, nq),
-                         dim3(jb::kTopThreads), 0, stream, s, nrows, per_block, k, scratch_d,
-                         scratch_i, nullptr, 0u);
-  } else if (mode == 0) {
+  if (mode == 0) {
     hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
                        nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
   } else {
@@ -420,13 +412,8 @@ extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
-  if (k <= jb::kListK)
-    hipLaunchKernelGGL((jb::topk_lists_kernel<0, jb::kListK>), dim3(blocks, nq),
-                       dim3(jb::kTopThreads), 0, stream, s, nrows, per_block, k, scratch_d,
-                       scratch_i, nullptr, 0u);
-  else
-    hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                       nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
+  hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
+                     nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;
