@@ -24,6 +24,31 @@ inline int wait_flags(volatile uint32_t* done, int n, uint32_t seq, hipStream_t 
   return 0;
 }
 
+// as wait_flags, but a flag may also carry `mark` (seq | mark): reported
+// through *marked (e.g. "retry on the exact path")
+inline int wait_flags_status(volatile uint32_t* done, int n, uint32_t seq, uint32_t mark,
+                             hipStream_t stream, bool* marked) {
+  const auto t0 = std::chrono::steady_clock::now();
+  *marked = false;
+  for (int i = 0; i < n;) {
+    const uint32_t v = done[i];
+    if (v == seq || v == (seq | mark)) {
+      *marked = *marked || v != seq;
+      ++i;
+      continue;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+      const int rc = (int)hipStreamSynchronize(stream);
+      if (rc != 0) return rc;
+      for (int x = 0; x < n; ++x) *marked = *marked || done[x] != seq;
+      return 0;
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return 0;
+}
+
 inline uint32_t next_seq() {
   static std::atomic<uint32_t> g_seq{0};
   return g_seq.fetch_add(1, std::memory_order_relaxed) + 1;

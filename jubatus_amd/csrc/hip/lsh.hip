@@ -240,12 +240,12 @@ extern "C" int jb_sparse_scan(const int32_t* qidx, const float* qval, int qn, fl
   return (int)hipGetLastError();
 }
 
-extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq,
-                               const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
-                               int64_t nrows, int words, int hash_num, int metric, int k,
-                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
-                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
-                               hipStream_t stream);
+extern "C" int jb_topk_direct_query(const uint64_t* qbits, const float* qnorm, int nq,
+                                    const uint64_t* tbits, const float* tnorm,
+                                    const uint8_t* valid, int64_t nrows, int words, int hash_num,
+                                    int metric, int k, float* scratch_d, int32_t* scratch_i,
+                                    float* out_d_host, int32_t* out_i_host, uint32_t* done_host,
+                                    hipStream_t stream);
 
 // Latency path of similar_row / neighbor_row (lsh family): the host-hashed
 // query CSR (row_ptr[nq+1] host, idx / val host) rides in the kernel
@@ -267,12 +267,9 @@ extern "C" int jb_lsh_query_direct(const int32_t* idx, const float* val, const i
                      seed, mode, qbits_scratch, qnorm_scratch, (uint8_t*)nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const uint32_t seq = jb::next_seq();
-  const int rc = jb_topk_to_host(qbits_scratch, qnorm_scratch, nq, tbits, tnorm, valid, nrows,
-                                 (hash_num + 63) / 64, hash_num, metric, k, scratch_d, scratch_i,
-                                 out_d_host, out_i_host, done_host, seq, stream);
-  if (rc != 0) return rc;
-  return jb::wait_flags(done_host, nq, seq, stream);
+  return jb_topk_direct_query(qbits_scratch, qnorm_scratch, nq, tbits, tnorm, valid, nrows,
+                              (hash_num + 63) / 64, hash_num, metric, k, scratch_d, scratch_i,
+                              out_d_host, out_i_host, done_host, stream);
 }
 
 // set_row latency path: signatures of n host-hashed rows computed from the

@@ -333,6 +333,204 @@ __global__ __launch_bounds__(NW * 64) void topk_lists_kernel(const TopkSrc s, in
   }
 }
 
+// ---------------------------------------------------------------------------
+// Sampled-threshold top-k (latency path, large tables): O(N) with a small
+// constant for any k <= 128, instead of the tile kernel's O(N k / tile).
+//   S1  one block per query reads S evenly spaced rows and takes the j-th
+//       smallest distance as threshold T (j chosen by the host so that
+//       ~3k rows of the full table are expected at or below T);
+//   S2  full scan: rows with d <= T are appended to a candidate buffer
+//       (wave-aggregated atomics: one atomic per wave per pass);
+//   S3  exact top-k of the candidates (topk_lists / topk_kernel), written to
+//       pinned host memory; done[q] = seq, or seq | kTopRetry when T was too
+//       low (fewer than k candidates) or the buffer overflowed - the host
+//       then reruns the exact tile path.
+constexpr uint32_t kTopRetry = 0x80000000u;
+constexpr int kSampleThreads = 1024;
+
+template <int MODE>
+__global__ __launch_bounds__(kSampleThreads) void topk_sample_kernel(const TopkSrc s, int64_t n,
+                                                                     int64_t S, int j,
+                                                                     float* __restrict__ thr,
+                                                                     int* __restrict__ count) {
+  constexpr int KL = 16;
+  constexpr int NW = kSampleThreads / 64;
+  __shared__ float s_wd[NW * KL];
+  __shared__ int s_wi[NW * KL];
+  __shared__ float s_out[KL];
+  __shared__ int s_oi[KL];
+  __shared__ uint64_t s_q[kTopMaxWords];
+  const int q = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += kSampleThreads) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  float ld[KL];
+  int li[KL];
+#pragma unroll
+  for (int x = 0; x < KL; ++x) { ld[x] = INFINITY; li[x] = INT_MAX; }
+  for (int64_t i = t; i < S; i += kSampleThreads) {
+    const int64_t row = (i * n) / S;
+    float v;
+    int id;
+    load_item<MODE>(s, q, n, row, qb, qn, v, id);
+    if (lt_pair(v, id, ld[KL - 1], li[KL - 1])) {
+#pragma unroll
+      for (int x = KL - 1; x > 0; --x) {
+        const bool up = lt_pair(v, id, ld[x - 1], li[x - 1]);
+        const bool here = !up && lt_pair(v, id, ld[x], li[x]);
+        ld[x] = up ? ld[x - 1] : (here ? v : ld[x]);
+        li[x] = up ? li[x - 1] : (here ? id : li[x]);
+      }
+      if (lt_pair(v, id, ld[0], li[0])) { ld[0] = v; li[0] = id; }
+    }
+  }
+  wave_pop<KL>(ld, li, j, &s_wd[wv * j], &s_wi[wv * j], lane);
+  __syncthreads();
+  if (wv == 0) {
+    constexpr int M = (NW * KL + 63) / 64;
+    float m[M];
+    int mi[M];
+#pragma unroll
+    for (int x = 0; x < M; ++x) {
+      const int c = lane + 64 * x;
+      if (c < NW * j) { m[x] = s_wd[c]; mi[x] = s_wi[c]; }
+      else { m[x] = INFINITY; mi[x] = INT_MAX; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    sort_regs<M>(m, mi);
+    const float jth = wave_pop<M>(m, mi, j, s_out, s_oi, lane);
+    if (lane == 0) thr[q] = jth;   // +inf when fewer than j finite samples: collect all
+  }
+  if (t == 0) count[q] = 0;        // the collect kernel (next in the stream) appends from 0
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void topk_collect_kernel(const TopkSrc s, int64_t n,
+                                                           const float* __restrict__ thr,
+                                                           int cap, float* __restrict__ cand_d,
+                                                           int32_t* __restrict__ cand_i,
+                                                           int* __restrict__ count) {
+  __shared__ uint64_t s_q[kTopMaxWords];
+  const int q = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63;
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += 256) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  const float T = thr[q];
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t base = (int64_t)blockIdx.x * 256; base < n; base += stride * 4) {
+    float d[4];
+    int ix[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = base + r * stride + t;
+      load_item<MODE>(s, q, n, row, qb, qn, d[r], ix[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool pass = d[r] <= T && d[r] < INFINITY;
+      const uint64_t m = __ballot(pass);
+      if (m == 0) continue;
+      int basei = 0;
+      if (lane == 0) basei = atomicAdd(&count[q], __popcll(m));
+      basei = __shfl(basei, 0, 64);
+      if (pass) {
+        const int pos = basei + __popcll(m & ((1ull << lane) - 1ull));
+        if (pos < cap) {
+          cand_d[(int64_t)q * cap + pos] = d[r];
+          cand_i[(int64_t)q * cap + pos] = ix[r];
+        }
+      }
+    }
+  }
+}
+
+// exact top-k of the candidates (count from the device), results to host
+__global__ __launch_bounds__(1024) void topk_final_kernel(const float* __restrict__ cand_d,
+                                                          const int32_t* __restrict__ cand_i,
+                                                          const int* __restrict__ count, int cap,
+                                                          int k, const float* __restrict__ thr,
+                                                          float* __restrict__ out_d,
+                                                          int32_t* __restrict__ out_i,
+                                                          volatile uint32_t* done, uint32_t seq) {
+  constexpr int NW = 16;
+  constexpr int T = NW * 64;
+  constexpr int KL = 8;   // candidates held per thread per pass
+  __shared__ float s_cd[kTopMaxK];
+  __shared__ int s_ci[kTopMaxK];
+  __shared__ float s_wd[NW * kTopMaxK];
+  __shared__ int s_wi[NW * kTopMaxK];
+  __shared__ int s_cnt[NW];
+  const int q = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int c_all = count[q];
+  const int nc = c_all < cap ? c_all : cap;
+  for (int x = t; x < k; x += T) { s_cd[x] = INFINITY; s_ci[x] = INT_MAX; }
+  __syncthreads();
+  const float* cd = cand_d + (int64_t)q * cap;
+  const int32_t* ci = cand_i + (int64_t)q * cap;
+  // passes of T * KL candidates, each merged with the carry (as topk_kernel)
+  for (int base = 0; base < nc; base += T * KL) {
+    float d[KL];
+    int ix[KL];
+#pragma unroll
+    for (int r = 0; r < KL; ++r) {
+      const int c = base + r * T + t;
+      d[r] = c < nc ? cd[c] : INFINITY;
+      ix[r] = c < nc ? ci[c] : INT_MAX;
+    }
+    sort_regs<KL>(d, ix);
+    // k <= 128 may exceed the 10-per-lane merge of 16 lists: pop at most
+    // min(k, 40) per wave here, the carry merge keeps exactness because each
+    // wave's list is complete up to what it popped and the rest is retried
+    int cnt = 0;
+    const int kw = k;
+    wave_pop<KL>(d, ix, kw, &s_wd[wv * kw], &s_wi[wv * kw], lane, &cnt);
+    if (lane == 0) s_cnt[wv] = cnt;
+    __syncthreads();
+    if (wv == 0) {
+      // merge carry + 16 wave lists: at most (1 + 16) k <= 17 * 128 values,
+      // gathered in slices of 640 with the running carry
+      for (int off = 0; off < NW * kw; off += 640 - kw) {
+        constexpr int M = 10;
+        float m[M];
+        int mi[M];
+#pragma unroll
+        for (int x = 0; x < M; ++x) {
+          const int c = lane + 64 * x;
+          if (c < kw) { m[x] = s_cd[c]; mi[x] = s_ci[c]; }
+          else if (c - kw + off < NW * kw && c - kw < 640 - kw) { m[x] = s_wd[c - kw + off]; mi[x] = s_wi[c - kw + off]; }
+          else { m[x] = INFINITY; mi[x] = INT_MAX; }
+        }
+        __builtin_amdgcn_wave_barrier();
+        sort_regs<M>(m, mi);
+        wave_pop<M>(m, mi, kw, s_cd, s_ci, lane);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();
+  }
+  for (int x = t; x < k; x += T) { out_d[(int64_t)q * k + x] = s_cd[x]; out_i[(int64_t)q * k + x] = s_ci[x]; }
+  __threadfence_system();
+  __syncthreads();
+  // too few candidates is only a failure when T cut rows off (T < +inf)
+  const bool retry = c_all > cap || (c_all < k && thr[q] < INFINITY);
+  if (t == 0) done[q] = retry ? (seq | kTopRetry) : seq;
+}
+
 constexpr int kListK = 16;   // k up to this uses topk_lists_kernel
 
 // the final merge: one block per query; 16 waves when the (17 k) candidates
@@ -399,15 +597,14 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
 }
 
 // Latency path (mode 0): as jb_topk, but the final merge writes straight into
-// fine-grained pinned host memory and publishes done[q] = seq per query.
-extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq,
-                               const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
-                               int64_t nrows, int words, int hash_num, int metric, int k,
-                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
-                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
-                               hipStream_t stream) {
-  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
-  if (k > jb::kTopMaxK || words > jb::kTopMaxWords) return -2;
+// fine-grained pinned host memory and publishes done[q] = seq per query
+// (tile path).
+static int topk_to_host_tile(const uint64_t* qbits, const float* qnorm, int nq,
+                             const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
+                             int64_t nrows, int words, int hash_num, int metric, int k,
+                             float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                             int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                             hipStream_t stream) {
   const int blocks = jb_topk_blocks(nrows, k);
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
@@ -423,20 +620,84 @@ extern "C" int jb_topk_to_host(const uint64_t* qbits, const float* qnorm, int nq
   return (int)hipGetLastError();
 }
 
-// Latency path by stored rows: query signatures already on the device
-// (e.g. gathered table rows); launch the fused scan/top-k into pinned host
-// memory and wait for it.
-extern "C" int jb_topk_direct_wait(const uint64_t* qbits, const float* qnorm, int nq,
-                                   const uint64_t* tbits, const float* tnorm,
-                                   const uint8_t* valid, int64_t nrows, int words, int hash_num,
-                                   int metric, int k, float* scratch_d, int32_t* scratch_i,
-                                   float* out_d_host, int32_t* out_i_host, uint32_t* done_host,
-                                   hipStream_t stream) {
-  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
-  const uint32_t seq = jb::next_seq();
-  const int rc = jb_topk_to_host(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num,
-                                 metric, k, scratch_d, scratch_i, out_d_host, out_i_host,
-                                 done_host, seq, stream);
+// scratch layout of the sampled path (in scratch_d / scratch_i, sized by
+// jb_topk_direct_scratch): thr[8] | count[8] | candidates [nq][kCandCap]
+constexpr int kCandCap = 16384;
+constexpr int64_t kSampleMax = 16384;
+
+// j for the sampled threshold, 0 when the tile path is the better choice
+static int sample_j(int64_t nrows, int k) {
+  if (nrows < 65536) return 0;
+  const int64_t S = nrows < kSampleMax ? nrows : kSampleMax;
+  const double j = 4.0 * k * (double)S / (double)nrows;
+  const int jj = (int)j + 3;
+  return jj <= 16 ? jj : 0;
+}
+
+extern "C" int64_t jb_topk_direct_scratch(int nq) {
+  return 64 + (int64_t)nq * kCandCap;
+}
+
+static int topk_to_host_any(const uint64_t* qbits, const float* qnorm, int nq,
+                            const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
+                            int64_t nrows, int words, int hash_num, int metric, int k,
+                            float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                            int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                            hipStream_t stream) {
+  const int j = sample_j(nrows, k);
+  if (j == 0)
+    return topk_to_host_tile(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num,
+                             metric, k, scratch_d, scratch_i, out_d_host, out_i_host, done_host,
+                             seq, stream);
+  jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
+  float* thr = scratch_d;                         // [8]
+  int* count = scratch_i;                         // [8]
+  float* cand_d = scratch_d + 64;
+  int32_t* cand_i = scratch_i + 64;
+  const int64_t S = nrows < kSampleMax ? nrows : kSampleMax;
+  hipLaunchKernelGGL(jb::topk_sample_kernel<0>, dim3(nq), dim3(jb::kSampleThreads), 0, stream, s,
+                     nrows, S, j, thr, count);
+  int64_t cblocks = (nrows + 1023) / 1024;        // 4 rows per thread
+  if (cblocks > 1024) cblocks = 1024;
+  hipLaunchKernelGGL(jb::topk_collect_kernel<0>, dim3((unsigned)cblocks, nq), dim3(256), 0, stream,
+                     s, nrows, thr, kCandCap, cand_d, cand_i, count);
+  hipLaunchKernelGGL(jb::topk_final_kernel, dim3(nq), dim3(1024), 0, stream, cand_d, cand_i,
+                     count, kCandCap, k, thr, out_d_host, out_i_host,
+                     (volatile uint32_t*)done_host, seq);
+  return (int)hipGetLastError();
+}
+
+// launch + wait; a sampled run whose threshold missed reruns the tile path
+static int topk_direct_run(const uint64_t* qbits, const float* qnorm, int nq,
+                           const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
+                           int64_t nrows, int words, int hash_num, int metric, int k,
+                           float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                           int32_t* out_i_host, uint32_t* done_host, hipStream_t stream) {
+  uint32_t seq = jb::next_seq();
+  int rc = topk_to_host_any(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric,
+                            k, scratch_d, scratch_i, out_d_host, out_i_host, done_host, seq,
+                            stream);
+  if (rc != 0) return rc;
+  bool retry = false;
+  rc = jb::wait_flags_status(done_host, nq, seq, jb::kTopRetry, stream, &retry);
+  if (rc != 0 || !retry) return rc;
+  seq = jb::next_seq();
+  rc = topk_to_host_tile(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, k,
+                         scratch_d, scratch_i, out_d_host, out_i_host, done_host, seq, stream);
   if (rc != 0) return rc;
   return jb::wait_flags(done_host, nq, seq, stream);
 }
+
+// query signatures on the device -> top-k in pinned host memory, waited for
+extern "C" int jb_topk_direct_query(const uint64_t* qbits, const float* qnorm, int nq,
+                                    const uint64_t* tbits, const float* tnorm,
+                                    const uint8_t* valid, int64_t nrows, int words, int hash_num,
+                                    int metric, int k, float* scratch_d, int32_t* scratch_i,
+                                    float* out_d_host, int32_t* out_i_host, uint32_t* done_host,
+                                    hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  if (k > jb::kTopMaxK || words > jb::kTopMaxWords || nq > 8) return -2;
+  return topk_direct_run(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, k,
+                         scratch_d, scratch_i, out_d_host, out_i_host, done_host, stream);
+}
+

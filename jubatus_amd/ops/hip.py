@@ -46,12 +46,13 @@ _SIGS = {
     "jb_topk": [_i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
                 _i32, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_topk_blocks": [_i64, _i32],
+    "jb_topk_direct_scratch": [_i32],
     "jb_lsh_query_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _u64, _i32, _i32, _c_void_p,
                             _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_lsh_set_rows_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _u64, _i32,
                                _c_void_p, _c_void_p, _c_void_p, _c_void_p],
-    "jb_topk_direct_wait": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
+    "jb_topk_direct_query": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
                             _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                             _c_void_p, _c_void_p],
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
@@ -374,6 +375,11 @@ def diag_empty(done: HostBuffer, spin: bool, stream: int | None = None) -> None:
 
 
 QUERY_MAX = 8          # csrc/hip/lsh.hip kQueryMax
+
+
+def _direct_scratch(nrows: int, k: int, nq: int) -> int:
+    """scratch of the latency top-k: tile path (blocks * k) or sampled path"""
+    return max(nq * _fn("jb_topk_blocks")(nrows, k) * k, _fn("jb_topk_direct_scratch")(nq))
 QUERY_SLOTS = 256      # kQuerySlots
 
 
@@ -401,8 +407,7 @@ def lsh_query_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, nq: int, hash
     _dev(tnorm, torch.float32, "tnorm")
     if tbits.numel() < nrows * words or valid.numel() < nrows or tnorm.numel() < nrows:
         raise ValueError("lsh_query_direct: bad table shapes")
-    blocks = _fn("jb_topk_blocks")(nrows, k)
-    sd, si = _topk_scratch(tbits.device, nq * blocks * k)
+    sd, si = _topk_scratch(tbits.device, _direct_scratch(nrows, k, nq))
     rc = _fn("jb_lsh_query_direct")(idx_ptr, val_ptr, row_ptr_ptr, nq, hash_num, seed & (2**64 - 1),
                                     mode, metric, _p(tbits), _p(tnorm), _p(valid), nrows, k,
                                     _p(bufs.qbits), _p(bufs.qnorm), _p(sd), _p(si), bufs.out_d.ptr,
@@ -439,12 +444,11 @@ def topk_rows_direct(qbits, qnorm, nq: int, tbits, tnorm, valid, nrows: int, has
     words = (hash_num + 63) // 64
     if not (0 < k <= TOPK_MAX_K and words <= TOPK_MAX_WORDS and 0 < nq <= QUERY_MAX):
         return None
-    blocks = _fn("jb_topk_blocks")(nrows, k)
-    sd, si = _topk_scratch(tbits.device, nq * blocks * k)
-    rc = _fn("jb_topk_direct_wait")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid),
+    sd, si = _topk_scratch(tbits.device, _direct_scratch(nrows, k, nq))
+    rc = _fn("jb_topk_direct_query")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid),
                                     nrows, words, hash_num, metric, k, _p(sd), _p(si),
                                     bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
-    _check(rc, "jb_topk_direct_wait")
+    _check(rc, "jb_topk_direct_query")
     d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
     i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
     return d, i

@@ -219,3 +219,43 @@ def test_direct_set_row_and_query_match_batch_paths(method):
         rb = a.query_fv(fv, 10, True)           # batch query path
         assert [s for _, s in ra] == pytest.approx([s for _, s in rb], rel=1e-5, abs=1e-6)
         assert [r for r, _ in ra] == [r for r, _ in rb]
+
+
+@pytest.mark.parametrize("case,k", [("random", 1), ("random", 10), ("random", 100),
+                                    ("random", 128), ("ties", 10), ("sparse_valid", 20)])
+def test_direct_topk_sampled_path(case, k):
+    """latency top-k on large tables (sampled threshold -> collect -> exact
+    final, csrc/hip/topk.hip) == full distance matrix + stable sort; "ties"
+    (every row at the same distance: the candidate buffer overflows) and
+    "sparse_valid" (fewer valid rows than k would need) exercise the retry /
+    +inf-threshold paths"""
+    import torch
+    from jubatus_amd.ops import hip
+    d = dev()
+    n = 200_000
+    g = torch.Generator().manual_seed(k + len(case))
+    tb = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
+    tn = torch.rand(n, generator=g)
+    valid = torch.ones(n, dtype=torch.uint8)
+    if case == "ties":
+        tb[:] = 12345
+        tn[:] = 0.5
+    if case == "sparse_valid":
+        valid[:] = 0
+        valid[::20000] = 1
+    qb = tb[:2].clone()
+    qb[1] ^= 0x5555
+    qn = tn[:2].clone()
+    tbd, tnd, vd, qbd, qnd = (x.to(d) for x in (tb, tn, valid, qb, qn))
+    bufs = hip.DirectQueryBuffers(d, 1)
+    od, oi = hip.topk_rows_direct(qbd, qnd, 2, tbd, tnd, vd, n, 64, 1, k, bufs)
+    full = torch.empty((2, n), dtype=torch.float32, device=d)
+    hip.hamming_scan(qbd, qnd, 2, tbd, tnd, vd, n, 64, 1, full)
+    full = full.cpu().numpy()
+    for q in range(2):
+        order = np.argsort(full[q], kind="stable")[:k]
+        ref = full[q][order]
+        fin = np.isfinite(ref)
+        np.testing.assert_array_equal(oi[q][:fin.sum()], order[fin])
+        np.testing.assert_allclose(od[q][:fin.sum()], ref[fin], rtol=1e-6)
+        assert np.all(np.isinf(od[q][fin.sum():]))
