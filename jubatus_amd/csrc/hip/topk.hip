@@ -622,12 +622,14 @@ static int topk_to_host_tile(const uint64_t* qbits, const float* qnorm, int nq,
 
 // scratch layout of the sampled path (in scratch_d / scratch_i, sized by
 // jb_topk_direct_scratch): thr[8] | count[8] | candidates [nq][kCandCap]
-constexpr int kCandCap = 16384;
+constexpr int kCandCap = 65536;
 constexpr int64_t kSampleMax = 16384;
 
 // j for the sampled threshold, 0 when the tile path is the better choice
+// (below ~2M rows the tile path is as fast, and it cannot overflow on rows
+// that tie at the threshold - e.g. duplicated data)
 static int sample_j(int64_t nrows, int k) {
-  if (nrows < 65536) return 0;
+  if (nrows < (int64_t)2 << 20) return 0;
   const int64_t S = nrows < kSampleMax ? nrows : kSampleMax;
   const double j = 4.0 * k * (double)S / (double)nrows;
   const int jj = (int)j + 3;

@@ -232,7 +232,7 @@ def test_direct_topk_sampled_path(case, k):
     import torch
     from jubatus_amd.ops import hip
     d = dev()
-    n = 200_000
+    n = 2_200_000
     g = torch.Generator().manual_seed(k + len(case))
     tb = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
     tn = torch.rand(n, generator=g)
@@ -242,7 +242,7 @@ def test_direct_topk_sampled_path(case, k):
         tn[:] = 0.5
     if case == "sparse_valid":
         valid[:] = 0
-        valid[::20000] = 1
+        valid[::220000] = 1
     qb = tb[:2].clone()
     qb[1] ^= 0x5555
     qn = tn[:2].clone()
