@@ -88,6 +88,34 @@ struct DatumShape {
   uint32_t n_str = 0, n_num = 0, n_bin = 0;
 };
 
+// Fast paths for the common encodings, used while at least kFastSlack bytes
+// remain (so no per-byte bounds checks are needed):
+//   string pair  0x92, fixraw key, fixraw value
+//   num pair     0x92, fixraw key, positive/negative fixint | float32 | float64
+// Anything else falls back to the checked cursor.
+constexpr size_t kFastSlack = 80;
+
+inline bool skip_str_pair_fast(Cursor& c) {
+  const uint8_t* p = c.p;
+  if (p[0] != 0x92 || (p[1] & 0xe0) != 0xa0) return false;
+  const uint8_t* q = p + 2 + (p[1] & 0x1f);
+  if ((q[0] & 0xe0) != 0xa0) return false;
+  c.p = q + 1 + (q[0] & 0x1f);
+  return true;
+}
+
+inline bool skip_num_pair_fast(Cursor& c) {
+  const uint8_t* p = c.p;
+  if (p[0] != 0x92 || (p[1] & 0xe0) != 0xa0) return false;
+  const uint8_t* q = p + 2 + (p[1] & 0x1f);
+  const uint8_t t = q[0];
+  if (t <= 0x7f || t >= 0xe0) c.p = q + 1;
+  else if (t == 0xcb) c.p = q + 9;
+  else if (t == 0xca) c.p = q + 5;
+  else return false;
+  return true;
+}
+
 // Validate one datum [sv, nv, bv] and count its pairs.
 inline bool scan_datum(Cursor& c, DatumShape* d) {
   uint32_t top;
@@ -95,12 +123,14 @@ inline bool scan_datum(Cursor& c, DatumShape* d) {
   uint32_t ns;
   if (!c.array(&ns)) return false;
   for (uint32_t i = 0; i < ns; ++i) {
+    if ((size_t)(c.end - c.p) >= kFastSlack && skip_str_pair_fast(c)) continue;
     uint32_t two; const uint8_t* s; uint32_t n;
     if (!c.array(&two) || two != 2 || !c.raw(&s, &n) || !c.raw(&s, &n)) return false;
   }
   uint32_t nn;
   if (!c.array(&nn)) return false;
   for (uint32_t i = 0; i < nn; ++i) {
+    if ((size_t)(c.end - c.p) >= kFastSlack && skip_num_pair_fast(c)) continue;
     uint32_t two; const uint8_t* s; uint32_t n; double x;
     if (!c.array(&two) || two != 2 || !c.raw(&s, &n) || !c.number(&x)) return false;
   }
