@@ -126,12 +126,14 @@ TOOLS = {
                         ["coord", "native", "../client_cpp/include"]),
     "jubaproxy": (["proxy/jubaproxy.cpp", "native/jb_rpc.cpp"],
                   ["proxy", "native", "../client_cpp/include"]),
+    "jubavisor": (["visor/jubavisor.cpp", "native/jb_rpc.cpp"],
+                  ["visor", "native", "../client_cpp/include"]),
     "jubaloadgen": (["tools/jubaloadgen.cpp", "native/jb_rpc.cpp"], ["native"]),
 }
 
 
 def build_tools(force: bool = False, nproc: int = 8, sanitize: str | None = None) -> str:
-    """Python-free native executables (coordinator, proxy). ``sanitize``
+    """Python-free native executables (coordinator, proxy, jubavisor, load generator). ``sanitize``
     ("address", "thread", "undefined") builds instrumented copies into
     native_bin/<sanitizer>/ (the reference's --fsanitize build option,
     wscript:55-57,143-146; host code only)."""

@@ -141,3 +141,67 @@ def test_proxy_concurrent_fanout(san, tmp_path):
     text = (tmp_path / "proxy.err").read_text()
     assert not _reports(text), text[-4000:]
     assert prc in (0, -15), (prc, text[-2000:])
+
+
+def test_jubavisor_spawn_stop_reap(san, tmp_path):
+    """supervisor start / stop / reap paths with concurrent RPCs; the children
+    are a stand-in program (JUBAVISOR_SERVER_DIR) so no engine server runs"""
+    kind, bindir = san
+    coord, cerr = _start_coord(bindir, tmp_path)
+    sdir = tmp_path / "servers"
+    sdir.mkdir()
+    fake = sdir / "jubafake"
+    fake.write_text("#!/bin/sh\nexec sleep 30\n")
+    fake.chmod(0o755)
+    quick = sdir / "jubaquick"
+    quick.write_text("#!/bin/sh\nexit 0\n")
+    quick.chmod(0o755)
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    vport = s.getsockname()[1]
+    s.close()
+    verr = open(tmp_path / "visor.err", "w")
+    visor = subprocess.Popen([os.path.join(bindir, "jubavisor"), "-p", str(vport), "-b", "127.0.0.1",
+                              "-z", f"127.0.0.1:{coord.port}", "-m", "8"],
+                             stdout=subprocess.PIPE, stderr=verr, text=True,
+                             env=dict(os.environ, JUBAVISOR_SERVER_DIR=str(sdir), **SAN_ENV))
+    vrc = None
+    try:
+        assert visor.stdout.readline().startswith("jubavisor ready")
+        errors = []
+
+        def client(i):
+            try:
+                c = RpcClient("127.0.0.1", vport, 20)
+                for j in range(5):
+                    assert c.call("start", f"jubafake/n{i}", 1, [0] * 19) == 0
+                    assert c.call("start", f"jubaquick/q{i}", 1, [0] * 19) == 0
+                    assert c.call("start", "bad", 1, [0] * 19) == -1
+                    assert c.call("stop", f"jubafake/n{i}", 1) == 0
+                c.close()
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+        ts = [threading.Thread(target=client, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors
+        c = RpcClient("127.0.0.1", vport, 20)
+        # quick children exited and were reaped: their ports are back, so a
+        # full pool of 8 long-running children fits
+        import time
+        time.sleep(0.5)
+        assert c.call("start", "jubafake/full", 8, [0] * 19) == 0
+        c.close()
+    finally:
+        visor.terminate()       # stops the 8 children too
+        vrc = visor.wait(60)
+        verr.close()
+        coord.stop()
+        cerr.close()
+    text = (tmp_path / "visor.err").read_text()
+    assert not _reports(text), text[-4000:]
+    assert vrc in (0, -15), (vrc, text[-2000:])
+    assert text.count("stopped jubafake/full") == 8, text[-2000:]

@@ -6,6 +6,7 @@ import io
 import json
 import os
 import socket
+import subprocess
 import time
 
 import pytest
@@ -15,9 +16,10 @@ from jubatus_amd.cmd.jubavisor import Jubavisor, argv_from_wire, argv_to_wire, s
 from jubatus_amd.common import membership as mb
 from jubatus_amd.common.coordinator import CoordinatorServer
 from jubatus_amd.common.lock_service import CoordinatorClient
-from jubatus_amd.common.mprpc import RpcServer
+from jubatus_amd.common.mprpc import RpcClient, RpcMethodNotFound, RpcServer
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NATIVE_BIN_DIR = os.path.join(ROOT, "jubatus_amd", "native_bin")
 
 
 def free_port():
@@ -80,6 +82,34 @@ def test_jubavisor_wire_helpers():
     assert jubactl.split_counts(5, 2) == [3, 2] and jubactl.split_counts(0, 3) == [1, 1, 1]
 
 
+def _cluster_roundtrip(zk, ls, tmp_path):
+    """jubactl start 2 / status / save / load / stop against the registered supervisor(s)"""
+    out = []
+    assert jubaconfig.main(["-c", "write", "-f", os.path.join(ROOT, "config/classifier/arow.json"),
+                            "-t", "classifier", "-n", "cl", "-z", zk], out=out.append) == 0
+    common = ["-s", "jubaclassifier", "-n", "cl", "-t", "classifier", "-z", zk]
+    assert jubactl.main(["-c", "start", "-N", "2", "-D", str(tmp_path), "-S", "0", "-I", "0", *common]) == 0
+    nodes_path = mb.build_actor_path("classifier", "cl") + "/nodes"
+    deadline = time.time() + 90
+    while len(ls.list(nodes_path)) < 2 and time.time() < deadline:
+        time.sleep(0.3)
+    nodes = ls.list(nodes_path)
+    assert len(nodes) == 2, nodes
+    assert jubactl.main(["-c", "status", *common]) == 0
+    assert jubactl.main(["-c", "save", "-i", "m1", *common]) == 0
+    saved = [f for f in os.listdir(tmp_path) if f.endswith("m1.jubatus")]
+    assert len(saved) == 2, os.listdir(tmp_path)
+    assert jubactl.main(["-c", "load", "-i", "m1", *common]) == 0
+    # jubadump reads one of the saved models
+    dumped = jubadump.dump(os.path.join(tmp_path, saved[0]))
+    assert dumped["system"]["type"] == "classifier" and dumped["model"]["method"] == "AROW"
+    assert jubactl.main(["-c", "stop", *common]) == 0
+    deadline = time.time() + 30
+    while ls.list(nodes_path) and time.time() < deadline:
+        time.sleep(0.3)
+    assert ls.list(nodes_path) == []
+
+
 def test_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
@@ -91,31 +121,79 @@ def test_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     rpc.listen(vport, "127.0.0.1")
     rpc.start()
     ls = CoordinatorClient(zk, timeout=5.0)
-    out = []
     try:
-        assert jubaconfig.main(["-c", "write", "-f", os.path.join(ROOT, "config/classifier/arow.json"),
-                                "-t", "classifier", "-n", "cl", "-z", zk], out=out.append) == 0
-        common = ["-s", "jubaclassifier", "-n", "cl", "-t", "classifier", "-z", zk]
-        assert jubactl.main(["-c", "start", "-N", "2", "-D", str(tmp_path), "-S", "0", "-I", "0", *common]) == 0
-        deadline = time.time() + 90
-        while len(ls.list(mb.build_actor_path("classifier", "cl") + "/nodes")) < 2 and time.time() < deadline:
-            time.sleep(0.3)
-        nodes = ls.list(mb.build_actor_path("classifier", "cl") + "/nodes")
-        assert len(nodes) == 2, nodes
-        assert jubactl.main(["-c", "status", *common]) == 0
-        assert jubactl.main(["-c", "save", "-i", "m1", *common]) == 0
-        saved = [f for f in os.listdir(tmp_path) if f.endswith("m1.jubatus")]
-        assert len(saved) == 2, os.listdir(tmp_path)
-        assert jubactl.main(["-c", "load", "-i", "m1", *common]) == 0
-        # jubadump reads one of the saved models
-        dumped = jubadump.dump(os.path.join(tmp_path, saved[0]))
-        assert dumped["system"]["type"] == "classifier" and dumped["model"]["method"] == "AROW"
-        assert jubactl.main(["-c", "stop", *common]) == 0
-        deadline = time.time() + 30
-        while ls.list(mb.build_actor_path("classifier", "cl") + "/nodes") and time.time() < deadline:
-            time.sleep(0.3)
-        assert ls.list(mb.build_actor_path("classifier", "cl") + "/nodes") == []
+        _cluster_roundtrip(zk, ls, tmp_path)
     finally:
         rpc.stop()
         visor.close()
         ls.close()
+
+
+def _native_visor(zk, vport, tmp_path, maxc=4):
+    exe = os.path.join(NATIVE_BIN_DIR, "jubavisor")
+    if not os.access(exe, os.X_OK):
+        pytest.skip("native jubavisor not built (python -m jubatus_amd.build_ext)")
+    err = open(tmp_path / "visor.err", "w")
+    p = subprocess.Popen([exe, "-p", str(vport), "-z", zk, "-m", str(maxc), "-b", "127.0.0.1"],
+                         stdout=subprocess.PIPE, stderr=err, text=True)
+    line = p.stdout.readline()
+    assert line.startswith("jubavisor ready"), (line, (tmp_path / "visor.err").read_text())
+    return p, err
+
+
+def test_native_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
+    monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
+    zk = f"127.0.0.1:{coord.port}"
+    vport = free_port()
+    proc, err = _native_visor(zk, vport, tmp_path)
+    ls = CoordinatorClient(zk, timeout=5.0)
+    try:
+        assert ls.list(mb.JUBAVISOR_BASE_PATH) == [f"127.0.0.1_{vport}"]
+        _cluster_roundtrip(zk, ls, tmp_path)
+    finally:
+        proc.terminate()
+        rc = proc.wait(30)
+        err.close()
+        ls.close()
+    assert rc == 0, (tmp_path / "visor.err").read_text()[-2000:]
+
+
+def test_native_jubavisor_rpc_errors_and_shutdown(coord, tmp_path, monkeypatch):
+    """bad names / arity, pool exhaustion, and SIGTERM stopping the children"""
+    monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
+    zk = f"127.0.0.1:{coord.port}"
+    vport = free_port()
+    proc, err = _native_visor(zk, vport, tmp_path, maxc=1)
+    ls = CoordinatorClient(zk, timeout=5.0)
+    argv = argv_to_wire({"threadnum": 2, "timeout": 10, "interval_sec": 0, "interval_count": 0,
+                         "datadir": str(tmp_path), "mixer": "linear_mixer"})
+    assert jubaconfig.main(["-c", "write", "-f", os.path.join(ROOT, "config/classifier/pa.json"),
+                            "-t", "classifier", "-n", "cx", "-z", zk], out=lambda *a, **k: None) == 0
+    try:
+        with RpcClient("127.0.0.1", vport, 10.0) as c:
+            assert c.call("start", "classifier", 1, argv) == -1          # not juba<engine>/<name>
+            assert c.call("start", "jubaclassifier/", 1, argv) == -1
+            assert c.call("stop", "nothing", 1) == -1
+            assert c.call("stop", "jubaclassifier/none", 1) == 0
+            with pytest.raises(RpcMethodNotFound):
+                c.call("restart", "jubaclassifier/x", 1)
+            with pytest.raises(Exception):
+                c.call("start", "jubaclassifier/x")                       # arity
+            assert c.call("start", "jubaclassifier/cx", 2, argv) == -1    # pool of 1 port
+            assert c.call("start", "jubaclassifier/cx", 1, argv) == 0
+        nodes_path = mb.build_actor_path("classifier", "cx") + "/nodes"
+        deadline = time.time() + 90
+        while not ls.list(nodes_path) and time.time() < deadline:
+            time.sleep(0.3)
+        assert ls.list(nodes_path) == [f"127.0.0.1_{vport + 1}"]
+    finally:
+        proc.terminate()          # the supervisor takes its children down with it
+        rc = proc.wait(30)
+        err.close()
+    deadline = time.time() + 30
+    while ls.list(nodes_path) and time.time() < deadline:
+        time.sleep(0.3)
+    assert ls.list(nodes_path) == []
+    assert ls.list(mb.JUBAVISOR_BASE_PATH) == []
+    ls.close()
+    assert rc == 0
