@@ -2,7 +2,7 @@
 # One GPU-box session: build, GPU tests, smoke, bench, rocprofv3 stats.
 # Stops at the first step that faults / aborts / times out (exit 124, 134,
 # 137, 139 or signal); plain test failures (exit 1) do not stop the session.
-# Usage: tools/gpu_session.sh [steps...]   steps: build tests alltests smoke kbench scan bench prof
+# Usage: tools/gpu_session.sh [steps...]   steps: build tests alltests smoke kbench scan engines bench prof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -32,6 +32,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     kbench) run kbench 300 python tools/bench_train_kernel.py ;;
     scan) run scan 300 python tools/bench_scan.py ;;
+    engines) run engines 900 python tools/bench_engines.py ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)
       rm -rf "$OUT/prof"
