@@ -8,12 +8,14 @@ server can answer random-routed queries over all rows.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import threading
 from typing import Any
 
 from ..fv_converter.converter import DatumToFvConverter
 from ..fv_converter.datum import Datum, as_datum
-from .rows import RowStore, Unlearner, datum_to_dicts, dicts_to_datum
+from .rows import RowStore, Unlearner, as_dicts, datum_to_dicts, dicts_to_datum, dicts_wire
 from .similarity import InvertedIndex, LshIndex
 
 LSH_METHODS = ("lsh", "euclid_lsh", "minhash")
@@ -30,6 +32,19 @@ def make_index(method: str, parameter: dict, device: Any):
         return InvertedIndex(True, device)
     raise ValueError(f"unknown similarity method: {method}")
 
+
+
+@contextlib.contextmanager
+def _gc_paused():
+    """no cyclic-GC passes while a bulk ingest allocates millions of small
+    objects (with a large live heap, collections cost more than the work)"""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 class RowEngine:
     def __init__(self, method: str, parameter: dict | None, converter: DatumToFvConverter,
@@ -79,6 +94,10 @@ class RowEngine:
     def _set_many(self, items: list, bump: bool = True, update_weight: bool = True) -> None:
         """set many rows at once: one native hashing pass over all datums and
         one bulk index insert (signatures of every row in one launch)."""
+        with _gc_paused():
+            self._set_many_impl(items, bump, update_weight)
+
+    def _set_many_impl(self, items: list, bump: bool, update_weight: bool) -> None:
         h = self._hasher()
         if h is None or len(items) < 2 or self.unlearner.kind:
             # (the lru unlearner interleaves evictions with inserts: sequential)
@@ -87,7 +106,7 @@ class RowEngine:
             return
         import msgpack
         import numpy as np
-        body = msgpack.packb([dicts_to_datum(*d).to_msgpack() for _, d in items], use_bin_type=False)
+        body = msgpack.packb([dicts_wire(d) for _, d in items], use_bin_type=False)
         n = len(items)
         cap = max(1024, 64 * n)
         while True:
@@ -101,26 +120,22 @@ class RowEngine:
             if err:
                 raise ValueError("malformed datum in bulk row update")
             break
-        slots = np.empty(n, np.int64)
-        for i, (rid, dicts) in enumerate(items):
-            a, b = rp[i], rp[i + 1]
-            keep = idx[a:b] >= 0
-            fv = (idx[a:b][keep].tolist(), val[a:b][keep].tolist())
-            slots[i] = self.rows.put(rid, dicts, fv, bump)
+        nnz = int(rp[n])
+        idx, val = idx[:nnz], val[:nnz]
+        slots = self.rows.put_many(items, rp, idx, val, bump)
         # a row set twice in one batch: the last write wins (same as sequential)
         last = {}
         for i, (rid, _) in enumerate(items):
             last[rid] = i
-        if len(last) != n:
-            sel = np.asarray(sorted(last.values()), np.int64)
+        if len(last) == n:
+            self.index.set_rows_csr(slots, rp, idx, val)
         else:
-            sel = np.arange(n, dtype=np.int64)
-        lens = rp[sel + 1] - rp[sel]
-        rp2 = np.zeros(sel.size + 1, np.int64)
-        np.cumsum(lens, out=rp2[1:])
-        gather = np.concatenate([np.arange(rp[i], rp[i + 1]) for i in sel]) if sel.size else \
-            np.zeros(0, np.int64)
-        self.index.set_rows_csr(slots[sel], rp2, idx[gather], val[gather])
+            sel = np.asarray(sorted(last.values()), np.int64)
+            lens = rp[sel + 1] - rp[sel]
+            rp2 = np.zeros(sel.size + 1, np.int64)
+            np.cumsum(lens, out=rp2[1:])
+            gather = np.repeat(rp[sel] - rp2[:-1], lens) + np.arange(int(rp2[-1]), dtype=np.int64)
+            self.index.set_rows_csr(slots[sel], rp2, idx[gather], val[gather])
         for rid, _ in items:
             for victim in self.unlearner.touch(rid):
                 if victim != rid:
@@ -151,8 +166,8 @@ class RowEngine:
 
     def set_rows(self, items: list) -> int:
         """bulk set_row: [(id, datum)] -> number of rows written"""
-        with self._lock:
-            self._set_many([(rid, datum_to_dicts(as_datum(d))) for rid, d in items])
+        with self._lock, _gc_paused():
+            self._set_many([(rid, as_dicts(d)) for rid, d in items])
             return len(items)
 
     def _remove(self, rid: str, record: bool = True) -> bool:

@@ -10,11 +10,108 @@ import threading
 from collections import OrderedDict
 from typing import Any
 
-from ..fv_converter.datum import Datum
+from ..common.exceptions import ArgumentError
+from ..fv_converter.datum import Datum, _b, _s, as_datum
 
 
 def datum_to_dicts(d: Datum) -> tuple[dict, dict, dict]:
     return (dict(d.string_values), dict(d.num_values), dict(d.binary_values))
+
+
+def as_dicts(x: Any) -> tuple[dict, dict, dict]:
+    """datum (Datum, {key: value} or the wire array) -> (string, num, binary)
+    dicts, without building a Datum for the common input forms (the bulk
+    row-ingest path; same validation as Datum.from_msgpack / Datum.add)"""
+    if isinstance(x, (list, tuple)) and len(x) in (2, 3):
+        try:
+            sv = {_s(k): _s(v) for k, v in x[0]}
+            nv = {}
+            for k, v in x[1]:
+                if isinstance(v, bool) or not isinstance(v, (int, float)):
+                    raise ArgumentError("num_values value must be a number")
+                nv[_s(k)] = float(v)
+            bv = {_s(k): (v if isinstance(v, bytes) else _b(v)) for k, v in x[2]} if len(x) == 3 else {}
+        except (ValueError, TypeError) as e:
+            raise ArgumentError(f"malformed datum: {e}") from e
+        return sv, nv, bv
+    if isinstance(x, dict):
+        # fast path: only str and float / int values
+        sv = {k: v for k, v in x.items() if type(v) is str}
+        nv = {k: float(v) for k, v in x.items() if type(v) is float or type(v) is int}
+        if len(sv) + len(nv) == len(x):
+            return sv, nv, {}
+        sv, nv, bv = {}, {}, {}
+        for k, v in x.items():
+            if isinstance(v, str):
+                sv[k] = v
+            elif isinstance(v, (int, float)):        # bool included, as Datum.add
+                nv[k] = float(v)
+            elif isinstance(v, (bytes, bytearray, memoryview)):
+                bv[k] = bytes(v)
+            else:
+                raise ArgumentError(f"unsupported datum value type {type(v)!r} for key {k!r}")
+        return sv, nv, bv
+    return datum_to_dicts(as_datum(x))
+
+
+def dicts_wire(d: tuple[dict, dict, dict]) -> list:
+    """(sv, nv, bv) -> the datum wire array with sorted keys (the feature
+    order dicts_to_datum(...).to_msgpack() gives)"""
+    sv, nv, bv = d
+    return [sorted(sv.items()), sorted(nv.items()), sorted(bv.items()) if bv else []]
+
+
+class _CsrBatch:
+    __slots__ = ("rp", "idx", "val")
+
+    def __init__(self, rp, idx, val):
+        self.rp, self.idx, self.val = rp, idx, val
+
+
+class FvTable:
+    """slot -> hashed feature vector ([idx], [val]). Rows written in bulk keep
+    a reference into their batch's CSR arrays and become Python lists only
+    when read (most rows are never read back on the host: queries use the
+    signatures in HBM)."""
+
+    def __init__(self):
+        self._d: dict[int, Any] = {}
+
+    def __setitem__(self, slot: int, fv) -> None:
+        self._d[slot] = fv
+
+    def put_batch(self, slots, rp, idx, val) -> None:
+        b = _CsrBatch(rp, idx, val)
+        d = self._d
+        for i, s in enumerate(slots.tolist()):
+            d[s] = (b, i)
+
+    def __getitem__(self, slot: int):
+        fv = self._d[slot]
+        if isinstance(fv[0], _CsrBatch):
+            b, i = fv
+            a, e = int(b.rp[i]), int(b.rp[i + 1])
+            ix = b.idx[a:e]
+            keep = ix >= 0
+            fv = (ix[keep].tolist(), b.val[a:e][keep].tolist())
+            self._d[slot] = fv
+        return fv
+
+    def get(self, slot: int, default=None):
+        return self[slot] if slot in self._d else default
+
+    def pop(self, slot: int, default=None):
+        if slot not in self._d:
+            return default
+        v = self[slot]
+        del self._d[slot]
+        return v
+
+    def __contains__(self, slot: int) -> bool:
+        return slot in self._d
+
+    def __len__(self) -> int:
+        return len(self._d)
 
 
 def dicts_to_datum(sv: dict, nv: dict, bv: dict | None = None) -> Datum:
@@ -65,7 +162,7 @@ class RowStore:
         self.slot_of: dict[str, int] = {}
         self.free: list[int] = []
         self.datum: dict[int, tuple[dict, dict, dict]] = {}
-        self.fv: dict[int, tuple[list[int], list[float]]] = {}
+        self.fv = FvTable()
         self.version: dict[str, int] = {}
         self.dirty: set[str] = set()      # rows changed since the last MIX
         self.removed: set[str] = set()
@@ -99,6 +196,24 @@ class RowStore:
             self.dirty.add(rid)
             self.removed.discard(rid)
         return s
+
+    def put_many(self, items: list, rp, idx, val, bump: bool = True):
+        """bulk put: items [(rid, dicts)], their feature vectors as one CSR
+        (rp / idx / val, row i = items[i]); returns the slots (int64 array)"""
+        import numpy as np
+        slots = np.fromiter((self.assign(rid) for rid, _ in items), np.int64, len(items))
+        datum = self.datum
+        for s, (_, dicts) in zip(slots.tolist(), items):
+            datum[s] = dicts
+        self.fv.put_batch(slots, rp, idx, val)
+        if bump:
+            version = self.version
+            for rid, _ in items:
+                version[rid] = version.get(rid, 0) + 1
+            self.dirty.update(rid for rid, _ in items)
+            if self.removed:
+                self.removed.difference_update(rid for rid, _ in items)
+        return slots
 
     def remove(self, rid: str, record: bool = True) -> int | None:
         s = self.slot_of.pop(rid, None)

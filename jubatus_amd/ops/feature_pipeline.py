@@ -40,6 +40,17 @@ def _grow(cap: int, need: int) -> int:
     return c
 
 
+def scan_threads() -> int:
+    """host scanner threads for this process: the CPUs it may run on, shared
+    by the ranks of this node (one process per GPU), at most 16"""
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        ncpu = os.cpu_count() or 4
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    return max(1, min(16, ncpu // local))
+
+
 @dataclass
 class DeviceBatch:
     n: int
@@ -135,7 +146,7 @@ class FeaturePipeline:
         self.device = torch.device(device)
         self.H = converter.hash_max_size
         self.fast = gpu_eligible(converter)
-        self.nthreads = nthreads or max(1, min(16, (os.cpu_count() or 4)))
+        self.nthreads = nthreads or scan_threads()
         self._pinned = [_Pinned(), _Pinned()]
         self._turn = 0
         self._devsets = [_DeviceBufs(self.device), _DeviceBufs(self.device)]
