@@ -18,6 +18,8 @@ giant-lock-free classifier (ChangeLog.rst:152).
 """
 from __future__ import annotations
 
+import collections
+import os
 import threading
 from typing import Any, Sequence
 
@@ -82,6 +84,12 @@ class LinearClassifier:
         self.device = device
         self.gpu = device is not None
         self.direct = True        # single-launch path for small classify requests
+        # train batches scanned on the GPU (csrc/hip/scan.hip); their checks
+        # complete asynchronously (_drain)
+        self.gpu_scan = os.environ.get("JUBATUS_GPU_SCAN", "1") != "0"
+        self._pending: collections.deque = collections.deque()
+        self._free_checks: list = []
+        self._draining = False
         self._result_cols = None
         self.LC = 0
         self._label_version = -1
@@ -152,16 +160,68 @@ class LinearClassifier:
 
     def train_arena(self, arena, offs, lens) -> int:
         """Train on request bodies that already sit in a pinned RequestArena
-        (zero-copy receive path; one stream per span)."""
+        (zero-copy receive path; one stream per span).
+
+        With the GPU scan the call returns once the batch is queued: the
+        arena spans must stay unchanged until the next call into this model
+        (which checks the batch; a batch the device scan could not take -
+        new labels, binary values, malformed bytes - is then re-run through
+        the host scanner, which adds labels / raises as before)."""
         with self._lock:
             if not (self.gpu and self.pipe.fast):
                 bodies = [bytes(arena.np[o:o + n]) for o, n in zip(offs, lens)]
                 return self.train_requests(bodies)
+            if self.gpu_scan and self.labels.size() > 0:
+                self._drain(block=len(self._pending) >= 4)
+                self._sync_labels()
+                chk = self._check_record(self.labels.size())
+                b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk)
+                if b is not None:
+                    n = self._train_batch(b)
+                    chk.replay = lambda: self._train_batch(
+                        self.pipe.from_arena(arena, offs, lens, True, self.labels))
+                    self._pending.append(chk)
+                    return n
+                self._free_checks.append(chk)
+            self._drain(block=True)
             return self._train_batch(self.pipe.from_arena(arena, offs, lens, True, self.labels))
+
+    def _check_record(self, nhist: int):
+        from ..ops.feature_pipeline import ScanCheck
+        while self._free_checks:
+            c = self._free_checks.pop()
+            if c.hist.numel() >= nhist:
+                return c
+        return ScanCheck(max(64, nhist * 2))
+
+    def _drain(self, block: bool = True) -> None:
+        """process completed GPU-scan checks in order (all of them when
+        block): label counts of accepted batches, host re-run of rejected ones"""
+        if self._draining:
+            return
+        self._draining = True
+        try:
+            while self._pending:
+                c = self._pending[0]
+                if not block and not c.done():
+                    break
+                c.wait()
+                self._pending.popleft()
+                replay, c.replay = c.replay, None
+                if int(c.err[0]):
+                    replay()
+                else:
+                    h = c.hist.numpy()[:c.nhist]
+                    for lid in np.flatnonzero(h).tolist():
+                        self.labels.add_count(lid, int(h[lid]))
+                self._free_checks.append(c)
+        finally:
+            self._draining = False
 
     def train_requests(self, bodies: Sequence[Any]) -> int:
         """Train on raw msgpack ``list<labeled_datum>`` bodies (one stream each)."""
         with self._lock:
+            self._drain()
             if self.gpu and self.pipe.fast:
                 return self._train_batch(self.pipe.from_requests(list(bodies), True, self.labels))
             total = 0
@@ -186,6 +246,7 @@ class LinearClassifier:
             body = _pack_body([[lab, as_datum(d).to_msgpack()] for lab, d in data])
             return self.train_requests([body])
         with self._lock:
+            self._drain()
             rows, labs = [], []
             for lab, d in data:
                 rows.append(self.conv.hashed(self.conv.convert_and_update_weight(as_datum(d))))
@@ -222,6 +283,7 @@ class LinearClassifier:
 
     def classify_requests(self, bodies: Sequence[Any]) -> list[list[tuple[str, float]]]:
         with self._lock:
+            self._drain()
             if self.gpu and self.pipe.fast:
                 from ..ops import hip
                 self._sync_labels()
@@ -247,6 +309,7 @@ class LinearClassifier:
             return self.classify_requests([_pack_body([as_datum(d).to_msgpack() for d in data])])
         rows = [self.conv.hashed(self.conv.convert(as_datum(d))) for d in data]
         with self._lock:
+            self._drain()
             self._sync_labels()
             if self.gpu:
                 from ..ops import hip
@@ -261,12 +324,15 @@ class LinearClassifier:
 
     # ------------------------------------------------------------- labels
     def get_labels(self) -> dict[str, int]:
+        with self._lock:
+            self._drain()
         names = self.labels.names()
         alive = self.labels.alive()
         return {n: int(self.labels.count(i)) for i, n in enumerate(names) if alive[i]}
 
     def set_label(self, label: str) -> bool:
         with self._lock:
+            self._drain()
             if self.labels.lookup(label) >= 0:
                 return False
             self.labels.get_or_add(label)
@@ -275,6 +341,7 @@ class LinearClassifier:
 
     def delete_label(self, label: str) -> bool:
         with self._lock:
+            self._drain()
             i = self.labels.lookup(label)
             if i < 0:
                 return False
@@ -287,6 +354,7 @@ class LinearClassifier:
 
     def clear(self) -> None:
         with self._lock:
+            self._drain()
             self.labels.clear()
             self.LC = 0
             self._alloc(LABEL_CAPS[0])
@@ -294,6 +362,8 @@ class LinearClassifier:
 
     # ------------------------------------------------------------ persist
     def synchronize(self) -> None:
+        with self._lock:
+            self._drain()
         if self.gpu:
             self.torch.cuda.synchronize(self.device)
 
@@ -312,6 +382,7 @@ class LinearClassifier:
         (P = diagonal precision of CW/AROW/NHERD).
         """
         with self._lock:
+            self._drain()
             self.synchronize()
             W, S = self._host_tables()
             names = self.labels.names()
@@ -338,6 +409,7 @@ class LinearClassifier:
     def unpack(self, obj: dict) -> None:
         obj = {(k.decode() if isinstance(k, bytes) else k): v for k, v in obj.items()}
         with self._lock:
+            self._drain()
             if int(obj["H"]) != self.H:
                 raise ValueError("model hash_max_size differs from the configuration")
             labels = [(x.decode() if isinstance(x, bytes) else x) for x in obj["labels"]]
@@ -411,6 +483,7 @@ class LinearClassifier:
         Returns the number of bytes all-reduced per rank."""
         from ..parallel import collective as coll
         with self._lock:
+            self._drain()
             names = self.labels.names()
             alive = self.labels.alive()
             fp = coll.fingerprint([n + ("+" if a else "-") for n, a in zip(names, alive)])
@@ -442,6 +515,7 @@ class LinearClassifier:
         import torch
         from ..parallel import collective as coll
         with self._lock:
+            self._drain()
             names = self.labels.names()
             alive = self.labels.alive()
             fp = coll.fingerprint([n + ("+" if a else "-") for n, a in zip(names, alive)])
@@ -483,6 +557,7 @@ class LinearClassifier:
             w.wait()
         n = coll.world() if coll.is_dist() else 1
         with self._lock:
+            self._drain()
             loc, red = self._mix_bufs
             for t, r, l in zip(self._tables(), red, loc):
                 if self.gpu:
@@ -531,6 +606,7 @@ class LinearClassifier:
         """hand the whole model to a newly joined member (obsolete protocol)"""
         import torch.distributed as dist
         with self._lock:
+            self._drain()
             names = self.labels.names()
             meta = [[names, [int(self.labels.count(i)) for i in range(len(names))],
                      self.labels.alive()]]
@@ -557,6 +633,7 @@ class LinearClassifier:
         import torch
         import torch.distributed as dist
         with self._lock:
+            self._drain()
             me = dist.get_rank()
             mine = [self._live_labels()]
             theirs = [None]

@@ -51,6 +51,81 @@ def scan_threads() -> int:
     return max(1, min(16, ncpu // local))
 
 
+
+def fnv1a64(b: bytes) -> int:
+    h = 0xCBF29CE484222325
+    for x in b:
+        h = ((h ^ x) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def label_table_arrays(names: list, alive: list) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """the device label table of csrc/hip/scan.hip: open addressing on
+    FNV-1a 64 of the label bytes; meta = [blob offset, length, id] (id -1:
+    empty). Only live labels are entered (a deleted one goes to the host
+    path, which revives it)."""
+    live = [(i, n.encode("utf-8", "surrogateescape")) for i, (n, a) in enumerate(zip(names, alive))
+            if a]
+    cap = 16
+    while cap < 2 * len(live):
+        cap *= 2
+    th = np.zeros(cap, np.uint64)
+    tm = np.full(3 * cap, -1, np.int32)
+    blob = bytearray()
+    mask = cap - 1
+    for lid, b in live:
+        h = fnv1a64(b)
+        j = h & mask
+        while tm[3 * j + 2] >= 0:
+            j = (j + 1) & mask
+        th[j] = h
+        tm[3 * j:3 * j + 3] = (len(blob), len(b), lid)
+        blob += b
+    return th.view(np.int64), tm, np.frombuffer(bytes(blob) or b"\0", np.uint8).copy()
+
+
+def body_counts(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> np.ndarray | None:
+    """element count of each body's top-level array header, None if any
+    body does not start with one (the host scanner reports those)"""
+    if offs.size == 0:
+        return np.zeros(0, np.int64)
+    if (lens < 1).any():
+        return None
+    t = buf[offs].astype(np.int64)
+    n = np.full(offs.size, -1, np.int64)
+    fix = (t & 0xF0) == 0x90
+    n[fix] = t[fix] & 0x0F
+    m16 = (t == 0xDC) & (lens >= 3)
+    if m16.any():
+        o = offs[m16]
+        n[m16] = (buf[o + 1].astype(np.int64) << 8) | buf[o + 2]
+    m32 = (t == 0xDD) & (lens >= 5)
+    if m32.any():
+        o = offs[m32]
+        n[m32] = ((buf[o + 1].astype(np.int64) << 24) | (buf[o + 2].astype(np.int64) << 16)
+                  | (buf[o + 3].astype(np.int64) << 8) | buf[o + 4])
+    return None if (n < 0).any() else n
+
+
+class ScanCheck:
+    """completion record of a GPU-scanned train batch: the batch's error
+    bits and label counts land in pinned memory when ``event`` completes"""
+
+    def __init__(self, nhist: int):
+        self.err = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.hist = torch.zeros(max(1, nhist), dtype=torch.int32, pin_memory=True)
+        self.event: torch.cuda.Event | None = None
+        self.replay = None        # re-runs the batch through the host scanner
+        self.nhist = 0
+
+    def done(self) -> bool:
+        return self.event is None or self.event.query()
+
+    def wait(self) -> None:
+        if self.event is not None:
+            self.event.synchronize()
+
+
 @dataclass
 class DeviceBatch:
     n: int
@@ -155,6 +230,9 @@ class FeaturePipeline:
         self._last_mark: torch.cuda.Event | None = None
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._direct = None
+        self._scan_meta = [None, None]    # pinned [req_off | req_len | sample_base] per turn
+        self._scan_meta_ev = [None, None]
+        self._ltab = None                 # (label version, device hash, meta, blob)
         if self.fast:
             rt = GpuRuleTable(converter)
             self.rules = rt
@@ -223,6 +301,100 @@ class FeaturePipeline:
                 raise RuntimeError("label table full")
             break
         return self._launch(pin, arena.buf, n, nbytes, nslots, R, labeled)
+
+    def label_table(self, table) -> tuple:
+        v = table.version()
+        if self._ltab is None or self._ltab[0] != v:
+            th, tm, blob = label_table_arrays(table.names(), table.alive())
+            self._ltab = (v, torch.from_numpy(th).to(self.device),
+                          torch.from_numpy(tm).to(self.device), torch.from_numpy(blob).to(self.device))
+        return self._ltab[1:]
+
+    def from_arena_gpu(self, arena: RequestArena, offs: np.ndarray, lens: np.ndarray, table,
+                       check: ScanCheck) -> DeviceBatch | None:
+        """Train batch from arena spans with the scan on the GPU
+        (csrc/hip/scan.hip): H2D of the raw arena, then scan -> fixup ->
+        fv_hash on the compute stream, no host walk. ``check`` receives the
+        batch's error bits and label counts (pinned, valid once its event
+        completes); a batch with error bits set trained nothing and must be
+        re-run through from_arena. None: a body header the host must report."""
+        if not self.fast:
+            raise RuntimeError("converter config is not eligible for the GPU fast path")
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int64)
+        counts = body_counts(arena.np, offs, lens)
+        if counts is None:
+            return None
+        R = int(offs.size)
+        sbase = np.zeros(R + 1, np.int64)
+        np.cumsum(counts, out=sbase[1:])
+        n = int(sbase[-1])
+        used = int((offs + lens).max()) if R else 0
+        empty_off = ((used + 15) & ~15) + 16
+        buf_need = empty_off + 16
+        sps, spn = self.rules.n_srules, self.rules.n_nrules
+        slot_cap = (used // 3 + 1) * max(1, sps, spn)
+        # the same alternation as from_arena/_launch: toggle, then use the
+        # device set of the new turn (so a host-path batch after this one
+        # never lands on the set this batch's kernels are still reading)
+        self._turn ^= 1
+        turn = self._turn
+        ev = self._scan_meta_ev[turn]
+        if ev is not None:
+            ev.synchronize()
+        meta = self._scan_meta[turn]
+        if meta is None or meta.numel() < 3 * R + 1:
+            meta = self._scan_meta[turn] = torch.empty(_grow(1024, 3 * R + 1), dtype=torch.int64,
+                                                       pin_memory=True)
+        mnp = meta.numpy()
+        mnp[:R] = offs
+        mnp[R:2 * R] = lens
+        mnp[2 * R:3 * R + 1] = sbase
+        compute = torch.cuda.current_stream(self.device)
+        dev = self._devsets[turn]
+        prev_mark = self._last_mark
+        mark = torch.cuda.Event()
+        mark.record(compute)
+        self._last_mark = mark
+        d_buf = dev.get("buf", buf_need, torch.uint8)
+        d_meta = dev.get("scan_meta", 3 * R + 1, torch.int64)
+        d_off = dev.get("datum_off", max(n, 1), torch.int64)
+        d_len = dev.get("datum_len", max(n, 1), torch.int32)
+        d_row = dev.get("row_ptr", n + 1, torch.int64)
+        d_lab = dev.get("labels", max(n, 1), torch.int32)
+        d_slots = dev.get("req_slots", max(R, 1), torch.int64)
+        d_idx = dev.get("fidx", slot_cap, torch.int32)
+        d_val = dev.get("fval", slot_cap, torch.float32)
+        d_hist = dev.get("label_hist", check.hist.numel(), torch.int32)
+        d_err = dev.get("scan_err", 1, torch.int32)
+        cs = self._copy_stream
+        if prev_mark is not None:
+            cs.wait_event(prev_mark)
+        else:
+            cs.wait_stream(compute)
+        with torch.cuda.stream(cs):
+            if used:
+                d_buf[:used].copy_(arena.buf[:used], non_blocking=True)
+            d_meta[:3 * R + 1].copy_(meta[:3 * R + 1], non_blocking=True)
+        cev = torch.cuda.Event()
+        cev.record(cs)
+        self._scan_meta_ev[turn] = cev
+        compute.wait_event(cev)
+        th, tm, tb = self.label_table(table)
+        d_sb = d_meta[2 * R:3 * R + 1]
+        nh = check.hist.numel()
+        hip.scan_train(d_buf, used, d_meta[:R], d_meta[R:2 * R], d_sb, R, n, th, tm, tb, sps, spn,
+                       d_off, d_len, d_lab, d_row, d_slots, d_hist[:nh], d_err, empty_off)
+        check.err.copy_(d_err[:1], non_blocking=True)
+        check.hist.copy_(d_hist[:nh], non_blocking=True)
+        check.nhist = nh
+        check.event = torch.cuda.Event()
+        check.event.record(compute)
+        if n > 0:
+            hip.fv_hash(d_buf, empty_off + 3, d_off, d_len, d_row, n, self.d_srules,
+                        self.rules.n_srules, self.d_nrules, self.rules.n_nrules, self.d_blob, self.H,
+                        d_idx, d_val, self.err)
+        return DeviceBatch(n, slot_cap, R, d_row, d_idx, d_val, d_lab, d_sb)
 
     def _launch(self, pin: "_Pinned", src: torch.Tensor, n: int, nbytes: int, nslots: int,
                 R: int, labeled: bool) -> DeviceBatch:

@@ -56,6 +56,9 @@ _SIGS = {
                             _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                             _c_void_p, _c_void_p],
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
+    "jb_scan_train": [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
+                      _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                      _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -235,6 +238,42 @@ def fv_hash(buf: torch.Tensor, buf_len: int, datum_off: torch.Tensor, datum_len:
                            _p(row_ptr), n, _p(srules), n_srules, _p(nrules), n_nrules, _p(blob),
                            blob.numel(), H, _p(out_idx), _p(out_val), _p(err), _stream())
     _check(rc, "jb_fv_hash")
+
+
+def scan_train(buf: torch.Tensor, buf_used: int, req_off: torch.Tensor, req_len: torch.Tensor,
+               sample_base: torch.Tensor, R: int, n: int, lt_hash: torch.Tensor,
+               lt_meta: torch.Tensor, lt_blob: torch.Tensor, sps: int, spn: int,
+               datum_off: torch.Tensor, datum_len: torch.Tensor, labels: torch.Tensor,
+               row_ptr: torch.Tensor, req_slots: torch.Tensor, hist: torch.Tensor,
+               err: torch.Tensor, empty_off: int) -> None:
+    """GPU scan of R train bodies already in ``buf`` (csrc/hip/scan.hip).
+    ``buf_used`` = end of the last body; the buffer needs 16 B of slack past
+    it and 3 writable bytes at ``empty_off``."""
+    for t, dt, name in ((buf, torch.uint8, "buf"), (req_off, torch.int64, "req_off"),
+                        (req_len, torch.int64, "req_len"), (sample_base, torch.int64, "sample_base"),
+                        (lt_hash, torch.int64, "lt_hash"), (lt_meta, torch.int32, "lt_meta"),
+                        (lt_blob, torch.uint8, "lt_blob"), (datum_off, torch.int64, "datum_off"),
+                        (datum_len, torch.int32, "datum_len"), (labels, torch.int32, "labels"),
+                        (row_ptr, torch.int64, "row_ptr"), (req_slots, torch.int64, "req_slots"),
+                        (hist, torch.int32, "hist"), (err, torch.int32, "err")):
+        _dev(t, dt, name)
+    cap = lt_hash.numel()
+    if cap <= 0 or cap & (cap - 1) or lt_meta.numel() < 3 * cap:
+        raise ValueError("scan_train: label table capacity must be a power of two")
+    if req_off.numel() < R or req_len.numel() < R or sample_base.numel() < R + 1 or \
+            req_slots.numel() < R:
+        raise ValueError("scan_train: request arrays shorter than R")
+    if datum_off.numel() < n or datum_len.numel() < n or labels.numel() < n or \
+            row_ptr.numel() < n + 1:
+        raise ValueError("scan_train: sample arrays shorter than n")
+    if buf.numel() < buf_used + 16 or buf.numel() < empty_off + 3 or buf.numel() % 4:
+        raise ValueError("scan_train: buffer lacks the 16-B slack / the stand-in datum")
+    rc = _fn("jb_scan_train")(_p(buf), buf.numel(), _p(req_off), _p(req_len), _p(sample_base), R, _p(lt_hash),
+                              _p(lt_meta), cap, _p(lt_blob), lt_blob.numel(), sps, spn,
+                              _p(datum_off), _p(datum_len), _p(labels), _p(row_ptr),
+                              _p(req_slots), _p(hist), hist.numel(), _p(err),
+                              buf.data_ptr() + empty_off, empty_off, _stream())
+    _check(rc, "jb_scan_train")
 
 
 def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
