@@ -172,6 +172,11 @@ def main() -> None:
                 finish_mix()
                 pending[0] = clf.mix_begin(meta_group=meta)
 
+    # setup objects (synthetic bodies, torch modules) move to the permanent
+    # generation, so a cyclic-GC pass in the timed loop does not traverse them
+    import gc
+    gc.collect()
+    gc.freeze()
     for i in range(args.warmup):
         step(i)
     finish_mix()
@@ -180,14 +185,21 @@ def main() -> None:
     sync()
     barrier()
     sync()
+    trace_steps = os.environ.get("JB_BENCH_TRACE") == "1"
+    marks = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+        if trace_steps:
+            marks.append(time.perf_counter())
     finish_mix()          # the last MIX completes inside the timed region
     sync()
     barrier()
     sync()
     elapsed = time.perf_counter() - t0
+    if trace_steps and rank == 0:
+        d = np.diff([t0] + marks) * 1e3
+        print("step host ms: " + " ".join(f"{x:.2f}" for x in d), file=sys.stderr)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device if device is not None else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -63,6 +63,56 @@ __device__ __forceinline__ uint32_t byte_at(const uint8_t* q, int p, int len) {
   return p < len ? q[p] : 0u;
 }
 
+// Header byte(s) read without the len check: q points into the LDS stage,
+// whose bytes past the request are stale but in bounds (`lim` = readable
+// positions from q). A token decoded from them runs past len, which ends
+// the walk; positions >= len are never marked.
+__device__ __forceinline__ uint32_t byte_fast(const uint8_t* q, int p, int lim) {
+  return q[min(p, lim - 1)];
+}
+
+// (arity - 1) of the token at p, the only quantity the depth scan needs:
+// containers give their element count - 1, everything else -1
+__device__ __forceinline__ int token_d(const uint8_t* q, int p, int lim) {
+  const uint32_t t = byte_fast(q, p, lim);
+  if ((t & 0xe0) == 0x80) return (t <= 0x8f ? 2 * (int)(t & 0x0f) : (int)(t & 0x0f)) - 1;
+  if (t < 0xdc || t > 0xdf) return -1;
+  const uint32_t b1 = byte_fast(q, p + 1, lim), b2 = byte_fast(q, p + 2, lim);
+  if (t == 0xdc) return (int)((b1 << 8) | b2) - 1;
+  if (t == 0xde) return 2 * (int)((b1 << 8) | b2) - 1;
+  uint32_t n = (b1 << 24) | (b2 << 16) | (byte_fast(q, p + 3, lim) << 8) | byte_fast(q, p + 4, lim);
+  if (n > 0x3fffffffu) n = 0x3fffffffu;
+  return (t == 0xdd ? (int)n : 2 * (int)n) - 1;
+}
+
+// size of the token at p (containers: header only), unchecked reads
+__device__ __forceinline__ int token_size(const uint8_t* q, int p, int lim) {
+  const uint32_t t = byte_fast(q, p, lim);
+  if (t <= 0x9f || t >= 0xe0) return 1;              // fixint, fixmap, fixarray, negative fixint
+  if (t <= 0xbf) return 1 + (int)(t & 0x1f);          // fixraw
+  const uint32_t b1 = byte_fast(q, p + 1, lim);
+  switch (t) {
+    case 0xc4: case 0xd9: case 0xc7: return (t == 0xc7 ? 3 : 2) + (int)b1;
+    case 0xc5: case 0xda: case 0xc8:
+      return (t == 0xc8 ? 4 : 3) + (int)((b1 << 8) | byte_fast(q, p + 2, lim));
+    case 0xc6: case 0xdb: case 0xc9: {
+      uint32_t n = (b1 << 24) | (byte_fast(q, p + 2, lim) << 16) |
+                   (byte_fast(q, p + 3, lim) << 8) | byte_fast(q, p + 4, lim);
+      if (n > 0x3fffffffu) n = 0x3fffffffu;
+      return (t == 0xc9 ? 6 : 5) + (int)n;
+    }
+    case 0xca: case 0xce: case 0xd2: case 0xdd: case 0xdf: return 5;
+    case 0xcb: case 0xcf: case 0xd3: return 9;
+    case 0xcc: case 0xd0: case 0xd4: return t == 0xd4 ? 3 : 2;
+    case 0xcd: case 0xd1: case 0xdc: case 0xde: return 3;
+    case 0xd5: return 4;
+    case 0xd6: return 6;
+    case 0xd7: return 10;
+    case 0xd8: return 18;
+    default: return 1;                                  // nil, false, true, 0xc1
+  }
+}
+
 // size of the token at p if one starts there (containers: header only) and
 // its element count (arrays / maps; 0 otherwise)
 __device__ __forceinline__ int token(const uint8_t* q, int p, int len, int* arity) {
@@ -213,7 +263,7 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
     int64_t* __restrict__ datum_off, int32_t* __restrict__ datum_len,
     int32_t* __restrict__ labels, int64_t* __restrict__ row_ptr,
     int64_t* __restrict__ req_slots, uint32_t* __restrict__ hist, int nhist,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, long long* __restrict__ prof) {
   __shared__ __attribute__((aligned(16))) uint8_t s_req[kScanBytes];
   __shared__ uint32_t s_bits[kBitWords];      // token starts; later the per-sample slot counts
   __shared__ uint16_t s_exit[kThreads];       // where chunk t's walk left the chunk
@@ -233,6 +283,7 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
   const int k = blockIdx.x;
   const int t = threadIdx.x;
   if (k >= R) return;
+  if (prof && t == 0) prof[8 * k + 6] = (long long)__builtin_amdgcn_s_memtime();
   const int64_t off = req_off[k];
   const int64_t len64 = req_len[k];
   const int64_t s0 = sample_base[k], nsamples = sample_base[k + 1] - s0;
@@ -270,27 +321,37 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
   if (t == 0) s_err = 0;
   __syncthreads();
 
-  // ---- 1. speculative walk of chunk t
+  if (prof && t == 0) prof[8 * k + 0] = (long long)__builtin_amdgcn_s_memtime();
+  // ---- 1. speculative walk of chunk t (bits gathered per word, one LDS
+  // atomic per 32 positions)
   const int C = (len + kThreads - 1) / kThreads;
   const int cb = min(t * C, len), ce = min(cb + C, len);
+  const int lim = kScanBytes - rel;
   {
-    int p = cb, a;
+    int p = cb, word = cb >> 5;
+    uint32_t acc = 0;
     while (p < ce) {
-      atomicOr(&s_bits[p >> 5], 1u << (p & 31));
-      p += token(q, p, len, &a);
+      if ((p >> 5) != word) {
+        if (acc) atomicOr(&s_bits[word], acc);
+        word = p >> 5;
+        acc = 0;
+      }
+      acc |= 1u << (p & 31);
+      p += token_size(q, p, lim);
     }
+    if (acc) atomicOr(&s_bits[word], acc);
     s_exit[t] = (uint16_t)min(p, len);
   }
   __syncthreads();
 
+  if (prof && t == 0) prof[8 * k + 1] = (long long)__builtin_amdgcn_s_memtime();
   // ---- 2. extension of chunk t's walk until it meets a later chunk's walk
   {
-    int p = s_exit[t], a, steps = 0;
+    int p = s_exit[t], steps = 0;   // p >= the end of chunk t: any marked p is a later chunk's
     int tc = kThreads;
     while (p < len) {
-      const int u = C > 0 ? p / C : 0;
-      if (u > t && bit(s_bits, p)) { tc = u; break; }
-      p += token(q, p, len, &a);
+      if (bit(s_bits, p)) { tc = p / C; break; }
+      p += token_size(q, p, lim);
       if (++steps > kExtMax) { tc = -1; break; }
     }
     s_tc[t] = (uint16_t)(tc < 0 ? 0xffff : tc);
@@ -298,6 +359,7 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
   }
   __syncthreads();
 
+  if (prof && t == 0) prof[8 * k + 2] = (long long)__builtin_amdgcn_s_memtime();
   // ---- 3. the true chain: chunk 0 -> its convergence chunk -> ... (reach
   // from chunk 0 by pointer doubling, 8 rounds for 256 chunks)
   {
@@ -336,15 +398,16 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
   __syncthreads();
   // ... and mark the chain's extensions
   if (s_valid[t]) {
-    int p = s_exit[t], a;
+    int p = s_exit[t];
     const int stop = s_conv[t];
     while (p < stop) {
       atomicOr(&s_bits[p >> 5], 1u << (p & 31));
-      p += token(q, p, len, &a);
+      p += token_size(q, p, lim);
     }
   }
   __syncthreads();
 
+  if (prof && t == 0) prof[8 * k + 3] = (long long)__builtin_amdgcn_s_memtime();
   // ---- 4. depth scan: samples start where sum(arity - 1) hits a new minimum
   int lsum = 0, lmin = 0x7fffffff;
   if (cb < ce)
@@ -353,10 +416,8 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
       while (m) {
         const int p = 32 * w + __builtin_ctz(m);
         m &= m - 1;
-        int a;
-        token(q, p, len, &a);
         lmin = min(lmin, lsum);
-        lsum += a - 1;
+        lsum += token_d(q, p, lim);
       }
     }
   int total;
@@ -380,14 +441,12 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
         while (m) {
           const int p = 32 * w + __builtin_ctz(m);
           m &= m - 1;
-          int a;
-          token(q, p, len, &a);
           if (h < mn) {               // a new minimum: sample -h starts here
             if (-h < nsamples) s_start[-h] = (uint16_t)p;
             else atomicOr(&s_err, kErrMalformed);
             mn = h;
           }
-          h += a - 1;
+          h += token_d(q, p, lim);
         }
       }
   }
@@ -397,6 +456,7 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
     return;
   }
 
+  if (prof && t == 0) prof[8 * k + 4] = (long long)__builtin_amdgcn_s_memtime();
   // ---- 5. one thread per sample
   const uint64_t* th = lab_lds ? s_th : lt_hash;
   const int32_t* tm = lab_lds ? s_tm : lt_meta;
@@ -434,20 +494,28 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
       if (s_err) atomicOr(err, s_err);
     }
   }
+  if (prof && t == 0) prof[8 * k + 5] = (long long)__builtin_amdgcn_s_memtime();
   if (s_err) return;
   const int top = nhist < kHist ? nhist : kHist;
   for (int i = t; i < top; i += kThreads)
     if (s_hist[i]) atomicAdd(&hist[i], s_hist[i]);
+  if (prof && t == 0) prof[8 * k + 7] = (long long)__builtin_amdgcn_s_memtime();
 }
 
 __global__ __launch_bounds__(64) void scan_fixup_kernel(
     const int64_t* __restrict__ sample_base, int R, const int64_t* __restrict__ req_slots,
     int64_t* __restrict__ row_ptr, int64_t* __restrict__ datum_off,
     int32_t* __restrict__ datum_len, int32_t* __restrict__ labels, uint8_t* __restrict__ empty_at,
-    int64_t empty_off, const int32_t* __restrict__ err) {
+    int64_t empty_off, const int32_t* __restrict__ err, const uint32_t* __restrict__ hist, int nhist,
+    int32_t* __restrict__ host_out) {
   const int k = blockIdx.x;
   const int lane = threadIdx.x;
   if (k >= R) return;
+  if (k == 0) {   // the batch's check, straight into coherent host memory
+    for (int i = lane; i < nhist; i += 64) host_out[1 + i] = (int32_t)hist[i];
+    if (lane == 0) host_out[0] = *err;
+    __threadfence_system();
+  }
   const int64_t s0 = sample_base[k], s1 = sample_base[k + 1];
   if (*err) {   // the batch goes to the host path: every sample becomes a no-op
     if (k == 0 && lane == 0) {
@@ -479,8 +547,9 @@ __global__ __launch_bounds__(64) void scan_fixup_kernel(
 // from the host's header pass (element count of each body). Outputs are the
 // device arrays of a DeviceBatch; hist[nhist] (label counts of the batch)
 // and *err are zeroed here. empty_at = buf + empty_off must have 3 writable
-// bytes (the stand-in datum of a rejected batch). Returns 0, or 1 on bad
-// arguments.
+// bytes (the stand-in datum of a rejected batch). host_out (fine-grained
+// host memory, 1 + nhist ints) receives [err, hist...] when the batch's
+// fixup kernel completes. Returns 0, or 1 on bad arguments.
 extern "C" int jb_scan_train(const uint8_t* buf, int64_t buf_cap, const int64_t* req_off,
                              const int64_t* req_len,
                              const int64_t* sample_base, int R, const uint64_t* lt_hash,
@@ -488,7 +557,8 @@ extern "C" int jb_scan_train(const uint8_t* buf, int64_t buf_cap, const int64_t*
                              int lt_blob_len, int sps, int spn, int64_t* datum_off,
                              int32_t* datum_len, int32_t* labels, int64_t* row_ptr,
                              int64_t* req_slots, uint32_t* hist, int nhist, int32_t* err,
-                             uint8_t* empty_at, int64_t empty_off, hipStream_t stream) {
+                             uint8_t* empty_at, int64_t empty_off, int32_t* host_out,
+                             hipStream_t stream) {
   if (R <= 0) return 0;
   if (lt_cap <= 0 || (lt_cap & (lt_cap - 1)) != 0 || nhist < 0) return 1;
   if (hipMemsetAsync(err, 0, sizeof(int32_t), stream) != hipSuccess) return 1;
@@ -497,8 +567,26 @@ extern "C" int jb_scan_train(const uint8_t* buf, int64_t buf_cap, const int64_t*
   (void)buf_cap;
   hipLaunchKernelGGL(jb::scan_train_kernel, dim3(R), dim3(jb::kThreads), 0, stream, buf, req_off, req_len,
                      sample_base, R, lt_hash, lt_meta, lt_cap, lt_blob, lt_blob_len, sps, spn,
-                     datum_off, datum_len, labels, row_ptr, req_slots, hist, nhist, err);
+                     datum_off, datum_len, labels, row_ptr, req_slots, hist, nhist, err,
+                     (long long*)nullptr);
   hipLaunchKernelGGL(jb::scan_fixup_kernel, dim3(R), dim3(64), 0, stream, sample_base, R,
-                     req_slots, row_ptr, datum_off, datum_len, labels, empty_at, empty_off, err);
+                     req_slots, row_ptr, datum_off, datum_len, labels, empty_at, empty_off, err,
+                     hist, nhist, host_out);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// Same as jb_scan_train's first kernel, recording s_memtime at the phase
+// boundaries of every workgroup into prof[8 * R] (tools/bench_scan_gpu.py).
+extern "C" int jb_scan_train_profile(const uint8_t* buf, const int64_t* req_off,
+                                     const int64_t* req_len, const int64_t* sample_base, int R,
+                                     const uint64_t* lt_hash, const int32_t* lt_meta, int lt_cap,
+                                     const uint8_t* lt_blob, int lt_blob_len, int sps, int spn,
+                                     int64_t* datum_off, int32_t* datum_len, int32_t* labels,
+                                     int64_t* row_ptr, int64_t* req_slots, uint32_t* hist,
+                                     int nhist, int32_t* err, long long* prof, hipStream_t stream) {
+  if (R <= 0 || lt_cap <= 0 || (lt_cap & (lt_cap - 1)) != 0) return 1;
+  hipLaunchKernelGGL(jb::scan_train_kernel, dim3(R), dim3(jb::kThreads), 0, stream, buf, req_off,
+                     req_len, sample_base, R, lt_hash, lt_meta, lt_cap, lt_blob, lt_blob_len, sps,
+                     spn, datum_off, datum_len, labels, row_ptr, req_slots, hist, nhist, err, prof);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -172,7 +172,7 @@ class LinearClassifier:
                 bodies = [bytes(arena.np[o:o + n]) for o, n in zip(offs, lens)]
                 return self.train_requests(bodies)
             if self.gpu_scan and self.labels.size() > 0:
-                self._drain(block=len(self._pending) >= 4)
+                self._drain(block=True, keep=3)
                 self._sync_labels()
                 chk = self._check_record(self.labels.size())
                 b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk)
@@ -187,23 +187,27 @@ class LinearClassifier:
             return self._train_batch(self.pipe.from_arena(arena, offs, lens, True, self.labels))
 
     def _check_record(self, nhist: int):
+        """a free completion record; allocated in a batch (fine-grained host
+        memory is slow to allocate and synchronises the device)"""
         from ..ops.feature_pipeline import ScanCheck
-        while self._free_checks:
-            c = self._free_checks.pop()
-            if c.hist.numel() >= nhist:
-                return c
-        return ScanCheck(max(64, nhist * 2))
+        while True:
+            while self._free_checks:
+                c = self._free_checks.pop()
+                if c.hist.size >= nhist:
+                    return c
+            self._free_checks = [ScanCheck(max(64, nhist * 2)) for _ in range(8)]
 
-    def _drain(self, block: bool = True) -> None:
-        """process completed GPU-scan checks in order (all of them when
-        block): label counts of accepted batches, host re-run of rejected ones"""
+    def _drain(self, block: bool = True, keep: int = 0) -> None:
+        """process GPU-scan checks in order: label counts of accepted batches,
+        host re-run of rejected ones. block: wait until at most ``keep``
+        batches are outstanding (completed ones are always processed)."""
         if self._draining:
             return
         self._draining = True
         try:
             while self._pending:
                 c = self._pending[0]
-                if not block and not c.done():
+                if not c.done() and not (block and len(self._pending) > keep):
                     break
                 c.wait()
                 self._pending.popleft()
@@ -211,7 +215,7 @@ class LinearClassifier:
                 if int(c.err[0]):
                     replay()
                 else:
-                    h = c.hist.numpy()[:c.nhist]
+                    h = c.hist[:c.nhist]
                     for lid in np.flatnonzero(h).tolist():
                         self.labels.add_count(lid, int(h[lid]))
                 self._free_checks.append(c)

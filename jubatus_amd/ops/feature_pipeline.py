@@ -112,8 +112,10 @@ class ScanCheck:
     bits and label counts land in pinned memory when ``event`` completes"""
 
     def __init__(self, nhist: int):
-        self.err = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        self.hist = torch.zeros(max(1, nhist), dtype=torch.int32, pin_memory=True)
+        nh = max(1, nhist)
+        self.buf = hip.HostBuffer(4 * (1 + nh))   # written by the fixup kernel
+        self.err = self.buf.view(np.int32, 1)
+        self.hist = self.buf.view(np.int32, nh, 4)
         self.event: torch.cuda.Event | None = None
         self.replay = None        # re-runs the batch through the host scanner
         self.nhist = 0
@@ -230,8 +232,18 @@ class FeaturePipeline:
         self._last_mark: torch.cuda.Event | None = None
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._direct = None
-        self._scan_meta = [None, None]    # pinned [req_off | req_len | sample_base] per turn
-        self._scan_meta_ev = [None, None]
+        # GPU-scan batches rotate over their own device sets; a set is reused
+        # once the host has seen its last batch's kernels complete (an event
+        # the host synchronises on, not a cross-stream wait: a copy-engine
+        # copy that waits on a compute-queue event can block the enqueuing
+        # thread for milliseconds)
+        self._gsets = [_DeviceBufs(self.device) for _ in range(4)]
+        self._gnext = 0
+        self._gprev = None
+        self._gfree = [None] * 4          # event: the set's last batch has finished
+        self._scan_meta = [None] * 4      # pinned [req_off | req_len | sample_base] per set
+        self._scan_meta_ev = [None] * 4
+
         self._ltab = None                 # (label version, device hash, meta, blob)
         if self.fast:
             rt = GpuRuleTable(converter)
@@ -334,14 +346,17 @@ class FeaturePipeline:
         buf_need = empty_off + 16
         sps, spn = self.rules.n_srules, self.rules.n_nrules
         slot_cap = (used // 3 + 1) * max(1, sps, spn)
-        # the same alternation as from_arena/_launch: toggle, then use the
-        # device set of the new turn (so a host-path batch after this one
-        # never lands on the set this batch's kernels are still reading)
-        self._turn ^= 1
-        turn = self._turn
-        ev = self._scan_meta_ev[turn]
-        if ev is not None:
-            ev.synchronize()
+        compute = torch.cuda.current_stream(self.device)
+        turn = self._gnext
+        self._gnext = (turn + 1) % len(self._gsets)
+        mark = torch.cuda.Event()
+        mark.record(compute)              # everything queued so far, incl. the previous batch
+        if self._gprev is not None:
+            self._gfree[self._gprev] = mark
+        self._gprev = turn
+        for ev in (self._gfree[turn], self._scan_meta_ev[turn]):
+            if ev is not None:
+                ev.synchronize()
         meta = self._scan_meta[turn]
         if meta is None or meta.numel() < 3 * R + 1:
             meta = self._scan_meta[turn] = torch.empty(_grow(1024, 3 * R + 1), dtype=torch.int64,
@@ -350,12 +365,7 @@ class FeaturePipeline:
         mnp[:R] = offs
         mnp[R:2 * R] = lens
         mnp[2 * R:3 * R + 1] = sbase
-        compute = torch.cuda.current_stream(self.device)
-        dev = self._devsets[turn]
-        prev_mark = self._last_mark
-        mark = torch.cuda.Event()
-        mark.record(compute)
-        self._last_mark = mark
+        dev = self._gsets[turn]
         d_buf = dev.get("buf", buf_need, torch.uint8)
         d_meta = dev.get("scan_meta", 3 * R + 1, torch.int64)
         d_off = dev.get("datum_off", max(n, 1), torch.int64)
@@ -365,13 +375,9 @@ class FeaturePipeline:
         d_slots = dev.get("req_slots", max(R, 1), torch.int64)
         d_idx = dev.get("fidx", slot_cap, torch.int32)
         d_val = dev.get("fval", slot_cap, torch.float32)
-        d_hist = dev.get("label_hist", check.hist.numel(), torch.int32)
+        d_hist = dev.get("label_hist", check.hist.size, torch.int32)
         d_err = dev.get("scan_err", 1, torch.int32)
         cs = self._copy_stream
-        if prev_mark is not None:
-            cs.wait_event(prev_mark)
-        else:
-            cs.wait_stream(compute)
         with torch.cuda.stream(cs):
             if used:
                 d_buf[:used].copy_(arena.buf[:used], non_blocking=True)
@@ -382,11 +388,10 @@ class FeaturePipeline:
         compute.wait_event(cev)
         th, tm, tb = self.label_table(table)
         d_sb = d_meta[2 * R:3 * R + 1]
-        nh = check.hist.numel()
+        nh = check.hist.size
+        check.err[0] = -1                 # not yet written
         hip.scan_train(d_buf, used, d_meta[:R], d_meta[R:2 * R], d_sb, R, n, th, tm, tb, sps, spn,
-                       d_off, d_len, d_lab, d_row, d_slots, d_hist[:nh], d_err, empty_off)
-        check.err.copy_(d_err[:1], non_blocking=True)
-        check.hist.copy_(d_hist[:nh], non_blocking=True)
+                       d_off, d_len, d_lab, d_row, d_slots, d_hist[:nh], d_err, empty_off, check.buf)
         check.nhist = nh
         check.event = torch.cuda.Event()
         check.event.record(compute)

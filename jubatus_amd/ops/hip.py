@@ -58,7 +58,12 @@ _SIGS = {
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
     "jb_scan_train": [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
                       _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
-                      _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _c_void_p],
+                      _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _c_void_p,
+                      _c_void_p],
+    "jb_scan_train_profile": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                              _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                              _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -245,10 +250,11 @@ def scan_train(buf: torch.Tensor, buf_used: int, req_off: torch.Tensor, req_len:
                lt_meta: torch.Tensor, lt_blob: torch.Tensor, sps: int, spn: int,
                datum_off: torch.Tensor, datum_len: torch.Tensor, labels: torch.Tensor,
                row_ptr: torch.Tensor, req_slots: torch.Tensor, hist: torch.Tensor,
-               err: torch.Tensor, empty_off: int) -> None:
+               err: torch.Tensor, empty_off: int, host_out: "HostBuffer") -> None:
     """GPU scan of R train bodies already in ``buf`` (csrc/hip/scan.hip).
     ``buf_used`` = end of the last body; the buffer needs 16 B of slack past
-    it and 3 writable bytes at ``empty_off``."""
+    it and 3 writable bytes at ``empty_off``. ``host_out`` receives [err,
+    label counts...] (int32) when the batch's kernels complete."""
     for t, dt, name in ((buf, torch.uint8, "buf"), (req_off, torch.int64, "req_off"),
                         (req_len, torch.int64, "req_len"), (sample_base, torch.int64, "sample_base"),
                         (lt_hash, torch.int64, "lt_hash"), (lt_meta, torch.int32, "lt_meta"),
@@ -268,11 +274,13 @@ def scan_train(buf: torch.Tensor, buf_used: int, req_off: torch.Tensor, req_len:
         raise ValueError("scan_train: sample arrays shorter than n")
     if buf.numel() < buf_used + 16 or buf.numel() < empty_off + 3 or buf.numel() % 4:
         raise ValueError("scan_train: buffer lacks the 16-B slack / the stand-in datum")
+    if host_out.nbytes < 4 * (1 + hist.numel()):
+        raise ValueError("scan_train: host_out shorter than 1 + len(hist) ints")
     rc = _fn("jb_scan_train")(_p(buf), buf.numel(), _p(req_off), _p(req_len), _p(sample_base), R, _p(lt_hash),
                               _p(lt_meta), cap, _p(lt_blob), lt_blob.numel(), sps, spn,
                               _p(datum_off), _p(datum_len), _p(labels), _p(row_ptr),
                               _p(req_slots), _p(hist), hist.numel(), _p(err),
-                              buf.data_ptr() + empty_off, empty_off, _stream())
+                              buf.data_ptr() + empty_off, empty_off, host_out.ptr, _stream())
     _check(rc, "jb_scan_train")
 
 

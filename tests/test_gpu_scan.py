@@ -96,7 +96,7 @@ def test_gpu_scan_matches_host_scan():
         np.testing.assert_array_equal(h, d, err_msg=name)
     # label counts of the batch
     want = np.bincount(host[2], minlength=16)
-    np.testing.assert_array_equal(chk.hist.numpy()[:16], want)
+    np.testing.assert_array_equal(chk.hist[:16], want)
 
 
 @pytest.mark.parametrize("case", ["unknown_label", "binary_values", "malformed", "too_big"])
