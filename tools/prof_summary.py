@@ -14,6 +14,7 @@ import sys
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*\)$", "", name)        # drop the parameter list
     name = name.replace("void ", "")
     return name if len(name) < 90 else name[:87] + "..."
