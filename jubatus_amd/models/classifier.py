@@ -519,7 +519,7 @@ class LinearClassifier:
         import torch
         from ..parallel import collective as coll
         with self._lock:
-            self._drain()
+            self._drain(block=False)   # batches still in flight join the next MIX
             names = self.labels.names()
             alive = self.labels.alive()
             fp = coll.fingerprint([n + ("+" if a else "-") for n, a in zip(names, alive)])
@@ -561,7 +561,7 @@ class LinearClassifier:
             w.wait()
         n = coll.world() if coll.is_dist() else 1
         with self._lock:
-            self._drain()
+            self._drain(block=False)   # batches still in flight join the next MIX
             loc, red = self._mix_bufs
             for t, r, l in zip(self._tables(), red, loc):
                 if self.gpu:
