@@ -85,7 +85,11 @@ def main() -> None:
     ap.add_argument("--vocab", type=int, default=100000)
     ap.add_argument("--hash-bits", type=int, default=20)
     ap.add_argument("--pools", type=int, default=4, help="distinct synthetic batches cycled")
-    ap.add_argument("--mix-every", type=int, default=1)
+    ap.add_argument("--mix-every", type=int, default=0,
+                    help="N > 0: MIX every N steps; 0 (default): the reference's trigger - a new MIX "
+                         "starts as soon as the previous one has finished and updates arrived "
+                         "(linear_mixer.cpp:337-344,358-390: interval_count 512 updates, the mixer "
+                         "wakes on the threshold), agreed across ranks each step")
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
                     help="how concurrent request streams update shared rows")
@@ -161,11 +165,22 @@ def main() -> None:
             clf.mix_end(pending[0])
             pending[0] = None
 
+    mixes = [0]
+
+    def mix_due(i: int) -> bool:
+        if args.mix_every > 0 or args.mix_mode == "sync":
+            return (i + 1) % max(1, args.mix_every) == 0
+        # adaptive: every rank must agree (the collectives have to match)
+        flag = torch.tensor([1 if clf.mix_ready(pending[0]) else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=meta)
+        return bool(flag.item())
+
     def step(i: int) -> None:
         arena, offs, lens = pools[i % len(pools)]
         n = clf.train_arena(arena, offs, lens)
         assert n == samples_per_step
-        if world > 1 and (i + 1) % args.mix_every == 0:
+        if world > 1 and mix_due(i):
+            mixes[0] += 1
             if args.mix_mode == "sync":
                 clf.mix()
             else:
@@ -187,6 +202,7 @@ def main() -> None:
     sync()
     trace_steps = os.environ.get("JB_BENCH_TRACE") == "1"
     marks = []
+    mixes[0] = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -253,8 +269,10 @@ def main() -> None:
                 "samples_per_request": args.per_request,
                 "hash_max_size": 1 << args.hash_bits,
                 "labels": args.labels,
-                "mix": (f"linear, RCCL all-reduce mean of W and P every {args.mix_every} step(s), "
-                        f"{args.mix_mode}") if world > 1 else "standalone",
+                "mix": (f"linear, RCCL all-reduce mean of W and P, {args.mix_mode}, "
+                        + (f"every {args.mix_every} step(s)" if args.mix_every > 0 else
+                           "back to back (a new MIX as soon as the previous one finished)")
+                        + f"; {mixes[0]} MIXes in the timed steps") if world > 1 else "standalone",
                 "concurrent_update": args.update_mode,
             },
             "classify_latency_us_p50": round(p50, 1),

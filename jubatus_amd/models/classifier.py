@@ -549,6 +549,13 @@ class LinearClassifier:
                     "meta": works, "meta_cnt": meta_cnt, "twork": twork,
                     "nbytes": sum(t.numel() * t.element_size() for t in tables)}
 
+    @staticmethod
+    def mix_ready(h: dict | None) -> bool:
+        """True when an overlapped MIX's collectives have finished (non-blocking)"""
+        if h is None or "sync" in h:
+            return True
+        return all(w is None or w.is_completed() for w in list(h["meta"]) + list(h["twork"]))
+
     def mix_end(self, h: dict) -> int:
         """Finish a ``mix_begin``; returns the bytes all-reduced per rank."""
         from ..parallel import collective as coll
