@@ -93,6 +93,9 @@ def main() -> None:
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
                     help="how concurrent request streams update shared rows")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="gloo: rehearse the multi-rank GPU path with several ranks on one GPU "
+                         "(not a benchmark configuration)")
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
                     help="cpu: host engine + gloo, for rehearsing the multi-rank path without a GPU "
                          "(not a benchmark configuration)")
@@ -111,10 +114,15 @@ def main() -> None:
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if args.device == "gpu":
+        if args.dist_backend == "gloo":
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
         if world > 1:
-            dist.init_process_group("nccl", device_id=device)
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group("gloo")
     else:
         device = None
         if world > 1:
