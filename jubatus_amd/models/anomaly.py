@@ -120,20 +120,26 @@ class LOF(RowEngine):
             return math.inf
         return mean_lo / lp
 
-    def _invalidate_near(self, fv, rid: str) -> None:
+    def _invalidate_near(self, fv, rid: str) -> list[tuple[str, float]]:
+        """drop the cached kdist / lrd the change of ``rid`` can affect;
+        returns its reverse_nearest_neighbor_num nearest rows"""
         self._kdist.pop(rid, None)
         self._lrd.pop(rid, None)
-        for o, _ in self._neighbors_fv(fv, self.rnn, exclude=rid):
+        near = self._neighbors_fv(fv, self.rnn, exclude=rid)
+        for o, _ in near:
             self._kdist.pop(o, None)
             self._lrd.pop(o, None)
         # lrd depends on the neighbours' kdist: drop every cached lrd
         self._lrd.clear()
+        return near
 
     def _insert(self, rid: str, dicts) -> float:
         self._set(rid, dicts)
         fv = self.rows.fv[self.rows.slot(rid)]
-        self._invalidate_near(fv, rid)
-        return self._score(self._neighbors_id(rid, self.k))
+        near = self._invalidate_near(fv, rid)
+        # the k nearest are the head of the rnn-nearest list (same query,
+        # rnn >= k): no second search
+        return self._score(near[:self.k])
 
     # ---------------------------------------------------------------- API
     def add(self, rid: str, d) -> float:
