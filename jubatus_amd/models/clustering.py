@@ -95,7 +95,12 @@ class Clustering:
         import torch
         return torch
 
-    def _dense(self, pts: list[dict], dims: list[str]):
+    # below this many matrix elements the coreset / Lloyd / EM steps run on
+    # the host: a bucket (1000 x a few hundred) is too small to amortise the
+    # launches and the host round trip each k-means++ draw needs
+    GPU_MIN_ELEMS = 1 << 22
+
+    def _dense(self, pts: list[dict], dims: list[str], device=None):
         torch = self._t()
         pos = {n: i for i, n in enumerate(dims)}
         X = np.zeros((len(pts), len(dims)), dtype=np.float32)
@@ -105,10 +110,12 @@ class Clustering:
                 if j is not None:
                     X[r, j] = v
         t = torch.from_numpy(X)
-        return t.to(self.device) if self.gpu else t
+        if device is not None:
+            return t.to(device)
+        return t.to(self.device) if self.gpu and X.size >= self.GPU_MIN_ELEMS else t
 
     def _sqdist(self, X, C):
-        if self.gpu:
+        if X.is_cuda:
             from ..ops import hip
             return hip.sqdist(X.contiguous(), C.contiguous())
         xn = (X * X).sum(1, keepdim=True)
@@ -261,7 +268,7 @@ class Clustering:
         fv: dict[str, float] = {}
         for name, v in self.conv.convert(as_datum(d)):
             fv[name] = fv.get(name, 0.0) + float(v)
-        X = self._dense([fv], self.dims)
+        X = self._dense([fv], self.dims, self.centers.device)
         return int(self._assign(X)[0])
 
     def get_nearest_center(self, d) -> Datum:

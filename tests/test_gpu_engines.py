@@ -131,7 +131,10 @@ def test_sqdist_mfma_matches_fp32(n, k, d):
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4 * d)
 
 
-def test_clustering_on_gpu_matches_cpu():
+@pytest.mark.parametrize("gpu_min_elems", [0, None])
+def test_clustering_on_gpu_matches_cpu(gpu_min_elems):
+    """0: every step on the device (MFMA sqdist, torch on HBM); None: the
+    default size rule (this small problem runs on the host)"""
     from jubatus_amd.models.clustering import Clustering
     p = {"k": 3, "compressor_method": "compressive_kmeans", "bucket_size": 90,
          "compressed_bucket_size": 30, "seed": 0}
@@ -140,7 +143,10 @@ def test_clustering_on_gpu_matches_cpu():
     pts = [{"x": cx + r.gauss(0, 0.3), "y": cy + r.gauss(0, 0.3)}
            for i in range(180) for cx, cy in [[(0, 0), (8, 8), (-8, 8)][i % 3]]]
     g = Clustering("kmeans", p, DatumToFvConverter(conv), dev())
+    if gpu_min_elems is not None:
+        g.GPU_MIN_ELEMS = gpu_min_elems
     g.push(pts)
+    assert g.centers.is_cuda == (gpu_min_elems == 0)
     cs = sorted(tuple(round(v) for _, v in sorted(c.num_values)) for c in g.get_k_center())
     assert cs == sorted([(0, 0), (8, 8), (-8, 8)])
 
