@@ -175,13 +175,19 @@ def main() -> None:
 
     mixes = [0]
 
+    agreed = {"version": None, "labels": False}
+
     def mix_due(i: int) -> bool:
         if args.mix_every > 0 or args.mix_mode == "sync":
             return (i + 1) % max(1, args.mix_every) == 0
-        # adaptive: every rank must agree (the collectives have to match)
-        flag = torch.tensor([1 if clf.mix_ready(pending[0]) else 0], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=meta)
-        return bool(flag.item())
+        # adaptive: every rank must agree (the collectives have to match);
+        # one tiny host all-reduce carries [not ready, labels changed]
+        v = clf.labels.version()
+        flags = torch.tensor([0 if clf.mix_ready(pending[0]) else 1,
+                              0 if v == agreed["version"] else 1], dtype=torch.int32)
+        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=meta)
+        agreed["labels"] = flags[1].item() == 0
+        return flags[0].item() == 0
 
     def step(i: int) -> None:
         arena, offs, lens = pools[i % len(pools)]
@@ -193,7 +199,11 @@ def main() -> None:
                 clf.mix()
             else:
                 finish_mix()
-                pending[0] = clf.mix_begin(meta_group=meta)
+                v = clf.labels.version()
+                pending[0] = clf.mix_begin(meta_group=meta,
+                                           agreed_version=agreed["version"] if agreed["labels"] else None)
+                if "sync" not in pending[0] and clf.labels.version() == v:
+                    agreed["version"] = v
 
     # setup objects (synthetic bodies, torch modules) move to the permanent
     # generation, so a cyclic-GC pass in the timed loop does not traverse them

@@ -507,7 +507,7 @@ class LinearClassifier:
             return sum(t.numel() * t.element_size() for t in tables)
 
     # ------------------------------------------------ overlapped MIX
-    def mix_begin(self, group=None, meta_group=None) -> dict:
+    def mix_begin(self, group=None, meta_group=None, agreed_version: int | None = None) -> dict:
         """Start an overlapped MIX: snapshot W / P, launch the cluster SUM
         all-reduce of the snapshot on the communicator stream and return;
         training continues meanwhile. ``mix_end`` folds the cluster mean in
@@ -515,7 +515,10 @@ class LinearClassifier:
         collective are kept. Label agreement and count deltas ride on
         ``meta_group`` (a host/gloo group: no GPU synchronisation). If the
         label layouts disagree the synchronous ``mix`` runs instead (it
-        re-lays the label columns first)."""
+        re-lays the label columns first). ``agreed_version``: the caller knows
+        every rank still has the label layout agreed at this label-table
+        version; if the table is still at it, the host collective that
+        compares the layouts is skipped."""
         import torch
         from ..parallel import collective as coll
         with self._lock:
@@ -531,7 +534,8 @@ class LinearClassifier:
             mdev = self.device if on_dev else "cpu"
             # the label-layout check is blocking (a host collective on the
             # meta group); everything after it is asynchronous
-            if not coll.all_equal(fp, mdev if on_dev else torch.device("cpu"), mg):
+            agreed = agreed_version is not None and self.labels.version() == agreed_version
+            if not agreed and not coll.all_equal(fp, mdev if on_dev else torch.device("cpu"), mg):
                 return {"sync": self.mix(group)}
             meta_cnt = torch.from_numpy(cur - b).to(mdev)
             works = [dist_all_reduce(meta_cnt, "sum", mg)]
