@@ -458,15 +458,16 @@ __global__ __launch_bounds__(kThreads) void scan_train_kernel(
 
   if (prof && t == 0) prof[8 * k + 4] = (long long)__builtin_amdgcn_s_memtime();
   // ---- 5. one thread per sample
-  const uint64_t* th = lab_lds ? s_th : lt_hash;
-  const int32_t* tm = lab_lds ? s_tm : lt_meta;
-  const uint8_t* tb = lab_lds ? s_blob : lt_blob;
   uint32_t* s_slots = s_bits;                 // the bitmap is no longer needed
   int my_err = 0;
   for (int m = t; m < nsamples; m += kThreads) {
     int id = -1, doff = 0, ns = 0, nn = 0;
-    const int e = sample_walk(q, s_start[m], s_start[m + 1], th, tm, lt_cap, tb, &id, &doff,
-                              &ns, &nn);
+    // two call sites so each inlined copy keeps its table's address space
+    // (LDS loads for the staged table instead of flat loads)
+    const int e = lab_lds
+        ? sample_walk(q, s_start[m], s_start[m + 1], s_th, s_tm, lt_cap, s_blob, &id, &doff, &ns, &nn)
+        : sample_walk(q, s_start[m], s_start[m + 1], lt_hash, lt_meta, lt_cap, lt_blob, &id, &doff,
+                      &ns, &nn);
     if (e) { my_err |= e; s_slots[m] = 0; continue; }
     const int64_t s = s0 + m;
     labels[s] = id;
