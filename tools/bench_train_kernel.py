@@ -36,6 +36,7 @@ def make(rng, nreq, per, nlab, n_str, n_num, vocab, hot=16):
 
 def main() -> None:
     ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="run the variants whose name contains this")
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
     import torch
@@ -52,12 +53,17 @@ def main() -> None:
         ("hogwild 1024x128 8s+8n", "hogwild", 1024, 128, 8, 8, 16),
         ("atomic 1024x128 16s cold", "atomic", 1024, 128, 16, 0, 100000),
         ("atomic 1024x128 8s+8n cold-str", "atomic", 1024, 128, 8, 8, 100000),
+        ("hogwild 1024x128 8s+8n cold-str", "hogwild", 1024, 128, 8, 8, 100000),
+        ("atomic 1024x128 8s+1n cold-str", "atomic", 1024, 128, 8, 1, 100000),
+        ("atomic 64x128 8s+8n cold-str", "atomic", 64, 128, 8, 8, 100000),
         ("atomic 4096x32 8s+8n", "atomic", 4096, 32, 8, 8, 16),
         ("atomic 256x512 8s+8n", "atomic", 256, 512, 8, 8, 16),
         ("exact 1x2048 8s+8n", "exact", 1, 2048, 8, 8, 16),
     ]
     out = []
     for name, mode, nreq, per, ns, nn, hot in variants:
+        if args.only and args.only not in name:
+            continue
         clf = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv),
                                device=dev)
         for y in range(16):
