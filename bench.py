@@ -75,8 +75,8 @@ def make_requests(rng: random.Random, nreq: int, per_req: int, nlabels: int, n_s
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--requests", type=int, default=1024, help="concurrent train requests per step per GPU")
     ap.add_argument("--per-request", type=int, default=128, help="samples per train request")
     ap.add_argument("--labels", type=int, default=16)
