@@ -551,8 +551,7 @@ __global__ __launch_bounds__(64) void scan_fixup_kernel(
 // bytes (the stand-in datum of a rejected batch). host_out (fine-grained
 // host memory, 1 + nhist ints) receives [err, hist...] when the batch's
 // fixup kernel completes. Returns 0, or 1 on bad arguments.
-extern "C" int jb_scan_train(const uint8_t* buf, int64_t buf_cap, const int64_t* req_off,
-                             const int64_t* req_len,
+extern "C" int jb_scan_train(const uint8_t* buf, const int64_t* req_off, const int64_t* req_len,
                              const int64_t* sample_base, int R, const uint64_t* lt_hash,
                              const int32_t* lt_meta, int lt_cap, const uint8_t* lt_blob,
                              int lt_blob_len, int sps, int spn, int64_t* datum_off,
@@ -565,7 +564,6 @@ extern "C" int jb_scan_train(const uint8_t* buf, int64_t buf_cap, const int64_t*
   if (hipMemsetAsync(err, 0, sizeof(int32_t), stream) != hipSuccess) return 1;
   if (nhist > 0 && hipMemsetAsync(hist, 0, sizeof(uint32_t) * (size_t)nhist, stream) != hipSuccess)
     return 1;
-  (void)buf_cap;
   hipLaunchKernelGGL(jb::scan_train_kernel, dim3(R), dim3(jb::kThreads), 0, stream, buf, req_off, req_len,
                      sample_base, R, lt_hash, lt_meta, lt_cap, lt_blob, lt_blob_len, sps, spn,
                      datum_off, datum_len, labels, row_ptr, req_slots, hist, nhist, err,

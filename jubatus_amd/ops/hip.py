@@ -56,7 +56,7 @@ _SIGS = {
                             _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                             _c_void_p, _c_void_p],
     "jb_diag_empty": [_c_void_p, _i32, _c_void_p],
-    "jb_scan_train": [_c_void_p, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
+    "jb_scan_train": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
                       _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                       _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i64, _c_void_p,
                       _c_void_p],
@@ -272,11 +272,11 @@ def scan_train(buf: torch.Tensor, buf_used: int, req_off: torch.Tensor, req_len:
     if datum_off.numel() < n or datum_len.numel() < n or labels.numel() < n or \
             row_ptr.numel() < n + 1:
         raise ValueError("scan_train: sample arrays shorter than n")
-    if buf.numel() < buf_used + 16 or buf.numel() < empty_off + 3 or buf.numel() % 4:
+    if buf.numel() < buf_used + 16 or buf.numel() < empty_off + 3:
         raise ValueError("scan_train: buffer lacks the 16-B slack / the stand-in datum")
     if host_out.nbytes < 4 * (1 + hist.numel()):
         raise ValueError("scan_train: host_out shorter than 1 + len(hist) ints")
-    rc = _fn("jb_scan_train")(_p(buf), buf.numel(), _p(req_off), _p(req_len), _p(sample_base), R, _p(lt_hash),
+    rc = _fn("jb_scan_train")(_p(buf), _p(req_off), _p(req_len), _p(sample_base), R, _p(lt_hash),
                               _p(lt_meta), cap, _p(lt_blob), lt_blob.numel(), sps, spn,
                               _p(datum_off), _p(datum_len), _p(labels), _p(row_ptr),
                               _p(req_slots), _p(hist), hist.numel(), _p(err),
