@@ -107,6 +107,18 @@ def body_counts(buf: np.ndarray, offs: np.ndarray, lens: np.ndarray) -> np.ndarr
     return None if (n < 0).any() else n
 
 
+SCAN_LDS_BYTES = 27 * 1024      # csrc/hip/scan.hip kScanBytes
+SCAN_MAX_SAMPLES = 768          # csrc/hip/scan.hip kMaxSamples
+
+
+def scan_too_big(offs: np.ndarray, lens: np.ndarray, counts: np.ndarray) -> bool:
+    """any request the GPU scan would reject for size (its 16-B aligned
+    window exceeds the LDS stage, or too many samples)"""
+    if offs.size == 0:
+        return False
+    return bool(((lens + (offs & 15)) > SCAN_LDS_BYTES).any() or (counts > SCAN_MAX_SAMPLES).any())
+
+
 class ScanCheck:
     """completion record of a GPU-scanned train batch: the batch's error
     bits and label counts land in pinned memory when ``event`` completes"""
@@ -336,6 +348,11 @@ class FeaturePipeline:
         lens = np.ascontiguousarray(lens, dtype=np.int64)
         counts = body_counts(arena.np, offs, lens)
         if counts is None:
+            return None
+        # requests the device scan does not stage (larger than its LDS window
+        # or with more samples than its slot table): the host scanner takes
+        # the batch right away instead of after a rejected launch
+        if scan_too_big(offs, lens, counts):
             return None
         R = int(offs.size)
         sbase = np.zeros(R + 1, np.int64)

@@ -127,6 +127,9 @@ def test_gpu_scan_rejects_batch(case):
         table.get_or_add(f"L{y}")
     chk = ScanCheck(16)
     b = pipe.from_arena_gpu(arena, offs, lens, table, chk)
+    if case == "too_big":                             # decided on the host: no launch
+        assert b is None
+        return
     torch.cuda.synchronize()
     pipe.check_errors()                               # the stand-in datums parse cleanly
     assert int(chk.err[0]) != 0

@@ -4,7 +4,7 @@ recomputes) and the body header pass. CPU only."""
 import msgpack
 import numpy as np
 
-from jubatus_amd.ops.feature_pipeline import body_counts, fnv1a64, label_table_arrays
+from jubatus_amd.ops.feature_pipeline import scan_too_big, body_counts, fnv1a64, label_table_arrays
 
 
 def _probe(th, tm, blob, label: bytes):
@@ -53,3 +53,12 @@ def test_body_counts_headers():
     bad = np.frombuffer(b"\xa1x" + bodies[1], np.uint8)
     assert body_counts(bad, np.array([0, 2]), np.array([2, len(bodies[1])])) is None
     assert body_counts(buf, np.array([0]), np.array([0])) is None
+
+
+def test_size_rule_matches_the_kernel_limits():
+    # the host decides up front what the device scan would reject as too big
+    offs = np.array([0, 16, 32], np.int64)
+    assert not scan_too_big(offs, np.array([100, 27 * 1024, 5]), np.array([1, 2, 768]))
+    assert scan_too_big(offs, np.array([100, 27 * 1024 + 1, 5]), np.array([1, 2, 3]))
+    assert scan_too_big(np.array([3]), np.array([27 * 1024 - 2]), np.array([1]))   # aligned window
+    assert scan_too_big(offs, np.array([1, 1, 1]), np.array([1, 769, 1]))
