@@ -88,6 +88,7 @@ class LinearClassifier:
         # complete asynchronously (_drain)
         self.gpu_scan = os.environ.get("JUBATUS_GPU_SCAN", "1") != "0"
         self._pending: collections.deque = collections.deque()
+        self._scan_stats = {"gpu": 0, "replayed": 0, "host": 0}   # train batches by scan path
         self._free_checks: list = []
         self._draining = False
         self._result_cols = None
@@ -177,6 +178,7 @@ class LinearClassifier:
                 chk = self._check_record(self.labels.size())
                 b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk)
                 if b is not None:
+                    self._scan_stats["gpu"] += 1
                     n = self._train_batch(b)
                     chk.replay = lambda: self._train_batch(
                         self.pipe.from_arena(arena, offs, lens, True, self.labels))
@@ -184,6 +186,7 @@ class LinearClassifier:
                     return n
                 self._free_checks.append(chk)
             self._drain(block=True)
+            self._scan_stats["host"] += 1
             return self._train_batch(self.pipe.from_arena(arena, offs, lens, True, self.labels))
 
     def _check_record(self, nhist: int):
@@ -213,6 +216,7 @@ class LinearClassifier:
                 self._pending.popleft()
                 replay, c.replay = c.replay, None
                 if int(c.err[0]):
+                    self._scan_stats["replayed"] += 1
                     replay()
                 else:
                     h = c.hist[:c.nhist]
@@ -679,6 +683,9 @@ class LinearClassifier:
               "label_capacity": str(self.LC), "method": self.method,
               "storage": "hbm" if self.gpu else "host",
               "fv_path": "gpu" if (self.gpu and self.pipe.fast) else "host"}
+        if self.gpu:
+            for k, v in self._scan_stats.items():
+                st[f"train_scan.{k}"] = str(v)
         return st
 
 

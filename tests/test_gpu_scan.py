@@ -160,6 +160,10 @@ def test_train_arena_gpu_scan_same_model(monkeypatch):
         clf.pipe.check_errors()
         models.append((clf.get_labels(), clf.W.cpu().numpy(), clf.P.cpu().numpy(),
                        clf.labels.names()))
+        st = clf.get_status()
+        if gpu_scan:   # step 0 has no labels yet (host), new labels in step 2 are re-run
+            assert int(st["train_scan.gpu"]) >= 4 and int(st["train_scan.replayed"]) >= 1
+            assert int(st["train_scan.host"]) >= 1
     (l0, w0, p0, n0), (l1, w1, p1, n1) = models
     assert l0 == l1 and n0 == n1
     np.testing.assert_allclose(w1, w0, rtol=1e-6, atol=1e-6)
