@@ -8,15 +8,20 @@ AROW classifier at 1/2/4/8 MI355X", config/classifier/arow.json
 
 One timed step on every rank =
   * R concurrent ``train`` request bodies (msgpack list<labeled_datum>, as
-    received by the RPC layer) of S samples each: native scan + label
-    resolution + pinned staging (host), H2D, GPU msgpack parse + feature
-    hashing (fv_hash kernel), GPU AROW update (R lock-free update streams,
-    each exact-sequential) - i.e. the complete train path minus the socket;
-  * one MIX: label-set agreement (host gloo group) + RCCL all-reduce mean
-    of W and P (hash_max_size x labels x 2 tables, fp32) over xGMI (N > 1).
-    Default ``--mix-mode overlap``: the all-reduce of step k's snapshot runs
-    on the communicator stream during step k+1 and is folded in as
-    W += mean(snapshot) - snapshot, so no update is lost; ``sync`` blocks.
+    the RPC reader leaves them in a pinned receive arena) of S samples each:
+    header pass (host), one H2D copy of the raw bytes, GPU request scan
+    (csrc/hip/scan.hip: sample boundaries, label ids, validation), GPU
+    msgpack parse + feature hashing (fv_hash), GPU AROW update (R lock-free
+    update streams, each exact-sequential) - the train path minus the socket.
+    Batches the device scan rejects (new labels, ...) are re-run through the
+    host scanner; the RPC server itself still feeds its (smaller, latency-
+    bound) batches through the host scanner, see docs/PERFORMANCE.md;
+  * the MIX: label-set agreement (host gloo group) + RCCL all-reduce mean
+    of W and P (hash_max_size x labels x 2 tables, fp32) over xGMI (N > 1),
+    overlapped: the all-reduce of a snapshot runs on the communicator stream
+    during the following steps and is folded in as W += mean(snapshot) -
+    snapshot, so no update is lost; a new MIX starts as soon as the previous
+    one finished (the reference's trigger); ``--mix-mode sync`` blocks.
 Per-GPU work is fixed as N grows (weak scaling). Data: synthetic datums
 (8 string + 8 numeric features, 16 labels), random-init (zero) model.
 
