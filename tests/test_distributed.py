@@ -94,6 +94,10 @@ def test_two_server_mix(coord, mixer):
             assert b.get_labels() == {"pos": 3, "neg": 3}  # counts mixed (sum of deltas)
         st = list(b.get_status().values())[0]
         assert st["mixer"] == mixer and st["is_standalone"] == "0"
+        # distributed-mode keys (reference client_test/status_test.hpp:47-56)
+        for k in ("connected_zookeeper", "interconnect_timeout", "interval_count", "interval_sec",
+                  "mixer", "name", "use_cht", "zk", "zookeeper_timeout"):
+            assert k in st, k
         assert int(st[f"{mixer}.mix_count"]) >= 1
         a.close()
         b.close()
