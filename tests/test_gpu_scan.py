@@ -70,22 +70,25 @@ def _batch_arrays(b):
             b.fidx[:rp[-1]].cpu().numpy(), b.fval[:rp[-1]].cpu().numpy())
 
 
-def test_gpu_scan_matches_host_scan():
+@pytest.mark.parametrize("nlabels", [5, 100])
+def test_gpu_scan_matches_host_scan(nlabels):
+    """5 labels: label table and counts in LDS; 100: the table is read from
+    global memory and labels >= 64 are counted with global atomics"""
     import torch
     from jubatus_amd._native import native
     from jubatus_amd.ops.feature_pipeline import FeaturePipeline, ScanCheck
 
     pipe = FeaturePipeline(DatumToFvConverter(CONV), _device())
-    bodies = _bodies()
+    bodies = _bodies(nlabels=nlabels)
     assert 16 * 1024 < max(len(b) for b in bodies) <= 27 * 1024 - 16
     arena, offs, lens = _arena(bodies)
     table = native().LabelTable()
-    for y in range(5):
+    for y in range(nlabels):
         table.get_or_add(f"L{y}")
     host = _batch_arrays(pipe.from_arena(arena, offs, lens, True, table))
     torch.cuda.synchronize()
     pipe.check_errors()
-    chk = ScanCheck(16)
+    chk = ScanCheck(128)
     b = pipe.from_arena_gpu(arena, offs, lens, table, chk)
     torch.cuda.synchronize()
     pipe.check_errors()
@@ -95,8 +98,8 @@ def test_gpu_scan_matches_host_scan():
     for h, d, name in zip(host[1:], dev[1:], ("row_ptr", "labels", "stream_ptr", "fidx", "fval")):
         np.testing.assert_array_equal(h, d, err_msg=name)
     # label counts of the batch
-    want = np.bincount(host[2], minlength=16)
-    np.testing.assert_array_equal(chk.hist[:16], want)
+    want = np.bincount(host[2], minlength=128)
+    np.testing.assert_array_equal(chk.hist[:128], want)
 
 
 @pytest.mark.parametrize("case", ["unknown_label", "binary_values", "malformed", "too_big"])
