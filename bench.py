@@ -182,17 +182,28 @@ def main() -> None:
 
     agreed = {"version": None, "labels": False}
 
+    inflight = {"work": None, "flags": None}
+
     def mix_due(i: int) -> bool:
         if args.mix_every > 0 or args.mix_mode == "sync":
             return (i + 1) % max(1, args.mix_every) == 0
-        # adaptive: every rank must agree (the collectives have to match);
-        # one tiny host all-reduce carries [not ready, labels changed]
+        # adaptive: every rank must agree (the collectives have to match).
+        # One tiny host all-reduce per step carries [not ready, labels
+        # changed]; it is issued asynchronously and read one step later, so
+        # the host never waits on it (all ranks act on the same lagged flags)
+        due = False
+        if inflight["work"] is not None:
+            inflight["work"].wait()
+            f = inflight["flags"]
+            agreed["labels"] = f[1].item() == 0
+            due = f[0].item() == 0
         v = clf.labels.version()
-        flags = torch.tensor([0 if clf.mix_ready(pending[0]) else 1,
+        # a MIX that starts this step is not finished by the next one
+        flags = torch.tensor([0 if (not due and clf.mix_ready(pending[0])) else 1,
                               0 if v == agreed["version"] else 1], dtype=torch.int32)
-        dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=meta)
-        agreed["labels"] = flags[1].item() == 0
-        return flags[0].item() == 0
+        inflight["flags"] = flags
+        inflight["work"] = dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=meta, async_op=True)
+        return due
 
     def step(i: int) -> None:
         arena, offs, lens = pools[i % len(pools)]
@@ -232,6 +243,8 @@ def main() -> None:
         if trace_steps:
             marks.append(time.perf_counter())
     finish_mix()          # the last MIX completes inside the timed region
+    if inflight["work"] is not None:
+        inflight["work"].wait()
     sync()
     barrier()
     sync()
