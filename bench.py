@@ -123,6 +123,8 @@ def main() -> None:
             local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
+        from jubatus_amd.utils.numa import bind_to_device
+        numa = bind_to_device(local)      # before pinned buffers and worker threads exist
         if world > 1:
             if args.dist_backend == "nccl":
                 dist.init_process_group("nccl", device_id=device)
@@ -130,6 +132,7 @@ def main() -> None:
                 dist.init_process_group("gloo")
     else:
         device = None
+        numa = {}
         if world > 1:
             dist.init_process_group("gloo")
 
@@ -310,6 +313,7 @@ def main() -> None:
                            "back to back (a new MIX as soon as the previous one finished)")
                         + f"; {mixes[0]} MIXes in the timed steps") if world > 1 else "standalone",
                 "concurrent_update": args.update_mode,
+                "numa_node": numa.get("node"),
             },
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),

@@ -32,6 +32,8 @@ def select_device(argv=None) -> Any:
     if idx is None:
         idx = int(os.environ.get("LOCAL_RANK", "0")) % max(n, 1)
     torch.cuda.set_device(idx)
+    from ..utils.numa import bind_to_device
+    bind_to_device(idx)
     from .._native import hip_lib
     hip_lib()  # fail loudly if the kernels are missing
     return torch.device("cuda", idx)

@@ -48,8 +48,11 @@ def scan_threads() -> int:
     except (AttributeError, OSError):
         ncpu = os.cpu_count() or 4
     local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+    from ..utils.numa import binding
+    b = binding()
+    if b.get("before"):       # bound to the GPU's node: shared by that node's ranks only
+        local = max(1, -(-local * b["cpus"] // b["before"]))
     return max(1, min(16, ncpu // local))
-
 
 
 def fnv1a64(b: bytes) -> int:
