@@ -23,6 +23,7 @@
 // Distances: metric 0 lsh (hamming / hash_num), 2 minhash (mismatch
 // fraction), 1 euclid_lsh (law of cosines on the norms). Invalid rows: +inf.
 #include <limits.h>
+#include <stdlib.h>
 
 #include "jb_device.hpp"
 #include "jb_host_wait.hpp"
@@ -156,8 +157,51 @@ __device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, in
   }
 }
 
-// NW waves per block; the merge of (NW + 1) * k candidates in wave 0 must fit
-// 10 per lane: NW = 4 for k <= 128, NW = 16 (the final merge) for k <= 37.
+// number of entries of the sorted list (d, ix)[0, len) that precede (v, id)
+__device__ __forceinline__ int rank_in(const float* d, const int* ix, int len, float v, int id) {
+  int lo = 0, hi = len;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (lt_pair(d[mid], ix[mid], v, id)) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Block-parallel merge of the carry (sorted, cc real entries) with NW sorted
+// wave lists (wave w: cnt[w] real entries at wd/wi + w k) into the k
+// smallest, written to nd/ni: every real entry's final position is its index
+// in its own list plus its rank (binary search) in each other non-empty list
+// - all (d, row) pairs are distinct, so the positions are a permutation.
+// Replaces a serial k-round wave pop, which costs k dependent arg-min
+// rounds per tile. Returns the merged count (<= k). Called by all threads;
+// the caller synchronises before reading nd/ni.
+template <int NW>
+__device__ __forceinline__ int rank_merge(const float* cd, const int* ci, int cc, const float* wd,
+                                          const int* wi, const int* cnt, int k, float* nd,
+                                          int* ni, int t, int T) {
+  int total = cc;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) total += cnt[w];
+  for (int e = t; e < total; e += T) {
+    // locate element e: carry first, then the wave lists in order
+    int list = -1, i = e;
+    if (i >= cc) {
+      i -= cc;
+      list = 0;
+      while (i >= cnt[list]) { i -= cnt[list]; ++list; }
+    }
+    const float v = list < 0 ? cd[i] : wd[list * k + i];
+    const int id = list < 0 ? ci[i] : wi[list * k + i];
+    int r = i;
+    if (list >= 0) r += rank_in(cd, ci, cc, v, id);
+    for (int w = 0; w < NW && r < k; ++w)
+      if (w != list && cnt[w] > 0) r += rank_in(wd + w * k, wi + w * k, cnt[w], v, id);
+    if (r < k) { nd[r] = v; ni[r] = id; }
+  }
+  return total < k ? total : k;
+}
+
+// NW waves per block (4 or 16); the carry merge is block-parallel (rank_merge).
 template <int MODE, int NW = 4>
 __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t n,
                                                            int64_t per_block, int k,
@@ -170,13 +214,13 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   __shared__ float s_wd[NW * kTopMaxK];   // wave w's list at [w k, w k + k)
   __shared__ int s_wi[NW * kTopMaxK];
   __shared__ int s_cnt[NW];
-  __shared__ float s_cd[kTopMaxK];
-  __shared__ int s_ci[kTopMaxK];
+  __shared__ float s_cbd[2][kTopMaxK];    // carry, double-buffered
+  __shared__ int s_cbi[2][kTopMaxK];
   __shared__ float s_thr;
   __shared__ uint64_t s_q[kTopMaxWords];
   const int q = blockIdx.y;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int j = t; j < k; j += T) { s_cd[j] = INFINITY; s_ci[j] = INT_MAX; }
+  int cur = 0, cc = 0;                     // carry buffer / real entries (block-uniform)
   float qn = 0.f;
   if (MODE == 0) {
     for (int w = t; w < s.words; w += T) s_q[w] = s.qbits[(int64_t)q * s.words + w];
@@ -200,7 +244,11 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
     for (int r = 0; r < kTopR; ++r) {
       const int64_t row = base + (int64_t)r * T + t;
       load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
-      if (d[r] > thr) { d[r] = INFINITY; ix[r] = INT_MAX; }
+      // MODE 0/1 visit rows in increasing index order, so a row that ties
+      // the carry's k-th distance loses the (distance, index) tie-break:
+      // drop it too (quantized hamming distances tie a lot). MODE 2 lists
+      // are distance-sorted per block, not index-ordered: keep ties.
+      if (MODE != 2 ? d[r] >= thr : d[r] > thr) { d[r] = INFINITY; ix[r] = INT_MAX; }
       any |= d[r] < INFINITY;
     }
     // once the block's k-th best is known almost every row fails the
@@ -214,32 +262,24 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
     }
     if (lane == 0) s_cnt[wv] = cnt;
     __syncthreads();
-    if (wv == 0) {
-      int total = 0;
+    int total = 0;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) total += s_cnt[w];
-      if (total > 0) {
-        // merge carry (k) + NW wave lists (NW k) <= 640 -> 10 per lane
-        constexpr int M = 10;
-        float m[M];
-        int mi[M];
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-          const int c = lane + 64 * j;
-          if (c < k) { m[j] = s_cd[c]; mi[j] = s_ci[c]; }
-          else if (c < (NW + 1) * k) { m[j] = s_wd[c - k]; mi[j] = s_wi[c - k]; }
-          else { m[j] = INFINITY; mi[j] = INT_MAX; }
-        }
-        __builtin_amdgcn_wave_barrier();
-        sort_regs<M>(m, mi);
-        const float kth = wave_pop<M>(m, mi, k, s_cd, s_ci, lane);
-        if (lane == 0) s_thr = kth;
-      }
+    for (int w = 0; w < NW; ++w) total += s_cnt[w];
+    if (total > 0) {                       // block-uniform
+      const int nn = rank_merge<NW>(s_cbd[cur], s_cbi[cur], cc, s_wd, s_wi, s_cnt, k,
+                                    s_cbd[cur ^ 1], s_cbi[cur ^ 1], t, T);
+      cur ^= 1;
+      cc = nn;
+      __syncthreads();
+      if (t == 0) s_thr = cc == k ? s_cbd[cur][k - 1] : INFINITY;
     }
     __syncthreads();
   }
   const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
-  for (int j = t; j < k; j += T) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
+  for (int j = t; j < k; j += T) {
+    out_d[o + j] = j < cc ? s_cbd[cur][j] : INFINITY;
+    out_i[o + j] = j < cc ? s_cbi[cur][j] : INT_MAX;
+  }
   if (done != nullptr) {   // latency path: results went to pinned host memory
     __threadfence_system();
     __syncthreads();
@@ -533,12 +573,54 @@ __global__ __launch_bounds__(1024) void topk_final_kernel(const float* __restric
 
 constexpr int kListK = 16;   // k up to this uses topk_lists_kernel
 
+// Waves per block of the scan stage (MODE 0/1). Every block scans a
+// contiguous range with a block-wide carry and two barriers per tile, so a
+// CU holding one 4-wave block spends most of a tile waiting on HBM latency;
+// 16 waves per block (one block per CU, k <= 37 so the 17 k merge fits) keep
+// 4x the rows in flight at the same candidate count. JB_TOPK_NW=4|16
+// overrides (tools/bench_topk.py compares them).
+inline int scan_waves(int k, int nq, int64_t nrows) {
+  static const int forced = [] {
+    const char* e = getenv("JB_TOPK_NW");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  if (forced == 4 || k > 37) return 4;
+  if (forced == 16) return 16;
+  // measured (tools/bench_topk.py): 16 waves win for one query over a large
+  // table (one block per CU, latency-bound: 10M rows k 10 74 vs 165 us) and
+  // lose once several queries fill the chip with 4-wave blocks (1M rows x 8
+  // queries: 182 vs 55 us); equal at 1M rows x 1 query
+  return nq == 1 && nrows >= ((int64_t)2 << 20) ? 16 : 4;
+}
+
+// the final merge of the blocks' candidates for k <= kListK: per-thread
+// register lists (default) or the tile kernel with the rank merge
+// (JB_TOPK_MERGE=tile, for comparison)
+inline bool merge_with_tile() {
+  static const bool tile = [] {
+    const char* e = getenv("JB_TOPK_MERGE");
+    return e != nullptr && e[0] == 't';
+  }();
+  return tile;
+}
+
+template <int MODE>
+inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
+                        int k, float* out_d, int32_t* out_i, hipStream_t stream) {
+  if (scan_waves(k, nq, nrows) == 16)
+    hipLaunchKernelGGL((topk_kernel<MODE, 16>), dim3(blocks, nq), dim3(16 * 64), 0, stream, s,
+                       nrows, per_block, k, out_d, out_i, nullptr, 0u);
+  else
+    hipLaunchKernelGGL((topk_kernel<MODE, 4>), dim3(blocks, nq), dim3(4 * 64), 0, stream, s,
+                       nrows, per_block, k, out_d, out_i, nullptr, 0u);
+}
+
 // the final merge: one block per query; 16 waves when the (17 k) candidates
 // of the merge stage fit (k <= 37), else 4
 inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out_d,
                          int32_t* out_i, volatile uint32_t* done, uint32_t seq,
                          hipStream_t stream) {
-  if (k <= kListK) {
+  if (k <= kListK && !merge_with_tile()) {
     hipLaunchKernelGGL((topk_lists_kernel<2, kListK, 16>), dim3(1, nq), dim3(16 * 64), 0, stream,
                        m, nc, nc, k, out_d, out_i, done, seq);
   } else if (k <= 37) {
@@ -581,13 +663,10 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
-  if (mode == 0) {
-    hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                       nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
-  } else {
-    hipLaunchKernelGGL(jb::topk_kernel<1>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                       nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
-  }
+  if (mode == 0)
+    jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+  else
+    jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;   // candidates per query
@@ -609,8 +688,7 @@ static int topk_to_host_tile(const uint64_t* qbits, const float* qnorm, int nq,
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
-  hipLaunchKernelGGL(jb::topk_kernel<0>, dim3(blocks, nq), dim3(jb::kTopThreads), 0, stream, s,
-                     nrows, per_block, k, scratch_d, scratch_i, nullptr, 0u);
+  jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)blocks * k;

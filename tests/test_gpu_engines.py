@@ -183,6 +183,35 @@ def test_topk_hamming_matches_full_sort(metric, k, nrows, nq):
         assert np.all(np.isinf(od[q][fin.sum():]))
 
 
+@pytest.mark.parametrize("k", [1, 10, 31, 100])
+def test_topk_hamming_heavy_ties(k):
+    """a table of 8 distinct signatures over 600k rows: every distance level
+    holds ~75k tied rows, so the exact answer is the lowest row indices of
+    the nearest level (the scan's tie pruning must keep exactly those)"""
+    import torch
+    from jubatus_amd.ops import hip
+    nrows, nq = 600_000, 3
+    g = torch.Generator().manual_seed(k)
+    pool = torch.randint(-2**62, 2**62, (8, 1), generator=g, dtype=torch.int64)
+    tb = pool[torch.randint(0, 8, (nrows,), generator=g)]
+    tn = torch.ones(nrows)
+    valid = (torch.rand(nrows, generator=g) > 0.05).to(torch.uint8)
+    qb = pool[:nq].clone()
+    qb[0, 0] ^= 1                        # no exact match for query 0
+    qn = torch.ones(nq)
+    d = dev()
+    tbd, tnd, vd, qbd, qnd = (x.to(d) for x in (tb, tn, valid, qb, qn))
+    full = torch.empty((nq, nrows), dtype=torch.float32, device=d)
+    hip.hamming_scan(qbd, qnd, nq, tbd, tnd, vd, nrows, 64, 0, full)
+    od, oi = hip.topk_hamming(qbd, qnd, nq, tbd, tnd, vd, nrows, 64, 0, k)
+    full = full.cpu().numpy()
+    od, oi = od.cpu().numpy(), oi.cpu().numpy()
+    for q in range(nq):
+        order = np.argsort(full[q], kind="stable")[:k]
+        np.testing.assert_array_equal(oi[q], order)
+        np.testing.assert_allclose(od[q], full[q][order], rtol=1e-6)
+
+
 def test_topk_scores_flip():
     import torch
     from jubatus_amd.ops import hip
