@@ -6,27 +6,34 @@ Metric/config: BASELINE.json - "samples/sec (train) + p50 classify latency,
 AROW classifier at 1/2/4/8 MI355X", config/classifier/arow.json
 (AROW, regularization_weight 1.0, converter str bin/bin + num).
 
-One timed step on every rank =
-  * R concurrent ``train`` request bodies (msgpack list<labeled_datum>, as
-    the RPC reader leaves them in a pinned receive arena) of S samples each:
-    header pass (host), one H2D copy of the raw bytes, GPU request scan
-    (csrc/hip/scan.hip: sample boundaries, label ids, validation), GPU
-    msgpack parse + feature hashing (fv_hash), GPU AROW update (R lock-free
-    update streams, each exact-sequential) - the train path minus the socket.
-    Batches the device scan rejects (new labels, ...) are re-run through the
-    host scanner; the RPC server itself still feeds its (smaller, latency-
-    bound) batches through the host scanner, see docs/PERFORMANCE.md;
-  * the MIX: label-set agreement (host gloo group) + RCCL all-reduce mean
-    of W and P (hash_max_size x labels x 2 tables, fp32) over xGMI (N > 1),
-    overlapped: the all-reduce of a snapshot runs on the communicator stream
-    during the following steps and is folded in as W += mean(snapshot) -
-    snapshot, so no update is lost; a new MIX starts as soon as the previous
-    one finished (the reference's trigger); ``--mix-mode sync`` blocks.
-Per-GPU work is fixed as N grows (weak scaling). Data: synthetic datums
-(8 string + 8 numeric features, 16 labels), random-init (zero) model.
+Data: a NON-REPEATING synthetic stream. Every timed batch is a distinct set
+of train request bodies (msgpack list<labeled_datum>, 8 string + 8 numeric
+values, 16 labels) generated before the timed region by the native
+generator (csrc/native/jb_synth.cpp) into pinned host memory, as the RPC
+reader would leave them; the warmup steps train on a separate data set, so
+no timed sample has been seen before. ``--worst-case`` makes every string
+value fresh noise (no label signal), so (almost) every sample updates the
+model; the numeric keys n0..n7 are in every sample (hot rows).
+
+One timed step on every rank = ``batches-per-step`` train batches of
+R concurrent requests x S samples:
+  * header pass (host), one H2D copy of the batch's raw bytes, GPU request
+    scan (csrc/hip/scan.hip: sample boundaries, label ids, validation), GPU
+    msgpack parse + feature hashing (fv_hash.hip), hot-row detection
+    (hot.hip) and the AROW update (linear.hip: R lock-free update streams,
+    each exact-sequential; hot rows in a block-shared LDS replica);
+  * the MIX (N > 1): label-set agreement (host gloo group) + RCCL all-reduce
+    mean of W and P over xGMI, overlapped with the following batches and
+    folded in as W += mean(snapshot) - snapshot; a new MIX starts as soon as
+    the previous one finished (the reference's trigger); ``--mix-mode sync``
+    blocks.
+Per-GPU work is fixed as N grows (weak scaling). The model starts from zero
+(random-init equivalent for a linear model); the JSON reports the fraction
+of timed samples that updated it.
 
 Usage: python bench.py --gpus N --steps K --warmup W
-       (N > 1: launched by torch.distributed.run, one process per GPU)
+       (N > 1: launched by torch.distributed.run, one process per GPU; without
+       WORLD_SIZE in the environment this script launches the N ranks itself)
 """
 from __future__ import annotations
 
@@ -34,7 +41,9 @@ import argparse
 import json
 import os
 import random
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -58,10 +67,12 @@ AROW_CONFIG = {
     "method": "AROW",
 }
 
+BLOCK_BYTES = 1 << 30          # pinned host blocks (a power of two: no allocator rounding)
+
 
 def make_requests(rng: random.Random, nreq: int, per_req: int, nlabels: int, n_str: int,
                   n_num: int, vocab: int) -> list[bytes]:
-    """Synthetic, label-correlated datums, msgpack-encoded per request."""
+    """Python twin of the native generator (held-out accuracy set)."""
     bodies = []
     for _ in range(nreq):
         items = []
@@ -77,24 +88,86 @@ def make_requests(rng: random.Random, nreq: int, per_req: int, nlabels: int, n_s
     return bodies
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mem_available() -> int:
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except OSError:
+        pass
+    return 16 << 30
+
+
+class FreshStream:
+    """Distinct request batches in pinned host blocks (generated once,
+    outside the timed region; consumed once)."""
+
+    def __init__(self, nat, torch, pinned: bool, args, seed: int, count: int, nthreads: int,
+                 p_corr: float, vocab: int):
+        from jubatus_amd.ops.feature_pipeline import RequestArena
+        self.batches = []
+        self.nbytes = 0
+        blk, blk_np, used_in_blk = None, None, 0
+        offs = np.zeros(args.requests, np.int64)
+        lens = np.zeros(args.requests, np.int64)
+        for b in range(count):
+            for attempt in range(2):
+                if blk is not None:
+                    start = (used_in_blk + 4095) & ~4095
+                    cap = BLOCK_BYTES - start - 64
+                    used = nat.synth_requests(blk_np.ctypes.data + start, cap, offs.ctypes.data,
+                                              lens.ctypes.data, seed, b * args.requests,
+                                              args.requests, args.per_request, args.labels,
+                                              args.str_features, args.num_features, vocab, 16,
+                                              p_corr, nthreads)
+                    if used >= 0:
+                        view = blk[start:start + used + 64]
+                        self.batches.append(RequestArena.over(view, offs.copy(), lens.copy()))
+                        used_in_blk = start + used + 64
+                        self.nbytes += used
+                        break
+                if attempt == 1:
+                    raise MemoryError("one batch does not fit a pinned block")
+                blk = torch.empty(BLOCK_BYTES, dtype=torch.uint8, pin_memory=pinned)
+                blk_np = blk.numpy()
+                used_in_blk = 0
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--requests", type=int, default=1024, help="concurrent train requests per step per GPU")
+    ap.add_argument("--requests", type=int, default=1024, help="concurrent train requests per batch per GPU")
     ap.add_argument("--per-request", type=int, default=128, help="samples per train request")
+    ap.add_argument("--batches-per-step", type=int, default=0,
+                    help="train batches per timed step (0: as many as the fresh-data budget allows, "
+                         "at most 96, so that the timed region lasts about a second)")
+    ap.add_argument("--fresh-gb", type=float, default=0.0,
+                    help="host memory for the non-repeating timed stream per rank "
+                         "(0: min(56 GB, 60%% of MemAvailable / local ranks))")
     ap.add_argument("--labels", type=int, default=16)
     ap.add_argument("--str-features", type=int, default=8)
     ap.add_argument("--num-features", type=int, default=8)
     ap.add_argument("--vocab", type=int, default=100000)
     ap.add_argument("--hash-bits", type=int, default=20)
-    ap.add_argument("--pools", type=int, default=4, help="distinct synthetic batches cycled")
+    ap.add_argument("--worst-case", action="store_true",
+                    help="string values are fresh noise: (almost) every sample updates the model")
+    ap.add_argument("--warmup-pools", type=int, default=4, help="distinct batches cycled by warmup")
     ap.add_argument("--mix-every", type=int, default=0,
-                    help="N > 0: MIX every N steps; 0 (default): the reference's trigger - a new MIX "
+                    help="N > 0: MIX every N batches; 0 (default): the reference's trigger - a new MIX "
                          "starts as soon as the previous one has finished and updates arrived "
                          "(linear_mixer.cpp:337-344,358-390: interval_count 512 updates, the mixer "
-                         "wakes on the threshold), agreed across ranks each step")
+                         "wakes on the threshold), agreed across ranks each batch")
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
                     help="how concurrent request streams update shared rows")
@@ -105,10 +178,17 @@ def main() -> None:
                     help="cpu: host engine + gloo, for rehearsing the multi-rank path without a GPU "
                          "(not a benchmark configuration)")
     ap.add_argument("--mix-mode", choices=("overlap", "sync"), default="overlap",
-                    help="overlap: the RCCL all-reduce of step k runs during step k+1 and its "
+                    help="overlap: the RCCL all-reduce of batch k runs during batch k+1 and its "
                          "mean is folded in afterwards (updates made meanwhile are kept); "
-                         "sync: blocking MIX at the end of every step")
+                         "sync: blocking MIX at the end of every batch")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one rank per GPU: launch them before this process touches the GPU
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+               "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     import torch
     import torch.distributed as dist
@@ -116,8 +196,10 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
     if args.device == "gpu":
         if args.dist_backend == "gloo":
             local = local % max(1, torch.cuda.device_count())
@@ -140,6 +222,7 @@ def main() -> None:
         if device is not None:
             torch.cuda.synchronize()
 
+    from jubatus_amd._native import native
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.classifier import LinearClassifier
 
@@ -151,21 +234,27 @@ def main() -> None:
     for y in range(args.labels):  # same label order on every rank (set_label, as a client would)
         clf.set_label(f"label{y}")
 
-    from jubatus_amd.ops.feature_pipeline import RequestArena
-
-    rng = random.Random(1234 + rank)
-    pools = []
-    for _ in range(args.pools):
-        bodies = make_requests(rng, args.requests, args.per_request, args.labels,
-                               args.str_features, args.num_features, args.vocab)
-        # the synthetic client "sends" the step's requests into a pinned
-        # receive arena, as the RPC reader does for real connections
-        arena = RequestArena(sum(len(b) for b in bodies) + 16 * len(bodies) + 64)
-        for b in bodies:
-            arena.append(b)
-        offs, lens = arena.spans()
-        pools.append((arena, offs, lens))
-    samples_per_step = args.requests * args.per_request
+    nat = native()
+    gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, local_world)))
+    p_corr, vocab = (0.0, (1 << 31) - 1) if args.worst_case else (0.6, args.vocab)
+    pinned = device is not None
+    # warmup data: its own seed, a few batches cycled (untimed)
+    warm = FreshStream(nat, torch, pinned, args, 1_000_003 * (rank + 1) + 17,
+                       max(1, args.warmup_pools), gen_threads, p_corr, vocab)
+    batch_bytes = warm.nbytes / max(1, len(warm.batches))
+    if args.batches_per_step > 0:
+        bps = args.batches_per_step
+    else:
+        budget = args.fresh_gb * 1e9 if args.fresh_gb > 0 else \
+            min(56e9, 0.6 * _mem_available() / max(1, local_world))
+        bps = int(budget // max(1.0, batch_bytes * args.steps))
+        bps = max(1, min(96, bps))
+    t_gen = time.perf_counter()
+    fresh = FreshStream(nat, torch, pinned, args, 7_919 * (rank + 1) + 3, bps * args.steps,
+                        gen_threads, p_corr, vocab)
+    t_gen = time.perf_counter() - t_gen
+    samples_per_batch = args.requests * args.per_request
+    samples_per_step = samples_per_batch * bps
 
     # host-side metadata (label agreement, count deltas) rides on a gloo group
     # so the MIX never forces a GPU synchronisation
@@ -182,17 +271,17 @@ def main() -> None:
             pending[0] = None
 
     mixes = [0]
-
     agreed = {"version": None, "labels": False}
-
     inflight = {"work": None, "flags": None}
+    nbatch = [0]
 
-    def mix_due(i: int) -> bool:
+    def mix_due() -> bool:
+        i = nbatch[0]
         if args.mix_every > 0 or args.mix_mode == "sync":
             return (i + 1) % max(1, args.mix_every) == 0
         # adaptive: every rank must agree (the collectives have to match).
-        # One tiny host all-reduce per step carries [not ready, labels
-        # changed]; it is issued asynchronously and read one step later, so
+        # One tiny host all-reduce per batch carries [not ready, labels
+        # changed]; it is issued asynchronously and read one batch later, so
         # the host never waits on it (all ranks act on the same lagged flags)
         due = False
         if inflight["work"] is not None:
@@ -201,18 +290,19 @@ def main() -> None:
             agreed["labels"] = f[1].item() == 0
             due = f[0].item() == 0
         v = clf.labels.version()
-        # a MIX that starts this step is not finished by the next one
+        # a MIX that starts this batch is not finished by the next one
         flags = torch.tensor([0 if (not due and clf.mix_ready(pending[0])) else 1,
                               0 if v == agreed["version"] else 1], dtype=torch.int32)
         inflight["flags"] = flags
         inflight["work"] = dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=meta, async_op=True)
         return due
 
-    def step(i: int) -> None:
-        arena, offs, lens = pools[i % len(pools)]
+    def train_batch(arena) -> None:
+        offs = np.asarray(arena.offs, np.int64)
+        lens = np.asarray(arena.lens, np.int64)
         n = clf.train_arena(arena, offs, lens)
-        assert n == samples_per_step
-        if world > 1 and mix_due(i):
+        assert n == samples_per_batch
+        if world > 1 and mix_due():
             mixes[0] += 1
             if args.mix_mode == "sync":
                 clf.mix()
@@ -223,6 +313,7 @@ def main() -> None:
                                            agreed_version=agreed["version"] if agreed["labels"] else None)
                 if "sync" not in pending[0] and clf.labels.version() == v:
                     agreed["version"] = v
+        nbatch[0] += 1
 
     # setup objects (synthetic bodies, torch modules) move to the permanent
     # generation, so a cyclic-GC pass in the timed loop does not traverse them
@@ -230,11 +321,13 @@ def main() -> None:
     gc.collect()
     gc.freeze()
     for i in range(args.warmup):
-        step(i)
+        for j in range(bps):
+            train_batch(warm.batches[(i * bps + j) % len(warm.batches)])
     finish_mix()
     if device is not None:
         clf.pipe.check_errors()
     sync()
+    st0 = clf.train_stats()
     barrier()
     sync()
     trace_steps = os.environ.get("JB_BENCH_TRACE") == "1"
@@ -242,7 +335,8 @@ def main() -> None:
     mixes[0] = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        for j in range(bps):
+            train_batch(fresh.batches[i * bps + j])
         if trace_steps:
             marks.append(time.perf_counter())
     finish_mix()          # the last MIX completes inside the timed region
@@ -261,6 +355,11 @@ def main() -> None:
         elapsed = float(t.item())
     if device is not None:
         clf.pipe.check_errors()
+    clf.synchronize()     # label-count records of the last batches
+    st1 = clf.train_stats()
+    trained = st1["trained"] - st0["trained"]
+    updated = st1["updated"] - st0["updated"]
+    replayed = clf._scan_stats.get("replayed", 0)
 
     # accuracy on a held-out synthetic request (sanity: the model learns)
     test = make_requests(random.Random(99), 1, 2048, args.labels, args.str_features,
@@ -297,24 +396,37 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic (label-correlated datums, 8 str + 8 num features), random-init model",
+            "data": ("synthetic, non-repeating: every timed sample is new (native generator, pinned "
+                     "host memory, H2D inside the timed region); "
+                     + ("worst case: noise string values, every sample updates; " if args.worst_case
+                        else "label-correlated datums; ")
+                     + "8 str + 8 num features, zero-init model"),
             "config": {
                 "model": "jubaclassifier AROW (config/classifier/arow.json: regularization_weight 1.0, "
                          "str bin/bin + num)",
                 "global_batch": samples_per_step * world,
                 "seq_len": None,
                 "parallelism": f"dp{world}",
-                "requests_per_step_per_gpu": args.requests,
+                "batches_per_step": bps,
+                "requests_per_batch_per_gpu": args.requests,
                 "samples_per_request": args.per_request,
                 "hash_max_size": 1 << args.hash_bits,
                 "labels": args.labels,
                 "mix": (f"linear, RCCL all-reduce mean of W and P, {args.mix_mode}, "
-                        + (f"every {args.mix_every} step(s)" if args.mix_every > 0 else
+                        + (f"every {args.mix_every} batch(es)" if args.mix_every > 0 else
                            "back to back (a new MIX as soon as the previous one finished)")
                         + f"; {mixes[0]} MIXes in the timed steps") if world > 1 else "standalone",
                 "concurrent_update": args.update_mode,
+                "hot_rows": clf.hot_rows,
                 "numa_node": numa.get("node"),
+                "world_size_observed": world,
             },
+            "timed_region_s": round(elapsed, 3),
+            "timed_samples_per_rank": samples_per_step * args.steps,
+            "timed_bytes_per_rank": int(fresh.nbytes),
+            "update_fraction": round(updated / trained, 4) if trained else None,
+            "samples_replayed_batches": replayed,
+            "data_gen_s": round(t_gen, 1),
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),
             "heldout_accuracy": round(acc, 4),

@@ -38,7 +38,9 @@ def native():
 
 
 def hip_lib_path() -> str:
-    return os.path.join(_PKG, "libjubatus_hip.so")
+    # JUBATUS_HIP_LIB: an alternative in-tree build (kernel experiments)
+    alt = os.environ.get("JUBATUS_HIP_LIB")
+    return os.path.join(_PKG, alt) if alt else os.path.join(_PKG, "libjubatus_hip.so")
 
 
 def hip_lib() -> ctypes.CDLL:

@@ -130,12 +130,17 @@ __device__ __forceinline__ void argmax_wrong(float& best, int& bl) {
 
 // One sample on the direct path: gathers straight from W / P (any feature
 // count, any label capacity) and applies the update. Used for samples wider
-// than the pipelined window and for label capacities above 64.
+// than the pipelined window and for label capacities above 64. Returns
+// whether the sample updated. The increments are applied with float atomics
+// in every mode: a row repeated inside the sample then counts every time
+// (as in the reference's per-feature loop), and in exact mode (one stream)
+// nothing else touches the table, so the result is the same as plain stores.
 template <int LC, int MODE>
-__device__ __forceinline__ void general_sample(const int32_t* __restrict__ fidx,
+__device__ __forceinline__ bool general_sample(const int32_t* __restrict__ fidx,
                                                const float* __restrict__ fval, int64_t beg, int n,
                                                int y, float* W, float* P, const bool (&act)[Lanes<LC>::K],
-                                               int lane, int method, float C) {
+                                               int lane, int method, float C,
+                                               uint8_t* __restrict__ touched) {
   using L = Lanes<LC>;
   const int l0 = lane % L::LW;
   const bool use_s = method >= CW;
@@ -173,7 +178,7 @@ __device__ __forceinline__ void general_sample(const int32_t* __restrict__ fidx,
   var = wave_sum(var);
   nrm = wave_sum(nrm);
   float tau = 0.f, beta = 0.f;
-  if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return;
+  if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return false;
   for (int base = 0; base < n; base += 64) {
     const int j = base + lane;
     if (j >= n) continue;
@@ -183,13 +188,10 @@ __device__ __forceinline__ void general_sample(const int32_t* __restrict__ fidx,
     const int64_t row = (int64_t)idx * LC;
     const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
     const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
-    float wy = 0.f, wl = 0.f;
-    if (MODE != kAtomic) {
-      wy = ld_agent(W + row + y);
-      wl = lstar >= 0 ? ld_agent(W + row + lstar) : 0.f;
-    }
-    apply_feature<LC, MODE>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, wy, wl);
+    apply_feature<LC, kAtomic>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, 0.f, 0.f);
+    if (touched != nullptr) touched[idx] = 1;
   }
+  return true;
 }
 
 // Label capacities above 64: every sample on the direct path.
@@ -198,7 +200,8 @@ __global__ __launch_bounds__(256) void linear_train_wide_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
-    const int32_t* __restrict__ active, int method, float C) {
+    const int32_t* __restrict__ active, int method, float C,
+    unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched) {
   using L = Lanes<LC>;
   const int lane = threadIdx.x & 63;
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -206,14 +209,160 @@ __global__ __launch_bounds__(256) void linear_train_wide_kernel(
   bool act[L::K];
 #pragma unroll
   for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
+  unsigned n_upd = 0, n_valid = 0;
   for (int64_t s = stream_ptr[wid]; s < stream_ptr[wid + 1]; ++s) {
     const int y = labels[s];
     if (y < 0 || y >= LC) continue;
+    ++n_valid;
     const int64_t beg = row_ptr[s];
-    general_sample<LC, MODE>(fidx, fval, beg, (int)(row_ptr[s + 1] - beg), y, W, P, act, lane,
-                             method, C);
+    if (general_sample<LC, MODE>(fidx, fval, beg, (int)(row_ptr[s + 1] - beg), y, W, P, act, lane,
+                                 method, C, touched))
+      ++n_upd;
     if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  if (stats != nullptr && lane == 0 && n_valid > 0) {
+    atomicAdd(stats, (unsigned long long)n_upd);
+    atomicAdd(stats + 1, (unsigned long long)n_valid);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Hot rows (concurrent modes). A feature row that most samples of a batch
+// carry (the headline's always-present numeric keys, a bias feature) makes
+// every stream issue memory-side atomics on the same few cache lines every
+// sample; those serialise (~60 ns per line request): 9-11 ms per 131 072
+// samples with 8 such rows (profiles/r01_train_kernel_contention.jsonl,
+// profiles/r02_train_kernel_hot.jsonl). csrc/hip/hot.hip finds such rows per
+// batch; the train kernel then keeps them out of the table:
+//   * every block holds an LDS replica of the hot rows that its 4 streams
+//     read and update (LDS atomics): the block's own updates are seen at once;
+//   * blocks exchange their progress through kRep delta shards in global
+//     memory (rep[r][t][e], block b adds to shard b % kRep): each sample, every
+//     wave swaps the block's new increments of the entries it owns out of hA,
+//     adds them to its shard with a returning atomic and reads the other
+//     shards; a sample later (the round trip hides behind it) the other
+//     blocks' progress is folded into hV. A shard line takes 1/kRep of the
+//     atomics a table line took, and nothing writes the table rows;
+//   * after the launch, hot_fold_kernel adds the summed shards to the table
+//     and clears them.
+// Every increment reaches the table exactly once; a stream sees other
+// blocks' updates about two samples late (merge_every = 1). LDS per block:
+//   hV  live value = table value at start + all shards seen + own since
+//   hA  the block's increments not yet added to its shard
+//   hB  the sum over shards at the block's last refresh
+// Precision increments are additive (see header), so the same scheme serves
+// W (t = 0) and P (t = 1).
+#ifndef JB_KREP
+#define JB_KREP 8
+#endif
+constexpr int kRep = JB_KREP;
+
+template <int LC>
+struct Hot {
+  static constexpr int E = 512;                               // entries per table
+  static constexpr int R = (E / LC) < 64 ? (E / LC) : 64;     // hot rows
+  static constexpr int T = 128;                               // lookup slots
+};
+
+// hot slot of a row (-1: not hot); open addressing over hK/hS
+__device__ __forceinline__ int hot_find(const int32_t* hK, const int32_t* hS, int32_t idx) {
+  if (idx < 0) return -1;
+  uint32_t h = ((uint32_t)idx * 0x9E3779B1u) >> 25;
+  for (int p = 0; p < 128; ++p) {
+    const int32_t k = hK[h];
+    if (k == idx) return hS[h];
+    if (k < 0) return -1;
+    h = (h + 1) & 127;
+  }
+  return -1;
+}
+
+// Merge of the (chunk, table) pairs owned by wave `wv` (pair q = wv + NW k:
+// chunk q / 2 of 64 entries, table q % 2), split in two: issue swaps the
+// block delta out of hA, adds it to the block's shard (returning
+// memory-side atomic) and loads the other shards; finish folds the other
+// blocks' progress into hV and moves hB. The train loop issues a merge
+// right after the sample's gather and descriptor loads and finishes it one
+// sample later, before the next merge: the in-order vmcnt then never makes a
+// gather wait for a merge (their ~us round trip stays off the sample chain),
+// and the finish waits only for the merge itself.
+template <int LC, int NW>
+struct HotMerge {
+  static constexpr int KQ = 2 * Hot<LC>::E / 64 / NW;  // pairs per wave
+  float d[KQ];
+  float own[KQ];
+  float oth[KQ][kRep - 1];
+  bool pending = false;
+
+  template <int E>
+  __device__ __forceinline__ void issue(const float* rep, int rr, bool use_s, int nent,
+                                        float (*hA)[E], int wv, int lane) {
+#pragma unroll
+    for (int k = 0; k < KQ; ++k) {
+      const int q = wv + NW * k;
+      const int t = q & 1;
+      const int e = (q >> 1) * 64 + lane;
+      if (e < nent && (t == 0 || use_s)) {
+        float* sh = const_cast<float*>(rep) + (int64_t)(rr * 2 + t) * E + e;
+        d[k] = atomicExch(&hA[t][e], 0.f);
+        own[k] = d[k] != 0.f ? atomicAdd(sh, d[k]) : ld_agent(sh);
+#pragma unroll
+        for (int j = 0; j < kRep - 1; ++j) {
+          const int r = j < rr ? j : j + 1;
+          oth[k][j] = ld_agent(rep + (int64_t)(r * 2 + t) * E + e);
+        }
+      }
+    }
+    pending = true;
+  }
+
+  template <int E>
+  __device__ __forceinline__ void finish(bool use_s, int nent, float (*hV)[E], float (*hB)[E],
+                                         int wv, int lane) {
+    if (!pending) return;
+#pragma unroll
+    for (int k = 0; k < KQ; ++k) {
+      const int q = wv + NW * k;
+      const int t = q & 1;
+      const int e = (q >> 1) * 64 + lane;
+      if (e < nent && (t == 0 || use_s)) {
+        float S = own[k] + d[k];
+#pragma unroll
+        for (int j = 0; j < kRep - 1; ++j) S += oth[k][j];
+        atomicAdd(&hV[t][e], S - hB[t][e] - d[k]);
+        hB[t][e] = S;
+      }
+    }
+    pending = false;
+  }
+};
+
+// After a hot launch: table += sum of the shards, shards := 0 (one thread
+// per hot entry and table; stream-ordered after the train kernel, so plain
+// read-modify-write).
+template <int LC>
+__global__ __launch_bounds__(256) void hot_fold_kernel(float* W, float* P, int use_s,
+                                                       const int32_t* __restrict__ hot_rows,
+                                                       const int32_t* __restrict__ hot_n,
+                                                       float* __restrict__ rep,
+                                                       uint8_t* __restrict__ touched) {
+  constexpr int E = Hot<LC>::E;
+  const int nh = min(*hot_n, Hot<LC>::R);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = i % E;
+  const int t = i / E;
+  if (e >= nh * LC || t > 1 || (t == 1 && !use_s)) return;
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < kRep; ++r) {
+    float* p = rep + (int64_t)(r * 2 + t) * E + e;
+    s += *p;
+    *p = 0.f;
+  }
+  const int32_t row = hot_rows[e / LC];
+  float* T = t == 0 ? W : P;
+  if (s != 0.f) T[(int64_t)row * LC + (e % LC)] += s;
+  if (touched != nullptr && t == 0 && e % LC == 0) touched[row] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -228,6 +377,8 @@ __global__ __launch_bounds__(256) void linear_train_wide_kernel(
 // them (the same lock-free semantics as before). Per-sample descriptors
 // (row offsets, labels) come from a 64-entry register window refreshed every
 // ~60 samples; feature descriptors of s+2 are prefetched during s.
+// Features of hot rows (HOT) are staged as -2 - slot and read from the LDS
+// replica at use time instead of being gathered.
 template <int LC>
 struct Pipe {
   static_assert(LC <= 64, "pipelined path covers label capacities up to 64");
@@ -242,10 +393,15 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int i) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+__device__ __forceinline__ float readlane_f(float v, int i) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i));
+}
+
 // Issue the gather of one staged sample: lane (g, l0) loads W / P of
-// features u*G + g, label l0. Every load is unconditional (invalid slots read
-// row 0) and nothing reads the results here, so the whole gather is U (or 2U)
-// loads in flight; ``vmask`` bit u marks the valid slots for the commit.
+// features u*G + g, label l0. Every load is unconditional (invalid and hot
+// slots read row 0) and nothing reads the results here, so the whole gather
+// is U (or 2U) loads in flight; ``vmask`` bit u marks the valid slots for the
+// commit.
 template <int LC>
 __device__ __forceinline__ uint32_t gather_issue(const float* W, const float* P, bool use_s,
                                                  const int32_t* sI, int n, int g, int l0,
@@ -295,13 +451,14 @@ __device__ __forceinline__ void gather_commit(float* sW, float* sP, bool use_s, 
   }
 }
 
-// feature list of a sample into its LDS slot (lane j = feature j)
+// feature list of a sample into its LDS slot (lane j = feature j); hot rows
+// are staged as -2 - slot
 template <int LC>
-__device__ __forceinline__ void put_features(int32_t* sI, float* sX, int32_t idx, float x, int n,
-                                             int lane) {
+__device__ __forceinline__ void put_features(int32_t* sI, float* sX, int32_t idx, int hs, float x,
+                                             int n, int lane) {
   if (lane < Pipe<LC>::F) {
     const bool v = lane < n && idx >= 0;
-    sI[lane] = v ? idx : -1;
+    sI[lane] = v ? (hs >= 0 ? -2 - hs : idx) : -1;
     sX[lane] = v ? x : 0.f;
   }
 }
@@ -335,29 +492,74 @@ __device__ __forceinline__ void group_argmax(float& best, int& bl, int lane) {
   if (LC >= 64) step(partner32_f(best, lane), partner32_i(bl, lane));
 }
 
-template <int LC, int MODE>
-__global__ __launch_bounds__(256) void linear_train_pipe_kernel(
+template <int LC, int MODE, bool HOT, int NW>
+__global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
-    const int32_t* __restrict__ active, int method, float C) {
+    const int32_t* __restrict__ active, int method, float C, const int32_t* __restrict__ hot_rows,
+    const int32_t* __restrict__ hot_n, float* __restrict__ hot_rep, int merge_every,
+    unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched) {
   using Q = Pipe<LC>;
+  using HT = Hot<LC>;
   constexpr int F = Q::F;
-  __shared__ float sW[4][2][F * LC];
-  __shared__ float sP[4][2][F * LC];
-  __shared__ int32_t sI[4][2][F];
-  __shared__ float sX[4][2][F];
+  constexpr int HE = HOT ? HT::E : 1;
+  constexpr int HK = HOT ? HT::T : 1;
+  constexpr int HR = HOT ? HT::R : 1;
+  __shared__ float sW[NW][2][F * LC];
+  __shared__ float sP[NW][2][F * LC];
+  __shared__ int32_t sI[NW][2][F];
+  __shared__ float sX[NW][2][F];
+  __shared__ float hV[2][HE];
+  __shared__ float hA[2][HE];
+  __shared__ float hB[2][HE];
+  __shared__ int32_t hK[HK];
+  __shared__ int32_t hS[HK];
+  __shared__ int32_t hR[HR];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (wid >= nstreams) return;
+  const bool use_s = method >= CW;
+  int nent = 0;
+  if (HOT) {
+    const int nh = min(*hot_n, HT::R);
+    nent = nh * LC;
+    for (int i = threadIdx.x; i < HT::T; i += blockDim.x) hK[i] = -1;
+    __syncthreads();
+    if ((int)threadIdx.x < nh) {
+      const int32_t r = hot_rows[threadIdx.x];
+      hR[threadIdx.x] = r;
+      uint32_t h = ((uint32_t)r * 0x9E3779B1u) >> 25;
+      for (int p = 0; p < HT::T; ++p) {
+        const int32_t old = atomicCAS(&hK[h], -1, r);
+        if (old == -1) { hS[h] = threadIdx.x; break; }
+        if (old == r) break;
+        h = (h + 1) & 127;
+      }
+    }
+    for (int e = threadIdx.x; e < nent; e += blockDim.x) {
+      const int64_t a = (int64_t)hot_rows[e / LC] * LC + (e % LC);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t == 1 && !use_s) break;
+        float S = 0.f;                  // shards of blocks that ran before this one
+#pragma unroll
+        for (int r = 0; r < kRep; ++r) S += ld_agent(hot_rep + (int64_t)(r * 2 + t) * HE + e);
+        hV[t][e] = ld_agent((t == 0 ? W : P) + a) + S;
+        hB[t][e] = S;
+        hA[t][e] = 0.f;
+      }
+    }
+    __syncthreads();
+  }
+  const int rr = blockIdx.x % kRep;
+  const int64_t s_beg = wid < nstreams ? stream_ptr[wid] : 0;
+  const int64_t s_end = wid < nstreams ? stream_ptr[wid + 1] : 0;
+  unsigned n_upd = 0, n_valid = 0;
+  if (s_beg < s_end) {
   const int g = lane / LC;
   const int l0 = lane % LC;
   bool act[1] = {active[l0] != 0};
-  const bool use_s = method >= CW;
-
-  const int64_t s_beg = stream_ptr[wid], s_end = stream_ptr[wid + 1];
-  if (s_beg >= s_end) return;
   // descriptor window: lane i holds row_ptr[wb + i] and labels[wb + i]
   int64_t wb = s_beg;
   int64_t rp = (wb + lane <= s_end) ? row_ptr[wb + lane] : 0;
@@ -383,8 +585,10 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
   JB_CONSUME(x_s);
   JB_CONSUME(idx1);
   JB_CONSUME(x1);
-  put_features<LC>(sI[wv][0], sX[wv][0], idx_s, x_s, n_s, lane);
-  put_features<LC>(sI[wv][1], sX[wv][1], idx1, x1, n1, lane);
+  int hs_s = (HOT && nent > 0) ? hot_find(hK, hS, idx_s) : -1;
+  int hs1 = (HOT && nent > 0) ? hot_find(hK, hS, idx1) : -1;
+  put_features<LC>(sI[wv][0], sX[wv][0], idx_s, hs_s, x_s, n_s, lane);
+  put_features<LC>(sI[wv][1], sX[wv][1], idx1, hs1, x1, n1, lane);
   float gw[Q::U], gp[Q::U];
   uint32_t vmask = 0;
   bool staged = n_s <= F;
@@ -392,6 +596,8 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
     vmask = gather_issue<LC>(W, P, use_s, sI[wv][0], n_s, g, l0, gw, gp);
     gather_commit<LC>(sW[wv][0], sP[wv][0], use_s, n_s, g, l0, vmask, gw, gp);
   }
+  int since_merge = 0;
+  HotMerge<LC, NW> mrg;
 
   for (int64_t s = s_beg; s < s_end; ++s) {
     const int c = (int)((s - s_beg) & 1);
@@ -421,28 +627,48 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       idx2 = lane < n2 ? fidx[b2 + lane] : -1;
       x2 = lane < n2 ? fval[b2 + lane] : 0.f;
     }
+    // 2b. hot rows: retire the previous merge, send the block's increments
+    //     so far (see HotMerge for why here)
+    if constexpr (HOT) {
+      if (nent > 0 && ++since_merge >= merge_every) {
+        since_merge = 0;
+        mrg.template finish<HE>(use_s, nent, hV, hB, wv, lane);
+        mrg.template issue<HE>(hot_rep, rr, use_s, nent, hA, wv, lane);
+      }
+    }
     // 3. sample s (LDS + registers only while the loads above are in flight)
     bool upd = false;
     int lstar = -1;
     float dwy = 0.f, dwl = 0.f, dpy = 0.f, dpl = 0.f, py = 1.f, pl = 1.f, wy = 0.f, wl = 0.f;
     const bool mine = lane < n_s && idx_s >= 0;
+    if (valid_s) ++n_valid;
     if (general_s) {
       const int i = (int)(s - wb);
       const int64_t b0 = readlane64(rp, i);
-      general_sample<LC, MODE>(fidx, fval, b0, (int)(readlane64(rp, i + 1) - b0), y_s, W, P, act,
-                               lane, method, C);
+      upd = general_sample<LC, MODE>(fidx, fval, b0, (int)(readlane64(rp, i + 1) - b0), y_s, W, P,
+                                     act, lane, method, C, touched);
+      if (upd) ++n_upd;
+      upd = false;        // applied already
     } else if (valid_s) {
       const float* cw = sW[wv][c];
       const float* cp = sP[wv][c];
       const float* cx = sX[wv][c];
+      const int32_t* ci = sI[wv][c];
       float acc = 0.f;
 #pragma unroll
       for (int u = 0; u < Q::U; ++u) {
         const int j = u * Q::G + g;
-        if (j < n_s) acc += cx[j] * cw[j * LC + l0];
+        if (j < n_s) {
+          float w = cw[j * LC + l0];
+          if (HOT) {
+            const int32_t si = ci[j];
+            if (si <= -2) w = hV[0][(-2 - si) * LC + l0];
+          }
+          acc += cx[j] * w;
+        }
       }
       acc = group_sum<LC>(acc, lane);
-      const float sy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), y_s));
+      const float sy = readlane_f(acc, y_s);
       float best = (act[0] && l0 != y_s) ? acc : -INFINITY;
       int bl = (act[0] && l0 != y_s) ? l0 : -1;
       group_argmax<LC>(best, bl, lane);
@@ -452,19 +678,32 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       float a = 1.f, b = 1.f, x2s = 0.f;
       if (mine) {
         x2s = x_s * x_s;
+        if (HOT && hs_s >= 0) {
+          const int hb = hs_s * LC;
+          wy = hV[0][hb + y_s];
+          wl = lstar >= 0 ? hV[0][hb + lstar] : 0.f;
+          if (use_s) {
+            py = hV[1][hb + y_s];
+            pl = lstar >= 0 ? hV[1][hb + lstar] : 1.f;
+          }
+        } else {
+          if (use_s) {
+            py = cp[lane * LC + y_s];
+            pl = lstar >= 0 ? cp[lane * LC + lstar] : 1.f;
+          }
+          wy = cw[lane * LC + y_s];
+          wl = lstar >= 0 ? cw[lane * LC + lstar] : 0.f;
+        }
         if (use_s) {
-          py = cp[lane * LC + y_s];
-          pl = lstar >= 0 ? cp[lane * LC + lstar] : 1.f;
           a = 1.f / py;
           b = lstar >= 0 ? 1.f / pl : 0.f;
         }
-        wy = cw[lane * LC + y_s];
-        wl = lstar >= 0 ? cw[lane * LC + lstar] : 0.f;
       }
       const float var = use_s ? wave_sum_fast(x2s * (a + b), lane) : 0.f;
       const float nrm = wave_sum_fast(x2s, lane);
       float tau = 0.f, beta = 0.f;
       upd = step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta);
+      if (upd) ++n_upd;
       if (upd && mine) {
         dwy = use_s ? tau * a * x_s : tau * x_s;
         dwl = use_s ? -tau * b * x_s : -tau * x_s;
@@ -480,15 +719,15 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
       if (upd) {
         float fwy = 0.f, fwl = 0.f, fpy = 0.f, fpl = 0.f;
-        const bool kv = lane < n1 && idx1 >= 0;
+        const bool kv = lane < n1 && idx1 >= 0 && hs1 < 0;
         for (int j = 0; j < n_s; ++j) {
           const int32_t ij = __builtin_amdgcn_readlane(idx_s, j);
           const bool hit = kv && ij == idx1;
           if (__builtin_amdgcn_ballot_w64(hit)) {
-            const float ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dwy), j));
-            const float al = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dwl), j));
-            const float by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dpy), j));
-            const float bq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dpl), j));
+            const float ay = readlane_f(dwy, j);
+            const float al = readlane_f(dwl, j);
+            const float by = readlane_f(dpy, j);
+            const float bq = readlane_f(dpl, j);
             if (hit) { fwy += ay; fwl += al; fpy += by; fpl += bq; }
           }
         }
@@ -508,23 +747,65 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
     }
     JB_CONSUME(idx2);
     JB_CONSUME(x2);
-    // 5. apply s to the table
-    if (upd && mine) {
-      const int64_t row = (int64_t)idx_s * LC;
-      if (MODE == kAtomic) {
-        atomicAdd(W + row + y_s, dwy);
-        if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+    const int hs2 = (HOT && nent > 0) ? hot_find(hK, hS, idx2) : -1;
+    // 5. apply s to the table. Plain-store modes first fold the increments
+    //    of a repeated row (same index twice in one sample) into its first
+    //    lane, so both count (as the atomic and LDS paths do).
+    bool skip = false;
+    if (MODE != kAtomic && upd) {
+      float cy = 0.f, cl = 0.f, qy = 0.f, ql = 0.f;
+      const bool plain = mine && hs_s < 0;
+      for (int j = 0; j < n_s; ++j) {
+        const int32_t ij = __builtin_amdgcn_readlane(idx_s, j);
+        const bool same = plain && ij == idx_s && j != lane;
+        if (__builtin_amdgcn_ballot_w64(same)) {
+          const float ay = readlane_f(dwy, j);
+          const float al = readlane_f(dwl, j);
+          const float by = readlane_f(dpy, j);
+          const float bq = readlane_f(dpl, j);
+          if (same) {
+            if (j < lane) skip = true;
+            else { cy += ay; cl += al; qy += by; ql += bq; }
+          }
+        }
+      }
+      dwy += cy; dwl += cl; dpy += qy; dpl += ql;
+    }
+    if (upd && mine && !skip) {
+      if (HOT && hs_s >= 0) {
+        const int hb = hs_s * LC;
+        atomicAdd(&hV[0][hb + y_s], dwy);
+        atomicAdd(&hA[0][hb + y_s], dwy);
+        if (lstar >= 0) {
+          atomicAdd(&hV[0][hb + lstar], dwl);
+          atomicAdd(&hA[0][hb + lstar], dwl);
+        }
         if (use_s) {
-          atomicAdd(P + row + y_s, dpy);
-          if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
+          atomicAdd(&hV[1][hb + y_s], dpy);
+          atomicAdd(&hA[1][hb + y_s], dpy);
+          if (lstar >= 0) {
+            atomicAdd(&hV[1][hb + lstar], dpl);
+            atomicAdd(&hA[1][hb + lstar], dpl);
+          }
         }
       } else {
-        W[row + y_s] = wy + dwy;
-        if (lstar >= 0) W[row + lstar] = wl + dwl;
-        if (use_s) {
-          P[row + y_s] = py + dpy;
-          if (lstar >= 0) P[row + lstar] = pl + dpl;
+        const int64_t row = (int64_t)idx_s * LC;
+        if (MODE == kAtomic) {
+          atomicAdd(W + row + y_s, dwy);
+          if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+          if (use_s) {
+            atomicAdd(P + row + y_s, dpy);
+            if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
+          }
+        } else {
+          W[row + y_s] = wy + dwy;
+          if (lstar >= 0) W[row + lstar] = wl + dwl;
+          if (use_s) {
+            P[row + y_s] = py + dpy;
+            if (lstar >= 0) P[row + lstar] = pl + dpl;
+          }
         }
+        if (touched != nullptr) touched[idx_s] = 1;
       }
     }
     if (MODE == kExact && (upd || general_s)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -535,11 +816,28 @@ __global__ __launch_bounds__(256) void linear_train_pipe_kernel(
       gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
     }
     // slot c is free again: it receives the features of s+2
-    put_features<LC>(sI[wv][c], sX[wv][c], idx2, x2, n2, lane);
+    put_features<LC>(sI[wv][c], sX[wv][c], idx2, hs2, x2, n2, lane);
     __builtin_amdgcn_wave_barrier();
     staged = pipe1;
-    idx_s = idx1; x_s = x1; n_s = n1; y_s = y1;
-    idx1 = idx2; x1 = x2; n1 = n2; y1 = y2;
+    idx_s = idx1; x_s = x1; n_s = n1; y_s = y1; hs_s = hs1;
+    idx1 = idx2; x1 = x2; n1 = n2; y1 = y2; hs1 = hs2;
+  }
+  if constexpr (HOT) mrg.template finish<HE>(use_s, nent, hV, hB, wv, lane);
+  }  // s_beg < s_end
+  if (stats != nullptr && lane == 0 && n_valid > 0) {
+    atomicAdd(stats, (unsigned long long)n_upd);
+    atomicAdd(stats + 1, (unsigned long long)n_valid);
+  }
+  if (HOT) {
+    __syncthreads();      // every stream of the block has applied its last sample
+    for (int e = threadIdx.x; e < nent; e += blockDim.x) {
+      const float dw = hA[0][e];
+      if (dw != 0.f) atomicAdd(hot_rep + (int64_t)(rr * 2) * HE + e, dw);
+      if (use_s) {
+        const float dp = hA[1][e];
+        if (dp != 0.f) atomicAdd(hot_rep + (int64_t)(rr * 2 + 1) * HE + e, dp);
+      }
+    }
   }
 }
 
@@ -597,22 +895,43 @@ __global__ void mix_apply_kernel(float* __restrict__ w, const float* __restrict_
 
 }  // namespace jb
 
+// hot_rows / hot_n (device): rows to keep in the block LDS replica (nullptr:
+// none; only the concurrent modes with LC <= 64 use them); hot_rep: the
+// delta shards (jb_hot_rep_bytes(), zero-initialised once, left zero). stats (device,
+// 2 x u64, nullable): += samples that updated, samples with a valid label.
+// touched (device, H bytes, nullable): set to 1 for every row an update wrote.
 extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                float* W, float* S, const int32_t* active, int LC, int method,
-                               float C, int mode, hipStream_t stream) {
+                               float C, int mode, const int32_t* hot_rows, const int32_t* hot_n,
+                               float* hot_rep, int merge_every, int hot_waves,
+                               unsigned long long* stats, uint8_t* touched, hipStream_t stream) {
   if (nstreams <= 0) return 0;
   const int threads = 256;
   const int blocks = (nstreams * 64 + threads - 1) / threads;
+  const bool hot = hot_rows != nullptr && hot_n != nullptr && hot_rep != nullptr &&
+                   mode != jb::kExact && LC <= 64;
+  if (merge_every < 1) merge_every = 1;
+  // hot launches: 8 streams per block (half the blocks exchanging hot-row
+  // progress through the shards; see "Hot rows")
+  const int hot_nw = (hot_waves == 16 && LC <= 16) ? 16 : (hot_waves == 4 ? 4 : 8);
+  const int hblocks = (nstreams + hot_nw - 1) / hot_nw;
+#define JB_PIPE(L, M, H, NWV, B)                                                                 \
+  hipLaunchKernelGGL((jb::linear_train_pipe_kernel<(L <= 64 ? L : 64), M, H, NWV>), dim3(B),      \
+                     dim3(64 * NWV), 0, stream, row_ptr, fidx, fval, labels, stream_ptr,          \
+                     nstreams, W, S, active, method, C, hot_rows, hot_n, hot_rep, merge_every,    \
+                     stats, touched);
 #define JB_TRAIN_M(L, M)                                                                      \
-  if (L <= 64)                                                                                \
-    hipLaunchKernelGGL((jb::linear_train_pipe_kernel<(L <= 64 ? L : 64), M>), dim3(blocks),    \
-                       dim3(threads), 0, stream, row_ptr, fidx, fval, labels, stream_ptr,      \
-                       nstreams, W, S, active, method, C);                                    \
-  else                                                                                        \
+  if (L <= 64) {                                                                              \
+    if (hot && M != jb::kExact) {                                                             \
+      if (hot_nw == 16 && L <= 16) { JB_PIPE(L, M, true, (L <= 16 ? 16 : 8), hblocks) }      \
+      else if (hot_nw == 4) { JB_PIPE(L, M, true, 4, hblocks) }                               \
+      else { JB_PIPE(L, M, true, 8, hblocks) }                                                \
+    } else { JB_PIPE(L, M, false, 4, blocks) }                                                \
+  } else                                                                                      \
     hipLaunchKernelGGL((jb::linear_train_wide_kernel<L, M>), dim3(blocks), dim3(threads), 0,  \
                        stream, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,       \
-                       active, method, C);
+                       active, method, C, stats, touched);
 #define JB_TRAIN(L)                                        \
   if (mode == jb::kAtomic) { JB_TRAIN_M(L, jb::kAtomic) }  \
   else if (mode == jb::kHogwild) { JB_TRAIN_M(L, jb::kHogwild) } \
@@ -620,8 +939,20 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
   JB_LC_DISPATCH(LC, JB_TRAIN)
 #undef JB_TRAIN
 #undef JB_TRAIN_M
+#undef JB_PIPE
+  if (hot) {
+#define JB_FOLD(L)                                                                            \
+  hipLaunchKernelGGL((jb::hot_fold_kernel<(L <= 64 ? L : 64)>), dim3(2 * jb::Hot<64>::E / 256), \
+                     dim3(256), 0, stream, W, S, method >= jb::CW ? 1 : 0, hot_rows, hot_n,     \
+                     hot_rep, touched);
+    JB_LC_DISPATCH(LC, JB_FOLD)
+#undef JB_FOLD
+  }
   return (int)hipGetLastError();
 }
+
+// bytes of the hot-row delta shards (float [kRep][2][E]); zero on first use
+extern "C" int64_t jb_hot_rep_bytes() { return (int64_t)jb::kRep * 2 * jb::Hot<8>::E * 4; }
 
 extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                   int n_samples, const float* W, int LC, float* out,

@@ -197,7 +197,10 @@ int64_t frame(py::buffer b) {
 
 }  // namespace
 
+void register_synth(py::module_& m);   // jb_synth.cpp
+
 PYBIND11_MODULE(_jubatus_native, m) {
+  register_synth(m);
   m.doc() = "jubatus_amd host-native runtime: request scanning, hashing, CRC32, MD5";
   py::class_<jb::LabelTable>(m, "LabelTable")
       .def(py::init<>())

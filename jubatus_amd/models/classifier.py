@@ -94,11 +94,29 @@ class LinearClassifier:
         self._result_cols = None
         self.LC = 0
         self._label_version = -1
+        self._host_stats = {"updated": 0, "trained": 0}
+        # hot-row replica of the concurrent train kernel (csrc/hip/hot.hip,
+        # linear.hip "Hot rows"): JUBATUS_HOT_ROWS=0 disables it,
+        # JUBATUS_HOT_MERGE sets the merge interval in samples
+        self.hot_rows = os.environ.get("JUBATUS_HOT_ROWS", "1") != "0"
+        self.hot_merge = max(1, int(os.environ.get("JUBATUS_HOT_MERGE", "1")))
+        self.hot_min_streams = 16
+        self.hot_min_count: int | None = None    # None: max(1024, samples / 128)
         if self.gpu:
             import torch
+            from ..ops import hip
             from ..ops.feature_pipeline import FeaturePipeline
             self.torch = torch
             self.pipe = FeaturePipeline(converter, device)
+            self._hot = hip.HotRows(device)
+            self._hot_count_buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            self._hot_seen = None            # (pinned count, event) of a detection in flight
+            self._hot_last = -1              # hot rows found by the last completed detection
+            self._hot_batches = 0
+            # [samples that updated, samples trained] (device counters)
+            self._train_stats = torch.zeros(2, dtype=torch.int64, device=device)
+            # rows written since the last MIX (sparse MIX, parallel/sparse_mix.py)
+            self.touched = torch.zeros(self.H, dtype=torch.uint8, device=device)
         self._alloc(LABEL_CAPS[0])
 
     # ------------------------------------------------------------ storage
@@ -151,13 +169,48 @@ class LinearClassifier:
         return hip.UPDATE_MODES[self.concurrent_update]
 
     def _train_batch(self, b) -> int:
-        from ..ops import hip
         self._sync_labels()
         if b.n:
-            hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
-                             self.W, self.P, self.active, self.mid, self.C,
-                             mode=self._mode(b.nstreams))
+            self._launch_train(b)
         return b.n
+
+    def _launch_train(self, b) -> None:
+        """one train launch over a device batch; concurrent batches first
+        look for hot rows (on the device, no host synchronisation). While the
+        last detection found none, detection runs on every 8th batch only and
+        the plain 4-stream-block launch is used."""
+        from ..ops import hip
+        mode = self._mode(b.nstreams)
+        hot = None
+        if (self.hot_rows and mode != hip.UPDATE_EXACT and self.LC <= 64
+                and b.nstreams >= self.hot_min_streams):
+            self._hot_batches += 1
+            seen = self._hot_seen
+            if seen is not None and seen[1].query():
+                self._hot_last = int(seen[0][0])
+                self._hot_seen = None
+            if self._hot_last != 0 or self._hot_batches % 8 == 0:
+                min_count = self.hot_min_count or max(1024, b.n // 128)
+                hip.hot_detect(b.row_ptr, b.n, b.fidx, b.nnz, self._hot, min_count,
+                               max_rows=hip.hot_max_rows(self.LC))
+                if self._hot_seen is None:       # learn the count without a sync
+                    buf = self._hot_count_buf
+                    buf.copy_(self._hot.n, non_blocking=True)
+                    ev = self.torch.cuda.Event()
+                    ev.record()
+                    self._hot_seen = (buf, ev)
+                hot = self._hot
+        hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
+                         self.W, self.P, self.active, self.mid, self.C, mode=mode, hot=hot,
+                         merge_every=self.hot_merge, stats=self._train_stats,
+                         touched=self.touched)
+
+    def train_stats(self) -> dict[str, int]:
+        """samples trained / samples that changed the model since creation"""
+        if not self.gpu:
+            return dict(self._host_stats)
+        v = self._train_stats.cpu().tolist()
+        return {"updated": int(v[0]), "trained": int(v[1])}
 
     def train_arena(self, arena, offs, lens) -> int:
         """Train on request bodies that already sit in a pinned RequestArena
@@ -266,15 +319,13 @@ class LinearClassifier:
     def _train_rows(self, rows, labs, sizes) -> None:
         self._sync_labels()
         if self.gpu:
-            from ..ops import hip
-            b = self.pipe.from_rows(rows, labs, sizes)
-            hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
-                             self.W, self.P, self.active, self.mid, self.C,
-                             mode=self._mode(b.nstreams))
+            self._launch_train(self.pipe.from_rows(rows, labs, sizes))
             return
         for (idx, val), y in zip(rows, labs):
-            lo.train_one(self.W, self.P, np.asarray(idx, np.int64), np.asarray(val, np.float32),
-                         y, self.active, self.mid, self.C)
+            up = lo.train_one(self.W, self.P, np.asarray(idx, np.int64), np.asarray(val, np.float32),
+                              y, self.active, self.mid, self.C)
+            self._host_stats["trained"] += 1
+            self._host_stats["updated"] += int(up)
 
     # ----------------------------------------------------------- classify
     def _results(self, scores: np.ndarray) -> list[list[tuple[str, float]]]:

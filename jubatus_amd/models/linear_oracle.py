@@ -31,7 +31,9 @@ always positive, and commutative (what lets concurrent GPU streams apply
 them with float atomics).
 
 Coordinates with idx < 0 are ignored. Every update reads the table before
-the sample and then writes (gather-compute-scatter), like the kernel.
+the sample and then adds its increments (gather-compute-scatter), like the
+kernel; a row that occurs twice in one sample receives both increments
+(the reference's per-feature update loop does the same).
 """
 from __future__ import annotations
 
@@ -108,23 +110,21 @@ def train_one(W: np.ndarray, P: np.ndarray | None, idx: np.ndarray, val: np.ndar
         beta = (C * C * var + 2.0 * C) / (cv * cv)
     else:
         raise ValueError(f"unknown method {method}")
-    wy = W[idx, y].copy()
-    wl = W[idx, lstar].copy() if lstar >= 0 else None
     if use_s:
-        W[idx, y] = wy + np.float32(tau) * a * x
+        np.add.at(W, (idx, y), (np.float32(tau) * a * x).astype(np.float32))
         if lstar >= 0:
-            W[idx, lstar] = wl - np.float32(tau) * b * x
+            np.add.at(W, (idx, lstar), (-np.float32(tau) * b * x).astype(np.float32))
         bx2 = np.float32(beta) * x * x
         if method == CW:
             dy = dl = bx2
         else:
             dy = bx2 / (np.float32(1.0) - bx2 * a)
             dl = bx2 / (np.float32(1.0) - bx2 * b)
-        P[idx, y] = np.float32(1.0) / a + dy
+        np.add.at(P, (idx, y), dy.astype(np.float32))
         if lstar >= 0:
-            P[idx, lstar] = np.float32(1.0) / b + dl
+            np.add.at(P, (idx, lstar), dl.astype(np.float32))
     else:
-        W[idx, y] = wy + np.float32(tau) * x
+        np.add.at(W, (idx, y), (np.float32(tau) * x).astype(np.float32))
         if lstar >= 0:
-            W[idx, lstar] = wl - np.float32(tau) * x
+            np.add.at(W, (idx, lstar), (-np.float32(tau) * x).astype(np.float32))
     return True

@@ -209,6 +209,19 @@ class RequestArena:
         self.lens.append(n)
         return off, n
 
+    @classmethod
+    def over(cls, buf: torch.Tensor, offs, lens) -> "RequestArena":
+        """an arena over an existing (pinned) uint8 tensor that already holds
+        request bodies at ``offs`` / ``lens`` (e.g. a slice of a large
+        pinned block filled by the native generator)"""
+        a = cls.__new__(cls)
+        a.buf = buf
+        a.np = buf.numpy()
+        a.offs = [int(x) for x in offs]
+        a.lens = [int(x) for x in lens]
+        a.used = (a.offs[-1] + a.lens[-1]) if a.offs else 0
+        return a
+
     def reset(self) -> None:
         self.used = 0
         self.offs.clear()

@@ -26,7 +26,11 @@ _SIGS = {
                    _c_void_p, _i32, _c_void_p, _i32, _u64, _c_void_p, _c_void_p, _c_void_p,
                    _c_void_p],
     "jb_linear_train": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
-                        _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p],
+                        _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p, _c_void_p,
+                        _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p],
+    "jb_hot_rep_bytes": [],
+    "jb_hot_detect": [_c_void_p, _i32, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
+                      _i32, _c_void_p, _c_void_p, _c_void_p],
     "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
                            _c_void_p],
     "jb_scale": [_c_void_p, _i64, _f32, _c_void_p],
@@ -194,7 +198,7 @@ def _fn(name: str):
         lib = hip_lib()
         raw = getattr(lib, name)
         raw.argtypes = _SIGS[name]
-        raw.restype = ctypes.c_int
+        raw.restype = ctypes.c_int64 if name.endswith("_bytes") else ctypes.c_int
         tag = "hip." + name[3:]
 
         def f(*args, _raw=raw, _tag=tag):
@@ -287,8 +291,13 @@ def scan_train(buf: torch.Tensor, buf_used: int, req_off: torch.Tensor, req_len:
 def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
                  labels: torch.Tensor, stream_ptr: torch.Tensor, nstreams: int, W: torch.Tensor,
                  S: torch.Tensor | None, active: torch.Tensor, method: int, C: float,
-                 mode: int) -> None:
-    """mode: UPDATE_EXACT (single stream), UPDATE_ATOMIC or UPDATE_HOGWILD."""
+                 mode: int, hot: "HotRows | None" = None, merge_every: int = 8,
+                 stats: torch.Tensor | None = None, touched: torch.Tensor | None = None) -> None:
+    """mode: UPDATE_EXACT (single stream), UPDATE_ATOMIC or UPDATE_HOGWILD.
+    hot: rows found by ``hot_detect`` for this batch (concurrent modes, label
+    capacity <= 64) - kept in a block-shared LDS replica merged every
+    ``merge_every`` samples. stats: int64[2] += (samples that updated,
+    samples with a valid label). touched: uint8[H] rows written := 1."""
     LC = W.shape[1]
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
@@ -302,10 +311,63 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
         _dev(S, torch.float32, "S")
     if stream_ptr.numel() < nstreams + 1:
         raise ValueError("stream_ptr shorter than nstreams+1")
+    if stats is not None:
+        _dev(stats, torch.int64, "stats")
+        if stats.numel() < 2:
+            raise ValueError("stats needs 2 counters")
+    if touched is not None:
+        _dev(touched, torch.uint8, "touched")
+        if touched.numel() < W.shape[0]:
+            raise ValueError("touched shorter than the table")
     rc = _fn("jb_linear_train")(_p(row_ptr), _p(fidx), _p(fval), _p(labels), _p(stream_ptr),
                                 nstreams, _p(W), _p(S) if S is not None else None, _p(active), LC,
-                                method, float(C), int(mode), _stream())
+                                method, float(C), int(mode),
+                                _p(hot.rows) if hot is not None else None,
+                                _p(hot.n) if hot is not None else None,
+                                _p(hot.rep) if hot is not None else None, int(merge_every),
+                                HOT_WAVES,
+                                _p(stats), _p(touched), _stream())
     _check(rc, "jb_linear_train")
+
+
+HOT_MAX_ROWS = 64           # csrc/hip/linear.hip Hot<LC>::R (LC = 8)
+# streams (waves) per block of a hot launch: 4, 8 or 16 (JUBATUS_HOT_WAVES)
+HOT_WAVES = int(__import__("os").environ.get("JUBATUS_HOT_WAVES", "8"))
+HOT_ENTRIES = 512           # Hot<LC>::E: hot rows x label capacity
+
+
+def hot_max_rows(LC: int) -> int:
+    return min(HOT_MAX_ROWS, HOT_ENTRIES // LC)
+
+
+class HotRows:
+    """device hot-row list of one batch, the candidate table hot_detect
+    leaves empty after every call (csrc/hip/hot.hip) and the train kernel's
+    delta shards (csrc/hip/linear.hip "Hot rows"; left zero by every launch)"""
+
+    CAP = 1 << 14
+
+    def __init__(self, device):
+        self.rows = torch.zeros(HOT_MAX_ROWS, dtype=torch.int32, device=device)
+        self.n = torch.zeros(1, dtype=torch.int32, device=device)
+        self.rep = torch.zeros(_fn("jb_hot_rep_bytes")() // 4, dtype=torch.float32, device=device)
+        self.gkey = torch.full((self.CAP,), -1, dtype=torch.int32, device=device)
+        self.gcnt = torch.zeros(self.CAP, dtype=torch.int32, device=device)
+
+
+def hot_detect(row_ptr: torch.Tensor, n: int, fidx: torch.Tensor, max_slots: int, hot: HotRows,
+               min_count: int, block_min: int = 8, max_rows: int = HOT_MAX_ROWS) -> None:
+    """rows carried by at least ``min_count`` of the batch's feature slots
+    -> hot.rows[:hot.n] (device; no host synchronisation)"""
+    _dev(row_ptr, torch.int64, "row_ptr")
+    _dev(fidx, torch.int32, "fidx")
+    if row_ptr.numel() < n + 1 or fidx.numel() < max_slots:
+        raise ValueError("hot_detect: bad operand shapes")
+    max_rows = min(max_rows, hot.rows.numel())
+    rc = _fn("jb_hot_detect")(_p(row_ptr), n, _p(fidx), int(max_slots), int(block_min),
+                              int(min_count), int(max_rows), _p(hot.gkey), _p(hot.gcnt),
+                              hot.CAP, _p(hot.rows), _p(hot.n), _stream())
+    _check(rc, "jb_hot_detect")
 
 
 def linear_classify(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor, n: int,

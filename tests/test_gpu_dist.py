@@ -27,12 +27,14 @@ def test_two_ranks_one_gpu_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--dist-backend", "gloo",
-           "--requests", "64", "--per-request", "32", "--hash-bits", "16", "--latency-iters", "5"]
+           "--requests", "64", "--per-request", "32", "--hash-bits", "16", "--latency-iters", "5",
+           "--batches-per-step", "3"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
-    assert out["config"]["global_batch"] == 2 * 64 * 32
+    assert out["config"]["global_batch"] == 2 * 3 * 64 * 32
+    assert out["config"]["world_size_observed"] == 2 and out["update_fraction"] > 0
     assert "MIXes in the timed steps" in out["config"]["mix"]
     assert out["heldout_accuracy"] > 0.9

@@ -253,3 +253,107 @@ def test_direct_classify_used_for_small_requests():
     assert scores is not None and scores.shape == (1, g.LC)
     big = mp.packb([Datum(d).to_msgpack() for _, d in data], use_bin_type=False)
     assert g.pipe.classify_direct([big], g.W) is None   # > kernarg block: batch path
+
+
+def _shared_data(n, nlabels=6, seed=21, dup=False):
+    """datums that all carry the same numeric keys (hot rows); dup: a key
+    repeated inside the datum (same hashed index twice in one sample)"""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        y = rng.randrange(nlabels)
+        sv = [[f"s{j}", f"v{(y * 7 + rng.randrange(3)) if rng.random() < 0.7 else rng.randrange(300)}"]
+              for j in range(4)]
+        nv = [[f"n{j}", (y - 2) * 0.3 + rng.gauss(0, 1)] for j in range(3)] + [["bias", 1.0]]
+        if dup:
+            nv.append(["n0", 0.5 + rng.random()])
+        out.append((f"L{y}", [sv, nv, []]))
+    return out
+
+
+def test_hot_detect_finds_shared_rows():
+    import torch
+    from jubatus_amd.ops import hip
+    from jubatus_amd.models.classifier import LinearClassifier
+    from jubatus_amd._native import native
+
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV),
+                         device=_device())
+    data = _shared_data(6000)
+    bodies = [msgpack.packb([[l, d] for l, d in data[i:i + 50]], use_bin_type=False)
+              for i in range(0, len(data), 50)]
+    b = g.pipe.from_requests(bodies, True, g.labels)
+    hot = hip.HotRows(_device())
+    hip.hot_detect(b.row_ptr, b.n, b.fidx, b.nnz, hot, min_count=3000)
+    torch.cuda.synchronize()
+    got = sorted(hot.rows[:int(hot.n.item())].cpu().tolist())
+    idx = b.fidx[:int(b.row_ptr[b.n].item())].cpu().numpy()
+    vals, cnt = np.unique(idx[idx >= 0], return_counts=True)
+    assert got == sorted(vals[cnt >= 3000].tolist())
+    assert len(got) >= 4                       # n0, n1, n2, bias (+ the log rule of n1)
+    assert int((hot.gkey != -1).sum().item()) == 0   # candidate table left empty
+
+
+@pytest.mark.parametrize("method", ["AROW", "PA1"])
+def test_hot_replica_single_stream_matches_oracle(method):
+    """one stream through the hot-row LDS replica (atomic mode, merges every
+    3 samples) == the exact sequential oracle"""
+    from jubatus_amd.models.classifier import LinearClassifier
+    from jubatus_amd.ops import hip
+
+    g = LinearClassifier(method, {"regularization_weight": 0.5}, DatumToFvConverter(CONV),
+                         device=_device())
+    c = LinearClassifier(method, {"regularization_weight": 0.5}, DatumToFvConverter(CONV))
+    g._mode = lambda n: hip.UPDATE_ATOMIC
+    g.hot_min_streams, g.hot_min_count, g.hot_merge = 1, 50, 3
+    data = _shared_data(600, seed=4)
+    for i in range(0, len(data), 200):
+        g.train(data[i:i + 200])
+        c.train(data[i:i + 200])
+    g.synchronize()
+    st = g.train_stats()
+    assert st["trained"] == 600 and st["updated"] == c.train_stats()["updated"]
+    scale = float(np.abs(c.W).max()) or 1.0
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+    if c.P is not None:
+        np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3,
+                                   atol=2e-3 * float(c.P.max()))
+
+
+@pytest.mark.parametrize("mode", ["exact", "atomic", "hogwild"])
+def test_repeated_index_in_sample_counts_twice(mode):
+    """a num key repeated inside a datum: both increments land (every mode)"""
+    from jubatus_amd.models.classifier import LinearClassifier
+    from jubatus_amd.ops import hip
+
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV),
+                         device=_device(), concurrent_update="atomic" if mode == "exact" else mode)
+    c = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV))
+    g._mode = lambda n: hip.UPDATE_MODES[mode]
+    g.hot_rows = False
+    data = _shared_data(300, seed=5, dup=True)
+    g.train(data)
+    c.train(data)
+    g.synchronize()
+    scale = float(np.abs(c.W).max()) or 1.0
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+    np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3, atol=2e-3 * float(c.P.max()))
+
+
+@pytest.mark.parametrize("mode", ["atomic", "hogwild"])
+def test_concurrent_streams_learn_with_hot_replica(mode):
+    """128 concurrent streams all sharing hot rows (LDS replica on) still learn"""
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV),
+                         device=_device(), concurrent_update=mode)
+    g.hot_min_count = 500
+    data = _shared_data(128 * 40, seed=7)
+    bodies = [msgpack.packb([[l, d] for l, d in data[i:i + 40]], use_bin_type=False)
+              for i in range(0, len(data), 40)]
+    assert g.train_requests(bodies) == len(data)
+    test = _shared_data(600, seed=8)
+    res = g.classify([d for _, d in test])
+    acc = np.mean([max(r, key=lambda t: t[1])[0] == l for r, (l, _) in zip(res, test)])
+    assert acc > 0.8, acc
+    g.pipe.check_errors()
