@@ -108,7 +108,8 @@ class LinearClassifier:
             from ..ops.feature_pipeline import FeaturePipeline
             self.torch = torch
             self.pipe = FeaturePipeline(converter, device)
-            self._hot = hip.HotRows(device)
+            self._hots = [hip.HotRows(device), hip.HotRows(device)]
+            self._hot_turn = 0
             self._hot_count_buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._hot_seen = None            # (pinned count, event) of a detection in flight
             self._hot_last = -1              # hot rows found by the last completed detection
@@ -174,36 +175,58 @@ class LinearClassifier:
             self._launch_train(b)
         return b.n
 
-    def _launch_train(self, b) -> None:
-        """one train launch over a device batch; concurrent batches first
-        look for hot rows (on the device, no host synchronisation). While the
-        last detection found none, detection runs on every 8th batch only and
-        the plain 4-stream-block launch is used."""
+    def _hot_wanted(self, nstreams: int) -> bool:
+        """detect hot rows for a batch of ``nstreams`` streams? While the last
+        detection found none, only every 8th batch looks (and trains with the
+        plain 4-stream-block launch)."""
         from ..ops import hip
+        if not (self.gpu and self.hot_rows and self.LC <= 64 and nstreams >= self.hot_min_streams
+                and self._mode(nstreams) != hip.UPDATE_EXACT):
+            return False
+        self._hot_batches += 1
+        seen = self._hot_seen
+        if seen is not None and seen[1].query():
+            self._hot_last = int(seen[0][0])
+            self._hot_seen = None
+        return self._hot_last != 0 or self._hot_batches % 8 == 0
+
+    def _detect_hot(self, b) -> None:
+        """enqueue hot-row detection of batch ``b`` on the current stream into
+        the next of two alternating sets (a set is reused once the train
+        launch that read it has run: a device-side wait)"""
+        from ..ops import hip
+        hs = self._hots[self._hot_turn]
+        self._hot_turn ^= 1
+        if hs.free is not None:
+            self.torch.cuda.current_stream().wait_event(hs.free)
+        min_count = self.hot_min_count or max(1024, b.n // 128)
+        hip.hot_detect(b.row_ptr, b.n, b.fidx, b.nnz, hs, min_count,
+                       max_rows=hip.hot_max_rows(self.LC))
+        if self._hot_seen is None:       # learn the count without a host sync
+            self._hot_count_buf.copy_(hs.n, non_blocking=True)
+            ev = self.torch.cuda.Event()
+            ev.record()
+            self._hot_seen = (self._hot_count_buf, ev)
+        b.hot = hs
+
+    def _launch_train(self, b) -> None:
+        """one train launch over a device batch (after its preparation, if it
+        was prepared on another stream); concurrent batches use the hot-row
+        replica when hot rows were detected (csrc/hip/hot.hip)"""
+        from ..ops import hip
+        if b.ready is not None:
+            self.torch.cuda.current_stream().wait_event(b.ready)
         mode = self._mode(b.nstreams)
-        hot = None
-        if (self.hot_rows and mode != hip.UPDATE_EXACT and self.LC <= 64
-                and b.nstreams >= self.hot_min_streams):
-            self._hot_batches += 1
-            seen = self._hot_seen
-            if seen is not None and seen[1].query():
-                self._hot_last = int(seen[0][0])
-                self._hot_seen = None
-            if self._hot_last != 0 or self._hot_batches % 8 == 0:
-                min_count = self.hot_min_count or max(1024, b.n // 128)
-                hip.hot_detect(b.row_ptr, b.n, b.fidx, b.nnz, self._hot, min_count,
-                               max_rows=hip.hot_max_rows(self.LC))
-                if self._hot_seen is None:       # learn the count without a sync
-                    buf = self._hot_count_buf
-                    buf.copy_(self._hot.n, non_blocking=True)
-                    ev = self.torch.cuda.Event()
-                    ev.record()
-                    self._hot_seen = (buf, ev)
-                hot = self._hot
+        if b.hot is None and b.ready is None and self._hot_wanted(b.nstreams):
+            self._detect_hot(b)
+        hs = b.hot
         hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
-                         self.W, self.P, self.active, self.mid, self.C, mode=mode, hot=hot,
+                         self.W, self.P, self.active, self.mid, self.C, mode=mode, hot=hs,
                          merge_every=self.hot_merge, stats=self._train_stats,
                          touched=self.touched)
+        if hs is not None:
+            hs.free = self.torch.cuda.Event()
+            hs.free.record()
 
     def train_stats(self) -> dict[str, int]:
         """samples trained / samples that changed the model since creation"""
@@ -229,7 +252,8 @@ class LinearClassifier:
                 self._drain(block=True, keep=3)
                 self._sync_labels()
                 chk = self._check_record(self.labels.size())
-                b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk)
+                post = self._detect_hot if self._hot_wanted(len(offs)) else None
+                b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk, post=post)
                 if b is not None:
                     self._scan_stats["gpu"] += 1
                     n = self._train_batch(b)

@@ -153,6 +153,8 @@ class DeviceBatch:
     fval: torch.Tensor        # float32 [nnz]
     labels: torch.Tensor | None   # int32 [n]
     stream_ptr: torch.Tensor  # int64 [nstreams+1]
+    ready: torch.cuda.Event | None = None   # prepared on the prep stream: wait before use
+    hot: object | None = None               # hot rows detected for this batch (classifier)
 
 
 class _Pinned:
@@ -257,6 +259,10 @@ class FeaturePipeline:
         self._devsets = [_DeviceBufs(self.device), _DeviceBufs(self.device)]
         self._dev = self._devsets[0]      # scratch for single-shot users (classify)
         self._copy_stream = torch.cuda.Stream(device=self.device)
+        # GPU-scan batches are prepared (scan, fv_hash, hot-row detection) on
+        # their own stream, so batch k+1's preparation runs beside batch k's
+        # train kernel (which occupies only part of the CUs)
+        self._prep_stream = torch.cuda.Stream(device=self.device)
         self._last_mark: torch.cuda.Event | None = None
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self._direct = None
@@ -351,13 +357,15 @@ class FeaturePipeline:
         return self._ltab[1:]
 
     def from_arena_gpu(self, arena: RequestArena, offs: np.ndarray, lens: np.ndarray, table,
-                       check: ScanCheck) -> DeviceBatch | None:
+                       check: ScanCheck, post=None) -> DeviceBatch | None:
         """Train batch from arena spans with the scan on the GPU
         (csrc/hip/scan.hip): H2D of the raw arena, then scan -> fixup ->
         fv_hash on the compute stream, no host walk. ``check`` receives the
         batch's error bits and label counts (pinned, valid once its event
         completes); a batch with error bits set trained nothing and must be
-        re-run through from_arena. None: a body header the host must report."""
+        re-run through from_arena. None: a body header the host must report.
+        The device work runs on the prep stream; ``post(batch)`` is enqueued
+        there after fv_hash; the batch's ``ready`` event covers all of it."""
         if not self.fast:
             raise RuntimeError("converter config is not eligible for the GPU fast path")
         offs = np.ascontiguousarray(offs, dtype=np.int64)
@@ -418,21 +426,29 @@ class FeaturePipeline:
         cev = torch.cuda.Event()
         cev.record(cs)
         self._scan_meta_ev[turn] = cev
-        compute.wait_event(cev)
-        th, tm, tb = self.label_table(table)
-        d_sb = d_meta[2 * R:3 * R + 1]
-        nh = check.hist.size
-        check.err[0] = -1                 # not yet written
-        hip.scan_train(d_buf, used, d_meta[:R], d_meta[R:2 * R], d_sb, R, n, th, tm, tb, sps, spn,
-                       d_off, d_len, d_lab, d_row, d_slots, d_hist[:nh], d_err, empty_off, check.buf)
-        check.nhist = nh
-        check.event = torch.cuda.Event()
-        check.event.record(compute)
-        if n > 0:
-            hip.fv_hash(d_buf, empty_off + 3, d_off, d_len, d_row, n, self.d_srules,
-                        self.rules.n_srules, self.d_nrules, self.rules.n_nrules, self.d_blob, self.H,
-                        d_idx, d_val, self.err)
-        return DeviceBatch(n, slot_cap, R, d_row, d_idx, d_val, d_lab, d_sb)
+        prep = self._prep_stream
+        prep.wait_event(cev)
+        with torch.cuda.stream(prep):
+            th, tm, tb = self.label_table(table)
+            d_sb = d_meta[2 * R:3 * R + 1]
+            nh = check.hist.size
+            check.err[0] = -1                 # not yet written
+            hip.scan_train(d_buf, used, d_meta[:R], d_meta[R:2 * R], d_sb, R, n, th, tm, tb, sps,
+                           spn, d_off, d_len, d_lab, d_row, d_slots, d_hist[:nh], d_err, empty_off,
+                           check.buf)
+            check.nhist = nh
+            check.event = torch.cuda.Event()
+            check.event.record(prep)
+            if n > 0:
+                hip.fv_hash(d_buf, empty_off + 3, d_off, d_len, d_row, n, self.d_srules,
+                            self.rules.n_srules, self.d_nrules, self.rules.n_nrules, self.d_blob,
+                            self.H, d_idx, d_val, self.err)
+            b = DeviceBatch(n, slot_cap, R, d_row, d_idx, d_val, d_lab, d_sb)
+            if post is not None and n > 0:
+                post(b)
+            b.ready = torch.cuda.Event()
+            b.ready.record(prep)
+        return b
 
     def _launch(self, pin: "_Pinned", src: torch.Tensor, n: int, nbytes: int, nslots: int,
                 R: int, labeled: bool) -> DeviceBatch:

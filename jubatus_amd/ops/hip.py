@@ -351,6 +351,7 @@ class HotRows:
         self.rows = torch.zeros(HOT_MAX_ROWS, dtype=torch.int32, device=device)
         self.n = torch.zeros(1, dtype=torch.int32, device=device)
         self.rep = torch.zeros(_fn("jb_hot_rep_bytes")() // 4, dtype=torch.float32, device=device)
+        self.free = None        # event: the train launch that read this set has run
         self.gkey = torch.full((self.CAP,), -1, dtype=torch.int32, device=device)
         self.gcnt = torch.zeros(self.CAP, dtype=torch.int32, device=device)
 
