@@ -52,6 +52,20 @@ def argv_from_wire(v) -> dict:
     return {k: (x.decode() if isinstance(x, bytes) else x) for k, x in zip(ARGV_FIELDS, v)}
 
 
+def count_gpus() -> int:
+    """GPUs of this host from the KFD topology (no HIP runtime needed)"""
+    n = 0
+    for i in range(256):
+        try:
+            with open(f"/sys/class/kfd/kfd/topology/nodes/{i}/properties") as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            break
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    return n
+
+
 def split_server_name(s: str) -> tuple[str, str]:
     """"jubaclassifier/name" -> ("jubaclassifier", "name") (process.cpp set_names)"""
     if "/" not in s:
@@ -63,10 +77,12 @@ def split_server_name(s: str) -> tuple[str, str]:
 
 
 def child_command(server: str, name: str, port: int, zk: str, a: dict,
-                  listen_addr: str = "") -> list[str]:
+                  listen_addr: str = "", gpu: int = -1) -> list[str]:
     engine = server[len("juba"):]
     cmd = [sys.executable, "-m", "jubatus_amd.cmd.server", engine, "-z", zk, "-n", name,
            "-p", str(port)]
+    if gpu >= 0:
+        cmd += ["--gpu", str(gpu)]
     if listen_addr:
         cmd += ["-b", listen_addr]
     if a.get("bind_if"):
@@ -84,8 +100,10 @@ def child_command(server: str, name: str, port: int, zk: str, a: dict,
 
 class Jubavisor:
     def __init__(self, zk: str, port: int, max_children: int = 16, timeout: float = 10.0,
-                 listen_addr: str = ""):
+                 listen_addr: str = "", gpus: int = -1):
         self.zk = zk
+        # one server process per GPU: children get the least used device
+        self.gpu_users = [0] * (gpus if gpus >= 0 else count_gpus())
         self.listen_addr = listen_addr
         self.ls = CoordinatorClient(zk, timeout=timeout)
         self.port_base = port
@@ -108,6 +126,7 @@ class Jubavisor:
                         if p[0].poll() is not None:
                             log.info("%s with port %d exited pid: %d", p[2], p[1], p[0].pid)
                             self.pool.append(p[1])
+                            self._give_gpu(p[3])
                             procs.remove(p)
 
     def start(self, server_name, n, argv) -> int:
@@ -131,15 +150,18 @@ class Jubavisor:
             env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
             for _ in range(need):
                 port = self.pool.pop(0)
-                cmd = child_command(server, name, port, self.zk, a, self.listen_addr)
+                gpu = self._take_gpu()
+                cmd = child_command(server, name, port, self.zk, a, self.listen_addr, gpu)
                 try:
                     p = subprocess.Popen(cmd, env=env, stdin=subprocess.DEVNULL)
                 except OSError as e:
                     log.error("cannot start: %s (%s)", name, e)
                     self.pool.append(port)
+                    self._give_gpu(gpu)
                     return -1
-                log.info("started %s on port %d (pid %d)", server_name, port, p.pid)
-                procs.append((p, port, server_name))
+                log.info("started %s on port %d (pid %d%s)", server_name, port, p.pid,
+                         f", gpu {gpu}" if gpu >= 0 else "")
+                procs.append((p, port, server_name, gpu))
         return 0
 
     def stop(self, server_name, n) -> int:
@@ -151,19 +173,31 @@ class Jubavisor:
         with self.lock:
             procs = self.children.pop(name, [])
         r = 0
-        for p, port, _ in procs:
+        for p, port, _, gpu in procs:
             if not _kill(p):
                 r -= 1
             else:
                 with self.lock:
                     self.pool.append(port)
+                    self._give_gpu(gpu)
         return r
+
+    def _take_gpu(self) -> int:
+        if not self.gpu_users:
+            return -1
+        g = min(range(len(self.gpu_users)), key=lambda i: self.gpu_users[i])
+        self.gpu_users[g] += 1
+        return g
+
+    def _give_gpu(self, g: int) -> None:
+        if 0 <= g < len(self.gpu_users) and self.gpu_users[g] > 0:
+            self.gpu_users[g] -= 1
 
     def stop_all(self) -> None:
         with self.lock:
             allp = [p for procs in self.children.values() for p in procs]
             self.children.clear()
-        for p, port, _ in allp:
+        for p, port, _, _ in allp:
             _kill(p)
 
     def close(self) -> None:
@@ -191,11 +225,13 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("-m", "--max-children", type=int, default=16)
     ap.add_argument("-l", "--logdir", default="")
     ap.add_argument("-t", "--timeout", type=int, default=10)
+    ap.add_argument("-G", "--gpus", type=int, default=-1,
+                    help="GPUs handed out one per child (--gpu i); default: the host's count")
     ap.add_argument("-b", "--listen_addr", default="",
                     help="address to register and to bind children to (default: primary IPv4)")
     a = ap.parse_args(argv)
     system.set_program_name("jubavisor")
-    v = Jubavisor(a.zookeeper, a.rpc_port, a.max_children, a.timeout, a.listen_addr)
+    v = Jubavisor(a.zookeeper, a.rpc_port, a.max_children, a.timeout, a.listen_addr, a.gpus)
     srv = RpcServer(2)
     srv.add("start", v.start, arity=3)
     srv.add("stop", v.stop, arity=2)

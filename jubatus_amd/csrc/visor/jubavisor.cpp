@@ -135,6 +135,7 @@ std::string default_server_dir() {
 }
 
 struct Args {
+  int gpus = -1;                 // GPUs handed out to children (-1: count the host's)
   int port = 9198;
   std::string zk = "localhost:2181";
   int max_children = 16;
@@ -148,12 +149,13 @@ struct Args {
 struct Child {
   pid_t pid;
   int port;
+  int gpu;                       // device index given with --gpu (-1: none)
   std::string server_name;
 };
 
 class Visor {
  public:
-  explicit Visor(const Args& a) : a_(a) {
+  explicit Visor(const Args& a) : a_(a), gpu_users_(a.gpus > 0 ? a.gpus : 0, 0) {
     for (int p = a.port + 1; p <= a.port + a.max_children; ++p) pool_.push_back(p);
     reaper_ = std::thread([this] { reap_loop(); });
   }
@@ -183,14 +185,17 @@ class Visor {
     for (int64_t i = 0; i < need; ++i) {
       const int port = pool_.front();
       pool_.pop_front();
-      const pid_t pid = spawn(server, name, port, f);
+      const int gpu = take_gpu();
+      const pid_t pid = spawn(server, name, port, gpu, f);
       if (pid <= 0) {
         pool_.push_back(port);
+        give_gpu(gpu);
         return -1;
       }
       log_line("INFO", "started " + server_name + " on port " + std::to_string(port) + " (pid " +
-                           std::to_string(pid) + ")");
-      procs.push_back(Child{pid, port, server_name});
+                           std::to_string(pid) + (gpu >= 0 ? ", gpu " + std::to_string(gpu) : "") +
+                           ")");
+      procs.push_back(Child{pid, port, gpu, server_name});
     }
     return 0;
   }
@@ -208,7 +213,10 @@ class Visor {
     }
     terminate(procs);
     std::lock_guard<std::mutex> g(mu_);
-    for (const auto& c : procs) pool_.push_back(c.port);
+    for (const auto& c : procs) {
+      pool_.push_back(c.port);
+      give_gpu(c.gpu);
+    }
     return 0;
   }
 
@@ -235,10 +243,26 @@ class Visor {
            server->find_first_of("./") == std::string::npos;
   }
 
-  pid_t spawn(const std::string& server, const std::string& name, int port,
+  // One server process per GPU: each child gets the least
+  // used device of this host (devices are reused round-robin once every one
+  // has a server). -1 when the host has no GPU (children run on the host).
+  int take_gpu() {
+    if (gpu_users_.empty()) return -1;
+    int best = 0;
+    for (int i = 1; i < (int)gpu_users_.size(); ++i)
+      if (gpu_users_[i] < gpu_users_[best]) best = i;
+    ++gpu_users_[best];
+    return best;
+  }
+  void give_gpu(int gpu) {
+    if (gpu >= 0 && gpu < (int)gpu_users_.size() && gpu_users_[gpu] > 0) --gpu_users_[gpu];
+  }
+
+  pid_t spawn(const std::string& server, const std::string& name, int port, int gpu,
               const std::map<std::string, std::string>& f) {
     const std::string prog = a_.server_dir + "/" + server;
     std::vector<std::string> args{prog, "-z", a_.zk, "-n", name, "-p", std::to_string(port)};
+    if (gpu >= 0) { args.push_back("--gpu"); args.push_back(std::to_string(gpu)); }
     if (!a_.listen_addr.empty()) { args.push_back("-b"); args.push_back(a_.listen_addr); }
     static const char* const opts[][2] = {
         {"-B", "bind_if"},      {"-c", "threadnum"}, {"-t", "timeout"},
@@ -323,6 +347,7 @@ class Visor {
             log_line("INFO", v[i].server_name + " with port " + std::to_string(v[i].port) +
                                  " exited pid: " + std::to_string(v[i].pid));
             pool_.push_back(v[i].port);
+            give_gpu(v[i].gpu);
             v.erase(v.begin() + i);
           } else {
             ++i;
@@ -336,6 +361,7 @@ class Visor {
   std::mutex mu_;
   std::map<std::string, std::vector<Child>> children_;
   std::deque<int> pool_;
+  std::vector<int> gpu_users_;   // children per device
   std::atomic<bool> stop_{false};
   std::thread reaper_;
 };
@@ -389,6 +415,8 @@ void usage() {
           "  -l, --logdir DIR          directory for the children's output\n"
           "  -t, --timeout SEC         coordinator session timeout (10)\n"
           "  -b, --listen_addr ADDR    address to bind, register and give the children\n"
+          "  -G, --gpus N              GPUs to hand out, one per child (--gpu i); default:\n"
+          "                            the host's GPU count (0: children get no --gpu)\n"
           "  -v, --version\n");
 }
 
@@ -412,6 +440,7 @@ int parse_args(int argc, char** argv, Args* a) {
     else if (s == "-l" || s == "--logdir") a->logdir = val();
     else if (s == "-t" || s == "--timeout") a->timeout = num(1);
     else if (s == "-b" || s == "--listen_addr") a->listen_addr = val();
+    else if (s == "-G" || s == "--gpus") a->gpus = num(0);
     else if (s == "-v" || s == "--version") { printf("jubatus-%s (mi355x, native jubavisor)\n", kVersion); return -1; }
     else if (s == "-h" || s == "--help") { usage(); return -1; }
     else { fprintf(stderr, "unknown option: %s\n", s.c_str()); usage(); return 1; }
@@ -421,6 +450,26 @@ int parse_args(int argc, char** argv, Args* a) {
     return 1;
   }
   return 0;
+}
+
+// GPUs of this host: KFD topology nodes with SIMDs (no HIP runtime needed)
+int count_gpus() {
+  int n = 0;
+  for (int i = 0; i < 256; ++i) {
+    const std::string path = "/sys/class/kfd/kfd/topology/nodes/" + std::to_string(i) + "/properties";
+    FILE* fp = fopen(path.c_str(), "r");
+    if (!fp) break;
+    char key[128];
+    long long v;
+    while (fscanf(fp, "%127s %lld", key, &v) == 2) {
+      if (strcmp(key, "simd_count") == 0) {
+        if (v > 0) ++n;
+        break;
+      }
+    }
+    fclose(fp);
+  }
+  return n;
 }
 
 std::string default_v4() {
@@ -452,6 +501,7 @@ int main(int argc, char** argv) {
   }
   if (rc) return rc < 0 ? 0 : rc;
   a.server_dir = default_server_dir();
+  if (a.gpus < 0) a.gpus = count_gpus();
   a.eth = a.listen_addr.empty() ? default_v4() : a.listen_addr;
 
   sigset_t ss;

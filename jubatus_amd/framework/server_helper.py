@@ -182,6 +182,12 @@ class ServerHelper:
             "last_loaded_path": s.last_loaded_path,
         }
         s.get_status(data)
+        # the device this server process owns (jubavisor hands out one GPU per
+        # child with --gpu; "cpu": host backend)
+        gpu = getattr(a, "gpu", None)
+        data["gpu"] = "" if gpu is None else str(gpu)
+        dev = getattr(s, "device", None)
+        data.setdefault("device", str(dev) if dev is not None else "cpu")
         if not a.is_standalone():
             data.update({
                 "zk": a.z, "name": a.name,

@@ -82,8 +82,9 @@ def test_jubavisor_wire_helpers():
     assert jubactl.split_counts(5, 2) == [3, 2] and jubactl.split_counts(0, 3) == [1, 1, 1]
 
 
-def _cluster_roundtrip(zk, ls, tmp_path):
-    """jubactl start 2 / status / save / load / stop against the registered supervisor(s)"""
+def _cluster_roundtrip(zk, ls, tmp_path, gpus=0):
+    """jubactl start 2 / status / save / load / stop against the registered supervisor(s);
+    gpus > 0: the supervisor hands out one device per child (--gpu), visible in get_status"""
     out = []
     assert jubaconfig.main(["-c", "write", "-f", os.path.join(ROOT, "config/classifier/arow.json"),
                             "-t", "classifier", "-n", "cl", "-z", zk], out=out.append) == 0
@@ -96,6 +97,18 @@ def _cluster_roundtrip(zk, ls, tmp_path):
     nodes = ls.list(nodes_path)
     assert len(nodes) == 2, nodes
     assert jubactl.main(["-c", "status", *common]) == 0
+    if gpus:
+        seen = []
+        for n in nodes:
+            host, port = n.rsplit("_", 1)
+            with RpcClient(host, int(port), 10.0) as c:
+                st = c.call("get_status", "cl")
+            st = {k.decode() if isinstance(k, bytes) else k: v for k, v in st.items()}
+            v = list(st.values())[0]
+            v = {(k.decode() if isinstance(k, bytes) else k): (x.decode() if isinstance(x, bytes) else x)
+                 for k, x in v.items()}
+            seen.append(v["gpu"])
+        assert sorted(seen) == ["0", "1"], seen
     assert jubactl.main(["-c", "save", "-i", "m1", *common]) == 0
     saved = [f for f in os.listdir(tmp_path) if f.endswith("m1.jubatus")]
     assert len(saved) == 2, os.listdir(tmp_path)
@@ -114,7 +127,7 @@ def test_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
     vport = free_port()
-    visor = Jubavisor(zk, vport, max_children=4, listen_addr="127.0.0.1")
+    visor = Jubavisor(zk, vport, max_children=4, listen_addr="127.0.0.1", gpus=2)
     rpc = RpcServer(2)
     rpc.add("start", visor.start, arity=3)
     rpc.add("stop", visor.stop, arity=2)
@@ -122,19 +135,20 @@ def test_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     rpc.start()
     ls = CoordinatorClient(zk, timeout=5.0)
     try:
-        _cluster_roundtrip(zk, ls, tmp_path)
+        _cluster_roundtrip(zk, ls, tmp_path, gpus=2)
     finally:
         rpc.stop()
         visor.close()
         ls.close()
 
 
-def _native_visor(zk, vport, tmp_path, maxc=4):
+def _native_visor(zk, vport, tmp_path, maxc=4, gpus=None):
     exe = os.path.join(NATIVE_BIN_DIR, "jubavisor")
     if not os.access(exe, os.X_OK):
         pytest.skip("native jubavisor not built (python -m jubatus_amd.build_ext)")
     err = open(tmp_path / "visor.err", "w")
-    p = subprocess.Popen([exe, "-p", str(vport), "-z", zk, "-m", str(maxc), "-b", "127.0.0.1"],
+    extra = ["-G", str(gpus)] if gpus is not None else []
+    p = subprocess.Popen([exe, "-p", str(vport), "-z", zk, "-m", str(maxc), "-b", "127.0.0.1", *extra],
                          stdout=subprocess.PIPE, stderr=err, text=True)
     line = p.stdout.readline()
     assert line.startswith("jubavisor ready"), (line, (tmp_path / "visor.err").read_text())
@@ -145,11 +159,11 @@ def test_native_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
     vport = free_port()
-    proc, err = _native_visor(zk, vport, tmp_path)
+    proc, err = _native_visor(zk, vport, tmp_path, gpus=2)
     ls = CoordinatorClient(zk, timeout=5.0)
     try:
         assert ls.list(mb.JUBAVISOR_BASE_PATH) == [f"127.0.0.1_{vport}"]
-        _cluster_roundtrip(zk, ls, tmp_path)
+        _cluster_roundtrip(zk, ls, tmp_path, gpus=2)
     finally:
         proc.terminate()
         rc = proc.wait(30)
