@@ -118,6 +118,10 @@ class LinearClassifier:
             self._train_stats = torch.zeros(2, dtype=torch.int64, device=device)
             # rows written since the last MIX (sparse MIX, parallel/sparse_mix.py)
             self.touched = torch.zeros(self.H, dtype=torch.uint8, device=device)
+        # False after a change the touched map does not describe (model load,
+        # label re-layout): the next MIX is dense
+        self._touched_valid = True
+        self._last_mix: dict = {}
         self._alloc(LABEL_CAPS[0])
 
     # ------------------------------------------------------------ storage
@@ -521,6 +525,7 @@ class LinearClassifier:
                 self.W, self.P = W, P
             if obj.get("weights"):
                 self.conv.weights.unpack(obj["weights"])
+            self._touched_valid = False
 
     # ----------------------------------------------------------------- MIX
     def _live_labels(self) -> list[str]:
@@ -556,14 +561,17 @@ class LinearClassifier:
             self.labels.get_or_add(n)
             self.labels.set_count(c, counts.get(n, 0))
         self.W, self.P, self.LC = W, P, LC
+        self._touched_valid = False
         self.active = (self.torch.zeros(LC, dtype=self.torch.int32, device=self.device)
                        if self.gpu else np.zeros(LC, dtype=np.int32))
         self._label_version = -1
         self._sync_labels()
 
     def mix(self, group=None) -> int:
-        """Collective model averaging across the ranks of ``group`` (RCCL).
-        Returns the number of bytes all-reduced per rank."""
+        """Collective model averaging across the ranks of ``group`` (RCCL):
+        label layout agreement, then a sparse (touched rows) or chunked
+        dense all-reduce mean (parallel/table_mix.py). Returns the bytes
+        all-reduced per rank."""
         from ..parallel import collective as coll
         with self._lock:
             self._drain()
@@ -580,24 +588,34 @@ class LinearClassifier:
                             seen.add(n)
                             order.append(n)
                 self._reorder_labels(order)
-            tables = self._tables()
-            coll.allreduce_mean_(tables, group)
+            job = self._table_mix(group)
+            nbytes = job.end()
+            self._last_mix = job.stats()
             self._mix_counts(group)
-            return sum(t.numel() * t.element_size() for t in tables)
+            return nbytes
+
+    def _table_mix(self, group):
+        from ..parallel.table_mix import TableMix
+        touched = self.touched if (self.gpu and self._touched_valid) else None
+        job = TableMix(self._tables(), touched, group).begin()
+        if self.gpu:
+            self._touched_valid = True        # the map is exact again from here on
+        return job
 
     # ------------------------------------------------ overlapped MIX
     def mix_begin(self, group=None, meta_group=None, agreed_version: int | None = None) -> dict:
-        """Start an overlapped MIX: snapshot W / P, launch the cluster SUM
-        all-reduce of the snapshot on the communicator stream and return;
-        training continues meanwhile. ``mix_end`` folds the cluster mean in
-        with W += mean(snapshot) - own snapshot, so updates made during the
-        collective are kept. Label agreement and count deltas ride on
-        ``meta_group`` (a host/gloo group: no GPU synchronisation). If the
-        label layouts disagree the synchronous ``mix`` runs instead (it
-        re-lays the label columns first). ``agreed_version``: the caller knows
-        every rank still has the label layout agreed at this label-table
-        version; if the table is still at it, the host collective that
-        compares the layouts is skipped."""
+        """Start an overlapped MIX: snapshot the touched rows (or the first
+        chunks of a dense MIX) and start their SUM all-reduce on the
+        communicator stream, then return; training continues meanwhile.
+        ``mix_ready`` advances it, ``mix_end`` folds the cluster mean in with
+        T += mean(snapshot) - snapshot, so updates made during the collective
+        are kept. Label agreement and count deltas ride on ``meta_group`` (a
+        host/gloo group: no GPU synchronisation). If the label layouts
+        disagree the synchronous ``mix`` runs instead (it re-lays the label
+        columns first). ``agreed_version``: the caller knows every rank still
+        has the label layout agreed at this label-table version; if the
+        table is still at it, the host collective comparing layouts is
+        skipped."""
         import torch
         from ..parallel import collective as coll
         with self._lock:
@@ -618,54 +636,36 @@ class LinearClassifier:
                 return {"sync": self.mix(group)}
             meta_cnt = torch.from_numpy(cur - b).to(mdev)
             works = [dist_all_reduce(meta_cnt, "sum", mg)]
-            tables = self._tables()
-            snap = getattr(self, "_mix_bufs", None)
-            if snap is None or any(a.shape != t.shape for a, t in zip(snap[0], tables)):
-                snap = ([torch.empty_like(t) for t in tables], [torch.empty_like(t) for t in tables])
-                self._mix_bufs = snap
-            loc, red = snap
-            for l, r, t in zip(loc, red, tables):
-                l.copy_(t)
-                r.copy_(t)
-            twork = coll.allreduce_sum_async(red, group)
+            job = self._table_mix(group)
             return {"group": group, "names": names, "cur": cur, "base": b,
-                    "meta": works, "meta_cnt": meta_cnt, "twork": twork,
-                    "nbytes": sum(t.numel() * t.element_size() for t in tables)}
+                    "meta": works, "meta_cnt": meta_cnt, "job": job}
 
     @staticmethod
     def mix_ready(h: dict | None) -> bool:
-        """True when an overlapped MIX's collectives have finished (non-blocking)"""
+        """True when an overlapped MIX's collectives have finished
+        (non-blocking; advances a chunked dense MIX)"""
         if h is None or "sync" in h:
             return True
-        return all(w is None or w.is_completed() for w in list(h["meta"]) + list(h["twork"]))
+        return h["job"].ready() and all(w is None or w.is_completed() for w in h["meta"])
 
     def mix_end(self, h: dict) -> int:
         """Finish a ``mix_begin``; returns the bytes all-reduced per rank."""
-        from ..parallel import collective as coll
         if "sync" in h:
             return h["sync"]
         for w in h["meta"]:
             if w is not None:
                 w.wait()
-        for w in h["twork"]:
-            w.wait()
-        n = coll.world() if coll.is_dist() else 1
         with self._lock:
             self._drain(block=False)   # batches still in flight join the next MIX
-            loc, red = self._mix_bufs
-            for t, r, l in zip(self._tables(), red, loc):
-                if self.gpu:
-                    from ..ops import hip
-                    hip.mix_apply_(t, r, l, 1.0 / n)
-                else:
-                    t.add_(r, alpha=1.0 / n).sub_(l)
+            nbytes = h["job"].end()
+            self._last_mix = h["job"].stats()
             names, cur, b = h["names"], h["cur"], h["base"]
             new_base = b + h["meta_cnt"].cpu().numpy()
             for i, nm in enumerate(names):
                 since = int(self.labels.count(i)) - int(cur[i])
                 self.labels.set_count(i, int(max(0, new_base[i] + since)))
             self._count_base = {nm: int(max(0, new_base[i])) for i, nm in enumerate(names)}
-            return h["nbytes"]
+            return nbytes
 
     def _tables(self) -> list:
         """the mixable tensors (torch views of the host arrays on the CPU backend)"""
@@ -696,8 +696,11 @@ class LinearClassifier:
             self.labels.set_count(i, int(max(0, new[i])))
         self._count_base = {n: int(max(0, new[i])) for i, n in enumerate(names)}
 
-    def broadcast_from(self, src: int) -> None:
-        """hand the whole model to a newly joined member (obsolete protocol)"""
+    def broadcast_from(self, src: int, apply: bool = True) -> None:
+        """hand the whole model to newly joined members (obsolete protocol);
+        apply=False: an up-to-date member takes part in the collectives
+        without replacing its model"""
+        import torch
         import torch.distributed as dist
         with self._lock:
             self._drain()
@@ -706,7 +709,8 @@ class LinearClassifier:
                      self.labels.alive()]]
             dist.broadcast_object_list(meta, src=src)
             names, counts, alive = meta[0]
-            if dist.get_rank() != src:
+            me = dist.get_rank()
+            if me != src and apply:
                 self.labels.clear()
                 self.LC = 0
                 self._alloc(_label_cap(max(1, len(names))))
@@ -717,9 +721,17 @@ class LinearClassifier:
                     if not a:
                         self.labels.remove(n)
                 self._sync_labels()
+            if me != src and not apply:
+                LC = _label_cap(max(1, len(names)))
+                shapes = [(self.H, LC)] * (2 if self.use_s else 1)
+                dev = self.device if self.gpu else "cpu"
+                for shp in shapes:
+                    dist.broadcast(torch.empty(shp, dtype=torch.float32, device=dev), src=src)
+                return
             for t in self._tables():
                 dist.broadcast(t, src=src)
             self._count_base = {n: int(c) for n, c in zip(names, counts)}
+            self._touched_valid = False
 
     def pair_mix(self, peer: int) -> None:
         """push_mixer exchange with one peer: agree on the label layout, then
@@ -761,6 +773,8 @@ class LinearClassifier:
         if self.gpu:
             for k, v in self._scan_stats.items():
                 st[f"train_scan.{k}"] = str(v)
+        for k, v in self._last_mix.items():
+            st[f"mix.last_{k}"] = str(v)
         return st
 
 

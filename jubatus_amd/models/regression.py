@@ -194,11 +194,17 @@ class PARegression:
             coll.allreduce_mean_(ts)
             return sum(t.numel() * t.element_size() for t in ts)
 
-    def broadcast_from(self, src: int) -> None:
+    def broadcast_from(self, src: int, apply: bool = True) -> None:
+        """model hand-over from rank ``src``; apply=False: take part in the
+        collective without replacing the local model (an up-to-date member)"""
+        import torch
         import torch.distributed as dist
         with self._lock:
             for t in self._tables():
-                dist.broadcast(t, src=src)
+                if apply or dist.get_rank() == src:
+                    dist.broadcast(t, src=src)
+                else:
+                    dist.broadcast(torch.empty_like(t), src=src)
 
     def pair_mix(self, peer: int) -> None:
         import torch

@@ -21,13 +21,32 @@ rank set, so membership changes become *group epochs*:
 
 One group per server process (= per GPU). The group carries the mixer's
 trigger agreement (a 2-int all-reduce) and the MIX collectives.
+
+Watchdog (reference: server-to-server calls are bounded by
+``--interconnect_timeout``, server_util.cpp:190-194, and a MIX skips peers
+that failed, linear_mixer.cpp:455-489): once formed, the group's operation
+timeout is the interconnect timeout, every collective the mixer waits for
+is polled against that deadline, and a collective that misses it aborts the
+communicator (``abort``: RCCL comm abort, then teardown) and marks the epoch
+failed, so the survivors re-form a group without the stuck member instead of
+hanging. RCCL's own watchdog runs in "clean up the communicator only" mode
+(TORCH_NCCL_ASYNC_ERROR_HANDLING=2): a timed-out collective raises in the
+waiting thread and the server process stays up.
 """
 from __future__ import annotations
 
 import json
+import os
 import socket
 import time
 from datetime import timedelta
+
+# a timed-out RCCL collective must not take the server process down
+os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
+
+
+class CollectiveTimeout(RuntimeError):
+    pass
 
 from ..common import membership as mb
 from ..utils import logger
@@ -46,12 +65,14 @@ def _free_port(host: str) -> int:
 
 class ProcessGroupManager:
     def __init__(self, coord, type_: str, name: str, ident: str, eth: str, backend: str,
-                 device=None, timeout: float = 30.0):
+                 device=None, timeout: float = 30.0, op_timeout: float | None = None):
         self.coord, self.type, self.name = coord, type_, name
         self.ident, self.eth = ident, eth
         self.backend = backend
         self.device = device
-        self.timeout = timeout
+        self.timeout = timeout                    # rendezvous
+        self.op_timeout = op_timeout or timeout   # every collective (interconnect_timeout)
+        self.aborts = 0
         self.epoch = -1
         self.members: list[str] = []
         self.rank = -1
@@ -121,9 +142,40 @@ class ProcessGroupManager:
                     pass
                 time.sleep(0.2)
                 return False
+            try:
+                from torch.distributed import distributed_c10d as c10d
+                c10d._set_pg_timeout(timedelta(seconds=self.op_timeout), None)
+            except Exception:  # noqa: BLE001 - older torch: the rendezvous timeout stays
+                pass
         self.epoch, self.members, self.rank, self.world = cur["epoch"], cur["members"], rank, world
         log.info("joined mix group epoch %d as rank %d/%d", self.epoch, rank, world)
         return True
+
+    # ---------------------------------------------------------- watchdog
+    def wait(self, done, what: str = "collective", timeout: float | None = None) -> None:
+        """poll ``done()`` (a work's is_completed, a job's ready) until it is
+        true; past the interconnect timeout abort the group and raise"""
+        deadline = time.time() + (timeout if timeout is not None else self.op_timeout)
+        spin = 0
+        while not done():
+            if time.time() > deadline:
+                self.abort(f"{what} exceeded the interconnect timeout ({self.op_timeout:g} s)")
+                raise CollectiveTimeout(what)
+            spin += 1
+            time.sleep(0 if spin < 100 else 0.001)
+
+    def abort(self, why: str) -> None:
+        """abort the communicator of a stuck collective and leave the epoch"""
+        self.aborts += 1
+        log.warning("aborting mix group epoch %d: %s", self.epoch, why)
+        try:
+            import torch.distributed as dist
+            from torch.distributed import distributed_c10d as c10d
+            if dist.is_initialized() and hasattr(c10d, "_abort_process_group"):
+                c10d._abort_process_group()
+        except Exception as e:  # noqa: BLE001
+            log.warning("communicator abort failed: %s", e)
+        self.close()
 
     def _destroy(self) -> None:
         import torch.distributed as dist
@@ -155,5 +207,7 @@ class ProcessGroupManager:
         import torch
         import torch.distributed as dist
         t = torch.tensor(vals, dtype=torch.int64, device=self.tensor_device())
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        w = dist.all_reduce(t, op=dist.ReduceOp.MAX, async_op=True)
+        self.wait(w.is_completed, "trigger all-reduce")
+        w.wait()
         return [int(x) for x in t.cpu().tolist()]

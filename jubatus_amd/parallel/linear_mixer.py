@@ -83,7 +83,8 @@ class CollectiveMixer(Mixer):
         backend = self.backend or ("nccl" if dev is not None else "gloo")
         self.group = ProcessGroupManager(self.coord, self.type, self.argv.name, self.ident,
                                          self.argv.eth, backend, dev,
-                                         timeout=max(5.0, 3.0 * self.argv.interconnect_timeout))
+                                         timeout=max(5.0, 3.0 * self.argv.interconnect_timeout),
+                                         op_timeout=max(1.0, float(self.argv.interconnect_timeout)))
         self.running = True
         self._thread = threading.Thread(target=self._loop, name=self.kind, daemon=True)
         self._thread.start()
@@ -123,7 +124,9 @@ class CollectiveMixer(Mixer):
         status[f"{k}.mix_count"] = str(self.mix_count)
         status[f"{k}.last_mix_bytes"] = str(self.last_mix["bytes"])
         status[f"{k}.last_mix_sec"] = f"{self.last_mix['seconds']:.6f}"
+        status[f"{k}.overlapped"] = str(self.last_mix.get("overlap", 0))
         if self.group is not None:
+            status[f"{k}.watchdog_aborts"] = str(self.group.aborts)
             status[f"{k}.group_epoch"] = str(self.group.epoch)
             status[f"{k}.group_rank"] = str(self.group.rank)
             status[f"{k}.group_size"] = str(self.group.world)
@@ -149,10 +152,10 @@ class CollectiveMixer(Mixer):
                 break
             try:
                 self._tick()
-            except Exception as e:  # noqa: BLE001 - a member died mid-collective
+            except Exception as e:  # noqa: BLE001 - a member died or stalled mid-collective
                 log.warning("mix tick failed (%s); re-forming the group", e)
-                if self.group is not None:
-                    self.group.close()
+                if self.group is not None and self.group.epoch >= 0:
+                    self.group.abort(f"collective failed: {e}")
                 time.sleep(TICK)
 
     def _tick(self) -> None:
@@ -182,8 +185,7 @@ class CollectiveMixer(Mixer):
             mb.shutdown_server()
             return
         if flags[0] or flags[1]:
-            with self.rw.write():
-                st = self.mix_once()
+            st = self.mix_once()
             with self._lock:
                 self._mixed(st)
             log.info("mixed with %d servers in %.6f secs, %d bytes", g.world, st["seconds"],
@@ -198,23 +200,44 @@ class CollectiveMixer(Mixer):
         self._lock.notify_all()
 
     def _hand_over(self) -> None:
-        """New group: broadcast the model from the lowest-rank up-to-date member."""
+        """New group: if a member is obsolete (newly joined), it receives the
+        model of the lowest-rank up-to-date member (linear_mixer.cpp:394-410,
+        582-611); up-to-date members keep theirs - a group re-formed after a
+        failure does not overwrite anyone's training."""
         g = self.group
         big = 1 << 30
-        r = g.allreduce_max_ints([-(big if self.is_obsolete else g.rank)])
-        src = -r[0]
-        if src < big:
+        r = g.allreduce_max_ints([-(big if self.is_obsolete else g.rank),
+                                  1 if self.is_obsolete else 0])
+        src, any_obsolete = -r[0], r[1]
+        if any_obsolete and src < big:
             with self.rw.write():
-                broadcast_model(self.driver, src)
+                broadcast_model(self.driver, src, apply=self.is_obsolete)
             if self.is_obsolete:
                 log.info("model fetched from rank %d", src)
         self.is_obsolete = False
         self._register_active()
 
     def mix_once(self) -> dict:
+        """One MIX. Drivers with an overlapped MIX (mix_begin / mix_ready /
+        mix_end: the linear classifier's sparse all-reduce) hold the model
+        write lock only to snapshot and to fold; the collective itself runs
+        while train/classify continue, polled by the group watchdog. Other
+        drivers mix synchronously under the write lock (the reference holds
+        it for put_diff, linear_mixer.cpp:613-662)."""
         fault.on_mix("allreduce")
+        d = self.driver
         with trace.span("mix.linear"):
-            return linear_mix(self.driver)
+            if hasattr(d, "mix_begin"):
+                t0 = time.perf_counter()
+                with self.rw.write():
+                    h = d.mix_begin()
+                self.group.wait(lambda: d.mix_ready(h), "MIX all-reduce")
+                with self.rw.write():
+                    nbytes = d.mix_end(h)
+                return {"bytes": int(nbytes or 0), "seconds": time.perf_counter() - t0,
+                        "overlap": 1}
+            with self.rw.write():
+                return linear_mix(d)
 
 
 class LinearMixer(CollectiveMixer):

@@ -58,14 +58,16 @@ def linear_mix(driver: Any) -> dict:
     return {"bytes": nbytes, "seconds": time.perf_counter() - t0}
 
 
-def broadcast_model(driver: Any, src: int) -> None:
+def broadcast_model(driver: Any, src: int, apply: bool = True) -> None:
+    """rank ``src`` hands its model to the group; members with apply=False
+    (up to date) take part in the collective but keep their own model"""
     dist = _dist()
     if hasattr(driver, "broadcast_from"):
-        driver.broadcast_from(src)
+        driver.broadcast_from(src, apply=apply)
         return
     box = [driver.pack() if dist.get_rank() == src else None]
     dist.broadcast_object_list(box, src=src)
-    if dist.get_rank() != src:
+    if dist.get_rank() != src and apply:
         driver.unpack(box[0])
 
 

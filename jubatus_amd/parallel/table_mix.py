@@ -1,0 +1,193 @@
+"""Sparse, memory-bounded MIX of HBM-resident row tables (linear models).
+
+Reference: ``linear_mixer`` ships only what changed since the last MIX -
+``get_diff`` packs the diff accumulated by the local_mixture storage
+(jubatus/server/framework/mixer/linear_mixer.cpp:547-564), the master folds
+the diffs and ``put_diff`` applies the result (:613-662). Here a MIX is a
+collective over the process group (RCCL over xGMI on GPUs, gloo on hosts):
+
+* the train kernel marks every row it writes in ``touched`` (uint8[H],
+  csrc/hip/linear.hip);
+* ``begin`` all-gathers the touched row lists, forms their union (the same
+  on every rank), snapshots those rows of every table into one contiguous
+  buffer and starts an asynchronous SUM all-reduce of it;
+* ``end`` folds the cluster mean in: ``T[rows] += mean(snapshot) - snapshot``,
+  so updates made while the collective ran are kept (and marked touched
+  again for the next MIX).
+
+Rows nobody touched since the last MIX are equal on every rank (the last MIX
+made them so), so leaving them out is exact. The bytes moved scale with the
+touched rows, and the extra memory is 2 x the union's rows.
+
+When the union exceeds ``dense_frac`` of the table (or no touched map
+exists: host backend, after a model load or a label re-layout), the MIX is
+dense but chunked: at most two chunks of ``chunk_bytes`` are snapshotted and
+in flight at a time (``poll`` advances them between train batches), so the
+extra memory stays <= 4 chunks (<= 1/4 of the tables for tables of 4 GiB
+and more) instead of two full copies.
+"""
+from __future__ import annotations
+
+import os
+from typing import Sequence
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_CHUNK_BYTES = int(os.environ.get("JUBATUS_MIX_CHUNK_BYTES", 256 << 20))
+DEFAULT_DENSE_FRAC = float(os.environ.get("JUBATUS_MIX_DENSE_FRAC", "0.5"))
+
+
+def _world(group) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+class TableMix:
+    """One MIX of ``tables`` (each [H, C], same H, same device)."""
+
+    def __init__(self, tables: Sequence[torch.Tensor], touched: torch.Tensor | None, group=None,
+                 dense_frac: float = DEFAULT_DENSE_FRAC, chunk_bytes: int = DEFAULT_CHUNK_BYTES):
+        if not tables:
+            raise ValueError("nothing to mix")
+        self.tables = list(tables)
+        self.H = self.tables[0].shape[0]
+        if any(t.shape[0] != self.H or not t.is_contiguous() for t in self.tables):
+            raise ValueError("mix tables must be contiguous with the same row count")
+        self.touched = touched
+        self.group = group
+        self.n = _world(group)
+        self.dense_frac = dense_frac
+        self.row_bytes = sum(t[0].numel() * t.element_size() for t in self.tables)
+        total = self.H * self.row_bytes
+        # chunk: at most chunk_bytes, at most 1/16 of the tables (>= 4 MiB)
+        cb = min(chunk_bytes, max(4 << 20, total // 16))
+        self.chunk_rows = max(1, cb // max(1, self.row_bytes))
+        self.mode = "none"
+        self.rows = 0              # rows mixed (union size or H)
+        self.nbytes = 0            # bytes all-reduced per rank
+        self._sparse = None        # (rows idx, snap, red, work)
+        self._next_row = 0         # dense: first row not launched yet
+        self._inflight: list = []  # dense: (r0, r1, snap, red, work)
+        self._done = False
+
+    # ----------------------------------------------------------- begin
+    def begin(self) -> "TableMix":
+        if self.n <= 1:
+            if self.touched is not None:
+                self.touched.zero_()
+            self.mode, self._done = "single", True
+            return self
+        rows = self._union()
+        if rows is None:
+            self.mode = "dense"
+            self.rows = self.H
+            self._pump()
+        else:
+            self.mode = "sparse"
+            self.rows = int(rows.numel())
+            if self.rows == 0:
+                self._done = True
+                return self
+            snap = torch.cat([t.index_select(0, rows).reshape(self.rows, -1) for t in self.tables],
+                             dim=1)
+            red = snap.clone()
+            self.nbytes = red.numel() * red.element_size()
+            work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._sparse = (rows, snap, red, work)
+        return self
+
+    def _union(self) -> torch.Tensor | None:
+        """union of the ranks' touched rows (sorted, int64, same on every
+        rank), or None for a dense MIX; clears the touched map"""
+        t = self.touched
+        dev = t.device if t is not None else self.tables[0].device
+        if t is not None:
+            local = torch.nonzero(t).flatten()
+            t.zero_()
+            cnt = torch.tensor([local.numel()], dtype=torch.int64, device=dev)
+        else:
+            local = None
+            cnt = torch.tensor([self.H + 1], dtype=torch.int64, device=dev)   # "dense"
+        counts = [torch.empty_like(cnt) for _ in range(self.n)]
+        dist.all_gather(counts, cnt, group=self.group)       # (gloo has no _into_tensor form)
+        mx = int(torch.cat(counts).max().item())
+        if mx > self.H or mx > self.dense_frac * self.H:
+            return None
+        if mx == 0:
+            return torch.zeros(0, dtype=torch.int64, device=dev)
+        pad = torch.full((mx,), -1, dtype=torch.int64, device=dev)
+        pad[:local.numel()] = local
+        every = [torch.empty_like(pad) for _ in range(self.n)]
+        dist.all_gather(every, pad, group=self.group)
+        every = torch.cat(every)
+        every = every[every >= 0]
+        mark = torch.zeros(self.H, dtype=torch.uint8, device=dev)
+        mark[every] = 1
+        rows = torch.nonzero(mark).flatten()
+        if rows.numel() > self.dense_frac * self.H:
+            return None
+        return rows
+
+    # ------------------------------------------------------------ dense
+    def _launch(self, r0: int, r1: int) -> None:
+        snap = torch.cat([t[r0:r1].reshape(r1 - r0, -1) for t in self.tables], dim=1)
+        red = snap.clone()
+        self.nbytes += red.numel() * red.element_size()
+        work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._inflight.append((r0, r1, snap, red, work))
+
+    def _fold(self, r0: int, r1: int, snap: torch.Tensor, red: torch.Tensor) -> None:
+        upd = red.mul_(1.0 / self.n).sub_(snap)
+        c0 = 0
+        for t in self.tables:
+            w = t[0].numel()
+            t[r0:r1].view(r1 - r0, -1).add_(upd[:, c0:c0 + w])
+            c0 += w
+
+    def _pump(self, block: bool = False) -> None:
+        """fold finished chunks (in order), keep two chunks in flight"""
+        while self._inflight:
+            r0, r1, snap, red, work = self._inflight[0]
+            if not block and not work.is_completed():
+                break
+            work.wait()
+            self._fold(r0, r1, snap, red)
+            self._inflight.pop(0)
+        while len(self._inflight) < 2 and self._next_row < self.H:
+            r0 = self._next_row
+            r1 = min(self.H, r0 + self.chunk_rows)
+            self._next_row = r1
+            self._launch(r0, r1)
+        if not self._inflight and self._next_row >= self.H:
+            self._done = True
+
+    # ------------------------------------------------------------ poll
+    def ready(self) -> bool:
+        """advance without blocking; True when ``end`` will not wait"""
+        if self._done:
+            return True
+        if self.mode == "dense":
+            self._pump()
+            return self._done
+        return self._sparse[3].is_completed()
+
+    def end(self) -> int:
+        """finish the MIX (blocking); returns the bytes all-reduced per rank"""
+        if self.mode == "dense":
+            while not self._done:
+                self._pump(block=True)
+        elif self._sparse is not None:
+            rows, snap, red, work = self._sparse
+            work.wait()
+            upd = red.mul_(1.0 / self.n).sub_(snap)
+            c0 = 0
+            for t in self.tables:
+                w = t[0].numel()
+                t.view(self.H, -1).index_add_(0, rows, upd[:, c0:c0 + w])
+                c0 += w
+            self._sparse = None
+        self._done = True
+        return self.nbytes
+
+    def stats(self) -> dict:
+        return {"mode": self.mode, "rows": self.rows, "bytes": self.nbytes}

@@ -8,6 +8,8 @@ a test-only non-responding socket; the new framework adds a hook).
   rpc_error:method=*,after=3             fail the 4th and later calls
   mix_kill:phase=allreduce,at=2          exit the process at the 2nd MIX
                                          reaching that phase (rank failure)
+  mix_hang:phase=allreduce,at=1,ms=8000  stall that MIX phase (a rank that
+                                         stops answering collectives)
 
 ``method`` / ``phase`` accept ``*``; ``every=N`` fires on every N-th match,
 ``after=N`` on matches beyond the first N, ``at=N`` on exactly the N-th.
@@ -58,7 +60,7 @@ def parse(spec: str) -> list[_Rule]:
         for kv in filter(None, rest.split(",")):
             k, _, v = kv.partition("=")
             params[k.strip()] = v.strip()
-        if kind not in ("rpc_delay", "rpc_drop", "rpc_error", "mix_kill"):
+        if kind not in ("rpc_delay", "rpc_drop", "rpc_error", "mix_kill", "mix_hang"):
             raise ValueError(f"unknown fault kind: {kind}")
         rules.append(_Rule(kind, params))
     return rules
@@ -106,7 +108,11 @@ def on_mix(phase: str) -> None:
     if not rs:
         return
     with _lock:
-        fired = [r for r in rs if r.kind == "mix_kill" and r.matches(phase=phase)]
-    if fired:
+        fired = [r for r in rs if r.kind in ("mix_kill", "mix_hang") and r.matches(phase=phase)]
+    for r in fired:
+        if r.kind == "mix_hang":
+            log.critical("fault injection: stalling MIX phase %s", phase)
+            time.sleep(float(r.p.get("ms", "5000")) / 1e3)
+    if any(r.kind == "mix_kill" for r in fired):
         log.critical("fault injection: killing this rank at MIX phase %s", phase)
         os._exit(17)

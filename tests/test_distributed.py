@@ -298,3 +298,61 @@ def test_rank_killed_mid_mix_survivor_recovers(coord):
                 except subprocess.TimeoutExpired:
                     p.kill()
         ls.close()
+
+
+def test_stalled_rank_watchdog_aborts_and_regroups(coord):
+    """one server stalls its first MIX past --interconnect_timeout (fault
+    mix_hang): the other one's watchdog aborts the group instead of hanging,
+    keeps serving, and the two re-form a group whose next MIX succeeds
+    (reference: interconnect_timeout bounds server-to-server calls,
+    server_util.cpp:190-194; failed peers are skipped, linear_mixer.cpp:455-489)."""
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    name = "stall"
+    zkconfig.config_tozk(ls, "classifier", name, open(os.path.join(ROOT, "config/classifier/pa.json")).read())
+    ports = [free_port(), free_port()]
+    good = spawn("classifier", coord.port, name, ports[0], extra=("-I", "2"))
+    slow = spawn("classifier", coord.port, name, ports[1], extra=("-I", "2"),
+                 env_extra={"JUBATUS_FAULT": "mix_hang:phase=allreduce,at=1,ms=7000"})
+    try:
+        for p in ports:
+            assert wait_server("127.0.0.1", p, 60)
+        assert wait_actives(ls, "classifier", name, 2)
+        a = Classifier("127.0.0.1", ports[0], name, timeout=90.0)
+        a.train([("pos", Datum({"w": "good"})), ("neg", Datum({"w": "bad"}))] * 3)
+        t0 = time.time()
+        try:
+            a.do_mix()                  # the slow rank stalls inside this MIX
+        except Exception:
+            pass
+        # the survivor is not stuck: it serves while the group is aborted
+        assert max(a.classify([Datum({"w": "good"})])[0], key=lambda e: e.score).label == "pos"
+        deadline = time.time() + 120
+        ok = False
+        while time.time() < deadline:
+            try:
+                if a.do_mix():
+                    st = list(a.get_status().values())[0]
+                    if st.get("linear_mixer.group_size") == "2":
+                        ok = True
+                        break
+            except Exception:
+                pass
+            time.sleep(0.5)
+        assert ok, "no MIX with both members after the stall"
+        st = list(a.get_status().values())[0]
+        assert int(st["linear_mixer.watchdog_aborts"]) >= 1
+        assert time.time() - t0 < 120
+        b = Classifier("127.0.0.1", ports[1], name, timeout=30.0)
+        top = max(b.classify([Datum({"w": "good"})])[0], key=lambda e: e.score)
+        assert top.label == "pos"       # the mixed model reached the stalled rank
+        a.close()
+        b.close()
+    finally:
+        for p in (good, slow):
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+        ls.close()
