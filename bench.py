@@ -412,7 +412,8 @@ def main() -> None:
                 "samples_per_request": args.per_request,
                 "hash_max_size": 1 << args.hash_bits,
                 "labels": args.labels,
-                "mix": (f"linear, RCCL all-reduce mean of W and P, {args.mix_mode}, "
+                "mix": (f"linear, RCCL all-reduce mean of the touched rows of W and P (sparse; "
+                        f"chunked dense past half the table), {args.mix_mode}, "
                         + (f"every {args.mix_every} batch(es)" if args.mix_every > 0 else
                            "back to back (a new MIX as soon as the previous one finished)")
                         + f"; {mixes[0]} MIXes in the timed steps") if world > 1 else "standalone",
@@ -425,6 +426,7 @@ def main() -> None:
             "timed_samples_per_rank": samples_per_step * args.steps,
             "timed_bytes_per_rank": int(fresh.nbytes),
             "update_fraction": round(updated / trained, 4) if trained else None,
+            "mix_last": getattr(clf, "_last_mix", {}),
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
             "classify_latency_us_p50": round(p50, 1),

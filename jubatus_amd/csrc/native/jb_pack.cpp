@@ -16,19 +16,25 @@ namespace jb {
 
 namespace {
 
+constexpr int kUnknownLabel = -3;
+
 // Per-thread label cache: open addressing on FNV-1a of the label bytes,
 // verified by a byte compare (labels are few and repeat on every sample).
+// add = false: a label the table does not know yet is reported as
+// kUnknownLabel instead of being added (the scan stays free of side effects
+// until every request of the batch has validated).
 class LabelCache {
  public:
-  explicit LabelCache(LabelTable* t) : table_(t), slots_(256) {}
+  LabelCache(LabelTable* t, bool add) : table_(t), add_(add), slots_(256) {}
   int get(const uint8_t* s, uint32_t n) {
     const uint64_t h = fnv_bytes(kFnvOffset, s, n);
     size_t mask = slots_.size() - 1;
     for (size_t i = h & mask;; i = (i + 1) & mask) {
       Slot& sl = slots_[i];
       if (sl.id < 0) {
-        int id = table_->get_or_add((const char*)s, n);
-        if (id < 0) return -1;
+        int id = add_ ? table_->get_or_add((const char*)s, n)
+                      : table_->lookup(std::string((const char*)s, n));
+        if (id < 0) return add_ ? -1 : kUnknownLabel;
         sl.h = h; sl.key.assign((const char*)s, n); sl.id = id;
         if (++used_ * 2 > slots_.size()) rehash();
         return id;
@@ -52,6 +58,7 @@ class LabelCache {
     }
   }
   LabelTable* table_;
+  bool add_;
   std::vector<Slot> slots_;
   size_t used_ = 0;
 };
@@ -65,10 +72,12 @@ bool body_count(const RequestView& r, uint32_t* n) {
 // Scan request k straight into the final output slots [s0, s0 + n): datum
 // offsets / lengths / labels, and row_ptr relative to the request (the
 // request's slot base is added afterwards). Returns the request's slot total
-// or -1 (malformed) / -2 (label table full).
+// or -1 (malformed) / -2 (label table full). *unknown is set when a label is
+// not in the table yet (lookup-only cache): its samples get label -1 and no
+// count.
 int64_t scan_into(const RequestView& r, int kind, int sps, int spn, LabelCache* cache,
                   const PackOut& out, uint64_t byte_base, int64_t s0, uint64_t* hist,
-                  size_t hist_cap) {
+                  size_t hist_cap, bool* unknown) {
   Cursor c{r.data, r.data + r.len};
   uint32_t n;
   if (!c.array(&n)) return -1;
@@ -79,9 +88,14 @@ int64_t scan_into(const RequestView& r, int kind, int sps, int spn, LabelCache* 
       uint32_t two; const uint8_t* ls; uint32_t ln;
       if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) return -1;
       const int id = cache->get(ls, ln);
-      if (id < 0) return -2;
-      if (out.labels) out.labels[s] = id;
-      if ((size_t)id < hist_cap) ++hist[id];
+      if (id == kUnknownLabel) {
+        *unknown = true;
+        if (out.labels) out.labels[s] = -1;
+      } else {
+        if (id < 0) return -2;
+        if (out.labels) out.labels[s] = id;
+        if ((size_t)id < hist_cap) ++hist[id];
+      }
     } else if (kind == 2) {  // scored_datum [score, datum]
       uint32_t two; double score;
       if (!c.array(&two) || two != 2 || !c.number(&score)) return -1;
@@ -156,18 +170,23 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, int kind, int sps
     *e = (c + 1) * (int64_t)R / nchunks;
   };
   std::vector<int64_t> req_slots(R, 0);
+  std::vector<uint8_t> unknown(R, 0);
   std::atomic<int64_t> bad{-1};
   std::atomic<int> bad_kind{0};
   constexpr size_t kHist = 4096;  // labels beyond this are counted one by one
+  const bool count = kind == 1 && table;
+  std::vector<std::vector<uint64_t>> hists((size_t)nchunks);
   pool.parallel_for(nchunks, [&](int64_t c) {
-    LabelCache cache(table);
-    std::vector<uint64_t> hist(kind == 1 && table ? kHist : 0, 0);
+    LabelCache cache(table, false);
+    std::vector<uint64_t>& hist = hists[(size_t)c];
+    hist.assign(count ? kHist : 0, 0);
     int64_t b, e;
     chunk(c, &b, &e);
     for (int64_t k = b; k < e; ++k) {
       if (copy) memcpy(out.staging + byte_base[k], reqs[k].data, reqs[k].len);
+      bool unk = false;
       const int64_t sl = scan_into(reqs[k], kind, sps, spn, &cache, out, byte_base[k],
-                                   sample_base[k], hist.data(), hist.size());
+                                   sample_base[k], hist.data(), hist.size(), &unk);
       if (sl < 0) {
         int64_t expect = -1;
         bad.compare_exchange_strong(expect, k);
@@ -175,21 +194,43 @@ PackResult pack_requests(const std::vector<RequestView>& reqs, int kind, int sps
         return;
       }
       req_slots[k] = sl;
-      if (kind == 1 && table && hist.empty() == false) {
-        // labels past the histogram range
-        const int64_t s0 = sample_base[k], s1 = sample_base[k + 1];
-        if (out.labels)
-          for (int64_t s = s0; s < s1; ++s)
-            if ((size_t)out.labels[s] >= kHist) table->add_count(out.labels[s], 1);
+      unknown[k] = unk ? 1 : 0;
+      if (unk && out.labels) {     // its known labels were counted: the commit recounts it
+        for (int64_t s = sample_base[k]; s < sample_base[k + 1]; ++s)
+          if (out.labels[s] >= 0 && (size_t)out.labels[s] < hist.size()) --hist[out.labels[s]];
       }
     }
-    for (size_t id = 0; id < hist.size(); ++id)
-      if (hist[id]) table->add_count((int)id, hist[id]);
   });
-  if (bad.load() >= 0) {
+  if (bad.load() >= 0) {        // nothing was added to the label table
     res.error = bad_kind.load();
     res.error_request = bad.load();
     return res;
+  }
+  // Every request validated: commit. Requests that carried new labels are
+  // re-scanned in request order with a label-adding cache (new labels get
+  // ids in the order they appear), the others' counts come from the chunk
+  // histograms and the per-sample pass for ids past the histogram.
+  if (count) {
+    LabelCache adder(table, true);
+    std::vector<uint64_t> dummy;
+    for (size_t k = 0; k < R; ++k) {
+      if (!unknown[k]) continue;
+      bool unk = false;
+      const int64_t sl = scan_into(reqs[k], kind, sps, spn, &adder, out, byte_base[k],
+                                   sample_base[k], dummy.data(), 0, &unk);
+      if (sl < 0) { res.error = sl == -2 ? 3 : 1; res.error_request = (int64_t)k; return res; }
+      for (int64_t s = sample_base[k]; s < sample_base[k + 1]; ++s)
+        if (out.labels && out.labels[s] >= 0) table->add_count(out.labels[s], 1);
+    }
+    for (const auto& hist : hists)
+      for (size_t id = 0; id < hist.size(); ++id)
+        if (hist[id]) table->add_count((int)id, hist[id]);
+    if (out.labels)
+      for (size_t k = 0; k < R; ++k) {
+        if (unknown[k]) continue;
+        for (int64_t s = sample_base[k]; s < sample_base[k + 1]; ++s)
+          if ((size_t)out.labels[s] >= kHist) table->add_count(out.labels[s], 1);
+      }
   }
 
   // ---- pass 3: slot bases

@@ -82,3 +82,40 @@ def test_label_table_delete_and_revive():
     assert t.remove("x") and not t.remove("x")
     assert t.lookup("x") == -1 and t.alive() == [False, True]
     assert t.get_or_add("x") == 0 and t.alive() == [True, True]
+
+
+def test_pack_requests_has_no_side_effects_on_a_bad_batch():
+    """a malformed request must leave the label table untouched
+    (labels and counts are committed only after every request validated), so
+    the per-request retry of the RPC batch path does not double-count."""
+    import msgpack
+    import numpy as np
+    from jubatus_amd._native import native
+    nat = native()
+    t = nat.LabelTable()
+    t.get_or_add("old")
+    good = msgpack.packb([["old", [[["a", "x"]], [], []]], ["new1", [[["a", "y"]], [], []]]],
+                         use_bin_type=False)
+    good2 = msgpack.packb([["new2", [[], [["n", 1.5]], []]]] * 3, use_bin_type=False)
+    bad = msgpack.packb([["new3", [[["a"]], [], []]]], use_bin_type=False)    # pair of 1
+    cap = 1 << 16
+    staging = np.zeros(cap, np.uint8)
+    off = np.zeros(64, np.int64)
+    ln = np.zeros(64, np.int32)
+    lab = np.zeros(64, np.int32)
+    rp = np.zeros(65, np.int64)
+    sp = np.zeros(8, np.int64)
+
+    def pack(bodies):
+        return nat.pack_requests(bodies, 1, 1, 1, t, staging.ctypes.data, cap, off.ctypes.data,
+                                 ln.ctypes.data, lab.ctypes.data, rp.ctypes.data, sp.ctypes.data,
+                                 64, 2)
+
+    n, nbytes, nslots, err, err_req = pack([good, bad, good2])
+    assert err == 1 and err_req == 1
+    assert t.names() == ["old"] and t.count(0) == 0          # nothing committed
+    n, nbytes, nslots, err, err_req = pack([good, good2])
+    assert err == 0 and n == 5
+    assert t.names() == ["old", "new1", "new2"]               # order of first appearance
+    assert [t.count(i) for i in range(3)] == [1, 1, 3]
+    assert lab[:5].tolist() == [0, 1, 2, 2, 2]
