@@ -142,6 +142,76 @@ class FreshStream:
                 used_in_blk = 0
 
 
+def served_train(args, local: int, nat) -> dict:
+    """The served train path: an in-process jubaclassifier (AROW, this GPU)
+    behind the native msgpack-RPC transport, driven by the native load
+    generator (csrc/tools/jubaloadgen.cpp) with train requests of
+    ``per_request`` samples over loopback TCP. The transport copies each
+    request body into a pinned arena slot; one Python call per slot runs
+    the GPU scan -> fv_hash -> train pipeline and replies per request
+    (classifier_impl.cpp:54-57 -> classifier_serv.cpp:128-147)."""
+    import tempfile
+    exe = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaloadgen")
+    if not os.access(exe, os.X_OK):
+        return {"skipped": "jubaloadgen not built"}
+    from jubatus_amd.framework.server_helper import ServerHelper
+    from jubatus_amd.framework.server_util import ServerArgv
+    from jubatus_amd.server import get_serv
+    tmp = tempfile.mkdtemp(prefix="jb_served_")
+    cfg = json.loads(json.dumps(AROW_CONFIG))
+    cfg["converter"]["hash_max_size"] = 1 << args.hash_bits
+    cfg_path = os.path.join(tmp, "arow.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg, f)
+    a = ServerArgv.parse(["-p", "9199", "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
+                          "-c", str(args.rpc_threads), "--gpu", str(local)], "classifier")
+    a.port = 0
+    h = ServerHelper(get_serv("classifier"), a, install_signals=False)
+    h.start(block=False)
+    try:
+        # K distinct train requests: params [cluster name "", body]
+        K = args.rpc_distinct
+        cap = K * args.per_request * 400 + (1 << 20)
+        buf = np.zeros(cap, np.uint8)
+        offs = np.zeros(K, np.int64)
+        lens = np.zeros(K, np.int64)
+        used = nat.synth_requests(buf.ctypes.data, cap, offs.ctypes.data, lens.ctypes.data, 4242, 0,
+                                  K, args.per_request, args.labels, args.str_features,
+                                  args.num_features, args.vocab, 16, 0.6, 8)
+        assert used > 0
+        pfile = os.path.join(tmp, "train_params.bin")
+        with open(pfile, "wb") as f:
+            for o, n in zip(offs, lens):
+                f.write(b"\x92\xa0" + buf[o:o + n].tobytes())
+        base = [exe, "-p", str(a.port), "-m", "train", "-f", pfile, "-c", str(args.rpc_conns),
+                "-d", str(args.rpc_depth)]
+        subprocess.run(base + ["-t", "1.5"], capture_output=True, text=True, timeout=120)  # warmup
+        clf = h.server.clf
+        clf.synchronize()
+        st0 = clf.train_stats()
+        r = subprocess.run(base + ["-t", str(args.rpc_seconds)], capture_output=True, text=True,
+                           timeout=args.rpc_seconds + 120)
+        if r.returncode != 0:
+            return {"error": (r.stderr or r.stdout)[-400:]}
+        lg = json.loads(r.stdout.strip().splitlines()[-1])
+        clf.synchronize()
+        st1 = clf.train_stats()
+        tr = st1["trained"] - st0["trained"]
+        return {"served_train_samples_per_sec": round(lg["requests_per_s"] * args.per_request, 1),
+                "requests_per_s": lg["requests_per_s"], "samples_per_request": args.per_request,
+                "connections": lg["connections"], "depth": lg["depth"],
+                "distinct_requests": lg["distinct_requests"], "rpc_p50_us": lg["p50_us"],
+                "rpc_p99_us": lg["p99_us"], "seconds": lg["seconds"],
+                "samples_trained_in_window": tr,
+                "update_fraction": round((st1["updated"] - st0["updated"]) / tr, 4) if tr else None,
+                "server_threads": args.rpc_threads,
+                "train_scan": dict(clf._scan_stats),
+                "path": "loopback TCP -> native epoll transport -> pinned arena slot -> GPU scan/"
+                        "fv_hash/AROW train; reply per request after the batch's scan check"}
+    finally:
+        h.stop()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -169,6 +239,14 @@ def main() -> None:
                          "(linear_mixer.cpp:337-344,358-390: interval_count 512 updates, the mixer "
                          "wakes on the threshold), agreed across ranks each batch")
     ap.add_argument("--latency-iters", type=int, default=300)
+    ap.add_argument("--no-rpc", action="store_true",
+                    help="skip the served-path measurement (jubaclassifier + jubaloadgen, N = 1)")
+    ap.add_argument("--rpc-seconds", type=float, default=4.0)
+    ap.add_argument("--rpc-conns", type=int, default=32)
+    ap.add_argument("--rpc-depth", type=int, default=8)
+    ap.add_argument("--rpc-threads", type=int, default=32,
+                    help="server RPC threads (a quarter of them are epoll IO threads)")
+    ap.add_argument("--rpc-distinct", type=int, default=512, help="distinct train requests cycled")
     ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
                     help="how concurrent request streams update shared rows")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -381,6 +459,10 @@ def main() -> None:
     p50 = statistics.median(lat)
     p99 = lat[min(len(lat) - 1, int(0.99 * len(lat)))]
 
+    served = None
+    if world == 1 and device is not None and not args.no_rpc:
+        served = served_train(args, local, nat)
+
     total = samples_per_step * args.steps * world
     value = total / elapsed
     if rank == 0:
@@ -429,6 +511,7 @@ def main() -> None:
             "mix_last": getattr(clf, "_last_mix", {}),
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
+            "served": served,
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),
             "heldout_accuracy": round(acc, 4),

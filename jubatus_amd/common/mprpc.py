@@ -132,6 +132,17 @@ class RpcServer:
         self._batch[name] = fn
         self._srv.set_batch(sorted(self._batch), self._dispatch_batch)
 
+    def set_arena(self, name: str, slots: list[int], slot_bytes: int, fn: Callable) -> None:
+        """Arena batching (csrc/native/jb_rpc.cpp): the IO threads copy each
+        ``name`` request's body (params [cluster name, body]) into one of the
+        pinned ``slots``; ``fn(slot, offs, lens) -> (results int64[n], errors
+        dict)`` serves a whole slot; the slot is reused after
+        ``release_slot``. Register before start()."""
+        self._srv.set_arena_batch(name, list(slots), int(slot_bytes), fn)
+
+    def release_slot(self, slot: int) -> None:
+        self._srv.release_slot(int(slot))
+
     def batches(self) -> int:
         return self._srv.batches()
 

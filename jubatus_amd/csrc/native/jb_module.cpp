@@ -1,5 +1,6 @@
 // Python bindings of the host-native runtime (_jubatus_native).
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include "jb_hash.hpp"
@@ -146,6 +147,79 @@ class PyRpcServer {
         },
         max_batch);
   }
+  // Arena batching (jb_rpc.hpp): fn(slot: int, offs: int64[n], lens: int64[n])
+  // -> (results: int64[n], errors: dict[int, str]); results[i] >= 0 is the
+  // reply value, -1 ARGUMENT_ERROR, -2 the message errors[i], -3 no reply.
+  // Responses are encoded here (old-spec msgpack), not in Python.
+  void set_arena_batch(const std::string& method, std::vector<uintptr_t> slots, size_t slot_bytes,
+                       py::object fn) {
+    arena_fn_ = std::move(fn);
+    std::vector<uint8_t*> ptrs;
+    for (auto p : slots) ptrs.push_back((uint8_t*)p);
+    srv_->set_arena_batch(method, ptrs, slot_bytes,
+                          [this](int slot, const std::vector<jb::ArenaReq>& reqs) {
+      const size_t n = reqs.size();
+      std::vector<std::string> out(n);
+      std::vector<int64_t> res(n, -2);
+      std::vector<std::string> msg(n);
+      {
+        py::gil_scoped_acquire gil;
+        try {
+          py::array_t<int64_t> offs(n), lens(n);
+          auto o = offs.mutable_unchecked<1>();
+          auto l = lens.mutable_unchecked<1>();
+          for (size_t i = 0; i < n; ++i) { o(i) = (int64_t)reqs[i].off; l(i) = (int64_t)reqs[i].len; }
+          py::tuple r = arena_fn_(slot, offs, lens);
+          py::array_t<int64_t> vals = r[0].cast<py::array_t<int64_t>>();
+          auto v = vals.unchecked<1>();
+          for (size_t i = 0; i < n && i < (size_t)v.shape(0); ++i) res[i] = v(i);
+          py::dict errs = r[1].cast<py::dict>();
+          for (auto kv : errs) {
+            const size_t i = kv.first.cast<size_t>();
+            if (i < n) msg[i] = py::str(kv.second).cast<std::string>();
+          }
+        } catch (py::error_already_set& e) {
+          for (size_t i = 0; i < n; ++i) msg[i] = e.what();
+        }
+      }
+      for (size_t i = 0; i < n; ++i) {
+        if (res[i] == -3) continue;
+        std::string& b = out[i];
+        b.push_back((char)0x94);
+        b.push_back((char)0x01);
+        b.push_back((char)0xce);
+        for (int k = 3; k >= 0; --k) b.push_back((char)((reqs[i].msgid >> (8 * k)) & 0xff));
+        if (res[i] >= 0) {
+          b.push_back((char)0xc0);
+          const uint64_t x = (uint64_t)res[i];
+          if (x < 128) {
+            b.push_back((char)x);
+          } else if (x < 65536) {
+            b.push_back((char)0xcd); b.push_back((char)(x >> 8)); b.push_back((char)x);
+          } else if (x < (1ull << 32)) {
+            b.push_back((char)0xce);
+            for (int k = 3; k >= 0; --k) b.push_back((char)(x >> (8 * k)));
+          } else {
+            b.push_back((char)0xcf);
+            for (int k = 7; k >= 0; --k) b.push_back((char)(x >> (8 * k)));
+          }
+        } else if (res[i] == -1) {
+          b.push_back((char)0x02);          // ARGUMENT_ERROR
+          b.push_back((char)0xc0);
+        } else {
+          std::string m = msg[i].empty() ? std::string("error") : msg[i];
+          if (m.size() > 65535) m.resize(65535);
+          if (m.size() < 32) b.push_back((char)(0xa0 | m.size()));
+          else { b.push_back((char)0xda); b.push_back((char)(m.size() >> 8)); b.push_back((char)m.size()); }
+          b += m;
+          b.push_back((char)0xc0);
+        }
+      }
+      return out;
+    });
+  }
+  void release_slot(int slot) { srv_->release_slot(slot); }
+  void set_max_message(uint64_t n) { srv_->set_max_message(n); }
   uint64_t batches() const { return srv_->batches(); }
   void set_io_threads(int n) { srv_->set_io_threads(n); }
   int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
@@ -161,6 +235,7 @@ class PyRpcServer {
  private:
   py::object handler_;
   py::object batch_fn_;
+  py::object arena_fn_;
   std::unique_ptr<jb::RpcServer> srv_;
 };
 
@@ -226,6 +301,10 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("set_batch", &PyRpcServer::set_batch, py::arg("methods"), py::arg("fn"),
            py::arg("max_batch") = 4096)
       .def("batches", &PyRpcServer::batches)
+      .def("set_arena_batch", &PyRpcServer::set_arena_batch, py::arg("method"), py::arg("slots"),
+           py::arg("slot_bytes"), py::arg("fn"))
+      .def("release_slot", &PyRpcServer::release_slot)
+      .def("set_max_message", &PyRpcServer::set_max_message)
       .def("set_io_threads", &PyRpcServer::set_io_threads)
       .def("listen", &PyRpcServer::listen)
       .def("start", &PyRpcServer::start)

@@ -14,6 +14,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <stdexcept>
 
 #include "jb_msgpack.hpp"
@@ -89,6 +90,68 @@ void set_nonblock(int fd) {
 
 }  // namespace
 
+int frame_resume(const uint8_t* b, size_t n, FrameState& st) {
+  for (;;) {
+    if (st.started && st.stack.empty()) return 1;
+    if (st.pos >= n) return 0;
+    const uint8_t* p = b + st.pos;
+    const uint8_t t = p[0];
+    auto have = [&](uint64_t k) { return st.pos + k <= n; };
+    auto be = [&](int off, int nb) -> uint64_t {
+      uint64_t v = 0;
+      for (int i = 0; i < nb; ++i) v = (v << 8) | p[off + i];
+      return v;
+    };
+    uint64_t hdr = 1, payload = 0, count = 0;
+    bool container = false;
+    if (t <= 0x7f || t >= 0xe0 || t == 0xc0 || t == 0xc2 || t == 0xc3) {
+    } else if ((t & 0xe0) == 0xa0) {
+      payload = t & 0x1f;
+    } else if ((t & 0xf0) == 0x90) {
+      container = true; count = t & 0x0f;
+    } else if ((t & 0xf0) == 0x80) {
+      container = true; count = 2u * (t & 0x0f);
+    } else {
+      switch (t) {
+        case 0xcc: case 0xd0: payload = 1; break;
+        case 0xcd: case 0xd1: payload = 2; break;
+        case 0xce: case 0xd2: case 0xca: payload = 4; break;
+        case 0xcf: case 0xd3: case 0xcb: payload = 8; break;
+        case 0xd9: case 0xc4: if (!have(2)) return 0; hdr = 2; payload = be(1, 1); break;
+        case 0xda: case 0xc5: if (!have(3)) return 0; hdr = 3; payload = be(1, 2); break;
+        case 0xdb: case 0xc6: if (!have(5)) return 0; hdr = 5; payload = be(1, 4); break;
+        case 0xd4: payload = 2; break;
+        case 0xd5: payload = 3; break;
+        case 0xd6: payload = 5; break;
+        case 0xd7: payload = 9; break;
+        case 0xd8: payload = 17; break;
+        case 0xc7: if (!have(2)) return 0; hdr = 2; payload = 1 + be(1, 1); break;
+        case 0xc8: if (!have(3)) return 0; hdr = 3; payload = 1 + be(1, 2); break;
+        case 0xc9: if (!have(5)) return 0; hdr = 5; payload = 1 + be(1, 4); break;
+        case 0xdc: case 0xde:
+          if (!have(3)) return 0;
+          hdr = 3; container = true; count = be(1, 2) * (t == 0xde ? 2 : 1); break;
+        case 0xdd: case 0xdf:
+          if (!have(5)) return 0;
+          hdr = 5; container = true; count = be(1, 4) * (t == 0xdf ? 2 : 1); break;
+        default: return -1;
+      }
+    }
+    if (!have(hdr + payload)) return 0;
+    st.pos += hdr + payload;
+    st.started = true;
+    if (container && count > 0) {
+      if (st.stack.size() >= 128) return -1;
+      st.stack.push_back(count);
+      continue;
+    }
+    while (!st.stack.empty()) {        // one element done
+      if (--st.stack.back() > 0) break;
+      st.stack.pop_back();
+    }
+  }
+}
+
 int64_t msgpack_frame(const uint8_t* p, size_t n) {
   Cursor c{p, p + n};
   int r = skip_status(c, 0);
@@ -131,11 +194,20 @@ void RpcServer::enqueue(RpcRequest&& req) {
 // the next (larger) batch - adaptive batching without a timer.
 void RpcServer::batch_loop() {
   for (;;) {
+    if (arena_handler_ && arena_batch_once()) continue;
     std::vector<RpcRequest> batch;
     {
       std::unique_lock<std::mutex> g(bmu_);
-      bcv_.wait(g, [this] { return !bqueue_.empty() || !running_.load(); });
+      bcv_.wait_for(g, std::chrono::milliseconds(arena_handler_ ? 1 : 100), [this] {
+        if (!bqueue_.empty() || !running_.load()) return true;
+        if (!arena_handler_) return false;
+        std::lock_guard<std::mutex> a(amu_);
+        for (const auto& s : slots_)
+          if (!s.busy && !s.reqs.empty()) return true;
+        return false;
+      });
       if (!running_.load()) return;
+      if (bqueue_.empty()) continue;
       const std::string method = bqueue_.front().method;
       for (auto it = bqueue_.begin(); it != bqueue_.end() && batch.size() < max_batch_;) {
         if (it->method == method) {
@@ -145,6 +217,17 @@ void RpcServer::batch_loop() {
           ++it;
         }
       }
+    }
+    if (!batch_handler_) {          // arena-only server: an overflow request
+      for (auto& r : batch)
+        if (!r.notify) {
+          std::string o("\x94\x01", 2);
+          o.push_back((char)0xce);
+          for (int k = 3; k >= 0; --k) o.push_back((char)((r.msgid >> (8 * k)) & 0xff));
+          o += "\xa4busy\xc0";
+          send_response(r.conn_id, o);
+        }
+      continue;
     }
     std::vector<std::string> resp = batch_handler_(batch[0].method, batch);
     batches_.fetch_add(1);
@@ -197,7 +280,7 @@ void RpcServer::start() {
   }
   for (int i = 0; i < nio_; ++i) loops_[i]->th = std::thread([this, i] { io_loop(i); });
   for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker_loop(); });
-  if (batch_handler_) batcher_ = std::thread([this] { batch_loop(); });
+  if (batch_handler_ || arena_handler_) batcher_ = std::thread([this] { batch_loop(); });
 }
 
 void RpcServer::stop() {
@@ -360,9 +443,15 @@ void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
   while (pos < c->rbuf.size()) {
     const uint8_t* p = (const uint8_t*)c->rbuf.data() + pos;
     const size_t avail = c->rbuf.size() - pos;
-    int64_t len = msgpack_frame(p, avail);
-    if (len == 0) break;
-    if (len < 0) { eof = true; break; }
+    const int fr = frame_resume(p, avail, c->fs);
+    if (fr == 0) {
+      // incomplete: keep the walk's state; refuse oversized messages
+      if (c->fs.pos > max_message_ || avail > max_message_) eof = true;
+      break;
+    }
+    if (fr < 0) { eof = true; break; }
+    const int64_t len = (int64_t)c->fs.pos;
+    c->fs.reset();
     Cursor cur{p, p + len};
     uint32_t n;
     double type = -1, msgid = 0;
@@ -372,8 +461,20 @@ void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
     if (ok && n == 4 && type == 0) {
       ok = cur.number(&msgid) && cur.raw(&m, &mlen);
       if (ok) {
-        enqueue(RpcRequest{c->id, (uint32_t)msgid, false, std::string((const char*)m, mlen),
-                           std::string((const char*)cur.p, (size_t)(p + len - cur.p))});
+        bool taken = false;
+        if (!arena_method_.empty() && mlen == arena_method_.size() &&
+            memcmp(m, arena_method_.data(), mlen) == 0) {
+          // params = [name, body]: the body goes straight into an arena slot
+          Cursor pc{cur.p, p + len};
+          uint32_t np;
+          const uint8_t* nm;
+          uint32_t nlen;
+          if (pc.array(&np) && np == 2 && pc.raw(&nm, &nlen))
+            taken = arena_take(c->id, (uint32_t)msgid, pc.p, (size_t)(p + len - pc.p));
+        }
+        if (!taken)
+          enqueue(RpcRequest{c->id, (uint32_t)msgid, false, std::string((const char*)m, mlen),
+                             std::string((const char*)cur.p, (size_t)(p + len - cur.p))});
       }
     } else if (ok && n == 3 && type == 2) {
       ok = cur.raw(&m, &mlen);
@@ -381,12 +482,97 @@ void RpcServer::on_readable(const std::shared_ptr<Conn>& c) {
         enqueue(RpcRequest{c->id, 0, true, std::string((const char*)m, mlen),
                            std::string((const char*)cur.p, (size_t)(p + len - cur.p))});
       }
+    } else if (ok && n == 4 && type == 1) {
+      ok = true;   // responses sent to a server are ignored
     }
-    // responses (type 1) sent to a server are ignored
+    if (!ok) { eof = true; break; }   // not an RPC envelope: no msgid to answer, drop the peer
     pos += (size_t)len;
   }
   if (pos) c->rbuf.erase(0, pos);
   if (eof) close_conn(c->id);
+}
+
+// ---------------------------------------------------------- arena batching
+void RpcServer::set_arena_batch(const std::string& method, const std::vector<uint8_t*>& slots,
+                                size_t slot_bytes, ArenaHandler h) {
+  arena_method_ = method;
+  arena_handler_ = std::move(h);
+  slot_bytes_ = slot_bytes;
+  slots_.assign(slots.size(), Slot());
+  for (size_t i = 0; i < slots.size(); ++i) slots_[i].base = slots[i];
+  open_ = -1;
+}
+
+void RpcServer::release_slot(int slot) {
+  std::lock_guard<std::mutex> g(amu_);
+  if (slot < 0 || slot >= (int)slots_.size()) return;
+  slots_[slot].busy = false;
+  slots_[slot].used = 0;
+  slots_[slot].reqs.clear();
+  acv_.notify_all();
+}
+
+// IO thread: reserve room in the open slot (opening a free one if needed),
+// copy the body outside the lock. false: no room anywhere (caller falls
+// back to the ordinary batch path).
+bool RpcServer::arena_take(uint64_t conn_id, uint32_t msgid, const uint8_t* body, size_t len) {
+  const uint64_t need = (len + 15) & ~(uint64_t)15;
+  if (need > slot_bytes_) return false;
+  int k;
+  uint64_t off;
+  {
+    std::lock_guard<std::mutex> g(amu_);
+    if (open_ >= 0 && slots_[open_].used + need > slot_bytes_) open_ = -1;   // full: batcher seals it
+    if (open_ < 0) {
+      for (size_t i = 0; i < slots_.size(); ++i) {
+        Slot& s = slots_[i];
+        if (!s.busy && s.reqs.empty() && s.writers == 0) { open_ = (int)i; break; }
+      }
+      if (open_ < 0) return false;
+    }
+    k = open_;
+    Slot& s = slots_[k];
+    off = s.used;
+    s.used += need;
+    ++s.writers;
+    s.reqs.push_back(ArenaReq{conn_id, msgid, off, (uint64_t)len});
+  }
+  memcpy(slots_[k].base + off, body, len);
+  {
+    std::lock_guard<std::mutex> g(amu_);
+    if (--slots_[k].writers == 0) acv_.notify_all();
+  }
+  {
+    std::lock_guard<std::mutex> g(bmu_);
+    bcv_.notify_one();
+  }
+  return true;
+}
+
+// Batch thread: seal the fullest slot that holds requests (the open one
+// included), wait until its copies landed, hand it to the handler.
+bool RpcServer::arena_batch_once() {
+  int k = -1;
+  std::vector<ArenaReq> reqs;
+  {
+    std::unique_lock<std::mutex> g(amu_);
+    for (size_t i = 0; i < slots_.size(); ++i)
+      if (!slots_[i].busy && !slots_[i].reqs.empty() &&
+          (k < 0 || slots_[i].used > slots_[k].used))
+        k = (int)i;
+    if (k < 0) return false;
+    if (open_ == k) open_ = -1;                 // sealed: new bodies go elsewhere
+    Slot& s = slots_[k];
+    s.busy = true;
+    acv_.wait(g, [&] { return s.writers == 0; });
+    reqs.swap(s.reqs);
+  }
+  std::vector<std::string> resp = arena_handler_(k, reqs);
+  batches_.fetch_add(1);
+  served_.fetch_add(reqs.size());
+  for (size_t i = 0; i < reqs.size() && i < resp.size(); ++i)
+    if (!resp[i].empty()) send_response(reqs[i].conn_id, resp[i]);
+  return true;
 }
 
 void RpcServer::flush(const std::shared_ptr<Conn>& c) {

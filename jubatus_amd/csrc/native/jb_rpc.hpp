@@ -37,6 +37,27 @@ struct RpcRequest {
   std::string params;  // msgpack array bytes
 };
 
+// A request of the arena-batched method: its body (params[1]) sits at
+// [off, off + len) of an arena slot.
+struct ArenaReq {
+  uint64_t conn_id;
+  uint32_t msgid;
+  uint64_t off;
+  uint64_t len;
+};
+
+// Resumable framing state of one connection's partial message: the walk
+// continues where the previous read stopped (no re-parse per read).
+struct FrameState {
+  uint64_t pos = 0;                 // next byte, relative to the message start
+  std::vector<uint64_t> stack;      // elements left per open container
+  bool started = false;
+  void reset() { pos = 0; stack.clear(); started = false; }
+};
+
+// 1 complete (st.pos = length), 0 need more bytes, -1 malformed
+int frame_resume(const uint8_t* b, size_t n, FrameState& st);
+
 class RpcServer {
  public:
   // handler(request) -> encoded response bytes (empty for notifications)
@@ -52,6 +73,20 @@ class RpcServer {
   // drains everything queued for a method and calls `h` once for all of it
   // (concurrent train / classify RPCs become one GPU launch). Call before start().
   void set_batch(const std::vector<std::string>& methods, BatchHandler h, size_t max_batch);
+
+  // arena handler(slot, requests) -> one encoded response per request
+  using ArenaHandler = std::function<std::vector<std::string>(int, const std::vector<ArenaReq>&)>;
+  // Arena batching for `method` (params [name, body], e.g. train): the IO
+  // thread that frames a request copies its body straight into the open slot
+  // of caller-owned (pinned) memory - no intermediate string, no Python;
+  // the batch thread seals the slot and calls `h` once for every request in
+  // it. A slot is reused after release_slot(); when no slot has room the
+  // request takes the ordinary batch path (the handler of set_batch).
+  void set_arena_batch(const std::string& method, const std::vector<uint8_t*>& slots,
+                       size_t slot_bytes, ArenaHandler h);
+  void release_slot(int slot);
+  // largest accepted request (bytes); a connection sending more is closed
+  void set_max_message(uint64_t n) { max_message_ = n; }
   uint64_t batches() const { return batches_.load(); }
   ~RpcServer();
   // returns the bound port (useful with port 0)
@@ -71,6 +106,7 @@ class RpcServer {
     uint64_t id;
     int loop = 0;
     std::string rbuf;
+    FrameState fs;     // framing progress of the message at the head of rbuf
     std::mutex wmu;
     std::string wbuf;  // pending output
     bool want_write = false;
@@ -92,6 +128,8 @@ class RpcServer {
   void send_response(uint64_t conn_id, const std::string& bytes);
   void batch_loop();
   void enqueue(RpcRequest&& req);
+  bool arena_take(uint64_t conn_id, uint32_t msgid, const uint8_t* body, size_t len);
+  bool arena_batch_once();
 
   Handler handler_;
   int nworkers_;
@@ -120,6 +158,22 @@ class RpcServer {
   std::deque<RpcRequest> bqueue_;
   std::thread batcher_;
   std::atomic<uint64_t> batches_{0};
+  uint64_t max_message_ = (uint64_t)1 << 31;
+  // arena batching
+  struct Slot {
+    uint8_t* base = nullptr;
+    uint64_t used = 0;
+    int writers = 0;          // IO threads still copying into this slot
+    bool busy = false;        // handed to the handler, not released yet
+    std::vector<ArenaReq> reqs;
+  };
+  std::string arena_method_;
+  ArenaHandler arena_handler_;
+  uint64_t slot_bytes_ = 0;
+  std::vector<Slot> slots_;
+  int open_ = -1;             // slot receiving bodies (-1: none)
+  std::mutex amu_;            // guards slots_ / open_; waits on bcv_ use bmu_
+  std::condition_variable acv_;   // writers drained / slot released
 };
 
 // Frame one complete msgpack object at the head of [p, p+n): returns its

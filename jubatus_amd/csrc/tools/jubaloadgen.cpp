@@ -1,10 +1,13 @@
 // jubaloadgen: native msgpack-RPC load generator (benchmarks of the servers'
 // request path without a Python client in the way).
 //
-// Sends one pre-encoded request (params = a msgpack array read from a file,
-// e.g. ["", [[label, datum]...]] for train) on C connections, each keeping
-// D requests in flight, for T seconds; prints one JSON line with the request
-// rate and the per-request latency distribution. Any error response aborts.
+// Sends pre-encoded requests (params = msgpack arrays read from a file, e.g.
+// ["", [[label, datum]...]] for train; several params objects concatenated in
+// the file are sent in turn, each connection starting at its own one) on C
+// connections, each keeping D requests in flight, for T seconds; prints one
+// JSON line with the request rate and the per-request latency distribution.
+// Any error response aborts. The envelope and the params go out with one
+// sendmsg (two iovecs, no per-request copy of the params).
 //
 // Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
 #include <arpa/inet.h>
@@ -14,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -32,7 +36,8 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
-std::string request_bytes(uint32_t msgid, const std::string& method, const std::string& params) {
+// envelope head [0, msgid, method, (params follow)
+std::string request_head(uint32_t msgid, const std::string& method) {
   std::string o;
   o.push_back((char)0x94);
   o.push_back((char)0x00);
@@ -42,8 +47,33 @@ std::string request_bytes(uint32_t msgid, const std::string& method, const std::
   if (n < 32) o.push_back((char)(0xa0 | n));
   else { o.push_back((char)0xda); o.push_back((char)(n >> 8)); o.push_back((char)n); }
   o += method;
-  o += params;
   return o;
+}
+
+bool send_all(int fd, const std::string& head, const std::string& params) {
+  size_t done = 0;
+  const size_t total = head.size() + params.size();
+  while (done < total) {
+    iovec iov[2];
+    int n = 0;
+    if (done < head.size()) {
+      iov[n].iov_base = (void*)(head.data() + done);
+      iov[n++].iov_len = head.size() - done;
+      iov[n].iov_base = (void*)params.data();
+      iov[n++].iov_len = params.size();
+    } else {
+      const size_t o = done - head.size();
+      iov[n].iov_base = (void*)(params.data() + o);
+      iov[n++].iov_len = params.size() - o;
+    }
+    msghdr m{};
+    m.msg_iov = iov;
+    m.msg_iovlen = n;
+    const ssize_t w = sendmsg(fd, &m, MSG_NOSIGNAL);
+    if (w <= 0) return false;
+    done += (size_t)w;
+  }
+  return true;
 }
 
 int connect_to(const std::string& host, int port) {
@@ -69,12 +99,14 @@ struct Result {
   std::string error;
 };
 
-void run_conn(const std::string& host, int port, const std::string& method, const std::string& params,
-              int depth, double secs, Result* r) {
+void run_conn(const std::string& host, int port, const std::string& method,
+              const std::vector<std::string>* params, size_t first, int depth, double secs,
+              Result* r) {
   const int fd = connect_to(host, port);
   if (fd < 0) { r->error = "connect failed"; return; }
   std::vector<Clock::time_point> sent(1 << 16);
   uint32_t next = 1;
+  size_t which = first;
   int inflight = 0;
   std::string rbuf;
   const auto t_end = Clock::now() + std::chrono::duration<double>(secs);
@@ -83,14 +115,10 @@ void run_conn(const std::string& host, int port, const std::string& method, cons
   while (sending || inflight > 0) {
     while (sending && inflight < depth) {
       if (Clock::now() >= t_end) { sending = false; break; }
-      const std::string req = request_bytes(next, method, params);
+      const std::string head = request_head(next, method);
       sent[next & 0xffff] = Clock::now();
-      size_t off = 0;
-      while (off < req.size()) {
-        ssize_t w = send(fd, req.data() + off, req.size() - off, MSG_NOSIGNAL);
-        if (w <= 0) { r->error = "send failed"; close(fd); return; }
-        off += (size_t)w;
-      }
+      if (!send_all(fd, head, (*params)[which])) { r->error = "send failed"; close(fd); return; }
+      which = (which + 1) % params->size();
       ++next;
       ++inflight;
     }
@@ -141,13 +169,21 @@ int main(int argc, char** argv) {
   std::ifstream ifs(file, std::ios::binary);
   std::stringstream ss;
   ss << ifs.rdbuf();
-  const std::string params = ss.str();
+  const std::string all = ss.str();
+  std::vector<std::string> params;
+  for (size_t pos = 0; pos < all.size();) {
+    const int64_t f = jb::msgpack_frame((const uint8_t*)all.data() + pos, all.size() - pos);
+    if (f <= 0) { fprintf(stderr, "params file: bad msgpack at byte %zu\n", pos); return 1; }
+    params.push_back(all.substr(pos, (size_t)f));
+    pos += (size_t)f;
+  }
   if (params.empty()) { fprintf(stderr, "empty params file\n"); return 1; }
   std::vector<Result> res(conns);
   std::vector<std::thread> ts;
   const auto t0 = Clock::now();
   for (int i = 0; i < conns; ++i)
-    ts.emplace_back(run_conn, host, port, method, params, depth, secs, &res[i]);
+    ts.emplace_back(run_conn, host, port, method, &params,
+                    (size_t)i * params.size() / (size_t)conns, depth, secs, &res[i]);
   for (auto& t : ts) t.join();
   const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
   uint64_t done = 0;
@@ -160,7 +196,7 @@ int main(int argc, char** argv) {
   std::sort(lat.begin(), lat.end());
   auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[(size_t)(q * (lat.size() - 1))]; };
   printf("{\"requests\": %llu, \"seconds\": %.3f, \"requests_per_s\": %.1f, \"connections\": %d, "
-         "\"depth\": %d, \"p50_us\": %.1f, \"p99_us\": %.1f}\n",
-         (unsigned long long)done, dt, done / dt, conns, depth, pct(0.5), pct(0.99));
+         "\"depth\": %d, \"distinct_requests\": %zu, \"p50_us\": %.1f, \"p99_us\": %.1f}\n",
+         (unsigned long long)done, dt, done / dt, conns, depth, params.size(), pct(0.5), pct(0.99));
   return 0;
 }

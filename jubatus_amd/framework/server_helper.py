@@ -106,6 +106,11 @@ class ServerHelper:
             raw = getattr(self.server, "raw_" + m.name, None)
             if raw is not None:  # zero-copy fast path (e.g. classifier train)
                 self.rpc.add(m.name, self._wrap_raw(m, raw), raw=True)
+        # arena batching: request bodies copied by the transport into pinned
+        # memory, one call per filled slot (classifier train on the GPU)
+        arenas = getattr(self.server, "arena_methods", lambda: {})()
+        for name, (slots, slot_bytes, fn) in arenas.items():
+            self.rpc.set_arena(name, slots, slot_bytes, self._wrap_arena(name, fn))
         # transport-level batching: every queued request of a method, one call
         batched = getattr(self.server, "batched_methods", lambda: {})()
         for m in specs.methods(self.type):
@@ -125,6 +130,19 @@ class ServerHelper:
                 with rw.read():
                     return fn(params)
             return fn(params)
+        return call
+
+    def _wrap_arena(self, name: str, fn: Callable) -> Callable:
+        srv = self.server
+        rpc = self.rpc
+
+        def call(slot: int, offs, lens):
+            try:
+                with srv.rw_mutex.write():
+                    srv.event_model_updated(len(offs))
+                return fn(slot, offs, lens)
+            finally:
+                rpc.release_slot(slot)
         return call
 
     def _wrap_batch(self, m: specs.Method, fn: Callable) -> Callable:

@@ -270,6 +270,59 @@ class LinearClassifier:
             self._scan_stats["host"] += 1
             return self._train_batch(self.pipe.from_arena(arena, offs, lens, True, self.labels))
 
+    def train_arena_sync(self, arena, offs, lens) -> tuple[np.ndarray, dict]:
+        """Served train batch (the RPC transport copied the request bodies
+        into a pinned arena slot, csrc/native/jb_rpc.cpp arena batching):
+        GPU scan -> fv_hash -> train, then wait (lock released) until the
+        batch's scan check is known, so each request gets its own reply.
+        -> (samples per request, or -1 = ARGUMENT_ERROR; {} reserved for
+        error messages). A batch the device scan rejected is re-run one
+        request at a time through the host scanner (which validates before
+        it changes the label table), so only the bad requests fail."""
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int64)
+        R = int(offs.size)
+        res = np.full(R, -1, dtype=np.int64)
+        from ..ops.feature_pipeline import body_counts
+        with self._lock:
+            counts = body_counts(arena.np, offs, lens)
+            chk = b = None
+            if (self.gpu and self.pipe.fast and self.gpu_scan and counts is not None
+                    and self.labels.size() > 0):
+                self._drain(block=True, keep=3)
+                self._sync_labels()
+                chk = self._check_record(self.labels.size())
+                post = self._detect_hot if self._hot_wanted(R) else None
+                b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk, post=post)
+                if b is not None:
+                    self._scan_stats["gpu"] += 1
+                    self._train_batch(b)
+                else:
+                    self._free_checks.append(chk)
+                    chk = None
+        if chk is not None:
+            chk.wait()                       # releases the GIL: other RPCs proceed
+            with self._lock:
+                if int(chk.err[0]) == 0:
+                    h = chk.hist[:chk.nhist]
+                    for lid in np.flatnonzero(h).tolist():
+                        self.labels.add_count(lid, int(h[lid]))
+                    self._free_checks.append(chk)
+                    res[:] = counts
+                    return res, {}
+                self._free_checks.append(chk)
+                self._scan_stats["replayed"] += 1
+        # host path, one request at a time (bad requests fail alone)
+        with self._lock:
+            self._scan_stats["host"] += 1
+            for k in range(R):
+                body = bytes(arena.np[offs[k]:offs[k] + lens[k]])
+                try:
+                    res[k] = self.train_requests([body])
+                except (TypeError, ValueError):
+                    res[k] = -1
+        return res, {}
+
     def _check_record(self, nhist: int):
         """a free completion record; allocated in a batch (fine-grained host
         memory is slow to allocate and synchronises the device)"""
@@ -775,6 +828,8 @@ class LinearClassifier:
                 st[f"train_scan.{k}"] = str(v)
         for k, v in self._last_mix.items():
             st[f"mix.last_{k}"] = str(v)
+        for k, v in self.train_stats().items():
+            st[f"train.samples_{k}"] = str(v)
         return st
 
 

@@ -12,6 +12,7 @@ the update counter (classifier_serv.cpp:131-134).
 from __future__ import annotations
 
 import json
+import os
 import math
 import time
 
@@ -237,6 +238,27 @@ class ClassifierServ(ServerBase):
                 except TypeError as e:
                     out[i] = ArgumentError(str(e))
         return out
+
+    def arena_methods(self) -> dict:
+        """train on the GPU pipeline straight from the transport's pinned
+        arena (no Python per request, no host scan; see RpcServer.set_arena)"""
+        clf = self.clf
+        if not (getattr(clf, "gpu", False) and getattr(clf.pipe, "fast", False)):
+            return {}
+        import torch
+        from ..ops.feature_pipeline import RequestArena
+        mb = int(os.environ.get("JUBATUS_TRAIN_ARENA_MB", "32"))
+        nslots = 4
+        self._arena_slots = [torch.empty(mb << 20, dtype=torch.uint8, pin_memory=True)
+                             for _ in range(nslots)]
+        views = [RequestArena.over(t, [], []) for t in self._arena_slots]
+
+        def serve(slot, offs, lens):
+            self.check_set_config()
+            self._batch_stats["train"][0] += len(offs)
+            self._batch_stats["train"][1] += 1
+            return self.clf.train_arena_sync(views[slot], offs, lens)
+        return {"train": ([t.data_ptr() for t in self._arena_slots], mb << 20, serve)}
 
     def get_labels(self) -> dict:
         self.check_set_config()

@@ -69,3 +69,46 @@ def test_concurrent_train_rpcs_are_batched(gpu_server):
     assert acc > 0.9, acc
     assert c.classify([]) == []
     c.close()
+
+
+def test_train_rpcs_take_the_arena_gpu_path_and_fail_alone(gpu_server):
+    """train bodies are copied by the transport into a pinned arena slot and
+    scanned on the GPU (train_scan.gpu); a malformed request in the same
+    batch gets ARGUMENT_ERROR alone while the good ones are trained"""
+    import msgpack
+    from jubatus_amd.common.mprpc import RpcClient, RpcTypeError
+    port = gpu_server.argv.port
+    c = Classifier("127.0.0.1", port, "", timeout=60)
+    rng = random.Random(5)
+    assert c.train(_data(rng, 32)) == 32          # labels become known
+    errors, bad_seen = [], []
+
+    def good(seed):
+        try:
+            cc = Classifier("127.0.0.1", port, "", timeout=60)
+            r = random.Random(seed)
+            for _ in range(10):
+                assert cc.train(_data(r, 64)) == 64
+            cc.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def bad():
+        with RpcClient("127.0.0.1", port, 60.0) as rc:
+            for _ in range(5):
+                try:
+                    rc.call("train", "", [["L1", [[["only-a-key"]], [], []]]])
+                except RpcTypeError:
+                    bad_seen.append(1)
+    ts = [threading.Thread(target=good, args=(s,)) for s in range(8)] + [threading.Thread(target=bad)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    assert len(bad_seen) == 5
+    (_, st), = c.get_status().items()
+    assert int(st["train_scan.gpu"]) >= 1
+    labels = c.get_labels()
+    assert sum(labels.values()) == 32 + 8 * 10 * 64      # the bad requests counted nothing
+    c.close()
