@@ -139,6 +139,7 @@ class RpcServer:
         dict)`` serves a whole slot; the slot is reused after
         ``release_slot``. Register before start()."""
         self._srv.set_arena_batch(name, list(slots), int(slot_bytes), fn)
+        self._srv.set_batch_threads(2)     # serve slot k while slot k+1 is submitted
 
     def release_slot(self, slot: int) -> None:
         self._srv.release_slot(int(slot))

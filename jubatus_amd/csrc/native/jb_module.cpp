@@ -222,6 +222,7 @@ class PyRpcServer {
   void set_max_message(uint64_t n) { srv_->set_max_message(n); }
   uint64_t batches() const { return srv_->batches(); }
   void set_io_threads(int n) { srv_->set_io_threads(n); }
+  void set_batch_threads(int n) { srv_->set_batch_threads(n); }
   int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
   void start() { srv_->start(); }
   void stop() {
@@ -306,6 +307,7 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("release_slot", &PyRpcServer::release_slot)
       .def("set_max_message", &PyRpcServer::set_max_message)
       .def("set_io_threads", &PyRpcServer::set_io_threads)
+      .def("set_batch_threads", &PyRpcServer::set_batch_threads)
       .def("listen", &PyRpcServer::listen)
       .def("start", &PyRpcServer::start)
       .def("stop", &PyRpcServer::stop)

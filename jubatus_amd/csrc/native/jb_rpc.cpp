@@ -280,7 +280,8 @@ void RpcServer::start() {
   }
   for (int i = 0; i < nio_; ++i) loops_[i]->th = std::thread([this, i] { io_loop(i); });
   for (int i = 0; i < nworkers_; ++i) workers_.emplace_back([this] { worker_loop(); });
-  if (batch_handler_ || arena_handler_) batcher_ = std::thread([this] { batch_loop(); });
+  if (batch_handler_ || arena_handler_)
+    for (int i = 0; i < nbatch_; ++i) batchers_.emplace_back([this] { batch_loop(); });
 }
 
 void RpcServer::stop() {
@@ -295,7 +296,9 @@ void RpcServer::stop() {
   }
   for (auto& L : loops_)
     if (L->th.joinable()) L->th.join();
-  if (batcher_.joinable()) batcher_.join();
+  for (auto& b : batchers_)
+    if (b.joinable()) b.join();
+  batchers_.clear();
   for (auto& w : workers_) if (w.joinable()) w.join();
   workers_.clear();
   {

@@ -96,6 +96,9 @@ class RpcServer {
   // number of epoll IO threads (connections are spread round-robin); call
   // before start(). One thread frames ~1 GB/s of request bytes.
   void set_io_threads(int n) { nio_ = n < 1 ? 1 : n; }
+  // batch threads (>1: a batch is served while the next one is collected
+  // and submitted; the arena handler waits on the GPU without the GIL)
+  void set_batch_threads(int n) { nbatch_ = n < 1 ? 1 : n; }
   bool running() const { return running_.load(); }
   uint64_t requests_served() const { return served_.load(); }
   uint64_t connections() const { return nconn_.load(); }
@@ -156,7 +159,8 @@ class RpcServer {
   std::mutex bmu_;
   std::condition_variable bcv_;
   std::deque<RpcRequest> bqueue_;
-  std::thread batcher_;
+  std::vector<std::thread> batchers_;
+  int nbatch_ = 1;
   std::atomic<uint64_t> batches_{0};
   uint64_t max_message_ = (uint64_t)1 << 31;
   // arena batching
