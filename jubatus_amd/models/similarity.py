@@ -401,23 +401,191 @@ def _csr_device(rows, device):
             torch.from_numpy(val).to(device))
 
 
+def normalize_csr(row_ptr: np.ndarray, idx: np.ndarray, val: np.ndarray):
+    """Per row: drop idx < 0, sort by feature, sum repeated features
+    (vectorised over the whole batch). -> (lens int64[n], idx int32[nnz],
+    val float32[nnz], squared norms float32[n])."""
+    row_ptr = np.asarray(row_ptr, dtype=np.int64)
+    n = row_ptr.size - 1
+    idx = np.asarray(idx, dtype=np.int64)[:row_ptr[-1]]
+    val = np.asarray(val, dtype=np.float64)[:row_ptr[-1]]
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(row_ptr))
+    m = idx >= 0
+    rows, idx, val = rows[m], idx[m], val[m]
+    order = np.lexsort((idx, rows))
+    rows, idx, val = rows[order], idx[order], val[order]
+    if rows.size:
+        new = np.ones(rows.size, dtype=bool)
+        new[1:] = (rows[1:] != rows[:-1]) | (idx[1:] != idx[:-1])
+        starts = np.flatnonzero(new)
+        val = np.add.reduceat(val, starts)
+        idx, rows = idx[starts], rows[starts]
+    lens = np.bincount(rows, minlength=n).astype(np.int64)
+    n2 = np.bincount(rows, weights=val * val, minlength=n).astype(np.float32)
+    return lens, idx.astype(np.int32), val.astype(np.float32), n2
+
+
+def _rows_to_csr(rows) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    lens = np.fromiter((len(r[0]) for r in rows), dtype=np.int64, count=len(rows))
+    rp = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum(lens, out=rp[1:])
+    nnz = int(rp[-1])
+    idx = np.fromiter((i for r in rows for i in r[0]), dtype=np.int64, count=nnz)
+    val = np.fromiter((v for r in rows for v in r[1]), dtype=np.float32, count=nnz)
+    return rp, idx, val
+
+
+class DevicePool:
+    """HBM row pool of the device inverted index (csrc/hip/sparse_pool.hip):
+    append-only runs of (feature, value) plus per-slot offset / length /
+    squared norm / valid. The host keeps only the slots' offsets and lengths
+    (no copy of the data) to size appends and compact the pool."""
+
+    def __init__(self, device):
+        self.device = device
+        self.cap_rows = 0
+        self.cap_entries = 0
+        self.end = 0                      # next free pool entry
+        self.live = 0                     # entries of the current runs
+        self.off_h = np.zeros(0, dtype=np.int64)
+        self.len_h = np.zeros(0, dtype=np.int64)
+        self._grow_rows(1024)
+        self._grow_entries(1 << 16)
+
+    def _grow_rows(self, need: int) -> None:
+        import torch
+        cap = max(1024, self.cap_rows)
+        while cap < need:
+            cap *= 2
+        if cap == self.cap_rows:
+            return
+        d = self.device
+
+        def grow(old, dtype, fill=0):
+            t = torch.full((cap,), fill, dtype=dtype, device=d)
+            if old is not None:
+                t[:old.numel()].copy_(old)
+            return t
+        self.r_off = grow(getattr(self, "r_off", None), torch.int64)
+        self.r_len = grow(getattr(self, "r_len", None), torch.int32)
+        self.r_n2 = grow(getattr(self, "r_n2", None), torch.float32)
+        self.valid = grow(getattr(self, "valid", None), torch.uint8)
+        off_h = np.zeros(cap, dtype=np.int64)
+        len_h = np.zeros(cap, dtype=np.int64)
+        off_h[:self.off_h.size] = self.off_h
+        len_h[:self.len_h.size] = self.len_h
+        self.off_h, self.len_h = off_h, len_h
+        self.cap_rows = cap
+
+    def _grow_entries(self, need: int) -> None:
+        import torch
+        cap = max(1 << 16, self.cap_entries)
+        while cap < need:
+            cap *= 2
+        if cap == self.cap_entries:
+            return
+        pi = torch.empty(cap, dtype=torch.int32, device=self.device)
+        pv = torch.empty(cap, dtype=torch.float32, device=self.device)
+        if self.cap_entries:
+            pi[:self.end].copy_(self.p_idx[:self.end])
+            pv[:self.end].copy_(self.p_val[:self.end])
+        self.p_idx, self.p_val = pi, pv
+        self.cap_entries = cap
+
+    def compact(self) -> None:
+        """rewrite the live runs contiguously (device gather), dropping the
+        runs that updates and removals left behind"""
+        import torch
+        live = np.flatnonzero(self.len_h > 0)
+        lens = self.len_h[live]
+        new_off = np.zeros(live.size, dtype=np.int64)
+        if live.size:
+            np.cumsum(lens[:-1], out=new_off[1:])
+        total = int(lens.sum())
+        if total:
+            d = self.device
+            src = torch.from_numpy(np.repeat(self.off_h[live] - new_off, lens)).to(d) + \
+                torch.arange(total, dtype=torch.int64, device=d)
+            self.p_idx[:total] = self.p_idx[src].clone()
+            self.p_val[:total] = self.p_val[src].clone()
+            self.r_off[torch.from_numpy(live).to(d)] = torch.from_numpy(new_off).to(d)
+        self.off_h[live] = new_off
+        self.end = self.live = total
+
+    def append(self, slots: np.ndarray, lens: np.ndarray, idx: np.ndarray, val: np.ndarray,
+               n2: np.ndarray) -> None:
+        import torch
+        from ..ops import hip
+        n, nnz = int(slots.size), int(idx.size)
+        if n == 0:
+            return
+        self._grow_rows(int(slots.max()) + 1)
+        if self.end + nnz > self.cap_entries and self.end - self.live > self.live:
+            self.compact()
+        self._grow_entries(self.end + nnz)
+        run = np.zeros(n, dtype=np.int64)
+        if n > 1:
+            np.cumsum(lens[:-1], out=run[1:])
+        meta = np.empty((n, 4), dtype=np.int64)
+        meta[:, 0] = slots
+        meta[:, 1] = lens
+        meta[:, 2] = n2.astype(np.float32).view(np.int32).astype(np.int64)
+        meta[:, 3] = run
+        pack = np.concatenate([meta.reshape(-1).view(np.uint8), idx.astype(np.int32).view(np.uint8),
+                               val.astype(np.float32).view(np.uint8)])
+        dev = torch.from_numpy(pack).to(self.device)
+        hip.pool_append(dev, n, nnz, self.end, self)
+        old = self.len_h[slots]
+        self.live += nnz - int(old.sum())
+        self.off_h[slots] = self.end + run
+        self.len_h[slots] = lens
+        self.end += nnz
+
+    def remove(self, slot: int) -> None:
+        if 0 <= slot < self.cap_rows and self.len_h[slot] >= 0:
+            self.live -= int(self.len_h[slot])
+            self.len_h[slot] = 0
+            self.valid[slot] = 0
+
+    def query_csr(self, slots: Sequence[int]):
+        """device (qptr, qidx, qval, qn2) of stored rows used as queries"""
+        import torch
+        d = self.device
+        slots = np.asarray(slots, dtype=np.int64)
+        lens = self.len_h[slots]
+        qptr = np.zeros(slots.size + 1, dtype=np.int64)
+        np.cumsum(lens, out=qptr[1:])
+        total = int(qptr[-1])
+        if total:
+            src = torch.from_numpy(np.repeat(self.off_h[slots] - qptr[:-1], lens)).to(d) + \
+                torch.arange(total, dtype=torch.int64, device=d)
+            qi, qv = self.p_idx[src], self.p_val[src]
+        else:
+            qi = torch.zeros(1, dtype=torch.int32, device=d)
+            qv = torch.zeros(1, dtype=torch.float32, device=d)
+        qn2 = self.r_n2[torch.from_numpy(slots).to(d)]
+        return torch.from_numpy(qptr).to(d), qi, qv, qn2, total
+
+
 class InvertedIndex:
     """Exact sparse similarity (inverted_index: cosine; inverted_index_euclid:
-    euclidean distance). Rows kept as sorted sparse vectors on the host; on a
-    GPU a CSR mirror is rebuilt lazily after changes and scanned by
-    ``sparse_scan`` (csrc/hip/lsh.hip)."""
+    euclidean distance). On a GPU the rows live in an HBM pool updated in
+    place (DevicePool, csrc/hip/sparse_pool.hip) and up to 8 queries are
+    scored per pass over it, then the fused top-k (csrc/hip/topk.hip) picks
+    the k best; without a GPU the rows are sorted sparse vectors on the
+    host (the oracle)."""
 
     def __init__(self, euclid: bool = False, device: Any = None):
         self.euclid = euclid
         self.device = device
         self.gpu = device is not None
         self.rows: dict[int, tuple[np.ndarray, np.ndarray]] = {}
-        self._dirty = True
-        self._dev = None
+        self.pool = DevicePool(device) if self.gpu else None
 
     def clear(self) -> None:
         self.rows.clear()
-        self._dirty = True
+        if self.gpu:
+            self.pool = DevicePool(self.device)
 
     @staticmethod
     def _norm_row(idx, val) -> tuple[np.ndarray, np.ndarray]:
@@ -429,64 +597,83 @@ class InvertedIndex:
         return ks, np.asarray([d[int(k)] for k in ks], dtype=np.float32)
 
     def set_rows(self, slots, rows) -> None:
+        if self.gpu:
+            rp, idx, val = _rows_to_csr(rows)
+            self.set_rows_csr(np.asarray(slots, dtype=np.int64), rp, idx, val)
+            return
         for s, (i, v) in zip(slots, rows):
             self.rows[int(s)] = self._norm_row(i, v)
-        self._dirty = True
 
     def set_rows_csr(self, slots: np.ndarray, row_ptr: np.ndarray, idx: np.ndarray,
                      val: np.ndarray) -> None:
+        slots = np.asarray(slots, dtype=np.int64)
+        if self.gpu:
+            lens, ni, nv, n2 = normalize_csr(row_ptr, idx, val)
+            self.pool.append(slots, lens, ni, nv, n2)
+            return
         rows = [(idx[row_ptr[i]:row_ptr[i + 1]], val[row_ptr[i]:row_ptr[i + 1]])
                 for i in range(int(slots.size))]
         self.set_rows(slots.tolist(), rows)
 
     def remove(self, slot: int) -> None:
+        if self.gpu:
+            self.pool.remove(int(slot))
+            return
         self.rows.pop(int(slot), None)
-        self._dirty = True
 
-    def _mirror(self, nrows: int):
+    # ------------------------------------------------------------ device
+    def _queries_device(self, rows):
         import torch
-        if not self._dirty and self._dev is not None and self._dev[0] == nrows:
-            return self._dev
-        lens = np.zeros(nrows, dtype=np.int64)
-        valid = np.zeros(nrows, dtype=np.uint8)
-        for s, (i, _) in self.rows.items():
-            if s < nrows:
-                lens[s] = len(i)
-                valid[s] = 1
-        rp = np.zeros(nrows + 1, dtype=np.int64)
-        np.cumsum(lens, out=rp[1:])
-        nnz = int(rp[-1])
-        idx = np.zeros(max(nnz, 1), dtype=np.int32)
-        val = np.zeros(max(nnz, 1), dtype=np.float32)
-        n2 = np.zeros(nrows, dtype=np.float32)
-        for s, (i, v) in self.rows.items():
-            if s < nrows:
-                idx[rp[s]:rp[s + 1]] = i
-                val[rp[s]:rp[s + 1]] = v
-                n2[s] = float((v.astype(np.float64) ** 2).sum())
+        rp, idx, val = _rows_to_csr(rows)
+        lens, qi, qv, qn2 = normalize_csr(rp, idx, val)
+        qptr = np.zeros(len(rows) + 1, dtype=np.int64)
+        np.cumsum(lens, out=qptr[1:])
         d = self.device
-        self._dev = (nrows, torch.from_numpy(rp).to(d), torch.from_numpy(idx).to(d),
-                     torch.from_numpy(val).to(d), torch.from_numpy(n2).to(d),
-                     torch.from_numpy(valid).to(d))
-        self._dirty = False
-        return self._dev
+        if qi.size == 0:
+            qi, qv = np.zeros(1, np.int32), np.zeros(1, np.float32)
+        return (torch.from_numpy(qptr).to(d), torch.from_numpy(qi).to(d),
+                torch.from_numpy(qv).to(d), torch.from_numpy(qn2).to(d), int(qptr[-1]))
+
+    def _scan(self, q, nq: int, nrows: int):
+        import torch
+        from ..ops import hip
+        qptr, qi, qv, qn2, total = q
+        if total > hip.POOL_MAX_Q_ENTRIES:
+            raise ValueError("query batch has more than 4096 features")
+        out = torch.empty(nq * nrows, dtype=torch.float32, device=self.device)
+        hip.pool_scan(qptr, qi, qv, qn2, nq, self.pool, nrows, 1 if self.euclid else 0, out)
+        return out
+
+    def _query_batches(self, make, n: int, nrows: int, k: int, similar: bool):
+        from ..ops import hip
+        res = []
+        for b0 in range(0, n, hip.POOL_MAX_Q):
+            b1 = min(n, b0 + hip.POOL_MAX_Q)
+            q = make(b0, b1)
+            if q[4] > hip.POOL_MAX_Q_ENTRIES and b1 - b0 > 1:      # one query at a time
+                for j in range(b0, b1):
+                    res += self._topk(self._scan(make(j, j + 1), 1, nrows), 1, nrows, k, similar)
+                continue
+            res += self._topk(self._scan(q, b1 - b0, nrows), b1 - b0, nrows, k, similar)
+        return res
+
+    def _topk(self, sc, nq: int, nrows: int, k: int, similar: bool):
+        from ..ops import hip
+        d, i = hip.topk_scores(sc, nq, nrows, k, flip=not self.euclid)
+        out = _pairs(d.cpu().numpy(), i.cpu().numpy())
+        if similar:
+            out = [[(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in r] for r in out]
+        return out
 
     def scores_device(self, row, nrows: int):
         """device score vector (cosine similarity / euclidean distance)"""
-        import torch
-        from ..ops import hip
-        qi, qv = self._norm_row(*row)
-        q2 = float((qv.astype(np.float64) ** 2).sum())
-        _, rp, ridx, rval, rn2, valid = self._mirror(nrows)
-        out = torch.empty(nrows, dtype=torch.float32, device=self.device)
-        hip.sparse_scan(torch.from_numpy(qi).to(self.device), torch.from_numpy(qv).to(self.device),
-                        q2, rp, ridx, rval, rn2, valid, nrows, 1 if self.euclid else 0, out)
-        return out
+        return self._scan(self._queries_device([row]), 1, nrows)
 
     def scores(self, row, nrows: int) -> np.ndarray:
         """similarity (cosine) or distance (euclid) of one query vs every slot"""
-        if self.gpu and nrows:
-            return self.scores_device(row, nrows).cpu().numpy()
+        if self.gpu:
+            return self.scores_device(row, nrows).cpu().numpy() if nrows else \
+                np.zeros(0, np.float32)
         qi, qv = self._norm_row(*row)
         q2 = float((qv.astype(np.float64) ** 2).sum())
         out = np.full(nrows, np.inf if self.euclid else -np.inf, dtype=np.float32)
@@ -504,18 +691,11 @@ class InvertedIndex:
         return out
 
     def query(self, rows: list, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
+        from ..ops import hip
+        if self.gpu and nrows > 0 and 0 < k <= hip.TOPK_MAX_K:
+            return self._query_batches(lambda a, b: self._queries_device(rows[a:b]), len(rows),
+                                       nrows, k, similar)
         res = []
-        if self.gpu and nrows > 0:
-            from ..ops import hip
-            if 0 < k <= hip.TOPK_MAX_K:
-                for row in rows:
-                    sc = self.scores_device(row, nrows)
-                    d, i = hip.topk_scores(sc, 1, nrows, k, flip=not self.euclid)
-                    (r,) = _pairs(d.cpu().numpy(), i.cpu().numpy())
-                    if similar:
-                        r = [(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in r]
-                    res.append(r)
-                return res
         for row in rows:
             s = self.scores(row, nrows)
             d = s if self.euclid else (1.0 - s)        # distance view
@@ -525,3 +705,14 @@ class InvertedIndex:
                 r = [(i, float(-dd if self.euclid else 1.0 - dd)) for i, dd in r]
             res.append(r)
         return res
+
+    def query_slots(self, slots, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
+        """queries that are stored rows (similar_row_from_id, LOF neighbours
+        of stored points): taken from the pool on the device"""
+        from ..ops import hip
+        slots = list(slots)
+        if self.gpu and nrows > 0 and 0 < k <= hip.TOPK_MAX_K:
+            return self._query_batches(lambda a, b: self.pool.query_csr(slots[a:b]), len(slots),
+                                       nrows, k, similar)
+        return self.query([self.rows.get(int(s), (np.zeros(0, np.int32), np.zeros(0, np.float32)))
+                           for s in slots], nrows, k, similar)

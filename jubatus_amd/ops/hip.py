@@ -68,6 +68,10 @@ _SIGS = {
                               _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                               _c_void_p],
+    "jb_pool_scan": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                     _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p],
+    "jb_pool_append": [_c_void_p, _i32, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                       _c_void_p, _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -183,6 +187,35 @@ def sparse_scan(qidx, qval, qnorm2: float, row_ptr, ridx, rval, rnorm2, valid, n
     rc = _fn("jb_sparse_scan")(_p(qidx), _p(qval), qn, float(qnorm2), _p(row_ptr), _p(ridx),
                                _p(rval), _p(rnorm2), _p(valid), nrows, metric, _p(out), _stream())
     _check(rc, "jb_sparse_scan")
+
+POOL_MAX_Q = 8              # csrc/hip/sparse_pool.hip kPoolMaxQ
+POOL_MAX_Q_ENTRIES = 4096   # kPoolMaxQEntries
+
+
+def pool_scan(qptr, qidx, qval, qn2, nq: int, pool, nrows: int, metric: int, out) -> None:
+    """[nq, nrows] cosine similarity (metric 0) / euclidean distance (1) of
+    nq sorted sparse queries (device CSR) vs the rows of ``pool``
+    (models/similarity.py DevicePool)."""
+    if not 0 < nq <= POOL_MAX_Q:
+        raise ValueError("pool_scan: 1..8 queries per pass")
+    _dev(out, torch.float32, "out")
+    if out.numel() < nq * nrows or qptr.numel() < nq + 1 or nrows > pool.cap_rows:
+        raise ValueError("pool_scan: bad operand shapes")
+    rc = _fn("jb_pool_scan")(_p(qptr), _p(qidx), _p(qval), _p(qn2), nq, _p(pool.r_off),
+                             _p(pool.r_len), _p(pool.r_n2), _p(pool.valid), nrows, _p(pool.p_idx),
+                             _p(pool.p_val), metric, _p(out), _stream())
+    _check(rc, "jb_pool_scan")
+
+
+def pool_append(pack, n: int, nnz: int, base: int, pool) -> None:
+    _dev(pack, torch.uint8, "pack")
+    if pack.numel() < 32 * n + 8 * nnz or base + nnz > pool.cap_entries:
+        raise ValueError("pool_append: bad operand shapes")
+    rc = _fn("jb_pool_append")(_p(pack), n, nnz, base, _p(pool.r_off), _p(pool.r_len),
+                               _p(pool.r_n2), _p(pool.valid), _p(pool.p_idx), _p(pool.p_val),
+                               _stream())
+    _check(rc, "jb_pool_append")
+
 
 _fns: dict = {}
 

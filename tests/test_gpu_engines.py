@@ -294,3 +294,37 @@ def test_direct_topk_sampled_path(case, k):
         np.testing.assert_array_equal(oi[q][:fin.sum()], order[fin])
         np.testing.assert_allclose(od[q][:fin.sum()], ref[fin], rtol=1e-6)
         assert np.all(np.isinf(od[q][fin.sum():]))
+
+
+@pytest.mark.parametrize("euclid", [False, True])
+def test_device_pool_updates_removals_compaction_match_host(euclid):
+    """HBM row pool (csrc/hip/sparse_pool.hip): in-place updates, removals,
+    a compaction, and batched queries (up to 8 per pass) == the host oracle"""
+    from jubatus_amd.models.similarity import InvertedIndex
+    g = InvertedIndex(euclid, dev())
+    c = InvertedIndex(euclid, None)
+    rs = rows(400, seed=5)
+    g.set_rows(range(400), rs)
+    c.set_rows(range(400), rs)
+    upd = rows(120, seed=6)
+    for j, s in enumerate(range(0, 360, 3)):       # rewrite every 3rd row
+        g.set_rows([s], [upd[j]])
+        c.set_rows([s], [upd[j]])
+    for s in (7, 8, 9, 250):
+        g.remove(s)
+        c.remove(s)
+    assert g.pool.end > g.pool.live
+    g.pool.compact()
+    assert g.pool.end == g.pool.live
+    qs = [rs[i] for i in range(11)] + [upd[3]]
+    a = g.query(qs, 400, 10, similar=False)
+    b = c.query(qs, 400, 10, similar=False)
+    for x, y in zip(a, b):
+        np.testing.assert_allclose([d for _, d in x], [d for _, d in y], rtol=1e-4, atol=1e-4)
+    for q in qs[:3]:
+        np.testing.assert_allclose(g.scores(q, 400), c.scores(q, 400), rtol=1e-4, atol=1e-4)
+    ids = [0, 1, 2, 300, 301]
+    a = g.query_slots(ids, 400, 5, similar=True)
+    b = c.query_slots(ids, 400, 5, similar=True)
+    for x, y in zip(a, b):
+        np.testing.assert_allclose([d for _, d in x], [d for _, d in y], rtol=1e-4, atol=1e-4)

@@ -74,7 +74,7 @@ def _sync(dev):
 def bench_recommender(args, dev) -> dict:
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.recommender import Recommender
-    cfg = _config("recommender/euclid_lsh.json")
+    cfg = _config(args.recommender_config)
     rec = Recommender(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]), dev)
     rng = random.Random(1)
     N = args.rows
@@ -89,6 +89,12 @@ def bench_recommender(args, dev) -> dict:
     upd = _lat(lambda: rec.update_row(f"u{next(it) % 5000}", pool[next(it) % 4096]), args.iters)
     q = pool[7]
     sim_d = _lat(lambda: rec.similar_row_from_datum(q, 10), args.iters)
+
+    def upd_query():
+        j = next(it)
+        rec.update_row(f"u{j % 5000}", pool[j % 4096])
+        rec.similar_row_from_datum(pool[(j * 7) % 4096], 10)
+    inter = _lat(upd_query, args.iters)
     sim_i = _lat(lambda: rec.similar_row_from_id("r123", 10), args.iters)
     # batched queries: nq signatures scanned + top-k'd in one launch
     from jubatus_amd.fv_converter.datum import as_datum
@@ -102,16 +108,17 @@ def bench_recommender(args, dev) -> dict:
         rec.index.query(fvs, n, 10, True)
     _sync(dev)
     qps = 256 * reps / (time.perf_counter() - t0)
-    return {"engine": "jubarecommender euclid_lsh (config/recommender/euclid_lsh.json, hash_num 64)",
+    return {"engine": f"jubarecommender {cfg['method']} (config/{args.recommender_config})",
             "rows": N, "bulk_ingest_rows_per_s": round(ingest, 1),
             "update_row_call": upd, "similar_row_from_datum_k10": sim_d,
-            "similar_row_from_id_k10": sim_i, "batched_query_k10_per_s": round(qps, 1)}
+            "similar_row_from_id_k10": sim_i, "batched_query_k10_per_s": round(qps, 1),
+            "interleaved_update_then_query": inter}
 
 
 def bench_anomaly(args, dev) -> dict:
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.anomaly import LOF
-    cfg = _config("anomaly/lof.json")
+    cfg = _config(args.anomaly_config)
     lof = LOF(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]), dev)
     rng = random.Random(2)
     N = args.rows
@@ -125,7 +132,8 @@ def bench_anomaly(args, dev) -> dict:
     it = iter(range(N, 10 ** 9))
     add = _lat(lambda: lof.add(str(next(it)), pool[next(it) % 4096]), args.iters)
     score = _lat(lambda: lof.calc_score(pool[11]), args.iters)
-    return {"engine": "jubaanomaly lof over euclid_lsh (config/anomaly/lof.json, k 10, rnn 30)",
+    return {"engine": f"jubaanomaly {cfg['method']} over {cfg['parameter']['method']} "
+                      f"(config/{args.anomaly_config})",
             "rows": N, "bulk_ingest_rows_per_s": round(ingest, 1), "add_call": add,
             "calc_score_call": score,
             "add_per_s": round(1e6 / add["p50_us"], 1)}
@@ -159,6 +167,8 @@ def main() -> None:
     ap.add_argument("--points", type=int, default=20_000)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu")
+    ap.add_argument("--recommender-config", default="recommender/euclid_lsh.json")
+    ap.add_argument("--anomaly-config", default="anomaly/lof.json")
     args = ap.parse_args()
     dev = _device(args.device)
     for e in args.engines:
