@@ -35,9 +35,9 @@ constexpr int kPoolMaxQEntries = 4096;
 
 __global__ __launch_bounds__(256) void pool_scan_kernel(
     const int64_t* __restrict__ qptr, const int32_t* __restrict__ qidx,
-    const float* __restrict__ qval, const float* __restrict__ qn2, int nq,
+    const float* __restrict__ qval, const double* __restrict__ qn2, int nq,
     const int64_t* __restrict__ r_off, const int32_t* __restrict__ r_len,
-    const float* __restrict__ r_n2, const uint8_t* __restrict__ valid, int64_t nrows,
+    const double* __restrict__ r_n2, const uint8_t* __restrict__ valid, int64_t nrows,
     const int32_t* __restrict__ p_idx, const float* __restrict__ p_val, int metric,
     float* __restrict__ out) {
   __shared__ int32_t s_idx[kPoolMaxQEntries];
@@ -52,9 +52,11 @@ __global__ __launch_bounds__(256) void pool_scan_kernel(
   __syncthreads();
   const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int l16 = threadIdx.x & 15;
-  float dot[kPoolMaxQ];
+  // dot products and norms in double: the euclidean distance of a row to
+  // itself (|q|^2 + |r|^2 - 2 q.r) must cancel to ~0, not to fp32 noise
+  double dot[kPoolMaxQ];
 #pragma unroll
-  for (int q = 0; q < kPoolMaxQ; ++q) dot[q] = 0.f;
+  for (int q = 0; q < kPoolMaxQ; ++q) dot[q] = 0.0;
   const bool live = r < nrows && valid[r];
   if (live) {
     const int64_t off = r_off[r];
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(256) void pool_scan_kernel(
         while (lo <= hi) {
           const int mid = (lo + hi) >> 1;
           const int32_t x = s_idx[mid];
-          if (x == f) { dot[q] += v * s_val[mid]; break; }
+          if (x == f) { dot[q] += (double)v * (double)s_val[mid]; break; }
           if (x < f) lo = mid + 1; else hi = mid - 1;
         }
       }
@@ -78,33 +80,34 @@ __global__ __launch_bounds__(256) void pool_scan_kernel(
 #pragma unroll
   for (int q = 0; q < kPoolMaxQ; ++q) {
     if (q >= nq) break;
-    dot[q] = row16_sum(dot[q]);      // the 16 lanes of a DPP row = one table row
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) dot[q] += __shfl_xor(dot[q], off, 64);  // one 16-lane row
   }
   if (l16 != 0 || r >= nrows) return;
-  const float b2 = live ? r_n2[r] : 0.f;
+  const double b2 = live ? r_n2[r] : 0.0;
   for (int q = 0; q < nq; ++q) {
     float o;
     if (!live) {
       o = metric == 0 ? -INFINITY : INFINITY;
     } else if (metric == 0) {
-      const float den = sqrtf(qn2[q]) * sqrtf(b2);
-      o = den > 0.f ? dot[q] / den : 0.f;
+      const double den = sqrt(qn2[q]) * sqrt(b2);
+      o = den > 0.0 ? (float)(dot[q] / den) : 0.f;
     } else {
-      o = sqrtf(fmaxf(0.f, qn2[q] + b2 - 2.f * dot[q]));
+      o = (float)sqrt(fmax(0.0, qn2[q] + b2 - 2.0 * dot[q]));
     }
     out[(int64_t)q * nrows + r] = o;
   }
 }
 
 // Append rows. `pack` (one H2D copy) = int64 meta[4 n] (slot, run length,
-// squared norm as float bits, run offset within this append) followed by
+// squared norm as double bits, run offset within this append) followed by
 // int32 feature indices[nnz] and float values[nnz]; row i's run lands at
 // pool position base + meta[4 i + 3] and the slot is repointed to it.
 __global__ __launch_bounds__(256) void pool_append_kernel(const uint8_t* __restrict__ pack, int n,
                                                           int64_t nnz, int64_t base,
                                                           int64_t* __restrict__ r_off,
                                                           int32_t* __restrict__ r_len,
-                                                          float* __restrict__ r_n2,
+                                                          double* __restrict__ r_n2,
                                                           uint8_t* __restrict__ valid,
                                                           int32_t* __restrict__ p_idx,
                                                           float* __restrict__ p_val) {
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(256) void pool_append_kernel(const uint8_t* __restr
     const int64_t slot = meta[4 * t];
     r_off[slot] = base + meta[4 * t + 3];
     r_len[slot] = (int32_t)meta[4 * t + 1];
-    r_n2[slot] = __int_as_float((int32_t)meta[4 * t + 2]);
+    r_n2[slot] = __longlong_as_double((long long)meta[4 * t + 2]);
     valid[slot] = 1;
   }
 }
@@ -128,8 +131,8 @@ __global__ __launch_bounds__(256) void pool_append_kernel(const uint8_t* __restr
 }  // namespace jb
 
 extern "C" int jb_pool_scan(const int64_t* qptr, const int32_t* qidx, const float* qval,
-                            const float* qn2, int nq, const int64_t* r_off, const int32_t* r_len,
-                            const float* r_n2, const uint8_t* valid, int64_t nrows,
+                            const double* qn2, int nq, const int64_t* r_off, const int32_t* r_len,
+                            const double* r_n2, const uint8_t* valid, int64_t nrows,
                             const int32_t* p_idx, const float* p_val, int metric, float* out,
                             hipStream_t stream) {
   if (nq <= 0 || nrows <= 0) return 0;
@@ -141,7 +144,7 @@ extern "C" int jb_pool_scan(const int64_t* qptr, const int32_t* qidx, const floa
 }
 
 extern "C" int jb_pool_append(const uint8_t* pack, int n, int64_t nnz, int64_t base,
-                              int64_t* r_off, int32_t* r_len, float* r_n2, uint8_t* valid,
+                              int64_t* r_off, int32_t* r_len, double* r_n2, uint8_t* valid,
                               int32_t* p_idx, float* p_val, hipStream_t stream) {
   const int64_t work = nnz > n ? nnz : n;
   if (work <= 0) return 0;

@@ -12,18 +12,23 @@ For a point p with neighbours N_k(p) at distances d(p, o):
     reach(p, o)    max(kdist(o), d(p, o))
     lrd(p)         1 / mean_o reach(p, o)
     LOF(p)         mean_o lrd(o) / lrd(p)
-kdist / lrd of stored rows are cached and invalidated for the
-``reverse_nearest_neighbor_num`` rows nearest to every inserted/updated
-row. ``ignore_kth_same_point`` skips zero-distance (duplicate) neighbours
-when taking the k-th distance.
+Every stored row keeps its k-neighbour list, kdist and lrd
+(models/lof_state.py; in HBM with csrc/hip/lof.hip on the GPU). An insert
+queries the new row's ``reverse_nearest_neighbor_num`` nearest once, takes
+the row into the lists of those neighbours it is close enough to, and marks
+stale exactly the lrd values that depend on a changed list; the score then
+refreshes only those. ``ignore_kth_same_point`` skips zero-distance
+(duplicate) neighbours when taking the k-th distance.
 """
 from __future__ import annotations
 
-import math
 from typing import Any
+
+import numpy as np
 
 from ..fv_converter.converter import DatumToFvConverter
 from ..fv_converter.datum import as_datum
+from .lof_state import DeviceLofState, HostLofState
 from .row_engine import INDEX_METHODS, LSH_METHODS, RowEngine
 from .rows import datum_to_dicts
 
@@ -46,100 +51,81 @@ class LOF(RowEngine):
         self.outer = method
         super().__init__(inner, dict(p.get("parameter") or {}), converter, device,
                          p.get("unlearner"), p.get("unlearner_parameter"))
-        self._kdist: dict[str, float] = {}
-        self._lrd: dict[str, float] = {}
+        self._st = None          # HostLofState / DeviceLofState (models/lof_state.py)
 
-    # neighbours in *distance* order
-    def _neighbors_fv(self, fv, k: int, exclude: str | None = None) -> list[tuple[str, float]]:
-        res = self.query_fv(fv, k + (1 if exclude else 0), similar=False)
-        return [(r, d) for r, d in res if r != exclude][:k]
+    # ------------------------------------------------------------ state
+    def _state(self):
+        if self._st is None:
+            if self.gpu:
+                self._st = DeviceLofState(self.k, self.ignore_kth_same, self.device)
+            else:
+                self._st = HostLofState(self.k, self.ignore_kth_same)
+        self._st.ensure(self.rows.nslots)
+        return self._st
 
-    def _neighbors_id(self, rid: str, k: int) -> list[tuple[str, float]]:
-        s = self.rows.slot(rid)
-        return self._neighbors_fv(self.rows.fv[s], k, exclude=rid)
+    @staticmethod
+    def _pairs(lst) -> tuple[np.ndarray, np.ndarray]:
+        return (np.asarray([o for o, _ in lst], np.int32),
+                np.asarray([d for _, d in lst], np.float32))
 
-    def _kth(self, nb: list[tuple[str, float]]) -> float:
-        ds = [d for _, d in nb]
-        if self.ignore_kth_same:
-            ds = [d for d in ds if d > 0] or [0.0]
-        return ds[-1] if ds else 0.0
-
-    def kdist(self, rid: str) -> float:
-        v = self._kdist.get(rid)
-        if v is None:
-            v = self._kth(self._neighbors_id(rid, self.k))
-            self._kdist[rid] = v
-        return v
-
-    def _lrd_of(self, nb: list[tuple[str, float]]) -> float:
-        if not nb:
-            return 0.0
-        mean_reach = sum(max(self.kdist(o), d) for o, d in nb) / len(nb)
-        return math.inf if mean_reach <= 0 else 1.0 / mean_reach
-
-    def lrd(self, rid: str) -> float:
-        v = self._lrd.get(rid)
-        if v is None:
-            v = self._lrd_of(self._neighbors_id(rid, self.k))
-            self._lrd[rid] = v
-        return v
-
-    def _knn_many(self, rids: list[str], k: int) -> dict[str, list[tuple[str, float]]]:
-        res = self.query_ids(rids, k + 1, similar=False)
-        return {rid: [(o, d) for o, d in nb if o != rid][:k] for rid, nb in res.items()}
-
-    def _prefetch(self, nb: list[tuple[str, float]]) -> None:
-        """warm the lrd/kdist caches _score(nb) needs with two batched kNN
-        launches (neighbours of the neighbours, then the kdist of theirs)
-        instead of one query per row"""
-        need = [o for o, _ in nb if o not in self._lrd]
-        if not need:
-            return
-        lists = self._knn_many(need, self.k)
-        for o, lo in lists.items():
-            self._kdist.setdefault(o, self._kth(lo))
-        need_k = sorted({x for lo in lists.values() for x, _ in lo if x not in self._kdist})
-        if need_k:
-            for x, lx in self._knn_many(need_k, self.k).items():
-                self._kdist[x] = self._kth(lx)
-        for o, lo in lists.items():
-            self._lrd[o] = self._lrd_of(lo)
-
-    def _score(self, nb: list[tuple[str, float]]) -> float:
-        if not nb:
-            return 1.0
-        self._prefetch(nb)
-        lp = self._lrd_of(nb)
-        lo = [self.lrd(o) for o, _ in nb]
-        mean_lo = sum(lo) / len(lo)
-        if math.isinf(lp):
-            return 1.0 if math.isinf(mean_lo) else 0.0
-        if lp == 0.0:
-            return math.inf
-        if math.isinf(mean_lo):
-            return math.inf
-        return mean_lo / lp
-
-    def _invalidate_near(self, fv, rid: str) -> list[tuple[str, float]]:
-        """drop the cached kdist / lrd the change of ``rid`` can affect;
-        returns its reverse_nearest_neighbor_num nearest rows"""
-        self._kdist.pop(rid, None)
-        self._lrd.pop(rid, None)
-        near = self._neighbors_fv(fv, self.rnn, exclude=rid)
-        for o, _ in near:
-            self._kdist.pop(o, None)
-            self._lrd.pop(o, None)
-        # lrd depends on the neighbours' kdist: drop every cached lrd
-        self._lrd.clear()
-        return near
+    def _score_from(self, ts: np.ndarray, td: np.ndarray, store: int = -1) -> float:
+        """LOF from the k nearest (slot, distance) pairs; rows whose
+        neighbour lists are missing (bulk-loaded, or next to a row that moved)
+        get them from batched kNN queries first"""
+        st = self._state()
+        for _ in range(1 + 2 * self.k):
+            sc, missing = st.score(ts, td, store)
+            if sc is not None:
+                return sc
+            lists = self.query_slot_lists(missing, self.k + 1, similar=False)
+            st.set_lists(missing, [self._pairs(lst) for lst in lists])
+        raise RuntimeError("lof: neighbour lists did not converge")
 
     def _insert(self, rid: str, dicts) -> float:
+        existed = self.rows.slot(rid) is not None
         self._set(rid, dicts)
-        fv = self.rows.fv[self.rows.slot(rid)]
-        near = self._invalidate_near(fv, rid)
+        s = self.rows.slot(rid)
+        st = self._state()
+        if existed:
+            st.moved([s])
+        (near,) = self.query_slot_lists([s], self.rnn + 1, similar=False)
+        cs, cd = self._pairs([(o, d) for o, d in near if o != s][:self.rnn])
+        st.insert(s, cs, cd)
         # the k nearest are the head of the rnn-nearest list (same query,
         # rnn >= k): no second search
-        return self._score(near[:self.k])
+        return self._score_from(cs[:self.k], cd[:self.k], store=s)
+
+    def _remove(self, rid: str, record: bool = True) -> bool:
+        s = self.rows.slot(rid)
+        ok = super()._remove(rid, record)
+        if ok and self._st is not None:
+            self._st.moved([s])
+        return ok
+
+    def _set_many(self, items: list, bump: bool = True, update_weight: bool = True) -> None:
+        super()._set_many(items, bump, update_weight)
+        if self._st is None or not items:
+            return
+        if len(items) > 4096:
+            self._st.clear()         # lists rebuilt on demand
+            return
+        self._st.moved([self.rows.slot(rid) for rid, _ in items])
+
+    def build_lists(self, chunk: int = 1024) -> int:
+        """compute the neighbour list of every stored row that has none
+        (after a bulk load / MIX / model load) with batched kNN queries, so
+        later adds and scores find a warm state; returns the rows built"""
+        with self._lock:
+            st = self._state()
+            n = self.rows.nslots
+            ok = st.ok[:n].cpu().numpy() if hasattr(st.ok, "cpu") else st.ok[:n]
+            ids = self.rows.ids
+            todo = [s for s in np.flatnonzero(ok == 0).tolist() if ids[s] is not None]
+            for i in range(0, len(todo), chunk):
+                part = todo[i:i + chunk]
+                lists = self.query_slot_lists(part, self.k + 1, similar=False)
+                st.set_lists(part, [self._pairs(lst) for lst in lists])
+            return len(todo)
 
     # ---------------------------------------------------------------- API
     def add(self, rid: str, d) -> float:
@@ -162,33 +148,27 @@ class LOF(RowEngine):
 
     def clear_row(self, rid: str) -> bool:
         with self._lock:
-            s = self.rows.slot(rid)
-            if s is None:
-                return False
-            fv = self.rows.fv[s]
-            ok = self._remove(rid)
-            self._invalidate_near(fv, rid)
-            return ok
+            return self._remove(rid)
 
     def calc_score(self, d) -> float:
         with self._lock:
-            return self._score(self._neighbors_fv(self.fv_of(as_datum(d)), self.k))
+            d = as_datum(d)
+            nb = None
+            if self.gpu and hasattr(self.index, "query_direct"):
+                nb = self._query_datum_slots_direct(d, self.k, similar=False)
+            if nb is None:
+                nb = self.query_fv_slots(self.fv_of(d), self.k, similar=False)
+            ids = self.rows.ids
+            ts, td = self._pairs([(o, dd) for o, dd in nb if ids[o] is not None])
+            return self._score_from(ts, td)
 
     def clear(self) -> None:
         super().clear()
-        self._kdist = {}
-        self._lrd = {}
-
-    def put_diff(self, mixed: dict) -> bool:
-        ok = super().put_diff(mixed)
-        self._kdist.clear()
-        self._lrd.clear()
-        return ok
+        self._st = None
 
     def unpack(self, obj: dict) -> None:
+        self._st = None
         super().unpack(obj)
-        self._kdist.clear()
-        self._lrd.clear()
 
     def find_max_int_id(self) -> int:
         m = -1

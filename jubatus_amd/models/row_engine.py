@@ -219,7 +219,8 @@ class RowEngine:
                 out.append((rid, float(score)))
         return out
 
-    def query_fv(self, fv, k: int, similar: bool) -> list[tuple[str, float]]:
+    def query_fv_slots(self, fv, k: int, similar: bool) -> list[tuple[int, float]]:
+        """k nearest stored rows of a feature vector -> [(slot, score)]"""
         with self._lock:
             n = self.rows.nslots
             if n == 0 or k <= 0:
@@ -231,9 +232,13 @@ class RowEngine:
                 rp = np.asarray([0, idx.size], np.int64)
                 r = self.index.query_direct(idx, val, rp, 1, n, k, similar)
                 if r is not None:
-                    return self._results(r[0])
+                    return list(r[0])
             (r,) = self.index.query([fv], n, k, similar)
-            return self._results(r)
+            return list(r)
+
+    def query_fv(self, fv, k: int, similar: bool) -> list[tuple[str, float]]:
+        with self._lock:
+            return self._results(self.query_fv_slots(fv, k, similar))
 
     def query_datum(self, d: Any, k: int, similar: bool) -> list[tuple[str, float]]:
         d = as_datum(d)
@@ -244,7 +249,12 @@ class RowEngine:
         return self.query_fv(self.fv_of(d), k, similar)
 
     def _query_datum_direct(self, d, k: int, similar: bool):
-        """native hashing of the datum + the single-shot LSH query kernel"""
+        r = self._query_datum_slots_direct(d, k, similar)
+        return None if r is None else self._results(r)
+
+    def _query_datum_slots_direct(self, d, k: int, similar: bool):
+        """native hashing of the datum + the single-shot LSH query kernel
+        -> [(slot, score)] or None (not eligible)"""
         h = self._hasher()
         if h is None:
             return None
@@ -266,7 +276,7 @@ class RowEngine:
             r = self.index.query_direct(idx, val, rp, 1, nrows, k, similar)
             if r is None:
                 return None
-            return self._results(r[0])
+            return list(r[0])
 
     def query_id(self, rid: str, k: int, similar: bool) -> list[tuple[str, float]]:
         with self._lock:
@@ -279,14 +289,12 @@ class RowEngine:
                     return self._results(r[0])
             return self.query_fv(self.rows.fv[s], k, similar)
 
-    def query_ids(self, rids: list[str], k: int, similar: bool) -> dict[str, list[tuple[str, float]]]:
-        """batched query_id (every row's neighbours, itself included): one
-        launch for the LSH family (stored signatures), per-row otherwise"""
+    def query_slot_lists(self, slots: list[int], k: int, similar: bool) -> list[list[tuple[int, float]]]:
+        """batched query by stored row (each row's neighbours, itself
+        included) -> per row [(slot, score)]: stored signatures / pool rows,
+        QUERY_MAX queries per launch on the GPU"""
         with self._lock:
             n = self.rows.nslots
-            slots = [self.rows.slot(r) for r in rids]
-            if any(s is None for s in slots):
-                raise KeyError("row not found")
             res = None
             if hasattr(self.index, "query_slots"):
                 from ..ops import hip
@@ -302,6 +310,16 @@ class RowEngine:
                     res = self.index.query_slots(slots, n, k, similar)
             if res is None:
                 res = self.index.query([self.rows.fv[s] for s in slots], n, k, similar)
+            ids = self.rows.ids
+            return [[(int(o), float(d)) for o, d in r if ids[o] is not None] for r in res]
+
+    def query_ids(self, rids: list[str], k: int, similar: bool) -> dict[str, list[tuple[str, float]]]:
+        """batched query_id (every row's neighbours, itself included)"""
+        with self._lock:
+            slots = [self.rows.slot(r) for r in rids]
+            if any(s is None for s in slots):
+                raise KeyError("row not found")
+            res = self.query_slot_lists(slots, k, similar)
             return {rid: self._results(r) for rid, r in zip(rids, res)}
 
     # ------------------------------------------------------------ MIX

@@ -421,8 +421,10 @@ def normalize_csr(row_ptr: np.ndarray, idx: np.ndarray, val: np.ndarray):
         val = np.add.reduceat(val, starts)
         idx, rows = idx[starts], rows[starts]
     lens = np.bincount(rows, minlength=n).astype(np.int64)
-    n2 = np.bincount(rows, weights=val * val, minlength=n).astype(np.float32)
-    return lens, idx.astype(np.int32), val.astype(np.float32), n2
+    val32 = val.astype(np.float32)
+    v = val32.astype(np.float64)           # the stored values, squared exactly
+    n2 = np.bincount(rows, weights=v * v, minlength=n)
+    return lens, idx.astype(np.int32), val32, n2
 
 
 def _rows_to_csr(rows) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
@@ -439,7 +441,8 @@ class DevicePool:
     """HBM row pool of the device inverted index (csrc/hip/sparse_pool.hip):
     append-only runs of (feature, value) plus per-slot offset / length /
     squared norm / valid. The host keeps only the slots' offsets and lengths
-    (no copy of the data) to size appends and compact the pool."""
+    (no copy of the data) to size appends and compact the pool. Squared
+    norms are float64 (the euclidean self-distance must cancel to ~0)."""
 
     def __init__(self, device):
         self.device = device
@@ -468,7 +471,7 @@ class DevicePool:
             return t
         self.r_off = grow(getattr(self, "r_off", None), torch.int64)
         self.r_len = grow(getattr(self, "r_len", None), torch.int32)
-        self.r_n2 = grow(getattr(self, "r_n2", None), torch.float32)
+        self.r_n2 = grow(getattr(self, "r_n2", None), torch.float64)
         self.valid = grow(getattr(self, "valid", None), torch.uint8)
         off_h = np.zeros(cap, dtype=np.int64)
         len_h = np.zeros(cap, dtype=np.int64)
@@ -529,7 +532,7 @@ class DevicePool:
         meta = np.empty((n, 4), dtype=np.int64)
         meta[:, 0] = slots
         meta[:, 1] = lens
-        meta[:, 2] = n2.astype(np.float32).view(np.int32).astype(np.int64)
+        meta[:, 2] = np.asarray(n2, dtype=np.float64).view(np.int64)
         meta[:, 3] = run
         pack = np.concatenate([meta.reshape(-1).view(np.uint8), idx.astype(np.int32).view(np.uint8),
                                val.astype(np.float32).view(np.uint8)])
@@ -632,7 +635,8 @@ class InvertedIndex:
         if qi.size == 0:
             qi, qv = np.zeros(1, np.int32), np.zeros(1, np.float32)
         return (torch.from_numpy(qptr).to(d), torch.from_numpy(qi).to(d),
-                torch.from_numpy(qv).to(d), torch.from_numpy(qn2).to(d), int(qptr[-1]))
+                torch.from_numpy(qv).to(d), torch.from_numpy(np.asarray(qn2, np.float64)).to(d),
+                int(qptr[-1]))
 
     def _scan(self, q, nq: int, nrows: int):
         import torch
@@ -659,7 +663,13 @@ class InvertedIndex:
 
     def _topk(self, sc, nq: int, nrows: int, k: int, similar: bool):
         from ..ops import hip
-        d, i = hip.topk_scores(sc, nq, nrows, k, flip=not self.euclid)
+        if k <= hip.TOPK_MAX_K:
+            d, i = hip.topk_scores(sc, nq, nrows, k, flip=not self.euclid)
+        else:       # wider than the fused top-k: torch.topk on the score matrix
+            import torch
+            m = sc.view(nq, nrows)
+            dist = m if self.euclid else (1.0 - m).nan_to_num(posinf=math.inf)
+            d, i = torch.topk(dist, min(k, nrows), dim=1, largest=False, sorted=True)
         out = _pairs(d.cpu().numpy(), i.cpu().numpy())
         if similar:
             out = [[(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in r] for r in out]
@@ -691,8 +701,7 @@ class InvertedIndex:
         return out
 
     def query(self, rows: list, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
-        from ..ops import hip
-        if self.gpu and nrows > 0 and 0 < k <= hip.TOPK_MAX_K:
+        if self.gpu and nrows > 0 and k > 0:
             return self._query_batches(lambda a, b: self._queries_device(rows[a:b]), len(rows),
                                        nrows, k, similar)
         res = []
@@ -709,9 +718,10 @@ class InvertedIndex:
     def query_slots(self, slots, nrows: int, k: int, similar: bool) -> list[list[tuple[int, float]]]:
         """queries that are stored rows (similar_row_from_id, LOF neighbours
         of stored points): taken from the pool on the device"""
-        from ..ops import hip
         slots = list(slots)
-        if self.gpu and nrows > 0 and 0 < k <= hip.TOPK_MAX_K:
+        if self.gpu:
+            if nrows <= 0 or k <= 0:
+                return [[] for _ in slots]
             return self._query_batches(lambda a, b: self.pool.query_csr(slots[a:b]), len(slots),
                                        nrows, k, similar)
         return self.query([self.rows.get(int(s), (np.zeros(0, np.int32), np.zeros(0, np.float32)))

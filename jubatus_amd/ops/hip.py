@@ -72,6 +72,15 @@ _SIGS = {
                      _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p],
     "jb_pool_append": [_c_void_p, _i32, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _c_void_p],
+    "jb_lof_insert": [_i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
+                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_lof_mark": [_i64, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                    _c_void_p],
+    "jb_lof_set_lists": [_i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p,
+                         _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                         _c_void_p],
+    "jb_lof_score": [_c_void_p, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                     _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -215,6 +224,55 @@ def pool_append(pack, n: int, nnz: int, base: int, pool) -> None:
                                _p(pool.r_n2), _p(pool.valid), _p(pool.p_idx), _p(pool.p_val),
                                _stream())
     _check(rc, "jb_pool_append")
+
+
+def _lof_check(st, *slots) -> None:
+    for s in slots:
+        if not 0 <= s < st.cap:
+            raise ValueError("lof: slot out of range")
+
+
+def lof_insert(p: int, cs, cd, nc: int, st) -> None:
+    """insert slot p with its nc nearest candidates (device int32 / fp32,
+    ascending) into the LOF lists of ``st`` (models/lof_state.py
+    DeviceLofState); writes the changed rows to st._changed"""
+    _lof_check(st, p)
+    if cs.numel() < nc or cd.numel() < nc:
+        raise ValueError("lof_insert: bad operand shapes")
+    rc = _fn("jb_lof_insert")(p, _p(cs), _p(cd), nc, st.k, int(st.ignore_same), _p(st.nb_slot),
+                              _p(st.nb_dist), _p(st.kdist), _p(st.ok), _p(st.lrd_ok),
+                              _p(st._changed), _p(st._nchanged), _stream())
+    _check(rc, "jb_lof_insert")
+
+
+def lof_mark(st, clear_ok: bool) -> None:
+    """rows listing one of st._changed[:st._nchanged]: lrd stale (and list
+    invalid when clear_ok)"""
+    rc = _fn("jb_lof_mark")(st.cap, st.k, _p(st.nb_slot), _p(st._changed), _p(st._nchanged),
+                            int(clear_ok), _p(st.ok), _p(st.lrd_ok), _stream())
+    _check(rc, "jb_lof_mark")
+
+
+def lof_set_lists(n: int, slots, cs, cd, kk: int, st) -> None:
+    if slots.numel() < n or cs.numel() < n * kk or cd.numel() < n * kk:
+        raise ValueError("lof_set_lists: bad operand shapes")
+    rc = _fn("jb_lof_set_lists")(n, _p(slots), _p(cs), _p(cd), kk, st.k, int(st.ignore_same),
+                                 _p(st.nb_slot), _p(st.nb_dist), _p(st.kdist), _p(st.ok),
+                                 _p(st.lrd_ok), _p(st._changed), _p(st._nchanged), _stream())
+    _check(rc, "jb_lof_set_lists")
+
+
+def lof_score(ts, td, nt: int, st, store: int, out: "HostBuffer", max_missing: int) -> None:
+    """LOF of one point from its nt nearest (device slot / distance) into
+    ``out`` = [status, score, lrd, nmissing, missing...] (pinned, int32)"""
+    if nt > 64 or ts.numel() < nt or td.numel() < nt:
+        raise ValueError("lof_score: 1..64 targets")
+    if store >= st.cap or out.nbytes < 4 * (4 + max_missing):
+        raise ValueError("lof_score: bad operand shapes")
+    rc = _fn("jb_lof_score")(_p(ts), _p(td), nt, st.k, _p(st.nb_slot), _p(st.nb_dist),
+                             _p(st.kdist), _p(st.ok), _p(st.lrd), _p(st.lrd_ok), store, out.ptr,
+                             max_missing, _stream())
+    _check(rc, "jb_lof_score")
 
 
 _fns: dict = {}

@@ -75,7 +75,7 @@ def bench_recommender(args, dev) -> dict:
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.recommender import Recommender
     cfg = _config(args.recommender_config)
-    rec = Recommender(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]), dev)
+    rec = Recommender(cfg["method"], cfg.get("parameter", {}), DatumToFvConverter(cfg["converter"]), dev)
     rng = random.Random(1)
     N = args.rows
     pool = [_datum(rng) for _ in range(4096)]
@@ -116,26 +116,37 @@ def bench_recommender(args, dev) -> dict:
 
 
 def bench_anomaly(args, dev) -> dict:
+    """1M distinct rows (16 clusters + noise) bulk-loaded, then every row's
+    neighbour list built in batched kNN launches (the state a model fed by
+    add() has); add = one rnn query + the device list insert / staleness
+    mark / fused lrd+LOF score"""
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.anomaly import LOF
     cfg = _config(args.anomaly_config)
     lof = LOF(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]), dev)
     rng = random.Random(2)
     N = args.rows
-    pool = [_datum(rng) for _ in range(4096)]
     t0 = time.perf_counter()
     B = 65536
     for b in range(0, N, B):
-        lof.set_rows([(str(i), pool[i % 4096]) for i in range(b, min(N, b + B))])
+        lof.set_rows([(str(i), _datum(rng)) for i in range(b, min(N, b + B))])
     _sync(dev)
     ingest = N / (time.perf_counter() - t0)
+    pool = [_datum(rng) for _ in range(4096)]
     it = iter(range(N, 10 ** 9))
+    cold = _lat(lambda: lof.add(str(next(it)), pool[next(it) % 4096]), args.iters)
+    t0 = time.perf_counter()
+    built = lof.build_lists()
+    _sync(dev)
+    build_s = time.perf_counter() - t0
     add = _lat(lambda: lof.add(str(next(it)), pool[next(it) % 4096]), args.iters)
     score = _lat(lambda: lof.calc_score(pool[11]), args.iters)
+    score_new = _lat(lambda: lof.calc_score(_datum(rng)), args.iters)
     return {"engine": f"jubaanomaly {cfg['method']} over {cfg['parameter']['method']} "
                       f"(config/{args.anomaly_config})",
-            "rows": N, "bulk_ingest_rows_per_s": round(ingest, 1), "add_call": add,
-            "calc_score_call": score,
+            "rows": N, "bulk_ingest_rows_per_s": round(ingest, 1),
+            "add_call_cold_lists": cold, "list_build_s": round(build_s, 2), "lists_built": built,
+            "add_call": add, "calc_score_call": score, "calc_score_new_point": score_new,
             "add_per_s": round(1e6 / add["p50_us"], 1)}
 
 
