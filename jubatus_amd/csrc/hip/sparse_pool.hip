@@ -15,8 +15,9 @@
 // host mirror is rebuilt on a write: an update is one small H2D copy plus
 // pool_append_kernel.
 //
-// Query: pool_scan_kernel scores up to kMaxQueries queries in ONE pass over
-// the pool (the queries sit in LDS; each 16-lane group walks one row's run
+// Query: pool_scan_kernel scores up to kPoolMaxQ queries in ONE pass over
+// the pool (the queries sit in LDS - uploaded CSR, or, for queries that are
+// stored rows, copied from the pool by slot; each 16-lane group walks one row's run
 // with coalesced loads and binary-searches every entry in each query; the
 // group sums with DPP), writing [nq][nrows] scores for the fused top-k
 // (topk.hip). For text-like data (n-gram features that most rows share) a
@@ -35,7 +36,8 @@ constexpr int kPoolMaxQEntries = 4096;
 
 __global__ __launch_bounds__(256) void pool_scan_kernel(
     const int64_t* __restrict__ qptr, const int32_t* __restrict__ qidx,
-    const float* __restrict__ qval, const double* __restrict__ qn2, int nq,
+    const float* __restrict__ qval, const double* __restrict__ qn2_in,
+    const int32_t* __restrict__ qslots, int nq,
     const int64_t* __restrict__ r_off, const int32_t* __restrict__ r_len,
     const double* __restrict__ r_n2, const uint8_t* __restrict__ valid, int64_t nrows,
     const int32_t* __restrict__ p_idx, const float* __restrict__ p_val, int metric,
@@ -43,13 +45,38 @@ __global__ __launch_bounds__(256) void pool_scan_kernel(
   __shared__ int32_t s_idx[kPoolMaxQEntries];
   __shared__ float s_val[kPoolMaxQEntries];
   __shared__ int s_ptr[kPoolMaxQ + 1];
-  if (threadIdx.x <= (unsigned)nq) s_ptr[threadIdx.x] = (int)(qptr[threadIdx.x] - qptr[0]);
-  const int qtot = (int)(qptr[nq] - qptr[0]);
-  for (int i = threadIdx.x; i < qtot; i += blockDim.x) {
-    s_idx[i] = qidx[qptr[0] + i];
-    s_val[i] = qval[qptr[0] + i];
+  __shared__ double s_qn2[kPoolMaxQ];
+  if (qslots) {
+    // queries are stored rows: their runs come straight from the pool
+    if (threadIdx.x == 0) {
+      int acc = 0;
+      for (int q = 0; q < nq; ++q) {
+        s_ptr[q] = acc;
+        acc += r_len[qslots[q]];
+      }
+      s_ptr[nq] = acc;
+    }
+    if (threadIdx.x < (unsigned)nq) s_qn2[threadIdx.x] = r_n2[qslots[threadIdx.x]];
+    __syncthreads();
+    for (int q = 0; q < nq; ++q) {
+      const int64_t o = r_off[qslots[q]];
+      const int b = s_ptr[q], len = s_ptr[q + 1] - b;
+      for (int i = threadIdx.x; i < len; i += blockDim.x) {
+        s_idx[b + i] = p_idx[o + i];
+        s_val[b + i] = p_val[o + i];
+      }
+    }
+  } else {
+    if (threadIdx.x <= (unsigned)nq) s_ptr[threadIdx.x] = (int)(qptr[threadIdx.x] - qptr[0]);
+    if (threadIdx.x < (unsigned)nq) s_qn2[threadIdx.x] = qn2_in[threadIdx.x];
+    const int qtot = (int)(qptr[nq] - qptr[0]);
+    for (int i = threadIdx.x; i < qtot; i += blockDim.x) {
+      s_idx[i] = qidx[qptr[0] + i];
+      s_val[i] = qval[qptr[0] + i];
+    }
   }
   __syncthreads();
+  const double* qn2 = s_qn2;
   const int64_t r = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int l16 = threadIdx.x & 15;
   // dot products and norms in double: the euclidean distance of a row to
@@ -131,7 +158,8 @@ __global__ __launch_bounds__(256) void pool_append_kernel(const uint8_t* __restr
 }  // namespace jb
 
 extern "C" int jb_pool_scan(const int64_t* qptr, const int32_t* qidx, const float* qval,
-                            const double* qn2, int nq, const int64_t* r_off, const int32_t* r_len,
+                            const double* qn2, const int32_t* qslots, int nq,
+                            const int64_t* r_off, const int32_t* r_len,
                             const double* r_n2, const uint8_t* valid, int64_t nrows,
                             const int32_t* p_idx, const float* p_val, int metric, float* out,
                             hipStream_t stream) {
@@ -139,7 +167,7 @@ extern "C" int jb_pool_scan(const int64_t* qptr, const int32_t* qidx, const floa
   if (nq > jb::kPoolMaxQ) return -2;
   const unsigned blocks = (unsigned)((nrows + 15) / 16);
   hipLaunchKernelGGL(jb::pool_scan_kernel, dim3(blocks), dim3(256), 0, stream, qptr, qidx, qval,
-                     qn2, nq, r_off, r_len, r_n2, valid, nrows, p_idx, p_val, metric, out);
+                     qn2, qslots, nq, r_off, r_len, r_n2, valid, nrows, p_idx, p_val, metric, out);
   return (int)hipGetLastError();
 }
 

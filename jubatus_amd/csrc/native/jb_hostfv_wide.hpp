@@ -1,0 +1,294 @@
+// Host-native converter for the wide rule set: string rules with the str /
+// space / ngram splitters, bin / tf / log_tf sample weights and bin / idf /
+// bm25 global weights (document frequencies in the WeightManager's dense
+// int64 arrays, updated in place), num rules num / log, and combination rules
+// add / mul over the finished feature list. Output order and values equal the
+// Python converter (jubatus_amd/fv_converter/converter.py `_convert`): per
+// string value and rule the distinct tokens in first-occurrence order, then
+// the num features, then for every combination rule the pairs i < j of that
+// list. Values are computed in double and stored as float, as the Python path
+// does. Rule tables come from fv_converter/gpu_path.py WideRuleTable; the GPU
+// twin is csrc/hip/fv_wide.hip.
+#pragma once
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "jb_hash.hpp"
+#include "jb_hostfv.hpp"
+#include "jb_msgpack.hpp"
+
+namespace jb {
+
+// string rule value_kind bit fields (fv_converter/gpu_path.py)
+constexpr int kSplitStr = 0, kSplitNgram = 1, kSplitSpace = 2;
+constexpr int kSwBin = 0, kSwTf = 1, kSwLogTf = 2;
+constexpr int kGwBin = 0, kGwIdf = 1, kGwBm25 = 2;
+
+struct WideName {        // a feature name as up to four byte segments
+  const uint8_t* p[4];
+  uint32_t n[4];
+  int k;
+  uint32_t len() const { uint32_t t = 0; for (int i = 0; i < k; ++i) t += n[i]; return t; }
+  uint8_t at(uint32_t pos) const {
+    for (int i = 0; i < k; ++i) {
+      if (pos < n[i]) return p[i][pos];
+      pos -= n[i];
+    }
+    return 0;
+  }
+  uint64_t fnv(uint64_t h) const {
+    for (int i = 0; i < k; ++i) h = fnv_bytes(h, p[i], n[i]);
+    return h;
+  }
+};
+
+struct WideFeat {
+  uint64_t h;       // FNV-1a/64 state of the full name
+  int32_t idx;
+  double w;
+  int gw;
+  WideName name;
+};
+
+class HostFvWide {
+ public:
+  HostFvWide(const uint8_t* srules, int n_srules, const uint8_t* nrules, int n_nrules,
+             const uint8_t* crules, int n_crules, const uint8_t* blob, size_t blob_len, uint64_t H)
+      : s_(n_srules), n_(n_nrules), c_(2 * n_crules), blob_(blob, blob + blob_len), H_(H) {
+    if (n_srules) memcpy(s_.data(), srules, sizeof(HostRule) * n_srules);
+    if (n_nrules) memcpy(n_.data(), nrules, sizeof(HostRule) * n_nrules);
+    if (n_crules) memcpy(c_.data(), crules, sizeof(HostRule) * 2 * n_crules);
+    for (const HostRule& r : s_)
+      if ((r.value_kind >> 8 & 15) != kGwBin) global_ = true;
+  }
+
+  // WeightManager storage: df[H], diff[H] (int64) and counts[4] =
+  // [doc_count, total_len, diff_docs, diff_len]
+  void set_weights(int64_t* df, int64_t* diff, int64_t* counts) {
+    df_ = df; diff_ = diff; counts_ = counts;
+  }
+  bool needs_weights() const { return global_; }
+
+  // Document-statistics journal of one hash call: on an error the caller
+  // rolls back every update it made (a capacity retry re-runs the batch).
+  void begin() { journal_.clear(); jdocs_ = jlen_ = 0; }
+  void rollback() {
+    for (int32_t i : journal_) { df_[i] -= 1; if (diff_) diff_[i] -= 1; }
+    counts_[0] -= jdocs_; counts_[2] -= jdocs_;
+    counts_[1] -= jlen_; counts_[3] -= jlen_;
+    begin();
+  }
+
+  // One body = msgpack list<datum>; same contract as HostFvHasher::hash_body.
+  int hash_body(const uint8_t* p, size_t len, int32_t* idx, float* val, int64_t* row_ptr,
+                int64_t max_samples, int64_t max_slots, int64_t* n, int64_t* slots,
+                bool update) {
+    if (global_ && (!df_ || !counts_)) return 1;
+    Cursor c{p, p + len};
+    uint32_t cnt;
+    if (!c.array(&cnt)) return 1;
+    for (uint32_t i = 0; i < cnt; ++i) {
+      if (*n >= max_samples) return 2;
+      int rc = datum(c, idx, val, max_slots, slots, update);
+      if (rc) return rc;
+      row_ptr[++*n] = *slots;
+    }
+    return 0;
+  }
+
+ private:
+  bool match_key(const HostRule& r, const uint8_t* k, uint32_t kn) const {
+    if (r.match_kind == 0) return true;
+    const uint8_t* m = blob_.data() + r.match_off;
+    const uint32_t mn = (uint32_t)r.match_len;
+    if (r.match_kind == 3 && kn != mn) return false;
+    if (kn < mn) return false;
+    const uint8_t* base = (r.match_kind == 2) ? (k + kn - mn) : k;
+    return memcmp(base, m, mn) == 0;
+  }
+
+  bool match_name(const HostRule& r, const WideName& nm) const {
+    if (r.match_kind == 0) return true;
+    const uint8_t* m = blob_.data() + r.match_off;
+    const uint32_t mn = (uint32_t)r.match_len, L = nm.len();
+    if (r.match_kind == 3 && L != mn) return false;
+    if (L < mn) return false;
+    const uint32_t base = (r.match_kind == 2) ? L - mn : 0;
+    for (uint32_t i = 0; i < mn; ++i)
+      if (nm.at(base + i) != m[i]) return false;
+    return true;
+  }
+
+  // tokens of one string value for a splitter -> tok_ (offset, length) pairs
+  void split(int kind, int ngram, const uint8_t* v, uint32_t vn) {
+    tok_.clear();
+    if (kind == kSplitStr) {
+      tok_.push_back({0, vn});
+    } else if (kind == kSplitSpace) {
+      uint32_t s = 0;
+      for (uint32_t i = 0; i <= vn; ++i) {
+        if (i == vn || v[i] == ' ') {
+          if (i > s) tok_.push_back({s, i - s});
+          s = i + 1;
+        }
+      }
+    } else {                              // ngram over code points
+      cp_.clear();
+      for (uint32_t i = 0; i < vn; ++i)
+        if ((v[i] & 0xC0) != 0x80) cp_.push_back(i);
+      const int ncp = (int)cp_.size();
+      cp_.push_back(vn);
+      for (int i = 0; i + ngram <= ncp; ++i) tok_.push_back({cp_[i], cp_[i + ngram] - cp_[i]});
+    }
+  }
+
+  int datum(Cursor& c, int32_t* idx, float* val, int64_t max_slots, int64_t* slots, bool update) {
+    uint32_t top, ns, nn;
+    if (!c.array(&top) || top < 2) return 1;
+    feats_.clear();
+    if (!c.array(&ns)) return 1;
+    for (uint32_t i = 0; i < ns; ++i) {
+      uint32_t two; const uint8_t *k, *v; uint32_t kn, vn;
+      if (!c.array(&two) || two != 2 || !c.raw(&k, &kn) || !c.raw(&v, &vn)) return 1;
+      uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
+      hk = fnv_bytes(hk, (const uint8_t*)"$", 1);
+      for (const HostRule& r : s_) {
+        if (!match_key(r, k, kn)) continue;
+        const int sp = r.value_kind & 15, sw = r.value_kind >> 4 & 15, gw = r.value_kind >> 8 & 15;
+        split(sp, r.pad, v, vn);
+        // distinct tokens in first-occurrence order with their counts
+        uniq_.clear();
+        if (tok_.size() <= 32) {
+          for (const auto& t : tok_) {
+            bool found = false;
+            for (auto& u : uniq_) {
+              if (u.len == t.len && memcmp(v + u.off, v + t.off, t.len) == 0) { ++u.cnt; found = true; break; }
+            }
+            if (!found) uniq_.push_back({t.off, t.len, 1});
+          }
+        } else {                          // long text: hash map over the token bytes
+          seen_.clear();
+          for (const auto& t : tok_) {
+            auto it = seen_.emplace(std::string_view((const char*)v + t.off, t.len), uniq_.size());
+            if (it.second) uniq_.push_back({t.off, t.len, 1});
+            else ++uniq_[it.first->second].cnt;
+          }
+        }
+        const uint8_t* suf = blob_.data() + r.suffix_off;
+        for (const auto& u : uniq_) {
+          WideFeat f;
+          f.h = fnv_bytes(fnv_bytes(hk, v + u.off, u.len), suf, (size_t)r.suffix_len);
+          f.idx = (int32_t)hash_to_index(f.h, H_);
+          f.w = sw == kSwBin ? 1.0 : sw == kSwTf ? (double)u.cnt : log(1.0 + (double)u.cnt);
+          f.gw = gw;
+          f.name = WideName{{k, (const uint8_t*)"$", v + u.off, suf}, {kn, 1, u.len, (uint32_t)r.suffix_len}, 4};
+          feats_.push_back(f);
+        }
+      }
+    }
+    if (global_) weigh(update);
+    if (!c.array(&nn)) return 1;
+    for (uint32_t i = 0; i < nn; ++i) {
+      uint32_t two; const uint8_t* k; uint32_t kn; double x;
+      if (!c.array(&two) || two != 2 || !c.raw(&k, &kn) || !c.number(&x)) return 1;
+      const uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
+      for (const HostRule& r : n_) {
+        if (!match_key(r, k, kn)) continue;
+        const uint8_t* suf = blob_.data() + r.suffix_off;
+        WideFeat f;
+        f.h = fnv_bytes(hk, suf, (size_t)r.suffix_len);
+        f.idx = (int32_t)hash_to_index(f.h, H_);
+        f.w = r.value_kind == 1 ? log(x > 1.0 ? x : 1.0) : x;
+        f.gw = kGwBin;
+        f.name = WideName{{k, suf, nullptr, nullptr}, {kn, (uint32_t)r.suffix_len, 0, 0}, 2};
+        feats_.push_back(f);
+      }
+    }
+    for (uint32_t i = 2; i < top; ++i)   // binary values carry no feature on this path
+      if (!c.skip()) return 1;
+    const size_t nb = feats_.size();
+    for (size_t i = 0; i < nb; ++i) {
+      if (*slots >= max_slots) return 2;
+      idx[*slots] = feats_[i].idx;
+      val[*slots] = (float)feats_[i].w;
+      ++*slots;
+    }
+    for (size_t r = 0; r + 1 < c_.size(); r += 2) {
+      const HostRule& L = c_[r];
+      const HostRule& R = c_[r + 1];
+      const uint8_t* suf = blob_.data() + L.suffix_off;
+      for (size_t i = 0; i < nb; ++i) {
+        if (!match_name(L, feats_[i].name)) continue;
+        const uint64_t hi = fnv_bytes(feats_[i].h, (const uint8_t*)"&", 1);
+        for (size_t j = i + 1; j < nb; ++j) {
+          if (!match_name(R, feats_[j].name)) continue;
+          if (*slots >= max_slots) return 2;
+          const uint64_t h = fnv_bytes(feats_[j].name.fnv(hi), suf, (size_t)L.suffix_len);
+          idx[*slots] = (int32_t)hash_to_index(h, H_);
+          const double a = feats_[i].w, b = feats_[j].w;
+          val[*slots] = (float)(L.value_kind == 1 ? a * b : a + b);
+          ++*slots;
+        }
+      }
+    }
+    return 0;
+  }
+
+  // update the document statistics with this datum (when asked), then apply
+  // the idf / bm25 weights (converter.py _convert)
+  void weigh(bool update) {
+    gidx_.clear();
+    for (const auto& f : feats_)
+      if (f.gw != kGwBin) gidx_.push_back(f.idx);
+    const int64_t dl = (int64_t)gidx_.size();
+    if (update) {
+      counts_[0] += 1; counts_[2] += 1;
+      counts_[1] += dl; counts_[3] += dl;
+      jdocs_ += 1; jlen_ += dl;
+      std::sort(gidx_.begin(), gidx_.end());
+      for (size_t i = 0; i < gidx_.size(); ++i) {
+        if (i && gidx_[i] == gidx_[i - 1]) continue;
+        df_[gidx_[i]] += 1;
+        if (diff_) diff_[gidx_[i]] += 1;
+        journal_.push_back(gidx_[i]);
+      }
+    }
+    const int64_t nd = counts_[0];
+    const double avg = nd ? (double)counts_[1] / (double)nd : 1.0;
+    for (auto& f : feats_) {
+      if (f.gw == kGwBin) continue;
+      const int64_t df = df_[f.idx];
+      const double idf = (df > 0 && nd > 0) ? log((double)nd / (double)df) : 0.0;
+      if (f.gw == kGwIdf) {
+        f.w *= idf;
+      } else {
+        const double k1 = 1.2, b = 0.75;
+        f.w = idf * (f.w * (k1 + 1)) / (f.w + k1 * (1 - b + b * (double)dl / (avg > 1e-9 ? avg : 1e-9)));
+      }
+    }
+  }
+
+  struct Tok { uint32_t off, len; };
+  struct Uniq { uint32_t off, len; int cnt; };
+  std::vector<HostRule> s_, n_, c_;
+  std::vector<uint8_t> blob_;
+  uint64_t H_;
+  bool global_ = false;
+  int64_t *df_ = nullptr, *diff_ = nullptr, *counts_ = nullptr;
+  std::vector<WideFeat> feats_;
+  std::vector<Tok> tok_;
+  std::vector<Uniq> uniq_;
+  std::vector<uint32_t> cp_;
+  std::unordered_map<std::string_view, size_t> seen_;
+  std::vector<int32_t> gidx_;
+  std::vector<int32_t> journal_;
+  int64_t jdocs_ = 0, jlen_ = 0;
+};
+
+}  // namespace jb

@@ -5,6 +5,7 @@
 
 #include "jb_hash.hpp"
 #include "jb_hostfv.hpp"
+#include "jb_hostfv_wide.hpp"
 #include "jb_pack.hpp"
 #include "jb_rpc.hpp"
 
@@ -250,9 +251,42 @@ jb::HostFvHasher* make_hasher(py::buffer srules, int n_srules, py::buffer nrules
                               (const uint8_t*)b.ptr, (size_t)(b.size * b.itemsize), H);
 }
 
+jb::HostFvWide* make_wide(py::buffer srules, int n_srules, py::buffer nrules, int n_nrules,
+                          py::buffer crules, int n_crules, py::buffer blob, uint64_t H) {
+  py::buffer_info s = srules.request(), n = nrules.request(), c = crules.request(),
+                  b = blob.request();
+  if ((size_t)s.size * s.itemsize < sizeof(jb::HostRule) * (size_t)n_srules ||
+      (size_t)n.size * n.itemsize < sizeof(jb::HostRule) * (size_t)n_nrules ||
+      (size_t)c.size * c.itemsize < sizeof(jb::HostRule) * 2 * (size_t)n_crules)
+    throw std::invalid_argument("rule table shorter than its rule count");
+  return new jb::HostFvWide((const uint8_t*)s.ptr, n_srules, (const uint8_t*)n.ptr, n_nrules,
+                            (const uint8_t*)c.ptr, n_crules, (const uint8_t*)b.ptr,
+                            (size_t)(b.size * b.itemsize), H);
+}
+
+py::tuple wide_hash(jb::HostFvWide& h, py::list reqs, uintptr_t idx, uintptr_t val,
+                    uintptr_t row_ptr, int64_t max_samples, int64_t max_slots, bool update) {
+  int64_t n = 0, slots = 0;
+  int64_t* rp = (int64_t*)row_ptr;
+  rp[0] = 0;
+  h.begin();
+  for (auto item : reqs) {
+    py::buffer b = py::reinterpret_borrow<py::buffer>(item);
+    py::buffer_info bi = b.request();
+    int rc = h.hash_body((const uint8_t*)bi.ptr, (size_t)(bi.size * bi.itemsize), (int32_t*)idx,
+                         (float*)val, rp, max_samples, max_slots, &n, &slots, update);
+    if (rc) {
+      if (update && h.needs_weights()) h.rollback();   // no partial statistics
+      return py::make_tuple(n, slots, rc);
+    }
+  }
+  return py::make_tuple(n, slots, 0);
+}
+
 // -> (n_samples, n_slots, error): 0 ok, 1 malformed request, 2 capacity
 py::tuple hasher_hash(const jb::HostFvHasher& h, py::list reqs, uintptr_t idx, uintptr_t val,
-                      uintptr_t row_ptr, int64_t max_samples, int64_t max_slots) {
+                      uintptr_t row_ptr, int64_t max_samples, int64_t max_slots, bool update) {
+  (void)update;    // no global weights on this rule set
   int64_t n = 0, slots = 0;
   int64_t* rp = (int64_t*)row_ptr;
   rp[0] = 0;
@@ -293,7 +327,18 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("add_count", &jb::LabelTable::add_count);
   py::class_<jb::HostFvHasher>(m, "HostFvHasher")
       .def(py::init(&make_hasher))
-      .def("hash", &hasher_hash, "hash msgpack list<datum> bodies into CSR (idx, val, row_ptr)");
+      .def("hash", &hasher_hash, "hash msgpack list<datum> bodies into CSR (idx, val, row_ptr)",
+           py::arg("reqs"), py::arg("idx"), py::arg("val"), py::arg("row_ptr"),
+           py::arg("max_samples"), py::arg("max_slots"), py::arg("update") = false);
+  py::class_<jb::HostFvWide>(m, "HostFvWide")
+      .def(py::init(&make_wide))
+      .def("set_weights", [](jb::HostFvWide& h, uintptr_t df, uintptr_t diff, uintptr_t counts) {
+        h.set_weights((int64_t*)df, (int64_t*)diff, (int64_t*)counts);
+      })
+      .def("needs_weights", &jb::HostFvWide::needs_weights)
+      .def("hash", &wide_hash, "wide-rule converter: msgpack list<datum> bodies -> CSR",
+           py::arg("reqs"), py::arg("idx"), py::arg("val"), py::arg("row_ptr"),
+           py::arg("max_samples"), py::arg("max_slots"), py::arg("update") = false);
   m.def("pack_requests", &pack, "scan msgpack request bodies into a device-ready batch");
   m.def("pack_spans", &pack_spans, "zero-copy scan of request spans inside one pinned arena");
   py::class_<PyRpcServer>(m, "RpcServer")

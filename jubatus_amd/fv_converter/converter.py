@@ -109,96 +109,169 @@ def _params(d: dict) -> dict:
 class WeightManager:
     """Document-frequency statistics for the idf / bm25 global weights.
 
-    Mixable: ``get_diff`` / ``put_diff`` exchange (doc_count, df) deltas
-    (the weight engine and recommenders MIX them like every other model).
+    The statistics are keyed by the hashed feature index (``feature_index``
+    of the feature name into ``[0, H)``) - the same index space as the
+    models - and held as dense int64 arrays: the native host hasher
+    (csrc/native/jb_hostfv.hpp) and the GPU fv path (ops/fv_wide.py) update
+    and read these very arrays; two names only share statistics when they
+    share a model index.
+
+    Mixable: ``get_diff`` / ``put_diff`` exchange the (doc_count, total
+    length, df) deltas since the last MIX as sparse (index, count) records.
     """
 
-    def __init__(self):
-        self._lock = threading.Lock()
-        self.doc_count = 0
-        self.df: dict[str, int] = {}
-        self.total_len = 0  # for bm25 average document length
-        self._diff_docs = 0
-        self._diff_df: dict[str, int] = {}
-        self._diff_len = 0
+    BM25_K1 = 1.2
+    BM25_B = 0.75
 
-    def update(self, names: list[str], length: int) -> None:
+    def __init__(self, H: int = DEFAULT_HASH_MAX_SIZE):
+        import numpy as np
+        self._np = np
+        self._lock = threading.RLock()
+        self.H = int(H)
+        # [doc_count, total_len, diff_docs, diff_len]
+        self.counts = np.zeros(4, np.int64)
+        self.df = None           # int64[H], allocated on first use
+        self.diff = None         # int64[H]: df delta since the last MIX
+        self.device_table = None  # ops/fv_wide.DeviceDf when a GPU path owns a copy
+
+    # ---------------------------------------------------------- storage
+    def arrays(self):
+        """(df, diff, counts) - allocated on first use"""
+        if self.df is None:
+            self.df = self._np.zeros(self.H, self._np.int64)
+            self.diff = self._np.zeros(self.H, self._np.int64)
+        if self.device_table is not None:
+            self.device_table.pull(self)
+        return self.df, self.diff, self.counts
+
+    @property
+    def doc_count(self) -> int:
+        self._sync()
+        return int(self.counts[0])
+
+    @property
+    def total_len(self) -> int:
+        self._sync()
+        return int(self.counts[1])
+
+    def _sync(self) -> None:
+        if self.device_table is not None:
+            self.device_table.pull(self)
+
+    def update_idx(self, idx: list[int]) -> None:
+        """one document whose non-bin-weighted features have these indices
+        (duplicates count toward the length, once toward df)"""
         with self._lock:
-            self.doc_count += 1
-            self._diff_docs += 1
-            self.total_len += length
-            self._diff_len += length
-            for n in set(names):
-                self.df[n] = self.df.get(n, 0) + 1
-                self._diff_df[n] = self._diff_df.get(n, 0) + 1
+            df, diff, c = self.arrays()
+            c[0] += 1
+            c[2] += 1
+            c[1] += len(idx)
+            c[3] += len(idx)
+            for i in set(idx):
+                df[i] += 1
+                diff[i] += 1
+            if self.device_table is not None:
+                self.device_table.host_changed()
 
-    def idf(self, name: str) -> float:
-        df = self.df.get(name, 0)
-        if df <= 0 or self.doc_count <= 0:
+    def df_of(self, i: int) -> int:
+        if self.df is None:
+            return 0
+        df, _, _ = self.arrays()
+        return int(df[i])
+
+    def idf_idx(self, i: int) -> float:
+        df = self.df_of(i)
+        n = self.doc_count
+        if df <= 0 or n <= 0:
             return 0.0
-        return math.log(self.doc_count / df)
+        return math.log(n / df)
 
     def avg_len(self) -> float:
-        return self.total_len / self.doc_count if self.doc_count else 1.0
+        n = self.doc_count
+        return self.total_len / n if n else 1.0
 
     def clear(self) -> None:
         with self._lock:
-            self.doc_count = 0
-            self.df.clear()
-            self.total_len = 0
-            self._diff_docs = 0
-            self._diff_df.clear()
-            self._diff_len = 0
+            if self.device_table is not None:
+                self.device_table.clear()
+            self.counts[:] = 0
+            if self.df is not None:
+                self.df[:] = 0
+                self.diff[:] = 0
 
     # MIX
     def get_diff(self) -> dict:
         with self._lock:
-            return {"docs": self._diff_docs, "len": self._diff_len, "df": dict(self._diff_df)}
+            df, diff, c = self.arrays()
+            nz = self._np.flatnonzero(diff)
+            return {"docs": int(c[2]), "len": int(c[3]), "idx": nz.tolist(),
+                    "df": diff[nz].tolist()}
 
     @staticmethod
     def mix(a: dict, b: dict) -> dict:
-        df = dict(a["df"])
-        for k, v in b["df"].items():
-            df[k] = df.get(k, 0) + v
-        return {"docs": a["docs"] + b["docs"], "len": a["len"] + b["len"], "df": df}
+        acc: dict[int, int] = dict(zip(a["idx"], a["df"]))
+        for i, v in zip(b["idx"], b["df"]):
+            acc[i] = acc.get(i, 0) + v
+        ks = sorted(acc)
+        return {"docs": a["docs"] + b["docs"], "len": a["len"] + b["len"], "idx": ks,
+                "df": [acc[k] for k in ks]}
 
     def put_diff(self, mixed: dict) -> None:
         with self._lock:
+            np = self._np
+            df, diff, c = self.arrays()
             # replace own contribution by the cluster-wide one
-            self.doc_count += mixed["docs"] - self._diff_docs
-            self.total_len += mixed["len"] - self._diff_len
-            for k, v in self._diff_df.items():
-                self.df[k] = self.df.get(k, 0) - v
-            for k, v in mixed["df"].items():
-                self.df[k] = self.df.get(k, 0) + v
-            self.df = {k: v for k, v in self.df.items() if v > 0}
-            self._diff_docs = 0
-            self._diff_len = 0
-            self._diff_df = {}
+            c[0] += mixed["docs"] - c[2]
+            c[1] += mixed["len"] - c[3]
+            df -= diff
+            if mixed["idx"]:
+                np.add.at(df, np.asarray(mixed["idx"], np.int64), np.asarray(mixed["df"], np.int64))
+            np.maximum(df, 0, out=df)
+            diff[:] = 0
+            c[2] = c[3] = 0
+            if self.device_table is not None:
+                self.device_table.host_changed()
 
     def pack(self) -> list:
         with self._lock:
-            return [self.doc_count, self.total_len, self.df]
+            c = self.counts
+            if self.df is None:
+                return [int(c[0]), int(c[1]), {"idx": [], "df": []}]
+            df, _, _ = self.arrays()
+            nz = self._np.flatnonzero(df)
+            return [int(c[0]), int(c[1]), {"idx": nz.tolist(), "df": df[nz].tolist()}]
 
     def unpack(self, obj: list) -> None:
+        from .hashing import feature_index
         with self._lock:
-            self.doc_count, self.total_len, df = obj[0], obj[1], obj[2]
-            self.df = {(k.decode() if isinstance(k, bytes) else k): int(v) for k, v in df.items()}
-            self._diff_docs = 0
-            self._diff_len = 0
-            self._diff_df = {}
+            np = self._np
+            self.clear()
+            df, diff, c = self.arrays()
+            c[0], c[1] = int(obj[0]), int(obj[1])
+            tab = obj[2]
+            tab = {(k.decode() if isinstance(k, bytes) else k): v for k, v in tab.items()}
+            if "idx" in tab and isinstance(tab.get("idx"), list):
+                if tab["idx"]:
+                    np.add.at(df, np.asarray(tab["idx"], np.int64), np.asarray(tab["df"], np.int64))
+            else:   # name-keyed statistics (older models)
+                for name, v in tab.items():
+                    df[feature_index(name, self.H)] += int(v)
+            if self.device_table is not None:
+                self.device_table.host_changed()
 
 
 class _StringRule:
-    def __init__(self, matcher, type_name, splitter, sw, gw):
+    def __init__(self, matcher, type_name, splitter, sw, gw, split=("str", 0)):
         self.matcher, self.type_name, self.splitter = matcher, type_name, splitter
         self.sw, self.gw = sw, gw
+        self.split_kind, self.split_n = split      # str / space / ngram(n) / regexp / dynamic
         self.suffix = f"@{type_name}#{sw}/{gw}"
 
 
 class _NumRule:
-    def __init__(self, matcher, type_name, fn):
+    def __init__(self, matcher, type_name, fn, kind="num"):
         self.matcher, self.type_name, self.fn = matcher, type_name, fn
+        self.kind = kind                           # num / log / str / add / dynamic
 
 
 class DatumToFvConverter:
@@ -211,7 +284,7 @@ class DatumToFvConverter:
         self.hash_max_size = int(config.get("hash_max_size") or DEFAULT_HASH_MAX_SIZE)
         if self.hash_max_size <= 0:
             raise ConverterError("hash_max_size must be positive")
-        self.weights = WeightManager()
+        self.weights = WeightManager(self.hash_max_size)
         self._plugins = plugin_loader
         self._build(config)
 
@@ -276,14 +349,18 @@ class DatumToFvConverter:
             self.num_filters.append((KeyMatcher(r["key"]), nf_types[r["type"]], r["suffix"]))
         # string types
         st = {"str": None, "space": _space}
+        split_meta = {"str": ("str", 0), "space": ("space", 0)}
         for name, p in (c.get("string_types") or {}).items():
             m = p.get("method")
             if m == "ngram":
                 st[name] = _ngram(int(p["char_num"]))
+                split_meta[name] = ("ngram", int(p["char_num"]))
             elif m == "regexp":
                 st[name] = _regexp_splitter(p["pattern"], int(p.get("group", 0)))
+                split_meta[name] = ("regexp", 0)
             elif m == "dynamic":
                 st[name] = self._plugin("string_feature", _params(p))
+                split_meta[name] = ("dynamic", 0)
             else:
                 raise ConverterError(f"unknown string type method: {m}")
         self.string_rules = []
@@ -297,11 +374,13 @@ class DatumToFvConverter:
                 raise ConverterError(f"unknown sample_weight: {sw}")
             if gw not in self.GLOBAL_WEIGHTS:
                 raise ConverterError(f"unknown global_weight: {gw}")
-            self.string_rules.append(_StringRule(KeyMatcher(r["key"]), t, st[t], sw, gw))
+            self.string_rules.append(_StringRule(KeyMatcher(r["key"]), t, st[t], sw, gw,
+                                                 split_meta[t]))
         # num types
         nt: dict[str, Any] = {"num": lambda k, x: [(f"{k}@num", x)],
                               "log": lambda k, x: [(f"{k}@log", math.log(max(1.0, x)))],
                               "str": lambda k, x: [(f"{k}${_num_str(x)}@str", 1.0)]}
+        num_meta = {"num": "num", "log": "log", "str": "str"}
         for name, p in (c.get("num_types") or {}).items():
             m = p.get("method")
             if m == "add":
@@ -314,12 +393,13 @@ class DatumToFvConverter:
                 nt[name] = nt[m]
             else:
                 raise ConverterError(f"unknown num type method: {m}")
+            num_meta[name] = m
         self.num_rules = []
         for r in c.get("num_rules") or []:
             t = r["type"]
             if t not in nt:
                 raise ConverterError(f"unknown num type: {t}")
-            self.num_rules.append(_NumRule(KeyMatcher(r["key"]), t, nt[t]))
+            self.num_rules.append(_NumRule(KeyMatcher(r["key"]), t, nt[t], num_meta[t]))
         # binary types
         bt = {}
         for name, p in (c.get("binary_types") or {}).items():
@@ -333,8 +413,10 @@ class DatumToFvConverter:
             self.binary_rules.append((KeyMatcher(r["key"]), r["type"], bt[r["type"]]))
         # combination
         ct = {"add": lambda a, b: a + b, "mul": lambda a, b: a * b}
+        self.combination_methods = {"add": "add", "mul": "mul"}
         for name, p in (c.get("combination_types") or {}).items():
             m = p.get("method")
+            self.combination_methods[name] = m
             if m in ("add", "mul"):
                 ct[name] = ct[m]
             elif m == "dynamic":
@@ -391,20 +473,29 @@ class DatumToFvConverter:
         d = as_datum(datum)
         sv, nv = self._filtered(d)
         sfeat = self._string_features(sv)
-        if update and self.uses_global_weight:
-            names = [n for n, _, gw in sfeat if gw != "bin"]
-            self.weights.update(names, len(names))
         fv: list[tuple[str, float]] = []
-        avg_len = self.weights.avg_len() if self.uses_global_weight else 1.0
-        doc_len = sum(1 for _, _, gw in sfeat if gw != "bin")
-        for name, w, gw in sfeat:
-            if gw == "idf":
-                w *= self.weights.idf(name)
-            elif gw == "bm25":
-                k1, b = 1.2, 0.75
-                idf = self.weights.idf(name)
-                w = idf * (w * (k1 + 1)) / (w + k1 * (1 - b + b * doc_len / max(avg_len, 1e-9)))
-            fv.append((name, w))
+        if self.uses_global_weight:
+            from .hashing import feature_index
+            H = self.hash_max_size
+            gidx = [feature_index(n, H) if gw != "bin" else -1 for n, _, gw in sfeat]
+            wm = self.weights
+            if update:
+                wm.update_idx([i for i in gidx if i >= 0])
+            n_docs = wm.doc_count
+            avg_len = wm.avg_len()
+            doc_len = sum(1 for i in gidx if i >= 0)
+            for (name, w, gw), i in zip(sfeat, gidx):
+                if gw != "bin":
+                    df = wm.df_of(i)
+                    idf = math.log(n_docs / df) if df > 0 and n_docs > 0 else 0.0
+                    if gw == "idf":
+                        w *= idf
+                    else:
+                        k1, b = WeightManager.BM25_K1, WeightManager.BM25_B
+                        w = idf * (w * (k1 + 1)) / (w + k1 * (1 - b + b * doc_len / max(avg_len, 1e-9)))
+                fv.append((name, w))
+        else:
+            fv.extend((name, w) for name, w, _ in sfeat)
         for k, x in nv:
             for r in self.num_rules:
                 if r.matcher.match(k):

@@ -68,3 +68,79 @@ class GpuRuleTable:
         self.nrules = np.frombuffer(b"".join(nrows) or b"\0" * _RULE.size, dtype=np.uint8).copy()
         self.blob = np.frombuffer(bytes(blob) or b"\0", dtype=np.uint8).copy()
         self.H = conv.hash_max_size
+
+
+# ------------------------------------------------------------- wide rule set
+# string rule value_kind = splitter | sample_weight << 4 | global_weight << 8
+# (csrc/native/jb_hostfv_wide.hpp, csrc/hip/fv_wide.hip); pad = ngram length
+_SPLIT = {"str": 0, "ngram": 1, "space": 2}
+_SW = {"bin": 0, "tf": 1, "log_tf": 2}
+_GW = {"bin": 0, "idf": 1, "bm25": 2}
+_COMB = {"add": 0, "mul": 1}
+
+
+def wide_eligible(conv: DatumToFvConverter) -> bool:
+    """configs the wide native / GPU converter reproduces exactly: str /
+    space / ngram splitters, every sample and global weight, num / log num
+    types, add / mul combinations; no filters, plug-ins or regex matchers"""
+    if conv.string_filters or conv.num_filters or conv.binary_rules:
+        return False
+    for r in conv.string_rules:
+        if r.split_kind not in _SPLIT or r.matcher.kind not in _KIND:
+            return False
+        if r.split_kind == "ngram" and r.split_n <= 0:
+            return False
+    for r in conv.num_rules:
+        if r.kind not in ("num", "log") or r.matcher.kind not in _KIND:
+            return False
+    for ml, mr, tname, _ in conv.combination_rules:
+        if conv.combination_methods.get(tname) not in _COMB:
+            return False
+        if ml.kind not in _KIND or mr.kind not in _KIND:
+            return False
+    return True
+
+
+class WideRuleTable:
+    """Packed wide rule tables: string rules, num rules, combination rules
+    (two entries each: left matcher + "/type" suffix + op, right matcher)."""
+
+    def __init__(self, conv: DatumToFvConverter):
+        if not wide_eligible(conv):
+            raise ValueError("converter config is not eligible for the wide native path")
+        blob = bytearray()
+
+        def put(b: bytes) -> tuple[int, int]:
+            off = len(blob)
+            blob.extend(b)
+            return off, len(b)
+
+        srows = []
+        for r in conv.string_rules:
+            mo, ml = put(r.matcher.arg.encode())
+            so, sl = put(r.suffix.encode())
+            vk = _SPLIT[r.split_kind] | _SW[r.sw] << 4 | _GW[r.gw] << 8
+            srows.append(_RULE.pack(_KIND[r.matcher.kind], mo, ml, so, sl, vk, 0.0, r.split_n))
+        nrows = []
+        for r in conv.num_rules:
+            mo, ml = put(r.matcher.arg.encode())
+            so, sl = put(f"@{r.type_name}".encode())
+            nrows.append(_RULE.pack(_KIND[r.matcher.kind], mo, ml, so, sl,
+                                    1 if r.kind == "log" else 0, 0.0, 0))
+        crows = []
+        for ml_, mr_, tname, _ in conv.combination_rules:
+            lo, ll = put(ml_.arg.encode())
+            so, sl = put(f"/{tname}".encode())
+            ro, rl = put(mr_.arg.encode())
+            crows.append(_RULE.pack(_KIND[ml_.kind], lo, ll, so, sl,
+                                    _COMB[conv.combination_methods[tname]], 0.0, 0))
+            crows.append(_RULE.pack(_KIND[mr_.kind], ro, rl, 0, 0, 0, 0.0, 0))
+        self.n_srules = len(srows)
+        self.n_nrules = len(nrows)
+        self.n_crules = len(crows) // 2
+        self.srules = np.frombuffer(b"".join(srows) or b"\0" * _RULE.size, dtype=np.uint8).copy()
+        self.nrules = np.frombuffer(b"".join(nrows) or b"\0" * _RULE.size, dtype=np.uint8).copy()
+        self.crules = np.frombuffer(b"".join(crows) or b"\0" * _RULE.size, dtype=np.uint8).copy()
+        self.blob = np.frombuffer(bytes(blob) or b"\0", dtype=np.uint8).copy()
+        self.H = conv.hash_max_size
+        self.global_weights = conv.uses_global_weight

@@ -67,7 +67,8 @@ class RowEngine:
         return self.conv.hashed(f)
 
     def _set(self, rid: str, dicts, bump: bool = True, update_weight: bool = True) -> None:
-        if self.gpu and hasattr(self.index, "set_rows_direct") and self._set_direct(rid, dicts, bump):
+        if self.gpu and hasattr(self.index, "set_rows_direct") and \
+                self._set_direct(rid, dicts, bump, update_weight):
             pass
         else:
             fv = self.fv_of(dicts_to_datum(*dicts), update_weight)
@@ -78,15 +79,27 @@ class RowEngine:
                 self._remove(victim)
 
     def _hasher(self):
-        """native host hasher (csrc/native/jb_hostfv.hpp) when the converter
-        config is eligible (no filters / global weights / plug-ins), else None"""
+        """native host converter when the converter config allows it, else
+        None: csrc/native/jb_hostfv.hpp for the plain rule set,
+        csrc/native/jb_hostfv_wide.hpp for ngram / space splitters, tf /
+        idf / bm25 weights (the WeightManager's arrays, updated in place) and
+        combinations. No filters / plug-ins / regex matchers."""
         if self._host_hasher is None:
-            from ..fv_converter.gpu_path import GpuRuleTable, gpu_eligible
+            from ..fv_converter.gpu_path import (GpuRuleTable, WideRuleTable, gpu_eligible,
+                                                 wide_eligible)
+            from .._native import native
             if gpu_eligible(self.conv):
-                from .._native import native
                 rt = GpuRuleTable(self.conv)
                 self._host_hasher = native().HostFvHasher(rt.srules, rt.n_srules, rt.nrules,
                                                           rt.n_nrules, rt.blob, rt.H)
+            elif wide_eligible(self.conv):
+                rt = WideRuleTable(self.conv)
+                h = native().HostFvWide(rt.srules, rt.n_srules, rt.nrules, rt.n_nrules, rt.crules,
+                                        rt.n_crules, rt.blob, rt.H)
+                if h.needs_weights():
+                    df, diff, counts = self.conv.weights.arrays()
+                    h.set_weights(df.ctypes.data, diff.ctypes.data, counts.ctypes.data)
+                self._host_hasher = h
             else:
                 self._host_hasher = False
         return self._host_hasher or None
@@ -113,7 +126,9 @@ class RowEngine:
             idx = np.empty(cap, np.int32)
             val = np.empty(cap, np.float32)
             rp = np.zeros(n + 1, np.int64)
-            got, _, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, n, cap)
+            # (a failed call rolls back its document-statistics updates)
+            got, _, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, n, cap,
+                                 update_weight)
             if err == 2:
                 cap *= 4
                 continue
@@ -141,8 +156,8 @@ class RowEngine:
                 if victim != rid:
                     self._remove(victim)
 
-    def _set_direct(self, rid: str, dicts, bump: bool) -> bool:
-        """native hashing + one signature launch into the row's slot"""
+    def _set_direct(self, rid: str, dicts, bump: bool, update_weight: bool = True) -> bool:
+        """native hashing + one index write into the row's slot"""
         h = self._hasher()
         if h is None:
             return False
@@ -154,7 +169,7 @@ class RowEngine:
         val = np.empty(hip.QUERY_SLOTS, np.float32)
         rp = np.zeros(2, np.int64)
         n, _, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 1,
-                           hip.QUERY_SLOTS)
+                           hip.QUERY_SLOTS, update_weight)
         if err or n != 1:
             return False
         keep = idx[:rp[1]] >= 0

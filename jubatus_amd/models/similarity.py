@@ -446,6 +446,7 @@ class DevicePool:
 
     def __init__(self, device):
         self.device = device
+        self._stager = None
         self.cap_rows = 0
         self.cap_entries = 0
         self.end = 0                      # next free pool entry
@@ -536,7 +537,10 @@ class DevicePool:
         meta[:, 3] = run
         pack = np.concatenate([meta.reshape(-1).view(np.uint8), idx.astype(np.int32).view(np.uint8),
                                val.astype(np.float32).view(np.uint8)])
-        dev = torch.from_numpy(pack).to(self.device)
+        if pack.nbytes <= (256 << 10):
+            (dev,) = self.stager().put(pack)      # latency path: pinned ring, async
+        else:
+            dev = torch.from_numpy(pack).to(self.device)
         hip.pool_append(dev, n, nnz, self.end, self)
         old = self.len_h[slots]
         self.live += nnz - int(old.sum())
@@ -549,6 +553,19 @@ class DevicePool:
             self.live -= int(self.len_h[slot])
             self.len_h[slot] = 0
             self.valid[slot] = 0
+
+    def stager(self):
+        if self._stager is None:
+            from ..ops.staging import Stager
+            self._stager = Stager(self.device)
+        return self._stager
+
+    def query_slots_device(self, slots: Sequence[int]):
+        """stored rows as queries, read by the scan kernel from the pool:
+        -> ("slots", device int32 slots, total entries)"""
+        slots = np.asarray(slots, dtype=np.int32)
+        (ds,) = self.stager().put(slots)
+        return ("slots", ds, int(self.len_h[slots].sum()))
 
     def query_csr(self, slots: Sequence[int]):
         """device (qptr, qidx, qval, qn2) of stored rows used as queries"""
@@ -624,28 +641,55 @@ class InvertedIndex:
             return
         self.rows.pop(int(slot), None)
 
+    # latency paths (models/row_engine.py): natively hashed host CSR
+    def set_rows_direct(self, slots: np.ndarray, row_ptr: np.ndarray, idx: np.ndarray,
+                        val: np.ndarray) -> bool:
+        if not self.gpu:
+            return False
+        n = int(np.asarray(slots).size)
+        self.set_rows_csr(np.asarray(slots, np.int64), row_ptr[:n + 1], idx[:int(row_ptr[n])],
+                          val[:int(row_ptr[n])])
+        return True
+
+    def query_direct(self, idx, val, row_ptr, nq: int, nrows: int, k: int,
+                     similar: bool) -> list[list[tuple[int, float]]] | None:
+        if not (self.gpu and nrows > 0 and k > 0):
+            return None
+        rp = np.asarray(row_ptr[:nq + 1], np.int64)
+        return self._query_batches(
+            lambda a, b: self._queries_csr(rp[a:b + 1] - rp[a], idx[rp[a]:rp[b]], val[rp[a]:rp[b]]),
+            nq, nrows, k, similar)
+
     # ------------------------------------------------------------ device
     def _queries_device(self, rows):
-        import torch
-        rp, idx, val = _rows_to_csr(rows)
+        return self._queries_csr(*_rows_to_csr(rows))
+
+    def _queries_csr(self, rp, idx, val):
+        """host query CSR (may hold idx < 0 / repeats) -> device queries,
+        one async H2D through the pool's pinned stager"""
         lens, qi, qv, qn2 = normalize_csr(rp, idx, val)
-        qptr = np.zeros(len(rows) + 1, dtype=np.int64)
+        qptr = np.zeros(lens.size + 1, dtype=np.int64)
         np.cumsum(lens, out=qptr[1:])
-        d = self.device
         if qi.size == 0:
             qi, qv = np.zeros(1, np.int32), np.zeros(1, np.float32)
-        return (torch.from_numpy(qptr).to(d), torch.from_numpy(qi).to(d),
-                torch.from_numpy(qv).to(d), torch.from_numpy(np.asarray(qn2, np.float64)).to(d),
-                int(qptr[-1]))
+        dq = self.pool.stager().put(qptr, qi, qv, np.asarray(qn2, np.float64))
+        return (*dq, int(qptr[-1]))
 
     def _scan(self, q, nq: int, nrows: int):
         import torch
         from ..ops import hip
+        out = torch.empty(nq * nrows, dtype=torch.float32, device=self.device)
+        metric = 1 if self.euclid else 0
+        if q[0] == "slots":
+            if q[2] > hip.POOL_MAX_Q_ENTRIES:
+                raise ValueError("query batch has more than 4096 features")
+            hip.pool_scan(None, None, None, None, nq, self.pool, nrows, metric, out,
+                          qslots=q[1], qtotal=q[2])
+            return out
         qptr, qi, qv, qn2, total = q
         if total > hip.POOL_MAX_Q_ENTRIES:
             raise ValueError("query batch has more than 4096 features")
-        out = torch.empty(nq * nrows, dtype=torch.float32, device=self.device)
-        hip.pool_scan(qptr, qi, qv, qn2, nq, self.pool, nrows, 1 if self.euclid else 0, out)
+        hip.pool_scan(qptr, qi, qv, qn2, nq, self.pool, nrows, metric, out)
         return out
 
     def _query_batches(self, make, n: int, nrows: int, k: int, similar: bool):
@@ -654,7 +698,7 @@ class InvertedIndex:
         for b0 in range(0, n, hip.POOL_MAX_Q):
             b1 = min(n, b0 + hip.POOL_MAX_Q)
             q = make(b0, b1)
-            if q[4] > hip.POOL_MAX_Q_ENTRIES and b1 - b0 > 1:      # one query at a time
+            if q[-1] > hip.POOL_MAX_Q_ENTRIES and b1 - b0 > 1:     # one query at a time
                 for j in range(b0, b1):
                     res += self._topk(self._scan(make(j, j + 1), 1, nrows), 1, nrows, k, similar)
                 continue
@@ -670,7 +714,8 @@ class InvertedIndex:
             m = sc.view(nq, nrows)
             dist = m if self.euclid else (1.0 - m).nan_to_num(posinf=math.inf)
             d, i = torch.topk(dist, min(k, nrows), dim=1, largest=False, sorted=True)
-        out = _pairs(d.cpu().numpy(), i.cpu().numpy())
+        d, i = self.pool.stager().fetch(d, i)
+        out = _pairs(d, i)
         if similar:
             out = [[(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in r] for r in out]
         return out
@@ -722,7 +767,7 @@ class InvertedIndex:
         if self.gpu:
             if nrows <= 0 or k <= 0:
                 return [[] for _ in slots]
-            return self._query_batches(lambda a, b: self.pool.query_csr(slots[a:b]), len(slots),
-                                       nrows, k, similar)
+            return self._query_batches(lambda a, b: self.pool.query_slots_device(slots[a:b]),
+                                       len(slots), nrows, k, similar)
         return self.query([self.rows.get(int(s), (np.zeros(0, np.int32), np.zeros(0, np.float32)))
                            for s in slots], nrows, k, similar)

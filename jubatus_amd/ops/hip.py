@@ -68,7 +68,7 @@ _SIGS = {
                               _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                               _c_void_p],
-    "jb_pool_scan": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+    "jb_pool_scan": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p],
     "jb_pool_append": [_c_void_p, _i32, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _c_void_p],
@@ -201,18 +201,28 @@ POOL_MAX_Q = 8              # csrc/hip/sparse_pool.hip kPoolMaxQ
 POOL_MAX_Q_ENTRIES = 4096   # kPoolMaxQEntries
 
 
-def pool_scan(qptr, qidx, qval, qn2, nq: int, pool, nrows: int, metric: int, out) -> None:
+def pool_scan(qptr, qidx, qval, qn2, nq: int, pool, nrows: int, metric: int, out,
+              qslots=None, qtotal: int = 0) -> None:
     """[nq, nrows] cosine similarity (metric 0) / euclidean distance (1) of
-    nq sorted sparse queries (device CSR) vs the rows of ``pool``
-    (models/similarity.py DevicePool)."""
+    nq sorted sparse queries vs the rows of ``pool`` (models/similarity.py
+    DevicePool). Queries are a device CSR (qptr, qidx, qval, qn2) or, with
+    ``qslots`` (device int32 [nq]), stored rows taken from the pool
+    (``qtotal`` = their total length, checked against the LDS capacity)."""
     if not 0 < nq <= POOL_MAX_Q:
         raise ValueError("pool_scan: 1..8 queries per pass")
     _dev(out, torch.float32, "out")
-    if out.numel() < nq * nrows or qptr.numel() < nq + 1 or nrows > pool.cap_rows:
+    if out.numel() < nq * nrows or nrows > pool.cap_rows:
         raise ValueError("pool_scan: bad operand shapes")
-    rc = _fn("jb_pool_scan")(_p(qptr), _p(qidx), _p(qval), _p(qn2), nq, _p(pool.r_off),
-                             _p(pool.r_len), _p(pool.r_n2), _p(pool.valid), nrows, _p(pool.p_idx),
-                             _p(pool.p_val), metric, _p(out), _stream())
+    if qslots is not None:
+        _dev(qslots, torch.int32, "qslots")
+        if qslots.numel() < nq or qtotal > POOL_MAX_Q_ENTRIES:
+            raise ValueError("pool_scan: bad query slots")
+        qptr = qidx = qval = qn2 = None
+    elif qptr.numel() < nq + 1:
+        raise ValueError("pool_scan: bad operand shapes")
+    rc = _fn("jb_pool_scan")(_p(qptr), _p(qidx), _p(qval), _p(qn2), _p(qslots), nq,
+                             _p(pool.r_off), _p(pool.r_len), _p(pool.r_n2), _p(pool.valid), nrows,
+                             _p(pool.p_idx), _p(pool.p_val), metric, _p(out), _stream())
     _check(rc, "jb_pool_scan")
 
 

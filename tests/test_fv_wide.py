@@ -1,0 +1,142 @@
+"""Wide-rule native converter (csrc/native/jb_hostfv_wide.hpp) and its GPU
+twin (csrc/hip/fv_wide.hip, ops/fv_wide.py) against the Python converter
+(fv_converter/converter.py `_convert`): ngram / space splitters, tf / log_tf
+sample weights, idf / bm25 global weights with document frequencies updated
+datum by datum, num / log num rules and add / mul combinations - identical
+feature order, indices and values, and identical document statistics."""
+import json
+import os
+import random
+
+import msgpack
+import numpy as np
+import pytest
+
+from helpers import ROOT
+from jubatus_amd.fv_converter.converter import DatumToFvConverter
+from jubatus_amd.fv_converter.datum import Datum
+from jubatus_amd.fv_converter.gpu_path import WideRuleTable, gpu_eligible, wide_eligible
+
+CONFIGS = ["recommender/default.json", "weight/default.json",
+           "classifier/arow_combinational_feature.json", "anomaly/default.json"]
+
+EXTRA = {
+    "string_types": {"tri": {"method": "ngram", "char_num": "3"}},
+    "string_rules": [{"key": "t*", "type": "space", "sample_weight": "log_tf", "global_weight": "bm25"},
+                     {"key": "*x", "type": "tri", "sample_weight": "tf", "global_weight": "idf"},
+                     {"key": "id", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+    "num_rules": [{"key": "n*", "type": "log"}, {"key": "*", "type": "num"}],
+    "combination_types": {"pr": {"method": "mul"}},
+    "combination_rules": [{"key_left": "id$*", "key_right": "*@num", "type": "pr"},
+                          {"key_left": "*", "key_right": "n1@log", "type": "add"}],
+    "hash_max_size": 1 << 16,
+}
+
+
+def _conv(name):
+    if name == "extra":
+        return DatumToFvConverter(EXTRA)
+    with open(os.path.join(ROOT, "config", name)) as f:
+        return DatumToFvConverter(json.load(f)["converter"])
+
+
+def datums(n, seed=0):
+    r = random.Random(seed)
+    words = ["ab", "abc", "日本語", "héllo", "a b", "x", "", "zzzz", "the cat sat", "cat"]
+    out = []
+    for _ in range(n):
+        sv = [(f"t{r.randrange(3)}", " ".join(r.choice(words) for _ in range(r.randrange(1, 4))))
+              for _ in range(r.randrange(0, 4))]
+        if r.random() < 0.5:
+            sv.append(("tx", r.choice(words) * 2))
+        if r.random() < 0.2:          # long text: the hashed token-count path
+            sv.append(("t9", " ".join(r.choice(words) for _ in range(40))))
+        sv.append(("id", f"u{r.randrange(5)}"))
+        nv = [(f"n{r.randrange(3)}", r.choice([0.5, 2.0, 10.0, -3.0, 1.0])) for _ in range(r.randrange(0, 3))]
+        d = Datum()
+        d.string_values, d.num_values = sv, nv
+        out.append(d)
+    return out
+
+
+def native_wide(conv):
+    from jubatus_amd._native import native
+    rt = WideRuleTable(conv)
+    h = native().HostFvWide(rt.srules, rt.n_srules, rt.nrules, rt.n_nrules, rt.crules,
+                            rt.n_crules, rt.blob, rt.H)
+    if h.needs_weights():
+        df, diff, counts = conv.weights.arrays()
+        h.set_weights(df.ctypes.data, diff.ctypes.data, counts.ctypes.data)
+    return h
+
+
+def run_native(h, ds, update):
+    out = []
+    for d in ds:
+        body = msgpack.packb([d.to_msgpack()], use_bin_type=False)
+        cap = 4096
+        idx = np.empty(cap, np.int32)
+        val = np.empty(cap, np.float32)
+        rp = np.zeros(2, np.int64)
+        n, slots, err = h.hash([body], idx.ctypes.data, val.ctypes.data, rp.ctypes.data, 1, cap,
+                               update)
+        assert err == 0 and n == 1
+        out.append((idx[:slots].copy(), val[:slots].copy()))
+    return out
+
+
+def run_python(conv, ds, update):
+    out = []
+    for d in ds:
+        fv = conv.convert_and_update_weight(d) if update else conv.convert(d)
+        i, v = conv.hashed(fv)
+        out.append((np.asarray(i, np.int32), np.asarray(v, np.float32)))
+    return out
+
+
+@pytest.mark.parametrize("name", CONFIGS + ["extra"])
+def test_wide_eligible_configs(name):
+    conv = _conv(name)
+    assert wide_eligible(conv)
+    if name != "extra":
+        assert not gpu_eligible(conv) or name.startswith("classifier")
+
+
+@pytest.mark.parametrize("name", CONFIGS + ["extra"])
+def test_native_wide_equals_python_converter(name):
+    ds = datums(60, seed=sum(map(ord, name)))
+    cpy, cnat = _conv(name), _conv(name)
+    h = native_wide(cnat)
+    for update in (True, False):
+        a = run_python(cpy, ds, update)
+        b = run_native(h, ds, update)
+        for (ia, va), (ib, vb) in zip(a, b):
+            np.testing.assert_array_equal(ia, ib)
+            np.testing.assert_allclose(va, vb, rtol=1e-6, atol=1e-7)
+    if cpy.uses_global_weight:
+        assert cpy.weights.doc_count == cnat.weights.doc_count == 60
+        assert cpy.weights.total_len == cnat.weights.total_len
+        np.testing.assert_array_equal(cpy.weights.df, cnat.weights.df)
+        np.testing.assert_array_equal(cpy.weights.diff, cnat.weights.diff)
+
+
+def test_weight_manager_mix_and_pack_roundtrip():
+    a, b = _conv("recommender/default.json"), _conv("recommender/default.json")
+    for d in datums(20, 1):
+        a.convert_and_update_weight(d)
+    for d in datums(30, 2):
+        b.convert_and_update_weight(d)
+    m = a.weights.mix(a.weights.get_diff(), b.weights.get_diff())
+    a.weights.put_diff(m)
+    b.weights.put_diff(m)
+    assert a.weights.doc_count == b.weights.doc_count == 50
+    np.testing.assert_array_equal(a.weights.df, b.weights.df)
+    c = _conv("recommender/default.json")
+    c.weights.unpack(msgpack.unpackb(msgpack.packb(a.weights.pack()), strict_map_key=False))
+    np.testing.assert_array_equal(c.weights.df, a.weights.df)
+    assert c.weights.avg_len() == a.weights.avg_len()
+    # older name-keyed statistics load into index space
+    d = _conv("recommender/default.json")
+    d.weights.unpack([4, 10, {"t$ab@bigram#tf/idf": 2}])
+    from jubatus_amd.fv_converter.hashing import feature_index
+    assert d.weights.df_of(feature_index("t$ab@bigram#tf/idf", d.hash_max_size)) == 2
