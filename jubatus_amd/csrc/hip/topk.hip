@@ -714,8 +714,10 @@ static int sample_j(int64_t nrows, int k) {
   return jj <= 16 ? jj : 0;
 }
 
+// + the radix-select histograms of the score path: 2 levels x nq x 4096
+constexpr int kRadixBins = 4096;
 extern "C" int64_t jb_topk_direct_scratch(int nq) {
-  return 64 + (int64_t)nq * kCandCap;
+  return 64 + (int64_t)nq * kCandCap + 2 * (int64_t)nq * kRadixBins;
 }
 
 static int topk_to_host_any(const uint64_t* qbits, const float* qnorm, int nq,
@@ -781,3 +783,179 @@ extern "C" int jb_topk_direct_query(const uint64_t* qbits, const float* qnorm, i
                          scratch_d, scratch_i, out_d_host, out_i_host, done_host, stream);
 }
 
+// Score-vector latency path (mode 1: [nq][nrows] similarity / distance from
+// the inverted index scan, csrc/hip/sparse_pool.hip), exact two-level radix
+// select instead of the tile kernel's per-tile selection:
+//   R1  histogram of the top 12 bits of the order-preserving key of every
+//       distance (LDS per block, then global atomics);
+//   R2  one block per query: the bucket holding the k-th smallest;
+//   R3  histogram of the next 12 bits inside that bucket;
+//   R4  the sub-bucket holding the k-th smallest -> threshold T (all rows
+//       with key <= T: at most k + that sub-bucket's size);
+//   R5  collect the rows <= T (topk_collect_kernel), R6 exact top-k of the
+//       candidates into pinned host memory (topk_final_kernel).
+// Cost: three 4-byte reads per row, no per-tile sorting, independent of k.
+// Ties beyond the candidate buffer (e.g. thousands of identical distances)
+// flag a retry and the exact tile path reruns.
+namespace jb {
+
+__device__ __forceinline__ uint32_t dist_key(float d) {
+  const uint32_t u = __float_as_uint(d);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);      // monotone in d
+}
+__device__ __forceinline__ float key_dist(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int LEVEL>
+__global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ src, int flip,
+                                                         int64_t n, const uint32_t* __restrict__ sel,
+                                                         uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kRadixBins];
+  const int q = blockIdx.y;
+  for (int i = threadIdx.x; i < kRadixBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint32_t pre = LEVEL == 2 ? sel[2 * q] : 0u;
+  const float* sq = src + (int64_t)q * n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t b = (int64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x; b < n; b += stride) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t i = b + u * blockDim.x;
+      v[u] = sq[i < n ? i : n - 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (b + u * blockDim.x >= n) continue;
+      const float d = flip ? 1.f - v[u] : v[u];
+      if (!(d < INFINITY)) continue;                        // invalid rows / NaN
+      const uint32_t key = dist_key(d);
+      if (LEVEL == 1) atomicAdd(&h[key >> 20], 1u);
+      else if ((key >> 20) == pre) atomicAdd(&h[(key >> 8) & 0xfff], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* gh = hist + (int64_t)q * kRadixBins;
+  for (int i = threadIdx.x; i < kRadixBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&gh[i], h[i]);
+}
+
+// sel[2q] = level-1 bucket, sel[2q + 1] = rows below it; level 2 writes the
+// float threshold thr[q] and zeroes the candidate count
+template <int LEVEL>
+__global__ __launch_bounds__(1024) void radix_select_kernel(const uint32_t* __restrict__ hist,
+                                                            int k, uint32_t* __restrict__ sel,
+                                                            float* __restrict__ thr,
+                                                            int* __restrict__ count) {
+  __shared__ uint32_t part[1024];
+  const int q = blockIdx.x;
+  const uint32_t* h = hist + (int64_t)q * kRadixBins;
+  const int t = threadIdx.x;
+  uint32_t c[4];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { c[j] = h[4 * t + j]; sum += c[j]; }
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {          // inclusive scan of the per-thread sums
+    const uint32_t x = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  const uint32_t before_me = part[t] - sum;
+  const uint32_t total = part[1023];
+  const uint32_t need = LEVEL == 1 ? (uint32_t)k : (uint32_t)k - sel[2 * q + 1];
+  if (t == 0 && total < need) {                 // fewer finite rows than needed
+    if (LEVEL == 1) { sel[2 * q] = 0xffffffffu; sel[2 * q + 1] = 0; }
+    else { thr[q] = INFINITY; count[q] = 0; }
+  }
+  uint32_t run = before_me;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (run < need && run + c[j] >= need) {     // exactly one bin satisfies this
+      const uint32_t bin = 4 * t + j;
+      if (LEVEL == 1) {
+        sel[2 * q] = bin;
+        sel[2 * q + 1] = run;
+      } else {
+        const uint32_t T = (sel[2 * q] << 20) | (bin << 8) | 0xffu;
+        thr[q] = key_dist(T);
+        count[q] = 0;
+      }
+    }
+    run += c[j];
+  }
+}
+
+}  // namespace jb
+
+static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, bool radix,
+                              float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                              int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                              hipStream_t stream) {
+  if (!radix) {
+    const int blocks = jb_topk_blocks(nrows, k);
+    const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
+    const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
+    jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    const int64_t nc = (int64_t)blocks * k;
+    jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
+    jb::launch_merge(m, nq, nc, k, out_d_host, out_i_host, (volatile uint32_t*)done_host, seq,
+                     stream);
+    return (int)hipGetLastError();
+  }
+  float* thr = scratch_d;                          // [8]
+  int* count = scratch_i;                          // [8]
+  uint32_t* sel = (uint32_t*)scratch_i + 16;       // [2 x 8]
+  float* cand_d = scratch_d + 64;
+  int32_t* cand_i = scratch_i + 64;
+  uint32_t* h1 = (uint32_t*)(scratch_i + 64 + (int64_t)nq * kCandCap);
+  uint32_t* h2 = h1 + (int64_t)nq * kRadixBins;
+  hipError_t e = hipMemsetAsync(h1, 0, sizeof(uint32_t) * 2 * (size_t)nq * kRadixBins, stream);
+  if (e != hipSuccess) return (int)e;
+  int64_t hb = (nrows + 1023) / 1024;
+  if (hb > 512) hb = 512;
+  const float* src = s.src_d;
+  hipLaunchKernelGGL(jb::radix_hist_kernel<1>, dim3((unsigned)hb, nq), dim3(256), 0, stream, src,
+                     s.flip, nrows, sel, h1);
+  hipLaunchKernelGGL(jb::radix_select_kernel<1>, dim3(nq), dim3(1024), 0, stream, h1, k, sel, thr,
+                     count);
+  hipLaunchKernelGGL(jb::radix_hist_kernel<2>, dim3((unsigned)hb, nq), dim3(256), 0, stream, src,
+                     s.flip, nrows, sel, h2);
+  hipLaunchKernelGGL(jb::radix_select_kernel<2>, dim3(nq), dim3(1024), 0, stream, h2, k, sel, thr,
+                     count);
+  int64_t cblocks = (nrows + 1023) / 1024;
+  if (cblocks > 1024) cblocks = 1024;
+  hipLaunchKernelGGL(jb::topk_collect_kernel<1>, dim3((unsigned)cblocks, nq), dim3(256), 0, stream,
+                     s, nrows, thr, kCandCap, cand_d, cand_i, count);
+  hipLaunchKernelGGL(jb::topk_final_kernel, dim3(nq), dim3(1024), 0, stream, cand_d, cand_i,
+                     count, kCandCap, k, thr, out_d_host, out_i_host,
+                     (volatile uint32_t*)done_host, seq);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64_t nrows, int k,
+                                     float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                                     int32_t* out_i_host, uint32_t* done_host,
+                                     hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  if (k > jb::kTopMaxK || nq > 8) return -2;
+  jb::TopkSrc s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, src_d, nullptr, flip};
+  const bool radix = nrows >= 16384 && getenv("JB_TOPK_SCORES_TILE") == nullptr;
+  uint32_t seq = jb::next_seq();
+  int rc = topk_scores_launch(s, nq, nrows, k, radix, scratch_d, scratch_i, out_d_host,
+                              out_i_host, done_host, seq, stream);
+  if (rc != 0) return rc;
+  bool retry = false;
+  rc = jb::wait_flags_status(done_host, nq, seq, jb::kTopRetry, stream, &retry);
+  if (rc != 0 || !retry) return rc;
+  seq = jb::next_seq();
+  rc = topk_scores_launch(s, nq, nrows, k, false, scratch_d, scratch_i, out_d_host, out_i_host,
+                          done_host, seq, stream);
+  if (rc != 0) return rc;
+  return jb::wait_flags(done_host, nq, seq, stream);
+}

@@ -111,7 +111,7 @@ class LOF(RowEngine):
             return
         self._st.moved([self.rows.slot(rid) for rid, _ in items])
 
-    def build_lists(self, chunk: int = 1024) -> int:
+    def build_lists(self, chunk: int = 1024, progress=None) -> int:
         """compute the neighbour list of every stored row that has none
         (after a bulk load / MIX / model load) with batched kNN queries, so
         later adds and scores find a warm state; returns the rows built"""
@@ -125,6 +125,8 @@ class LOF(RowEngine):
                 part = todo[i:i + chunk]
                 lists = self.query_slot_lists(part, self.k + 1, similar=False)
                 st.set_lists(part, [self._pairs(lst) for lst in lists])
+                if progress and (i // chunk) % 64 == 0:
+                    progress(i + len(part), len(todo))
             return len(todo)
 
     # ---------------------------------------------------------------- API

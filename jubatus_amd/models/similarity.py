@@ -447,12 +447,15 @@ class DevicePool:
     def __init__(self, device):
         self.device = device
         self._stager = None
+        self._scores = None
+        self.nlive = 0                    # slots holding a row
         self.cap_rows = 0
         self.cap_entries = 0
         self.end = 0                      # next free pool entry
         self.live = 0                     # entries of the current runs
         self.off_h = np.zeros(0, dtype=np.int64)
         self.len_h = np.zeros(0, dtype=np.int64)
+        self.has_h = np.zeros(0, dtype=bool)
         self._grow_rows(1024)
         self._grow_entries(1 << 16)
 
@@ -476,9 +479,11 @@ class DevicePool:
         self.valid = grow(getattr(self, "valid", None), torch.uint8)
         off_h = np.zeros(cap, dtype=np.int64)
         len_h = np.zeros(cap, dtype=np.int64)
+        has_h = np.zeros(cap, dtype=bool)
         off_h[:self.off_h.size] = self.off_h
         len_h[:self.len_h.size] = self.len_h
-        self.off_h, self.len_h = off_h, len_h
+        has_h[:self.has_h.size] = self.has_h
+        self.off_h, self.len_h, self.has_h = off_h, len_h, has_h
         self.cap_rows = cap
 
     def _grow_entries(self, need: int) -> None:
@@ -495,6 +500,20 @@ class DevicePool:
             pv[:self.end].copy_(self.p_val[:self.end])
         self.p_idx, self.p_val = pi, pv
         self.cap_entries = cap
+
+    def score_scratch(self, n: int):
+        """device score matrix of the latency query path ([nq][nrows] fp32)"""
+        import torch
+        if self._scores is None or self._scores.numel() < n:
+            self._scores = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=self.device)
+        return self._scores
+
+    def lanes_per_row(self) -> int:
+        """scan lanes per row from the mean run length: one lane walks a
+        short row alone, text-like rows get 4 / 16 lanes"""
+        rows = max(1, self.nlive)
+        mean = self.live / rows
+        return 1 if mean <= 24 else 4 if mean <= 96 else 16
 
     def compact(self) -> None:
         """rewrite the live runs contiguously (device gather), dropping the
@@ -544,13 +563,19 @@ class DevicePool:
         hip.pool_append(dev, n, nnz, self.end, self)
         old = self.len_h[slots]
         self.live += nnz - int(old.sum())
+        self.nlive += int((~self.has_h[slots]).sum())
+        self.has_h[slots] = True
         self.off_h[slots] = self.end + run
         self.len_h[slots] = lens
         self.end += nnz
 
     def remove(self, slot: int) -> None:
         if 0 <= slot < self.cap_rows and self.len_h[slot] >= 0:
-            self.live -= int(self.len_h[slot])
+            ln = int(self.len_h[slot])
+            self.live -= ln
+            if self.has_h[slot]:
+                self.nlive -= 1
+                self.has_h[slot] = False
             self.len_h[slot] = 0
             self.valid[slot] = 0
 
@@ -567,25 +592,6 @@ class DevicePool:
         (ds,) = self.stager().put(slots)
         return ("slots", ds, int(self.len_h[slots].sum()))
 
-    def query_csr(self, slots: Sequence[int]):
-        """device (qptr, qidx, qval, qn2) of stored rows used as queries"""
-        import torch
-        d = self.device
-        slots = np.asarray(slots, dtype=np.int64)
-        lens = self.len_h[slots]
-        qptr = np.zeros(slots.size + 1, dtype=np.int64)
-        np.cumsum(lens, out=qptr[1:])
-        total = int(qptr[-1])
-        if total:
-            src = torch.from_numpy(np.repeat(self.off_h[slots] - qptr[:-1], lens)).to(d) + \
-                torch.arange(total, dtype=torch.int64, device=d)
-            qi, qv = self.p_idx[src], self.p_val[src]
-        else:
-            qi = torch.zeros(1, dtype=torch.int32, device=d)
-            qv = torch.zeros(1, dtype=torch.float32, device=d)
-        qn2 = self.r_n2[torch.from_numpy(slots).to(d)]
-        return torch.from_numpy(qptr).to(d), qi, qv, qn2, total
-
 
 class InvertedIndex:
     """Exact sparse similarity (inverted_index: cosine; inverted_index_euclid:
@@ -601,6 +607,7 @@ class InvertedIndex:
         self.gpu = device is not None
         self.rows: dict[int, tuple[np.ndarray, np.ndarray]] = {}
         self.pool = DevicePool(device) if self.gpu else None
+        self._direct = None
 
     def clear(self) -> None:
         self.rows.clear()
@@ -651,10 +658,30 @@ class InvertedIndex:
                           val[:int(row_ptr[n])])
         return True
 
+    def _direct_pairs(self, r, similar: bool):
+        out = _pairs(r[0], r[1])
+        if similar:
+            out = [[(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in x] for x in out]
+        return out
+
+    def _bufs(self):
+        if self._direct is None:
+            from ..ops import hip
+            self._direct = hip.DirectQueryBuffers(self.device, 1)
+        return self._direct
+
     def query_direct(self, idx, val, row_ptr, nq: int, nrows: int, k: int,
                      similar: bool) -> list[list[tuple[int, float]]] | None:
         if not (self.gpu and nrows > 0 and k > 0):
             return None
+        from ..ops import hip
+        if nq <= hip.POOL_MAX_Q and k <= hip.TOPK_MAX_K:
+            r = hip.pool_query_direct(self.pool, nrows, 1 if self.euclid else 0, k, self._bufs(),
+                                      idx=np.ascontiguousarray(idx, np.int32),
+                                      val=np.ascontiguousarray(val, np.float32),
+                                      row_ptr=np.ascontiguousarray(row_ptr, np.int64), nq=nq)
+            if r is not None:
+                return self._direct_pairs(r, similar)
         rp = np.asarray(row_ptr[:nq + 1], np.int64)
         return self._query_batches(
             lambda a, b: self._queries_csr(rp[a:b + 1] - rp[a], idx[rp[a]:rp[b]], val[rp[a]:rp[b]]),
@@ -667,7 +694,8 @@ class InvertedIndex:
     def _queries_csr(self, rp, idx, val):
         """host query CSR (may hold idx < 0 / repeats) -> device queries,
         one async H2D through the pool's pinned stager"""
-        lens, qi, qv, qn2 = normalize_csr(rp, idx, val)
+        from .._native import native
+        lens, qi, qv, qn2 = native().csr_normalize(rp, idx, val)
         qptr = np.zeros(lens.size + 1, dtype=np.int64)
         np.cumsum(lens, out=qptr[1:])
         if qi.size == 0:
@@ -689,7 +717,7 @@ class InvertedIndex:
         qptr, qi, qv, qn2, total = q
         if total > hip.POOL_MAX_Q_ENTRIES:
             raise ValueError("query batch has more than 4096 features")
-        hip.pool_scan(qptr, qi, qv, qn2, nq, self.pool, nrows, metric, out)
+        hip.pool_scan(qptr, qi, qv, qn2, nq, self.pool, nrows, metric, out, qtotal=total)
         return out
 
     def _query_batches(self, make, n: int, nrows: int, k: int, similar: bool):
@@ -707,6 +735,14 @@ class InvertedIndex:
 
     def _topk(self, sc, nq: int, nrows: int, k: int, similar: bool):
         from ..ops import hip
+        if k <= hip.TOPK_MAX_K and nq <= hip.QUERY_MAX:
+            # latency path: result lands in pinned host memory
+            d, i = hip.topk_scores_direct(sc, nq, nrows, k, not self.euclid, self._bufs())
+            self.pool.stager().synced()
+            out = _pairs(d, i)
+            if similar:
+                out = [[(j, float(-dd if self.euclid else 1.0 - dd)) for j, dd in r] for r in out]
+            return out
         if k <= hip.TOPK_MAX_K:
             d, i = hip.topk_scores(sc, nq, nrows, k, flip=not self.euclid)
         else:       # wider than the fused top-k: torch.topk on the score matrix
@@ -767,6 +803,13 @@ class InvertedIndex:
         if self.gpu:
             if nrows <= 0 or k <= 0:
                 return [[] for _ in slots]
+            from ..ops import hip
+            if len(slots) <= hip.POOL_MAX_Q and k <= hip.TOPK_MAX_K:
+                r = hip.pool_query_direct(self.pool, nrows, 1 if self.euclid else 0, k,
+                                          self._bufs(), slots=np.asarray(slots, np.int32),
+                                          nq=len(slots))
+                if r is not None:
+                    return self._direct_pairs(r, similar)
             return self._query_batches(lambda a, b: self.pool.query_slots_device(slots[a:b]),
                                        len(slots), nrows, k, similar)
         return self.query([self.rows.get(int(s), (np.zeros(0, np.int32), np.zeros(0, np.float32)))

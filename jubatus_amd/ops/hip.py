@@ -56,6 +56,12 @@ _SIGS = {
                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_lsh_set_rows_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _u64, _i32,
                                _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_pool_query_direct": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
+                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p,
+                             _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
+                             _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_topk_scores_direct": [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p],
     "jb_topk_direct_query": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32,
                             _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                             _c_void_p, _c_void_p],
@@ -68,8 +74,9 @@ _SIGS = {
                               _i32, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                               _c_void_p],
-    "jb_pool_scan": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
-                     _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p],
+    "jb_pool_scan": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p,
+                     _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p, _c_void_p, _i32, _i32,
+                     _c_void_p, _c_void_p],
     "jb_pool_append": [_c_void_p, _i32, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _c_void_p],
     "jb_lof_insert": [_i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
@@ -205,9 +212,10 @@ def pool_scan(qptr, qidx, qval, qn2, nq: int, pool, nrows: int, metric: int, out
               qslots=None, qtotal: int = 0) -> None:
     """[nq, nrows] cosine similarity (metric 0) / euclidean distance (1) of
     nq sorted sparse queries vs the rows of ``pool`` (models/similarity.py
-    DevicePool). Queries are a device CSR (qptr, qidx, qval, qn2) or, with
-    ``qslots`` (device int32 [nq]), stored rows taken from the pool
-    (``qtotal`` = their total length, checked against the LDS capacity)."""
+    DevicePool), one pass over the pool. Queries are a device CSR (qptr,
+    qidx, qval, qn2 [nq] float64) or, with ``qslots`` (device int32 [nq]),
+    stored rows taken from the pool. ``qtotal`` = the queries' total entries
+    (sizes the kernel's LDS hash table; must be exact)."""
     if not 0 < nq <= POOL_MAX_Q:
         raise ValueError("pool_scan: 1..8 queries per pass")
     _dev(out, torch.float32, "out")
@@ -215,14 +223,20 @@ def pool_scan(qptr, qidx, qval, qn2, nq: int, pool, nrows: int, metric: int, out
         raise ValueError("pool_scan: bad operand shapes")
     if qslots is not None:
         _dev(qslots, torch.int32, "qslots")
-        if qslots.numel() < nq or qtotal > POOL_MAX_Q_ENTRIES:
+        if qslots.numel() < nq:
             raise ValueError("pool_scan: bad query slots")
         qptr = qidx = qval = qn2 = None
-    elif qptr.numel() < nq + 1:
-        raise ValueError("pool_scan: bad operand shapes")
-    rc = _fn("jb_pool_scan")(_p(qptr), _p(qidx), _p(qval), _p(qn2), _p(qslots), nq,
+    else:
+        _dev(qn2, torch.float64, "qn2")
+        if qptr.numel() < nq + 1 or qidx.numel() < qtotal or qval.numel() < qtotal or \
+                qn2.numel() < nq:
+            raise ValueError("pool_scan: bad operand shapes")
+    if not 0 <= qtotal <= POOL_MAX_Q_ENTRIES:
+        raise ValueError("pool_scan: more than 4096 query entries")
+    rc = _fn("jb_pool_scan")(_p(qptr), _p(qidx), _p(qval), _p(qn2), _p(qslots), nq, qtotal,
                              _p(pool.r_off), _p(pool.r_len), _p(pool.r_n2), _p(pool.valid), nrows,
-                             _p(pool.p_idx), _p(pool.p_val), metric, _p(out), _stream())
+                             _p(pool.p_idx), _p(pool.p_val), metric, pool.lanes_per_row(),
+                             _p(out), _stream())
     _check(rc, "jb_pool_scan")
 
 
@@ -627,6 +641,65 @@ def lsh_query_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, nq: int, hash
     if rc == 1:
         return None
     _check(rc, "jb_lsh_query_direct")
+    d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
+    i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
+    return d, i
+
+
+def topk_scores_direct(scores, nq: int, nrows: int, k: int, flip: bool,
+                       bufs: DirectQueryBuffers):
+    """exact top-k smallest of a [nq, nrows] score matrix (flip: 1 - score)
+    -> (dist [nq, k], row [nq, k]) numpy; sampled threshold + collect + final
+    merge written to pinned host memory and waited for (csrc/hip/topk.hip
+    jb_topk_scores_direct)"""
+    import numpy as np
+    if not (0 < k <= TOPK_MAX_K and 0 < nq <= QUERY_MAX):
+        raise ValueError("topk_scores_direct: k / nq out of range")
+    _dev(scores, torch.float32, "scores")
+    if scores.numel() < nq * nrows:
+        raise ValueError("topk_scores_direct: bad operand shapes")
+    sd, si = _topk_scratch(scores.device, _direct_scratch(nrows, k, nq))
+    rc = _fn("jb_topk_scores_direct")(_p(scores), 1 if flip else 0, nq, nrows, k, _p(sd), _p(si),
+                                      bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
+    _check(rc, "jb_topk_scores_direct")
+    d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
+    i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
+    return d, i
+
+
+def pool_query_direct(pool, nrows: int, metric: int, k: int, bufs: DirectQueryBuffers,
+                      idx=None, val=None, row_ptr=None, slots=None, nq: int = 0):
+    """latency path of the device inverted index (csrc/hip/sparse_pool.hip
+    jb_pool_query_direct): nq host queries - a hashed CSR (numpy int32 /
+    float32 / int64; normalized natively) or stored-row slots - scored with
+    the query in the kernel arguments, exact top-k returned from pinned
+    memory -> (dist [nq, k], row [nq, k]) numpy, or None when the query does
+    not fit the kernel arguments. Distances: euclidean, or 1 - cosine."""
+    import numpy as np
+    if not (0 < k <= TOPK_MAX_K and 0 < nq <= POOL_MAX_Q) or nrows <= 0:
+        return None
+    if nrows > pool.cap_rows:
+        raise ValueError("pool_query_direct: nrows beyond the pool")
+    sd, si = _topk_scratch(pool.device, _direct_scratch(nrows, k, nq))
+    scores = pool.score_scratch(nq * nrows)
+    if slots is not None:
+        slots = np.ascontiguousarray(slots, dtype=np.int32)
+        if slots.size < nq or int(slots.max()) >= pool.cap_rows or int(slots.min()) < 0:
+            raise ValueError("pool_query_direct: bad slots")
+        slen = np.ascontiguousarray(pool.len_h[slots], dtype=np.int64)
+        args = (None, None, None, slots.ctypes.data, slen.ctypes.data)
+    else:
+        if row_ptr.dtype != np.int64 or idx.dtype != np.int32 or val.dtype != np.float32 or \
+                row_ptr.size < nq + 1 or idx.size < row_ptr[nq] or val.size < row_ptr[nq]:
+            raise ValueError("pool_query_direct: bad query CSR")
+        args = (idx.ctypes.data, val.ctypes.data, row_ptr.ctypes.data, None, None)
+    rc = _fn("jb_pool_query_direct")(*args, nq, _p(pool.r_off), _p(pool.r_len), _p(pool.r_n2),
+                                     _p(pool.valid), nrows, _p(pool.p_idx), _p(pool.p_val),
+                                     metric, pool.lanes_per_row(), k, _p(scores), _p(sd), _p(si),
+                                     bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
+    if rc == 1:
+        return None
+    _check(rc, "jb_pool_query_direct")
     d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
     i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
     return d, i

@@ -328,3 +328,40 @@ def test_device_pool_updates_removals_compaction_match_host(euclid):
     b = c.query_slots(ids, 400, 5, similar=True)
     for x, y in zip(a, b):
         np.testing.assert_allclose([d for _, d in x], [d for _, d in y], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("euclid", [False, True])
+@pytest.mark.parametrize("k", [1, 10, 31, 128])
+def test_pool_direct_query_radix_topk_matches_exact(euclid, k):
+    """the latency path (query in the kernel arguments, then the two-level
+    radix-select top-k into pinned memory, csrc/hip/topk.hip) on a table
+    large enough to take it == the exact top-k of the scan's own scores, for
+    CSR queries and stored-row (slot) queries, 1 and several at once"""
+    import torch
+    from jubatus_amd.models.similarity import InvertedIndex
+    from jubatus_amd.ops import hip
+    n = 40000
+    g = InvertedIndex(euclid, dev())
+    rs = rows(n, seed=11)
+    g.set_rows(range(n), rs)
+    for s in range(0, n, 97):
+        g.remove(s)
+    qs = [rs[5], rows(1, seed=12)[0], rs[777]]
+    for nq in (1, 3):
+        rp, idx, val = __import__("jubatus_amd.models.similarity", fromlist=["_rows_to_csr"])._rows_to_csr(qs[:nq])
+        got = g.query_direct(idx.astype(np.int32), val, rp, nq, n, k, similar=False)
+        ref = g._query_batches(lambda a, b: g._queries_device(qs[a:b]), nq, n, k, similar=False)
+        for x, y in zip(got, ref):
+            assert [i for i, _ in x] == [i for i, _ in y]
+            np.testing.assert_allclose([d for _, d in x], [d for _, d in y], rtol=1e-6)
+        # the scan's scores themselves, against torch.topk
+        sc = g.scores_device(qs[0], n)
+        dist = sc if euclid else (1.0 - sc)
+        dist = torch.where(torch.isfinite(sc), dist, torch.full_like(dist, float("inf")))
+        tv, ti = torch.topk(dist, k, largest=False, sorted=True)
+        np.testing.assert_allclose([d for _, d in got[0]], tv.cpu().numpy(), rtol=1e-6)
+    a = g.query_slots([5, 777], n, k, similar=True)
+    b = g._query_batches(lambda x, y: g.pool.query_slots_device([5, 777][x:y]), 2, n, k, True)
+    for x, y in zip(a, b):
+        assert [i for i, _ in x] == [i for i, _ in y]
+    assert hip.TOPK_MAX_K >= k

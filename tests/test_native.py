@@ -119,3 +119,21 @@ def test_pack_requests_has_no_side_effects_on_a_bad_batch():
     assert t.names() == ["old", "new1", "new2"]               # order of first appearance
     assert [t.count(i) for i in range(3)] == [1, 1, 3]
     assert lab[:5].tolist() == [0, 1, 2, 2, 2]
+
+
+def test_csr_normalize_matches_numpy():
+    """native per-row sort / merge / norm (query latency path) == the numpy
+    normalize_csr of models/similarity.py"""
+    import numpy as np
+    from jubatus_amd._native import native
+    from jubatus_amd.models.similarity import normalize_csr
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 30, 50)
+    rp = np.zeros(51, np.int64)
+    np.cumsum(lens, out=rp[1:])
+    idx = rng.integers(-2, 40, int(rp[-1])).astype(np.int32)
+    val = rng.standard_normal(int(rp[-1])).astype(np.float32)
+    a = normalize_csr(rp, idx, val)
+    b = native().csr_normalize(rp, idx, val)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))

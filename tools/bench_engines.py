@@ -32,6 +32,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _log(msg: str) -> None:
+    print(f"[bench_engines {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _lat(fn, iters: int, warm: int = 5) -> dict:
     for _ in range(warm):
         fn()
@@ -130,13 +134,15 @@ def bench_anomaly(args, dev) -> dict:
     B = 65536
     for b in range(0, N, B):
         lof.set_rows([(str(i), _datum(rng)) for i in range(b, min(N, b + B))])
+        _log(f"anomaly ingest {min(N, b + B)}/{N}")
     _sync(dev)
     ingest = N / (time.perf_counter() - t0)
     pool = [_datum(rng) for _ in range(4096)]
     it = iter(range(N, 10 ** 9))
     cold = _lat(lambda: lof.add(str(next(it)), pool[next(it) % 4096]), args.iters)
+    _log("anomaly cold adds done; building neighbour lists")
     t0 = time.perf_counter()
-    built = lof.build_lists()
+    built = lof.build_lists(progress=lambda d, t: _log(f"lists {d}/{t}"))
     _sync(dev)
     build_s = time.perf_counter() - t0
     add = _lat(lambda: lof.add(str(next(it)), pool[next(it) % 4096]), args.iters)

@@ -68,7 +68,14 @@ def main() -> None:
         q8 = idx._queries_device(q * 8)
         out["pool_scan_kernel_nq8"] = _p50(lambda: idx._scan(q8, 8, n), sync=sync)
         out["topk_scores_k31"] = _p50(lambda: hip.topk_scores(sc, 1, n, 31, flip=False), sync=sync)
-        out["query_csr_slot"] = _p50(lambda: idx.pool.query_csr([5]), sync=sync)
+        out["topk_scores_k10"] = _p50(lambda: hip.topk_scores(sc, 1, n, 10, flip=False), sync=sync)
+        db = hip.DirectQueryBuffers(dev, 1)
+        out["topk_scores_direct_k10"] = _p50(lambda: hip.topk_scores_direct(sc, 1, n, 10, False, db))
+        out["topk_scores_direct_k31"] = _p50(lambda: hip.topk_scores_direct(sc, 1, n, 31, False, db))
+        sc8 = idx._scan(q8, 8, n)
+        out["topk_scores_q8_k10"] = _p50(lambda: hip.topk_scores(sc8, 8, n, 10, flip=False),
+                                         sync=sync)
+        out["query_slots_device"] = _p50(lambda: idx.pool.query_slots_device([5]), sync=sync)
         out["pool_bytes_per_scan"] = int(idx.pool.live * 8 + n * 21)
     out["query_slot_lists_k31"] = _p50(lambda: lof.query_slot_lists([5], 31, False))
     out["query_fv_slots_k10"] = _p50(lambda: lof.query_fv_slots(q[0], 10, False))
