@@ -102,6 +102,14 @@ class LOF(RowEngine):
             self._st.moved([s])
         return ok
 
+    def _rows_changed(self, slots) -> None:
+        if self._st is None or not len(slots):
+            return
+        if len(slots) > 4096:
+            self._st.clear()
+        else:
+            self._st.moved(list(slots))
+
     def _set_many(self, items: list, bump: bool = True, update_weight: bool = True) -> None:
         super()._set_many(items, bump, update_weight)
         if self._st is None or not items:

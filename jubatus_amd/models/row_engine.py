@@ -59,6 +59,7 @@ class RowEngine:
         self.rows = RowStore()
         self.unlearner = Unlearner(unlearner, unlearner_parameter)
         self._lock = threading.RLock()
+        self._last_mix: dict = {}
         self._host_hasher = None
 
     # ------------------------------------------------------------ rows
@@ -338,6 +339,23 @@ class RowEngine:
             return {rid: self._results(r) for rid, r in zip(rids, res)}
 
     # ------------------------------------------------------------ MIX
+    def mix(self, group=None) -> int:
+        """collective MIX over the process group (parallel/row_mix.py: one
+        byte tensor per rank, RCCL / gloo all-gather, no pickling); returns
+        the bytes this rank contributed"""
+        from ..parallel.row_mix import row_mix
+        st = row_mix(self, group)
+        self._last_mix = st
+        return st["bytes"]
+
+    def pair_mix(self, peer: int, group=None) -> None:
+        """symmetric MIX with one peer (push mixers)"""
+        from ..parallel.row_mix import row_mix
+        self._last_mix = row_mix(self, group, peer=peer)
+
+    def _rows_changed(self, slots) -> None:
+        """rows rewritten by a MIX (hook: derived state such as LOF lists)"""
+
     def get_diff(self) -> dict:
         return self.rows.get_diff()
 
@@ -379,6 +397,9 @@ class RowEngine:
                 self.rows.version[rid] = v
 
     def get_status(self) -> dict[str, str]:
-        return {"method": self.method, "num_rows": str(len(self.rows.slot_of)),
-                "storage": "hbm" if self.gpu else "host",
-                "unlearner": self.unlearner.kind or "none"}
+        st = {"method": self.method, "num_rows": str(len(self.rows.slot_of)),
+              "storage": "hbm" if self.gpu else "host",
+              "unlearner": self.unlearner.kind or "none"}
+        for k, v in self._last_mix.items():
+            st[f"mix.last_{k}"] = str(v)
+        return st

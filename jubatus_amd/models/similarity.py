@@ -195,6 +195,39 @@ class LshIndex:
         self.norms.index_copy_(0, st, norms)
         self.valid.index_fill_(0, st, 1)
 
+    # MIX (parallel/row_mix.py): signatures travel as they are in the table
+    def export_signatures(self, slots: np.ndarray):
+        if self.gpu:
+            import torch
+            s = torch.as_tensor(np.asarray(slots, np.int64), device=self.device)
+            return self.bits.index_select(0, s), self.norms.index_select(0, s)
+        s = np.asarray(slots, np.int64)
+        return self.bits[s].view(np.int64), self.norms[s]
+
+    def import_signatures(self, slots: np.ndarray, bits, norms) -> None:
+        n = int(np.asarray(slots).size)
+        if n == 0:
+            return
+        need = int(np.max(slots)) + 1
+        if need > self.cap:
+            c = self.cap
+            while c < need:
+                c *= 2
+            self._alloc(c)
+        if self.gpu:
+            import torch
+            st = torch.as_tensor(np.asarray(slots, np.int64), device=self.device)
+            self.bits.index_copy_(0, st, bits.to(self.device).view(torch.int64).reshape(n, self.words))
+            self.norms.index_copy_(0, st, norms.to(self.device).view(torch.float32))
+            self.valid.index_fill_(0, st, 1)
+            return
+        b = bits.cpu().numpy() if hasattr(bits, "cpu") else np.asarray(bits)
+        nm = norms.cpu().numpy() if hasattr(norms, "cpu") else np.asarray(norms)
+        s = np.asarray(slots, np.int64)
+        self.bits[s] = b.reshape(n, self.words).view(np.uint64)
+        self.norms[s] = nm
+        self.valid[s] = 1
+
     def set_rows_direct(self, slots: np.ndarray, row_ptr: np.ndarray, idx: np.ndarray,
                         val: np.ndarray) -> bool:
         """latency path of set_row / update_row: one launch, the rows in the
