@@ -891,6 +891,54 @@ __global__ __launch_bounds__(1024) void radix_select_kernel(const uint32_t* __re
 
 }  // namespace jb
 
+namespace jb {
+
+// exact top-k of a small candidate set by ranking: every candidate's final
+// position is the number of candidates before it in (distance, row) order;
+// more than kRankMax candidates (massive ties) -> retry on the tile path.
+constexpr int kRankMax = 4096;
+__global__ __launch_bounds__(1024) void topk_rank_final_kernel(
+    const float* __restrict__ cand_d, const int32_t* __restrict__ cand_i,
+    const int* __restrict__ count, int cap, int k, const float* __restrict__ thr,
+    float* __restrict__ out_d, int32_t* __restrict__ out_i, volatile uint32_t* done,
+    uint32_t seq) {
+  __shared__ float s_d[kRankMax];
+  __shared__ int32_t s_i[kRankMax];
+  const int q = blockIdx.x;
+  const int t = threadIdx.x;
+  const int c_all = count[q];
+  const bool over = c_all > kRankMax || c_all > cap;
+  const int nc = over ? 0 : c_all;
+  for (int j = t; j < nc; j += blockDim.x) {
+    s_d[j] = cand_d[(int64_t)q * cap + j];
+    s_i[j] = cand_i[(int64_t)q * cap + j];
+  }
+  for (int j = nc + t; j < k; j += blockDim.x) {          // fewer candidates than k: padding
+    out_d[(int64_t)q * k + j] = INFINITY;
+    out_i[(int64_t)q * k + j] = INT_MAX;
+  }
+  __syncthreads();
+  for (int j = t; j < nc; j += blockDim.x) {
+    const float d = s_d[j];
+    const int32_t id = s_i[j];
+    int rank = 0;
+    for (int x = 0; x < nc; ++x) {
+      const float e = s_d[x];
+      rank += (e < d) || (e == d && s_i[x] < id);
+    }
+    if (rank < k) {
+      out_d[(int64_t)q * k + rank] = d;
+      out_i[(int64_t)q * k + rank] = id;
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  const bool retry = over || (c_all < k && thr[q] < INFINITY);
+  if (t == 0) done[q] = retry ? (seq | kTopRetry) : seq;
+}
+
+}  // namespace jb
+
 static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, bool radix,
                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
@@ -932,7 +980,7 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   if (cblocks > 1024) cblocks = 1024;
   hipLaunchKernelGGL(jb::topk_collect_kernel<1>, dim3((unsigned)cblocks, nq), dim3(256), 0, stream,
                      s, nrows, thr, kCandCap, cand_d, cand_i, count);
-  hipLaunchKernelGGL(jb::topk_final_kernel, dim3(nq), dim3(1024), 0, stream, cand_d, cand_i,
+  hipLaunchKernelGGL(jb::topk_rank_final_kernel, dim3(nq), dim3(1024), 0, stream, cand_d, cand_i,
                      count, kCandCap, k, thr, out_d_host, out_i_host,
                      (volatile uint32_t*)done_host, seq);
   return (int)hipGetLastError();

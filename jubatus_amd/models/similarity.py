@@ -14,6 +14,7 @@ splitmix64 hyperplane coefficients, same distance formulas).
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Sequence
 
 import numpy as np
@@ -541,12 +542,19 @@ class DevicePool:
             self._scores = torch.empty(max(n, 1 << 16), dtype=torch.float32, device=self.device)
         return self._scores
 
-    def lanes_per_row(self) -> int:
-        """scan lanes per row from the mean run length: one lane walks a
-        short row alone, text-like rows get 4 / 16 lanes"""
+    def lanes_per_row(self, nq: int = 1) -> int:
+        """scan lanes per row from the mean run length (measured at 1M rows:
+        4 lanes beat 1 from ~12 entries per row for one query, 148 -> 104 us
+        at ~20; with 4+ queries per pass the per-entry work dominates and one
+        lane per row stays ahead up to ~24)"""
+        forced = os.environ.get("JUBATUS_POOL_LPR")
+        if forced in ("1", "4", "16"):
+            return int(forced)
         rows = max(1, self.nlive)
         mean = self.live / rows
-        return 1 if mean <= 24 else 4 if mean <= 96 else 16
+        if nq >= 4 and mean <= 24:
+            return 1
+        return 1 if mean <= 8 else 4 if mean <= 64 else 16
 
     def compact(self) -> None:
         """rewrite the live runs contiguously (device gather), dropping the
@@ -668,7 +676,8 @@ class InvertedIndex:
                      val: np.ndarray) -> None:
         slots = np.asarray(slots, dtype=np.int64)
         if self.gpu:
-            lens, ni, nv, n2 = normalize_csr(row_ptr, idx, val)
+            from .._native import native
+            lens, ni, nv, n2 = native().csr_normalize(row_ptr[:slots.size + 1], idx, val)
             self.pool.append(slots, lens, ni, nv, n2)
             return
         rows = [(idx[row_ptr[i]:row_ptr[i + 1]], val[row_ptr[i]:row_ptr[i + 1]])

@@ -235,7 +235,7 @@ def pool_scan(qptr, qidx, qval, qn2, nq: int, pool, nrows: int, metric: int, out
         raise ValueError("pool_scan: more than 4096 query entries")
     rc = _fn("jb_pool_scan")(_p(qptr), _p(qidx), _p(qval), _p(qn2), _p(qslots), nq, qtotal,
                              _p(pool.r_off), _p(pool.r_len), _p(pool.r_n2), _p(pool.valid), nrows,
-                             _p(pool.p_idx), _p(pool.p_val), metric, pool.lanes_per_row(),
+                             _p(pool.p_idx), _p(pool.p_val), metric, pool.lanes_per_row(nq),
                              _p(out), _stream())
     _check(rc, "jb_pool_scan")
 
@@ -695,7 +695,7 @@ def pool_query_direct(pool, nrows: int, metric: int, k: int, bufs: DirectQueryBu
         args = (idx.ctypes.data, val.ctypes.data, row_ptr.ctypes.data, None, None)
     rc = _fn("jb_pool_query_direct")(*args, nq, _p(pool.r_off), _p(pool.r_len), _p(pool.r_n2),
                                      _p(pool.valid), nrows, _p(pool.p_idx), _p(pool.p_val),
-                                     metric, pool.lanes_per_row(), k, _p(scores), _p(sd), _p(si),
+                                     metric, pool.lanes_per_row(nq), k, _p(scores), _p(sd), _p(si),
                                      bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
     if rc == 1:
         return None

@@ -77,6 +77,31 @@ def main() -> None:
                                          sync=sync)
         out["query_slots_device"] = _p50(lambda: idx.pool.query_slots_device([5]), sync=sync)
         out["pool_bytes_per_scan"] = int(idx.pool.live * 8 + n * 21)
+    # recommender default-config latency path, stage by stage
+    import msgpack
+    import numpy as np
+    from jubatus_amd.models.recommender import Recommender
+    with open(os.path.join(ROOT, "config", "recommender", "default.json")) as f:
+        rcfg = json.load(f)
+    rec = Recommender(rcfg["method"], rcfg.get("parameter", {}),
+                      DatumToFvConverter(rcfg["converter"]), dev)
+    for b in range(0, args.rows, 65536):
+        rec.set_rows([(f"r{i}", _datum(rng)) for i in range(b, min(args.rows, b + 65536))])
+    dq = as_datum(_datum(rng))
+    h = rec._hasher()
+    body = msgpack.packb([dq.to_msgpack()], use_bin_type=False)
+    hi = np.empty(256, np.int32)
+    hv = np.empty(256, np.float32)
+    hr = np.zeros(2, np.int64)
+    out["rec_hash_datum"] = _p50(lambda: h.hash([body], hi.ctypes.data, hv.ctypes.data,
+                                                  hr.ctypes.data, 1, 256, False))
+    h.hash([body], hi.ctypes.data, hv.ctypes.data, hr.ctypes.data, 1, 256, False)
+    nr = rec.rows.nslots
+    out["rec_index_query_direct_k10"] = _p50(lambda: rec.index.query_direct(hi, hv, hr, 1, nr, 10, True))
+    out["rec_similar_row_from_datum_k10"] = _p50(lambda: rec.similar_row_from_datum(dq, 10))
+    it2 = iter(range(10 ** 9))
+    out["rec_update_row"] = _p50(lambda: rec.update_row(f"u{next(it2) % 5000}", _datum(rng)))
+    out["rec_datum_gen"] = _p50(lambda: _datum(rng))
     out["query_slot_lists_k31"] = _p50(lambda: lof.query_slot_lists([5], 31, False))
     out["query_fv_slots_k10"] = _p50(lambda: lof.query_fv_slots(q[0], 10, False))
     lof.build_lists() if n <= 200_000 else None
