@@ -45,6 +45,160 @@ __global__ __launch_bounds__(256) void sqdist_mfma_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Coreset construction and Lloyd on one workgroup (bucket-sized problems:
+// bucket_size 1000 x a few hundred dims). A bucket is far too small to fill
+// the chip, and the host path's cost is not the arithmetic but the round
+// trip per k-means++ draw / per Lloyd iteration; here every draw and every
+// iteration stays on the device, one launch each, no host sync in between.
+
+constexpr int kClBlock = 1024;
+
+// squared distance of row i to row c of X (d dims)
+__device__ __forceinline__ float cl_dist2(const float* __restrict__ X, int64_t i, int64_t c, int d) {
+  const float* a = X + i * d;
+  const float* b = X + c * d;
+  float s = 0.f;
+  for (int j = 0; j < d; ++j) {
+    const float t = a[j] - b[j];
+    s = fmaf(t, t, s);
+  }
+  return s;
+}
+
+// block-wide weighted draw with Python's random.choices semantics
+// (bisect_right over the running sum of the weights at u * total): each
+// thread owns a contiguous chunk of rows; chunk sums are scanned in double.
+// Returns the index, or -1 when the weights sum to zero.
+__device__ int cl_draw(const float* __restrict__ wt, int n, double u, double* part, int* pick) {
+  const int t = threadIdx.x;
+  const int per = (n + kClBlock - 1) / kClBlock;
+  const int i0 = t * per, i1 = min(n, i0 + per);
+  double s = 0.0;
+  for (int i = i0; i < i1; ++i) s += (double)wt[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < kClBlock; o <<= 1) {       // inclusive scan of the chunk sums
+    const double x = t >= o ? part[t - o] : 0.0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  const double total = part[kClBlock - 1];
+  if (t == 0) *pick = -1;
+  __syncthreads();
+  if (total > 0.0) {
+    const double target = u * total;
+    double run = part[t] - s;                      // before my chunk
+    if (run <= target && target < part[t]) {
+      int r = i1 - 1;
+      for (int i = i0; i < i1; ++i) {
+        run += (double)wt[i];
+        if (run > target) { r = i; break; }
+      }
+      *pick = r;
+    }
+  }
+  __syncthreads();
+  int r = *pick;
+  if (r < 0 && total > 0.0) r = n - 1;             // u * total rounded onto the end
+  return r;
+}
+
+// k-means++ seeding: m draws (u: host-drawn uniforms, one per draw, as the
+// host path consumes its RNG). out[j] = chosen row, or status = 1 when every
+// remaining weight is zero (the host continues with its uniform fallback).
+__global__ __launch_bounds__(kClBlock) void kmeanspp_kernel(const float* __restrict__ X, int n,
+                                                            int d, const float* __restrict__ w,
+                                                            const double* __restrict__ u, int m,
+                                                            float* __restrict__ d2,
+                                                            float* __restrict__ prob,
+                                                            int32_t* __restrict__ out,
+                                                            int32_t* __restrict__ status) {
+  __shared__ double part[kClBlock];
+  __shared__ int pick;
+  const int t = threadIdx.x;
+  int c = cl_draw(w, n, u[0], part, &pick);
+  if (t == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
+  if (c < 0) return;
+  for (int i = t; i < n; i += kClBlock) d2[i] = cl_dist2(X, i, c, d);
+  __syncthreads();
+  for (int j = 1; j < m; ++j) {
+    for (int i = t; i < n; i += kClBlock) prob[i] = d2[i] * w[i];
+    __syncthreads();
+    c = cl_draw(prob, n, u[j], part, &pick);
+    if (c < 0) {
+      if (t == 0) { out[j] = -1; *status = 1 + j; }
+      return;
+    }
+    if (t == 0) out[j] = c;
+    for (int i = t; i < n; i += kClBlock) d2[i] = fminf(d2[i], cl_dist2(X, i, c, d));
+    __syncthreads();
+  }
+}
+
+// Weighted Lloyd iterations to convergence (|C' - C| <= atol + rtol |C|, as
+// torch.allclose) or `iters`, then the final assignment. C [k, d] in/out.
+__global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict__ X, int n, int d,
+                                                         const float* __restrict__ w,
+                                                         float* __restrict__ C, int k, int iters,
+                                                         float atol, float rtol,
+                                                         int32_t* __restrict__ assign,
+                                                         float* __restrict__ S,
+                                                         int32_t* __restrict__ done_iters) {
+  extern __shared__ float s_c[];                   // C [k][d] | S [k][d] | W [k]
+  float* s_s = s_c + (int64_t)k * d;
+  float* s_w = s_s + (int64_t)k * d;
+  __shared__ int changed;
+  const int t = threadIdx.x;
+  for (int i = t; i < k * d; i += kClBlock) s_c[i] = C[i];
+  __syncthreads();
+  int it = 0;
+  for (; it <= iters; ++it) {
+    // assignment (the last pass only assigns)
+    for (int i = t; i < n; i += kClBlock) {
+      const float* x = X + (int64_t)i * d;
+      int best = 0;
+      float bd = INFINITY;
+      for (int j = 0; j < k; ++j) {
+        float s = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float tt = x[q] - s_c[j * d + q];
+          s = fmaf(tt, tt, s);
+        }
+        if (s < bd) { bd = s; best = j; }
+      }
+      assign[i] = best;
+    }
+    if (it == iters) break;
+    for (int i = t; i < k * d; i += kClBlock) s_s[i] = 0.f;
+    for (int i = t; i < k; i += kClBlock) s_w[i] = 0.f;
+    if (t == 0) changed = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += kClBlock) {
+      const int a = assign[i];
+      const float wi = w[i];
+      atomicAdd(&s_w[a], wi);
+      const float* x = X + (int64_t)i * d;
+      for (int q = 0; q < d; ++q) atomicAdd(&s_s[a * d + q], wi * x[q]);
+    }
+    __syncthreads();
+    for (int i = t; i < k * d; i += kClBlock) {
+      const int j = i / d;
+      const float nc = s_w[j] > 0.f ? s_s[i] / fmaxf(s_w[j], 1e-12f) : s_c[i];
+      if (fabsf(nc - s_c[i]) > atol + rtol * fabsf(s_c[i])) changed = 1;
+      s_c[i] = nc;
+    }
+    __syncthreads();
+    if (!changed) {                                // converged: final assignment next
+      it = iters - 1;
+    }
+    __syncthreads();
+  }
+  for (int i = t; i < k * d; i += kClBlock) C[i] = s_c[i];
+  if (t == 0) *done_iters = it;
+}
+
 }  // namespace jb
 
 extern "C" int jb_sqdist_mfma(const float* X, int64_t n, const float* C, int k, int d,
@@ -52,5 +206,26 @@ extern "C" int jb_sqdist_mfma(const float* X, int64_t n, const float* C, int k, 
   if (n <= 0 || k <= 0) return 0;
   dim3 grid((unsigned)((n + 63) / 64), (unsigned)((k + 15) / 16));
   hipLaunchKernelGGL(jb::sqdist_mfma_kernel, grid, dim3(256), 0, stream, X, n, C, k, d, xn2, cn2, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jb_kmeanspp(const float* X, int n, int d, const float* w, const double* u, int m,
+                           float* d2, float* prob, int32_t* out, int32_t* status,
+                           hipStream_t stream) {
+  if (n <= 0 || m <= 0) return 0;
+  hipLaunchKernelGGL(jb::kmeanspp_kernel, dim3(1), dim3(jb::kClBlock), 0, stream, X, n, d, w, u, m,
+                     d2, prob, out, status);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jb_lloyd(const float* X, int n, int d, const float* w, float* C, int k, int iters,
+                        float atol, float rtol, int32_t* assign, float* S, int32_t* done_iters,
+                        hipStream_t stream) {
+  if (n <= 0 || k <= 0) return 0;
+  const size_t lds = sizeof(float) * (2 * (size_t)k * d + k);
+  if (lds > 64 * 1024) return -2;
+  (void)S;
+  hipLaunchKernelGGL(jb::lloyd_kernel, dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, k,
+                     iters, atol, rtol, assign, S, done_iters);
   return (int)hipGetLastError();
 }

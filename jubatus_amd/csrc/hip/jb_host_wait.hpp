@@ -49,6 +49,18 @@ inline int wait_flags_status(volatile uint32_t* done, int n, uint32_t seq, uint3
   return 0;
 }
 
+// spin until *flag != 0 (a kernel's final status store), then acquire
+inline int wait_nonzero(volatile uint32_t* flag, hipStream_t stream) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (*flag == 0) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2))
+      return (int)hipStreamSynchronize(stream);
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return 0;
+}
+
 inline uint32_t next_seq() {
   static std::atomic<uint32_t> g_seq{0};
   return g_seq.fetch_add(1, std::memory_order_relaxed) + 1;

@@ -24,6 +24,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "jb_host_wait.hpp"
+
 namespace jb {
 
 constexpr int kLofMaxK = 64;
@@ -38,9 +40,18 @@ __device__ __forceinline__ float lof_kth(const int32_t* s, const float* d, int k
   return kd;
 }
 
+// Candidate / target lists travel in the kernel arguments (latency path:
+// no H2D copy): up to kLofArgMax (slot, distance) pairs.
+constexpr int kLofArgMax = 128;
+struct LofArgs {
+  int32_t n, pad;
+  int32_t s[kLofArgMax];
+  float d[kLofArgMax];
+};
+
 // p's list from its candidates; candidates o take p in. One block of 64
 // threads; each thread's working copy of a list sits in LDS.
-__global__ __launch_bounds__(64) void lof_insert_kernel(
+__device__ __forceinline__ void lof_insert_body(
     int p, const int32_t* __restrict__ cs, const float* __restrict__ cd, int nc, int k,
     int ignore_same, int32_t* __restrict__ nb_slot, float* __restrict__ nb_dist,
     float* __restrict__ kdist, uint8_t* __restrict__ ok, uint8_t* __restrict__ lrd_ok,
@@ -98,6 +109,18 @@ __global__ __launch_bounds__(64) void lof_insert_kernel(
   }
   __syncthreads();
   if (threadIdx.x == 0) *nchanged = n_ch < kLofMaxChanged ? n_ch : kLofMaxChanged;
+}
+
+__global__ __launch_bounds__(64) void lof_add_kernel(
+    const LofArgs a, int p, int k, int ignore_same, int32_t* __restrict__ nb_slot,
+    float* __restrict__ nb_dist, float* __restrict__ kdist, uint8_t* __restrict__ ok,
+    uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged) {
+  __shared__ int32_t cs[kLofArgMax];
+  __shared__ float cd[kLofArgMax];
+  for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
+  __syncthreads();
+  lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
+                  nchanged);
 }
 
 // Every row listing a changed row: lrd_ok = 0 (and, clear_ok: ok = 0 -
@@ -191,7 +214,7 @@ __device__ __forceinline__ float lof_lrd(const int32_t* s, const float* d, int k
 // out = [status, score bits, lrd(q) bits, nmissing, missing slots...]:
 // (status published last, after a system-scope fence) status 1 = done, 2 = rows without a valid list (missing) - the host
 // installs their lists and runs the kernel again. One block.
-__global__ __launch_bounds__(64) void lof_score_kernel(
+__device__ __forceinline__ void lof_score_body(
     const int32_t* __restrict__ ts, const float* __restrict__ td, int nt, int k,
     const int32_t* __restrict__ nb_slot, const float* __restrict__ nb_dist,
     const float* __restrict__ kdist, const uint8_t* __restrict__ ok, float* __restrict__ lrd,
@@ -256,17 +279,21 @@ __global__ __launch_bounds__(64) void lof_score_kernel(
   *(volatile uint32_t*)&out[0] = 1u;
 }
 
-}  // namespace jb
-
-extern "C" int jb_lof_insert(int p, const int32_t* cs, const float* cd, int nc, int k,
-                             int ignore_same, int32_t* nb_slot, float* nb_dist, float* kdist,
-                             uint8_t* ok, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
-                             hipStream_t stream) {
-  if (k <= 0 || k > jb::kLofMaxK || nc > jb::kLofMaxChanged - 1) return -2;
-  hipLaunchKernelGGL(jb::lof_insert_kernel, dim3(1), dim3(64), 0, stream, p, cs, cd, nc, k,
-                     ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed, nchanged);
-  return (int)hipGetLastError();
+__global__ __launch_bounds__(64) void lof_score_kernel(
+    const LofArgs a, int k, const int32_t* __restrict__ nb_slot,
+    const float* __restrict__ nb_dist, const float* __restrict__ kdist,
+    const uint8_t* __restrict__ ok, float* __restrict__ lrd, uint8_t* __restrict__ lrd_ok,
+    int store_slot, uint32_t* __restrict__ out, int max_missing) {
+  __shared__ int32_t ts[kLofMaxK];
+  __shared__ float td[kLofMaxK];
+  const int nt = a.n < kLofMaxK ? a.n : kLofMaxK;
+  if ((int)threadIdx.x < nt) { ts[threadIdx.x] = a.s[threadIdx.x]; td[threadIdx.x] = a.d[threadIdx.x]; }
+  __syncthreads();
+  lof_score_body(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, store_slot, out,
+                 max_missing);
 }
+
+}  // namespace jb
 
 extern "C" int jb_lof_mark(int64_t nrows, int k, const int32_t* nb_slot, const int32_t* changed,
                            const int32_t* nchanged, int clear_ok, uint8_t* ok, uint8_t* lrd_ok,
@@ -290,12 +317,59 @@ extern "C" int jb_lof_set_lists(int n, const int32_t* slots, const int32_t* cs, 
   return (int)hipGetLastError();
 }
 
+namespace {
+int fill_args(jb::LofArgs* a, const int32_t* sl, const float* d, int n) {
+  if (n < 0 || n > jb::kLofArgMax) return -2;
+  a->n = n;
+  a->pad = 0;
+  for (int i = 0; i < n; ++i) { a->s[i] = sl[i]; a->d[i] = d[i]; }
+  return 0;
+}
+}  // namespace
+
+// One LOF add on the device (latency path): the candidates (rnn nearest of
+// p, ascending, p excluded; host arrays) go in the kernel arguments; p's
+// list is written and p enters its candidates' lists (lof_add_kernel), the
+// rows depending on a changed list are marked (lof_mark_kernel), then p is
+// scored from its k nearest (lof_score_kernel, lrd[p] stored). Waits for
+// the score; out_host = [status, score, lrd, nmissing, missing...].
+extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int k,
+                          int ignore_same, int64_t nrows, int32_t* nb_slot, float* nb_dist,
+                          float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
+                          int32_t* changed, int32_t* nchanged, uint32_t* out_host,
+                          int max_missing, hipStream_t stream) {
+  if (k <= 0 || k > jb::kLofMaxK) return -2;
+  jb::LofArgs a;
+  int rc = fill_args(&a, cs, cd, nc);
+  if (rc) return rc;
+  hipLaunchKernelGGL(jb::lof_add_kernel, dim3(1), dim3(64), 0, stream, a, p, k, ignore_same,
+                     nb_slot, nb_dist, kdist, ok, lrd_ok, changed, nchanged);
+  const unsigned blocks = (unsigned)((nrows + 255) / 256);
+  hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(blocks), dim3(256), 0, stream, nrows, k, nb_slot,
+                     changed, nchanged, 0, ok, lrd_ok);
+  a.n = nc < k ? nc : k;               // score from the k nearest
+  out_host[0] = 0;
+  hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist,
+                     kdist, ok, lrd, lrd_ok, p, out_host, max_missing);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return jb::wait_nonzero(out_host, stream);
+}
+
+// LOF of a point from its nt (<= 64) nearest (host arrays), lrd of the
+// targets refreshed; waits; same out_host layout
 extern "C" int jb_lof_score(const int32_t* ts, const float* td, int nt, int k,
                             const int32_t* nb_slot, const float* nb_dist, const float* kdist,
                             const uint8_t* ok, float* lrd, uint8_t* lrd_ok, int store_slot,
                             uint32_t* out_host, int max_missing, hipStream_t stream) {
   if (nt > 64 || k > jb::kLofMaxK) return -2;
-  hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, ts, td, nt, k, nb_slot,
-                     nb_dist, kdist, ok, lrd, lrd_ok, store_slot, out_host, max_missing);
-  return (int)hipGetLastError();
+  jb::LofArgs a;
+  int rc = fill_args(&a, ts, td, nt);
+  if (rc) return rc;
+  out_host[0] = 0;
+  hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist,
+                     kdist, ok, lrd, lrd_ok, store_slot, out_host, max_missing);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return jb::wait_nonzero(out_host, stream);
 }

@@ -430,6 +430,13 @@ class DatumToFvConverter:
             self.combination_rules.append((KeyMatcher(r["key_left"]), KeyMatcher(r["key_right"]),
                                            r["type"], ct[r["type"]]))
         self.uses_global_weight = any(r.gw != "bin" for r in self.string_rules)
+        # the common "every number as itself" config (clustering, anomaly,
+        # regression defaults): conversion is one comprehension
+        self._num_only = (not self.string_filters and not self.num_filters and
+                          not self.string_rules and not self.binary_rules and
+                          not self.combination_rules and len(self.num_rules) == 1 and
+                          self.num_rules[0].matcher.kind == "all" and
+                          self.num_rules[0].kind == "num" and self.num_rules[0].type_name == "num")
 
     # -------------------------------------------------------------- convert
     def _filtered(self, d: Datum) -> tuple[list, list]:
@@ -471,6 +478,8 @@ class DatumToFvConverter:
 
     def _convert(self, datum: Any, update: bool) -> list[tuple[str, float]]:
         d = as_datum(datum)
+        if self._num_only:
+            return [(f"{k}@num", x) for k, x in d.num_values]
         sv, nv = self._filtered(d)
         sfeat = self._string_features(sv)
         fv: list[tuple[str, float]] = []

@@ -48,6 +48,9 @@ class LOF(RowEngine):
         if self.k <= 0 or self.rnn < self.k:
             raise ValueError("nearest_neighbor_num must be > 0 and <= reverse_nearest_neighbor_num")
         self.ignore_kth_same = bool(p.get("ignore_kth_same_point", False))
+        if device is not None and self.rnn > 127:
+            # the device add carries the candidates in its kernel arguments
+            raise ValueError("reverse_nearest_neighbor_num must be <= 127 on the GPU")
         self.outer = method
         super().__init__(inner, dict(p.get("parameter") or {}), converter, device,
                          p.get("unlearner"), p.get("unlearner_parameter"))
@@ -90,9 +93,11 @@ class LOF(RowEngine):
             st.moved([s])
         (near,) = self.query_slot_lists([s], self.rnn + 1, similar=False)
         cs, cd = self._pairs([(o, d) for o, d in near if o != s][:self.rnn])
-        st.insert(s, cs, cd)
-        # the k nearest are the head of the rnn-nearest list (same query,
-        # rnn >= k): no second search
+        # insert + score in one device call; the k nearest are the head of
+        # the rnn-nearest list (same query, rnn >= k): no second search
+        sc, missing = st.add(s, cs, cd)
+        if sc is not None:
+            return sc
         return self._score_from(cs[:self.k], cd[:self.k], store=s)
 
     def _remove(self, rid: str, record: bool = True) -> bool:

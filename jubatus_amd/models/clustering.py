@@ -95,10 +95,12 @@ class Clustering:
         import torch
         return torch
 
-    # below this many matrix elements the coreset / Lloyd / EM steps run on
-    # the host: a bucket (1000 x a few hundred) is too small to amortise the
-    # launches and the host round trip each k-means++ draw needs
-    GPU_MIN_ELEMS = 1 << 22
+    # with a device every coreset / Lloyd / EM step runs in HBM: the k-means++
+    # draws and the Lloyd iterations of a bucket each run in ONE single-
+    # workgroup launch (csrc/hip/clustering.hip), so a 1000-point bucket no
+    # longer pays a host round trip per draw / iteration. (Set higher to keep
+    # small problems on the host.)
+    GPU_MIN_ELEMS = 0
 
     def _dense(self, pts: list[dict], dims: list[str], device=None):
         torch = self._t()
@@ -142,10 +144,20 @@ class Clustering:
         torch = self._t()
         n = X.shape[0]
         m = min(m, n)
-        first = rng.choices(range(n), weights=w.cpu().tolist(), k=1)[0]
-        chosen = [first]
-        d2 = self._sqdist(X, X[first:first + 1])[:, 0]
-        for _ in range(1, m):
+        chosen: list[int] = []
+        if X.is_cuda:
+            from ..ops import hip
+            # one uniform per draw, as the host path's random.choices uses
+            chosen, status = hip.kmeanspp(X.contiguous(), w.contiguous(),
+                                          [rng.random() for _ in range(m)], m)
+            if status == 0:
+                return chosen
+            chosen = chosen[:status - 1]      # zero mass left: finish on the host
+        if not chosen:
+            chosen = [rng.choices(range(n), weights=w.cpu().tolist(), k=1)[0]]
+        d2 = self._sqdist(X, X[chosen])
+        d2 = d2.min(1).values if d2.shape[1] > 1 else d2[:, 0]
+        for _ in range(len(chosen), m):
             prob = (d2 * w).cpu().numpy().astype(np.float64)
             s = prob.sum()
             if s <= 0:
@@ -173,7 +185,8 @@ class Clustering:
         reps = self._kmeanspp(X, w, m, self._rng)
         a = self._sqdist(X, X[reps]).argmin(1)
         wsum = torch.zeros(len(reps), dtype=torch.float32, device=X.device).index_add_(0, a, w)
-        return [(float(wsum[j]), pts[i][1], pts[i][2]) for j, i in enumerate(reps) if float(wsum[j]) > 0]
+        ws = wsum.cpu().tolist()
+        return [(ws[j], pts[i][1], pts[i][2]) for j, i in enumerate(reps) if ws[j] > 0]
 
     def _close_bucket(self) -> None:
         core = self._compress(self.pending, self.compressed)
@@ -203,7 +216,12 @@ class Clustering:
         w = torch.tensor([p[0] for p in pts], dtype=torch.float32, device=X.device)
         rng = random.Random(self.seed + self.revision)
         C = X[self._kmeanspp(X, w, self.k, rng)].clone()
-        for _ in range(100):
+        fused = None
+        if X.is_cuda:
+            from ..ops import hip
+            C = C.contiguous()
+            fused = hip.lloyd(X.contiguous(), w.contiguous(), C, 100, 1e-6, 1e-5)
+        for _ in range(0 if fused is not None else 100):
             a = self._sqdist(X, C).argmin(1)
             wsum = torch.zeros(C.shape[0], dtype=torch.float32, device=X.device).index_add_(0, a, w)
             S = torch.zeros_like(C).index_add_(0, a, X * w[:, None])
@@ -217,7 +235,10 @@ class Clustering:
             self.variances, self.mix_weights = var, pi
         self.centers, self.dims = C, dims
         self.core = pts
-        self.assign = self._assign(X).cpu().tolist()
+        if fused is not None and self.method == "kmeans":
+            self.assign = fused[0].cpu().tolist()    # the kernel's final assignment pass
+        else:
+            self.assign = self._assign(X).cpu().tolist()
         self.revision += 1
 
     def _log_resp(self, X, C, var, pi):

@@ -126,6 +126,12 @@ class HostLofState:
             changed.append(o)
         self._mark(changed, False)
 
+    def add(self, p: int, cs: np.ndarray, cd: np.ndarray, store: bool = True):
+        """insert p with its candidates, then score it from the k nearest
+        -> (score, []) or (None, missing)"""
+        self.insert(p, cs, cd)
+        return self.score(cs[:self.k], cd[:self.k], p if store else -1)
+
     def moved(self, slots) -> None:
         slots = [int(s) for s in slots]
         self.ensure(max(slots) + 1 if slots else 0)
@@ -256,14 +262,24 @@ class DeviceLofState:
         return [self._up_dev[o:o + n].view(torch.int32 if dt == np.int32 else torch.float32)
                 for o, n, dt in views]
 
-    def insert(self, p: int, cs: np.ndarray, cd: np.ndarray) -> None:
+    def _result(self):
+        o = self._out
+        if o[0] == 2:
+            nm = int(o[3])
+            return None, list(dict.fromkeys(o[4:4 + nm].tolist()))
+        if o[0] != 1:
+            raise RuntimeError("lof: kernel did not complete")
+        return float(o[1:2].view(np.float32)[0]), []
+
+    def add(self, p: int, cs: np.ndarray, cd: np.ndarray, store: bool = True):
+        """insert + mark + score of p in one host call (csrc/hip/lof.hip
+        jb_lof_add; candidates in the kernel arguments)"""
         from ..ops import hip
-        nc = int(cs.size)
-        if nc >= LOF_MAX_CHANGED:
-            cs, cd, nc = cs[:LOF_MAX_CHANGED - 1], cd[:LOF_MAX_CHANGED - 1], LOF_MAX_CHANGED - 1
-        ds, dd = self._upload(np.ascontiguousarray(cs, np.int32), np.ascontiguousarray(cd, np.float32))
-        hip.lof_insert(p, ds, dd, nc, self)
-        hip.lof_mark(self, False)
+        cs = np.ascontiguousarray(cs[:128], np.int32)
+        cd = np.ascontiguousarray(cd[:128], np.float32)
+        hip.lof_add(p, cs, cd, self, self._outbuf, LOF_MAX_MISSING)
+        self._pos = 0
+        return self._result()
 
     def moved(self, slots) -> None:
         slots = np.asarray(slots, np.int32)
@@ -300,23 +316,9 @@ class DeviceLofState:
 
     def score(self, ts: np.ndarray, td: np.ndarray, store: int = -1):
         from ..ops import hip
-        nt = int(ts.size)
-        if nt == 0:
+        if int(ts.size) == 0:
             return 1.0, []
-        dts, dtd = self._upload(np.ascontiguousarray(ts, np.int32), np.ascontiguousarray(td, np.float32))
-        o = self._out
-        o[0] = 0
-        hip.lof_score(dts, dtd, nt, self, store, self._outbuf, LOF_MAX_MISSING)
-        # the kernel stores status last (release): spin briefly, then block
-        t_end = time.perf_counter() + 0.002
-        while o[0] == 0 and time.perf_counter() < t_end:
-            pass
-        if o[0] == 0:
-            self.torch.cuda.current_stream(self.device).synchronize()
+        hip.lof_score(np.ascontiguousarray(ts, np.int32), np.ascontiguousarray(td, np.float32),
+                      self, store, self._outbuf, LOF_MAX_MISSING)
         self._pos = 0
-        if o[0] == 2:
-            nm = int(o[3])
-            return None, list(dict.fromkeys(o[4:4 + nm].tolist()))
-        if o[0] != 1:
-            raise RuntimeError("lof_score: kernel did not complete")
-        return float(o[1:2].view(np.float32)[0]), []
+        return self._result()

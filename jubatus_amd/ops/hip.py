@@ -79,8 +79,9 @@ _SIGS = {
                      _c_void_p, _c_void_p],
     "jb_pool_append": [_c_void_p, _i32, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p, _c_void_p, _c_void_p],
-    "jb_lof_insert": [_i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
-                      _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_lof_add": [_i32, _c_void_p, _c_void_p, _i32, _i32, _i32, _i64, _c_void_p, _c_void_p,
+                   _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                   _i32, _c_void_p],
     "jb_lof_mark": [_i64, _i32, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                     _c_void_p],
     "jb_lof_set_lists": [_i32, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _i32, _c_void_p,
@@ -88,6 +89,10 @@ _SIGS = {
                          _c_void_p],
     "jb_lof_score": [_c_void_p, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p],
+    "jb_kmeanspp": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
+                    _c_void_p, _c_void_p, _c_void_p],
+    "jb_lloyd": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _f32, _f32, _c_void_p,
+                 _c_void_p, _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
 }
@@ -107,6 +112,49 @@ def sqdist(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     rc = _fn("jb_sqdist_mfma")(_p(X), n, _p(C), k, d, _p(xn2), _p(cn2), _p(out), _stream())
     _check(rc, "jb_sqdist_mfma")
     return out
+
+
+def kmeanspp(X: torch.Tensor, w: torch.Tensor, u, m: int):
+    """k-means++ seeding of m rows of X [n, d] (weights w [n]) on one
+    workgroup (csrc/hip/clustering.hip), u: m host-drawn uniforms ->
+    (rows list, status): status 0 ok, j + 1 when draw j found zero mass"""
+    import numpy as np
+    _dev(X, torch.float32, "X")
+    _dev(w, torch.float32, "w")
+    n, d = X.shape
+    if w.numel() < n or len(u) < m or m <= 0:
+        raise ValueError("kmeanspp: bad operand shapes")
+    dev = X.device
+    ud = torch.from_numpy(np.asarray(u[:m], dtype=np.float64)).to(dev)
+    scratch = torch.empty(2 * n, dtype=torch.float32, device=dev)
+    out = torch.empty(m + 1, dtype=torch.int32, device=dev)
+    rc = _fn("jb_kmeanspp")(_p(X), n, d, _p(w), _p(ud), m, _p(scratch), scratch.data_ptr() + 4 * n,
+                            _p(out), out.data_ptr() + 4 * m, _stream())
+    _check(rc, "jb_kmeanspp")
+    o = out.cpu().tolist()
+    return o[:m], o[m]
+
+
+def lloyd(X: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: int, atol: float,
+          rtol: float):
+    """weighted Lloyd iterations on one workgroup until allclose(C', C) or
+    ``iters``; C [k, d] updated in place -> (assignment [n] device int32,
+    iterations run), or None when k x d does not fit the kernel's LDS"""
+    _dev(X, torch.float32, "X")
+    _dev(w, torch.float32, "w")
+    _dev(C, torch.float32, "C")
+    n, d = X.shape
+    k = C.shape[0]
+    if C.shape[1] != d or w.numel() < n:
+        raise ValueError("lloyd: bad operand shapes")
+    if 4 * (2 * k * d + k) > 64 * 1024:
+        return None
+    assign = torch.empty(n, dtype=torch.int32, device=X.device)
+    done = torch.empty(1, dtype=torch.int32, device=X.device)
+    rc = _fn("jb_lloyd")(_p(X), n, d, _p(w), _p(C), k, iters, atol, rtol, _p(assign), None,
+                         _p(done), _stream())
+    _check(rc, "jb_lloyd")
+    return assign, int(done.item())
 
 
 def signature(row_ptr, fidx, fval, n: int, hash_num: int, seed: int, mode: int, bits, norms) -> None:
@@ -256,17 +304,22 @@ def _lof_check(st, *slots) -> None:
             raise ValueError("lof: slot out of range")
 
 
-def lof_insert(p: int, cs, cd, nc: int, st) -> None:
-    """insert slot p with its nc nearest candidates (device int32 / fp32,
-    ascending) into the LOF lists of ``st`` (models/lof_state.py
-    DeviceLofState); writes the changed rows to st._changed"""
+def lof_add(p: int, cs, cd, st, out: "HostBuffer", max_missing: int) -> None:
+    """one LOF add on the device (csrc/hip/lof.hip jb_lof_add): candidates
+    (host int32 / float32 arrays, the rnn nearest of p ascending, p excluded)
+    in the kernel arguments; insert + staleness mark + score of p, waited
+    for; ``out`` = [status, score, lrd, nmissing, missing...]"""
     _lof_check(st, p)
-    if cs.numel() < nc or cd.numel() < nc:
-        raise ValueError("lof_insert: bad operand shapes")
-    rc = _fn("jb_lof_insert")(p, _p(cs), _p(cd), nc, st.k, int(st.ignore_same), _p(st.nb_slot),
-                              _p(st.nb_dist), _p(st.kdist), _p(st.ok), _p(st.lrd_ok),
-                              _p(st._changed), _p(st._nchanged), _stream())
-    _check(rc, "jb_lof_insert")
+    nc = int(cs.size)
+    if nc > 128 or cd.size < nc or cs.dtype.itemsize != 4 or cd.dtype.itemsize != 4:
+        raise ValueError("lof_add: at most 128 int32 / float32 candidates")
+    if out.nbytes < 4 * (4 + max_missing):
+        raise ValueError("lof_add: output buffer too small")
+    rc = _fn("jb_lof_add")(p, cs.ctypes.data, cd.ctypes.data, nc, st.k, int(st.ignore_same),
+                           st.cap, _p(st.nb_slot), _p(st.nb_dist), _p(st.kdist), _p(st.ok),
+                           _p(st.lrd), _p(st.lrd_ok), _p(st._changed), _p(st._nchanged), out.ptr,
+                           max_missing, _stream())
+    _check(rc, "jb_lof_add")
 
 
 def lof_mark(st, clear_ok: bool) -> None:
@@ -286,16 +339,18 @@ def lof_set_lists(n: int, slots, cs, cd, kk: int, st) -> None:
     _check(rc, "jb_lof_set_lists")
 
 
-def lof_score(ts, td, nt: int, st, store: int, out: "HostBuffer", max_missing: int) -> None:
-    """LOF of one point from its nt nearest (device slot / distance) into
-    ``out`` = [status, score, lrd, nmissing, missing...] (pinned, int32)"""
-    if nt > 64 or ts.numel() < nt or td.numel() < nt:
-        raise ValueError("lof_score: 1..64 targets")
+def lof_score(ts, td, st, store: int, out: "HostBuffer", max_missing: int) -> None:
+    """LOF of one point from its nearest (host int32 slots / float32
+    distances, at most 64) into ``out`` = [status, score, lrd, nmissing,
+    missing...]; waited for"""
+    nt = int(ts.size)
+    if nt > 64 or td.size < nt or ts.dtype.itemsize != 4 or td.dtype.itemsize != 4:
+        raise ValueError("lof_score: at most 64 int32 / float32 targets")
     if store >= st.cap or out.nbytes < 4 * (4 + max_missing):
         raise ValueError("lof_score: bad operand shapes")
-    rc = _fn("jb_lof_score")(_p(ts), _p(td), nt, st.k, _p(st.nb_slot), _p(st.nb_dist),
-                             _p(st.kdist), _p(st.ok), _p(st.lrd), _p(st.lrd_ok), store, out.ptr,
-                             max_missing, _stream())
+    rc = _fn("jb_lof_score")(ts.ctypes.data, td.ctypes.data, nt, st.k, _p(st.nb_slot),
+                             _p(st.nb_dist), _p(st.kdist), _p(st.ok), _p(st.lrd), _p(st.lrd_ok),
+                             store, out.ptr, max_missing, _stream())
     _check(rc, "jb_lof_score")
 
 

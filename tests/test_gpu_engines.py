@@ -131,10 +131,10 @@ def test_sqdist_mfma_matches_fp32(n, k, d):
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4 * d)
 
 
-@pytest.mark.parametrize("gpu_min_elems", [0, None])
+@pytest.mark.parametrize("gpu_min_elems", [0, 1 << 40])
 def test_clustering_on_gpu_matches_cpu(gpu_min_elems):
-    """0: every step on the device (MFMA sqdist, torch on HBM); None: the
-    default size rule (this small problem runs on the host)"""
+    """0: every step on the device (single-workgroup k-means++ / Lloyd
+    kernels, MFMA sqdist); 1 << 40: the same engine kept on the host"""
     from jubatus_amd.models.clustering import Clustering
     p = {"k": 3, "compressor_method": "compressive_kmeans", "bucket_size": 90,
          "compressed_bucket_size": 30, "seed": 0}
@@ -143,12 +143,40 @@ def test_clustering_on_gpu_matches_cpu(gpu_min_elems):
     pts = [{"x": cx + r.gauss(0, 0.3), "y": cy + r.gauss(0, 0.3)}
            for i in range(180) for cx, cy in [[(0, 0), (8, 8), (-8, 8)][i % 3]]]
     g = Clustering("kmeans", p, DatumToFvConverter(conv), dev())
-    if gpu_min_elems is not None:
-        g.GPU_MIN_ELEMS = gpu_min_elems
+    g.GPU_MIN_ELEMS = gpu_min_elems
     g.push(pts)
     assert g.centers.is_cuda == (gpu_min_elems == 0)
     cs = sorted(tuple(round(v) for _, v in sorted(c.num_values)) for c in g.get_k_center())
     assert cs == sorted([(0, 0), (8, 8), (-8, 8)])
+
+
+@pytest.mark.parametrize("method", ["kmeans", "gmm"])
+def test_default_clustering_config_runs_on_device(method):
+    """config/clustering/{kmeans,gmm}.json (bucket_size 1000, compressed 100,
+    k 3): every bucket is compressed and reclustered in HBM; the device
+    engine draws the same k-means++ seeds from the same RNG as the host
+    engine, so both find the same centres"""
+    import json
+    import os
+    from helpers import ROOT
+    from jubatus_amd.models.clustering import Clustering
+    with open(os.path.join(ROOT, "config", "clustering", f"{method}.json")) as f:
+        cfg = json.load(f)
+    r = random.Random(1)
+    truth = [(0.0, 0.0, 0.0), (10.0, 10.0, 0.0), (-10.0, 10.0, 5.0)]
+    pts = [{"a": c[0] + r.gauss(0, 0.5), "b": c[1] + r.gauss(0, 0.5), "c": c[2] + r.gauss(0, 0.5)}
+           for i in range(3000) for c in [truth[i % 3]]]
+    g = Clustering(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]), dev())
+    h = Clustering(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]))
+    for b in range(0, 3000, 500):
+        g.push(pts[b:b + 500])
+        h.push(pts[b:b + 500])
+    assert g.centers.is_cuda and g.get_revision() == h.get_revision() == 3
+    got = sorted(tuple(round(v) for _, v in sorted(c.num_values)) for c in g.get_k_center())
+    assert got == sorted(tuple(round(x) for x in c) for c in truth)
+    ref = sorted(tuple(round(v, 2) for _, v in sorted(c.num_values)) for c in h.get_k_center())
+    got2 = sorted(tuple(round(v, 2) for _, v in sorted(c.num_values)) for c in g.get_k_center())
+    np.testing.assert_allclose(np.asarray(got2), np.asarray(ref), atol=0.05)
 
 
 @pytest.mark.parametrize("metric,k,nrows,nq", [(0, 10, 100_000, 3), (1, 10, 250_000, 2),

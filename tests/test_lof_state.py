@@ -178,16 +178,16 @@ def test_device_lof_state_matches_host(method):
 @pytest.mark.gpu
 def test_device_lof_exact_with_full_rnn():
     import torch
-    g = _lof(torch.device("cuda", 0), k=4, rnn=1000)
+    g = _lof(torch.device("cuda", 0), k=4, rnn=127)
     _run(g, _ops(11, n=80), check=_close)
 
 
 def test_device_bindings_present():
     """the device state's kernel wrappers exist (checked without a GPU)"""
     from jubatus_amd.ops import hip
-    for name in ("lof_insert", "lof_mark", "lof_set_lists", "lof_score", "pool_scan",
+    for name in ("lof_add", "lof_mark", "lof_set_lists", "lof_score", "pool_scan",
                  "pool_append"):
         assert callable(getattr(hip, name)), name
-    for name in ("jb_lof_insert", "jb_lof_mark", "jb_lof_set_lists", "jb_lof_score",
+    for name in ("jb_lof_add", "jb_lof_mark", "jb_lof_set_lists", "jb_lof_score",
                  "jb_pool_scan", "jb_pool_append"):
         assert name in hip._SIGS, name
