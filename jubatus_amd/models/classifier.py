@@ -760,8 +760,8 @@ class LinearClassifier:
             names = self.labels.names()
             meta = [[names, [int(self.labels.count(i)) for i in range(len(names))],
                      self.labels.alive()]]
-            dist.broadcast_object_list(meta, src=src)
-            names, counts, alive = meta[0]
+            from ..parallel import wire
+            names, counts, alive = wire.broadcast(meta[0], src)
             me = dist.get_rank()
             if me != src and apply:
                 self.labels.clear()
@@ -793,17 +793,11 @@ class LinearClassifier:
         import torch.distributed as dist
         with self._lock:
             self._drain()
+            from ..parallel import wire
             me = dist.get_rank()
-            mine = [self._live_labels()]
-            theirs = [None]
-            if me < peer:
-                dist.send_object_list(mine, dst=peer)
-                dist.recv_object_list(theirs, src=peer)
-                lists = [mine[0], theirs[0]]
-            else:
-                dist.recv_object_list(theirs, src=peer)
-                dist.send_object_list(mine, dst=peer)
-                lists = [theirs[0], mine[0]]
+            mine = self._live_labels()
+            theirs = wire.exchange(mine, peer)
+            lists = [mine, theirs] if me < peer else [theirs, mine]
             order: list[str] = []
             for lst in lists:
                 for n in lst:

@@ -108,8 +108,6 @@ def all_equal(value: int, device: torch.device | None = None, group=None) -> boo
 
 
 def all_gather_object(obj, group=None) -> list:
-    if not is_dist():
-        return [obj]
-    out = [None] * dist.get_world_size(group)
-    dist.all_gather_object(out, obj, group=group)
-    return out
+    """every rank's (msgpack-encodable) object, no pickling (parallel/wire.py)"""
+    from . import wire
+    return wire.all_gather(obj, group)

@@ -8,9 +8,11 @@ A driver supports one of:
   the GPU: label/row reconciliation + RCCL all-reduce mean of the HBM
   tables; models/classifier.py);
 * ``get_diff() / mix_diff(a, b) / put_diff(m)`` - the reference's
-  linear_mixable protocol, run as an all-gather of diffs, a fold in rank
-  order (the reference folds in arrival order, linear_mixer.cpp:455-485;
-  rank order makes it deterministic) and a local put_diff.
+  linear_mixable protocol, run as an all-gather of the msgpack-encoded diffs
+  (parallel/wire.py: bytes in a tensor, no pickling), a fold in rank order
+  (the reference folds in arrival order, linear_mixer.cpp:455-485; rank
+  order makes it deterministic) and a local put_diff. Row engines use their
+  own tensor MIX (parallel/row_mix.py).
 
 Model hand-over to an obsolete (newly joined) member: ``broadcast_from(src)``
 if the driver has it, else ``pack()`` / ``unpack()`` through a broadcast of
@@ -36,23 +38,14 @@ def linear_mix(driver: Any) -> dict:
     if hasattr(driver, "mix"):
         nbytes = int(driver.mix() or 0)
     elif hasattr(driver, "get_diff"):
-        dist = _dist()
+        from . import wire
         diff = driver.get_diff()
-        world = dist.get_world_size() if dist.is_initialized() else 1
-        diffs = [None] * world
-        if world > 1:
-            dist.all_gather_object(diffs, diff)
-        else:
-            diffs = [diff]
+        diffs = wire.all_gather(diff)          # msgpack bytes over the collective
         mixed = diffs[0]
         for d in diffs[1:]:
             mixed = driver.mix_diff(mixed, d)
         driver.put_diff(mixed)
-        try:
-            import pickle
-            nbytes = sum(len(pickle.dumps(d)) for d in diffs)
-        except Exception:  # noqa: BLE001
-            nbytes = 0
+        nbytes = len(wire.encode(diff))
     else:
         raise UnsupportedMixables(f"{type(driver).__name__} is not mixable")
     return {"bytes": nbytes, "seconds": time.perf_counter() - t0}
@@ -65,10 +58,10 @@ def broadcast_model(driver: Any, src: int, apply: bool = True) -> None:
     if hasattr(driver, "broadcast_from"):
         driver.broadcast_from(src, apply=apply)
         return
-    box = [driver.pack() if dist.get_rank() == src else None]
-    dist.broadcast_object_list(box, src=src)
+    from . import wire
+    model = wire.broadcast(driver.pack() if dist.get_rank() == src else None, src)
     if dist.get_rank() != src and apply:
-        driver.unpack(box[0])
+        driver.unpack(model)
 
 
 def pair_exchange(driver: Any, peer: int) -> None:
@@ -83,16 +76,8 @@ def pair_exchange(driver: Any, peer: int) -> None:
         return
     if not hasattr(driver, "get_diff"):
         raise UnsupportedMixables(f"{type(driver).__name__} is not push-mixable")
+    from . import wire
     mine = driver.get_diff()
-    out = [mine]
-    inb = [None]
-    # lower rank sends first: matched send/recv order on both sides
-    if me < peer:
-        dist.send_object_list(out, dst=peer)
-        dist.recv_object_list(inb, src=peer)
-    else:
-        dist.recv_object_list(inb, src=peer)
-        dist.send_object_list(out, dst=peer)
-    theirs = inb[0]
+    theirs = wire.exchange(mine, peer)     # lower rank sends first
     mixed = driver.mix_diff(mine, theirs) if me < peer else driver.mix_diff(theirs, mine)
     driver.put_diff(mixed)

@@ -105,7 +105,8 @@ class _FakeDist:
 
 
 def test_linear_mix_fold_order(monkeypatch):
-    monkeypatch.setattr(mixable, "_dist", lambda: _FakeDist(["1", "2", "3", "4"]))
+    from jubatus_amd.parallel import wire
+    monkeypatch.setattr(wire, "all_gather", lambda obj, group=None: ["1", "2", "3", "4"])
     d = _StringDriver()
     st = mixable.linear_mix(d)
     assert d.put == "(4+(3+(2+1)))"
@@ -121,3 +122,17 @@ def test_linear_mix_single_member():
 def test_unsupported_mixables():
     with pytest.raises(UnsupportedMixables):
         mixable.linear_mix(object())
+
+
+def test_wire_roundtrip_without_pickle(monkeypatch):
+    """driver diffs cross the model plane as msgpack (parallel/wire.py):
+    numpy values are converted, nothing is pickled"""
+    import pickle
+
+    import numpy as np
+    from jubatus_amd.parallel import wire
+    monkeypatch.setattr(pickle, "dumps", None)
+    obj = {"a": [1, 2.5, "x"], 3: {"n": np.float32(1.5), "v": np.arange(3)}, "b": b"\x00\x01"}
+    back = wire.decode(wire.encode(obj))
+    assert back == {"a": [1, 2.5, "x"], 3: {"n": 1.5, "v": [0, 1, 2]}, "b": b"\x00\x01"}
+    assert wire.all_gather(obj) == [obj]          # no process group: identity
