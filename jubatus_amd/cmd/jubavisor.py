@@ -25,7 +25,6 @@ import signal
 import subprocess
 import sys
 import threading
-import time
 
 from ..common import membership as mb
 from ..common.lock_service import CoordinatorClient

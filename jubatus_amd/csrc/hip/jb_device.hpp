@@ -92,7 +92,12 @@ struct Reader {
       case 0xd2: if (!need(4)) return false; *out = (double)(int32_t)be32(); return true;
       case 0xd3: if (!need(8)) return false; *out = (double)(int64_t)be64(); return true;
       case 0xca: { if (!need(4)) return false; uint32_t u = be32(); *out = (double)__uint_as_float(u); return true; }
-      case 0xcb: { if (!need(8)) return false; uint64_t u = be64(); *out = __longlong_as_double((long long)u); return true; }
+      case 0xcb: {
+        if (!need(8)) return false;
+        uint64_t u = be64();
+        *out = __longlong_as_double((long long)u);
+        return true;
+      }
       default: ok = false; return false;
     }
   }

@@ -212,7 +212,8 @@ __device__ __forceinline__ float lof_lrd(const int32_t* s, const float* d, int k
 // LOF of one point from its neighbours (ts, td: nt entries, ascending):
 // refreshes the stale lrd of those neighbours, writes to pinned host memory
 // out = [status, score bits, lrd(q) bits, nmissing, missing slots...]:
-// (status published last, after a system-scope fence) status 1 = done, 2 = rows without a valid list (missing) - the host
+// (status published last, after a system-scope fence) status 1 = done,
+// 2 = rows without a valid list (missing) - the host
 // installs their lists and runs the kernel again. One block.
 __device__ __forceinline__ void lof_score_body(
     const int32_t* __restrict__ ts, const float* __restrict__ td, int nt, int k,

@@ -552,7 +552,10 @@ __global__ __launch_bounds__(1024) void topk_final_kernel(const float* __restric
         for (int x = 0; x < M; ++x) {
           const int c = lane + 64 * x;
           if (c < kw) { m[x] = s_cd[c]; mi[x] = s_ci[c]; }
-          else if (c - kw + off < NW * kw && c - kw < 640 - kw) { m[x] = s_wd[c - kw + off]; mi[x] = s_wi[c - kw + off]; }
+          else if (c - kw + off < NW * kw && c - kw < 640 - kw) {
+            m[x] = s_wd[c - kw + off];
+            mi[x] = s_wi[c - kw + off];
+          }
           else { m[x] = INFINITY; mi[x] = INT_MAX; }
         }
         __builtin_amdgcn_wave_barrier();

@@ -70,7 +70,11 @@ struct MecabApi {
     lib = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     if (!lib) { *err = std::string("cannot load libmecab (") + path + "): " + dlerror(); return false; }
     bool ok = true;
-    auto sym = [&](const char* n) { void* p = dlsym(lib, n); if (!p) { ok = false; *err = std::string("libmecab lacks ") + n; } return p; };
+    auto sym = [&](const char* n) {
+      void* p = dlsym(lib, n);
+      if (!p) { ok = false; *err = std::string("libmecab lacks ") + n; }
+      return p;
+    };
     model_new2 = (void* (*)(const char*))sym("mecab_model_new2");
     model_destroy = (void (*)(void*))sym("mecab_model_destroy");
     model_new_tagger = (void* (*)(void*))sym("mecab_model_new_tagger");
@@ -93,7 +97,11 @@ struct Matcher {
   std::regex re;
   explicit Matcher(const std::string& s) {
     if (s == "*" || s.empty()) { kind = 0; }
-    else if (s.size() >= 2 && s.front() == '/' && s.back() == '/') { kind = 4; arg = s.substr(1, s.size() - 2); re = std::regex(arg); }
+    else if (s.size() >= 2 && s.front() == '/' && s.back() == '/') {
+      kind = 4;
+      arg = s.substr(1, s.size() - 2);
+      re = std::regex(arg);
+    }
     else if (s.back() == '*') { kind = 1; arg = s.substr(0, s.size() - 1); }
     else if (s.front() == '*') { kind = 2; arg = s.substr(1); }
     else { kind = 3; arg = s; }
@@ -220,8 +228,14 @@ jb_plugin* create(const char** keys, const char** values, int n) {
   }
   char* end = nullptr;
   const long ng = std::strtol(ngram.c_str(), &end, 10);
-  if (!end || *end || ng <= 0) { std::fprintf(stderr, "mecab_splitter: ngram must be a positive number\n"); return nullptr; }
-  if (base != "true" && base != "false") { std::fprintf(stderr, "mecab_splitter: base must be a boolean value\n"); return nullptr; }
+  if (!end || *end || ng <= 0) {
+    std::fprintf(stderr, "mecab_splitter: ngram must be a positive number\n");
+    return nullptr;
+  }
+  if (base != "true" && base != "false") {
+    std::fprintf(stderr, "mecab_splitter: base must be a boolean value\n");
+    return nullptr;
+  }
   if (inc.empty()) { std::fprintf(stderr, "mecab_splitter: include_features must not be empty\n"); return nullptr; }
   if (lib.empty()) {
     const char* env = std::getenv("JUBATUS_MECAB_LIB");

@@ -133,7 +133,11 @@ void run_conn(const std::string& host, int port, const std::string& method,
       jb::Cursor c{(const uint8_t*)rbuf.data(), (const uint8_t*)rbuf.data() + f};
       uint32_t n;
       double type, id;
-      if (!c.array(&n) || n != 4 || !c.number(&type) || !c.number(&id)) { r->error = "bad response"; close(fd); return; }
+      if (!c.array(&n) || n != 4 || !c.number(&type) || !c.number(&id)) {
+        r->error = "bad response";
+        close(fd);
+        return;
+      }
       if (*c.p != 0xc0) { r->error = "error response from server"; close(fd); return; }
       const auto now = Clock::now();
       r->lat_us.push_back(std::chrono::duration<double, std::micro>(now - sent[(uint32_t)id & 0xffff]).count());
@@ -163,7 +167,9 @@ int main(int argc, char** argv) {
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
   }
   if (!port || method.empty() || file.empty() || conns < 1 || depth < 1) {
-    fprintf(stderr, "usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]\n");
+    fprintf(stderr,
+            "usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH]"
+            " [-t SECONDS]\n");
     return 1;
   }
   std::ifstream ifs(file, std::ios::binary);

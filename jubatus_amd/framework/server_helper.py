@@ -19,7 +19,7 @@ from __future__ import annotations
 import os
 import threading
 import time
-from typing import Any, Callable
+from typing import Callable
 
 from .. import __version__
 from ..common import mprpc

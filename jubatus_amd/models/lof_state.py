@@ -31,7 +31,6 @@ lrd_ok[s] (lrd is current). Operations:
 from __future__ import annotations
 
 import math
-import time
 
 import numpy as np
 

@@ -90,7 +90,9 @@ def test_recommender(srv):
 
 
 def test_recommender_lru_unlearner(tmp_path):
-    cfg = '{"method": "inverted_index", "parameter": {"unlearner": "lru", "unlearner_parameter": {"max_size": 3}}, "converter": {"num_rules": [{"key": "*", "type": "num"}]}}'
+    cfg = ('{"method": "inverted_index", "parameter": {"unlearner": "lru", '
+           '"unlearner_parameter": {"max_size": 3}}, '
+           '"converter": {"num_rules": [{"key": "*", "type": "num"}]}}')
     h = start_standalone("recommender", cfg, tmp_path)
     try:
         with Recommender("127.0.0.1", h.argv.port, "") as c:

@@ -211,3 +211,22 @@ def test_native_jubavisor_rpc_errors_and_shutdown(coord, tmp_path, monkeypatch):
     assert ls.list(mb.JUBAVISOR_BASE_PATH) == []
     ls.close()
     assert rc == 0
+
+
+def test_codestyle_clean():
+    """tools/codestyle.py (include guards, whitespace, line length, unused
+    imports) finds nothing in the tree"""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "codestyle.py")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+
+
+def test_man_pages_current():
+    """man/*.{1,8} are rendered from the tools' own --help (tools/gen_man.py)"""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gen_man.py"), "--check"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr

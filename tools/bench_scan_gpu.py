@@ -7,7 +7,6 @@ Usage: python tools/bench_scan_gpu.py [nreq] [per_request]
 import os
 import random
 import sys
-import time
 
 import numpy as np
 import torch
