@@ -287,6 +287,120 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   }
 }
 
+// Several queries per table pass (MODE 0, W <= 2 signature words): a block
+// loads each tile's signatures / norms / valid flags ONCE into registers and
+// runs the threshold-pruned selection of every query against them, each
+// query with its own carry in LDS. The single-query kernel's grid is
+// (blocks, nq): every query re-reads the whole table (8 queries at 10M rows
+// moved 4x the table through HBM, profiles/r02_pmc_*); here the table is
+// read once per batch of queries. Output layout as topk_kernel's.
+// Measured (profiles/r02_pmc_roofline.md, 10M rows, 8 queries, k 10): the
+// table traffic drops from 4x to 1x (63 MiB) but the kernel takes 686 us
+// vs 336 us for the (blocks, nq) grid - the queries' selections serialize
+// inside a block and the re-reads hit the 256 MB MALL anyway - so it is
+// opt-in (JB_TOPK_MQ=1) until the selection itself is batched.
+constexpr int kMqMax = 8;
+template <int NW, int W>
+__global__ __launch_bounds__(NW * 64) void topk_mq_kernel(const TopkSrc s, int nq, int64_t n,
+                                                          int64_t per_block, int k,
+                                                          float* __restrict__ out_d,
+                                                          int32_t* __restrict__ out_i) {
+  constexpr int T = NW * 64;
+  constexpr int TILE = T * kTopR;
+  __shared__ float s_wd[NW * kTopMaxK];
+  __shared__ int s_wi[NW * kTopMaxK];
+  __shared__ int s_cnt[NW];
+  __shared__ float s_cbd[kMqMax][2][kTopMaxK];
+  __shared__ int s_cbi[kMqMax][2][kTopMaxK];
+  __shared__ float s_thr[kMqMax];
+  __shared__ int s_cc[kMqMax], s_cur[kMqMax];
+  __shared__ uint64_t s_q[kMqMax][W];
+  __shared__ float s_qn[kMqMax];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int i = t; i < nq * W; i += T) s_q[i / W][i % W] = s.qbits[(int64_t)(i / W) * s.words + i % W];
+  if (t < nq) {
+    s_qn[t] = s.qnorm[t];
+    s_thr[t] = INFINITY;
+    s_cc[t] = 0;
+    s_cur[t] = 0;
+  }
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  float* wd = &s_wd[wv * k];
+  int* wi = &s_wi[wv * k];
+  const float inv = 1.f / (float)s.hash_num;
+  for (int64_t base = b0; base < b1; base += TILE) {
+    // the tile's rows, loaded once (unpredicated: clamped row index)
+    uint64_t rb[kTopR][W];
+    float rn[kTopR];
+    bool ok[kTopR];
+#pragma unroll
+    for (int r = 0; r < kTopR; ++r) {
+      const int64_t row = base + (int64_t)r * T + t;
+      const int64_t rc = row < b1 ? row : b1 - 1;
+#pragma unroll
+      for (int w = 0; w < W; ++w) rb[r][w] = s.tbits[rc * s.words + w];
+      rn[r] = s.metric == 1 ? s.tnorm[rc] : 0.f;
+      ok[r] = row < b1 && s.valid[rc];
+    }
+    for (int q = 0; q < nq; ++q) {
+      const float thr = s_thr[q];
+      const float qn = s_qn[q];
+      float d[kTopR];
+      int ix[kTopR];
+      bool any = false;
+#pragma unroll
+      for (int r = 0; r < kTopR; ++r) {
+        int ham = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) ham += __popcll(s_q[q][w] ^ rb[r][w]);
+        const float frac = (float)ham * inv;
+        float v = s.metric == 1
+                      ? sqrtf(fmaxf(0.f, qn * qn + rn[r] * rn[r] -
+                                         2.f * qn * rn[r] * __cosf(3.14159265f * frac)))
+                      : frac;
+        if (!ok[r] || v >= thr) v = INFINITY;
+        d[r] = v;
+        ix[r] = v < INFINITY ? (int)(base + (int64_t)r * T + t) : INT_MAX;
+        any |= v < INFINITY;
+      }
+      int cnt = 0;
+      if (__ballot(any)) {
+        sort_regs<kTopR>(d, ix);
+        wave_pop<kTopR>(d, ix, k, wd, wi, lane, &cnt);
+      } else {
+        for (int j = lane; j < k; j += 64) { wd[j] = INFINITY; wi[j] = INT_MAX; }
+      }
+      if (lane == 0) s_cnt[wv] = cnt;
+      __syncthreads();
+      int total = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) total += s_cnt[w];
+      if (total > 0) {                       // block-uniform
+        const int cur = s_cur[q];
+        const int nn = rank_merge<NW>(s_cbd[q][cur], s_cbi[q][cur], s_cc[q], s_wd, s_wi, s_cnt, k,
+                                      s_cbd[q][cur ^ 1], s_cbi[q][cur ^ 1], t, T);
+        __syncthreads();
+        if (t == 0) {
+          s_cur[q] = cur ^ 1;
+          s_cc[q] = nn;
+          s_thr[q] = nn == k ? s_cbd[q][cur ^ 1][k - 1] : INFINITY;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int q = 0; q < nq; ++q) {
+    const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
+    const int cur = s_cur[q], cc = s_cc[q];
+    for (int j = t; j < k; j += T) {
+      out_d[o + j] = j < cc ? s_cbd[q][cur][j] : INFINITY;
+      out_i[o + j] = j < cc ? s_cbi[q][cur][j] : INT_MAX;
+    }
+  }
+}
+
 // Small k (<= KL): every thread keeps its own sorted top-KL of the items it
 // reads (strided across the block's range) in registers and the block merges
 // once at the end (per-wave pops, then wave 0). Used for the final merge of
@@ -610,6 +724,17 @@ inline bool merge_with_tile() {
 template <int MODE>
 inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
                         int k, float* out_d, int32_t* out_i, hipStream_t stream) {
+  static const bool mq_on = getenv("JB_TOPK_MQ") != nullptr;
+  if (MODE == 0 && nq > 1 && nq <= kMqMax && s.words <= 2 && mq_on) {
+    // several queries per table pass (topk_mq_kernel)
+    if (s.words == 1)
+      hipLaunchKernelGGL((topk_mq_kernel<4, 1>), dim3(blocks), dim3(4 * 64), 0, stream, s, nq,
+                         nrows, per_block, k, out_d, out_i);
+    else
+      hipLaunchKernelGGL((topk_mq_kernel<4, 2>), dim3(blocks), dim3(4 * 64), 0, stream, s, nq,
+                         nrows, per_block, k, out_d, out_i);
+    return;
+  }
   if (scan_waves(k, nq, nrows) == 16)
     hipLaunchKernelGGL((topk_kernel<MODE, 16>), dim3(blocks, nq), dim3(16 * 64), 0, stream, s,
                        nrows, per_block, k, out_d, out_i, nullptr, 0u);
