@@ -144,19 +144,15 @@ class WeightManager:
             self.device_table.pull(self)
         return self.df, self.diff, self.counts
 
+    # the counts are always current on the host (a device batch updates
+    # them there); df / diff may sit in HBM (ops/fv_wide.py DeviceDf)
     @property
     def doc_count(self) -> int:
-        self._sync()
         return int(self.counts[0])
 
     @property
     def total_len(self) -> int:
-        self._sync()
         return int(self.counts[1])
-
-    def _sync(self) -> None:
-        if self.device_table is not None:
-            self.device_table.pull(self)
 
     def update_idx(self, idx: list[int]) -> None:
         """one document whose non-bin-weighted features have these indices

@@ -89,6 +89,14 @@ _SIGS = {
                          _c_void_p],
     "jb_lof_score": [_c_void_p, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
                      _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p],
+    "jb_fvw_count": [_c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _i32,
+                     _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_fvw_emit": [_c_void_p, _i64, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
+                    _c_void_p, _i32, _c_void_p, _u64, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+                    _c_void_p, _c_void_p, _c_void_p],
+    "jb_fvw_comb": [_c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
+                    _c_void_p, _u64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
+    "jb_fvw_name_bytes": [],
     "jb_kmeanspp": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                     _c_void_p, _c_void_p, _c_void_p],
     "jb_lloyd": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _f32, _f32, _c_void_p,
@@ -112,6 +120,47 @@ def sqdist(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
     rc = _fn("jb_sqdist_mfma")(_p(X), n, _p(C), k, d, _p(xn2), _p(cn2), _p(out), _stream())
     _check(rc, "jb_sqdist_mfma")
     return out
+
+
+def fvw_name_bytes() -> int:
+    return int(_fn("jb_fvw_name_bytes")())
+
+
+def fvw_count(buf, buf_len: int, datum_off, datum_len, n: int, srules, ns: int, nrules, nn: int,
+              ncomb: int, blob, base_cnt, total_cnt, err) -> None:
+    """wide converter, pass 1: base and total slots per datum (csrc/hip/fv_wide.hip)"""
+    _dev(buf, torch.uint8, "buf")
+    _dev(datum_off, torch.int64, "datum_off")
+    _dev(datum_len, torch.int32, "datum_len")
+    if datum_off.numel() < n or datum_len.numel() < n or base_cnt.numel() < n or \
+            total_cnt.numel() < n or buf.numel() < buf_len:
+        raise ValueError("fvw_count: bad operand shapes")
+    rc = _fn("jb_fvw_count")(_p(buf), buf_len, _p(datum_off), _p(datum_len), n, _p(srules), ns,
+                             _p(nrules), nn, ncomb, _p(blob), _p(base_cnt), _p(total_cnt), _p(err),
+                             _stream())
+    _check(rc, "jb_fvw_count")
+
+
+def fvw_emit(buf, buf_len: int, datum_off, datum_len, n: int, row_ptr, srules, ns: int, nrules,
+             nn: int, blob, H: int, idx, val, hs, names, gw, err) -> None:
+    """wide converter, pass 2: base features into each datum's slot range"""
+    total = int(row_ptr[n].item()) if n else 0
+    if idx.numel() < total or val.numel() < total or hs.numel() < total or gw.numel() < total or \
+            names.numel() < total * fvw_name_bytes():
+        raise ValueError("fvw_emit: output shorter than the slot count")
+    rc = _fn("jb_fvw_emit")(_p(buf), buf_len, _p(datum_off), _p(datum_len), n, _p(row_ptr),
+                            _p(srules), ns, _p(nrules), nn, _p(blob), H, _p(idx), _p(val), _p(hs),
+                            _p(names), _p(gw), _p(err), _stream())
+    _check(rc, "jb_fvw_emit")
+
+
+def fvw_comb(buf, n: int, row_ptr, base_cnt, srules, nrules, crules, ncomb: int, blob, H: int,
+             idx, val, hs, names) -> None:
+    """wide converter, pass 3: combination features of the weighted base"""
+    rc = _fn("jb_fvw_comb")(_p(buf), n, _p(row_ptr), _p(base_cnt), _p(srules), _p(nrules),
+                            _p(crules), ncomb, _p(blob), H, _p(idx), _p(val), _p(hs), _p(names),
+                            _stream())
+    _check(rc, "jb_fvw_comb")
 
 
 def kmeanspp(X: torch.Tensor, w: torch.Tensor, u, m: int):

@@ -140,3 +140,48 @@ def test_weight_manager_mix_and_pack_roundtrip():
     d.weights.unpack([4, 10, {"t$ab@bigram#tf/idf": 2}])
     from jubatus_amd.fv_converter.hashing import feature_index
     assert d.weights.df_of(feature_index("t$ab@bigram#tf/idf", d.hash_max_size)) == 2
+
+
+def _device_convert(conv, ds, update):
+    import torch
+    from jubatus_amd.ops.fv_wide import WideDevice
+    dev = torch.device("cuda", 0)
+    wd = getattr(conv, "_test_wide", None)
+    if wd is None:
+        wd = conv._test_wide = WideDevice(conv, dev)
+    blobs = [msgpack.packb(d.to_msgpack(), use_bin_type=False) for d in ds]
+    offs = np.zeros(len(blobs), np.int64)
+    np.cumsum([len(b) for b in blobs[:-1]], out=offs[1:])
+    buf = b"".join(blobs) + b"\0" * 16
+    d_buf = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_len = torch.tensor([len(b) for b in blobs], dtype=torch.int32, device=dev)
+    rp, idx, val, total = wd.convert(d_buf, len(buf) - 16, d_off, d_len, len(ds), update)
+    rp, idx, val = rp.cpu().numpy(), idx[:total].cpu().numpy(), val[:total].cpu().numpy()
+    assert int(wd.err.item()) == 0
+    out = []
+    for i in range(len(ds)):
+        a, b = rp[i], rp[i + 1]
+        keep = idx[a:b] >= 0
+        out.append((idx[a:b][keep], val[a:b][keep]))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CONFIGS + ["extra"])
+def test_device_wide_converter_equals_host(name):
+    """csrc/hip/fv_wide.hip + ops/fv_wide.py (DF table in HBM, sequential
+    semantics inside a batch) == the native host converter, datum by datum,
+    for a training batch (statistics updated) and then a query batch"""
+    ds = datums(200, seed=sum(map(ord, name)) + 7)
+    chost, cdev = _conv(name), _conv(name)
+    h = native_wide(chost)
+    for update in (True, False):
+        a = run_native(h, ds, update)
+        b = _device_convert(cdev, ds, update)
+        for (ia, va), (ib, vb) in zip(a, b):
+            np.testing.assert_array_equal(ia, ib)
+            np.testing.assert_allclose(va, vb, rtol=2e-6, atol=1e-7)
+    if chost.uses_global_weight:
+        assert cdev.weights.doc_count == chost.weights.doc_count
+        np.testing.assert_array_equal(cdev.weights.arrays()[0], chost.weights.df)
