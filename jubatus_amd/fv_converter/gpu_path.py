@@ -1,14 +1,19 @@
 """GPU fv_converter fast path (host half).
 
-Decides whether a converter config can run entirely in
-csrc/hip/fv_hash.hip and packs its rules into the device rule table.
+Decides whether a converter config runs on the GPU and packs its rules
+into the device rule tables.
 
-Eligible configs (the common ones: config/classifier/*.json, anomaly,
-clustering, nearest_neighbor defaults): no filters, no binary or combination
-rules; every string rule is of built-in type ``str`` with sample weight
-bin/tf/log_tf and global weight ``bin``; every num rule is ``num`` or
-``log``; key matchers are ``*``, prefix, suffix or exact (regex needs the
-host path).
+* fast path (``fast_eligible``, csrc/hip/fv_hash.hip + scan.hip, one slot
+  per (value, rule)): no filters, no binary or combination rules; every
+  string rule is of built-in type ``str`` with global weight ``bin``; every
+  num rule is ``num`` or ``log``; key matchers ``*``, prefix, suffix, exact;
+* wide rule set (``wide_eligible``, csrc/hip/fv_wide.hip and the native host
+  twin csrc/native/jb_hostfv_wide.hpp): adds the ``space`` / ``ngram``
+  splitters, tf / log_tf with idf / bm25 global weights and add / mul
+  combinations.
+
+``gpu_eligible`` is either; regex matchers, filters and plug-ins keep the
+host converter.
 """
 from __future__ import annotations
 
@@ -23,7 +28,9 @@ _RULE = struct.Struct("<iiiiiifi")  # mirrors jb::GpuRule
 _KIND = {"all": 0, "prefix": 1, "suffix": 2, "exact": 3}
 
 
-def gpu_eligible(conv: DatumToFvConverter) -> bool:
+def fast_eligible(conv: DatumToFvConverter) -> bool:
+    """the fixed-slot fast path (fv_hash.hip / scan.hip): one slot per
+    (value, rule), constant string weights"""
     if conv.string_filters or conv.num_filters or conv.binary_rules or conv.combination_rules:
         return False
     for r in conv.string_rules:
@@ -41,7 +48,7 @@ class GpuRuleTable:
     """Packed rule tables: (string rules, num rules, byte blob)."""
 
     def __init__(self, conv: DatumToFvConverter):
-        if not gpu_eligible(conv):
+        if not fast_eligible(conv):
             raise ValueError("converter config is not eligible for the GPU fast path")
         blob = bytearray()
 
@@ -144,3 +151,10 @@ class WideRuleTable:
         self.blob = np.frombuffer(bytes(blob) or b"\0", dtype=np.uint8).copy()
         self.H = conv.hash_max_size
         self.global_weights = conv.uses_global_weight
+
+
+def gpu_eligible(conv: DatumToFvConverter) -> bool:
+    """the GPU converts this config: the fixed-slot fast path or the wide
+    rule-set kernels (csrc/hip/fv_wide.hip: ngram / space, tf / idf / bm25 with
+    the DF table in HBM, combinations)"""
+    return fast_eligible(conv) or wide_eligible(conv)

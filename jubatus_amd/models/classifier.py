@@ -83,6 +83,7 @@ class LinearClassifier:
         self._lock = threading.RLock()
         self.device = device
         self.gpu = device is not None
+        self._devfv = False
         self.direct = True        # single-launch path for small classify requests
         # train batches scanned on the GPU (csrc/hip/scan.hip); their checks
         # complete asynchronously (_drain)
@@ -108,6 +109,9 @@ class LinearClassifier:
             from ..ops.feature_pipeline import FeaturePipeline
             self.torch = torch
             self.pipe = FeaturePipeline(converter, device)
+            # datum -> features on the device: the fixed-slot fast path or the
+            # wide rule-set kernels (ngram / idf / bm25 / combinations)
+            self._devfv = self.pipe.fast or self.pipe.wide
             self._hots = [hip.HotRows(device), hip.HotRows(device)]
             self._hot_turn = 0
             self._hot_count_buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
@@ -249,10 +253,10 @@ class LinearClassifier:
         new labels, binary values, malformed bytes - is then re-run through
         the host scanner, which adds labels / raises as before)."""
         with self._lock:
-            if not (self.gpu and self.pipe.fast):
+            if not self._devfv:
                 bodies = [bytes(arena.np[o:o + n]) for o, n in zip(offs, lens)]
                 return self.train_requests(bodies)
-            if self.gpu_scan and self.labels.size() > 0:
+            if self.gpu_scan and self.pipe.fast and self.labels.size() > 0:
                 self._drain(block=True, keep=3)
                 self._sync_labels()
                 chk = self._check_record(self.labels.size())
@@ -364,7 +368,7 @@ class LinearClassifier:
         """Train on raw msgpack ``list<labeled_datum>`` bodies (one stream each)."""
         with self._lock:
             self._drain()
-            if self.gpu and self.pipe.fast:
+            if self._devfv:
                 return self._train_batch(self.pipe.from_requests(list(bodies), True, self.labels))
             total = 0
             streams = [msgpack.unpackb(bytes(x), raw=False) for x in bodies]
@@ -384,7 +388,7 @@ class LinearClassifier:
         data = list(data)
         if not data:
             return 0
-        if self.gpu and self.pipe.fast:
+        if self._devfv:
             body = _pack_body([[lab, as_datum(d).to_msgpack()] for lab, d in data])
             return self.train_requests([body])
         with self._lock:
@@ -424,10 +428,11 @@ class LinearClassifier:
     def classify_requests(self, bodies: Sequence[Any]) -> list[list[tuple[str, float]]]:
         with self._lock:
             self._drain()
-            if self.gpu and self.pipe.fast:
+            if self._devfv:
                 from ..ops import hip
                 self._sync_labels()
-                scores = self.pipe.classify_direct(list(bodies), self.W) if self.direct else None
+                scores = self.pipe.classify_direct(list(bodies), self.W) \
+                    if self.direct and self.pipe.fast else None
                 if scores is not None:
                     return self._results(scores)
                 b = self.pipe.from_requests(list(bodies), False, None)
@@ -445,7 +450,7 @@ class LinearClassifier:
         data = list(data)
         if not data:
             return []
-        if self.gpu and self.pipe.fast:
+        if self._devfv:
             return self.classify_requests([_pack_body([as_datum(d).to_msgpack() for d in data])])
         rows = [self.conv.hashed(self.conv.convert(as_datum(d))) for d in data]
         with self._lock:
@@ -816,7 +821,7 @@ class LinearClassifier:
         st = {"num_classes": str(len(self.get_labels())), "num_features": str(self.H),
               "label_capacity": str(self.LC), "method": self.method,
               "storage": "hbm" if self.gpu else "host",
-              "fv_path": "gpu" if (self.gpu and self.pipe.fast) else "host"}
+              "fv_path": ("gpu" if self.pipe.fast else "gpu-wide") if self._devfv else "host"}
         if self.gpu:
             for k, v in self._scan_stats.items():
                 st[f"train_scan.{k}"] = str(v)

@@ -86,10 +86,10 @@ class RowEngine:
         idf / bm25 weights (the WeightManager's arrays, updated in place) and
         combinations. No filters / plug-ins / regex matchers."""
         if self._host_hasher is None:
-            from ..fv_converter.gpu_path import (GpuRuleTable, WideRuleTable, gpu_eligible,
+            from ..fv_converter.gpu_path import (GpuRuleTable, WideRuleTable, fast_eligible,
                                                  wide_eligible)
             from .._native import native
-            if gpu_eligible(self.conv):
+            if fast_eligible(self.conv):
                 rt = GpuRuleTable(self.conv)
                 self._host_hasher = native().HostFvHasher(rt.srules, rt.n_srules, rt.nrules,
                                                           rt.n_nrules, rt.blob, rt.H)

@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from .._native import native
-from ..fv_converter.gpu_path import GpuRuleTable, gpu_eligible
+from ..fv_converter.gpu_path import GpuRuleTable, fast_eligible, wide_eligible
 from ..utils import trace
 from . import hip
 
@@ -252,7 +252,10 @@ class FeaturePipeline:
         self.conv = converter
         self.device = torch.device(device)
         self.H = converter.hash_max_size
-        self.fast = gpu_eligible(converter)
+        self.fast = fast_eligible(converter)
+        # the wide rule set (ngram / idf / bm25 / combinations) converts on
+        # the device too (csrc/hip/fv_wide.hip), after the host scanner
+        self.wide = not self.fast and wide_eligible(converter)
         self.nthreads = nthreads or scan_threads()
         self._pinned = [_Pinned(), _Pinned()]
         self._turn = 0
@@ -285,13 +288,18 @@ class FeaturePipeline:
             self.d_srules = torch.from_numpy(rt.srules).to(self.device)
             self.d_nrules = torch.from_numpy(rt.nrules).to(self.device)
             self.d_blob = torch.from_numpy(rt.blob).to(self.device)
+        elif self.wide:
+            from .fv_wide import WideDevice
+            self.wdev = WideDevice(converter, self.device)
+            # the host scanner's slot estimate is unused on this path
+            self.rules = type("SlotCounts", (), {"n_srules": 1, "n_nrules": 1})()
 
     # ------------------------------------------------------------ fast path
     def from_requests(self, bodies: list, labeled: bool, table=None) -> DeviceBatch:
         """bodies: buffer-protocol objects, each a msgpack list<labeled_datum>
         (labeled) or list<datum>; every body is one update stream."""
-        if not self.fast:
-            raise RuntimeError("converter config is not eligible for the GPU fast path")
+        if not (self.fast or self.wide):
+            raise RuntimeError("converter config is not eligible for the GPU path")
         nat = native()
         pin = self._pinned[self._turn]
         self._turn ^= 1
@@ -322,8 +330,8 @@ class FeaturePipeline:
         """Zero-copy variant of from_requests: bodies are spans of a pinned
         RequestArena; the scanner reads them in place and one H2D copy moves
         the arena prefix to HBM."""
-        if not self.fast:
-            raise RuntimeError("converter config is not eligible for the GPU fast path")
+        if not (self.fast or self.wide):
+            raise RuntimeError("converter config is not eligible for the GPU path")
         nat = native()
         pin = self._pinned[self._turn]
         self._turn ^= 1
@@ -483,6 +491,13 @@ class FeaturePipeline:
         ev.record(cs)
         compute.wait_event(ev)
         pin.event = ev
+        if self.wide:
+            # train batches (labeled) advance the document statistics
+            row, idx, val, total = self.wdev.convert(d_buf, nbytes, d_off, d_len, n, labeled)
+            if int(self.wdev.err.item()):
+                self.wdev.err.zero_()
+                raise TypeError("malformed datum (device wide converter)")
+            return DeviceBatch(n, max(total, 1), R, row, idx, val, d_lab, d_sp)
         if n > 0:
             hip.fv_hash(d_buf, nbytes, d_off, d_len, d_row, n, self.d_srules, self.rules.n_srules,
                         self.d_nrules, self.rules.n_nrules, self.d_blob, self.H, d_idx, d_val,

@@ -66,10 +66,15 @@ def test_errors():
 def test_gpu_eligibility():
     base = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
             "num_rules": [{"key": "*", "type": "num"}]}
-    assert gpu_eligible(DatumToFvConverter(base))
+    from jubatus_amd.fv_converter.gpu_path import fast_eligible, wide_eligible
+    assert gpu_eligible(DatumToFvConverter(base)) and fast_eligible(DatumToFvConverter(base))
     ng = dict(base, string_types={"u": {"method": "ngram", "char_num": "1"}},
               string_rules=[{"key": "*", "type": "u", "sample_weight": "tf", "global_weight": "idf"}])
-    assert not gpu_eligible(DatumToFvConverter(ng))
+    assert not fast_eligible(DatumToFvConverter(ng))
+    assert wide_eligible(DatumToFvConverter(ng)) and gpu_eligible(DatumToFvConverter(ng))
+    rx = dict(base, string_rules=[{"key": "/x.*/", "type": "str", "sample_weight": "bin",
+                                   "global_weight": "bin"}])
+    assert not gpu_eligible(DatumToFvConverter(rx))
 
 
 def test_native_host_hasher_matches_converter():

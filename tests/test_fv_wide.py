@@ -97,9 +97,7 @@ def run_python(conv, ds, update):
 @pytest.mark.parametrize("name", CONFIGS + ["extra"])
 def test_wide_eligible_configs(name):
     conv = _conv(name)
-    assert wide_eligible(conv)
-    if name != "extra":
-        assert not gpu_eligible(conv) or name.startswith("classifier")
+    assert wide_eligible(conv) and gpu_eligible(conv)
 
 
 @pytest.mark.parametrize("name", CONFIGS + ["extra"])
@@ -185,3 +183,42 @@ def test_device_wide_converter_equals_host(name):
     if chost.uses_global_weight:
         assert cdev.weights.doc_count == chost.weights.doc_count
         np.testing.assert_array_equal(cdev.weights.arrays()[0], chost.weights.df)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["classifier/arow_combinational_feature.json", "idf"])
+def test_classifier_trains_on_device_wide_converter(name):
+    """a classifier whose converter needs the wide rule set converts on the
+    device (fv_path gpu-wide) and, trained as one update stream, equals the
+    host engine (the reference's per-sample online update order)"""
+    import torch
+    from jubatus_amd.models.classifier import LinearClassifier
+    if name == "idf":
+        cfg = {"method": "AROW", "parameter": {"regularization_weight": 1.0},
+               "converter": {"string_types": {"bi": {"method": "ngram", "char_num": "2"}},
+                             "string_rules": [{"key": "*", "type": "bi", "sample_weight": "tf",
+                                               "global_weight": "idf"}],
+                             "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 16}}
+    else:
+        with open(os.path.join(ROOT, "config", name)) as f:
+            cfg = json.load(f)
+    r = random.Random(3)
+    data = []
+    for _ in range(300):
+        y = r.randrange(3)
+        data.append((f"L{y}", {"a": f"w{y}{r.randrange(4)}x", "b": f"v{r.randrange(9)}",
+                               "x": y + r.gauss(0, 0.3), "z": r.gauss(0, 1)}))
+    g = LinearClassifier(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]),
+                         device=torch.device("cuda", 0))
+    h = LinearClassifier(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]))
+    assert g.get_status()["fv_path"] == "gpu-wide"
+    for i in range(0, 300, 100):
+        g.train(data[i:i + 100])
+        h.train(data[i:i + 100])
+    G = g.W.cpu().numpy()[:, :g.labels.size()]
+    Hm = h.W[:, :h.labels.size()]
+    np.testing.assert_allclose(G, Hm, rtol=1e-3, atol=1e-4)
+    test = [d for _, d in data[:50]]
+    pg = [max(x, key=lambda e: e[1])[0] for x in g.classify(test)]
+    ph = [max(x, key=lambda e: e[1])[0] for x in h.classify(test)]
+    assert pg == ph
