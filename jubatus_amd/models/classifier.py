@@ -650,7 +650,25 @@ class LinearClassifier:
             nbytes = job.end()
             self._last_mix = job.stats()
             self._mix_counts(group)
+            nbytes += self._mix_weights(group)
             return nbytes
+
+    def _mix_weights(self, group=None) -> int:
+        """document-frequency diffs of idf / bm25 converters (the reference
+        mixes the weight manager with the model, linear_mixer get_diff):
+        sparse (index, count) records over the collective"""
+        if not self.conv.uses_global_weight:
+            return 0
+        from ..fv_converter.converter import WeightManager
+        from ..parallel import wire
+        wm = self.conv.weights
+        mine = wm.get_diff()
+        diffs = wire.all_gather(mine, group)
+        mixed = diffs[0]
+        for d in diffs[1:]:
+            mixed = WeightManager.mix(mixed, d)
+        wm.put_diff(mixed)
+        return len(wire.encode(mine))
 
     def _table_mix(self, group):
         from ..parallel.table_mix import TableMix
@@ -723,7 +741,7 @@ class LinearClassifier:
                 since = int(self.labels.count(i)) - int(cur[i])
                 self.labels.set_count(i, int(max(0, new_base[i] + since)))
             self._count_base = {nm: int(max(0, new_base[i])) for i, nm in enumerate(names)}
-            return nbytes
+            return nbytes + self._mix_weights(h.get("group"))
 
     def _tables(self) -> list:
         """the mixable tensors (torch views of the host arrays on the CPU backend)"""
