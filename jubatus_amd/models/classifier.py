@@ -89,7 +89,9 @@ class LinearClassifier:
         # complete asynchronously (_drain)
         self.gpu_scan = os.environ.get("JUBATUS_GPU_SCAN", "1") != "0"
         self._pending: collections.deque = collections.deque()
-        self._scan_stats = {"gpu": 0, "replayed": 0, "host": 0}   # train batches by scan path
+        self._scan_stats = {"gpu": 0, "replayed": 0, "host": 0,  # train batches by scan path
+                            "replay_failed": 0}
+        self._replay_error = ""
         self._free_checks: list = []
         self._draining = False
         self._result_cols = None
@@ -353,14 +355,24 @@ class LinearClassifier:
                 c.wait()
                 self._pending.popleft()
                 replay, c.replay = c.replay, None
-                if int(c.err[0]):
-                    self._scan_stats["replayed"] += 1
-                    replay()
-                else:
-                    h = c.hist[:c.nhist]
-                    for lid in np.flatnonzero(h).tolist():
-                        self.labels.add_count(lid, int(h[lid]))
-                self._free_checks.append(c)
+                try:
+                    if int(c.err[0]):
+                        self._scan_stats["replayed"] += 1
+                        try:
+                            replay()
+                        except (TypeError, ValueError, RuntimeError) as e:
+                            # the batch was acknowledged when it was queued: its
+                            # failure is recorded here (status train_scan.replay_failed
+                            # / last_replay_error), not raised into whichever call
+                            # happens to drain it
+                            self._scan_stats["replay_failed"] += 1
+                            self._replay_error = f"{type(e).__name__}: {e}"
+                    else:
+                        h = c.hist[:c.nhist]
+                        for lid in np.flatnonzero(h).tolist():
+                            self.labels.add_count(lid, int(h[lid]))
+                finally:
+                    self._free_checks.append(c)
         finally:
             self._draining = False
 
@@ -843,6 +855,8 @@ class LinearClassifier:
         if self.gpu:
             for k, v in self._scan_stats.items():
                 st[f"train_scan.{k}"] = str(v)
+            if self._replay_error:
+                st["train_scan.last_replay_error"] = self._replay_error
         for k, v in self._last_mix.items():
             st[f"mix.last_{k}"] = str(v)
         for k, v in self.train_stats().items():

@@ -393,3 +393,50 @@ def test_pool_direct_query_radix_topk_matches_exact(euclid, k):
     for x, y in zip(a, b):
         assert [i for i, _ in x] == [i for i, _ in y]
     assert hip.TOPK_MAX_K >= k
+
+
+@pytest.mark.parametrize("k", [1, 10, 37])
+def test_topk_16_wave_path_matches_full_sort(k):
+    """nq 1 over >= 2M rows takes the 16-wave scan blocks (topk.hip
+    scan_waves); heavy ties (hash_num 16: 17 distinct distances) must still
+    give the stable (distance, row) order of a full sort"""
+    import torch
+    from jubatus_amd.ops import hip
+    n = 2_200_000
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(k)
+    tb = torch.randint(0, 1 << 16, (n, 1), generator=g, device=d, dtype=torch.int64)
+    tn = torch.ones(n, dtype=torch.float32, device=d)
+    valid = (torch.rand(n, generator=g, device=d) > 0.01).to(torch.uint8)
+    qb = torch.randint(0, 1 << 16, (1, 1), generator=g, device=d, dtype=torch.int64)
+    qn = torch.ones(1, dtype=torch.float32, device=d)
+    dist, row = hip.topk_hamming(qb, qn, 1, tb, tn, valid, n, 16, 0, k)
+    x = (tb[:, 0] ^ qb[0, 0]).cpu().numpy().astype(np.uint64)
+    ham = np.unpackbits(x.view(np.uint8).reshape(-1, 8)[:, :2], axis=1).sum(1)
+    ref = np.where(valid.cpu().numpy() > 0, ham / 16.0, np.inf)
+    order = np.argsort(ref, kind="stable")[:k]
+    assert row[0].cpu().numpy().tolist() == order.tolist()
+    np.testing.assert_allclose(dist[0].cpu().numpy(), ref[order], rtol=1e-6)
+
+
+def test_topk_forced_variants_match_default():
+    """JB_TOPK_NW=16 / JB_TOPK_MERGE=tile are read once per process (static):
+    run them in child processes against the default path"""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = ("import json,torch,numpy as np;from jubatus_amd.ops import hip;"
+            "d=torch.device('cuda',0);g=torch.Generator(device=d).manual_seed(5);"
+            "n=300000;tb=torch.randint(0,1<<16,(n,1),generator=g,device=d,dtype=torch.int64);"
+            "tn=torch.ones(n,device=d);v=torch.ones(n,dtype=torch.uint8,device=d);"
+            "qb=torch.randint(0,1<<16,(3,1),generator=g,device=d,dtype=torch.int64);"
+            "qn=torch.ones(3,device=d);dd,rr=hip.topk_hamming(qb,qn,3,tb,tn,v,n,16,0,10);"
+            "print(json.dumps(rr.cpu().numpy().tolist()))")
+    outs = []
+    for env in ({}, {"JB_TOPK_NW": "16"}, {"JB_TOPK_MERGE": "tile"}):
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env),
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert outs[0] == outs[1] == outs[2]
