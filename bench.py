@@ -142,6 +142,40 @@ class FreshStream:
                 used_in_blk = 0
 
 
+def _cpu(a, b) -> float:
+    return (b.ru_utime - a.ru_utime) + (b.ru_stime - a.ru_stime)
+
+
+def _thread_cpu() -> dict:
+    """CPU seconds of this process's threads, summed by thread name"""
+    out: dict = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        fields = st[st.rindex(")") + 2:].split()
+        out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tck
+    return out
+
+
+def _handler_profile(clf) -> dict:
+    """mean time per served batch in the arena handler (models/classifier.py
+    train_arena_sync): waiting for the model lock, submitting the GPU work,
+    waiting for the scan check, finishing"""
+    p = clf._served_prof
+    if not p[0]:
+        return {}
+    return {"batches": p[0], "requests_per_batch": round(p[1] / p[0], 1),
+            "lock_wait": round(p[2] / p[0] * 1e6, 1), "submit": round(p[3] / p[0] * 1e6, 1),
+            "scan_wait": round(p[4] / p[0] * 1e6, 1), "finish": round(p[5] / p[0] * 1e6, 1),
+            "submit_pre": round(p[6] / p[0] * 1e6, 1), "submit_call": round(p[7] / p[0] * 1e6, 1),
+            "submit_set_wait": round(clf.pipe.set_wait_s / p[0] * 1e6, 1)}
+
+
 def served_train(args, local: int, nat) -> dict:
     """The served train path: an in-process jubaclassifier (AROW, this GPU)
     behind the native msgpack-RPC transport, driven by the native load
@@ -150,6 +184,7 @@ def served_train(args, local: int, nat) -> dict:
     request body into a pinned arena slot; one Python call per slot runs
     the GPU scan -> fv_hash -> train pipeline and replies per request
     (classifier_impl.cpp:54-57 -> classifier_serv.cpp:128-147)."""
+    import resource
     import tempfile
     exe = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaloadgen")
     if not os.access(exe, os.X_OK):
@@ -189,8 +224,17 @@ def served_train(args, local: int, nat) -> dict:
         clf = h.server.clf
         clf.synchronize()
         st0 = clf.train_stats()
+        ru_self0 = resource.getrusage(resource.RUSAGE_SELF)
+        thr0 = _thread_cpu()
+        ans0, nb0 = h.rpc.arena_ns(), h.rpc.batches()
+        ru_kid0 = resource.getrusage(resource.RUSAGE_CHILDREN)
         r = subprocess.run(base + ["-t", str(args.rpc_seconds)], capture_output=True, text=True,
                            timeout=args.rpc_seconds + 120)
+        ru_self1 = resource.getrusage(resource.RUSAGE_SELF)
+        thr1 = _thread_cpu()
+        ans1, nb1 = h.rpc.arena_ns(), h.rpc.batches()
+        nb = max(1, nb1 - nb0)
+        ru_kid1 = resource.getrusage(resource.RUSAGE_CHILDREN)
         if r.returncode != 0:
             return {"error": (r.stderr or r.stdout)[-400:]}
         lg = json.loads(r.stdout.strip().splitlines()[-1])
@@ -205,7 +249,18 @@ def served_train(args, local: int, nat) -> dict:
                 "samples_trained_in_window": tr,
                 "update_fraction": round((st1["updated"] - st0["updated"]) / tr, 4) if tr else None,
                 "server_threads": args.rpc_threads,
+                # CPU seconds per second of the timed window: the server process
+                # (transport + Python + GPU driver threads) and the load generator
+                "server_cpus": round(_cpu(ru_self0, ru_self1) / lg["seconds"], 2),
+                "loadgen_cpus": round(_cpu(ru_kid0, ru_kid1) / lg["seconds"], 2),
+                "server_cpus_by_thread": {k: round((v - thr0.get(k, 0.0)) / lg["seconds"], 2)
+                                          for k, v in sorted(thr1.items())
+                                          if v - thr0.get(k, 0.0) > 0.01 * lg["seconds"]},
                 "train_scan": dict(clf._scan_stats),
+                "handler_us_per_batch": _handler_profile(clf),
+                "batches_in_window": nb,
+                "transport_us_per_batch": {"handler_call": round((ans1[0] - ans0[0]) / nb / 1e3, 1),
+                                           "send_replies": round((ans1[1] - ans0[1]) / nb / 1e3, 1)},
                 "path": "loopback TCP -> native epoll transport -> pinned arena slot -> GPU scan/"
                         "fv_hash/AROW train; reply per request after the batch's scan check"}
     finally:
@@ -241,6 +296,8 @@ def main() -> None:
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--no-rpc", action="store_true",
                     help="skip the served-path measurement (jubaclassifier + jubaloadgen, N = 1)")
+    ap.add_argument("--served-only", action="store_true",
+                    help="measure only the served path (prints its record; not the headline)")
     ap.add_argument("--rpc-seconds", type=float, default=4.0)
     ap.add_argument("--rpc-conns", type=int, default=64)
     ap.add_argument("--rpc-depth", type=int, default=16)
@@ -313,6 +370,9 @@ def main() -> None:
         clf.set_label(f"label{y}")
 
     nat = native()
+    if args.served_only:
+        print(json.dumps(served_train(args, local, nat)), flush=True)
+        return
     gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, local_world)))
     p_corr, vocab = (0.0, (1 << 31) - 1) if args.worst_case else (0.6, args.vocab)
     pinned = device is not None

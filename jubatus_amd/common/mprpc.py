@@ -21,6 +21,7 @@ from __future__ import annotations
 import concurrent.futures as cf
 import errno
 import itertools
+import os
 import random
 import socket
 import threading
@@ -139,13 +140,18 @@ class RpcServer:
         dict)`` serves a whole slot; the slot is reused after
         ``release_slot``. Register before start()."""
         self._srv.set_arena_batch(name, list(slots), int(slot_bytes), fn)
-        self._srv.set_batch_threads(2)     # serve slot k while slot k+1 is submitted
+        # serve slot k while slot k+1 is submitted
+        self._srv.set_batch_threads(int(os.environ.get("JUBATUS_ARENA_THREADS", "2")))
 
     def release_slot(self, slot: int) -> None:
         self._srv.release_slot(int(slot))
 
     def batches(self) -> int:
         return self._srv.batches()
+
+    def arena_ns(self) -> tuple[int, int]:
+        """nanoseconds the arena batches spent in the handler / sending replies"""
+        return tuple(self._srv.arena_ns())
 
     def _dispatch_batch(self, method: str, params: list, msgids: list) -> list:
         fn = self._batch[method]

@@ -225,6 +225,9 @@ class PyRpcServer {
   void release_slot(int slot) { srv_->release_slot(slot); }
   void set_max_message(uint64_t n) { srv_->set_max_message(n); }
   uint64_t batches() const { return srv_->batches(); }
+  py::tuple arena_ns() const {
+    return py::make_tuple(srv_->arena_handler_ns(), srv_->arena_send_ns());
+  }
   void set_io_threads(int n) { srv_->set_io_threads(n); }
   void set_batch_threads(int n) { srv_->set_batch_threads(n); }
   int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
@@ -408,6 +411,7 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("set_max_message", &PyRpcServer::set_max_message)
       .def("set_io_threads", &PyRpcServer::set_io_threads)
       .def("set_batch_threads", &PyRpcServer::set_batch_threads)
+      .def("arena_ns", &PyRpcServer::arena_ns)
       .def("listen", &PyRpcServer::listen)
       .def("start", &PyRpcServer::start)
       .def("stop", &PyRpcServer::stop)
@@ -415,6 +419,39 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("served", &PyRpcServer::served)
       .def("connections", &PyRpcServer::connections);
   m.def("msgpack_frame", &frame, "length of the first complete msgpack object (0: incomplete, -1: bad)");
+  m.def("frame_stream",
+        [](py::buffer b, size_t cut, bool speculative) {
+          // tests: frame a byte stream delivered in two reads ([0, cut), then
+          // the rest) -> (message ends, rc, pending pos, pending rem)
+          py::buffer_info bi = b.request();
+          const uint8_t* p = (const uint8_t*)bi.ptr;
+          const size_t n = (size_t)(bi.size * bi.itemsize);
+          std::vector<uint64_t> ends;
+          jb::FrameState st;
+          int rc = 0;
+          uint64_t base = 0;
+          for (size_t upto : {std::min(cut, n), n}) {
+            if (upto <= base) continue;
+            std::vector<uint64_t> e;
+            if (speculative) {
+              rc = jb::frame_all(p + base, upto - base, st, &e, true);
+            } else {
+              for (;;) {
+                const uint64_t off = e.empty() ? 0 : e.back();
+                rc = jb::frame_resume(p + base + off, upto - base - off, st);
+                if (rc <= 0) break;
+                e.push_back(off + st.pos);
+                st.reset();
+              }
+            }
+            for (auto x : e) ends.push_back(base + x);
+            if (!e.empty()) base += e.back();
+            if (rc < 0) break;
+          }
+          if (!st.started) { st.pos = 0; st.rem = 1; }    // a fresh message: nothing pending
+          return py::make_tuple(ends, rc, st.pos, st.rem);
+        },
+        py::arg("buf"), py::arg("cut"), py::arg("speculative"));
   m.def("crc32", &crc32, py::arg("data"), py::arg("init") = 0u);
   m.def("md5_hex", &md5_hex);
   m.def("feature_index", &feature_index);

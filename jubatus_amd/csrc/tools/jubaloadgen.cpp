@@ -6,8 +6,9 @@
 // the file are sent in turn, each connection starting at its own one) on C
 // connections, each keeping D requests in flight, for T seconds; prints one
 // JSON line with the request rate and the per-request latency distribution.
-// Any error response aborts. The envelope and the params go out with one
-// sendmsg (two iovecs, no per-request copy of the params).
+// Any error response aborts. Every request the in-flight window allows goes
+// out in one sendmsg (envelope + params iovecs, no per-request copy of the
+// params), as a pipelining client library would write them.
 //
 // Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
 #include <arpa/inet.h>
@@ -50,28 +51,30 @@ std::string request_head(uint32_t msgid, const std::string& method) {
   return o;
 }
 
-bool send_all(int fd, const std::string& head, const std::string& params) {
-  size_t done = 0;
-  const size_t total = head.size() + params.size();
-  while (done < total) {
-    iovec iov[2];
-    int n = 0;
-    if (done < head.size()) {
-      iov[n].iov_base = (void*)(head.data() + done);
-      iov[n++].iov_len = head.size() - done;
-      iov[n].iov_base = (void*)params.data();
-      iov[n++].iov_len = params.size();
-    } else {
-      const size_t o = done - head.size();
-      iov[n].iov_base = (void*)(params.data() + o);
-      iov[n++].iov_len = params.size() - o;
-    }
+// several requests (head + params each) with as few sendmsg calls as the
+// socket takes
+bool send_many(int fd, const std::vector<std::string>& heads,
+               const std::vector<const std::string*>& bodies) {
+  std::vector<iovec> iov;
+  iov.reserve(2 * heads.size());
+  for (size_t i = 0; i < heads.size(); ++i) {
+    iov.push_back(iovec{(void*)heads[i].data(), heads[i].size()});
+    iov.push_back(iovec{(void*)bodies[i]->data(), bodies[i]->size()});
+  }
+  size_t k = 0;
+  while (k < iov.size()) {
     msghdr m{};
-    m.msg_iov = iov;
-    m.msg_iovlen = n;
+    m.msg_iov = iov.data() + k;
+    m.msg_iovlen = std::min<size_t>(iov.size() - k, 1024);
     const ssize_t w = sendmsg(fd, &m, MSG_NOSIGNAL);
     if (w <= 0) return false;
-    done += (size_t)w;
+    size_t left = (size_t)w;
+    while (left > 0 && k < iov.size()) {            // drop what went out
+      if (left >= iov[k].iov_len) { left -= iov[k].iov_len; ++k; continue; }
+      iov[k].iov_base = (char*)iov[k].iov_base + left;
+      iov[k].iov_len -= left;
+      left = 0;
+    }
   }
   return true;
 }
@@ -112,15 +115,26 @@ void run_conn(const std::string& host, int port, const std::string& method,
   const auto t_end = Clock::now() + std::chrono::duration<double>(secs);
   bool sending = true;
   char buf[1 << 16];
+  std::vector<std::string> heads;
+  std::vector<const std::string*> bodies;
   while (sending || inflight > 0) {
+    // every request the window allows goes out in one sendmsg
+    heads.clear();
+    bodies.clear();
+    const auto now = Clock::now();
+    if (sending && now >= t_end) sending = false;
     while (sending && inflight < depth) {
-      if (Clock::now() >= t_end) { sending = false; break; }
-      const std::string head = request_head(next, method);
-      sent[next & 0xffff] = Clock::now();
-      if (!send_all(fd, head, (*params)[which])) { r->error = "send failed"; close(fd); return; }
+      heads.push_back(request_head(next, method));
+      bodies.push_back(&(*params)[which]);
+      sent[next & 0xffff] = now;
       which = (which + 1) % params->size();
       ++next;
       ++inflight;
+    }
+    if (!heads.empty() && !send_many(fd, heads, bodies)) {
+      r->error = "send failed";
+      close(fd);
+      return;
     }
     if (inflight == 0) break;
     ssize_t k = recv(fd, buf, sizeof buf, 0);

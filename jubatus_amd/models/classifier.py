@@ -21,6 +21,7 @@ from __future__ import annotations
 import collections
 import os
 import threading
+import time
 from typing import Any, Sequence
 
 import msgpack
@@ -89,6 +90,7 @@ class LinearClassifier:
         # complete asynchronously (_drain)
         self.gpu_scan = os.environ.get("JUBATUS_GPU_SCAN", "1") != "0"
         self._pending: collections.deque = collections.deque()
+        self._served_prof = [0, 0] + [0.0] * 6   # train_arena_sync timing sums
         self._scan_stats = {"gpu": 0, "replayed": 0, "host": 0,  # train batches by scan path
                             "replay_failed": 0}
         self._replay_error = ""
@@ -118,6 +120,7 @@ class LinearClassifier:
             self._hot_turn = 0
             self._hot_count_buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._hot_seen = None            # (pinned count, event) of a detection in flight
+            self._hot_seen_ev = hip.DevEvent()
             self._hot_last = -1              # hot rows found by the last completed detection
             self._hot_batches = 0
             # [samples that updated, samples trained] (device counters)
@@ -207,16 +210,15 @@ class LinearClassifier:
         from ..ops import hip
         hs = self._hots[self._hot_turn]
         self._hot_turn ^= 1
-        if hs.free is not None:
-            self.torch.cuda.current_stream().wait_event(hs.free)
+        if hs.free_used:
+            hs.free.wait_on()
         min_count = self.hot_min_count or max(1024, b.n // 128)
         hip.hot_detect(b.row_ptr, b.n, b.fidx, b.nnz, hs, min_count,
                        max_rows=hip.hot_max_rows(self.LC))
         if self._hot_seen is None:       # learn the count without a host sync
             self._hot_count_buf.copy_(hs.n, non_blocking=True)
-            ev = self.torch.cuda.Event()
-            ev.record()
-            self._hot_seen = (self._hot_count_buf, ev)
+            self._hot_seen_ev.record()
+            self._hot_seen = (self._hot_count_buf, self._hot_seen_ev)
         b.hot = hs
 
     def _launch_train(self, b) -> None:
@@ -225,7 +227,7 @@ class LinearClassifier:
         replica when hot rows were detected (csrc/hip/hot.hip)"""
         from ..ops import hip
         if b.ready is not None:
-            self.torch.cuda.current_stream().wait_event(b.ready)
+            hip.stream_wait(b.ready)
         mode = self._mode(b.nstreams)
         if b.hot is None and b.ready is None and self._hot_wanted(b.nstreams):
             self._detect_hot(b)
@@ -235,8 +237,55 @@ class LinearClassifier:
                          merge_every=self.hot_merge, stats=self._train_stats,
                          touched=self.touched)
         if hs is not None:
-            hs.free = self.torch.cuda.Event()
             hs.free.record()
+            hs.free_used = True
+
+    def _submit_scan(self, arena, offs, lens, chk, counts=None) -> int | None:
+        """One GPU-scan train batch in a single native call
+        (csrc/hip/train_batch.hip: H2D, scan, hashing, hot-row detection,
+        train). -> samples queued, or None when the host scanner must take
+        the batch (nothing was launched)."""
+        from ..ops import hip
+        self._sync_labels()
+        r = self.pipe.scan_batch_args(arena, offs, lens, self.labels, chk, counts)
+        if r is None:
+            return None
+        a, _ = r
+        R, n = int(a.R), int(a.n)
+        if self.LC not in hip.LABEL_CAPS or (self.mid >= hip.METHODS["CW"] and self.P is None):
+            raise ValueError("label capacity / covariance table not supported by the train kernel")
+        a.W = self.W.data_ptr()
+        a.S = self.P.data_ptr() if self.P is not None else None
+        a.active = self.active.data_ptr()
+        a.LC = self.LC
+        a.method = self.mid
+        a.C = float(self.C)
+        a.mode = self._mode(R)
+        a.merge_every = self.hot_merge
+        a.hot_waves = hip.HOT_WAVES
+        a.stats = self._train_stats.data_ptr()
+        a.touched = self.touched.data_ptr() if self.touched is not None else None
+        if n > 0 and self._hot_wanted(R):
+            hs = self._hots[self._hot_turn]
+            self._hot_turn ^= 1
+            a.hot_rows = hs.rows.data_ptr()
+            a.hot_n = hs.n.data_ptr()
+            a.hot_rep = hs.rep.data_ptr()
+            a.gkey = hs.gkey.data_ptr()
+            a.gcnt = hs.gcnt.data_ptr()
+            a.gcap = hs.CAP
+            a.block_min = 8
+            a.min_count = self.hot_min_count or max(1024, n // 128)
+            a.max_rows = min(hip.hot_max_rows(self.LC), hs.rows.numel())
+            a.hot_free = hs.free.h
+            a.hot_free_valid = int(hs.free_used)
+            hs.free_used = True
+            if self._hot_seen is None:       # learn the count without a host sync
+                a.hot_count_host = self._hot_count_buf.data_ptr()
+                a.hot_seen = self._hot_seen_ev.h
+                self._hot_seen = (self._hot_count_buf, self._hot_seen_ev)
+        hip.train_batch_submit(a)
+        return n
 
     def train_stats(self) -> dict[str, int]:
         """samples trained / samples that changed the model since creation"""
@@ -262,11 +311,11 @@ class LinearClassifier:
                 self._drain(block=True, keep=3)
                 self._sync_labels()
                 chk = self._check_record(self.labels.size())
-                post = self._detect_hot if self._hot_wanted(len(offs)) else None
-                b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk, post=post)
-                if b is not None:
+                offs = np.ascontiguousarray(offs, dtype=np.int64)
+                lens = np.ascontiguousarray(lens, dtype=np.int64)
+                n = self._submit_scan(arena, offs, lens, chk)
+                if n is not None:
                     self._scan_stats["gpu"] += 1
-                    n = self._train_batch(b)
                     chk.replay = lambda: self._train_batch(
                         self.pipe.from_arena(arena, offs, lens, True, self.labels))
                     self._pending.append(chk)
@@ -290,7 +339,10 @@ class LinearClassifier:
         R = int(offs.size)
         res = np.full(R, -1, dtype=np.int64)
         from ..ops.feature_pipeline import body_counts
+        prof = self._served_prof
+        t0 = time.perf_counter()
         with self._lock:
+            t1 = time.perf_counter()
             counts = body_counts(arena.np, offs, lens)
             chk = b = None
             if (self.gpu and self.pipe.fast and self.gpu_scan and counts is not None
@@ -298,16 +350,18 @@ class LinearClassifier:
                 self._drain(block=True, keep=3)
                 self._sync_labels()
                 chk = self._check_record(self.labels.size())
-                post = self._detect_hot if self._hot_wanted(R) else None
-                b = self.pipe.from_arena_gpu(arena, offs, lens, self.labels, chk, post=post)
-                if b is not None:
+                ta = time.perf_counter()
+                if self._submit_scan(arena, offs, lens, chk, counts) is not None:
                     self._scan_stats["gpu"] += 1
-                    self._train_batch(b)
+                    prof[6] += ta - t1
+                    prof[7] += time.perf_counter() - ta
                 else:
                     self._free_checks.append(chk)
                     chk = None
         if chk is not None:
+            t2 = time.perf_counter()
             chk.wait()                       # releases the GIL: other RPCs proceed
+            t3 = time.perf_counter()
             with self._lock:
                 if int(chk.err[0]) == 0:
                     h = chk.hist[:chk.nhist]
@@ -315,6 +369,14 @@ class LinearClassifier:
                         self.labels.add_count(lid, int(h[lid]))
                     self._free_checks.append(chk)
                     res[:] = counts
+                    # batches, requests, lock wait, submit, scan wait, finish (seconds)
+                    t4 = time.perf_counter()
+                    prof[0] += 1
+                    prof[1] += R
+                    prof[2] += t1 - t0
+                    prof[3] += t2 - t1
+                    prof[4] += t3 - t2
+                    prof[5] += t4 - t3
                     return res, {}
                 self._free_checks.append(chk)
                 self._scan_stats["replayed"] += 1

@@ -131,9 +131,15 @@ class ScanCheck:
         self.buf = hip.HostBuffer(4 * (1 + nh))   # written by the fixup kernel
         self.err = self.buf.view(np.int32, 1)
         self.hist = self.buf.view(np.int32, nh, 4)
-        self.event: torch.cuda.Event | None = None
+        self.event: hip.DevEvent | None = None
         self.replay = None        # re-runs the batch through the host scanner
         self.nhist = 0
+        self._ev: hip.DevEvent | None = None     # this record's scan-complete event
+
+    def scan_event(self) -> "hip.DevEvent":
+        if self._ev is None:
+            self._ev = hip.DevEvent()
+        return self._ev
 
     def done(self) -> bool:
         return self.event is None or self.event.query()
@@ -153,7 +159,7 @@ class DeviceBatch:
     fval: torch.Tensor        # float32 [nnz]
     labels: torch.Tensor | None   # int32 [n]
     stream_ptr: torch.Tensor  # int64 [nstreams+1]
-    ready: torch.cuda.Event | None = None   # prepared on the prep stream: wait before use
+    ready: object | None = None    # torch.cuda.Event / hip.DevEvent: prepared on the prep stream
     hot: object | None = None               # hot rows detected for this batch (classifier)
 
 
@@ -247,6 +253,21 @@ class _DeviceBufs:
         return self.t[name]
 
 
+class _ScanSet:
+    """device buffers + pinned request table + events of one GPU-scan batch
+    slot (csrc/hip/train_batch.hip); the set is reused once ``free`` (the
+    compute-stream work of its last batch) has completed"""
+
+    def __init__(self, device):
+        self.bufs = _DeviceBufs(device)
+        self.meta: torch.Tensor | None = None      # pinned [off R | len R | base R+1]
+        self.copy_done = hip.DevEvent()
+        self.ready = hip.DevEvent()
+        self.free = hip.DevEvent()
+        self.used = False
+        self.args = hip.TrainBatchArgs()
+
+
 class FeaturePipeline:
     def __init__(self, converter, device, nthreads: int | None = None):
         self.conv = converter
@@ -274,12 +295,10 @@ class FeaturePipeline:
         # the host synchronises on, not a cross-stream wait: a copy-engine
         # copy that waits on a compute-queue event can block the enqueuing
         # thread for milliseconds)
-        self._gsets = [_DeviceBufs(self.device) for _ in range(4)]
+        self._gsets: list[_ScanSet] | None = None     # created on the first GPU-scan batch
         self._gnext = 0
         self._gprev = None
-        self._gfree = [None] * 4          # event: the set's last batch has finished
-        self._scan_meta = [None] * 4      # pinned [req_off | req_len | sample_base] per set
-        self._scan_meta_ev = [None] * 4
+        self.set_wait_s = 0.0           # host time waiting for a device set to come free
 
         self._ltab = None                 # (label version, device hash, meta, blob)
         if self.fast:
@@ -364,99 +383,128 @@ class FeaturePipeline:
                           torch.from_numpy(tm).to(self.device), torch.from_numpy(blob).to(self.device))
         return self._ltab[1:]
 
-    def from_arena_gpu(self, arena: RequestArena, offs: np.ndarray, lens: np.ndarray, table,
-                       check: ScanCheck, post=None) -> DeviceBatch | None:
-        """Train batch from arena spans with the scan on the GPU
-        (csrc/hip/scan.hip): H2D of the raw arena, then scan -> fixup ->
-        fv_hash on the compute stream, no host walk. ``check`` receives the
-        batch's error bits and label counts (pinned, valid once its event
-        completes); a batch with error bits set trained nothing and must be
-        re-run through from_arena. None: a body header the host must report.
-        The device work runs on the prep stream; ``post(batch)`` is enqueued
-        there after fv_hash; the batch's ``ready`` event covers all of it."""
+    def scan_batch_args(self, arena: RequestArena, offs: np.ndarray, lens: np.ndarray, table,
+                        check: ScanCheck, counts: np.ndarray | None = None):
+        """Prepare one GPU-scan batch (csrc/hip/scan.hip -> fv_hash.hip) for
+        ``hip.train_batch_submit``: the H2D of the raw arena prefix on the
+        copy stream, scan + hashing on the prep stream, the ready event the
+        compute stream waits on. -> (args, set) with the scan / hash fields
+        filled (the caller adds the train and hot-row fields, or leaves W
+        null), or None when a request must go to the host scanner (a body
+        that does not start with an array header, or one larger than the
+        device scan stages). ``check`` receives the batch's error bits and
+        label counts (pinned, valid once ``check.event`` completes); a batch
+        with error bits set trained nothing and must be re-run on the host."""
         if not self.fast:
             raise RuntimeError("converter config is not eligible for the GPU fast path")
-        offs = np.ascontiguousarray(offs, dtype=np.int64)
-        lens = np.ascontiguousarray(lens, dtype=np.int64)
-        counts = body_counts(arena.np, offs, lens)
         if counts is None:
-            return None
+            counts = body_counts(arena.np, offs, lens)
+            if counts is None:
+                return None
         # requests the device scan does not stage (larger than its LDS window
         # or with more samples than its slot table): the host scanner takes
         # the batch right away instead of after a rejected launch
         if scan_too_big(offs, lens, counts):
             return None
         R = int(offs.size)
-        sbase = np.zeros(R + 1, np.int64)
-        np.cumsum(counts, out=sbase[1:])
-        n = int(sbase[-1])
-        used = int((offs + lens).max()) if R else 0
+        if R == 0:
+            return None
+        if self._gsets is None:
+            self._gsets = [_ScanSet(self.device) for _ in range(4)]
+        n = int(counts.sum())
+        used = int((offs + lens).max())
         empty_off = ((used + 15) & ~15) + 16
         buf_need = empty_off + 16
         sps, spn = self.rules.n_srules, self.rules.n_nrules
         slot_cap = (used // 3 + 1) * max(1, sps, spn)
-        compute = torch.cuda.current_stream(self.device)
         turn = self._gnext
         self._gnext = (turn + 1) % len(self._gsets)
-        mark = torch.cuda.Event()
-        mark.record(compute)              # everything queued so far, incl. the previous batch
-        if self._gprev is not None:
-            self._gfree[self._gprev] = mark
         self._gprev = turn
-        for ev in (self._gfree[turn], self._scan_meta_ev[turn]):
-            if ev is not None:
-                ev.synchronize()
-        meta = self._scan_meta[turn]
-        if meta is None or meta.numel() < 3 * R + 1:
-            meta = self._scan_meta[turn] = torch.empty(_grow(1024, 3 * R + 1), dtype=torch.int64,
-                                                       pin_memory=True)
-        mnp = meta.numpy()
+        st = self._gsets[turn]
+        if st.used:
+            t0 = time.perf_counter()
+            st.free.synchronize()          # its last batch's train (and so its copies) finished
+            self.set_wait_s += time.perf_counter() - t0
+        st.used = True
+        if st.meta is None or st.meta.numel() < 3 * R + 1:
+            st.meta = torch.empty(_grow(1024, 3 * R + 1), dtype=torch.int64, pin_memory=True)
+        mnp = st.meta.numpy()
         mnp[:R] = offs
         mnp[R:2 * R] = lens
-        mnp[2 * R:3 * R + 1] = sbase
-        dev = self._gsets[turn]
-        d_buf = dev.get("buf", buf_need, torch.uint8)
-        d_meta = dev.get("scan_meta", 3 * R + 1, torch.int64)
-        d_off = dev.get("datum_off", max(n, 1), torch.int64)
-        d_len = dev.get("datum_len", max(n, 1), torch.int32)
-        d_row = dev.get("row_ptr", n + 1, torch.int64)
-        d_lab = dev.get("labels", max(n, 1), torch.int32)
-        d_slots = dev.get("req_slots", max(R, 1), torch.int64)
-        d_idx = dev.get("fidx", slot_cap, torch.int32)
-        d_val = dev.get("fval", slot_cap, torch.float32)
-        d_hist = dev.get("label_hist", check.hist.size, torch.int32)
-        d_err = dev.get("scan_err", 1, torch.int32)
-        cs = self._copy_stream
-        with torch.cuda.stream(cs):
-            if used:
-                d_buf[:used].copy_(arena.buf[:used], non_blocking=True)
-            d_meta[:3 * R + 1].copy_(meta[:3 * R + 1], non_blocking=True)
-        cev = torch.cuda.Event()
-        cev.record(cs)
-        self._scan_meta_ev[turn] = cev
-        prep = self._prep_stream
-        prep.wait_event(cev)
-        with torch.cuda.stream(prep):
-            th, tm, tb = self.label_table(table)
-            d_sb = d_meta[2 * R:3 * R + 1]
-            nh = check.hist.size
-            check.err[0] = -1                 # not yet written
-            hip.scan_train(d_buf, used, d_meta[:R], d_meta[R:2 * R], d_sb, R, n, th, tm, tb, sps,
-                           spn, d_off, d_len, d_lab, d_row, d_slots, d_hist[:nh], d_err, empty_off,
-                           check.buf)
-            check.nhist = nh
-            check.event = torch.cuda.Event()
-            check.event.record(prep)
-            if n > 0:
-                hip.fv_hash(d_buf, empty_off + 3, d_off, d_len, d_row, n, self.d_srules,
-                            self.rules.n_srules, self.d_nrules, self.rules.n_nrules, self.d_blob,
-                            self.H, d_idx, d_val, self.err)
-            b = DeviceBatch(n, slot_cap, R, d_row, d_idx, d_val, d_lab, d_sb)
-            if post is not None and n > 0:
-                post(b)
-            b.ready = torch.cuda.Event()
-            b.ready.record(prep)
-        return b
+        mnp[2 * R] = 0
+        np.cumsum(counts, out=mnp[2 * R + 1:3 * R + 1])
+        dev = st.bufs
+        g = dev.get
+        a = st.args
+        d_buf = g("buf", buf_need, torch.uint8)
+        a.d_buf = d_buf.data_ptr()
+        a.buf_cap = d_buf.numel()
+        a.d_meta = g("scan_meta", 3 * R + 1, torch.int64).data_ptr()
+        a.d_off = g("datum_off", max(n, 1), torch.int64).data_ptr()
+        a.d_len = g("datum_len", max(n, 1), torch.int32).data_ptr()
+        a.d_row = g("row_ptr", n + 1, torch.int64).data_ptr()
+        a.d_lab = g("labels", max(n, 1), torch.int32).data_ptr()
+        a.d_slots = g("req_slots", R, torch.int64).data_ptr()
+        a.d_idx = g("fidx", slot_cap, torch.int32).data_ptr()
+        a.d_val = g("fval", slot_cap, torch.float32).data_ptr()
+        a.d_hist = g("label_hist", check.hist.size, torch.int32).data_ptr()
+        a.d_err = g("scan_err", 1, torch.int32).data_ptr()
+        if not a.copy_stream:                # constant for the set
+            a.copy_stream = self._copy_stream.cuda_stream
+            a.prep_stream = self._prep_stream.cuda_stream
+            a.copy_done = st.copy_done.h
+            a.ready = st.ready.h
+            a.set_free = st.free.h
+            a.srules = self.d_srules.data_ptr()
+            a.nrules = self.d_nrules.data_ptr()
+            a.n_srules = sps
+            a.n_nrules = spn
+            a.blob = self.d_blob.data_ptr()
+            a.blob_len = self.d_blob.numel()
+            a.H = self.H
+            a.hash_err = self.err.data_ptr()
+        a.compute_stream = torch.cuda.current_stream(self.device).cuda_stream
+        ev = check.scan_event()
+        a.check_done = ev.h
+        a.host_out = check.buf.ptr
+        a.nhist = check.hist.size
+        check.nhist = check.hist.size
+        check.event = ev
+        th, tm, tb = self.label_table(table)
+        a.lt_hash = th.data_ptr()
+        a.lt_meta = tm.data_ptr()
+        a.lt_cap = th.numel()
+        a.lt_blob = tb.data_ptr()
+        a.lt_blob_len = tb.numel()
+        a.sps = sps
+        a.spn = spn
+        a.arena = arena.buf.data_ptr()
+        a.used = used
+        a.meta_host = st.meta.data_ptr()
+        a.R = R
+        a.n = n
+        a.empty_off = empty_off
+        a.slot_cap = slot_cap
+        a.hot_rows = None
+        a.hot_count_host = None
+        a.W = None
+        return a, st
+
+    def from_arena_gpu(self, arena: RequestArena, offs: np.ndarray, lens: np.ndarray, table,
+                       check: ScanCheck) -> DeviceBatch | None:
+        """A GPU-scan batch without training (tests, tools): the device CSR
+        of the scanned and hashed requests; its ``ready`` event covers the
+        work. None: a request the host scanner must take."""
+        offs = np.ascontiguousarray(offs, dtype=np.int64)
+        lens = np.ascontiguousarray(lens, dtype=np.int64)
+        r = self.scan_batch_args(arena, offs, lens, table, check)
+        if r is None:
+            return None
+        a, st = r
+        hip.train_batch_submit(a)
+        R, n, t = int(a.R), int(a.n), st.bufs.t
+        return DeviceBatch(n, int(a.slot_cap), R, t["row_ptr"], t["fidx"], t["fval"], t["labels"],
+                           t["scan_meta"][2 * R:3 * R + 1], ready=st.ready)
 
     def _launch(self, pin: "_Pinned", src: torch.Tensor, n: int, nbytes: int, nslots: int,
                 R: int, labeled: bool) -> DeviceBatch:

@@ -22,6 +22,14 @@ _u64 = ctypes.c_uint64
 _f32 = ctypes.c_float
 
 _SIGS = {
+    "jb_train_batch_submit": [_c_void_p],
+    "jb_train_batch_args_bytes": [],
+    "jb_event_create": [],
+    "jb_event_destroy": [_i64],
+    "jb_event_record": [_i64, _c_void_p],
+    "jb_stream_wait_event": [_c_void_p, _i64],
+    "jb_event_query": [_i64],
+    "jb_event_sync": [_i64],
     "jb_fv_hash": [_c_void_p, _i64, _i64, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32,
                    _c_void_p, _i32, _c_void_p, _i32, _u64, _c_void_p, _c_void_p, _c_void_p,
                    _c_void_p],
@@ -417,7 +425,7 @@ def _fn(name: str):
         lib = hip_lib()
         raw = getattr(lib, name)
         raw.argtypes = _SIGS[name]
-        raw.restype = ctypes.c_int64 if name.endswith("_bytes") else ctypes.c_int
+        raw.restype = ctypes.c_int64 if name.endswith(("_bytes", "_create")) else ctypes.c_int
         tag = "hip." + name[3:]
 
         def f(*args, _raw=raw, _tag=tag):
@@ -570,7 +578,8 @@ class HotRows:
         self.rows = torch.zeros(HOT_MAX_ROWS, dtype=torch.int32, device=device)
         self.n = torch.zeros(1, dtype=torch.int32, device=device)
         self.rep = torch.zeros(_fn("jb_hot_rep_bytes")() // 4, dtype=torch.float32, device=device)
-        self.free = None        # event: the train launch that read this set has run
+        self.free = DevEvent()  # recorded after the train launch that read this set
+        self.free_used = False  # recorded at least once
         self.gkey = torch.full((self.CAP,), -1, dtype=torch.int32, device=device)
         self.gcnt = torch.zeros(self.CAP, dtype=torch.int32, device=device)
 
@@ -641,6 +650,85 @@ def regression_estimate(row_ptr, fidx, fval, n: int, W, out) -> None:
     rc = _fn("jb_regression_estimate")(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), _p(out),
                                        _stream())
     _check(rc, "jb_regression_estimate")
+
+
+# ------------------------------------------------------- train batch submit
+class DevEvent:
+    """A HIP event owned by the caller (csrc/hip/train_batch.hip event API):
+    the events of the one-call train batch submit. Duck-types the parts of
+    torch.cuda.Event the pipeline uses (query / synchronize / record)."""
+
+    def __init__(self):
+        self.h = int(_fn("jb_event_create")())
+        if not self.h:
+            raise RuntimeError("hipEventCreate failed")
+        self._destroy = _fn("jb_event_destroy")
+
+    def record(self, stream: int | None = None) -> None:
+        _check(_fn("jb_event_record")(self.h, _stream() if stream is None else stream),
+               "jb_event_record")
+
+    def wait_on(self, stream: int | None = None) -> None:
+        """make ``stream`` (default: the current one) wait for this event"""
+        _check(_fn("jb_stream_wait_event")(_stream() if stream is None else stream, self.h),
+               "jb_stream_wait_event")
+
+    def query(self) -> bool:
+        rc = _fn("jb_event_query")(self.h)
+        if rc not in (0, 1):
+            raise RuntimeError(f"hipEventQuery failed (code {rc})")
+        return rc == 0
+
+    def synchronize(self) -> None:
+        _check(_fn("jb_event_sync")(self.h), "jb_event_sync")
+
+    def __del__(self):
+        if getattr(self, "h", 0):
+            self._destroy(self.h)
+            self.h = 0
+
+
+def stream_wait(ev, stream=None) -> None:
+    """make ``stream`` (a torch stream; default the current one) wait for a
+    torch.cuda.Event or a DevEvent"""
+    if isinstance(ev, DevEvent):
+        ev.wait_on(None if stream is None else stream.cuda_stream)
+    elif stream is None:
+        torch.cuda.current_stream().wait_event(ev)
+    else:
+        stream.wait_event(ev)
+
+
+_TB_FIELDS = """copy_stream prep_stream compute_stream copy_done check_done ready set_free hot_free
+hot_seen arena used:i meta_host R:i n:i d_buf buf_cap:i empty_off:i d_meta d_off d_len d_lab d_row
+d_slots d_hist nhist:i d_err host_out lt_hash lt_meta lt_cap:i lt_blob lt_blob_len:i sps:i spn:i
+srules nrules n_srules:i n_nrules:i blob blob_len:i H:i d_idx d_val slot_cap:i hash_err hot_rows
+hot_n hot_rep gkey gcnt gcap:i block_min:i min_count:i max_rows:i hot_free_valid:i hot_count_host
+W S active LC:i method:i C:d mode:i merge_every:i hot_waves:i stats touched""".split()
+
+
+class TrainBatchArgs(ctypes.Structure):
+    """csrc/hip/train_batch.hip JbTrainBatch (every field 8 bytes; the
+    unsuffixed names are pointers / handles)"""
+    _fields_ = [(f.split(":")[0], {"i": _i64, "d": ctypes.c_double}.get(f.partition(":")[2],
+                                                                        _c_void_p))
+                for f in _TB_FIELDS]
+
+
+def train_batch_submit(a: TrainBatchArgs) -> None:
+    """one call: H2D -> scan -> fv_hash -> [hot detect] -> train (see
+    csrc/hip/train_batch.hip); the caller has checked the capacities"""
+    global _tb_checked
+    if not _tb_checked:
+        want = int(_fn("jb_train_batch_args_bytes")())
+        if want != ctypes.sizeof(TrainBatchArgs):
+            raise RuntimeError(f"TrainBatchArgs is {ctypes.sizeof(TrainBatchArgs)} bytes, "
+                               f"the library expects {want}")
+        _tb_checked = True
+    _check(_fn("jb_train_batch_submit")(ctypes.addressof(a)), "jb_train_batch_submit")
+
+
+_tb_checked = False
 
 
 # ------------------------------------------------------------ direct classify

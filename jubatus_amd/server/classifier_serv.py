@@ -248,7 +248,7 @@ class ClassifierServ(ServerBase):
         import torch
         from ..ops.feature_pipeline import RequestArena
         mb = int(os.environ.get("JUBATUS_TRAIN_ARENA_MB", "32"))
-        nslots = 4
+        nslots = int(os.environ.get("JUBATUS_ARENA_THREADS", "2")) + 2
         self._arena_slots = [torch.empty(mb << 20, dtype=torch.uint8, pin_memory=True)
                              for _ in range(nslots)]
         views = [RequestArena.over(t, [], []) for t in self._arena_slots]

@@ -30,6 +30,26 @@ def free_port():
     return p
 
 
+def free_port_block(n: int = 4) -> int:
+    """a free port whose next n ports are free too (jubavisor hands its
+    children the ports after its own)"""
+    for _ in range(200):
+        base = free_port()
+        socks = []
+        try:
+            for q in range(base, base + n + 1):
+                s = socket.socket()
+                socks.append(s)
+                s.bind(("127.0.0.1", q))
+            return base
+        except OSError:
+            continue
+        finally:
+            for s in socks:
+                s.close()
+    raise RuntimeError("no free port block")
+
+
 @pytest.fixture
 def coord():
     srv = CoordinatorServer(0, "127.0.0.1").start()
@@ -126,7 +146,7 @@ def _cluster_roundtrip(zk, ls, tmp_path, gpus=0):
 def test_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
-    vport = free_port()
+    vport = free_port_block()
     visor = Jubavisor(zk, vport, max_children=4, listen_addr="127.0.0.1", gpus=2)
     rpc = RpcServer(2)
     rpc.add("start", visor.start, arity=3)
@@ -158,7 +178,7 @@ def _native_visor(zk, vport, tmp_path, maxc=4, gpus=None):
 def test_native_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
-    vport = free_port()
+    vport = free_port_block()
     proc, err = _native_visor(zk, vport, tmp_path, gpus=2)
     ls = CoordinatorClient(zk, timeout=5.0)
     try:
@@ -176,7 +196,7 @@ def test_native_jubavisor_rpc_errors_and_shutdown(coord, tmp_path, monkeypatch):
     """bad names / arity, pool exhaustion, and SIGTERM stopping the children"""
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
-    vport = free_port()
+    vport = free_port_block(1)
     proc, err = _native_visor(zk, vport, tmp_path, maxc=1)
     ls = CoordinatorClient(zk, timeout=5.0)
     argv = argv_to_wire({"threadnum": 2, "timeout": 10, "interval_sec": 0, "interval_count": 0,

@@ -42,7 +42,7 @@ def main():
     torch.cuda.synchronize()
     assert int(chk.err[0]) == 0
     # kernel-only timing through the profile entry point
-    dset = pipe._gsets[pipe._gprev]
+    dset = pipe._gsets[pipe._gprev].bufs
     R = nreq
     n = nreq * per
     th, tm, tb = pipe.label_table(clf.labels)
