@@ -300,7 +300,7 @@ def main() -> None:
                     help="measure only the served path (prints its record; not the headline)")
     ap.add_argument("--rpc-seconds", type=float, default=4.0)
     ap.add_argument("--rpc-conns", type=int, default=64)
-    ap.add_argument("--rpc-depth", type=int, default=16)
+    ap.add_argument("--rpc-depth", type=int, default=32)
     ap.add_argument("--rpc-threads", type=int, default=32,
                     help="server RPC threads (a quarter of them are epoll IO threads)")
     ap.add_argument("--rpc-distinct", type=int, default=512, help="distinct train requests cycled")

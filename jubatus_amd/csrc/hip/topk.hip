@@ -287,117 +287,206 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   }
 }
 
-// Several queries per table pass (MODE 0, W <= 2 signature words): a block
-// loads each tile's signatures / norms / valid flags ONCE into registers and
-// runs the threshold-pruned selection of every query against them, each
-// query with its own carry in LDS. The single-query kernel's grid is
-// (blocks, nq): every query re-reads the whole table (8 queries at 10M rows
-// moved 4x the table through HBM, profiles/r02_pmc_*); here the table is
-// read once per batch of queries. Output layout as topk_kernel's.
-// Measured (profiles/r02_pmc_roofline.md, 10M rows, 8 queries, k 10): the
-// table traffic drops from 4x to 1x (63 MiB) but the kernel takes 686 us
-// vs 336 us for the (blocks, nq) grid - the queries' selections serialize
-// inside a block and the re-reads hit the 256 MB MALL anyway - so it is
-// opt-in (JB_TOPK_MQ=1) until the selection itself is batched.
-constexpr int kMqMax = 8;
-template <int NW, int W>
-__global__ __launch_bounds__(NW * 64) void topk_mq_kernel(const TopkSrc s, int nq, int64_t n,
-                                                          int64_t per_block, int k,
-                                                          float* __restrict__ out_d,
-                                                          int32_t* __restrict__ out_i) {
-  constexpr int T = NW * 64;
-  constexpr int TILE = T * kTopR;
-  __shared__ float s_wd[NW * kTopMaxK];
-  __shared__ int s_wi[NW * kTopMaxK];
-  __shared__ int s_cnt[NW];
-  __shared__ float s_cbd[kMqMax][2][kTopMaxK];
-  __shared__ int s_cbi[kMqMax][2][kTopMaxK];
-  __shared__ float s_thr[kMqMax];
-  __shared__ int s_cc[kMqMax], s_cur[kMqMax];
-  __shared__ uint64_t s_q[kMqMax][W];
-  __shared__ float s_qn[kMqMax];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int i = t; i < nq * W; i += T) s_q[i / W][i % W] = s.qbits[(int64_t)(i / W) * s.words + i % W];
-  if (t < nq) {
-    s_qn[t] = s.qnorm[t];
-    s_thr[t] = INFINITY;
-    s_cc[t] = 0;
-    s_cur[t] = 0;
+// Several queries per table pass (MODE 0, W <= 2 signature words): waves
+// per query. A block of 16 waves loads each tile of 8192 rows (signatures,
+// and the norm with the valid flag folded in) into LDS once; the G = 16 / nq
+// waves of a query (G a power of two) take every G-th 512-row chunk of the
+// tile and run the threshold-pruned selection with a wave-private carry
+// (merged by rank inside the wave): no block barrier per query, and the table
+// crosses HBM once per batch of up to 8 queries instead of once per query
+// (the (blocks, nq) grid re-reads it). A query's G carries merge at the end.
+// euclid_lsh takes cos(pi h / hash_num) from a per-block table of the
+// hash_num + 1 values (the same expression as load_item, so distances are
+// bit-identical). Each wave visits its rows in increasing index order, so the
+// tie rule of topk_kernel holds. Output layout as topk_kernel's.
+constexpr int kWqWaves = 16;
+constexpr int kWqT = kWqWaves * 64;
+constexpr int kWqLoads = 4;                       // rows a thread stages per tile
+constexpr int kWqTile = kWqT * kWqLoads;          // 4096 rows per tile
+constexpr int kWqChunks = kWqTile / 512;          // 512-row chunks (8 rows a lane)
+
+// wave-level LDS ordering: the lanes of one wave read what others wrote
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// merge two sorted lists of distinct (d, ix) pairs into the k smallest (one wave)
+__device__ __forceinline__ int wave_merge(const float* ad, const int* ai, int na, const float* bd,
+                                          const int* bi, int nb, int k, float* od, int* oi,
+                                          int lane) {
+  for (int e = lane; e < na + nb; e += 64) {
+    const bool inA = e < na;
+    const int i = inA ? e : e - na;
+    const float v = inA ? ad[i] : bd[i];
+    const int id = inA ? ai[i] : bi[i];
+    const int r = i + (inA ? rank_in(bd, bi, nb, v, id) : rank_in(ad, ai, na, v, id));
+    if (r < k) { od[r] = v; oi[r] = id; }
   }
-  __syncthreads();
+  return na + nb < k ? na + nb : k;
+}
+
+template <int W>
+__global__ __launch_bounds__(kWqT) void topk_wq_kernel(const TopkSrc s, int nq, int64_t n,
+                                                       int64_t per_block, int k,
+                                                       float* __restrict__ out_d,
+                                                       int32_t* __restrict__ out_i) {
+  __shared__ uint64_t s_bits[kWqTile * W];
+  __shared__ float s_nv[kWqTile];                 // norm, or -1 for an invalid row
+  __shared__ float s_lut[64 * W + 1];
+  __shared__ float s_cd[kWqWaves][2][kTopMaxK];   // per-wave carry, double-buffered
+  __shared__ int s_ci[kWqWaves][2][kTopMaxK];
+  __shared__ float s_wd[kWqWaves][kTopMaxK];      // per-wave winners of a chunk
+  __shared__ int s_wi[kWqWaves][kTopMaxK];
+  __shared__ int s_cc[kWqWaves], s_cur[kWqWaves];
+  const int t = threadIdx.x, lane = t & 63;
+  // wave-uniform in scalar registers: the query's bits and norm come from
+  // scalar loads, so no vector-memory wait inside the scan waits for them
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  int G = kWqWaves;                               // waves per query
+  while (G > 1 && G * nq > kWqWaves) G >>= 1;
+  const int q = wv / G, part = wv % G;
+  const bool active = q < nq;
+  const int qq = active ? q : 0;
+  const bool euclid = s.metric == 1;
+  uint64_t qb[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) qb[w] = s.qbits[(int64_t)qq * s.words + w];
+  const float qn = s.qnorm[qq];
+  const float hn = (float)s.hash_num;
+  // per hamming distance h: cos(pi h / hash_num) (euclid_lsh) or h / hash_num
+  // (lsh / minhash), the expressions of load_item
+  for (int h = t; h <= s.hash_num && h <= 64 * W; h += kWqT)
+    s_lut[h] = euclid ? __cosf(3.14159265f * ((float)h / hn)) : (float)h / hn;
+  int cur = 0, cc = 0;                             // wave-uniform
+  float thr = INFINITY;
   const int64_t b0 = (int64_t)blockIdx.x * per_block;
   const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
-  float* wd = &s_wd[wv * k];
-  int* wi = &s_wi[wv * k];
-  const float inv = 1.f / (float)s.hash_num;
-  for (int64_t base = b0; base < b1; base += TILE) {
-    // the tile's rows, loaded once (unpredicated: clamped row index)
-    uint64_t rb[kTopR][W];
-    float rn[kTopR];
-    bool ok[kTopR];
+  // the next tile's rows are fetched into registers while the current one is
+  // scanned from LDS (the HBM latency hides behind the selection)
+  uint64_t pb[kWqLoads][W];
+  float pn[kWqLoads];
+  uint32_t pv[kWqLoads];
+  auto fetch = [&](int64_t base) {      // plain loads only: no branch waits on them
 #pragma unroll
-    for (int r = 0; r < kTopR; ++r) {
-      const int64_t row = base + (int64_t)r * T + t;
-      const int64_t rc = row < b1 ? row : b1 - 1;
+    for (int r = 0; r < kWqLoads; ++r) {
+      const int64_t row = base + r * kWqT + t;
+      const int64_t rc = row < b1 ? row : b1 - 1;  // clamped, never out of range
 #pragma unroll
-      for (int w = 0; w < W; ++w) rb[r][w] = s.tbits[rc * s.words + w];
-      rn[r] = s.metric == 1 ? s.tnorm[rc] : 0.f;
-      ok[r] = row < b1 && s.valid[rc];
+      for (int w = 0; w < W; ++w) pb[r][w] = s.tbits[rc * W + w];
+      pn[r] = euclid ? s.tnorm[rc] : 0.f;
+      pv[r] = s.valid[rc];
     }
-    for (int q = 0; q < nq; ++q) {
-      const float thr = s_thr[q];
-      const float qn = s_qn[q];
+  };
+  if (b0 < b1) fetch(b0);
+  for (int64_t base = b0; base < b1; base += kWqTile) {
+    __syncthreads();                               // the previous tile is consumed
+#pragma unroll
+    for (int r = 0; r < kWqLoads; ++r) {
+      const int j = r * kWqT + t;
+#pragma unroll
+      for (int w = 0; w < W; ++w) s_bits[j * W + w] = pb[r][w];
+      s_nv[j] = (base + j < b1 && pv[r] != 0) ? pn[r] : -1.f;
+    }
+    __syncthreads();
+    if (base + kWqTile < b1) fetch(base + kWqTile);
+    if (!active) continue;
+    for (int c = part; c < kWqChunks; c += G) {
       float d[kTopR];
       int ix[kTopR];
       bool any = false;
+      // euclid: rows whose squared distance is surely above thr^2 skip the sqrt
+      const float thr2 = thr < INFINITY ? thr * thr * 1.0001f + 1e-30f : INFINITY;
 #pragma unroll
-      for (int r = 0; r < kTopR; ++r) {
+      for (int i = 0; i < kTopR; ++i) {
+        const int j = c * 512 + i * 64 + lane;
         int ham = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) ham += __popcll(s_q[q][w] ^ rb[r][w]);
-        const float frac = (float)ham * inv;
-        float v = s.metric == 1
-                      ? sqrtf(fmaxf(0.f, qn * qn + rn[r] * rn[r] -
-                                         2.f * qn * rn[r] * __cosf(3.14159265f * frac)))
-                      : frac;
-        if (!ok[r] || v >= thr) v = INFINITY;
-        d[r] = v;
-        ix[r] = v < INFINITY ? (int)(base + (int64_t)r * T + t) : INT_MAX;
+        for (int w = 0; w < W; ++w) ham += __popcll(qb[w] ^ s_bits[j * W + w]);
+        const float b = s_nv[j];
+        float v;
+        if (euclid) {
+          const float x = qn * qn + b * b - 2.f * qn * b * s_lut[ham];
+          v = x > thr2 ? INFINITY : sqrtf(fmaxf(0.f, x));
+        } else {
+          v = s_lut[ham];
+        }
+        if (b < 0.f || v >= thr) v = INFINITY;
+        d[i] = v;
+        ix[i] = v < INFINITY ? (int)(base + j) : INT_MAX;
         any |= v < INFINITY;
       }
-      int cnt = 0;
-      if (__ballot(any)) {
-        sort_regs<kTopR>(d, ix);
-        wave_pop<kTopR>(d, ix, k, wd, wi, lane, &cnt);
-      } else {
-        for (int j = lane; j < k; j += 64) { wd[j] = INFINITY; wi[j] = INT_MAX; }
-      }
-      if (lane == 0) s_cnt[wv] = cnt;
-      __syncthreads();
+      if (!__ballot(any)) continue;                // wave-uniform
+      // survivors per register slot: past the first chunks a handful per
+      // wave, which are compacted and ranked directly (no register sort and
+      // no k pop rounds); a chunk with more than 64 takes the pop path
+      uint64_t masks[kTopR];
       int total = 0;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) total += s_cnt[w];
-      if (total > 0) {                       // block-uniform
-        const int cur = s_cur[q];
-        const int nn = rank_merge<NW>(s_cbd[q][cur], s_cbi[q][cur], s_cc[q], s_wd, s_wi, s_cnt, k,
-                                      s_cbd[q][cur ^ 1], s_cbi[q][cur ^ 1], t, T);
-        __syncthreads();
-        if (t == 0) {
-          s_cur[q] = cur ^ 1;
-          s_cc[q] = nn;
-          s_thr[q] = nn == k ? s_cbd[q][cur ^ 1][k - 1] : INFINITY;
-        }
+      for (int i = 0; i < kTopR; ++i) {
+        masks[i] = __ballot(d[i] < INFINITY);
+        total += __popcll(masks[i]);
       }
-      __syncthreads();
+      int cnt = 0;
+      float* wd = s_wd[wv];
+      int* wi = s_wi[wv];
+      if (total <= 64) {
+        int at = 64;                               // raw survivors at [64, 64 + total)
+#pragma unroll
+        for (int i = 0; i < kTopR; ++i) {
+          if (d[i] < INFINITY) {
+            const int pos = at + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(masks[i] >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)masks[i], 0u));
+            wd[pos] = d[i];
+            wi[pos] = ix[i];
+          }
+          at += __popcll(masks[i]);
+        }
+        wave_sync();
+        if (lane < total) {                        // sorted into [0, total) by rank
+          const float v = wd[64 + lane];
+          const int id = wi[64 + lane];
+          int r = 0;
+          for (int e = 0; e < total; ++e) r += lt_pair(wd[64 + e], wi[64 + e], v, id) ? 1 : 0;
+          wd[r] = v;
+          wi[r] = id;
+        }
+        cnt = total < k ? total : k;
+      } else {
+        sort_regs<kTopR>(d, ix);
+        wave_pop<kTopR>(d, ix, k, wd, wi, lane, &cnt);
+      }
+      wave_sync();
+      cc = wave_merge(s_cd[wv][cur], s_ci[wv][cur], cc, s_wd[wv], s_wi[wv], cnt, k,
+                      s_cd[wv][cur ^ 1], s_ci[wv][cur ^ 1], lane);
+      cur ^= 1;
+      wave_sync();
+      thr = cc == k ? s_cd[wv][cur][k - 1] : INFINITY;
     }
   }
-  for (int q = 0; q < nq; ++q) {
-    const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
-    const int cur = s_cur[q], cc = s_cc[q];
-    for (int j = t; j < k; j += T) {
-      out_d[o + j] = j < cc ? s_cbd[q][cur][j] : INFINITY;
-      out_i[o + j] = j < cc ? s_cbi[q][cur][j] : INT_MAX;
+  if (lane == 0) {
+    s_cc[wv] = cc;
+    s_cur[wv] = cur;
+  }
+  __syncthreads();
+  if (!active || part != 0) return;
+  // the query's first wave folds in the carries of its other G - 1 waves
+  for (int g = 1; g < G; ++g) {
+    const int ow = wv + g;
+    cc = wave_merge(s_cd[wv][cur], s_ci[wv][cur], cc, s_cd[ow][s_cur[ow]], s_ci[ow][s_cur[ow]],
+                    s_cc[ow], k, s_wd[wv], s_wi[wv], lane);
+    wave_sync();
+    for (int j = lane; j < cc; j += 64) {
+      s_cd[wv][cur][j] = s_wd[wv][j];
+      s_ci[wv][cur][j] = s_wi[wv][j];
     }
+    wave_sync();
+  }
+  const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
+  for (int j = lane; j < k; j += 64) {
+    out_d[o + j] = j < cc ? s_cd[wv][cur][j] : INFINITY;
+    out_i[o + j] = j < cc ? s_ci[wv][cur][j] : INT_MAX;
   }
 }
 
@@ -724,15 +813,16 @@ inline bool merge_with_tile() {
 template <int MODE>
 inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
                         int k, float* out_d, int32_t* out_i, hipStream_t stream) {
-  static const bool mq_on = getenv("JB_TOPK_MQ") != nullptr;
-  if (MODE == 0 && nq > 1 && nq <= kMqMax && s.words <= 2 && mq_on) {
-    // several queries per table pass (topk_mq_kernel)
+  static const bool wq_off = getenv("JB_TOPK_WQ_OFF") != nullptr;
+  if (MODE == 0 && nq > 1 && nq <= kWqWaves && s.words <= 2 && s.hash_num <= 64 * s.words &&
+      !wq_off) {
+    // several queries per table pass, one wave per query (topk_wq_kernel)
     if (s.words == 1)
-      hipLaunchKernelGGL((topk_mq_kernel<4, 1>), dim3(blocks), dim3(4 * 64), 0, stream, s, nq,
-                         nrows, per_block, k, out_d, out_i);
+      hipLaunchKernelGGL((topk_wq_kernel<1>), dim3(blocks), dim3(kWqT), 0, stream, s, nq, nrows,
+                         per_block, k, out_d, out_i);
     else
-      hipLaunchKernelGGL((topk_mq_kernel<4, 2>), dim3(blocks), dim3(4 * 64), 0, stream, s, nq,
-                         nrows, per_block, k, out_d, out_i);
+      hipLaunchKernelGGL((topk_wq_kernel<2>), dim3(blocks), dim3(kWqT), 0, stream, s, nq, nrows,
+                         per_block, k, out_d, out_i);
     return;
   }
   if (scan_waves(k, nq, nrows) == 16)

@@ -179,27 +179,34 @@ def test_default_clustering_config_runs_on_device(method):
     np.testing.assert_allclose(np.asarray(got2), np.asarray(ref), atol=0.05)
 
 
-@pytest.mark.parametrize("metric,k,nrows,nq", [(0, 10, 100_000, 3), (1, 10, 250_000, 2),
-                                               (2, 1, 5000, 4), (1, 128, 70_000, 2),
-                                               (0, 37, 3000, 5), (1, 100, 50, 1)])
-def test_topk_hamming_matches_full_sort(metric, k, nrows, nq):
+@pytest.mark.parametrize("metric,k,nrows,nq,bits", [(0, 10, 100_000, 3, 64), (1, 10, 250_000, 2, 64),
+                                                    (2, 1, 5000, 4, 64), (1, 128, 70_000, 2, 64),
+                                                    (0, 37, 3000, 5, 64), (1, 100, 50, 1, 64),
+                                                    (0, 10, 400_000, 8, 64), (1, 31, 300_000, 8, 100),
+                                                    (2, 100, 200_000, 7, 128)])
+def test_topk_hamming_matches_full_sort(metric, k, nrows, nq, bits):
     """csrc/hip/topk.hip (fused scan + exact top-k) == full distance matrix
     + stable argsort, including ties (lsh/minhash distances are multiples of
-    1/hash_num) and invalid rows."""
+    1/hash_num) and invalid rows. 2..8 queries with <= 128 bits take the
+    one-wave-per-query kernel (topk_wq_kernel)."""
     import torch
     from jubatus_amd.ops import hip
     g = torch.Generator().manual_seed(nrows + k)
-    words = 1
+    words = (bits + 63) // 64
     tb = torch.randint(-2**62, 2**62, (nrows, words), generator=g, dtype=torch.int64)
+    qb = torch.randint(-2**62, 2**62, (nq, words), generator=g, dtype=torch.int64)
+    if bits % 64:                        # bits past hash_num are zero in a signature
+        mask = (1 << (bits % 64)) - 1
+        tb[:, -1] &= mask
+        qb[:, -1] &= mask
     tn = torch.rand(nrows, generator=g) * 3
     valid = (torch.rand(nrows, generator=g) > 0.1).to(torch.uint8)
-    qb = torch.randint(-2**62, 2**62, (nq, words), generator=g, dtype=torch.int64)
     qn = torch.rand(nq, generator=g) * 3
     d = dev()
     tbd, tnd, vd, qbd, qnd = (x.to(d) for x in (tb, tn, valid, qb, qn))
     full = torch.empty((nq, nrows), dtype=torch.float32, device=d)
-    hip.hamming_scan(qbd, qnd, nq, tbd, tnd, vd, nrows, 64, metric, full)
-    od, oi = hip.topk_hamming(qbd, qnd, nq, tbd, tnd, vd, nrows, 64, metric, k)
+    hip.hamming_scan(qbd, qnd, nq, tbd, tnd, vd, nrows, bits, metric, full)
+    od, oi = hip.topk_hamming(qbd, qnd, nq, tbd, tnd, vd, nrows, bits, metric, k)
     full = full.cpu().numpy()
     od, oi = od.cpu().numpy(), oi.cpu().numpy()
     for q in range(nq):
@@ -434,9 +441,9 @@ def test_topk_forced_variants_match_default():
             "qn=torch.ones(3,device=d);dd,rr=hip.topk_hamming(qb,qn,3,tb,tn,v,n,16,0,10);"
             "print(json.dumps(rr.cpu().numpy().tolist()))")
     outs = []
-    for env in ({}, {"JB_TOPK_NW": "16"}, {"JB_TOPK_MERGE": "tile"}):
+    for env in ({}, {"JB_TOPK_NW": "16"}, {"JB_TOPK_MERGE": "tile"}, {"JB_TOPK_WQ_OFF": "1"}):
         r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env),
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    assert outs[0] == outs[1] == outs[2]
+    assert outs[0] == outs[1] == outs[2] == outs[3]

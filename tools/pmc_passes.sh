@@ -2,7 +2,7 @@ set -e
 mkdir -p gpurun_out/pmc
 timeout -k 10 300 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_gpu_engines.py -k "topk or pool or sparse" > gpurun_out/pmc/tests.log 2>&1
 timeout -k 10 200 python -u tools/pmc_engines.py > gpurun_out/pmc/eng_time.jsonl 2>&1
-JB_TOPK_MQ_OFF=1 timeout -k 10 200 python -u tools/pmc_engines.py > gpurun_out/pmc/eng_time_mqoff.jsonl 2>&1
+JB_TOPK_WQ_OFF=1 timeout -k 10 200 python -u tools/pmc_engines.py > gpurun_out/pmc/eng_time_wqoff.jsonl 2>&1
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 P="python3 tools/pmc_engines.py --iters 5"
 B="python3 bench.py --steps 3 --warmup 1 --no-rpc --batches-per-step 4 --warmup-pools 2 --latency-iters 5"
