@@ -267,6 +267,102 @@ def served_train(args, local: int, nat) -> dict:
         h.stop()
 
 
+def _proc_cpu(pid: int) -> float:
+    tck = os.sysconf("SC_CLK_TCK")
+    with open(f"/proc/{pid}/stat") as f:
+        st = f.read()
+    fields = st[st.rindex(")") + 2:].split()
+    return (int(fields[11]) + int(fields[12])) / tck
+
+
+def served_train_native(args, local: int, nat) -> dict:
+    """The served train path of the native server binary
+    (csrc/server/jubaclassifier.cpp: no Python in the server process): the
+    same load generator, request set and configuration as served_train."""
+    import socket
+    import tempfile
+    from jubatus_amd.common.mprpc import RpcClient
+    exe = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaloadgen")
+    srv = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaclassifier")
+    if not (os.access(exe, os.X_OK) and os.access(srv, os.X_OK)):
+        return {"skipped": "native server / jubaloadgen not built"}
+    tmp = tempfile.mkdtemp(prefix="jb_served_native_")
+    cfg = json.loads(json.dumps(AROW_CONFIG))
+    cfg["converter"]["hash_max_size"] = 1 << args.hash_bits
+    cfg_path = os.path.join(tmp, "arow.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg, f)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
+                          "-c", str(args.rpc_threads), "--gpu", str(local)],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+
+    def status():
+        with RpcClient("127.0.0.1", port, 30.0) as c:
+            (_, st), = c.call("get_status", "").items()
+        return {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
+                for k, v in st.items()}
+    try:
+        deadline = time.time() + 60
+        while True:
+            try:
+                st = status()
+                break
+            except Exception:  # noqa: BLE001 - not listening yet
+                if p.poll() is not None or time.time() > deadline:
+                    return {"error": (p.stderr.read() or b"").decode(errors="replace")[-400:]}
+                time.sleep(0.2)
+        if st.get("server_runtime") != "native":
+            return {"error": "the binary handed the configuration to the Python server"}
+        K = args.rpc_distinct
+        cap = K * args.per_request * 400 + (1 << 20)
+        buf = np.zeros(cap, np.uint8)
+        offs = np.zeros(K, np.int64)
+        lens = np.zeros(K, np.int64)
+        used = nat.synth_requests(buf.ctypes.data, cap, offs.ctypes.data, lens.ctypes.data, 4242, 0,
+                                  K, args.per_request, args.labels, args.str_features,
+                                  args.num_features, args.vocab, 16, 0.6, 8)
+        assert used > 0
+        pfile = os.path.join(tmp, "train_params.bin")
+        with open(pfile, "wb") as f:
+            for o, n in zip(offs, lens):
+                f.write(b"\x92\xa0" + buf[o:o + n].tobytes())
+        base = [exe, "-p", str(port), "-m", "train", "-f", pfile, "-c", str(args.rpc_conns),
+                "-d", str(args.rpc_depth)]
+        subprocess.run(base + ["-t", "1.5"], capture_output=True, text=True, timeout=120)  # warmup
+        st0 = status()
+        cpu0 = _proc_cpu(p.pid)
+        r = subprocess.run(base + ["-t", str(args.rpc_seconds)], capture_output=True, text=True,
+                           timeout=args.rpc_seconds + 120)
+        cpu1 = _proc_cpu(p.pid)
+        if r.returncode != 0:
+            return {"error": (r.stderr or r.stdout)[-400:]}
+        lg = json.loads(r.stdout.strip().splitlines()[-1])
+        st1 = status()
+        tr = int(st1["train.samples_trained"]) - int(st0["train.samples_trained"])
+        up = int(st1["train.samples_updated"]) - int(st0["train.samples_updated"])
+        return {"served_train_samples_per_sec": round(lg["requests_per_s"] * args.per_request, 1),
+                "requests_per_s": lg["requests_per_s"], "samples_per_request": args.per_request,
+                "connections": lg["connections"], "depth": lg["depth"],
+                "rpc_p50_us": lg["p50_us"], "rpc_p99_us": lg["p99_us"], "seconds": lg["seconds"],
+                "samples_trained_in_window": tr,
+                "update_fraction": round(up / tr, 4) if tr else None,
+                "server_cpus": round((cpu1 - cpu0) / lg["seconds"], 2),
+                "train_scan": {k[len("train_scan."):]: int(v) for k, v in st1.items()
+                               if k.startswith("train_scan.") and v.isdigit()},
+                "path": "loopback TCP -> native jubaclassifier (no Python) -> pinned arena slot -> "
+                        "GPU scan/fv_hash/AROW train; reply per request after the batch's scan check"}
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -371,7 +467,8 @@ def main() -> None:
 
     nat = native()
     if args.served_only:
-        print(json.dumps(served_train(args, local, nat)), flush=True)
+        print(json.dumps({"python": served_train(args, local, nat),
+                          "native": served_train_native(args, local, nat)}), flush=True)
         return
     gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, local_world)))
     p_corr, vocab = (0.0, (1 << 31) - 1) if args.worst_case else (0.6, args.vocab)
@@ -519,9 +616,10 @@ def main() -> None:
     p50 = statistics.median(lat)
     p99 = lat[min(len(lat) - 1, int(0.99 * len(lat)))]
 
-    served = None
+    served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:
         served = served_train(args, local, nat)
+        served_native = served_train_native(args, local, nat)
 
     total = samples_per_step * args.steps * world
     value = total / elapsed
@@ -572,6 +670,7 @@ def main() -> None:
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
             "served": served,
+            "served_native": served_native,
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),
             "heldout_accuracy": round(acc, 4),

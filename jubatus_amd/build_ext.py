@@ -10,6 +10,8 @@
   plug-in directory.
 * ``jubatus_amd/native_bin/{jubacoordinator,jubaproxy}`` - the Python-free
   coordination server (csrc/coord) and request router (csrc/proxy).
+* ``jubatus_amd/native_bin/jubaclassifier`` - the Python-free classifier
+  server (csrc/server), linked against ``libjubatus_hip.so``.
 
 All are built in-tree so they travel with the repository snapshot to the
 GPU box. Incremental: a target is rebuilt only if a source is newer.
@@ -154,10 +156,38 @@ def build_tools(force: bool = False, nproc: int = 8, sanitize: str | None = None
     return out
 
 
+# native engine servers (csrc/server): host C++ over the HIP runtime and the
+# kernel library (linked against libjubatus_hip.so, found via $ORIGIN/..)
+SERVERS = {
+    "jubaclassifier": (["server/jubaclassifier.cpp", "native/jb_rpc.cpp"],
+                       ["server", "native", "hip"]),
+}
+
+
+def build_servers(force: bool = False, nproc: int = 8) -> str:
+    """Python-free engine servers (they exec the Python server for the
+    configurations they do not serve natively)."""
+    os.makedirs(NATIVE_BIN, exist_ok=True)
+    jobs = []
+    for name, (srcs, incs) in SERVERS.items():
+        target = os.path.join(NATIVE_BIN, name)
+        paths = [os.path.join(CSRC, x) for x in srcs]
+        deps = paths + [HIP_SO] + [h for d in incs for h in glob.glob(os.path.join(CSRC, d, "*.h*"))]
+        if force or _newer(target, deps):
+            jobs.append((target, ["g++", "-O2", "-std=c++17", "-pthread", "-Wall",
+                                  "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                                  *[f"-I{os.path.join(CSRC, d)}" for d in incs], *paths,
+                                  f"-L{PKG}", "-ljubatus_hip", "-L/opt/rocm/lib", "-lamdhip64",
+                                  "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,/opt/rocm/lib",
+                                  "-o", target]))
+    _compile_all(jobs, nproc)
+    return NATIVE_BIN
+
+
 def build_all(force: bool = False, nproc: int | None = None) -> tuple[str, ...]:
     nproc = nproc or min(8, os.cpu_count() or 4)
     return (build_native(force, nproc), build_hip(force, nproc), build_plugins(force),
-            build_tools(force, nproc))
+            build_tools(force, nproc), build_servers(force, nproc))
 
 
 def main() -> None:

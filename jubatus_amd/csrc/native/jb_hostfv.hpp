@@ -46,6 +46,12 @@ class HostFvHasher {
     return 0;
   }
 
+  // One datum at the cursor: appends its slots (used by the native server's
+  // host train path, which parses [label, datum] pairs itself).
+  int hash_datum(Cursor& c, int32_t* idx, float* val, int64_t max_slots, int64_t* slots) const {
+    return datum(c, idx, val, max_slots, slots);
+  }
+
  private:
   bool match(const HostRule& r, const uint8_t* k, uint32_t kn) const {
     if (r.match_kind == 0) return true;

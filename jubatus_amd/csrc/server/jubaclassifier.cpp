@@ -1,0 +1,1720 @@
+// jubaclassifier, native: the classifier server without Python.
+//
+// Reference: jubatus/server/server/classifier_serv.cpp (train :128-147,
+// classify :149-173, labels :175-225), classifier_impl.cpp (RPC table),
+// framework/server_base.cpp (save / load / status) and server_helper.hpp
+// (startup). SURVEY section 7.1: server binaries must not need Python.
+//
+// Scope: standalone servers of the linear methods (perceptron, PA, PA1, PA2,
+// CW, AROW, NHERD) whose converter runs on the fixed-slot GPU path
+// (fv_converter/gpu_path.py fast_eligible: str rules with bin global
+// weights, num / log rules, no filters / combinations / plug-ins). Every
+// other configuration - and distributed mode (-z), --cpu, a host without
+// /dev/kfd - is handed to the Python server (jubatus_amd.cmd.server) by exec
+// BEFORE anything touches the GPU.
+//
+// Data path (the same kernels as the Python server, csrc/hip):
+//   train    the transport copies request bodies into pinned arena slots
+//            (csrc/native/jb_rpc.cpp); one jb_train_batch_submit per slot
+//            (H2D, scan.hip, fv_hash.hip, hot.hip, linear.hip); the reply of
+//            every request waits for the batch's scan check. A batch the
+//            device scan rejects (new labels, malformed bytes, binary
+//            values) is re-run one request at a time on the host path:
+//            validate, commit labels, hash (jb_hostfv.hpp), one exact
+//            single-stream train launch.
+//   classify the batch of queued classify RPCs is hashed on the host; up to
+//            32 datums / 320 slots ride in the kernel arguments
+//            (classify_direct.hip), larger batches take jb_linear_classify.
+// Model files are byte-compatible with the Python server's
+// (framework/save_load.py container, models/classifier.py pack()).
+#include <dirent.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <getopt.h>
+#include <ifaddrs.h>
+#include <limits.h>
+#include <math.h>
+#include <netinet/in.h>
+#include <arpa/inet.h>
+#include <pwd.h>
+#include <signal.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <chrono>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "jb_hash.hpp"
+#include "jb_hostfv.hpp"
+#include "jb_msgpack.hpp"
+#include "jb_pack.hpp"
+#include "jb_rpc.hpp"
+#include "jb_train_batch.hpp"
+#include "jb_value.hpp"
+
+extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                               const int32_t* labels, const int64_t* stream_ptr, int nstreams,
+                               float* W, float* S, const int32_t* active, int LC, int method,
+                               float C, int mode, const int32_t* hot_rows, const int32_t* hot_n,
+                               float* hot_rep, int merge_every, int hot_waves,
+                               unsigned long long* stats, uint8_t* touched, hipStream_t stream);
+extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                  int n_samples, const float* W, int LC, float* out,
+                                  hipStream_t stream);
+extern "C" int jb_classify_direct(const int32_t* idx, const float* val, const int64_t* row_ptr,
+                                  int n, const float* W, int LC, float* out_host,
+                                  uint32_t* done_host, hipStream_t stream);
+extern "C" void* jb_host_alloc(int64_t nbytes);
+extern "C" int jb_host_free(void* p);
+extern "C" int64_t jb_hot_rep_bytes();
+
+namespace {
+
+using jb::val::MsgpackReader;
+using jb::val::MsgpackWriter;
+using jb::val::Value;
+
+const char* const kVersion = "0.9.2";
+const uint32_t kVersionParts[3] = {0, 9, 2};
+const char* const kMethods[] = {"perceptron", "PA", "PA1", "PA2", "CW", "AROW", "NHERD"};
+const int kLabelCaps[] = {8, 16, 32, 64, 128, 256, 512, 1024};
+constexpr int kUpdateExact = 0, kUpdateAtomic = 1;
+constexpr int kMethodCW = 4;
+constexpr int kHotMaxRows = 64, kHotEntries = 512, kHotCap = 1 << 14, kHotWaves = 8;
+constexpr int kDirectMaxSamples = 32, kDirectMaxSlots = 320;
+constexpr int64_t kScanLdsBytes = 27 * 1024, kScanMaxSamples = 768;   // scan.hip
+constexpr int kArgumentError = 2, kNoMethodError = 1;
+
+#define HIPCHK(x)                                                                    \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess)                                                            \
+      throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_));      \
+  } while (0)
+
+void logf_(const char* level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+void logf_(const char* level, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  time_t t = time(nullptr);
+  struct tm tm;
+  localtime_r(&t, &tm);
+  char ts[32];
+  strftime(ts, sizeof ts, "%Y-%m-%d %H:%M:%S", &tm);
+  fprintf(stderr, "%s %d %-5s [jubaclassifier.cpp] %s\n", ts, (int)getpid(), level, buf);
+}
+
+// ------------------------------------------------------------------ argv
+struct Args {
+  int port = 9199;
+  std::string listen_addr, listen_if, bind = "0.0.0.0", eth;
+  int threads = 2, timeout = 10, zk_timeout = 10, ic_timeout = 10;
+  bool daemon = false, version = false, cpu = false;
+  bool native_check = false;   // print whether the config is served natively, exit
+  std::string logdir, log_config, datadir = "/tmp", configpath, model_file, zookeeper, name,
+      mixer = "linear_mixer";
+  int interval_sec = 16, interval_count = 512;
+  int gpu = -1;
+};
+
+std::string real_path(const std::string& p) {
+  char buf[PATH_MAX];
+  return realpath(p.c_str(), buf) ? std::string(buf) : p;
+}
+
+std::string default_v4() {
+  std::string out = "127.0.0.1";
+  struct ifaddrs* ifa = nullptr;
+  if (getifaddrs(&ifa) != 0) return out;
+  for (auto* p = ifa; p; p = p->ifa_next) {
+    if (!p->ifa_addr || p->ifa_addr->sa_family != AF_INET) continue;
+    char b[INET_ADDRSTRLEN];
+    inet_ntop(AF_INET, &((struct sockaddr_in*)p->ifa_addr)->sin_addr, b, sizeof b);
+    if (strncmp(b, "127.", 4) != 0) { out = b; break; }
+  }
+  freeifaddrs(ifa);
+  return out;
+}
+
+std::string if_v4(const std::string& nic) {
+  std::string out;
+  struct ifaddrs* ifa = nullptr;
+  if (getifaddrs(&ifa) != 0) return out;
+  for (auto* p = ifa; p; p = p->ifa_next)
+    if (p->ifa_addr && p->ifa_addr->sa_family == AF_INET && nic == p->ifa_name) {
+      char b[INET_ADDRSTRLEN];
+      inet_ntop(AF_INET, &((struct sockaddr_in*)p->ifa_addr)->sin_addr, b, sizeof b);
+      out = b;
+      break;
+    }
+  freeifaddrs(ifa);
+  return out;
+}
+
+std::string user_name() {
+  struct passwd* pw = getpwuid(getuid());
+  return pw ? std::string(pw->pw_name) : std::to_string(getuid());
+}
+
+const char* const kUsage =
+    "usage: jubaclassifier [-p port] [-b listen_addr] [-B listen_if] [-c thread] [-t timeout]\n"
+    "                      [-d datadir] [-l logdir] [-g log_config] [-f configpath]\n"
+    "                      [-m model_file] [-z zookeeper] [-n name] [-x mixer] [-s interval_sec]\n"
+    "                      [-i interval_count] [-Z zookeeper_timeout] [-I interconnect_timeout]\n"
+    "                      [-D] [-v] [--gpu N] [--cpu]\n";
+
+// 0 ok, >0 exit code
+int parse_args(int argc, char** argv, Args* a) {
+  static const struct option opts[] = {
+      {"rpc-port", required_argument, nullptr, 'p'}, {"listen_addr", required_argument, nullptr, 'b'},
+      {"listen_if", required_argument, nullptr, 'B'}, {"thread", required_argument, nullptr, 'c'},
+      {"timeout", required_argument, nullptr, 't'}, {"zookeeper_timeout", required_argument, nullptr, 'Z'},
+      {"interconnect_timeout", required_argument, nullptr, 'I'}, {"daemon", no_argument, nullptr, 'D'},
+      {"logdir", required_argument, nullptr, 'l'}, {"log_config", required_argument, nullptr, 'g'},
+      {"version", no_argument, nullptr, 'v'}, {"datadir", required_argument, nullptr, 'd'},
+      {"configpath", required_argument, nullptr, 'f'}, {"model_file", required_argument, nullptr, 'm'},
+      {"zookeeper", required_argument, nullptr, 'z'}, {"name", required_argument, nullptr, 'n'},
+      {"mixer", required_argument, nullptr, 'x'}, {"interval_sec", required_argument, nullptr, 's'},
+      {"interval_count", required_argument, nullptr, 'i'}, {"gpu", required_argument, nullptr, 1000},
+      {"cpu", no_argument, nullptr, 1001}, {"help", no_argument, nullptr, 'h'},
+      {"native-check", no_argument, nullptr, 1002},
+      {nullptr, 0, nullptr, 0}};
+  auto num = [](const char* s, long lo, long hi, int* out) {
+    char* e = nullptr;
+    long v = strtol(s, &e, 10);
+    if (!*s || *e || v < lo || v > hi) return false;
+    *out = (int)v;
+    return true;
+  };
+  int c;
+  optind = 1;
+  while ((c = getopt_long(argc, argv, "p:b:B:c:t:Z:I:Dl:g:vd:f:m:z:n:x:s:i:h", opts, nullptr)) != -1) {
+    bool ok = true;
+    switch (c) {
+      case 'p': ok = num(optarg, 1, 65535, &a->port); break;
+      case 'b': a->listen_addr = optarg; break;
+      case 'B': a->listen_if = optarg; break;
+      case 'c': ok = num(optarg, 1, INT_MAX, &a->threads); break;
+      case 't': ok = num(optarg, 0, INT_MAX, &a->timeout); break;
+      case 'Z': ok = num(optarg, INT_MIN, INT_MAX, &a->zk_timeout); break;
+      case 'I': ok = num(optarg, INT_MIN, INT_MAX, &a->ic_timeout); break;
+      case 'D': a->daemon = true; break;
+      case 'l': a->logdir = optarg; break;
+      case 'g': a->log_config = optarg; break;
+      case 'v': a->version = true; break;
+      case 'd': a->datadir = optarg; break;
+      case 'f': a->configpath = optarg; break;
+      case 'm': a->model_file = optarg; break;
+      case 'z': a->zookeeper = optarg; break;
+      case 'n': a->name = optarg; break;
+      case 'x': a->mixer = optarg; break;
+      case 's': ok = num(optarg, 0, INT_MAX, &a->interval_sec); break;
+      case 'i': ok = num(optarg, 0, INT_MAX, &a->interval_count); break;
+      case 1000: ok = num(optarg, 0, 1023, &a->gpu); break;
+      case 1001: a->cpu = true; break;
+      case 1002: a->native_check = true; break;
+      case 'h': fputs(kUsage, stdout); return -1;
+      default: ok = false;
+    }
+    if (!ok) {
+      fputs(kUsage, stderr);
+      return 2;
+    }
+  }
+  if (optind < argc) {
+    fputs(kUsage, stderr);
+    return 2;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------- config
+struct Rules {
+  std::vector<jb::HostRule> s, n;
+  std::string blob;
+  uint64_t H = 1ull << 20;
+};
+
+int matcher_kind(const std::string& spec, std::string* arg) {
+  if (spec.empty() || spec == "*") { arg->clear(); return 0; }
+  if (spec.size() >= 2 && spec.front() == '/' && spec.back() == '/') return -1;   // regex
+  if (spec.back() == '*') { *arg = spec.substr(0, spec.size() - 1); return 1; }
+  if (spec.front() == '*') { *arg = spec.substr(1); return 2; }
+  *arg = spec;
+  return 3;
+}
+
+bool nonempty_list(const Value& conv, const char* key) {
+  const Value* v = conv.get(key);
+  return v && v->kind == Value::ARR && !v->a.empty();
+}
+
+// the fixed-slot GPU converter (fv_converter/gpu_path.py fast_eligible +
+// GpuRuleTable): false with a reason when the config needs the host converter
+bool build_rules(const Value& conv, Rules* r, std::string* why) {
+  if (conv.kind != Value::MAP) { *why = "converter is not an object"; return false; }
+  for (const char* k : {"string_filter_rules", "num_filter_rules", "binary_rules", "combination_rules"})
+    if (nonempty_list(conv, k)) { *why = std::string(k) + " need the host converter"; return false; }
+  const Value* st = conv.get("string_types");
+  const Value* nt = conv.get("num_types");
+  if (const Value* h = conv.get("hash_max_size")) {
+    if (h->kind == Value::INT && h->i > 0) r->H = (uint64_t)h->i;
+    else if (h->kind != Value::NIL) { *why = "hash_max_size"; return false; }
+  }
+  auto put = [&](const std::string& b, int32_t* off, int32_t* len) {
+    *off = (int32_t)r->blob.size();
+    *len = (int32_t)b.size();
+    r->blob += b;
+  };
+  if (const Value* sr = conv.get("string_rules")) {
+    if (sr->kind != Value::ARR) { *why = "string_rules"; return false; }
+    for (const Value& x : sr->a) {
+      const std::string type = x.str_or("type", "");
+      const std::string sw = x.str_or("sample_weight", "bin");
+      const std::string gw = x.str_or("global_weight", "bin");
+      if (type != "str" || (st && st->get("str"))) { *why = "string type " + type; return false; }
+      if (gw != "bin") { *why = "global_weight " + gw; return false; }
+      float w;
+      if (sw == "bin" || sw == "tf") w = 1.f;
+      else if (sw == "log_tf") w = logf(2.f);
+      else { *why = "sample_weight " + sw; return false; }
+      std::string arg;
+      const int kind = matcher_kind(x.str_or("key", ""), &arg);
+      if (kind < 0) { *why = "regex key matcher"; return false; }
+      jb::HostRule h{};
+      h.match_kind = kind;
+      put(arg, &h.match_off, &h.match_len);
+      put("@str#" + sw + "/" + gw, &h.suffix_off, &h.suffix_len);
+      h.weight = w;
+      r->s.push_back(h);
+    }
+  }
+  if (const Value* nr = conv.get("num_rules")) {
+    if (nr->kind != Value::ARR) { *why = "num_rules"; return false; }
+    for (const Value& x : nr->a) {
+      const std::string type = x.str_or("type", "");
+      if ((type != "num" && type != "log") || (nt && nt->get(type))) { *why = "num type " + type; return false; }
+      std::string arg;
+      const int kind = matcher_kind(x.str_or("key", ""), &arg);
+      if (kind < 0) { *why = "regex key matcher"; return false; }
+      jb::HostRule h{};
+      h.match_kind = kind;
+      put(arg, &h.match_off, &h.match_len);
+      put("@" + type, &h.suffix_off, &h.suffix_len);
+      h.value_kind = type == "log" ? 1 : 0;
+      r->n.push_back(h);
+    }
+  }
+  return true;
+}
+
+struct Config {
+  std::string text;
+  int method = -1;
+  float C = 1.f;
+  Rules rules;
+};
+
+bool parse_config(const std::string& text, Config* c, std::string* why) {
+  Value v;
+  try {
+    v = jb::val::parse_json(text);
+  } catch (const std::exception& e) {
+    *why = e.what();
+    return false;
+  }
+  if (v.kind != Value::MAP) { *why = "configuration must be a JSON object"; return false; }
+  const std::string m = v.str_or("method", "");
+  c->method = -1;
+  for (int k = 0; k < 7; ++k)
+    if (m == kMethods[k]) c->method = k;
+  if (c->method < 0) { *why = "method " + m + " is not a linear method"; return false; }
+  const Value* p = v.get("parameter");
+  const Value* rw = p ? p->get("regularization_weight") : nullptr;
+  if (c->method >= 2) {
+    if (!rw || !rw->is_num() || !(rw->num() > 0)) { *why = "regularization_weight"; return false; }
+  }
+  c->C = rw && rw->is_num() ? (float)rw->num() : 1.f;
+  const Value* conv = v.get("converter");
+  Value empty;
+  empty.kind = Value::MAP;
+  if (!build_rules(conv ? *conv : empty, &c->rules, why)) return false;
+  c->text = text;
+  return true;
+}
+
+bool read_file(const std::string& path, std::string* out) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  char buf[1 << 16];
+  size_t n;
+  out->clear();
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) out->append(buf, n);
+  fclose(f);
+  return true;
+}
+
+// ------------------------------------------------------------ model file
+// framework/save_load.py: 48-byte big-endian header, CRC32 over header[0:28]
+// ++ header[32:48] ++ system ++ user; system = [1, ts, type, id, config]
+// (old-spec raw strings), user = [1, driver pack] (bin types).
+uint64_t rd_be(const uint8_t* p, int n) {
+  uint64_t x = 0;
+  for (int k = 0; k < n; ++k) x = (x << 8) | p[k];
+  return x;
+}
+
+void wr_be(uint8_t* p, uint64_t x, int n) {
+  for (int k = n - 1; k >= 0; --k) { p[k] = (uint8_t)x; x >>= 8; }
+}
+
+struct ModelFile {
+  std::string type, id, config;
+  Value user;      // the driver pack
+  int64_t user_version = 0;
+};
+
+std::string read_model_file(const std::string& bytes, ModelFile* mf) {
+  if (bytes.size() < 48) return "failed to read header: truncated file";
+  const uint8_t* h = (const uint8_t*)bytes.data();
+  if (memcmp(h, "jubatus\0", 8) != 0) return "invalid file format";
+  if (rd_be(h + 8, 8) != 1) return "invalid format version: " + std::to_string(rd_be(h + 8, 8)) + ", expected 1";
+  const uint32_t maj = (uint32_t)rd_be(h + 16, 4), min = (uint32_t)rd_be(h + 20, 4),
+                 mnt = (uint32_t)rd_be(h + 24, 4);
+  if (maj != kVersionParts[0] || min != kVersionParts[1] || mnt != kVersionParts[2])
+    return std::string("jubatus version mismatched: current version: ") + kVersion +
+           ", saved version: " + std::to_string(maj) + "." + std::to_string(min) + "." + std::to_string(mnt);
+  const uint32_t crc = (uint32_t)rd_be(h + 28, 4);
+  const uint64_t ssz = rd_be(h + 32, 8), usz = rd_be(h + 40, 8);
+  if (bytes.size() < 48 + ssz + usz || ssz > bytes.size() || usz > bytes.size()) return "model file truncated";
+  uint32_t c = jb::crc32_update(0, h, 28);
+  c = jb::crc32_update(c, h + 32, 16);
+  c = jb::crc32_update(c, h + 48, ssz);
+  c = jb::crc32_update(c, h + 48 + ssz, usz);
+  if (c != crc) {
+    char b[96];
+    snprintf(b, sizeof b, "invalid crc32 checksum: %#x, read %#x", c, crc);
+    return b;
+  }
+  try {
+    Value sys = MsgpackReader(h + 48, ssz).read();
+    Value usr = MsgpackReader(h + 48 + ssz, usz).read();
+    if (sys.kind != Value::ARR || sys.a.size() != 5) return "invalid system data";
+    if (usr.kind != Value::ARR || usr.a.size() != 2) return "invalid user data";
+    if (sys.a[0].kind != Value::INT || sys.a[0].i != 1)
+      return "invalid system data version: saved version: " + std::to_string(sys.a[0].i) + ", expected version: 1";
+    mf->type = sys.a[2].s;
+    mf->id = sys.a[3].s;
+    mf->config = sys.a[4].s;
+    mf->user_version = usr.a[0].kind == Value::INT ? usr.a[0].i : -1;
+    mf->user = std::move(usr.a[1]);
+  } catch (const std::exception& e) {
+    return std::string("broken model data: ") + e.what();
+  }
+  return "";
+}
+
+// --------------------------------------------------------------- buffers
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  T* get(size_t n) {
+    if (n > cap) {
+      if (p) HIPCHK(hipFree(p));
+      size_t c = cap ? cap : 1024;
+      while (c < n) c *= 2;
+      HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
+      cap = c;
+    }
+    return p;
+  }
+};
+
+template <class T>
+struct PinBuf {   // page-locked host memory (H2D staging)
+  T* p = nullptr;
+  size_t cap = 0;
+  T* get(size_t n) {
+    if (n > cap) {
+      if (p) HIPCHK(hipHostFree(p));
+      size_t c = cap ? cap : 1024;
+      while (c < n) c *= 2;
+      HIPCHK(hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault));
+      cap = c;
+    }
+    return p;
+  }
+};
+
+uint64_t fnv1a64(const std::string& s) { return jb::fnv_bytes(jb::kFnvOffset, (const uint8_t*)s.data(), s.size()); }
+
+// element count of a body's top-level array header (-1: none)
+int64_t body_count(const uint8_t* b, uint64_t n) {
+  if (n < 1) return -1;
+  const uint8_t t = b[0];
+  if ((t & 0xf0) == 0x90) return t & 0x0f;
+  if (t == 0xdc && n >= 3) return ((int64_t)b[1] << 8) | b[2];
+  if (t == 0xdd && n >= 5) return (int64_t)rd_be(b + 1, 4);
+  return -1;
+}
+
+// ------------------------------------------------------------------ model
+class Classifier {
+ public:
+  std::atomic<uint64_t> update_count{0};
+  std::atomic<uint64_t> train_calls{0}, train_batches{0};
+  uint64_t scan_gpu = 0, scan_replayed = 0, scan_host = 0;
+  int device = 0;
+
+  Classifier(const Config& cfg, int device_index) : device(device_index) {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&copy_, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&prep_, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&compute_, hipStreamNonBlocking));
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&prio_, hipStreamNonBlocking, hi));
+    HIPCHK(hipMalloc((void**)&stats_, 2 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(stats_, 0, 2 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc((void**)&hash_err_, sizeof(int32_t)));
+    HIPCHK(hipMemset(hash_err_, 0, sizeof(int32_t)));
+    direct_out_ = (float*)jb_host_alloc((int64_t)kDirectMaxSamples * 1024 * 4);
+    direct_done_ = (uint32_t*)jb_host_alloc(4 * kDirectMaxSamples);
+    hot_count_host_ = (int32_t*)jb_host_alloc(4);
+    if (!direct_out_ || !direct_done_ || !hot_count_host_) throw std::runtime_error("hipHostMalloc failed");
+    memset(direct_done_, 0, 4 * kDirectMaxSamples);
+    HIPCHK(hipEventCreateWithFlags(&hot_seen_ev_, hipEventDisableTiming));
+    const size_t rep = (size_t)jb_hot_rep_bytes();
+    for (Hot& h : hots_) {
+      HIPCHK(hipMalloc((void**)&h.rows, kHotMaxRows * 4));
+      HIPCHK(hipMemset(h.rows, 0, kHotMaxRows * 4));
+      HIPCHK(hipMalloc((void**)&h.n, 4));
+      HIPCHK(hipMemset(h.n, 0, 4));
+      HIPCHK(hipMalloc((void**)&h.rep, rep));
+      HIPCHK(hipMemset(h.rep, 0, rep));
+      HIPCHK(hipMalloc((void**)&h.gkey, kHotCap * 4));
+      HIPCHK(hipMemset(h.gkey, 0xff, kHotCap * 4));
+      HIPCHK(hipMalloc((void**)&h.gcnt, kHotCap * 4));
+      HIPCHK(hipMemset(h.gcnt, 0, kHotCap * 4));
+      HIPCHK(hipEventCreateWithFlags(&h.free, hipEventDisableTiming));
+    }
+    for (Set& s : sets_)
+      for (hipEvent_t* e : {&s.copy_done, &s.check_done, &s.ready, &s.free})
+        HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    configure(cfg);
+  }
+
+  // (re)build the model for a configuration (set_config / load with the file's config)
+  void configure(const Config& cfg) {
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipDeviceSynchronize());
+    cfg_ = cfg;
+    mid_ = cfg.method;
+    C_ = cfg.C;
+    use_s_ = mid_ >= kMethodCW;
+    H_ = cfg.rules.H;
+    const Rules& r = cfg.rules;
+    hasher_.reset(new jb::HostFvHasher((const uint8_t*)r.s.data(), (int)r.s.size(),
+                                       (const uint8_t*)r.n.data(), (int)r.n.size(),
+                                       (const uint8_t*)r.blob.data(), r.blob.size(), H_));
+    const size_t rs = sizeof(jb::HostRule);
+    for (void** p : {&d_srules_, &d_nrules_, (void**)&d_blob_})
+      if (*p) { HIPCHK(hipFree(*p)); *p = nullptr; }
+    HIPCHK(hipMalloc(&d_srules_, rs * std::max<size_t>(1, r.s.size())));
+    HIPCHK(hipMalloc(&d_nrules_, rs * std::max<size_t>(1, r.n.size())));
+    HIPCHK(hipMalloc((void**)&d_blob_, std::max<size_t>(1, r.blob.size())));
+    if (!r.s.empty()) HIPCHK(hipMemcpy(d_srules_, r.s.data(), rs * r.s.size(), hipMemcpyHostToDevice));
+    if (!r.n.empty()) HIPCHK(hipMemcpy(d_nrules_, r.n.data(), rs * r.n.size(), hipMemcpyHostToDevice));
+    if (!r.blob.empty()) HIPCHK(hipMemcpy(d_blob_, r.blob.data(), r.blob.size(), hipMemcpyHostToDevice));
+    labels_.clear();
+    alloc_locked(kLabelCaps[0], true);
+  }
+
+  const std::string& config_text() const { return cfg_.text; }
+
+  // --------------------------------------------------------------- train
+  // served train batch over an arena slot: -> per request sample count, -1
+  // ARGUMENT_ERROR, -2 error message in msgs[k]
+  void train_arena(const uint8_t* arena, const std::vector<jb::ArenaReq>& reqs,
+                   std::vector<int64_t>* res, std::vector<std::string>* msgs) {
+    const size_t R = reqs.size();
+    res->assign(R, -1);
+    msgs->assign(R, std::string());
+    train_calls += R;
+    train_batches += 1;
+    update_count += R;
+    std::vector<int64_t> counts(R);
+    bool gpu_ok = R > 0;
+    uint64_t used = 0;
+    for (size_t k = 0; k < R && gpu_ok; ++k) {
+      counts[k] = body_count(arena + reqs[k].off, reqs[k].len);
+      if (counts[k] < 0 || (int64_t)(reqs[k].len + (reqs[k].off & 15)) > kScanLdsBytes ||
+          counts[k] > kScanMaxSamples)
+        gpu_ok = false;
+      used = std::max<uint64_t>(used, reqs[k].off + reqs[k].len);
+    }
+    if (gpu_ok) {
+      int si = -1;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (labels_.size() > 0) si = submit_scan_locked(arena, reqs, counts, used);
+      }
+      if (si >= 0) {
+        Set& s = sets_[si];
+        HIPCHK(hipEventSynchronize(s.check_done));
+        std::lock_guard<std::mutex> g(mu_);
+        const int32_t err = ((volatile int32_t*)s.host_out)[0];
+        if (err == 0) {
+          const int32_t* hist = s.host_out + 1;
+          for (int64_t l = 0; l < s.nhist; ++l)
+            if (hist[l]) labels_.add_count((int)l, (uint64_t)hist[l]);
+          s.inflight = false;
+          for (size_t k = 0; k < R; ++k) (*res)[k] = counts[k];
+          scan_gpu += 1;
+          return;
+        }
+        s.inflight = false;
+        scan_replayed += 1;
+      }
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    scan_host += 1;
+    for (size_t k = 0; k < R; ++k)
+      host_train_locked(arena + reqs[k].off, reqs[k].len, &(*res)[k], &(*msgs)[k]);
+  }
+
+  // one request body (list<labeled_datum>) on the host path
+  void train_body(const uint8_t* b, size_t n, int64_t* res, std::string* msg) {
+    train_calls += 1;
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    scan_host += 1;
+    host_train_locked(b, n, res, msg);
+  }
+
+  // -------------------------------------------------------------- classify
+  // bodies: list<datum> each; -> per body rows of (label, score) over the
+  // live labels, or an error (ok[k] false: ARGUMENT_ERROR)
+  std::vector<std::string> classify(const std::vector<std::pair<const uint8_t*, size_t>>& bodies,
+                                    const std::vector<uint32_t>& msgids) {
+    const size_t R = bodies.size();
+    std::vector<std::string> out(R);
+    std::vector<int64_t> first(R + 1, 0);
+    std::vector<bool> ok(R, true);
+    int64_t n = 0, slots = 0;
+    cidx_.get(std::max<size_t>(cidx_.cap, 1024));
+    cval_.get(cidx_.cap);
+    row_.get(std::max<size_t>(row_.cap, 1024));
+    row_.p[0] = 0;
+    for (size_t k = 0; k < R; ++k) {
+      first[k] = n;
+      const int64_t n0 = n, s0 = slots;
+      while (true) {
+        int rc = hasher_->hash_body(bodies[k].first, bodies[k].second, cidx_.p, cval_.p, row_.p,
+                                    (int64_t)row_.cap - 1, (int64_t)cidx_.cap, &n, &slots);
+        if (rc == 2) {   // grow and re-hash this body
+          n = n0;
+          slots = s0;
+          cidx_.get(2 * cidx_.cap);
+          cval_.get(cidx_.cap);
+          row_.get(2 * row_.cap);
+          continue;
+        }
+        if (rc == 1) { ok[k] = false; n = n0; slots = s0; }
+        break;
+      }
+    }
+    first[R] = n;
+    std::vector<float> scores;
+    std::vector<std::string> names;
+    std::vector<int> cols;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      sync_labels_locked();
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      for (size_t c = 0; c < nm.size(); ++c)
+        if (al[c]) { cols.push_back((int)c); names.push_back(nm[c]); }
+      scores.resize((size_t)n * LC_);
+      if (n > 0) score_locked(n, slots, scores.data());
+    }
+    for (size_t k = 0; k < R; ++k) {
+      if (!ok[k]) { out[k] = jb::val::response_code(msgids[k], kArgumentError); continue; }
+      MsgpackWriter w;
+      const int64_t nk = first[k + 1] - first[k];
+      w.arr((size_t)nk);
+      for (int64_t i = first[k]; i < first[k + 1]; ++i) {
+        w.arr(cols.size());
+        for (size_t c = 0; c < cols.size(); ++c) {
+          w.arr(2);
+          w.raw(names[c]);
+          w.dbl((double)scores[(size_t)i * LC_ + cols[c]]);
+        }
+      }
+      out[k] = jb::val::response_ok(msgids[k], w.out);
+    }
+    return out;
+  }
+
+  // ---------------------------------------------------------------- labels
+  std::vector<std::pair<std::string, uint64_t>> get_labels() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::pair<std::string, uint64_t>> out;
+    auto nm = labels_.names();
+    auto al = labels_.alive();
+    for (size_t c = 0; c < nm.size(); ++c)
+      if (al[c]) out.emplace_back(nm[c], labels_.count((int)c));
+    return out;
+  }
+
+  bool set_label(const std::string& l) {
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    if (labels_.lookup(l) >= 0) return false;
+    if (labels_.get_or_add(l.data(), l.size()) < 0) throw std::runtime_error("label table full");
+    sync_labels_locked();
+    return true;
+  }
+
+  bool delete_label(const std::string& l) {
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    const int i = labels_.lookup(l);
+    if (i < 0) return false;
+    labels_.remove(l);
+    HIPCHK(hipMemset2DAsync(W_ + i, (size_t)LC_ * 4, 0, 4, H_, compute_));
+    if (S_) {
+      float* ones = ones_.get(H_);
+      fill_ones(ones, H_);
+      HIPCHK(hipMemcpy2DAsync(S_ + i, (size_t)LC_ * 4, ones, 4, 4, H_, hipMemcpyDeviceToDevice, compute_));
+    }
+    HIPCHK(hipStreamSynchronize(compute_));
+    sync_labels_locked();
+    return true;
+  }
+
+  void clear() {
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipDeviceSynchronize());
+    labels_.clear();
+    alloc_locked(kLabelCaps[0], true);
+  }
+
+  // ---------------------------------------------------------------- persist
+  // models/classifier.py pack(): rows that differ from the initial state over
+  // the live label columns
+  std::string pack_user_data() {
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipDeviceSynchronize());
+    std::vector<float> W((size_t)H_ * LC_), S;
+    HIPCHK(hipMemcpy(W.data(), W_, W.size() * 4, hipMemcpyDeviceToHost));
+    if (S_) {
+      S.resize(W.size());
+      HIPCHK(hipMemcpy(S.data(), S_, S.size() * 4, hipMemcpyDeviceToHost));
+    }
+    auto nm = labels_.names();
+    auto al = labels_.alive();
+    std::vector<int> cols;
+    for (size_t c = 0; c < nm.size(); ++c)
+      if (al[c]) cols.push_back((int)c);
+    std::vector<int64_t> rows;
+    std::vector<float> Wr, Sr;
+    for (uint64_t h = 0; h < H_; ++h) {
+      const float* w = W.data() + h * LC_;
+      bool t = false;
+      for (int c : cols) t |= w[c] != 0.f;
+      if (S_) {
+        const float* s = S.data() + h * LC_;
+        for (int c : cols) t |= s[c] != 1.f;
+      }
+      if (!t) continue;
+      rows.push_back((int64_t)h);
+      for (int c : cols) Wr.push_back(w[c]);
+      if (S_)
+        for (int c : cols) Sr.push_back(S[h * LC_ + c]);
+    }
+    MsgpackWriter u;
+    u.arr(2);
+    u.uint(1);   // user_data_version
+    u.map(8);
+    u.str("method"); u.str(kMethods[mid_]);
+    u.str("H"); u.uint(H_);
+    u.str("labels"); u.arr(cols.size());
+    for (int c : cols) u.str(nm[c]);
+    u.str("counts"); u.arr(cols.size());
+    for (int c : cols) u.uint(labels_.count(c));
+    u.str("rows"); u.bin(rows.data(), rows.size() * 8);
+    u.str("W"); u.bin(Wr.data(), Wr.size() * 4);
+    u.str("P"); u.bin(Sr.data(), Sr.size() * 4);
+    u.str("weights"); u.arr(3); u.uint(0); u.uint(0);
+    u.map(2); u.str("idx"); u.arr(0); u.str("df"); u.arr(0);
+    return std::move(u.out);
+  }
+
+  // models/classifier.py unpack()
+  void unpack(const Value& obj) {
+    if (obj.kind != Value::MAP) throw std::runtime_error("broken model data: driver pack");
+    const Value* H = obj.get("H");
+    if (!H || !H->is_num() || (uint64_t)H->num() != H_)
+      throw std::runtime_error("model hash_max_size differs from the configuration");
+    const Value* lv = obj.get("labels");
+    const Value* cv = obj.get("counts");
+    const Value* rv = obj.get("rows");
+    const Value* wv = obj.get("W");
+    const Value* pv = obj.get("P");
+    if (!lv || lv->kind != Value::ARR || !cv || cv->kind != Value::ARR || !rv || !wv)
+      throw std::runtime_error("broken model data: classifier tables");
+    const size_t L = lv->a.size();
+    const size_t nr = rv->s.size() / 8;
+    if (wv->s.size() != nr * L * 4) throw std::runtime_error("broken model data: W rows");
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipDeviceSynchronize());
+    labels_.clear();
+    int cap = -1;
+    for (int c : kLabelCaps)
+      if ((size_t)c >= std::max<size_t>(1, L)) { cap = c; break; }
+    if (cap < 0) throw std::runtime_error("at most 1024 labels are supported");
+    alloc_locked(cap, true);
+    for (size_t k = 0; k < L; ++k) {
+      labels_.get_or_add(lv->a[k].s.data(), lv->a[k].s.size());
+      labels_.set_count((int)k, k < cv->a.size() ? (uint64_t)cv->a[k].num() : 0);
+    }
+    sync_labels_locked();
+    std::vector<float> W((size_t)H_ * LC_, 0.f), S;
+    const int64_t* rows = (const int64_t*)rv->s.data();
+    const float* wr = (const float*)wv->s.data();
+    for (size_t k = 0; k < nr; ++k) {
+      if (rows[k] < 0 || (uint64_t)rows[k] >= H_) throw std::runtime_error("broken model data: row index");
+      memcpy(&W[(size_t)rows[k] * LC_], wr + k * L, L * 4);
+    }
+    HIPCHK(hipMemcpy(W_, W.data(), W.size() * 4, hipMemcpyHostToDevice));
+    if (S_) {
+      S.assign((size_t)H_ * LC_, 1.f);
+      if (pv && pv->s.size() == nr * L * 4) {
+        const float* sr = (const float*)pv->s.data();
+        for (size_t k = 0; k < nr; ++k) memcpy(&S[(size_t)rows[k] * LC_], sr + k * L, L * 4);
+      }
+      HIPCHK(hipMemcpy(S_, S.data(), S.size() * 4, hipMemcpyHostToDevice));
+    }
+  }
+
+  void status(std::vector<std::pair<std::string, std::string>>* st) {
+    std::lock_guard<std::mutex> g(mu_);
+    unsigned long long sv[2] = {0, 0};
+    HIPCHK(hipMemcpy(sv, stats_, sizeof sv, hipMemcpyDeviceToHost));
+    int live = 0;
+    for (bool a : labels_.alive()) live += a;
+    size_t fr = 0, total = 0;
+    if (hipMemGetInfo(&fr, &total) != hipSuccess) fr = total = 0;
+    auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
+    add("num_classes", std::to_string(live));
+    add("num_features", std::to_string(H_));
+    add("label_capacity", std::to_string(LC_));
+    add("method", kMethods[mid_]);
+    add("storage", "hbm");
+    add("fv_path", "gpu");
+    add("server_runtime", "native");
+    add("train_scan.gpu", std::to_string(scan_gpu));
+    add("train_scan.replayed", std::to_string(scan_replayed));
+    add("train_scan.host", std::to_string(scan_host));
+    add("train_scan.replay_failed", "0");
+    add("train.samples_updated", std::to_string(sv[0]));
+    add("train.samples_trained", std::to_string(sv[1]));
+    add("batching.train.calls", std::to_string(train_calls.load()));
+    add("batching.train.launches", std::to_string(train_batches.load()));
+    add("device", "cuda:" + std::to_string(device));
+    add("hbm_used_bytes", std::to_string(total - fr));
+  }
+
+ private:
+  struct Set {
+    DevBuf<uint8_t> buf;
+    DevBuf<int64_t> meta, off, row, slots;
+    DevBuf<int32_t> len, lab, idx, err;
+    DevBuf<float> val;
+    DevBuf<uint32_t> hist;
+    PinBuf<int64_t> meta_host;
+    int32_t* host_out = nullptr;   // fine-grained: [err | hist nhist]
+    int64_t nhist = 0, host_cap = 0;
+    hipEvent_t copy_done, check_done, ready, free;
+    bool used = false, inflight = false;
+    JbTrainBatch a;
+  };
+  struct Hot {
+    int32_t *rows, *n, *gkey, *gcnt;
+    float* rep;
+    hipEvent_t free;
+    bool free_used = false;
+  };
+
+  template <class T>
+  struct HostBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    T* get(size_t n) {
+      if (n > cap) {
+        T* np = (T*)realloc(p, n * sizeof(T));
+        if (!np) throw std::bad_alloc();
+        p = np;
+        cap = n;
+      }
+      return p;
+    }
+  };
+
+  void fill_ones(float* d, size_t n) {
+    uint32_t one;
+    const float f = 1.f;
+    memcpy(&one, &f, 4);
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d, (int)one, n, compute_));
+  }
+
+  // (re)allocate the tables for LC label columns (copy: keep old columns)
+  void alloc_locked(int LC, bool fresh) {
+    float* W = nullptr;
+    float* S = nullptr;
+    HIPCHK(hipMalloc((void**)&W, (size_t)H_ * LC * 4));
+    HIPCHK(hipMemsetAsync(W, 0, (size_t)H_ * LC * 4, compute_));
+    if (use_s_) {
+      HIPCHK(hipMalloc((void**)&S, (size_t)H_ * LC * 4));
+      fill_ones(S, (size_t)H_ * LC);
+    }
+    if (!fresh && LC_ && W_) {
+      HIPCHK(hipMemcpy2DAsync(W, (size_t)LC * 4, W_, (size_t)LC_ * 4, (size_t)LC_ * 4, H_,
+                              hipMemcpyDeviceToDevice, compute_));
+      if (S && S_)
+        HIPCHK(hipMemcpy2DAsync(S, (size_t)LC * 4, S_, (size_t)LC_ * 4, (size_t)LC_ * 4, H_,
+                                hipMemcpyDeviceToDevice, compute_));
+    }
+    HIPCHK(hipStreamSynchronize(compute_));
+    HIPCHK(hipDeviceSynchronize());      // nothing in flight reads the old tables
+    if (W_) HIPCHK(hipFree(W_));
+    if (S_) HIPCHK(hipFree(S_));
+    if (active_) HIPCHK(hipFree(active_));
+    W_ = W;
+    S_ = S;
+    HIPCHK(hipMalloc((void**)&active_, (size_t)LC * 4));
+    HIPCHK(hipMemset(active_, 0, (size_t)LC * 4));
+    LC_ = LC;
+    label_version_ = ~0ull;
+  }
+
+  // grow the tables / refresh the active mask and the device label table
+  void sync_labels_locked() {
+    const uint64_t v = labels_.version();
+    if (v == label_version_) return;
+    const int n = labels_.size();
+    if (n > LC_) {
+      int cap = -1;
+      for (int c : kLabelCaps)
+        if (c >= n) { cap = c; break; }
+      if (cap < 0) throw std::runtime_error("at most 1024 labels are supported");
+      alloc_locked(cap, false);
+    }
+    auto names = labels_.names();
+    auto alive = labels_.alive();
+    std::vector<int32_t> mask(LC_, 0);
+    for (size_t i = 0; i < alive.size(); ++i) mask[i] = alive[i] ? 1 : 0;
+    // device label table of scan.hip: open addressing on FNV-1a 64,
+    // meta = [blob offset, length, id] (feature_pipeline.label_table_arrays)
+    int cap = 16;
+    size_t live = 0;
+    for (bool a : alive) live += a;
+    while ((size_t)cap < 2 * live) cap *= 2;
+    std::vector<uint64_t> th(cap, 0);
+    std::vector<int32_t> tm(3 * (size_t)cap, -1);
+    std::string blob;
+    for (size_t i = 0; i < names.size(); ++i) {
+      if (!alive[i]) continue;
+      const uint64_t h = fnv1a64(names[i]);
+      size_t j = h & (uint64_t)(cap - 1);
+      while (tm[3 * j + 2] >= 0) j = (j + 1) & (size_t)(cap - 1);
+      th[j] = h;
+      tm[3 * j] = (int32_t)blob.size();
+      tm[3 * j + 1] = (int32_t)names[i].size();
+      tm[3 * j + 2] = (int32_t)i;
+      blob += names[i];
+    }
+    if (blob.empty()) blob.push_back('\0');
+    HIPCHK(hipDeviceSynchronize());      // in-flight scans read the old table
+    HIPCHK(hipMemcpy(active_, mask.data(), mask.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(lt_hash_.get(th.size()), th.data(), th.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(lt_meta_.get(tm.size()), tm.data(), tm.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(lt_blob_.get(blob.size()), blob.data(), blob.size(), hipMemcpyHostToDevice));
+    lt_cap_ = cap;
+    lt_blob_len_ = (int64_t)blob.size();
+    label_version_ = v;
+  }
+
+  // models/classifier.py _hot_wanted
+  bool hot_wanted(int64_t nstreams) {
+    if (!(LC_ <= 64 && nstreams >= 16)) return false;
+    ++hot_batches_;
+    if (hot_seen_pending_ && hipEventQuery(hot_seen_ev_) == hipSuccess) {
+      hot_last_ = ((volatile int32_t*)hot_count_host_)[0];
+      hot_seen_pending_ = false;
+    }
+    return hot_last_ != 0 || hot_batches_ % 8 == 0;
+  }
+
+  // one GPU-scan batch (feature_pipeline.scan_batch_args + classifier._submit_scan)
+  int submit_scan_locked(const uint8_t* arena, const std::vector<jb::ArenaReq>& reqs,
+                         const std::vector<int64_t>& counts, uint64_t used) {
+    sync_labels_locked();
+    const int64_t R = (int64_t)reqs.size();
+    int64_t n = 0;
+    for (int64_t c : counts) n += c;
+    int si = -1;
+    for (int t = 0; t < 4; ++t) {
+      const int k = (next_set_ + t) % 4;
+      if (!sets_[k].inflight) { si = k; break; }
+    }
+    if (si < 0) return -1;
+    next_set_ = (si + 1) % 4;
+    Set& s = sets_[si];
+    if (s.used) HIPCHK(hipEventSynchronize(s.free));
+    s.used = true;
+    const int64_t empty_off = (int64_t)((used + 15) & ~15ull) + 16;
+    const int64_t buf_need = empty_off + 16;
+    const int64_t sps = (int64_t)cfg_.rules.s.size(), spn = (int64_t)cfg_.rules.n.size();
+    const int64_t slot_cap = (int64_t)(used / 3 + 1) * std::max<int64_t>(1, std::max(sps, spn));
+    int64_t* mh = s.meta_host.get(3 * R + 1);
+    mh[2 * R] = 0;
+    for (int64_t k = 0; k < R; ++k) {
+      mh[k] = (int64_t)reqs[k].off;
+      mh[R + k] = (int64_t)reqs[k].len;
+      mh[2 * R + 1 + k] = mh[2 * R + k] + counts[k];
+    }
+    const int64_t nhist = std::max<int64_t>(64, 2 * labels_.size());
+    if (s.host_cap < 1 + nhist) {
+      if (s.host_out) jb_host_free(s.host_out);
+      s.host_out = (int32_t*)jb_host_alloc(4 * (1 + nhist));
+      if (!s.host_out) throw std::runtime_error("hipHostMalloc failed");
+      s.host_cap = 1 + nhist;
+    }
+    s.nhist = nhist;
+    JbTrainBatch& a = s.a;
+    memset(&a, 0, sizeof a);
+    a.copy_stream = copy_;
+    a.prep_stream = prep_;
+    a.compute_stream = compute_;
+    a.copy_done = s.copy_done;
+    a.check_done = s.check_done;
+    a.ready = s.ready;
+    a.set_free = s.free;
+    a.arena = arena;
+    a.used = (int64_t)used;
+    a.meta_host = mh;
+    a.R = R;
+    a.n = n;
+    a.d_buf = s.buf.get(buf_need);
+    a.buf_cap = (int64_t)s.buf.cap;
+    a.empty_off = empty_off;
+    a.d_meta = s.meta.get(3 * R + 1);
+    a.d_off = s.off.get(std::max<int64_t>(n, 1));
+    a.d_len = s.len.get(std::max<int64_t>(n, 1));
+    a.d_lab = s.lab.get(std::max<int64_t>(n, 1));
+    a.d_row = s.row.get(n + 1);
+    a.d_slots = s.slots.get(R);
+    a.d_hist = s.hist.get(nhist);
+    a.nhist = nhist;
+    a.d_err = s.err.get(1);
+    a.host_out = s.host_out;
+    a.lt_hash = lt_hash_.p;
+    a.lt_meta = lt_meta_.p;
+    a.lt_cap = lt_cap_;
+    a.lt_blob = lt_blob_.p;
+    a.lt_blob_len = lt_blob_len_;
+    a.sps = sps;
+    a.spn = spn;
+    a.srules = d_srules_;
+    a.nrules = d_nrules_;
+    a.n_srules = sps;
+    a.n_nrules = spn;
+    a.blob = d_blob_;
+    a.blob_len = (int64_t)std::max<size_t>(1, cfg_.rules.blob.size());
+    a.H = (int64_t)H_;
+    a.d_idx = s.idx.get(slot_cap);
+    a.d_val = s.val.get(slot_cap);
+    a.slot_cap = slot_cap;
+    a.hash_err = hash_err_;
+    a.W = W_;
+    a.S = S_;
+    a.active = active_;
+    a.LC = LC_;
+    a.method = mid_;
+    a.C = C_;
+    a.mode = R > 1 ? kUpdateAtomic : kUpdateExact;
+    a.merge_every = 1;
+    a.hot_waves = kHotWaves;
+    a.stats = stats_;
+    a.touched = nullptr;
+    if (n > 0 && a.mode != kUpdateExact && hot_wanted(R)) {
+      Hot& h = hots_[hot_turn_];
+      hot_turn_ ^= 1;
+      a.hot_rows = h.rows;
+      a.hot_n = h.n;
+      a.hot_rep = h.rep;
+      a.gkey = h.gkey;
+      a.gcnt = h.gcnt;
+      a.gcap = kHotCap;
+      a.block_min = 8;
+      a.min_count = std::max<int64_t>(1024, n / 128);
+      a.max_rows = std::min(kHotMaxRows, kHotEntries / LC_);
+      a.hot_free = h.free;
+      a.hot_free_valid = h.free_used ? 1 : 0;
+      h.free_used = true;
+      if (!hot_seen_pending_) {
+        a.hot_count_host = hot_count_host_;
+        a.hot_seen = hot_seen_ev_;
+        hot_seen_pending_ = true;
+      }
+    }
+    const int rc = jb_train_batch_submit(&a);
+    if (rc != 0) {
+      HIPCHK(hipDeviceSynchronize());
+      throw std::runtime_error("jb_train_batch_submit failed: " + std::to_string(rc));
+    }
+    s.inflight = true;
+    return si;
+  }
+
+  // host path of one request: validate the whole body, then commit labels
+  // and counts, hash, one exact single-stream train launch
+  void host_train_locked(const uint8_t* b, size_t len, int64_t* res, std::string* msg) {
+    jb::Cursor c{b, b + len};
+    uint32_t cnt;
+    if (!c.array(&cnt) || cnt > len) { *res = -1; return; }
+    std::vector<std::pair<const uint8_t*, uint32_t>> labs;
+    labs.reserve(cnt);
+    int64_t slots = 0;
+    HostBuf<int64_t>& row = hrow_;
+    row.get((size_t)cnt + 1)[0] = 0;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      uint32_t two;
+      const uint8_t* ls;
+      uint32_t ln;
+      if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { *res = -1; return; }
+      labs.emplace_back(ls, ln);
+      while (true) {
+        jb::Cursor save = c;
+        const int64_t s0 = slots;
+        const int64_t cap = (int64_t)std::max<size_t>(hidx_.cap, 256);
+        int rc = hasher_->hash_datum(c, hidx_.get(cap), hval_.get(cap), cap, &slots);
+        if (rc == 2) { c = save; slots = s0; hidx_.get(2 * cap); hval_.get(2 * cap); continue; }
+        if (rc != 0) { *res = -1; return; }
+        break;
+      }
+      row.p[k + 1] = slots;
+    }
+    if (c.p != c.end) { *res = -1; return; }
+    int32_t* lab = hlab_.get(std::max<uint32_t>(cnt, 1));
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const int id = labels_.get_or_add((const char*)labs[k].first, labs[k].second);
+      if (id < 0) { *res = -2; *msg = "label table full"; return; }
+      lab[k] = id;
+    }
+    try {
+      sync_labels_locked();
+    } catch (const std::exception& e) {
+      *res = -2;
+      *msg = e.what();
+      return;
+    }
+    for (uint32_t k = 0; k < cnt; ++k) labels_.add_count(lab[k], 1);
+    *res = cnt;
+    if (cnt == 0) return;
+    const int64_t nnz = std::max<int64_t>(slots, 1);
+    int64_t sp[2] = {0, (int64_t)cnt};
+    HIPCHK(hipMemcpyAsync(d_hrow_.get(cnt + 1), row.p, 8 * ((size_t)cnt + 1), hipMemcpyHostToDevice, compute_));
+    HIPCHK(hipMemcpyAsync(d_hidx_.get(nnz), hidx_.p, 4 * (size_t)std::max<int64_t>(slots, 0),
+                          hipMemcpyHostToDevice, compute_));
+    HIPCHK(hipMemcpyAsync(d_hval_.get(nnz), hval_.p, 4 * (size_t)std::max<int64_t>(slots, 0),
+                          hipMemcpyHostToDevice, compute_));
+    HIPCHK(hipMemcpyAsync(d_hlab_.get(cnt), lab, 4 * (size_t)cnt, hipMemcpyHostToDevice, compute_));
+    HIPCHK(hipMemcpyAsync(d_hsp_.get(2), sp, sizeof sp, hipMemcpyHostToDevice, compute_));
+    const int rc = jb_linear_train(d_hrow_.p, d_hidx_.p, d_hval_.p, d_hlab_.p, d_hsp_.p, 1, W_, S_,
+                                   active_, LC_, mid_, C_, kUpdateExact, nullptr, nullptr, nullptr, 1,
+                                   kHotWaves, stats_, nullptr, compute_);
+    if (rc != 0) throw std::runtime_error("jb_linear_train failed: " + std::to_string(rc));
+    HIPCHK(hipStreamSynchronize(compute_));   // host sources are reused by the next request
+  }
+
+  // scores of the hashed classify batch (cidx_/cval_/row_) into out[n * LC]
+  void score_locked(int64_t n, int64_t slots, float* out) {
+    const int64_t* row = row_.p;
+    if (n <= kDirectMaxSamples && row[n] - row[0] <= kDirectMaxSlots) {
+      hipStream_t st = hipStreamQuery(compute_) == hipSuccess ? prio_ : compute_;
+      const int rc = jb_classify_direct(cidx_.p, cval_.p, row, (int)n, W_, LC_, direct_out_,
+                                        direct_done_, st);
+      if (rc == 0) {
+        memcpy(out, direct_out_, (size_t)n * LC_ * 4);
+        return;
+      }
+      if (rc != 1) throw std::runtime_error("jb_classify_direct failed: " + std::to_string(rc));
+    }
+    const int64_t nnz = std::max<int64_t>(slots, 1);
+    int64_t* prow = pin_row_.get(n + 1);
+    int32_t* pidx = pin_idx_.get(nnz);
+    float* pval = pin_val_.get(nnz);
+    memcpy(prow, row, 8 * ((size_t)n + 1));
+    memcpy(pidx, cidx_.p, 4 * (size_t)slots);
+    memcpy(pval, cval_.p, 4 * (size_t)slots);
+    HIPCHK(hipMemcpyAsync(d_crow_.get(n + 1), prow, 8 * ((size_t)n + 1), hipMemcpyHostToDevice, compute_));
+    HIPCHK(hipMemcpyAsync(d_cidx_.get(nnz), pidx, 4 * (size_t)slots, hipMemcpyHostToDevice, compute_));
+    HIPCHK(hipMemcpyAsync(d_cval_.get(nnz), pval, 4 * (size_t)slots, hipMemcpyHostToDevice, compute_));
+    float* dout = d_cout_.get((size_t)n * LC_);
+    const int rc = jb_linear_classify(d_crow_.p, d_cidx_.p, d_cval_.p, (int)n, W_, LC_, dout, compute_);
+    if (rc != 0) throw std::runtime_error("jb_linear_classify failed: " + std::to_string(rc));
+    float* pout = pin_out_.get((size_t)n * LC_);
+    HIPCHK(hipMemcpyAsync(pout, dout, (size_t)n * LC_ * 4, hipMemcpyDeviceToHost, compute_));
+    HIPCHK(hipStreamSynchronize(compute_));
+    memcpy(out, pout, (size_t)n * LC_ * 4);
+  }
+
+  std::mutex mu_;
+  Config cfg_;
+  int mid_ = 0;
+  float C_ = 1.f;
+  bool use_s_ = false;
+  uint64_t H_ = 0;
+  int LC_ = 0;
+  float* W_ = nullptr;
+  float* S_ = nullptr;
+  int32_t* active_ = nullptr;
+  jb::LabelTable labels_;
+  uint64_t label_version_ = ~0ull;
+  DevBuf<uint64_t> lt_hash_;
+  DevBuf<int32_t> lt_meta_;
+  DevBuf<uint8_t> lt_blob_;
+  int64_t lt_cap_ = 16, lt_blob_len_ = 1;
+  std::unique_ptr<jb::HostFvHasher> hasher_;
+  void* d_srules_ = nullptr;
+  void* d_nrules_ = nullptr;
+  uint8_t* d_blob_ = nullptr;
+  hipStream_t copy_, prep_, compute_, prio_;
+  Set sets_[4];
+  int next_set_ = 0;
+  int32_t* hash_err_ = nullptr;
+  Hot hots_[2];
+  int hot_turn_ = 0;
+  int32_t* hot_count_host_ = nullptr;
+  hipEvent_t hot_seen_ev_;
+  bool hot_seen_pending_ = false;
+  int hot_last_ = -1;
+  uint64_t hot_batches_ = 0;
+  unsigned long long* stats_ = nullptr;
+  DevBuf<float> ones_;
+  // host train path
+  HostBuf<int32_t> hidx_, hlab_;
+  HostBuf<float> hval_;
+  HostBuf<int64_t> hrow_;
+  DevBuf<int64_t> d_hrow_, d_hsp_;
+  DevBuf<int32_t> d_hidx_, d_hlab_;
+  DevBuf<float> d_hval_;
+  // classify
+  HostBuf<int32_t> cidx_;
+  HostBuf<float> cval_;
+  HostBuf<int64_t> row_;
+  PinBuf<int64_t> pin_row_;
+  PinBuf<int32_t> pin_idx_;
+  PinBuf<float> pin_val_, pin_out_;
+  DevBuf<int64_t> d_crow_;
+  DevBuf<int32_t> d_cidx_;
+  DevBuf<float> d_cval_, d_cout_;
+  float* direct_out_ = nullptr;
+  uint32_t* direct_done_ = nullptr;
+};
+
+// ----------------------------------------------------------------- server
+class Server {
+ public:
+  Server(const Args& a, const Config& cfg, int device) : a_(a) {
+    clf_.reset(new Classifier(cfg, device));
+    start_time_ = time(nullptr);
+  }
+
+  void load_file(const std::string& path) { load_impl(path, true); }
+
+  int run() {
+    rpc_.reset(new jb::RpcServer([this](const jb::RpcRequest& r) { return dispatch(r); }, a_.threads,
+                                 (double)0));
+    rpc_->set_io_threads(std::max(1, a_.threads / 4));
+    rpc_->set_batch({"classify", "train"},
+                    [this](const std::string& m, std::vector<jb::RpcRequest>& reqs) {
+                      return batch(m, reqs);
+                    },
+                    4096);
+    const char* mb = getenv("JUBATUS_TRAIN_ARENA_MB");
+    const size_t slot_bytes = (size_t)atoll(mb ? mb : "32") << 20;
+    const int nbatch = atoi(getenv("JUBATUS_ARENA_THREADS") ? getenv("JUBATUS_ARENA_THREADS") : "2");
+    for (int k = 0; k < std::max(1, nbatch) + 2; ++k) {
+      uint8_t* p = nullptr;
+      HIPCHK(hipHostMalloc((void**)&p, slot_bytes, hipHostMallocDefault));
+      slots_.push_back(p);
+    }
+    rpc_->set_arena_batch("train", slots_, slot_bytes,
+                          [this](int slot, const std::vector<jb::ArenaReq>& reqs) {
+                            return arena(slot, reqs);
+                          });
+    rpc_->set_batch_threads(std::max(1, nbatch));
+    int port;
+    try {
+      port = rpc_->listen(a_.bind, a_.port);
+    } catch (const std::exception& e) {
+      logf_("FATAL", "server failed to start: any process using port %d? (%s)", a_.port, e.what());
+      return 1;
+    }
+    a_.port = port;
+    logf_("INFO", "start listening at port %d", port);
+    start_time_ = time(nullptr);
+    rpc_->start();
+    logf_("INFO", "jubaclassifier RPC server startup (native)");
+    sigset_t set;
+    sigemptyset(&set);
+    sigaddset(&set, SIGTERM);
+    sigaddset(&set, SIGINT);
+    int sig = 0;
+    while (true) {
+      if (sigwait(&set, &sig) == 0 && (sig == SIGTERM || sig == SIGINT)) break;
+    }
+    logf_("INFO", "stopping RPC server");
+    rpc_->stop();
+    return 0;
+  }
+
+ private:
+  std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
+
+  std::vector<std::string> arena(int slot, const std::vector<jb::ArenaReq>& reqs) {
+    std::vector<int64_t> res;
+    std::vector<std::string> msgs;
+    std::vector<std::string> out(reqs.size());
+    try {
+      clf_->train_arena(slots_[slot], reqs, &res, &msgs);
+    } catch (const std::exception& e) {
+      res.assign(reqs.size(), -2);
+      msgs.assign(reqs.size(), e.what());
+    }
+    rpc_->release_slot(slot);
+    for (size_t k = 0; k < reqs.size(); ++k) {
+      if (res[k] >= 0) {
+        MsgpackWriter w;
+        w.uint((uint64_t)res[k]);
+        out[k] = jb::val::response_ok(reqs[k].msgid, w.out);
+      } else if (res[k] == -1) {
+        out[k] = jb::val::response_code(reqs[k].msgid, kArgumentError);
+      } else {
+        out[k] = jb::val::response_msg(reqs[k].msgid, msgs[k]);
+      }
+    }
+    return out;
+  }
+
+  // params [cluster name, body]: the body's span, or false
+  static bool name_and_body(const std::string& params, const uint8_t** b, size_t* n) {
+    jb::Cursor c{(const uint8_t*)params.data(), (const uint8_t*)params.data() + params.size()};
+    uint32_t two;
+    const uint8_t* s;
+    uint32_t sn;
+    if (!c.array(&two) || two != 2 || !c.raw(&s, &sn)) return false;
+    *b = c.p;
+    *n = (size_t)(c.end - c.p);
+    return true;
+  }
+
+  std::vector<std::string> batch(const std::string& method, std::vector<jb::RpcRequest>& reqs) {
+    std::vector<std::string> out(reqs.size());
+    if (method == "classify") {
+      std::vector<std::pair<const uint8_t*, size_t>> bodies;
+      std::vector<uint32_t> ids;
+      std::vector<size_t> where;
+      for (size_t k = 0; k < reqs.size(); ++k) {
+        const uint8_t* b;
+        size_t n;
+        if (!name_and_body(reqs[k].params, &b, &n)) {
+          out[k] = jb::val::response_code(reqs[k].msgid, kArgumentError);
+          continue;
+        }
+        bodies.emplace_back(b, n);
+        ids.push_back(reqs[k].msgid);
+        where.push_back(k);
+      }
+      try {
+        auto res = clf_->classify(bodies, ids);
+        for (size_t j = 0; j < where.size(); ++j) out[where[j]] = std::move(res[j]);
+      } catch (const std::exception& e) {
+        for (size_t j = 0; j < where.size(); ++j) out[where[j]] = jb::val::response_msg(ids[j], e.what());
+      }
+    } else {   // train requests that found no arena room
+      for (size_t k = 0; k < reqs.size(); ++k) {
+        const uint8_t* b;
+        size_t n;
+        if (!name_and_body(reqs[k].params, &b, &n)) {
+          out[k] = jb::val::response_code(reqs[k].msgid, kArgumentError);
+          continue;
+        }
+        int64_t res = -1;
+        std::string msg;
+        try {
+          clf_->train_body(b, n, &res, &msg);
+        } catch (const std::exception& e) {
+          res = -2;
+          msg = e.what();
+        }
+        if (res >= 0) {
+          MsgpackWriter w;
+          w.uint((uint64_t)res);
+          out[k] = jb::val::response_ok(reqs[k].msgid, w.out);
+        } else if (res == -1) {
+          out[k] = jb::val::response_code(reqs[k].msgid, kArgumentError);
+        } else {
+          out[k] = jb::val::response_msg(reqs[k].msgid, msg);
+        }
+      }
+    }
+    for (size_t k = 0; k < reqs.size(); ++k)
+      if (reqs[k].notify) out[k].clear();
+    return out;
+  }
+
+  std::string dispatch(const jb::RpcRequest& r) {
+    std::string out;
+    Value args;
+    try {
+      args = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
+    } catch (const std::exception&) {
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    }
+    if (args.kind != Value::ARR) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    const std::string& m = r.method;
+    static const std::vector<std::pair<std::string, size_t>> arity = {
+        {"get_config", 1}, {"save", 2}, {"load", 2}, {"get_status", 1}, {"get_labels", 1},
+        {"set_label", 2}, {"clear", 1}, {"delete_label", 2}, {"train", 2}, {"classify", 2}};
+    size_t want = 0;
+    for (const auto& x : arity)
+      if (x.first == m) want = x.second;
+    if (want == 0) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
+    if (args.a.size() != want || (want == 2 && m != "train" && m != "classify" && !args.a[1].is_str()))
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    MsgpackWriter w;
+    try {
+      if (m == "get_config") {
+        w.raw(clf_->config_text());
+      } else if (m == "get_labels") {
+        auto l = clf_->get_labels();
+        w.map(l.size());
+        for (auto& kv : l) { w.raw(kv.first); w.uint(kv.second); }
+      } else if (m == "set_label") {
+        w.boolean(clf_->set_label(args.a[1].s));
+      } else if (m == "delete_label") {
+        w.boolean(clf_->delete_label(args.a[1].s));
+      } else if (m == "clear") {
+        clf_->clear();
+        logf_("INFO", "model cleared: %s", a_.name.c_str());
+        w.boolean(true);
+      } else if (m == "save") {
+        auto p = save(args.a[1].s);
+        w.map(1);
+        w.raw(ident());
+        w.raw(p);
+      } else if (m == "load") {
+        if (args.a[1].s.empty()) throw std::runtime_error("empty id is not allowed");
+        load_impl(local_path(args.a[1].s), false);
+        w.boolean(true);
+      } else if (m == "get_status") {
+        status(&w);
+      } else {   // train / classify outside the batch path (not reached: batched methods)
+        std::vector<jb::RpcRequest> one{r};
+        return batch(m, one)[0];
+      }
+    } catch (const std::exception& e) {
+      return r.notify ? std::string() : jb::val::response_msg(r.msgid, e.what());
+    }
+    return r.notify ? std::string() : jb::val::response_ok(r.msgid, w.out);
+  }
+
+  std::string local_path(const std::string& id) const {
+    return a_.datadir + "/" + a_.eth + "_" + std::to_string(a_.port) + "_classifier_" + id + ".jubatus";
+  }
+
+  std::string save(const std::string& id) {
+    if (id.empty()) throw std::runtime_error("empty id is not allowed");
+    const std::string path = local_path(id);
+    logf_("INFO", "starting save to %s", path.c_str());
+    const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) throw std::runtime_error("cannot open output file: " + path + ": " + strerror(errno));
+    if (flock(fd, LOCK_EX | LOCK_NB) != 0) {
+      close(fd);
+      throw std::runtime_error("cannot get the lock of file; any RPC is saving to same file?: " + path);
+    }
+    MsgpackWriter sys;
+    sys.arr(5);
+    sys.uint(1);
+    sys.uint((uint64_t)time(nullptr));
+    sys.raw(std::string("classifier"));
+    sys.raw(id);
+    sys.raw(clf_->config_text());
+    std::string user;
+    try {
+      user = clf_->pack_user_data();
+    } catch (const std::exception& e) {
+      close(fd);
+      unlink(path.c_str());
+      throw std::runtime_error("cannot write output file: " + path + ": " + e.what());
+    }
+    uint8_t head[48];
+    memcpy(head, "jubatus\0", 8);
+    wr_be(head + 8, 1, 8);
+    for (int k = 0; k < 3; ++k) wr_be(head + 16 + 4 * k, kVersionParts[k], 4);
+    wr_be(head + 28, 0, 4);
+    wr_be(head + 32, sys.out.size(), 8);
+    wr_be(head + 40, user.size(), 8);
+    uint32_t c = jb::crc32_update(0, head, 28);
+    c = jb::crc32_update(c, head + 32, 16);
+    c = jb::crc32_update(c, (const uint8_t*)sys.out.data(), sys.out.size());
+    c = jb::crc32_update(c, (const uint8_t*)user.data(), user.size());
+    wr_be(head + 28, c, 4);
+    bool ok = write_all(fd, head, 48) && write_all(fd, sys.out.data(), sys.out.size()) &&
+              write_all(fd, user.data(), user.size());
+    close(fd);
+    if (!ok) {
+      unlink(path.c_str());
+      throw std::runtime_error("cannot write output file: " + path);
+    }
+    std::lock_guard<std::mutex> g(st_mu_);
+    last_saved_ = time(nullptr);
+    last_saved_path_ = path;
+    logf_("INFO", "saved to %s", path.c_str());
+    return path;
+  }
+
+  static bool write_all(int fd, const void* p, size_t n) {
+    const char* c = (const char*)p;
+    while (n) {
+      ssize_t w = write(fd, c, n);
+      if (w <= 0) {
+        if (w < 0 && errno == EINTR) continue;
+        return false;
+      }
+      c += w;
+      n -= (size_t)w;
+    }
+    return true;
+  }
+
+  void load_impl(const std::string& path, bool overwrite_config) {
+    logf_("INFO", "starting load from %s", path.c_str());
+    std::string bytes;
+    if (!read_file(path, &bytes)) throw std::runtime_error("cannot open input file: " + path + ": " + strerror(errno));
+    ModelFile mf;
+    std::string err = read_model_file(bytes, &mf);
+    if (!err.empty()) throw std::runtime_error(err);
+    if (mf.type != "classifier")
+      throw std::runtime_error("invalid model type: saved type: " + mf.type + ", expected type: classifier");
+    const std::string current = clf_->config_text();
+    if (!overwrite_config && !jb::val::same_config(mf.config, current))
+      throw std::runtime_error("model config mismatched with the running config");
+    if (mf.user_version != 1)
+      throw std::runtime_error("user data version mismatched: " + std::to_string(mf.user_version) +
+                               ", current version: 1");
+    if (overwrite_config && !jb::val::same_config(mf.config, current)) {
+      Config cfg;
+      std::string why;
+      if (!parse_config(mf.config, &cfg, &why))
+        throw std::runtime_error("model config is not served natively: " + why);
+      clf_->configure(cfg);
+    }
+    clf_->unpack(mf.user);
+    std::lock_guard<std::mutex> g(st_mu_);
+    last_loaded_ = time(nullptr);
+    last_loaded_path_ = path;
+    logf_("INFO", "loaded from %s", path.c_str());
+  }
+
+  void status(MsgpackWriter* w) {
+    std::vector<std::pair<std::string, std::string>> st;
+    const time_t now = time(nullptr);
+    long vsz = 0, rss = 0, shr = 0;
+    if (FILE* f = fopen("/proc/self/statm", "r")) {
+      if (fscanf(f, "%ld %ld %ld", &vsz, &rss, &shr) != 3) vsz = rss = shr = 0;
+      fclose(f);
+    }
+    const long kb = sysconf(_SC_PAGESIZE) / 1024;
+    auto add = [&](const char* k, const std::string& v) { st.emplace_back(k, v); };
+    add("clock_time", std::to_string(now));
+    add("start_time", std::to_string(start_time_));
+    add("uptime", std::to_string(now - start_time_));
+    add("VIRT", std::to_string(vsz * kb));
+    add("RSS", std::to_string(rss * kb));
+    add("SHR", std::to_string(shr * kb));
+    add("timeout", std::to_string(a_.timeout));
+    add("threadnum", std::to_string(a_.threads));
+    add("datadir", a_.datadir);
+    add("is_standalone", "1");
+    add("VERSION", kVersion);
+    add("PROGNAME", "jubaclassifier");
+    add("type", "classifier");
+    add("logdir", a_.logdir);
+    add("log_config", a_.log_config);
+    add("configpath", a_.configpath);
+    add("pid", std::to_string(getpid()));
+    add("user", user_name());
+    add("update_count", std::to_string(clf_->update_count.load()));
+    {
+      std::lock_guard<std::mutex> g(st_mu_);
+      add("last_saved", std::to_string(last_saved_));
+      add("last_saved_path", last_saved_path_);
+      add("last_loaded", std::to_string(last_loaded_));
+      add("last_loaded_path", last_loaded_path_);
+    }
+    add("gpu", a_.gpu >= 0 ? std::to_string(a_.gpu) : std::string());
+    clf_->status(&st);
+    if (rpc_) add("rpc.batches", std::to_string(rpc_->batches()));
+    w->map(1);
+    w->raw(ident());
+    w->map(st.size());
+    for (auto& kv : st) { w->raw(kv.first); w->raw(kv.second); }
+  }
+
+  Args a_;
+  std::unique_ptr<Classifier> clf_;
+  std::unique_ptr<jb::RpcServer> rpc_;
+  std::vector<uint8_t*> slots_;
+  time_t start_time_ = 0;
+  std::mutex st_mu_;
+  time_t last_saved_ = 0, last_loaded_ = 0;
+  std::string last_saved_path_, last_loaded_path_;
+};
+
+// hand the server to the Python implementation (before any HIP call)
+[[noreturn]] void exec_python(int argc, char** argv, const char* why) {
+  fprintf(stderr, "jubaclassifier: %s: starting the Python server\n", why);
+  char exe[PATH_MAX];
+  ssize_t n = readlink("/proc/self/exe", exe, sizeof exe - 1);
+  std::string root = ".";
+  if (n > 0) {
+    exe[n] = 0;
+    std::string p(exe);   // <root>/jubatus_amd/native_bin/jubaclassifier
+    for (int k = 0; k < 3; ++k) p = p.substr(0, p.rfind('/'));
+    root = p;
+  }
+  const char* pp = getenv("PYTHONPATH");
+  std::string path = root + (pp && *pp ? std::string(":") + pp : std::string());
+  setenv("PYTHONPATH", path.c_str(), 1);
+  std::vector<char*> av;
+  static char py[] = "python3", m[] = "-m", mod[] = "jubatus_amd.cmd.server", eng[] = "classifier";
+  av.push_back(py);
+  av.push_back(m);
+  av.push_back(mod);
+  av.push_back(eng);
+  for (int k = 1; k < argc; ++k) av.push_back(argv[k]);
+  av.push_back(nullptr);
+  execvp("python3", av.data());
+  perror("execvp python3");
+  _exit(127);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  int rc = parse_args(argc, argv, &a);
+  if (rc == -1) return 0;
+  if (rc) return rc;
+  if (a.version) {
+    printf("jubatus-%s (mi355x, native)\n", kVersion);
+    return 0;
+  }
+  const char* force = a.native_check ? nullptr : getenv("JUBATUS_NATIVE_SERVER");
+  if (force && strcmp(force, "0") == 0) exec_python(argc, argv, "JUBATUS_NATIVE_SERVER=0");
+  if (!a.native_check) {
+    if (!a.zookeeper.empty()) exec_python(argc, argv, "distributed mode");
+    if (a.cpu || getenv("JUBATUS_FORCE_CPU")) exec_python(argc, argv, "host backend requested");
+    if (access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
+  }
+  if (a.configpath.empty() && a.model_file.empty()) {
+    fprintf(stderr, "config path or model file must be specified for standalone mode\n%s", kUsage);
+    return 1;
+  }
+  if (!a.configpath.empty()) a.configpath = real_path(a.configpath);
+  if (!a.model_file.empty()) a.model_file = real_path(a.model_file);
+  if (!a.datadir.empty()) {
+    a.datadir = real_path(a.datadir);
+    if (access(a.datadir.c_str(), W_OK) != 0) {
+      fprintf(stderr, "can't use datadir: %s\n%s", a.datadir.c_str(), kUsage);
+      return 1;
+    }
+  }
+  if (!a.listen_addr.empty()) {
+    a.bind = a.eth = a.listen_addr;
+  } else if (!a.listen_if.empty()) {
+    a.bind = a.eth = if_v4(a.listen_if);
+  } else {
+    a.eth = default_v4();
+  }
+  // the configuration this process will serve: the model file's (it wins
+  // over -f, server_helper.hpp) or the config file
+  std::string text;
+  if (!a.model_file.empty()) {
+    std::string bytes;
+    ModelFile mf;
+    if (!read_file(a.model_file, &bytes)) exec_python(argc, argv, "unreadable model file");
+    if (!read_model_file(bytes, &mf).empty()) exec_python(argc, argv, "model file check");
+    text = mf.config;
+  } else if (!read_file(a.configpath, &text)) {
+    exec_python(argc, argv, "unreadable config file");
+  }
+  Config cfg;
+  std::string why;
+  if (a.native_check) {   // the config check alone (tests, operators): no GPU, no exec
+    const bool ok = parse_config(text, &cfg, &why);
+    printf("%s\n", ok ? "native" : ("python: " + why).c_str());
+    return 0;
+  }
+  if (!parse_config(text, &cfg, &why)) exec_python(argc, argv, why.c_str());
+  // below this line the process owns the GPU: no exec
+  int device = a.gpu;
+  if (device < 0) {
+    const char* lr = getenv("LOCAL_RANK");
+    device = lr ? atoi(lr) : 0;
+  }
+  sigset_t set;
+  sigemptyset(&set);
+  sigaddset(&set, SIGTERM);
+  sigaddset(&set, SIGINT);
+  pthread_sigmask(SIG_BLOCK, &set, nullptr);   // every thread inherits it; main sigwaits
+  signal(SIGPIPE, SIG_IGN);
+  logf_("INFO", "starting jubaclassifier %s RPC server at %s:%d (native, device %d)", kVersion,
+        a.eth.c_str(), a.port, device);
+  try {
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) throw std::runtime_error("no HIP device");
+    device %= ndev;
+    Server srv(a, cfg, device);
+    if (!a.model_file.empty()) srv.load_file(a.model_file);
+    logf_("INFO", "config loaded: %s", kMethods[cfg.method]);
+    return srv.run();
+  } catch (const std::exception& e) {
+    logf_("FATAL", "failed to start classifier: %s", e.what());
+    return 1;
+  }
+}

@@ -1,0 +1,101 @@
+"""Native jubaclassifier (csrc/server/jubaclassifier.cpp): the configuration
+check that decides native vs Python service, and the hand-over to the Python
+server (exec before any GPU call) on hosts without a GPU. The GPU behaviour
+is in tests/test_native_server_gpu.py."""
+import os
+import socket
+import subprocess
+import time
+
+import pytest
+
+from helpers import ROOT, config_path
+from jubatus_amd.common.mprpc import RpcClient, RpcIOError, RpcTimeoutError
+
+BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaclassifier")
+
+NATIVE = ["arow.json", "cw.json", "nherd.json", "pa.json", "pa1.json", "pa2.json", "perceptron.json"]
+PYTHON = {"arow_combinational_feature.json": "combination_rules", "cosine.json": "not a linear method",
+          "default.json": "string type", "nn.json": "not a linear method",
+          "euclidean.json": "not a linear method"}
+
+
+def _check(cfg_file):
+    r = subprocess.run([BIN, "--native-check", "-f", cfg_file], capture_output=True, text=True,
+                       timeout=30)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+@pytest.mark.parametrize("name", NATIVE)
+def test_linear_configs_are_native(name):
+    assert _check(config_path(f"classifier/{name}")) == "native"
+
+
+@pytest.mark.parametrize("name,why", sorted(PYTHON.items()))
+def test_other_configs_go_to_python(name, why):
+    out = _check(config_path(f"classifier/{name}"))
+    assert out.startswith("python: ") and why in out, out
+
+
+@pytest.mark.parametrize("cfg,why", [
+    ({"method": "AROW", "converter": {"num_rules": [{"key": "/x.*/", "type": "num"}]},
+      "parameter": {"regularization_weight": 1.0}}, "regex"),
+    ({"method": "AROW", "converter": {"string_rules": [
+        {"key": "*", "type": "str", "sample_weight": "tf", "global_weight": "idf"}]},
+      "parameter": {"regularization_weight": 1.0}}, "global_weight idf"),
+    ({"method": "CW", "converter": {}, "parameter": {}}, "regularization_weight"),
+    ({"method": "PA", "converter": {"string_rules": [{"key": "*", "type": "str"}],
+                                    "num_types": {"num": {"method": "add", "value": 1}},
+                                    "num_rules": [{"key": "*", "type": "num"}]}}, "num type num"),
+])
+def test_config_details(tmp_path, cfg, why):
+    import json
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps(cfg))
+    out = _check(str(p))
+    assert why in out, out
+
+
+def test_version():
+    r = subprocess.run([BIN, "-v"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0 and "native" in r.stdout
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU host serves natively")
+def test_hands_over_to_python_without_gpu(tmp_path):
+    """no /dev/kfd: the binary execs the Python server with the same flags"""
+    port = _free_port()
+    env = dict(os.environ, JUBATUS_FORCE_CPU="1")
+    p = subprocess.Popen([BIN, "-p", str(port), "-b", "127.0.0.1", "-f",
+                          config_path("classifier/arow.json"), "-d", str(tmp_path)],
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+    try:
+        deadline = time.time() + 120
+        st = None
+        while time.time() < deadline:
+            try:
+                with RpcClient("127.0.0.1", port, 5.0) as c:
+                    st = c.call("get_status", "")
+                    assert c.call("train", "", [["a", [[["w", "x"]], [], []]]]) == 1
+                break
+            except (OSError, RpcIOError, RpcTimeoutError):
+                if p.poll() is not None:
+                    break
+                time.sleep(0.5)
+        assert st is not None, p.stdout.read().decode(errors="replace") if p.poll() is not None else ""
+        (_, s), = st.items()
+        s = {(k.decode() if isinstance(k, bytes) else k): v for k, v in s.items()}
+        assert "server_runtime" not in s       # the Python server answered
+        assert s["storage"] == "host"
+    finally:
+        p.terminate()
+        p.wait(timeout=30)

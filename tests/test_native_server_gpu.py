@@ -1,0 +1,224 @@
+"""Native jubaclassifier on the GPU (csrc/server/jubaclassifier.cpp, no
+Python in the server process): RPC behaviour of the reference client tests,
+numerics against the host oracle (models/linear_oracle.py through
+LinearClassifier on the host), concurrent train RPCs through the arena /
+GPU-scan path, and model files interchangeable with the Python server's."""
+import json
+import os
+import random
+import socket
+import subprocess
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from helpers import ROOT, config_path
+from jubatus_amd.client import Classifier, Datum
+from jubatus_amd.common.mprpc import RpcClient, RpcIOError, RpcTimeoutError, RpcTypeError
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaclassifier")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _start(cfg, tmp_path):
+    port = _free_port()
+    p = subprocess.Popen([BIN, "-p", str(port), "-b", "127.0.0.1", "-f", cfg, "-d", str(tmp_path),
+                          "-c", "16"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    deadline = time.time() + 60
+    while time.time() < deadline:
+        try:
+            with RpcClient("127.0.0.1", port, 5.0) as c:
+                c.call("get_config", "")
+            return port, p
+        except (OSError, RpcIOError, RpcTimeoutError):
+            if p.poll() is not None:
+                break
+            time.sleep(0.2)
+    p.kill()
+    raise RuntimeError("native server did not start: " + p.stdout.read().decode(errors="replace"))
+
+
+@pytest.fixture
+def native(tmp_path):
+    port, p = _start(config_path("classifier/arow.json"), tmp_path)
+    yield port
+    p.terminate()
+    try:
+        p.wait(timeout=30)
+    except subprocess.TimeoutExpired:
+        p.kill()
+
+
+def _data(rng, n):
+    out = []
+    for _ in range(n):
+        y = rng.randrange(4)
+        out.append((f"L{y}", Datum({"w": f"t{y * 10 + rng.randrange(3)}", "u": f"n{rng.randrange(50)}",
+                                    "x": float(y) + rng.random()})))
+    return out
+
+
+def _status(c):
+    (ident, st), = c.get_status().items()
+    return ident, st
+
+
+def _oracle(cfg_file):
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.classifier import LinearClassifier
+    cfg = json.load(open(cfg_file))
+    return LinearClassifier(cfg["method"], cfg.get("parameter"), DatumToFvConverter(cfg["converter"]),
+                            device=None)
+
+
+def _scores(rows):
+    return [{e.label: e.score for e in r} for r in rows]
+
+
+def test_native_server_matches_host_oracle(native):
+    """sequential train requests (host path for new labels, then the GPU
+    scan, exact single-stream updates) give the oracle's AROW model"""
+    cfg = config_path("classifier/arow.json")
+    c = Classifier("127.0.0.1", native, "", timeout=60)
+    ora = _oracle(cfg)
+    rng = random.Random(3)
+    for _ in range(6):
+        chunk = _data(rng, 50)
+        assert c.train(chunk) == 50
+        ora.train([(l, d) for l, d in chunk])
+    test = [d for _, d in _data(random.Random(9), 40)]
+    got = _scores(c.classify(test))
+    want = [dict(r) for r in ora.classify(test)]
+    for g, w in zip(got, want):
+        assert set(g) == set(w)
+        for k in w:
+            assert abs(g[k] - w[k]) <= 1e-4 * max(1.0, abs(w[k])), (k, g[k], w[k])
+    ident, st = _status(c)
+    assert st["server_runtime"] == "native" and st["storage"] == "hbm"
+    assert int(st["train_scan.gpu"]) >= 1 and int(st["train_scan.host"]) >= 1
+    for k in ("PROGNAME", "RSS", "VERSION", "clock_time", "configpath", "datadir", "is_standalone",
+              "last_loaded", "last_saved", "pid", "threadnum", "timeout", "update_count", "uptime",
+              "user"):
+        assert k in st, k
+    assert st["is_standalone"] == "1"
+    assert sum(c.get_labels().values()) == 300
+    c.close()
+
+
+def test_native_concurrent_train_and_bad_requests(native):
+    c = Classifier("127.0.0.1", native, "", timeout=60)
+    assert c.train(_data(random.Random(1), 32)) == 32
+    errors, bad_seen = [], []
+
+    def good(seed):
+        try:
+            cc = Classifier("127.0.0.1", native, "", timeout=60)
+            r = random.Random(seed)
+            for _ in range(20):
+                assert cc.train(_data(r, 64)) == 64
+            cc.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def bad():
+        with RpcClient("127.0.0.1", native, 60.0) as rc:
+            for _ in range(5):
+                try:
+                    rc.call("train", "", [["L1", [[["only-a-key"]], [], []]]])
+                except RpcTypeError:
+                    bad_seen.append(1)
+    ts = [threading.Thread(target=good, args=(s,)) for s in range(16)] + [threading.Thread(target=bad)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+    assert len(bad_seen) == 5
+    assert sum(c.get_labels().values()) == 32 + 16 * 20 * 64
+    test = _data(random.Random(77), 200)
+    res = c.classify([d for _, d in test])
+    acc = np.mean([max(r, key=lambda e: e.score).label == l for r, (l, _) in zip(res, test)])
+    assert acc > 0.9, acc
+    assert c.classify([]) == []
+    big = c.classify([d for _, d in _data(random.Random(5), 300)])     # batch (non-direct) path
+    assert len(big) == 300 and all(len(r) == 4 for r in big)
+    c.close()
+
+
+def test_native_labels_and_clear(native):
+    c = Classifier("127.0.0.1", native, "", timeout=60)
+    assert c.set_label("new") is True
+    assert c.set_label("new") is False
+    assert c.train(_data(random.Random(2), 20)) == 20
+    labels = c.get_labels()
+    assert labels["new"] == 0 and len(labels) == 5
+    assert c.delete_label("L0") is True
+    assert c.delete_label("L0") is False
+    assert "L0" not in c.get_labels()
+    r = c.classify([Datum({"w": "t1"})])
+    assert {e.label for e in r[0]} == set(c.get_labels())
+    assert c.clear() is True
+    assert c.get_labels() == {}
+    assert json.loads(c.get_config()) == json.load(open(config_path("classifier/arow.json")))
+    with RpcClient("127.0.0.1", native, 10.0) as rc:
+        with pytest.raises(Exception):
+            rc.call("no_such_method", "")
+    c.close()
+
+
+def test_native_model_files_interoperate_with_python(native, tmp_path):
+    from jubatus_amd.framework import save_load
+    cfg_file = config_path("classifier/arow.json")
+    cfg_text = open(cfg_file).read()
+    c = Classifier("127.0.0.1", native, "", timeout=60)
+    rng = random.Random(11)
+    data = _data(rng, 300)
+    for k in range(0, 300, 100):
+        assert c.train(data[k:k + 100]) == 100
+    test = [d for _, d in _data(random.Random(12), 30)]
+    before = _scores(c.classify(test))
+    ident, _ = _status(c)
+    (_, path), = c.save("m1").items()
+    assert os.path.exists(path)
+    # native file -> Python driver
+    with open(path, "rb") as f:
+        _, pack = save_load.load_server(f, "classifier", cfg_text, 1, False)
+    ora = _oracle(cfg_file)
+    ora.unpack(pack)
+    py = [dict(r) for r in ora.classify(test)]
+    for g, w in zip(before, py):
+        for k in w:
+            assert abs(g[k] - w[k]) <= 1e-5 * max(1.0, abs(w[k]))
+    assert ora.get_labels() == c.get_labels()
+    # native load of its own file after clear
+    assert c.clear() is True
+    assert c.load("m1") is True
+    again = _scores(c.classify(test))
+    for g, w in zip(again, before):
+        for k in w:
+            assert abs(g[k] - w[k]) <= 1e-6 * max(1.0, abs(w[k]))
+    # Python file -> native server
+    ora2 = _oracle(cfg_file)
+    ora2.train([(l, d) for l, d in _data(random.Random(13), 120)])
+    p2 = os.path.join(os.path.dirname(path), f"{ident}_classifier_py.jubatus")
+    with open(p2, "wb") as f:
+        save_load.save_server(f, "classifier", "py", cfg_text, 1, ora2.pack())
+    assert c.load("py") is True
+    got = _scores(c.classify(test))
+    want = [dict(r) for r in ora2.classify(test)]
+    for g, w in zip(got, want):
+        for k in w:
+            assert abs(g[k] - w[k]) <= 1e-5 * max(1.0, abs(w[k]))
+    assert c.get_labels() == ora2.get_labels()
+    c.close()
