@@ -392,6 +392,8 @@ def main() -> None:
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--no-rpc", action="store_true",
                     help="skip the served-path measurement (jubaclassifier + jubaloadgen, N = 1)")
+    ap.add_argument("--served-runtime", choices=("python", "native", "both"), default="both",
+                    help="which server --served-only measures")
     ap.add_argument("--served-only", action="store_true",
                     help="measure only the served path (prints its record; not the headline)")
     ap.add_argument("--rpc-seconds", type=float, default=4.0)
@@ -467,8 +469,13 @@ def main() -> None:
 
     nat = native()
     if args.served_only:
-        print(json.dumps({"python": served_train(args, local, nat),
-                          "native": served_train_native(args, local, nat)}), flush=True)
+        out = {}
+        if args.served_runtime in ("python", "both"):
+            out["python"] = served_train(args, local, nat)
+        if args.served_runtime in ("native", "both"):
+            out["native"] = served_train_native(args, local, nat)
+        out["arena_threads"] = os.environ.get("JUBATUS_ARENA_THREADS", "2")
+        print(json.dumps(out), flush=True)
         return
     gen_threads = max(1, min(16, (os.cpu_count() or 8) // max(1, local_world)))
     p_corr, vocab = (0.0, (1 << 31) - 1) if args.worst_case else (0.6, args.vocab)

@@ -51,6 +51,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -514,9 +515,17 @@ class Classifier {
       HIPCHK(hipMemset(h.gcnt, 0, kHotCap * 4));
       HIPCHK(hipEventCreateWithFlags(&h.free, hipEventDisableTiming));
     }
-    for (Set& s : sets_)
-      for (hipEvent_t* e : {&s.copy_done, &s.check_done, &s.ready, &s.free})
+    // the batch threads wait on check_done; JUBATUS_SERVER_BLOCKING_WAIT=1
+    // parks them (blocking-sync event) instead of spinning. Measured neutral
+    // on the served path, which is bound by the transport's framing
+    // (profiles/r02_served_native_sweep.jsonl), so spinning stays the default.
+    const char* blk = getenv("JUBATUS_SERVER_BLOCKING_WAIT");
+    const unsigned wait_flags = (blk && strcmp(blk, "1") == 0) ? (unsigned)hipEventBlockingSync : 0u;
+    for (Set& s : sets_) {
+      for (hipEvent_t* e : {&s.copy_done, &s.ready, &s.free})
         HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&s.check_done, hipEventDisableTiming | wait_flags));
+    }
     configure(cfg);
   }
 
@@ -572,7 +581,13 @@ class Classifier {
     if (gpu_ok) {
       int si = -1;
       {
-        std::lock_guard<std::mutex> g(mu_);
+        std::unique_lock<std::mutex> g(mu_);
+        // every scan set busy (more batch threads than sets): wait for one
+        set_cv_.wait(g, [&] {
+          for (const Set& s : sets_)
+            if (!s.inflight) return true;
+          return false;
+        });
         if (labels_.size() > 0) si = submit_scan_locked(arena, reqs, counts, used);
       }
       if (si >= 0) {
@@ -580,16 +595,16 @@ class Classifier {
         HIPCHK(hipEventSynchronize(s.check_done));
         std::lock_guard<std::mutex> g(mu_);
         const int32_t err = ((volatile int32_t*)s.host_out)[0];
+        s.inflight = false;
+        set_cv_.notify_one();
         if (err == 0) {
           const int32_t* hist = s.host_out + 1;
           for (int64_t l = 0; l < s.nhist; ++l)
             if (hist[l]) labels_.add_count((int)l, (uint64_t)hist[l]);
-          s.inflight = false;
           for (size_t k = 0; k < R; ++k) (*res)[k] = counts[k];
           scan_gpu += 1;
           return;
         }
-        s.inflight = false;
         scan_replayed += 1;
       }
     }
@@ -1190,6 +1205,7 @@ class Classifier {
   }
 
   std::mutex mu_;
+  std::condition_variable set_cv_;   // a scan set left flight
   Config cfg_;
   int mid_ = 0;
   float C_ = 1.f;
