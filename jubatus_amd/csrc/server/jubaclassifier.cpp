@@ -580,6 +580,7 @@ class Classifier {
     }
     if (gpu_ok) {
       int si = -1;
+      const auto t0 = std::chrono::steady_clock::now();
       {
         std::unique_lock<std::mutex> g(mu_);
         // every scan set busy (more batch threads than sets): wait for one
@@ -592,8 +593,13 @@ class Classifier {
       }
       if (si >= 0) {
         Set& s = sets_[si];
+        const auto t1 = std::chrono::steady_clock::now();
         HIPCHK(hipEventSynchronize(s.check_done));
+        const auto t2 = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> g(mu_);
+        prof_[0] += 1;
+        prof_[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+        prof_[2] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
         const int32_t err = ((volatile int32_t*)s.host_out)[0];
         s.inflight = false;
         set_cv_.notify_one();
@@ -854,6 +860,11 @@ class Classifier {
     add("train.samples_trained", std::to_string(sv[1]));
     add("batching.train.calls", std::to_string(train_calls.load()));
     add("batching.train.launches", std::to_string(train_batches.load()));
+    if (prof_[0]) {   // GPU-scan batches: submit (lock + set wait + launch) / scan-check wait
+      add("served.batches", std::to_string(prof_[0]));
+      add("served.submit_us_per_batch", std::to_string(prof_[1] / prof_[0] / 1000));
+      add("served.check_wait_us_per_batch", std::to_string(prof_[2] / prof_[0] / 1000));
+    }
     add("device", "cuda:" + std::to_string(device));
     add("hbm_used_bytes", std::to_string(total - fr));
   }
@@ -1206,6 +1217,7 @@ class Classifier {
 
   std::mutex mu_;
   std::condition_variable set_cv_;   // a scan set left flight
+  uint64_t prof_[3] = {0, 0, 0};     // GPU-scan batches, submit ns, check-wait ns
   Config cfg_;
   int mid_ = 0;
   float C_ = 1.f;

@@ -103,8 +103,14 @@ def loadgen(port, method, params, per, conns=16, depth=4, secs=4.0):
     return d
 
 
+class _SkipPython(Exception):
+    pass
+
+
 def main():
-    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 500
+    native_only = "--native-only" in sys.argv
+    argv = [a for a in sys.argv[1:] if a != "--native-only"]
+    iters = int(argv[0]) if argv else 500
     from jubatus_amd import build_ext
     from jubatus_amd.client import Classifier, Datum
     from jubatus_amd.common import config as zkconfig
@@ -113,6 +119,7 @@ def main():
     from jubatus_amd.common.lock_service import CoordinatorClient
 
     build_ext.build_tools()
+    build_ext.build_servers()
     env = dict(os.environ, PYTHONPATH=ROOT)
     cfg = os.path.join(ROOT, "config", "classifier", "arow.json")
     tmp = tempfile.mkdtemp()
@@ -141,6 +148,8 @@ def main():
     try:
         # standalone server, client -> server
         sp = free_port()
+        if native_only:
+            raise _SkipPython()
         procs.append(subprocess.Popen([sys.executable, "-m", "jubatus_amd.cmd.server", "classifier",
                                        "-p", str(sp), "-b", "127.0.0.1", "-f", cfg, "-d", tmp, "-c", "16"],
                                       env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL))
@@ -162,6 +171,8 @@ def main():
         out["direct_loadgen_train_1024_inflight"] = loadgen(sp, "train", p_train(""), len(enc_train),
                                                             conns=64, depth=16)
         out["direct_loadgen_classify_1"] = loadgen(sp, "classify", p_one(""), 1, conns=8, depth=1)
+        out["direct_loadgen_classify_1_single_conn"] = loadgen(sp, "classify", p_one(""), 1, conns=1,
+                                                               depth=1)
         rc = RpcClient("127.0.0.1", sp, 30)
         (_, st), = rc.call("get_status", "").items()
         out["server_spans"] = {k: v for k, v in st.items()
@@ -169,6 +180,34 @@ def main():
                                                 "trace.pipe.",
                                                 "batching."))}
         rc.close()
+    except _SkipPython:
+        pass
+    try:
+        # the native server binary (csrc/server/jubaclassifier.cpp), same calls
+        nbin = os.path.join(build_ext.NATIVE_BIN, "jubaclassifier")
+        if os.access(nbin, os.X_OK):
+            npt = free_port()
+            procs.append(subprocess.Popen([nbin, "-p", str(npt), "-b", "127.0.0.1", "-f", cfg, "-d", tmp,
+                                           "-c", "16"], stdout=subprocess.DEVNULL,
+                                          stderr=subprocess.DEVNULL))
+            assert wait_port(npt), "native server did not start"
+            rc = RpcClient("127.0.0.1", npt, 30)
+            for _ in range(20):
+                rc.call_raw("train", p_train(""))
+            (_, st), = rc.call("get_status", "").items()
+            out["native_server_runtime"] = st.get("server_runtime", "python")
+            out["native_direct_train_128"] = lat(lambda: rc.call_raw("train", p_train("")), iters // 5)
+            out["native_direct_classify_1"] = lat(lambda: rc.call_raw("classify", p_one("")), iters)
+            rc.close()
+            out["native_loadgen_classify_1"] = loadgen(npt, "classify", p_one(""), 1, conns=8, depth=1)
+            out["native_loadgen_classify_1_single_conn"] = loadgen(npt, "classify", p_one(""), 1,
+                                                                   conns=1, depth=1)
+            rc = RpcClient("127.0.0.1", npt, 30)
+            (_, st), = rc.call("get_status", "").items()
+            out["native_status"] = {k: v for k, v in st.items() if k.startswith(("served.", "train_scan."))}
+            rc.close()
+        if native_only:
+            raise _SkipPython()
         # distributed: native coordinator + server + native proxy
         coord = NativeCoordinator(0, "127.0.0.1")
         ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
@@ -198,6 +237,8 @@ def main():
         out["proxy_status"] = {k: st[k] for k in ("request_count", "forward_count", "implementation")}
         c.close()
         ls.close()
+    except _SkipPython:
+        pass
     finally:
         for p in procs:
             p.terminate()
