@@ -357,3 +357,53 @@ def test_concurrent_streams_learn_with_hot_replica(mode):
     acc = np.mean([max(r, key=lambda t: t[1])[0] == l for r, (l, _) in zip(res, test)])
     assert acc > 0.8, acc
     g.pipe.check_errors()
+
+
+@pytest.mark.parametrize("hot", [False, True])
+def test_concurrent_deviation_from_serial_order(hot, monkeypatch, capsys):
+    """1020 concurrent atomic streams (one per request, the served batch
+    shape) against the same requests applied one after another on the
+    host oracle. Step i of every stream reads the model as the streams left
+    it at step i-1, so a row that all streams carry receives ~1000 AROW
+    steps computed from the same confidence: the concurrent weights grow
+    far larger than the serial ones (measured ~35-45x in norm on this data,
+    profiles/r02_concurrent_vs_serial.jsonl), while the decisions agree on
+    ~97% of held-out datums and accuracy drops ~1 point. Bounded here: the
+    predictions, the accuracy and that every sample was trained once."""
+    from jubatus_amd.fv_converter.datum import Datum
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    conv = {**CONV, "hash_max_size": 1 << 16}
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv),
+                         device=_device())
+    g.hot_rows = hot
+    g.hot_min_count = 64 if hot else None
+    c = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(conv))
+    data = _data(1024 * 16, seed=21, wild=False)
+    reqs = [data[i:i + 16] for i in range(0, len(data), 16)]
+    warm = reqs[:4]                      # labels known before the concurrent batch
+    for r in warm:
+        g.train(r)
+        c.train(r)
+    bodies = [msgpack.packb([[l, Datum(d).to_msgpack()] for l, d in r], use_bin_type=False)
+              for r in reqs[4:]]
+    assert g.train_requests(bodies) == 16 * (len(reqs) - 4)
+    for r in reqs[4:]:                   # serialized: request after request
+        c.train(r)
+    g.synchronize()
+    Wg, Wc = g.W.cpu().numpy()[:, :c.LC], c.W
+    rel = float(np.linalg.norm(Wg - Wc) / np.linalg.norm(Wc))
+    test = _data(2000, seed=22, wild=False)
+    pg = [max(r, key=lambda t: t[1])[0] for r in g.classify([d for _, d in test])]
+    pc = [max(r, key=lambda t: t[1])[0] for r in c.classify([d for _, d in test])]
+    agree = float(np.mean([a == b for a, b in zip(pg, pc)]))
+    acc_g = float(np.mean([p == l for p, (l, _) in zip(pg, test)]))
+    acc_c = float(np.mean([p == l for p, (l, _) in zip(pc, test)]))
+    with capsys.disabled():
+        print(f"\nconcurrent vs serial (hot={hot}): rel W diff {rel:.3f}, agreement {agree:.3f}, "
+              f"acc {acc_g:.3f} vs {acc_c:.3f}")
+    assert agree >= 0.95, agree
+    assert acc_g >= acc_c - 0.025, (acc_g, acc_c)
+    assert np.isfinite(rel)
+    st = g.train_stats()
+    assert st["trained"] == len(data)
