@@ -161,6 +161,8 @@ def build_tools(force: bool = False, nproc: int = 8, sanitize: str | None = None
 SERVERS = {
     "jubaclassifier": (["server/jubaclassifier.cpp", "native/jb_rpc.cpp"],
                        ["server", "native", "hip"]),
+    "jubaregression": (["server/jubaregression.cpp", "native/jb_rpc.cpp"],
+                       ["server", "native", "hip"]),
 }
 
 

@@ -27,23 +27,8 @@
 //            (classify_direct.hip), larger batches take jb_linear_classify.
 // Model files are byte-compatible with the Python server's
 // (framework/save_load.py container, models/classifier.py pack()).
-#include <dirent.h>
-#include <errno.h>
-#include <fcntl.h>
-#include <getopt.h>
-#include <ifaddrs.h>
-#include <limits.h>
-#include <math.h>
-#include <netinet/in.h>
-#include <arpa/inet.h>
-#include <pwd.h>
 #include <signal.h>
-#include <stdarg.h>
-#include <stdio.h>
-#include <stdlib.h>
 #include <string.h>
-#include <sys/file.h>
-#include <sys/stat.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -63,6 +48,7 @@
 #include "jb_pack.hpp"
 #include "jb_rpc.hpp"
 #include "jb_train_batch.hpp"
+#include "jb_server_common.hpp"
 #include "jb_value.hpp"
 
 extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
@@ -83,12 +69,6 @@ extern "C" int64_t jb_hot_rep_bytes();
 
 namespace {
 
-using jb::val::MsgpackReader;
-using jb::val::MsgpackWriter;
-using jb::val::Value;
-
-const char* const kVersion = "0.9.2";
-const uint32_t kVersionParts[3] = {0, 9, 2};
 const char* const kMethods[] = {"perceptron", "PA", "PA1", "PA2", "CW", "AROW", "NHERD"};
 const int kLabelCaps[] = {8, 16, 32, 64, 128, 256, 512, 1024};
 constexpr int kUpdateExact = 0, kUpdateAtomic = 1;
@@ -96,233 +76,8 @@ constexpr int kMethodCW = 4;
 constexpr int kHotMaxRows = 64, kHotEntries = 512, kHotCap = 1 << 14, kHotWaves = 8;
 constexpr int kDirectMaxSamples = 32, kDirectMaxSlots = 320;
 constexpr int64_t kScanLdsBytes = 27 * 1024, kScanMaxSamples = 768;   // scan.hip
-constexpr int kArgumentError = 2, kNoMethodError = 1;
 
-#define HIPCHK(x)                                                                    \
-  do {                                                                               \
-    hipError_t e_ = (x);                                                             \
-    if (e_ != hipSuccess)                                                            \
-      throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_));      \
-  } while (0)
-
-void logf_(const char* level, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-void logf_(const char* level, const char* fmt, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  time_t t = time(nullptr);
-  struct tm tm;
-  localtime_r(&t, &tm);
-  char ts[32];
-  strftime(ts, sizeof ts, "%Y-%m-%d %H:%M:%S", &tm);
-  fprintf(stderr, "%s %d %-5s [jubaclassifier.cpp] %s\n", ts, (int)getpid(), level, buf);
-}
-
-// ------------------------------------------------------------------ argv
-struct Args {
-  int port = 9199;
-  std::string listen_addr, listen_if, bind = "0.0.0.0", eth;
-  int threads = 2, timeout = 10, zk_timeout = 10, ic_timeout = 10;
-  bool daemon = false, version = false, cpu = false;
-  bool native_check = false;   // print whether the config is served natively, exit
-  std::string logdir, log_config, datadir = "/tmp", configpath, model_file, zookeeper, name,
-      mixer = "linear_mixer";
-  int interval_sec = 16, interval_count = 512;
-  int gpu = -1;
-};
-
-std::string real_path(const std::string& p) {
-  char buf[PATH_MAX];
-  return realpath(p.c_str(), buf) ? std::string(buf) : p;
-}
-
-std::string default_v4() {
-  std::string out = "127.0.0.1";
-  struct ifaddrs* ifa = nullptr;
-  if (getifaddrs(&ifa) != 0) return out;
-  for (auto* p = ifa; p; p = p->ifa_next) {
-    if (!p->ifa_addr || p->ifa_addr->sa_family != AF_INET) continue;
-    char b[INET_ADDRSTRLEN];
-    inet_ntop(AF_INET, &((struct sockaddr_in*)p->ifa_addr)->sin_addr, b, sizeof b);
-    if (strncmp(b, "127.", 4) != 0) { out = b; break; }
-  }
-  freeifaddrs(ifa);
-  return out;
-}
-
-std::string if_v4(const std::string& nic) {
-  std::string out;
-  struct ifaddrs* ifa = nullptr;
-  if (getifaddrs(&ifa) != 0) return out;
-  for (auto* p = ifa; p; p = p->ifa_next)
-    if (p->ifa_addr && p->ifa_addr->sa_family == AF_INET && nic == p->ifa_name) {
-      char b[INET_ADDRSTRLEN];
-      inet_ntop(AF_INET, &((struct sockaddr_in*)p->ifa_addr)->sin_addr, b, sizeof b);
-      out = b;
-      break;
-    }
-  freeifaddrs(ifa);
-  return out;
-}
-
-std::string user_name() {
-  struct passwd* pw = getpwuid(getuid());
-  return pw ? std::string(pw->pw_name) : std::to_string(getuid());
-}
-
-const char* const kUsage =
-    "usage: jubaclassifier [-p port] [-b listen_addr] [-B listen_if] [-c thread] [-t timeout]\n"
-    "                      [-d datadir] [-l logdir] [-g log_config] [-f configpath]\n"
-    "                      [-m model_file] [-z zookeeper] [-n name] [-x mixer] [-s interval_sec]\n"
-    "                      [-i interval_count] [-Z zookeeper_timeout] [-I interconnect_timeout]\n"
-    "                      [-D] [-v] [--gpu N] [--cpu]\n";
-
-// 0 ok, >0 exit code
-int parse_args(int argc, char** argv, Args* a) {
-  static const struct option opts[] = {
-      {"rpc-port", required_argument, nullptr, 'p'}, {"listen_addr", required_argument, nullptr, 'b'},
-      {"listen_if", required_argument, nullptr, 'B'}, {"thread", required_argument, nullptr, 'c'},
-      {"timeout", required_argument, nullptr, 't'}, {"zookeeper_timeout", required_argument, nullptr, 'Z'},
-      {"interconnect_timeout", required_argument, nullptr, 'I'}, {"daemon", no_argument, nullptr, 'D'},
-      {"logdir", required_argument, nullptr, 'l'}, {"log_config", required_argument, nullptr, 'g'},
-      {"version", no_argument, nullptr, 'v'}, {"datadir", required_argument, nullptr, 'd'},
-      {"configpath", required_argument, nullptr, 'f'}, {"model_file", required_argument, nullptr, 'm'},
-      {"zookeeper", required_argument, nullptr, 'z'}, {"name", required_argument, nullptr, 'n'},
-      {"mixer", required_argument, nullptr, 'x'}, {"interval_sec", required_argument, nullptr, 's'},
-      {"interval_count", required_argument, nullptr, 'i'}, {"gpu", required_argument, nullptr, 1000},
-      {"cpu", no_argument, nullptr, 1001}, {"help", no_argument, nullptr, 'h'},
-      {"native-check", no_argument, nullptr, 1002},
-      {nullptr, 0, nullptr, 0}};
-  auto num = [](const char* s, long lo, long hi, int* out) {
-    char* e = nullptr;
-    long v = strtol(s, &e, 10);
-    if (!*s || *e || v < lo || v > hi) return false;
-    *out = (int)v;
-    return true;
-  };
-  int c;
-  optind = 1;
-  while ((c = getopt_long(argc, argv, "p:b:B:c:t:Z:I:Dl:g:vd:f:m:z:n:x:s:i:h", opts, nullptr)) != -1) {
-    bool ok = true;
-    switch (c) {
-      case 'p': ok = num(optarg, 1, 65535, &a->port); break;
-      case 'b': a->listen_addr = optarg; break;
-      case 'B': a->listen_if = optarg; break;
-      case 'c': ok = num(optarg, 1, INT_MAX, &a->threads); break;
-      case 't': ok = num(optarg, 0, INT_MAX, &a->timeout); break;
-      case 'Z': ok = num(optarg, INT_MIN, INT_MAX, &a->zk_timeout); break;
-      case 'I': ok = num(optarg, INT_MIN, INT_MAX, &a->ic_timeout); break;
-      case 'D': a->daemon = true; break;
-      case 'l': a->logdir = optarg; break;
-      case 'g': a->log_config = optarg; break;
-      case 'v': a->version = true; break;
-      case 'd': a->datadir = optarg; break;
-      case 'f': a->configpath = optarg; break;
-      case 'm': a->model_file = optarg; break;
-      case 'z': a->zookeeper = optarg; break;
-      case 'n': a->name = optarg; break;
-      case 'x': a->mixer = optarg; break;
-      case 's': ok = num(optarg, 0, INT_MAX, &a->interval_sec); break;
-      case 'i': ok = num(optarg, 0, INT_MAX, &a->interval_count); break;
-      case 1000: ok = num(optarg, 0, 1023, &a->gpu); break;
-      case 1001: a->cpu = true; break;
-      case 1002: a->native_check = true; break;
-      case 'h': fputs(kUsage, stdout); return -1;
-      default: ok = false;
-    }
-    if (!ok) {
-      fputs(kUsage, stderr);
-      return 2;
-    }
-  }
-  if (optind < argc) {
-    fputs(kUsage, stderr);
-    return 2;
-  }
-  return 0;
-}
-
-// ---------------------------------------------------------------- config
-struct Rules {
-  std::vector<jb::HostRule> s, n;
-  std::string blob;
-  uint64_t H = 1ull << 20;
-};
-
-int matcher_kind(const std::string& spec, std::string* arg) {
-  if (spec.empty() || spec == "*") { arg->clear(); return 0; }
-  if (spec.size() >= 2 && spec.front() == '/' && spec.back() == '/') return -1;   // regex
-  if (spec.back() == '*') { *arg = spec.substr(0, spec.size() - 1); return 1; }
-  if (spec.front() == '*') { *arg = spec.substr(1); return 2; }
-  *arg = spec;
-  return 3;
-}
-
-bool nonempty_list(const Value& conv, const char* key) {
-  const Value* v = conv.get(key);
-  return v && v->kind == Value::ARR && !v->a.empty();
-}
-
-// the fixed-slot GPU converter (fv_converter/gpu_path.py fast_eligible +
-// GpuRuleTable): false with a reason when the config needs the host converter
-bool build_rules(const Value& conv, Rules* r, std::string* why) {
-  if (conv.kind != Value::MAP) { *why = "converter is not an object"; return false; }
-  for (const char* k : {"string_filter_rules", "num_filter_rules", "binary_rules", "combination_rules"})
-    if (nonempty_list(conv, k)) { *why = std::string(k) + " need the host converter"; return false; }
-  const Value* st = conv.get("string_types");
-  const Value* nt = conv.get("num_types");
-  if (const Value* h = conv.get("hash_max_size")) {
-    if (h->kind == Value::INT && h->i > 0) r->H = (uint64_t)h->i;
-    else if (h->kind != Value::NIL) { *why = "hash_max_size"; return false; }
-  }
-  auto put = [&](const std::string& b, int32_t* off, int32_t* len) {
-    *off = (int32_t)r->blob.size();
-    *len = (int32_t)b.size();
-    r->blob += b;
-  };
-  if (const Value* sr = conv.get("string_rules")) {
-    if (sr->kind != Value::ARR) { *why = "string_rules"; return false; }
-    for (const Value& x : sr->a) {
-      const std::string type = x.str_or("type", "");
-      const std::string sw = x.str_or("sample_weight", "bin");
-      const std::string gw = x.str_or("global_weight", "bin");
-      if (type != "str" || (st && st->get("str"))) { *why = "string type " + type; return false; }
-      if (gw != "bin") { *why = "global_weight " + gw; return false; }
-      float w;
-      if (sw == "bin" || sw == "tf") w = 1.f;
-      else if (sw == "log_tf") w = logf(2.f);
-      else { *why = "sample_weight " + sw; return false; }
-      std::string arg;
-      const int kind = matcher_kind(x.str_or("key", ""), &arg);
-      if (kind < 0) { *why = "regex key matcher"; return false; }
-      jb::HostRule h{};
-      h.match_kind = kind;
-      put(arg, &h.match_off, &h.match_len);
-      put("@str#" + sw + "/" + gw, &h.suffix_off, &h.suffix_len);
-      h.weight = w;
-      r->s.push_back(h);
-    }
-  }
-  if (const Value* nr = conv.get("num_rules")) {
-    if (nr->kind != Value::ARR) { *why = "num_rules"; return false; }
-    for (const Value& x : nr->a) {
-      const std::string type = x.str_or("type", "");
-      if ((type != "num" && type != "log") || (nt && nt->get(type))) { *why = "num type " + type; return false; }
-      std::string arg;
-      const int kind = matcher_kind(x.str_or("key", ""), &arg);
-      if (kind < 0) { *why = "regex key matcher"; return false; }
-      jb::HostRule h{};
-      h.match_kind = kind;
-      put(arg, &h.match_off, &h.match_len);
-      put("@" + type, &h.suffix_off, &h.suffix_len);
-      h.value_kind = type == "log" ? 1 : 0;
-      r->n.push_back(h);
-    }
-  }
-  return true;
-}
+using namespace jb::srv;
 
 struct Config {
   std::string text;
@@ -357,122 +112,6 @@ bool parse_config(const std::string& text, Config* c, std::string* why) {
   if (!build_rules(conv ? *conv : empty, &c->rules, why)) return false;
   c->text = text;
   return true;
-}
-
-bool read_file(const std::string& path, std::string* out) {
-  FILE* f = fopen(path.c_str(), "rb");
-  if (!f) return false;
-  char buf[1 << 16];
-  size_t n;
-  out->clear();
-  while ((n = fread(buf, 1, sizeof buf, f)) > 0) out->append(buf, n);
-  fclose(f);
-  return true;
-}
-
-// ------------------------------------------------------------ model file
-// framework/save_load.py: 48-byte big-endian header, CRC32 over header[0:28]
-// ++ header[32:48] ++ system ++ user; system = [1, ts, type, id, config]
-// (old-spec raw strings), user = [1, driver pack] (bin types).
-uint64_t rd_be(const uint8_t* p, int n) {
-  uint64_t x = 0;
-  for (int k = 0; k < n; ++k) x = (x << 8) | p[k];
-  return x;
-}
-
-void wr_be(uint8_t* p, uint64_t x, int n) {
-  for (int k = n - 1; k >= 0; --k) { p[k] = (uint8_t)x; x >>= 8; }
-}
-
-struct ModelFile {
-  std::string type, id, config;
-  Value user;      // the driver pack
-  int64_t user_version = 0;
-};
-
-std::string read_model_file(const std::string& bytes, ModelFile* mf) {
-  if (bytes.size() < 48) return "failed to read header: truncated file";
-  const uint8_t* h = (const uint8_t*)bytes.data();
-  if (memcmp(h, "jubatus\0", 8) != 0) return "invalid file format";
-  if (rd_be(h + 8, 8) != 1) return "invalid format version: " + std::to_string(rd_be(h + 8, 8)) + ", expected 1";
-  const uint32_t maj = (uint32_t)rd_be(h + 16, 4), min = (uint32_t)rd_be(h + 20, 4),
-                 mnt = (uint32_t)rd_be(h + 24, 4);
-  if (maj != kVersionParts[0] || min != kVersionParts[1] || mnt != kVersionParts[2])
-    return std::string("jubatus version mismatched: current version: ") + kVersion +
-           ", saved version: " + std::to_string(maj) + "." + std::to_string(min) + "." + std::to_string(mnt);
-  const uint32_t crc = (uint32_t)rd_be(h + 28, 4);
-  const uint64_t ssz = rd_be(h + 32, 8), usz = rd_be(h + 40, 8);
-  if (bytes.size() < 48 + ssz + usz || ssz > bytes.size() || usz > bytes.size()) return "model file truncated";
-  uint32_t c = jb::crc32_update(0, h, 28);
-  c = jb::crc32_update(c, h + 32, 16);
-  c = jb::crc32_update(c, h + 48, ssz);
-  c = jb::crc32_update(c, h + 48 + ssz, usz);
-  if (c != crc) {
-    char b[96];
-    snprintf(b, sizeof b, "invalid crc32 checksum: %#x, read %#x", c, crc);
-    return b;
-  }
-  try {
-    Value sys = MsgpackReader(h + 48, ssz).read();
-    Value usr = MsgpackReader(h + 48 + ssz, usz).read();
-    if (sys.kind != Value::ARR || sys.a.size() != 5) return "invalid system data";
-    if (usr.kind != Value::ARR || usr.a.size() != 2) return "invalid user data";
-    if (sys.a[0].kind != Value::INT || sys.a[0].i != 1)
-      return "invalid system data version: saved version: " + std::to_string(sys.a[0].i) + ", expected version: 1";
-    mf->type = sys.a[2].s;
-    mf->id = sys.a[3].s;
-    mf->config = sys.a[4].s;
-    mf->user_version = usr.a[0].kind == Value::INT ? usr.a[0].i : -1;
-    mf->user = std::move(usr.a[1]);
-  } catch (const std::exception& e) {
-    return std::string("broken model data: ") + e.what();
-  }
-  return "";
-}
-
-// --------------------------------------------------------------- buffers
-template <class T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t cap = 0;
-  T* get(size_t n) {
-    if (n > cap) {
-      if (p) HIPCHK(hipFree(p));
-      size_t c = cap ? cap : 1024;
-      while (c < n) c *= 2;
-      HIPCHK(hipMalloc((void**)&p, c * sizeof(T)));
-      cap = c;
-    }
-    return p;
-  }
-};
-
-template <class T>
-struct PinBuf {   // page-locked host memory (H2D staging)
-  T* p = nullptr;
-  size_t cap = 0;
-  T* get(size_t n) {
-    if (n > cap) {
-      if (p) HIPCHK(hipHostFree(p));
-      size_t c = cap ? cap : 1024;
-      while (c < n) c *= 2;
-      HIPCHK(hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault));
-      cap = c;
-    }
-    return p;
-  }
-};
-
-uint64_t fnv1a64(const std::string& s) { return jb::fnv_bytes(jb::kFnvOffset, (const uint8_t*)s.data(), s.size()); }
-
-// element count of a body's top-level array header (-1: none)
-int64_t body_count(const uint8_t* b, uint64_t n) {
-  if (n < 1) return -1;
-  const uint8_t t = b[0];
-  if ((t & 0xf0) == 0x90) return t & 0x0f;
-  if (t == 0xdc && n >= 3) return ((int64_t)b[1] << 8) | b[2];
-  if (t == 0xdd && n >= 5) return (int64_t)rd_be(b + 1, 4);
-  return -1;
 }
 
 // ------------------------------------------------------------------ model
@@ -1276,7 +915,7 @@ class Server {
  public:
   Server(const Args& a, const Config& cfg, int device) : a_(a) {
     clf_.reset(new Classifier(cfg, device));
-    start_time_ = time(nullptr);
+    cs_.start_time = time(nullptr);
   }
 
   void load_file(const std::string& path) { load_impl(path, true); }
@@ -1312,17 +951,10 @@ class Server {
     }
     a_.port = port;
     logf_("INFO", "start listening at port %d", port);
-    start_time_ = time(nullptr);
+    cs_.start_time = time(nullptr);
     rpc_->start();
     logf_("INFO", "jubaclassifier RPC server startup (native)");
-    sigset_t set;
-    sigemptyset(&set);
-    sigaddset(&set, SIGTERM);
-    sigaddset(&set, SIGINT);
-    int sig = 0;
-    while (true) {
-      if (sigwait(&set, &sig) == 0 && (sig == SIGTERM || sig == SIGINT)) break;
-    }
+    wait_for_term();
     logf_("INFO", "stopping RPC server");
     rpc_->stop();
     return 0;
@@ -1487,65 +1119,18 @@ class Server {
     if (id.empty()) throw std::runtime_error("empty id is not allowed");
     const std::string path = local_path(id);
     logf_("INFO", "starting save to %s", path.c_str());
-    const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
-    if (fd < 0) throw std::runtime_error("cannot open output file: " + path + ": " + strerror(errno));
-    if (flock(fd, LOCK_EX | LOCK_NB) != 0) {
-      close(fd);
-      throw std::runtime_error("cannot get the lock of file; any RPC is saving to same file?: " + path);
-    }
-    MsgpackWriter sys;
-    sys.arr(5);
-    sys.uint(1);
-    sys.uint((uint64_t)time(nullptr));
-    sys.raw(std::string("classifier"));
-    sys.raw(id);
-    sys.raw(clf_->config_text());
     std::string user;
     try {
       user = clf_->pack_user_data();
     } catch (const std::exception& e) {
-      close(fd);
-      unlink(path.c_str());
       throw std::runtime_error("cannot write output file: " + path + ": " + e.what());
     }
-    uint8_t head[48];
-    memcpy(head, "jubatus\0", 8);
-    wr_be(head + 8, 1, 8);
-    for (int k = 0; k < 3; ++k) wr_be(head + 16 + 4 * k, kVersionParts[k], 4);
-    wr_be(head + 28, 0, 4);
-    wr_be(head + 32, sys.out.size(), 8);
-    wr_be(head + 40, user.size(), 8);
-    uint32_t c = jb::crc32_update(0, head, 28);
-    c = jb::crc32_update(c, head + 32, 16);
-    c = jb::crc32_update(c, (const uint8_t*)sys.out.data(), sys.out.size());
-    c = jb::crc32_update(c, (const uint8_t*)user.data(), user.size());
-    wr_be(head + 28, c, 4);
-    bool ok = write_all(fd, head, 48) && write_all(fd, sys.out.data(), sys.out.size()) &&
-              write_all(fd, user.data(), user.size());
-    close(fd);
-    if (!ok) {
-      unlink(path.c_str());
-      throw std::runtime_error("cannot write output file: " + path);
-    }
+    write_model_file(path, "classifier", id, clf_->config_text(), user);
     std::lock_guard<std::mutex> g(st_mu_);
-    last_saved_ = time(nullptr);
-    last_saved_path_ = path;
+    cs_.last_saved = time(nullptr);
+    cs_.last_saved_path = path;
     logf_("INFO", "saved to %s", path.c_str());
     return path;
-  }
-
-  static bool write_all(int fd, const void* p, size_t n) {
-    const char* c = (const char*)p;
-    while (n) {
-      ssize_t w = write(fd, c, n);
-      if (w <= 0) {
-        if (w < 0 && errno == EINTR) continue;
-        return false;
-      }
-      c += w;
-      n -= (size_t)w;
-    }
-    return true;
   }
 
   void load_impl(const std::string& path, bool overwrite_config) {
@@ -1572,50 +1157,19 @@ class Server {
     }
     clf_->unpack(mf.user);
     std::lock_guard<std::mutex> g(st_mu_);
-    last_loaded_ = time(nullptr);
-    last_loaded_path_ = path;
+    cs_.last_loaded = time(nullptr);
+    cs_.last_loaded_path = path;
     logf_("INFO", "loaded from %s", path.c_str());
   }
 
   void status(MsgpackWriter* w) {
     std::vector<std::pair<std::string, std::string>> st;
-    const time_t now = time(nullptr);
-    long vsz = 0, rss = 0, shr = 0;
-    if (FILE* f = fopen("/proc/self/statm", "r")) {
-      if (fscanf(f, "%ld %ld %ld", &vsz, &rss, &shr) != 3) vsz = rss = shr = 0;
-      fclose(f);
-    }
-    const long kb = sysconf(_SC_PAGESIZE) / 1024;
-    auto add = [&](const char* k, const std::string& v) { st.emplace_back(k, v); };
-    add("clock_time", std::to_string(now));
-    add("start_time", std::to_string(start_time_));
-    add("uptime", std::to_string(now - start_time_));
-    add("VIRT", std::to_string(vsz * kb));
-    add("RSS", std::to_string(rss * kb));
-    add("SHR", std::to_string(shr * kb));
-    add("timeout", std::to_string(a_.timeout));
-    add("threadnum", std::to_string(a_.threads));
-    add("datadir", a_.datadir);
-    add("is_standalone", "1");
-    add("VERSION", kVersion);
-    add("PROGNAME", "jubaclassifier");
-    add("type", "classifier");
-    add("logdir", a_.logdir);
-    add("log_config", a_.log_config);
-    add("configpath", a_.configpath);
-    add("pid", std::to_string(getpid()));
-    add("user", user_name());
-    add("update_count", std::to_string(clf_->update_count.load()));
     {
       std::lock_guard<std::mutex> g(st_mu_);
-      add("last_saved", std::to_string(last_saved_));
-      add("last_saved_path", last_saved_path_);
-      add("last_loaded", std::to_string(last_loaded_));
-      add("last_loaded_path", last_loaded_path_);
+      common_status(a_, cs_, clf_->update_count.load(), &st);
     }
-    add("gpu", a_.gpu >= 0 ? std::to_string(a_.gpu) : std::string());
     clf_->status(&st);
-    if (rpc_) add("rpc.batches", std::to_string(rpc_->batches()));
+    if (rpc_) st.emplace_back("rpc.batches", std::to_string(rpc_->batches()));
     w->map(1);
     w->raw(ident());
     w->map(st.size());
@@ -1626,117 +1180,26 @@ class Server {
   std::unique_ptr<Classifier> clf_;
   std::unique_ptr<jb::RpcServer> rpc_;
   std::vector<uint8_t*> slots_;
-  time_t start_time_ = 0;
   std::mutex st_mu_;
-  time_t last_saved_ = 0, last_loaded_ = 0;
-  std::string last_saved_path_, last_loaded_path_;
+  CommonStatus cs_;
 };
-
-// hand the server to the Python implementation (before any HIP call)
-[[noreturn]] void exec_python(int argc, char** argv, const char* why) {
-  fprintf(stderr, "jubaclassifier: %s: starting the Python server\n", why);
-  char exe[PATH_MAX];
-  ssize_t n = readlink("/proc/self/exe", exe, sizeof exe - 1);
-  std::string root = ".";
-  if (n > 0) {
-    exe[n] = 0;
-    std::string p(exe);   // <root>/jubatus_amd/native_bin/jubaclassifier
-    for (int k = 0; k < 3; ++k) p = p.substr(0, p.rfind('/'));
-    root = p;
-  }
-  const char* pp = getenv("PYTHONPATH");
-  std::string path = root + (pp && *pp ? std::string(":") + pp : std::string());
-  setenv("PYTHONPATH", path.c_str(), 1);
-  std::vector<char*> av;
-  static char py[] = "python3", m[] = "-m", mod[] = "jubatus_amd.cmd.server", eng[] = "classifier";
-  av.push_back(py);
-  av.push_back(m);
-  av.push_back(mod);
-  av.push_back(eng);
-  for (int k = 1; k < argc; ++k) av.push_back(argv[k]);
-  av.push_back(nullptr);
-  execvp("python3", av.data());
-  perror("execvp python3");
-  _exit(127);
-}
 
 }  // namespace
 
 int main(int argc, char** argv) {
+  set_engine("classifier");
   Args a;
-  int rc = parse_args(argc, argv, &a);
-  if (rc == -1) return 0;
-  if (rc) return rc;
-  if (a.version) {
-    printf("jubatus-%s (mi355x, native)\n", kVersion);
-    return 0;
-  }
-  const char* force = a.native_check ? nullptr : getenv("JUBATUS_NATIVE_SERVER");
-  if (force && strcmp(force, "0") == 0) exec_python(argc, argv, "JUBATUS_NATIVE_SERVER=0");
-  if (!a.native_check) {
-    if (!a.zookeeper.empty()) exec_python(argc, argv, "distributed mode");
-    if (a.cpu || getenv("JUBATUS_FORCE_CPU")) exec_python(argc, argv, "host backend requested");
-    if (access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
-  }
-  if (a.configpath.empty() && a.model_file.empty()) {
-    fprintf(stderr, "config path or model file must be specified for standalone mode\n%s", kUsage);
-    return 1;
-  }
-  if (!a.configpath.empty()) a.configpath = real_path(a.configpath);
-  if (!a.model_file.empty()) a.model_file = real_path(a.model_file);
-  if (!a.datadir.empty()) {
-    a.datadir = real_path(a.datadir);
-    if (access(a.datadir.c_str(), W_OK) != 0) {
-      fprintf(stderr, "can't use datadir: %s\n%s", a.datadir.c_str(), kUsage);
-      return 1;
-    }
-  }
-  if (!a.listen_addr.empty()) {
-    a.bind = a.eth = a.listen_addr;
-  } else if (!a.listen_if.empty()) {
-    a.bind = a.eth = if_v4(a.listen_if);
-  } else {
-    a.eth = default_v4();
-  }
-  // the configuration this process will serve: the model file's (it wins
-  // over -f, server_helper.hpp) or the config file
   std::string text;
-  if (!a.model_file.empty()) {
-    std::string bytes;
-    ModelFile mf;
-    if (!read_file(a.model_file, &bytes)) exec_python(argc, argv, "unreadable model file");
-    if (!read_model_file(bytes, &mf).empty()) exec_python(argc, argv, "model file check");
-    text = mf.config;
-  } else if (!read_file(a.configpath, &text)) {
-    exec_python(argc, argv, "unreadable config file");
-  }
   Config cfg;
-  std::string why;
-  if (a.native_check) {   // the config check alone (tests, operators): no GPU, no exec
-    const bool ok = parse_config(text, &cfg, &why);
-    printf("%s\n", ok ? "native" : ("python: " + why).c_str());
-    return 0;
-  }
-  if (!parse_config(text, &cfg, &why)) exec_python(argc, argv, why.c_str());
+  const int rc = startup(argc, argv, &a, &text, [&cfg](const std::string& t, std::string* why) {
+    return parse_config(t, &cfg, why);
+  });
+  if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
-  int device = a.gpu;
-  if (device < 0) {
-    const char* lr = getenv("LOCAL_RANK");
-    device = lr ? atoi(lr) : 0;
-  }
-  sigset_t set;
-  sigemptyset(&set);
-  sigaddset(&set, SIGTERM);
-  sigaddset(&set, SIGINT);
-  pthread_sigmask(SIG_BLOCK, &set, nullptr);   // every thread inherits it; main sigwaits
-  signal(SIGPIPE, SIG_IGN);
-  logf_("INFO", "starting jubaclassifier %s RPC server at %s:%d (native, device %d)", kVersion,
-        a.eth.c_str(), a.port, device);
   try {
-    int ndev = 0;
-    HIPCHK(hipGetDeviceCount(&ndev));
-    if (ndev <= 0) throw std::runtime_error("no HIP device");
-    device %= ndev;
+    const int device = device_and_signals(a);
+    logf_("INFO", "starting jubaclassifier %s RPC server at %s:%d (native, device %d)", kVersion,
+          a.eth.c_str(), a.port, device);
     Server srv(a, cfg, device);
     if (!a.model_file.empty()) srv.load_file(a.model_file);
     logf_("INFO", "config loaded: %s", kMethods[cfg.method]);

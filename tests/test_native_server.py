@@ -13,6 +13,7 @@ from helpers import ROOT, config_path
 from jubatus_amd.common.mprpc import RpcClient, RpcIOError, RpcTimeoutError
 
 BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaclassifier")
+REG_BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaregression")
 
 NATIVE = ["arow.json", "cw.json", "nherd.json", "pa.json", "pa1.json", "pa2.json", "perceptron.json"]
 PYTHON = {"arow_combinational_feature.json": "combination_rules", "cosine.json": "not a linear method",
@@ -20,8 +21,8 @@ PYTHON = {"arow_combinational_feature.json": "combination_rules", "cosine.json":
           "euclidean.json": "not a linear method"}
 
 
-def _check(cfg_file):
-    r = subprocess.run([BIN, "--native-check", "-f", cfg_file], capture_output=True, text=True,
+def _check(cfg_file, binary=BIN):
+    r = subprocess.run([binary, "--native-check", "-f", cfg_file], capture_output=True, text=True,
                        timeout=30)
     assert r.returncode == 0, r.stderr
     return r.stdout.strip()
@@ -55,6 +56,22 @@ def test_config_details(tmp_path, cfg, why):
     p.write_text(json.dumps(cfg))
     out = _check(str(p))
     assert why in out, out
+
+
+@pytest.mark.parametrize("name,want", [("pa.json", "native"), ("default.json", "python: string type"),
+                                       ("pa_combinational_feature.json", "python: combination_rules")])
+def test_regression_configs(name, want):
+    assert _check(config_path(f"regression/{name}"), REG_BIN).startswith(want)
+
+
+def test_regression_parameter_checks(tmp_path):
+    import json
+    p = tmp_path / "r.json"
+    p.write_text(json.dumps({"method": "PA", "parameter": {"sensitivity": -1},
+                             "converter": {"num_rules": [{"key": "*", "type": "num"}]}}))
+    assert "sensitivity" in _check(str(p), REG_BIN)
+    p.write_text(json.dumps({"method": "NN", "converter": {}}))
+    assert "not PA" in _check(str(p), REG_BIN)
 
 
 def test_version():

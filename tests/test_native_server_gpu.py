@@ -222,3 +222,80 @@ def test_native_model_files_interoperate_with_python(native, tmp_path):
             assert abs(g[k] - w[k]) <= 1e-5 * max(1.0, abs(w[k]))
     assert c.get_labels() == ora2.get_labels()
     c.close()
+
+
+# ------------------------------------------------------------------ regression
+REG_BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaregression")
+
+
+def _reg_data(rng, n):
+    out = []
+    for _ in range(n):
+        x = rng.random() * 4
+        out.append((3.0 * x + 1.0 + rng.gauss(0, 0.1), Datum({"x": x, "c": f"k{rng.randrange(5)}"})))
+    return out
+
+
+def test_native_regression_matches_oracle_and_files(tmp_path):
+    """native jubaregression: sequential requests equal the host oracle
+    (models/regression.py train_one), model files shared with the Python
+    driver, status and clear"""
+    from jubatus_amd.client import Regression
+    from jubatus_amd.framework import save_load
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.regression import PARegression
+    cfg_file = config_path("regression/pa.json")
+    cfg = json.load(open(cfg_file))
+    port = _free_port()
+    p = subprocess.Popen([REG_BIN, "-p", str(port), "-b", "127.0.0.1", "-f", cfg_file, "-d", str(tmp_path)],
+                         stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    try:
+        deadline = time.time() + 60
+        while True:
+            try:
+                with RpcClient("127.0.0.1", port, 5.0) as c:
+                    c.call("get_config", "")
+                break
+            except (OSError, RpcIOError, RpcTimeoutError):
+                assert p.poll() is None and time.time() < deadline, p.stdout.read()
+                time.sleep(0.2)
+        c = Regression("127.0.0.1", port, "", timeout=60)
+        ora = PARegression("PA", cfg.get("parameter"), DatumToFvConverter(cfg["converter"]), device=None)
+        rng = random.Random(4)
+        for _ in range(5):
+            chunk = _reg_data(rng, 40)
+            assert c.train(chunk) == 40
+            ora.train([(s, d) for s, d in chunk])
+        test = [d for _, d in _reg_data(random.Random(8), 30)]
+        got = c.estimate(test)
+        want = ora.estimate(test)
+        np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-4)
+        (ident, st), = c.get_status().items()
+        assert st["server_runtime"] == "native" and st["is_standalone"] == "1"
+        assert int(st["train.samples_trained"]) == 200
+        with RpcClient("127.0.0.1", port, 10.0) as rc:
+            with pytest.raises(RpcTypeError):
+                rc.call("train", "", [[True, [[], [["x", 1.0]], []]]])
+        (_, path), = c.save("r1").items()
+        with open(path, "rb") as f:
+            _, pack = save_load.load_server(f, "regression", open(cfg_file).read(), 1, False)
+        ora2 = PARegression("PA", cfg.get("parameter"), DatumToFvConverter(cfg["converter"]), device=None)
+        ora2.unpack(pack)
+        np.testing.assert_allclose(ora2.estimate(test), got, rtol=1e-6, atol=1e-6)
+        assert c.clear() is True
+        assert all(v == 0.0 for v in c.estimate(test))
+        assert c.load("r1") is True
+        np.testing.assert_allclose(c.estimate(test), got, rtol=1e-6, atol=1e-6)
+        # Python-written file -> native
+        p2 = os.path.join(str(tmp_path), f"{ident}_regression_py.jubatus")
+        with open(p2, "wb") as f:
+            save_load.save_server(f, "regression", "py", open(cfg_file).read(), 1, ora.pack())
+        assert c.load("py") is True
+        np.testing.assert_allclose(c.estimate(test), want, rtol=1e-4, atol=1e-4)
+        c.close()
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
