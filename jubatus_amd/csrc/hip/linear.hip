@@ -640,6 +640,8 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     bool upd = false;
     int lstar = -1;
     float dwy = 0.f, dwl = 0.f, dpy = 0.f, dpl = 0.f, py = 1.f, pl = 1.f, wy = 0.f, wl = 0.f;
+    float tau_s = 0.f;
+    bool ser = false, p_done = false;   // serialized confidence (atomic mode), P applied
     const bool mine = lane < n_s && idx_s >= 0;
     if (valid_s) ++n_valid;
     if (general_s) {
@@ -712,6 +714,36 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
           dpl = lstar >= 0 ? dprec(method, beta, x_s, b) : 0.f;
         }
       }
+      // Serialized confidence (concurrent atomic streams, confidence methods):
+      // the precision increment goes first with a returning atomic, and the W
+      // step uses the variance 1/P at this update's place in the atomic order
+      // of the row instead of the value gathered before the sample. Streams
+      // that update a shared row at the same time then shrink each other's
+      // steps as sequential updates would (without it, ~1000 streams sharing a
+      // row all step with the same stale confidence and the weights grow
+      // ~40x past the serial model's, profiles/r02_concurrent_vs_serial.jsonl).
+      // One stream is unaffected: its returned P is the value it gathered.
+      // Rows repeated inside the sample keep the gathered value (the
+      // reference applies a sample's features against the pre-sample state).
+      // Cost: one returning atomic per updated feature on the sample chain;
+      // the worst case (every sample updates) runs ~10% slower end to end,
+      // data with few updates is unchanged (profiles/r02_serialized_confidence.jsonl).
+      if (MODE == kAtomic && use_s && upd) {
+        bool dup = false;
+        for (int j = 0; j < n_s; ++j) {
+          const int32_t ij = __builtin_amdgcn_readlane(idx_s, j);
+          dup |= mine && j != lane && ij == idx_s;
+        }
+        tau_s = tau;
+        ser = mine && !dup;
+        // (rows of the hot-row replica are serialized in LDS at apply time)
+        if (ser && !(HOT && hs_s >= 0)) {
+          const int64_t row = (int64_t)idx_s * LC;
+          dwy = tau * x_s / atomicAdd(P + row + y_s, dpy);
+          if (lstar >= 0) dwl = -tau * x_s / atomicAdd(P + row + lstar, dpl);
+          p_done = true;
+        }
+      }
     }
     // 4. stage s+1 and forward s's own increments into it: lane k (feature k
     //    of s+1) scans s's features through readlane (registers only)
@@ -774,26 +806,28 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     if (upd && mine && !skip) {
       if (HOT && hs_s >= 0) {
         const int hb = hs_s * LC;
+        if (use_s) {   // precision first: its returned value serializes the W step
+          const float p0 = atomicAdd(&hV[1][hb + y_s], dpy);
+          atomicAdd(&hA[1][hb + y_s], dpy);
+          if (MODE == kAtomic && ser) dwy = tau_s * x_s / p0;
+          if (lstar >= 0) {
+            const float q0 = atomicAdd(&hV[1][hb + lstar], dpl);
+            atomicAdd(&hA[1][hb + lstar], dpl);
+            if (MODE == kAtomic && ser) dwl = -tau_s * x_s / q0;
+          }
+        }
         atomicAdd(&hV[0][hb + y_s], dwy);
         atomicAdd(&hA[0][hb + y_s], dwy);
         if (lstar >= 0) {
           atomicAdd(&hV[0][hb + lstar], dwl);
           atomicAdd(&hA[0][hb + lstar], dwl);
         }
-        if (use_s) {
-          atomicAdd(&hV[1][hb + y_s], dpy);
-          atomicAdd(&hA[1][hb + y_s], dpy);
-          if (lstar >= 0) {
-            atomicAdd(&hV[1][hb + lstar], dpl);
-            atomicAdd(&hA[1][hb + lstar], dpl);
-          }
-        }
       } else {
         const int64_t row = (int64_t)idx_s * LC;
         if (MODE == kAtomic) {
           atomicAdd(W + row + y_s, dwy);
           if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
-          if (use_s) {
+          if (use_s && !p_done) {
             atomicAdd(P + row + y_s, dpy);
             if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
           }

@@ -364,12 +364,13 @@ def test_concurrent_deviation_from_serial_order(hot, monkeypatch, capsys):
     """1020 concurrent atomic streams (one per request, the served batch
     shape) against the same requests applied one after another on the
     host oracle. Step i of every stream reads the model as the streams left
-    it at step i-1, so a row that all streams carry receives ~1000 AROW
-    steps computed from the same confidence: the concurrent weights grow
-    far larger than the serial ones (measured ~35-45x in norm on this data,
-    profiles/r02_concurrent_vs_serial.jsonl), while the decisions agree on
-    ~97% of held-out datums and accuracy drops ~1 point. Bounded here: the
-    predictions, the accuracy and that every sample was trained once."""
+    it at step i-1; without the serialized confidence of csrc/hip/linear.hip
+    a row that all streams carry took ~1000 AROW steps computed from the
+    same confidence and the weights grew 35-45x past the serial ones
+    (profiles/r02_concurrent_vs_serial.jsonl). With it the weight distance
+    is ~1.3x the serial norm (hot-row replica: ~12x, its blocks see each
+    other's confidence one sample late), the decisions agree on ~98% of
+    held-out datums and accuracy is within ~0.5 point."""
     from jubatus_amd.fv_converter.datum import Datum
     from jubatus_amd.models.classifier import LinearClassifier
 
@@ -402,8 +403,8 @@ def test_concurrent_deviation_from_serial_order(hot, monkeypatch, capsys):
     with capsys.disabled():
         print(f"\nconcurrent vs serial (hot={hot}): rel W diff {rel:.3f}, agreement {agree:.3f}, "
               f"acc {acc_g:.3f} vs {acc_c:.3f}")
-    assert agree >= 0.95, agree
-    assert acc_g >= acc_c - 0.025, (acc_g, acc_c)
-    assert np.isfinite(rel)
+    assert agree >= 0.96, agree
+    assert acc_g >= acc_c - 0.015, (acc_g, acc_c)
+    assert rel <= (25.0 if hot else 3.0), rel
     st = g.train_stats()
     assert st["trained"] == len(data)
