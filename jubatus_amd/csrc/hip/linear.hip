@@ -318,7 +318,7 @@ struct HotMerge {
 
   template <int E>
   __device__ __forceinline__ void finish(bool use_s, int nent, float (*hV)[E], float (*hB)[E],
-                                         int wv, int lane) {
+                                         float* hD, int wv, int lane) {
     if (!pending) return;
 #pragma unroll
     for (int k = 0; k < KQ; ++k) {
@@ -329,7 +329,9 @@ struct HotMerge {
         float S = own[k] + d[k];
 #pragma unroll
         for (int j = 0; j < kRep - 1; ++j) S += oth[k][j];
-        atomicAdd(&hV[t][e], S - hB[t][e] - d[k]);
+        const float others = S - hB[t][e] - d[k];
+        atomicAdd(&hV[t][e], others);
+        if (t == 1) hD[e] = others;     // the other blocks' precision growth per merge
         hB[t][e] = S;
       }
     }
@@ -513,6 +515,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
   __shared__ float hV[2][HE];
   __shared__ float hA[2][HE];
   __shared__ float hB[2][HE];
+  __shared__ float hD[HE];
   __shared__ int32_t hK[HK];
   __shared__ int32_t hS[HK];
   __shared__ int32_t hR[HR];
@@ -548,6 +551,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
         hV[t][e] = ld_agent((t == 0 ? W : P) + a) + S;
         hB[t][e] = S;
         hA[t][e] = 0.f;
+        if (t == 1) hD[e] = 0.f;
       }
     }
     __syncthreads();
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     if constexpr (HOT) {
       if (nent > 0 && ++since_merge >= merge_every) {
         since_merge = 0;
-        mrg.template finish<HE>(use_s, nent, hV, hB, wv, lane);
+        mrg.template finish<HE>(use_s, nent, hV, hB, hD, wv, lane);
         mrg.template issue<HE>(hot_rep, rr, use_s, nent, hA, wv, lane);
       }
     }
@@ -807,13 +811,16 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
       if (HOT && hs_s >= 0) {
         const int hb = hs_s * LC;
         if (use_s) {   // precision first: its returned value serializes the W step
+          // inside the block; the other blocks' updates of this sample arrive
+          // a merge later, so their expected growth (the last merge's) counts
+          // half: this update's mean place among them
           const float p0 = atomicAdd(&hV[1][hb + y_s], dpy);
           atomicAdd(&hA[1][hb + y_s], dpy);
-          if (MODE == kAtomic && ser) dwy = tau_s * x_s / p0;
+          if (MODE == kAtomic && ser) dwy = tau_s * x_s / (p0 + 0.5f * hD[hb + y_s]);
           if (lstar >= 0) {
             const float q0 = atomicAdd(&hV[1][hb + lstar], dpl);
             atomicAdd(&hA[1][hb + lstar], dpl);
-            if (MODE == kAtomic && ser) dwl = -tau_s * x_s / q0;
+            if (MODE == kAtomic && ser) dwl = -tau_s * x_s / (q0 + 0.5f * hD[hb + lstar]);
           }
         }
         atomicAdd(&hV[0][hb + y_s], dwy);
@@ -856,7 +863,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     idx_s = idx1; x_s = x1; n_s = n1; y_s = y1; hs_s = hs1;
     idx1 = idx2; x1 = x2; n1 = n2; y1 = y2; hs1 = hs2;
   }
-  if constexpr (HOT) mrg.template finish<HE>(use_s, nent, hV, hB, wv, lane);
+  if constexpr (HOT) mrg.template finish<HE>(use_s, nent, hV, hB, hD, wv, lane);
   }  // s_beg < s_end
   if (stats != nullptr && lane == 0 && n_valid > 0) {
     atomicAdd(stats, (unsigned long long)n_upd);
