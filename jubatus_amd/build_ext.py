@@ -163,7 +163,11 @@ SERVERS = {
                        ["server", "native", "hip"]),
     "jubaregression": (["server/jubaregression.cpp", "native/jb_rpc.cpp"],
                        ["server", "native", "hip"]),
+    # host engines: no GPU, no HIP libraries
+    "jubastat": (["server/jubastat.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }
+HOST_SERVERS = {"jubastat", "jubabandit"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:
@@ -175,12 +179,13 @@ def build_servers(force: bool = False, nproc: int = 8) -> str:
         target = os.path.join(NATIVE_BIN, name)
         paths = [os.path.join(CSRC, x) for x in srcs]
         deps = paths + [HIP_SO] + [h for d in incs for h in glob.glob(os.path.join(CSRC, d, "*.h*"))]
+        libs = [] if name in HOST_SERVERS else [
+            f"-L{PKG}", "-ljubatus_hip", "-L/opt/rocm/lib", "-lamdhip64",
+            "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,/opt/rocm/lib"]
         if force or _newer(target, deps):
             jobs.append((target, ["g++", "-O2", "-std=c++17", "-pthread", "-Wall",
                                   "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
-                                  *[f"-I{os.path.join(CSRC, d)}" for d in incs], *paths,
-                                  f"-L{PKG}", "-ljubatus_hip", "-L/opt/rocm/lib", "-lamdhip64",
-                                  "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,/opt/rocm/lib",
+                                  *[f"-I{os.path.join(CSRC, d)}" for d in incs], *paths, *libs,
                                   "-o", target]))
     _compile_all(jobs, nproc)
     return NATIVE_BIN

@@ -1,0 +1,252 @@
+// RPC shell of the native host-engine servers (jubastat, jubabandit): the
+// engines whose state is small per-key bookkeeping and stays on the host
+// (SURVEY K14), served without Python. Reference: the generated
+// <engine>_impl.cpp RPC tables and framework/server_base.cpp (save / load /
+// get_status); the lock discipline of server_helper.hpp:296-303 (update =
+// write lock, analysis = read lock) is a reader/writer mutex here.
+//
+// An engine supplies its methods (name, arity incl. the cluster name, update
+// or analysis, handler writing the result), pack / unpack of its model
+// payload (the same msgpack maps as the Python drivers, so model files move
+// between the two servers) and its status keys.
+#pragma once
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "jb_rpc.hpp"
+#include "jb_server_common.hpp"
+#include "jb_value.hpp"
+
+namespace jb {
+namespace srv {
+
+struct HostMethod {
+  std::string name;
+  size_t arity;        // including the leading cluster name
+  bool update;         // write lock + update_count
+  std::function<void(const std::vector<Value>&, MsgpackWriter*)> fn;
+};
+
+class HostEngine {
+ public:
+  virtual ~HostEngine() = default;
+  virtual std::vector<HostMethod> methods() = 0;
+  virtual std::string pack() = 0;                 // msgpack of the driver pack (bin types)
+  virtual void unpack(const Value& obj) = 0;
+  virtual void clear() = 0;
+  virtual void status(std::vector<std::pair<std::string, std::string>>* st) = 0;
+};
+
+// a method error reported to the client as the message string
+struct EngineError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+class HostServer {
+ public:
+  // make(config text) -> engine, or throws (the config is validated first)
+  using Factory = std::function<std::unique_ptr<HostEngine>(const std::string&)>;
+
+  HostServer(const Args& a, const std::string& config, Factory make)
+      : a_(a), config_(config), make_(std::move(make)) {
+    eng_ = make_(config_);
+    for (auto& m : eng_->methods()) table_.push_back(m);
+  }
+
+  void load_file(const std::string& path) { load_impl(path, true); }
+
+  int run() {
+    rpc_.reset(new jb::RpcServer([this](const jb::RpcRequest& r) { return dispatch(r); }, a_.threads, 0.0));
+    rpc_->set_io_threads(std::max(1, a_.threads / 4));
+    int port;
+    try {
+      port = rpc_->listen(a_.bind, a_.port);
+    } catch (const std::exception& e) {
+      logf_("FATAL", "server failed to start: any process using port %d? (%s)", a_.port, e.what());
+      return 1;
+    }
+    a_.port = port;
+    logf_("INFO", "start listening at port %d", port);
+    cs_.start_time = time(nullptr);
+    rpc_->start();
+    logf_("INFO", "%s RPC server startup (native)", prog_name());
+    wait_for_term();
+    logf_("INFO", "stopping RPC server");
+    rpc_->stop();
+    return 0;
+  }
+
+ private:
+  std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
+  std::string local_path(const std::string& id) const {
+    return a_.datadir + "/" + a_.eth + "_" + std::to_string(a_.port) + "_" + engine_name() + "_" + id +
+           ".jubatus";
+  }
+
+  std::string dispatch(const jb::RpcRequest& r) {
+    Value args;
+    try {
+      args = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
+    } catch (const std::exception&) {
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    }
+    if (args.kind != Value::ARR) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    MsgpackWriter w;
+    try {
+      const std::string& m = r.method;
+      if (m == "get_config" || m == "get_status" || m == "save" || m == "load") {
+        const size_t want = (m == "save" || m == "load") ? 2 : 1;
+        if (args.a.size() != want || (want == 2 && !args.a[1].is_str()))
+          return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+        common(m, args, &w);
+      } else {
+        const HostMethod* hm = nullptr;
+        for (const auto& x : table_)
+          if (x.name == m) hm = &x;
+        if (!hm) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
+        if (args.a.size() != hm->arity)
+          return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+        std::vector<Value> rest(args.a.begin() + 1, args.a.end());
+        if (hm->update) {
+          std::unique_lock<std::shared_mutex> g(model_mu_);
+          update_count_ += 1;
+          hm->fn(rest, &w);
+        } else {
+          std::shared_lock<std::shared_mutex> g(model_mu_);
+          hm->fn(rest, &w);
+        }
+      }
+    } catch (const std::invalid_argument&) {
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    } catch (const std::exception& e) {
+      return r.notify ? std::string() : jb::val::response_msg(r.msgid, e.what());
+    }
+    return r.notify ? std::string() : jb::val::response_ok(r.msgid, w.out);
+  }
+
+  void common(const std::string& m, const Value& args, MsgpackWriter* w) {
+    if (m == "get_config") {
+      w->raw(config_);
+    } else if (m == "get_status") {
+      std::vector<std::pair<std::string, std::string>> st;
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        common_status(a_, cs_, update_count_, &st);
+      }
+      st.emplace_back("server_runtime", "native");
+      {
+        std::shared_lock<std::shared_mutex> g(model_mu_);
+        eng_->status(&st);
+      }
+      w->map(1);
+      w->raw(ident());
+      w->map(st.size());
+      for (auto& kv : st) { w->raw(kv.first); w->raw(kv.second); }
+    } else if (m == "save") {
+      const std::string& id = args.a[1].s;
+      if (id.empty()) throw std::runtime_error("empty id is not allowed");
+      const std::string path = local_path(id);
+      std::string user;
+      {
+        std::shared_lock<std::shared_mutex> g(model_mu_);
+        user = eng_->pack();
+      }
+      write_model_file(path, engine_name(), id, config_, user);
+      {
+        std::lock_guard<std::mutex> g(st_mu_);
+        cs_.last_saved = time(nullptr);
+        cs_.last_saved_path = path;
+      }
+      logf_("INFO", "saved to %s", path.c_str());
+      w->map(1);
+      w->raw(ident());
+      w->raw(path);
+    } else {   // load
+      if (args.a[1].s.empty()) throw std::runtime_error("empty id is not allowed");
+      load_impl(local_path(args.a[1].s), false);
+      w->boolean(true);
+    }
+  }
+
+  void load_impl(const std::string& path, bool overwrite_config) {
+    std::string bytes;
+    if (!read_file(path, &bytes)) throw std::runtime_error("cannot open input file: " + path + ": " + strerror(errno));
+    ModelFile mf;
+    const std::string err = read_model_file(bytes, &mf);
+    if (!err.empty()) throw std::runtime_error(err);
+    if (mf.type != engine_name())
+      throw std::runtime_error("invalid model type: saved type: " + mf.type + ", expected type: " + engine_name());
+    if (!overwrite_config && !jb::val::same_config(mf.config, config_))
+      throw std::runtime_error("model config mismatched with the running config");
+    if (mf.user_version != 1)
+      throw std::runtime_error("user data version mismatched: " + std::to_string(mf.user_version) +
+                               ", current version: 1");
+    std::unique_lock<std::shared_mutex> g(model_mu_);
+    if (overwrite_config && !jb::val::same_config(mf.config, config_)) {
+      eng_ = make_(mf.config);
+      config_ = mf.config;
+      table_.clear();
+      for (auto& m : eng_->methods()) table_.push_back(m);
+    }
+    eng_->unpack(mf.user);
+    std::lock_guard<std::mutex> s(st_mu_);
+    cs_.last_loaded = time(nullptr);
+    cs_.last_loaded_path = path;
+    logf_("INFO", "loaded from %s", path.c_str());
+  }
+
+  Args a_;
+  std::string config_;
+  Factory make_;
+  std::unique_ptr<HostEngine> eng_;
+  std::vector<HostMethod> table_;
+  std::unique_ptr<jb::RpcServer> rpc_;
+  std::shared_mutex model_mu_;
+  std::mutex st_mu_;
+  CommonStatus cs_;
+  uint64_t update_count_ = 0;
+};
+
+// main() of a host-engine server: flags, config check (native vs Python),
+// model file, serve
+template <class Check>
+int host_main(int argc, char** argv, const char* engine, Check check, HostServer::Factory make) {
+  set_engine(engine);
+  Args a;
+  std::string text;
+  const int rc = startup(argc, argv, &a, &text, check, /*needs_gpu=*/false);
+  if (rc >= 0) return rc;
+  block_signals();
+  logf_("INFO", "starting %s %s RPC server at %s:%d (native, host engine)", prog_name(), kVersion,
+        a.eth.c_str(), a.port);
+  try {
+    HostServer srv(a, text, make);
+    if (!a.model_file.empty()) srv.load_file(a.model_file);
+    return srv.run();
+  } catch (const std::exception& e) {
+    logf_("FATAL", "failed to start %s: %s", engine, e.what());
+    return 1;
+  }
+}
+
+// argument helpers for the handlers (std::invalid_argument -> ARGUMENT_ERROR)
+inline const std::string& arg_str(const Value& v) {
+  if (!v.is_str()) throw std::invalid_argument("string expected");
+  return v.s;
+}
+inline double arg_num(const Value& v) {
+  if (!v.is_num()) throw std::invalid_argument("number expected");
+  return v.num();
+}
+inline int64_t arg_int(const Value& v) {
+  if (v.kind == Value::INT) return v.i;
+  if (v.kind == Value::UINT) return (int64_t)v.u;
+  throw std::invalid_argument("integer expected");
+}
+
+}  // namespace srv
+}  // namespace jb

@@ -536,7 +536,7 @@ inline void common_status(const Args& a, const CommonStatus& cs, uint64_t update
 // otherwise the exit code. check(text, why) says whether the config is
 // served natively; --native-check prints that decision and exits.
 template <class Check>
-int startup(int argc, char** argv, Args* a, std::string* text, Check check) {
+int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool needs_gpu = true) {
   int rc = parse_args(argc, argv, a);
   if (rc == -1) return 0;
   if (rc) return rc;
@@ -548,8 +548,9 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check) {
   if (force && strcmp(force, "0") == 0) exec_python(argc, argv, "JUBATUS_NATIVE_SERVER=0");
   if (!a->native_check) {
     if (!a->zookeeper.empty()) exec_python(argc, argv, "distributed mode");
-    if (a->cpu || getenv("JUBATUS_FORCE_CPU")) exec_python(argc, argv, "host backend requested");
-    if (access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
+    if (needs_gpu && (a->cpu || getenv("JUBATUS_FORCE_CPU")))
+      exec_python(argc, argv, "host backend requested");
+    if (needs_gpu && access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
   }
   if (a->configpath.empty() && a->model_file.empty()) {
     fprintf(stderr, "config path or model file must be specified for standalone mode\n");
@@ -592,20 +593,24 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check) {
   return -1;
 }
 
-// the HIP device of this process (--gpu, else LOCAL_RANK) and the signal
-// set the main thread waits on (blocked in every thread)
-inline int device_and_signals(const Args& a) {
-  int device = a.gpu;
-  if (device < 0) {
-    const char* lr = getenv("LOCAL_RANK");
-    device = lr ? atoi(lr) : 0;
-  }
+// block the signals the main thread waits on (every thread inherits it)
+inline void block_signals() {
   sigset_t set;
   sigemptyset(&set);
   sigaddset(&set, SIGTERM);
   sigaddset(&set, SIGINT);
   pthread_sigmask(SIG_BLOCK, &set, nullptr);
   signal(SIGPIPE, SIG_IGN);
+}
+
+// the HIP device of this process (--gpu, else LOCAL_RANK); blocks the signals
+inline int device_and_signals(const Args& a) {
+  int device = a.gpu;
+  if (device < 0) {
+    const char* lr = getenv("LOCAL_RANK");
+    device = lr ? atoi(lr) : 0;
+  }
+  block_signals();
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (ndev <= 0) throw std::runtime_error("no HIP device");

@@ -1,0 +1,240 @@
+"""Native host-engine servers (csrc/server/jb_host_server.hpp: jubastat):
+no Python and no GPU in the process, so these run on the CPU. Every call is
+checked against the Python driver fed the same sequence (models/stat.py),
+including the error messages, and model files move both ways."""
+import json
+import os
+import random
+import socket
+import subprocess
+import time
+
+import pytest
+
+from helpers import ROOT, config_path
+from jubatus_amd.common.mprpc import RpcClient, RpcIOError, RpcMethodNotFound, RpcTimeoutError, RpcTypeError
+
+NATIVE_BIN = os.path.join(ROOT, "jubatus_amd", "native_bin")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def stat_server(tmp_path):
+    port = _free_port()
+    cfg = tmp_path / "stat.json"
+    cfg.write_text(json.dumps({"window_size": 16}))
+    p = subprocess.Popen([os.path.join(NATIVE_BIN, "jubastat"), "-p", str(port), "-b", "127.0.0.1",
+                          "-f", str(cfg), "-d", str(tmp_path)], stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT)
+    deadline = time.time() + 30
+    while True:
+        try:
+            with RpcClient("127.0.0.1", port, 5.0) as c:
+                c.call("get_config", "")
+            break
+        except (OSError, RpcIOError, RpcTimeoutError):
+            assert p.poll() is None and time.time() < deadline, p.stdout.read()
+            time.sleep(0.1)
+    yield port, str(cfg)
+    p.terminate()
+    p.wait(timeout=30)
+
+
+def _call(c, m, *a):
+    try:
+        return ("ok", c.call(m, "", *a))
+    except RpcTypeError:
+        return ("arg", None)
+    except Exception as e:  # noqa: BLE001 - application error text
+        return ("err", str(e))
+
+
+def test_native_stat_matches_python_driver(stat_server):
+    from jubatus_amd.models.stat import Stat, StatError
+    port, _ = stat_server
+    ref = Stat(16)
+    rng = random.Random(0)
+    keys = ["a", "b", "c", "d"]
+    with RpcClient("127.0.0.1", port, 10.0) as c:
+        for step in range(400):
+            op = rng.choice(["push"] * 4 + ["sum", "stddev", "max", "min", "entropy", "moment"])
+            k = rng.choice(keys + ["zz"])
+            if op == "push":
+                v = rng.uniform(-10, 10)
+                assert c.call("push", "", k, v) is ref.push(k, v)
+                continue
+            args = (k, rng.randrange(0, 4), rng.uniform(-1, 1)) if op == "moment" else (k,)
+            got = _call(c, op, *args)
+            try:
+                want = ("ok", ref.entropy() if op == "entropy" else getattr(ref, op)(*args))
+            except StatError as e:
+                want = ("err", str(e))
+            assert got[0] == want[0], (step, op, got, want)
+            if got[0] == "ok":
+                assert got[1] == pytest.approx(want[1], rel=1e-9, abs=1e-9), (step, op, args)
+            else:
+                assert want[1] in got[1]
+        (_, st), = c.call("get_status", "").items()
+        st = {(k.decode() if isinstance(k, bytes) else k): v for k, v in st.items()}
+        assert st["server_runtime"] == "native" and st["window_size"] == "16"
+        from test_status_keys import COMMON, DISTRIBUTED
+        assert not [k for k in COMMON if k not in st]
+        assert not [k for k in DISTRIBUTED if k in st]
+        assert int(st["window_population"]) == 16
+        assert _call(c, "moment", "a", -1, 0.0)[0] in ("err", "arg") or "a" not in ref.stats
+        with pytest.raises(RpcMethodNotFound):
+            c.call("no_such", "")
+        assert _call(c, "push", "a")[0] == "arg"           # arity
+        assert _call(c, "push", "a", "x")[0] == "arg"      # type
+
+
+def test_native_stat_model_files_both_ways(stat_server, tmp_path):
+    from jubatus_amd.framework import save_load
+    from jubatus_amd.models.stat import Stat
+    port, cfg = stat_server
+    text = open(cfg).read()
+    with RpcClient("127.0.0.1", port, 10.0) as c:
+        for i in range(40):
+            c.call("push", "", f"k{i % 3}", float(i))
+        (ident, path), = c.call("save", "", "m").items()
+        path = path.decode() if isinstance(path, bytes) else path
+        ident = ident.decode() if isinstance(ident, bytes) else ident
+        with open(path, "rb") as f:
+            _, pack = save_load.load_server(f, "stat", text, 1, False)
+        ref = Stat(16)
+        ref.unpack(pack)
+        assert c.call("sum", "", "k1") == pytest.approx(ref.sum("k1"))
+        assert c.call("clear", "") is True
+        with pytest.raises(Exception):
+            c.call("sum", "", "k1")
+        assert c.call("load", "", "m") is True
+        assert c.call("max", "", "k2") == pytest.approx(ref.max("k2"))
+        ref2 = Stat(16)
+        for i in range(10):
+            ref2.push("p", float(i * i))
+        with open(os.path.join(os.path.dirname(path), f"{ident}_stat_py.jubatus"), "wb") as f:
+            save_load.save_server(f, "stat", "py", text, 1, ref2.pack())
+        assert c.call("load", "", "py") is True
+        assert c.call("stddev", "", "p") == pytest.approx(ref2.stddev("p"))
+        assert c.call("entropy", "", "ignored") == pytest.approx(ref2.entropy())
+
+
+def test_native_stat_config_check(tmp_path):
+    p = tmp_path / "s.json"
+    exe = os.path.join(NATIVE_BIN, "jubastat")
+    for cfg, want in ((config_path("stat/default.json"), "native"),):
+        r = subprocess.run([exe, "--native-check", "-f", cfg], capture_output=True, text=True, timeout=30)
+        assert r.stdout.strip() == want
+    p.write_text("{}")
+    r = subprocess.run([exe, "--native-check", "-f", str(p)], capture_output=True, text=True, timeout=30)
+    assert "window_size" in r.stdout
+
+
+# ------------------------------------------------------------------ bandit
+def _start(exe, cfg_obj, tmp_path):
+    port = _free_port()
+    cfg = tmp_path / "cfg.json"
+    cfg.write_text(json.dumps(cfg_obj))
+    p = subprocess.Popen([os.path.join(NATIVE_BIN, exe), "-p", str(port), "-b", "127.0.0.1",
+                          "-f", str(cfg), "-d", str(tmp_path)], stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT)
+    deadline = time.time() + 30
+    while True:
+        try:
+            with RpcClient("127.0.0.1", port, 5.0) as c:
+                c.call("get_config", "")
+            return p, port, str(cfg)
+        except (OSError, RpcIOError, RpcTimeoutError):
+            assert p.poll() is None and time.time() < deadline, p.stdout.read()
+            time.sleep(0.1)
+
+
+def _norm(x):
+    if isinstance(x, bytes):
+        return x.decode()
+    if isinstance(x, dict):
+        return {_norm(k): _norm(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_norm(v) for v in x]
+    return x
+
+
+@pytest.mark.parametrize("unrewarded", [False, True])
+def test_native_bandit_ucb1_matches_python_driver(tmp_path, unrewarded):
+    """ucb1 is deterministic: the native server and the Python driver pick
+    the same arms and keep the same arm_info for the same reward stream"""
+    from jubatus_amd.models.bandit import Bandit
+    cfg = {"method": "ucb1", "parameter": {"assume_unrewarded": unrewarded}}
+    p, port, _ = _start("jubabandit", cfg, tmp_path)
+    ref = Bandit("ucb1", cfg["parameter"])
+    rng = random.Random(3)
+    try:
+        with RpcClient("127.0.0.1", port, 10.0) as c:
+            assert _call(c, "select_arm", "p")[0] == "err"      # no arm
+            for a in ("a0", "a1", "a2"):
+                assert c.call("register_arm", "", a) is True and ref.register_arm(a)
+            assert c.call("register_arm", "", "a1") is False
+            truth = {"a0": 0.2, "a1": 0.8, "a2": 0.5}
+            for _ in range(200):
+                player = rng.choice(["p", "q"])
+                arm = _norm(c.call("select_arm", "", player))
+                assert arm == ref.select_arm(player)
+                r = 1.0 if rng.random() < truth[arm] else 0.0
+                assert c.call("register_reward", "", player, arm, r) is True
+                ref.register_reward(player, arm, r)
+            for player in ("p", "q"):
+                got = _norm(c.call("get_arm_info", "", player))
+                want = {a: [n, w] for a, (n, w) in ref.get_arm_info(player).items()}
+                assert got == want
+            assert c.call("register_reward", "", "p", "nope", 1.0) is False
+            assert c.call("delete_arm", "", "a2") is True and ref.delete_arm("a2")
+            assert sorted(_norm(c.call("get_arm_info", "", "p"))) == ["a0", "a1"]
+            assert c.call("reset", "", "p") is True and ref.reset("p")
+            assert _norm(c.call("get_arm_info", "", "p")) == {"a0": [0, 0.0], "a1": [0, 0.0]}
+            (_, st), = _norm(c.call("get_status", "")).items()
+            assert st["server_runtime"] == "native" and st["num_arms"] == "2"
+    finally:
+        p.terminate()
+        p.wait(timeout=30)
+
+
+@pytest.mark.parametrize("method,param", [("epsilon_greedy", {"epsilon": 0.1}), ("softmax", {"tau": 0.05}),
+                                          ("exp3", {"gamma": 0.1})])
+def test_native_bandit_randomized_methods_learn(tmp_path, method, param):
+    cfg = {"method": method, "parameter": {"assume_unrewarded": False, "seed": 7, **param}}
+    p, port, text = _start("jubabandit", cfg, tmp_path)
+    rng = random.Random(5)
+    try:
+        with RpcClient("127.0.0.1", port, 10.0) as c:
+            for a in ("bad", "good"):
+                c.call("register_arm", "", a)
+            picks = []
+            for _ in range(600):
+                arm = _norm(c.call("select_arm", "", "u"))
+                picks.append(arm)
+                c.call("register_reward", "", "u", arm, 1.0 if (arm == "good") == (rng.random() < 0.9) else 0.0)
+            assert picks[-200:].count("good") > 120, (method, picks[-200:].count("good"))
+            # model file -> the Python driver
+            from jubatus_amd.framework import save_load
+            from jubatus_amd.models.bandit import Bandit
+            (_, path), = _norm(c.call("save", "", "b")).items()
+            with open(path, "rb") as f:
+                _, pack = save_load.load_server(f, "bandit", open(text).read(), 1, False)
+            ref = Bandit(method, cfg["parameter"])
+            ref.unpack(pack)
+            want = {a: [n, w] for a, (n, w) in ref.get_arm_info("u").items()}
+            assert _norm(c.call("get_arm_info", "", "u")) == want
+            assert c.call("clear", "") is True
+            assert _norm(c.call("get_arm_info", "", "u")) == {}
+            assert c.call("load", "", "b") is True
+            assert _norm(c.call("get_arm_info", "", "u")) == want
+    finally:
+        p.terminate()
+        p.wait(timeout=30)
