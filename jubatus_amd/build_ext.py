@@ -166,8 +166,9 @@ SERVERS = {
     # host engines: no GPU, no HIP libraries
     "jubastat": (["server/jubastat.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    "jubaburst": (["server/jubaburst.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }
-HOST_SERVERS = {"jubastat", "jubabandit"}
+HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:

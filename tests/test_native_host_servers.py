@@ -238,3 +238,86 @@ def test_native_bandit_randomized_methods_learn(tmp_path, method, param):
     finally:
         p.terminate()
         p.wait(timeout=30)
+
+
+# ------------------------------------------------------------------- burst
+def _flat(x):
+    if isinstance(x, (list, tuple)):
+        return [v for e in x for v in _flat(e)]
+    return [x]
+
+
+def _same(a, b):
+    fa, fb = _flat(a), _flat(b)
+    assert len(fa) == len(fb), (a, b)
+    assert fa == pytest.approx(fb, rel=1e-9, abs=1e-9), (a, b)
+    return True
+
+
+def test_native_burst_matches_python_driver(tmp_path):
+    from jubatus_amd.framework import save_load
+    from jubatus_amd.models.burst import Burst
+    from jubatus_amd.server.burst_serv import _window
+    cfg = json.load(open(config_path("burst/burst.json")))
+    p, port, text = _start("jubaburst", cfg, tmp_path)
+    ref = Burst(cfg["method"], cfg["parameter"])
+    rng = random.Random(11)
+    try:
+        with RpcClient("127.0.0.1", port, 10.0) as c:
+            for kw, s, g in (("fire", 2.0, 1.0), ("quake", 3.0, 0.5), ("rain", 2.5, 1.0)):
+                assert c.call("add_keyword", "", [kw, s, g]) is True
+                ref.add_keyword(kw, s, g)
+            assert c.call("add_keyword", "", ["fire", 2.0, 1.0]) is False
+            assert _call(c, "add_keyword", ["bad", 0.5, 1.0])[0] == "err"
+            pos = 0.0
+            seen = 0
+            for step in range(120):
+                docs = []
+                for _ in range(rng.randrange(1, 6)):
+                    pos += rng.uniform(0, 3)
+                    burst = 40 < step < 70
+                    words = ["fire" if rng.random() < (0.8 if burst else 0.1) else "calm",
+                             "quake" if rng.random() < 0.2 else "", "rain" if rng.random() < 0.3 else ""]
+                    docs.append([pos - rng.uniform(0, 60) if rng.random() < 0.05 else pos, " ".join(words)])
+                n = c.call("add_documents", "", docs)
+                want = sum(ref.add_document(t, float(ps)) for ps, t in docs)
+                if want:
+                    ref.calculate_results()
+                assert n == want
+                if step % 10 == 9:
+                    for kw in ("fire", "quake", "rain", "none"):
+                        assert _same(_norm(c.call("get_result", "", kw)), _window(ref.get_result(kw)))
+                        q = pos - rng.uniform(0, 40)
+                        assert _same(_norm(c.call("get_result_at", "", kw, q)), _window(ref.get_result_at(kw, q)))
+                    got = _norm(c.call("get_all_bursted_results", ""))
+                    want_b = {k: _window(v) for k, v in ref.get_all_bursted_results().items()}
+                    assert sorted(got) == sorted(want_b)
+                    seen += len(got)
+                    for k in got:
+                        assert _same(got[k], want_b[k])
+            assert seen > 0                      # bursts were detected and compared
+            q = pos - 30.0
+            got = _norm(c.call("get_all_bursted_results_at", "", q))
+            assert sorted(got) == sorted(ref.get_all_bursted_results_at(q))
+            assert _norm(c.call("get_all_keywords", "")) == [[k, s, g] for k, s, g in ref.get_all_keywords()]
+            (ident, path), = _norm(c.call("save", "", "b")).items()
+            with open(path, "rb") as f:
+                _, pack = save_load.load_server(f, "burst", open(text).read(), 1, False)
+            ref2 = Burst(cfg["method"], cfg["parameter"])
+            ref2.unpack(pack)
+            assert _same(_window(ref2.get_result("fire")), _window(ref.get_result("fire")))
+            assert c.call("remove_keyword", "", "rain") is True and c.call("remove_keyword", "", "rain") is False
+            assert c.call("clear", "") is True
+            assert _norm(c.call("get_result", "", "fire")) == [0.0, []]
+            assert c.call("load", "", "b") is True
+            assert _same(_norm(c.call("get_result", "", "fire")), _window(ref.get_result("fire")))
+            with open(os.path.join(os.path.dirname(path), f"{ident}_burst_py.jubatus"), "wb") as f:
+                save_load.save_server(f, "burst", "py", open(text).read(), 1, ref.pack())
+            assert c.call("remove_all_keywords", "") is True
+            assert c.call("load", "", "py") is True
+            assert _norm(c.call("get_all_keywords", "")) == [[k, s, g] for k, s, g in ref.get_all_keywords()]
+            (_, st), = _norm(c.call("get_status", "")).items()
+            assert st["server_runtime"] == "native" and st["num_keywords"] == "3"
+    finally:
+        p.terminate()
+        p.wait(timeout=30)
