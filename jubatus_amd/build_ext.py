@@ -167,8 +167,9 @@ SERVERS = {
     "jubastat": (["server/jubastat.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubaburst": (["server/jubaburst.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    "jubagraph": (["server/jubagraph.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }
-HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst"}
+HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:

@@ -321,3 +321,97 @@ def test_native_burst_matches_python_driver(tmp_path):
     finally:
         p.terminate()
         p.wait(timeout=30)
+
+
+# ------------------------------------------------------------------- graph
+def _both(tmp_path, engine, cfg_file):
+    """(native port, Python server helper) serving the same config"""
+    from helpers import start_standalone
+    p, port, _ = _start(f"juba{engine}", json.load(open(cfg_file)), tmp_path / "n" if False else tmp_path)
+    (tmp_path / "py").mkdir()
+    h = start_standalone(engine, cfg_file, tmp_path / "py")
+    return p, port, h
+
+
+def test_native_graph_matches_python_server(tmp_path):
+    """the same RPC sequence against the native and the Python jubagraph:
+    identical answers and error classes (ids, properties, edges, centrality,
+    shortest paths, queries, removal rules)"""
+    p, nport, h = _both(tmp_path, "graph", config_path("graph/default.json"))
+    rng = random.Random(2)
+    try:
+        with RpcClient("127.0.0.1", nport, 10.0) as n, RpcClient("127.0.0.1", h.argv.port, 10.0) as y:
+            def both(m, *a, same=True):
+                rn, ry = _call(n, m, *a), _call(y, m, *a)
+                assert rn[0] == ry[0], (m, a, rn, ry)
+                if same and rn[0] == "ok":
+                    if isinstance(ry[1], float):
+                        assert rn[1] == pytest.approx(ry[1], rel=1e-9), (m, a)
+                    else:
+                        assert _norm(rn[1]) == _norm(ry[1]), (m, a)
+                return _norm(rn[1])
+            ids = [both("create_node") for _ in range(12)]
+            for i in ids:
+                both("update_node", i, {"kind": rng.choice(["a", "b"]), "w": str(rng.randrange(3))})
+            q_all = [[], []]
+            q_a = [[["t", "x"]], [["kind", "a"]]]
+            for q in (q_all, q_a):
+                both("add_centrality_query", q)
+                both("add_shortest_path_query", q)
+            eids = []
+            for _ in range(30):
+                s, t = rng.choice(ids), rng.choice(ids)
+                eids.append(both("create_edge", s, [{"t": rng.choice(["x", "y"])}, s, t]))
+            both("create_edge", ids[0], [{}, ids[0], "999"])           # unknown target
+            both("create_edge", "999", [{}, "999", ids[0]])            # unknown source
+            both("get_centrality", ids[0], 0, q_all)                   # before update_index
+            both("update_index")
+            for i in ids:
+                for q in (q_all, q_a):
+                    both("get_centrality", i, 0, q)
+                both("get_node", i)
+            both("get_centrality", ids[0], 1, q_all)                   # unknown type
+            both("get_centrality", ids[0], 0, [[["no", "pe"]], []])    # unregistered
+            for _ in range(20):
+                s, t = rng.choice(ids), rng.choice(ids)
+                for q in (q_all, q_a):
+                    both("get_shortest_path", [s, t, rng.randrange(1, 5), q])
+            both("get_shortest_path", [ids[0], ids[1], 3, [[["x", "y"]], []]])
+            for e in eids[:5]:
+                both("get_edge", ids[0], e)
+                both("update_edge", ids[0], e, [{"t": "z"}, "0", "0"])
+                both("get_edge", ids[0], e)
+            both("get_edge", ids[0], 10 ** 6)
+            both("remove_node", ids[0])                                # has edges
+            lonely = both("create_node")
+            both("remove_node", lonely)
+            both("get_node", lonely)
+            for e in eids[5:10]:
+                both("remove_edge", ids[0], e)
+            both("remove_edge", ids[0], eids[5])
+            both("remove_centrality_query", q_a)
+            both("get_centrality", ids[1], 0, q_a)
+            both("get_node", "not-an-id")
+            both("update_index")
+            for i in ids[1:4]:
+                both("get_centrality", i, 0, q_all)
+            # model files: native save -> native load and Python load of the same file
+            (_, path), = _norm(n.call("save", "", "g")).items()
+            from jubatus_amd.framework import save_load
+            from jubatus_amd.models.graph import Graph
+            with open(path, "rb") as f:
+                _, pack = save_load.load_server(f, "graph", open(config_path("graph/default.json")).read(), 1,
+                                                False)
+            ref = Graph("graph_wo_index", {})
+            ref.unpack(pack)
+            assert ref.get_centrality(int(ids[2]), 0, q_all) == pytest.approx(
+                n.call("get_centrality", "", ids[2], 0, q_all))
+            assert n.call("clear", "") is True
+            assert n.call("load", "", "g") is True
+            assert _norm(n.call("get_node", "", ids[3])) == _norm(y.call("get_node", "", ids[3]))
+            (_, st), = _norm(n.call("get_status", "")).items()
+            assert st["server_runtime"] == "native" and st["local_node_num"] == "12"
+    finally:
+        h.stop()
+        p.terminate()
+        p.wait(timeout=30)
