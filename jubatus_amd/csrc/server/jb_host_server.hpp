@@ -1,4 +1,5 @@
-// RPC shell of the native host-engine servers (jubastat, jubabandit): the
+// RPC shell of the native host-engine servers (jubastat, jubabandit,
+// jubaburst, jubagraph): the
 // engines whose state is small per-key bookkeeping and stays on the host
 // (SURVEY K14), served without Python. Reference: the generated
 // <engine>_impl.cpp RPC tables and framework/server_base.cpp (save / load /
@@ -10,6 +11,7 @@
 // payload (the same msgpack maps as the Python drivers, so model files move
 // between the two servers) and its status keys.
 #pragma once
+#include <atomic>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -135,7 +137,7 @@ class HostServer {
       std::vector<std::pair<std::string, std::string>> st;
       {
         std::lock_guard<std::mutex> g(st_mu_);
-        common_status(a_, cs_, update_count_, &st);
+        common_status(a_, cs_, update_count_.load(), &st);
       }
       st.emplace_back("server_runtime", "native");
       {
@@ -208,7 +210,7 @@ class HostServer {
   std::shared_mutex model_mu_;
   std::mutex st_mu_;
   CommonStatus cs_;
-  uint64_t update_count_ = 0;
+  std::atomic<uint64_t> update_count_{0};
 };
 
 // main() of a host-engine server: flags, config check (native vs Python),

@@ -233,7 +233,13 @@ class Classifier {
       if (si >= 0) {
         Set& s = sets_[si];
         const auto t1 = std::chrono::steady_clock::now();
-        HIPCHK(hipEventSynchronize(s.check_done));
+        const hipError_t we = hipEventSynchronize(s.check_done);
+        if (we != hipSuccess) {   // leave the set usable for the error replies that follow
+          std::lock_guard<std::mutex> g(mu_);
+          s.inflight = false;
+          set_cv_.notify_one();
+          throw std::runtime_error(std::string("hipEventSynchronize: ") + hipGetErrorString(we));
+        }
         const auto t2 = std::chrono::steady_clock::now();
         std::lock_guard<std::mutex> g(mu_);
         prof_[0] += 1;
