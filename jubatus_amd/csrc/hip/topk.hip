@@ -1204,8 +1204,6 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   return (int)hipGetLastError();
 }
 
-constexpr int kTileMaxK = 16;
-
 extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64_t nrows, int k,
                                      float* scratch_d, int32_t* scratch_i, float* out_d_host,
                                      int32_t* out_i_host, uint32_t* done_host,
@@ -1213,12 +1211,7 @@ extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64
   if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
   if (k > jb::kTopMaxK || nq > 8) return -2;
   jb::TopkSrc s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, src_d, nullptr, flip};
-  // small k: the tile path (per-block selection + one merge, 2 launches) is
-  // faster than the 7-launch radix chain (recommender default config, 1M
-  // rows, k 10: similar_row_from_datum 140 -> 125 us,
-  // profiles/r02_topk_small_k_tile.jsonl); the radix chain is k-independent
-  // and wins for larger k
-  const bool radix = nrows >= 16384 && k > kTileMaxK && getenv("JB_TOPK_SCORES_TILE") == nullptr;
+  const bool radix = nrows >= 16384 && getenv("JB_TOPK_SCORES_TILE") == nullptr;
   uint32_t seq = jb::next_seq();
   int rc = topk_scores_launch(s, nq, nrows, k, radix, scratch_d, scratch_i, out_d_host,
                               out_i_host, done_host, seq, stream);
