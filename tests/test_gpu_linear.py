@@ -368,7 +368,7 @@ def test_concurrent_deviation_from_serial_order(hot, monkeypatch, capsys):
     a row that all streams carry took ~1000 AROW steps computed from the
     same confidence and the weights grew 35-45x past the serial ones
     (profiles/r02_concurrent_vs_serial.jsonl). With it the weight distance
-    is ~1.3x the serial norm (hot-row replica: ~11x, its blocks see each
+    is ~1.3x the serial norm (hot-row replica: ~10x, its blocks see each
     other's confidence one merge late and estimate it from the last merge),
     the decisions agree on ~98% of held-out datums and accuracy is within
     ~0.7 point."""
