@@ -1025,37 +1025,54 @@ __device__ __forceinline__ float key_dist(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
+// Histogram of one radix level's 12-bit digit of every distance (LDS per
+// block, merged with global atomics). Most rows of a cosine score vector
+// share one digit (score 0 -> distance 1, 99% of the rows here), so each
+// wave adds the digit of its first active lane with one LDS atomic and only
+// the other lanes add their own (hist 1 under the tracer: 13.1 -> 11.4 us).
+// A last-block select fused into this kernel measured slower (the
+// agent-scope fence per block, then 512 blocks serialized on the
+// finished-block counter; profiles/r02_topk_scores.jsonl).
 template <int LEVEL>
 __global__ __launch_bounds__(256) void radix_hist_kernel(const float* __restrict__ src, int flip,
-                                                         int64_t n, const uint32_t* __restrict__ sel,
+                                                         int64_t n,
+                                                         const uint32_t* __restrict__ sel,
                                                          uint32_t* __restrict__ hist) {
+  constexpr int T = 256;
   __shared__ uint32_t h[kRadixBins];
   const int q = blockIdx.y;
-  for (int i = threadIdx.x; i < kRadixBins; i += blockDim.x) h[i] = 0;
+  const int t = threadIdx.x, lane = t & 63;
+  for (int i = t; i < kRadixBins; i += T) h[i] = 0;
   __syncthreads();
   const uint32_t pre = LEVEL == 2 ? sel[2 * q] : 0u;
   const float* sq = src + (int64_t)q * n;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
-  for (int64_t b = (int64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x; b < n; b += stride) {
+  const int64_t stride = (int64_t)gridDim.x * T * 4;
+  for (int64_t b = (int64_t)blockIdx.x * T * 4 + t; b < n; b += stride) {
     float v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t i = b + u * blockDim.x;
+      const int64_t i = b + u * T;
       v[u] = sq[i < n ? i : n - 1];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (b + u * blockDim.x >= n) continue;
       const float d = flip ? 1.f - v[u] : v[u];
-      if (!(d < INFINITY)) continue;                        // invalid rows / NaN
       const uint32_t key = dist_key(d);
-      if (LEVEL == 1) atomicAdd(&h[key >> 20], 1u);
-      else if ((key >> 20) == pre) atomicAdd(&h[(key >> 8) & 0xfff], 1u);
+      const uint32_t bin = LEVEL == 1 ? key >> 20 : (key >> 8) & 0xfff;
+      // invalid rows / NaN (!(d < inf)) and, on level 2, rows outside the bucket
+      const bool act = b + u * T < n && d < INFINITY && (LEVEL == 1 || (key >> 20) == pre);
+      const uint64_t am = __ballot(act);
+      if (am == 0) continue;
+      const int leader = __ffsll((unsigned long long)am) - 1;
+      const uint32_t b0 = __shfl(bin, leader, 64);
+      const uint64_t same = __ballot(act && bin == b0);
+      if (lane == leader) atomicAdd(&h[b0], (uint32_t)__popcll(same));
+      else if (act && bin != b0) atomicAdd(&h[bin], 1u);
     }
   }
   __syncthreads();
   uint32_t* gh = hist + (int64_t)q * kRadixBins;
-  for (int i = threadIdx.x; i < kRadixBins; i += blockDim.x)
+  for (int i = t; i < kRadixBins; i += T)
     if (h[i]) atomicAdd(&gh[i], h[i]);
 }
 
@@ -1113,7 +1130,9 @@ namespace jb {
 
 // exact top-k of a small candidate set by ranking: every candidate's final
 // position is the number of candidates before it in (distance, row) order;
-// more than kRankMax candidates (massive ties) -> retry on the tile path.
+// for k <= kListK and more than 32 candidates (ties at the threshold) register
+// lists instead (the rank loop is LDS-latency bound: 156 tied candidates
+// 20 us, lists ~5 us); more than kRankMax candidates -> retry on the tile path.
 constexpr int kRankMax = 4096;
 __global__ __launch_bounds__(1024) void topk_rank_final_kernel(
     const float* __restrict__ cand_d, const int32_t* __restrict__ cand_i,
@@ -1136,17 +1155,61 @@ __global__ __launch_bounds__(1024) void topk_rank_final_kernel(
     out_i[(int64_t)q * k + j] = INT_MAX;
   }
   __syncthreads();
-  for (int j = t; j < nc; j += blockDim.x) {
-    const float d = s_d[j];
-    const int32_t id = s_i[j];
-    int rank = 0;
-    for (int x = 0; x < nc; ++x) {
-      const float e = s_d[x];
-      rank += (e < d) || (e == d && s_i[x] < id);
+  if (k <= kListK && nc > 32) {
+    // many candidates (ties at the threshold): per-thread sorted top-16 of
+    // its strided candidates, per-wave pops, then wave 0 merges the 16 waves'
+    // lists - O(nc k / threads) instead of the rank's O(nc^2 / threads)
+    constexpr int NW = 16;
+    float ld[kListK];
+    int li[kListK];
+#pragma unroll
+    for (int j = 0; j < kListK; ++j) { ld[j] = INFINITY; li[j] = INT_MAX; }
+    for (int j = t; j < nc; j += blockDim.x) {
+      const float v = s_d[j];
+      const int id = s_i[j];
+      if (lt_pair(v, id, ld[kListK - 1], li[kListK - 1])) {
+#pragma unroll
+        for (int x = kListK - 1; x > 0; --x) {
+          const bool up = lt_pair(v, id, ld[x - 1], li[x - 1]);
+          const bool here = !up && lt_pair(v, id, ld[x], li[x]);
+          ld[x] = up ? ld[x - 1] : (here ? v : ld[x]);
+          li[x] = up ? li[x - 1] : (here ? id : li[x]);
+        }
+        if (lt_pair(v, id, ld[0], li[0])) { ld[0] = v; li[0] = id; }
+      }
     }
-    if (rank < k) {
-      out_d[(int64_t)q * k + rank] = d;
-      out_i[(int64_t)q * k + rank] = id;
+    __syncthreads();                               // s_d / s_i reused for the wave lists
+    const int lane = t & 63, wv = t >> 6;
+    wave_pop<kListK>(ld, li, k, &s_d[wv * k], &s_i[wv * k], lane);
+    __syncthreads();
+    if (wv == 0) {
+      constexpr int M = (NW * kListK + 63) / 64;
+      float m[M];
+      int mi[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const int c = lane + 64 * j;
+        if (c < NW * k) { m[j] = s_d[c]; mi[j] = s_i[c]; }
+        else { m[j] = INFINITY; mi[j] = INT_MAX; }
+      }
+      __builtin_amdgcn_wave_barrier();
+      sort_regs<M>(m, mi);
+      wave_pop<M>(m, mi, k, out_d + (int64_t)q * k, out_i + (int64_t)q * k, lane);
+    }
+  } else {
+    for (int j = t; j < nc; j += blockDim.x) {
+      const float d = s_d[j];
+      const int32_t id = s_i[j];
+      int rank = 0;
+      for (int x = 0; x < nc; ++x) {
+        const float e = s_d[x];
+        rank += (e < d) || (e == d && s_i[x] < id);
+        if ((x & 63) == 63 && rank >= k) break;    // already out of the top k
+      }
+      if (rank < k) {
+        out_d[(int64_t)q * k + rank] = d;
+        out_i[(int64_t)q * k + rank] = id;
+      }
     }
   }
   __threadfence_system();
@@ -1183,8 +1246,15 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   uint32_t* h2 = h1 + (int64_t)nq * kRadixBins;
   hipError_t e = hipMemsetAsync(h1, 0, sizeof(uint32_t) * 2 * (size_t)nq * kRadixBins, stream);
   if (e != hipSuccess) return (int)e;
+  // blocks of the histogram passes: every block adds its bins to the global
+  // histogram with atomics, and on a score vector most rows share a bin, so
+  // the block count bounds the atomics serialized on that address
+  static const int64_t hb_max = [] {
+    const char* e = getenv("JB_RADIX_BLOCKS");
+    return e != nullptr && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)512;
+  }();
   int64_t hb = (nrows + 1023) / 1024;
-  if (hb > 512) hb = 512;
+  if (hb > hb_max) hb = hb_max;
   const float* src = s.src_d;
   hipLaunchKernelGGL(jb::radix_hist_kernel<1>, dim3((unsigned)hb, nq), dim3(256), 0, stream, src,
                      s.flip, nrows, sel, h1);
