@@ -864,7 +864,12 @@ extern "C" int jb_topk_blocks(int64_t nrows, int k) {
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   // bound the candidates K2 merges; one block per CU is enough to stream
   // the table (the scan is a few bytes per row)
-  int64_t max_blocks = 8192 / k < 256 ? 8192 / k : 256;
+  // JB_TOPK_MAX_BLOCKS: block cap override (tools / A-B runs)
+  static const int64_t cap = [] {
+    const char* e = getenv("JB_TOPK_MAX_BLOCKS");
+    return e != nullptr && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)256;
+  }();
+  int64_t max_blocks = 8192 / k < cap ? 8192 / k : cap;
   if (max_blocks < 1) max_blocks = 1;
   const int64_t tiles_per_block = (tiles + max_blocks - 1) / max_blocks;
   return (int)((tiles + tiles_per_block - 1) / tiles_per_block);
