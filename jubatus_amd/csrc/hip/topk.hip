@@ -288,7 +288,7 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
 }
 
 // Several queries per table pass (MODE 0, W <= 2 signature words): waves
-// per query. A block of 16 waves loads each tile of 8192 rows (signatures,
+// per query. A block of 16 waves loads each tile of 4096 rows (signatures,
 // and the norm with the valid flag folded in) into LDS once; the G = 16 / nq
 // waves of a query (G a power of two) take every G-th 512-row chunk of the
 // tile and run the threshold-pruned selection with a wave-private carry
@@ -304,6 +304,14 @@ constexpr int kWqT = kWqWaves * 64;
 constexpr int kWqLoads = 4;                       // rows a thread stages per tile
 constexpr int kWqTile = kWqT * kWqLoads;          // 4096 rows per tile
 constexpr int kWqChunks = kWqTile / 512;          // 512-row chunks (8 rows a lane)
+// static LDS of topk_wq_kernel<W> (tile bits + norms + carries): ~128 KB at
+// W = 2, which fits gfx950's 160 KB per workgroup only (CDNA3 has 64 KB);
+// this library is built for gfx950 alone (build_ext.py ARCH)
+constexpr int wq_lds_bytes(int w) {
+  return kWqTile * 8 * w + kWqTile * 4 + (64 * w + 1) * 4 + kWqWaves * 2 * kTopMaxK * 8 +
+         kWqWaves * kTopMaxK * 8 + kWqWaves * 8;
+}
+static_assert(wq_lds_bytes(2) <= 160 * 1024, "topk_wq_kernel<2> exceeds gfx950 LDS (160 KB)");
 
 // wave-level LDS ordering: the lanes of one wave read what others wrote
 __device__ __forceinline__ void wave_sync() {
@@ -783,15 +791,10 @@ constexpr int kListK = 16;   // k up to this uses topk_lists_kernel
 // contiguous range with a block-wide carry and two barriers per tile, so a
 // CU holding one 4-wave block spends most of a tile waiting on HBM latency;
 // 16 waves per block (one block per CU, k <= 37 so the 17 k merge fits) keep
-// 4x the rows in flight at the same candidate count. JB_TOPK_NW=4|16
-// overrides (tools/bench_topk.py compares them).
+// 4x the rows in flight at the same candidate count (measured choices below,
+// frozen: tools/bench_topk.py, profiles/r01_topk_kernels.md).
 inline int scan_waves(int k, int nq, int64_t nrows) {
-  static const int forced = [] {
-    const char* e = getenv("JB_TOPK_NW");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  if (forced == 4 || k > 37) return 4;
-  if (forced == 16) return 16;
+  if (k > 37) return 4;
   // measured (tools/bench_topk.py): 16 waves win for one query over a large
   // table (one block per CU, latency-bound: 10M rows k 10 74 vs 165 us) and
   // lose once several queries fill the chip with 4-wave blocks (1M rows x 8
@@ -799,23 +802,14 @@ inline int scan_waves(int k, int nq, int64_t nrows) {
   return nq == 1 && nrows >= ((int64_t)2 << 20) ? 16 : 4;
 }
 
-// the final merge of the blocks' candidates for k <= kListK: per-thread
-// register lists (default) or the tile kernel with the rank merge
-// (JB_TOPK_MERGE=tile, for comparison)
-inline bool merge_with_tile() {
-  static const bool tile = [] {
-    const char* e = getenv("JB_TOPK_MERGE");
-    return e != nullptr && e[0] == 't';
-  }();
-  return tile;
-}
+// the final merge of the blocks' candidates for k <= kListK uses per-thread
+// register lists (measured ~3 us faster than the tile kernel's rank merge,
+// profiles/r02_lsh_merge_ab.jsonl)
 
 template <int MODE>
 inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
                         int k, float* out_d, int32_t* out_i, hipStream_t stream) {
-  static const bool wq_off = getenv("JB_TOPK_WQ_OFF") != nullptr;
-  if (MODE == 0 && nq > 1 && nq <= kWqWaves && s.words <= 2 && s.hash_num <= 64 * s.words &&
-      !wq_off) {
+  if (MODE == 0 && nq > 1 && nq <= kWqWaves && s.words <= 2 && s.hash_num <= 64 * s.words) {
     // several queries per table pass, one wave per query (topk_wq_kernel)
     if (s.words == 1)
       hipLaunchKernelGGL((topk_wq_kernel<1>), dim3(blocks), dim3(kWqT), 0, stream, s, nq, nrows,
@@ -838,7 +832,7 @@ inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int
 inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out_d,
                          int32_t* out_i, volatile uint32_t* done, uint32_t seq,
                          hipStream_t stream) {
-  if (k <= kListK && !merge_with_tile()) {
+  if (k <= kListK) {
     hipLaunchKernelGGL((topk_lists_kernel<2, kListK, 16>), dim3(1, nq), dim3(16 * 64), 0, stream,
                        m, nc, nc, k, out_d, out_i, done, seq);
   } else if (k <= 37) {
@@ -864,11 +858,9 @@ extern "C" int jb_topk_blocks(int64_t nrows, int k) {
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   // bound the candidates K2 merges; one block per CU is enough to stream
   // the table (the scan is a few bytes per row)
-  // JB_TOPK_MAX_BLOCKS: block cap override (tools / A-B runs)
-  static const int64_t cap = [] {
-    const char* e = getenv("JB_TOPK_MAX_BLOCKS");
-    return e != nullptr && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)256;
-  }();
+  // (256: more blocks measured slower for batched queries,
+  // profiles/r02_lsh_block_cap.jsonl)
+  constexpr int64_t cap = 256;
   int64_t max_blocks = 8192 / k < cap ? 8192 / k : cap;
   if (max_blocks < 1) max_blocks = 1;
   const int64_t tiles_per_block = (tiles + max_blocks - 1) / max_blocks;
@@ -1254,10 +1246,7 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   // blocks of the histogram passes: every block adds its bins to the global
   // histogram with atomics, and on a score vector most rows share a bin, so
   // the block count bounds the atomics serialized on that address
-  static const int64_t hb_max = [] {
-    const char* e = getenv("JB_RADIX_BLOCKS");
-    return e != nullptr && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)512;
-  }();
+  constexpr int64_t hb_max = 512;
   int64_t hb = (nrows + 1023) / 1024;
   if (hb > hb_max) hb = hb_max;
   const float* src = s.src_d;
@@ -1286,7 +1275,7 @@ extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64
   if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
   if (k > jb::kTopMaxK || nq > 8) return -2;
   jb::TopkSrc s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, src_d, nullptr, flip};
-  const bool radix = nrows >= 16384 && getenv("JB_TOPK_SCORES_TILE") == nullptr;
+  const bool radix = nrows >= 16384;
   uint32_t seq = jb::next_seq();
   int rc = topk_scores_launch(s, nq, nrows, k, radix, scratch_d, scratch_i, out_d_host,
                               out_i_host, done_host, seq, stream);

@@ -347,7 +347,7 @@ void RpcServer::enqueue(RpcRequest&& req) {
     if (m == req.method) {
       std::lock_guard<std::mutex> g(bmu_);
       bqueue_.push_back(std::move(req));
-      bcv_.notify_one();
+      bcv_.notify_all();  // the generic-queue thread must see it
       return;
     }
   std::lock_guard<std::mutex> g(qmu_);
@@ -359,14 +359,15 @@ void RpcServer::enqueue(RpcRequest&& req) {
 // Drain every queued request of the method at the head of the batch queue
 // and serve them with one handler call; requests arriving meanwhile form
 // the next (larger) batch - adaptive batching without a timer.
-void RpcServer::batch_loop() {
+void RpcServer::batch_loop(int idx) {
+  const bool generic = idx == 0;
   for (;;) {
     if (arena_handler_ && arena_batch_once()) continue;
     std::vector<RpcRequest> batch;
     {
       std::unique_lock<std::mutex> g(bmu_);
-      bcv_.wait_for(g, std::chrono::milliseconds(arena_handler_ ? 1 : 100), [this] {
-        if (!bqueue_.empty() || !running_.load()) return true;
+      bcv_.wait_for(g, std::chrono::milliseconds(arena_handler_ ? 1 : 100), [this, generic] {
+        if (!running_.load() || (generic && !bqueue_.empty())) return true;
         if (!arena_handler_) return false;
         std::lock_guard<std::mutex> a(amu_);
         for (const auto& s : slots_)
@@ -374,7 +375,7 @@ void RpcServer::batch_loop() {
         return false;
       });
       if (!running_.load()) return;
-      if (bqueue_.empty()) continue;
+      if (!generic || bqueue_.empty()) continue;
       const std::string method = bqueue_.front().method;
       for (auto it = bqueue_.begin(); it != bqueue_.end() && batch.size() < max_batch_;) {
         if (it->method == method) {
@@ -462,9 +463,9 @@ void RpcServer::start() {
     });
   if (batch_handler_ || arena_handler_)
     for (int i = 0; i < nbatch_; ++i)
-      batchers_.emplace_back([this] {
+      batchers_.emplace_back([this, i] {
         pthread_setname_np(pthread_self(), "jb-rpc-batch");
-        batch_loop();
+        batch_loop(i);
       });
 }
 

@@ -80,8 +80,17 @@ class RecvBuf {
   void produced(size_t n) { tail_ += n; }
   void consume(size_t n) {
     head_ += n;
-    if (head_ == tail_) head_ = tail_ = 0;
+    if (head_ == tail_) {
+      head_ = tail_ = 0;
+      // one large request must not pin its buffer for the connection's
+      // lifetime: drop back to the steady-state size once drained
+      if (cap_ > kShrinkAbove) {
+        d_.reset();
+        cap_ = 0;
+      }
+    }
   }
+  static constexpr size_t kShrinkAbove = (size_t)4 << 20;
 
  private:
   std::unique_ptr<uint8_t[]> d_;
@@ -163,7 +172,9 @@ class RpcServer {
   void close_conn(uint64_t id);
   void send_response(uint64_t conn_id, const std::string& bytes);
   void send_responses(const std::vector<uint64_t>& conn_ids, const std::vector<std::string>& resp);
-  void batch_loop();
+  // idx 0 also serves the generic batch queue (one thread, so batched
+  // requests are handled in arrival order); the others take arena slots only
+  void batch_loop(int idx);
   void enqueue(RpcRequest&& req);
   bool arena_take(uint64_t conn_id, uint32_t msgid, const uint8_t* body, size_t len);
   bool arena_batch_once();

@@ -131,11 +131,23 @@ class LinearClassifier:
         # label re-layout): the next MIX is dense
         self._touched_valid = True
         self._last_mix: dict = {}
+        self._mix_job = None      # TableMix of an overlapped MIX in flight
         self._alloc(LABEL_CAPS[0])
 
     # ------------------------------------------------------------ storage
+    def _tables_replaced(self) -> None:
+        """the W / P tensors (or their contents, on a load) change outside the
+        train path: an overlapped MIX in flight must not fold its result into
+        them (its snapshot describes the old tables), and the touched map no
+        longer tells which rows differ across ranks, so the next MIX is dense"""
+        job = self._mix_job
+        if job is not None:
+            job.abandon()
+        self._touched_valid = False
+
     def _alloc(self, LC: int) -> None:
         H = self.H
+        self._tables_replaced()
         if self.gpu:
             t = self.torch
             W = t.zeros((H, LC), dtype=t.float32, device=self.device)
@@ -565,6 +577,7 @@ class LinearClassifier:
             if i < 0:
                 return False
             self.labels.remove(label)
+            self._tables_replaced()
             self.W[:, i] = 0.0
             if self.P is not None:
                 self.P[:, i] = 1.0
@@ -639,6 +652,7 @@ class LinearClassifier:
                 self.labels.get_or_add(name)
                 self.labels.set_count(i, int(cnt))
             self._sync_labels()
+            self._tables_replaced()
             rows = np.frombuffer(obj["rows"], dtype=np.int64)
             L = len(labels)
             Wr = np.frombuffer(obj["W"], dtype=np.float32).reshape(len(rows), L)
@@ -692,8 +706,8 @@ class LinearClassifier:
         for c, n in enumerate(order):
             self.labels.get_or_add(n)
             self.labels.set_count(c, counts.get(n, 0))
+        self._tables_replaced()
         self.W, self.P, self.LC = W, P, LC
-        self._touched_valid = False
         self.active = (self.torch.zeros(LC, dtype=self.torch.int32, device=self.device)
                        if self.gpu else np.zeros(LC, dtype=np.int32))
         self._label_version = -1
@@ -787,6 +801,7 @@ class LinearClassifier:
             meta_cnt = torch.from_numpy(cur - b).to(mdev)
             works = [dist_all_reduce(meta_cnt, "sum", mg)]
             job = self._table_mix(group)
+            self._mix_job = job
             return {"group": group, "names": names, "cur": cur, "base": b,
                     "meta": works, "meta_cnt": meta_cnt, "job": job}
 
@@ -807,14 +822,24 @@ class LinearClassifier:
                 w.wait()
         with self._lock:
             self._drain(block=False)   # batches still in flight join the next MIX
-            nbytes = h["job"].end()
-            self._last_mix = h["job"].stats()
+            job = h["job"]
+            nbytes = job.end()         # (no fold if the tables were replaced meanwhile)
+            if self._mix_job is job:
+                self._mix_job = None
+            self._last_mix = job.stats()
             names, cur, b = h["names"], h["cur"], h["base"]
             new_base = b + h["meta_cnt"].cpu().numpy()
+            # keyed by label name: a clear / load / re-layout between begin and
+            # end moves or removes columns; labels that are gone are skipped
+            base = {}
             for i, nm in enumerate(names):
-                since = int(self.labels.count(i)) - int(cur[i])
-                self.labels.set_count(i, int(max(0, new_base[i] + since)))
-            self._count_base = {nm: int(max(0, new_base[i])) for i, nm in enumerate(names)}
+                j = self.labels.lookup(nm)
+                if j < 0:
+                    continue
+                since = int(self.labels.count(j)) - int(cur[i])
+                self.labels.set_count(j, int(max(0, new_base[i] + since)))
+                base[nm] = int(max(0, new_base[i]))
+            self._count_base = base
             return nbytes + self._mix_weights(h.get("group"))
 
     def _tables(self) -> list:
@@ -878,10 +903,10 @@ class LinearClassifier:
                 for shp in shapes:
                     dist.broadcast(torch.empty(shp, dtype=torch.float32, device=dev), src=src)
                 return
+            self._tables_replaced()
             for t in self._tables():
                 dist.broadcast(t, src=src)
             self._count_base = {n: int(c) for n, c in zip(names, counts)}
-            self._touched_valid = False
 
     def pair_mix(self, peer: int) -> None:
         """push_mixer exchange with one peer: agree on the label layout, then
@@ -902,6 +927,7 @@ class LinearClassifier:
                         order.append(n)
             if order != self.labels.names() or not all(self.labels.alive()):
                 self._reorder_labels(order)
+            self._tables_replaced()
             for t in self._tables():
                 buf = torch.empty_like(t)
                 ops = [dist.P2POp(dist.isend, t, peer), dist.P2POp(dist.irecv, buf, peer)]

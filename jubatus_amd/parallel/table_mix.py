@@ -69,6 +69,7 @@ class TableMix:
         self._next_row = 0         # dense: first row not launched yet
         self._inflight: list = []  # dense: (r0, r1, snap, red, work)
         self._done = False
+        self.abandoned = False     # tables replaced meanwhile: run the collectives, fold nothing
 
     # ----------------------------------------------------------- begin
     def begin(self) -> "TableMix":
@@ -136,7 +137,15 @@ class TableMix:
         work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight.append((r0, r1, snap, red, work))
 
+    def abandon(self) -> None:
+        """The owner replaced (or reloaded) its tables while this MIX was in
+        flight: the remaining collectives still run (every rank must issue
+        the same sequence), but no result is folded into the tables"""
+        self.abandoned = True
+
     def _fold(self, r0: int, r1: int, snap: torch.Tensor, red: torch.Tensor) -> None:
+        if self.abandoned:
+            return
         upd = red.mul_(1.0 / self.n).sub_(snap)
         c0 = 0
         for t in self.tables:
@@ -179,15 +188,17 @@ class TableMix:
         elif self._sparse is not None:
             rows, snap, red, work = self._sparse
             work.wait()
-            upd = red.mul_(1.0 / self.n).sub_(snap)
-            c0 = 0
-            for t in self.tables:
-                w = t[0].numel()
-                t.view(self.H, -1).index_add_(0, rows, upd[:, c0:c0 + w])
-                c0 += w
+            if not self.abandoned:
+                upd = red.mul_(1.0 / self.n).sub_(snap)
+                c0 = 0
+                for t in self.tables:
+                    w = t[0].numel()
+                    t.view(self.H, -1).index_add_(0, rows, upd[:, c0:c0 + w])
+                    c0 += w
             self._sparse = None
         self._done = True
         return self.nbytes
 
     def stats(self) -> dict:
-        return {"mode": self.mode, "rows": self.rows, "bytes": self.nbytes}
+        return {"mode": self.mode, "rows": self.rows, "bytes": self.nbytes,
+                "abandoned": self.abandoned}

@@ -424,26 +424,3 @@ def test_topk_16_wave_path_matches_full_sort(k):
     order = np.argsort(ref, kind="stable")[:k]
     assert row[0].cpu().numpy().tolist() == order.tolist()
     np.testing.assert_allclose(dist[0].cpu().numpy(), ref[order], rtol=1e-6)
-
-
-def test_topk_forced_variants_match_default():
-    """JB_TOPK_NW=16 / JB_TOPK_MERGE=tile are read once per process (static):
-    run them in child processes against the default path"""
-    import json
-    import os
-    import subprocess
-    import sys
-    code = ("import json,torch,numpy as np;from jubatus_amd.ops import hip;"
-            "d=torch.device('cuda',0);g=torch.Generator(device=d).manual_seed(5);"
-            "n=300000;tb=torch.randint(0,1<<16,(n,1),generator=g,device=d,dtype=torch.int64);"
-            "tn=torch.ones(n,device=d);v=torch.ones(n,dtype=torch.uint8,device=d);"
-            "qb=torch.randint(0,1<<16,(3,1),generator=g,device=d,dtype=torch.int64);"
-            "qn=torch.ones(3,device=d);dd,rr=hip.topk_hamming(qb,qn,3,tb,tn,v,n,16,0,10);"
-            "print(json.dumps(rr.cpu().numpy().tolist()))")
-    outs = []
-    for env in ({}, {"JB_TOPK_NW": "16"}, {"JB_TOPK_MERGE": "tile"}, {"JB_TOPK_WQ_OFF": "1"}):
-        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env),
-                           capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stderr[-2000:]
-        outs.append(json.loads(r.stdout.strip().splitlines()[-1]))
-    assert outs[0] == outs[1] == outs[2] == outs[3]

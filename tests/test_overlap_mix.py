@@ -21,7 +21,7 @@ def _port():
     return p
 
 
-def _worker(rank, port, q, mismatch):
+def _worker(rank, port, q, mismatch, grow=False):
     import torch.distributed as dist
     os.environ.setdefault("JUBATUS_FORCE_CPU", "1")
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
@@ -37,9 +37,23 @@ def _worker(rank, port, q, mismatch):
     snapW, snapP = clf.W.copy(), clf.P.copy()
     h = clf.mix_begin()
     late = [("a", {"x": "late", "n": 1.0})] if rank == 1 and not mismatch else []
+    if grow and rank == 1:               # 9 labels: the label capacity grows 8 -> 16
+        late = [(f"g{i}", {"x": "late", "n": 1.0}) for i in range(7)]
     clf.train(late)                      # keeps going while the collective runs
     W_after, P_after = clf.W.copy(), clf.P.copy()
     clf.mix_end(h)
+    if grow:
+        # rank 1 replaced its tables during the collective: nothing folded in;
+        # the next (synchronous) MIX reconciles both ranks
+        stats = dict(clf._last_mix)
+        same = bool(np.array_equal(clf.W, W_after))
+        clf.mix()
+        out = [None, None]
+        dist.all_gather_object(out, (stats, same, clf.W.copy(), clf.get_labels()))
+        if rank == 0:
+            q.put(out)
+        dist.destroy_process_group()
+        return
     # every rank's snapshot, for the reference computation
     out = [None, None]
     dist.all_gather_object(out, (snapW, snapP, W_after, P_after, clf.W.copy(), clf.P.copy(),
@@ -72,3 +86,24 @@ def test_overlapped_mix(mismatch):
         # fell back to the synchronous MIX: one label layout, identical tables
         assert set(l0) == set(l1) == {"a", "b", "extra"}
         np.testing.assert_allclose(f0W, f1W, rtol=1e-6, atol=1e-7)
+
+
+def test_overlapped_mix_tables_replaced_during_collective():
+    """a train that grows the label capacity while the overlapped
+    MIX runs replaces W / P; mix_end must not fold the stale snapshot into
+    the new tables (the collectives still complete on both ranks)"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q, False, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (st0, same0, W0, l0), (st1, same1, W1, l1) = res
+    assert st1["abandoned"] and same1          # rank 1: no fold into the new tables
+    assert not st0["abandoned"] and not same0  # rank 0 folded the mean
+    assert l0 == l1 and len(l0) == 9
+    np.testing.assert_allclose(W0, W1, rtol=1e-6, atol=1e-7)
