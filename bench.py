@@ -402,8 +402,10 @@ def main() -> None:
     ap.add_argument("--rpc-threads", type=int, default=32,
                     help="server RPC threads (a quarter of them are epoll IO threads)")
     ap.add_argument("--rpc-distinct", type=int, default=512, help="distinct train requests cycled")
-    ap.add_argument("--update-mode", choices=("atomic", "hogwild"), default="atomic",
-                    help="how concurrent request streams update shared rows")
+    ap.add_argument("--update-mode", choices=("exact", "atomic", "hogwild"), default="exact",
+                    help="how the concurrent requests of a batch update the model: exact = the "
+                         "result of applying them one after the other (csrc/hip/serial.hip); "
+                         "atomic / hogwild = lock-free concurrent streams")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: rehearse the multi-rank GPU path with several ranks on one GPU "
                          "(not a benchmark configuration)")

@@ -163,6 +163,11 @@ SERVERS = {
                        ["server", "native", "hip"]),
     "jubaregression": (["server/jubaregression.cpp", "native/jb_rpc.cpp"],
                        ["server", "native", "hip"]),
+    # row engines over the LSH / inverted-index kernels (jb_row_server.hpp)
+    "jubarecommender": (["server/jubarecommender.cpp", "native/jb_rpc.cpp"],
+                        ["server", "native", "hip"]),
+    "jubanearest_neighbor": (["server/jubanearest_neighbor.cpp", "native/jb_rpc.cpp"],
+                             ["server", "native", "hip"]),
     # host engines: no GPU, no HIP libraries
     "jubastat": (["server/jubastat.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),

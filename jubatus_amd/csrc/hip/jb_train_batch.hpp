@@ -68,6 +68,9 @@ struct JbTrainBatch {
   int64_t mode, merge_every, hot_waves;
   unsigned long long* stats;
   uint8_t* touched;
+  // mode kSerial: scratch of jb_serial_scratch_bytes(n) bytes (serial.hip)
+  void* serial_scratch;
+  int64_t serial_bytes;
 };
 
 extern "C" int64_t jb_train_batch_args_bytes();

@@ -39,59 +39,6 @@
 
 namespace jb {
 
-enum Method : int { PERCEPTRON = 0, PA = 1, PA1 = 2, PA2 = 3, CW = 4, AROW = 5, NHERD = 6 };
-enum UpdateMode : int { kExact = 0, kAtomic = 1, kHogwild = 2 };
-
-// step sizes of one update; returns false when the sample causes no update.
-// W += tau * (S) * x ; precision increments use beta (see header).
-__device__ __forceinline__ bool step_coeffs(int method, float margin, float var, float nrm,
-                                            bool has_l, float C, float* tau, float* beta) {
-  switch (method) {
-    case PERCEPTRON:
-      if (margin <= 0.f) { *tau = 1.f; *beta = 0.f; return true; }
-      return false;
-    case PA: case PA1: case PA2: {
-      const float loss = 1.f - margin;
-      if (!(loss > 0.f && nrm > 0.f)) return false;
-      const float sq = (has_l ? 2.f : 1.f) * nrm;
-      if (method == PA) *tau = loss / sq;
-      else if (method == PA1) *tau = fminf(C, loss / sq);
-      else *tau = loss / (sq + 0.5f / C);
-      *beta = 0.f;
-      return true;
-    }
-    case CW: {
-      if (!(var > 0.f)) return false;
-      const float phi = C;
-      const float b = 1.f + 2.f * phi * margin;
-      const float disc = b * b - 8.f * phi * (margin - phi * var);
-      const float gamma = (-b + sqrtf(fmaxf(disc, 0.f))) / (4.f * phi * var);
-      if (!(gamma > 0.f)) return false;
-      *tau = gamma; *beta = 2.f * gamma * phi;
-      return true;
-    }
-    case AROW:
-      if (!(margin < 1.f)) return false;
-      *beta = 1.f / (var + 1.f / C);
-      *tau = (1.f - margin) * *beta;
-      return true;
-    case NHERD: {
-      if (!(margin < 1.f)) return false;
-      *tau = (1.f - margin) / (var + 1.f / C);
-      const float cv = 1.f + C * var;
-      *beta = (C * C * var + 2.f * C) / (cv * cv);
-      return true;
-    }
-    default: return false;
-  }
-}
-
-// precision increment for one (feature, label): s = 1/P before the update
-__device__ __forceinline__ float dprec(int method, float beta, float x, float s) {
-  const float bx2 = beta * x * x;
-  return method == CW ? bx2 : bx2 / (1.f - bx2 * s);
-}
-
 // apply the update of one feature (lane-per-feature form)
 template <int LC, int MODE>
 __device__ __forceinline__ void apply_feature(float* W, float* P, int32_t idx, float x, int y,
@@ -114,17 +61,6 @@ __device__ __forceinline__ void apply_feature(float* W, float* P, int32_t idx, f
       P[row + y] = 1.f / a + dprec(method, beta, x, a);
       if (lstar >= 0) P[row + lstar] = 1.f / b + dprec(method, beta, x, b);
     }
-  }
-}
-
-// best wrong label among the lanes of one feature group (lowest index on ties)
-template <int LW>
-__device__ __forceinline__ void argmax_wrong(float& best, int& bl) {
-#pragma unroll
-  for (int off = 1; off < LW; off <<= 1) {
-    const float ob = __shfl_xor(best, off, 64);
-    const int ol = __shfl_xor(bl, off, 64);
-    if (ol >= 0 && (bl < 0 || ob > best || (ob == best && ol < bl))) { best = ob; bl = ol; }
   }
 }
 
@@ -943,13 +879,41 @@ __global__ void mix_apply_kernel(float* __restrict__ w, const float* __restrict_
 // delta shards (jb_hot_rep_bytes(), zero-initialised once, left zero). stats (device,
 // 2 x u64, nullable): += samples that updated, samples with a valid label.
 // touched (device, H bytes, nullable): set to 1 for every row an update wrote.
+// mode kSerial (several streams, serial-equivalent result, serial.hip) needs
+// n_max >= the batch's sample count and scratch of jb_serial_scratch_bytes(n_max).
+extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max);
+extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
+                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
+                                 int method, float C, unsigned long long* stats, uint8_t* touched,
+                                 void* scratch, int64_t scratch_bytes, int bail_after,
+                                 hipStream_t stream);
+// exact steps per 1024-sample committer round past which the rest of a
+// kSerial batch goes to the sequential kernel (an exact step costs a few
+// times a sequential sample; see serial.hip)
+constexpr int kSerialBail = 128;
+
 extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                float* W, float* S, const int32_t* active, int LC, int method,
                                float C, int mode, const int32_t* hot_rows, const int32_t* hot_n,
                                float* hot_rep, int merge_every, int hot_waves,
-                               unsigned long long* stats, uint8_t* touched, hipStream_t stream) {
+                               unsigned long long* stats, uint8_t* touched, int64_t n_max,
+                               void* scratch, int64_t scratch_bytes, hipStream_t stream) {
   if (nstreams <= 0) return 0;
+  if (mode == jb::kSerial && nstreams == 1) mode = jb::kExact;
+  if (mode == jb::kExact && nstreams > 1) mode = jb::kSerial;   // exact means serial-equivalent
+  if (mode == jb::kSerial) {
+    // score + ordered commit, then the sequential kernel over what is left
+    const int rc = jb_serial_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W,
+                                     S, active, LC, method, C, stats, touched, scratch,
+                                     scratch_bytes, kSerialBail, stream);
+    if (rc != 0) return rc;
+    stream_ptr = (const int64_t*)scratch;
+    nstreams = 1;
+    mode = jb::kExact;
+    hot_rows = nullptr;
+  }
   const int threads = 256;
   const int blocks = (nstreams * 64 + threads - 1) / threads;
   const bool hot = hot_rows != nullptr && hot_n != nullptr && hot_rep != nullptr &&

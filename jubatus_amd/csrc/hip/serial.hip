@@ -1,0 +1,409 @@
+// Serial-equivalent training of many concurrent train requests (update mode
+// kSerial): the result is exactly that of applying the batch's samples one
+// after the other in request order - request 0's samples, then request 1's,
+// ... - i.e. one valid serialization of concurrent train RPCs against the
+// reference's classifier, whose driver applies every sample to the model
+// left by the previous one (jubatus/server/server/classifier_serv.cpp:138-144).
+//
+// Online updates are sequential, but on a trained model most samples do not
+// update it (their margin clears the loss threshold), and a sample that does
+// not update leaves the model unchanged. So:
+//
+//   1. serial_score_kernel (whole GPU, one wave per sample): every sample is
+//      scored against the model at the start of the batch (M0) and gets its
+//      *slack*: how far its margin is from the update threshold of the method
+//      (< 0: it would update under M0).
+//   2. serial_commit_kernel (one 1024-thread workgroup) walks the batch in
+//      order, 1024 samples per round. It keeps, in LDS, D[f] = the summed
+//      magnitude of every increment the batch has applied to row f so far.
+//      A sample j's margin can have moved by at most 2 * sum_f |x_jf| D[f]
+//      since M0 (each label score moves by at most sum_f |x_jf| D[f]), so if
+//      that bound is below its slack its decision under the current model is
+//      the one it had under M0 - no update - and it is settled without
+//      touching the table. The first sample of the round that is not settled
+//      this way is applied *exactly* (one wave rescoring it against the live
+//      table, as the single-stream path would), D grows by its increments,
+//      and the rest of the round is re-checked against the new D.
+//   3. When the batch updates too much for this to pay (a round with many
+//      exact steps, or the D table full), the committer stops and the rest of
+//      the batch runs through the single-stream exact pipelined kernel
+//      (linear.hip, kExact) - the plain sequential update.
+//
+// Rounding: the M0 margin and the exact rescoring sum in different orders, so
+// the slack keeps a relative guard band (kSlackGuard) - a sample within it of
+// the threshold always takes the exact step.
+#include "jb_linear.hpp"
+
+namespace jb {
+
+constexpr int kCommitThreads = 1024;
+constexpr int kDCap = 8192;          // D table slots (LDS hash, power of two)
+constexpr int kDBits = 13;
+constexpr int kDProbe = 32;          // linear-probe limit (a miss past it saturates)
+constexpr int kDFull = kDCap * 3 / 4;
+constexpr int kSerialNF = 16;        // features of a sample kept in registers
+constexpr float kSlackGuard = 1e-4f; // relative guard band of the slack
+
+// scores of all labels of one sample with plain (L1-cached) loads: the
+// score pass reads a table nothing writes during the kernel
+template <int LC>
+__device__ __forceinline__ void sample_scores_ro(const int32_t* __restrict__ fidx,
+                                                 const float* __restrict__ fval, int64_t beg, int n,
+                                                 const float* __restrict__ W, int lane,
+                                                 float (&acc)[Lanes<LC>::K]) {
+  using L = Lanes<LC>;
+  const int g = lane / L::LW;
+  const int l0 = lane % L::LW;
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) acc[k] = 0.f;
+  for (int j = g; j < n; j += L::G) {
+    const int32_t idx = fidx[beg + j];
+    const float x = fval[beg + j];
+    if (idx >= 0) {
+      const float* wr = W + (int64_t)idx * LC + l0;
+#pragma unroll
+      for (int k = 0; k < L::K; ++k) acc[k] += x * wr[64 * k];
+    }
+  }
+#pragma unroll
+  for (int off = L::LW; off < 64; off <<= 1) {
+#pragma unroll
+    for (int k = 0; k < L::K; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
+  }
+}
+
+// margin = score(y) - best wrong active label (0 when there is none);
+// every lane gets the result
+template <int LC>
+__device__ __forceinline__ float margin_of(const float (&acc)[Lanes<LC>::K], int y,
+                                           const bool (&act)[Lanes<LC>::K], int lane, int* lstar,
+                                           float* sy_out, float* best_out) {
+  using L = Lanes<LC>;
+  const int l0 = lane % L::LW;
+  float sy = 0.f, best = -INFINITY;
+  int bl = -1;
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) {
+    const int l = l0 + 64 * k;
+    if (l == y) sy = acc[k];
+    if (act[k] && l != y && acc[k] > best) { best = acc[k]; bl = l; }
+  }
+  sy = __shfl(sy, y % L::LW, 64);
+  argmax_wrong<L::LW>(best, bl);
+  *lstar = bl;
+  *sy_out = sy;
+  *best_out = bl >= 0 ? best : 0.f;
+  return sy - (bl >= 0 ? best : 0.f);
+}
+
+// Slack of one sample's decision (see header): >= 0 how far its margin may
+// move before its update decision changes, < 0 it updates under this model,
+// +inf it can never update (no features), NaN: not a trainable sample.
+__device__ __forceinline__ float decision_slack(int method, float margin, float nrm, bool has_l,
+                                                float C, float sy, float best) {
+  float s;
+  switch (method) {
+    case PERCEPTRON: s = margin; break;               // updates iff margin <= 0
+    case PA: case PA1: case PA2:
+      if (!(nrm > 0.f)) return INFINITY;
+      s = margin - 1.f;                               // updates iff margin < 1
+      break;
+    case CW: {
+      // updates iff margin < phi * var; var <= (2 or 1) * |x|^2 since P >= 1
+      if (!(nrm > 0.f)) return INFINITY;
+      s = margin - C * (has_l ? 2.f : 1.f) * nrm;
+      break;
+    }
+    default:                                          // AROW, NHERD: margin < 1
+      s = margin - 1.f;
+      break;
+  }
+  const float guard = kSlackGuard * (1.f + fabsf(sy) + fabsf(best));
+  if (method == PERCEPTRON ? !(s > guard) : !(s >= guard)) return -1.f;
+  return s - guard;
+}
+
+template <int LC>
+__global__ __launch_bounds__(256) void serial_score_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
+    const float* __restrict__ fval, const int32_t* __restrict__ labels,
+    const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
+    const int32_t* __restrict__ active, int method, float C, float* __restrict__ slack) {
+  using L = Lanes<LC>;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t beg = stream_ptr[0];
+  const int64_t s = beg + wid;
+  if (s >= stream_ptr[nstreams]) return;
+  const int y = labels[s];
+  if (y < 0 || y >= LC) {
+    if (lane == 0) slack[wid] = NAN;
+    return;
+  }
+  bool act[L::K];
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
+  const int64_t fb = row_ptr[s];
+  const int n = (int)(row_ptr[s + 1] - fb);
+  float acc[L::K];
+  sample_scores_ro<LC>(fidx, fval, fb, n, W, lane, acc);
+  int lstar;
+  float sy, best;
+  const float margin = margin_of<LC>(acc, y, act, lane, &lstar, &sy, &best);
+  float nrm = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    const float x = fval[fb + j];
+    if (fidx[fb + j] >= 0) nrm += x * x;
+  }
+  nrm = wave_sum(nrm);
+  if (lane == 0) slack[wid] = decision_slack(method, margin, nrm, lstar >= 0, C, sy, best);
+}
+
+// ------------------------------------------------------------ D table (LDS)
+struct DTable {
+  int32_t* key;
+  float* val;
+  int* nkeys;
+  int* sat;
+
+  __device__ __forceinline__ static uint32_t slot(int32_t idx) {
+    return ((uint32_t)idx * 0x9E3779B1u) >> (32 - kDBits);
+  }
+  __device__ __forceinline__ float get(int32_t idx) const {
+    uint32_t h = slot(idx);
+    for (int p = 0; p < kDProbe; ++p) {
+      const int32_t k = key[h];
+      if (k == idx) return val[h];
+      if (k < 0) return 0.f;
+      h = (h + 1) & (kDCap - 1);
+    }
+    return 0.f;   // never inserted past the probe limit (that saturates instead)
+  }
+  __device__ __forceinline__ void add(int32_t idx, float v) {
+    uint32_t h = slot(idx);
+    for (int p = 0; p < kDProbe; ++p) {
+      const int32_t old = atomicCAS(&key[h], -1, idx);
+      if (old == -1 || old == idx) {
+        atomicAdd(&val[h], v);
+        if (old == -1 && atomicAdd(nkeys, 1) + 1 >= kDFull) *sat = 1;
+        return;
+      }
+      h = (h + 1) & (kDCap - 1);
+    }
+    *sat = 1;
+  }
+};
+
+// Exact step of one sample against the live table (one wave; the committer
+// is the only writer while it runs). The single-stream semantics of
+// linear.hip's direct path, plus the increment magnitudes into D. Returns
+// whether the sample updated.
+template <int LC>
+__device__ bool commit_sample(const int32_t* __restrict__ fidx, const float* __restrict__ fval,
+                              int64_t beg, int n, int y, float* W, float* P,
+                              const bool (&act)[Lanes<LC>::K], int lane, int method, float C,
+                              uint8_t* __restrict__ touched, DTable& d) {
+  const bool use_s = method >= CW;
+  float acc[Lanes<LC>::K];
+  sample_scores<LC>(fidx, fval, beg, n, W, lane, acc);     // agent-scope loads
+  int lstar;
+  float sy, best;
+  const float margin = margin_of<LC>(acc, y, act, lane, &lstar, &sy, &best);
+  float var = 0.f, nrm = 0.f;
+  for (int j = lane; j < n; j += 64) {
+    const int32_t idx = fidx[beg + j];
+    const float x = fval[beg + j];
+    if (idx >= 0) {
+      const int64_t row = (int64_t)idx * LC;
+      nrm += x * x;
+      if (use_s) {
+        const float a = 1.f / ld_agent(P + row + y);
+        const float b = lstar >= 0 ? 1.f / ld_agent(P + row + lstar) : 0.f;
+        var += x * x * (a + b);
+      }
+    }
+  }
+  var = wave_sum(var);
+  nrm = wave_sum(nrm);
+  float tau = 0.f, beta = 0.f;
+  if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return false;
+  for (int j = lane; j < n; j += 64) {
+    const int32_t idx = fidx[beg + j];
+    if (idx < 0) continue;
+    const float x = fval[beg + j];
+    const int64_t row = (int64_t)idx * LC;
+    const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
+    const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
+    const float dwy = tau * a * x;
+    const float dwl = lstar >= 0 ? -tau * b * x : 0.f;
+    // atomics: a row repeated inside the sample counts every time, each
+    // occurrence against the pre-sample state (as the other paths)
+    atomicAdd(W + row + y, dwy);
+    if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+    if (use_s) {
+      atomicAdd(P + row + y, dprec(method, beta, x, a));
+      if (lstar >= 0) atomicAdd(P + row + lstar, dprec(method, beta, x, b));
+    }
+    if (touched != nullptr) touched[idx] = 1;
+    d.add(idx, fabsf(dwy) + fabsf(dwl));
+  }
+  return true;
+}
+
+// The ordered committer (see header). One workgroup of 1024 threads; thread t
+// owns sample p + t of the round starting at p. tail[0] receives the first
+// sample it did not settle (the end of the batch when it finished), tail[1]
+// the end of the batch: the exact single-stream kernel runs [tail[0], tail[1]).
+template <int LC>
+__global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
+    const float* __restrict__ fval, const int32_t* __restrict__ labels,
+    const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
+    const int32_t* __restrict__ active, int method, float C, const float* __restrict__ slack,
+    unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
+    int64_t* __restrict__ tail, int bail_after) {
+  using L = Lanes<LC>;
+  constexpr int T = kCommitThreads;
+  constexpr int NF = kSerialNF;
+  __shared__ int32_t s_key[kDCap];
+  __shared__ float s_val[kDCap];
+  __shared__ int s_first, s_sat, s_nkeys;
+  __shared__ unsigned s_valid;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  for (int i = tid; i < kDCap; i += T) {
+    s_key[i] = -1;
+    s_val[i] = 0.f;
+  }
+  if (tid == 0) {
+    s_sat = 0;
+    s_nkeys = 0;
+    s_valid = 0;
+  }
+  DTable d{s_key, s_val, &s_nkeys, &s_sat};
+  bool act[L::K];
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
+  __syncthreads();
+  const int64_t beg = stream_ptr[0];
+  const int64_t end = stream_ptr[nstreams];
+  unsigned n_upd = 0;
+  int64_t stop = end;
+  for (int64_t p = beg; p < end; p += T) {
+    const int64_t j = p + tid;
+    const bool live = j < end;
+    const float sl = live ? slack[j - beg] : NAN;
+    int64_t fb = 0;
+    int nf = 0;
+    if (live) {
+      fb = row_ptr[j];
+      nf = (int)(row_ptr[j + 1] - fb);
+    }
+    int32_t fi[NF];
+    float fx[NF];
+#pragma unroll
+    for (int u = 0; u < NF; ++u) {
+      const bool v = u < nf;
+      fi[u] = v ? fidx[fb + u] : -1;
+      fx[u] = v ? fabsf(fval[fb + u]) : 0.f;
+    }
+    // only finite, non-negative slacks can be settled by the bound
+    const bool open = live && !(sl != sl) && sl < INFINITY;
+    int lim = -1;          // round offsets <= lim are settled
+    int steps = 0;
+    for (;;) {
+      bool unsafe = false;
+      if (open && tid > lim) {
+        if (sl < 0.f || s_sat) {
+          unsafe = true;
+        } else {
+          float b = 0.f;
+#pragma unroll
+          for (int u = 0; u < NF; ++u)
+            if (fi[u] >= 0) b += fx[u] * d.get(fi[u]);
+          for (int u = NF; u < nf; ++u) {
+            const int32_t idx = fidx[fb + u];
+            if (idx >= 0) b += fabsf(fval[fb + u]) * d.get(idx);
+          }
+          unsafe = 2.f * b >= sl;
+        }
+      }
+      __syncthreads();     // every thread has read s_first / D of the last step
+      if (tid == 0) s_first = INT_MAX;
+      __syncthreads();
+      const uint64_t m = __builtin_amdgcn_ballot_w64(unsafe);
+      if (lane == 0 && m != 0) atomicMin(&s_first, wv * 64 + (int)__builtin_ctzll(m));
+      __syncthreads();
+      const int k = s_first;
+      if (k == INT_MAX) break;
+      if (wv == 0) {
+        const int64_t s = p + k;
+        const int64_t b0 = row_ptr[s];
+        if (commit_sample<LC>(fidx, fval, b0, (int)(row_ptr[s + 1] - b0), labels[s], W, P, act,
+                              lane, method, C, touched, d))
+          ++n_upd;
+        // the next exact step reads what this one wrote
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lim = k;
+      ++steps;
+      __syncthreads();     // D / s_sat of the step visible to every wave
+      if (s_sat || steps > bail_after) {
+        stop = p + k + 1;
+        break;
+      }
+    }
+    // samples of this round settled here (valid label)
+    const bool counted = live && !(sl != sl) && j < stop;
+    const uint64_t cm = __builtin_amdgcn_ballot_w64(counted);
+    if (lane == 0 && cm != 0) atomicAdd(&s_valid, (unsigned)__popcll(cm));
+    if (stop != end) break;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    tail[0] = stop;
+    tail[1] = end;
+    if (stats != nullptr && s_valid > 0) atomicAdd(stats + 1, (unsigned long long)s_valid);
+  }
+  if (tid == 0 && stats != nullptr && n_upd > 0) atomicAdd(stats, (unsigned long long)n_upd);
+}
+
+}  // namespace jb
+
+// bytes of the kSerial scratch for batches of up to n_max samples:
+// [tail int64 x 2, padded to 256 B][slack float x n_max]; n_max bounds the
+// batch's sample count stream_ptr[nstreams] - stream_ptr[0]
+extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max) {
+  return 256 + 4 * (n_max > 0 ? n_max : 1);
+}
+
+// Steps 1-2 of a kSerial batch (score, commit); the caller then runs the
+// exact single-stream kernel over stream_ptr = (int64_t*)scratch (step 3).
+// bail_after: exact steps per 1024-sample round past which the committer
+// hands the rest of the batch to the sequential kernel.
+extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
+                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
+                                 int method, float C, unsigned long long* stats, uint8_t* touched,
+                                 void* scratch, int64_t scratch_bytes, int bail_after,
+                                 hipStream_t stream) {
+  if (nstreams <= 0 || n_max <= 0) return 0;
+  if (scratch == nullptr || scratch_bytes < jb_serial_scratch_bytes(n_max)) return -3;
+  if (method >= jb::CW && S == nullptr) return -4;
+  int64_t* tail = (int64_t*)scratch;
+  float* slack = (float*)((uint8_t*)scratch + 256);
+  // (slack[i] belongs to sample stream_ptr[0] + i)
+  const int64_t blocks = (n_max * 64 + 255) / 256;
+  if (blocks > INT32_MAX) return -5;
+#define JB_SERIAL(L)                                                                              \
+  hipLaunchKernelGGL((jb::serial_score_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream,  \
+                     row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, active, method, C,     \
+                     slack);                                                                      \
+  hipLaunchKernelGGL((jb::serial_commit_kernel<L>), dim3(1), dim3(jb::kCommitThreads), 0, stream, \
+                     row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active, method, C,  \
+                     slack, stats, touched, tail, bail_after);
+  JB_LC_DISPATCH(LC, JB_SERIAL)
+#undef JB_SERIAL
+  return (int)hipGetLastError();
+}

@@ -39,7 +39,8 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
                                float* W, float* S, const int32_t* active, int LC, int method,
                                float C, int mode, const int32_t* hot_rows, const int32_t* hot_n,
                                float* hot_rep, int merge_every, int hot_waves,
-                               unsigned long long* stats, uint8_t* touched, hipStream_t stream);
+                               unsigned long long* stats, uint8_t* touched, int64_t n_max,
+                               void* scratch, int64_t scratch_bytes, hipStream_t stream);
 
 #include "jb_train_batch.hpp"
 
@@ -94,7 +95,8 @@ extern "C" int jb_train_batch_submit(const JbTrainBatch* a) {
                         (int)a->LC, (int)a->method, (float)a->C, (int)a->mode,
                         hot ? a->hot_rows : nullptr, hot ? a->hot_n : nullptr,
                         hot ? a->hot_rep : nullptr, (int)a->merge_every, (int)a->hot_waves,
-                        a->stats, a->touched, a->compute_stream) != 0)
+                        a->stats, a->touched, a->n, a->serial_scratch, a->serial_bytes,
+                        a->compute_stream) != 0)
       return 1;
     if (hot) JB_TRY(hipEventRecord(a->hot_free, a->compute_stream));
   }

@@ -1,0 +1,545 @@
+// The RPC server of the native row engines: jubarecommender and
+// jubanearest_neighbor (one binary each, csrc/server/juba{recommender,
+// nearest_neighbor}.cpp), no Python in the process.
+//
+// Reference: jubatus/server/server/recommender_serv.cpp:126-224,
+// recommender_impl.cpp (RPC table) and nearest_neighbor_serv.cpp:121-178,
+// nearest_neighbor_impl.cpp; the Python twins are server/recommender_serv.py
+// and server/nearest_neighbor_serv.py over models/recommender.py.
+//
+// Scope: standalone servers whose converter runs on the native hashers
+// (jb_row_engine.hpp Converter); other configurations, distributed mode,
+// --cpu and hosts without a GPU go to the Python server (exec before any GPU
+// call). Every call takes the engine lock (the Python driver's RLock).
+#pragma once
+#include <time.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "jb_msgpack.hpp"
+#include "jb_row_engine.hpp"
+#include "jb_rpc.hpp"
+#include "jb_server_common.hpp"
+#include "jb_value.hpp"
+
+namespace jb {
+namespace rowsrv {
+
+using namespace jb::srv;
+using jb::row::ArgError;
+using jb::row::Datum;
+using jb::row::Hit;
+using jb::row::RowEngine;
+
+constexpr int kCompleteK = 10;   // models/recommender.py COMPLETE_K
+
+enum class Kind { kRecommender, kNearestNeighbor };
+
+struct Config {
+  std::string text;
+  std::string outer;     // config "method" (status)
+  std::string inner;     // the similarity method of the index
+  Value param;           // parameters of the index (hash_num, seed, unlearner...)
+  Value conv;
+};
+
+inline bool is_lsh(const std::string& m) { return m == "lsh" || m == "euclid_lsh" || m == "minhash"; }
+
+// models/recommender.py Recommender / NearestNeighbor __init__ + the
+// converter check
+inline bool parse_config(Kind kind, const std::string& text, Config* c, std::string* why) {
+  Value v;
+  try {
+    v = jb::val::parse_json(text);
+  } catch (const std::exception& e) {
+    *why = e.what();
+    return false;
+  }
+  if (v.kind != Value::MAP) { *why = "configuration must be a JSON object"; return false; }
+  c->outer = v.str_or("method", "");
+  const Value* p = v.get("parameter");
+  Value empty;
+  empty.kind = Value::MAP;
+  c->param = p && p->kind == Value::MAP ? *p : empty;
+  c->inner = c->outer;
+  if (kind == Kind::kNearestNeighbor) {
+    if (!is_lsh(c->outer)) { *why = "nearest_neighbor method " + c->outer; return false; }
+  } else if (c->outer == "nearest_neighbor_recommender") {
+    c->inner = c->param.str_or("method", "");
+    if (!is_lsh(c->inner)) { *why = "nearest_neighbor_recommender inner method"; return false; }
+    // the unlearner of the outer parameters applies (Recommender.__init__)
+    Value inner = empty;
+    if (const Value* ip = c->param.get("parameter"))
+      if (ip->kind == Value::MAP) inner = *ip;
+    for (const char* k : {"unlearner", "unlearner_parameter"})
+      if (const Value* x = c->param.get(k)) inner.o.emplace_back(k, *x);
+    c->param = inner;
+  } else if (!is_lsh(c->outer) && c->outer != "inverted_index" && c->outer != "inverted_index_euclid") {
+    *why = "recommender method " + c->outer;
+    return false;
+  }
+  if (const Value* h = c->param.get("hash_num"))
+    if (!h->is_num() || h->num() <= 0) { *why = "hash_num"; return false; }
+  if (const Value* u = c->param.get("unlearner")) {
+    if (u->kind != Value::NIL && !(u->is_str() && u->s == "lru")) { *why = "unlearner"; return false; }
+    if (u->is_str()) {
+      const Value* up = c->param.get("unlearner_parameter");
+      const Value* ms = up ? up->get("max_size") : nullptr;
+      if (!ms || !ms->is_num() || ms->num() <= 0) { *why = "unlearner_parameter.max_size"; return false; }
+    }
+  }
+  const Value* conv = v.get("converter");
+  c->conv = conv ? *conv : empty;
+  jb::row::Converter probe;
+  if (!probe.configure(c->conv, why)) return false;
+  c->text = text;
+  return true;
+}
+
+class Model {
+ public:
+  std::atomic<uint64_t> update_count{0};
+  uint64_t clear_row_cnt = 0, update_row_cnt = 0;
+
+  Model(Kind kind, const Config& cfg, int device) : kind_(kind), device_(device) {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    configure(cfg);
+  }
+
+  void configure(const Config& cfg) {
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipStreamSynchronize(stream_));
+    eng_.reset(new RowEngine(cfg.inner, &cfg.param, stream_));
+    std::string why;
+    if (!eng_->conv.configure(cfg.conv, &why)) throw std::runtime_error("converter: " + why);
+    cfg_ = cfg;
+  }
+  const std::string& config_text() const { return cfg_.text; }
+
+  // ------------------------------------------------------------- updates
+  bool clear_row(const std::string& id) {
+    std::lock_guard<std::mutex> g(mu_);
+    ++update_count;
+    ++clear_row_cnt;
+    return eng_->remove(id);
+  }
+  // recommender update_row: merge into the stored datum (RowEngine.update_row)
+  bool update_row(const std::string& id, const Value& dv) {
+    Datum nd;
+    jb::row::parse_datum(dv, &nd);
+    std::lock_guard<std::mutex> g(mu_);
+    ++update_count;
+    ++update_row_cnt;
+    if (const jb::row::Row* r = eng_->find(id)) {
+      Datum m = r->d;
+      for (auto& kv : nd.sv) m.sv[kv.first] = kv.second;
+      for (auto& kv : nd.nv) m.nv[kv.first] = kv.second;
+      for (auto& kv : nd.bv) m.bv[kv.first] = kv.second;
+      nd = std::move(m);
+    }
+    eng_->set(id, std::move(nd));
+    return true;
+  }
+  // nearest_neighbor set_row: replace
+  bool set_row(const std::string& id, const Value& dv) {
+    Datum nd;
+    jb::row::parse_datum(dv, &nd);
+    std::lock_guard<std::mutex> g(mu_);
+    ++update_count;
+    eng_->set(id, std::move(nd));
+    return true;
+  }
+  void clear() {
+    std::lock_guard<std::mutex> g(mu_);
+    ++update_count;
+    clear_row_cnt = update_row_cnt = 0;
+    eng_->clear();
+  }
+
+  // ------------------------------------------------------------- queries
+  std::vector<std::pair<std::string, double>> query_id(const std::string& id, int64_t k, bool similar) {
+    std::lock_guard<std::mutex> g(mu_);
+    const int32_t s = eng_->slot(id);
+    if (s < 0) throw std::runtime_error("'row not found: " + id + "'");   // str(KeyError)
+    if (k <= 0) return {};
+    return eng_->results(eng_->query_slot(s, clamp_k(k)), similar);
+  }
+  std::vector<std::pair<std::string, double>> query_datum(const Value& dv, int64_t k, bool similar) {
+    Datum chk;
+    jb::row::parse_datum(dv, &chk);                  // validate first (ARGUMENT_ERROR)
+    MsgpackWriter w;
+    write_value(w, dv);
+    std::lock_guard<std::mutex> g(mu_);
+    if (eng_->nslots() == 0 || k <= 0) return {};
+    std::vector<int32_t> idx;
+    std::vector<float> val;
+    eng_->conv.hash((const uint8_t*)w.out.data(), w.out.size(), &idx, &val, false);
+    return eng_->results(eng_->query_fv(idx, val, clamp_k(k)), similar);
+  }
+
+  Datum decode_row(const std::string& id) {
+    std::lock_guard<std::mutex> g(mu_);
+    const jb::row::Row* r = eng_->find(id);
+    return r ? r->d : Datum();
+  }
+  std::vector<std::string> get_all_rows() {
+    std::lock_guard<std::mutex> g(mu_);
+    return eng_->all_ids();
+  }
+
+  // models/recommender.py complete_row_from_id / _from_datum / _complete
+  Datum complete_row_from_id(const std::string& id) {
+    std::lock_guard<std::mutex> g(mu_);
+    const jb::row::Row* r = eng_->find(id);
+    if (!r) return Datum();
+    const std::vector<int32_t> idx = r->idx;
+    const std::vector<float> val = r->val;
+    const std::map<std::string, double> base = r->d.nv;
+    auto nb = eng_->results(eng_->query_fv(idx, val, kCompleteK + 1), true);
+    std::vector<std::pair<std::string, double>> keep;
+    for (auto& x : nb)
+      if (x.first != id) keep.push_back(x);
+    if (keep.size() > (size_t)kCompleteK) keep.resize(kCompleteK);
+    return complete(base, keep);
+  }
+  Datum complete_row_from_datum(const Value& dv) {
+    Datum d;
+    jb::row::parse_datum(dv, &d);
+    auto nb = query_datum(dv, kCompleteK, true);
+    std::lock_guard<std::mutex> g(mu_);
+    return complete(d.nv, nb);
+  }
+
+  double calc_similarity(const Value& a, const Value& b) {
+    std::vector<int32_t> ai, bi;
+    std::vector<float> av, bv;
+    fv_of(a, &ai, &av);
+    fv_of(b, &bi, &bv);
+    std::lock_guard<std::mutex> g(mu_);
+    return eng_->calc_similarity(ai, av, bi, bv);
+  }
+  double calc_l2norm(const Value& a) {
+    std::vector<int32_t> ai;
+    std::vector<float> av;
+    fv_of(a, &ai, &av);
+    double s = 0.0;
+    for (size_t i = 0; i < ai.size(); ++i)
+      if (ai[i] >= 0) s += (double)av[i] * (double)av[i];
+    return sqrt(s);
+  }
+
+  // ------------------------------------------------------------ persist
+  std::string pack_user_data() {
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipStreamSynchronize(stream_));
+    MsgpackWriter u;
+    u.arr(2);
+    u.uint(1);
+    eng_->pack(u, eng_->method());
+    return std::move(u.out);
+  }
+  void unpack(const Value& obj) {
+    std::lock_guard<std::mutex> g(mu_);
+    eng_->unpack(obj);
+    HIPCHK(hipStreamSynchronize(stream_));
+  }
+
+  void status(std::vector<std::pair<std::string, std::string>>* st) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
+    add("method", kind_ == Kind::kRecommender ? cfg_.outer : eng_->method());
+    add("num_rows", std::to_string(eng_->size()));
+    add("storage", "hbm");
+    add("unlearner", eng_->lru() ? "lru" : "none");
+    add("device", "cuda:" + std::to_string(device_));
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) add("hbm_used_bytes", std::to_string(tot - fr));
+    add("server_runtime", "native");
+    if (kind_ == Kind::kRecommender) {
+      add("clear_row_cnt", std::to_string(clear_row_cnt));
+      add("update_row_cnt", std::to_string(update_row_cnt));
+    }
+  }
+
+ private:
+  int clamp_k(int64_t k) const { return (int)std::min<int64_t>(k, 1 << 30); }
+
+  void fv_of(const Value& dv, std::vector<int32_t>* idx, std::vector<float>* val) {
+    Datum chk;
+    jb::row::parse_datum(dv, &chk);
+    MsgpackWriter w;
+    write_value(w, dv);
+    std::lock_guard<std::mutex> g(mu_);
+    eng_->conv.hash((const uint8_t*)w.out.data(), w.out.size(), idx, val, false);
+  }
+
+  Datum complete(const std::map<std::string, double>& base,
+                 const std::vector<std::pair<std::string, double>>& nb) {
+    const std::string& m = eng_->method();
+    const bool raw_w = m == "inverted_index" || m == "lsh" || m == "minhash";
+    std::map<std::string, double> acc, wsum;
+    for (const auto& x : nb) {
+      const jb::row::Row* r = eng_->find(x.first);
+      if (!r) continue;
+      const double w = raw_w ? x.second : 1.0 / (1.0 + std::max(0.0, -x.second));
+      if (w <= 0) continue;
+      for (const auto& kv : r->d.nv) {
+        acc[kv.first] += w * kv.second;
+        wsum[kv.first] += w;
+      }
+    }
+    Datum out;
+    for (const auto& kv : acc)
+      if (wsum[kv.first] > 0) out.nv[kv.first] = kv.second / wsum[kv.first];
+    for (const auto& kv : base) out.nv[kv.first] = kv.second;
+    return out;
+  }
+
+  // re-encode a decoded datum Value (the query's own order kept)
+  static void write_value(MsgpackWriter& w, const Value& v) {
+    switch (v.kind) {
+      case Value::NIL: w.nil(); break;
+      case Value::BOOL: w.boolean(v.b); break;
+      case Value::INT: w.sint(v.i); break;
+      case Value::UINT: w.uint(v.u); break;
+      case Value::DBL: w.dbl(v.d); break;
+      case Value::STR: case Value::BIN: w.raw(v.s); break;
+      case Value::ARR:
+        w.arr(v.a.size());
+        for (const Value& x : v.a) write_value(w, x);
+        break;
+      case Value::MAP:
+        w.map(v.o.size());
+        for (const auto& kv : v.o) { w.raw(kv.first); write_value(w, kv.second); }
+        break;
+    }
+  }
+
+  Kind kind_;
+  int device_;
+  hipStream_t stream_;
+  std::mutex mu_;
+  Config cfg_;
+  std::unique_ptr<RowEngine> eng_;
+};
+
+inline void write_pairs(MsgpackWriter& w, const std::vector<std::pair<std::string, double>>& r) {
+  w.arr(r.size());
+  for (const auto& x : r) {
+    w.arr(2);
+    w.raw(x.first);
+    w.dbl(x.second);
+  }
+}
+
+class Server {
+ public:
+  Server(Kind kind, const Args& a, const Config& cfg, int device) : kind_(kind), a_(a) {
+    model_.reset(new Model(kind, cfg, device));
+  }
+
+  void load_file(const std::string& path) { load_impl(path, true); }
+
+  int run() {
+    rpc_.reset(new jb::RpcServer([this](const jb::RpcRequest& r) { return dispatch(r); }, a_.threads, 0.0));
+    rpc_->set_io_threads(std::max(1, a_.threads / 4));
+    int port;
+    try {
+      port = rpc_->listen(a_.bind, a_.port);
+    } catch (const std::exception& e) {
+      logf_("FATAL", "server failed to start: any process using port %d? (%s)", a_.port, e.what());
+      return 1;
+    }
+    a_.port = port;
+    logf_("INFO", "start listening at port %d", port);
+    cs_.start_time = time(nullptr);
+    rpc_->start();
+    logf_("INFO", "%s RPC server startup (native)", prog_name());
+    wait_for_term();
+    logf_("INFO", "stopping RPC server");
+    rpc_->stop();
+    return 0;
+  }
+
+ private:
+  std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
+  const char* type() const { return kind_ == Kind::kRecommender ? "recommender" : "nearest_neighbor"; }
+
+  std::string dispatch(const jb::RpcRequest& r) {
+    Value args;
+    try {
+      args = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
+    } catch (const std::exception&) {
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    }
+    if (args.kind != Value::ARR) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    const std::string& m = r.method;
+    // arity including the leading cluster name; argument kinds (s: string,
+    // d: datum, k: size)
+    static const std::vector<std::pair<std::string, std::string>> rec = {
+        {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
+        {"clear_row", "s"}, {"update_row", "sd"}, {"complete_row_from_id", "s"},
+        {"complete_row_from_datum", "d"}, {"similar_row_from_id", "sk"}, {"similar_row_from_datum", "dk"},
+        {"decode_row", "s"}, {"get_all_rows", ""}, {"calc_similarity", "dd"}, {"calc_l2norm", "d"}};
+    static const std::vector<std::pair<std::string, std::string>> nn = {
+        {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
+        {"set_row", "sd"}, {"neighbor_row_from_id", "sk"}, {"neighbor_row_from_datum", "dk"},
+        {"similar_row_from_id", "sk"}, {"similar_row_from_datum", "dk"}, {"get_all_rows", ""}};
+    const auto& table = kind_ == Kind::kRecommender ? rec : nn;
+    const std::string* sig = nullptr;
+    for (const auto& x : table)
+      if (x.first == m) sig = &x.second;
+    if (!sig) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
+    bool ok = args.a.size() == sig->size() + 1 && args.a[0].is_str();
+    for (size_t k = 0; ok && k < sig->size(); ++k) {
+      const Value& x = args.a[k + 1];
+      const char c = (*sig)[k];
+      ok = c == 's' ? x.is_str() : c == 'k' ? (x.kind == Value::INT || x.kind == Value::UINT) : x.kind == Value::ARR;
+    }
+    if (!ok) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    auto size_arg = [&](size_t i) -> int64_t {
+      const Value& x = args.a[i];
+      return x.kind == Value::UINT ? (int64_t)std::min<uint64_t>(x.u, (uint64_t)INT64_MAX) : x.i;
+    };
+    MsgpackWriter w;
+    try {
+      if (m == "get_config") {
+        w.raw(model_->config_text());
+      } else if (m == "clear") {
+        model_->clear();
+        w.boolean(true);
+      } else if (m == "clear_row") {
+        w.boolean(model_->clear_row(args.a[1].s));
+      } else if (m == "update_row") {
+        w.boolean(model_->update_row(args.a[1].s, args.a[2]));
+      } else if (m == "set_row") {
+        w.boolean(model_->set_row(args.a[1].s, args.a[2]));
+      } else if (m == "similar_row_from_id") {
+        write_pairs(w, model_->query_id(args.a[1].s, size_arg(2), true));
+      } else if (m == "neighbor_row_from_id") {
+        write_pairs(w, model_->query_id(args.a[1].s, size_arg(2), false));
+      } else if (m == "similar_row_from_datum") {
+        write_pairs(w, model_->query_datum(args.a[1], size_arg(2), true));
+      } else if (m == "neighbor_row_from_datum") {
+        write_pairs(w, model_->query_datum(args.a[1], size_arg(2), false));
+      } else if (m == "complete_row_from_id") {
+        jb::row::write_datum(w, model_->complete_row_from_id(args.a[1].s));
+      } else if (m == "complete_row_from_datum") {
+        jb::row::write_datum(w, model_->complete_row_from_datum(args.a[1]));
+      } else if (m == "decode_row") {
+        jb::row::write_datum(w, model_->decode_row(args.a[1].s));
+      } else if (m == "get_all_rows") {
+        const auto ids = model_->get_all_rows();
+        w.arr(ids.size());
+        for (const auto& s : ids) w.raw(s);
+      } else if (m == "calc_similarity") {
+        w.dbl(model_->calc_similarity(args.a[1], args.a[2]));
+      } else if (m == "calc_l2norm") {
+        w.dbl(model_->calc_l2norm(args.a[1]));
+      } else if (m == "save") {
+        const std::string& id = args.a[1].s;
+        if (id.empty()) throw std::runtime_error("empty id is not allowed");
+        const std::string path = local_path(id);
+        write_model_file(path, type(), id, model_->config_text(), model_->pack_user_data());
+        {
+          std::lock_guard<std::mutex> g(st_mu_);
+          cs_.last_saved = time(nullptr);
+          cs_.last_saved_path = path;
+        }
+        logf_("INFO", "saved to %s", path.c_str());
+        w.map(1);
+        w.raw(ident());
+        w.raw(path);
+      } else if (m == "load") {
+        if (args.a[1].s.empty()) throw std::runtime_error("empty id is not allowed");
+        load_impl(local_path(args.a[1].s), false);
+        w.boolean(true);
+      } else if (m == "get_status") {
+        std::vector<std::pair<std::string, std::string>> st;
+        {
+          std::lock_guard<std::mutex> g(st_mu_);
+          common_status(a_, cs_, model_->update_count.load(), &st);
+        }
+        model_->status(&st);
+        w.map(1);
+        w.raw(ident());
+        w.map(st.size());
+        for (auto& kv : st) { w.raw(kv.first); w.raw(kv.second); }
+      }
+    } catch (const ArgError&) {
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+    } catch (const std::exception& e) {
+      return r.notify ? std::string() : jb::val::response_msg(r.msgid, e.what());
+    }
+    return r.notify ? std::string() : jb::val::response_ok(r.msgid, w.out);
+  }
+
+  std::string local_path(const std::string& id) const {
+    return a_.datadir + "/" + a_.eth + "_" + std::to_string(a_.port) + "_" + type() + "_" + id + ".jubatus";
+  }
+
+  void load_impl(const std::string& path, bool overwrite_config) {
+    std::string bytes;
+    if (!read_file(path, &bytes)) throw std::runtime_error("cannot open input file: " + path + ": " + strerror(errno));
+    ModelFile mf;
+    const std::string err = read_model_file(bytes, &mf);
+    if (!err.empty()) throw std::runtime_error(err);
+    if (mf.type != type())
+      throw std::runtime_error("invalid model type: saved type: " + mf.type + ", expected type: " + type());
+    const std::string current = model_->config_text();
+    if (!overwrite_config && !jb::val::same_config(mf.config, current))
+      throw std::runtime_error("model config mismatched with the running config");
+    if (mf.user_version != 1)
+      throw std::runtime_error("user data version mismatched: " + std::to_string(mf.user_version) +
+                               ", current version: 1");
+    if (overwrite_config && !jb::val::same_config(mf.config, current)) {
+      Config cfg;
+      std::string why;
+      if (!parse_config(kind_, mf.config, &cfg, &why)) throw std::runtime_error("model config is not served natively: " + why);
+      model_->configure(cfg);
+    }
+    model_->unpack(mf.user);
+    std::lock_guard<std::mutex> g(st_mu_);
+    cs_.last_loaded = time(nullptr);
+    cs_.last_loaded_path = path;
+    logf_("INFO", "loaded from %s", path.c_str());
+  }
+
+  Kind kind_;
+  Args a_;
+  std::unique_ptr<Model> model_;
+  std::unique_ptr<jb::RpcServer> rpc_;
+  std::mutex st_mu_;
+  CommonStatus cs_;
+};
+
+inline int row_main(int argc, char** argv, Kind kind) {
+  set_engine(kind == Kind::kRecommender ? "recommender" : "nearest_neighbor");
+  Args a;
+  std::string text;
+  Config cfg;
+  const int rc = startup(argc, argv, &a, &text, [&cfg, kind](const std::string& t, std::string* why) {
+    return parse_config(kind, t, &cfg, why);
+  });
+  if (rc >= 0) return rc;
+  // below this line the process owns the GPU: no exec
+  try {
+    const int device = device_and_signals(a);
+    logf_("INFO", "starting %s %s RPC server at %s:%d (native, device %d)", prog_name(), kVersion,
+          a.eth.c_str(), a.port, device);
+    Server srv(kind, a, cfg, device);
+    if (!a.model_file.empty()) srv.load_file(a.model_file);
+    return srv.run();
+  } catch (const std::exception& e) {
+    logf_("FATAL", "failed to start %s: %s", engine_name(), e.what());
+    return 1;
+  }
+}
+
+}  // namespace rowsrv
+}  // namespace jb

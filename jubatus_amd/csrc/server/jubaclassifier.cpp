@@ -56,7 +56,9 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
                                float* W, float* S, const int32_t* active, int LC, int method,
                                float C, int mode, const int32_t* hot_rows, const int32_t* hot_n,
                                float* hot_rep, int merge_every, int hot_waves,
-                               unsigned long long* stats, uint8_t* touched, hipStream_t stream);
+                               unsigned long long* stats, uint8_t* touched, int64_t n_max,
+                               void* scratch, int64_t scratch_bytes, hipStream_t stream);
+extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max);
 extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                   int n_samples, const float* W, int LC, float* out,
                                   hipStream_t stream);
@@ -71,7 +73,15 @@ namespace {
 
 const char* const kMethods[] = {"perceptron", "PA", "PA1", "PA2", "CW", "AROW", "NHERD"};
 const int kLabelCaps[] = {8, 16, 32, 64, 128, 256, 512, 1024};
-constexpr int kUpdateExact = 0, kUpdateAtomic = 1;
+constexpr int kUpdateExact = 0, kUpdateAtomic = 1, kUpdateSerial = 3;
+
+// how concurrent train requests of one batch update the model: serial-
+// equivalent (default; csrc/hip/serial.hip) or lock-free atomic streams
+// (JUBATUS_UPDATE_MODE=atomic; models/classifier.py concurrent_update)
+int concurrent_update_mode() {
+  const char* e = getenv("JUBATUS_UPDATE_MODE");
+  return (e != nullptr && strcmp(e, "atomic") == 0) ? kUpdateAtomic : kUpdateSerial;
+}
 constexpr int kMethodCW = 4;
 constexpr int kHotMaxRows = 64, kHotEntries = 512, kHotCap = 1 << 14, kHotWaves = 8;
 constexpr int kDirectMaxSamples = 32, kDirectMaxSlots = 320;
@@ -503,6 +513,7 @@ class Classifier {
     add("train_scan.replay_failed", "0");
     add("train.samples_updated", std::to_string(sv[0]));
     add("train.samples_trained", std::to_string(sv[1]));
+    add("train.update_mode", update_mode_ == kUpdateSerial ? "exact" : "atomic");
     add("batching.train.calls", std::to_string(train_calls.load()));
     add("batching.train.launches", std::to_string(train_batches.load()));
     if (prof_[0]) {   // GPU-scan batches: submit (lock + set wait + launch) / scan-check wait
@@ -521,6 +532,7 @@ class Classifier {
     DevBuf<int32_t> len, lab, idx, err;
     DevBuf<float> val;
     DevBuf<uint32_t> hist;
+    DevBuf<uint8_t> serial;        // kSerial scratch (tail range + slack per sample)
     PinBuf<int64_t> meta_host;
     int32_t* host_out = nullptr;   // fine-grained: [err | hist nhist]
     int64_t nhist = 0, host_cap = 0;
@@ -636,7 +648,7 @@ class Classifier {
 
   // models/classifier.py _hot_wanted
   bool hot_wanted(int64_t nstreams) {
-    if (!(LC_ <= 64 && nstreams >= 16)) return false;
+    if (!(hot_rows_ && LC_ <= 64 && nstreams >= 16)) return false;
     ++hot_batches_;
     if (hot_seen_pending_ && hipEventQuery(hot_seen_ev_) == hipSuccess) {
       hot_last_ = ((volatile int32_t*)hot_count_host_)[0];
@@ -732,12 +744,17 @@ class Classifier {
     a.LC = LC_;
     a.method = mid_;
     a.C = C_;
-    a.mode = R > 1 ? kUpdateAtomic : kUpdateExact;
+    a.mode = R > 1 ? update_mode_ : kUpdateExact;
+    if (a.mode == kUpdateSerial) {
+      const int64_t sb = jb_serial_scratch_bytes(std::max<int64_t>(n, 1));
+      a.serial_scratch = s.serial.get((size_t)sb);
+      a.serial_bytes = sb;
+    }
     a.merge_every = 1;
     a.hot_waves = kHotWaves;
     a.stats = stats_;
     a.touched = nullptr;
-    if (n > 0 && a.mode != kUpdateExact && hot_wanted(R)) {
+    if (n > 0 && a.mode == kUpdateAtomic && hot_wanted(R)) {
       Hot& h = hots_[hot_turn_];
       hot_turn_ ^= 1;
       a.hot_rows = h.rows;
@@ -823,7 +840,7 @@ class Classifier {
     HIPCHK(hipMemcpyAsync(d_hsp_.get(2), sp, sizeof sp, hipMemcpyHostToDevice, compute_));
     const int rc = jb_linear_train(d_hrow_.p, d_hidx_.p, d_hval_.p, d_hlab_.p, d_hsp_.p, 1, W_, S_,
                                    active_, LC_, mid_, C_, kUpdateExact, nullptr, nullptr, nullptr, 1,
-                                   kHotWaves, stats_, nullptr, compute_);
+                                   kHotWaves, stats_, nullptr, 0, nullptr, 0, compute_);
     if (rc != 0) throw std::runtime_error("jb_linear_train failed: " + std::to_string(rc));
     HIPCHK(hipStreamSynchronize(compute_));   // host sources are reused by the next request
   }
@@ -887,6 +904,9 @@ class Classifier {
   int next_set_ = 0;
   int32_t* hash_err_ = nullptr;
   Hot hots_[2];
+  const int update_mode_ = concurrent_update_mode();
+  // hot-row replica of the atomic mode (models/classifier.py hot_rows)
+  const bool hot_rows_ = getenv("JUBATUS_HOT_ROWS") != nullptr && strcmp(getenv("JUBATUS_HOT_ROWS"), "1") == 0;
   int hot_turn_ = 0;
   int32_t* hot_count_host_ = nullptr;
   hipEvent_t hot_seen_ev_;

@@ -62,7 +62,7 @@ def _label_cap(n: int) -> int:
 
 class LinearClassifier:
     def __init__(self, method: str, parameter: dict | None, converter: DatumToFvConverter,
-                 device: Any = None, concurrent_update: str = "atomic"):
+                 device: Any = None, concurrent_update: str = "exact"):
         if method not in LINEAR_METHODS:
             raise ClassifierConfigError(f"unknown linear method: {method}")
         parameter = dict(parameter or {})
@@ -74,8 +74,8 @@ class LinearClassifier:
         self.C = float(parameter.get("regularization_weight", 1.0))
         if method not in ("perceptron", "PA") and not self.C > 0:
             raise ClassifierConfigError("regularization_weight must be positive")
-        if concurrent_update not in ("atomic", "hogwild"):
-            raise ClassifierConfigError("concurrent_update must be 'atomic' or 'hogwild'")
+        if concurrent_update not in ("exact", "atomic", "hogwild"):
+            raise ClassifierConfigError("concurrent_update must be 'exact', 'atomic' or 'hogwild'")
         self.concurrent_update = concurrent_update
         self.conv = converter
         self.H = converter.hash_max_size
@@ -101,9 +101,10 @@ class LinearClassifier:
         self._label_version = -1
         self._host_stats = {"updated": 0, "trained": 0}
         # hot-row replica of the concurrent train kernel (csrc/hip/hot.hip,
-        # linear.hip "Hot rows"): JUBATUS_HOT_ROWS=0 disables it,
+        # linear.hip "Hot rows"; atomic / hogwild modes only): off unless
+        # JUBATUS_HOT_ROWS=1 (it trades distance to the serial model for speed),
         # JUBATUS_HOT_MERGE sets the merge interval in samples
-        self.hot_rows = os.environ.get("JUBATUS_HOT_ROWS", "1") != "0"
+        self.hot_rows = os.environ.get("JUBATUS_HOT_ROWS", "0") == "1"
         self.hot_merge = max(1, int(os.environ.get("JUBATUS_HOT_MERGE", "1")))
         self.hot_min_streams = 16
         self.hot_min_count: int | None = None    # None: max(1024, samples / 128)
@@ -117,6 +118,7 @@ class LinearClassifier:
             # wide rule-set kernels (ngram / idf / bm25 / combinations)
             self._devfv = self.pipe.fast or self.pipe.wide
             self._hots = [hip.HotRows(device), hip.HotRows(device)]
+            self._serial = hip.SerialScratch(device)
             self._hot_turn = 0
             self._hot_count_buf = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             self._hot_seen = None            # (pinned count, event) of a detection in flight
@@ -189,6 +191,9 @@ class LinearClassifier:
 
     # -------------------------------------------------------------- train
     def _mode(self, nstreams: int) -> int:
+        """exact (default): several streams give the result of applying them
+        one after the other (csrc/hip/serial.hip); atomic / hogwild: lock-free
+        concurrent streams"""
         from ..ops import hip
         if nstreams <= 1:
             return hip.UPDATE_EXACT
@@ -206,7 +211,7 @@ class LinearClassifier:
         plain 4-stream-block launch)."""
         from ..ops import hip
         if not (self.gpu and self.hot_rows and self.LC <= 64 and nstreams >= self.hot_min_streams
-                and self._mode(nstreams) != hip.UPDATE_EXACT):
+                and self._mode(nstreams) in (hip.UPDATE_ATOMIC, hip.UPDATE_HOGWILD)):
             return False
         self._hot_batches += 1
         seen = self._hot_seen
@@ -247,7 +252,7 @@ class LinearClassifier:
         hip.linear_train(b.row_ptr, b.fidx, b.fval, b.labels, b.stream_ptr, b.nstreams,
                          self.W, self.P, self.active, self.mid, self.C, mode=mode, hot=hs,
                          merge_every=self.hot_merge, stats=self._train_stats,
-                         touched=self.touched)
+                         touched=self.touched, n_max=b.n, scratch=self._serial)
         if hs is not None:
             hs.free.record()
             hs.free_used = True
@@ -273,6 +278,9 @@ class LinearClassifier:
         a.method = self.mid
         a.C = float(self.C)
         a.mode = self._mode(R)
+        if a.mode == hip.UPDATE_SERIAL:
+            a.serial_scratch = self._serial.ptr(max(1, n))
+            a.serial_bytes = self._serial.nbytes
         a.merge_every = self.hot_merge
         a.hot_waves = hip.HOT_WAVES
         a.stats = self._train_stats.data_ptr()
@@ -949,6 +957,7 @@ class LinearClassifier:
             st[f"mix.last_{k}"] = str(v)
         for k, v in self.train_stats().items():
             st[f"train.samples_{k}"] = str(v)
+        st["train.update_mode"] = self.concurrent_update
         return st
 
 

@@ -35,8 +35,10 @@ _SIGS = {
                    _c_void_p],
     "jb_linear_train": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
                         _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p, _c_void_p,
-                        _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p],
+                        _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i64, _c_void_p, _i64,
+                        _c_void_p],
     "jb_hot_rep_bytes": [],
+    "jb_serial_scratch_bytes": [_i64],
     "jb_hot_detect": [_c_void_p, _i32, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                       _i32, _c_void_p, _c_void_p, _c_void_p],
     "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
@@ -414,8 +416,11 @@ def lof_score(ts, td, st, store: int, out: "HostBuffer", max_missing: int) -> No
 _fns: dict = {}
 
 LABEL_CAPS = (8, 16, 32, 64, 128, 256, 512, 1024)
-UPDATE_EXACT, UPDATE_ATOMIC, UPDATE_HOGWILD = 0, 1, 2
-UPDATE_MODES = {"exact": UPDATE_EXACT, "atomic": UPDATE_ATOMIC, "hogwild": UPDATE_HOGWILD}
+# EXACT: one stream; SERIAL: several streams with the result of applying them
+# one after the other (csrc/hip/serial.hip); ATOMIC / HOGWILD: lock-free
+# concurrent streams (not serial-equivalent)
+UPDATE_EXACT, UPDATE_ATOMIC, UPDATE_HOGWILD, UPDATE_SERIAL = 0, 1, 2, 3
+UPDATE_MODES = {"exact": UPDATE_SERIAL, "atomic": UPDATE_ATOMIC, "hogwild": UPDATE_HOGWILD}
 METHODS = {"perceptron": 0, "PA": 1, "PA1": 2, "PA2": 3, "CW": 4, "AROW": 5, "NHERD": 6}
 
 
@@ -519,8 +524,11 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
                  labels: torch.Tensor, stream_ptr: torch.Tensor, nstreams: int, W: torch.Tensor,
                  S: torch.Tensor | None, active: torch.Tensor, method: int, C: float,
                  mode: int, hot: "HotRows | None" = None, merge_every: int = 8,
-                 stats: torch.Tensor | None = None, touched: torch.Tensor | None = None) -> None:
-    """mode: UPDATE_EXACT (single stream), UPDATE_ATOMIC or UPDATE_HOGWILD.
+                 stats: torch.Tensor | None = None, touched: torch.Tensor | None = None,
+                 n_max: int = 0, scratch: "SerialScratch | None" = None) -> None:
+    """mode: UPDATE_EXACT (single stream), UPDATE_SERIAL (several streams,
+    serial-equivalent; needs ``scratch`` and n_max >= the batch's samples),
+    UPDATE_ATOMIC or UPDATE_HOGWILD.
     hot: rows found by ``hot_detect`` for this batch (concurrent modes, label
     capacity <= 64) - kept in a block-shared LDS replica merged every
     ``merge_every`` samples. stats: int64[2] += (samples that updated,
@@ -553,8 +561,30 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
                                 _p(hot.n) if hot is not None else None,
                                 _p(hot.rep) if hot is not None else None, int(merge_every),
                                 HOT_WAVES,
-                                _p(stats), _p(touched), _stream())
+                                _p(stats), _p(touched), int(n_max),
+                                scratch.ptr(n_max) if scratch is not None else None,
+                                scratch.nbytes if scratch is not None else 0, _stream())
     _check(rc, "jb_linear_train")
+
+
+class SerialScratch:
+    """device scratch of the serial-equivalent train mode (csrc/hip/serial.hip:
+    the committer's tail range and the per-sample slack), grown on demand.
+    Growth synchronises the device (the old buffer may still be in use)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = None
+        self.nbytes = 0
+
+    def ptr(self, n_max: int) -> int:
+        need = int(_fn("jb_serial_scratch_bytes")(int(n_max)))
+        if need > self.nbytes:
+            if self.buf is not None:
+                torch.cuda.synchronize(self.device)
+            self.nbytes = max(need, 2 * self.nbytes)
+            self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=self.device)
+        return self.buf.data_ptr()
 
 
 HOT_MAX_ROWS = 64           # csrc/hip/linear.hip Hot<LC>::R (LC = 8)
@@ -704,7 +734,8 @@ hot_seen arena used:i meta_host R:i n:i d_buf buf_cap:i empty_off:i d_meta d_off
 d_slots d_hist nhist:i d_err host_out lt_hash lt_meta lt_cap:i lt_blob lt_blob_len:i sps:i spn:i
 srules nrules n_srules:i n_nrules:i blob blob_len:i H:i d_idx d_val slot_cap:i hash_err hot_rows
 hot_n hot_rep gkey gcnt gcap:i block_min:i min_count:i max_rows:i hot_free_valid:i hot_count_host
-W S active LC:i method:i C:d mode:i merge_every:i hot_waves:i stats touched""".split()
+W S active LC:i method:i C:d mode:i merge_every:i hot_waves:i stats touched serial_scratch
+serial_bytes:i""".split()
 
 
 class TrainBatchArgs(ctypes.Structure):

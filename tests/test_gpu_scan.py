@@ -171,3 +171,39 @@ def test_train_arena_gpu_scan_same_model(monkeypatch):
     assert l0 == l1 and n0 == n1
     np.testing.assert_allclose(w1, w0, rtol=1e-6, atol=1e-6)
     np.testing.assert_allclose(p1, p0, rtol=1e-6, atol=1e-6)
+
+
+def test_train_arena_concurrent_requests_serial_equivalent():
+    """the GPU-scan batch path (csrc/hip/train_batch.hip) with many requests
+    per batch in the default exact mode: the model equals the requests
+    trained one after another on the host oracle"""
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    rng = random.Random(9)
+    batches, reqs = [], []
+    for b in range(4):
+        items_per = []
+        for r in range(64):
+            items = [[f"L{(y := rng.randrange(5))}", _sample(rng, y)] for _ in range(rng.randrange(1, 30))]
+            items_per.append(items)
+            reqs.append(items)
+        batches.append(_arena([msgpack.packb(it, use_bin_type=False) for it in items_per]))
+    g = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV),
+                         device=_device())
+    c = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV))
+    for y in range(5):
+        g.set_label(f"L{y}")
+        c.set_label(f"L{y}")
+    for a, offs, lens in batches:
+        g.train_arena(a, offs, lens)
+    for items in reqs:
+        c.train_requests([msgpack.packb(items, use_bin_type=False)])
+    g.synchronize()
+    g.pipe.check_errors()
+    st = g.get_status()
+    assert int(st["train_scan.gpu"]) == 4 and st["train.update_mode"] == "exact"
+    assert g.train_stats()["updated"] == c.train_stats()["updated"]
+    scale = float(np.abs(c.W).max()) or 1.0
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+    np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3,
+                               atol=2e-3 * float(c.P.max()))
