@@ -168,6 +168,7 @@ SERVERS = {
                         ["server", "native", "hip"]),
     "jubanearest_neighbor": (["server/jubanearest_neighbor.cpp", "native/jb_rpc.cpp"],
                              ["server", "native", "hip"]),
+    "jubaanomaly": (["server/jubaanomaly.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     # host engines: no GPU, no HIP libraries
     "jubastat": (["server/jubastat.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),

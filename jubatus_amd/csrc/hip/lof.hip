@@ -374,3 +374,25 @@ extern "C" int jb_lof_score(const int32_t* ts, const float* td, int nt, int k,
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host, stream);
 }
+
+namespace jb {
+// rows that changed or were removed: their list and lrd are no longer valid
+// (models/lof_state.py DeviceLofState.moved: ok[s] = lrd_ok[s] = 0)
+__global__ void lof_invalidate_kernel(const int32_t* __restrict__ slots, int n, int64_t nrows,
+                                      uint8_t* __restrict__ ok, uint8_t* __restrict__ lrd_ok) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t s = slots[i];
+  if (s < 0 || s >= nrows) return;
+  ok[s] = 0;
+  lrd_ok[s] = 0;
+}
+}  // namespace jb
+
+extern "C" int jb_lof_invalidate(const int32_t* slots, int n, int64_t nrows, uint8_t* ok,
+                                 uint8_t* lrd_ok, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(jb::lof_invalidate_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, slots,
+                     n, nrows, ok, lrd_ok);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,207 @@
+// Incremental LOF state in HBM for the native jubaanomaly: the C++ twin of
+// models/lof_state.py DeviceLofState over csrc/hip/lof.hip (per-slot k
+// nearest neighbour lists, k-distance, lrd, validity flags; insert + mark +
+// score of an add in one host call; staleness marks over all lists).
+//
+// Reference: anomaly_serv.cpp:157-244 over jubatus_core's lof_storage
+// (EXTERNAL); the algorithm (Breunig et al. 2000) and its host oracle are
+// documented in models/anomaly.py and models/lof_state.py.
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "jb_server_common.hpp"
+
+extern "C" {
+int jb_lof_mark(int64_t nrows, int k, const int32_t* nb_slot, const int32_t* changed,
+                const int32_t* nchanged, int clear_ok, uint8_t* ok, uint8_t* lrd_ok,
+                hipStream_t stream);
+int jb_lof_set_lists(int n, const int32_t* slots, const int32_t* cs, const float* cd, int kk, int k,
+                     int ignore_same, int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok,
+                     uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged, hipStream_t stream);
+int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int k, int ignore_same,
+               int64_t nrows, int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok,
+               float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
+               uint32_t* out_host, int max_missing, hipStream_t stream);
+int jb_lof_score(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
+                 const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd,
+                 uint8_t* lrd_ok, int store_slot, uint32_t* out_host, int max_missing,
+                 hipStream_t stream);
+int jb_lof_invalidate(const int32_t* slots, int n, int64_t nrows, uint8_t* ok, uint8_t* lrd_ok,
+                      hipStream_t stream);
+void* jb_host_alloc(int64_t nbytes);
+int jb_host_free(void* p);
+}
+
+namespace jb {
+namespace row {
+
+using jb::srv::DevBuf;
+
+constexpr int kLofMaxK = 64;          // lof.hip kLofMaxK
+constexpr int kLofMaxChanged = 1024;  // kLofMaxChanged
+constexpr int kLofMaxMissing = 1024;
+constexpr int kLofArgMax = 128;       // candidates in the kernel arguments
+
+class LofState {
+ public:
+  LofState(int k, bool ignore_same, hipStream_t st) : k_(k), ignore_(ignore_same), stream_(st) {
+    out_ = (uint32_t*)jb_host_alloc(4 * (4 + kLofMaxMissing));
+    if (!out_) throw std::runtime_error("hipHostMalloc failed");
+    changed_.get(kLofMaxChanged);
+    nchanged_.get(1);
+  }
+
+  ~LofState() {
+    for (void* q : {(void*)nb_slot_.p, (void*)nb_dist_.p, (void*)kdist_.p, (void*)lrd_.p, (void*)ok_.p,
+                    (void*)lrd_ok_.p, (void*)changed_.p, (void*)nchanged_.p, (void*)up_[0].p, (void*)up_[1].p,
+                    (void*)up_[2].p})
+      if (q) (void)hipFree(q);
+    if (out_) jb_host_free(out_);
+  }
+  LofState(const LofState&) = delete;
+  LofState& operator=(const LofState&) = delete;
+
+  int64_t cap() const { return cap_; }
+
+  void ensure(int64_t n) {
+    if (n <= cap_) return;
+    const int64_t cap = std::max<int64_t>(std::max<int64_t>(n, 2 * cap_), 1024);
+    regrow(nb_slot_, cap_ * k_, cap * k_, 0xff);          // -1
+    regrow_inf(nb_dist_, cap_ * k_, cap * k_);
+    regrow(kdist_, cap_, cap, 0);
+    regrow(lrd_, cap_, cap, 0);
+    regrow(ok_, cap_, cap, 0);
+    regrow(lrd_ok_, cap_, cap, 0);
+    cap_ = cap;
+  }
+
+  // DeviceLofState.add: -> true and *score, or false and the slots whose
+  // lists are missing
+  bool add(int32_t p, const std::vector<int32_t>& cs, const std::vector<float>& cd, float* score,
+           std::vector<int32_t>* missing) {
+    const int nc = (int)std::min<size_t>(cs.size(), kLofArgMax);
+    const int rc = jb_lof_add(p, cs.data(), cd.data(), nc, k_, ignore_ ? 1 : 0, cap_, nb_slot_.p,
+                              nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p,
+                              out_, kLofMaxMissing, stream_);
+    if (rc != 0) throw std::runtime_error("lof add failed: " + std::to_string(rc));
+    return result(score, missing);
+  }
+
+  bool score(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store, float* sc,
+             std::vector<int32_t>* missing) {
+    if (ts.empty()) { *sc = 1.f; return true; }
+    const int rc = jb_lof_score(ts.data(), td.data(), (int)ts.size(), k_, nb_slot_.p, nb_dist_.p, kdist_.p,
+                                ok_.p, lrd_.p, lrd_ok_.p, store, out_, kLofMaxMissing, stream_);
+    if (rc != 0) throw std::runtime_error("lof score failed: " + std::to_string(rc));
+    return result(sc, missing);
+  }
+
+  // rows changed or removed: their lists and every list naming them invalid
+  void moved(const std::vector<int32_t>& slots) {
+    if (slots.empty()) return;
+    ensure((int64_t)*std::max_element(slots.begin(), slots.end()) + 1);
+    for (size_t i = 0; i < slots.size(); i += kLofMaxChanged) {
+      const int n = (int)std::min<size_t>(kLofMaxChanged, slots.size() - i);
+      int32_t* d = upload(slots.data() + i, (size_t)n);
+      HIPCHK(hipMemcpyAsync(changed_.p, d, 4 * (size_t)n, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(nchanged_.p, &n_host(n), 4, hipMemcpyHostToDevice, stream_));
+      int rc = jb_lof_mark(cap_, k_, nb_slot_.p, changed_.p, nchanged_.p, 1, ok_.p, lrd_ok_.p, stream_);
+      if (rc == 0) rc = jb_lof_invalidate(d, n, cap_, ok_.p, lrd_ok_.p, stream_);
+      if (rc != 0) throw std::runtime_error("lof mark failed: " + std::to_string(rc));
+      HIPCHK(hipStreamSynchronize(stream_));   // the staging buffers are reused
+    }
+  }
+
+  // lists[i] = ascending (slot, dist) of row slots[i], itself possibly included
+  void set_lists(const std::vector<int32_t>& slots,
+                 const std::vector<std::vector<std::pair<int32_t, float>>>& lists) {
+    size_t kk = 0;
+    for (const auto& l : lists) kk = std::max(kk, l.size());
+    if (!kk || slots.empty()) return;
+    for (size_t i = 0; i < slots.size(); i += kLofMaxChanged) {
+      const size_t n = std::min<size_t>(kLofMaxChanged, slots.size() - i);
+      std::vector<int32_t> cs(n * kk, -1);
+      std::vector<float> cd(n * kk, INFINITY);
+      for (size_t r = 0; r < n; ++r)
+        for (size_t j = 0; j < lists[i + r].size(); ++j) {
+          cs[r * kk + j] = lists[i + r][j].first;
+          cd[r * kk + j] = lists[i + r][j].second;
+        }
+      int32_t* dsl = upload(slots.data() + i, n);
+      int32_t* dcs = upload(cs.data(), cs.size(), 1);
+      float* dcd = (float*)upload((const int32_t*)cd.data(), cd.size(), 2);
+      int rc = jb_lof_set_lists((int)n, dsl, dcs, dcd, (int)kk, k_, ignore_ ? 1 : 0, nb_slot_.p, nb_dist_.p,
+                                kdist_.p, ok_.p, lrd_ok_.p, changed_.p, nchanged_.p, stream_);
+      if (rc == 0) rc = jb_lof_mark(cap_, k_, nb_slot_.p, changed_.p, nchanged_.p, 0, ok_.p, lrd_ok_.p, stream_);
+      if (rc != 0) throw std::runtime_error("lof set_lists failed: " + std::to_string(rc));
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+  }
+
+ private:
+  bool result(float* score, std::vector<int32_t>* missing) {
+    const uint32_t st = ((volatile uint32_t*)out_)[0];
+    if (st == 2) {
+      const uint32_t nm = std::min<uint32_t>(out_[3], kLofMaxMissing);
+      missing->clear();
+      for (uint32_t i = 0; i < nm; ++i) {
+        const int32_t s = (int32_t)out_[4 + i];
+        if (std::find(missing->begin(), missing->end(), s) == missing->end()) missing->push_back(s);
+      }
+      return false;
+    }
+    if (st != 1) throw std::runtime_error("lof: kernel did not complete");
+    memcpy(score, &out_[1], 4);
+    return true;
+  }
+
+  int32_t& n_host(int n) {
+    nh_ = n;
+    return nh_;
+  }
+
+  // small host array -> device (one of three staging slots), synchronous
+  int32_t* upload(const int32_t* p, size_t n, int which = 0) {
+    DevBuf<int32_t>& b = up_[which];
+    int32_t* d = b.get(std::max<size_t>(n, 1));
+    HIPCHK(hipMemcpyAsync(d, p, 4 * n, hipMemcpyHostToDevice, stream_));
+    return d;
+  }
+
+  template <class T>
+  void regrow(DevBuf<T>& b, int64_t old, int64_t cap, int fill) {
+    T* np = nullptr;
+    HIPCHK(hipMalloc((void**)&np, (size_t)cap * sizeof(T)));
+    HIPCHK(hipMemsetAsync(np, fill, (size_t)cap * sizeof(T), stream_));
+    if (old > 0 && b.p) HIPCHK(hipMemcpyAsync(np, b.p, (size_t)old * sizeof(T), hipMemcpyDeviceToDevice, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    if (b.p) HIPCHK(hipFree(b.p));
+    b.p = np;
+    b.cap = (size_t)cap;
+  }
+  void regrow_inf(DevBuf<float>& b, int64_t old, int64_t cap) {
+    regrow(b, old, cap, 0);
+    std::vector<float> inf((size_t)(cap - old), INFINITY);
+    HIPCHK(hipMemcpy(b.p + old, inf.data(), 4 * inf.size(), hipMemcpyHostToDevice));
+  }
+
+  int k_;
+  bool ignore_;
+  hipStream_t stream_;
+  int64_t cap_ = 0;
+  DevBuf<int32_t> nb_slot_;
+  DevBuf<float> nb_dist_, kdist_, lrd_;
+  DevBuf<uint8_t> ok_, lrd_ok_;
+  DevBuf<int32_t> changed_, nchanged_;
+  DevBuf<int32_t> up_[3];
+  uint32_t* out_ = nullptr;
+  int32_t nh_ = 0;
+};
+
+}  // namespace row
+}  // namespace jb

@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
 #include <list>
 #include <map>
 #include <memory>
@@ -996,10 +997,14 @@ class RowEngine {
     }
   }
 
+  // called with the slot of every removed row (the LOF state's moved())
+  std::function<void(int32_t)> on_remove;
+
   bool remove(const std::string& id, bool record = true) {
     auto it = slot_of_.find(id);
     if (it == slot_of_.end()) return false;
     const int32_t s = it->second.first;
+    if (on_remove) on_remove(s);
     insertion_.erase(it->second.second);
     slot_of_.erase(it);
     Row& r = rows_[(size_t)s];

@@ -1,11 +1,13 @@
-// The RPC server of the native row engines: jubarecommender and
-// jubanearest_neighbor (one binary each, csrc/server/juba{recommender,
-// nearest_neighbor}.cpp), no Python in the process.
+// The RPC server of the native row engines: jubarecommender,
+// jubanearest_neighbor and jubaanomaly (one binary each, csrc/server/
+// juba{recommender,nearest_neighbor,anomaly}.cpp), no Python in the process.
 //
 // Reference: jubatus/server/server/recommender_serv.cpp:126-224,
-// recommender_impl.cpp (RPC table) and nearest_neighbor_serv.cpp:121-178,
-// nearest_neighbor_impl.cpp; the Python twins are server/recommender_serv.py
-// and server/nearest_neighbor_serv.py over models/recommender.py.
+// recommender_impl.cpp (RPC table), nearest_neighbor_serv.cpp:121-178,
+// nearest_neighbor_impl.cpp, anomaly_serv.cpp:149-320 (standalone add with
+// the id counter, update / overwrite, calc_score, the id reset on load);
+// the Python twins are server/{recommender,nearest_neighbor,anomaly}_serv.py
+// over models/recommender.py and models/anomaly.py.
 //
 // Scope: standalone servers whose converter runs on the native hashers
 // (jb_row_engine.hpp Converter); other configurations, distributed mode,
@@ -20,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "jb_lof_state.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_row_engine.hpp"
 #include "jb_rpc.hpp"
@@ -37,7 +40,11 @@ using jb::row::RowEngine;
 
 constexpr int kCompleteK = 10;   // models/recommender.py COMPLETE_K
 
-enum class Kind { kRecommender, kNearestNeighbor };
+enum class Kind { kRecommender, kNearestNeighbor, kAnomaly };
+
+inline const char* kind_name(Kind k) {
+  return k == Kind::kRecommender ? "recommender" : k == Kind::kNearestNeighbor ? "nearest_neighbor" : "anomaly";
+}
 
 struct Config {
   std::string text;
@@ -45,6 +52,9 @@ struct Config {
   std::string inner;     // the similarity method of the index
   Value param;           // parameters of the index (hash_num, seed, unlearner...)
   Value conv;
+  // anomaly (models/anomaly.py LOF)
+  int k = 10, rnn = 30;
+  bool ignore_kth_same = false;
 };
 
 inline bool is_lsh(const std::string& m) { return m == "lsh" || m == "euclid_lsh" || m == "minhash"; }
@@ -68,6 +78,28 @@ inline bool parse_config(Kind kind, const std::string& text, Config* c, std::str
   c->inner = c->outer;
   if (kind == Kind::kNearestNeighbor) {
     if (!is_lsh(c->outer)) { *why = "nearest_neighbor method " + c->outer; return false; }
+  } else if (kind == Kind::kAnomaly) {
+    // lof: any recommender backend; light_lof: the nearest_neighbor (LSH) ones
+    if (c->outer != "lof" && c->outer != "light_lof") { *why = "anomaly method " + c->outer; return false; }
+    c->inner = c->param.str_or("method", "");
+    const bool ok = is_lsh(c->inner) ||
+                    (c->outer == "lof" && (c->inner == "inverted_index" || c->inner == "inverted_index_euclid"));
+    if (!ok) { *why = c->outer + ": parameter.method " + c->inner; return false; }
+    auto num = [&](const char* key, double d) {
+      const Value* x = c->param.get(key);
+      return x && x->is_num() ? x->num() : d;
+    };
+    c->k = (int)num("nearest_neighbor_num", 10);
+    c->rnn = (int)num("reverse_nearest_neighbor_num", 30);
+    if (c->k <= 0 || c->rnn < c->k) { *why = "nearest_neighbor_num / reverse_nearest_neighbor_num"; return false; }
+    if (c->k > jb::row::kLofMaxK || c->rnn >= jb::row::kLofArgMax) { *why = "k / rnn beyond the device limits"; return false; }
+    if (const Value* b = c->param.get("ignore_kth_same_point")) c->ignore_kth_same = b->kind == Value::BOOL ? b->b : b->num() != 0;
+    Value inner = empty;
+    if (const Value* ip = c->param.get("parameter"))
+      if (ip->kind == Value::MAP) inner = *ip;
+    for (const char* key : {"unlearner", "unlearner_parameter"})
+      if (const Value* x = c->param.get(key)) inner.o.emplace_back(key, *x);
+    c->param = inner;
   } else if (c->outer == "nearest_neighbor_recommender") {
     c->inner = c->param.str_or("method", "");
     if (!is_lsh(c->inner)) { *why = "nearest_neighbor_recommender inner method"; return false; }
@@ -114,10 +146,13 @@ class Model {
   void configure(const Config& cfg) {
     std::lock_guard<std::mutex> g(mu_);
     HIPCHK(hipStreamSynchronize(stream_));
+    lof_.reset();
     eng_.reset(new RowEngine(cfg.inner, &cfg.param, stream_));
     std::string why;
     if (!eng_->conv.configure(cfg.conv, &why)) throw std::runtime_error("converter: " + why);
     cfg_ = cfg;
+    if (kind_ == Kind::kAnomaly)   // LOF._remove: a removed row's dependants go stale
+      eng_->on_remove = [this](int32_t s) { if (lof_) lof_->moved({s}); };
   }
   const std::string& config_text() const { return cfg_.text; }
 
@@ -159,6 +194,53 @@ class Model {
     ++update_count;
     clear_row_cnt = update_row_cnt = 0;
     eng_->clear();
+    lof_.reset();
+    next_id_ = 0;
+  }
+
+  // ------------------------------------------------------------- anomaly
+  // anomaly_serv.cpp add (standalone): a new id from the counter, insert
+  std::pair<std::string, double> add(const Value& dv) {
+    Datum d;
+    jb::row::parse_datum(dv, &d);
+    std::lock_guard<std::mutex> g(mu_);
+    ++update_count;
+    const std::string id = std::to_string(next_id_++);
+    return {id, (double)insert(id, std::move(d))};
+  }
+  // update merges into the stored datum, overwrite replaces it
+  double update(const std::string& id, const Value& dv, bool merge) {
+    Datum nd;
+    jb::row::parse_datum(dv, &nd);
+    std::lock_guard<std::mutex> g(mu_);
+    ++update_count;
+    if (merge)
+      if (const jb::row::Row* r = eng_->find(id)) {
+        Datum m = r->d;
+        for (auto& kv : nd.sv) m.sv[kv.first] = kv.second;
+        for (auto& kv : nd.nv) m.nv[kv.first] = kv.second;
+        for (auto& kv : nd.bv) m.bv[kv.first] = kv.second;
+        nd = std::move(m);
+      }
+    return (double)insert(id, std::move(nd));
+  }
+  // models/anomaly.py calc_score: the k nearest stored rows, then LOF
+  double calc_score(const Value& dv) {
+    Datum chk;
+    jb::row::parse_datum(dv, &chk);
+    MsgpackWriter w;
+    write_value(w, dv);
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<int32_t> ts;
+    std::vector<float> td;
+    if (eng_->nslots() > 0) {
+      std::vector<int32_t> idx;
+      std::vector<float> val;
+      eng_->conv.hash((const uint8_t*)w.out.data(), w.out.size(), &idx, &val, false);
+      for (const Hit& h : eng_->query_fv(idx, val, cfg_.k))
+        if (live(h.slot)) { ts.push_back(h.slot); td.push_back(h.dist); }
+    }
+    return (double)score_from(ts, td, -1);
   }
 
   // ------------------------------------------------------------- queries
@@ -245,14 +327,27 @@ class Model {
   }
   void unpack(const Value& obj) {
     std::lock_guard<std::mutex> g(mu_);
+    lof_.reset();                  // LOF.unpack: lists rebuilt on demand
     eng_->unpack(obj);
+    lof_.reset();
     HIPCHK(hipStreamSynchronize(stream_));
+    if (kind_ == Kind::kAnomaly) {
+      // anomaly_serv.cpp:299-320: the id counter restarts past the largest
+      // all-digit id
+      int64_t m = -1;
+      for (const std::string& id : eng_->all_ids()) {
+        if (id.empty() || id.size() > 18 || id.find_first_not_of("0123456789") != std::string::npos) continue;
+        m = std::max<int64_t>(m, std::stoll(id));
+      }
+      next_id_ = m + 1;
+    }
   }
 
   void status(std::vector<std::pair<std::string, std::string>>* st) {
     std::lock_guard<std::mutex> g(mu_);
     auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
-    add("method", kind_ == Kind::kRecommender ? cfg_.outer : eng_->method());
+    add("method", kind_ == Kind::kNearestNeighbor ? eng_->method() : cfg_.outer);
+    if (kind_ == Kind::kAnomaly) add("backend", eng_->method());
     add("num_rows", std::to_string(eng_->size()));
     add("storage", "hbm");
     add("unlearner", eng_->lru() ? "lru" : "none");
@@ -320,12 +415,69 @@ class Model {
     }
   }
 
+  bool live(int32_t s) const { return s >= 0 && s < eng_->nslots() && eng_->at(s).live; }
+
+  jb::row::LofState& state() {
+    if (!lof_) lof_.reset(new jb::row::LofState(cfg_.k, cfg_.ignore_kth_same, stream_));
+    lof_->ensure(eng_->nslots());
+    return *lof_;
+  }
+
+  // row_engine.query_slot_lists: each row's nearest (itself included), live rows
+  std::vector<std::vector<std::pair<int32_t, float>>> slot_lists(const std::vector<int32_t>& slots, int k) {
+    std::vector<std::vector<std::pair<int32_t, float>>> out;
+    for (int32_t s : slots) {
+      std::vector<std::pair<int32_t, float>> l;
+      for (const Hit& h : eng_->query_slot(s, k))
+        if (live(h.slot)) l.push_back({h.slot, h.dist});
+      out.push_back(std::move(l));
+    }
+    return out;
+  }
+
+  // LOF._score_from: refresh missing neighbour lists until the score resolves
+  float score_from(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store) {
+    jb::row::LofState& st = state();
+    std::vector<int32_t> missing;
+    for (int it = 0; it < 1 + 2 * cfg_.k; ++it) {
+      float sc;
+      if (st.score(ts, td, store, &sc, &missing)) return sc;
+      st.set_lists(missing, slot_lists(missing, cfg_.k + 1));
+    }
+    throw std::runtime_error("lof: neighbour lists did not converge");
+  }
+
+  // LOF._insert
+  float insert(const std::string& id, Datum&& d) {
+    const bool existed = eng_->slot(id) >= 0;
+    eng_->set(id, std::move(d));
+    const int32_t s = eng_->slot(id);
+    jb::row::LofState& st = state();
+    if (existed) st.moved({s});
+    std::vector<int32_t> cs;
+    std::vector<float> cd;
+    for (const Hit& h : eng_->query_slot(s, cfg_.rnn + 1)) {
+      if (!live(h.slot) || h.slot == s) continue;
+      if ((int)cs.size() >= cfg_.rnn) break;
+      cs.push_back(h.slot);
+      cd.push_back(h.dist);
+    }
+    float sc;
+    std::vector<int32_t> missing;
+    if (st.add(s, cs, cd, &sc, &missing)) return sc;
+    const size_t kk = std::min<size_t>(cs.size(), (size_t)cfg_.k);
+    return score_from(std::vector<int32_t>(cs.begin(), cs.begin() + kk),
+                      std::vector<float>(cd.begin(), cd.begin() + kk), s);
+  }
+
   Kind kind_;
   int device_;
   hipStream_t stream_;
   std::mutex mu_;
   Config cfg_;
   std::unique_ptr<RowEngine> eng_;
+  std::unique_ptr<jb::row::LofState> lof_;
+  int64_t next_id_ = 0;
 };
 
 inline void write_pairs(MsgpackWriter& w, const std::vector<std::pair<std::string, double>>& r) {
@@ -368,7 +520,7 @@ class Server {
 
  private:
   std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
-  const char* type() const { return kind_ == Kind::kRecommender ? "recommender" : "nearest_neighbor"; }
+  const char* type() const { return kind_name(kind_); }
 
   std::string dispatch(const jb::RpcRequest& r) {
     Value args;
@@ -390,7 +542,11 @@ class Server {
         {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
         {"set_row", "sd"}, {"neighbor_row_from_id", "sk"}, {"neighbor_row_from_datum", "dk"},
         {"similar_row_from_id", "sk"}, {"similar_row_from_datum", "dk"}, {"get_all_rows", ""}};
-    const auto& table = kind_ == Kind::kRecommender ? rec : nn;
+    static const std::vector<std::pair<std::string, std::string>> an = {
+        {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
+        {"clear_row", "s"}, {"add", "d"}, {"update", "sd"}, {"overwrite", "sd"}, {"calc_score", "d"},
+        {"get_all_rows", ""}};
+    const auto& table = kind_ == Kind::kRecommender ? rec : kind_ == Kind::kNearestNeighbor ? nn : an;
     const std::string* sig = nullptr;
     for (const auto& x : table)
       if (x.first == m) sig = &x.second;
@@ -415,6 +571,15 @@ class Server {
         w.boolean(true);
       } else if (m == "clear_row") {
         w.boolean(model_->clear_row(args.a[1].s));
+      } else if (m == "add") {
+        const auto r = model_->add(args.a[1]);
+        w.arr(2);
+        w.raw(r.first);
+        w.dbl(r.second);
+      } else if (m == "update" || m == "overwrite") {
+        w.dbl(model_->update(args.a[1].s, args.a[2], m == "update"));
+      } else if (m == "calc_score") {
+        w.dbl(model_->calc_score(args.a[1]));
       } else if (m == "update_row") {
         w.boolean(model_->update_row(args.a[1].s, args.a[2]));
       } else if (m == "set_row") {
@@ -519,7 +684,7 @@ class Server {
 };
 
 inline int row_main(int argc, char** argv, Kind kind) {
-  set_engine(kind == Kind::kRecommender ? "recommender" : "nearest_neighbor");
+  set_engine(kind_name(kind));
   Args a;
   std::string text;
   Config cfg;

@@ -125,9 +125,12 @@ def _datum(rng, with_bin=True):
 
 def _drive(pair, rng, steps, kind):
     ids = [f"r{i}" for i in range(40)]
-    upd = "update_row" if kind == "recommender" else "set_row"
+    upd = {"recommender": "update_row", "nearest_neighbor": "set_row", "anomaly": "update"}[kind]
     for i in range(steps):
-        if kind == "recommender":
+        if kind == "anomaly":
+            op = rng.choice(["add"] * 4 + ["update", "overwrite"] * 2 + ["clear_row", "calc_score"] * 2
+                            + ["get_all_rows"])
+        elif kind == "recommender":
             op = rng.choice([upd] * 6 + ["clear_row", "similar_row_from_id", "similar_row_from_datum",
                                          "complete_row_from_id", "complete_row_from_datum", "decode_row",
                                          "get_all_rows", "calc_similarity", "calc_l2norm"])
@@ -136,8 +139,12 @@ def _drive(pair, rng, steps, kind):
                                          "similar_row_from_id", "similar_row_from_datum", "get_all_rows"])
         rid = rng.choice(ids + ["missing"])
         k = rng.choice([1, 3, 10, 200])
-        if op == upd:
+        if op == "add":
+            args = (_datum(rng, False),)
+        elif op in (upd, "overwrite"):
             args = (rid, _datum(rng))
+        elif op == "calc_score":
+            args = (_datum(rng, False),)
         elif op in ("clear_row", "decode_row", "complete_row_from_id"):
             args = (rid,)
         elif op.endswith("_from_id"):
@@ -170,6 +177,10 @@ CASES = [
     ("recommender", "recommender/nearest_neighbor_recommender_euclid_lsh.json"),
     ("nearest_neighbor", "nearest_neighbor/euclid_lsh.json"),
     ("nearest_neighbor", "nearest_neighbor/default.json"),       # lsh, bigram tf-idf
+    ("anomaly", "anomaly/lof.json"),                             # lof over euclid_lsh
+    ("anomaly", "anomaly/lof_inverted_index_euclid.json"),
+    ("anomaly", "anomaly/light_lof_unlearn_lru.json"),
+    ("anomaly", "anomaly/default.json"),
 ]
 
 
@@ -198,16 +209,17 @@ def test_native_row_server_matches_python(engine, cfg, tmp_path):
 
 @pytest.mark.parametrize("engine,cfg", [("recommender", "recommender/default.json"),
                                         ("recommender", "recommender/euclid_lsh_unlearn_lru.json"),
-                                        ("nearest_neighbor", "nearest_neighbor/minhash.json")])
+                                        ("nearest_neighbor", "nearest_neighbor/minhash.json"),
+                                        ("anomaly", "anomaly/lof.json")])
 def test_native_row_model_files_both_ways(engine, cfg, tmp_path):
     pair = Pair(engine, open(config_path(cfg)).read(), tmp_path)
     try:
         rng = random.Random(7)
-        upd = "update_row" if engine == "recommender" else "set_row"
+        upd = {"recommender": "update_row", "nearest_neighbor": "set_row", "anomaly": "overwrite"}[engine]
         for i in range(60):
             d = _datum(rng)
-            assert pair.n.call(upd, "", f"r{i % 45}", d) is True
-            assert pair.p.call(upd, "", f"r{i % 45}", d) is True
+            a, b = pair.n.call(upd, "", f"{i % 45}", d), pair.p.call(upd, "", f"{i % 45}", d)
+            _same(_norm(a), _norm(b), f"fill {i}")
         # native -> Python
         (_, npath), = pair.n.call("save", "", "m1").items()
         npath = _norm(npath)
