@@ -41,6 +41,7 @@ import argparse
 import json
 import os
 import random
+import shutil
 import socket
 import statistics
 import subprocess
@@ -363,6 +364,139 @@ def served_train_native(args, local: int, nat) -> dict:
             p.kill()
 
 
+# ------------------------------------------------------- engine records
+# BASELINE.json secondary configs measured over RPC against the native
+# servers (csrc/server/jb_row_server.hpp; no Python in the server process),
+# driven by the native load generator (csrc/tools/jubaloadgen.cpp)
+ENGINE_CASES = (
+    # (record name, engine, config, fill method, query method)
+    ("recommender_euclid_lsh", "recommender", "config/recommender/euclid_lsh.json", "update_row",
+     "similar_row_from_datum"),
+    ("recommender_default", "recommender", "config/recommender/default.json", "update_row",
+     "similar_row_from_datum"),
+    ("anomaly_lof", "anomaly", "config/anomaly/lof.json", "add", "calc_score"),
+)
+
+
+def _row_datums(n: int, seed: int) -> list[bytes]:
+    """n distinct synthetic rows (msgpack datums): 4 string values from a
+    Zipf-like vocabulary (words of 3-8 letters, so ngram converters see
+    text) and 4 numeric values"""
+    rng = np.random.default_rng(seed)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", dtype=np.uint8)
+    vocab = ["".join(chr(c) for c in rng.choice(letters, size=int(rng.integers(3, 9))))
+             for _ in range(4096)]
+    widx = np.minimum((rng.pareto(1.2, size=(n, 4)) * 40).astype(np.int64), 4095)
+    nums = np.round(rng.normal(0.0, 1.0, size=(n, 4)) + (widx[:, :1] % 7) * 0.5, 4)
+    out = []
+    for i in range(n):
+        w = widx[i]
+        x = nums[i]
+        out.append(msgpack.packb([[["title", vocab[w[0]] + " " + vocab[w[1]]], ["genre", vocab[w[2]]],
+                                   ["tag", vocab[w[3]]], ["src", "s%d" % (w[0] % 13)]],
+                                  [["n0", float(x[0])], ["n1", float(x[1])], ["n2", float(x[2])],
+                                   ["n3", float(x[3])]], []], use_bin_type=False))
+    return out
+
+
+def _loadgen(exe: str, port: int, method: str, pfile: str, conns: int, depth: int, secs: float = 0.0,
+             once: bool = False, timeout: float = 900.0) -> dict:
+    cmd = [exe, "-p", str(port), "-m", method, "-f", pfile, "-c", str(conns), "-d", str(depth)]
+    cmd += ["-o", "1"] if once else ["-t", str(secs)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"jubaloadgen {method}: {(r.stderr or r.stdout)[-300:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def engine_records(args, local: int) -> dict:
+    """Per BASELINE secondary config: fill N distinct rows through the
+    engine's update RPC (rate over the whole fill), then over-RPC latency of
+    the query RPC (one connection, one request in flight: p50 / p99) and its
+    throughput (8 connections x 4 in flight), and of the update RPC on the
+    filled table. Queries are fresh datums (not stored rows)."""
+    import tempfile
+    from jubatus_amd.common.mprpc import RpcClient
+    exe = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaloadgen")
+    out: dict = {}
+    t_gen = time.perf_counter()
+    rows = _row_datums(max(args.engine_rows, args.lof_rows) + 4096, 11)
+    queries, rows = rows[-4096:], rows[:-4096]
+    t_gen = time.perf_counter() - t_gen
+    tmp = tempfile.mkdtemp(prefix="jb_engines_")
+    nil = b"\xa0"          # cluster name ""
+    for name, engine, cfg, fill_m, query_m in ENGINE_CASES:
+        if args.engines != "all" and name not in args.engines.split(","):
+            continue
+        srv = os.path.join(ROOT, "jubatus_amd", "native_bin", f"juba{engine}")
+        nrows = args.lof_rows if engine == "anomaly" else args.engine_rows
+        rec: dict = {"config": cfg, "rows": nrows, "server": f"native juba{engine} (no Python)"}
+        port = _free_port()
+        p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", os.path.join(ROOT, cfg),
+                              "-d", tmp, "-c", "4", "--gpu", str(local)],
+                             stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        try:
+            deadline = time.time() + 60
+            while True:
+                try:
+                    with RpcClient("127.0.0.1", port, 30.0) as c:
+                        (_, st), = c.call("get_status", "").items()
+                    break
+                except Exception:  # noqa: BLE001 - not listening yet
+                    if p.poll() is not None or time.time() > deadline:
+                        raise RuntimeError((p.stderr.read() or b"").decode(errors="replace")[-300:])
+                    time.sleep(0.2)
+            st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
+                  for k, v in st.items()}
+            if st.get("server_runtime") != "native":
+                raise RuntimeError("the binary handed the configuration to the Python server")
+            fill = os.path.join(tmp, f"{name}_fill.bin")
+            with open(fill, "wb") as f:
+                for i in range(nrows):
+                    if fill_m == "add":
+                        f.write(b"\x92" + nil + rows[i])
+                    else:
+                        f.write(b"\x93" + nil + msgpack.packb(f"row{i}") + rows[i])
+            q = os.path.join(tmp, f"{name}_query.bin")
+            with open(q, "wb") as f:
+                for d in queries:
+                    f.write((b"\x93" + nil + d + b"\x0a") if query_m.startswith("similar") else
+                            (b"\x92" + nil + d))
+            t0 = time.perf_counter()
+            r = _loadgen(exe, port, fill_m, fill, 16, 8, once=True)
+            rec["fill_s"] = round(time.perf_counter() - t0, 2)
+            rec[f"{fill_m}_per_s_fill"] = r["requests_per_s"]
+            with RpcClient("127.0.0.1", port, 60.0) as c:
+                (_, st), = c.call("get_status", "").items()
+            st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
+                  for k, v in st.items()}
+            rec["rows_stored"] = int(st.get("num_rows", -1))
+            lat = _loadgen(exe, port, query_m, q, 1, 1, secs=args.engine_seconds)
+            rec[f"{query_m}_p50_us"] = lat["p50_us"]
+            rec[f"{query_m}_p99_us"] = lat["p99_us"]
+            thr = _loadgen(exe, port, query_m, q, 8, 4, secs=args.engine_seconds)
+            rec[f"{query_m}_per_s"] = thr["requests_per_s"]
+            # the update RPC on the filled table (fresh rows beyond the fill for
+            # add; rewrites of stored rows for update_row)
+            ulat = _loadgen(exe, port, fill_m, fill, 1, 1, secs=args.engine_seconds)
+            rec[f"{fill_m}_p50_us"] = ulat["p50_us"]
+            rec[f"{fill_m}_p99_us"] = ulat["p99_us"]
+            rec["rpc"] = "loopback TCP, native jubaloadgen; latency: 1 connection x 1 in flight; " \
+                         "throughput: 8 connections x 4 in flight; k = 10"
+        except Exception as e:  # noqa: BLE001 - recorded, the headline still prints
+            rec["error"] = f"{type(e).__name__}: {e}"[:400]
+        finally:
+            p.terminate()
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        out[name] = rec
+    out["row_gen_s"] = round(t_gen, 1)
+    shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -390,6 +524,14 @@ def main() -> None:
                          "(linear_mixer.cpp:337-344,358-390: interval_count 512 updates, the mixer "
                          "wakes on the threshold), agreed across ranks each batch")
     ap.add_argument("--latency-iters", type=int, default=300)
+    ap.add_argument("--engines", default="all",
+                    help="engine records (N = 1): all, none, or a comma list of "
+                         + ", ".join(c[0] for c in ENGINE_CASES))
+    ap.add_argument("--engine-rows", type=int, default=1_000_000,
+                    help="rows filled into the recommender servers before their queries")
+    ap.add_argument("--lof-rows", type=int, default=100_000,
+                    help="rows added to the LOF server before its queries")
+    ap.add_argument("--engine-seconds", type=float, default=3.0)
     ap.add_argument("--no-rpc", action="store_true",
                     help="skip the served-path measurement (jubaclassifier + jubaloadgen, N = 1)")
     ap.add_argument("--served-runtime", choices=("python", "native", "both"), default="both",
@@ -629,6 +771,9 @@ def main() -> None:
     if world == 1 and device is not None and not args.no_rpc:
         served = served_train(args, local, nat)
         served_native = served_train_native(args, local, nat)
+    engines = None
+    if world == 1 and device is not None and args.engines != "none":
+        engines = engine_records(args, local)
 
     total = samples_per_step * args.steps * world
     value = total / elapsed
@@ -680,6 +825,7 @@ def main() -> None:
             "data_gen_s": round(t_gen, 1),
             "served": served,
             "served_native": served_native,
+            "engines": engines,
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),
             "heldout_accuracy": round(acc, 4),

@@ -92,8 +92,12 @@ inline bool parse_config(Kind kind, const std::string& text, Config* c, std::str
     c->k = (int)num("nearest_neighbor_num", 10);
     c->rnn = (int)num("reverse_nearest_neighbor_num", 30);
     if (c->k <= 0 || c->rnn < c->k) { *why = "nearest_neighbor_num / reverse_nearest_neighbor_num"; return false; }
-    if (c->k > jb::row::kLofMaxK || c->rnn >= jb::row::kLofArgMax) { *why = "k / rnn beyond the device limits"; return false; }
-    if (const Value* b = c->param.get("ignore_kth_same_point")) c->ignore_kth_same = b->kind == Value::BOOL ? b->b : b->num() != 0;
+    if (c->k > jb::row::kLofMaxK || c->rnn >= jb::row::kLofArgMax) {
+      *why = "k / rnn beyond the device limits";
+      return false;
+    }
+    if (const Value* b = c->param.get("ignore_kth_same_point"))
+      c->ignore_kth_same = b->kind == Value::BOOL ? b->b : b->num() != 0;
     Value inner = empty;
     if (const Value* ip = c->param.get("parameter"))
       if (ip->kind == Value::MAP) inner = *ip;
@@ -665,7 +669,8 @@ class Server {
     if (overwrite_config && !jb::val::same_config(mf.config, current)) {
       Config cfg;
       std::string why;
-      if (!parse_config(kind_, mf.config, &cfg, &why)) throw std::runtime_error("model config is not served natively: " + why);
+      if (!parse_config(kind_, mf.config, &cfg, &why))
+        throw std::runtime_error("model config is not served natively: " + why);
       model_->configure(cfg);
     }
     model_->unpack(mf.user);

@@ -10,7 +10,12 @@
 // out in one sendmsg (envelope + params iovecs, no per-request copy of the
 // params), as a pipelining client library would write them.
 //
+// -o 1 (once): every params object is sent exactly once - connection i takes
+// the i-th contiguous share of the file - and the run ends when all replied
+// (bulk loads: each row once, in file order per connection).
+//
 // Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
+//                    [-o 1]
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/tcp.h>
@@ -103,8 +108,8 @@ struct Result {
 };
 
 void run_conn(const std::string& host, int port, const std::string& method,
-              const std::vector<std::string>* params, size_t first, int depth, double secs,
-              Result* r) {
+              const std::vector<std::string>* params, size_t first, size_t last, bool once, int depth,
+              double secs, Result* r) {
   const int fd = connect_to(host, port);
   if (fd < 0) { r->error = "connect failed"; return; }
   std::vector<Clock::time_point> sent(1 << 16);
@@ -122,12 +127,13 @@ void run_conn(const std::string& host, int port, const std::string& method,
     heads.clear();
     bodies.clear();
     const auto now = Clock::now();
-    if (sending && now >= t_end) sending = false;
-    while (sending && inflight < depth) {
+    if (sending && !once && now >= t_end) sending = false;
+    if (sending && once && which >= last) sending = false;
+    while (sending && inflight < depth && !(once && which >= last)) {
       heads.push_back(request_head(next, method));
       bodies.push_back(&(*params)[which]);
       sent[next & 0xffff] = now;
-      which = (which + 1) % params->size();
+      which = once ? which + 1 : (which + 1) % params->size();
       ++next;
       ++inflight;
     }
@@ -168,6 +174,7 @@ void run_conn(const std::string& host, int port, const std::string& method,
 int main(int argc, char** argv) {
   std::string host = "127.0.0.1", method, file;
   int port = 0, conns = 8, depth = 4;
+  bool once = false;
   double secs = 3.0;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string a = argv[i], v = argv[i + 1];
@@ -178,6 +185,7 @@ int main(int argc, char** argv) {
     else if (a == "-c") conns = atoi(v.c_str());
     else if (a == "-d") depth = atoi(v.c_str());
     else if (a == "-t") secs = atof(v.c_str());
+    else if (a == "-o") once = atoi(v.c_str()) != 0;
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
   }
   if (!port || method.empty() || file.empty() || conns < 1 || depth < 1) {
@@ -203,7 +211,8 @@ int main(int argc, char** argv) {
   const auto t0 = Clock::now();
   for (int i = 0; i < conns; ++i)
     ts.emplace_back(run_conn, host, port, method, &params,
-                    (size_t)i * params.size() / (size_t)conns, depth, secs, &res[i]);
+                    (size_t)i * params.size() / (size_t)conns,
+                    (size_t)(i + 1) * params.size() / (size_t)conns, once, depth, secs, &res[i]);
   for (auto& t : ts) t.join();
   const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
   uint64_t done = 0;

@@ -18,15 +18,16 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 PAGES = [
-    ("jubatus_server", 8, ["bin/jubarecommender", "--help"],
+    ("jubatus_server", 8, ["bin/jubaclustering", "--help"],
      "engine server (jubaclassifier, jubaregression, jubarecommender, jubanearest_neighbor, "
      "jubaanomaly, jubaclustering, jubaburst, jubabandit, jubastat, jubagraph, jubaweight)",
      "Serves one engine over msgpack-RPC. Each server process drives one GPU (--gpu, or "
      "LOCAL_RANK, or the least-used device assigned by jubavisor); models live in HBM and are "
      "mixed with the other members of the cluster over RCCL. Without --zookeeper the server "
-     "runs standalone. jubaclassifier and jubaregression are native binaries (no Python) for "
-     "standalone configurations on the fixed-slot GPU converter; they hand every other setup "
-     "to this server with the same flags."),
+     "runs standalone. jubaclassifier, jubaregression, jubarecommender, jubanearest_neighbor, "
+     "jubaanomaly, jubastat, jubabandit, jubaburst and jubagraph are native binaries (no "
+     "Python) for standalone configurations whose converter runs on the native hashers; they "
+     "hand every other setup to this server with the same flags."),
     ("jubatus_proxy", 8, ["bin/jubaclassifier_proxy", "--help"],
      "engine proxy (juba*_proxy)",
      "Native proxy in front of a cluster of engine servers: routes every request to one, "
