@@ -8,9 +8,12 @@ collective over the process group (RCCL over xGMI on GPUs, gloo on hosts):
 
 * the train kernel marks every row it writes in ``touched`` (uint8[H],
   csrc/hip/linear.hip);
-* ``begin`` all-gathers the touched row lists, forms their union (the same
-  on every rank), snapshots those rows of every table into one contiguous
-  buffer and starts an asynchronous SUM all-reduce of it;
+* ``begin`` starts an asynchronous MAX all-reduce of the touched bitmap (the
+  union, the same on every rank) and returns - no host synchronisation;
+* ``ready`` (polled between train batches) copies the union's row count to
+  the host once the all-reduce finished (async D2H + event), then compacts
+  the rows on the device (``nonzero_static`` with that size), snapshots them
+  of every table into one contiguous buffer and starts the SUM all-reduce;
 * ``end`` folds the cluster mean in: ``T[rows] += mean(snapshot) - snapshot``,
   so updates made while the collective ran are kept (and marked touched
   again for the next MIX).
@@ -69,65 +72,87 @@ class TableMix:
         self._next_row = 0         # dense: first row not launched yet
         self._inflight: list = []  # dense: (r0, r1, snap, red, work)
         self._done = False
+        self._mark = None          # union bitmap (all-reduce MAX in flight)
+        self._mark_work = None
+        self._count = None         # (pinned count, event) of the union size copy
+        self._aux = None           # the union all-reduce of a rank that went dense at once
         self.abandoned = False     # tables replaced meanwhile: run the collectives, fold nothing
 
     # ----------------------------------------------------------- begin
     def begin(self) -> "TableMix":
+        """start the MIX (asynchronous: no host synchronisation here)"""
         if self.n <= 1:
             if self.touched is not None:
                 self.touched.zero_()
             self.mode, self._done = "single", True
             return self
-        rows = self._union()
-        if rows is None:
+        # union of the ranks' touched rows = MAX all-reduce of the bitmaps; a
+        # rank without a map (after a load / re-layout) contributes all rows,
+        # so every rank then sees a dense union
+        t = self.touched
+        if t is not None:
+            self._mark = t.clone()
+            t.zero_()
+        else:
+            self._mark = torch.ones(self.H, dtype=torch.uint8, device=self.tables[0].device)
+        self._mark_work = dist.all_reduce(self._mark, op=dist.ReduceOp.MAX, group=self.group,
+                                          async_op=True)
+        self.nbytes = self.H
+        self.mode = "union"
+        if t is None:
+            # this rank's all-ones map makes the union dense on every rank:
+            # the first chunks go out right away (the other ranks issue the
+            # same collectives once they see the union)
+            self._aux = self._mark_work       # waited for in end()
+            self._mark = None
+            self._mark_work = None
             self.mode = "dense"
             self.rows = self.H
             self._pump()
-        else:
-            self.mode = "sparse"
-            self.rows = int(rows.numel())
-            if self.rows == 0:
-                self._done = True
-                return self
-            snap = torch.cat([t.index_select(0, rows).reshape(self.rows, -1) for t in self.tables],
-                             dim=1)
-            red = snap.clone()
-            self.nbytes = red.numel() * red.element_size()
-            work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            self._sparse = (rows, snap, red, work)
         return self
 
-    def _union(self) -> torch.Tensor | None:
-        """union of the ranks' touched rows (sorted, int64, same on every
-        rank), or None for a dense MIX; clears the touched map"""
-        t = self.touched
-        dev = t.device if t is not None else self.tables[0].device
-        if t is not None:
-            local = torch.nonzero(t).flatten()
-            t.zero_()
-            cnt = torch.tensor([local.numel()], dtype=torch.int64, device=dev)
-        else:
-            local = None
-            cnt = torch.tensor([self.H + 1], dtype=torch.int64, device=dev)   # "dense"
-        counts = [torch.empty_like(cnt) for _ in range(self.n)]
-        dist.all_gather(counts, cnt, group=self.group)       # (gloo has no _into_tensor form)
-        mx = int(torch.cat(counts).max().item())
-        if mx > self.H or mx > self.dense_frac * self.H:
-            return None
-        if mx == 0:
-            return torch.zeros(0, dtype=torch.int64, device=dev)
-        pad = torch.full((mx,), -1, dtype=torch.int64, device=dev)
-        pad[:local.numel()] = local
-        every = [torch.empty_like(pad) for _ in range(self.n)]
-        dist.all_gather(every, pad, group=self.group)
-        every = torch.cat(every)
-        every = every[every >= 0]
-        mark = torch.zeros(self.H, dtype=torch.uint8, device=dev)
-        mark[every] = 1
-        rows = torch.nonzero(mark).flatten()
-        if rows.numel() > self.dense_frac * self.H:
-            return None
-        return rows
+    def _advance_union(self, block: bool) -> bool:
+        """union all-reduce -> size on the host -> the sparse or dense MIX
+        proper; False while waiting (block=False)"""
+        if self._count is None:
+            if not block and not self._mark_work.is_completed():
+                return False
+            self._mark_work.wait()
+            cnt = self._mark.sum(dtype=torch.int64).reshape(1)
+            if cnt.is_cuda:
+                host = torch.empty(1, dtype=torch.int64, pin_memory=True)
+                host.copy_(cnt, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                self._count = (host, ev)
+            else:
+                self._count = (cnt, None)
+        host, ev = self._count
+        if ev is not None:
+            if not block and not ev.query():
+                return False
+            ev.synchronize()
+        rows_n = int(host[0])
+        if rows_n > self.dense_frac * self.H:
+            self._mark = None
+            self.mode = "dense"
+            self.rows = self.H
+            self._pump()
+            return True
+        self.mode = "sparse"
+        self.rows = rows_n
+        if rows_n == 0:
+            self._mark = None
+            self._done = True
+            return True
+        rows = torch.nonzero_static(self._mark, size=rows_n).flatten()   # sorted, same on every rank
+        self._mark = None
+        snap = torch.cat([t.index_select(0, rows).reshape(self.rows, -1) for t in self.tables], dim=1)
+        red = snap.clone()
+        self.nbytes += red.numel() * red.element_size()
+        work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._sparse = (rows, snap, red, work)
+        return True
 
     # ------------------------------------------------------------ dense
     def _launch(self, r0: int, r1: int) -> None:
@@ -175,6 +200,10 @@ class TableMix:
         """advance without blocking; True when ``end`` will not wait"""
         if self._done:
             return True
+        if self.mode == "union" and not self._advance_union(block=False):
+            return False
+        if self._done:
+            return True
         if self.mode == "dense":
             self._pump()
             return self._done
@@ -182,6 +211,11 @@ class TableMix:
 
     def end(self) -> int:
         """finish the MIX (blocking); returns the bytes all-reduced per rank"""
+        if self.mode == "union":
+            self._advance_union(block=True)
+        if self._aux is not None:
+            self._aux.wait()
+            self._aux = None
         if self.mode == "dense":
             while not self._done:
                 self._pump(block=True)

@@ -107,3 +107,54 @@ def test_overlapped_mix_tables_replaced_during_collective():
     assert not st0["abandoned"] and not same0  # rank 0 folded the mean
     assert l0 == l1 and len(l0) == 9
     np.testing.assert_allclose(W0, W1, rtol=1e-6, atol=1e-7)
+
+
+def _nosync_worker(rank, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("JUBATUS_FORCE_CPU", "1")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    from jubatus_amd.parallel.table_mix import TableMix
+    H, C = 4096, 8
+    W = torch.zeros(H, C)
+    touched = torch.zeros(H, dtype=torch.uint8)
+    touched[rank * 100:rank * 100 + 50] = 1
+    W[touched.bool()] = 1.0 + rank
+    calls = []
+    real_item, real_nonzero = torch.Tensor.item, torch.nonzero
+
+    def item(self):
+        calls.append("item")
+        return real_item(self)
+
+    def nonzero(*a, **k):
+        calls.append("nonzero")
+        return real_nonzero(*a, **k)
+    torch.Tensor.item, torch.nonzero = item, nonzero
+    try:
+        job = TableMix([W], touched, None).begin()      # must not synchronise with the device
+    finally:
+        torch.Tensor.item, torch.nonzero = real_item, real_nonzero
+    job.end()
+    q.put((rank, calls, job.stats(), float(W[0, 0]), float(W[100, 0])))
+    dist.destroy_process_group()
+
+
+def test_mix_begin_has_no_host_sync():
+    """the union of the touched rows is a MAX all-reduce of the
+    bitmaps, sized on the host only once it completed (ready / end) - begin
+    itself calls neither .item() nor nonzero"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_nosync_worker, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, calls, st, w0, w100 in res:
+        assert calls == [], calls
+        assert st["mode"] == "sparse" and st["rows"] == 100
+        assert w0 == 0.5 and w100 == 1.0                  # the mean of the two ranks' rows

@@ -82,7 +82,7 @@ def test_table_mix_equals_dense_mean(mode):
         if mode == "sparse":
             assert st["mode"] == "sparse"
             assert 200 <= st["rows"] <= 420                 # the union, not the table
-            assert nbytes == st["rows"] * 2 * C * 4
+            assert nbytes == st["rows"] * 2 * C * 4 + H      # rows + the union bitmap (uint8[H])
             assert left == 0                                 # touched map cleared
         else:
-            assert st["mode"] == "dense" and nbytes == H * 2 * C * 4
+            assert st["mode"] == "dense" and nbytes == H * 2 * C * 4 + H
