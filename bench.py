@@ -89,6 +89,12 @@ def make_requests(rng: random.Random, nreq: int, per_req: int, nlabels: int, n_s
     return bodies
 
 
+def _progress(msg: str) -> None:
+    """a progress line on stderr (long runs keep writing; the JSON line on
+    stdout stays the only stdout output)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -431,6 +437,7 @@ def engine_records(args, local: int) -> dict:
         srv = os.path.join(ROOT, "jubatus_amd", "native_bin", f"juba{engine}")
         nrows = args.lof_rows if engine == "anomaly" else args.engine_rows
         rec: dict = {"config": cfg, "rows": nrows, "server": f"native juba{engine} (no Python)"}
+        _progress(f"engine {name}: fill {nrows} rows")
         port = _free_port()
         p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", os.path.join(ROOT, cfg),
                               "-d", tmp, "-c", "4", "--gpu", str(local)],
@@ -471,6 +478,7 @@ def engine_records(args, local: int) -> dict:
             st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
                   for k, v in st.items()}
             rec["rows_stored"] = int(st.get("num_rows", -1))
+            _progress(f"engine {name}: filled in {rec['fill_s']} s; queries")
             lat = _loadgen(exe, port, query_m, q, 1, 1, secs=args.engine_seconds)
             rec[f"{query_m}_p50_us"] = lat["p50_us"]
             rec[f"{query_m}_p99_us"] = lat["p99_us"]
@@ -706,9 +714,12 @@ def main() -> None:
     import gc
     gc.collect()
     gc.freeze()
+    _progress(f"data ready ({t_gen:.1f} s): {bps} batches x {args.steps} steps; warmup")
     for i in range(args.warmup):
         for j in range(bps):
             train_batch(warm.batches[(i * bps + j) % len(warm.batches)])
+        sync()
+        _progress(f"warmup step {i + 1}/{args.warmup} done")
     finish_mix()
     if device is not None:
         clf.pipe.check_errors()
@@ -725,6 +736,8 @@ def main() -> None:
             train_batch(fresh.batches[i * bps + j])
         if trace_steps:
             marks.append(time.perf_counter())
+        if rank == 0 and (i + 1) % 5 == 0:
+            _progress(f"timed step {i + 1}/{args.steps} queued")
     finish_mix()          # the last MIX completes inside the timed region
     if inflight["work"] is not None:
         inflight["work"].wait()

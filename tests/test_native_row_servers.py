@@ -163,9 +163,32 @@ def _drive(pair, rng, steps, kind):
         want = _call(pair.p, op, *args)
         assert got[0] == want[0], (i, op, args, got, want)
         if got[0] == "ok":
-            _same(_norm(got[1]), _norm(want[1]), f"{i}:{op}")
+            g, w = _norm(got[1]), _norm(want[1])
+            if op.startswith(("similar_row", "neighbor_row")):
+                _same_ranked(g, w, f"{i}:{op}")
+            else:
+                _same(g, w, f"{i}:{op}")
         elif got[0] == "err":
             assert got[1] == want[1], (i, op, got, want)
+
+
+def _same_ranked(a, b, path):
+    """[(id, score)] rankings: the same scores in the same order; ids equal
+    up to the order inside a group of equal scores (the last group may be
+    cut at a different member by k)"""
+    assert len(a) == len(b), (path, a, b)
+    for x, y in zip(a, b):
+        assert math.isclose(x[1], y[1], rel_tol=1e-5, abs_tol=1e-5), (path, a, b)
+    groups = {}
+    for (ia, sa), (ib, _) in zip(a, b):
+        key = round(sa, 5)
+        ga, gb = groups.setdefault(key, (set(), set()))
+        ga.add(ia)
+        gb.add(ib)
+    last = round(a[-1][1], 5) if a else None
+    for key, (ga, gb) in groups.items():
+        if key != last:
+            assert ga == gb, (path, a, b)
 
 
 CASES = [
@@ -201,8 +224,11 @@ def test_native_row_server_matches_python(engine, cfg, tmp_path):
         assert not [k for k in COMMON if k not in st]
         # arity / type errors, unknown methods
         assert _call(pair.n, "get_all_rows", "x")[0] == "arg"
-        assert _call(pair.n, "similar_row_from_id", "r1", "five")[0] == "arg"
-        assert _call(pair.n, "similar_row_from_datum", [[["k", 1]], []], 3)[0] == "arg"
+        if engine != "anomaly":
+            assert _call(pair.n, "similar_row_from_id", "r1", "five")[0] == "arg"
+            assert _call(pair.n, "similar_row_from_datum", [[["k", 1]], []], 3)[0] == "arg"
+        else:
+            assert _call(pair.n, "calc_score", [[["k", 1]], []])[0] == "arg"
     finally:
         pair.close()
 
@@ -221,12 +247,17 @@ def test_native_row_model_files_both_ways(engine, cfg, tmp_path):
             a, b = pair.n.call(upd, "", f"{i % 45}", d), pair.p.call(upd, "", f"{i % 45}", d)
             _same(_norm(a), _norm(b), f"fill {i}")
         # native -> Python
+        # native -> Python: both load the native file (a load re-hashes the
+        # stored rows with the loaded document frequencies, re-lays the slots
+        # and resets the anomaly id counter - on both sides alike)
         (_, npath), = pair.n.call("save", "", "m1").items()
         npath = _norm(npath)
         ppath = os.path.join(str(tmp_path), f"127.0.0.1_{pair.pport}_{engine}_m1.jubatus")
         shutil.copy(npath, ppath)
         assert pair.p.call("clear", "") is True
         assert pair.p.call("load", "", "m1") is True
+        assert pair.n.call("load", "", "m1") is True
+        assert _norm(pair.n.call("get_all_rows", "")) == _norm(pair.p.call("get_all_rows", ""))
         _drive(pair, random.Random(8), 80, engine)
         # Python -> native
         (_, ppath2), = pair.p.call("save", "", "m2").items()
@@ -234,6 +265,7 @@ def test_native_row_model_files_both_ways(engine, cfg, tmp_path):
         shutil.copy(_norm(ppath2), npath2)
         assert pair.n.call("clear", "") is True
         assert pair.n.call("load", "", "m2") is True
+        assert pair.p.call("load", "", "m2") is True
         _drive(pair, random.Random(9), 80, engine)
         assert sorted(_norm(pair.n.call("get_all_rows", ""))) == sorted(_norm(pair.p.call("get_all_rows", "")))
     finally:
