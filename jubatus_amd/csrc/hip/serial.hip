@@ -25,9 +25,9 @@
 //      table, as the single-stream path would), D grows by its increments,
 //      and the rest of the round is re-checked against the new D.
 //   3. When the batch updates too much for this to pay (a round with many
-//      exact steps, or the D table full), the committer stops and the rest of
-//      the batch runs through the single-stream exact pipelined kernel
-//      (linear.hip, kExact) - the plain sequential update.
+//      exact steps), the committer stops and the rest of the batch runs
+//      through the single-stream exact pipelined kernel (linear.hip, kExact)
+//      - the plain sequential update.
 //
 // Rounding: the M0 margin and the exact rescoring sum in different orders, so
 // the slack keeps a relative guard band (kSlackGuard) - a sample within it of
@@ -36,11 +36,9 @@
 
 namespace jb {
 
-constexpr int kCommitThreads = 1024;
-constexpr int kDCap = 8192;          // D table slots (LDS hash, power of two)
-constexpr int kDBits = 13;
-constexpr int kDProbe = 32;          // linear-probe limit (a miss past it saturates)
-constexpr int kDFull = kDCap * 3 / 4;
+constexpr int kCommitThreads = 512;
+constexpr int kDBits = 14;
+constexpr int kDCap = 1 << kDBits;   // D table slots (LDS, direct-mapped)
 constexpr int kSerialNF = 16;        // features of a sample kept in registers
 constexpr float kSlackGuard = 1e-4f; // relative guard band of the slack
 
@@ -160,38 +158,18 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
 }
 
 // ------------------------------------------------------------ D table (LDS)
+// Direct-mapped, keyless: slot h(f) accumulates the increments of every row
+// that maps to it, so a lookup returns D[f] plus whatever collides with f -
+// an upper bound, which keeps the settle test conservative (a collision can
+// only cost an exact step, never a wrong decision). One LDS read per
+// feature, no probing, never full.
 struct DTable {
-  int32_t* key;
   float* val;
-  int* nkeys;
-  int* sat;
-
   __device__ __forceinline__ static uint32_t slot(int32_t idx) {
     return ((uint32_t)idx * 0x9E3779B1u) >> (32 - kDBits);
   }
-  __device__ __forceinline__ float get(int32_t idx) const {
-    uint32_t h = slot(idx);
-    for (int p = 0; p < kDProbe; ++p) {
-      const int32_t k = key[h];
-      if (k == idx) return val[h];
-      if (k < 0) return 0.f;
-      h = (h + 1) & (kDCap - 1);
-    }
-    return 0.f;   // never inserted past the probe limit (that saturates instead)
-  }
-  __device__ __forceinline__ void add(int32_t idx, float v) {
-    uint32_t h = slot(idx);
-    for (int p = 0; p < kDProbe; ++p) {
-      const int32_t old = atomicCAS(&key[h], -1, idx);
-      if (old == -1 || old == idx) {
-        atomicAdd(&val[h], v);
-        if (old == -1 && atomicAdd(nkeys, 1) + 1 >= kDFull) *sat = 1;
-        return;
-      }
-      h = (h + 1) & (kDCap - 1);
-    }
-    *sat = 1;
-  }
+  __device__ __forceinline__ float get(int32_t idx) const { return val[slot(idx)]; }
+  __device__ __forceinline__ void add(int32_t idx, float v) { atomicAdd(&val[slot(idx)], v); }
 };
 
 // Exact step of one sample against the live table (one wave; the committer
@@ -250,10 +228,81 @@ __device__ bool commit_sample(const int32_t* __restrict__ fidx, const float* __r
   return true;
 }
 
+// Exact step of one sample whose features sit in LDS (the owning thread
+// staged them), LC <= 64: every W / P element of the sample is gathered in
+// ONE round trip (lane (g, l0) loads features g, g + G, ... of label l0),
+// then the margin, the confidence of y / l* and the update follow from
+// registers. Same semantics as commit_sample.
+template <int LC>
+__device__ bool commit_staged(const int32_t* sI, const float* sX, int n, int y, float* W, float* P,
+                              bool act, int lane, int method, float C,
+                              uint8_t* __restrict__ touched, DTable& d) {
+  constexpr int G = 64 / LC;
+  constexpr int U = (kSerialNF + G - 1) / G;
+  const bool use_s = method >= CW;
+  const int g = lane / LC;
+  const int l0 = lane % LC;
+  int32_t ix[U];
+  float xv[U], w[U], pv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int j = u * G + g;
+    ix[u] = j < n ? sI[j] : -1;
+    xv[u] = j < n ? sX[j] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t row = (int64_t)(ix[u] >= 0 ? ix[u] : 0) * LC + l0;
+    w[u] = ld_agent(W + row);
+    pv[u] = use_s ? ld_agent(P + row) : 1.f;
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (ix[u] >= 0) acc += xv[u] * w[u];
+#pragma unroll
+  for (int off = LC; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
+  const float sy = __shfl(acc, y, 64);
+  float best = (act && l0 != y) ? acc : -INFINITY;
+  int bl = (act && l0 != y) ? l0 : -1;
+  argmax_wrong<LC>(best, bl);
+  const int lstar = __builtin_amdgcn_readfirstlane(bl);
+  best = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(best)));
+  const float margin = sy - (lstar >= 0 ? best : 0.f);
+  float v = 0.f, q = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (ix[u] < 0) continue;
+    const float x2 = xv[u] * xv[u];
+    if (l0 == 0) q += x2;
+    if (use_s && (l0 == y || (lstar >= 0 && l0 == lstar))) v += x2 * (1.f / pv[u]);
+  }
+  const float var = use_s ? wave_sum(v) : 0.f;
+  const float nrm = wave_sum(q);
+  float tau = 0.f, beta = 0.f;
+  if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return false;
+  const bool mine = l0 == y || (lstar >= 0 && l0 == lstar);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (ix[u] < 0 || !mine) continue;
+    const int64_t row = (int64_t)ix[u] * LC + l0;
+    const float a = use_s ? 1.f / pv[u] : 1.f;
+    const float dw = (l0 == y ? tau : -tau) * a * xv[u];
+    atomicAdd(W + row, dw);
+    if (use_s) atomicAdd(P + row, dprec(method, beta, xv[u], a));
+    if (touched != nullptr && l0 == y) touched[ix[u]] = 1;
+    d.add(ix[u], fabsf(dw));
+  }
+  return true;
+}
+
 // The ordered committer (see header). One workgroup of 1024 threads; thread t
-// owns sample p + t of the round starting at p. tail[0] receives the first
-// sample it did not settle (the end of the batch when it finished), tail[1]
-// the end of the batch: the exact single-stream kernel runs [tail[0], tail[1]).
+// owns sample p + t of the round starting at p, with the sample's slack,
+// label and features in registers (prefetched a round ahead: one load round
+// trip per round). The owner of the first unsettled sample stages it in LDS
+// for wave 0's exact step. tail[0] receives the first sample it did not
+// settle (the end of the batch when it finished), tail[1] the end of the
+// batch: the exact single-stream kernel runs [tail[0], tail[1]).
 template <int LC>
 __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
@@ -265,48 +314,67 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   using L = Lanes<LC>;
   constexpr int T = kCommitThreads;
   constexpr int NF = kSerialNF;
-  __shared__ int32_t s_key[kDCap];
+  constexpr bool kStaged = LC <= 64;
   __shared__ float s_val[kDCap];
-  __shared__ int s_first, s_sat, s_nkeys;
+  __shared__ int s_first[2];
   __shared__ unsigned s_valid;
+  __shared__ int32_t s_fi[NF];
+  __shared__ float s_fx[NF];
+  __shared__ int s_n, s_y;
+  __shared__ int64_t s_fb;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  for (int i = tid; i < kDCap; i += T) {
-    s_key[i] = -1;
-    s_val[i] = 0.f;
-  }
+  for (int i = tid; i < kDCap; i += T) s_val[i] = 0.f;
   if (tid == 0) {
-    s_sat = 0;
-    s_nkeys = 0;
     s_valid = 0;
+    s_first[0] = s_first[1] = INT_MAX;
   }
-  DTable d{s_key, s_val, &s_nkeys, &s_sat};
+  DTable d{s_val};
   bool act[L::K];
 #pragma unroll
   for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
-  __syncthreads();
   const int64_t beg = stream_ptr[0];
   const int64_t end = stream_ptr[nstreams];
+  // round descriptors of the next round (prefetched)
+  float n_sl = NAN;
+  int64_t n_fb = 0, n_fe = 0;
+  int n_y = -1;
+  if (beg + tid < end) {
+    n_sl = slack[tid];
+    n_fb = row_ptr[beg + tid];
+    n_fe = row_ptr[beg + tid + 1];
+    n_y = labels[beg + tid];
+  }
+  __syncthreads();
   unsigned n_upd = 0;
   int64_t stop = end;
+  int iter = 0;
   for (int64_t p = beg; p < end; p += T) {
     const int64_t j = p + tid;
     const bool live = j < end;
-    const float sl = live ? slack[j - beg] : NAN;
-    int64_t fb = 0;
-    int nf = 0;
-    if (live) {
-      fb = row_ptr[j];
-      nf = (int)(row_ptr[j + 1] - fb);
-    }
+    const float sl = n_sl;
+    const int64_t fb = n_fb;
+    const int nf = (int)(n_fe - n_fb);
+    const int yl = n_y;
     int32_t fi[NF];
     float fx[NF];
 #pragma unroll
     for (int u = 0; u < NF; ++u) {
-      const bool v = u < nf;
+      const bool v = live && u < nf;
       fi[u] = v ? fidx[fb + u] : -1;
-      fx[u] = v ? fabsf(fval[fb + u]) : 0.f;
+      fx[u] = v ? fval[fb + u] : 0.f;
+    }
+    // the next round's descriptors go in flight behind this round's features
+    const int64_t jn = j + T;
+    n_sl = NAN;
+    n_fb = n_fe = 0;
+    n_y = -1;
+    if (jn < end) {
+      n_sl = slack[jn - beg];
+      n_fb = row_ptr[jn];
+      n_fe = row_ptr[jn + 1];
+      n_y = labels[jn];
     }
     // only finite, non-negative slacks can be settled by the bound
     const bool open = live && !(sl != sl) && sl < INFINITY;
@@ -315,13 +383,13 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     for (;;) {
       bool unsafe = false;
       if (open && tid > lim) {
-        if (sl < 0.f || s_sat) {
+        if (sl < 0.f) {
           unsafe = true;
         } else {
           float b = 0.f;
 #pragma unroll
           for (int u = 0; u < NF; ++u)
-            if (fi[u] >= 0) b += fx[u] * d.get(fi[u]);
+            if (fi[u] >= 0) b += fabsf(fx[u]) * d.get(fi[u]);
           for (int u = NF; u < nf; ++u) {
             const int32_t idx = fidx[fb + u];
             if (idx >= 0) b += fabsf(fval[fb + u]) * d.get(idx);
@@ -329,27 +397,37 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
           unsafe = 2.f * b >= sl;
         }
       }
-      __syncthreads();     // every thread has read s_first / D of the last step
-      if (tid == 0) s_first = INT_MAX;
-      __syncthreads();
       const uint64_t m = __builtin_amdgcn_ballot_w64(unsafe);
-      if (lane == 0 && m != 0) atomicMin(&s_first, wv * 64 + (int)__builtin_ctzll(m));
-      __syncthreads();
-      const int k = s_first;
+      if (lane == 0 && m != 0) atomicMin(&s_first[iter & 1], wv * 64 + (int)__builtin_ctzll(m));
+      __syncthreads();     // A: the first unsettled sample of the round is known
+      const int k = s_first[iter & 1];
+      if (tid == 0) s_first[(iter + 1) & 1] = INT_MAX;
+      ++iter;
       if (k == INT_MAX) break;
+      if (tid == k) {      // the owner stages its sample for wave 0
+        s_n = nf;
+        s_y = yl;
+        s_fb = fb;
+        if (nf <= NF)
+          for (int u = 0; u < nf; ++u) { s_fi[u] = fi[u]; s_fx[u] = fx[u]; }
+      }
+      __syncthreads();     // B1
       if (wv == 0) {
-        const int64_t s = p + k;
-        const int64_t b0 = row_ptr[s];
-        if (commit_sample<LC>(fidx, fval, b0, (int)(row_ptr[s + 1] - b0), labels[s], W, P, act,
-                              lane, method, C, touched, d))
-          ++n_upd;
+        const int n = s_n;
+        bool up;
+        if (kStaged && n <= NF)
+          up = commit_staged<(LC <= 64 ? LC : 64)>(s_fi, s_fx, n, s_y, W, P, act[0], lane, method, C,
+                                                   touched, d);
+        else
+          up = commit_sample<LC>(fidx, fval, s_fb, n, s_y, W, P, act, lane, method, C, touched, d);
+        if (up) ++n_upd;
         // the next exact step reads what this one wrote
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       lim = k;
       ++steps;
-      __syncthreads();     // D / s_sat of the step visible to every wave
-      if (s_sat || steps > bail_after) {
+      __syncthreads();     // B2: D of the step visible to every wave
+      if (steps > bail_after) {
         stop = p + k + 1;
         break;
       }
