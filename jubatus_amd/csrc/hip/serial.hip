@@ -25,9 +25,9 @@
 //      table, as the single-stream path would), D grows by its increments,
 //      and the rest of the round is re-checked against the new D.
 //   3. When the batch updates too much for this to pay (a round with many
-//      exact steps), the committer stops and the rest of the batch runs
-//      through the single-stream exact pipelined kernel (linear.hip, kExact)
-//      - the plain sequential update.
+//      exact steps, or the D table full), the committer stops and the rest of
+//      the batch runs through the single-stream exact pipelined kernel
+//      (linear.hip, kExact) - the plain sequential update.
 //
 // Rounding: the M0 margin and the exact rescoring sum in different orders, so
 // the slack keeps a relative guard band (kSlackGuard) - a sample within it of
@@ -38,7 +38,10 @@ namespace jb {
 
 constexpr int kCommitThreads = 512;
 constexpr int kDBits = 14;
-constexpr int kDCap = 1 << kDBits;   // D table slots (LDS, direct-mapped)
+constexpr int kDCap = 1 << kDBits;   // D table slots (LDS hash, power of two)
+constexpr int kDProbe = 32;          // linear-probe limit (a miss past it saturates)
+constexpr int kDFull = kDCap * 5 / 8;
+constexpr int kBloomBits = 16;       // filter bits (8 KB of LDS)
 constexpr int kSerialNF = 16;        // features of a sample kept in registers
 constexpr float kSlackGuard = 1e-4f; // relative guard band of the slack
 
@@ -158,18 +161,54 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
 }
 
 // ------------------------------------------------------------ D table (LDS)
-// Direct-mapped, keyless: slot h(f) accumulates the increments of every row
-// that maps to it, so a lookup returns D[f] plus whatever collides with f -
-// an upper bound, which keeps the settle test conservative (a collision can
-// only cost an exact step, never a wrong decision). One LDS read per
-// feature, no probing, never full.
+// D[f] per row the batch has written, keyed (open addressing over kDCap
+// slots) behind a one-hash Bloom filter: the common lookup - a row nothing
+// wrote - is one LDS read of the filter. Keys past kDFull (or a probe run
+// past kDProbe) saturate the table: every later sample is then unsafe and
+// the committer hands the batch to the sequential kernel.
 struct DTable {
+  int32_t* key;
   float* val;
+  uint32_t* bloom;
+  int* nkeys;
+  int* sat;
+
   __device__ __forceinline__ static uint32_t slot(int32_t idx) {
     return ((uint32_t)idx * 0x9E3779B1u) >> (32 - kDBits);
   }
-  __device__ __forceinline__ float get(int32_t idx) const { return val[slot(idx)]; }
-  __device__ __forceinline__ void add(int32_t idx, float v) { atomicAdd(&val[slot(idx)], v); }
+  __device__ __forceinline__ static uint32_t fbit(int32_t idx) {
+    return ((uint32_t)idx * 0x85EBCA77u) >> (32 - kBloomBits);
+  }
+  __device__ __forceinline__ bool maybe(int32_t idx) const {
+    const uint32_t b = fbit(idx);
+    return (bloom[b >> 5] >> (b & 31)) & 1u;
+  }
+  __device__ __attribute__((noinline)) float probe(int32_t idx) const {
+    uint32_t h = slot(idx);
+    for (int p = 0; p < kDProbe; ++p) {
+      const int32_t k = key[h];
+      if (k == idx) return val[h];
+      if (k < 0) return 0.f;
+      h = (h + 1) & (kDCap - 1);
+    }
+    return 0.f;   // never inserted past the probe limit (that saturates instead)
+  }
+  __device__ __forceinline__ float get(int32_t idx) const { return maybe(idx) ? probe(idx) : 0.f; }
+  __device__ void add(int32_t idx, float v) {
+    const uint32_t b = fbit(idx);
+    atomicOr(&bloom[b >> 5], 1u << (b & 31));
+    uint32_t h = slot(idx);
+    for (int p = 0; p < kDProbe; ++p) {
+      const int32_t old = atomicCAS(&key[h], -1, idx);
+      if (old == -1 || old == idx) {
+        atomicAdd(&val[h], v);
+        if (old == -1 && atomicAdd(nkeys, 1) + 1 >= kDFull) *sat = 1;
+        return;
+      }
+      h = (h + 1) & (kDCap - 1);
+    }
+    *sat = 1;
+  }
 };
 
 // Exact step of one sample against the live table (one wave; the committer
@@ -315,8 +354,11 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   constexpr int T = kCommitThreads;
   constexpr int NF = kSerialNF;
   constexpr bool kStaged = LC <= 64;
+  __shared__ int32_t s_key[kDCap];
   __shared__ float s_val[kDCap];
+  __shared__ uint32_t s_bloom[(1 << kBloomBits) / 32];
   __shared__ int s_first[2];
+  __shared__ int s_sat, s_nkeys;
   __shared__ unsigned s_valid;
   __shared__ int32_t s_fi[NF];
   __shared__ float s_fx[NF];
@@ -325,12 +367,18 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wv = tid >> 6;
-  for (int i = tid; i < kDCap; i += T) s_val[i] = 0.f;
+  for (int i = tid; i < kDCap; i += T) {
+    s_key[i] = -1;
+    s_val[i] = 0.f;
+  }
+  for (int i = tid; i < (1 << kBloomBits) / 32; i += T) s_bloom[i] = 0u;
   if (tid == 0) {
     s_valid = 0;
+    s_sat = 0;
+    s_nkeys = 0;
     s_first[0] = s_first[1] = INT_MAX;
   }
-  DTable d{s_val};
+  DTable d{s_key, s_val, s_bloom, &s_nkeys, &s_sat};
   bool act[L::K];
 #pragma unroll
   for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
@@ -383,7 +431,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     for (;;) {
       bool unsafe = false;
       if (open && tid > lim) {
-        if (sl < 0.f) {
+        if (sl < 0.f || s_sat) {
           unsafe = true;
         } else {
           float b = 0.f;
@@ -426,8 +474,8 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       }
       lim = k;
       ++steps;
-      __syncthreads();     // B2: D of the step visible to every wave
-      if (steps > bail_after) {
+      __syncthreads();     // B2: D / s_sat of the step visible to every wave
+      if (s_sat || steps > bail_after) {
         stop = p + k + 1;
         break;
       }
