@@ -398,6 +398,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   unsigned n_upd = 0;
   int64_t stop = end;
   int iter = 0;
+  int64_t n_steps = 0, n_rounds = 0;
   for (int64_t p = beg; p < end; p += T) {
     const int64_t j = p + tid;
     const bool live = j < end;
@@ -474,12 +475,14 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       }
       lim = k;
       ++steps;
+      ++n_steps;
       __syncthreads();     // B2: D / s_sat of the step visible to every wave
       if (s_sat || steps > bail_after) {
         stop = p + k + 1;
         break;
       }
     }
+    ++n_rounds;
     // samples of this round settled here (valid label)
     const bool counted = live && !(sl != sl) && j < stop;
     const uint64_t cm = __builtin_amdgcn_ballot_w64(counted);
@@ -490,6 +493,8 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   if (tid == 0) {
     tail[0] = stop;
     tail[1] = end;
+    tail[2] = n_steps;      // diagnostics: exact steps, rounds of this batch
+    tail[3] = n_rounds;
     if (stats != nullptr && s_valid > 0) atomicAdd(stats + 1, (unsigned long long)s_valid);
   }
   if (tid == 0 && stats != nullptr && n_upd > 0) atomicAdd(stats, (unsigned long long)n_upd);

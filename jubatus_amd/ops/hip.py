@@ -577,6 +577,14 @@ class SerialScratch:
         self.buf = None
         self.nbytes = 0
 
+    def last_batch(self) -> dict:
+        """diagnostics of the last kSerial batch (synchronises): first sample
+        left to the sequential kernel, batch end, exact steps, rounds"""
+        if self.buf is None:
+            return {}
+        v = self.buf[:32].view(torch.int64).tolist()
+        return {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3]}
+
     def ptr(self, n_max: int) -> int:
         need = int(_fn("jb_serial_scratch_bytes")(int(n_max)))
         if need > self.nbytes:

@@ -44,7 +44,7 @@ def main():
                                device=dev, concurrent_update=mode)
         for y in range(16):
             clf.set_label(f"label{y}")
-        times, upd = [], []
+        times, upd, diag = [], [], []
         for b, arena in enumerate(data.batches):
             st0 = clf.train_stats()
             torch.cuda.synchronize()
@@ -54,17 +54,25 @@ def main():
             times.append((time.perf_counter() - t1) * 1e3)
             st1 = clf.train_stats()
             upd.append((st1["updated"] - st0["updated"]) / max(1, st1["trained"] - st0["trained"]))
+            if mode == "exact":
+                d = clf._serial.last_batch()
+                diag.append((d["exact_steps"], (d["end"] - d["tail_start"]) / max(1, d["end"])))
             if b % 10 == 9:
-                print(f"{mode} batch {b + 1}: {times[-1]:.2f} ms, update fraction {upd[-1]:.4f}",
+                print(f"{mode} batch {b + 1}: {times[-1]:.2f} ms, update fraction {upd[-1]:.4f}"
+                      + (f", exact steps {diag[-1][0]}, sequential tail {diag[-1][1]:.3f}" if diag else ""),
                       file=sys.stderr, flush=True)
-        for lo, hi in ((0, 5), (5, 20), (20, len(times))):
-            if lo >= len(times):
+        edges = [0, 5, 20] + list(range(40, len(times) + 1, max(20, len(times) // 10)))
+        for lo, hi in zip(edges, edges[1:] + [len(times)]):
+            if lo >= len(times) or hi <= lo:
                 continue
-            print(json.dumps({"mode": mode, "batches": [lo, min(hi, len(times))],
-                              "ms_per_batch": round(float(np.mean(times[lo:hi])), 3),
-                              "update_fraction": round(float(np.mean(upd[lo:hi])), 5),
-                              "samples_per_batch": a.requests * a.per_request,
-                              "worst_case": a.worst_case}), flush=True)
+            rec = {"mode": mode, "batches": [lo, min(hi, len(times))],
+                   "ms_per_batch": round(float(np.mean(times[lo:hi])), 3),
+                   "update_fraction": round(float(np.mean(upd[lo:hi])), 5),
+                   "samples_per_batch": a.requests * a.per_request, "worst_case": a.worst_case}
+            if diag:
+                rec["exact_steps"] = round(float(np.mean([x[0] for x in diag[lo:hi]])), 1)
+                rec["sequential_tail_fraction"] = round(float(np.mean([x[1] for x in diag[lo:hi]])), 4)
+            print(json.dumps(rec), flush=True)
         del clf
         torch.cuda.empty_cache()
 
