@@ -1,0 +1,86 @@
+"""8-rank rehearsals on the CPU (gloo, 127.0.0.1 rendezvous) of the paths an
+8-GPU node runs over RCCL: bench.py's self-launched data-parallel run with
+the overlapped MIX, and the push_mixer skip schedule (recursive doubling,
+skip_mixer.hpp:46-57) whose pairwise averages reach the exact cluster mean
+for a power-of-two world."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLD = 8
+
+CONV = {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+        "num_rules": [{"key": "*", "type": "num"}], "hash_max_size": 1 << 10}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _skip_worker(rank, port, q):
+    import torch.distributed as dist
+    os.environ["JUBATUS_FORCE_CPU"] = "1"
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=WORLD)
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.classifier import LinearClassifier
+    from jubatus_amd.parallel.push_mixer import skip_peers
+    clf = LinearClassifier("AROW", {"regularization_weight": 1.0}, DatumToFvConverter(CONV))
+    for lab in ("a", "b", "c"):
+        clf.set_label(lab)
+    data = [("abc"[(i + rank) % 3], {"x": f"v{(i * 7 + rank) % 11}", "n": float(i % 5 - rank)})
+            for i in range(30)]
+    clf.train(data)
+    W0, P0 = clf.W.copy(), clf.P.copy()
+    for peer in skip_peers(rank, WORLD):          # strides 4, 2, 1
+        clf.pair_mix(peer)
+    out = [None] * WORLD
+    dist.all_gather_object(out, (W0, P0, clf.W.copy(), clf.P.copy()))
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def test_skip_mixer_eight_ranks_reaches_the_mean():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_skip_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    meanW = np.mean([r[0] for r in res], axis=0)
+    meanP = np.mean([r[1] for r in res], axis=0)
+    for W0, P0, W, P in res:
+        np.testing.assert_allclose(W, meanW, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(P, meanP, rtol=1e-5, atol=1e-6)
+
+
+def test_bench_eight_ranks_cpu():
+    """bench.py --gpus 8 self-launches 8 ranks; the overlapped MIX runs on
+    every rank and rank 0 prints the one JSON line. The fresh stream of a
+    rank is bounded by --fresh-gb (here a few MB per rank)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(WORLD), "--steps", "2",
+           "--warmup", "1", "--device", "cpu", "--requests", "4", "--per-request", "8",
+           "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "2", "--engines", "none"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["n_gpus"] == WORLD and out["config"]["world_size_observed"] == WORLD
+    assert out["config"]["parallelism"] == f"dp{WORLD}"
+    assert out["timed_samples_per_rank"] == 2 * 2 * 4 * 8
+    assert out["config"]["global_batch"] == WORLD * 2 * 4 * 8
+    assert out["mix_last"] and out["mix_last"]["mode"] in ("sparse", "dense")
