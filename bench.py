@@ -505,6 +505,35 @@ def engine_records(args, local: int) -> dict:
     return out
 
 
+PIN_FRACTION = 0.6       # of MemAvailable, shared by the node's local ranks
+PIN_CAP = 56e9           # per rank
+
+
+def fresh_budget(fresh_gb: float, local_ranks: int) -> float:
+    """pinned bytes one rank may take for its fresh (timed) stream: the
+    ranks of a node together stay within PIN_FRACTION of the host's
+    available memory, each within PIN_CAP"""
+    if fresh_gb > 0:
+        return fresh_gb * 1e9
+    return min(PIN_CAP, PIN_FRACTION * _mem_available() / max(1, local_ranks))
+
+
+def _mix_summary(log: list) -> dict:
+    """per-MIX bytes per rank and host-observed latency (begin -> done) of
+    the MIXes completed in the timed steps"""
+    if not log:
+        return {"count": 0}
+    lat = sorted(m["latency_ms"] for m in log if m.get("latency_ms") is not None)
+    modes = {}
+    for m in log:
+        modes[m.get("mode")] = modes.get(m.get("mode"), 0) + 1
+    return {"count": len(log), "world": log[-1].get("world"), "modes": modes,
+            "bytes_per_rank_mean": int(np.mean([m.get("bytes", 0) for m in log])),
+            "rows_mean": int(np.mean([m.get("rows", 0) for m in log])),
+            "latency_ms_p50": lat[len(lat) // 2] if lat else None,
+            "latency_ms_max": lat[-1] if lat else None}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -639,8 +668,7 @@ def main() -> None:
     if args.batches_per_step > 0:
         bps = args.batches_per_step
     else:
-        budget = args.fresh_gb * 1e9 if args.fresh_gb > 0 else \
-            min(56e9, 0.6 * _mem_available() / max(1, local_world))
+        budget = fresh_budget(args.fresh_gb, local_world)
         bps = int(budget // max(1.0, batch_bytes * args.steps))
         bps = max(1, min(96, bps))
     t_gen = time.perf_counter()
@@ -659,10 +687,13 @@ def main() -> None:
         if world > 1:
             dist.barrier()
 
+    mix_log = []          # per-MIX stats (bytes per rank, begin->done latency) of the timed steps
+
     def finish_mix():
         if pending[0] is not None:
             clf.mix_end(pending[0])
             pending[0] = None
+            mix_log.append(dict(clf._last_mix))
 
     mixes = [0]
     agreed = {"version": None, "labels": False}
@@ -699,7 +730,9 @@ def main() -> None:
         if world > 1 and mix_due():
             mixes[0] += 1
             if args.mix_mode == "sync":
+                t1 = time.perf_counter()
                 clf.mix()
+                mix_log.append(dict(clf._last_mix, latency_ms=round((time.perf_counter() - t1) * 1e3, 3)))
             else:
                 finish_mix()
                 v = clf.labels.version()
@@ -730,6 +763,7 @@ def main() -> None:
     trace_steps = os.environ.get("JB_BENCH_TRACE") == "1"
     marks = []
     mixes[0] = 0
+    mix_log.clear()
     t0 = time.perf_counter()
     for i in range(args.steps):
         for j in range(bps):
@@ -834,6 +868,12 @@ def main() -> None:
             "timed_bytes_per_rank": int(fresh.nbytes),
             "update_fraction": round(updated / trained, 4) if trained else None,
             "mix_last": getattr(clf, "_last_mix", {}),
+            "mix_timed": _mix_summary(mix_log),
+            "pinned_bytes_per_rank": int(fresh.nbytes + warm.nbytes) if pinned else 0,
+            "pinned_budget": ({"fresh_gb_flag": args.fresh_gb,
+                               "rule": f"min({PIN_CAP / 1e9:.0f} GB, {PIN_FRACTION} x MemAvailable / local ranks)",
+                               "host_mem_available_bytes": int(_mem_available()), "local_ranks": local_world}
+                              if args.batches_per_step <= 0 else {"batches_per_step_flag": bps}),
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
             "served": served,

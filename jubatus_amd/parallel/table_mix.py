@@ -32,6 +32,7 @@ and more) instead of two full copies.
 from __future__ import annotations
 
 import os
+import time
 from typing import Sequence
 
 import torch
@@ -77,10 +78,13 @@ class TableMix:
         self._count = None         # (pinned count, event) of the union size copy
         self._aux = None           # the union all-reduce of a rank that went dense at once
         self.abandoned = False     # tables replaced meanwhile: run the collectives, fold nothing
+        self._t0 = None            # host clock at begin()
+        self.latency_ms = None     # begin() -> first observed completion (ready() or end())
 
     # ----------------------------------------------------------- begin
     def begin(self) -> "TableMix":
         """start the MIX (asynchronous: no host synchronisation here)"""
+        self._t0 = time.perf_counter()
         if self.n <= 1:
             if self.touched is not None:
                 self.touched.zero_()
@@ -198,6 +202,16 @@ class TableMix:
     # ------------------------------------------------------------ poll
     def ready(self) -> bool:
         """advance without blocking; True when ``end`` will not wait"""
+        r = self._ready()
+        if r:
+            self._stamp()
+        return r
+
+    def _stamp(self) -> None:
+        if self.latency_ms is None and self._t0 is not None:
+            self.latency_ms = round((time.perf_counter() - self._t0) * 1e3, 3)
+
+    def _ready(self) -> bool:
         if self._done:
             return True
         if self.mode == "union" and not self._advance_union(block=False):
@@ -231,8 +245,9 @@ class TableMix:
                     c0 += w
             self._sparse = None
         self._done = True
+        self._stamp()
         return self.nbytes
 
     def stats(self) -> dict:
         return {"mode": self.mode, "rows": self.rows, "bytes": self.nbytes,
-                "abandoned": self.abandoned}
+                "abandoned": self.abandoned, "latency_ms": self.latency_ms, "world": self.n}

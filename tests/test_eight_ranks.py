@@ -84,3 +84,18 @@ def test_bench_eight_ranks_cpu():
     assert out["timed_samples_per_rank"] == 2 * 2 * 4 * 8
     assert out["config"]["global_batch"] == WORLD * 2 * 4 * 8
     assert out["mix_last"] and out["mix_last"]["mode"] in ("sparse", "dense")
+    mt = out["mix_timed"]
+    assert mt["count"] >= 1 and mt["world"] == WORLD and mt["bytes_per_rank_mean"] > 0
+    assert mt["latency_ms_p50"] is not None and mt["latency_ms_p50"] >= 0
+    assert out["config"]["world_size_observed"] == WORLD
+
+
+def test_bench_pinned_budget_eight_ranks():
+    """the fresh-stream sizing rule: 8 local ranks together pin at most
+    0.6 x MemAvailable and each at most 56 GB"""
+    sys.path.insert(0, ROOT)
+    import bench
+    avail = bench._mem_available()
+    per_rank = bench.fresh_budget(0, WORLD)
+    assert per_rank <= 56e9 and WORLD * per_rank <= 0.6 * avail * 1.01
+    assert bench.fresh_budget(2.5, WORLD) == 2.5e9
