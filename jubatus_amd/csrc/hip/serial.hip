@@ -44,6 +44,9 @@ constexpr int kDFull = kDCap * 5 / 8;
 constexpr int kBloomBits = 16;       // filter bits (8 KB of LDS)
 constexpr int kSerialNF = 16;        // features of a sample kept in registers
 constexpr float kSlackGuard = 1e-4f; // relative guard band of the slack
+constexpr int kStepBits = 8;
+constexpr int kStepCap = 1 << kStepBits;  // step table slots
+constexpr int kStepList = 64;        // distinct rows of one step the table holds
 
 // scores of all labels of one sample with plain (L1-cached) loads: the
 // score pass reads a table nothing writes during the kernel
@@ -172,12 +175,22 @@ struct DTable {
   uint32_t* bloom;
   int* nkeys;
   int* sat;
+  // the current exact step's increments (row -> summed |increment|): a
+  // small keyed table the other threads read to grow their bounds
+  // incrementally after the step (cleared by wave 0 before the next one)
+  int32_t* skey;
+  float* sval;
+  int32_t* slist;
+  int* sn;
 
   __device__ __forceinline__ static uint32_t slot(int32_t idx) {
     return ((uint32_t)idx * 0x9E3779B1u) >> (32 - kDBits);
   }
   __device__ __forceinline__ static uint32_t fbit(int32_t idx) {
     return ((uint32_t)idx * 0x85EBCA77u) >> (32 - kBloomBits);
+  }
+  __device__ __forceinline__ static uint32_t sslot(int32_t idx) {
+    return ((uint32_t)idx * 0x9E3779B1u) >> (32 - kStepBits);
   }
   __device__ __forceinline__ bool maybe(int32_t idx) const {
     const uint32_t b = fbit(idx);
@@ -194,20 +207,115 @@ struct DTable {
     return 0.f;   // never inserted past the probe limit (that saturates instead)
   }
   __device__ __forceinline__ float get(int32_t idx) const { return maybe(idx) ? probe(idx) : 0.f; }
+  // increment of row idx in the last step (valid while *sn <= kStepList)
+  __device__ __forceinline__ float step_get(int32_t idx) const {
+    uint32_t h = sslot(idx);
+    for (int p = 0; p < kStepCap; ++p) {
+      const int32_t k = skey[h];
+      if (k == idx) return sval[h];
+      if (k < 0) return 0.f;
+      h = (h + 1) & (kStepCap - 1);
+    }
+    return 0.f;
+  }
   __device__ void add(int32_t idx, float v) {
     const uint32_t b = fbit(idx);
     atomicOr(&bloom[b >> 5], 1u << (b & 31));
     uint32_t h = slot(idx);
+    bool done = false;
     for (int p = 0; p < kDProbe; ++p) {
       const int32_t old = atomicCAS(&key[h], -1, idx);
       if (old == -1 || old == idx) {
         atomicAdd(&val[h], v);
         if (old == -1 && atomicAdd(nkeys, 1) + 1 >= kDFull) *sat = 1;
-        return;
+        done = true;
+        break;
       }
       h = (h + 1) & (kDCap - 1);
     }
-    *sat = 1;
+    if (!done) *sat = 1;
+    // the step table (past kStepList distinct rows the readers recompute
+    // their bounds from the D table instead)
+    if (*sn > kStepList) return;
+    h = sslot(idx);
+    for (int p = 0; p < kStepCap; ++p) {
+      const int32_t old = atomicCAS(&skey[h], -1, idx);
+      if (old == -1 || old == idx) {
+        atomicAdd(&sval[h], v);
+        if (old == -1) {
+          const int n = atomicAdd(sn, 1);
+          if (n < kStepList) slist[n] = (int32_t)h;
+          else *sn = kStepList + 1;
+        }
+        return;
+      }
+      h = (h + 1) & (kStepCap - 1);
+    }
+    *sn = kStepList + 1;
+  }
+  // sum_u |x_u| D[idx_u] over a sample's first NF features: the filter
+  // words and first probe slots of all features are read together (one LDS
+  // round trip), the rare longer probe chains after
+  // (in chunks of 8 features: fewer live registers)
+  template <int NF>
+  __device__ __forceinline__ float bound(const int32_t (&ix)[NF], const float (&xv)[NF]) const {
+    constexpr int B = 8;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < NF; c += B) {
+      uint32_t bw[B];
+      int32_t k0[B];
+      float v0[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int32_t idx = ix[c + u] >= 0 ? ix[c + u] : 0;
+        const uint32_t b = fbit(idx);
+        const uint32_t h = slot(idx);
+        bw[u] = (bloom[b >> 5] >> (b & 31)) & 1u;
+        k0[u] = key[h];
+        v0[u] = val[h];
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int32_t idx = ix[c + u];
+        if (idx < 0 || !bw[u] || k0[u] < 0) continue;
+        acc += fabsf(xv[c + u]) * (k0[u] == idx ? v0[u] : probe(idx));
+      }
+    }
+    return acc;
+  }
+  // the same over the step table (the increments of the last exact step)
+  template <int NF>
+  __device__ __forceinline__ float step_bound(const int32_t (&ix)[NF], const float (&xv)[NF]) const {
+    constexpr int B = 8;
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < NF; c += B) {
+      int32_t k0[B];
+      float v0[B];
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const uint32_t h = sslot(ix[c + u] >= 0 ? ix[c + u] : 0);
+        k0[u] = skey[h];
+        v0[u] = sval[h];
+      }
+#pragma unroll
+      for (int u = 0; u < B; ++u) {
+        const int32_t idx = ix[c + u];
+        if (idx < 0 || k0[u] < 0) continue;
+        acc += fabsf(xv[c + u]) * (k0[u] == idx ? v0[u] : step_get(idx));
+      }
+    }
+    return acc;
+  }
+  // wave 0, before a step: empty the step table
+  __device__ void step_clear(int lane) {
+    const int n = *sn;
+    if (n > kStepList) {
+      for (int i = lane; i < kStepCap; i += 64) { skey[i] = -1; sval[i] = 0.f; }
+    } else {
+      for (int i = lane; i < n; i += 64) { skey[slist[i]] = -1; sval[slist[i]] = 0.f; }
+    }
   }
 };
 
@@ -323,14 +431,19 @@ __device__ bool commit_staged(const int32_t* sI, const float* sX, int n, int y, 
   const bool mine = l0 == y || (lstar >= 0 && l0 == lstar);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (ix[u] < 0 || !mine) continue;
-    const int64_t row = (int64_t)ix[u] * LC + l0;
-    const float a = use_s ? 1.f / pv[u] : 1.f;
-    const float dw = (l0 == y ? tau : -tau) * a * xv[u];
-    atomicAdd(W + row, dw);
-    if (use_s) atomicAdd(P + row, dprec(method, beta, xv[u], a));
-    if (touched != nullptr && l0 == y) touched[ix[u]] = 1;
-    d.add(ix[u], fabsf(dw));
+    float mag = 0.f;
+    if (ix[u] >= 0 && mine) {
+      const int64_t row = (int64_t)ix[u] * LC + l0;
+      const float a = use_s ? 1.f / pv[u] : 1.f;
+      const float dw = (l0 == y ? tau : -tau) * a * xv[u];
+      atomicAdd(W + row, dw);
+      if (use_s) atomicAdd(P + row, dprec(method, beta, xv[u], a));
+      if (touched != nullptr && l0 == y) touched[ix[u]] = 1;
+      mag = fabsf(dw);
+    }
+    // the y lane adds the feature's two increments to D in one go
+    const float other = __shfl(mag, g * LC + (lstar >= 0 ? lstar : y), 64);
+    if (ix[u] >= 0 && l0 == y) d.add(ix[u], mag + (lstar >= 0 ? other : 0.f));
   }
   return true;
 }
@@ -357,6 +470,10 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   __shared__ int32_t s_key[kDCap];
   __shared__ float s_val[kDCap];
   __shared__ uint32_t s_bloom[(1 << kBloomBits) / 32];
+  __shared__ int32_t s_skey[kStepCap];
+  __shared__ float s_sval[kStepCap];
+  __shared__ int32_t s_slist[kStepList];
+  __shared__ int s_sn;
   __shared__ int s_first[2];
   __shared__ int s_sat, s_nkeys;
   __shared__ unsigned s_valid;
@@ -372,13 +489,18 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     s_val[i] = 0.f;
   }
   for (int i = tid; i < (1 << kBloomBits) / 32; i += T) s_bloom[i] = 0u;
+  for (int i = tid; i < kStepCap; i += T) {
+    s_skey[i] = -1;
+    s_sval[i] = 0.f;
+  }
   if (tid == 0) {
+    s_sn = 0;
     s_valid = 0;
     s_sat = 0;
     s_nkeys = 0;
     s_first[0] = s_first[1] = INT_MAX;
   }
-  DTable d{s_key, s_val, s_bloom, &s_nkeys, &s_sat};
+  DTable d{s_key, s_val, s_bloom, &s_nkeys, &s_sat, s_skey, s_sval, s_slist, &s_sn};
   bool act[L::K];
 #pragma unroll
   for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
@@ -399,6 +521,11 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   int64_t stop = end;
   int iter = 0;
   int64_t n_steps = 0, n_rounds = 0;
+  // diagnostics: shader-clock cycles thread 0 spends per phase (bound
+  // checks, barrier A, staging + B1, the exact step, B2, round setup)
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  const uint64_t w0 = wall_clock64();
+  uint64_t tc = clock64();
   for (int64_t p = beg; p < end; p += T) {
     const int64_t j = p + tid;
     const bool live = j < end;
@@ -429,26 +556,25 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     const bool open = live && !(sl != sl) && sl < INFINITY;
     int lim = -1;          // round offsets <= lim are settled
     int steps = 0;
-    for (;;) {
-      bool unsafe = false;
-      if (open && tid > lim) {
-        if (sl < 0.f || s_sat) {
-          unsafe = true;
-        } else {
-          float b = 0.f;
-#pragma unroll
-          for (int u = 0; u < NF; ++u)
-            if (fi[u] >= 0) b += fabsf(fx[u]) * d.get(fi[u]);
-          for (int u = NF; u < nf; ++u) {
-            const int32_t idx = fidx[fb + u];
-            if (idx >= 0) b += fabsf(fval[fb + u]) * d.get(idx);
-          }
-          unsafe = 2.f * b >= sl;
-        }
+    // the sample's bound 2 * sum_f |x_f| D_f: from the D table once per
+    // round, then grown by each exact step's increments (step table)
+    auto full_bound = [&]() {
+      float b = d.bound<NF>(fi, fx);
+      for (int u = NF; u < nf; ++u) {
+        const int32_t idx = fidx[fb + u];
+        if (idx >= 0) b += fabsf(fval[fb + u]) * d.get(idx);
       }
+      return b;
+    };
+    float bnd = (open && sl >= 0.f && !s_sat) ? full_bound() : 0.f;
+    { const uint64_t t = clock64(); ph[5] += t - tc; tc = t; }
+    for (;;) {
+      const bool unsafe = open && tid > lim && (sl < 0.f || s_sat || 2.f * bnd >= sl);
       const uint64_t m = __builtin_amdgcn_ballot_w64(unsafe);
       if (lane == 0 && m != 0) atomicMin(&s_first[iter & 1], wv * 64 + (int)__builtin_ctzll(m));
+      { const uint64_t t = clock64(); ph[0] += t - tc; tc = t; }
       __syncthreads();     // A: the first unsettled sample of the round is known
+      { const uint64_t t = clock64(); ph[1] += t - tc; tc = t; }
       const int k = s_first[iter & 1];
       if (tid == 0) s_first[(iter + 1) & 1] = INT_MAX;
       ++iter;
@@ -460,8 +586,17 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         if (nf <= NF)
           for (int u = 0; u < nf; ++u) { s_fi[u] = fi[u]; s_fx[u] = fx[u]; }
       }
+      if (wv == 0) {       // nobody reads the previous step's table past barrier A
+        d.step_clear(lane);
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) s_sn = 0;
+      }
       __syncthreads();     // B1
+      { const uint64_t t = clock64(); ph[2] += t - tc; tc = t; }
       if (wv == 0) {
+        // this step reads what the previous one wrote (its atomics drained
+        // meanwhile, behind barriers A / B1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int n = s_n;
         bool up;
         if (kStaged && n <= NF)
@@ -470,16 +605,23 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         else
           up = commit_sample<LC>(fidx, fval, s_fb, n, s_y, W, P, act, lane, method, C, touched, d);
         if (up) ++n_upd;
-        // the next exact step reads what this one wrote
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       lim = k;
       ++steps;
       ++n_steps;
-      __syncthreads();     // B2: D / s_sat of the step visible to every wave
+      { const uint64_t t = clock64(); ph[3] += t - tc; tc = t; }
+      __syncthreads();     // B2: D / the step table / s_sat visible to every wave
+      { const uint64_t t = clock64(); ph[4] += t - tc; tc = t; }
       if (s_sat || steps > bail_after) {
         stop = p + k + 1;
         break;
+      }
+      if (open && tid > k && sl >= 0.f) {
+        if (s_sn > kStepList || nf > NF) {
+          bnd = full_bound();
+        } else {
+          bnd += d.step_bound<NF>(fi, fx);
+        }
       }
     }
     ++n_rounds;
@@ -495,6 +637,9 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     tail[1] = end;
     tail[2] = n_steps;      // diagnostics: exact steps, rounds of this batch
     tail[3] = n_rounds;
+    for (int i = 0; i < 6; ++i) tail[4 + i] = (int64_t)ph[i];
+    tail[10] = (int64_t)(wall_clock64() - w0);    // 100 MHz ticks
+    tail[11] = (int64_t)(clock64() - tc) + (int64_t)(ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5]);
     if (stats != nullptr && s_valid > 0) atomicAdd(stats + 1, (unsigned long long)s_valid);
   }
   if (tid == 0 && stats != nullptr && n_upd > 0) atomicAdd(stats, (unsigned long long)n_upd);

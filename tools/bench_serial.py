@@ -56,7 +56,8 @@ def main():
             upd.append((st1["updated"] - st0["updated"]) / max(1, st1["trained"] - st0["trained"]))
             if mode == "exact":
                 d = clf._serial.last_batch()
-                diag.append((d["exact_steps"], (d["end"] - d["tail_start"]) / max(1, d["end"])))
+                diag.append((d["exact_steps"], (d["end"] - d["tail_start"]) / max(1, d["end"]),
+                             {k: v for k, v in d.items() if k.startswith("commit")}))
             if b % 10 == 9:
                 print(f"{mode} batch {b + 1}: {times[-1]:.2f} ms, update fraction {upd[-1]:.4f}"
                       + (f", exact steps {diag[-1][0]}, sequential tail {diag[-1][1]:.3f}" if diag else ""),
@@ -72,6 +73,8 @@ def main():
             if diag:
                 rec["exact_steps"] = round(float(np.mean([x[0] for x in diag[lo:hi]])), 1)
                 rec["sequential_tail_fraction"] = round(float(np.mean([x[1] for x in diag[lo:hi]])), 4)
+                for key in diag[lo][2]:
+                    rec[key] = round(float(np.mean([x[2].get(key, 0) for x in diag[lo:hi]])), 1)
             print(json.dumps(rec), flush=True)
         del clf
         torch.cuda.empty_cache()
