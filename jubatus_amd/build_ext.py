@@ -131,6 +131,9 @@ TOOLS = {
     "jubavisor": (["visor/jubavisor.cpp", "native/jb_rpc.cpp"],
                   ["visor", "native", "../client_cpp/include"]),
     "jubaloadgen": (["tools/jubaloadgen.cpp", "native/jb_rpc.cpp"], ["native"]),
+    # host-only rehearsal of the native distributed model plane (jb_mix_group.hpp)
+    "jb_mix_rehearsal": (["tools/jb_mix_rehearsal.cpp", "native/jb_rpc.cpp"],
+                         ["native", "../client_cpp/include"]),
 }
 
 
@@ -160,7 +163,7 @@ def build_tools(force: bool = False, nproc: int = 8, sanitize: str | None = None
 # kernel library (linked against libjubatus_hip.so, found via $ORIGIN/..)
 SERVERS = {
     "jubaclassifier": (["server/jubaclassifier.cpp", "native/jb_rpc.cpp"],
-                       ["server", "native", "hip"]),
+                       ["server", "native", "hip"]),   # + RCCL (distributed mode)
     "jubaregression": (["server/jubaregression.cpp", "native/jb_rpc.cpp"],
                        ["server", "native", "hip"]),
     # row engines over the LSH / inverted-index kernels (jb_row_server.hpp)
@@ -174,8 +177,12 @@ SERVERS = {
     "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubaburst": (["server/jubaburst.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubagraph": (["server/jubagraph.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    # check of the RCCL data plane of the native MIX on one GPU (not a server)
+    "jb_rccl_check": (["tools/jb_rccl_check.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }
 HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph"}
+# servers with a native distributed mode (the model plane over RCCL)
+RCCL_SERVERS = {"jubaclassifier", "jb_rccl_check"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:
@@ -186,10 +193,13 @@ def build_servers(force: bool = False, nproc: int = 8) -> str:
     for name, (srcs, incs) in SERVERS.items():
         target = os.path.join(NATIVE_BIN, name)
         paths = [os.path.join(CSRC, x) for x in srcs]
+        incs = incs + ["../client_cpp/include"]
         deps = paths + [HIP_SO] + [h for d in incs for h in glob.glob(os.path.join(CSRC, d, "*.h*"))]
         libs = [] if name in HOST_SERVERS else [
             f"-L{PKG}", "-ljubatus_hip", "-L/opt/rocm/lib", "-lamdhip64",
             "-Wl,-rpath,$ORIGIN/..", "-Wl,-rpath,/opt/rocm/lib"]
+        if name in RCCL_SERVERS:
+            libs.append("-lrccl")
         if force or _newer(target, deps):
             jobs.append((target, ["g++", "-O2", "-std=c++17", "-pthread", "-Wall",
                                   "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",

@@ -524,6 +524,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   // diagnostics: shader-clock cycles thread 0 spends per phase (bound
   // checks, barrier A, staging + B1, the exact step, B2, round setup)
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t wwork = 0, tw = clock64();   // per wave: cycles from B2 to the next ballot
   const uint64_t w0 = wall_clock64();
   uint64_t tc = clock64();
   for (int64_t p = beg; p < end; p += T) {
@@ -566,10 +567,12 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       }
       return b;
     };
+    tw = clock64();
     float bnd = (open && sl >= 0.f && !s_sat) ? full_bound() : 0.f;
     { const uint64_t t = clock64(); ph[5] += t - tc; tc = t; }
     for (;;) {
       const bool unsafe = open && tid > lim && (sl < 0.f || s_sat || 2.f * bnd >= sl);
+      wwork += clock64() - tw;
       const uint64_t m = __builtin_amdgcn_ballot_w64(unsafe);
       if (lane == 0 && m != 0) atomicMin(&s_first[iter & 1], wv * 64 + (int)__builtin_ctzll(m));
       { const uint64_t t = clock64(); ph[0] += t - tc; tc = t; }
@@ -612,6 +615,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       { const uint64_t t = clock64(); ph[3] += t - tc; tc = t; }
       __syncthreads();     // B2: D / the step table / s_sat visible to every wave
       { const uint64_t t = clock64(); ph[4] += t - tc; tc = t; }
+      tw = clock64();
       if (s_sat || steps > bail_after) {
         stop = p + k + 1;
         break;
@@ -632,6 +636,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     if (stop != end) break;
   }
   __syncthreads();
+  if (lane == 0) tail[12 + wv] = (int64_t)wwork;
   if (tid == 0) {
     tail[0] = stop;
     tail[1] = end;

@@ -298,6 +298,7 @@ class Coord {
     return true;
   }
   const std::string& connected() const { return connected_; }
+  int64_t session() const { return sid_; }
 
  private:
   Value call_locked(const std::string& m, std::vector<Value> args) {

@@ -6,6 +6,7 @@
 //
 // Every server names itself once (set_engine) before anything else runs.
 #pragma once
+#include "jb_coord_client.hpp"
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -94,6 +95,7 @@ struct Args {
       mixer = "linear_mixer";
   int interval_sec = 16, interval_count = 512;
   int gpu = -1;
+  std::string connected_zookeeper;   // distributed mode: the coordinator in use
 };
 
 inline std::string real_path(const std::string& p) {
@@ -513,13 +515,14 @@ inline void common_status(const Args& a, const CommonStatus& cs, uint64_t update
   add("timeout", std::to_string(a.timeout));
   add("threadnum", std::to_string(a.threads));
   add("datadir", a.datadir);
-  add("is_standalone", "1");
+  add("is_standalone", a.zookeeper.empty() ? "1" : "0");
   add("VERSION", kVersion);
   add("PROGNAME", prog_name());
   add("type", engine_name());
   add("logdir", a.logdir);
   add("log_config", a.log_config);
-  add("configpath", a.configpath);
+  add("configpath",
+      a.zookeeper.empty() ? a.configpath : std::string("/jubatus/config/") + engine_name() + "/" + a.name);
   add("pid", std::to_string(getpid()));
   add("user", user_name());
   add("update_count", std::to_string(update_count));
@@ -528,6 +531,17 @@ inline void common_status(const Args& a, const CommonStatus& cs, uint64_t update
   add("last_loaded", std::to_string(cs.last_loaded));
   add("last_loaded_path", cs.last_loaded_path);
   add("gpu", a.gpu >= 0 ? std::to_string(a.gpu) : std::string());
+  if (!a.zookeeper.empty()) {   // distributed mode (server_helper.py get_status)
+    add("zk", a.zookeeper);
+    add("name", a.name);
+    add("interval_sec", std::to_string(a.interval_sec));
+    add("interval_count", std::to_string(a.interval_count));
+    add("zookeeper_timeout", std::to_string(a.zk_timeout));
+    add("interconnect_timeout", std::to_string(a.ic_timeout));
+    add("connected_zookeeper", a.connected_zookeeper);
+    add("use_cht", "0");
+    add("mixer", a.mixer);
+  }
 }
 
 // Startup shared by the servers, before any GPU call: flags, the decision
@@ -535,8 +549,27 @@ inline void common_status(const Args& a, const CommonStatus& cs, uint64_t update
 // (the model file's wins over -f, server_helper.hpp). Returns -1 to go on,
 // otherwise the exit code. check(text, why) says whether the config is
 // served natively; --native-check prints that decision and exits.
+// config text of a distributed server: /jubatus/config/<engine>/<name> on
+// the coordinator (server_util.py get_conf); false when absent/unreachable
+inline bool config_from_coordinator(const Args& a, std::string* text, std::string* why) {
+  try {
+    jb::cc::Coord c(a.zookeeper, std::max(1, a.zk_timeout), "config");
+    const bool ok = c.read(std::string("/jubatus/config/") + engine_name() + "/" + a.name, text);
+    c.close();
+    if (!ok) *why = std::string("config is not found: /jubatus/config/") + engine_name() + "/" + a.name;
+    return ok;
+  } catch (const std::exception& e) {
+    *why = e.what();
+    return false;
+  }
+}
+
+// native_dist: the engine serves distributed mode (-z) natively with the
+// linear mixer (csrc/native/jb_mix_group.hpp); other mixers and engines are
+// handed to the Python server
 template <class Check>
-int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool needs_gpu = true) {
+int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool needs_gpu = true,
+            bool native_dist = false) {
   int rc = parse_args(argc, argv, a);
   if (rc == -1) return 0;
   if (rc) return rc;
@@ -546,13 +579,20 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool
   }
   const char* force = a->native_check ? nullptr : getenv("JUBATUS_NATIVE_SERVER");
   if (force && strcmp(force, "0") == 0) exec_python(argc, argv, "JUBATUS_NATIVE_SERVER=0");
+  const bool dist = !a->zookeeper.empty();
   if (!a->native_check) {
-    if (!a->zookeeper.empty()) exec_python(argc, argv, "distributed mode");
+    if (dist && !native_dist) exec_python(argc, argv, "distributed mode");
+    if (dist && a->mixer != "linear_mixer") exec_python(argc, argv, "distributed mode with a push mixer");
     if (needs_gpu && (a->cpu || getenv("JUBATUS_FORCE_CPU")))
       exec_python(argc, argv, "host backend requested");
     if (needs_gpu && access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
   }
-  if (a->configpath.empty() && a->model_file.empty()) {
+  if (dist && a->name.empty()) {
+    fprintf(stderr, "can't start multinode mode without name specified\n");
+    usage(stderr);
+    return 1;
+  }
+  if (!dist && a->configpath.empty() && a->model_file.empty()) {
     fprintf(stderr, "config path or model file must be specified for standalone mode\n");
     usage(stderr);
     return 1;
@@ -574,7 +614,17 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool
   } else {
     a->eth = default_v4();
   }
-  if (!a->model_file.empty()) {
+  if (dist) {
+    std::string why;
+    if (!config_from_coordinator(*a, text, &why)) {
+      if (a->native_check) {
+        printf("python: %s\n", why.c_str());
+        return 0;
+      }
+      fprintf(stderr, "%s: %s\n", prog_name(), why.c_str());
+      return 1;
+    }
+  } else if (!a->model_file.empty()) {
     std::string bytes;
     ModelFile mf;
     if (!read_file(a->model_file, &bytes)) exec_python(argc, argv, "unreadable model file");

@@ -38,12 +38,15 @@
 #include <chrono>
 #include <condition_variable>
 #include <memory>
+#include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
 #include "jb_hash.hpp"
 #include "jb_hostfv.hpp"
+#include "jb_mix_device.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_pack.hpp"
 #include "jb_rpc.hpp"
@@ -65,6 +68,14 @@ extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, c
 extern "C" int jb_classify_direct(const int32_t* idx, const float* val, const int64_t* row_ptr,
                                   int n, const float* W, int LC, float* out_host,
                                   uint32_t* done_host, hipStream_t stream);
+extern "C" int jb_mix_take(uint8_t* touched, uint8_t* mark, int64_t H, hipStream_t st);
+extern "C" int64_t jb_mix_compact_temp_bytes(int64_t H);
+extern "C" int jb_mix_compact(const uint8_t* mark, int64_t H, int64_t* rows, int64_t* count, void* temp,
+                              int64_t temp_bytes, hipStream_t st);
+extern "C" int jb_mix_gather(const float* W, const float* S, int LC, const int64_t* rows, int64_t n,
+                             const int32_t* map, int Lc, float* snap, hipStream_t st);
+extern "C" int jb_mix_fold(float* W, float* S, int LC, const int64_t* rows, int64_t n, const int32_t* map,
+                           int Lc, const float* snap, const float* red, float inv_n, hipStream_t st);
 extern "C" void* jb_host_alloc(int64_t nbytes);
 extern "C" int jb_host_free(void* p);
 extern "C" int64_t jb_hot_rep_bytes();
@@ -125,7 +136,7 @@ bool parse_config(const std::string& text, Config* c, std::string* why) {
 }
 
 // ------------------------------------------------------------------ model
-class Classifier {
+class Classifier : public jb::mix::Mixable {
  public:
   std::atomic<uint64_t> update_count{0};
   std::atomic<uint64_t> train_calls{0}, train_batches{0};
@@ -389,6 +400,7 @@ class Classifier {
     update_count += 1;
     std::lock_guard<std::mutex> g(mu_);
     HIPCHK(hipDeviceSynchronize());
+    count_base_.clear();
     labels_.clear();
     alloc_locked(kLabelCaps[0], true);
   }
@@ -491,6 +503,204 @@ class Classifier {
     }
   }
 
+  // ------------------------------------------------------------ MIX
+  // distributed mode: the train kernels mark the rows they write (touched_)
+  // and the linear mixer (jb_mix_group.hpp) runs mix() / hand_over() on its
+  // thread. Python twin: models/classifier.py mix_begin / mix_end /
+  // broadcast_from over parallel/table_mix.py.
+  void enable_mix() {
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipStreamCreateWithFlags(&mixs_, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&mix_ev_, hipEventDisableTiming));
+    HIPCHK(hipMalloc((void**)&touched_, H_));
+    HIPCHK(hipMemset(touched_, 1, H_));   // the first MIX is dense
+    count_host_ = (int64_t*)jb_host_alloc(8);
+    if (!count_host_) throw std::runtime_error("hipHostMalloc failed");
+  }
+
+  std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& star, double dl) {
+    return jb::mix::make_device_plane(star, device, mixs_, dl);
+  }
+
+  uint64_t mix(jb::mix::Group& grp) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    // 1. label agreement: the canonical order is rank 0's labels, then the
+    //    labels only later ranks have, in rank order
+    std::string mine;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      for (size_t c = 0; c < nm.size(); ++c)
+        if (al[c]) put_name(&mine, nm[c]);
+    }
+    const auto parts = star.allgather(mine, grp.deadline());
+    std::vector<std::string> canon;
+    {
+      std::set<std::string> seen;
+      for (const auto& p : parts)
+        for (auto& n : get_names(p))
+          if (seen.insert(n).second) canon.push_back(n);
+    }
+    const int Lc = (int)canon.size();
+    std::vector<int32_t> map((size_t)std::max(Lc, 1), 0);
+    std::vector<int64_t> delta((size_t)std::max(Lc, 1), 0);
+    std::vector<uint64_t> cur_at((size_t)std::max(Lc, 1), 0);
+    uint64_t gen;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& n : canon)
+        if (labels_.lookup(n) < 0 && labels_.get_or_add(n.data(), n.size()) < 0)
+          throw std::runtime_error("label table full");
+      sync_labels_locked();
+      for (int c = 0; c < Lc; ++c) {
+        const int col = labels_.lookup(canon[c]);
+        map[c] = col;
+        cur_at[c] = labels_.count(col);
+        delta[c] = (int64_t)cur_at[c] - (int64_t)count_base_[canon[c]];
+      }
+      mark_.get(H_);
+      // the touched rows so far, in stream order behind the queued training
+      if (jb_mix_take(touched_, mark_.p, (int64_t)H_, compute_) != 0) throw std::runtime_error("jb_mix_take failed");
+      HIPCHK(hipEventRecord(mix_ev_, compute_));
+      HIPCHK(hipStreamWaitEvent(mixs_, mix_ev_, 0));
+      gen = gen_;
+    }
+    // 2. label counts: base + the cluster's summed deltas since the last MIX
+    star.allreduce_sum(delta.data(), (size_t)Lc, grp.deadline());
+    uint64_t bytes = 8ull * Lc;
+    // 3. the union of the touched rows (MAX all-reduce of the bitmaps)
+    pl.allreduce_max(mark_.p, H_, grp.deadline());
+    bytes += H_;
+    const int64_t tb = jb_mix_compact_temp_bytes((int64_t)H_);
+    if (tb < 0) throw std::runtime_error("jb_mix_compact_temp_bytes failed");
+    rows_.get(H_);
+    count_dev_.get(1);
+    temp_.get((size_t)std::max<int64_t>(tb, 1));
+    if (jb_mix_compact(mark_.p, (int64_t)H_, rows_.p, count_dev_.p, temp_.p, tb, mixs_) != 0)
+      throw std::runtime_error("jb_mix_compact failed");
+    HIPCHK(hipMemcpyAsync(count_host_, count_dev_.p, 8, hipMemcpyDeviceToHost, mixs_));
+    jb::mix::wait_stream(mixs_, grp.deadline());
+    const int64_t nu = *(volatile int64_t*)count_host_;
+    const bool dense = (uint64_t)nu * 2 > H_;
+    const int64_t* rows = dense ? nullptr : rows_.p;
+    const int64_t n = dense ? (int64_t)H_ : nu;
+    last_rows_ = (uint64_t)n;
+    last_dense_ = dense;
+    bool applied = true;
+    if (n > 0 && Lc > 0) {
+      const size_t width = (size_t)(use_s_ ? 2 : 1) * Lc;
+      const size_t elems = (size_t)n * width;
+      // 4. snapshot of the union rows (behind the queued training), then the
+      //    SUM all-reduce while training goes on
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (gen != gen_) {
+          applied = false;
+        } else {
+          HIPCHK(hipMemcpyAsync(map_dev_.get((size_t)Lc), map.data(), 4 * (size_t)Lc, hipMemcpyHostToDevice,
+                                compute_));
+          if (jb_mix_gather(W_, S_, LC_, rows, n, map_dev_.p, Lc, snap_.get(elems), compute_) != 0)
+            throw std::runtime_error("jb_mix_gather failed");
+          HIPCHK(hipMemcpyAsync(red_.get(elems), snap_.p, elems * 4, hipMemcpyDeviceToDevice, compute_));
+          HIPCHK(hipEventRecord(mix_ev_, compute_));
+          HIPCHK(hipStreamWaitEvent(mixs_, mix_ev_, 0));
+        }
+      }
+      int64_t ok[1] = {applied ? 0 : 1};
+      star.allreduce_max(ok, 1, grp.deadline());   // a rank whose tables changed: nobody folds
+      if (ok[0] == 0) {
+        pl.allreduce_sum(red_.p, elems, grp.deadline());
+        bytes += elems * 4;
+        // 5. fold: T += mean(snapshot) - snapshot (updates made meanwhile stay)
+        std::lock_guard<std::mutex> g(mu_);
+        HIPCHK(hipEventRecord(mix_ev_, mixs_));
+        HIPCHK(hipStreamWaitEvent(compute_, mix_ev_, 0));
+        if (gen == gen_) {
+          if (jb_mix_fold(W_, S_, LC_, rows, n, map_dev_.p, Lc, snap_.p, red_.p, 1.f / (float)grp.world(),
+                          compute_) != 0)
+            throw std::runtime_error("jb_mix_fold failed");
+        } else {
+          applied = false;
+        }
+      } else {
+        applied = false;
+      }
+      if (!applied) {   // every row of the next MIX: the union is dense again
+        std::lock_guard<std::mutex> g(mu_);
+        HIPCHK(hipMemsetAsync(touched_, 1, H_, compute_));
+      }
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (int c = 0; c < Lc; ++c) {
+        const uint64_t nb = (uint64_t)((int64_t)count_base_[canon[c]] + delta[c]);
+        const int col = labels_.lookup(canon[c]);
+        if (col >= 0) labels_.set_count(col, nb + (labels_.count(col) - cur_at[c]));
+        count_base_[canon[c]] = nb;
+      }
+      HIPCHK(hipStreamSynchronize(compute_));
+    }
+    last_applied_ = applied;
+    return bytes;
+  }
+
+  // obsolete protocol: rank src sends its tables and labels; apply = take them
+  void hand_over(jb::mix::Group& grp, int src, bool apply) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    std::string meta;
+    int LC = 0;
+    if (grp.rank() == src) {
+      std::lock_guard<std::mutex> g(mu_);
+      HIPCHK(hipStreamSynchronize(compute_));
+      LC = LC_;
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      meta.append((const char*)&LC, 4);
+      for (size_t c = 0; c < nm.size(); ++c) {
+        put_name(&meta, nm[c]);
+        const uint64_t cnt = labels_.count((int)c);
+        meta.append((const char*)&cnt, 8);
+        meta.push_back(al[c] ? 1 : 0);
+      }
+      HIPCHK(hipMemcpyAsync(hw_.get(H_ * LC), W_, H_ * LC * 4, hipMemcpyDeviceToDevice, compute_));
+      if (S_) HIPCHK(hipMemcpyAsync(hs_.get(H_ * LC), S_, H_ * LC * 4, hipMemcpyDeviceToDevice, compute_));
+      HIPCHK(hipStreamSynchronize(compute_));
+    }
+    meta = star.bcast_str(src, meta, grp.deadline());
+    if (meta.size() < 4) throw std::runtime_error("hand-over: broken label table");
+    memcpy(&LC, meta.data(), 4);
+    const size_t tb = H_ * (size_t)LC;
+    pl.bcast(hw_.get(tb), tb * 4, src, grp.deadline());
+    if (use_s_) pl.bcast(hs_.get(tb), tb * 4, src, grp.deadline());
+    if (!apply || grp.rank() == src) return;
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipDeviceSynchronize());
+    labels_.clear();
+    alloc_locked(LC, true);
+    size_t o = 4;
+    std::vector<std::pair<std::string, bool>> dead;
+    count_base_.clear();
+    while (o < meta.size()) {
+      std::string nm = take_name(meta, &o);
+      uint64_t cnt;
+      memcpy(&cnt, meta.data() + o, 8);
+      const bool alive = meta[o + 8] != 0;
+      o += 9;
+      const int id = labels_.get_or_add(nm.data(), nm.size());
+      labels_.set_count(id, cnt);
+      count_base_[nm] = cnt;
+      if (!alive) labels_.remove(nm);
+    }
+    HIPCHK(hipMemcpy(W_, hw_.p, tb * 4, hipMemcpyDeviceToDevice));
+    if (S_) HIPCHK(hipMemcpy(S_, hs_.p, tb * 4, hipMemcpyDeviceToDevice));
+    sync_labels_locked();
+  }
+
+  bool distributed() const { return touched_ != nullptr; }
+
   void status(std::vector<std::pair<std::string, std::string>>* st) {
     std::lock_guard<std::mutex> g(mu_);
     unsigned long long sv[2] = {0, 0};
@@ -523,6 +733,11 @@ class Classifier {
     }
     add("device", "cuda:" + std::to_string(device));
     add("hbm_used_bytes", std::to_string(total - fr));
+    if (touched_) {
+      add("mix.last_rows", std::to_string(last_rows_));
+      add("mix.last_mode", last_dense_ ? "dense" : "sparse");
+      add("mix.last_applied", last_applied_ ? "1" : "0");
+    }
   }
 
  private:
@@ -597,6 +812,7 @@ class Classifier {
     HIPCHK(hipMemset(active_, 0, (size_t)LC * 4));
     LC_ = LC;
     label_version_ = ~0ull;
+    ++gen_;   // an in-flight MIX must not fold into the new tables
   }
 
   // grow the tables / refresh the active mask and the device label table
@@ -753,7 +969,7 @@ class Classifier {
     a.merge_every = 1;
     a.hot_waves = kHotWaves;
     a.stats = stats_;
-    a.touched = nullptr;
+    a.touched = touched_;
     if (n > 0 && a.mode == kUpdateAtomic && hot_wanted(R)) {
       Hot& h = hots_[hot_turn_];
       hot_turn_ ^= 1;
@@ -840,7 +1056,7 @@ class Classifier {
     HIPCHK(hipMemcpyAsync(d_hsp_.get(2), sp, sizeof sp, hipMemcpyHostToDevice, compute_));
     const int rc = jb_linear_train(d_hrow_.p, d_hidx_.p, d_hval_.p, d_hlab_.p, d_hsp_.p, 1, W_, S_,
                                    active_, LC_, mid_, C_, kUpdateExact, nullptr, nullptr, nullptr, 1,
-                                   kHotWaves, stats_, nullptr, 0, nullptr, 0, compute_);
+                                   kHotWaves, stats_, touched_, 0, nullptr, 0, compute_);
     if (rc != 0) throw std::runtime_error("jb_linear_train failed: " + std::to_string(rc));
     HIPCHK(hipStreamSynchronize(compute_));   // host sources are reused by the next request
   }
@@ -934,6 +1150,41 @@ class Classifier {
   DevBuf<float> d_cval_, d_cout_;
   float* direct_out_ = nullptr;
   uint32_t* direct_done_ = nullptr;
+  // distributed mode (MIX)
+  uint8_t* touched_ = nullptr;
+  uint64_t gen_ = 0;
+  hipStream_t mixs_ = nullptr;
+  hipEvent_t mix_ev_ = nullptr;
+  DevBuf<uint8_t> mark_, temp_;
+  DevBuf<int64_t> rows_, count_dev_;
+  DevBuf<int32_t> map_dev_;
+  DevBuf<float> snap_, red_, hw_, hs_;
+  int64_t* count_host_ = nullptr;
+  std::map<std::string, uint64_t> count_base_;
+  uint64_t last_rows_ = 0;
+  bool last_dense_ = false, last_applied_ = true;
+
+  static void put_name(std::string* o, const std::string& n) {
+    const uint32_t k = (uint32_t)n.size();
+    o->append((const char*)&k, 4);
+    *o += n;
+  }
+  static std::string take_name(const std::string& b, size_t* o) {
+    if (*o + 4 > b.size()) throw std::runtime_error("MIX: broken label list");
+    uint32_t k;
+    memcpy(&k, b.data() + *o, 4);
+    *o += 4;
+    if (*o + k > b.size()) throw std::runtime_error("MIX: broken label list");
+    std::string n = b.substr(*o, k);
+    *o += k;
+    return n;
+  }
+  static std::vector<std::string> get_names(const std::string& b) {
+    std::vector<std::string> out;
+    size_t o = 0;
+    while (o < b.size()) out.push_back(take_name(b, &o));
+    return out;
+  }
 };
 
 // ----------------------------------------------------------------- server
@@ -979,17 +1230,48 @@ class Server {
     logf_("INFO", "start listening at port %d", port);
     cs_.start_time = time(nullptr);
     rpc_->start();
+    if (node_) {   // distributed mode: register, then the mixer thread
+      node_->register_actor(a_.eth, a_.port);
+      jb::mix::MixerArgs ma;
+      ma.type = "classifier";
+      ma.name = a_.name;
+      ma.eth = a_.eth;
+      ma.port = a_.port;
+      ma.interval_sec = a_.interval_sec;
+      ma.interval_count = a_.interval_count;
+      ma.interconnect_timeout = a_.ic_timeout;
+      Classifier* c = clf_.get();
+      mixer_.reset(new jb::mix::LinearMixer(node_->coord(), ma, c, [c](jb::mix::Group& g, double dl) {
+        return c->make_plane(g.star(), dl);
+      }));
+      mixer_->start();
+      logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
+    }
     logf_("INFO", "jubaclassifier RPC server startup (native)");
     wait_for_term();
+    if (mixer_) {
+      logf_("INFO", "stopping mixer thread");
+      mixer_->stop();
+    }
+    if (node_) node_->leave();
     logf_("INFO", "stopping RPC server");
     rpc_->stop();
     return 0;
+  }
+
+  // distributed mode (-z): coordinator session, config lock, MIX state
+  void join_cluster(std::unique_ptr<jb::mix::ClusterNode> node) {
+    node_ = std::move(node);
+    a_.connected_zookeeper = node_->connected();
+    if (!node_->config_rlock()) throw std::runtime_error("failed to get config lock");
+    clf_->enable_mix();
   }
 
  private:
   std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
 
   std::vector<std::string> arena(int slot, const std::vector<jb::ArenaReq>& reqs) {
+    if (mixer_) mixer_->updated(reqs.size());
     std::vector<int64_t> res;
     std::vector<std::string> msgs;
     std::vector<std::string> out(reqs.size());
@@ -1050,6 +1332,7 @@ class Server {
         for (size_t j = 0; j < where.size(); ++j) out[where[j]] = jb::val::response_msg(ids[j], e.what());
       }
     } else {   // train requests that found no arena room
+      if (mixer_) mixer_->updated(reqs.size());
       for (size_t k = 0; k < reqs.size(); ++k) {
         const uint8_t* b;
         size_t n;
@@ -1097,6 +1380,7 @@ class Server {
     size_t want = 0;
     for (const auto& x : arity)
       if (x.first == m) want = x.second;
+    if (m == "do_mix" && mixer_) want = 1;
     if (want == 0) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
     if (args.a.size() != want || (want == 2 && m != "train" && m != "classify" && !args.a[1].is_str()))
       return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
@@ -1109,6 +1393,7 @@ class Server {
         w.map(l.size());
         for (auto& kv : l) { w.raw(kv.first); w.uint(kv.second); }
       } else if (m == "set_label") {
+        if (mixer_) mixer_->updated(1);
         w.boolean(clf_->set_label(args.a[1].s));
       } else if (m == "delete_label") {
         w.boolean(clf_->delete_label(args.a[1].s));
@@ -1127,6 +1412,8 @@ class Server {
         w.boolean(true);
       } else if (m == "get_status") {
         status(&w);
+      } else if (m == "do_mix") {
+        w.boolean(mixer_->do_mix());
       } else {   // train / classify outside the batch path (not reached: batched methods)
         std::vector<jb::RpcRequest> one{r};
         return batch(m, one)[0];
@@ -1195,6 +1482,7 @@ class Server {
       common_status(a_, cs_, clf_->update_count.load(), &st);
     }
     clf_->status(&st);
+    if (mixer_) mixer_->status(&st);
     if (rpc_) st.emplace_back("rpc.batches", std::to_string(rpc_->batches()));
     w->map(1);
     w->raw(ident());
@@ -1204,6 +1492,8 @@ class Server {
 
   Args a_;
   std::unique_ptr<Classifier> clf_;
+  std::unique_ptr<jb::mix::ClusterNode> node_;
+  std::unique_ptr<jb::mix::LinearMixer> mixer_;
   std::unique_ptr<jb::RpcServer> rpc_;
   std::vector<uint8_t*> slots_;
   std::mutex st_mu_;
@@ -1219,7 +1509,7 @@ int main(int argc, char** argv) {
   Config cfg;
   const int rc = startup(argc, argv, &a, &text, [&cfg](const std::string& t, std::string* why) {
     return parse_config(t, &cfg, why);
-  });
+  }, true, true);
   if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
   try {
@@ -1227,7 +1517,12 @@ int main(int argc, char** argv) {
     logf_("INFO", "starting jubaclassifier %s RPC server at %s:%d (native, device %d)", kVersion,
           a.eth.c_str(), a.port, device);
     Server srv(a, cfg, device);
-    if (!a.model_file.empty()) srv.load_file(a.model_file);
+    if (!a.zookeeper.empty()) {
+      srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
+          new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), "classifier", a.name)));
+    } else if (!a.model_file.empty()) {
+      srv.load_file(a.model_file);
+    }
     logf_("INFO", "config loaded: %s", kMethods[cfg.method]);
     return srv.run();
   } catch (const std::exception& e) {

@@ -582,7 +582,7 @@ class SerialScratch:
         left to the sequential kernel, batch end, exact steps, rounds"""
         if self.buf is None:
             return {}
-        v = self.buf[:96].view(torch.int64).tolist()
+        v = self.buf[:160].view(torch.int64).tolist()
         out = {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3]}
         # committer phases in shader cycles, scaled to us by the wall clock
         wall_us = v[10] / 100.0
@@ -591,6 +591,8 @@ class SerialScratch:
             out["commit_us"] = round(wall_us, 1)
             for i, nm in enumerate(("bound", "barrier_a", "stage_b1", "step", "barrier_b2", "round")):
                 out[f"commit_{nm}_us"] = round(v[4 + i] * us, 1)
+            for w in range(8):     # per wave: round-start bounds + post-step work
+                out[f"commit_wave{w}_work_us"] = round(v[12 + w] * us, 1)
         return out
 
     def ptr(self, n_max: int) -> int:
