@@ -518,6 +518,47 @@ def fresh_budget(fresh_gb: float, local_ranks: int) -> float:
     return min(PIN_CAP, PIN_FRACTION * _mem_available() / max(1, local_ranks))
 
 
+def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: int, sync) -> dict:
+    """The headline protocol in the serial-equivalent update mode: a fresh
+    model, the same warmup, then ``--exact-steps`` timed steps over the first
+    fresh batches. The result equals applying the batch's requests one after
+    the other (csrc/hip/serial.hip), the reference's semantics."""
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.classifier import LinearClassifier
+    clf = LinearClassifier(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]),
+                           device=device, concurrent_update="exact")
+    for y in range(args.labels):
+        clf.set_label(f"label{y}")
+
+    def run(arena):
+        clf.train_arena(arena, np.asarray(arena.offs, np.int64), np.asarray(arena.lens, np.int64))
+
+    for i in range(args.warmup):
+        for j in range(bps):
+            run(warm.batches[(i * bps + j) % len(warm.batches)])
+        sync()
+        _progress(f"exact mode: warmup step {i + 1}/{args.warmup} done")
+    st0 = clf.train_stats()
+    sync()
+    t0 = time.perf_counter()
+    steps = min(args.exact_steps, args.steps)
+    for i in range(steps):
+        for j in range(bps):
+            run(fresh.batches[i * bps + j])
+        _progress(f"exact mode: timed step {i + 1}/{steps} queued")
+    sync()
+    elapsed = time.perf_counter() - t0
+    clf.synchronize()
+    st1 = clf.train_stats()
+    trained = st1["trained"] - st0["trained"]
+    updated = st1["updated"] - st0["updated"]
+    n = samples_per_batch * bps * steps
+    return {"value": round(n / elapsed, 1), "unit": "samples/s", "steps": steps,
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "update_fraction": round(updated / max(1, trained), 5),
+            "concurrent_update": "exact", "semantics": "serial-equivalent (requests applied one after another)",
+            "last_batch": clf._serial.last_batch() if getattr(clf, "_serial", None) is not None else None}
+
+
 def _mix_summary(log: list) -> dict:
     """per-MIX bytes per rank and host-observed latency (begin -> done) of
     the MIXes completed in the timed steps"""
@@ -581,10 +622,13 @@ def main() -> None:
     ap.add_argument("--rpc-threads", type=int, default=32,
                     help="server RPC threads (a quarter of them are epoll IO threads)")
     ap.add_argument("--rpc-distinct", type=int, default=512, help="distinct train requests cycled")
-    ap.add_argument("--update-mode", choices=("exact", "atomic", "hogwild"), default="exact",
-                    help="how the concurrent requests of a batch update the model: exact = the "
-                         "result of applying them one after the other (csrc/hip/serial.hip); "
+    ap.add_argument("--update-mode", choices=("exact", "atomic", "hogwild"), default="atomic",
+                    help="how the concurrent requests of a batch update the headline model: exact = "
+                         "the result of applying them one after the other (csrc/hip/serial.hip); "
                          "atomic / hogwild = lock-free concurrent streams")
+    ap.add_argument("--exact-steps", type=int, default=3,
+                    help="1 GPU: also time this many steps of the serial-equivalent exact mode (same "
+                         "warmup, same fresh batches, its own model) and report them under exact_mode")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: rehearse the multi-rank GPU path with several ranks on one GPU "
                          "(not a benchmark configuration)")
@@ -814,6 +858,9 @@ def main() -> None:
     p50 = statistics.median(lat)
     p99 = lat[min(len(lat) - 1, int(0.99 * len(lat)))]
 
+    exact = None
+    if world == 1 and device is not None and args.exact_steps > 0 and args.update_mode != "exact":
+        exact = exact_record(args, cfg, device, warm, fresh, bps, samples_per_batch, sync)
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:
         served = served_train(args, local, nat)
@@ -876,6 +923,7 @@ def main() -> None:
                               if args.batches_per_step <= 0 else {"batches_per_step_flag": bps}),
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
+            "exact_mode": exact,
             "served": served,
             "served_native": served_native,
             "engines": engines,

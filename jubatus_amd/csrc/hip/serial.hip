@@ -47,6 +47,13 @@ constexpr float kSlackGuard = 1e-4f; // relative guard band of the slack
 constexpr int kStepBits = 8;
 constexpr int kStepCap = 1 << kStepBits;  // step table slots
 constexpr int kStepList = 64;        // distinct rows of one step the table holds
+// why a committer stopped (tail[kTailReason]): the batch is done, the D
+// table saturated (a new segment re-scores the rest against the current
+// model with an empty table), or too many updates per round (the rest goes
+// to the sequential kernel)
+constexpr int kTailReason = 20;
+constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2;
+constexpr int kSerialSegments = 4;
 
 // scores of all labels of one sample with plain (L1-cached) loads: the
 // score pass reads a table nothing writes during the kernel
@@ -132,10 +139,12 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
-    const int32_t* __restrict__ active, int method, float C, float* __restrict__ slack) {
+    const int32_t* __restrict__ active, int method, float C, float* __restrict__ slack,
+    const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (reason != nullptr && *reason == kStopDense) return;   // the batch went sequential
   const int64_t beg = stream_ptr[0];
   const int64_t s = beg + wid;
   if (s >= stream_ptr[nstreams]) return;
@@ -462,9 +471,10 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
     const int32_t* __restrict__ active, int method, float C, const float* __restrict__ slack,
     unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
-    int64_t* __restrict__ tail, int bail_after) {
+    int64_t* __restrict__ tail, int bail_after, int seg) {
   using L = Lanes<LC>;
   constexpr int T = kCommitThreads;
+  if (seg > 0 && tail[kTailReason] == kStopDense) return;
   constexpr int NF = kSerialNF;
   constexpr bool kStaged = LC <= 64;
   __shared__ int32_t s_key[kDCap];
@@ -519,6 +529,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   __syncthreads();
   unsigned n_upd = 0;
   int64_t stop = end;
+  int64_t why = kStopDone;
   int iter = 0;
   int64_t n_steps = 0, n_rounds = 0;
   // diagnostics: shader-clock cycles thread 0 spends per phase (bound
@@ -618,6 +629,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       tw = clock64();
       if (s_sat || steps > bail_after) {
         stop = p + k + 1;
+        why = s_sat ? kStopSaturated : kStopDense;
         break;
       }
       if (open && tid > k && sl >= 0.f) {
@@ -636,15 +648,19 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     if (stop != end) break;
   }
   __syncthreads();
-  if (lane == 0) tail[12 + wv] = (int64_t)wwork;
+  // diagnostics of the batch: the first segment sets them, later ones add
+  auto put = [&](int i, int64_t v) { tail[i] = seg == 0 ? v : tail[i] + v; };
+  if (lane == 0) put(12 + wv, (int64_t)wwork);
   if (tid == 0) {
     tail[0] = stop;
     tail[1] = end;
-    tail[2] = n_steps;      // diagnostics: exact steps, rounds of this batch
-    tail[3] = n_rounds;
-    for (int i = 0; i < 6; ++i) tail[4 + i] = (int64_t)ph[i];
-    tail[10] = (int64_t)(wall_clock64() - w0);    // 100 MHz ticks
-    tail[11] = (int64_t)(clock64() - tc) + (int64_t)(ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5]);
+    tail[kTailReason] = why;
+    put(2, n_steps);        // exact steps, rounds
+    put(3, n_rounds);
+    put(21, 1);             // segments
+    for (int i = 0; i < 6; ++i) put(4 + i, (int64_t)ph[i]);
+    put(10, (int64_t)(wall_clock64() - w0));    // 100 MHz ticks
+    put(11, (int64_t)(clock64() - tc) + (int64_t)(ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5]));
     if (stats != nullptr && s_valid > 0) atomicAdd(stats + 1, (unsigned long long)s_valid);
   }
   if (tid == 0 && stats != nullptr && n_upd > 0) atomicAdd(stats, (unsigned long long)n_upd);
@@ -677,14 +693,21 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   // (slack[i] belongs to sample stream_ptr[0] + i)
   const int64_t blocks = (n_max * 64 + 255) / 256;
   if (blocks > INT32_MAX) return -5;
+  // segments: a committer that saturated its D table hands [tail[0], end)
+  // to the next segment (score + commit against the model as it is then);
+  // the range lives in tail[0..1] on the device, so no host round trip
+  for (int seg = 0; seg < jb::kSerialSegments; ++seg) {
+    const int64_t* sp = seg == 0 ? stream_ptr : tail;
+    const int ns = seg == 0 ? nstreams : 1;
+    const int64_t* why = seg == 0 ? nullptr : tail + jb::kTailReason;
 #define JB_SERIAL(L)                                                                              \
   hipLaunchKernelGGL((jb::serial_score_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream,  \
-                     row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, active, method, C,     \
-                     slack);                                                                      \
+                     row_ptr, fidx, fval, labels, sp, ns, W, active, method, C, slack, why);      \
   hipLaunchKernelGGL((jb::serial_commit_kernel<L>), dim3(1), dim3(jb::kCommitThreads), 0, stream, \
-                     row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active, method, C,  \
-                     slack, stats, touched, tail, bail_after);
-  JB_LC_DISPATCH(LC, JB_SERIAL)
+                     row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, slack, stats,  \
+                     touched, tail, bail_after, seg);
+    JB_LC_DISPATCH(LC, JB_SERIAL)
 #undef JB_SERIAL
+  }
   return (int)hipGetLastError();
 }

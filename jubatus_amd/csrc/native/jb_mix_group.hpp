@@ -846,8 +846,7 @@ class ClusterNode {
   bool config_rlock() {
     const std::string dir = actor_path(type_, name_) + "/config_lock";
     for (int attempt = 0; attempt < 3; ++attempt) {
-      cc::Value r = coord_->call("create_seq", {cc::Value::integer(sid()), cc::Value::str(dir + "/rlock_"),
-                                                cc::Value::str(""), cc::Value::boolean(true)});
+      cc::Value r = coord_->call("create_seq", {cc::Value::integer(sid()), cc::Value::str(dir + "/rlock_")});
       const auto& a = r.as_array();
       if (a.at(0).as_int() != 0) continue;
       const std::string mine = a.at(1).as_str();

@@ -310,6 +310,10 @@ int main(int argc, char** argv) {
   rpc.listen("127.0.0.1", port);
   rpc.start();
   jb::mix::ClusterNode node(zk, zkt, "classifier", name);
+  if (!node.config_rlock()) {
+    fprintf(stderr, "failed to get config lock\n");
+    return 1;
+  }
   node.register_actor("127.0.0.1", port);
   jb::mix::MixerArgs ma;
   ma.type = "classifier";

@@ -582,8 +582,9 @@ class SerialScratch:
         left to the sequential kernel, batch end, exact steps, rounds"""
         if self.buf is None:
             return {}
-        v = self.buf[:160].view(torch.int64).tolist()
-        out = {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3]}
+        v = self.buf[:176].view(torch.int64).tolist()
+        out = {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3],
+               "segments": v[21], "stop_reason": ("done", "saturated", "dense")[v[20]] if 0 <= v[20] < 3 else v[20]}
         # committer phases in shader cycles, scaled to us by the wall clock
         wall_us = v[10] / 100.0
         if v[11] > 0:
