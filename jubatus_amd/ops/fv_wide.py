@@ -105,63 +105,27 @@ class WideDevice:
         hip.fvw_emit(buf, buf_len, datum_off, datum_len, n, row_ptr, self.srules, rt.n_srules,
                      self.nrules, rt.n_nrules, self.blob, self.H, idx, val, hs, names, gw, self.err)
         if self.df is not None:
-            self._weigh(row_ptr, tot, n, idx, val, gw, update)
+            self._weigh(row_ptr, total, n, idx, val, gw, update)
         if rt.n_crules:
             hip.fvw_comb(buf, n, row_ptr, base, self.srules, self.nrules, self.crules,
                          rt.n_crules, self.blob, self.H, idx, val, hs, names)
         return row_ptr, idx, val, total
 
-    def _weigh(self, row_ptr, tot, n: int, idx, val, gw, update: bool) -> None:
+    def _weigh(self, row_ptr, total: int, n: int, idx, val, gw, update: bool) -> None:
         """idf / bm25 on the slots of global-weighted rules (converter.py
-        _convert semantics, datum by datum within the batch)"""
+        _convert semantics, datum by datum within the batch): one HIP launch
+        chain (csrc/hip/df.hip), the table advanced in HBM"""
         wm = self.conv.weights
         self.df.push()
-        d = self.device
-        total = int(row_ptr[n].item()) if n else 0
-        if total == 0:
-            if update:
-                wm.counts[0] += n
-                wm.counts[2] += n
-            return
-        datum = torch.repeat_interleave(torch.arange(n, device=d), tot[:n], output_size=total)
-        m = (gw[:total] > 0) & (idx[:total] >= 0)
-        sel = torch.nonzero(m).flatten()
-        ds = datum[sel]
-        fs = idx[sel].long()
-        lens = torch.bincount(ds, minlength=n).to(torch.float64)
         N0, L0 = int(wm.counts[0]), int(wm.counts[1])
+        if n == 0:
+            return
+        sel_len = torch.zeros(1, dtype=torch.int64, device=self.device)
+        hip.df_weigh(row_ptr, n, total, idx, val, gw, self.df.df, self.df.diff, N0, L0, update, sel_len)
         if update:
-            key = fs * n + ds
-            uk, inv = torch.unique(key, sorted=True, return_inverse=True)
-            uf = uk // n
-            # rank of each (feature, datum) pair among the pairs of its feature
-            starts = torch.ones_like(uf, dtype=torch.bool)
-            starts[1:] = uf[1:] != uf[:-1]
-            pos = torch.arange(uf.numel(), device=d)
-            first = torch.cummax(torch.where(starts, pos, torch.zeros_like(pos)), 0).values
-            rank = pos - first
-            df_at = (self.df.df[uf] + rank + 1)[inv].to(torch.float64)
-            docs = (N0 + 1 + torch.arange(n, device=d, dtype=torch.float64))
-            cum_len = L0 + torch.cumsum(lens, 0)
-            self.df.df.index_add_(0, uf, torch.ones_like(uf))
-            self.df.diff.index_add_(0, uf, torch.ones_like(uf))
             self.df.device_changed()
-            tl = int(lens.sum().item())
+            tl = int(sel_len.item())
             wm.counts[0] += n
             wm.counts[2] += n
             wm.counts[1] += tl
             wm.counts[3] += tl
-        else:
-            df_at = self.df.df[fs].to(torch.float64)
-            docs = torch.full((n,), float(N0), dtype=torch.float64, device=d)
-            cum_len = torch.full((n,), float(L0), dtype=torch.float64, device=d)
-        nd = docs[ds]
-        idf = torch.where((df_at > 0) & (nd > 0), torch.log(nd / df_at.clamp_min(1)),
-                          torch.zeros_like(df_at))
-        w = val[sel].to(torch.float64)
-        g = gw[sel]
-        avg = torch.where(docs > 0, cum_len / docs.clamp_min(1), torch.ones_like(docs))[ds]
-        k1, b = 1.2, 0.75
-        bm = idf * (w * (k1 + 1)) / (w + k1 * (1 - b + b * lens[ds] / avg.clamp_min(1e-9)))
-        out = torch.where(g == 1, w * idf, bm)
-        val[sel] = out.to(torch.float32)

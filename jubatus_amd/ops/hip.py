@@ -38,6 +38,9 @@ _SIGS = {
                         _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i64, _c_void_p, _i64,
                         _c_void_p],
     "jb_hot_rep_bytes": [],
+    "jb_df_scratch_bytes": [_i64, _i64],
+    "jb_df_weigh": [_c_void_p, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
+                    _i64, _i32, _c_void_p, _i64, _c_void_p, _c_void_p],
     "jb_serial_scratch_bytes": [_i64],
     "jb_hot_detect": [_c_void_p, _i32, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                       _i32, _c_void_p, _c_void_p, _c_void_p],
@@ -134,6 +137,34 @@ def sqdist(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
 
 def fvw_name_bytes() -> int:
     return int(_fn("jb_fvw_name_bytes")())
+
+
+_df_scratch: dict = {}
+
+
+def df_weigh(row_ptr, n: int, total: int, idx, val, gw, df, diff, N0: int, L0: int, update: bool,
+             sel_len=None) -> None:
+    """idf / bm25 of a converted batch's global-weighted slots in place, the
+    document-frequency table advanced by the batch with the sequential
+    semantics when ``update`` (csrc/hip/df.hip: one launch chain)"""
+    _dev(row_ptr, torch.int64, "row_ptr")
+    _dev(idx, torch.int32, "idx")
+    _dev(val, torch.float32, "val")
+    _dev(gw, torch.uint8, "gw")
+    _dev(df, torch.int64, "df")
+    _dev(diff, torch.int64, "diff")
+    if row_ptr.numel() < n + 1 or idx.numel() < total or val.numel() < total or gw.numel() < total \
+            or diff.numel() != df.numel():
+        raise ValueError("df_weigh: bad operand shapes")
+    need = int(_fn("jb_df_scratch_bytes")(int(total), int(n)))
+    buf = _df_scratch.get(val.device)
+    if buf is None or buf.numel() < need:
+        buf = torch.empty(max(need, 2 * (buf.numel() if buf is not None else 0)), dtype=torch.uint8,
+                          device=val.device)
+        _df_scratch[val.device] = buf
+    rc = _fn("jb_df_weigh")(_p(row_ptr), n, total, _p(idx), _p(val), _p(gw), _p(df), _p(diff), int(N0), int(L0),
+                            1 if update else 0, _p(buf), buf.numel(), _p(sel_len), _stream())
+    _check(rc, "jb_df_weigh")
 
 
 def fvw_count(buf, buf_len: int, datum_off, datum_len, n: int, srules, ns: int, nrules, nn: int,
