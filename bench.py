@@ -208,7 +208,15 @@ def served_train(args, local: int, nat) -> dict:
     a = ServerArgv.parse(["-p", "9199", "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
                           "-c", str(args.rpc_threads), "--gpu", str(local)], "classifier")
     a.port = 0
-    h = ServerHelper(get_serv("classifier"), a, install_signals=False)
+    old_mode = os.environ.get("JUBATUS_UPDATE_MODE")
+    os.environ["JUBATUS_UPDATE_MODE"] = args.update_mode      # the headline's update mode
+    try:
+        h = ServerHelper(get_serv("classifier"), a, install_signals=False)
+    finally:
+        if old_mode is None:
+            os.environ.pop("JUBATUS_UPDATE_MODE", None)
+        else:
+            os.environ["JUBATUS_UPDATE_MODE"] = old_mode
     h.start(block=False)
     try:
         # K distinct train requests: params [cluster name "", body]
@@ -268,6 +276,7 @@ def served_train(args, local: int, nat) -> dict:
                 "batches_in_window": nb,
                 "transport_us_per_batch": {"handler_call": round((ans1[0] - ans0[0]) / nb / 1e3, 1),
                                            "send_replies": round((ans1[1] - ans0[1]) / nb / 1e3, 1)},
+                "concurrent_update": clf.concurrent_update,
                 "path": "loopback TCP -> native epoll transport -> pinned arena slot -> GPU scan/"
                         "fv_hash/AROW train; reply per request after the batch's scan check"}
     finally:
@@ -305,7 +314,8 @@ def served_train_native(args, local: int, nat) -> dict:
     s.close()
     p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
                           "-c", str(args.rpc_threads), "--gpu", str(local)],
-                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                         env=dict(os.environ, JUBATUS_UPDATE_MODE=args.update_mode))
 
     def status():
         with RpcClient("127.0.0.1", port, 30.0) as c:
@@ -360,6 +370,7 @@ def served_train_native(args, local: int, nat) -> dict:
                 "server_cpus": round((cpu1 - cpu0) / lg["seconds"], 2),
                 "train_scan": {k[len("train_scan."):]: int(v) for k, v in st1.items()
                                if k.startswith("train_scan.") and v.isdigit()},
+                "concurrent_update": st1.get("train.update_mode"),
                 "path": "loopback TCP -> native jubaclassifier (no Python) -> pinned arena slot -> "
                         "GPU scan/fv_hash/AROW train; reply per request after the batch's scan check"}
     finally:

@@ -199,7 +199,110 @@ __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict
   if (t == 0) *done_iters = it;
 }
 
+// Diagonal-covariance GMM EM, every iteration in one single-workgroup launch
+// (the Python path ran ~10 torch launches per iteration). Same formulas as
+// models/clustering.py _em: responsibilities r_ij = w_i softmax_j(log N(x_i |
+// C_j, var_j) + log pi_j); nk = max(sum_i r_ij, 1e-9); C = S1 / nk;
+// var = max(S2 / nk - C^2, 1e-6); pi = nk / sum nk. LDS: C, var, S1, S2
+// [k][d], nk / logdet / log pi [k].
+__global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restrict__ X, int n, int d,
+                                                          const float* __restrict__ w, float* __restrict__ C,
+                                                          float* __restrict__ var, float* __restrict__ pi,
+                                                          int k, int iters) {
+  extern __shared__ float s_em[];
+  float* sC = s_em;
+  float* sV = sC + k * d;
+  float* s1 = sV + k * d;
+  float* s2 = s1 + k * d;
+  float* nk = s2 + k * d;          // [k]
+  float* lc = nk + k;              // [k] log pi_j - 0.5 sum_q log(2 pi var_jq)
+  __shared__ float s_tot;
+  const int t = threadIdx.x;
+  const float kLog2Pi = 1.8378770664093453f;
+  for (int i = t; i < k * d; i += kClBlock) { sC[i] = C[i]; sV[i] = var[i]; }
+  for (int j = t; j < k; j += kClBlock) nk[j] = pi[j];   // (pi until the first M-step)
+  __syncthreads();
+  for (int it = 0; it < iters; ++it) {
+    for (int j = t; j < k; j += kClBlock) {
+      float ld = 0.f;
+      for (int q = 0; q < d; ++q) ld += logf(6.283185307179586f * sV[j * d + q]);
+      lc[j] = logf(fmaxf(nk[j], 1e-12f)) - 0.5f * ld;
+    }
+    for (int i = t; i < k * d; i += kClBlock) { s1[i] = 0.f; s2[i] = 0.f; }
+    __syncthreads();
+    for (int j = t; j < k; j += kClBlock) nk[j] = 0.f;
+    __syncthreads();
+    (void)kLog2Pi;
+    for (int i = t; i < n; i += kClBlock) {
+      const float* x = X + (int64_t)i * d;
+      // log-sum-exp over the clusters (k is small: two passes over d)
+      float mx = -INFINITY;
+      for (int j = 0; j < k; ++j) {
+        float q2 = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float df = x[q] - sC[j * d + q];
+          q2 += df * df / sV[j * d + q];
+        }
+        mx = fmaxf(mx, lc[j] - 0.5f * q2);
+      }
+      float den = 0.f;
+      for (int j = 0; j < k; ++j) {
+        float q2 = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float df = x[q] - sC[j * d + q];
+          q2 += df * df / sV[j * d + q];
+        }
+        den += expf(lc[j] - 0.5f * q2 - mx);
+      }
+      const float wi = w[i];
+      for (int j = 0; j < k; ++j) {
+        float q2 = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float df = x[q] - sC[j * d + q];
+          q2 += df * df / sV[j * d + q];
+        }
+        const float r = wi * expf(lc[j] - 0.5f * q2 - mx) / den;
+        if (r == 0.f) continue;
+        atomicAdd(&nk[j], r);
+        for (int q = 0; q < d; ++q) {
+          atomicAdd(&s1[j * d + q], r * x[q]);
+          atomicAdd(&s2[j * d + q], r * x[q] * x[q]);
+        }
+      }
+    }
+    __syncthreads();
+    for (int j = t; j < k; j += kClBlock) nk[j] = fmaxf(nk[j], 1e-9f);
+    __syncthreads();
+    for (int i = t; i < k * d; i += kClBlock) {
+      const float m = nk[i / d];
+      const float c = s1[i] / m;
+      sC[i] = c;
+      sV[i] = fmaxf(s2[i] / m - c * c, 1e-6f);
+    }
+    if (t == 0) {
+      float tot = 0.f;
+      for (int j = 0; j < k; ++j) tot += nk[j];
+      s_tot = tot;
+    }
+    __syncthreads();
+    for (int j = t; j < k; j += kClBlock) nk[j] = nk[j] / s_tot;   // pi of the next E-step
+    __syncthreads();
+  }
+  for (int i = t; i < k * d; i += kClBlock) { C[i] = sC[i]; var[i] = sV[i]; }
+  for (int j = t; j < k; j += kClBlock) pi[j] = nk[j];
+}
+
 }  // namespace jb
+
+extern "C" int jb_gmm_em(const float* X, int n, int d, const float* w, float* C, float* var, float* pi, int k,
+                         int iters, hipStream_t stream) {
+  if (n <= 0 || k <= 0 || d <= 0) return 0;
+  const size_t lds = sizeof(float) * (4 * (size_t)k * d + 2 * (size_t)k);
+  if (lds > 64 * 1024) return -2;
+  hipLaunchKernelGGL(jb::gmm_em_kernel, dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var, pi, k,
+                     iters);
+  return (int)hipGetLastError();
+}
 
 extern "C" int jb_sqdist_mfma(const float* X, int64_t n, const float* C, int k, int d,
                               const float* xn2, const float* cn2, float* out, hipStream_t stream) {

@@ -152,7 +152,9 @@ DfPlan plan(int64_t total, int64_t n) {
 }  // namespace
 
 // scratch bytes of jb_df_weigh for `total` slots over `n` datums
-extern "C" int64_t jb_df_scratch_bytes(int64_t total, int64_t n) { return (int64_t)plan(total, n).total_bytes(total, n); }
+extern "C" int64_t jb_df_scratch_bytes(int64_t total, int64_t n) {
+  return (int64_t)plan(total, n).total_bytes(total, n);
+}
 
 // idf / bm25 of the global-weighted slots (gw 1 idf, 2 bm25; 0 none) of a
 // converted batch, in place in val. update: the batch is added to the table

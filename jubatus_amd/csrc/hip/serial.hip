@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
     const int32_t* __restrict__ active, int method, float C, float* __restrict__ slack,
-    const int64_t* __restrict__ reason) {
+    float* __restrict__ l1n, const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -163,13 +163,20 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
   int lstar;
   float sy, best;
   const float margin = margin_of<LC>(acc, y, act, lane, &lstar, &sy, &best);
-  float nrm = 0.f;
+  float nrm = 0.f, l1 = 0.f;
   for (int j = lane; j < n; j += 64) {
     const float x = fval[fb + j];
-    if (fidx[fb + j] >= 0) nrm += x * x;
+    if (fidx[fb + j] >= 0) {
+      nrm += x * x;
+      l1 += fabsf(x);
+    }
   }
   nrm = wave_sum(nrm);
-  if (lane == 0) slack[wid] = decision_slack(method, margin, nrm, lstar >= 0, C, sy, best);
+  l1 = wave_sum(l1);
+  if (lane == 0) {
+    slack[wid] = decision_slack(method, margin, nrm, lstar >= 0, C, sy, best);
+    l1n[wid] = l1;
+  }
 }
 
 // ------------------------------------------------------------ D table (LDS)
@@ -191,6 +198,7 @@ struct DTable {
   float* sval;
   int32_t* slist;
   int* sn;
+  float* dmax;      // max_f D[f] (the cheap bound 2 |x|_1 Dmax)
 
   __device__ __forceinline__ static uint32_t slot(int32_t idx) {
     return ((uint32_t)idx * 0x9E3779B1u) >> (32 - kDBits);
@@ -205,7 +213,10 @@ struct DTable {
     const uint32_t b = fbit(idx);
     return (bloom[b >> 5] >> (b & 31)) & 1u;
   }
-  __device__ __attribute__((noinline)) float probe(int32_t idx) const {
+  // (static: a member taking `this` would force the LDS pointer table into
+  // memory)
+  __device__ __attribute__((noinline)) static float probe_at(const int32_t* key, const float* val,
+                                                             int32_t idx) {
     uint32_t h = slot(idx);
     for (int p = 0; p < kDProbe; ++p) {
       const int32_t k = key[h];
@@ -215,6 +226,7 @@ struct DTable {
     }
     return 0.f;   // never inserted past the probe limit (that saturates instead)
   }
+  __device__ __forceinline__ float probe(int32_t idx) const { return probe_at(key, val, idx); }
   __device__ __forceinline__ float get(int32_t idx) const { return maybe(idx) ? probe(idx) : 0.f; }
   // increment of row idx in the last step (valid while *sn <= kStepList)
   __device__ __forceinline__ float step_get(int32_t idx) const {
@@ -235,14 +247,18 @@ struct DTable {
     for (int p = 0; p < kDProbe; ++p) {
       const int32_t old = atomicCAS(&key[h], -1, idx);
       if (old == -1 || old == idx) {
-        atomicAdd(&val[h], v);
+        const float prev = atomicAdd(&val[h], v);
+        atomicMax((int*)dmax, __float_as_int(prev + v));   // non-negative floats order as ints
         if (old == -1 && atomicAdd(nkeys, 1) + 1 >= kDFull) *sat = 1;
         done = true;
         break;
       }
       h = (h + 1) & (kDCap - 1);
     }
-    if (!done) *sat = 1;
+    if (!done) {
+    *sat = 1;
+    atomicMax((int*)dmax, __float_as_int(INFINITY));
+  }
     // the step table (past kStepList distinct rows the readers recompute
     // their bounds from the D table instead)
     if (*sn > kStepList) return;
@@ -457,6 +473,27 @@ __device__ bool commit_staged(const int32_t* sI, const float* sX, int n, int y, 
   return true;
 }
 
+// Workgroup barrier over LDS only: the committer's waves exchange state
+// through LDS alone (only wave 0 touches W / P, and it drains its own stores
+// before it reads them again), so outstanding global loads - the next
+// round's prefetched descriptors, wave 0's atomics - stay in flight across
+// it (__syncthreads() would wait for every one of them: vmcnt(0)).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// a sample's first NF features into registers
+template <int NF>
+__device__ __forceinline__ void load_features(int32_t (&fi)[NF], float (&fx)[NF], bool live, int nf, int64_t fb,
+                                              const int32_t* __restrict__ fidx, const float* __restrict__ fval) {
+#pragma unroll
+  for (int u = 0; u < NF; ++u) {
+    const bool v = live && u < nf;
+    fi[u] = v ? fidx[fb + u] : -1;
+    fx[u] = v ? fval[fb + u] : 0.f;
+  }
+}
+
 // The ordered committer (see header). One workgroup of 1024 threads; thread t
 // owns sample p + t of the round starting at p, with the sample's slack,
 // label and features in registers (prefetched a round ahead: one load round
@@ -470,13 +507,13 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
     const int32_t* __restrict__ active, int method, float C, const float* __restrict__ slack,
-    unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
+    const float* __restrict__ l1n, unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
     int64_t* __restrict__ tail, int bail_after, int seg) {
   using L = Lanes<LC>;
   constexpr int T = kCommitThreads;
   if (seg > 0 && tail[kTailReason] == kStopDense) return;
   constexpr int NF = kSerialNF;
-  constexpr bool kStaged = LC <= 64;
+  constexpr bool kStaged = LC <= 32;   // (LC 64: 16 features per lane would spill)
   __shared__ int32_t s_key[kDCap];
   __shared__ float s_val[kDCap];
   __shared__ uint32_t s_bloom[(1 << kBloomBits) / 32];
@@ -484,6 +521,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   __shared__ float s_sval[kStepCap];
   __shared__ int32_t s_slist[kStepList];
   __shared__ int s_sn;
+  __shared__ float s_dmax;
   __shared__ int s_first[2];
   __shared__ int s_sat, s_nkeys;
   __shared__ unsigned s_valid;
@@ -505,23 +543,25 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   }
   if (tid == 0) {
     s_sn = 0;
+    s_dmax = 0.f;
     s_valid = 0;
     s_sat = 0;
     s_nkeys = 0;
     s_first[0] = s_first[1] = INT_MAX;
   }
-  DTable d{s_key, s_val, s_bloom, &s_nkeys, &s_sat, s_skey, s_sval, s_slist, &s_sn};
+  DTable d{s_key, s_val, s_bloom, &s_nkeys, &s_sat, s_skey, s_sval, s_slist, &s_sn, &s_dmax};
   bool act[L::K];
 #pragma unroll
   for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
   const int64_t beg = stream_ptr[0];
   const int64_t end = stream_ptr[nstreams];
   // round descriptors of the next round (prefetched)
-  float n_sl = NAN;
+  float n_sl = NAN, n_l1 = 0.f;
   int64_t n_fb = 0, n_fe = 0;
   int n_y = -1;
   if (beg + tid < end) {
     n_sl = slack[tid];
+    n_l1 = l1n[tid];
     n_fb = row_ptr[beg + tid];
     n_fe = row_ptr[beg + tid + 1];
     n_y = labels[beg + tid];
@@ -542,24 +582,29 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     const int64_t j = p + tid;
     const bool live = j < end;
     const float sl = n_sl;
+    const float l1 = n_l1;
     const int64_t fb = n_fb;
     const int nf = (int)(n_fe - n_fb);
     const int yl = n_y;
+    // features are loaded only by samples the cheap bound 2 |x|_1 Dmax does
+    // not settle (most samples of a trained model never read them)
     int32_t fi[NF];
     float fx[NF];
 #pragma unroll
     for (int u = 0; u < NF; ++u) {
-      const bool v = live && u < nf;
-      fi[u] = v ? fidx[fb + u] : -1;
-      fx[u] = v ? fval[fb + u] : 0.f;
+      fi[u] = -1;
+      fx[u] = 0.f;
     }
-    // the next round's descriptors go in flight behind this round's features
+    bool loaded = false;
+    // the next round's descriptors go in flight
     const int64_t jn = j + T;
     n_sl = NAN;
+    n_l1 = 0.f;
     n_fb = n_fe = 0;
     n_y = -1;
     if (jn < end) {
       n_sl = slack[jn - beg];
+      n_l1 = l1n[jn - beg];
       n_fb = row_ptr[jn];
       n_fe = row_ptr[jn + 1];
       n_y = labels[jn];
@@ -579,21 +624,32 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       return b;
     };
     tw = clock64();
-    float bnd = (open && sl >= 0.f && !s_sat) ? full_bound() : 0.f;
+    float bnd = 0.f;
+    if (open && (sl < 0.f || 2.f * l1 * s_dmax >= sl)) {
+      load_features<NF>(fi, fx, live, nf, fb, fidx, fval);
+      loaded = true;
+      if (sl >= 0.f && !s_sat) bnd = full_bound();
+    }
     { const uint64_t t = clock64(); ph[5] += t - tc; tc = t; }
     for (;;) {
-      const bool unsafe = open && tid > lim && (sl < 0.f || s_sat || 2.f * bnd >= sl);
+      if (open && tid > lim && sl >= 0.f && !loaded && 2.f * l1 * s_dmax >= sl) {
+        load_features<NF>(fi, fx, live, nf, fb, fidx, fval);   // Dmax grew past the cheap test
+        loaded = true;
+        bnd = full_bound();
+      }
+      const bool unsafe = open && tid > lim && (sl < 0.f || s_sat || (loaded && 2.f * bnd >= sl));
       wwork += clock64() - tw;
       const uint64_t m = __builtin_amdgcn_ballot_w64(unsafe);
       if (lane == 0 && m != 0) atomicMin(&s_first[iter & 1], wv * 64 + (int)__builtin_ctzll(m));
       { const uint64_t t = clock64(); ph[0] += t - tc; tc = t; }
-      __syncthreads();     // A: the first unsettled sample of the round is known
+      lds_barrier();       // A: the first unsettled sample of the round is known
       { const uint64_t t = clock64(); ph[1] += t - tc; tc = t; }
       const int k = s_first[iter & 1];
       if (tid == 0) s_first[(iter + 1) & 1] = INT_MAX;
       ++iter;
       if (k == INT_MAX) break;
       if (tid == k) {      // the owner stages its sample for wave 0
+        if (!loaded) load_features<NF>(fi, fx, live, nf, fb, fidx, fval);
         s_n = nf;
         s_y = yl;
         s_fb = fb;
@@ -605,7 +661,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) s_sn = 0;
       }
-      __syncthreads();     // B1
+      lds_barrier();       // B1
       { const uint64_t t = clock64(); ph[2] += t - tc; tc = t; }
       if (wv == 0) {
         // this step reads what the previous one wrote (its atomics drained
@@ -614,7 +670,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         const int n = s_n;
         bool up;
         if (kStaged && n <= NF)
-          up = commit_staged<(LC <= 64 ? LC : 64)>(s_fi, s_fx, n, s_y, W, P, act[0], lane, method, C,
+          up = commit_staged<(LC <= 32 ? LC : 32)>(s_fi, s_fx, n, s_y, W, P, act[0], lane, method, C,
                                                    touched, d);
         else
           up = commit_sample<LC>(fidx, fval, s_fb, n, s_y, W, P, act, lane, method, C, touched, d);
@@ -624,7 +680,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       ++steps;
       ++n_steps;
       { const uint64_t t = clock64(); ph[3] += t - tc; tc = t; }
-      __syncthreads();     // B2: D / the step table / s_sat visible to every wave
+      lds_barrier();       // B2: D / the step table / s_sat visible to every wave
       { const uint64_t t = clock64(); ph[4] += t - tc; tc = t; }
       tw = clock64();
       if (s_sat || steps > bail_after) {
@@ -632,7 +688,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         why = s_sat ? kStopSaturated : kStopDense;
         break;
       }
-      if (open && tid > k && sl >= 0.f) {
+      if (loaded && open && tid > k && sl >= 0.f) {
         if (s_sn > kStepList || nf > NF) {
           bnd = full_bound();
         } else {
@@ -672,7 +728,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
 // [tail int64 x 2, padded to 256 B][slack float x n_max]; n_max bounds the
 // batch's sample count stream_ptr[nstreams] - stream_ptr[0]
 extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max) {
-  return 256 + 4 * (n_max > 0 ? n_max : 1);
+  return 256 + 8 * (n_max > 0 ? n_max : 1);
 }
 
 // Steps 1-2 of a kSerial batch (score, commit); the caller then runs the
@@ -690,6 +746,7 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   if (method >= jb::CW && S == nullptr) return -4;
   int64_t* tail = (int64_t*)scratch;
   float* slack = (float*)((uint8_t*)scratch + 256);
+  float* l1n = slack + n_max;     // |x|_1 of each sample
   // (slack[i] belongs to sample stream_ptr[0] + i)
   const int64_t blocks = (n_max * 64 + 255) / 256;
   if (blocks > INT32_MAX) return -5;
@@ -702,9 +759,10 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
     const int64_t* why = seg == 0 ? nullptr : tail + jb::kTailReason;
 #define JB_SERIAL(L)                                                                              \
   hipLaunchKernelGGL((jb::serial_score_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream,  \
-                     row_ptr, fidx, fval, labels, sp, ns, W, active, method, C, slack, why);      \
+                     row_ptr, fidx, fval, labels, sp, ns, W, active, method, C, slack, l1n, why); \
   hipLaunchKernelGGL((jb::serial_commit_kernel<L>), dim3(1), dim3(jb::kCommitThreads), 0, stream, \
-                     row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, slack, stats,  \
+                     row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, slack, l1n,    \
+                     stats,                                                                       \
                      touched, tail, bail_after, seg);
     JB_LC_DISPATCH(LC, JB_SERIAL)
 #undef JB_SERIAL

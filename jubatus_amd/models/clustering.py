@@ -253,6 +253,11 @@ class Clustering:
         k, d = C.shape
         var = torch.ones((k, d), dtype=torch.float32, device=X.device)
         pi = torch.full((k,), 1.0 / k, dtype=torch.float32, device=X.device)
+        if X.is_cuda:
+            from ..ops import hip
+            C = C.contiguous().clone()
+            if hip.gmm_em(X.contiguous(), w.contiguous(), C, var, pi, iters):
+                return C, var, pi
         for _ in range(iters):
             r = torch.softmax(self._log_resp(X, C, var, pi), dim=1) * w[:, None]
             nk = r.sum(0).clamp_min(1e-9)

@@ -112,6 +112,7 @@ _SIGS = {
     "jb_fvw_name_bytes": [],
     "jb_kmeanspp": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                     _c_void_p, _c_void_p, _c_void_p],
+    "jb_gmm_em": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p],
     "jb_lloyd": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _f32, _f32, _c_void_p,
                  _c_void_p, _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
@@ -245,6 +246,24 @@ def lloyd(X: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: int, atol: f
                          _p(done), _stream())
     _check(rc, "jb_lloyd")
     return assign, int(done.item())
+
+
+def gmm_em(X: torch.Tensor, w: torch.Tensor, C: torch.Tensor, var: torch.Tensor, pi: torch.Tensor,
+           iters: int) -> bool:
+    """diagonal-covariance GMM EM on one workgroup (csrc/hip/clustering.hip
+    gmm_em_kernel); C / var [k, d] and pi [k] updated in place. False when
+    k x d does not fit the kernel's LDS (the caller keeps its own path)."""
+    for t, nm in ((X, "X"), (w, "w"), (C, "C"), (var, "var"), (pi, "pi")):
+        _dev(t, torch.float32, nm)
+    n, d = X.shape
+    k = C.shape[0]
+    if C.shape[1] != d or var.shape != C.shape or pi.numel() != k or w.numel() < n:
+        raise ValueError("gmm_em: bad operand shapes")
+    if 4 * (4 * k * d + 2 * k) > 64 * 1024:
+        return False
+    rc = _fn("jb_gmm_em")(_p(X), n, d, _p(w), _p(C), _p(var), _p(pi), k, iters, _stream())
+    _check(rc, "jb_gmm_em")
+    return True
 
 
 def signature(row_ptr, fidx, fval, n: int, hash_num: int, seed: int, mode: int, bits, norms) -> None:

@@ -38,7 +38,12 @@ def build_classifier(cfg: dict, device):
     conv = DatumToFvConverter(cfg.get("converter") or {})
     param = cfg.get("parameter")
     if method in LINEAR_METHODS:
-        return LinearClassifier(method, param, conv, device=device)
+        # how concurrent train requests update the model: serial-equivalent by
+        # default; JUBATUS_UPDATE_MODE=atomic opts into lock-free streams (the
+        # native server reads the same variable)
+        mode = os.environ.get("JUBATUS_UPDATE_MODE", "exact")
+        return LinearClassifier(method, param, conv, device=device,
+                                concurrent_update=mode if mode in ("exact", "atomic", "hogwild") else "exact")
     if method in NN_METHODS:
         from ..models.nn_classifier import NNClassifier
         return NNClassifier(method, param or {}, conv, device=device)

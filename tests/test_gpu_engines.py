@@ -150,6 +150,27 @@ def test_clustering_on_gpu_matches_cpu(gpu_min_elems):
     assert cs == sorted([(0, 0), (8, 8), (-8, 8)])
 
 
+@pytest.mark.parametrize("n,k,d", [(300, 3, 4), (1000, 5, 17), (64, 1, 2)])
+def test_gmm_em_kernel_matches_fp32_torch(n, k, d):
+    """csrc/hip/clustering.hip gmm_em_kernel (one launch for all iterations)
+    == the fp32 torch EM of models/clustering.py on the host"""
+    import torch
+    from jubatus_amd.models.clustering import Clustering
+    from jubatus_amd.ops import hip
+    g = torch.Generator().manual_seed(n + k + d)
+    centers = torch.randn(k, d, generator=g) * 6
+    X = centers[torch.arange(n) % k] + torch.randn(n, d, generator=g)
+    w = torch.rand(n, generator=g) + 0.5
+    C0 = X[:k].clone()
+    ref = Clustering._em(Clustering.__new__(Clustering), X, w, C0.clone(), iters=20)
+    C, var = C0.clone().to(dev()), torch.ones(k, d, device=dev())
+    pi = torch.full((k,), 1.0 / k, device=dev())
+    assert hip.gmm_em(X.to(dev()), w.to(dev()), C, var, pi, 20)
+    torch.testing.assert_close(C.cpu(), ref[0], rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(var.cpu(), ref[1], rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(pi.cpu(), ref[2], rtol=1e-3, atol=1e-4)
+
+
 @pytest.mark.parametrize("method", ["kmeans", "gmm"])
 def test_default_clustering_config_runs_on_device(method):
     """config/clustering/{kmeans,gmm}.json (bucket_size 1000, compressed 100,
