@@ -454,6 +454,14 @@ __device__ bool commit_staged(const int32_t* sI, const float* sX, int n, int y, 
   float tau = 0.f, beta = 0.f;
   if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return false;
   const bool mine = l0 == y || (lstar >= 0 && l0 == lstar);
+  // Plain read-modify-write stores unless a row repeats inside the sample:
+  // this wave is the table's only writer while the committer runs, and a
+  // plain store keeps the line in the XCD's L2 for the next step's loads (a
+  // float atomic executes at the memory side and drops it)
+  bool dup = false;
+  if (lane < n)
+    for (int j = lane + 1; j < n; ++j) dup |= sI[j] == sI[lane] && sI[lane] >= 0;
+  const bool plain = __builtin_amdgcn_ballot_w64(dup) == 0;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     float mag = 0.f;
@@ -461,8 +469,13 @@ __device__ bool commit_staged(const int32_t* sI, const float* sX, int n, int y, 
       const int64_t row = (int64_t)ix[u] * LC + l0;
       const float a = use_s ? 1.f / pv[u] : 1.f;
       const float dw = (l0 == y ? tau : -tau) * a * xv[u];
-      atomicAdd(W + row, dw);
-      if (use_s) atomicAdd(P + row, dprec(method, beta, xv[u], a));
+      if (plain) {
+        W[row] = w[u] + dw;
+        if (use_s) P[row] = pv[u] + dprec(method, beta, xv[u], a);
+      } else {
+        atomicAdd(W + row, dw);
+        if (use_s) atomicAdd(P + row, dprec(method, beta, xv[u], a));
+      }
       if (touched != nullptr && l0 == y) touched[ix[u]] = 1;
       mag = fabsf(dw);
     }

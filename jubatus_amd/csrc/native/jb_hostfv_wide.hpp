@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
 #include <string_view>
 #include <unordered_map>
 #include <vector>
@@ -75,6 +76,14 @@ class HostFvWide {
   }
   bool needs_weights() const { return global_; }
 
+  // Optional sinks of hash_body: the name of every emitted slot (appended to
+  // *names, end offsets in *name_end) and the byte span of every datum in the
+  // body (datum_span: begin / end pairs relative to the body). Engines that
+  // keep named features (clustering, weight) use them; null = off.
+  void set_sinks(std::string* names, std::vector<int64_t>* name_end, std::vector<int64_t>* datum_span) {
+    names_ = names; name_end_ = name_end; span_ = datum_span;
+  }
+
   // Document-statistics journal of one hash call: on an error the caller
   // rolls back every update it made (a capacity retry re-runs the batch).
   void begin() { journal_.clear(); jdocs_ = jlen_ = 0; }
@@ -95,8 +104,13 @@ class HostFvWide {
     if (!c.array(&cnt)) return 1;
     for (uint32_t i = 0; i < cnt; ++i) {
       if (*n >= max_samples) return 2;
+      const uint8_t* d0 = c.p;
       int rc = datum(c, idx, val, max_slots, slots, update);
       if (rc) return rc;
+      if (span_) {
+        span_->push_back((int64_t)(d0 - p));
+        span_->push_back((int64_t)(c.p - p));
+      }
       row_ptr[++*n] = *slots;
     }
     return 0;
@@ -218,6 +232,7 @@ class HostFvWide {
       idx[*slots] = feats_[i].idx;
       val[*slots] = (float)feats_[i].w;
       ++*slots;
+      if (names_) put_name(feats_[i].name);
     }
     for (size_t r = 0; r + 1 < c_.size(); r += 2) {
       const HostRule& L = c_[r];
@@ -234,6 +249,13 @@ class HostFvWide {
           const double a = feats_[i].w, b = feats_[j].w;
           val[*slots] = (float)(L.value_kind == 1 ? a * b : a + b);
           ++*slots;
+          if (names_) {     // left & right + the rule's suffix (the hashed bytes)
+            put_name(feats_[i].name, false);
+            names_->push_back('&');
+            put_name(feats_[j].name, false);
+            names_->append((const char*)suf, (size_t)L.suffix_len);
+            name_end_->push_back((int64_t)names_->size());
+          }
         }
       }
     }
@@ -273,6 +295,15 @@ class HostFvWide {
       }
     }
   }
+
+  void put_name(const WideName& nm, bool end = true) {
+    for (int i = 0; i < nm.k; ++i) names_->append((const char*)nm.p[i], nm.n[i]);
+    if (end) name_end_->push_back((int64_t)names_->size());
+  }
+
+  std::string* names_ = nullptr;
+  std::vector<int64_t>* name_end_ = nullptr;
+  std::vector<int64_t>* span_ = nullptr;
 
   struct Tok { uint32_t off, len; };
   struct Uniq { uint32_t off, len; int cnt; };

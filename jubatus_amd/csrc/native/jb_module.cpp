@@ -289,6 +289,53 @@ py::tuple wide_hash(jb::HostFvWide& h, py::list reqs, uintptr_t idx, uintptr_t v
   return py::make_tuple(n, slots, 0);
 }
 
+// One body (msgpack list<datum>) with feature names: -> (error, row_ptr
+// int64 [n+1], idx int32, val float32, names bytes, name_end int64 [slots],
+// datum spans int64 [n][2] relative to the body). error 1: malformed (no
+// statistics were updated).
+py::tuple wide_hash_named(jb::HostFvWide& h, py::buffer body, bool update) {
+  py::buffer_info bi = body.request();
+  const uint8_t* p = (const uint8_t*)bi.ptr;
+  const size_t len = (size_t)(bi.size * bi.itemsize);
+  int64_t cap_n = 256, cap_s = 4096;
+  for (;;) {
+    std::vector<int64_t> rp((size_t)cap_n + 1, 0), name_end, spans;
+    std::vector<int32_t> idx((size_t)cap_s);
+    std::vector<float> val((size_t)cap_s);
+    std::string names;
+    int64_t n = 0, slots = 0;
+    h.begin();
+    h.set_sinks(&names, &name_end, &spans);
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = h.hash_body(p, len, idx.data(), val.data(), rp.data(), cap_n, cap_s, &n, &slots, update);
+    }
+    h.set_sinks(nullptr, nullptr, nullptr);
+    if (rc == 2) {
+      if (update && h.needs_weights()) h.rollback();
+      cap_n *= 4;
+      cap_s *= 4;
+      continue;
+    }
+    if (rc) {
+      if (update && h.needs_weights()) h.rollback();
+      return py::make_tuple(rc, py::none(), py::none(), py::none(), py::none(), py::none(), py::none());
+    }
+    py::array_t<int64_t> a_rp(n + 1), a_ne(slots), a_sp(2 * n);
+    py::array_t<int32_t> a_idx(slots);
+    py::array_t<float> a_val(slots);
+    memcpy(a_rp.mutable_data(), rp.data(), 8 * (size_t)(n + 1));
+    if (slots) {
+      memcpy(a_idx.mutable_data(), idx.data(), 4 * (size_t)slots);
+      memcpy(a_val.mutable_data(), val.data(), 4 * (size_t)slots);
+      memcpy(a_ne.mutable_data(), name_end.data(), 8 * (size_t)slots);
+    }
+    if (n) memcpy(a_sp.mutable_data(), spans.data(), 16 * (size_t)n);
+    return py::make_tuple(0, a_rp, a_idx, a_val, py::bytes(names), a_ne, a_sp);
+  }
+}
+
 // -> (n_samples, n_slots, error): 0 ok, 1 malformed request, 2 capacity
 py::tuple hasher_hash(const jb::HostFvHasher& h, py::list reqs, uintptr_t idx, uintptr_t val,
                       uintptr_t row_ptr, int64_t max_samples, int64_t max_slots, bool update) {
@@ -396,7 +443,10 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("needs_weights", &jb::HostFvWide::needs_weights)
       .def("hash", &wide_hash, "wide-rule converter: msgpack list<datum> bodies -> CSR",
            py::arg("reqs"), py::arg("idx"), py::arg("val"), py::arg("row_ptr"),
-           py::arg("max_samples"), py::arg("max_slots"), py::arg("update") = false);
+           py::arg("max_samples"), py::arg("max_slots"), py::arg("update") = false)
+      .def("hash_named", &wide_hash_named,
+           "one list<datum> body -> (err, row_ptr, idx, val, names, name_end, datum spans)",
+           py::arg("body"), py::arg("update") = false);
   m.def("pack_requests", &pack, "scan msgpack request bodies into a device-ready batch");
   m.def("pack_spans", &pack_spans, "zero-copy scan of request spans inside one pinned arena");
   py::class_<PyRpcServer>(m, "RpcServer")

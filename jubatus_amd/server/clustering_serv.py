@@ -8,7 +8,10 @@ Queries before the first clustering raise "clustering is not performed yet"
 """
 from __future__ import annotations
 
+import msgpack
+
 from ..common.exceptions import ArgumentError
+from ..common.mprpc import split_params
 from ..framework.engine_serv import EngineServ
 from ..fv_converter.converter import DatumToFvConverter
 from ..fv_converter.datum import Datum
@@ -27,6 +30,17 @@ class ClusteringServ(EngineServ):
         if not isinstance(points, list):
             raise ArgumentError("push: points must be a list")
         return self.driver.push([Datum.from_msgpack(p) for p in points])
+
+    def raw_push(self, params: bytes) -> bool:
+        """zero-copy path: the list<datum> bytes go to the native named
+        converter in one call (models/clustering.py push_body)"""
+        self.check_set_config()
+        parts = split_params(params)
+        if len(parts) != 2:
+            raise ArgumentError("push: expected 2 arguments")
+        if getattr(self.driver, "_native", None) is None:
+            return self.push(msgpack.unpackb(parts[1], raw=False))
+        return self.driver.push_body(parts[1])
 
     def get_revision(self) -> int:
         self.check_set_config()
