@@ -55,11 +55,12 @@ __device__ __forceinline__ void lof_insert_body(
     int p, const int32_t* __restrict__ cs, const float* __restrict__ cd, int nc, int k,
     int ignore_same, int32_t* __restrict__ nb_slot, float* __restrict__ nb_dist,
     float* __restrict__ kdist, uint8_t* __restrict__ ok, uint8_t* __restrict__ lrd_ok,
-    int32_t* __restrict__ changed, int32_t* __restrict__ nchanged) {
+    int32_t* __restrict__ changed, int32_t* __restrict__ nchanged, bool first = true) {
   __shared__ int n_ch;
   __shared__ int32_t l_s[64][kLofMaxK];
   __shared__ float l_d[64][kLofMaxK];
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && !first) n_ch = *nchanged;   // a later chunk of candidates: reverse inserts only
+  if (threadIdx.x == 0 && first) {
     n_ch = 0;
     int32_t* ps = nb_slot + (int64_t)p * k;
     float* pd = nb_dist + (int64_t)p * k;
@@ -114,13 +115,14 @@ __device__ __forceinline__ void lof_insert_body(
 __global__ __launch_bounds__(64) void lof_add_kernel(
     const LofArgs a, int p, int k, int ignore_same, int32_t* __restrict__ nb_slot,
     float* __restrict__ nb_dist, float* __restrict__ kdist, uint8_t* __restrict__ ok,
-    uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged) {
+    uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged,
+    int first) {
   __shared__ int32_t cs[kLofArgMax];
   __shared__ float cd[kLofArgMax];
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
   __syncthreads();
   lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
-                  nchanged);
+                  nchanged, first != 0);
 }
 
 // Every row listing a changed row: lrd_ok = 0 (and, clear_ok: ok = 0 -
@@ -339,12 +341,22 @@ extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int
                           float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                           int32_t* changed, int32_t* nchanged, uint32_t* out_host,
                           int max_missing, hipStream_t stream) {
-  if (k <= 0 || k > jb::kLofMaxK) return -2;
+  if (k <= 0 || k > jb::kLofMaxK || nc < 0) return -2;
+  // the candidates travel in the kernel arguments, kLofArgMax per launch: the
+  // first launch sets p's own list (its k nearest are the head of the first
+  // chunk) and the reverse inserts of that chunk, later ones (a
+  // reverse_nearest_neighbor_num above the argument budget) only insert p
+  // into their candidates' lists
   jb::LofArgs a;
-  int rc = fill_args(&a, cs, cd, nc);
+  for (int c0 = 0; c0 == 0 || c0 < nc; c0 += jb::kLofArgMax) {
+    const int cn = nc - c0 < jb::kLofArgMax ? nc - c0 : jb::kLofArgMax;
+    int rc = fill_args(&a, cs + c0, cd + c0, cn < 0 ? 0 : cn);
+    if (rc) return rc;
+    hipLaunchKernelGGL(jb::lof_add_kernel, dim3(1), dim3(64), 0, stream, a, p, k, ignore_same,
+                       nb_slot, nb_dist, kdist, ok, lrd_ok, changed, nchanged, c0 == 0 ? 1 : 0);
+  }
+  int rc = fill_args(&a, cs, cd, nc < jb::kLofArgMax ? nc : jb::kLofArgMax);
   if (rc) return rc;
-  hipLaunchKernelGGL(jb::lof_add_kernel, dim3(1), dim3(64), 0, stream, a, p, k, ignore_same,
-                     nb_slot, nb_dist, kdist, ok, lrd_ok, changed, nchanged);
   const unsigned blocks = (unsigned)((nrows + 255) / 256);
   hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(blocks), dim3(256), 0, stream, nrows, k, nb_slot,
                      changed, nchanged, 0, ok, lrd_ok);

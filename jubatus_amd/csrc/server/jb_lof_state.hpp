@@ -84,7 +84,7 @@ class LofState {
   // lists are missing
   bool add(int32_t p, const std::vector<int32_t>& cs, const std::vector<float>& cd, float* score,
            std::vector<int32_t>* missing) {
-    const int nc = (int)std::min<size_t>(cs.size(), kLofArgMax);
+    const int nc = (int)cs.size();     // (kLofArgMax candidates per launch inside)
     const int rc = jb_lof_add(p, cs.data(), cd.data(), nc, k_, ignore_ ? 1 : 0, cap_, nb_slot_.p,
                               nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p,
                               out_, kLofMaxMissing, stream_);

@@ -92,8 +92,8 @@ inline bool parse_config(Kind kind, const std::string& text, Config* c, std::str
     c->k = (int)num("nearest_neighbor_num", 10);
     c->rnn = (int)num("reverse_nearest_neighbor_num", 30);
     if (c->k <= 0 || c->rnn < c->k) { *why = "nearest_neighbor_num / reverse_nearest_neighbor_num"; return false; }
-    if (c->k > jb::row::kLofMaxK || c->rnn >= jb::row::kLofArgMax) {
-      *why = "k / rnn beyond the device limits";
+    if (c->k > jb::row::kLofMaxK) {
+      *why = "nearest_neighbor_num beyond the device limit";
       return false;
     }
     if (const Value* b = c->param.get("ignore_kth_same_point"))

@@ -48,9 +48,7 @@ class LOF(RowEngine):
         if self.k <= 0 or self.rnn < self.k:
             raise ValueError("nearest_neighbor_num must be > 0 and <= reverse_nearest_neighbor_num")
         self.ignore_kth_same = bool(p.get("ignore_kth_same_point", False))
-        if device is not None and self.rnn > 127:
-            # the device add carries the candidates in its kernel arguments
-            raise ValueError("reverse_nearest_neighbor_num must be <= 127 on the GPU")
+
         self.outer = method
         super().__init__(inner, dict(p.get("parameter") or {}), converter, device,
                          p.get("unlearner"), p.get("unlearner_parameter"))
@@ -107,22 +105,61 @@ class LOF(RowEngine):
             self._st.moved([s])
         return ok
 
+    # a MIX / bulk write that changes at least this share of the stored rows
+    # rebuilds every neighbour list (exact k-NN of the whole set); smaller ones
+    # are applied incrementally
+    REBUILD_ALL_FRACTION = 0.25
+
     def _rows_changed(self, slots) -> None:
+        """rows written by a MIX (inserted, replaced or removed): applied
+        incrementally, as a batch of adds - the changed rows' lists and every
+        list naming them are invalidated (one device pass per 1024 rows), the
+        rows among the reverse_nearest_neighbor_num nearest of a changed row
+        that now have it inside their k-distance join them, and all those
+        lists are rebuilt with batched k-NN queries right away, so the first
+        adds and scores after the MIX find a warm state (the lists were
+        wiped past 4096 rows before)."""
         if self._st is None or not len(slots):
             return
-        if len(slots) > 4096:
-            self._st.clear()
-        else:
-            self._st.moved(list(slots))
+        self._apply_changed([int(s) for s in slots])
 
     def _set_many(self, items: list, bump: bool = True, update_weight: bool = True) -> None:
         super()._set_many(items, bump, update_weight)
         if self._st is None or not items:
             return
-        if len(items) > 4096:
-            self._st.clear()         # lists rebuilt on demand
+        self._apply_changed([self.rows.slot(rid) for rid, _ in items])
+
+    def _apply_changed(self, slots: list, chunk: int = 1024) -> None:
+        st = self._state()
+        ids = self.rows.ids
+        live_n = sum(1 for r in ids if r is not None)
+        slots = sorted(set(s for s in slots if s is not None))
+        if not slots:
             return
-        self._st.moved([self.rows.slot(rid) for rid, _ in items])
+        st.moved(slots)
+        if live_n == 0:
+            return
+        if len(slots) >= self.REBUILD_ALL_FRACTION * live_n:
+            st.moved([s for s, r in enumerate(ids) if r is not None])
+            self.build_lists(chunk)
+            return
+        alive = [s for s in slots if s < len(ids) and ids[s] is not None]
+        kd = st.kdist[:len(ids)].cpu().numpy() if hasattr(st.kdist, "cpu") else np.asarray(st.kdist[:len(ids)])
+        ok = st.ok[:len(ids)].cpu().numpy() if hasattr(st.ok, "cpu") else np.asarray(st.ok[:len(ids)])
+        affected = set(alive)
+        for i in range(0, len(alive), chunk):
+            part = alive[i:i + chunk]
+            for s, lst in zip(part, self.query_slot_lists(part, self.rnn + 1, similar=False)):
+                for o, d in lst:
+                    if o != s and (not ok[o] or d <= kd[o]):
+                        affected.add(o)
+        todo = sorted(affected)
+        for i in range(0, len(todo), chunk):
+            part = todo[i:i + chunk]
+            st.set_lists(part, [self._pairs(lst) for lst in self.query_slot_lists(part, self.k + 1,
+                                                                                   similar=False)])
+        # lists invalidated because they named a changed row
+        self.build_lists(chunk)
 
     def build_lists(self, chunk: int = 1024, progress=None) -> int:
         """compute the neighbour list of every stored row that has none

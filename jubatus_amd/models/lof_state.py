@@ -274,8 +274,8 @@ class DeviceLofState:
         """insert + mark + score of p in one host call (csrc/hip/lof.hip
         jb_lof_add; candidates in the kernel arguments)"""
         from ..ops import hip
-        cs = np.ascontiguousarray(cs[:128], np.int32)
-        cd = np.ascontiguousarray(cd[:128], np.float32)
+        cs = np.ascontiguousarray(cs, np.int32)
+        cd = np.ascontiguousarray(cd, np.float32)
         hip.lof_add(p, cs, cd, self, self._outbuf, LOF_MAX_MISSING)
         self._pos = 0
         return self._result()

@@ -416,12 +416,12 @@ def _lof_check(st, *slots) -> None:
 def lof_add(p: int, cs, cd, st, out: "HostBuffer", max_missing: int) -> None:
     """one LOF add on the device (csrc/hip/lof.hip jb_lof_add): candidates
     (host int32 / float32 arrays, the rnn nearest of p ascending, p excluded)
-    in the kernel arguments; insert + staleness mark + score of p, waited
-    for; ``out`` = [status, score, lrd, nmissing, missing...]"""
+    in the kernel arguments, 128 per launch; insert + staleness mark + score
+    of p, waited for; ``out`` = [status, score, lrd, nmissing, missing...]"""
     _lof_check(st, p)
     nc = int(cs.size)
-    if nc > 128 or cd.size < nc or cs.dtype.itemsize != 4 or cd.dtype.itemsize != 4:
-        raise ValueError("lof_add: at most 128 int32 / float32 candidates")
+    if cd.size < nc or cs.dtype.itemsize != 4 or cd.dtype.itemsize != 4:
+        raise ValueError("lof_add: int32 / float32 candidates")
     if out.nbytes < 4 * (4 + max_missing):
         raise ValueError("lof_add: output buffer too small")
     rc = _fn("jb_lof_add")(p, cs.ctypes.data, cd.ctypes.data, nc, st.k, int(st.ignore_same),
