@@ -177,10 +177,11 @@ SERVERS = {
     "jubabandit": (["server/jubabandit.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubaburst": (["server/jubaburst.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubagraph": (["server/jubagraph.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    "jubaweight": (["server/jubaweight.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     # check of the RCCL data plane of the native MIX on one GPU (not a server)
     "jb_rccl_check": (["tools/jb_rccl_check.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }
-HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph"}
+HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph", "jubaweight"}
 # servers with a native distributed mode (the model plane over RCCL)
 RCCL_SERVERS = {"jubaclassifier", "jb_rccl_check"}
 

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict
 __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restrict__ X, int n, int d,
                                                           const float* __restrict__ w, float* __restrict__ C,
                                                           float* __restrict__ var, float* __restrict__ pi,
-                                                          int k, int iters) {
+                                                          int k, int iters, int32_t* __restrict__ assign) {
   extern __shared__ float s_em[];
   float* sC = s_em;
   float* sV = sC + k * d;
@@ -290,17 +290,41 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
   }
   for (int i = t; i < k * d; i += kClBlock) { C[i] = sC[i]; var[i] = sV[i]; }
   for (int j = t; j < k; j += kClBlock) pi[j] = nk[j];
+  if (assign == nullptr) return;
+  // the most likely component of every point under the final parameters
+  // (models/clustering.py _assign: argmax of the log responsibilities)
+  for (int j = t; j < k; j += kClBlock) {
+    float ld = 0.f;
+    for (int q = 0; q < d; ++q) ld += logf(6.283185307179586f * sV[j * d + q]);
+    lc[j] = logf(fmaxf(nk[j], 1e-12f)) - 0.5f * ld;
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += kClBlock) {
+    const float* x = X + (int64_t)i * d;
+    int best = 0;
+    float bv = -INFINITY;
+    for (int j = 0; j < k; ++j) {
+      float q2 = 0.f;
+      for (int q = 0; q < d; ++q) {
+        const float df = x[q] - sC[j * d + q];
+        q2 += df * df / sV[j * d + q];
+      }
+      const float v = lc[j] - 0.5f * q2;
+      if (v > bv) { bv = v; best = j; }
+    }
+    assign[i] = best;
+  }
 }
 
 }  // namespace jb
 
 extern "C" int jb_gmm_em(const float* X, int n, int d, const float* w, float* C, float* var, float* pi, int k,
-                         int iters, hipStream_t stream) {
+                         int iters, int32_t* assign, hipStream_t stream) {
   if (n <= 0 || k <= 0 || d <= 0) return 0;
   const size_t lds = sizeof(float) * (4 * (size_t)k * d + 2 * (size_t)k);
   if (lds > 64 * 1024) return -2;
   hipLaunchKernelGGL(jb::gmm_em_kernel, dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var, pi, k,
-                     iters);
+                     iters, assign);
   return (int)hipGetLastError();
 }
 

@@ -54,6 +54,14 @@ constexpr int kStepList = 64;        // distinct rows of one step the table hold
 constexpr int kTailReason = 20;
 constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2;
 constexpr int kSerialSegments = 4;
+// committer phase timings (tail[4..19]): shader-clock reads in the step loop
+// cost more than the phases they measure, so they are compiled in only for
+// diagnosis (JB_SERIAL_TIMING=1 at build time)
+#ifndef JB_SERIAL_TIMING
+#define JB_SERIAL_TIMING 0
+#endif
+constexpr bool kSerialTiming = JB_SERIAL_TIMING != 0;
+__device__ __forceinline__ uint64_t stamp() { return kSerialTiming ? clock64() : 0; }
 
 // scores of all labels of one sample with plain (L1-cached) loads: the
 // score pass reads a table nothing writes during the kernel
@@ -588,9 +596,9 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   // diagnostics: shader-clock cycles thread 0 spends per phase (bound
   // checks, barrier A, staging + B1, the exact step, B2, round setup)
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
-  uint64_t wwork = 0, tw = clock64();   // per wave: cycles from B2 to the next ballot
-  const uint64_t w0 = wall_clock64();
-  uint64_t tc = clock64();
+  uint64_t wwork = 0, tw = stamp();   // per wave: cycles from B2 to the next ballot
+  const uint64_t w0 = kSerialTiming ? wall_clock64() : 0;
+  uint64_t tc = stamp();
   for (int64_t p = beg; p < end; p += T) {
     const int64_t j = p + tid;
     const bool live = j < end;
@@ -636,14 +644,14 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       }
       return b;
     };
-    tw = clock64();
+    tw = stamp();
     float bnd = 0.f;
     if (open && (sl < 0.f || 2.f * l1 * s_dmax >= sl)) {
       load_features<NF>(fi, fx, live, nf, fb, fidx, fval);
       loaded = true;
       if (sl >= 0.f && !s_sat) bnd = full_bound();
     }
-    { const uint64_t t = clock64(); ph[5] += t - tc; tc = t; }
+    { const uint64_t t = stamp(); ph[5] += t - tc; tc = t; }
     for (;;) {
       if (open && tid > lim && sl >= 0.f && !loaded && 2.f * l1 * s_dmax >= sl) {
         load_features<NF>(fi, fx, live, nf, fb, fidx, fval);   // Dmax grew past the cheap test
@@ -651,12 +659,12 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         bnd = full_bound();
       }
       const bool unsafe = open && tid > lim && (sl < 0.f || s_sat || (loaded && 2.f * bnd >= sl));
-      wwork += clock64() - tw;
+      wwork += stamp() - tw;
       const uint64_t m = __builtin_amdgcn_ballot_w64(unsafe);
       if (lane == 0 && m != 0) atomicMin(&s_first[iter & 1], wv * 64 + (int)__builtin_ctzll(m));
-      { const uint64_t t = clock64(); ph[0] += t - tc; tc = t; }
+      { const uint64_t t = stamp(); ph[0] += t - tc; tc = t; }
       lds_barrier();       // A: the first unsettled sample of the round is known
-      { const uint64_t t = clock64(); ph[1] += t - tc; tc = t; }
+      { const uint64_t t = stamp(); ph[1] += t - tc; tc = t; }
       const int k = s_first[iter & 1];
       if (tid == 0) s_first[(iter + 1) & 1] = INT_MAX;
       ++iter;
@@ -675,7 +683,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
         if (lane == 0) s_sn = 0;
       }
       lds_barrier();       // B1
-      { const uint64_t t = clock64(); ph[2] += t - tc; tc = t; }
+      { const uint64_t t = stamp(); ph[2] += t - tc; tc = t; }
       if (wv == 0) {
         // this step reads what the previous one wrote (its atomics drained
         // meanwhile, behind barriers A / B1)
@@ -692,10 +700,10 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       lim = k;
       ++steps;
       ++n_steps;
-      { const uint64_t t = clock64(); ph[3] += t - tc; tc = t; }
+      { const uint64_t t = stamp(); ph[3] += t - tc; tc = t; }
       lds_barrier();       // B2: D / the step table / s_sat visible to every wave
-      { const uint64_t t = clock64(); ph[4] += t - tc; tc = t; }
-      tw = clock64();
+      { const uint64_t t = stamp(); ph[4] += t - tc; tc = t; }
+      tw = stamp();
       if (s_sat || steps > bail_after) {
         stop = p + k + 1;
         why = s_sat ? kStopSaturated : kStopDense;
@@ -728,8 +736,8 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     put(3, n_rounds);
     put(21, 1);             // segments
     for (int i = 0; i < 6; ++i) put(4 + i, (int64_t)ph[i]);
-    put(10, (int64_t)(wall_clock64() - w0));    // 100 MHz ticks
-    put(11, (int64_t)(clock64() - tc) + (int64_t)(ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5]));
+    put(10, kSerialTiming ? (int64_t)(wall_clock64() - w0) : 0);    // 100 MHz ticks
+    put(11, (int64_t)(stamp() - tc) + (int64_t)(ph[0] + ph[1] + ph[2] + ph[3] + ph[4] + ph[5]));
     if (stats != nullptr && s_valid > 0) atomicAdd(stats + 1, (unsigned long long)s_valid);
   }
   if (tid == 0 && stats != nullptr && n_upd > 0) atomicAdd(stats, (unsigned long long)n_upd);

@@ -400,13 +400,17 @@ class Clustering:
             C = newC
             if done:
                 break
+        em_assign = None
         if self.method == "gmm":
             C, var, pi = self._em(X, w, C)
             self.variances, self.mix_weights = var, pi
+            em_assign = getattr(self, "_em_assign", None)
         self.centers, self.dims, self._dim_keys = C, dims, keys
         self.core = pts
         if fused is not None and self.method == "kmeans":
             self.assign = fused[0].cpu().tolist()    # the kernel's final assignment pass
+        elif em_assign is not None:
+            self.assign = em_assign.cpu().tolist()   # the EM kernel's final E-step argmax
         else:
             self.assign = self._assign(X).cpu().tolist()
         self.revision += 1
@@ -426,8 +430,10 @@ class Clustering:
         if X.is_cuda:
             from ..ops import hip
             C = C.contiguous().clone()
-            if hip.gmm_em(X.contiguous(), w.contiguous(), C, var, pi, iters):
+            self._em_assign = torch.empty(X.shape[0], dtype=torch.int32, device=X.device)
+            if hip.gmm_em(X.contiguous(), w.contiguous(), C, var, pi, iters, self._em_assign):
                 return C, var, pi
+        self._em_assign = None
         for _ in range(iters):
             r = torch.softmax(self._log_resp(X, C, var, pi), dim=1) * w[:, None]
             nk = r.sum(0).clamp_min(1e-9)

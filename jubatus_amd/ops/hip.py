@@ -112,7 +112,8 @@ _SIGS = {
     "jb_fvw_name_bytes": [],
     "jb_kmeanspp": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p,
                     _c_void_p, _c_void_p, _c_void_p],
-    "jb_gmm_em": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p],
+    "jb_gmm_em": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _c_void_p,
+                  _c_void_p],
     "jb_lloyd": [_c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i32, _i32, _f32, _f32, _c_void_p,
                  _c_void_p, _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
@@ -249,10 +250,11 @@ def lloyd(X: torch.Tensor, w: torch.Tensor, C: torch.Tensor, iters: int, atol: f
 
 
 def gmm_em(X: torch.Tensor, w: torch.Tensor, C: torch.Tensor, var: torch.Tensor, pi: torch.Tensor,
-           iters: int) -> bool:
+           iters: int, assign: torch.Tensor | None = None) -> bool:
     """diagonal-covariance GMM EM on one workgroup (csrc/hip/clustering.hip
-    gmm_em_kernel); C / var [k, d] and pi [k] updated in place. False when
-    k x d does not fit the kernel's LDS (the caller keeps its own path)."""
+    gmm_em_kernel); C / var [k, d] and pi [k] updated in place, and (assign,
+    int32 [n]) every point's most likely component. False when k x d does
+    not fit the kernel's LDS (the caller keeps its own path)."""
     for t, nm in ((X, "X"), (w, "w"), (C, "C"), (var, "var"), (pi, "pi")):
         _dev(t, torch.float32, nm)
     n, d = X.shape
@@ -261,7 +263,11 @@ def gmm_em(X: torch.Tensor, w: torch.Tensor, C: torch.Tensor, var: torch.Tensor,
         raise ValueError("gmm_em: bad operand shapes")
     if 4 * (4 * k * d + 2 * k) > 64 * 1024:
         return False
-    rc = _fn("jb_gmm_em")(_p(X), n, d, _p(w), _p(C), _p(var), _p(pi), k, iters, _stream())
+    if assign is not None:
+        _dev(assign, torch.int32, "assign")
+        if assign.numel() < n:
+            raise ValueError("gmm_em: assign shorter than X")
+    rc = _fn("jb_gmm_em")(_p(X), n, d, _p(w), _p(C), _p(var), _p(pi), k, iters, _p(assign), _stream())
     _check(rc, "jb_gmm_em")
     return True
 
