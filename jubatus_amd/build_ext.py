@@ -178,6 +178,8 @@ SERVERS = {
     "jubaburst": (["server/jubaburst.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubagraph": (["server/jubagraph.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     "jubaweight": (["server/jubaweight.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    # coresets + k-means++ / Lloyd / GMM EM in csrc/hip/clustering.hip
+    "jubaclustering": (["server/jubaclustering.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     # check of the RCCL data plane of the native MIX on one GPU (not a server)
     "jb_rccl_check": (["tools/jb_rccl_check.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }

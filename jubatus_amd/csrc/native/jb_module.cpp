@@ -9,6 +9,7 @@
 #include "jb_hash.hpp"
 #include "jb_hostfv.hpp"
 #include "jb_hostfv_wide.hpp"
+#include "jb_pyrandom.hpp"
 #include "jb_pack.hpp"
 #include "jb_rpc.hpp"
 
@@ -435,6 +436,13 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("hash", &hasher_hash, "hash msgpack list<datum> bodies into CSR (idx, val, row_ptr)",
            py::arg("reqs"), py::arg("idx"), py::arg("val"), py::arg("row_ptr"),
            py::arg("max_samples"), py::arg("max_slots"), py::arg("update") = false);
+  py::class_<jb::PyRandom>(m, "PyRandom", "CPython random.Random twin (jb_pyrandom.hpp)")
+      .def(py::init<int64_t>())
+      .def("random", &jb::PyRandom::random)
+      .def("getrandbits", &jb::PyRandom::getrandbits)
+      .def("randbelow", &jb::PyRandom::randbelow)
+      .def("sample_range", &jb::PyRandom::sample_range)
+      .def("choice_weighted", &jb::PyRandom::choice_weighted);
   py::class_<jb::HostFvWide>(m, "HostFvWide")
       .def(py::init(&make_wide))
       .def("set_weights", [](jb::HostFvWide& h, uintptr_t df, uintptr_t diff, uintptr_t counts) {

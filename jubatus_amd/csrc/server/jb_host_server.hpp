@@ -31,6 +31,9 @@ struct HostMethod {
   size_t arity;        // including the leading cluster name
   bool update;         // write lock + update_count
   std::function<void(const std::vector<Value>&, MsgpackWriter*)> fn;
+  // optional zero-decode handler: the raw msgpack params array (arity
+  // checked), for bulk payloads the engine reads in place (clustering push)
+  std::function<void(const std::string&, MsgpackWriter*)> raw = nullptr;
 };
 
 class HostEngine {
@@ -89,7 +92,40 @@ class HostServer {
            ".jubatus";
   }
 
+  // elements of a params array header (-1: not an array)
+  static int64_t params_count(const std::string& p) {
+    if (p.empty()) return -1;
+    const uint8_t t = (uint8_t)p[0];
+    if ((t & 0xf0) == 0x90) return t & 0x0f;
+    if (t == 0xdc && p.size() >= 3) return ((int64_t)(uint8_t)p[1] << 8) | (uint8_t)p[2];
+    if (t == 0xdd && p.size() >= 5)
+      return ((int64_t)(uint8_t)p[1] << 24) | ((int64_t)(uint8_t)p[2] << 16) | ((int64_t)(uint8_t)p[3] << 8) |
+             (uint8_t)p[4];
+    return -1;
+  }
+
   std::string dispatch(const jb::RpcRequest& r) {
+    for (const auto& x : table_) {
+      if (x.name != r.method || !x.raw) continue;
+      if (params_count(r.params) != (int64_t)x.arity)
+        return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+      MsgpackWriter w;
+      try {
+        if (x.update) {
+          std::unique_lock<std::shared_mutex> g(model_mu_);
+          update_count_ += 1;
+          x.raw(r.params, &w);
+        } else {
+          std::shared_lock<std::shared_mutex> g(model_mu_);
+          x.raw(r.params, &w);
+        }
+      } catch (const std::invalid_argument&) {
+        return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+      } catch (const std::exception& e) {
+        return r.notify ? std::string() : jb::val::response_msg(r.msgid, e.what());
+      }
+      return r.notify ? std::string() : jb::val::response_ok(r.msgid, w.out);
+    }
     Value args;
     try {
       args = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
