@@ -208,7 +208,8 @@ __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict
 __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restrict__ X, int n, int d,
                                                           const float* __restrict__ w, float* __restrict__ C,
                                                           float* __restrict__ var, float* __restrict__ pi,
-                                                          int k, int iters, int32_t* __restrict__ assign) {
+                                                          int k, int iters, int32_t* __restrict__ assign,
+                                                          bool staged) {
   extern __shared__ float s_em[];
   float* sC = s_em;
   float* sV = sC + k * d;
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
   float* s2 = s1 + k * d;
   float* nk = s2 + k * d;          // [k]
   float* lc = nk + k;              // [k] log pi_j - 0.5 sum_q log(2 pi var_jq)
+  float* sR = lc + k;              // [n][k] responsibilities (staged)
   __shared__ float s_tot;
   const int t = threadIdx.x;
   const float kLog2Pi = 1.8378770664093453f;
@@ -233,7 +235,51 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
     for (int j = t; j < k; j += kClBlock) nk[j] = 0.f;
     __syncthreads();
     (void)kLog2Pi;
-    for (int i = t; i < n; i += kClBlock) {
+    if (staged) {
+      // E-step: each point's responsibilities into LDS (one distance pass)
+      for (int i = t; i < n; i += kClBlock) {
+        const float* x = X + (int64_t)i * d;
+        float* r = sR + (size_t)i * k;
+        float mx = -INFINITY;
+        for (int j = 0; j < k; ++j) {
+          float q2 = 0.f;
+          for (int q = 0; q < d; ++q) {
+            const float df = x[q] - sC[j * d + q];
+            q2 += df * df / sV[j * d + q];
+          }
+          r[j] = lc[j] - 0.5f * q2;
+          mx = fmaxf(mx, r[j]);
+        }
+        float den = 0.f;
+        for (int j = 0; j < k; ++j) den += expf(r[j] - mx);
+        const float wi = w[i] / den;
+        for (int j = 0; j < k; ++j) r[j] = wi * expf(r[j] - mx);
+      }
+      __syncthreads();
+      // M-step sums: one wave per (cluster, column) pair, lanes over the
+      // points, a shuffle reduction and one plain store (no LDS atomics)
+      const int lane = t & 63, wave = t >> 6, cols = 2 * d + 1;
+      for (int pr = wave; pr < k * cols; pr += kClBlock / 64) {
+        const int j = pr / cols, col = pr - j * cols;
+        float acc = 0.f;
+        for (int i = lane; i < n; i += 64) {
+          const float r = sR[(size_t)i * k + j];
+          if (col == 2 * d) {
+            acc += r;
+          } else {
+            const float xv = X[(int64_t)i * d + (col < d ? col : col - d)];
+            acc += col < d ? r * xv : r * xv * xv;
+          }
+        }
+        for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (lane == 0) {
+          if (col == 2 * d) nk[j] = acc;
+          else if (col < d) s1[j * d + col] = acc;
+          else s2[j * d + col - d] = acc;
+        }
+      }
+    }
+    for (int i = staged ? n : t; i < n; i += kClBlock) {
       const float* x = X + (int64_t)i * d;
       // log-sum-exp over the clusters (k is small: two passes over d)
       float mx = -INFINITY;
@@ -321,10 +367,15 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
 extern "C" int jb_gmm_em(const float* X, int n, int d, const float* w, float* C, float* var, float* pi, int k,
                          int iters, int32_t* assign, hipStream_t stream) {
   if (n <= 0 || k <= 0 || d <= 0) return 0;
-  const size_t lds = sizeof(float) * (4 * (size_t)k * d + 2 * (size_t)k);
+  size_t lds = sizeof(float) * (4 * (size_t)k * d + 2 * (size_t)k);
   if (lds > 64 * 1024) return -2;
+  // responsibilities staged in LDS when they fit: the M-step then reduces
+  // per (cluster, column) instead of contending on LDS float atomics
+  const size_t staged = lds + sizeof(float) * (size_t)n * k;
+  const bool stage = staged <= 64 * 1024;
+  if (stage) lds = staged;
   hipLaunchKernelGGL(jb::gmm_em_kernel, dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var, pi, k,
-                     iters, assign);
+                     iters, assign, stage);
   return (int)hipGetLastError();
 }
 

@@ -25,7 +25,8 @@ PAGES = [
      "LOCAL_RANK, or the least-used device assigned by jubavisor); models live in HBM and are "
      "mixed with the other members of the cluster over RCCL. Without --zookeeper the server "
      "runs standalone. jubaclassifier, jubaregression, jubarecommender, jubanearest_neighbor, "
-     "jubaanomaly, jubastat, jubabandit, jubaburst and jubagraph are native binaries (no "
+     "jubaanomaly, jubaclustering, jubastat, jubabandit, jubaburst, jubagraph and jubaweight "
+     "are native binaries (no "
      "Python) for standalone configurations whose converter runs on the native hashers; they "
      "hand every other setup to this server with the same flags."),
     ("jubatus_proxy", 8, ["bin/jubaclassifier_proxy", "--help"],
@@ -61,7 +62,8 @@ def _esc(s: str) -> str:
 
 
 def render(name: str, sec: int, cmd: list[str], short: str, desc: str) -> str:
-    env = dict(os.environ, PYTHONPATH=ROOT, COLUMNS="100")
+    # the Python server's help (the launchers' native binaries take the same flags)
+    env = dict(os.environ, PYTHONPATH=ROOT, COLUMNS="100", JUBATUS_NATIVE_SERVER="0")
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     help_text = (out.stdout or out.stderr).rstrip()
     lines = [f'.TH {name.upper()} {sec} "" "jubatus_amd" "jubatus_amd manual"',
