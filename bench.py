@@ -529,15 +529,18 @@ def fresh_budget(fresh_gb: float, local_ranks: int) -> float:
     return min(PIN_CAP, PIN_FRACTION * _mem_available() / max(1, local_ranks))
 
 
-def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: int, sync) -> dict:
-    """The headline protocol in the serial-equivalent update mode: a fresh
-    model, the same warmup, then ``--exact-steps`` timed steps over the first
-    fresh batches. The result equals applying the batch's requests one after
-    the other (csrc/hip/serial.hip), the reference's semantics."""
+def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: int, sync,
+                 mode: str = "exact", weight_dtype: str = "fp32", steps: int | None = None) -> dict:
+    """The headline protocol in another configuration: a fresh model, the
+    same warmup, then timed steps over the first fresh batches. Default: the
+    serial-equivalent update mode (``--exact-steps`` steps), whose result
+    equals applying the batch's requests one after the other
+    (csrc/hip/serial.hip), the reference's semantics. With weight_dtype
+    bf16: the headline update mode over a bf16 W table."""
     from jubatus_amd.fv_converter.converter import DatumToFvConverter
     from jubatus_amd.models.classifier import LinearClassifier
     clf = LinearClassifier(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]),
-                           device=device, concurrent_update="exact")
+                           device=device, concurrent_update=mode, weight_dtype=weight_dtype)
     for y in range(args.labels):
         clf.set_label(f"label{y}")
 
@@ -548,15 +551,15 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
         for j in range(bps):
             run(warm.batches[(i * bps + j) % len(warm.batches)])
         sync()
-        _progress(f"exact mode: warmup step {i + 1}/{args.warmup} done")
+        _progress(f"{mode}/{weight_dtype}: warmup step {i + 1}/{args.warmup} done")
     st0 = clf.train_stats()
     sync()
     t0 = time.perf_counter()
-    steps = min(args.exact_steps, args.steps)
+    steps = min(args.exact_steps if steps is None else steps, args.steps)
     for i in range(steps):
         for j in range(bps):
             run(fresh.batches[i * bps + j])
-        _progress(f"exact mode: timed step {i + 1}/{steps} queued")
+        _progress(f"{mode}/{weight_dtype}: timed step {i + 1}/{steps} queued")
     sync()
     elapsed = time.perf_counter() - t0
     clf.synchronize()
@@ -564,10 +567,15 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
     trained = st1["trained"] - st0["trained"]
     updated = st1["updated"] - st0["updated"]
     n = samples_per_batch * bps * steps
-    return {"value": round(n / elapsed, 1), "unit": "samples/s", "steps": steps,
-            "ms_per_step": round(elapsed / steps * 1e3, 3), "update_fraction": round(updated / max(1, trained), 5),
-            "concurrent_update": "exact", "semantics": "serial-equivalent (requests applied one after another)",
-            "last_batch": clf._serial.last_batch() if getattr(clf, "_serial", None) is not None else None}
+    out = {"value": round(n / elapsed, 1), "unit": "samples/s", "steps": steps,
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "update_fraction": round(updated / max(1, trained), 5),
+           "concurrent_update": mode, "weight_dtype": weight_dtype}
+    if mode == "exact":
+        out["semantics"] = "serial-equivalent (requests applied one after another)"
+        out["last_batch"] = clf._serial.last_batch() if getattr(clf, "_serial", None) is not None else None
+    else:
+        out["w_bytes"] = int(clf.W.numel() * clf.W.element_size())
+    return out
 
 
 def _mix_summary(log: list) -> dict:
@@ -640,6 +648,11 @@ def main() -> None:
     ap.add_argument("--exact-steps", type=int, default=3,
                     help="1 GPU: also time this many steps of the serial-equivalent exact mode (same "
                          "warmup, same fresh batches, its own model) and report them under exact_mode")
+    ap.add_argument("--weight-dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="storage of the headline model's W table (P and arithmetic stay fp32)")
+    ap.add_argument("--bf16-steps", type=int, default=5,
+                    help="1 GPU, fp32 headline: also time this many steps with a bf16 W table (same "
+                         "warmup, same fresh batches, its own model) and report them under bf16_weights")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="gloo: rehearse the multi-rank GPU path with several ranks on one GPU "
                          "(not a benchmark configuration)")
@@ -699,7 +712,7 @@ def main() -> None:
     cfg["converter"]["hash_max_size"] = 1 << args.hash_bits
     conv = DatumToFvConverter(cfg["converter"])
     clf = LinearClassifier(cfg["method"], cfg["parameter"], conv, device=device,
-                           concurrent_update=args.update_mode)
+                           concurrent_update=args.update_mode, weight_dtype=args.weight_dtype)
     for y in range(args.labels):  # same label order on every rank (set_label, as a client would)
         clf.set_label(f"label{y}")
 
@@ -872,6 +885,10 @@ def main() -> None:
     exact = None
     if world == 1 and device is not None and args.exact_steps > 0 and args.update_mode != "exact":
         exact = exact_record(args, cfg, device, warm, fresh, bps, samples_per_batch, sync)
+    bf16 = None
+    if world == 1 and device is not None and args.bf16_steps > 0 and args.weight_dtype == "fp32":
+        bf16 = exact_record(args, cfg, device, warm, fresh, bps, samples_per_batch, sync,
+                            mode=args.update_mode, weight_dtype="bf16", steps=args.bf16_steps)
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:
         served = served_train(args, local, nat)
@@ -894,7 +911,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32" if args.weight_dtype == "fp32" else "bf16 W, fp32 P and arithmetic",
             "data": ("synthetic, non-repeating: every timed sample is new (native generator, pinned "
                      "host memory, H2D inside the timed region); "
                      + ("worst case: noise string values, every sample updates; " if args.worst_case
@@ -935,6 +952,7 @@ def main() -> None:
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
             "exact_mode": exact,
+            "bf16_weights": bf16,
             "served": served,
             "served_native": served_native,
             "engines": engines,

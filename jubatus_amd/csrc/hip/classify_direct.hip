@@ -36,8 +36,8 @@ struct alignas(16) DirectArgs {
 };
 static_assert(sizeof(DirectArgs) <= 3072, "kernarg block too large");
 
-template <int LC>
-__global__ __launch_bounds__(64) void classify_direct_kernel(const DirectArgs a, const float* W,
+template <int LC, typename WT>
+__global__ __launch_bounds__(64) void classify_direct_kernel(const DirectArgs a, const WT* W,
                                                              float* __restrict__ out,
                                                              volatile uint32_t* __restrict__ done,
                                                              uint32_t seq) {
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(64) void classify_direct_kernel(const DirectArgs a,
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int k = 0; k < L::K; ++k)
-        w[u][k] = id[u] >= 0 ? ld_agent(W + (int64_t)id[u] * LC + l0 + 64 * k) : 0.f;
+        w[u][k] = id[u] >= 0 ? ldw(W + (int64_t)id[u] * LC + l0 + 64 * k) : 0.f;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -99,9 +99,10 @@ __global__ void empty_flag_kernel(volatile uint32_t* done, uint32_t seq) {
 // out_host[n*LC]. Returns 0 on success, 1 when the request does not fit the
 // direct path (caller uses the batch path), a HIP error code otherwise.
 // Blocks until the scores landed.
-extern "C" int jb_classify_direct(const int32_t* idx, const float* val, const int64_t* row_ptr,
-                                  int n, const float* W, int LC, float* out_host,
-                                  uint32_t* done_host, hipStream_t stream) {
+template <typename WT>
+static int classify_direct_impl(const int32_t* idx, const float* val, const int64_t* row_ptr,
+                                int n, const WT* W, int LC, float* out_host,
+                                uint32_t* done_host, hipStream_t stream) {
   if (n <= 0) return 0;
   if (n > jb::kDirectMaxSamples || row_ptr[n] - row_ptr[0] > jb::kDirectMaxSlots) return 1;
   jb::DirectArgs a;
@@ -112,14 +113,28 @@ extern "C" int jb_classify_direct(const int32_t* idx, const float* val, const in
   std::memcpy(a.idx, idx + base, sizeof(int32_t) * (size_t)ns);
   std::memcpy(a.val, val + base, sizeof(float) * (size_t)ns);
   const uint32_t seq = jb::next_seq();
-#define JB_DIRECT(L)                                                                       \
-  hipLaunchKernelGGL((jb::classify_direct_kernel<L>), dim3(n), dim3(64), 0, stream, a, W, \
+#define JB_DIRECT(L)                                                                           \
+  hipLaunchKernelGGL((jb::classify_direct_kernel<L, WT>), dim3(n), dim3(64), 0, stream, a, W, \
                      out_host, done_host, seq);
   JB_LC_DISPATCH(LC, JB_DIRECT)
 #undef JB_DIRECT
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_flags(done_host, n, seq, stream);
+}
+
+extern "C" int jb_classify_direct(const int32_t* idx, const float* val, const int64_t* row_ptr,
+                                  int n, const float* W, int LC, float* out_host,
+                                  uint32_t* done_host, hipStream_t stream) {
+  return classify_direct_impl<float>(idx, val, row_ptr, n, W, LC, out_host, done_host, stream);
+}
+
+// the same over a bf16 W table
+extern "C" int jb_classify_direct_bf16(const int32_t* idx, const float* val,
+                                       const int64_t* row_ptr, int n, const jb::bf16_t* W, int LC,
+                                       float* out_host, uint32_t* done_host, hipStream_t stream) {
+  return classify_direct_impl<jb::bf16_t>(idx, val, row_ptr, n, W, LC, out_host, done_host,
+                                          stream);
 }
 
 // Launch-latency probe: one empty kernel that publishes a flag, then wait by

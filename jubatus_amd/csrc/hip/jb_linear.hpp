@@ -10,6 +10,70 @@ __device__ __forceinline__ float ld_agent(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---------------------------------------------------------------------------
+// W storage type. fp32 (float) or bf16 (uint16_t bit pattern, the upper half
+// of the fp32 value): the bf16 table halves W's HBM footprint and gather
+// bytes; arithmetic stays fp32 (loads widen, the precision table P stays
+// fp32). A bf16 store rounds stochastically - the increment of an online
+// update is often far below half a bf16 ulp of the weight, and
+// round-to-nearest would drop it every time; stochastic rounding keeps the
+// expected value of the stored weight equal to the fp32 sum. The random bits
+// come from a hash of (element address, sample), so a run is reproducible.
+using bf16_t = uint16_t;
+
+__device__ __forceinline__ uint32_t jb_mix32(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
+
+__device__ __forceinline__ float bf16_f(uint32_t b) { return __uint_as_float(b << 16); }
+
+// fp32 -> bf16 with stochastic rounding (r: 32 random bits; the low 16 are
+// used). Adding r to the magnitude's discarded bits carries into the kept
+// part with probability (discarded / 2^16). Inf stays inf; NaN stays NaN.
+__device__ __forceinline__ uint32_t f_bf16_sr(float v, uint32_t r) {
+  const uint32_t u = __float_as_uint(v);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffffu) ? 0x40u : 0u);
+  const uint32_t t = u + (r & 0xffffu);
+  // rounding up past the largest finite value gives inf (as RNE would)
+  return t >> 16;
+}
+
+// W element access, overloaded on the storage type. ldw: agent-scope load
+// (a stream sees other streams' updates in L2, not a stale L1 line; bf16
+// loads the aligned 32-bit word and takes its half). stw: plain store.
+// addw: memory-side add that no concurrent add loses (bf16: a CAS loop on the
+// word; under contention it retries, the fp32 table takes a float atomic).
+__device__ __forceinline__ float ldw(const float* p) { return ld_agent(p); }
+__device__ __forceinline__ float ldw(const bf16_t* p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+  const uint32_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ((uintptr_t)p & 2) ? __uint_as_float(v & 0xffff0000u) : __uint_as_float(v << 16);
+}
+__device__ __forceinline__ void stw(float* p, float v, uint32_t) { *p = v; }
+__device__ __forceinline__ void stw(bf16_t* p, float v, uint32_t r) { *p = (bf16_t)f_bf16_sr(v, r); }
+__device__ __forceinline__ void addw(float* p, float d, uint32_t) { atomicAdd(p, d); }
+__device__ __forceinline__ void addw(bf16_t* p, float d, uint32_t r) {
+  uint32_t* w = reinterpret_cast<uint32_t*>((uintptr_t)p & ~(uintptr_t)3);
+  const int sh = ((uintptr_t)p & 2) ? 16 : 0;
+  uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    const float cur = bf16_f((old >> sh) & 0xffffu);
+    const uint32_t nb = f_bf16_sr(cur + d, r);
+    const uint32_t nw = (old & ~(0xffffu << sh)) | (nb << sh);
+    if (nw == old) return;                     // the rounded sum equals the stored value
+    const uint32_t seen = atomicCAS(w, old, nw);
+    if (seen == old) return;
+    old = seen;
+    r = jb_mix32(r, seen);                     // fresh bits for the retry
+  }
+}
+
 enum Method : int { PERCEPTRON = 0, PA = 1, PA1 = 2, PA2 = 3, CW = 4, AROW = 5, NHERD = 6 };
 // kSerial: several streams with the result of applying them one after the
 // other (serial.hip: speculative scoring + an ordered committer)
@@ -73,10 +137,10 @@ struct Lanes {
 };
 
 // scores of all LC labels of one sample; acc[k] = score of label (lane%LW)+64k
-template <int LC>
+template <int LC, typename WT>
 __device__ __forceinline__ void sample_scores(const int32_t* __restrict__ fidx,
                                               const float* __restrict__ fval, int64_t beg,
-                                              int n, const float* W, int lane, float (&acc)[Lanes<LC>::K]) {
+                                              int n, const WT* W, int lane, float (&acc)[Lanes<LC>::K]) {
   using L = Lanes<LC>;
   const int g = lane / L::LW;
   const int l0 = lane % L::LW;
@@ -86,9 +150,9 @@ __device__ __forceinline__ void sample_scores(const int32_t* __restrict__ fidx,
     const int32_t idx = fidx[beg + j];
     const float x = fval[beg + j];
     if (idx >= 0) {
-      const float* wr = W + (int64_t)idx * LC + l0;
+      const WT* wr = W + (int64_t)idx * LC + l0;
 #pragma unroll
-      for (int k = 0; k < L::K; ++k) acc[k] += x * ld_agent(wr + 64 * k);
+      for (int k = 0; k < L::K; ++k) acc[k] += x * ldw(wr + 64 * k);
     }
   }
 #pragma unroll

@@ -71,6 +71,8 @@ struct JbTrainBatch {
   // mode kSerial: scratch of jb_serial_scratch_bytes(n) bytes (serial.hip)
   void* serial_scratch;
   int64_t serial_bytes;
+  // 1: W is a bf16 table (uint16 bit patterns; jb_linear_train_bf16)
+  int64_t w_bf16;
 };
 
 extern "C" int64_t jb_train_batch_args_bytes();

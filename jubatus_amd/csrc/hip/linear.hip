@@ -40,23 +40,24 @@
 namespace jb {
 
 // apply the update of one feature (lane-per-feature form)
-template <int LC, int MODE>
-__device__ __forceinline__ void apply_feature(float* W, float* P, int32_t idx, float x, int y,
+template <int LC, int MODE, typename WT>
+__device__ __forceinline__ void apply_feature(WT* W, float* P, int32_t idx, float x, int y,
                                               int lstar, bool use_s, int method, float tau,
-                                              float beta, float a, float b, float wy, float wl) {
+                                              float beta, float a, float b, float wy, float wl,
+                                              uint32_t rnd) {
   const int64_t row = (int64_t)idx * LC;
   const float dwy = use_s ? tau * a * x : tau * x;
   const float dwl = use_s ? -tau * b * x : -tau * x;
   if (MODE == kAtomic) {
-    atomicAdd(W + row + y, dwy);
-    if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+    addw(W + row + y, dwy, jb_mix32((uint32_t)(row + y), rnd));
+    if (lstar >= 0) addw(W + row + lstar, dwl, jb_mix32((uint32_t)(row + lstar), rnd));
     if (use_s) {
       atomicAdd(P + row + y, dprec(method, beta, x, a));
       if (lstar >= 0) atomicAdd(P + row + lstar, dprec(method, beta, x, b));
     }
   } else {
-    W[row + y] = wy + dwy;
-    if (lstar >= 0) W[row + lstar] = wl + dwl;
+    stw(W + row + y, wy + dwy, jb_mix32((uint32_t)(row + y), rnd));
+    if (lstar >= 0) stw(W + row + lstar, wl + dwl, jb_mix32((uint32_t)(row + lstar), rnd));
     if (use_s) {
       P[row + y] = 1.f / a + dprec(method, beta, x, a);
       if (lstar >= 0) P[row + lstar] = 1.f / b + dprec(method, beta, x, b);
@@ -71,10 +72,10 @@ __device__ __forceinline__ void apply_feature(float* W, float* P, int32_t idx, f
 // in every mode: a row repeated inside the sample then counts every time
 // (as in the reference's per-feature loop), and in exact mode (one stream)
 // nothing else touches the table, so the result is the same as plain stores.
-template <int LC, int MODE>
+template <int LC, int MODE, typename WT>
 __device__ __forceinline__ bool general_sample(const int32_t* __restrict__ fidx,
                                                const float* __restrict__ fval, int64_t beg, int n,
-                                               int y, float* W, float* P, const bool (&act)[Lanes<LC>::K],
+                                               int y, WT* W, float* P, const bool (&act)[Lanes<LC>::K],
                                                int lane, int method, float C,
                                                uint8_t* __restrict__ touched) {
   using L = Lanes<LC>;
@@ -124,18 +125,19 @@ __device__ __forceinline__ bool general_sample(const int32_t* __restrict__ fidx,
     const int64_t row = (int64_t)idx * LC;
     const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
     const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
-    apply_feature<LC, kAtomic>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, 0.f, 0.f);
+    apply_feature<LC, kAtomic>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, 0.f, 0.f,
+                               (uint32_t)beg);
     if (touched != nullptr) touched[idx] = 1;
   }
   return true;
 }
 
 // Label capacities above 64: every sample on the direct path.
-template <int LC, int MODE>
+template <int LC, int MODE, typename WT>
 __global__ __launch_bounds__(256) void linear_train_wide_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
-    const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
+    const int64_t* __restrict__ stream_ptr, int nstreams, WT* W, float* P,
     const int32_t* __restrict__ active, int method, float C,
     unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched) {
   using L = Lanes<LC>;
@@ -151,7 +153,7 @@ __global__ __launch_bounds__(256) void linear_train_wide_kernel(
     if (y < 0 || y >= LC) continue;
     ++n_valid;
     const int64_t beg = row_ptr[s];
-    if (general_sample<LC, MODE>(fidx, fval, beg, (int)(row_ptr[s + 1] - beg), y, W, P, act, lane,
+    if (general_sample<LC, MODE, WT>(fidx, fval, beg, (int)(row_ptr[s + 1] - beg), y, W, P, act, lane,
                                  method, C, touched))
       ++n_upd;
     if (MODE == kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -340,8 +342,8 @@ __device__ __forceinline__ float readlane_f(float v, int i) {
 // slots read row 0) and nothing reads the results here, so the whole gather
 // is U (or 2U) loads in flight; ``vmask`` bit u marks the valid slots for the
 // commit.
-template <int LC>
-__device__ __forceinline__ uint32_t gather_issue(const float* W, const float* P, bool use_s,
+template <int LC, typename WT>
+__device__ __forceinline__ uint32_t gather_issue(const WT* W, const float* P, bool use_s,
                                                  const int32_t* sI, int n, int g, int l0,
                                                  float (&gw)[Pipe<LC>::U],
                                                  float (&gp)[Pipe<LC>::U]) {
@@ -359,13 +361,13 @@ __device__ __forceinline__ uint32_t gather_issue(const float* W, const float* P,
   if (use_s) {
 #pragma unroll
     for (int u = 0; u < Q::U; ++u) {
-      gw[u] = ld_agent(W + rows[u]);
+      gw[u] = ldw(W + rows[u]);
       gp[u] = ld_agent(P + rows[u]);
     }
   } else {
 #pragma unroll
     for (int u = 0; u < Q::U; ++u) {
-      gw[u] = ld_agent(W + rows[u]);
+      gw[u] = ldw(W + rows[u]);
       gp[u] = 1.f;
     }
   }
@@ -430,11 +432,11 @@ __device__ __forceinline__ void group_argmax(float& best, int& bl, int lane) {
   if (LC >= 64) step(partner32_f(best, lane), partner32_i(bl, lane));
 }
 
-template <int LC, int MODE, bool HOT, int NW>
+template <int LC, int MODE, bool HOT, int NW, typename WT>
 __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
-    const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
+    const int64_t* __restrict__ stream_ptr, int nstreams, WT* W, float* P,
     const int32_t* __restrict__ active, int method, float C, const int32_t* __restrict__ hot_rows,
     const int32_t* __restrict__ hot_n, float* __restrict__ hot_rep, int merge_every,
     unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched) {
@@ -484,7 +486,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
         float S = 0.f;                  // shards of blocks that ran before this one
 #pragma unroll
         for (int r = 0; r < kRep; ++r) S += ld_agent(hot_rep + (int64_t)(r * 2 + t) * HE + e);
-        hV[t][e] = ld_agent((t == 0 ? W : P) + a) + S;
+        hV[t][e] = (t == 0 ? ldw(W + a) : ld_agent(P + a)) + S;
         hB[t][e] = S;
         hA[t][e] = 0.f;
         if (t == 1) hD[e] = 0.f;
@@ -533,7 +535,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
   uint32_t vmask = 0;
   bool staged = n_s <= F;
   if (staged) {
-    vmask = gather_issue<LC>(W, P, use_s, sI[wv][0], n_s, g, l0, gw, gp);
+    vmask = gather_issue<LC, WT>(W, P, use_s, sI[wv][0], n_s, g, l0, gw, gp);
     gather_commit<LC>(sW[wv][0], sP[wv][0], use_s, n_s, g, l0, vmask, gw, gp);
   }
   int since_merge = 0;
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     const bool pipe1 = s + 1 < s_end && n1 <= F;
     const bool early = pipe1 && !general_s;
     // 1. the gather of s+1 goes in flight first
-    if (early) vmask = gather_issue<LC>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
+    if (early) vmask = gather_issue<LC, WT>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
     // 2. feature descriptors of s+2
     int n2 = 0, y2 = -1;
     int32_t idx2 = -1;
@@ -587,7 +589,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     if (general_s) {
       const int i = (int)(s - wb);
       const int64_t b0 = readlane64(rp, i);
-      upd = general_sample<LC, MODE>(fidx, fval, b0, (int)(readlane64(rp, i + 1) - b0), y_s, W, P,
+      upd = general_sample<LC, MODE, WT>(fidx, fval, b0, (int)(readlane64(rp, i + 1) - b0), y_s, W, P,
                                      act, lane, method, C, touched);
       if (upd) ++n_upd;
       upd = false;        // applied already
@@ -769,16 +771,18 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
         }
       } else {
         const int64_t row = (int64_t)idx_s * LC;
+        const uint32_t ry = jb_mix32((uint32_t)(row + y_s), (uint32_t)s);
+        const uint32_t rl = jb_mix32((uint32_t)(row + lstar), (uint32_t)s);
         if (MODE == kAtomic) {
-          atomicAdd(W + row + y_s, dwy);
-          if (lstar >= 0) atomicAdd(W + row + lstar, dwl);
+          addw(W + row + y_s, dwy, ry);
+          if (lstar >= 0) addw(W + row + lstar, dwl, rl);
           if (use_s && !p_done) {
             atomicAdd(P + row + y_s, dpy);
             if (lstar >= 0) atomicAdd(P + row + lstar, dpl);
           }
         } else {
-          W[row + y_s] = wy + dwy;
-          if (lstar >= 0) W[row + lstar] = wl + dwl;
+          stw(W + row + y_s, wy + dwy, ry);
+          if (lstar >= 0) stw(W + row + lstar, wl + dwl, rl);
           if (use_s) {
             P[row + y_s] = py + dpy;
             if (lstar >= 0) P[row + lstar] = pl + dpl;
@@ -791,7 +795,7 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
     // 6. s+1 not prefetched (s took the direct path): stage it now that s landed
     if (pipe1 && !early) {
       if (MODE != kExact) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      vmask = gather_issue<LC>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
+      vmask = gather_issue<LC, WT>(W, P, use_s, sI[wv][c1], n1, g, l0, gw, gp);
       gather_commit<LC>(sW[wv][c1], sP[wv][c1], use_s, n1, g, l0, vmask, gw, gp);
     }
     // slot c is free again: it receives the features of s+2
@@ -820,10 +824,10 @@ __global__ __launch_bounds__(64 * NW) void linear_train_pipe_kernel(
   }
 }
 
-template <int LC>
+template <int LC, typename WT>
 __global__ __launch_bounds__(256) void linear_classify_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
-    const float* __restrict__ fval, int n_samples, const float* W, float* __restrict__ out) {
+    const float* __restrict__ fval, int n_samples, const WT* W, float* __restrict__ out) {
   using L = Lanes<LC>;
   const int lane = threadIdx.x & 63;
   const int s = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -893,6 +897,125 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
 // times a sequential sample; see serial.hip)
 constexpr int kSerialBail = 128;
 
+namespace jb {
+
+// one stream spanning a whole batch: sp[0] .. sp[nstreams] (the streams are
+// contiguous in request order, so this is the batch applied serially)
+__global__ void stream_span_kernel(const int64_t* __restrict__ sp, int nstreams,
+                                   int64_t* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    out[0] = sp[0];
+    out[1] = sp[nstreams];
+  }
+}
+
+template <typename WT, int L, int M>
+void launch_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                  const int32_t* labels, const int64_t* stream_ptr, int nstreams, WT* W, float* S,
+                  const int32_t* active, int method, float C, bool hot, int hot_nw,
+                  const int32_t* hot_rows, const int32_t* hot_n, float* hot_rep, int merge_every,
+                  unsigned long long* stats, uint8_t* touched, hipStream_t stream) {
+  const int threads = 256;
+  const int blocks = (nstreams * 64 + threads - 1) / threads;
+  const int hblocks = (nstreams + hot_nw - 1) / hot_nw;
+#define JB_PIPE(H, NWV, B)                                                                      \
+  hipLaunchKernelGGL((linear_train_pipe_kernel<L, M, H, NWV, WT>), dim3(B), dim3(64 * NWV), 0,  \
+                     stream, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active,   \
+                     method, C, hot_rows, hot_n, hot_rep, merge_every, stats, touched);
+  if constexpr (L <= 64) {
+    // the hot-row replica (concurrent modes) keeps fp32 rows in LDS and folds
+    // them into an fp32 table; bf16 tables train without it
+    if constexpr (M != kExact && sizeof(WT) == 4) {
+      if (hot) {
+        if constexpr (L <= 16) {
+          if (hot_nw == 16) { JB_PIPE(true, 16, hblocks) return; }
+        }
+        if (hot_nw == 4) { JB_PIPE(true, 4, hblocks) }
+        else { JB_PIPE(true, 8, hblocks) }
+        return;
+      }
+    }
+    JB_PIPE(false, 4, blocks)
+  } else {
+    hipLaunchKernelGGL((linear_train_wide_kernel<L, M, WT>), dim3(blocks), dim3(threads), 0, stream,
+                       row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active, method, C,
+                       stats, touched);
+  }
+#undef JB_PIPE
+}
+
+template <typename WT, int L>
+void launch_train_mode(int mode, const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                       const int32_t* labels, const int64_t* stream_ptr, int nstreams, WT* W,
+                       float* S, const int32_t* active, int method, float C, bool hot, int hot_nw,
+                       const int32_t* hot_rows, const int32_t* hot_n, float* hot_rep,
+                       int merge_every, unsigned long long* stats, uint8_t* touched,
+                       hipStream_t stream) {
+#define JB_ARGS row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active, method, C, hot, \
+                hot_nw, hot_rows, hot_n, hot_rep, merge_every, stats, touched, stream
+  if (mode == kAtomic) launch_train<WT, L, kAtomic>(JB_ARGS);
+  else if (mode == kHogwild) launch_train<WT, L, kHogwild>(JB_ARGS);
+  else launch_train<WT, L, kExact>(JB_ARGS);
+#undef JB_ARGS
+}
+
+}  // namespace jb
+
+// kSerial over a bf16 table: the committer of serial.hip works on fp32
+// tables, so the batch runs as one sequential stream (the same serial result)
+template <typename WT>
+static int linear_train_impl(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                             const int32_t* labels, const int64_t* stream_ptr, int nstreams,
+                             WT* W, float* S, const int32_t* active, int LC, int method, float C,
+                             int mode, const int32_t* hot_rows, const int32_t* hot_n,
+                             float* hot_rep, int merge_every, int hot_waves,
+                             unsigned long long* stats, uint8_t* touched, int64_t n_max,
+                             void* scratch, int64_t scratch_bytes, hipStream_t stream) {
+  if (nstreams <= 0) return 0;
+  if (mode == jb::kSerial && nstreams == 1) mode = jb::kExact;
+  if (mode == jb::kExact && nstreams > 1) mode = jb::kSerial;   // exact means serial-equivalent
+  if (mode == jb::kSerial) {
+    if constexpr (sizeof(WT) == 4) {
+      // score + ordered commit, then the sequential kernel over what is left
+      const int rc = jb_serial_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max,
+                                       W, S, active, LC, method, C, stats, touched, scratch,
+                                       scratch_bytes, kSerialBail, stream);
+      if (rc != 0) return rc;
+    } else {
+      if (scratch == nullptr || scratch_bytes < 16) return -3;
+      hipLaunchKernelGGL(jb::stream_span_kernel, dim3(1), dim3(64), 0, stream, stream_ptr,
+                         nstreams, (int64_t*)scratch);
+    }
+    stream_ptr = (const int64_t*)scratch;
+    nstreams = 1;
+    mode = jb::kExact;
+    hot_rows = nullptr;
+  }
+  const bool hot = sizeof(WT) == 4 && hot_rows != nullptr && hot_n != nullptr &&
+                   hot_rep != nullptr && mode != jb::kExact && LC <= 64;
+  if (merge_every < 1) merge_every = 1;
+  // hot launches: 8 streams per block (half the blocks exchanging hot-row
+  // progress through the shards; see "Hot rows")
+  const int hot_nw = (hot_waves == 16 && LC <= 16) ? 16 : (hot_waves == 4 ? 4 : 8);
+#define JB_TRAIN(L)                                                                             \
+  jb::launch_train_mode<WT, L>(mode, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,   \
+                               active, method, C, hot, hot_nw, hot_rows, hot_n, hot_rep,        \
+                               merge_every, stats, touched, stream);
+  JB_LC_DISPATCH(LC, JB_TRAIN)
+#undef JB_TRAIN
+  if constexpr (sizeof(WT) == 4) {
+    if (hot) {
+#define JB_FOLD(L)                                                                            \
+  hipLaunchKernelGGL((jb::hot_fold_kernel<(L <= 64 ? L : 64)>), dim3(2 * jb::Hot<64>::E / 256), \
+                     dim3(256), 0, stream, W, S, method >= jb::CW ? 1 : 0, hot_rows, hot_n,     \
+                     hot_rep, touched);
+      JB_LC_DISPATCH(LC, JB_FOLD)
+#undef JB_FOLD
+    }
+  }
+  return (int)hipGetLastError();
+}
+
 extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                float* W, float* S, const int32_t* active, int LC, int method,
@@ -900,79 +1023,51 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
                                float* hot_rep, int merge_every, int hot_waves,
                                unsigned long long* stats, uint8_t* touched, int64_t n_max,
                                void* scratch, int64_t scratch_bytes, hipStream_t stream) {
-  if (nstreams <= 0) return 0;
-  if (mode == jb::kSerial && nstreams == 1) mode = jb::kExact;
-  if (mode == jb::kExact && nstreams > 1) mode = jb::kSerial;   // exact means serial-equivalent
-  if (mode == jb::kSerial) {
-    // score + ordered commit, then the sequential kernel over what is left
-    const int rc = jb_serial_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W,
-                                     S, active, LC, method, C, stats, touched, scratch,
-                                     scratch_bytes, kSerialBail, stream);
-    if (rc != 0) return rc;
-    stream_ptr = (const int64_t*)scratch;
-    nstreams = 1;
-    mode = jb::kExact;
-    hot_rows = nullptr;
-  }
-  const int threads = 256;
-  const int blocks = (nstreams * 64 + threads - 1) / threads;
-  const bool hot = hot_rows != nullptr && hot_n != nullptr && hot_rep != nullptr &&
-                   mode != jb::kExact && LC <= 64;
-  if (merge_every < 1) merge_every = 1;
-  // hot launches: 8 streams per block (half the blocks exchanging hot-row
-  // progress through the shards; see "Hot rows")
-  const int hot_nw = (hot_waves == 16 && LC <= 16) ? 16 : (hot_waves == 4 ? 4 : 8);
-  const int hblocks = (nstreams + hot_nw - 1) / hot_nw;
-#define JB_PIPE(L, M, H, NWV, B)                                                                 \
-  hipLaunchKernelGGL((jb::linear_train_pipe_kernel<(L <= 64 ? L : 64), M, H, NWV>), dim3(B),      \
-                     dim3(64 * NWV), 0, stream, row_ptr, fidx, fval, labels, stream_ptr,          \
-                     nstreams, W, S, active, method, C, hot_rows, hot_n, hot_rep, merge_every,    \
-                     stats, touched);
-#define JB_TRAIN_M(L, M)                                                                      \
-  if (L <= 64) {                                                                              \
-    if (hot && M != jb::kExact) {                                                             \
-      if (hot_nw == 16 && L <= 16) { JB_PIPE(L, M, true, (L <= 16 ? 16 : 8), hblocks) }      \
-      else if (hot_nw == 4) { JB_PIPE(L, M, true, 4, hblocks) }                               \
-      else { JB_PIPE(L, M, true, 8, hblocks) }                                                \
-    } else { JB_PIPE(L, M, false, 4, blocks) }                                                \
-  } else                                                                                      \
-    hipLaunchKernelGGL((jb::linear_train_wide_kernel<L, M>), dim3(blocks), dim3(threads), 0,  \
-                       stream, row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,       \
-                       active, method, C, stats, touched);
-#define JB_TRAIN(L)                                        \
-  if (mode == jb::kAtomic) { JB_TRAIN_M(L, jb::kAtomic) }  \
-  else if (mode == jb::kHogwild) { JB_TRAIN_M(L, jb::kHogwild) } \
-  else { JB_TRAIN_M(L, jb::kExact) }
-  JB_LC_DISPATCH(LC, JB_TRAIN)
-#undef JB_TRAIN
-#undef JB_TRAIN_M
-#undef JB_PIPE
-  if (hot) {
-#define JB_FOLD(L)                                                                            \
-  hipLaunchKernelGGL((jb::hot_fold_kernel<(L <= 64 ? L : 64)>), dim3(2 * jb::Hot<64>::E / 256), \
-                     dim3(256), 0, stream, W, S, method >= jb::CW ? 1 : 0, hot_rows, hot_n,     \
-                     hot_rep, touched);
-    JB_LC_DISPATCH(LC, JB_FOLD)
-#undef JB_FOLD
-  }
-  return (int)hipGetLastError();
+  return linear_train_impl<float>(row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S, active,
+                                  LC, method, C, mode, hot_rows, hot_n, hot_rep, merge_every,
+                                  hot_waves, stats, touched, n_max, scratch, scratch_bytes, stream);
+}
+
+// the same over a bf16 W table (fp32 S); hot-row arguments are ignored
+extern "C" int jb_linear_train_bf16(const int64_t* row_ptr, const int32_t* fidx,
+                                    const float* fval, const int32_t* labels,
+                                    const int64_t* stream_ptr, int nstreams, jb::bf16_t* W,
+                                    float* S, const int32_t* active, int LC, int method, float C,
+                                    int mode, unsigned long long* stats, uint8_t* touched,
+                                    void* scratch, int64_t scratch_bytes, hipStream_t stream) {
+  return linear_train_impl<jb::bf16_t>(row_ptr, fidx, fval, labels, stream_ptr, nstreams, W, S,
+                                       active, LC, method, C, mode, nullptr, nullptr, nullptr, 1,
+                                       8, stats, touched, 0, scratch, scratch_bytes, stream);
 }
 
 // bytes of the hot-row delta shards (float [kRep][2][E]); zero on first use
 extern "C" int64_t jb_hot_rep_bytes() { return (int64_t)jb::kRep * 2 * jb::Hot<8>::E * 4; }
 
-extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
-                                  int n_samples, const float* W, int LC, float* out,
-                                  hipStream_t stream) {
+template <typename WT>
+static int linear_classify_impl(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                int n_samples, const WT* W, int LC, float* out,
+                                hipStream_t stream) {
   if (n_samples <= 0) return 0;
   const int threads = 256;
   const int blocks = (n_samples * 64 + threads - 1) / threads;
-#define JB_CLS(L)                                                                       \
-  hipLaunchKernelGGL((jb::linear_classify_kernel<L>), dim3(blocks), dim3(threads), 0, \
+#define JB_CLS(L)                                                                           \
+  hipLaunchKernelGGL((jb::linear_classify_kernel<L, WT>), dim3(blocks), dim3(threads), 0, \
                      stream, row_ptr, fidx, fval, n_samples, W, out);
   JB_LC_DISPATCH(LC, JB_CLS)
 #undef JB_CLS
   return (int)hipGetLastError();
+}
+
+extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                  int n_samples, const float* W, int LC, float* out,
+                                  hipStream_t stream) {
+  return linear_classify_impl<float>(row_ptr, fidx, fval, n_samples, W, LC, out, stream);
+}
+
+extern "C" int jb_linear_classify_bf16(const int64_t* row_ptr, const int32_t* fidx,
+                                       const float* fval, int n_samples, const jb::bf16_t* W,
+                                       int LC, float* out, hipStream_t stream) {
+  return linear_classify_impl<jb::bf16_t>(row_ptr, fidx, fval, n_samples, W, LC, out, stream);
 }
 
 extern "C" int jb_scale(float* p, int64_t n, float a, hipStream_t stream) {

@@ -931,18 +931,47 @@ static int sample_j(int64_t nrows, int k) {
 
 // + the radix-select histograms of the score path: 2 levels x nq x 4096
 constexpr int kRadixBins = 4096;
+// the one-launch score top-k keeps per-query histograms and counters that
+// must be zero when it starts (it leaves them zero when it ends): a fixed
+// region after the candidates of 8 queries, out of reach of the tile path's
+// block candidates (<= 8 x 256 x 128 entries)
+constexpr int64_t kFuseStateOff = 64 + 8 * (int64_t)kCandCap;
+constexpr int64_t kFuseStateWords = 2 * 8 * (int64_t)kRadixBins + 8 * 4;
 extern "C" int64_t jb_topk_direct_scratch(int nq) {
-  return 64 + (int64_t)nq * kCandCap + 2 * (int64_t)nq * kRadixBins;
+  (void)nq;
+  return kFuseStateOff + kFuseStateWords;
 }
 
+// zero the score top-k's state region of a scratch allocation (once, after
+// allocating it; scratch_i as passed to jb_topk_scores_direct)
+extern "C" int jb_topk_scratch_init(int32_t* scratch_i, hipStream_t stream) {
+  hipError_t e = hipMemsetAsync(scratch_i + kFuseStateOff, 0, sizeof(int32_t) * kFuseStateWords,
+                                stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);   // done before any stream uses it
+  return (int)e;
+}
+
+template <int MODE>
+static int topk_fused_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k,
+                             float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                             int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                             hipStream_t stream);
+
+// path: -1 default (one launch from 16384 rows up to the sampled path's
+// 2M), 0 tile, 2 one launch
 static int topk_to_host_any(const uint64_t* qbits, const float* qnorm, int nq,
                             const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
                             int64_t nrows, int words, int hash_num, int metric, int k,
                             float* scratch_d, int32_t* scratch_i, float* out_d_host,
                             int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
-                            hipStream_t stream) {
+                            hipStream_t stream, int path = -1) {
   const int j = sample_j(nrows, k);
-  if (j == 0)
+  if (path == 2 || (path < 0 && j == 0 && nrows >= 16384)) {
+    jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
+    return topk_fused_launch<0>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
+                                done_host, seq, stream);
+  }
+  if (j == 0 || path == 0)
     return topk_to_host_tile(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num,
                              metric, k, scratch_d, scratch_i, out_d_host, out_i_host, done_host,
                              seq, stream);
@@ -969,11 +998,12 @@ static int topk_direct_run(const uint64_t* qbits, const float* qnorm, int nq,
                            const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
                            int64_t nrows, int words, int hash_num, int metric, int k,
                            float* scratch_d, int32_t* scratch_i, float* out_d_host,
-                           int32_t* out_i_host, uint32_t* done_host, hipStream_t stream) {
+                           int32_t* out_i_host, uint32_t* done_host, hipStream_t stream,
+                           int path = -1) {
   uint32_t seq = jb::next_seq();
   int rc = topk_to_host_any(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric,
                             k, scratch_d, scratch_i, out_d_host, out_i_host, done_host, seq,
-                            stream);
+                            stream, path);
   if (rc != 0) return rc;
   bool retry = false;
   rc = jb::wait_flags_status(done_host, nq, seq, jb::kTopRetry, stream, &retry);
@@ -996,6 +1026,21 @@ extern "C" int jb_topk_direct_query(const uint64_t* qbits, const float* qnorm, i
   if (k > jb::kTopMaxK || words > jb::kTopMaxWords || nq > 8) return -2;
   return topk_direct_run(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, k,
                          scratch_d, scratch_i, out_d_host, out_i_host, done_host, stream);
+}
+
+// as jb_topk_direct_query with the path forced (A/B in tools/bench_topk_lsh.py):
+// -1 default, 0 tile, 2 one launch
+extern "C" int jb_topk_direct_query_path(const uint64_t* qbits, const float* qnorm, int nq,
+                                         const uint64_t* tbits, const float* tnorm,
+                                         const uint8_t* valid, int64_t nrows, int words,
+                                         int hash_num, int metric, int k, float* scratch_d,
+                                         int32_t* scratch_i, float* out_d_host,
+                                         int32_t* out_i_host, uint32_t* done_host, int path,
+                                         hipStream_t stream) {
+  if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
+  if (k > jb::kTopMaxK || words > jb::kTopMaxWords || nq > 8) return -2;
+  return topk_direct_run(qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, k,
+                         scratch_d, scratch_i, out_d_host, out_i_host, done_host, stream, path);
 }
 
 // Score-vector latency path (mode 1: [nq][nrows] similarity / distance from
@@ -1217,11 +1262,328 @@ __global__ __launch_bounds__(1024) void topk_rank_final_kernel(
 
 }  // namespace jb
 
-static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, bool radix,
+namespace jb {
+
+// ---------------------------------------------------------------------------
+// Exact top-k as ONE launch, for a score vector (MODE 1: the inverted-index
+// scan's output) or straight off the signature table (MODE 0: lsh /
+// minhash / euclid_lsh distances computed in place). Replaces chains of
+// dependent launches (score path: hist / select / hist / select / collect /
+// final plus a histogram memset; signature path: per-block tile top-k, then
+// a merge of blocks x k candidates) whose gaps and serial merges dominated a
+// ~1M-row query. A grid of B blocks per query, at most as many blocks as are
+// co-resident (kFuseThreads threads, 48 KB of LDS each), every block owning a
+// contiguous range of rows:
+//   A  distances of its rows (kept in LDS for the first kFuseCache rows),
+//      level-1 histogram of the top 12 key bits -> global h1
+//   -- grid barrier (per query: arrival counter, agent-scope atomics) --
+//   B  every block reads h1 and finds the bucket of the k-th smallest
+//      (redundantly: no extra barrier), level-2 histogram of its rows in that
+//      bucket -> global h2
+//   -- grid barrier --
+//   C  threshold T from h2, rows with key <= T appended to the candidates;
+//      the last block to finish (finished-block counter) ranks the
+//      candidates, writes the k results into pinned host memory, publishes
+//      the flag and zeroes the query's histograms and counters for the next
+//      launch (so no memset precedes it)
+// HBM is read once for up to B x kFuseCache rows; passes B and C read LDS.
+// Ties are broken by the lower row index (lt_pair), like the tile path.
+constexpr int kFuseThreads = 256;
+constexpr int kFuseMaxBlocks = 256;
+constexpr int kFuseSync = 4;            // per query: arrivals, candidates, finished, pad
+constexpr int kFuseCache = 8192;        // distances kept in LDS per block
+
+__device__ __forceinline__ uint32_t ld_agent_u32(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// every block of the query arrives; returns once `target` blocks did
+__device__ __forceinline__ void fused_barrier(uint32_t* arrive, uint32_t target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();                                   // release this block's atomics / stores
+    atomicAdd(arrive, 1u);
+    while (ld_agent_u32(arrive) < target) __builtin_amdgcn_s_sleep(1);
+    __threadfence();                                   // acquire
+  }
+  __syncthreads();
+}
+
+// bucket of the need-th smallest in a 4096-bin global histogram: out[0] bin
+// (0xffffffff: fewer than `need` entries), out[1] entries below it
+__device__ __forceinline__ void fused_select(const uint32_t* g, uint32_t need, uint32_t* part,
+                                             uint32_t* out) {
+  const int t = threadIdx.x;
+  constexpr int P = kRadixBins / kFuseThreads;       // 16 bins per thread
+  uint32_t c[P];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < P; ++j) { c[j] = ld_agent_u32(g + P * t + j); sum += c[j]; }
+  part[t] = sum;
+  if (t == 0) out[0] = 0xffffffffu;
+  __syncthreads();
+  for (int o = 1; o < kFuseThreads; o <<= 1) {
+    const uint32_t x = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+#pragma unroll
+  for (int j = 0; j < P; ++j) {
+    if (run < need && run + c[j] >= need) { out[0] = P * t + j; out[1] = run; }
+    run += c[j];
+  }
+  __syncthreads();
+}
+
+// histogram of a wave's 64 keys into LDS: most rows of a score vector (and
+// many of a hamming scan) share one bin, so the wave's first active lane
+// adds the count of its bin and the others their own
+__device__ __forceinline__ void fused_bin(uint32_t* h, bool act, uint32_t bin, int lane) {
+  const uint64_t am = __ballot(act);
+  if (am == 0) return;
+  const int leader = __ffsll((unsigned long long)am) - 1;
+  const uint32_t b0 = __shfl(bin, leader, 64);
+  const uint64_t same = __ballot(act && bin == b0);
+  if (lane == leader) atomicAdd(&h[b0], (uint32_t)__popcll(same));
+  else if (act && bin != b0) atomicAdd(&h[bin], 1u);
+}
+
+// the distance of row r (MODE as load_item; r < n)
+template <int MODE>
+__device__ __forceinline__ float fused_dist(const TopkSrc& s, int q, int64_t n, int64_t r,
+                                            const uint64_t* qb, float qn) {
+  float d;
+  int id;
+  load_item<MODE>(s, q, n, r, qb, qn, d, id);
+  return d;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kFuseThreads) void topk_fused_kernel(
+    const TopkSrc s, int64_t n, int k, uint32_t* __restrict__ h1, uint32_t* __restrict__ h2,
+    uint32_t* __restrict__ sync, float* __restrict__ cand_d, int32_t* __restrict__ cand_i,
+    int cap, float* __restrict__ out_d, int32_t* __restrict__ out_i, volatile uint32_t* done,
+    uint32_t seq) {
+  __shared__ uint32_t h[kRadixBins];
+  __shared__ float s_cache[kFuseCache];                // pass A distances; later the final's lists
+  __shared__ uint64_t s_q[kTopMaxWords];
+  __shared__ uint32_t sel[4];
+  __shared__ int s_last;
+  float* s_d = s_cache;                                // final stage: kRankMax candidates
+  int32_t* s_i = reinterpret_cast<int32_t*>(s_cache + kRankMax);
+  const int q = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63;
+  const uint32_t B = gridDim.x;
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += kFuseThreads) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  uint32_t* g1 = h1 + (int64_t)q * kRadixBins;
+  uint32_t* g2 = h2 + (int64_t)q * kRadixBins;
+  uint32_t* qs = sync + (int64_t)q * kFuseSync;
+  const int64_t per = ((n + B - 1) / B + 1023) & ~(int64_t)1023;
+  const int64_t beg = min(n, (int64_t)blockIdx.x * per);
+  const int64_t end = min(n, beg + per);
+  const int64_t cend = min(end, beg + kFuseCache);    // rows [beg, cend) cached in LDS
+  // A: distances (4 rows in flight per thread), level-1 histogram
+  for (int i = t; i < kRadixBins; i += kFuseThreads) h[i] = 0;
+  __syncthreads();
+  for (int64_t b = beg + t; b < end; b += 4 * kFuseThreads) {
+    float d[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = b + u * kFuseThreads;
+      d[u] = fused_dist<MODE>(s, q, n, r < end ? r : end - 1, qb, qn);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = b + u * kFuseThreads;
+      if (r < cend) s_cache[r - beg] = d[u];
+      fused_bin(h, r < end && d[u] < INFINITY, dist_key(d[u]) >> 20, lane);
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < kRadixBins; i += kFuseThreads)
+    if (h[i]) atomicAdd(&g1[i], h[i]);
+  fused_barrier(qs, B);
+  // the distance of row r in passes B and C: LDS for the cached rows
+  auto dist_of = [&](int64_t r) -> float {
+    return r < cend ? s_cache[r - beg] : fused_dist<MODE>(s, q, n, r, qb, qn);
+  };
+  // B
+  fused_select(g1, (uint32_t)k, h, sel);               // h doubles as the scan buffer
+  const uint32_t b1 = sel[0];
+  const uint32_t below = sel[1];
+  float T = INFINITY;                                 // fewer finite rows than k: take them all
+  if (b1 != 0xffffffffu) {
+    for (int i = t; i < kRadixBins; i += kFuseThreads) h[i] = 0;
+    __syncthreads();
+    for (int64_t r = beg + t; r < end; r += kFuseThreads) {
+      const float d = dist_of(r);
+      const uint32_t key = dist_key(d);
+      fused_bin(h, d < INFINITY && (key >> 20) == b1, (key >> 8) & 0xfff, lane);
+    }
+    __syncthreads();
+    for (int i = t; i < kRadixBins; i += kFuseThreads)
+      if (h[i]) atomicAdd(&g2[i], h[i]);
+    fused_barrier(qs, 2 * B);
+    fused_select(g2, (uint32_t)k - below, h, sel);
+    T = key_dist((b1 << 20) | (sel[0] << 8) | 0xffu);
+  }
+  // C: candidates <= T
+  for (int64_t r0 = beg; r0 < end; r0 += kFuseThreads) {
+    const int64_t r = r0 + t;
+    const float d = r < end ? dist_of(r) : INFINITY;
+    const bool pass = d <= T && d < INFINITY;
+    const uint64_t m = __ballot(pass);
+    if (m == 0) continue;
+    int base = 0;
+    if (lane == 0) base = atomicAdd((int*)&qs[1], __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (pass) {
+      const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+      if (pos < cap) {
+        cand_d[(int64_t)q * cap + pos] = d;
+        cand_i[(int64_t)q * cap + pos] = (int32_t)r;
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    s_last = atomicAdd(&qs[2], 1u) == B - 1;
+    __threadfence();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last block of the query: exact top-k of the candidates
+  // k <= kListK reads the candidates from L2 (any count up to cap: heavy
+  // ties at the threshold, e.g. quantized hamming distances); larger k
+  // ranks them in LDS (at most kRankMax)
+  const int c_all = (int)ld_agent_u32(&qs[1]);
+  const bool over = c_all > cap || (k > kListK && c_all > kRankMax);
+  const int nc = over ? 0 : c_all;
+  float* od = out_d + (int64_t)q * k;
+  int32_t* oi = out_i + (int64_t)q * k;
+  const float* gcd = cand_d + (int64_t)q * cap;
+  const int32_t* gci = cand_i + (int64_t)q * cap;
+  if (k > kListK) {
+    for (int j = t; j < nc; j += kFuseThreads) {
+      s_d[j] = __hip_atomic_load(gcd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_i[j] = __hip_atomic_load(gci + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  for (int j = nc + t; j < k; j += kFuseThreads) { od[j] = INFINITY; oi[j] = INT_MAX; }
+  __syncthreads();
+  if (k <= kListK) {
+    // per-thread sorted lists of the strided candidates, per-wave pops into
+    // LDS, wave 0 pops the 4 waves' lists
+    constexpr int NW = kFuseThreads / 64;
+    float ld[kListK];
+    int li[kListK];
+#pragma unroll
+    for (int j = 0; j < kListK; ++j) { ld[j] = INFINITY; li[j] = INT_MAX; }
+    for (int j = t; j < nc; j += kFuseThreads) {
+      const float v = __hip_atomic_load(gcd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int id = __hip_atomic_load(gci + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lt_pair(v, id, ld[kListK - 1], li[kListK - 1])) {
+#pragma unroll
+        for (int x = kListK - 1; x > 0; --x) {
+          const bool up = lt_pair(v, id, ld[x - 1], li[x - 1]);
+          const bool here = !up && lt_pair(v, id, ld[x], li[x]);
+          ld[x] = up ? ld[x - 1] : (here ? v : ld[x]);
+          li[x] = up ? li[x - 1] : (here ? id : li[x]);
+        }
+        if (lt_pair(v, id, ld[0], li[0])) { ld[0] = v; li[0] = id; }
+      }
+    }
+    const int wv = t >> 6;
+    wave_pop<kListK>(ld, li, k, &s_d[wv * k], &s_i[wv * k], lane);
+    __syncthreads();
+    if (wv == 0) {
+      float m[1];
+      int mi[1];
+      m[0] = lane < NW * k ? s_d[lane] : INFINITY;
+      mi[0] = lane < NW * k ? s_i[lane] : INT_MAX;
+      __builtin_amdgcn_wave_barrier();
+      wave_pop<1>(m, mi, k, od, oi, lane);
+    }
+  } else {
+    for (int j = t; j < nc; j += kFuseThreads) {
+      const float d = s_d[j];
+      const int32_t id = s_i[j];
+      int rank = 0;
+      for (int x = 0; x < nc; ++x) {
+        const float e = s_d[x];
+        rank += (e < d) || (e == d && s_i[x] < id);
+        if ((x & 63) == 63 && rank >= k) break;
+      }
+      if (rank < k) { od[rank] = d; oi[rank] = id; }
+    }
+  }
+  // state for the next launch
+  for (int i = t; i < kRadixBins; i += kFuseThreads) { g1[i] = 0u; g2[i] = 0u; }
+  if (t < kFuseSync) qs[t] = 0u;
+  __threadfence_system();
+  __syncthreads();
+  const bool retry = over || (c_all < k && T < INFINITY);
+  if (t == 0) done[q] = retry ? (seq | kTopRetry) : seq;
+}
+
+}  // namespace jb
+
+// blocks of one fused launch that are resident at once (all queries): the
+// grid barrier needs every block running; bounded by kFuseMaxBlocks
+static int fused_resident_blocks() {
+  static int cached = 0;
+  if (cached == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, jb::topk_fused_kernel<1>,
+                                                     jb::kFuseThreads, 0) != hipSuccess) {
+      cus = 64;
+      per_cu = 1;
+    }
+    int64_t r = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+    cached = (int)(r < jb::kFuseMaxBlocks ? r : jb::kFuseMaxBlocks);
+  }
+  return cached;
+}
+
+template <int MODE>
+static int topk_fused_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k,
+                             float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                             int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
+                             hipStream_t stream) {
+  uint32_t* st = (uint32_t*)(scratch_i + kFuseStateOff);
+  int64_t B = (nrows + 1023) / 1024;
+  const int64_t bmax = fused_resident_blocks() / nq;
+  if (B > bmax) B = bmax;
+  if (B < 1) B = 1;
+  hipLaunchKernelGGL(jb::topk_fused_kernel<MODE>, dim3((unsigned)B, nq), dim3(jb::kFuseThreads), 0,
+                     stream, s, nrows, k, st, st + 8 * kRadixBins, st + 16 * kRadixBins,
+                     scratch_d + 64, scratch_i + 64, kCandCap, out_d_host, out_i_host,
+                     (volatile uint32_t*)done_host, seq);
+  return (int)hipGetLastError();
+}
+
+// path: 0 tile scan + merge, 1 radix chain (6 launches + memset), 2 one launch
+static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, int path,
                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
                               hipStream_t stream) {
-  if (!radix) {
+  if (path == 2)
+    return topk_fused_launch<1>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
+                                done_host, seq, stream);
+  if (path == 0) {
     const int blocks = jb_topk_blocks(nrows, k);
     const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
     const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
@@ -1268,24 +1630,34 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   return (int)hipGetLastError();
 }
 
-extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64_t nrows, int k,
-                                     float* scratch_d, int32_t* scratch_i, float* out_d_host,
-                                     int32_t* out_i_host, uint32_t* done_host,
-                                     hipStream_t stream) {
+// path_sel: -1 default (one launch from 16384 rows), 0 tile, 1 radix chain,
+// 2 one launch (A/B in tools/bench_topk_scores.py)
+extern "C" int jb_topk_scores_direct_path(const float* src_d, int flip, int nq, int64_t nrows,
+                                          int k, float* scratch_d, int32_t* scratch_i,
+                                          float* out_d_host, int32_t* out_i_host,
+                                          uint32_t* done_host, int path_sel, hipStream_t stream) {
   if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
   if (k > jb::kTopMaxK || nq > 8) return -2;
   jb::TopkSrc s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, src_d, nullptr, flip};
-  const bool radix = nrows >= 16384;
+  const int path = nrows >= 16384 ? (path_sel < 0 ? 2 : path_sel) : 0;
   uint32_t seq = jb::next_seq();
-  int rc = topk_scores_launch(s, nq, nrows, k, radix, scratch_d, scratch_i, out_d_host,
+  int rc = topk_scores_launch(s, nq, nrows, k, path, scratch_d, scratch_i, out_d_host,
                               out_i_host, done_host, seq, stream);
   if (rc != 0) return rc;
   bool retry = false;
   rc = jb::wait_flags_status(done_host, nq, seq, jb::kTopRetry, stream, &retry);
   if (rc != 0 || !retry) return rc;
   seq = jb::next_seq();
-  rc = topk_scores_launch(s, nq, nrows, k, false, scratch_d, scratch_i, out_d_host, out_i_host,
+  rc = topk_scores_launch(s, nq, nrows, k, 0, scratch_d, scratch_i, out_d_host, out_i_host,
                           done_host, seq, stream);
   if (rc != 0) return rc;
   return jb::wait_flags(done_host, nq, seq, stream);
+}
+
+extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64_t nrows, int k,
+                                     float* scratch_d, int32_t* scratch_i, float* out_d_host,
+                                     int32_t* out_i_host, uint32_t* done_host,
+                                     hipStream_t stream) {
+  return jb_topk_scores_direct_path(src_d, flip, nq, nrows, k, scratch_d, scratch_i, out_d_host,
+                                    out_i_host, done_host, -1, stream);
 }

@@ -41,6 +41,12 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
                                float* hot_rep, int merge_every, int hot_waves,
                                unsigned long long* stats, uint8_t* touched, int64_t n_max,
                                void* scratch, int64_t scratch_bytes, hipStream_t stream);
+extern "C" int jb_linear_train_bf16(const int64_t* row_ptr, const int32_t* fidx,
+                                    const float* fval, const int32_t* labels,
+                                    const int64_t* stream_ptr, int nstreams, uint16_t* W,
+                                    float* S, const int32_t* active, int LC, int method, float C,
+                                    int mode, unsigned long long* stats, uint8_t* touched,
+                                    void* scratch, int64_t scratch_bytes, hipStream_t stream);
 
 #include "jb_train_batch.hpp"
 
@@ -90,7 +96,13 @@ extern "C" int jb_train_batch_submit(const JbTrainBatch* a) {
   }
   JB_TRY(hipEventRecord(a->ready, a->prep_stream));
   JB_TRY(hipStreamWaitEvent(a->compute_stream, a->ready, 0));
-  if (a->W != nullptr && n > 0) {
+  if (a->W != nullptr && n > 0 && a->w_bf16) {
+    if (jb_linear_train_bf16(a->d_row, a->d_idx, a->d_val, a->d_lab, sbase, R, (uint16_t*)a->W,
+                             a->S, a->active, (int)a->LC, (int)a->method, (float)a->C,
+                             (int)a->mode, a->stats, a->touched, a->serial_scratch,
+                             a->serial_bytes, a->compute_stream) != 0)
+      return 1;
+  } else if (a->W != nullptr && n > 0) {
     if (jb_linear_train(a->d_row, a->d_idx, a->d_val, a->d_lab, sbase, R, a->W, a->S, a->active,
                         (int)a->LC, (int)a->method, (float)a->C, (int)a->mode,
                         hot ? a->hot_rows : nullptr, hot ? a->hot_n : nullptr,

@@ -62,6 +62,7 @@ int jb_topk_direct_query(const uint64_t* qbits, const float* qnorm, int nq, cons
                          hipStream_t stream);
 int jb_topk_blocks(int64_t nrows, int k);
 int64_t jb_topk_direct_scratch(int nq);
+int jb_topk_scratch_init(int32_t* scratch_i, hipStream_t stream);
 int jb_pool_scan(const int64_t* qptr, const int32_t* qidx, const float* qval, const double* qn2,
                  const int32_t* qslots, int nq, int qtot, const int64_t* r_off,
                  const int32_t* r_len, const double* r_n2, const uint8_t* valid, int64_t nrows,
@@ -285,7 +286,11 @@ struct QueryBufs {
     const int64_t b = jb_topk_direct_scratch(nq);
     const size_t n = (size_t)std::max<int64_t>(std::max(a, b), 1 << 16);
     sd.get(n);
+    int32_t* before = si.p;
     si.get(n);
+    // the one-launch score top-k expects its state region zeroed
+    if (si.p != before && jb_topk_scratch_init(si.p, nullptr) != 0)
+      throw std::runtime_error("jb_topk_scratch_init failed");
   }
 };
 

@@ -218,6 +218,21 @@ struct Rules {
   uint64_t H = 1ull << 20;
 };
 
+// Feature-table height of the GPU linear models (classifier, regression)
+// when the configuration gives no hash_max_size: HBM-sized, 2^24 rows unless
+// JUBATUS_DEVICE_HASH_BITS says otherwise (AROW at 64 labels: 8 GiB of W + P
+// on a 288 GB device). Python twin: fv_converter/converter.py
+// device_hash_max_size (both servers pick the same height, so their model
+// files interchange).
+inline uint64_t device_hash_max_size() {
+  int bits = 24;
+  if (const char* e = getenv("JUBATUS_DEVICE_HASH_BITS")) {
+    const int b = atoi(e);
+    if (b >= 10 && b <= 34) bits = b;
+  }
+  return 1ull << bits;
+}
+
 inline int matcher_kind(const std::string& spec, std::string* arg) {
   if (spec.empty() || spec == "*") { arg->clear(); return 0; }
   if (spec.size() >= 2 && spec.front() == '/' && spec.back() == '/') return -1;   // regex

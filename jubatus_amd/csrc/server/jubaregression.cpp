@@ -79,6 +79,7 @@ bool parse_config(const std::string& text, Config* c, std::string* why) {
   const Value* conv = v.get("converter");
   Value empty;
   empty.kind = Value::MAP;
+  c->rules.H = device_hash_max_size();   // unless the converter names hash_max_size
   if (!build_rules(conv ? *conv : empty, &c->rules, why)) return false;
   c->text = text;
   return true;

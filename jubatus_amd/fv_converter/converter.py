@@ -45,6 +45,25 @@ from .datum import Datum, as_datum
 DEFAULT_HASH_MAX_SIZE = 1 << 20
 
 
+def device_hash_max_size() -> int:
+    """Feature-table height of the GPU linear models (classifier,
+    regression) when the configuration gives no ``hash_max_size``:
+    HBM-sized, 2^24 rows unless JUBATUS_DEVICE_HASH_BITS says otherwise
+    (AROW at 64 labels: 8 GiB of W + P on a 288 GB device). The reference
+    keeps feature names unhashed when the key is absent; a 2^24-row table
+    makes collisions among 10^5 distinct features ~16x rarer than the host
+    default of 2^20. Native twin: csrc/server/jb_server_common.hpp."""
+    import os
+    bits = 24
+    try:
+        b = int(os.environ.get("JUBATUS_DEVICE_HASH_BITS", "24"))
+        if 10 <= b <= 34:
+            bits = b
+    except ValueError:
+        pass
+    return 1 << bits
+
+
 class ConverterError(ValueError):
     pass
 
@@ -274,10 +293,12 @@ class DatumToFvConverter:
     SAMPLE_WEIGHTS = ("bin", "tf", "log_tf")
     GLOBAL_WEIGHTS = ("bin", "idf", "bm25")
 
-    def __init__(self, config: dict | None, plugin_loader=None):
+    def __init__(self, config: dict | None, plugin_loader=None,
+                 default_hash_max_size: int | None = None):
         config = dict(config or {})
         self.config = config
-        self.hash_max_size = int(config.get("hash_max_size") or DEFAULT_HASH_MAX_SIZE)
+        self.hash_max_size = int(config.get("hash_max_size") or default_hash_max_size
+                                 or DEFAULT_HASH_MAX_SIZE)
         if self.hash_max_size <= 0:
             raise ConverterError("hash_max_size must be positive")
         self.weights = WeightManager(self.hash_max_size)

@@ -62,7 +62,7 @@ def _label_cap(n: int) -> int:
 
 class LinearClassifier:
     def __init__(self, method: str, parameter: dict | None, converter: DatumToFvConverter,
-                 device: Any = None, concurrent_update: str = "exact"):
+                 device: Any = None, concurrent_update: str = "exact", weight_dtype: str = "fp32"):
         if method not in LINEAR_METHODS:
             raise ClassifierConfigError(f"unknown linear method: {method}")
         parameter = dict(parameter or {})
@@ -77,6 +77,12 @@ class LinearClassifier:
         if concurrent_update not in ("exact", "atomic", "hogwild"):
             raise ClassifierConfigError("concurrent_update must be 'exact', 'atomic' or 'hogwild'")
         self.concurrent_update = concurrent_update
+        if weight_dtype not in ("fp32", "bf16"):
+            raise ClassifierConfigError("weight_dtype must be 'fp32' or 'bf16'")
+        # storage of W on the GPU: fp32, or bf16 with stochastic rounding
+        # (csrc/hip/jb_linear.hpp; P stays fp32, arithmetic is fp32). The host
+        # path has no bf16 table and keeps fp32.
+        self.weight_dtype = weight_dtype if device is not None else "fp32"
         self.conv = converter
         self.H = converter.hash_max_size
         self.use_s = self.mid in lo.USES_COVARIANCE
@@ -152,7 +158,7 @@ class LinearClassifier:
         self._tables_replaced()
         if self.gpu:
             t = self.torch
-            W = t.zeros((H, LC), dtype=t.float32, device=self.device)
+            W = t.zeros((H, LC), dtype=self._wdt(), device=self.device)
             P = t.ones((H, LC), dtype=t.float32, device=self.device) if self.use_s else None
             if self.LC:
                 W[:, :self.LC].copy_(self.W)
@@ -171,6 +177,9 @@ class LinearClassifier:
             self.active = np.zeros(LC, dtype=np.int32)
         self.LC = LC
         self._label_version = -1
+
+    def _wdt(self):
+        return self.torch.bfloat16 if self.weight_dtype == "bf16" else self.torch.float32
 
     def _sync_labels(self) -> None:
         """grow the tables and refresh the active-column mask after label changes"""
@@ -210,7 +219,8 @@ class LinearClassifier:
         detection found none, only every 8th batch looks (and trains with the
         plain 4-stream-block launch)."""
         from ..ops import hip
-        if not (self.gpu and self.hot_rows and self.LC <= 64 and nstreams >= self.hot_min_streams
+        if not (self.gpu and self.hot_rows and self.weight_dtype == "fp32"
+                and self.LC <= 64 and nstreams >= self.hot_min_streams
                 and self._mode(nstreams) in (hip.UPDATE_ATOMIC, hip.UPDATE_HOGWILD)):
             return False
         self._hot_batches += 1
@@ -272,6 +282,7 @@ class LinearClassifier:
         if self.LC not in hip.LABEL_CAPS or (self.mid >= hip.METHODS["CW"] and self.P is None):
             raise ValueError("label capacity / covariance table not supported by the train kernel")
         a.W = self.W.data_ptr()
+        a.w_bf16 = int(self.weight_dtype == "bf16")
         a.S = self.P.data_ptr() if self.P is not None else None
         a.active = self.active.data_ptr()
         a.LC = self.LC
@@ -609,7 +620,7 @@ class LinearClassifier:
 
     def _host_tables(self) -> tuple[np.ndarray, np.ndarray | None]:
         if self.gpu:
-            W = self.W.cpu().numpy()
+            W = self.W.float().cpu().numpy()
             S = self.P.cpu().numpy() if self.P is not None else None
             return W, S
         return self.W, self.P
@@ -696,7 +707,7 @@ class LinearClassifier:
             t = self.torch
             perm = t.tensor([old.get(n, -1) for n in order], dtype=t.int64, device=self.device)
             have = perm >= 0
-            W = t.zeros((self.H, LC), dtype=t.float32, device=self.device)
+            W = t.zeros((self.H, LC), dtype=self._wdt(), device=self.device)
             P = t.ones((self.H, LC), dtype=t.float32, device=self.device) if self.use_s else None
             src = perm.clamp(min=0)
             W[:, :len(order)] = t.where(have, self.W.index_select(1, src), W[:, :len(order)])
@@ -906,10 +917,10 @@ class LinearClassifier:
                 self._sync_labels()
             if me != src and not apply:
                 LC = _label_cap(max(1, len(names)))
-                shapes = [(self.H, LC)] * (2 if self.use_s else 1)
+                dts = [self._wdt() if self.gpu else torch.float32] + ([torch.float32] if self.use_s else [])
                 dev = self.device if self.gpu else "cpu"
-                for shp in shapes:
-                    dist.broadcast(torch.empty(shp, dtype=torch.float32, device=dev), src=src)
+                for dt in dts:
+                    dist.broadcast(torch.empty((self.H, LC), dtype=dt, device=dev), src=src)
                 return
             self._tables_replaced()
             for t in self._tables():
@@ -941,12 +952,15 @@ class LinearClassifier:
                 ops = [dist.P2POp(dist.isend, t, peer), dist.P2POp(dist.irecv, buf, peer)]
                 for r in dist.batch_isend_irecv(ops):
                     r.wait()
-                t.add_(buf).mul_(0.5)
+                if t.dtype == torch.float32:
+                    t.add_(buf).mul_(0.5)
+                else:                      # bf16 W: the mean in fp32, one rounding
+                    t.copy_(t.float().add_(buf.float()).mul_(0.5))
 
     def get_status(self) -> dict[str, str]:
         st = {"num_classes": str(len(self.get_labels())), "num_features": str(self.H),
               "label_capacity": str(self.LC), "method": self.method,
-              "storage": "hbm" if self.gpu else "host",
+              "storage": "hbm" if self.gpu else "host", "weight_dtype": self.weight_dtype,
               "fv_path": ("gpu" if self.pipe.fast else "gpu-wide") if self._devfv else "host"}
         if self.gpu:
             for k, v in self._scan_stats.items():

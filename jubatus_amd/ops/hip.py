@@ -37,6 +37,13 @@ _SIGS = {
                         _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p, _c_void_p,
                         _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _i64, _c_void_p, _i64,
                         _c_void_p],
+    "jb_linear_train_bf16": [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32,
+                             _c_void_p, _c_void_p, _c_void_p, _i32, _i32, _f32, _i32, _c_void_p,
+                             _c_void_p, _c_void_p, _i64, _c_void_p],
+    "jb_linear_classify_bf16": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32,
+                                _c_void_p, _c_void_p],
+    "jb_classify_direct_bf16": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32,
+                                _c_void_p, _c_void_p, _c_void_p],
     "jb_hot_rep_bytes": [],
     "jb_df_scratch_bytes": [_i64, _i64],
     "jb_df_weigh": [_c_void_p, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
@@ -64,6 +71,12 @@ _SIGS = {
                 _i32, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_topk_blocks": [_i64, _i32],
     "jb_topk_direct_scratch": [_i32],
+    "jb_topk_scratch_init": [_c_void_p, _c_void_p],
+    "jb_topk_direct_query_path": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64,
+                                  _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
+                                  _c_void_p, _c_void_p, _i32, _c_void_p],
+    "jb_topk_scores_direct_path": [_c_void_p, _i32, _i32, _i64, _i32, _c_void_p, _c_void_p,
+                                   _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p],
     "jb_lsh_query_direct": [_c_void_p, _c_void_p, _c_void_p, _i32, _i32, _u64, _i32, _i32, _c_void_p,
                             _c_void_p, _c_void_p, _i64, _i32, _c_void_p, _c_void_p, _c_void_p,
                             _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
@@ -307,6 +320,9 @@ def _topk_scratch(device, n: int):
         c = max(n, 1 << 16)
         buf = (torch.empty(c, dtype=torch.float32, device=device),
                torch.empty(c, dtype=torch.int32, device=device))
+        if c >= _fn("jb_topk_direct_scratch")(1):
+            # the one-launch score top-k expects its state region zeroed
+            _check(_fn("jb_topk_scratch_init")(_p(buf[1]), _stream()), "jb_topk_scratch_init")
         _scratch[key] = buf
     return buf
 
@@ -472,6 +488,8 @@ def lof_score(ts, td, st, store: int, out: "HostBuffer", max_missing: int) -> No
 _fns: dict = {}
 
 LABEL_CAPS = (8, 16, 32, 64, 128, 256, 512, 1024)
+# storage types of the linear W table (P / S stays fp32)
+W_DTYPES = (torch.float32, torch.bfloat16)
 # EXACT: one stream; SERIAL: several streams with the result of applying them
 # one after the other (csrc/hip/serial.hip); ATOMIC / HOGWILD: lock-free
 # concurrent streams (not serial-equivalent)
@@ -592,7 +610,7 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
     LC = W.shape[1]
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
-    _dev(W, torch.float32, "W")
+    _dev(W, W.dtype if W.dtype in W_DTYPES else torch.float32, "W")
     _dev(active, torch.int32, "active")
     if active.numel() < LC:
         raise ValueError("active mask shorter than label capacity")
@@ -610,6 +628,18 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
         _dev(touched, torch.uint8, "touched")
         if touched.numel() < W.shape[0]:
             raise ValueError("touched shorter than the table")
+    if W.dtype == torch.bfloat16:
+        # bf16 table: no hot-row replica; UPDATE_SERIAL runs as one
+        # sequential stream (needs 16 bytes of scratch)
+        if mode == UPDATE_SERIAL and scratch is None:
+            raise ValueError("UPDATE_SERIAL needs scratch")
+        rc = _fn("jb_linear_train_bf16")(
+            _p(row_ptr), _p(fidx), _p(fval), _p(labels), _p(stream_ptr), nstreams, _p(W),
+            _p(S) if S is not None else None, _p(active), LC, method, float(C), int(mode),
+            _p(stats), _p(touched), scratch.ptr(max(n_max, 1)) if scratch is not None else None,
+            scratch.nbytes if scratch is not None else 0, _stream())
+        _check(rc, "jb_linear_train_bf16")
+        return
     rc = _fn("jb_linear_train")(_p(row_ptr), _p(fidx), _p(fval), _p(labels), _p(stream_ptr),
                                 nstreams, _p(W), _p(S) if S is not None else None, _p(active), LC,
                                 method, float(C), int(mode),
@@ -709,13 +739,13 @@ def linear_classify(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tenso
     LC = W.shape[1]
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
-    _dev(W, torch.float32, "W")
+    _dev(W, W.dtype if W.dtype in W_DTYPES else torch.float32, "W")
     _dev(out, torch.float32, "out")
     if out.numel() < n * LC or row_ptr.numel() < n + 1:
         raise ValueError("linear_classify: output / row_ptr too small")
-    rc = _fn("jb_linear_classify")(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), LC, _p(out),
-                                   _stream())
-    _check(rc, "jb_linear_classify")
+    fn = "jb_linear_classify_bf16" if W.dtype == torch.bfloat16 else "jb_linear_classify"
+    rc = _fn(fn)(_p(row_ptr), _p(fidx), _p(fval), n, _p(W), LC, _p(out), _stream())
+    _check(rc, fn)
 
 
 def mix_apply_(w: torch.Tensor, red: torch.Tensor, loc: torch.Tensor, inv_n: float) -> None:
@@ -810,7 +840,7 @@ d_slots d_hist nhist:i d_err host_out lt_hash lt_meta lt_cap:i lt_blob lt_blob_l
 srules nrules n_srules:i n_nrules:i blob blob_len:i H:i d_idx d_val slot_cap:i hash_err hot_rows
 hot_n hot_rep gkey gcnt gcap:i block_min:i min_count:i max_rows:i hot_free_valid:i hot_count_host
 W S active LC:i method:i C:d mode:i merge_every:i hot_waves:i stats touched serial_scratch
-serial_bytes:i""".split()
+serial_bytes:i w_bf16:i""".split()
 
 
 class TrainBatchArgs(ctypes.Structure):
@@ -881,14 +911,15 @@ def classify_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, n: int, W: tor
     LC = W.shape[1]
     if LC not in LABEL_CAPS:
         raise ValueError(f"label capacity {LC} not supported")
-    _dev(W, torch.float32, "W")
+    _dev(W, W.dtype if W.dtype in W_DTYPES else torch.float32, "W")
     if out.nbytes < n * LC * 4 or done.nbytes < 4 * n:
         raise ValueError("classify_direct: output buffer too small")
-    rc = _fn("jb_classify_direct")(idx_ptr, val_ptr, row_ptr_ptr, n, _p(W), LC, out.ptr, done.ptr,
-                                   _stream() if stream is None else stream)
+    fn = "jb_classify_direct_bf16" if W.dtype == torch.bfloat16 else "jb_classify_direct"
+    rc = _fn(fn)(idx_ptr, val_ptr, row_ptr_ptr, n, _p(W), LC, out.ptr, done.ptr,
+                 _stream() if stream is None else stream)
     if rc == 1:
         return False
-    _check(rc, "jb_classify_direct")
+    _check(rc, fn)
     return True
 
 

@@ -151,7 +151,10 @@ class TableMix:
             return True
         rows = torch.nonzero_static(self._mark, size=rows_n).flatten()   # sorted, same on every rank
         self._mark = None
-        snap = torch.cat([t.index_select(0, rows).reshape(self.rows, -1) for t in self.tables], dim=1)
+        # fp32 snapshot and sums whatever the tables store (bf16 W: the
+        # collective adds fp32, the fold rounds once)
+        snap = torch.cat([t.index_select(0, rows).reshape(self.rows, -1).float() for t in self.tables],
+                         dim=1)
         red = snap.clone()
         self.nbytes += red.numel() * red.element_size()
         work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -160,7 +163,7 @@ class TableMix:
 
     # ------------------------------------------------------------ dense
     def _launch(self, r0: int, r1: int) -> None:
-        snap = torch.cat([t[r0:r1].reshape(r1 - r0, -1) for t in self.tables], dim=1)
+        snap = torch.cat([t[r0:r1].reshape(r1 - r0, -1).float() for t in self.tables], dim=1)
         red = snap.clone()
         self.nbytes += red.numel() * red.element_size()
         work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
@@ -179,7 +182,11 @@ class TableMix:
         c0 = 0
         for t in self.tables:
             w = t[0].numel()
-            t[r0:r1].view(r1 - r0, -1).add_(upd[:, c0:c0 + w])
+            tv = t[r0:r1].view(r1 - r0, -1)
+            if t.dtype == torch.float32:
+                tv.add_(upd[:, c0:c0 + w])
+            else:
+                tv.copy_(tv.float().add_(upd[:, c0:c0 + w]))
             c0 += w
 
     def _pump(self, block: bool = False) -> None:
@@ -241,7 +248,12 @@ class TableMix:
                 c0 = 0
                 for t in self.tables:
                     w = t[0].numel()
-                    t.view(self.H, -1).index_add_(0, rows, upd[:, c0:c0 + w])
+                    tv = t.view(self.H, -1)
+                    if t.dtype == torch.float32:
+                        tv.index_add_(0, rows, upd[:, c0:c0 + w])
+                    else:            # bf16: current rows + delta in fp32, one rounding
+                        cur = tv.index_select(0, rows).float().add_(upd[:, c0:c0 + w])
+                        tv.index_copy_(0, rows, cur.to(t.dtype))
                     c0 += w
             self._sparse = None
         self._done = True

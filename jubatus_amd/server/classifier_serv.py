@@ -21,7 +21,7 @@ from ..common.mprpc import name_and_rest, split_params
 from ..framework.device import select_device
 from ..framework.batching import MicroBatcher, msgpack_array_len
 from ..framework.server_base import ServerBase
-from ..fv_converter.converter import DatumToFvConverter
+from ..fv_converter.converter import DatumToFvConverter, device_hash_max_size
 from ..fv_converter.datum import Datum
 from ..models.classifier import LINEAR_METHODS, LinearClassifier
 from ..utils import logger, trace
@@ -35,15 +35,22 @@ def build_classifier(cfg: dict, device):
     method = cfg.get("method")
     if not isinstance(method, str):
         raise ValueError("config: 'method' is required")
-    conv = DatumToFvConverter(cfg.get("converter") or {})
     param = cfg.get("parameter")
     if method in LINEAR_METHODS:
+        # HBM-sized feature table on a GPU when the config names no
+        # hash_max_size (the native server picks the same height)
+        conv = DatumToFvConverter(cfg.get("converter") or {},
+                                  default_hash_max_size=device_hash_max_size() if device is not None else None)
         # how concurrent train requests update the model: serial-equivalent by
         # default; JUBATUS_UPDATE_MODE=atomic opts into lock-free streams (the
         # native server reads the same variable)
         mode = os.environ.get("JUBATUS_UPDATE_MODE", "exact")
+        # W storage: fp32 (default) or bf16 (JUBATUS_WEIGHT_DTYPE=bf16; GPU only)
+        wdt = os.environ.get("JUBATUS_WEIGHT_DTYPE", "fp32")
         return LinearClassifier(method, param, conv, device=device,
-                                concurrent_update=mode if mode in ("exact", "atomic", "hogwild") else "exact")
+                                concurrent_update=mode if mode in ("exact", "atomic", "hogwild") else "exact",
+                                weight_dtype=wdt if wdt in ("fp32", "bf16") else "fp32")
+    conv = DatumToFvConverter(cfg.get("converter") or {})
     if method in NN_METHODS:
         from ..models.nn_classifier import NNClassifier
         return NNClassifier(method, param or {}, conv, device=device)

@@ -8,7 +8,7 @@ from __future__ import annotations
 from ..common.exceptions import ArgumentError
 from ..common.mprpc import split_params
 from ..framework.engine_serv import EngineServ
-from ..fv_converter.converter import DatumToFvConverter
+from ..fv_converter.converter import DatumToFvConverter, device_hash_max_size
 from ..models.regression import PARegression
 
 
@@ -17,7 +17,10 @@ class RegressionServ(EngineServ):
 
     def build_driver(self, cfg: dict):
         return PARegression(cfg.get("method"), cfg.get("parameter"),
-                            DatumToFvConverter(cfg.get("converter") or {}), device=self.device)
+                            DatumToFvConverter(cfg.get("converter") or {},
+                                               default_hash_max_size=(device_hash_max_size()
+                                                                      if self.device is not None else None)),
+                            device=self.device)
 
     def train(self, data) -> int:
         self.check_set_config()

@@ -217,3 +217,48 @@ def test_cached_lock_service(ls):
     while c.list("/cc") != ["x"] and time.time() < deadline:
         time.sleep(0.05)
     assert c.list("/cc") == ["x"]
+
+
+def test_coordinator_twins_agree_op_by_op(coord, native_coord):
+    """the Python coordinator (common/coordinator.py, the test harness and
+    fallback) and the native one (csrc/coord/jubacoordinator.cpp, production)
+    answer a seeded random sequence of lock_service operations identically,
+    call by call"""
+    import random
+    py = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=2.0)
+    na = CoordinatorClient(f"127.0.0.1:{native_coord.port}", timeout=2.0)
+    for s in (py, na):
+        for top in s.list("/"):
+            _rm_tree(s, "/" + top)
+        s.create("/twin")
+    rng = random.Random(7)
+    names = ["/twin/a", "/twin/b", "/twin/a/x", "/twin/b/y", "/twin/c", "/twin/a/x/z"]
+    for step in range(400):
+        op = rng.choice(["create", "create_eph", "set", "read", "exists", "list", "remove", "seq", "id"])
+        p = rng.choice(names)
+        val = f"v{rng.randrange(5)}"
+        res = []
+        for s in (py, na):
+            if op == "create":
+                r = s.create(p, val)
+            elif op == "create_eph":
+                r = s.create(p, val, True)
+            elif op == "set":
+                r = s.set(p, val)
+            elif op == "read":
+                r = s.read(p)
+            elif op == "exists":
+                r = s.exists(p)
+            elif op == "list":
+                r = sorted(s.list(p))
+            elif op == "remove":
+                r = s.remove(p)
+            elif op == "seq":
+                r = s.create_seq(p + "/q_")
+            else:
+                r = s.create_id(p, 1) if s.exists(p) else None
+            res.append(r)
+        assert res[0] == res[1], (step, op, p, res)
+    assert sorted(py.list("/twin")) == sorted(na.list("/twin"))
+    py.close()
+    na.close()

@@ -445,3 +445,52 @@ def test_topk_16_wave_path_matches_full_sort(k):
     order = np.argsort(ref, kind="stable")[:k]
     assert row[0].cpu().numpy().tolist() == order.tolist()
     np.testing.assert_allclose(dist[0].cpu().numpy(), ref[order], rtol=1e-6)
+
+
+@pytest.mark.parametrize("case,k,nq,metric", [("random", 1, 1, 1), ("random", 10, 1, 1),
+                                              ("random", 100, 2, 1), ("random", 10, 8, 1),
+                                              ("random", 10, 3, 0), ("ties", 10, 2, 1),
+                                              ("ties", 100, 1, 1), ("sparse_valid", 20, 2, 1),
+                                              ("levels", 10, 4, 0), ("levels", 31, 2, 2)])
+def test_direct_topk_one_launch_path(case, k, nq, metric):
+    """latency top-k below the sampled path's 2M rows: ONE launch
+    (csrc/hip/topk.hip topk_fused_kernel: distances cached in LDS, two radix
+    levels across grid barriers, last-block selection) == full distance
+    matrix + stable sort. "ties" (every row at one distance: the candidates
+    overflow the LDS ranking and k > 16 retries on the tile path, k <= 16
+    selects from L2), "levels" (8 distinct signatures: ~125k rows per
+    distance level) and "sparse_valid" (fewer valid rows than k)"""
+    import torch
+    from jubatus_amd.ops import hip
+    d = dev()
+    n = 1_000_000
+    g = torch.Generator().manual_seed(k + nq + len(case) + metric)
+    tb = torch.randint(-2**62, 2**62, (n, 1), generator=g, dtype=torch.int64)
+    tn = torch.rand(n, generator=g)
+    valid = torch.ones(n, dtype=torch.uint8)
+    if case == "ties":
+        tb[:] = 12345
+        tn[:] = 0.5
+    if case == "levels":
+        pool = torch.randint(-2**62, 2**62, (8, 1), generator=g, dtype=torch.int64)
+        tb = pool[torch.randint(0, 8, (n,), generator=g)]
+    if case == "sparse_valid":
+        valid[:] = 0
+        valid[::110000] = 1
+    qb = tb[:nq].clone()
+    qb[-1] ^= 0x5555
+    qn = tn[:nq].clone()
+    tbd, tnd, vd, qbd, qnd = (x.to(d) for x in (tb, tn, valid, qb, qn))
+    bufs = hip.DirectQueryBuffers(d, 1)
+    full = torch.empty((nq, n), dtype=torch.float32, device=d)
+    hip.hamming_scan(qbd, qnd, nq, tbd, tnd, vd, n, 64, metric, full)
+    full = full.cpu().numpy()
+    for rep in range(2):                 # the second call checks the state the first left behind
+        od, oi = hip.topk_rows_direct(qbd, qnd, nq, tbd, tnd, vd, n, 64, metric, k, bufs)
+        for q in range(nq):
+            order = np.argsort(full[q], kind="stable")[:k]
+            ref = full[q][order]
+            fin = np.isfinite(ref)
+            np.testing.assert_array_equal(oi[q][:fin.sum()], order[fin])
+            np.testing.assert_allclose(od[q][:fin.sum()], ref[fin], rtol=1e-6)
+            assert np.all(np.isinf(od[q][fin.sum():]))
