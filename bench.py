@@ -234,7 +234,7 @@ def served_train(args, local: int, nat) -> dict:
             for o, n in zip(offs, lens):
                 f.write(b"\x92\xa0" + buf[o:o + n].tobytes())
         base = [exe, "-p", str(a.port), "-m", "train", "-f", pfile, "-c", str(args.rpc_conns),
-                "-d", str(args.rpc_depth)]
+                "-d", str(args.rpc_depth)] + _fresh_flag(args)
         subprocess.run(base + ["-t", "1.5"], capture_output=True, text=True, timeout=120)  # warmup
         clf = h.server.clf
         clf.synchronize()
@@ -259,7 +259,8 @@ def served_train(args, local: int, nat) -> dict:
         return {"served_train_samples_per_sec": round(lg["requests_per_s"] * args.per_request, 1),
                 "requests_per_s": lg["requests_per_s"], "samples_per_request": args.per_request,
                 "connections": lg["connections"], "depth": lg["depth"],
-                "distinct_requests": lg["distinct_requests"], "rpc_p50_us": lg["p50_us"],
+                "distinct_requests": lg["distinct_requests"], "fresh_values": lg.get("fresh_values"),
+                "rpc_p50_us": lg["p50_us"],
                 "rpc_p99_us": lg["p99_us"], "seconds": lg["seconds"],
                 "samples_trained_in_window": tr,
                 "update_fraction": round((st1["updated"] - st0["updated"]) / tr, 4) if tr else None,
@@ -348,7 +349,7 @@ def served_train_native(args, local: int, nat) -> dict:
             for o, n in zip(offs, lens):
                 f.write(b"\x92\xa0" + buf[o:o + n].tobytes())
         base = [exe, "-p", str(port), "-m", "train", "-f", pfile, "-c", str(args.rpc_conns),
-                "-d", str(args.rpc_depth)]
+                "-d", str(args.rpc_depth)] + _fresh_flag(args)
         subprocess.run(base + ["-t", "1.5"], capture_output=True, text=True, timeout=120)  # warmup
         st0 = status()
         cpu0 = _proc_cpu(p.pid)
@@ -361,13 +362,23 @@ def served_train_native(args, local: int, nat) -> dict:
         st1 = status()
         tr = int(st1["train.samples_trained"]) - int(st0["train.samples_trained"])
         up = int(st1["train.samples_updated"]) - int(st0["train.samples_updated"])
+        # classify over RPC: one datum per request, one connection, one in flight
+        one = msgpack.unpackb(buf[offs[0]:offs[0] + lens[0]].tobytes(), raw=False)[0][1]
+        cfile = os.path.join(tmp, "classify_params.bin")
+        with open(cfile, "wb") as f:
+            f.write(msgpack.packb(["", [one]], use_bin_type=False))
+        cl = _loadgen(exe, port, "classify", cfile, 1, 1, secs=2.0, timeout=120)
         return {"served_train_samples_per_sec": round(lg["requests_per_s"] * args.per_request, 1),
                 "requests_per_s": lg["requests_per_s"], "samples_per_request": args.per_request,
                 "connections": lg["connections"], "depth": lg["depth"],
+                "distinct_requests": lg["distinct_requests"], "fresh_values": lg.get("fresh_values"),
                 "rpc_p50_us": lg["p50_us"], "rpc_p99_us": lg["p99_us"], "seconds": lg["seconds"],
                 "samples_trained_in_window": tr,
                 "update_fraction": round(up / tr, 4) if tr else None,
+                "server_threads": args.rpc_threads,
                 "server_cpus": round((cpu1 - cpu0) / lg["seconds"], 2),
+                "classify_rpc_p50_us": cl["p50_us"], "classify_rpc_p99_us": cl["p99_us"],
+                "classify_rpc": "one datum per request, 1 connection x 1 in flight, loopback TCP",
                 "train_scan": {k[len("train_scan."):]: int(v) for k, v in st1.items()
                                if k.startswith("train_scan.") and v.isdigit()},
                 "concurrent_update": st1.get("train.update_mode"),
@@ -379,6 +390,12 @@ def served_train_native(args, local: int, nat) -> dict:
             p.wait(timeout=30)
         except subprocess.TimeoutExpired:
             p.kill()
+
+
+def _fresh_flag(args) -> list:
+    """jubaloadgen -r: every sample sent carries a freshly drawn numeric value
+    (csrc/tools/jubaloadgen.cpp), so the served stream does not repeat"""
+    return ["-r", "4243"] if args.rpc_fresh else []
 
 
 # ------------------------------------------------------- engine records
@@ -641,6 +658,9 @@ def main() -> None:
     ap.add_argument("--rpc-threads", type=int, default=32,
                     help="server RPC threads (a quarter of them are epoll IO threads)")
     ap.add_argument("--rpc-distinct", type=int, default=512, help="distinct train requests cycled")
+    ap.add_argument("--rpc-fresh", type=int, default=1,
+                    help="1 (default): the load generator redraws a numeric value of every sample it "
+                         "sends, so no served sample repeats; 0: the distinct requests are replayed as is")
     ap.add_argument("--update-mode", choices=("exact", "atomic", "hogwild"), default="atomic",
                     help="how the concurrent requests of a batch update the headline model: exact = "
                          "the result of applying them one after the other (csrc/hip/serial.hip); "

@@ -14,8 +14,16 @@
 // the i-th contiguous share of the file - and the run ends when all replied
 // (bulk loads: each row once, in file order per connection).
 //
+// -r SEED (fresh): train params only ([name, [[label, datum]...]]). Every
+// sample sent carries a freshly drawn numeric value: the first float64 of its
+// datum's num_values becomes v + N(0, 1/4) (a per-connection splitmix64
+// stream), written into a private copy of the request just before it goes
+// out. So no two samples of a run are alike - the model keeps meeting data
+// it has not seen, as in the in-process bench's non-repeating stream -
+// while the per-request cost stays a memcpy plus one draw per sample.
+//
 // Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
-//                    [-o 1]
+//                    [-o 1] [-r SEED]
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/tcp.h>
@@ -101,6 +109,65 @@ int connect_to(const std::string& host, int port) {
   return fd;
 }
 
+// byte offsets of the float64 payload of the first numeric value of every
+// sample of a train params object (empty: not that layout)
+std::vector<uint32_t> fresh_slots(const std::string& prm) {
+  std::vector<uint32_t> out;
+  const uint8_t* b = (const uint8_t*)prm.data();
+  jb::Cursor c{b, b + prm.size()};
+  uint32_t n, ns;
+  const uint8_t* s;
+  if (!c.array(&n) || n != 2 || !c.raw(&s, &n) || !c.array(&ns)) return {};
+  for (uint32_t i = 0; i < ns; ++i) {
+    uint32_t two, three, nn;
+    if (!c.array(&two) || two != 2 || !c.raw(&s, &n) || !c.array(&three) || three < 2) return {};
+    if (!c.skip()) return {};                      // string_values
+    if (!c.array(&nn)) return {};
+    for (uint32_t j = 0; j < nn; ++j) {
+      uint32_t kv;
+      if (!c.array(&kv) || kv != 2 || !c.raw(&s, &n) || !c.need(1)) return {};
+      if (j == 0 && *c.p == 0xcb) out.push_back((uint32_t)(c.p + 1 - b));
+      double d;
+      if (!c.number(&d)) return {};
+    }
+    for (uint32_t k = 2; k < three; ++k)
+      if (!c.skip()) return {};
+  }
+  return out;
+}
+
+struct Fresh {
+  uint64_t s;
+  uint64_t next() {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  }
+  // N(0, 1/4) from the sum of four 16-bit uniforms (Irwin-Hall, variance 1/3
+  // each -> scaled)
+  double half_gauss() {
+    const uint64_t r = next();
+    const double u = (double)(r & 0xffff) + (double)((r >> 16) & 0xffff) +
+                     (double)((r >> 32) & 0xffff) + (double)(r >> 48);
+    return (u / 65536.0 - 2.0) * 0.8660254037844386;   // sqrt(3)/2: sd 0.5
+  }
+};
+
+void refresh(std::string* dst, const std::string& src, const std::vector<uint32_t>& slots, Fresh* rng) {
+  dst->assign(src);
+  uint8_t* b = (uint8_t*)&(*dst)[0];
+  for (const uint32_t o : slots) {
+    uint64_t u = 0;
+    for (int k = 0; k < 8; ++k) u = (u << 8) | b[o + k];
+    double v;
+    memcpy(&v, &u, 8);
+    v += rng->half_gauss();
+    memcpy(&u, &v, 8);
+    for (int k = 7; k >= 0; --k) { b[o + k] = (uint8_t)u; u >>= 8; }
+  }
+}
+
 struct Result {
   uint64_t done = 0;
   std::vector<double> lat_us;
@@ -108,8 +175,8 @@ struct Result {
 };
 
 void run_conn(const std::string& host, int port, const std::string& method,
-              const std::vector<std::string>* params, size_t first, size_t last, bool once, int depth,
-              double secs, Result* r) {
+              const std::vector<std::string>* params, const std::vector<std::vector<uint32_t>>* fresh,
+              uint64_t seed, size_t first, size_t last, bool once, int depth, double secs, Result* r) {
   const int fd = connect_to(host, port);
   if (fd < 0) { r->error = "connect failed"; return; }
   std::vector<Clock::time_point> sent(1 << 16);
@@ -122,6 +189,10 @@ void run_conn(const std::string& host, int port, const std::string& method,
   char buf[1 << 16];
   std::vector<std::string> heads;
   std::vector<const std::string*> bodies;
+  // fresh mode: private copies of the requests of one sendmsg (the kernel
+  // has copied them when send_many returns)
+  std::vector<std::string> priv(fresh ? (size_t)depth : 0);
+  Fresh rng{seed * 0xD1B54A32D192ED03ull + first};
   while (sending || inflight > 0) {
     // every request the window allows goes out in one sendmsg
     heads.clear();
@@ -131,7 +202,13 @@ void run_conn(const std::string& host, int port, const std::string& method,
     if (sending && once && which >= last) sending = false;
     while (sending && inflight < depth && !(once && which >= last)) {
       heads.push_back(request_head(next, method));
-      bodies.push_back(&(*params)[which]);
+      if (fresh) {
+        std::string* d = &priv[heads.size() - 1];
+        refresh(d, (*params)[which], (*fresh)[which], &rng);
+        bodies.push_back(d);
+      } else {
+        bodies.push_back(&(*params)[which]);
+      }
       sent[next & 0xffff] = now;
       which = once ? which + 1 : (which + 1) % params->size();
       ++next;
@@ -176,6 +253,7 @@ int main(int argc, char** argv) {
   int port = 0, conns = 8, depth = 4;
   bool once = false;
   double secs = 3.0;
+  long long fresh_seed = -1;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string a = argv[i], v = argv[i + 1];
     if (a == "-H") host = v;
@@ -186,12 +264,13 @@ int main(int argc, char** argv) {
     else if (a == "-d") depth = atoi(v.c_str());
     else if (a == "-t") secs = atof(v.c_str());
     else if (a == "-o") once = atoi(v.c_str()) != 0;
+    else if (a == "-r") fresh_seed = atoll(v.c_str());
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
   }
   if (!port || method.empty() || file.empty() || conns < 1 || depth < 1) {
     fprintf(stderr,
             "usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH]"
-            " [-t SECONDS]\n");
+            " [-t SECONDS] [-o 1] [-r SEED]\n");
     return 1;
   }
   std::ifstream ifs(file, std::ios::binary);
@@ -206,11 +285,21 @@ int main(int argc, char** argv) {
     pos += (size_t)f;
   }
   if (params.empty()) { fprintf(stderr, "empty params file\n"); return 1; }
+  std::vector<std::vector<uint32_t>> slots;
+  uint64_t fresh_samples = 0;
+  if (fresh_seed >= 0) {
+    for (const auto& p : params) {
+      slots.push_back(fresh_slots(p));
+      if (slots.back().empty()) { fprintf(stderr, "-r: params without float64 num values\n"); return 1; }
+      fresh_samples += slots.back().size();
+    }
+  }
   std::vector<Result> res(conns);
   std::vector<std::thread> ts;
   const auto t0 = Clock::now();
   for (int i = 0; i < conns; ++i)
-    ts.emplace_back(run_conn, host, port, method, &params,
+    ts.emplace_back(run_conn, host, port, method, &params, fresh_seed >= 0 ? &slots : nullptr,
+                    (uint64_t)(fresh_seed >= 0 ? fresh_seed : 0),
                     (size_t)i * params.size() / (size_t)conns,
                     (size_t)(i + 1) * params.size() / (size_t)conns, once, depth, secs, &res[i]);
   for (auto& t : ts) t.join();
@@ -225,7 +314,9 @@ int main(int argc, char** argv) {
   std::sort(lat.begin(), lat.end());
   auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[(size_t)(q * (lat.size() - 1))]; };
   printf("{\"requests\": %llu, \"seconds\": %.3f, \"requests_per_s\": %.1f, \"connections\": %d, "
-         "\"depth\": %d, \"distinct_requests\": %zu, \"p50_us\": %.1f, \"p99_us\": %.1f}\n",
-         (unsigned long long)done, dt, done / dt, conns, depth, params.size(), pct(0.5), pct(0.99));
+         "\"depth\": %d, \"distinct_requests\": %zu, \"fresh_values\": %s, \"p50_us\": %.1f, "
+         "\"p99_us\": %.1f}\n",
+         (unsigned long long)done, dt, done / dt, conns, depth, params.size(),
+         fresh_seed >= 0 ? "true" : "false", pct(0.5), pct(0.99));
   return 0;
 }
