@@ -131,6 +131,10 @@ TOOLS = {
     "jubavisor": (["visor/jubavisor.cpp", "native/jb_rpc.cpp"],
                   ["visor", "native", "../client_cpp/include"]),
     "jubaloadgen": (["tools/jubaloadgen.cpp", "native/jb_rpc.cpp"], ["native"]),
+    # operator tools (csrc/cmd): cluster control and configs in the coordinator
+    "jubactl": (["cmd/jubactl.cpp", "native/jb_rpc.cpp"], ["cmd", "native", "../client_cpp/include"]),
+    "jubaconfig": (["cmd/jubaconfig.cpp", "native/jb_rpc.cpp"],
+                   ["cmd", "native", "server", "../client_cpp/include"]),
     # host-only rehearsal of the native distributed model plane (jb_mix_group.hpp)
     "jb_mix_rehearsal": (["tools/jb_mix_rehearsal.cpp", "native/jb_rpc.cpp"],
                          ["native", "../client_cpp/include"]),

@@ -93,6 +93,86 @@ def test_jubaconfig(coord):
     assert jubaconfig.main(["-c", "read", "-t", "classifier", "-n", "c1", "-z", zk], out=out.append) == 1
 
 
+def _native_tool(name):
+    exe = os.path.join(NATIVE_BIN_DIR, name)
+    if not os.access(exe, os.X_OK):
+        pytest.skip(f"native {name} not built (python -m jubatus_amd.build_ext)")
+    return exe
+
+
+def _run_native(name, args):
+    r = subprocess.run([_native_tool(name), *args], capture_output=True, text=True, timeout=60)
+    return r.returncode, r.stdout.splitlines(), r.stderr
+
+
+def test_native_jubaconfig_matches_python(coord):
+    """csrc/cmd/jubaconfig.cpp: same nodes, same output lines and exit codes
+    as the Python twin; each reads what the other wrote"""
+    zk = f"127.0.0.1:{coord.port}"
+    pa = os.path.join(ROOT, "config/classifier/pa.json")
+    arow = os.path.join(ROOT, "config/classifier/arow.json")
+    assert _run_native("jubaconfig", ["-c", "write", "-f", pa, "-t", "classifier", "-n", "c1", "-z", zk])[0] == 0
+    assert jubaconfig.main(["-c", "write", "-f", arow, "-t", "classifier", "-n", "c2", "-z", zk],
+                           out=lambda *a: None) == 0
+    rc, lines, _ = _run_native("jubaconfig", ["-c", "read", "-t", "classifier", "-n", "c2", "-z", zk])
+    assert rc == 0 and json.loads("\n".join(lines))["method"] == "AROW"
+    py = []
+    assert jubaconfig.main(["-c", "read", "-t", "classifier", "-n", "c1", "-z", zk], out=py.append) == 0
+    assert json.loads(py[0]) == json.load(open(pa))
+    py = []
+    assert jubaconfig.main(["-c", "list", "-z", zk], out=py.append) == 0
+    rc, lines, _ = _run_native("jubaconfig", ["-c", "list", "-z", zk])
+    assert rc == 0 and lines == "".join(x + "\n" for x in py).splitlines()   # print() lines
+    assert lines[0] == "config of classifier/c1:"
+    # bad JSON, missing config, delete, and a config refused while a server is registered
+    bad = os.path.join(os.path.dirname(pa), "..", "..", "README.md")
+    rc, lines, _ = _run_native("jubaconfig", ["-c", "write", "-f", bad, "-t", "classifier", "-n", "c3", "-z", zk])
+    assert rc == 1 and lines[0].startswith("error: invalid config json")
+    assert _run_native("jubaconfig", ["-c", "delete", "-t", "classifier", "-n", "c1", "-z", zk])[0] == 0
+    rc, lines, _ = _run_native("jubaconfig", ["-c", "read", "-t", "classifier", "-n", "c1", "-z", zk])
+    assert rc == 1 and lines == ["error: config is not found: /jubatus/config/classifier/c1"]
+    ls = CoordinatorClient(zk, timeout=5.0)
+    try:
+        assert ls.create(mb.build_actor_path("classifier", "c2") + "/nodes/127.0.0.1_1", "", ephemeral=True)
+        rc, lines, _ = _run_native("jubaconfig", ["-c", "write", "-f", pa, "-t", "classifier", "-n", "c2",
+                                                  "-z", zk])
+        assert rc == 1 and lines == ["error: any server is running"]
+    finally:
+        ls.close()
+    rc, lines, _ = _run_native("jubaconfig", ["-c", "read", "-t", "classifier", "-z", zk])
+    assert rc == 1 and lines == ["type (-t) and name (-n) are required"]
+    assert _run_native("jubaconfig", ["--help"])[0] == 0
+
+
+def test_native_jubactl_without_supervisors(coord):
+    zk = f"127.0.0.1:{coord.port}"
+    common = ["-s", "jubaclassifier", "-n", "none", "-t", "classifier", "-z", zk]
+    rc, lines, _ = _run_native("jubactl", ["-c", "start", *common])
+    assert rc == 1 and lines == ["no server to start jubaclassifier/none"]
+    rc, lines, _ = _run_native("jubactl", ["-c", "save", *common])
+    assert rc == 0 and lines == ["no server to save none"]
+    rc, lines, _ = _run_native("jubactl", ["-c", "bogus", *common])
+    assert rc == 1
+    env = {k: v for k, v in os.environ.items() if k != "ZK"}
+    r = subprocess.run([_native_tool("jubactl"), "-c", "status", "-s", "x", "-n", "y", "-t", "z"],
+                       capture_output=True, text=True, timeout=30, env=env)
+    assert r.returncode == 1 and "can't get ZK location" in r.stdout
+
+
+@pytest.mark.parametrize("tool", ["jubactl", "jubaconfig"])
+def test_native_tool_flags_match_python(tool):
+    """the native tool takes every flag of the Python twin's --help (the man
+    page is rendered from the latter, tools/gen_man.py)"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from gen_man import flags_of
+    rc, lines, _ = _run_native(tool, ["--help"])
+    assert rc == 0
+    py = subprocess.run([sys.executable, "-m", f"jubatus_amd.cmd.{tool}", "--help"], cwd=ROOT,
+                        capture_output=True, text=True, timeout=60).stdout
+    assert flags_of(py) <= flags_of("\n".join(lines)), flags_of(py) - flags_of("\n".join(lines))
+
+
 def test_jubavisor_wire_helpers():
     assert split_server_name("jubaclassifier/foo") == ("jubaclassifier", "foo")
     with pytest.raises(ValueError):
@@ -102,10 +182,21 @@ def test_jubavisor_wire_helpers():
     assert jubactl.split_counts(5, 2) == [3, 2] and jubactl.split_counts(0, 3) == [1, 1, 1]
 
 
-def _cluster_roundtrip(zk, ls, tmp_path, gpus=0):
+def _cluster_roundtrip(zk, ls, tmp_path, gpus=0, native_ctl=False):
     """jubactl start 2 / status / save / load / stop against the registered supervisor(s);
-    gpus > 0: the supervisor hands out one device per child (--gpu), visible in get_status"""
+    gpus > 0: the supervisor hands out one device per child (--gpu), visible in get_status;
+    native_ctl: the native jubactl (csrc/cmd/jubactl.cpp) drives it"""
     out = []
+    if native_ctl:
+        class _Native:
+            @staticmethod
+            def main(args):
+                rc, lines, err = _run_native("jubactl", args)
+                assert all(ln.endswith("ok.") for ln in lines if ln.startswith("sending")), lines
+                return rc
+        jubactl = _Native
+    else:
+        from jubatus_amd.cmd import jubactl
     assert jubaconfig.main(["-c", "write", "-f", os.path.join(ROOT, "config/classifier/arow.json"),
                             "-t", "classifier", "-n", "cl", "-z", zk], out=out.append) == 0
     common = ["-s", "jubaclassifier", "-n", "cl", "-t", "classifier", "-z", zk]
@@ -183,7 +274,7 @@ def test_native_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     ls = CoordinatorClient(zk, timeout=5.0)
     try:
         assert ls.list(mb.JUBAVISOR_BASE_PATH) == [f"127.0.0.1_{vport}"]
-        _cluster_roundtrip(zk, ls, tmp_path, gpus=2)
+        _cluster_roundtrip(zk, ls, tmp_path, gpus=2, native_ctl=True)
     finally:
         proc.terminate()
         rc = proc.wait(30)

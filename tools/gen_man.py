@@ -63,7 +63,7 @@ def _esc(s: str) -> str:
 
 def render(name: str, sec: int, cmd: list[str], short: str, desc: str) -> str:
     # the Python server's help (the launchers' native binaries take the same flags)
-    env = dict(os.environ, PYTHONPATH=ROOT, COLUMNS="100", JUBATUS_NATIVE_SERVER="0")
+    env = dict(os.environ, PYTHONPATH=ROOT, COLUMNS="100", JUBATUS_NATIVE_SERVER="0", JUBATUS_PY_TOOLS="1")
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
     help_text = (out.stdout or out.stderr).rstrip()
     lines = [f'.TH {name.upper()} {sec} "" "jubatus_amd" "jubatus_amd manual"',
