@@ -184,10 +184,12 @@ SERVERS = {
     "jubaweight": (["server/jubaweight.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
     # coresets + k-means++ / Lloyd / GMM EM in csrc/hip/clustering.hip
     "jubaclustering": (["server/jubaclustering.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
+    # jubaconv (operator tool) over the native wide converter: host code only
+    "jubaconv": (["cmd/jubaconv.cpp", "native/jb_rpc.cpp"], ["cmd", "server", "native", "hip"]),
     # check of the RCCL data plane of the native MIX on one GPU (not a server)
     "jb_rccl_check": (["tools/jb_rccl_check.cpp", "native/jb_rpc.cpp"], ["server", "native", "hip"]),
 }
-HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph", "jubaweight"}
+HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph", "jubaweight", "jubaconv"}
 # servers with a native distributed mode (the model plane over RCCL)
 RCCL_SERVERS = {"jubaclassifier", "jb_rccl_check"}
 

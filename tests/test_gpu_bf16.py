@@ -78,21 +78,32 @@ def test_bf16_weights_track_fp32_oracle(method, mode, capsys):
     g.synchronize()
     Wg = g.W.float().cpu().numpy()[:, :c.LC]
     rel = float(np.linalg.norm(Wg - c.W) / np.linalg.norm(c.W))
+    rel_f = 0.0
+    if mode == "atomic":
+        # the lock-free streams race in any storage: the fp32 table under the
+        # same concurrency is the yardstick of the trajectory divergence
+        f = LinearClassifier(method, param, DatumToFvConverter(CONV), device=_device(),
+                             concurrent_update=mode)
+        for r in reqs[:4]:
+            f.train(r)
+        f.train_requests(bodies)
+        f.synchronize()
+        rel_f = float(np.linalg.norm(f.W.float().cpu().numpy()[:, :c.LC] - c.W) / np.linalg.norm(c.W))
     test = _data(2000, seed=6)
     pg, pc = _top(g, test), _top(c, test)
     agree = float(np.mean([a == b for a, b in zip(pg, pc)]))
     acc_g = float(np.mean([p == l for p, (l, _) in zip(pg, test)]))
     acc_c = float(np.mean([p == l for p, (l, _) in zip(pc, test)]))
     with capsys.disabled():
-        print(f"\nbf16 {method} {mode}: rel W diff {rel:.4f}, agreement {agree:.3f}, "
-              f"acc {acc_g:.3f} vs fp32 {acc_c:.3f}")
+        print(f"\nbf16 {method} {mode}: rel W diff {rel:.4f} (fp32 {mode}: {rel_f:.4f}), "
+              f"agreement {agree:.3f}, acc {acc_g:.3f} vs fp32 {acc_c:.3f}")
     assert acc_g >= acc_c - 0.02, (acc_g, acc_c)
     assert agree >= (0.97 if mode == "exact" else 0.95), agree
     # the weight distance mixes rounding noise (a bf16 ulp is 2^-8 of the
     # weight, stochastically rounded on every store) with the divergence of
     # the online trajectory it causes (margins differ, so which samples update
     # differs); decisions stay the fp32 model's
-    assert rel <= (0.3 if mode == "exact" else 2.0), rel
+    assert rel <= (0.3 if mode == "exact" else max(2.0, 2.0 * rel_f)), (rel, rel_f)
     assert g.train_stats()["trained"] == len(data)
 
 

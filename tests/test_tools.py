@@ -79,6 +79,52 @@ def test_jubaconv_json_datum_fv(tmp_path):
     assert jubaconv.main(["-i", "datum", "-o", "json"], stdin=io.StringIO(json.dumps(d)), out=io.StringIO()) == -1
 
 
+JUBACONV_INPUTS = [
+    '{"user": {"name": "taro", "age": 31, "tags": ["a", "b"], "vip": true, "x": null}}',
+    r'{"t": "caf\u00e9 \ud83d\ude00 \"q\" \t", "n": [1.5, -0.0, 1e-05, 1e16, 123456789.125, 3e30], '
+    '"e": {}, "l": [], "deep": {"a": [{"b": false}]}}',
+    '{"text": "the quick brown fox jumps over the lazy dog the end", "w": 2.0}',
+]
+
+
+@pytest.mark.parametrize("conf", [
+    None,
+    {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+     "num_rules": [{"key": "*", "type": "num"}]},
+    {"string_types": {"bi": {"method": "ngram", "char_num": "2"}},
+     "string_rules": [{"key": "/text", "type": "bi", "sample_weight": "tf", "global_weight": "bin"},
+                      {"key": "*", "type": "space", "sample_weight": "log_tf", "global_weight": "bin"}],
+     "num_rules": [{"key": "*", "type": "log"}],
+     "combination_rules": [{"key_left": "*", "key_right": "*", "type": "add"}]},
+    # outside the wide set (a filter): the native tool hands it to the Python twin
+    {"string_filter_types": {"dl": {"method": "regexp", "pattern": "o", "replace": ""}},
+     "string_filter_rules": [{"key": "/text", "type": "dl", "suffix": "-x"}],
+     "string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}]},
+])
+def test_native_jubaconv_matches_python(tmp_path, conf):
+    """csrc/cmd/jubaconv.cpp against jubatus_amd/cmd/jubaconv.py: json / datum
+    outputs byte for byte (json.dumps indent=2), fv lines of the same config"""
+    exe = _native_tool("jubaconv")
+    cfg = tmp_path / "c.json"
+    cfg.write_text(json.dumps({"converter": conf or {}}))
+    modes = [("json", "json"), ("json", "datum")] if conf is None else [("json", "fv")]
+    for js in JUBACONV_INPUTS:
+        for i, o in modes:
+            args = ["-i", i, "-o", o] + (["-c", str(cfg)] if o == "fv" else [])
+            py = io.StringIO()
+            prc = jubaconv.main(args, stdin=io.StringIO(js), out=py)
+            r = subprocess.run([exe, *args], input=js, capture_output=True, text=True, timeout=60,
+                               env=dict(os.environ, PYTHONPATH=ROOT))
+            assert (r.returncode, r.stdout) == (prc & 0xff, py.getvalue()), (i, o, js, r.stderr)
+            if o == "datum":    # the datum output read back as input
+                d = r.stdout
+                py2 = io.StringIO()
+                jubaconv.main(["-i", "datum", "-o", "datum"], stdin=io.StringIO(d), out=py2)
+                r2 = subprocess.run([exe, "-i", "datum", "-o", "datum"], input=d, capture_output=True,
+                                    text=True, timeout=60)
+                assert r2.stdout == py2.getvalue() == d
+
+
 def test_jubaconfig(coord):
     zk = f"127.0.0.1:{coord.port}"
     out = []
@@ -159,7 +205,7 @@ def test_native_jubactl_without_supervisors(coord):
     assert r.returncode == 1 and "can't get ZK location" in r.stdout
 
 
-@pytest.mark.parametrize("tool", ["jubactl", "jubaconfig"])
+@pytest.mark.parametrize("tool", ["jubactl", "jubaconfig", "jubaconv"])
 def test_native_tool_flags_match_python(tool):
     """the native tool takes every flag of the Python twin's --help (the man
     page is rendered from the latter, tools/gen_man.py)"""
