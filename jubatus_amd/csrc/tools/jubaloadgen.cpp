@@ -14,13 +14,15 @@
 // the i-th contiguous share of the file - and the run ends when all replied
 // (bulk loads: each row once, in file order per connection).
 //
-// -r SEED (fresh): train params only ([name, [[label, datum]...]]). Every
-// sample sent carries a freshly drawn numeric value: the first float64 of its
-// datum's num_values becomes v + N(0, 1/4) (a per-connection splitmix64
-// stream), written into a private copy of the request just before it goes
-// out. So no two samples of a run are alike - the model keeps meeting data
-// it has not seen, as in the in-process bench's non-repeating stream -
-// while the per-request cost stays a memcpy plus one draw per sample.
+// -r SEED (fresh, with -t): train params only ([name, [[label, datum]...]]).
+// Every sample sent carries freshly drawn values: the first float64 of its
+// datum's num_values becomes v + N(0, 1/4) and the digits of its last string
+// value are redrawn (a new token of the same length: a feature the model has
+// likely not seen), from a per-connection splitmix64 stream. Each connection
+// owns `depth` private copies of params objects and refreshes one in place
+// just before it goes out, so no two samples of a run are alike - the model
+// keeps meeting data it has not seen, as in the in-process bench's
+// non-repeating stream - at the cost of a few draws per sample, no copy.
 //
 // Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
 //                    [-o 1] [-r SEED]
@@ -109,24 +111,42 @@ int connect_to(const std::string& host, int port) {
   return fd;
 }
 
-// byte offsets of the float64 payload of the first numeric value of every
-// sample of a train params object (empty: not that layout)
-std::vector<uint32_t> fresh_slots(const std::string& prm) {
-  std::vector<uint32_t> out;
+// what a fresh send redraws in a train params object: the float64 payload
+// of the first numeric value of every sample, and the decimal digits of the
+// last string value of every sample (empty: not that layout)
+struct FreshSlots {
+  std::vector<uint32_t> f64;                          // payload offsets
+  std::vector<std::pair<uint32_t, uint32_t>> digits;  // (offset, length) runs
+  bool empty() const { return f64.empty(); }
+};
+
+FreshSlots fresh_slots(const std::string& prm) {
+  FreshSlots out;
   const uint8_t* b = (const uint8_t*)prm.data();
   jb::Cursor c{b, b + prm.size()};
   uint32_t n, ns;
   const uint8_t* s;
   if (!c.array(&n) || n != 2 || !c.raw(&s, &n) || !c.array(&ns)) return {};
   for (uint32_t i = 0; i < ns; ++i) {
-    uint32_t two, three, nn;
+    uint32_t two, three, nn, sn;
     if (!c.array(&two) || two != 2 || !c.raw(&s, &n) || !c.array(&three) || three < 2) return {};
-    if (!c.skip()) return {};                      // string_values
+    if (!c.array(&sn)) return {};                   // string_values
+    for (uint32_t j = 0; j < sn; ++j) {
+      uint32_t kv;
+      if (!c.array(&kv) || kv != 2 || !c.raw(&s, &n) || !c.raw(&s, &n)) return {};
+      if (j + 1 == sn) {                              // the last value's digits
+        uint32_t k = 0;
+        while (k < n && !(s[k] >= '0' && s[k] <= '9')) ++k;
+        uint32_t e = k;
+        while (e < n && s[e] >= '0' && s[e] <= '9') ++e;
+        if (e > k) out.digits.emplace_back((uint32_t)(s + k - b), e - k);
+      }
+    }
     if (!c.array(&nn)) return {};
     for (uint32_t j = 0; j < nn; ++j) {
       uint32_t kv;
       if (!c.array(&kv) || kv != 2 || !c.raw(&s, &n) || !c.need(1)) return {};
-      if (j == 0 && *c.p == 0xcb) out.push_back((uint32_t)(c.p + 1 - b));
+      if (j == 0 && *c.p == 0xcb) out.f64.push_back((uint32_t)(c.p + 1 - b));
       double d;
       if (!c.number(&d)) return {};
     }
@@ -154,19 +174,42 @@ struct Fresh {
   }
 };
 
-void refresh(std::string* dst, const std::string& src, const std::vector<uint32_t>& slots, Fresh* rng) {
-  dst->assign(src);
-  uint8_t* b = (uint8_t*)&(*dst)[0];
-  for (const uint32_t o : slots) {
-    uint64_t u = 0;
-    for (int k = 0; k < 8; ++k) u = (u << 8) | b[o + k];
-    double v;
-    memcpy(&v, &u, 8);
-    v += rng->half_gauss();
-    memcpy(&u, &v, 8);
-    for (int k = 7; k >= 0; --k) { b[o + k] = (uint8_t)u; u >>= 8; }
-  }
+inline double get_f64(const uint8_t* p) {
+  uint64_t u = 0;
+  for (int k = 0; k < 8; ++k) u = (u << 8) | p[k];
+  double v;
+  memcpy(&v, &u, 8);
+  return v;
 }
+
+// One private request of a connection in fresh mode: a copy of a params
+// object refreshed in place before every send (the kernel has copied the
+// bytes when sendmsg returns, so the buffer is free again)
+struct FreshReq {
+  std::string buf;
+  std::vector<double> base;          // the template's float64 values
+  const FreshSlots* slots = nullptr;
+  void init(const std::string& src, const FreshSlots* sl) {
+    buf = src;
+    slots = sl;
+    base.clear();
+    for (const uint32_t o : sl->f64) base.push_back(get_f64((const uint8_t*)src.data() + o));
+  }
+  void refresh(Fresh* rng) {
+    uint8_t* b = (uint8_t*)&buf[0];
+    for (size_t i = 0; i < slots->f64.size(); ++i) {
+      const double v = base[i] + rng->half_gauss();
+      uint64_t u;
+      memcpy(&u, &v, 8);
+      uint8_t* p = b + slots->f64[i];
+      for (int k = 7; k >= 0; --k) { p[k] = (uint8_t)u; u >>= 8; }
+    }
+    for (const auto& d : slots->digits) {
+      uint64_t r = rng->next();
+      for (uint32_t k = 0; k < d.second; ++k, r /= 10) b[d.first + k] = (uint8_t)('0' + r % 10);
+    }
+  }
+};
 
 struct Result {
   uint64_t done = 0;
@@ -175,7 +218,7 @@ struct Result {
 };
 
 void run_conn(const std::string& host, int port, const std::string& method,
-              const std::vector<std::string>* params, const std::vector<std::vector<uint32_t>>* fresh,
+              const std::vector<std::string>* params, const std::vector<FreshSlots>* fresh,
               uint64_t seed, size_t first, size_t last, bool once, int depth, double secs, Result* r) {
   const int fd = connect_to(host, port);
   if (fd < 0) { r->error = "connect failed"; return; }
@@ -189,9 +232,13 @@ void run_conn(const std::string& host, int port, const std::string& method,
   char buf[1 << 16];
   std::vector<std::string> heads;
   std::vector<const std::string*> bodies;
-  // fresh mode: private copies of the requests of one sendmsg (the kernel
-  // has copied them when send_many returns)
-  std::vector<std::string> priv(fresh ? (size_t)depth : 0);
+  // fresh mode: the connection's depth private requests (templates
+  // first, first + 1, ... of the params), each refreshed before it goes out
+  std::vector<FreshReq> priv(fresh ? (size_t)depth : 0);
+  for (size_t j = 0; j < priv.size(); ++j) {
+    const size_t t = (first + j) % params->size();
+    priv[j].init((*params)[t], &(*fresh)[t]);
+  }
   Fresh rng{seed * 0xD1B54A32D192ED03ull + first};
   while (sending || inflight > 0) {
     // every request the window allows goes out in one sendmsg
@@ -203,9 +250,9 @@ void run_conn(const std::string& host, int port, const std::string& method,
     while (sending && inflight < depth && !(once && which >= last)) {
       heads.push_back(request_head(next, method));
       if (fresh) {
-        std::string* d = &priv[heads.size() - 1];
-        refresh(d, (*params)[which], (*fresh)[which], &rng);
-        bodies.push_back(d);
+        FreshReq& f = priv[heads.size() - 1];
+        f.refresh(&rng);
+        bodies.push_back(&f.buf);
       } else {
         bodies.push_back(&(*params)[which]);
       }
@@ -285,13 +332,12 @@ int main(int argc, char** argv) {
     pos += (size_t)f;
   }
   if (params.empty()) { fprintf(stderr, "empty params file\n"); return 1; }
-  std::vector<std::vector<uint32_t>> slots;
-  uint64_t fresh_samples = 0;
+  std::vector<FreshSlots> slots;
   if (fresh_seed >= 0) {
+    if (once) { fprintf(stderr, "-r: not with -o\n"); return 1; }
     for (const auto& p : params) {
       slots.push_back(fresh_slots(p));
       if (slots.back().empty()) { fprintf(stderr, "-r: params without float64 num values\n"); return 1; }
-      fresh_samples += slots.back().size();
     }
   }
   std::vector<Result> res(conns);

@@ -155,7 +155,13 @@ class LinearClassifier:
 
     def _alloc(self, LC: int) -> None:
         H = self.H
-        self._tables_replaced()
+        # a label re-layout copies every column over and zero-fills the new
+        # ones on every rank alike: the touched map still names every row that
+        # differs across ranks - unless an overlapped MIX was in flight (its
+        # fold is abandoned, and the rows it had taken out of the map were not
+        # reconciled), which makes the next MIX dense
+        if self._mix_job is not None:
+            self._tables_replaced()
         if self.gpu:
             t = self.torch
             W = t.zeros((H, LC), dtype=self._wdt(), device=self.device)

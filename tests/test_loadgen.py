@@ -26,7 +26,8 @@ def _params(tmp_path, n_req=4, per_req=32):
             body = []
             for _ in range(per_req):
                 y = int(rng.integers(2))
-                body.append([f"l{y}", [[["w", "a" if y else "b"]], [["x", float(y)], ["z", 0.5]], []]])
+                body.append([f"l{y}", [[["w", "a" if y else "b"], ["t", f"t{int(rng.integers(100, 999))}"]],
+                                       [["x", float(y)], ["z", 0.5]], []]])
             reqs.append(["", body])
             f.write(msgpack.packb(["", body], use_bin_type=False))
     return str(tmp_path / "p.bin"), reqs
@@ -71,8 +72,8 @@ class Recorder:
 
 
 def _run(port, pfile, *extra):
-    r = subprocess.run([EXE, "-p", str(port), "-m", "train", "-f", pfile, "-c", "2", "-d", "2",
-                        "-o", "1", *extra], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([EXE, "-p", str(port), "-m", "train", "-f", pfile, "-c", "2", "-d", "2", *extra],
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -81,25 +82,30 @@ def test_loadgen_replay_and_fresh_values(tmp_path):
     pfile, reqs = _params(tmp_path)
     rec = Recorder()
     try:
-        out = _run(rec.port, pfile)
+        out = _run(rec.port, pfile, "-o", "1")
         assert out["requests"] == 4 and out["fresh_values"] is False
         assert sorted(map(repr, rec.got)) == sorted(map(repr, reqs))
         rec.got.clear()
-        out = _run(rec.port, pfile, "-r", "7")
-        assert out["requests"] == 4 and out["fresh_values"] is True
-        assert len(rec.got) == 4
-        deltas = []
-        for got in rec.got:
-            # match each received request to its source by the string values
-            src = next(r for r in reqs if all(g[0] == s[0] and g[1][0] == s[1][0] and g[1][1][1] == s[1][1][1]
-                                              for g, s in zip(got[1], r[1])))
-            for g, s in zip(got[1], src[1]):
-                assert g[0] == s[0] and g[1][0] == s[1][0]          # label, strings untouched
-                assert g[1][1][0][0] == "x" and g[1][1][1] == s[1][1][1]   # only x redrawn
-                deltas.append(g[1][1][0][1] - s[1][1][0][1])
+        out = _run(rec.port, pfile, "-t", "0.3", "-r", "7")
+        assert out["fresh_values"] is True and out["requests"] >= 8
+        with rec.lock:
+            got = list(rec.got)
+        deltas, tokens = [], set()
+        for g in got:
+            # the source: same labels and first string values (the templates)
+            src = next(r for r in reqs if all(a[0] == b[0] and a[1][0][0] == b[1][0][0]
+                                              for a, b in zip(g[1], r[1])))
+            for a, b in zip(g[1], src[1]):
+                assert a[1][0][0] == b[1][0][0] and a[1][1][1] == b[1][1][1]  # untouched
+                ta, tb = a[1][0][1][1], b[1][0][1][1]
+                assert ta[0] == "t" and len(ta) == len(tb) and ta[1:].isdigit()   # redrawn digits
+                tokens.add(ta)
+                assert a[1][1][0][0] == "x"
+                deltas.append(a[1][1][0][1] - b[1][1][0][1])
         d = np.asarray(deltas)
         assert np.all(d != 0.0)
-        assert 0.3 < d.std() < 0.7 and abs(d.mean()) < 0.2, (d.mean(), d.std())
+        assert 0.4 < d.std() < 0.6 and abs(d.mean()) < 0.1, (d.mean(), d.std())   # N(0, 1/4) around v
+        assert len(tokens) > 900          # 3-digit tokens: (nearly) all 1000 drawn
     finally:
         rec.close()
 

@@ -49,6 +49,18 @@ def spawn(zport, name, port, extra=(), env=None):
     return subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=log, env=dict(os.environ, **(env or {})))
 
 
+def _logs(name, ports):
+    """the servers' stderr (spawn), for assertion messages"""
+    out = {}
+    for p in ports:
+        try:
+            with open(os.path.join(tempfile.gettempdir(), f"native_dist_{name}_{p}.log"), "rb") as f:
+                out[p] = f.read().decode(errors="replace")[-3000:]
+        except OSError:
+            out[p] = ""
+    return out
+
+
 def stop(procs):
     for p in procs:
         if p.poll() is None:
@@ -109,8 +121,8 @@ def test_native_classifier_distributed_mix(coord):
         assert int(sa["linear_mixer.mix_count"]) >= 1
         # both learnt all four labels through the MIX
         for c in (a, b):
-            assert top(c, Datum({"w": "good"})) == "pos"
-            assert top(c, Datum({"w": "offer"})) == "spam"
+            got = (top(c, Datum({"w": "good"})), top(c, Datum({"w": "offer"})))
+            assert got == ("pos", "spam"), (got, sa, sb, _logs(name, ports))
             assert sorted(c.get_labels()) == ["ham", "neg", "pos", "spam"]
         # label counts are the cluster totals on both
         la, lb = a.get_labels(), b.get_labels()

@@ -75,11 +75,14 @@ def _status(c):
 
 
 def _oracle(cfg_file):
-    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    """the host model of a configuration, at the feature-table height the GPU
+    servers resolve for it (device_hash_max_size when the converter names
+    none), so model files of either load into it"""
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter, device_hash_max_size
     from jubatus_amd.models.classifier import LinearClassifier
     cfg = json.load(open(cfg_file))
-    return LinearClassifier(cfg["method"], cfg.get("parameter"), DatumToFvConverter(cfg["converter"]),
-                            device=None)
+    conv = DatumToFvConverter(cfg["converter"], default_hash_max_size=device_hash_max_size())
+    return LinearClassifier(cfg["method"], cfg.get("parameter"), conv, device=None)
 
 
 def _scores(rows):
@@ -242,7 +245,7 @@ def test_native_regression_matches_oracle_and_files(tmp_path):
     driver, status and clear"""
     from jubatus_amd.client import Regression
     from jubatus_amd.framework import save_load
-    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter, device_hash_max_size
     from jubatus_amd.models.regression import PARegression
     cfg_file = config_path("regression/pa.json")
     cfg = json.load(open(cfg_file))
@@ -260,7 +263,9 @@ def test_native_regression_matches_oracle_and_files(tmp_path):
                 assert p.poll() is None and time.time() < deadline, p.stdout.read()
                 time.sleep(0.2)
         c = Regression("127.0.0.1", port, "", timeout=60)
-        ora = PARegression("PA", cfg.get("parameter"), DatumToFvConverter(cfg["converter"]), device=None)
+        ora = PARegression("PA", cfg.get("parameter"),
+                           DatumToFvConverter(cfg["converter"], default_hash_max_size=device_hash_max_size()),
+                           device=None)
         rng = random.Random(4)
         for _ in range(5):
             chunk = _reg_data(rng, 40)
@@ -279,7 +284,9 @@ def test_native_regression_matches_oracle_and_files(tmp_path):
         (_, path), = c.save("r1").items()
         with open(path, "rb") as f:
             _, pack = save_load.load_server(f, "regression", open(cfg_file).read(), 1, False)
-        ora2 = PARegression("PA", cfg.get("parameter"), DatumToFvConverter(cfg["converter"]), device=None)
+        ora2 = PARegression("PA", cfg.get("parameter"),
+                            DatumToFvConverter(cfg["converter"], default_hash_max_size=device_hash_max_size()),
+                            device=None)
         ora2.unpack(pack)
         np.testing.assert_allclose(ora2.estimate(test), got, rtol=1e-6, atol=1e-6)
         assert c.clear() is True
