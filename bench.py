@@ -668,6 +668,10 @@ def main() -> None:
     ap.add_argument("--exact-steps", type=int, default=3,
                     help="1 GPU: also time this many steps of the serial-equivalent exact mode (same "
                          "warmup, same fresh batches, its own model) and report them under exact_mode")
+    ap.add_argument("--worst-steps", type=int, default=5,
+                    help="1 GPU: also time this many steps (16 batches each) of the headline's update "
+                         "mode on the worst-case stream (noise string values: every sample updates) "
+                         "and report them under worst_case")
     ap.add_argument("--weight-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="storage of the headline model's W table (P and arithmetic stay fp32)")
     ap.add_argument("--bf16-steps", type=int, default=5,
@@ -909,6 +913,18 @@ def main() -> None:
     if world == 1 and device is not None and args.bf16_steps > 0 and args.weight_dtype == "fp32":
         bf16 = exact_record(args, cfg, device, warm, fresh, bps, samples_per_batch, sync,
                             mode=args.update_mode, weight_dtype="bf16", steps=args.bf16_steps)
+    worst = None
+    if world == 1 and device is not None and args.worst_steps > 0 and not args.worst_case:
+        # the headline's update mode on the worst-case stream: string values
+        # are fresh noise, so (almost) every sample updates the model
+        wb = 16
+        ws = FreshStream(nat, torch, pinned, args, 31_337 * (rank + 1) + 5, wb * args.worst_steps,
+                         gen_threads, 0.0, (1 << 31) - 1)
+        worst = exact_record(args, cfg, device, warm, ws, wb, samples_per_batch, sync,
+                             mode=args.update_mode, steps=args.worst_steps)
+        worst["data"] = "worst case: noise string values (every sample a new feature set), fresh stream"
+        worst["batches_per_step"] = wb
+        del ws
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:
         served = served_train(args, local, nat)
@@ -973,6 +989,7 @@ def main() -> None:
             "data_gen_s": round(t_gen, 1),
             "exact_mode": exact,
             "bf16_weights": bf16,
+            "worst_case": worst,
             "served": served,
             "served_native": served_native,
             "engines": engines,

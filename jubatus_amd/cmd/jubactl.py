@@ -19,6 +19,9 @@ from ..common.mprpc import RpcClient
 from .jubavisor import argv_to_wire
 
 
+VISOR_CALL_TIMEOUT = 30.0
+
+
 def _parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="jubactl")
     p.add_argument("-c", "--cmd", required=True, choices=("start", "stop", "save", "load", "status"))
@@ -73,7 +76,9 @@ def send2supervisor(ls, a, out=print) -> int:
         host, port = mb.revert(loc)
         out(f"sending {a.cmd} / {name} to {loc}...", end="")
         try:
-            with RpcClient(host, port, 10.0) as c:
+            # a supervisor's stop waits up to 10 s per child before SIGKILL:
+            # the call gets more than that
+            with RpcClient(host, port, VISOR_CALL_TIMEOUT) as c:
                 r = c.call(a.cmd, name, n, argv_to_wire(argv)) if a.cmd == "start" else c.call(a.cmd, name, n)
         except Exception as e:  # noqa: BLE001
             r = -1

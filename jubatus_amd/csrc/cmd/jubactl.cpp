@@ -22,6 +22,8 @@ namespace {
 
 using jb::cmd::Value;
 
+constexpr double kVisorCallTimeout = 30.0;
+
 std::vector<int> split_counts(int n, int nvisors) {
   if (n == 0) n = nvisors;
   std::vector<int> out;
@@ -65,7 +67,9 @@ int send2supervisor(jb::cmd::Zk& zk, const jb::cmd::Flags& f, const std::string&
     if (!jb::cmd::revert(visors[i], &host, &port)) { printf("failed (bad location).\n"); rc = -1; continue; }
     int64_t r;
     try {
-      jubatus_amd::RpcClient c(host, port, 10.0);
+      // a supervisor's stop waits up to 10 s for each child before SIGKILL
+      // (csrc/visor/jubavisor.cpp terminate): the call gets more than that
+      jubatus_amd::RpcClient c(host, port, kVisorCallTimeout);
       std::vector<Value> params{Value::str(name), Value::integer(counts[i])};
       if (cmd == "start") params.push_back(argv);
       r = c.call_values(cmd, params).as_int();

@@ -126,20 +126,31 @@ struct TopkSrc {
   int flip;
 };
 
+// The distance of row r (n: rows of the source, 0 = r is out of range).
+// Branch-free: an out-of-range row loads row 0 and is masked afterwards, and
+// the norm's address is selected rather than branched on, so the loads of a
+// thread's R rows sit in one basic block and issue back to back (a branch per
+// row made the compiler drain vmcnt after every load: R serial HBM round
+// trips per tile).
 template <int MODE>
 __device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, int64_t r,
                                           const uint64_t* qb, float qn, float& d, int& id) {
-  if (r >= n) { d = INFINITY; id = INT_MAX; return; }
+  const bool in = r < n;
+  const int64_t rr = in ? r : 0;
   if (MODE == 0) {
-    id = (int)r;
-    // every load issued unconditionally (no branch between them): the rows
-    // of a tile are in flight together instead of valid -> bits -> norm
-    const uint8_t ok = s.valid[r];
-    const float b = s.metric == 1 ? s.tnorm[r] : 0.f;
-    int ham = 0;
+    const int64_t w0 = rr * s.words;
+    const uint8_t ok = s.valid[rr];
+    // metric 1 reads the norm; the others read (and ignore) 4 bytes of the
+    // row's own signature, which always exist
+    const float* np = s.metric == 1 ? s.tnorm + rr : reinterpret_cast<const float*>(s.tbits + w0);
+    const float braw = *np;
+    int ham = __popcll(qb[0] ^ s.tbits[w0]);
+    if (s.words > 1) {
 #pragma unroll
-    for (int w = 0; w < kTopMaxWords; ++w)
-      if (w < s.words) ham += __popcll(qb[w] ^ s.tbits[r * s.words + w]);
+      for (int w = 1; w < kTopMaxWords; ++w)
+        if (w < s.words) ham += __popcll(qb[w] ^ s.tbits[w0 + w]);
+    }
+    const float b = s.metric == 1 ? braw : 0.f;
     const float frac = (float)ham / (float)s.hash_num;
     if (s.metric == 1)
       d = sqrtf(fmaxf(0.f, qn * qn + b * b - 2.f * qn * b * __cosf(3.14159265f * frac)));
@@ -147,13 +158,62 @@ __device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, in
       d = frac;
     if (!ok) d = INFINITY;
   } else if (MODE == 1) {
-    id = (int)r;
-    const float v = s.src_d[(int64_t)q * n + r];
+    const float v = s.src_d[(int64_t)q * n + rr];
     d = s.flip ? 1.f - v : v;
     if (!(d < INFINITY) || d != d) d = INFINITY;   // -inf scores / NaN -> absent
   } else {
-    d = s.src_d[(int64_t)q * n + r];
-    id = s.src_i[(int64_t)q * n + r];
+    d = s.src_d[(int64_t)q * n + rr];
+    id = s.src_i[(int64_t)q * n + rr];
+  }
+  if (MODE != 2) id = (int)r;
+  if (!in) { d = INFINITY; id = INT_MAX; }
+}
+
+// R rows at once (nn[u]: n for row u, 0 = out of range). MODE 0 in phases -
+// every row's valid byte, norm and first signature word, then (tables wider
+// than 64 bits only) the other words, then the distances - so the first
+// phase's loads are one basic block and all R rows are in flight together
+template <int MODE, int R>
+__device__ __forceinline__ void load_rows(const TopkSrc& s, int q, const int64_t (&nn)[R],
+                                          const int64_t (&r)[R], const uint64_t* qb, float qn,
+                                          float (&d)[R], int (&id)[R]) {
+  if (MODE != 0) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) load_item<MODE>(s, q, nn[u], r[u], qb, qn, d[u], id[u]);
+    return;
+  }
+  int64_t w0[R];
+  uint8_t ok[R];
+  float braw[R];
+  uint64_t b0[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const int64_t rr = r[u] < nn[u] ? r[u] : 0;
+    w0[u] = rr * s.words;
+    ok[u] = s.valid[rr];
+    const float* np = s.metric == 1 ? s.tnorm + rr : reinterpret_cast<const float*>(s.tbits + w0[u]);
+    braw[u] = *np;
+    b0[u] = s.tbits[w0[u]];
+  }
+  int ham[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) ham[u] = __popcll(qb[0] ^ b0[u]);
+  if (s.words > 1) {
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      for (int w = 1; w < s.words; ++w) ham[u] += __popcll(qb[w] ^ s.tbits[w0[u] + w]);
+  }
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const float frac = (float)ham[u] / (float)s.hash_num;
+    float v;
+    if (s.metric == 1)
+      v = sqrtf(fmaxf(0.f, qn * qn + braw[u] * braw[u] - 2.f * qn * braw[u] * __cosf(3.14159265f * frac)));
+    else
+      v = frac;
+    const bool in = r[u] < nn[u];
+    d[u] = (in && ok[u]) ? v : INFINITY;
+    id[u] = in ? (int)r[u] : INT_MAX;
   }
 }
 
@@ -240,10 +300,17 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
     float d[kTopR];
     int ix[kTopR];
     bool any = false;
+    {
+      int64_t rows[kTopR], nn[kTopR];
+#pragma unroll
+      for (int r = 0; r < kTopR; ++r) {
+        rows[r] = base + (int64_t)r * T + t;
+        nn[r] = rows[r] < b1 ? n : 0;
+      }
+      load_rows<MODE, kTopR>(s, q, nn, rows, qb, qn, d, ix);
+    }
 #pragma unroll
     for (int r = 0; r < kTopR; ++r) {
-      const int64_t row = base + (int64_t)r * T + t;
-      load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
       // MODE 0/1 visit rows in increasing index order, so a row that ties
       // the carry's k-th distance loses the (distance, index) tie-break:
       // drop it too (quantized hamming distances tie a lot). MODE 2 lists
@@ -537,10 +604,14 @@ __global__ __launch_bounds__(NW * 64) void topk_lists_kernel(const TopkSrc s, in
   for (int64_t base = b0; base < b1; base += (int64_t)T * 4) {
     float d[4];
     int ix[4];
+    {   // 4 rows in flight per thread
+      int64_t rows[4], nn[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {   // 4 rows in flight per thread
-      const int64_t row = base + (int64_t)r * T + t;
-      load_item<MODE>(s, q, row < b1 ? n : 0, row, qb, qn, d[r], ix[r]);
+      for (int r = 0; r < 4; ++r) {
+        rows[r] = base + (int64_t)r * T + t;
+        nn[r] = rows[r] < b1 ? n : 0;
+      }
+      load_rows<MODE, 4>(s, q, nn, rows, qb, qn, d, ix);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -957,8 +1028,17 @@ static int topk_fused_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k,
                              int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
                              hipStream_t stream);
 
-// path: -1 default (one launch from 16384 rows up to the sampled path's
-// 2M), 0 tile, 2 one launch
+template <int MODE>
+static int topk_onepass_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, float* scratch_d,
+                               int32_t* scratch_i, float* out_d_host, int32_t* out_i_host,
+                               uint32_t* done_host, uint32_t seq, hipStream_t stream);
+
+// path: -1 default, 0 tile, 2 one launch (grid barriers), 3 one pass. Default (measured at 1M rows,
+// profiles/r03_topk_paths_ab.jsonl): the tile path up to k = kListK (k 10:
+// 58 us vs 86 us one launch, whose two grid barriers cost more than the
+// tile path's second launch), one launch past it (k 100: 94 us vs 224 us,
+// the tile path's per-tile selection grows with k); the sampled path from 2M
+// rows
 static int topk_to_host_any(const uint64_t* qbits, const float* qnorm, int nq,
                             const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
                             int64_t nrows, int words, int hash_num, int metric, int k,
@@ -966,7 +1046,12 @@ static int topk_to_host_any(const uint64_t* qbits, const float* qnorm, int nq,
                             int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
                             hipStream_t stream, int path = -1) {
   const int j = sample_j(nrows, k);
-  if (path == 2 || (path < 0 && j == 0 && nrows >= 16384)) {
+  if (path == 3) {
+    jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
+    return topk_onepass_launch<0>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
+                                  done_host, seq, stream);
+  }
+  if (path == 2 || (path < 0 && j == 0 && nrows >= 16384 && k > jb::kListK)) {
     jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
     return topk_fused_launch<0>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
                                 done_host, seq, stream);
@@ -1537,6 +1622,160 @@ __global__ __launch_bounds__(kFuseThreads) void topk_fused_kernel(
   if (t == 0) done[q] = retry ? (seq | kTopRetry) : seq;
 }
 
+// ---------------------------------------------------------------------------
+// One pass, one launch, no grid barrier (k <= kListK): B blocks of 256
+// threads each stream a contiguous range of rows, 8 rows per thread in flight
+// (every load of a round issued before the first use). A thread keeps its
+// sorted top-KL (distance, row) pairs in registers and inserts only below its
+// current KL-th, so after the first rounds a row costs a compare. The block
+// pops its k best (wave pops, then wave 0) into global candidates (write-
+// through stores, no fence) and counts itself finished; the last block of
+// the query merges the B x k
+// candidates the same way, writes the k results into pinned host memory,
+// resets the counter and publishes done[q]. Every block's range is read once
+// from HBM; the only serialization is the one counter per block.
+constexpr int kOnepassRows = 8;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void topk_onepass_kernel(const TopkSrc s, int64_t n, int64_t per_block,
+                                                           int k, float* __restrict__ cand_d,
+                                                           int32_t* __restrict__ cand_i, int cap,
+                                                           uint32_t* __restrict__ counter,
+                                                           float* __restrict__ out_d,
+                                                           int32_t* __restrict__ out_i,
+                                                           volatile uint32_t* done, uint32_t seq,
+                                                           long long* __restrict__ prof) {
+  constexpr int NW = 4, T = NW * 64, KL = kListK, R = kOnepassRows;
+  // diagnostics (prof != nullptr): realtime stamps (100 MHz) per block:
+  // start, rows done, block pop done, published; the last block adds merge
+  // loads done, final pop done, end
+  auto stamp = [&](int i) {
+    if (prof != nullptr && threadIdx.x == 0)
+      prof[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + i] = (long long)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  __shared__ float s_wd[NW * KL];
+  __shared__ int s_wi[NW * KL];
+  __shared__ float s_cd[KL];
+  __shared__ int s_ci[KL];
+  __shared__ uint64_t s_q[kTopMaxWords];
+  __shared__ int s_last;
+  const int q = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += T) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  float ld[KL];
+  int li[KL];
+#pragma unroll
+  for (int j = 0; j < KL; ++j) { ld[j] = INFINITY; li[j] = INT_MAX; }
+  auto insert = [&](float v, int id) {
+    if (lt_pair(v, id, ld[KL - 1], li[KL - 1])) {
+#pragma unroll
+      for (int j = KL - 1; j > 0; --j) {
+        const bool up = lt_pair(v, id, ld[j - 1], li[j - 1]);
+        const bool here = !up && lt_pair(v, id, ld[j], li[j]);
+        ld[j] = up ? ld[j - 1] : (here ? v : ld[j]);
+        li[j] = up ? li[j - 1] : (here ? id : li[j]);
+      }
+      if (lt_pair(v, id, ld[0], li[0])) { ld[0] = v; li[0] = id; }
+    }
+  };
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  for (int64_t base = b0; base < b1; base += (int64_t)T * R) {
+    float d[R];
+    int ix[R];
+    {
+      int64_t rows[R], nn[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        rows[r] = base + (int64_t)r * T + t;
+        nn[r] = rows[r] < b1 ? n : 0;
+      }
+      load_rows<MODE, R>(s, q, nn, rows, qb, qn, d, ix);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) insert(d[r], ix[r]);
+  }
+  stamp(1);
+  // the block's k best (wave pops, then wave 0) -> s_cd / s_ci
+  auto block_pop = [&]() {
+    wave_pop<KL>(ld, li, k, &s_wd[wv * k], &s_wi[wv * k], lane);
+    __syncthreads();
+    if (wv == 0) {
+      constexpr int M = (NW * KL + 63) / 64;
+      float m[M];
+      int mi[M];
+#pragma unroll
+      for (int j = 0; j < M; ++j) {
+        const int c = lane + 64 * j;
+        m[j] = c < NW * k ? s_wd[c] : INFINITY;
+        mi[j] = c < NW * k ? s_wi[c] : INT_MAX;
+      }
+      __builtin_amdgcn_wave_barrier();
+      sort_regs<M>(m, mi);
+      wave_pop<M>(m, mi, k, s_cd, s_ci, lane);
+    }
+    __syncthreads();
+  };
+  block_pop();
+  stamp(2);
+  // publish the candidates [q][block][k] cross-XCD without a fence
+  // (MI355X_MICROARCH.md, visibility): write-through (sc1) stores, every
+  // storing wave drains them, a barrier, then ONE agent-scope add whose
+  // returned value tells the last block; that block reads them with sc1 loads
+  float* cd = cand_d + (int64_t)q * cap;
+  int32_t* ci = cand_i + (int64_t)q * cap;
+  if (t < k) {
+    __hip_atomic_store(cd + (int64_t)blockIdx.x * k + t, s_cd[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ci + (int64_t)blockIdx.x * k + t, s_ci[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t* qc = counter + (int64_t)q * kFuseSync;     // the query's counter word
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(qc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  stamp(3);
+  if (!s_last) return;
+  // the last block: merge the B x k candidates, 8 pairs in flight per
+  // thread (a load -> insert loop would wait one L2 round trip per pair)
+#pragma unroll
+  for (int j = 0; j < KL; ++j) { ld[j] = INFINITY; li[j] = INT_MAX; }
+  const int nc = (int)gridDim.x * k;
+  for (int j0 = t; j0 < nc; j0 += 8 * T) {
+    float v[8];
+    int vi[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * T < nc ? j0 + u * T : nc - 1;
+      v[u] = __hip_atomic_load(cd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      vi[u] = __hip_atomic_load(ci + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u * T < nc) insert(v[u], vi[u]);
+  }
+  stamp(4);
+  block_pop();
+  stamp(5);
+  float* od = out_d + (int64_t)q * k;
+  int32_t* oi = out_i + (int64_t)q * k;
+  if (t < k) { od[t] = s_cd[t]; oi[t] = s_ci[t]; }
+  if (t == 0) __hip_atomic_store(qc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) done[q] = seq;
+  stamp(6);
+}
+
 }  // namespace jb
 
 // blocks of one fused launch that are resident at once (all queries): the
@@ -1575,7 +1814,33 @@ static int topk_fused_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k,
   return (int)hipGetLastError();
 }
 
+// diagnostics: phase stamps of the one-pass kernel (tools/bench_topk_phases.py)
+static long long* g_topk_prof = nullptr;
+extern "C" void jb_topk_set_prof(long long* prof) { g_topk_prof = prof; }
+
+// one-pass launch (k <= kListK): blocks of 2048 rows (one round of 8 rows a
+// thread) up to 512 blocks; the counter is word 3 of the query's sync words
+// in the zeroed state region (the fused kernel leaves it zero too)
+template <int MODE>
+static int topk_onepass_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, float* scratch_d,
+                               int32_t* scratch_i, float* out_d_host, int32_t* out_i_host,
+                               uint32_t* done_host, uint32_t seq, hipStream_t stream) {
+  if (k > jb::kListK) return -2;
+  uint32_t* counter = (uint32_t*)(scratch_i + kFuseStateOff) + 16 * kRadixBins + 3;
+  constexpr int64_t rows_per_round = 256 * jb::kOnepassRows;
+  int64_t B = (nrows + rows_per_round - 1) / rows_per_round;
+  if (B > 512) B = 512;
+  const int64_t rounds = (nrows + B * rows_per_round - 1) / (B * rows_per_round);
+  const int64_t per_block = rounds * rows_per_round;
+  B = (nrows + per_block - 1) / per_block;
+  hipLaunchKernelGGL(jb::topk_onepass_kernel<MODE>, dim3((unsigned)B, nq), dim3(256), 0, stream, s, nrows,
+                     per_block, k, scratch_d + 64, scratch_i + 64, kCandCap, counter, out_d_host,
+                     out_i_host, (volatile uint32_t*)done_host, seq, g_topk_prof);
+  return (int)hipGetLastError();
+}
+
 // path: 0 tile scan + merge, 1 radix chain (6 launches + memset), 2 one launch
+// (grid barriers), 3 one pass (k <= kListK)
 static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, int path,
                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
@@ -1583,6 +1848,9 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   if (path == 2)
     return topk_fused_launch<1>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
                                 done_host, seq, stream);
+  if (path == 3)
+    return topk_onepass_launch<1>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
+                                  done_host, seq, stream);
   if (path == 0) {
     const int blocks = jb_topk_blocks(nrows, k);
     const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
@@ -1630,8 +1898,10 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   return (int)hipGetLastError();
 }
 
-// path_sel: -1 default (one launch from 16384 rows), 0 tile, 1 radix chain,
-// 2 one launch (A/B in tools/bench_topk_scores.py)
+// path_sel: -1 default (the radix chain from 16384 rows), 0 tile, 1 radix
+// chain, 2 one launch (A/B in tools/bench_topk_scores.py: at 1M rows the
+// chain measured 48-61 us, the one launch 80-86 us, and 6x slower on heavy
+// ties at k = 100; profiles/r03_topk_paths_ab.jsonl)
 extern "C" int jb_topk_scores_direct_path(const float* src_d, int flip, int nq, int64_t nrows,
                                           int k, float* scratch_d, int32_t* scratch_i,
                                           float* out_d_host, int32_t* out_i_host,
@@ -1639,7 +1909,7 @@ extern "C" int jb_topk_scores_direct_path(const float* src_d, int flip, int nq, 
   if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
   if (k > jb::kTopMaxK || nq > 8) return -2;
   jb::TopkSrc s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, src_d, nullptr, flip};
-  const int path = nrows >= 16384 ? (path_sel < 0 ? 2 : path_sel) : 0;
+  const int path = nrows >= 16384 ? (path_sel < 0 ? 1 : path_sel) : 0;
   uint32_t seq = jb::next_seq();
   int rc = topk_scores_launch(s, nq, nrows, k, path, scratch_d, scratch_i, out_d_host,
                               out_i_host, done_host, seq, stream);

@@ -244,6 +244,12 @@ class Star {
     for (int& f : fds_)
       if (f >= 0) { ::shutdown(f, SHUT_RDWR); ::close(f); f = -1; }
   }
+  // from another thread: fail every send / recv in progress at once (the
+  // descriptors stay open until the owner closes them)
+  void interrupt() {
+    for (const int f : fds_)
+      if (f >= 0) ::shutdown(f, SHUT_RDWR);
+  }
 
   std::vector<std::string> allgather(const std::string& mine, double dl) {
     std::vector<std::string> parts((size_t)world_);
@@ -491,9 +497,12 @@ class Group {
     const double dl = now_s() + rdv_timeout_;
     try {
       if (world > 1) {
-        star_ = rank == 0 ? Star::lead(*listener_, cur.epoch, world, dl)
-                          : Star::join(cur.addr, cur.port, cur.epoch, rank, world, dl);
+        std::unique_ptr<Star> st = rank == 0 ? Star::lead(*listener_, cur.epoch, world, dl)
+                                             : Star::join(cur.addr, cur.port, cur.epoch, rank, world, dl);
+        std::lock_guard<std::mutex> g(smu_);
+        star_ = std::move(st);
       } else {
+        std::lock_guard<std::mutex> g(smu_);
         star_.reset(new Star(0, 1));
       }
       rank_ = rank;
@@ -527,9 +536,18 @@ class Group {
     epoch_ = -1;
   }
 
+  // any thread (shutdown): a collective blocked on the control plane - or on
+  // the host data plane, which runs over it - fails now instead of at the
+  // interconnect deadline
+  void interrupt() {
+    std::lock_guard<std::mutex> g(smu_);
+    if (star_) star_->interrupt();
+  }
+
  private:
   void teardown() {
     plane_.reset();
+    std::lock_guard<std::mutex> g(smu_);
     if (star_) star_->close();
     star_.reset();
     rank_ = -1;
@@ -542,6 +560,7 @@ class Group {
   PlaneFactory pf_;
   std::unique_ptr<Listener> listener_;
   std::unique_ptr<Star> star_;
+  std::mutex smu_;                 // star_'s lifetime vs interrupt()
   std::unique_ptr<Plane> plane_;
   std::string plane_name_ = "none";
   int rank_ = -1, world_ = 0;
@@ -657,6 +676,7 @@ class LinearMixer {
       stop_ = true;
       cv_.notify_all();
     }
+    group_->interrupt();     // a MIX in flight fails now (its peers abort their epoch)
     if (th_.joinable()) th_.join();
     running_ = false;
     group_->close();
@@ -734,7 +754,8 @@ class LinearMixer {
         tick();
       } catch (const std::exception& e) {
         if (group_->epoch() >= 0) group_->abort(std::string("collective failed: ") + e.what());
-        std::this_thread::sleep_for(std::chrono::milliseconds(500));
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait_for(g, std::chrono::milliseconds(500), [this] { return stop_; });
       }
     }
   }

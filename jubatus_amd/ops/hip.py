@@ -72,6 +72,7 @@ _SIGS = {
     "jb_topk_blocks": [_i64, _i32],
     "jb_topk_direct_scratch": [_i32],
     "jb_topk_scratch_init": [_c_void_p, _c_void_p],
+    "jb_topk_set_prof": [_c_void_p],
     "jb_topk_direct_query_path": [_c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64,
                                   _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                                   _c_void_p, _c_void_p, _i32, _c_void_p],
@@ -976,11 +977,12 @@ def lsh_query_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, nq: int, hash
 
 
 def topk_scores_direct(scores, nq: int, nrows: int, k: int, flip: bool,
-                       bufs: DirectQueryBuffers):
+                       bufs: DirectQueryBuffers, path: int = -1):
     """exact top-k smallest of a [nq, nrows] score matrix (flip: 1 - score)
     -> (dist [nq, k], row [nq, k]) numpy; sampled threshold + collect + final
     merge written to pinned host memory and waited for (csrc/hip/topk.hip
-    jb_topk_scores_direct)"""
+    jb_topk_scores_direct; path >= 0 forces a path: 0 tile, 1 radix chain,
+    2 one launch with grid barriers, 3 one pass, k <= 16)"""
     import numpy as np
     if not (0 < k <= TOPK_MAX_K and 0 < nq <= QUERY_MAX):
         raise ValueError("topk_scores_direct: k / nq out of range")
@@ -988,8 +990,8 @@ def topk_scores_direct(scores, nq: int, nrows: int, k: int, flip: bool,
     if scores.numel() < nq * nrows:
         raise ValueError("topk_scores_direct: bad operand shapes")
     sd, si = _topk_scratch(scores.device, _direct_scratch(nrows, k, nq))
-    rc = _fn("jb_topk_scores_direct")(_p(scores), 1 if flip else 0, nq, nrows, k, _p(sd), _p(si),
-                                      bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
+    rc = _fn("jb_topk_scores_direct_path")(_p(scores), 1 if flip else 0, nq, nrows, k, _p(sd), _p(si),
+                                           bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, path, _stream())
     _check(rc, "jb_topk_scores_direct")
     d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
     i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()
@@ -1050,17 +1052,19 @@ def lsh_set_rows_direct(idx_ptr: int, val_ptr: int, row_ptr_ptr: int, n: int, sl
 
 
 def topk_rows_direct(qbits, qnorm, nq: int, tbits, tnorm, valid, nrows: int, hash_num: int,
-                     metric: int, k: int, bufs: DirectQueryBuffers):
+                     metric: int, k: int, bufs: DirectQueryBuffers, path: int = -1):
     """queries whose signatures are device rows (gathered table rows): fused
-    scan/top-k straight into pinned host memory -> numpy (dist, row) or None"""
+    scan/top-k straight into pinned host memory -> numpy (dist, row) or None
+    (path >= 0 forces a path: 0 tile, 2 one launch with grid barriers, 3 one
+    pass, k <= 16)"""
     import numpy as np
     words = (hash_num + 63) // 64
     if not (0 < k <= TOPK_MAX_K and words <= TOPK_MAX_WORDS and 0 < nq <= QUERY_MAX):
         return None
     sd, si = _topk_scratch(tbits.device, _direct_scratch(nrows, k, nq))
-    rc = _fn("jb_topk_direct_query")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid),
-                                    nrows, words, hash_num, metric, k, _p(sd), _p(si),
-                                    bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, _stream())
+    rc = _fn("jb_topk_direct_query_path")(_p(qbits), _p(qnorm), nq, _p(tbits), _p(tnorm), _p(valid),
+                                         nrows, words, hash_num, metric, k, _p(sd), _p(si),
+                                         bufs.out_d.ptr, bufs.out_i.ptr, bufs.done.ptr, path, _stream())
     _check(rc, "jb_topk_direct_query")
     d = bufs.out_d.view(np.float32, nq * k).reshape(nq, k).copy()
     i = bufs.out_i.view(np.int32, nq * k).reshape(nq, k).copy()

@@ -452,16 +452,21 @@ def test_topk_16_wave_path_matches_full_sort(k):
                                               ("random", 10, 3, 0), ("ties", 10, 2, 1),
                                               ("ties", 100, 1, 1), ("sparse_valid", 20, 2, 1),
                                               ("levels", 10, 4, 0), ("levels", 31, 2, 2)])
-def test_direct_topk_one_launch_path(case, k, nq, metric):
+@pytest.mark.parametrize("path", [-1, 2, 3])
+def test_direct_topk_one_launch_path(case, k, nq, metric, path):
     """latency top-k below the sampled path's 2M rows: ONE launch
     (csrc/hip/topk.hip topk_fused_kernel: distances cached in LDS, two radix
     levels across grid barriers, last-block selection) == full distance
-    matrix + stable sort. "ties" (every row at one distance: the candidates
+    matrix + stable sort; also the default choice (-1) and the one-pass
+    kernel (3, topk_onepass_kernel: register lists, last-block merge; k <= 16
+    only). "ties" (every row at one distance: the candidates
     overflow the LDS ranking and k > 16 retries on the tile path, k <= 16
     selects from L2), "levels" (8 distinct signatures: ~125k rows per
     distance level) and "sparse_valid" (fewer valid rows than k)"""
     import torch
     from jubatus_amd.ops import hip
+    if path == 3 and k > 16:
+        pytest.skip("the one-pass kernel takes k <= 16")
     d = dev()
     n = 1_000_000
     g = torch.Generator().manual_seed(k + nq + len(case) + metric)
@@ -486,7 +491,7 @@ def test_direct_topk_one_launch_path(case, k, nq, metric):
     hip.hamming_scan(qbd, qnd, nq, tbd, tnd, vd, n, 64, metric, full)
     full = full.cpu().numpy()
     for rep in range(2):                 # the second call checks the state the first left behind
-        od, oi = hip.topk_rows_direct(qbd, qnd, nq, tbd, tnd, vd, n, 64, metric, k, bufs)
+        od, oi = hip.topk_rows_direct(qbd, qnd, nq, tbd, tnd, vd, n, 64, metric, k, bufs, path=path)
         for q in range(nq):
             order = np.argsort(full[q], kind="stable")[:k]
             ref = full[q][order]

@@ -20,7 +20,8 @@ def _oracle(sc, k, flip):
 
 @pytest.mark.parametrize("frac,levels", [(0.01, 0), (0.2, 0), (0.2, 64), (0.00001, 0)])
 @pytest.mark.parametrize("nq", [1, 3])
-def test_scores_topk_matches_oracle(frac, levels, nq):
+@pytest.mark.parametrize("path", [-1, 1, 2, 3])
+def test_scores_topk_matches_oracle(frac, levels, nq, path):
     from jubatus_amd.ops import hip
     dev = torch.device("cuda", 0)
     rows, k = 200_000, 10
@@ -33,7 +34,7 @@ def test_scores_topk_matches_oracle(frac, levels, nq):
             v = np.ceil(v * levels) / levels
         sc[q, m] = v[m]
     bufs = hip.DirectQueryBuffers(dev, 1)
-    dist, idx = hip.topk_scores_direct(torch.from_numpy(sc).to(dev), nq, rows, k, True, bufs)
+    dist, idx = hip.topk_scores_direct(torch.from_numpy(sc).to(dev), nq, rows, k, True, bufs, path=path)
     for q in range(nq):
         rd, ri = _oracle(sc[q], k, True)
         np.testing.assert_allclose(dist[q], rd, atol=1e-6)
@@ -56,8 +57,8 @@ def test_scores_topk_repeated_calls_reset_counters():
         np.testing.assert_array_equal(idx[0], ri)
 
 
-@pytest.mark.parametrize("k", [16, 20])
-def test_scores_topk_ties_list_and_rank_paths(k):
+@pytest.mark.parametrize("k,path", [(16, -1), (20, -1), (16, 2), (20, 2), (16, 3)])
+def test_scores_topk_ties_list_and_rank_paths(k, path):
     """~1000 rows tied at the threshold: k <= 16 merges register lists, larger
     k ranks the candidates (early exit once a candidate is out of the top k)"""
     from jubatus_amd.ops import hip
@@ -68,7 +69,7 @@ def test_scores_topk_ties_list_and_rank_paths(k):
     m = rng.random(rows) < 0.2
     sc[0, m] = np.ceil(rng.random(rows)[m] * 60) / 60
     bufs = hip.DirectQueryBuffers(dev, 1)
-    dist, idx = hip.topk_scores_direct(torch.from_numpy(sc).to(dev), 1, rows, k, True, bufs)
+    dist, idx = hip.topk_scores_direct(torch.from_numpy(sc).to(dev), 1, rows, k, True, bufs, path=path)
     rd, ri = _oracle(sc[0], k, True)
     np.testing.assert_allclose(dist[0], rd, atol=1e-6)
     np.testing.assert_array_equal(idx[0], ri)

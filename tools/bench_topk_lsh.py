@@ -45,7 +45,9 @@ def main():
             qn = torch.rand(nq, generator=g)
             t = tuple(x.to(d) for x in (qb, qn, tb, tn, valid))
             ref = None
-            for name, path in (("tile", 0), ("fused", 2)):
+            for name, path in (("tile", 0), ("fused", 2), ("onepass", 3), ("default", -1)):
+                if path == 3 and k > 16:
+                    continue
                 lat = []
                 for it in range(a.iters + 20):
                     t0 = time.perf_counter()

@@ -17,7 +17,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from jubatus_amd.ops import hip  # noqa: E402
 
-PATHS = {"tile": 0, "chain": 1, "fused": 2}
+PATHS = {"tile": 0, "chain": 1, "fused": 2, "onepass": 3, "default": -1}
 
 
 def run(sc, nq, rows, k, path, bufs):
@@ -35,7 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=300)
-    ap.add_argument("--paths", default="chain,fused")
+    ap.add_argument("--paths", default="chain,fused,onepass,default")
     a = ap.parse_args()
     d = torch.device("cuda", 0)
     bufs = hip.DirectQueryBuffers(d, 8)
@@ -52,6 +52,8 @@ def main():
                 dist_ref = (1.0 - sc).cpu().numpy()
                 ref_i = [np.lexsort((np.arange(a.rows), dist_ref[q]))[:k] for q in range(nq)]
                 for path in a.paths.split(","):
+                    if path == "onepass" and k > 16:
+                        continue
                     torch.cuda.synchronize()
                     lat = []
                     ok = True
