@@ -547,7 +547,8 @@ def fresh_budget(fresh_gb: float, local_ranks: int) -> float:
 
 
 def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: int, sync,
-                 mode: str = "exact", weight_dtype: str = "fp32", steps: int | None = None) -> dict:
+                 mode: str = "exact", weight_dtype: str = "fp32", steps: int | None = None,
+                 hot_rows: bool = False) -> dict:
     """The headline protocol in another configuration: a fresh model, the
     same warmup, then timed steps over the first fresh batches. Default: the
     serial-equivalent update mode (``--exact-steps`` steps), whose result
@@ -558,6 +559,7 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
     from jubatus_amd.models.classifier import LinearClassifier
     clf = LinearClassifier(cfg["method"], cfg["parameter"], DatumToFvConverter(cfg["converter"]),
                            device=device, concurrent_update=mode, weight_dtype=weight_dtype)
+    clf.hot_rows = hot_rows
     for y in range(args.labels):
         clf.set_label(f"label{y}")
 
@@ -586,7 +588,7 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
     n = samples_per_batch * bps * steps
     out = {"value": round(n / elapsed, 1), "unit": "samples/s", "steps": steps,
            "ms_per_step": round(elapsed / steps * 1e3, 3), "update_fraction": round(updated / max(1, trained), 5),
-           "concurrent_update": mode, "weight_dtype": weight_dtype}
+           "concurrent_update": mode, "weight_dtype": weight_dtype, "hot_rows": hot_rows}
     if mode == "exact":
         out["semantics"] = "serial-equivalent (requests applied one after another)"
         out["last_batch"] = clf._serial.last_batch() if getattr(clf, "_serial", None) is not None else None
@@ -924,6 +926,12 @@ def main() -> None:
                              mode=args.update_mode, steps=args.worst_steps)
         worst["data"] = "worst case: noise string values (every sample a new feature set), fresh stream"
         worst["batches_per_step"] = wb
+        # the same with the hot-row LDS replica (opt-in, JUBATUS_HOT_ROWS=1:
+        # rows every stream writes - here the 8 numeric keys - are merged in
+        # LDS instead of contended with device-scope atomics)
+        hot = exact_record(args, cfg, device, warm, ws, wb, samples_per_batch, sync,
+                           mode=args.update_mode, steps=args.worst_steps, hot_rows=True)
+        worst["hot_rows_replica"] = {k: hot[k] for k in ("value", "ms_per_step", "update_fraction")}
         del ws
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:

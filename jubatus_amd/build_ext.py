@@ -191,7 +191,7 @@ SERVERS = {
 }
 HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph", "jubaweight", "jubaconv"}
 # servers with a native distributed mode (the model plane over RCCL)
-RCCL_SERVERS = {"jubaclassifier", "jb_rccl_check"}
+RCCL_SERVERS = {"jubaclassifier", "jubaregression", "jb_rccl_check"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:

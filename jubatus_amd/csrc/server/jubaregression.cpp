@@ -31,10 +31,16 @@
 #include <vector>
 
 #include "jb_hostfv.hpp"
+#include "jb_mix_device.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_rpc.hpp"
 #include "jb_server_common.hpp"
 #include "jb_value.hpp"
+
+extern "C" int jb_mix_gather(const float* W, const float* S, int LC, const int64_t* rows, int64_t n,
+                             const int32_t* map, int Lc, float* snap, hipStream_t st);
+extern "C" int jb_mix_fold(float* W, float* S, int LC, const int64_t* rows, int64_t n, const int32_t* map,
+                           int Lc, const float* snap, const float* red, float inv_n, hipStream_t st);
 
 extern "C" int jb_regression_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                    const float* targets, const int64_t* stream_ptr, int nstreams,
@@ -100,7 +106,7 @@ struct HostVec {   // growable host array (realloc keeps the contents)
   }
 };
 
-class Regression {
+class Regression : public jb::mix::Mixable {
  public:
   std::atomic<uint64_t> update_count{0}, train_calls{0}, train_batches{0};
 
@@ -113,6 +119,7 @@ class Regression {
   void configure(const Config& cfg) {
     std::lock_guard<std::mutex> g(mu_);
     HIPCHK(hipStreamSynchronize(stream_));
+    ++gen_;
     cfg_ = cfg;
     const Rules& r = cfg.rules;
     hasher_.reset(new jb::HostFvHasher((const uint8_t*)r.s.data(), (int)r.s.size(),
@@ -207,7 +214,101 @@ class Regression {
   void clear() {
     update_count += 1;
     std::lock_guard<std::mutex> g(mu_);
+    ++gen_;
     clear_locked();
+  }
+
+  // ------------------------------------------------------------ MIX
+  // distributed mode: the linear mixer (jb_mix_group.hpp) runs mix() /
+  // hand_over() on its thread. The model is small and dense (w[H] + the 3
+  // target statistics), so a MIX is the mean of the whole table, as the
+  // Python twin's (models/regression.py mix: all-reduce mean of w and stats;
+  // reference: regression's linear mixable, get_diff / put_diff of w).
+  // Training goes on during the collective: the table is snapshotted behind
+  // the queued training, the snapshot is SUM-reduced, and the fold adds
+  // mean - snapshot, so updates made meanwhile are kept.
+  void enable_mix() {
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipStreamCreateWithFlags(&mixs_, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&mix_ev_, hipEventDisableTiming));
+    const int32_t zero = 0;
+    HIPCHK(hipMemcpy(map_.get(1), &zero, 4, hipMemcpyHostToDevice));
+    mixing_ = true;
+  }
+  bool distributed() const { return mixing_; }
+
+  std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& star, double dl) {
+    return jb::mix::make_device_plane(star, device_, mixs_, dl);
+  }
+
+  uint64_t mix(jb::mix::Group& grp) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    uint64_t gen, H;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      gen = gen_;
+      H = cfg_.rules.H;
+      // snapshot (behind the queued training): [w | stats] -> snap, red
+      if (jb_mix_gather(w_, nullptr, 1, nullptr, (int64_t)H, map_.p, 1, snap_.get(H + 3), stream_) != 0)
+        throw std::runtime_error("jb_mix_gather failed");
+      HIPCHK(hipMemcpyAsync(snap_.p + H, stats_, 12, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(red_.get(H + 3), snap_.p, (H + 3) * 4, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipEventRecord(mix_ev_, stream_));
+      HIPCHK(hipStreamWaitEvent(mixs_, mix_ev_, 0));
+    }
+    // every member checks the layout (a different table height cannot mix)
+    int64_t hh[2] = {(int64_t)H, -(int64_t)H};
+    star.allreduce_max(hh, 2, grp.deadline());
+    if (hh[0] != -hh[1]) throw std::runtime_error("mix: members disagree on hash_max_size");
+    pl.allreduce_sum(red_.p, H + 3, grp.deadline());
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipEventRecord(mix_ev_, mixs_));
+    HIPCHK(hipStreamWaitEvent(stream_, mix_ev_, 0));
+    if (gen != gen_) {          // cleared / reconfigured / loaded meanwhile: nothing to fold into
+      last_applied_ = false;
+      return (H + 3) * 4;
+    }
+    const float inv = 1.f / (float)grp.world();
+    if (jb_mix_fold(w_, nullptr, 1, nullptr, (int64_t)H, map_.p, 1, snap_.p, red_.p, inv, stream_) != 0)
+      throw std::runtime_error("jb_mix_fold failed");
+    float sn[3], rd[3], cur[3];
+    HIPCHK(hipMemcpyAsync(sn, snap_.p + H, 12, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipMemcpyAsync(rd, red_.p + H, 12, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipMemcpyAsync(cur, stats_, 12, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    for (int i = 0; i < 3; ++i) cur[i] += rd[i] * inv - sn[i];
+    HIPCHK(hipMemcpy(stats_, cur, 12, hipMemcpyHostToDevice));
+    last_applied_ = true;
+    ++mixes_;
+    return (H + 3) * 4;
+  }
+
+  // obsolete protocol: rank src sends w and stats; apply = take them
+  void hand_over(jb::mix::Group& grp, int src, bool apply) override {
+    jb::mix::Plane& pl = grp.plane();
+    uint64_t H;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      H = cfg_.rules.H;
+      if (grp.rank() == src) {
+        HIPCHK(hipMemcpyAsync(red_.get(H + 3), w_, H * 4, hipMemcpyDeviceToDevice, stream_));
+        HIPCHK(hipMemcpyAsync(red_.p + H, stats_, 12, hipMemcpyDeviceToDevice, stream_));
+      } else {
+        red_.get(H + 3);
+      }
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+    int64_t hh[2] = {(int64_t)H, -(int64_t)H};
+    grp.star().allreduce_max(hh, 2, grp.deadline());
+    if (hh[0] != -hh[1]) throw std::runtime_error("hand-over: members disagree on hash_max_size");
+    pl.bcast(red_.p, (H + 3) * 4, src, grp.deadline());
+    if (!apply || grp.rank() == src) return;
+    std::lock_guard<std::mutex> g(mu_);
+    ++gen_;
+    HIPCHK(hipMemcpyAsync(w_, red_.p, H * 4, hipMemcpyDeviceToDevice, stream_));
+    HIPCHK(hipMemcpyAsync(stats_, red_.p + H, 12, hipMemcpyDeviceToDevice, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
   }
 
   // models/regression.py pack(): the nonzero rows of w, the target statistics
@@ -248,6 +349,7 @@ class Regression {
     if (!rv || !wv || rv->s.size() / 8 != wv->s.size() / 4 || !sv || sv->kind != Value::ARR || sv->a.size() != 3)
       throw std::runtime_error("broken model data: regression tables");
     std::lock_guard<std::mutex> g(mu_);
+    ++gen_;
     const uint64_t Hn = cfg_.rules.H;
     std::vector<float> w(Hn, 0.f);
     const int64_t* rows = (const int64_t*)rv->s.data();
@@ -273,6 +375,11 @@ class Regression {
     add("batching.train.launches", std::to_string(train_batches.load()));
     add("train.samples_trained", std::to_string(samples_));
     add("device", "cuda:" + std::to_string(device_));
+    if (mixing_) {
+      add("mix.mode", "dense");
+      add("mix.last_applied", last_applied_ ? "1" : "0");
+      add("mix.applied_count", std::to_string(mixes_));
+    }
   }
 
  private:
@@ -324,6 +431,14 @@ class Regression {
   Config cfg_;
   int device_;
   hipStream_t stream_;
+  // MIX state: table generation (bumped when the tables are replaced), the
+  // mixer's stream / event, snapshot and reduction buffers [w | stats]
+  uint64_t gen_ = 0, mixes_ = 0;
+  bool mixing_ = false, last_applied_ = false;
+  hipStream_t mixs_ = nullptr;
+  hipEvent_t mix_ev_ = nullptr;
+  DevBuf<float> snap_, red_;
+  DevBuf<int32_t> map_;
   float* w_ = nullptr;
   float* stats_ = nullptr;
   uint64_t samples_ = 0;
@@ -359,11 +474,41 @@ class Server {
     logf_("INFO", "start listening at port %d", port);
     cs_.start_time = time(nullptr);
     rpc_->start();
+    if (node_) {   // distributed mode: register, then the mixer thread
+      node_->register_actor(a_.eth, a_.port);
+      jb::mix::MixerArgs ma;
+      ma.type = "regression";
+      ma.name = a_.name;
+      ma.eth = a_.eth;
+      ma.port = a_.port;
+      ma.interval_sec = a_.interval_sec;
+      ma.interval_count = a_.interval_count;
+      ma.interconnect_timeout = a_.ic_timeout;
+      Regression* r = reg_.get();
+      mixer_.reset(new jb::mix::LinearMixer(node_->coord(), ma, r, [r](jb::mix::Group& g, double dl) {
+        return r->make_plane(g.star(), dl);
+      }));
+      mixer_->start();
+      logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
+    }
     logf_("INFO", "jubaregression RPC server startup (native)");
     wait_for_term();
+    if (mixer_) {
+      logf_("INFO", "stopping mixer thread");
+      mixer_->stop();
+    }
+    if (node_) node_->leave();
     logf_("INFO", "stopping RPC server");
     rpc_->stop();
     return 0;
+  }
+
+  // distributed mode (-z): coordinator session, config lock, MIX state
+  void join_cluster(std::unique_ptr<jb::mix::ClusterNode> node) {
+    node_ = std::move(node);
+    a_.connected_zookeeper = node_->connected();
+    if (!node_->config_rlock()) throw std::runtime_error("failed to get config lock");
+    reg_->enable_mix();
   }
 
  private:
@@ -396,6 +541,7 @@ class Server {
     }
     try {
       if (method == "train") {
+        if (mixer_) mixer_->updated(bodies.size());
         std::vector<int64_t> res;
         reg_->train(bodies, &res);
         for (size_t j = 0; j < where.size(); ++j) {
@@ -447,6 +593,7 @@ class Server {
     size_t want = 0;
     for (const auto& x : arity)
       if (x.first == m) want = x.second;
+    if (m == "do_mix" && mixer_) want = 1;
     if (want == 0) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
     if (args.a.size() != want || ((m == "save" || m == "load") && !args.a[1].is_str()))
       return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
@@ -482,10 +629,13 @@ class Server {
           common_status(a_, cs_, reg_->update_count.load(), &st);
         }
         reg_->status(&st);
+        if (mixer_) mixer_->status(&st);
         w.map(1);
         w.raw(ident());
         w.map(st.size());
         for (auto& kv : st) { w.raw(kv.first); w.raw(kv.second); }
+      } else if (m == "do_mix") {
+        w.boolean(mixer_->do_mix());
       } else {   // train / estimate outside the batch path (not reached: batched methods)
         std::vector<jb::RpcRequest> one{r};
         return batch(m, one)[0];
@@ -529,6 +679,8 @@ class Server {
 
   Args a_;
   std::unique_ptr<Regression> reg_;
+  std::unique_ptr<jb::mix::ClusterNode> node_;
+  std::unique_ptr<jb::mix::LinearMixer> mixer_;
   std::unique_ptr<jb::RpcServer> rpc_;
   std::mutex st_mu_;
   CommonStatus cs_;
@@ -543,7 +695,7 @@ int main(int argc, char** argv) {
   Config cfg;
   const int rc = startup(argc, argv, &a, &text, [&cfg](const std::string& t, std::string* why) {
     return parse_config(t, &cfg, why);
-  });
+  }, true, true);
   if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
   try {
@@ -551,7 +703,12 @@ int main(int argc, char** argv) {
     logf_("INFO", "starting jubaregression %s RPC server at %s:%d (native, device %d)", kVersion,
           a.eth.c_str(), a.port, device);
     Server srv(a, cfg, device);
-    if (!a.model_file.empty()) srv.load_file(a.model_file);
+    if (!a.zookeeper.empty()) {
+      srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
+          new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), "regression", a.name)));
+    } else if (!a.model_file.empty()) {
+      srv.load_file(a.model_file);
+    }
     return srv.run();
   } catch (const std::exception& e) {
     logf_("FATAL", "failed to start regression: %s", e.what());

@@ -42,9 +42,9 @@ def coord():
     srv.stop()
 
 
-def spawn(zport, name, port, extra=(), env=None):
+def spawn(zport, name, port, extra=(), env=None, exe="jubaclassifier"):
     log = open(os.path.join(tempfile.gettempdir(), f"native_dist_{name}_{port}.log"), "wb")
-    cmd = [os.path.join(NB, "jubaclassifier"), "-z", f"127.0.0.1:{zport}", "-n", name, "-p", str(port),
+    cmd = [os.path.join(NB, exe), "-z", f"127.0.0.1:{zport}", "-n", name, "-p", str(port),
            "-b", "127.0.0.1", "-s", "0", "-i", "0", "-I", "5", "-Z", "5", *extra]
     return subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=log, env=dict(os.environ, **(env or {})))
 
@@ -71,10 +71,10 @@ def stop(procs):
                 p.kill()
 
 
-def wait_actives(ls, name, n, timeout=90):
+def wait_actives(ls, name, n, timeout=90, engine="classifier"):
     deadline = time.time() + timeout
     while time.time() < deadline:
-        if len(mb.get_all_actives(ls, "classifier", name)) >= n:
+        if len(mb.get_all_actives(ls, engine, name)) >= n:
             return True
         time.sleep(0.2)
     return False
@@ -178,4 +178,41 @@ def test_native_stalled_rank_watchdog_aborts_and_regroups(coord):
         b.close()
     finally:
         stop([good, slow])
+        ls.close()
+
+
+def test_native_regression_distributed_mix(coord):
+    """native jubaregression in distributed mode (csrc/server/jubaregression.cpp
+    Mixable over the same linear mixer): two servers train different
+    features, one MIX averages w and the target statistics, so both then
+    estimate alike and know both features (models/regression.py mix: the
+    mean of w and stats)"""
+    from jubatus_amd.client import Regression
+    ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+    name = "nreg"
+    zkconfig.config_tozk(ls, "regression", name, open(os.path.join(ROOT, "config/regression/pa.json")).read())
+    ports = [free_port(), free_port()]
+    procs = [spawn(coord.port, name, p, exe="jubaregression") for p in ports]
+    try:
+        for p in ports:
+            assert wait_server("127.0.0.1", p, 90)
+        assert wait_actives(ls, name, 2, engine="regression")
+        a = Regression("127.0.0.1", ports[0], name, timeout=60.0)
+        b = Regression("127.0.0.1", ports[1], name, timeout=60.0)
+        assert a.train([(4.0, Datum({"x": 1.0}))] * 8) == 8
+        assert b.train([(-2.0, Datum({"z": 1.0}))] * 8) == 8
+        before = (a.estimate([Datum({"z": 1.0})])[0], b.estimate([Datum({"x": 1.0})])[0])
+        assert before == (0.0, 0.0)          # neither knows the other's feature yet
+        assert a.do_mix() is True
+        for st in (status(a), status(b)):
+            assert st["server_runtime"] == "native" and st["linear_mixer.runtime"] == "native", st
+            assert st["linear_mixer.group_size"] == "2" and st["mix.last_applied"] == "1", st
+        probe = [Datum({"x": 1.0}), Datum({"z": 1.0})]
+        ea, eb = a.estimate(probe), b.estimate(probe)
+        assert ea == pytest.approx(eb, abs=1e-5), (ea, eb)
+        assert ea[0] > 0.5 and ea[1] < -0.2, ea     # both features, each at about half its weight
+        a.close()
+        b.close()
+    finally:
+        stop(procs)
         ls.close()
