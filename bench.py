@@ -528,9 +528,86 @@ def engine_records(args, local: int) -> dict:
             except subprocess.TimeoutExpired:
                 p.kill()
         out[name] = rec
+    for method in ("kmeans", "gmm"):
+        name = f"clustering_{method}"
+        if args.engines != "all" and name not in args.engines.split(","):
+            continue
+        _progress(f"engine {name}: push")
+        out[name] = _clustering_record(args, local, method, exe, tmp)
     out["row_gen_s"] = round(t_gen, 1)
     shutil.rmtree(tmp, ignore_errors=True)
     return out
+
+
+def _clustering_record(args, local: int, method: str, exe: str, tmp: str) -> dict:
+    """BASELINE config #5 on one GPU: the native jubaclustering
+    (config/clustering/<method>.json, coresets + k-means++ / Lloyd / GMM EM
+    on the device) fed push requests of 1000 points each (3 numeric features
+    + 1 string, three well-separated blobs) over RPC by the native load
+    generator, then get_nearest_center over RPC (1 connection, 1 in flight)"""
+    from jubatus_amd.common.mprpc import RpcClient
+    cfg = f"config/clustering/{method}.json"
+    rec: dict = {"config": cfg, "server": "native jubaclustering (no Python)"}
+    rng = np.random.default_rng(5)
+    centers = np.array([[0.0, 0.0, 0.0], [10.0, 10.0, 0.0], [-10.0, 10.0, 5.0]])
+    npts, per = args.cluster_points, 1000
+    push = os.path.join(tmp, f"{method}_push.bin")
+    with open(push, "wb") as f:
+        for b in range(0, npts, per):
+            pts = []
+            for i in range(per):
+                c = centers[(b + i) % 3] + rng.normal(0, 0.5, 3)
+                pts.append([[["tag", f"t{(b + i) % 7}"]], [["a", float(c[0])], ["b", float(c[1])],
+                                                          ["c", float(c[2])]], []])
+            f.write(msgpack.packb(["", pts], use_bin_type=False))
+    q = os.path.join(tmp, f"{method}_query.bin")
+    with open(q, "wb") as f:
+        for i in range(512):
+            c = centers[i % 3] + rng.normal(0, 0.5, 3)
+            f.write(msgpack.packb(["", [[["tag", f"t{i % 7}"]], [["a", float(c[0])], ["b", float(c[1])],
+                                                                 ["c", float(c[2])]], []]],
+                                  use_bin_type=False))
+    port = _free_port()
+    srv = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaclustering")
+    p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", os.path.join(ROOT, cfg), "-d", tmp,
+                          "-c", "4", "--gpu", str(local)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        deadline = time.time() + 60
+        while True:
+            try:
+                with RpcClient("127.0.0.1", port, 30.0) as c:
+                    (_, st), = c.call("get_status", "").items()
+                break
+            except Exception:  # noqa: BLE001 - not listening yet
+                if p.poll() is not None or time.time() > deadline:
+                    raise RuntimeError((p.stderr.read() or b"").decode(errors="replace")[-300:])
+                time.sleep(0.2)
+        st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
+              for k, v in st.items()}
+        if st.get("server_runtime") != "native":
+            raise RuntimeError("the binary handed the configuration to the Python server")
+        t0 = time.perf_counter()
+        r = _loadgen(exe, port, "push", push, 1, 2, once=True)
+        dt = time.perf_counter() - t0
+        rec["points"] = npts
+        rec["push_points_per_s"] = round(npts / dt, 1)
+        rec["push_rpc_p50_us"] = r["p50_us"]
+        lat = _loadgen(exe, port, "get_nearest_center", q, 1, 1, secs=args.engine_seconds)
+        rec["get_nearest_center_p50_us"] = lat["p50_us"]
+        rec["get_nearest_center_p99_us"] = lat["p99_us"]
+        with RpcClient("127.0.0.1", port, 30.0) as c:
+            rec["revision"] = int(c.call("get_revision", ""))
+        rec["rpc"] = ("loopback TCP, native jubaloadgen; push: 1000-point requests, 1 connection x 2 in "
+                      "flight (order kept); get_nearest_center: 1 connection x 1 in flight")
+    except Exception as e:  # noqa: BLE001 - recorded, the headline still prints
+        rec["error"] = f"{type(e).__name__}: {e}"[:400]
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rec
 
 
 PIN_FRACTION = 0.6       # of MemAvailable, shared by the node's local ranks
@@ -642,12 +719,14 @@ def main() -> None:
     ap.add_argument("--latency-iters", type=int, default=300)
     ap.add_argument("--engines", default="all",
                     help="engine records (N = 1): all, none, or a comma list of "
-                         + ", ".join(c[0] for c in ENGINE_CASES))
+                         + ", ".join(c[0] for c in ENGINE_CASES) + ", clustering_kmeans, clustering_gmm")
     ap.add_argument("--engine-rows", type=int, default=1_000_000,
                     help="rows filled into the recommender servers before their queries")
     ap.add_argument("--lof-rows", type=int, default=100_000,
                     help="rows added to the LOF server before its queries")
     ap.add_argument("--engine-seconds", type=float, default=3.0)
+    ap.add_argument("--cluster-points", type=int, default=200_000,
+                    help="points pushed into each clustering server (kmeans.json, gmm.json)")
     ap.add_argument("--no-rpc", action="store_true",
                     help="skip the served-path measurement (jubaclassifier + jubaloadgen, N = 1)")
     ap.add_argument("--served-runtime", choices=("python", "native", "both"), default="both",

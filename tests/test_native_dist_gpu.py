@@ -86,6 +86,18 @@ def status(c):
             for k, v in st.items()}
 
 
+def wait_group(a, b, n, timeout=60):
+    """both servers in one n-member group, neither obsolete"""
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        sa, sb = status(a), status(b)
+        if all(st.get("linear_mixer.group_size") == str(n) and st.get("linear_mixer.is_obsolete") == "0"
+               for st in (sa, sb)):
+            return True
+        time.sleep(0.2)
+    return False
+
+
 def top(c, d):
     return max(c.classify([d])[0], key=lambda e: e.score).label
 
@@ -109,6 +121,10 @@ def test_native_classifier_distributed_mix(coord):
         assert wait_actives(ls, name, 2)
         a = Classifier("127.0.0.1", ports[0], name, timeout=60.0)
         b = Classifier("127.0.0.1", ports[1], name, timeout=60.0)
+        # the two-member group has formed and its hand-over is done: a member
+        # still obsolete then would take the other's model (the obsolete
+        # protocol), replacing what it trained in between
+        assert wait_group(a, b, 2)
         # each server learns a different pair of labels
         a.train([("pos", Datum({"w": "good"})), ("neg", Datum({"w": "bad"}))] * 8)
         b.train([("spam", Datum({"w": "offer"})), ("ham", Datum({"w": "meeting"}))] * 8)
@@ -199,6 +215,7 @@ def test_native_regression_distributed_mix(coord):
         assert wait_actives(ls, name, 2, engine="regression")
         a = Regression("127.0.0.1", ports[0], name, timeout=60.0)
         b = Regression("127.0.0.1", ports[1], name, timeout=60.0)
+        assert wait_group(a, b, 2)
         assert a.train([(4.0, Datum({"x": 1.0}))] * 8) == 8
         assert b.train([(-2.0, Datum({"z": 1.0}))] * 8) == 8
         before = (a.estimate([Datum({"z": 1.0})])[0], b.estimate([Datum({"x": 1.0})])[0])
