@@ -94,7 +94,18 @@ class CollectiveMixer(Mixer):
         with self._lock:
             self._lock.notify_all()
         if self._thread is not None:
-            self._thread.join(timeout=10.0)
+            self._thread.join(timeout=0.5)
+            if self._thread.is_alive() and self.group is not None and self.group.epoch >= 0:
+                # a collective in flight would hold the shutdown for the whole
+                # interconnect timeout: abort it (the watchdog's abort; the
+                # peers then leave the epoch too)
+                self.group.abort("server stopping")
+            self._thread.join(timeout=2.0)
+            if self._thread.is_alive():
+                # still inside a group rendezvous (its timeout is several
+                # interconnect timeouts): the thread is a daemon, the server
+                # goes on stopping without it
+                log.warning("mixer thread still in a collective or rendezvous: not waiting for it")
         self.running = False
         if self.group is not None:
             self.group.close()
