@@ -257,10 +257,20 @@ class Regression : public jb::mix::Mixable {
       HIPCHK(hipEventRecord(mix_ev_, stream_));
       HIPCHK(hipStreamWaitEvent(mixs_, mix_ev_, 0));
     }
-    // every member checks the layout (a different table height cannot mix)
-    int64_t hh[2] = {(int64_t)H, -(int64_t)H};
-    star.allreduce_max(hh, 2, grp.deadline());
+    // every member checks the layout (a different table height cannot mix),
+    // and a member whose tables were replaced since its snapshot makes the
+    // whole group skip the fold (slot 2: max of "replaced")
+    int64_t hh[3] = {(int64_t)H, -(int64_t)H, 0};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      hh[2] = gen != gen_ ? 1 : 0;
+    }
+    star.allreduce_max(hh, 3, grp.deadline());
     if (hh[0] != -hh[1]) throw std::runtime_error("mix: members disagree on hash_max_size");
+    if (hh[2] != 0) {
+      last_applied_ = false;
+      return 24;
+    }
     pl.allreduce_sum(red_.p, H + 3, grp.deadline());
     std::lock_guard<std::mutex> g(mu_);
     HIPCHK(hipEventRecord(mix_ev_, mixs_));
