@@ -135,7 +135,11 @@ def test_native_classifier_distributed_mix(coord):
             assert st["linear_mixer.group_size"] == "2" and st["is_standalone"] == "0"
             assert st["linear_mixer.backend"] == "host"      # both on one GPU: the staged plane
         assert int(sa["linear_mixer.mix_count"]) >= 1
-        # both learnt all four labels through the MIX
+        # both learnt all four labels through the MIX (the peer's fold may
+        # still be running when do_mix returns here)
+        deadline = time.time() + 30
+        while time.time() < deadline and int(status(b).get("linear_mixer.mix_count", "0")) < 1:
+            time.sleep(0.1)
         for c in (a, b):
             got = (top(c, Datum({"w": "good"})), top(c, Datum({"w": "offer"})))
             assert got == ("pos", "spam"), (got, sa, sb, _logs(name, ports))
@@ -221,6 +225,11 @@ def test_native_regression_distributed_mix(coord):
         before = (a.estimate([Datum({"z": 1.0})])[0], b.estimate([Datum({"x": 1.0})])[0])
         assert before == (0.0, 0.0)          # neither knows the other's feature yet
         assert a.do_mix() is True
+        # do_mix returns when this server's MIX is done; the peer folds on its
+        # own mixer thread
+        deadline = time.time() + 30
+        while time.time() < deadline and status(b).get("mix.applied_count") in (None, "0"):
+            time.sleep(0.1)
         for st in (status(a), status(b)):
             assert st["server_runtime"] == "native" and st["linear_mixer.runtime"] == "native", st
             assert st["linear_mixer.group_size"] == "2" and st["mix.last_applied"] == "1", st
