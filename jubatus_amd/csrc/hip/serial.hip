@@ -52,8 +52,17 @@ constexpr int kStepList = 64;        // distinct rows of one step the table hold
 // model with an empty table), or too many updates per round (the rest goes
 // to the sequential kernel)
 constexpr int kTailReason = 20;
-constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2;
-constexpr int kSerialSegments = 4;
+// kStopRescore: the segment's exact steps that did not update passed
+// rescore_waste - the bound, grown by every step since the segment's scores,
+// no longer settles samples that would not update; scoring the rest of the
+// batch again against the live model (whole GPU, ~tens of us) is cheaper than
+// more wasted single-wave steps (~3.4 us each, profiles/r03_serial_v5_segments.jsonl)
+constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2, kStopRescore = 3;
+constexpr int kSerialSegments = 4;       // segments of a small batch
+constexpr int kSerialSegmentsBig = 48;   // of a batch of >= kSerialBigBatch samples
+constexpr int64_t kSerialBigBatch = 16384;
+constexpr int kRescoreWaste = 16;        // wasted exact steps that end a segment
+constexpr int kScoreMaxBlocks = 8192;    // serial_score_kernel grid cap (grid-stride)
 // committer phase timings (tail[4..19]): shader-clock reads in the step loop
 // cost more than the phases they measure, so they are compiled in only for
 // diagnosis (JB_SERIAL_TIMING=1 at build time)
@@ -151,19 +160,22 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
     float* __restrict__ l1n, const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   const int lane = threadIdx.x & 63;
-  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (reason != nullptr && *reason == kStopDense) return;   // the batch went sequential
+  // the batch went sequential, or the previous segment finished it
+  if (reason != nullptr && (*reason == kStopDense || *reason == kStopDone)) return;
   const int64_t beg = stream_ptr[0];
-  const int64_t s = beg + wid;
-  if (s >= stream_ptr[nstreams]) return;
-  const int y = labels[s];
-  if (y < 0 || y >= LC) {
-    if (lane == 0) slack[wid] = NAN;
-    return;
-  }
+  const int64_t cnt = stream_ptr[nstreams] - beg;
   bool act[L::K];
 #pragma unroll
   for (int k = 0; k < L::K; ++k) act[k] = active[lane % L::LW + 64 * k] != 0;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wid < cnt;
+       wid += nwaves) {
+  const int64_t s = beg + wid;
+  const int y = labels[s];
+  if (y < 0 || y >= LC) {
+    if (lane == 0) slack[wid] = NAN;
+    continue;
+  }
   const int64_t fb = row_ptr[s];
   const int n = (int)(row_ptr[s + 1] - fb);
   float acc[L::K];
@@ -184,6 +196,7 @@ __global__ __launch_bounds__(256) void serial_score_kernel(
   if (lane == 0) {
     slack[wid] = decision_slack(method, margin, nrm, lstar >= 0, C, sy, best);
     l1n[wid] = l1;
+  }
   }
 }
 
@@ -529,10 +542,11 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     const int64_t* __restrict__ stream_ptr, int nstreams, float* W, float* P,
     const int32_t* __restrict__ active, int method, float C, const float* __restrict__ slack,
     const float* __restrict__ l1n, unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
-    int64_t* __restrict__ tail, int bail_after, int seg) {
+    int64_t* __restrict__ tail, int bail_after, int seg, int rescore_waste) {
   using L = Lanes<LC>;
   constexpr int T = kCommitThreads;
-  if (seg > 0 && tail[kTailReason] == kStopDense) return;
+  // a later segment runs only when the previous one stopped early for a re-score
+  if (seg > 0 && (tail[kTailReason] == kStopDense || tail[kTailReason] == kStopDone)) return;
   constexpr int NF = kSerialNF;
   constexpr bool kStaged = LC <= 32;   // (LC 64: 16 features per lane would spill)
   __shared__ int32_t s_key[kDCap];
@@ -544,7 +558,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   __shared__ int s_sn;
   __shared__ float s_dmax;
   __shared__ int s_first[2];
-  __shared__ int s_sat, s_nkeys;
+  __shared__ int s_sat, s_nkeys, s_waste;
   __shared__ unsigned s_valid;
   __shared__ int32_t s_fi[NF];
   __shared__ float s_fx[NF];
@@ -568,6 +582,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
     s_valid = 0;
     s_sat = 0;
     s_nkeys = 0;
+    s_waste = 0;
     s_first[0] = s_first[1] = INT_MAX;
   }
   DTable d{s_key, s_val, s_bloom, &s_nkeys, &s_sat, s_skey, s_sval, s_slist, &s_sn, &s_dmax};
@@ -589,6 +604,7 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
   }
   __syncthreads();
   unsigned n_upd = 0;
+  int n_waste = 0;         // wave 0: exact steps of this segment that did not update
   int64_t stop = end;
   int64_t why = kStopDone;
   int iter = 0;
@@ -695,7 +711,8 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
                                                    touched, d);
         else
           up = commit_sample<LC>(fidx, fval, s_fb, n, s_y, W, P, act, lane, method, C, touched, d);
-        if (up) ++n_upd;
+        if (up) ++n_upd; else ++n_waste;
+        if (lane == 0) s_waste = n_waste;
       }
       lim = k;
       ++steps;
@@ -704,9 +721,9 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
       lds_barrier();       // B2: D / the step table / s_sat visible to every wave
       { const uint64_t t = stamp(); ph[4] += t - tc; tc = t; }
       tw = stamp();
-      if (s_sat || steps > bail_after) {
+      if (s_sat || steps > bail_after || (rescore_waste > 0 && s_waste > rescore_waste)) {
         stop = p + k + 1;
-        why = s_sat ? kStopSaturated : kStopDense;
+        why = s_sat ? kStopSaturated : steps > bail_after ? kStopDense : kStopRescore;
         break;
       }
       if (loaded && open && tid > k && sl >= 0.f) {
@@ -769,12 +786,15 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   float* slack = (float*)((uint8_t*)scratch + 256);
   float* l1n = slack + n_max;     // |x|_1 of each sample
   // (slack[i] belongs to sample stream_ptr[0] + i)
-  const int64_t blocks = (n_max * 64 + 255) / 256;
-  if (blocks > INT32_MAX) return -5;
+  const int64_t blocks = std::min<int64_t>((n_max * 64 + 255) / 256, jb::kScoreMaxBlocks);
+  // a big batch that updates often re-scores its rest many times (kStopRescore);
+  // the last segment never stops for that (its rest would go sequential)
+  const int nseg = n_max >= jb::kSerialBigBatch ? jb::kSerialSegmentsBig : jb::kSerialSegments;
   // segments: a committer that saturated its D table hands [tail[0], end)
   // to the next segment (score + commit against the model as it is then);
   // the range lives in tail[0..1] on the device, so no host round trip
-  for (int seg = 0; seg < jb::kSerialSegments; ++seg) {
+  for (int seg = 0; seg < nseg; ++seg) {
+    const int waste = seg + 1 < nseg ? jb::kRescoreWaste : 0;
     const int64_t* sp = seg == 0 ? stream_ptr : tail;
     const int ns = seg == 0 ? nstreams : 1;
     const int64_t* why = seg == 0 ? nullptr : tail + jb::kTailReason;
@@ -784,7 +804,7 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   hipLaunchKernelGGL((jb::serial_commit_kernel<L>), dim3(1), dim3(jb::kCommitThreads), 0, stream, \
                      row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, slack, l1n,    \
                      stats,                                                                       \
-                     touched, tail, bail_after, seg);
+                     touched, tail, bail_after, seg, waste);
     JB_LC_DISPATCH(LC, JB_SERIAL)
 #undef JB_SERIAL
   }

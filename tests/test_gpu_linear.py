@@ -465,6 +465,44 @@ def test_serial_mode_matches_oracle(method):
                                    atol=2e-3 * float(c.P.max()))
 
 
+@pytest.mark.parametrize("method", ["PA1", "AROW"])
+def test_serial_mode_big_batch_rescores(method):
+    """one batch of >= 16384 samples (csrc/hip/serial.hip kSerialBigBatch):
+    the committer ends a segment once kRescoreWaste exact steps did not
+    update and the next segment re-scores the rest against the live model -
+    the result must still be the requests applied one after the other"""
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    param = {"regularization_weight": 0.5}
+    rng = random.Random(41)
+    data = []                            # mostly separable: few updates, many bound misses
+    for _ in range(160 * 130):
+        y = rng.randrange(6)
+        sv = [[f"s{j}", f"v{y * 7 + rng.randrange(3) if rng.random() < 0.9 else rng.randrange(300)}"]
+              for j in range(4)]
+        nv = [[f"n{j}", (y - 2) * 0.5 + rng.gauss(0, 1)] for j in range(3)] + [["bias", 1.0]]
+        data.append((f"L{y}", [sv, nv, []]))
+    reqs = [data[i:i + 160] for i in range(0, len(data), 160)]
+    g = LinearClassifier(method, param, DatumToFvConverter(CONV), device=_device())
+    for r in reqs[:2]:
+        g.train(r)
+    g.train_requests([msgpack.packb([[l, d] for l, d in r], use_bin_type=False) for r in reqs[2:]])
+    c = _oracle_serial(method, param, CONV, reqs)
+    g.synchronize()
+    g.pipe.check_errors()
+    diag = g._serial.last_batch()
+    assert diag["tail_start"] == diag["end"], diag   # the committer settled the whole batch
+    assert diag["segments"] > 1, diag                # in more than one re-scored segment
+    st = g.train_stats()
+    assert st["trained"] == len(data)
+    assert st["updated"] == c.train_stats()["updated"], (st, c.train_stats())
+    scale = float(np.abs(c.W).max()) or 1.0
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+    if c.P is not None:
+        np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3,
+                                   atol=2e-3 * float(c.P.max()))
+
+
 @pytest.mark.parametrize("nlabels", [6, 100])
 def test_serial_mode_every_sample_updates(nlabels):
     """noise labels: (almost) every sample updates, so the committer hands
