@@ -670,8 +670,9 @@ class SerialScratch:
         if self.buf is None:
             return {}
         v = self.buf[:176].view(torch.int64).tolist()
+        reasons = ("done", "saturated", "dense", "rescore")
         out = {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3],
-               "segments": v[21], "stop_reason": ("done", "saturated", "dense", "rescore")[v[20]] if 0 <= v[20] < 4 else v[20]}
+               "segments": v[21], "stop_reason": reasons[v[20]] if 0 <= v[20] < 4 else v[20]}
         # committer phases in shader cycles, scaled to us by the wall clock
         wall_us = v[10] / 100.0
         if v[11] > 0:
