@@ -33,6 +33,8 @@
 // the slack keeps a relative guard band (kSlackGuard) - a sample within it of
 // the threshold always takes the exact step.
 #include "jb_linear.hpp"
+#include <cstdlib>
+#include <cstring>
 
 namespace jb {
 
@@ -763,10 +765,28 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
 }  // namespace jb
 
 // bytes of the kSerial scratch for batches of up to n_max samples:
-// [tail int64 x 2, padded to 256 B][slack float x n_max]; n_max bounds the
-// batch's sample count stream_ptr[nstreams] - stream_ptr[0]
+// [tail int64 x 32 = 256 B][per sample: the delta committer's S0 scores
+// (commit.hip, LC <= 64 floats) or this file's slack + |x|_1 (LC > 64)];
+// n_max bounds the batch's sample count stream_ptr[nstreams] - stream_ptr[0]
 extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max) {
-  return 256 + 8 * (n_max > 0 ? n_max : 1);
+  return 256 + 256 * (n_max > 0 ? n_max : 1);
+}
+
+// commit.hip: the delta committer (label capacities <= 64)
+extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                const int32_t* labels, const int64_t* stream_ptr, int nstreams,
+                                int64_t n_max, float* W, float* S, const int32_t* active, int LC,
+                                int method, float C, unsigned long long* stats, uint8_t* touched,
+                                void* scratch, int nseg, hipStream_t stream);
+
+// committer of LC <= 64: 1 = delta (commit.hip, default), 0 = this file's
+// bound committer (JB_SERIAL_COMMITTER=bound, for A/B runs)
+static int serial_committer() {
+  static const int v = [] {
+    const char* e = getenv("JB_SERIAL_COMMITTER");
+    return (e != nullptr && strcmp(e, "bound") == 0) ? 0 : 1;
+  }();
+  return v;
 }
 
 // Steps 1-2 of a kSerial batch (score, commit); the caller then runs the
@@ -782,6 +802,12 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   if (nstreams <= 0 || n_max <= 0) return 0;
   if (scratch == nullptr || scratch_bytes < jb_serial_scratch_bytes(n_max)) return -3;
   if (method >= jb::CW && S == nullptr) return -4;
+  if (LC <= 64 && serial_committer() == 1) {
+    // delta committer: segments end only when the LDS row store fills
+    const int nseg = n_max >= jb::kSerialBigBatch ? 24 : jb::kSerialSegments;
+    return jb_delta_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W, S, active,
+                            LC, method, C, stats, touched, scratch, nseg, stream);
+  }
   int64_t* tail = (int64_t*)scratch;
   float* slack = (float*)((uint8_t*)scratch + 256);
   float* l1n = slack + n_max;     // |x|_1 of each sample

@@ -219,16 +219,19 @@ struct Rules {
 };
 
 // Feature-table height of the GPU linear models (classifier, regression)
-// when the configuration gives no hash_max_size: HBM-sized, 2^24 rows unless
-// JUBATUS_DEVICE_HASH_BITS says otherwise (AROW at 64 labels: 8 GiB of W + P
-// on a 288 GB device). Python twin: fv_converter/converter.py
-// device_hash_max_size (both servers pick the same height, so their model
-// files interchange).
+// when the configuration gives no hash_max_size (JUBATUS_DEVICE_HASH_BITS=24:
+// AROW at 64 labels is 8 GiB of W + P on a 288 GB device). Python twin:
+// fv_converter/converter.py device_hash_max_size (both servers pick the same
+// height, so their model files interchange).
 inline uint64_t device_hash_max_size() {
-  int bits = 24;
+  // one default on every backend (the host servers' 2^20): a model file saved
+  // by a GPU server loads on a --cpu one and back, and mixed members agree on
+  // the height; JUBATUS_DEVICE_HASH_BITS opts into an HBM-sized table (rows
+  // are int32 feature indices, so at most 2^31)
+  int bits = 20;
   if (const char* e = getenv("JUBATUS_DEVICE_HASH_BITS")) {
     const int b = atoi(e);
-    if (b >= 10 && b <= 34) bits = b;
+    if (b >= 10 && b <= 31) bits = b;
   }
   return 1ull << bits;
 }

@@ -47,17 +47,17 @@ DEFAULT_HASH_MAX_SIZE = 1 << 20
 
 def device_hash_max_size() -> int:
     """Feature-table height of the GPU linear models (classifier,
-    regression) when the configuration gives no ``hash_max_size``:
-    HBM-sized, 2^24 rows unless JUBATUS_DEVICE_HASH_BITS says otherwise
-    (AROW at 64 labels: 8 GiB of W + P on a 288 GB device). The reference
-    keeps feature names unhashed when the key is absent; a 2^24-row table
-    makes collisions among 10^5 distinct features ~16x rarer than the host
-    default of 2^20. Native twin: csrc/server/jb_server_common.hpp."""
+    regression) when the configuration gives no ``hash_max_size``: the host
+    default 2^20 on every backend, so model files interchange between GPU
+    and --cpu servers and mixed members agree on the height.
+    JUBATUS_DEVICE_HASH_BITS opts into an HBM-sized table (e.g. 24: AROW at
+    64 labels is 8 GiB of W + P on a 288 GB device); feature indices are
+    int32, so at most 31 bits. Native twin: csrc/server/jb_server_common.hpp."""
     import os
-    bits = 24
+    bits = 20
     try:
-        b = int(os.environ.get("JUBATUS_DEVICE_HASH_BITS", "24"))
-        if 10 <= b <= 34:
+        b = int(os.environ.get("JUBATUS_DEVICE_HASH_BITS", "20"))
+        if 10 <= b <= 31:
             bits = b
     except ValueError:
         pass

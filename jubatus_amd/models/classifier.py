@@ -295,7 +295,9 @@ class LinearClassifier:
         a.method = self.mid
         a.C = float(self.C)
         a.mode = self._mode(R)
-        if a.mode == hip.UPDATE_SERIAL:
+        # exact with several streams runs as serial-equivalent (linear.hip),
+        # which needs the scratch as much as an explicit serial mode does
+        if a.mode == hip.UPDATE_SERIAL or (a.mode == hip.UPDATE_EXACT and R > 1):
             a.serial_scratch = self._serial.ptr(max(1, n))
             a.serial_bytes = self._serial.nbytes
         a.merge_every = self.hot_merge

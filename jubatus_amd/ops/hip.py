@@ -669,10 +669,15 @@ class SerialScratch:
         left to the sequential kernel, batch end, exact steps, rounds"""
         if self.buf is None:
             return {}
-        v = self.buf[:176].view(torch.int64).tolist()
+        v = self.buf[:256].view(torch.int64).tolist()
         reasons = ("done", "saturated", "dense", "rescore")
         out = {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3],
                "segments": v[21], "stop_reason": reasons[v[20]] if 0 <= v[20] < 4 else v[20]}
+        if v[24] > 0 or v[22] > 0:
+            # delta committer (csrc/hip/commit.hip): steps that did not update,
+            # guard-band re-scores, updates, rows in the LDS store at the end
+            out.update(wasted_steps=v[22], refreshes=v[23], committer_updates=v[24],
+                       last_segment_rows=v[25])
         # committer phases in shader cycles, scaled to us by the wall clock
         wall_us = v[10] / 100.0
         if v[11] > 0:

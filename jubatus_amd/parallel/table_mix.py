@@ -137,7 +137,10 @@ class TableMix:
                 return False
             ev.synchronize()
         rows_n = int(host[0])
-        if rows_n > self.dense_frac * self.H:
+        # a full union always goes dense: a rank without a touched map went
+        # dense in begin() (its all-ones map makes the union full on every
+        # rank), so whatever dense_frac is, every rank must pick the same path
+        if rows_n >= self.H or rows_n > self.dense_frac * self.H:
             self._mark = None
             self.mode = "dense"
             self.rows = self.H

@@ -44,6 +44,16 @@ def _worker(rank, world, port, mode, q):
         dist.all_gather(allp, P)
         ref_w = torch.stack(allw).mean(0)
         ref_p = torch.stack(allp).mean(0)
+        if mode == "full_union":
+            # dense_frac 1.0 and one rank without a touched map: that rank
+            # goes dense at once, the other sees a full union and must follow
+            job = TableMix([W, P], touched if rank == 0 else None, None, dense_frac=1.0).begin()
+            while not job.ready():
+                pass
+            nbytes = job.end()
+            q.put((rank, job.stats(), nbytes, float((W - ref_w).abs().max()),
+                   float((P - ref_p).abs().max()), int(touched.sum())))
+            return
         if mode == "sparse":
             job = TableMix([W, P], touched, None).begin()
         else:      # dense, chunked into 16 KiB pieces
@@ -64,7 +74,7 @@ def _worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "full_union"])
 def test_table_mix_equals_dense_mean(mode):
     world = 2
     ctx = mp.get_context("spawn")
