@@ -38,6 +38,7 @@
 #include "jb_msgpack.hpp"
 #include "jb_rpc.hpp"
 #include "jubatus_amd/msgpack_rpc.hpp"
+#include "jb_log.hpp"
 
 namespace jb {
 namespace cc {
@@ -49,13 +50,7 @@ inline double now_s() {
 }
 
 inline void log_tagged(const char* tag, const char* level, const std::string& msg) {
-  char ts[64];
-  time_t t = time(nullptr);
-  struct tm tmv;
-  localtime_r(&t, &tmv);
-  strftime(ts, sizeof ts, "%Y-%m-%d %H:%M:%S", &tmv);
-  fprintf(stderr, "%s %d %-5s [%s] %s\n", ts, (int)getpid(), level, tag, msg.c_str());
-  fflush(stderr);
+  jb::jlog::write(level, tag, msg.c_str());
 }
 
 // ------------------------------------------------------------ msgpack bits
@@ -231,6 +226,7 @@ class Coord {
           conn_.reset(new Conn(hp.substr(0, colon), atoi(hp.c_str() + colon + 1), timeout));
           connected_ = hp;
           sid_ = call_locked("open_session", {Value::real(timeout)}).as_int();
+          jb::jlog::zk("INFO", tag_, "coordinator session " + std::to_string(sid_) + " opened on " + hp);
           break;
         } catch (const std::exception& ex) {
           conn_.reset();
@@ -252,6 +248,7 @@ class Coord {
     if (hb_.joinable()) hb_.join();
     if (poll_.joinable()) poll_.join();
     try { call("close_session", {Value::integer(sid_)}); } catch (...) {}
+    jb::jlog::zk("INFO", tag_, "coordinator session " + std::to_string(sid_) + " closed");
   }
 
   Value call(const std::string& m, std::vector<Value> args) {
@@ -320,6 +317,7 @@ class Coord {
       if (stop_.load()) break;
       try {
         if (!call("heartbeat", {Value::integer(sid_)}).as_bool()) {
+          jb::jlog::zk("ERROR", tag_, "coordinator session expired: shutting down");
           log_tagged(tag_, "ERROR", "coordinator session expired: shutting down");
           kill(getpid(), SIGTERM);   // the reference's shutdown_server (membership.cpp:257-259)
           return;

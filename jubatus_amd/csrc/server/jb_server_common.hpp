@@ -76,12 +76,7 @@ inline void logf_(const char* level, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  time_t t = time(nullptr);
-  struct tm tm;
-  localtime_r(&t, &tm);
-  char ts[32];
-  strftime(ts, sizeof ts, "%Y-%m-%d %H:%M:%S", &tm);
-  fprintf(stderr, "%s %d %-5s [%s] %s\n", ts, (int)getpid(), level, prog_name(), buf);
+  jb::jlog::write(level, prog_name(), buf);
 }
 
 // ------------------------------------------------------------------ argv
@@ -632,6 +627,36 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool
   } else {
     a->eth = default_v4();
   }
+  if (!a->native_check) {
+    // logging (server_util.cpp:236-242,305-311; server_helper.cpp:34-44)
+    std::string err;
+    if (!a->logdir.empty()) {
+      a->logdir = real_path(a->logdir);
+      if (access(a->logdir.c_str(), W_OK) != 0) {
+        fprintf(stderr, "can't create log file in logdir: %s\n", a->logdir.c_str());
+        usage(stderr);
+        return 1;
+      }
+    }
+    if (!a->log_config.empty()) a->log_config = real_path(a->log_config);
+    jb::jlog::set_parameters(prog_name(), a->eth, a->port);
+    if (!jb::jlog::configure(a->log_config, &err)) {
+      fprintf(stderr, "failed to configure logger: %s\n", err.c_str());
+      exit(1);
+    }
+    if (dist && !a->logdir.empty() && !jb::jlog::set_zk_log(a->logdir, prog_name(), a->eth, a->port, &err)) {
+      fprintf(stderr, "%s\n", err.c_str());
+      exit(1);
+    }
+    if (a->daemon) {
+      // daemon mode keeps the process in the foreground and ignores SIGHUP
+      // (server_util.cpp:379-388)
+      if (a->logdir.empty() && a->log_config.empty() && isatty(fileno(stderr)))
+        logf_("WARN", "logs may be lost because started in daemon mode without log directory");
+      jb::jlog::sink().daemon = true;
+      logf_("INFO", "set daemon mode (SIGHUP is now ignored)");
+    }
+  }
   if (dist) {
     std::string why;
     if (!config_from_coordinator(*a, text, &why)) {
@@ -667,6 +692,7 @@ inline void block_signals() {
   sigemptyset(&set);
   sigaddset(&set, SIGTERM);
   sigaddset(&set, SIGINT);
+  sigaddset(&set, SIGHUP);
   pthread_sigmask(SIG_BLOCK, &set, nullptr);
   signal(SIGPIPE, SIG_IGN);
 }
@@ -685,14 +711,20 @@ inline int device_and_signals(const Args& a) {
   return device % ndev;
 }
 
+// the main thread's signal loop (signals.cpp:98-181): TERM / INT return (the
+// caller shuts down), HUP reloads the log configuration unless in daemon mode
 inline void wait_for_term() {
   sigset_t set;
   sigemptyset(&set);
   sigaddset(&set, SIGTERM);
   sigaddset(&set, SIGINT);
+  sigaddset(&set, SIGHUP);
   int sig = 0;
-  while (true)
-    if (sigwait(&set, &sig) == 0 && (sig == SIGTERM || sig == SIGINT)) return;
+  while (true) {
+    if (sigwait(&set, &sig) != 0) continue;
+    if (sig == SIGTERM || sig == SIGINT) return;
+    if (sig == SIGHUP && !jb::jlog::sink().daemon) jb::jlog::reload(prog_name());
+  }
 }
 
 }  // namespace srv
