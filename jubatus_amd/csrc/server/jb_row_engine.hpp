@@ -93,6 +93,7 @@ using jb::srv::DevBuf;
 constexpr int kTopMaxK = 128;        // csrc/hip/topk.hip kTopMaxK
 constexpr int kQueryMax = 8;         // lsh.hip kQueryMax
 constexpr int kQuerySlots = 256;     // lsh.hip kQuerySlots (direct paths)
+constexpr int kPoolMaxQ = 8;          // sparse_pool.hip kPoolMaxQ (queries per pass)
 constexpr int kPoolMaxQEntries = 4096;
 
 struct ArgError : std::runtime_error {   // -> ARGUMENT_ERROR on the wire
@@ -378,6 +379,34 @@ class LshIndex {
     return query_sig(q_bits(), q_norm(), nrows, k);
   }
 
+  // up to kQueryMax hashed vectors in ONE launch sequence (signatures, the
+  // fused scan + top-k of every query in one pass over the table); false
+  // when they do not fit the kernel arguments (the caller goes one by one)
+  bool query_fv_many(const std::vector<const std::vector<int32_t>*>& idx,
+                     const std::vector<const std::vector<float>*>& val, int64_t nrows, int k,
+                     std::vector<std::vector<Hit>>* out) {
+    const int nq = (int)idx.size();
+    if (nq <= 0 || nq > kQueryMax || nrows <= 0 || k <= 0 || k > kTopMaxK) return false;
+    std::vector<int64_t> rp(1, 0);
+    std::vector<int32_t> ci;
+    std::vector<float> cv;
+    for (int q = 0; q < nq; ++q) {
+      ci.insert(ci.end(), idx[q]->begin(), idx[q]->end());
+      cv.insert(cv.end(), val[q]->begin(), val[q]->end());
+      rp.push_back((int64_t)ci.size());
+    }
+    if ((int64_t)ci.size() > kQuerySlots) return false;
+    bufs_.scratch(nrows, k, nq);
+    const int rc = jb_lsh_query_direct(ci.data(), cv.data(), rp.data(), nq, hash_num_, seed_, mode_, metric_,
+                                       (const uint64_t*)bits_.p, norms_.p, valid_.p, nrows, k, q_bits(), q_norm(),
+                                       bufs_.sd.p, bufs_.si.p, bufs_.out_d, bufs_.out_i, bufs_.done, stream_);
+    if (rc == 1) return false;
+    if (rc != 0) throw std::runtime_error("lsh query failed: " + std::to_string(rc));
+    out->resize((size_t)nq);
+    for (int q = 0; q < nq; ++q) (*out)[(size_t)q] = direct_hits(bufs_, q, k);
+    return true;
+  }
+
   std::vector<Hit> query_slot(int32_t slot, int64_t nrows, int k) {
     if (nrows <= 0 || k <= 0) return {};
     return query_sig((const uint64_t*)bits_.p + (size_t)slot * words_, norms_.p + slot, nrows, k);
@@ -645,6 +674,34 @@ class PoolIndex {
                           out, stream_);
     if (rc != 0) throw std::runtime_error("pool scan failed: " + std::to_string(rc));
     return scores_topk(out, nrows, k);
+  }
+
+  // up to kPoolMaxQ hashed vectors scored in ONE pass over the pool
+  // (pool_rows_kernel), each with its own fused top-k; false when they do
+  // not fit the kernel arguments (the caller goes one by one)
+  bool query_fv_many(const std::vector<const std::vector<int32_t>*>& idx,
+                     const std::vector<const std::vector<float>*>& val, int64_t nrows, int k,
+                     std::vector<std::vector<Hit>>* out) {
+    const int nq = (int)idx.size();
+    if (nq <= 0 || nq > kPoolMaxQ || nrows <= 0 || k <= 0 || k > kTopMaxK) return false;
+    std::vector<int64_t> rp(1, 0);
+    std::vector<int32_t> ci;
+    std::vector<float> cv;
+    for (int q = 0; q < nq; ++q) {
+      ci.insert(ci.end(), idx[q]->begin(), idx[q]->end());
+      cv.insert(cv.end(), val[q]->begin(), val[q]->end());
+      rp.push_back((int64_t)ci.size());
+    }
+    bufs_.scratch(nrows, k, nq);
+    const int rc = jb_pool_query_direct(ci.data(), cv.data(), rp.data(), nullptr, nullptr, nq, r_off_.p,
+                                        r_len_.p, r_n2_.p, valid_.p, nrows, p_idx_.p, p_val_.p, metric(),
+                                        lanes_per_row(nq), k, bufs_.scores.get((size_t)nrows * nq), bufs_.sd.p,
+                                        bufs_.si.p, bufs_.out_d, bufs_.out_i, bufs_.done, stream_);
+    if (rc == 1) return false;
+    if (rc != 0) throw std::runtime_error("pool query failed: " + std::to_string(rc));
+    out->resize((size_t)nq);
+    for (int q = 0; q < nq; ++q) (*out)[(size_t)q] = direct_hits(bufs_, q, k);
+    return true;
   }
 
   std::vector<Hit> query_slot(int32_t slot, int64_t nrows, int k) {
@@ -931,6 +988,34 @@ class RowEngine {
   std::vector<Hit> query_fv(const std::vector<int32_t>& idx, const std::vector<float>& val, int k) {
     if (nslots() == 0 || k <= 0) return {};
     return lsh_ ? lsh_->query_fv(idx, val, nslots(), k) : pool_->query_fv(idx, val, nslots(), k);
+  }
+  // several hashed vectors at one k: multi-query passes of up to 8 where
+  // the index takes them (the LSH signature arguments hold 256 feature
+  // slots per launch), one by one otherwise
+  std::vector<std::vector<Hit>> query_fv_many(const std::vector<const std::vector<int32_t>*>& idx,
+                                              const std::vector<const std::vector<float>*>& val, int k) {
+    const size_t n = idx.size();
+    std::vector<std::vector<Hit>> out(n);
+    if (nslots() == 0 || k <= 0) return out;
+    size_t i = 0;
+    while (i < n) {
+      size_t j = i + 1;
+      size_t feats = idx[i]->size();
+      while (j < n && j - i < (size_t)kQueryMax && (!lsh_ || feats + idx[j]->size() <= (size_t)kQuerySlots))
+        feats += idx[j++]->size();
+      std::vector<const std::vector<int32_t>*> bi(idx.begin() + i, idx.begin() + j);
+      std::vector<const std::vector<float>*> bv(val.begin() + i, val.begin() + j);
+      std::vector<std::vector<Hit>> r;
+      const bool ok = j - i > 1 && (lsh_ ? lsh_->query_fv_many(bi, bv, nslots(), k, &r)
+                                         : pool_->query_fv_many(bi, bv, nslots(), k, &r));
+      if (ok) {
+        for (size_t q = i; q < j; ++q) out[q] = std::move(r[q - i]);
+      } else {
+        for (size_t q = i; q < j; ++q) out[q] = query_fv(*idx[q], *val[q], k);
+      }
+      i = j;
+    }
+    return out;
   }
   std::vector<Hit> query_slot(int32_t s, int k) {
     if (nslots() == 0 || k <= 0) return {};

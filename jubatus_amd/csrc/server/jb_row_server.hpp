@@ -12,14 +12,30 @@
 // Scope: standalone servers whose converter runs on the native hashers
 // (jb_row_engine.hpp Converter); other configurations, distributed mode,
 // --cpu and hosts without a GPU go to the Python server (exec before any GPU
-// call). Every call takes the engine lock (the Python driver's RLock).
+// call).
+//
+// Concurrency (the reference: nearest_neighbor analysis lock-free,
+// ChangeLog.rst:102, nearest_neighbor_serv.cpp:138-172 NOLOCK; recommender
+// analysis read-locked, recommender_serv.cpp:170-224 JRLOCK): updates take
+// the model lock exclusively; analysis takes it shared. Every query that
+// needs the device (similar_row_* / neighbor_row_* / calc_score) is handed
+// to ONE batcher thread, which takes all the queries the RPC threads have
+// queued, hashes them and scores up to 8 at one k in a single pass over the
+// index (LSH signatures: lsh.hip + topk.hip; inverted index: sparse_pool.hip
+// pool_rows_kernel), so concurrent clients share the table scan.
 #pragma once
 #include <time.h>
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <exception>
+#include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "jb_lof_state.hpp"
@@ -145,10 +161,24 @@ class Model {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     configure(cfg);
+    batcher_ = std::thread([this] {
+      HIPCHK(hipSetDevice(device_));
+      batch_loop();
+    });
   }
+  ~Model() {
+    {
+      std::lock_guard<std::mutex> lk(qmu_);
+      stop_ = true;
+    }
+    qcv_.notify_all();
+    if (batcher_.joinable()) batcher_.join();
+  }
+  uint64_t batches() const { return n_batches_.load(); }
+  uint64_t batched_queries() const { return n_batched_.load(); }
 
   void configure(const Config& cfg) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     HIPCHK(hipStreamSynchronize(stream_));
     lof_.reset();
     eng_.reset(new RowEngine(cfg.inner, &cfg.param, stream_));
@@ -162,7 +192,7 @@ class Model {
 
   // ------------------------------------------------------------- updates
   bool clear_row(const std::string& id) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     ++update_count;
     ++clear_row_cnt;
     return eng_->remove(id);
@@ -171,7 +201,7 @@ class Model {
   bool update_row(const std::string& id, const Value& dv) {
     Datum nd;
     jb::row::parse_datum(dv, &nd);
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     ++update_count;
     ++update_row_cnt;
     if (const jb::row::Row* r = eng_->find(id)) {
@@ -188,13 +218,13 @@ class Model {
   bool set_row(const std::string& id, const Value& dv) {
     Datum nd;
     jb::row::parse_datum(dv, &nd);
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     ++update_count;
     eng_->set(id, std::move(nd));
     return true;
   }
   void clear() {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     ++update_count;
     clear_row_cnt = update_row_cnt = 0;
     eng_->clear();
@@ -207,7 +237,7 @@ class Model {
   std::pair<std::string, double> add(const Value& dv) {
     Datum d;
     jb::row::parse_datum(dv, &d);
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     ++update_count;
     const std::string id = std::to_string(next_id_++);
     return {id, (double)insert(id, std::move(d))};
@@ -216,7 +246,7 @@ class Model {
   double update(const std::string& id, const Value& dv, bool merge) {
     Datum nd;
     jb::row::parse_datum(dv, &nd);
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     ++update_count;
     if (merge)
       if (const jb::row::Row* r = eng_->find(id)) {
@@ -229,58 +259,59 @@ class Model {
     return (double)insert(id, std::move(nd));
   }
   // models/anomaly.py calc_score: the k nearest stored rows, then LOF
+  // (batched: the neighbours of every queued calc_score in one pass)
   double calc_score(const Value& dv) {
     Datum chk;
     jb::row::parse_datum(dv, &chk);
+    QReq r;
+    r.kind = QReq::kScore;
     MsgpackWriter w;
     write_value(w, dv);
-    std::lock_guard<std::mutex> g(mu_);
-    std::vector<int32_t> ts;
-    std::vector<float> td;
-    if (eng_->nslots() > 0) {
-      std::vector<int32_t> idx;
-      std::vector<float> val;
-      eng_->conv.hash((const uint8_t*)w.out.data(), w.out.size(), &idx, &val, false);
-      for (const Hit& h : eng_->query_fv(idx, val, cfg_.k))
-        if (live(h.slot)) { ts.push_back(h.slot); td.push_back(h.dist); }
-    }
-    return (double)score_from(ts, td, -1);
+    r.datum = std::move(w.out);
+    r.k = cfg_.k;
+    submit(&r);
+    return r.score;
   }
 
   // ------------------------------------------------------------- queries
   std::vector<std::pair<std::string, double>> query_id(const std::string& id, int64_t k, bool similar) {
-    std::lock_guard<std::mutex> g(mu_);
-    const int32_t s = eng_->slot(id);
-    if (s < 0) throw std::runtime_error("'row not found: " + id + "'");   // str(KeyError)
-    if (k <= 0) return {};
-    return eng_->results(eng_->query_slot(s, clamp_k(k)), similar);
+    QReq r;
+    r.kind = QReq::kId;
+    r.id = id;
+    r.k = k <= 0 ? 0 : clamp_k(k);
+    r.neg_k = k <= 0;
+    r.similar = similar;
+    submit(&r);
+    return std::move(r.res);
   }
   std::vector<std::pair<std::string, double>> query_datum(const Value& dv, int64_t k, bool similar) {
     Datum chk;
     jb::row::parse_datum(dv, &chk);                  // validate first (ARGUMENT_ERROR)
+    if (k <= 0) return {};
+    QReq r;
+    r.kind = QReq::kDatum;
     MsgpackWriter w;
     write_value(w, dv);
-    std::lock_guard<std::mutex> g(mu_);
-    if (eng_->nslots() == 0 || k <= 0) return {};
-    std::vector<int32_t> idx;
-    std::vector<float> val;
-    eng_->conv.hash((const uint8_t*)w.out.data(), w.out.size(), &idx, &val, false);
-    return eng_->results(eng_->query_fv(idx, val, clamp_k(k)), similar);
+    r.datum = std::move(w.out);
+    r.k = clamp_k(k);
+    r.similar = similar;
+    submit(&r);
+    return std::move(r.res);
   }
 
   Datum decode_row(const std::string& id) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     const jb::row::Row* r = eng_->find(id);
     return r ? r->d : Datum();
   }
   std::vector<std::string> get_all_rows() {
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     return eng_->all_ids();
   }
 
   // models/recommender.py complete_row_from_id / _from_datum / _complete
   Datum complete_row_from_id(const std::string& id) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     const jb::row::Row* r = eng_->find(id);
     if (!r) return Datum();
     const std::vector<int32_t> idx = r->idx;
@@ -297,7 +328,7 @@ class Model {
     Datum d;
     jb::row::parse_datum(dv, &d);
     auto nb = query_datum(dv, kCompleteK, true);
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     return complete(d.nv, nb);
   }
 
@@ -306,7 +337,7 @@ class Model {
     std::vector<float> av, bv;
     fv_of(a, &ai, &av);
     fv_of(b, &bi, &bv);
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     return eng_->calc_similarity(ai, av, bi, bv);
   }
   double calc_l2norm(const Value& a) {
@@ -321,7 +352,7 @@ class Model {
 
   // ------------------------------------------------------------ persist
   std::string pack_user_data() {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     HIPCHK(hipStreamSynchronize(stream_));
     MsgpackWriter u;
     u.arr(2);
@@ -330,7 +361,7 @@ class Model {
     return std::move(u.out);
   }
   void unpack(const Value& obj) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::shared_mutex> g(mu_);
     lof_.reset();                  // LOF.unpack: lists rebuilt on demand
     eng_->unpack(obj);
     lof_.reset();
@@ -348,7 +379,7 @@ class Model {
   }
 
   void status(std::vector<std::pair<std::string, std::string>>* st) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
     auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
     add("method", kind_ == Kind::kNearestNeighbor ? eng_->method() : cfg_.outer);
     if (kind_ == Kind::kAnomaly) add("backend", eng_->method());
@@ -359,6 +390,8 @@ class Model {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) add("hbm_used_bytes", std::to_string(tot - fr));
     add("server_runtime", "native");
+    add("query_batches", std::to_string(n_batches_.load()));
+    add("batched_queries", std::to_string(n_batched_.load()));
     if (kind_ == Kind::kRecommender) {
       add("clear_row_cnt", std::to_string(clear_row_cnt));
       add("update_row_cnt", std::to_string(update_row_cnt));
@@ -373,7 +406,8 @@ class Model {
     jb::row::parse_datum(dv, &chk);
     MsgpackWriter w;
     write_value(w, dv);
-    std::lock_guard<std::mutex> g(mu_);
+    std::shared_lock<std::shared_mutex> g(mu_);
+    std::lock_guard<std::mutex> h(hash_mu_);
     eng_->conv.hash((const uint8_t*)w.out.data(), w.out.size(), idx, val, false);
   }
 
@@ -416,6 +450,108 @@ class Model {
         w.map(v.o.size());
         for (const auto& kv : v.o) { w.raw(kv.first); write_value(w, kv.second); }
         break;
+    }
+  }
+
+  // ------------------------------------------------------------ batcher
+  struct QReq {
+    enum { kDatum = 0, kScore = 1, kId = 2 };
+    int kind = kDatum;
+    std::string datum;        // msgpack of the query datum (kDatum, kScore)
+    std::string id;           // kId
+    int k = 0;
+    bool neg_k = false;       // kId with k <= 0: only the existence check
+    bool similar = true;
+    std::vector<std::pair<std::string, double>> res;
+    double score = 0.0;
+    std::exception_ptr err;
+    bool done = false;
+  };
+
+  void submit(QReq* r) {
+    std::unique_lock<std::mutex> lk(qmu_);
+    q_.push_back(r);
+    qcv_.notify_one();
+    dcv_.wait(lk, [&] { return r->done; });
+    if (r->err) std::rethrow_exception(r->err);
+  }
+
+  void batch_loop() {
+    std::vector<QReq*> take;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(qmu_);
+        qcv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;   // stop_ and drained
+        take.assign(q_.begin(), q_.end());
+        q_.clear();
+      }
+      run_batch(take);
+      {
+        std::lock_guard<std::mutex> lk(qmu_);
+        for (QReq* r : take) r->done = true;
+      }
+      dcv_.notify_all();
+    }
+  }
+
+  // one batch under the shared model lock: the batcher is the only reader
+  // that touches the device index / LOF state (updates hold the lock
+  // exclusively)
+  void run_batch(std::vector<QReq*>& rs) {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    ++n_batches_;
+    n_batched_ += rs.size();
+    const size_t n = rs.size();
+    std::vector<std::vector<int32_t>> idx(n);
+    std::vector<std::vector<float>> val(n);
+    std::map<int, std::vector<size_t>> byk;
+    {
+      std::lock_guard<std::mutex> h(hash_mu_);
+      for (size_t i = 0; i < n; ++i) {
+        QReq* r = rs[i];
+        if (r->kind == QReq::kId) continue;
+        if (eng_->nslots() == 0) continue;        // nothing stored: no query
+        try {
+          eng_->conv.hash((const uint8_t*)r->datum.data(), r->datum.size(), &idx[i], &val[i], false);
+          byk[r->k].push_back(i);
+        } catch (...) {
+          r->err = std::current_exception();
+        }
+      }
+    }
+    std::vector<std::vector<Hit>> hits(n);
+    for (auto& kv : byk) {
+      std::vector<const std::vector<int32_t>*> pi;
+      std::vector<const std::vector<float>*> pv;
+      for (size_t i : kv.second) { pi.push_back(&idx[i]); pv.push_back(&val[i]); }
+      try {
+        auto h = eng_->query_fv_many(pi, pv, kv.first);
+        for (size_t q = 0; q < kv.second.size(); ++q) hits[kv.second[q]] = std::move(h[q]);
+      } catch (...) {
+        for (size_t i : kv.second) rs[i]->err = std::current_exception();
+      }
+    }
+    for (size_t i = 0; i < n; ++i) {
+      QReq* r = rs[i];
+      if (r->err) continue;
+      try {
+        if (r->kind == QReq::kDatum) {
+          r->res = eng_->results(hits[i], r->similar);
+        } else if (r->kind == QReq::kScore) {
+          std::vector<int32_t> ts;
+          std::vector<float> td;
+          for (const Hit& hh : hits[i])
+            if (live(hh.slot)) { ts.push_back(hh.slot); td.push_back(hh.dist); }
+          r->score = (double)score_from(ts, td, -1);
+        } else {
+          const int32_t s = eng_->slot(r->id);
+          if (s < 0) throw std::runtime_error("'row not found: " + r->id + "'");   // str(KeyError)
+          if (!r->neg_k) r->res = eng_->results(eng_->query_slot(s, r->k), r->similar);
+        }
+      } catch (...) {
+        r->err = std::current_exception();
+      }
     }
   }
 
@@ -477,7 +613,14 @@ class Model {
   Kind kind_;
   int device_;
   hipStream_t stream_;
-  std::mutex mu_;
+  std::shared_mutex mu_;      // the model: updates exclusive, analysis shared
+  std::mutex hash_mu_;        // the converter's hashers (scratch state) under a shared lock
+  std::mutex qmu_;            // the batcher's queue
+  std::condition_variable qcv_, dcv_;
+  std::deque<QReq*> q_;
+  bool stop_ = false;
+  std::thread batcher_;
+  std::atomic<uint64_t> n_batches_{0}, n_batched_{0};
   Config cfg_;
   std::unique_ptr<RowEngine> eng_;
   std::unique_ptr<jb::row::LofState> lof_;
