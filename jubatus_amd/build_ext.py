@@ -137,7 +137,7 @@ TOOLS = {
                    ["cmd", "native", "server", "../client_cpp/include"]),
     # host-only rehearsal of the native distributed model plane (jb_mix_group.hpp)
     "jb_mix_rehearsal": (["tools/jb_mix_rehearsal.cpp", "native/jb_rpc.cpp"],
-                         ["native", "../client_cpp/include"]),
+                         ["native", "server", "../client_cpp/include"]),
 }
 
 
@@ -191,7 +191,8 @@ SERVERS = {
 }
 HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph", "jubaweight", "jubaconv"}
 # servers with a native distributed mode (the model plane over RCCL)
-RCCL_SERVERS = {"jubaclassifier", "jubaregression", "jb_rccl_check"}
+RCCL_SERVERS = {"jubaclassifier", "jubaregression", "jb_rccl_check", "jubarecommender",
+                "jubanearest_neighbor", "jubaanomaly"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:

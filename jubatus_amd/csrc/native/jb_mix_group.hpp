@@ -53,6 +53,7 @@
 #include <vector>
 
 #include "jb_coord_client.hpp"
+#include "jb_hash.hpp"
 
 namespace jb {
 namespace mix {
@@ -344,6 +345,16 @@ class Plane {
   virtual void allreduce_max(uint8_t* p, size_t n, double dl) = 0;
   virtual void bcast(void* p, size_t bytes, int root, double dl) = 0;
   virtual void abort() {}
+  // variable-size host byte strings (row diffs, whole models): every rank's
+  // bytes to every rank / the root's bytes to every rank. The default moves
+  // them over the control plane; the device plane moves the payload over
+  // RCCL (the sizes over the control plane)
+  virtual std::vector<std::string> allgather_bytes(Star& s, const std::string& mine, double dl) {
+    return s.allgather(mine, dl);
+  }
+  virtual std::string bcast_bytes(Star& s, int root, const std::string& b, double dl) {
+    return s.bcast_str(root, b, dl);
+  }
 };
 
 // host memory over the star (CPU servers, rehearsals)
@@ -907,6 +918,7 @@ class ClusterNode {
     if (stop_.exchange(true)) return;
     if (fence_.joinable()) fence_.join();
     try {
+      for (const auto& c : cht_nodes_) coord_->call("remove", {cc::Value::str(c)});
       if (!node_.empty()) coord_->call("remove", {cc::Value::str(active_)});
       if (!node_.empty()) coord_->call("remove", {cc::Value::str(node_)});
       if (!rlock_.empty()) coord_->call("remove", {cc::Value::str(rlock_)});
@@ -917,9 +929,50 @@ class ClusterNode {
 
   std::string connected() const { return coord_->connected(); }
 
+  // CHT registration: NUM_VSERV = 8 ephemeral vnodes <actor>/cht/<md5(ip_port[_i])>
+  // with payload ip_port (cht.cpp:42-93, membership.cpp:40-47)
+  void register_cht(const std::string& eth, int port) {
+    const std::string dir = actor_path(type_, name_) + "/cht";
+    coord_->create(dir, "", false);
+    const std::string loc = eth + "_" + std::to_string(port);
+    for (int i = 0; i < 8; ++i) {
+      const std::string key = i > 0 ? loc + "_" + std::to_string(i) : loc;
+      const std::string path = dir + "/" + jb::Md5::hex(key);
+      if (!coord_->create(path, loc, true)) throw std::runtime_error("Failed to register cht node: " + path);
+      cht_nodes_.push_back(path);
+    }
+  }
+  // n consecutive vnodes from lower_bound(md5(key)), wrapping (cht.cpp:107-143)
+  std::vector<std::pair<std::string, int>> cht_find(const std::string& key, int n) {
+    const std::string dir = actor_path(type_, name_) + "/cht";
+    std::vector<std::string> h = coord_->list(dir);
+    if (h.empty()) throw std::runtime_error("no server found in cht: " + name_);
+    std::sort(h.begin(), h.end());
+    size_t idx = (size_t)(std::lower_bound(h.begin(), h.end(), jb::Md5::hex(key)) - h.begin()) % h.size();
+    std::vector<std::pair<std::string, int>> out;
+    for (int i = 0; i < n; ++i) {
+      std::string loc;
+      if (!coord_->read(dir + "/" + h[idx], &loc)) throw std::runtime_error("failed to read CHT entry: " + dir);
+      const size_t u = loc.find('_');
+      out.push_back(u == std::string::npos ? std::make_pair(loc, 0)
+                                           : std::make_pair(loc.substr(0, u), atoi(loc.c_str() + u + 1)));
+      idx = (idx + 1) % h.size();
+    }
+    return out;
+  }
+  // global_id_generator_zk: the data version of <actor>/id_generator
+  uint64_t create_id() {
+    const std::string path = actor_path(type_, name_) + "/id_generator";
+    cc::Value r = coord_->call("set", {cc::Value::str(path), cc::Value::str("dummy")});
+    const auto& a = r.as_array();
+    if (a.at(0).as_int() != 0) throw std::runtime_error("failed to increment version of node: " + path);
+    return (uint64_t)a.at(1).as_int();
+  }
+
  private:
   int64_t sid() { return coord_->session(); }
   std::string type_, name_, node_, active_, rlock_;
+  std::vector<std::string> cht_nodes_;
   std::unique_ptr<cc::Coord> coord_;
   std::thread fence_;
   std::atomic<bool> stop_{false};

@@ -53,6 +53,7 @@ class RcclPlane : public Plane {
     settle(dl, "ncclCommInitRank");
   }
   ~RcclPlane() override {
+    if (dbuf_ && !aborted_) { (void)hipStreamSynchronize(st_); (void)hipFree(dbuf_); }
     if (comm_) {
       if (aborted_) return;
       (void)hipStreamSynchronize(st_);
@@ -76,6 +77,37 @@ class RcclPlane : public Plane {
     check(ncclBroadcast(p, p, bytes, ncclUint8, root, comm_, st_), dl, "ncclBroadcast");
     wait_stream(st_, dl);
   }
+  // the payload over RCCL (padded to the largest rank's), the sizes over
+  // the control plane
+  std::vector<std::string> allgather_bytes(Star& s, const std::string& mine, double dl) override {
+    const std::vector<std::string> sz = s.allgather(std::to_string(mine.size()), dl);
+    size_t mx = 1;
+    for (const auto& x : sz) mx = std::max<size_t>(mx, (size_t)std::stoull(x));
+    const int w = s.world();
+    uint8_t* d = dev_bytes(mx * (size_t)(w + 1));
+    hipchk(hipMemsetAsync(d, 0, mx, st_), "MIX memset");
+    if (!mine.empty()) hipchk(hipMemcpyAsync(d, mine.data(), mine.size(), hipMemcpyHostToDevice, st_), "MIX H2D");
+    check(ncclAllGather(d, d + mx, mx, ncclUint8, comm_, st_), dl, "ncclAllGather");
+    std::string all(mx * (size_t)w, '\0');
+    hipchk(hipMemcpyAsync(&all[0], d + mx, all.size(), hipMemcpyDeviceToHost, st_), "MIX D2H");
+    wait_stream(st_, dl);
+    std::vector<std::string> out((size_t)w);
+    for (int r = 0; r < w; ++r) out[(size_t)r] = all.substr((size_t)r * mx, (size_t)std::stoull(sz[(size_t)r]));
+    return out;
+  }
+  std::string bcast_bytes(Star& s, int root, const std::string& b, double dl) override {
+    uint64_t n = b.size();
+    s.bcast(root, &n, 8, dl);
+    if (n == 0) return std::string();
+    uint8_t* d = dev_bytes((size_t)n);
+    if (s.rank() == root) hipchk(hipMemcpyAsync(d, b.data(), n, hipMemcpyHostToDevice, st_), "MIX H2D");
+    check(ncclBroadcast(d, d, n, ncclUint8, root, comm_, st_), dl, "ncclBroadcast");
+    std::string out((size_t)n, '\0');
+    hipchk(hipMemcpyAsync(&out[0], d, n, hipMemcpyDeviceToHost, st_), "MIX D2H");
+    wait_stream(st_, dl);
+    return out;
+  }
+
   void abort() override {
     if (comm_ && !aborted_) {
       aborted_ = true;
@@ -100,9 +132,21 @@ class RcclPlane : public Plane {
     if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
   }
 
+  uint8_t* dev_bytes(size_t n) {
+    if (n > dcap_) {
+      if (dbuf_) { (void)hipStreamSynchronize(st_); (void)hipFree(dbuf_); }
+      dbuf_ = nullptr;
+      hipchk(hipMalloc((void**)&dbuf_, n), "hipMalloc");
+      dcap_ = n;
+    }
+    return dbuf_;
+  }
+
   hipStream_t st_;
   ncclComm_t comm_ = nullptr;
   bool aborted_ = false;
+  uint8_t* dbuf_ = nullptr;   // byte collectives (row diffs, model hand-over)
+  size_t dcap_ = 0;
 };
 
 class StagedPlane : public Plane {

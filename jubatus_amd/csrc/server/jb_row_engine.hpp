@@ -30,11 +30,13 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
 #include "jb_hostfv.hpp"
 #include "jb_hostfv_wide.hpp"
+#include "jb_row_mix.hpp"
 #include "jb_server_common.hpp"
 #include "jb_wide_rules.hpp"
 #include "jb_value.hpp"
@@ -95,50 +97,6 @@ constexpr int kQueryMax = 8;         // lsh.hip kQueryMax
 constexpr int kQuerySlots = 256;     // lsh.hip kQuerySlots (direct paths)
 constexpr int kPoolMaxQ = 8;          // sparse_pool.hip kPoolMaxQ (queries per pass)
 constexpr int kPoolMaxQEntries = 4096;
-
-struct ArgError : std::runtime_error {   // -> ARGUMENT_ERROR on the wire
-  explicit ArgError(const std::string& s) : std::runtime_error(s) {}
-};
-
-// ------------------------------------------------------------------ datum
-// models/rows.py as_dicts: (string, num, binary) maps; a repeated key keeps
-// its last value; serialised with sorted keys (dicts_wire)
-struct Datum {
-  std::map<std::string, std::string> sv;
-  std::map<std::string, double> nv;
-  std::map<std::string, std::string> bv;
-};
-
-inline void parse_datum(const Value& v, Datum* d) {
-  // Datum.from_msgpack: at least [string_values, num_values]; more is ignored
-  if (v.kind != Value::ARR || v.a.size() < 2) throw ArgError("malformed datum");
-  for (size_t part = 0; part < std::min<size_t>(v.a.size(), 3); ++part) {
-    const Value& lst = v.a[part];
-    if (lst.kind != Value::ARR) throw ArgError("malformed datum");
-    for (const Value& kv : lst.a) {
-      if (kv.kind != Value::ARR || kv.a.size() != 2 || !kv.a[0].is_str()) throw ArgError("malformed datum");
-      const Value& x = kv.a[1];
-      if (part == 1) {
-        if (!x.is_num()) throw ArgError("num_values value must be a number");
-        d->nv[kv.a[0].s] = x.num();
-      } else {
-        if (!x.is_str()) throw ArgError("malformed datum");
-        (part == 0 ? d->sv : d->bv)[kv.a[0].s] = x.s;
-      }
-    }
-  }
-}
-
-inline void write_datum(MsgpackWriter& w, const Datum& d) {
-  w.arr(3);
-  w.arr(d.sv.size());
-  for (const auto& kv : d.sv) { w.arr(2); w.raw(kv.first); w.raw(kv.second); }
-  w.arr(d.nv.size());
-  for (const auto& kv : d.nv) { w.arr(2); w.raw(kv.first); w.dbl(kv.second); }
-  w.arr(d.bv.size());
-  for (const auto& kv : d.bv) { w.arr(2); w.raw(kv.first); w.raw(kv.second); }
-}
-
 
 // datum -> hashed feature vector; owns the document-frequency statistics of
 // the idf / bm25 weights (fv_converter/converter.py WeightManager layout)
@@ -203,6 +161,30 @@ class Converter {
       val->resize((size_t)rp[1]);
       return;
     }
+  }
+
+  // document statistics of the MIX (WeightManager.get_diff / put_diff):
+  // this server's contribution since the last MIX, then the cluster's sum
+  // replaces it
+  bool uses_weights() const { return !df_.empty(); }
+  void get_diff(int64_t* docs, int64_t* len, std::vector<int64_t>* idx, std::vector<int64_t>* cnt) const {
+    *docs = counts_[2];
+    *len = counts_[3];
+    idx->clear();
+    cnt->clear();
+    for (size_t i = 0; i < diff_.size(); ++i)
+      if (diff_[i] != 0) { idx->push_back((int64_t)i); cnt->push_back(diff_[i]); }
+  }
+  void put_diff(int64_t docs, int64_t len, const std::vector<int64_t>& idx, const std::vector<int64_t>& cnt) {
+    if (df_.empty()) return;
+    counts_[0] += docs - counts_[2];
+    counts_[1] += len - counts_[3];
+    for (size_t i = 0; i < df_.size(); ++i) df_[i] -= diff_[i];
+    for (size_t k = 0; k < idx.size() && k < cnt.size(); ++k)
+      if (idx[k] >= 0 && (uint64_t)idx[k] < H_) df_[(size_t)idx[k]] += cnt[k];
+    for (auto& x : df_) x = std::max<int64_t>(x, 0);
+    std::fill(diff_.begin(), diff_.end(), 0);
+    counts_[2] = counts_[3] = 0;
   }
 
   void clear() {
@@ -918,19 +900,30 @@ class RowEngine {
     write_datum(w, d);
     Row tmp;
     conv.hash((const uint8_t*)w.out.data(), w.out.size(), &tmp.idx, &tmp.val, bump);
+    store(id, std::move(d), tmp.idx, tmp.val, bump);
+  }
+
+  // a row whose feature vector was hashed elsewhere (a MIX diff: the sender's
+  // vector is kept, as rows.put_many does)
+  void store(const std::string& id, Datum&& d, const std::vector<int32_t>& idx, const std::vector<float>& val,
+             bool bump) {
     std::vector<int32_t> fi;
     std::vector<float> fv;
-    for (size_t i = 0; i < tmp.idx.size(); ++i)
-      if (tmp.idx[i] >= 0) { fi.push_back(tmp.idx[i]); fv.push_back(tmp.val[i]); }
+    for (size_t i = 0; i < idx.size(); ++i)
+      if (idx[i] >= 0) { fi.push_back(idx[i]); fv.push_back(val[i]); }
     const int32_t s = assign(id);
     Row& r = rows_[(size_t)s];
     r.d = std::move(d);
     r.idx = fi;
     r.val = fv;
     r.live = true;
-    if (bump) version_[id] += 1;
-    if (lsh_) lsh_->set(s, tmp.idx, tmp.val);
-    else pool_->set(s, tmp.idx, tmp.val);
+    if (bump) {
+      version_[id] += 1;
+      dirty_.insert(id);
+      removed_.erase(id);
+    }
+    if (lsh_) lsh_->set(s, idx, val);
+    else pool_->set(s, idx, val);
     if (lru_) {
       touch(id);
       while ((int64_t)lru_order_.size() > max_size_) {
@@ -954,7 +947,11 @@ class RowEngine {
     Row& r = rows_[(size_t)s];
     r = Row();
     free_.push_back(s);
-    if (record) version_[id] += 1;
+    if (record) {
+      version_[id] += 1;
+      removed_.insert(id);
+      dirty_.erase(id);
+    }
     if (lsh_) lsh_->remove(s);
     else pool_->remove(s);
     if (lru_) {
@@ -970,6 +967,8 @@ class RowEngine {
     insertion_.clear();
     free_.clear();
     version_.clear();
+    dirty_.clear();
+    removed_.clear();
     lru_order_.clear();
     lru_pos_.clear();
     if (lsh_) lsh_->clear();
@@ -1062,6 +1061,64 @@ class RowEngine {
     return den > 0 ? dot / den : 0.0;
   }
 
+  // ---------------------------------------------------------------- MIX
+  // the row-diff protocol of jb_row_mix.hpp (parallel/row_mix.py) over this
+  // store: the written rows' hashed vectors travel, receivers keep them
+  size_t dirty_rows() const { return dirty_.size() + removed_.size(); }
+  void pack_diff(MsgpackWriter& w) const { pack_row_diff(*this, w); }
+  size_t apply_diffs(const std::vector<Value>& parts, std::vector<int32_t>* changed) {
+    return apply_row_diffs(*this, parts, changed);
+  }
+  // store interface of pack_row_diff / apply_row_diffs
+  std::vector<std::string> mix_ids() const {
+    std::vector<std::string> ids;
+    for (const auto& id : dirty_)
+      if (slot_of_.count(id)) ids.push_back(id);
+    std::sort(ids.begin(), ids.end());
+    return ids;
+  }
+  std::vector<std::string> mix_removed() const {
+    std::vector<std::string> rm(removed_.begin(), removed_.end());
+    std::sort(rm.begin(), rm.end());
+    return rm;
+  }
+  bool version_of(const std::string& id, uint64_t* v) const {
+    auto it = version_.find(id);
+    if (it == version_.end()) { *v = 0; return false; }
+    *v = it->second;
+    return true;
+  }
+  bool holds(const std::string& id) const { return slot_of_.count(id) != 0; }
+  void row_view(const std::string& id, const Datum** d, const std::vector<int32_t>** ix,
+                const std::vector<float>** vx) const {
+    const Row& r = rows_[(size_t)slot_of_.at(id).first];
+    *d = &r.d;
+    *ix = &r.idx;
+    *vx = &r.val;
+  }
+  int32_t slot_id(const std::string& id) const { return slot(id); }
+  void store_mixed(const std::string& id, Datum&& d, const std::vector<int32_t>& idx,
+                   const std::vector<float>& val, uint64_t v) {
+    store(id, std::move(d), idx, val, false);
+    version_[id] = v;
+  }
+  void remove_mixed(const std::string& id, uint64_t v) {
+    remove(id, false);
+    version_[id] = v;
+  }
+  bool weight_diff(int64_t* docs, int64_t* len, std::vector<int64_t>* idx, std::vector<int64_t>* cnt) const {
+    if (!conv.uses_weights()) { *docs = *len = 0; return false; }
+    conv.get_diff(docs, len, idx, cnt);
+    return true;
+  }
+  void put_weight_diff(int64_t docs, int64_t len, const std::vector<int64_t>& idx, const std::vector<int64_t>& cnt) {
+    conv.put_diff(docs, len, idx, cnt);
+  }
+  void mix_done() {
+    dirty_.clear();
+    removed_.clear();
+  }
+
   // RowEngine.pack(): {"method", "rows": {id: [version, [sv, nv, bv]]}, "weights"}
   void pack(MsgpackWriter& w, const std::string& method_name) const {
     w.map(3);
@@ -1143,6 +1200,7 @@ class RowEngine {
   std::unordered_map<std::string, std::pair<int32_t, std::list<std::string>::iterator>> slot_of_;
   std::vector<int32_t> free_;
   std::unordered_map<std::string, uint64_t> version_;
+  std::unordered_set<std::string> dirty_, removed_;   // since the last MIX
   bool lru_ = false;
   int64_t max_size_ = 0;
   std::list<std::string> lru_order_;

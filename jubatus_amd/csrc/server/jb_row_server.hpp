@@ -9,10 +9,15 @@
 // the Python twins are server/{recommender,nearest_neighbor,anomaly}_serv.py
 // over models/recommender.py and models/anomaly.py.
 //
-// Scope: standalone servers whose converter runs on the native hashers
-// (jb_row_engine.hpp Converter); other configurations, distributed mode,
-// --cpu and hosts without a GPU go to the Python server (exec before any GPU
-// call).
+// Scope: servers whose converter runs on the native hashers
+// (jb_row_engine.hpp Converter), standalone or distributed with the linear
+// mixer: the row diffs of a MIX move as one byte buffer per rank over the
+// group's plane (RCCL all-gather over xGMI between GPUs, the control plane
+// when members share a device), newest version wins (parallel/row_mix.py's
+// protocol); CHT registration, and anomaly's add over the coordinator's id
+// generator + CHT owners with server-to-server update (anomaly_serv.cpp:
+// 178-211,275-297). Push mixers, other configurations, --cpu and hosts
+// without a GPU go to the Python server (exec before any GPU call).
 //
 // Concurrency (the reference: nearest_neighbor analysis lock-free,
 // ChangeLog.rst:102, nearest_neighbor_serv.cpp:138-172 NOLOCK; recommender
@@ -39,6 +44,8 @@
 #include <vector>
 
 #include "jb_lof_state.hpp"
+#include "jb_mix_device.hpp"
+#include "jb_mix_group.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_row_engine.hpp"
 #include "jb_rpc.hpp"
@@ -152,7 +159,7 @@ inline bool parse_config(Kind kind, const std::string& text, Config* c, std::str
   return true;
 }
 
-class Model {
+class Model : public jb::mix::Mixable {
  public:
   std::atomic<uint64_t> update_count{0};
   uint64_t clear_row_cnt = 0, update_row_cnt = 0;
@@ -161,11 +168,51 @@ class Model {
     HIPCHK(hipSetDevice(device));
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     configure(cfg);
+    HIPCHK(hipStreamCreateWithFlags(&mix_stream_, hipStreamNonBlocking));
     batcher_ = std::thread([this] {
       HIPCHK(hipSetDevice(device_));
       batch_loop();
     });
   }
+
+  // ------------------------------------------------------------- MIX
+  std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& star, double dl) {
+    return jb::mix::make_device_plane(star, device_, mix_stream_, dl);
+  }
+  // one MIX (all ranks): the model is held exclusively from packing this
+  // server's diff to applying the cluster's (the reference's put_diff takes
+  // the model write lock, linear_mixer.cpp:613-662)
+  uint64_t mix(jb::mix::Group& g) override {
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    MsgpackWriter w;
+    eng_->pack_diff(w);
+    const auto raw = g.plane().allgather_bytes(g.star(), w.out, g.deadline());
+    std::vector<Value> parts;
+    parts.reserve(raw.size());
+    for (const auto& r : raw) parts.push_back(MsgpackReader((const uint8_t*)r.data(), r.size()).read());
+    std::vector<int32_t> changed;
+    const size_t n = eng_->apply_diffs(parts, &changed);
+    // LOF: the neighbour lists are caches of the row set; rows written by the
+    // MIX invalidate them (rebuilt on demand against the mixed rows)
+    if (kind_ == Kind::kAnomaly && n > 0) lof_.reset();
+    HIPCHK(hipStreamSynchronize(stream_));
+    last_mix_rows_ = n;
+    uint64_t bytes = 0;
+    for (const auto& r : raw) bytes += r.size();
+    return bytes;
+  }
+  // obsolete protocol: rank src's whole model replaces an obsolete member's
+  void hand_over(jb::mix::Group& g, int src, bool apply) override {
+    std::string mine;
+    if (g.rank() == src) mine = pack_user_data();
+    const std::string got = g.plane().bcast_bytes(g.star(), src, mine, g.deadline());
+    if (apply) {
+      const Value v = MsgpackReader((const uint8_t*)got.data(), got.size()).read();
+      if (v.kind != Value::ARR || v.a.size() != 2) throw std::runtime_error("hand-over: malformed model");
+      unpack(v.a[1]);
+    }
+  }
+  size_t last_mix_rows() const { return last_mix_rows_; }
   ~Model() {
     {
       std::lock_guard<std::mutex> lk(qmu_);
@@ -434,6 +481,7 @@ class Model {
   }
 
   // re-encode a decoded datum Value (the query's own order kept)
+ public:
   static void write_value(MsgpackWriter& w, const Value& v) {
     switch (v.kind) {
       case Value::NIL: w.nil(); break;
@@ -452,6 +500,8 @@ class Model {
         break;
     }
   }
+ private:
+
 
   // ------------------------------------------------------------ batcher
   struct QReq {
@@ -613,6 +663,8 @@ class Model {
   Kind kind_;
   int device_;
   hipStream_t stream_;
+  hipStream_t mix_stream_ = nullptr;   // the RCCL plane's collectives
+  size_t last_mix_rows_ = 0;
   std::shared_mutex mu_;      // the model: updates exclusive, analysis shared
   std::mutex hash_mu_;        // the converter's hashers (scratch state) under a shared lock
   std::mutex qmu_;            // the batcher's queue
@@ -644,6 +696,13 @@ class Server {
 
   void load_file(const std::string& path) { load_impl(path, true); }
 
+  // distributed mode (-z): coordinator session, config read lock
+  void join_cluster(std::unique_ptr<jb::mix::ClusterNode> node) {
+    node_ = std::move(node);
+    a_.connected_zookeeper = node_->connected();
+    if (!node_->config_rlock()) throw std::runtime_error("failed to get config lock");
+  }
+
   int run() {
     rpc_.reset(new jb::RpcServer([this](const jb::RpcRequest& r) { return dispatch(r); }, a_.threads, 0.0));
     rpc_->set_io_threads(std::max(1, a_.threads / 4));
@@ -658,8 +717,31 @@ class Server {
     logf_("INFO", "start listening at port %d", port);
     cs_.start_time = time(nullptr);
     rpc_->start();
+    if (node_) {   // distributed mode: actor + CHT vnodes, then the mixer thread
+      node_->register_actor(a_.eth, a_.port);
+      node_->register_cht(a_.eth, a_.port);
+      jb::mix::MixerArgs ma;
+      ma.type = type();
+      ma.name = a_.name;
+      ma.eth = a_.eth;
+      ma.port = a_.port;
+      ma.interval_sec = a_.interval_sec;
+      ma.interval_count = a_.interval_count;
+      ma.interconnect_timeout = a_.ic_timeout;
+      Model* m = model_.get();
+      mixer_.reset(new jb::mix::LinearMixer(node_->coord(), ma, m, [m](jb::mix::Group& g, double dl) {
+        return m->make_plane(g.star(), dl);
+      }));
+      mixer_->start();
+      logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
+    }
     logf_("INFO", "%s RPC server startup (native)", prog_name());
     wait_for_term();
+    if (mixer_) {
+      logf_("INFO", "stopping mixer thread");
+      mixer_->stop();
+    }
+    if (node_) node_->leave();
     logf_("INFO", "stopping RPC server");
     rpc_->stop();
     return 0;
@@ -684,20 +766,22 @@ class Server {
         {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
         {"clear_row", "s"}, {"update_row", "sd"}, {"complete_row_from_id", "s"},
         {"complete_row_from_datum", "d"}, {"similar_row_from_id", "sk"}, {"similar_row_from_datum", "dk"},
-        {"decode_row", "s"}, {"get_all_rows", ""}, {"calc_similarity", "dd"}, {"calc_l2norm", "d"}};
+        {"decode_row", "s"}, {"get_all_rows", ""}, {"calc_similarity", "dd"}, {"calc_l2norm", "d"},
+        {"do_mix", ""}};
     static const std::vector<std::pair<std::string, std::string>> nn = {
         {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
         {"set_row", "sd"}, {"neighbor_row_from_id", "sk"}, {"neighbor_row_from_datum", "dk"},
-        {"similar_row_from_id", "sk"}, {"similar_row_from_datum", "dk"}, {"get_all_rows", ""}};
+        {"similar_row_from_id", "sk"}, {"similar_row_from_datum", "dk"}, {"get_all_rows", ""},
+        {"do_mix", ""}};
     static const std::vector<std::pair<std::string, std::string>> an = {
         {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
         {"clear_row", "s"}, {"add", "d"}, {"update", "sd"}, {"overwrite", "sd"}, {"calc_score", "d"},
-        {"get_all_rows", ""}};
+        {"get_all_rows", ""}, {"do_mix", ""}};
     const auto& table = kind_ == Kind::kRecommender ? rec : kind_ == Kind::kNearestNeighbor ? nn : an;
     const std::string* sig = nullptr;
     for (const auto& x : table)
       if (x.first == m) sig = &x.second;
-    if (!sig) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
+    if (!sig || (m == "do_mix" && !mixer_)) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
     bool ok = args.a.size() == sig->size() + 1 && args.a[0].is_str();
     for (size_t k = 0; ok && k < sig->size(); ++k) {
       const Value& x = args.a[k + 1];
@@ -710,16 +794,24 @@ class Server {
       return x.kind == Value::UINT ? (int64_t)std::min<uint64_t>(x.u, (uint64_t)INT64_MAX) : x.i;
     };
     MsgpackWriter w;
+    // update calls drive the MIX trigger (event_model_updated)
+    static const char* const kUpdates[] = {"clear", "clear_row", "update_row", "set_row", "add", "update",
+                                           "overwrite", "load"};
+    if (mixer_)
+      for (const char* u : kUpdates)
+        if (m == u && !(m == "add" && node_)) { mixer_->updated(1); break; }
     try {
       if (m == "get_config") {
         w.raw(model_->config_text());
+      } else if (m == "do_mix") {
+        w.boolean(mixer_->do_mix());
       } else if (m == "clear") {
         model_->clear();
         w.boolean(true);
       } else if (m == "clear_row") {
         w.boolean(model_->clear_row(args.a[1].s));
       } else if (m == "add") {
-        const auto r = model_->add(args.a[1]);
+        const auto r = node_ ? add_zk(args.a[1]) : model_->add(args.a[1]);
         w.arr(2);
         w.raw(r.first);
         w.dbl(r.second);
@@ -778,6 +870,7 @@ class Server {
           common_status(a_, cs_, model_->update_count.load(), &st);
         }
         model_->status(&st);
+        if (mixer_) mixer_->status(&st);
         w.map(1);
         w.raw(ident());
         w.map(st.size());
@@ -789,6 +882,53 @@ class Server {
       return r.notify ? std::string() : jb::val::response_msg(r.msgid, e.what());
     }
     return r.notify ? std::string() : jb::val::response_ok(r.msgid, w.out);
+  }
+
+  // anomaly_serv.cpp:178-211 add_zk: a cluster-wide id, the CHT(2) owners of
+  // it; the first owner's update must succeed, the replica is best effort
+  std::pair<std::string, double> add_zk(const Value& dv) {
+    Datum chk;
+    jb::row::parse_datum(dv, &chk);
+    const std::string id = std::to_string(node_->create_id());
+    const auto owners = node_->cht_find(id, 2);
+    if (owners.empty()) throw std::runtime_error("no server found in cht: " + a_.name);
+    double score;
+    try {
+      score = selective_update(owners[0], id, dv);
+    } catch (const std::exception& e) {
+      throw std::runtime_error("failed to add ID " + id + " (" + e.what() + "): " + owners[0].first + ":" +
+                               std::to_string(owners[0].second));
+    }
+    for (size_t i = 1; i < owners.size(); ++i) {
+      try {
+        selective_update(owners[i], id, dv);
+      } catch (const std::exception& e) {
+        logf_("WARN", "cannot create %zuth replica (%s): %s:%d", i, e.what(), owners[i].first.c_str(),
+              owners[i].second);
+      }
+    }
+    return {id, score};
+  }
+  // anomaly_serv.cpp:275-297: locally when this server owns the id, else a
+  // server-to-server update RPC
+  double selective_update(const std::pair<std::string, int>& owner, const std::string& id, const Value& dv) {
+    if (owner.first == a_.eth && owner.second == a_.port) {
+      if (mixer_) mixer_->updated(1);
+      return model_->update(id, dv, true);
+    }
+    const double tmo = std::max(1, a_.ic_timeout);
+    jb::cc::Conn c(owner.first, owner.second, tmo);
+    MsgpackWriter w;
+    w.arr(3);
+    w.raw(a_.name);
+    w.raw(id);
+    Model::write_value(w, dv);
+    const double dl = jb::cc::now_s() + tmo;
+    const uint32_t mid = c.send_request("update", w.out, dl);
+    jb::cc::CallResult res;
+    c.recv_response(mid, dl, &res);
+    if (!res.err.empty()) throw std::runtime_error("server-to-server update failed");
+    return MsgpackReader((const uint8_t*)res.res.data(), res.res.size()).read().num();
   }
 
   std::string local_path(const std::string& id) const {
@@ -826,6 +966,8 @@ class Server {
   Kind kind_;
   Args a_;
   std::unique_ptr<Model> model_;
+  std::unique_ptr<jb::mix::ClusterNode> node_;
+  std::unique_ptr<jb::mix::LinearMixer> mixer_;
   std::unique_ptr<jb::RpcServer> rpc_;
   std::mutex st_mu_;
   CommonStatus cs_;
@@ -838,7 +980,7 @@ inline int row_main(int argc, char** argv, Kind kind) {
   Config cfg;
   const int rc = startup(argc, argv, &a, &text, [&cfg, kind](const std::string& t, std::string* why) {
     return parse_config(kind, t, &cfg, why);
-  });
+  }, true, /*native_dist=*/true);
   if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
   try {
@@ -846,6 +988,9 @@ inline int row_main(int argc, char** argv, Kind kind) {
     logf_("INFO", "starting %s %s RPC server at %s:%d (native, device %d)", prog_name(), kVersion,
           a.eth.c_str(), a.port, device);
     Server srv(kind, a, cfg, device);
+    if (!a.zookeeper.empty())
+      srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
+          new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), kind_name(kind), a.name)));
     if (!a.model_file.empty()) srv.load_file(a.model_file);
     return srv.run();
   } catch (const std::exception& e) {

@@ -13,8 +13,15 @@
 //   do_mix(name) -> bool                 force a MIX and wait for it
 //   get_status(name) -> {ident: {key: value}}
 //
+// With -R the process is a row engine instead (recommender / nearest_neighbor
+// / anomaly): a host row store under the row-diff MIX protocol the native
+// GPU row servers run (csrc/server/jb_row_mix.hpp - the same code):
+//   put(name, seed, n, keys) -> n       n rows written (ids from a keyspace)
+//   remove(name, id) -> bool
+//   rows(name) -> {id: [version, x]}    the store (x: the row's "x" value)
+//
 // usage: jb_mix_rehearsal -z host:port -n name -p port [-H rows] [-I ic_timeout]
-//                         [-i interval_count] [-s interval_sec] [-Z zk_timeout]
+//                         [-i interval_count] [-s interval_sec] [-Z zk_timeout] [-R]
 #include <getopt.h>
 #include <signal.h>
 
@@ -23,6 +30,7 @@
 
 #include "jb_mix_group.hpp"
 #include "jb_msgpack.hpp"
+#include "jb_row_mix.hpp"
 #include "jb_rpc.hpp"
 
 namespace {
@@ -246,14 +254,174 @@ class HostModel : public jb::mix::Mixable {
   bool last_dense_ = false;
 };
 
+// A row store with versions (models/rows.py semantics) under the shared
+// row-diff protocol: every write bumps the row's version and marks it
+// written, a removal bumps it and records the removal.
+class HostRowModel : public jb::mix::Mixable {
+ public:
+  struct Row {
+    jb::row::Datum d;
+    std::vector<int32_t> idx;
+    std::vector<float> val;
+    int32_t slot;
+  };
+
+  int64_t put(uint64_t seed, int64_t n, int64_t keys) {
+    std::lock_guard<std::mutex> g(mu_);
+    uint64_t x = seed * 0x9E3779B97F4A7C15ull + 7;
+    for (int64_t i = 0; i < n; ++i) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      const int64_t k = (int64_t)(x % (uint64_t)std::max<int64_t>(1, keys));
+      const std::string id = "r" + std::to_string(k);
+      Row r;
+      r.d.sv["x"] = std::to_string(x % 100000);
+      r.d.nv["v"] = (double)(x % 1000) / 10.0;
+      r.idx = {(int32_t)(k % 97), (int32_t)(x % 1021)};
+      r.val = {1.f, (float)(x % 7)};
+      write(id, std::move(r));
+      ++version_[id];
+      dirty_.insert(id);
+      removed_.erase(id);
+    }
+    return n;
+  }
+  bool remove(const std::string& id) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!rows_.erase(id)) return false;
+    ++version_[id];
+    removed_.insert(id);
+    dirty_.erase(id);
+    return true;
+  }
+  Value rows() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::pair<Value, Value>> m;
+    for (const auto& kv : rows_)
+      m.emplace_back(Value::str(kv.first), Value::array({Value::uinteger(version_[kv.first]),
+                                                          Value::str(kv.second.d.sv.at("x"))}));
+    return Value::map(std::move(m));
+  }
+
+  uint64_t mix(Group& grp) override {
+    std::lock_guard<std::mutex> g(mu_);
+    jb::val::MsgpackWriter w;
+    jb::row::pack_row_diff(*this, w);
+    const auto raw = grp.plane().allgather_bytes(grp.star(), w.out, grp.deadline());
+    std::vector<jb::val::Value> parts;
+    for (const auto& r : raw) parts.push_back(jb::val::MsgpackReader((const uint8_t*)r.data(), r.size()).read());
+    last_applied_ = jb::row::apply_row_diffs(*this, parts, nullptr);
+    uint64_t bytes = 0;
+    for (const auto& r : raw) bytes += r.size();
+    return bytes;
+  }
+  // obsolete protocol: rank src's whole store (every row as written) replaces mine
+  void hand_over(Group& grp, int src, bool apply) override {
+    std::lock_guard<std::mutex> g(mu_);
+    jb::val::MsgpackWriter w;
+    if (grp.rank() == src) {
+      full_ = true;
+      jb::row::pack_row_diff(*this, w);
+      full_ = false;
+    }
+    const std::string got = grp.plane().bcast_bytes(grp.star(), src, w.out, grp.deadline());
+    if (!apply || grp.rank() == src) return;
+    rows_.clear();
+    version_.clear();
+    dirty_.clear();
+    removed_.clear();
+    jb::row::apply_row_diffs(*this, {jb::val::MsgpackReader((const uint8_t*)got.data(), got.size()).read()},
+                             nullptr);
+  }
+  void status(std::vector<std::pair<std::string, std::string>>* st) {
+    std::lock_guard<std::mutex> g(mu_);
+    st->emplace_back("num_rows", std::to_string(rows_.size()));
+    st->emplace_back("mix.last_rows_applied", std::to_string(last_applied_));
+  }
+
+  // ---- the store interface of jb_row_mix.hpp (mu_ held by the caller)
+  std::vector<std::string> mix_ids() const {
+    std::vector<std::string> ids;
+    if (full_) {
+      for (const auto& kv : rows_) ids.push_back(kv.first);
+    } else {
+      for (const auto& id : dirty_)
+        if (rows_.count(id)) ids.push_back(id);
+    }
+    std::sort(ids.begin(), ids.end());
+    return ids;
+  }
+  std::vector<std::string> mix_removed() const {
+    if (full_) return {};
+    std::vector<std::string> v(removed_.begin(), removed_.end());
+    std::sort(v.begin(), v.end());
+    return v;
+  }
+  bool version_of(const std::string& id, uint64_t* v) const {
+    auto it = version_.find(id);
+    if (it == version_.end()) { *v = 0; return false; }
+    *v = it->second;
+    return true;
+  }
+  bool holds(const std::string& id) const { return rows_.count(id) != 0; }
+  void row_view(const std::string& id, const jb::row::Datum** d, const std::vector<int32_t>** ix,
+                const std::vector<float>** vx) const {
+    const Row& r = rows_.at(id);
+    *d = &r.d;
+    *ix = &r.idx;
+    *vx = &r.val;
+  }
+  int32_t slot_id(const std::string& id) const {
+    auto it = rows_.find(id);
+    return it == rows_.end() ? -1 : it->second.slot;
+  }
+  void store_mixed(const std::string& id, jb::row::Datum&& d, const std::vector<int32_t>& idx,
+                   const std::vector<float>& val, uint64_t v) {
+    Row r;
+    r.d = std::move(d);
+    r.idx = idx;
+    r.val = val;
+    write(id, std::move(r));
+    version_[id] = v;
+  }
+  void remove_mixed(const std::string& id, uint64_t v) {
+    rows_.erase(id);
+    version_[id] = v;
+  }
+  bool weight_diff(int64_t* docs, int64_t* len, std::vector<int64_t>*, std::vector<int64_t>*) const {
+    *docs = *len = 0;
+    return false;
+  }
+  void put_weight_diff(int64_t, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&) {}
+  void mix_done() {
+    dirty_.clear();
+    removed_.clear();
+  }
+
+ private:
+  void write(const std::string& id, Row&& r) {
+    auto it = rows_.find(id);
+    r.slot = it != rows_.end() ? it->second.slot : next_slot_++;
+    rows_[id] = std::move(r);
+  }
+  std::mutex mu_;
+  std::map<std::string, Row> rows_;
+  std::map<std::string, uint64_t> version_;
+  std::set<std::string> dirty_, removed_;
+  int32_t next_slot_ = 0;
+  bool full_ = false;
+  size_t last_applied_ = 0;
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
   std::string zk, name;
   int port = 0, H = 1024, ic = 10, icount = 0, isec = 0, zkt = 10;
+  bool rows_mode = false;
   int c;
-  while ((c = getopt(argc, argv, "z:n:p:H:I:i:s:Z:")) != -1) {
+  while ((c = getopt(argc, argv, "z:n:p:H:I:i:s:Z:R")) != -1) {
     switch (c) {
+      case 'R': rows_mode = true; break;
       case 'z': zk = optarg; break;
       case 'n': name = optarg; break;
       case 'p': port = atoi(optarg); break;
@@ -277,6 +445,8 @@ int main(int argc, char** argv) {
   signal(SIGPIPE, SIG_IGN);
 
   HostModel model(H);
+  HostRowModel rmodel;
+  jb::mix::Mixable* mixable = rows_mode ? (jb::mix::Mixable*)&rmodel : (jb::mix::Mixable*)&model;
   std::unique_ptr<jb::mix::LinearMixer> mixer;
   const std::string ident = "127.0.0.1_" + std::to_string(port);
   jb::RpcServer rpc(
@@ -292,10 +462,22 @@ int main(int argc, char** argv) {
             return resp_ok(r.msgid, Value::integer(n));
           }
           if (r.method == "model") return resp_ok(r.msgid, model.model());
+          if (r.method == "put" && a.size() == 4) {
+            const int64_t n = rmodel.put(a[1].as_uint(), a[2].as_int(), a[3].as_int());
+            if (mixer) mixer->updated((uint64_t)n);
+            return resp_ok(r.msgid, Value::integer(n));
+          }
+          if (r.method == "remove" && a.size() == 2) {
+            const bool ok = rmodel.remove(a[1].as_str());
+            if (mixer && ok) mixer->updated(1);
+            return resp_ok(r.msgid, Value::boolean(ok));
+          }
+          if (r.method == "rows") return resp_ok(r.msgid, rmodel.rows());
           if (r.method == "do_mix") return resp_ok(r.msgid, Value::boolean(mixer && mixer->do_mix()));
           if (r.method == "get_status") {
             std::vector<std::pair<std::string, std::string>> st;
-            model.status(&st);
+            if (rows_mode) rmodel.status(&st);
+            else model.status(&st);
             if (mixer) mixer->status(&st);
             std::vector<std::pair<Value, Value>> m;
             for (auto& kv : st) m.emplace_back(Value::str(kv.first), Value::str(kv.second));
@@ -309,21 +491,22 @@ int main(int argc, char** argv) {
       2, 0.0);
   rpc.listen("127.0.0.1", port);
   rpc.start();
-  jb::mix::ClusterNode node(zk, zkt, "classifier", name);
+  const char* type = rows_mode ? "recommender" : "classifier";
+  jb::mix::ClusterNode node(zk, zkt, type, name);
   if (!node.config_rlock()) {
     fprintf(stderr, "failed to get config lock\n");
     return 1;
   }
   node.register_actor("127.0.0.1", port);
   jb::mix::MixerArgs ma;
-  ma.type = "classifier";
+  ma.type = type;
   ma.name = name;
   ma.eth = "127.0.0.1";
   ma.port = port;
   ma.interval_sec = isec;
   ma.interval_count = icount;
   ma.interconnect_timeout = ic;
-  mixer.reset(new jb::mix::LinearMixer(node.coord(), ma, &model, [](Group& g, double) {
+  mixer.reset(new jb::mix::LinearMixer(node.coord(), ma, mixable, [](Group& g, double) {
     return std::unique_ptr<jb::mix::Plane>(new jb::mix::HostPlane(&g.star()));
   }));
   mixer->start();
