@@ -10,6 +10,15 @@
 // or analysis, handler writing the result), pack / unpack of its model
 // payload (the same msgpack maps as the Python drivers, so model files move
 // between the two servers) and its status keys.
+//
+// Distributed mode (-z, linear mixer): an engine that can mix supplies its
+// diff and the fold of every member's diff (the Python drivers' get_diff /
+// mix_diff / put_diff, folded in rank order on every member); the server
+// joins the cluster (coordinator membership, config lock, actor node, CHT
+// vnodes when the engine routes by CHT) and runs the native linear mixer
+// (csrc/native/jb_mix_group.hpp): the diffs move as byte strings over the
+// group's plane - the control plane for the host engines, RCCL all-gather
+// for an engine with device state (clustering).
 #pragma once
 #include <atomic>
 #include <functional>
@@ -19,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "jb_mix_group.hpp"
 #include "jb_rpc.hpp"
 #include "jb_server_common.hpp"
 #include "jb_value.hpp"
@@ -44,6 +54,15 @@ class HostEngine {
   virtual void unpack(const Value& obj) = 0;
   virtual void clear() = 0;
   virtual void status(std::vector<std::pair<std::string, std::string>>* st) = 0;
+  // ---- distributed mode (model lock held exclusively by the caller)
+  virtual bool mixable() const { return false; }
+  virtual bool uses_cht() const { return false; }
+  virtual std::string get_diff() { return std::string(); }            // msgpack
+  virtual void put_diffs(const std::vector<Value>& parts) { (void)parts; }  // every rank's, rank order
+  virtual std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& s, double dl) {
+    (void)dl;
+    return std::unique_ptr<jb::mix::Plane>(new jb::mix::HostPlane(&s));
+  }
 };
 
 // a method error reported to the client as the message string
@@ -51,7 +70,7 @@ struct EngineError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
-class HostServer {
+class HostServer : public jb::mix::Mixable {
  public:
   // make(config text) -> engine, or throws (the config is validated first)
   using Factory = std::function<std::unique_ptr<HostEngine>(const std::string&)>;
@@ -63,6 +82,41 @@ class HostServer {
   }
 
   void load_file(const std::string& path) { load_impl(path, true); }
+
+  // distributed mode (-z): coordinator session, config read lock
+  void join_cluster(std::unique_ptr<jb::mix::ClusterNode> node) {
+    node_ = std::move(node);
+    a_.connected_zookeeper = node_->connected();
+    if (!node_->config_rlock()) throw std::runtime_error("failed to get config lock");
+  }
+
+  // ---- jb::mix::Mixable: one MIX / the obsolete hand-over (mixer thread)
+  uint64_t mix(jb::mix::Group& g) override {
+    std::unique_lock<std::shared_mutex> lk(model_mu_);
+    const std::string mine = eng_->get_diff();
+    const auto raw = g.plane().allgather_bytes(g.star(), mine, g.deadline());
+    std::vector<Value> parts;
+    uint64_t bytes = 0;
+    for (const auto& r : raw) {
+      parts.push_back(MsgpackReader((const uint8_t*)r.data(), r.size()).read());
+      bytes += r.size();
+    }
+    eng_->put_diffs(parts);
+    return bytes;
+  }
+  void hand_over(jb::mix::Group& g, int src, bool apply) override {
+    std::string mine;
+    if (g.rank() == src) {
+      std::shared_lock<std::shared_mutex> lk(model_mu_);
+      mine = eng_->pack();
+    }
+    const std::string got = g.plane().bcast_bytes(g.star(), src, mine, g.deadline());
+    if (!apply || g.rank() == src) return;
+    const Value v = MsgpackReader((const uint8_t*)got.data(), got.size()).read();
+    if (v.kind != Value::ARR || v.a.size() != 2) throw std::runtime_error("hand-over: malformed model");
+    std::unique_lock<std::shared_mutex> lk(model_mu_);
+    eng_->unpack(v.a[1]);
+  }
 
   int run() {
     rpc_.reset(new jb::RpcServer([this](const jb::RpcRequest& r) { return dispatch(r); }, a_.threads, 0.0));
@@ -78,8 +132,30 @@ class HostServer {
     logf_("INFO", "start listening at port %d", port);
     cs_.start_time = time(nullptr);
     rpc_->start();
+    if (node_) {   // distributed mode: actor (+ CHT vnodes), then the mixer thread
+      node_->register_actor(a_.eth, a_.port);
+      if (eng_->uses_cht()) node_->register_cht(a_.eth, a_.port);
+      jb::mix::MixerArgs ma;
+      ma.type = engine_name();
+      ma.name = a_.name;
+      ma.eth = a_.eth;
+      ma.port = a_.port;
+      ma.interval_sec = a_.interval_sec;
+      ma.interval_count = a_.interval_count;
+      ma.interconnect_timeout = a_.ic_timeout;
+      mixer_.reset(new jb::mix::LinearMixer(node_->coord(), ma, this, [this](jb::mix::Group& g, double dl) {
+        return eng_->make_plane(g.star(), dl);
+      }));
+      mixer_->start();
+      logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
+    }
     logf_("INFO", "%s RPC server startup (native)", prog_name());
     wait_for_term();
+    if (mixer_) {
+      logf_("INFO", "stopping mixer thread");
+      mixer_->stop();
+    }
+    if (node_) node_->leave();
     logf_("INFO", "stopping RPC server");
     rpc_->stop();
     return 0;
@@ -112,6 +188,7 @@ class HostServer {
       MsgpackWriter w;
       try {
         if (x.update) {
+          if (mixer_) mixer_->updated(1);
           std::unique_lock<std::shared_mutex> g(model_mu_);
           update_count_ += 1;
           x.raw(r.params, &w);
@@ -136,7 +213,10 @@ class HostServer {
     MsgpackWriter w;
     try {
       const std::string& m = r.method;
-      if (m == "get_config" || m == "get_status" || m == "save" || m == "load") {
+      if (m == "do_mix" && mixer_) {
+        if (args.a.size() != 1) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+        w.boolean(mixer_->do_mix());
+      } else if (m == "get_config" || m == "get_status" || m == "save" || m == "load") {
         const size_t want = (m == "save" || m == "load") ? 2 : 1;
         if (args.a.size() != want || (want == 2 && !args.a[1].is_str()))
           return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
@@ -150,6 +230,7 @@ class HostServer {
           return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
         std::vector<Value> rest(args.a.begin() + 1, args.a.end());
         if (hm->update) {
+          if (mixer_) mixer_->updated(1);
           std::unique_lock<std::shared_mutex> g(model_mu_);
           update_count_ += 1;
           hm->fn(rest, &w);
@@ -180,6 +261,7 @@ class HostServer {
         std::shared_lock<std::shared_mutex> g(model_mu_);
         eng_->status(&st);
       }
+      if (mixer_) mixer_->status(&st);
       w->map(1);
       w->raw(ident());
       w->map(st.size());
@@ -242,6 +324,8 @@ class HostServer {
   Factory make_;
   std::unique_ptr<HostEngine> eng_;
   std::vector<HostMethod> table_;
+  std::unique_ptr<jb::mix::ClusterNode> node_;
+  std::unique_ptr<jb::mix::LinearMixer> mixer_;
   std::unique_ptr<jb::RpcServer> rpc_;
   std::shared_mutex model_mu_;
   std::mutex st_mu_;
@@ -252,17 +336,21 @@ class HostServer {
 // main() of a host-engine server: flags, config check (native vs Python),
 // model file, serve
 template <class Check>
-int host_main(int argc, char** argv, const char* engine, Check check, HostServer::Factory make) {
+int host_main(int argc, char** argv, const char* engine, Check check, HostServer::Factory make,
+              bool native_dist = false) {
   set_engine(engine);
   Args a;
   std::string text;
-  const int rc = startup(argc, argv, &a, &text, check, /*needs_gpu=*/false);
+  const int rc = startup(argc, argv, &a, &text, check, /*needs_gpu=*/false, native_dist);
   if (rc >= 0) return rc;
   block_signals();
   logf_("INFO", "starting %s %s RPC server at %s:%d (native, host engine)", prog_name(), kVersion,
         a.eth.c_str(), a.port);
   try {
     HostServer srv(a, text, make);
+    if (!a.zookeeper.empty())
+      srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
+          new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), engine, a.name)));
     if (!a.model_file.empty()) srv.load_file(a.model_file);
     return srv.run();
   } catch (const std::exception& e) {

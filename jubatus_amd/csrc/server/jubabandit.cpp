@@ -95,13 +95,18 @@ class Bandit : public HostEngine {
            arms_.erase(it);
            for (auto& kv : info_) kv.second.erase(arm);
            for (auto& kv : logw_) kv.second.erase(arm);
+           for (auto& kv : dinfo_) kv.second.erase(arm);
+           for (auto& kv : dlogw_) kv.second.erase(arm);
            w->boolean(true);
          }},
         {"select_arm", 2, true, [this](const std::vector<Value>& a, MsgpackWriter* w) {
            const std::string& player = arg_str(a[0]);
            if (arms_.empty()) throw EngineError("select_arm: no arm registered");
            const std::string arm = choose(player);
-           if (p_.assume_unrewarded) info_[player][arm].n += 1;
+           if (p_.assume_unrewarded) {
+             info_[player][arm].n += 1;
+             dinfo_[player][arm].n += 1;
+           }
            w->raw(arm);
          }},
         {"register_reward", 4, true, [this](const std::vector<Value>& a, MsgpackWriter* w) {
@@ -112,11 +117,14 @@ class Bandit : public HostEngine {
            if (it == arms_.end()) { w->boolean(false); return; }
            if (p_.method == "exp3") {
              const double pr = exp3_probs(player)[(size_t)(it - arms_.begin())];
-             logw_[player][arm] += p_.gamma * (r / pr) / (double)arms_.size();
+             const double dl = p_.gamma * (r / pr) / (double)arms_.size();
+             logw_[player][arm] += dl;
+             dlogw_[player][arm] += dl;
            }
-           ArmInfo& ai = info_[player][arm];
-           ai.n += p_.assume_unrewarded ? 0 : 1;
-           ai.w += r;
+           for (ArmInfo* ai : {&info_[player][arm], &dinfo_[player][arm]}) {
+             ai->n += p_.assume_unrewarded ? 0 : 1;
+             ai->w += r;
+           }
            w->boolean(true);
          }},
         {"get_arm_info", 2, false, [this](const std::vector<Value>& a, MsgpackWriter* w) {
@@ -134,6 +142,8 @@ class Bandit : public HostEngine {
            const std::string& player = arg_str(a[0]);
            info_.erase(player);
            logw_.erase(player);
+           dinfo_.erase(player);
+           dlogw_.erase(player);
            w->boolean(true);
          }},
         {"clear", 1, true, [this](const std::vector<Value>&, MsgpackWriter* w) {
@@ -147,6 +157,66 @@ class Bandit : public HostEngine {
     arms_.clear();
     info_.clear();
     logw_.clear();
+    dinfo_.clear();
+    dlogw_.clear();
+  }
+
+  // ---- MIX (models/bandit.py get_diff / mix_diff / put_diff): each member
+  // ships its arm list and the (trial, reward) / exp3 log-weight increments
+  // since the last MIX; every member adds the cluster's increments
+  bool mixable() const override { return true; }
+  bool uses_cht() const override { return true; }
+  std::string get_diff() override {
+    MsgpackWriter u;
+    u.arr(3);
+    u.arr(arms_.size());
+    for (const auto& a : arms_) u.str(a);
+    u.map(dinfo_.size());
+    for (const auto& pp : dinfo_) {
+      u.str(pp.first);
+      u.map(pp.second.size());
+      for (const auto& aa : pp.second) {
+        u.str(aa.first);
+        u.arr(2);
+        u.sint(aa.second.n);
+        u.dbl(aa.second.w);
+      }
+    }
+    u.map(dlogw_.size());
+    for (const auto& pp : dlogw_) {
+      u.str(pp.first);
+      u.map(pp.second.size());
+      for (const auto& aa : pp.second) { u.str(aa.first); u.dbl(aa.second); }
+    }
+    return std::move(u.out);
+  }
+  void put_diffs(const std::vector<Value>& parts) override {
+    for (const Value& d : parts)
+      if (d.kind != Value::ARR || d.a.size() != 3) throw std::runtime_error("mix: malformed bandit diff");
+    for (const Value& d : parts)
+      for (const Value& a : d.a[0].a)
+        if (std::find(arms_.begin(), arms_.end(), a.s) == arms_.end()) arms_.push_back(a.s);
+    // my totals already hold my increments: add everyone's, less mine
+    for (const auto& pp : dinfo_)
+      for (const auto& aa : pp.second) {
+        ArmInfo& t = info_[pp.first][aa.first];
+        t.n -= aa.second.n;
+        t.w -= aa.second.w;
+      }
+    for (const auto& pp : dlogw_)
+      for (const auto& aa : pp.second) logw_[pp.first][aa.first] -= aa.second;
+    for (const Value& d : parts) {
+      for (const auto& pp : d.a[1].o)
+        for (const auto& aa : pp.second.o) {
+          ArmInfo& t = info_[pp.first][aa.first];
+          t.n += (int64_t)aa.second.a.at(0).num();
+          t.w += aa.second.a.at(1).num();
+        }
+      for (const auto& pp : d.a[2].o)
+        for (const auto& aa : pp.second.o) logw_[pp.first][aa.first] += aa.second.num();
+    }
+    dinfo_.clear();
+    dlogw_.clear();
   }
 
   // models/bandit.py pack(): {"method", "arms", "info": {player: {arm: [n, w]}}, "exp3": {player: {arm: logw}}}
@@ -276,6 +346,9 @@ class Bandit : public HostEngine {
   std::vector<std::string> arms_;
   std::map<std::string, std::map<std::string, ArmInfo>> info_;
   std::map<std::string, std::map<std::string, double>> logw_;
+  // increments since the last MIX (distributed mode)
+  std::map<std::string, std::map<std::string, ArmInfo>> dinfo_;
+  std::map<std::string, std::map<std::string, double>> dlogw_;
 };
 
 }  // namespace
@@ -292,5 +365,6 @@ int main(int argc, char** argv) {
         std::string why;
         if (!parse_params(text, &p, &why)) throw std::runtime_error(why);
         return std::unique_ptr<HostEngine>(new Bandit(p));
-      });
+      },
+      /*native_dist=*/true);
 }

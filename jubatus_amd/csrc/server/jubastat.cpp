@@ -167,6 +167,35 @@ class Stat : public HostEngine {
   double f_max(const KeyStat& s) { return s.mx; }
   double f_min(const KeyStat& s) { return s.mn; }
 
+  // ---- MIX (models/stat.py get_diff / mix_diff / put_diff): the cluster's
+  // entropy terms sum over the members' windows
+  bool mixable() const override { return true; }
+  bool uses_cht() const override { return true; }
+  std::string get_diff() override {
+    MsgpackWriter w;
+    w.arr(2);
+    w.dbl(local_e());
+    w.sint((int64_t)window_.size());
+    return std::move(w.out);
+  }
+  void put_diffs(const std::vector<Value>& parts) override {
+    double e = 0;
+    int64_t n = 0;
+    for (const Value& p : parts) {
+      if (p.kind != Value::ARR || p.a.size() != 2) throw std::runtime_error("mix: malformed stat diff");
+      e += p.a[0].num();
+      n += (int64_t)p.a[1].num();
+    }
+    mixed_e_ = e;
+    mixed_n_ = n;
+  }
+
+  double local_e() const {
+    double e = 0;
+    for (const auto& kv : stats_) e += (double)kv.second.n * log((double)kv.second.n);
+    return e;
+  }
+
   double entropy() const {
     double e;
     int64_t n;
@@ -174,8 +203,7 @@ class Stat : public HostEngine {
       e = mixed_e_;
       n = mixed_n_;
     } else {
-      e = 0;
-      for (const auto& kv : stats_) e += (double)kv.second.n * log((double)kv.second.n);
+      e = local_e();
       n = (int64_t)window_.size();
     }
     if (n == 0) return 0.0;
@@ -210,5 +238,6 @@ int main(int argc, char** argv) {
         std::string why;
         if (!check_config(text, &why, &w)) throw std::runtime_error(why);
         return std::unique_ptr<HostEngine>(new Stat(w));
-      });
+      },
+      /*native_dist=*/true);
 }

@@ -195,6 +195,48 @@ class Weight : public HostEngine {
 
   WideConfig cfg_;
   std::unique_ptr<jb::HostFvWide> hw_;
+ public:
+  // ---- MIX (models/weight.py: WeightManager get_diff / mix / put_diff): the
+  // document statistics each member counted since the last MIX; the
+  // cluster's sum replaces this member's contribution
+  bool mixable() const override { return true; }
+  std::string get_diff() override {
+    MsgpackWriter u;
+    u.arr(4);
+    u.sint(counts_[2]);
+    u.sint(counts_[3]);
+    std::vector<int64_t> ix, cn;
+    for (size_t i = 0; i < diff_.size(); ++i)
+      if (diff_[i]) { ix.push_back((int64_t)i); cn.push_back(diff_[i]); }
+    u.bin(ix.data(), ix.size() * 8);
+    u.bin(cn.data(), cn.size() * 8);
+    return std::move(u.out);
+  }
+  void put_diffs(const std::vector<Value>& parts) override {
+    int64_t docs = 0, len = 0;
+    std::vector<int64_t> acc(df_.size(), 0);
+    for (const Value& d : parts) {
+      if (d.kind != Value::ARR || d.a.size() != 4) throw std::runtime_error("mix: malformed weight diff");
+      docs += (int64_t)d.a[0].num();
+      len += (int64_t)d.a[1].num();
+      const std::string& ix = d.a[2].s;
+      const std::string& cn = d.a[3].s;
+      const size_t n = std::min(ix.size(), cn.size()) / 8;
+      for (size_t k = 0; k < n; ++k) {
+        int64_t i, c;
+        memcpy(&i, ix.data() + 8 * k, 8);
+        memcpy(&c, cn.data() + 8 * k, 8);
+        if (i >= 0 && (size_t)i < acc.size()) acc[(size_t)i] += c;
+      }
+    }
+    counts_[0] += docs - counts_[2];
+    counts_[1] += len - counts_[3];
+    for (size_t i = 0; i < df_.size(); ++i) df_[i] = std::max<int64_t>(0, df_[i] - diff_[i] + acc[i]);
+    std::fill(diff_.begin(), diff_.end(), 0);
+    counts_[2] = counts_[3] = 0;
+  }
+
+ private:
   std::vector<int64_t> df_, diff_;
   int64_t counts_[4] = {0, 0, 0, 0};
   std::vector<int32_t> idx_;
@@ -212,5 +254,6 @@ int main(int argc, char** argv) {
         std::string why;
         if (!check_config(text, &why, &cfg)) throw std::runtime_error(why);
         return std::unique_ptr<HostEngine>(new Weight(std::move(cfg)));
-      });
+      },
+      /*native_dist=*/true);
 }

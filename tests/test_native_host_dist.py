@@ -1,0 +1,178 @@
+"""Distributed mode of the native host-engine servers on the CPU (no GPU, no
+Python in the server processes): two jubastat / jubabandit / jubaweight
+servers join a cluster through the native coordinator, register their actor
+(and CHT vnodes for the CHT-routed engines), and mix with the native linear
+mixer over the control plane (csrc/server/jb_host_server.hpp). After a MIX
+both answer as one server holding everything would: stat's entropy over the
+cluster's windows, bandit's summed arm statistics, weight's document
+frequencies. Reference: linear_mixer.cpp:358-544 and the Python drivers'
+get_diff / mix_diff / put_diff (models/{stat,bandit,weight}.py)."""
+import json
+import math
+import os
+import socket
+import subprocess
+import tempfile
+import time
+
+import pytest
+
+from jubatus_amd.client import Client, Datum
+from jubatus_amd.common import config as zkconfig
+from jubatus_amd.common import membership as mb
+from jubatus_amd.common.coordinator import NativeCoordinator, native_available
+from jubatus_amd.common.lock_service import CoordinatorClient
+from jubatus_amd.common.mprpc import wait_server
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NB = os.path.join(ROOT, "jubatus_amd", "native_bin")
+
+pytestmark = pytest.mark.skipif(not (native_available() and os.path.exists(os.path.join(NB, "jubastat"))),
+                                reason="native binaries not built")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def coord():
+    srv = NativeCoordinator(0, "127.0.0.1")
+    yield srv
+    srv.stop()
+
+
+def status(c):
+    (_, st), = c.get_status().items()
+    return {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
+            for k, v in st.items()}
+
+
+class Cluster:
+    def __init__(self, coord, engine, name, cfg, n=2, extra=()):
+        self.ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
+        zkconfig.config_tozk(self.ls, engine, name, json.dumps(cfg))
+        self.engine, self.name = engine, name
+        self.ports = [free_port() for _ in range(n)]
+        self.procs = []
+        for p in self.ports:
+            log = open(os.path.join(tempfile.gettempdir(), f"hostdist_{name}_{p}.log"), "wb")
+            self.procs.append(subprocess.Popen(
+                [os.path.join(NB, f"juba{engine}"), "-z", f"127.0.0.1:{coord.port}", "-n", name, "-p", str(p),
+                 "-b", "127.0.0.1", "-s", "0", "-i", "0", "-I", "5", "-Z", "5", *extra],
+                stdout=subprocess.DEVNULL, stderr=log))
+        for p in self.ports:
+            assert wait_server("127.0.0.1", p, 60)
+        self.c = [Client("127.0.0.1", p, name, timeout=30.0) for p in self.ports]
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            sts = [status(c) for c in self.c]
+            if all(s.get("linear_mixer.group_size") == str(n) and s.get("linear_mixer.is_obsolete") == "0"
+                   for s in sts):
+                break
+            time.sleep(0.2)
+        else:
+            raise AssertionError("group did not form")
+
+    def mix(self):
+        assert self.c[0].do_mix() is True
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            if all(int(status(c).get("linear_mixer.mix_count", "0")) >= 1 for c in self.c):
+                return
+            time.sleep(0.1)
+
+    def close(self):
+        for c in self.c:
+            c.close()
+        for p in self.procs:
+            if p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=15)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+        self.ls.close()
+
+
+def test_native_stat_distributed_entropy(coord):
+    cl = Cluster(coord, "stat", "sdist", {"window_size": 64})
+    try:
+        st = status(cl.c[0])
+        assert st["server_runtime"] == "native" and st["linear_mixer.runtime"] == "native"
+        assert st["is_standalone"] == "0"
+        # CHT-routed engine: 8 vnodes per server
+        assert len(cl.ls.list(mb.build_actor_path("stat", "sdist") + "/cht")) == 16
+        keys = {}
+        for i in range(20):
+            k = f"k{i % 5}"
+            # cht(1): a key lives on one server (k0, k1 here; the rest there)
+            cl.c[0 if k in ("k0", "k1") else 1].call("push", k, float(i))
+            keys[k] = keys.get(k, 0) + 1
+        cl.mix()
+        n = sum(keys.values())
+        want = math.log(n) - sum(c * math.log(c) for c in keys.values()) / n
+        for c in cl.c:
+            assert abs(c.call("entropy", "k0") - want) < 1e-9
+    finally:
+        cl.close()
+
+
+def test_native_bandit_distributed_arm_info(coord):
+    cl = Cluster(coord, "bandit", "bdist", {"method": "ucb1", "parameter": {"assume_unrewarded": False}})
+    try:
+        a, b = cl.c
+        a.call("register_arm", "x")
+        b.call("register_arm", "y")
+        for _ in range(3):
+            a.call("register_reward", "p", "x", 1.0)
+        b.call("register_arm", "x")
+        b.call("register_reward", "p", "x", 0.5)
+        b.call("register_reward", "p", "y", 2.0)
+        cl.mix()
+        want = {"x": [4, 3.5], "y": [1, 2.0]}
+        for c in cl.c:
+            info = {(k.decode() if isinstance(k, bytes) else k): list(v) for k, v in c.call("get_arm_info", "p").items()}
+            assert info == want, info
+        # increments after the MIX are shipped once, not again
+        a.call("register_reward", "p", "y", 1.0)
+        cl.mix()
+        for c in cl.c:
+            info = {(k.decode() if isinstance(k, bytes) else k): list(v) for k, v in c.call("get_arm_info", "p").items()}
+            assert info["y"] == [2, 3.0] and info["x"] == [4, 3.5], info
+    finally:
+        cl.close()
+
+
+def test_native_weight_distributed_idf(coord):
+    cfg = json.load(open(os.path.join(ROOT, "config/weight/default.json")))
+    cl = Cluster(coord, "weight", "wdist", cfg)
+    solo_port = free_port()
+    cfg_path = os.path.join(tempfile.gettempdir(), f"wsolo_{solo_port}.json")
+    json.dump(cfg, open(cfg_path, "w"))
+    solo = subprocess.Popen([os.path.join(NB, "jubaweight"), "-f", cfg_path, "-p", str(solo_port), "-b", "127.0.0.1"],
+                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        assert wait_server("127.0.0.1", solo_port, 60)
+        s = Client("127.0.0.1", solo_port, "", timeout=30.0)
+        docs = [Datum({"text": "the quick brown fox"}), Datum({"text": "the lazy dog"}),
+                Datum({"text": "quick quick fox"}), Datum({"text": "a dog and a fox"})]
+        for i, d in enumerate(docs):
+            cl.c[i % 2].call("update", d)
+            s.call("update", d)
+        cl.mix()
+        q = Datum({"text": "quick dog"})
+        want = sorted((k, round(v, 5)) for k, v in s.call("calc_weight", q))
+        for c in cl.c:
+            got = sorted((k, round(v, 5)) for k, v in c.call("calc_weight", q))
+            assert got == want, (got, want)
+        s.close()
+    finally:
+        if solo.poll() is None:
+            solo.terminate()
+            solo.wait(timeout=15)
+        cl.close()
