@@ -192,7 +192,7 @@ SERVERS = {
 HOST_SERVERS = {"jubastat", "jubabandit", "jubaburst", "jubagraph", "jubaweight", "jubaconv"}
 # servers with a native distributed mode (the model plane over RCCL)
 RCCL_SERVERS = {"jubaclassifier", "jubaregression", "jb_rccl_check", "jubarecommender",
-                "jubanearest_neighbor", "jubaanomaly"}
+                "jubanearest_neighbor", "jubaanomaly", "jubaclustering"}
 
 
 def build_servers(force: bool = False, nproc: int = 8) -> str:

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "jb_host_server.hpp"
+#include "jb_mix_device.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_pyrandom.hpp"
 #include "jb_wide_rules.hpp"
@@ -183,8 +184,53 @@ class Clustering : public HostEngine {
                                  (int)p_.n.size(), (const uint8_t*)p_.c.data(), (int)p_.c.size() / 2,
                                  (const uint8_t*)p_.blob.data(), p_.blob.size(), kKeySpace));
     HIPCHK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&mix_st_, hipStreamNonBlocking));
+    HIPCHK(hipGetDevice(&device_));
+    token_ = std::to_string((uint64_t)getpid() * 0x9E3779B97F4A7C15ull ^ (uint64_t)time(nullptr) ^
+                            (uint64_t)(uintptr_t)this);
   }
-  ~Clustering() override { (void)hipStreamDestroy(st_); }
+  ~Clustering() override {
+    (void)hipStreamDestroy(st_);
+    (void)hipStreamDestroy(mix_st_);
+  }
+
+  // ---------------------------------------------------------- MIX
+  // models/clustering.py get_diff / mix_diff / put_diff: every member ships
+  // its coresets (all buckets) under its token; each member clusters its
+  // own coresets plus every other member's (clustering_serv.cpp:108-142)
+  bool mixable() const override { return true; }
+  std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& s, double dl) override {
+    return jb::mix::make_device_plane(s, device_, mix_st_, dl);
+  }
+  // The members agree on the clustering of a MIX: every member clusters the
+  // coresets in rank order (its own at its rank) and seeds k-means++ from
+  // the largest revision among them, so the centers are the same everywhere.
+  std::string get_diff() override {
+    PointSet all;
+    for (const auto& b : buckets_) all.append(b);
+    MsgpackWriter u;
+    u.arr(3);
+    u.str(token_);
+    wire(u, all);
+    u.uint(revision_);
+    return std::move(u.out);
+  }
+  void put_diffs(const std::vector<Value>& parts) override {
+    PointSet before, after, others;
+    bool mine = false;
+    uint64_t rev = revision_;
+    for (const Value& d : parts) {
+      if (d.kind != Value::ARR || d.a.size() != 3) throw std::runtime_error("mix: malformed clustering diff");
+      rev = std::max<uint64_t>(rev, (uint64_t)d.a[2].num());
+      if (d.a[0].s == token_) { mine = true; continue; }
+      PointSet ps = unwire(d.a[1]);
+      others.append(ps);
+      (mine ? after : before).append(ps);
+    }
+    others_ = std::move(others);
+    revision_ = rev;
+    if (!buckets_.empty() || others_.size()) recluster(&before, &after);
+  }
 
   std::vector<HostMethod> methods() override {
     std::vector<HostMethod> m = {
@@ -500,10 +546,13 @@ class Clustering : public HostEngine {
   }
 
   // ---------------------------------------------------------- cluster
-  void recluster() {
+  // over this member's coresets and the others' (a MIX passes the others
+  // split around this member's rank: the rank order every member shares)
+  void recluster(const PointSet* before = nullptr, const PointSet* after = nullptr) {
     PointSet pts;
+    if (before) pts.append(*before);
     for (const auto& b : buckets_) pts.append(b);
-    pts.append(others_);
+    pts.append(after ? *after : others_);
     if ((int64_t)pts.size() < p_.k) return;
     std::vector<int64_t> keys;
     std::vector<std::string> dims;
@@ -764,6 +813,9 @@ class Clustering : public HostEngine {
   jb::PyRandom rng_;
   std::unique_ptr<jb::HostFvWide> hw_;
   hipStream_t st_ = nullptr;
+  hipStream_t mix_st_ = nullptr;   // the RCCL plane of the MIX
+  int device_ = 0;
+  std::string token_;              // this member's coresets in a MIX
   std::unordered_map<int64_t, std::string> names_;
   PointSet pending_, others_, core_;
   std::vector<PointSet> buckets_;
@@ -789,7 +841,7 @@ int main(int argc, char** argv) {
   std::string text;
   const int rc = startup(argc, argv, &a, &text,
                          [](const std::string& t, std::string* why) { return check_config(t, why, nullptr); },
-                         /*needs_gpu=*/true);
+                         /*needs_gpu=*/true, /*native_dist=*/true);
   if (rc >= 0) return rc;
   try {
     const int device = device_and_signals(a);
@@ -802,6 +854,9 @@ int main(int argc, char** argv) {
       if (!check_config(t, &why, &p)) throw std::runtime_error(why);
       return std::unique_ptr<HostEngine>(new Clustering(std::move(p)));
     });
+    if (!a.zookeeper.empty())
+      srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
+          new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), "clustering", a.name)));
     if (!a.model_file.empty()) srv.load_file(a.model_file);
     return srv.run();
   } catch (const std::exception& e) {

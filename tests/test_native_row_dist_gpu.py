@@ -168,3 +168,39 @@ def test_native_recommender_distributed_mix(coord):
     finally:
         stop(procs)
         ls.close()
+
+
+def test_native_clustering_distributed_mix_agrees(coord):
+    """two native jubaclustering servers (kmeans.json: 1000-point buckets)
+    each push their own points; after a MIX both cluster the union of the
+    members' coresets in the same order from the same revision: the same
+    k centers (clustering_serv.cpp:108-142; BASELINE config #5)"""
+    cfg_path = os.path.join(ROOT, "config/clustering/kmeans.json")
+    ls, ports, procs, (a, b) = _cluster(coord, "clustering", "cdist", cfg_path)
+    try:
+        rng = random.Random(11)
+        centers = [(0.0, 0.0), (10.0, 0.0), (0.0, 10.0)]
+
+        def pts(n, which):
+            out = []
+            for _ in range(n):
+                cx, cy = centers[rng.choice(which)]
+                out.append(Datum({"x": cx + rng.gauss(0, 0.5), "y": cy + rng.gauss(0, 0.5)}))
+            return out
+        assert a.call("push", pts(1000, [0, 1])) is True      # a closes one bucket
+        assert b.call("push", pts(1000, [1, 2])) is True
+        assert a.do_mix() is True
+        deadline = time.time() + 30
+        while time.time() < deadline and int(status(b).get("linear_mixer.mix_count", "0")) < 1:
+            time.sleep(0.1)
+        ca = sorted((round(d[1][0][1], 3), round(d[1][1][1], 3)) for d in a.call("get_k_center"))
+        cb = sorted((round(d[1][0][1], 3), round(d[1][1][1], 3)) for d in b.call("get_k_center"))
+        assert ca == cb, (ca, cb)
+        # every true center is found (a's and b's data together)
+        for cx, cy in centers:
+            assert min(abs(x - cx) + abs(y - cy) for x, y in ca) < 1.5, ca
+        sa = status(a)
+        assert sa["linear_mixer.runtime"] == "native" and int(sa["linear_mixer.last_mix_bytes"]) > 0
+    finally:
+        stop(procs)
+        ls.close()
