@@ -328,6 +328,39 @@ class Star {
     return out;
   }
 
+  // one round of a pairwise schedule (push mixers): every rank names its
+  // peer (-1: none this round) and gets the bytes its peer sent it; the
+  // leader routes the frames. Collective: every rank calls it once per round
+  std::string permute(int peer, const std::string& mine, double dl) {
+    if (world_ == 1) return std::string();
+    auto frame = [](int32_t to, const std::string& b) {
+      std::string f((const char*)&to, 4);
+      return f + b;
+    };
+    if (rank_ != 0) {
+      send_frame(fds_[0], frame(peer, mine), dl);
+      return recv_frame(fds_[0], dl);
+    }
+    std::vector<std::string> in((size_t)world_);
+    std::vector<int32_t> to((size_t)world_, -1);
+    in[0] = mine;
+    to[0] = peer;
+    for (int r = 1; r < world_; ++r) {
+      const std::string f = recv_frame(fds_[(size_t)r], dl);
+      if (f.size() < 4) throw std::runtime_error("control plane: short permute frame");
+      memcpy(&to[(size_t)r], f.data(), 4);
+      in[(size_t)r] = f.substr(4);
+    }
+    // rank r receives what its peer addressed to it (empty if none)
+    std::vector<std::string> out((size_t)world_);
+    for (int r = 0; r < world_; ++r) {
+      const int32_t d = to[(size_t)r];
+      if (d >= 0 && d < world_ && to[(size_t)d] == r) out[(size_t)d] = in[(size_t)r];
+    }
+    for (int r = 1; r < world_; ++r) send_frame(fds_[(size_t)r], out[(size_t)r], dl);
+    return out[0];
+  }
+
  private:
   int rank_, world_;
   std::vector<int> fds_;
@@ -354,6 +387,11 @@ class Plane {
   }
   virtual std::string bcast_bytes(Star& s, int root, const std::string& b, double dl) {
     return s.bcast_str(root, b, dl);
+  }
+  // one round of a pairwise schedule: this rank's bytes to `peer`, the
+  // peer's back (peer -1: no exchange this round, still a collective call)
+  virtual std::string exchange_bytes(Star& s, int peer, const std::string& mine, double dl) {
+    return s.permute(peer, mine, dl);
   }
 };
 
@@ -590,7 +628,75 @@ class Mixable {
   virtual uint64_t mix(Group& g) = 0;
   // obsolete protocol: rank `src` sends its whole model; apply = replace mine
   virtual void hand_over(Group& g, int src, bool apply) = 0;
+  // push mixers: one round of the pairwise schedule - a symmetric exchange
+  // with `peer` (-1: this rank sits the round out, but still takes part in
+  // the round's collective calls); -> bytes this rank sent
+  virtual uint64_t pair_mix(Group& g, int peer) {
+    (void)g;
+    (void)peer;
+    throw std::runtime_error("this model is not push-mixable");
+  }
+  virtual bool push_mixable() const { return false; }
+  // around the rounds of one push MIX (a model may forward what it received
+  // in earlier rounds of the same MIX, then forget its diff at the end)
+  virtual void push_begin() {}
+  virtual void push_end() {}
 };
+
+// Pairwise schedules of the push mixers (parallel/push_mixer.py, reference
+// random_mixer.hpp:45-59, broadcast_mixer.hpp:45-55, skip_mixer.hpp:46-57):
+// every rank derives the same rounds from (epoch, mix count); a round is a
+// perfect matching (peer -1 for a rank without one).
+inline std::vector<std::vector<int>> push_schedule(const std::string& kind, int n, int64_t epoch,
+                                                   uint64_t round_no) {
+  std::vector<std::vector<int>> rounds;
+  if (n <= 1) return rounds;
+  auto tournament = [&](int limit) {
+    std::vector<int> pl;
+    for (int i = 0; i < n; ++i) pl.push_back(i);
+    if (n % 2) pl.push_back(-1);
+    const int k = (int)pl.size();
+    for (int r = 0; r < k - 1 && (int)rounds.size() < limit; ++r) {
+      std::vector<int> m((size_t)n, -1);
+      for (int i = 0; i < k / 2; ++i) {
+        const int a = pl[(size_t)i], b = pl[(size_t)(k - 1 - i)];
+        if (a >= 0 && b >= 0) { m[(size_t)a] = b; m[(size_t)b] = a; }
+      }
+      rounds.push_back(m);
+      std::vector<int> nx{pl[0], pl[(size_t)(k - 1)]};
+      for (int i = 1; i < k - 1; ++i) nx.push_back(pl[(size_t)i]);
+      pl.swap(nx);
+    }
+  };
+  if (kind == "random_mixer") {
+    // one random perfect matching: a shuffle seeded by (epoch, round)
+    std::vector<int> order;
+    for (int i = 0; i < n; ++i) order.push_back(i);
+    uint64_t x = ((uint64_t)epoch << 20) ^ round_no ^ 0x9E3779B97F4A7C15ull;
+    for (int i = n - 1; i > 0; --i) {
+      x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+      std::swap(order[(size_t)i], order[(size_t)(x % (uint64_t)(i + 1))]);
+    }
+    std::vector<int> m((size_t)n, -1);
+    for (int i = 0; i + 1 < n; i += 2) { m[(size_t)order[(size_t)i]] = order[(size_t)i + 1]; m[(size_t)order[(size_t)i + 1]] = order[(size_t)i]; }
+    rounds.push_back(m);
+  } else if (kind == "broadcast_mixer") {
+    tournament(n);                     // every pair once
+  } else {                             // skip_mixer: strides N/2, N/4, ..., 1
+    int nstr = 0;
+    for (int st = n / 2; st >= 1; st /= 2) ++nstr;
+    if ((n & (n - 1)) == 0) {
+      for (int st = n / 2; st >= 1; st /= 2) {
+        std::vector<int> m((size_t)n, -1);
+        for (int r = 0; r < n; ++r) m[(size_t)r] = r ^ st;   // butterfly
+        rounds.push_back(m);
+      }
+    } else {
+      tournament(std::max(1, nstr));   // log2 rounds of the tournament
+    }
+  }
+  return rounds;
+}
 
 // fault injection (utils/fault.py rules mix_hang / mix_kill, phase and at=N)
 class Faults {
@@ -656,6 +762,7 @@ class Faults {
 };
 
 struct MixerArgs {
+  std::string kind = "linear_mixer";   // or random_mixer / broadcast_mixer / skip_mixer
   std::string type, name, eth;
   int port = 0;
   int interval_sec = 16, interval_count = 512;
@@ -663,7 +770,9 @@ struct MixerArgs {
   int protocol_version = 1;
 };
 
-// The linear mixer's stabilizer loop (parallel/linear_mixer.py CollectiveMixer).
+// The mixer's stabilizer loop (parallel/linear_mixer.py CollectiveMixer): the
+// linear mixer (all members fold every member's diff) or, with a push kind,
+// the rounds of a pairwise schedule (parallel/push_mixer.py PushMixer).
 class LinearMixer {
  public:
   LinearMixer(cc::Coord* coord, const MixerArgs& a, Mixable* model, PlaneFactory pf)
@@ -712,7 +821,7 @@ class LinearMixer {
 
   void status(std::vector<std::pair<std::string, std::string>>* st) {
     std::lock_guard<std::mutex> g(mu_);
-    auto add = [&](const std::string& k, const std::string& v) { st->emplace_back("linear_mixer." + k, v); };
+    auto add = [&](const std::string& k, const std::string& v) { st->emplace_back(a_.kind + "." + k, v); };
     add("count", std::to_string(counter_));
     add("ticktime", std::to_string((int64_t)ticktime_wall_));
     add("is_obsolete", obsolete_ ? "1" : "0");
@@ -805,7 +914,23 @@ class LinearMixer {
     if (!(flags[0] || flags[1])) return;
     faults_.on_mix("allreduce");
     const double t0 = now_s();
-    const uint64_t bytes = model_->mix(g);
+    uint64_t bytes = 0;
+    if (a_.kind == "linear_mixer") {
+      bytes = model_->mix(g);
+    } else {
+      // push mixers: the rounds of the pairwise schedule (push_mixer.cpp:335-408)
+      uint64_t round_no;
+      {
+        std::lock_guard<std::mutex> l(mu_);
+        round_no = mix_count_;
+      }
+      model_->push_begin();
+      for (const auto& m : push_schedule(a_.kind, g.world(), g.epoch(), round_no)) {
+        faults_.on_mix("pair");
+        bytes += model_->pair_mix(g, m[(size_t)g.rank()]);
+      }
+      model_->push_end();
+    }
     const double sec = now_s() - t0;
     std::lock_guard<std::mutex> l(mu_);
     mixed_locked(bytes, sec);

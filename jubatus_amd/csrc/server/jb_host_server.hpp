@@ -104,6 +104,22 @@ class HostServer : public jb::mix::Mixable {
     eng_->put_diffs(parts);
     return bytes;
   }
+  // push mixers: the pair folds its two diffs, lower rank first
+  uint64_t pair_mix(jb::mix::Group& g, int peer) override {
+    std::unique_lock<std::shared_mutex> lk(model_mu_);
+    const std::string mine = peer >= 0 ? eng_->get_diff() : std::string();
+    const std::string theirs = g.plane().exchange_bytes(g.star(), peer, mine, g.deadline());
+    if (peer < 0) return 0;
+    Value a = MsgpackReader((const uint8_t*)mine.data(), mine.size()).read();
+    Value b = MsgpackReader((const uint8_t*)theirs.data(), theirs.size()).read();
+    std::vector<Value> parts;
+    if (g.rank() < peer) { parts.push_back(std::move(a)); parts.push_back(std::move(b)); }
+    else { parts.push_back(std::move(b)); parts.push_back(std::move(a)); }
+    eng_->put_diffs(parts);
+    return mine.size();
+  }
+  bool push_mixable() const override { return true; }
+
   void hand_over(jb::mix::Group& g, int src, bool apply) override {
     std::string mine;
     if (g.rank() == src) {
@@ -136,6 +152,7 @@ class HostServer : public jb::mix::Mixable {
       node_->register_actor(a_.eth, a_.port);
       if (eng_->uses_cht()) node_->register_cht(a_.eth, a_.port);
       jb::mix::MixerArgs ma;
+      ma.kind = a_.mixer;
       ma.type = engine_name();
       ma.name = a_.name;
       ma.eth = a_.eth;
@@ -147,7 +164,7 @@ class HostServer : public jb::mix::Mixable {
         return eng_->make_plane(g.star(), dl);
       }));
       mixer_->start();
-      logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
+      logf_("INFO", "registered group membership as %s (native %s)", ident().c_str(), a_.mixer.c_str());
     }
     logf_("INFO", "%s RPC server startup (native)", prog_name());
     wait_for_term();
@@ -341,7 +358,7 @@ int host_main(int argc, char** argv, const char* engine, Check check, HostServer
   set_engine(engine);
   Args a;
   std::string text;
-  const int rc = startup(argc, argv, &a, &text, check, /*needs_gpu=*/false, native_dist);
+  const int rc = startup(argc, argv, &a, &text, check, /*needs_gpu=*/false, native_dist, native_dist);
   if (rc >= 0) return rc;
   block_signals();
   logf_("INFO", "starting %s %s RPC server at %s:%d (native, host engine)", prog_name(), kVersion,

@@ -1066,8 +1066,8 @@ class RowEngine {
   // store: the written rows' hashed vectors travel, receivers keep them
   size_t dirty_rows() const { return dirty_.size() + removed_.size(); }
   void pack_diff(MsgpackWriter& w) const { pack_row_diff(*this, w); }
-  size_t apply_diffs(const std::vector<Value>& parts, std::vector<int32_t>* changed) {
-    return apply_row_diffs(*this, parts, changed);
+  size_t apply_diffs(const std::vector<Value>& parts, std::vector<int32_t>* changed, bool forward = false) {
+    return apply_row_diffs(*this, parts, changed, forward);
   }
   // store interface of pack_row_diff / apply_row_diffs
   std::vector<std::string> mix_ids() const {
@@ -1098,13 +1098,21 @@ class RowEngine {
   }
   int32_t slot_id(const std::string& id) const { return slot(id); }
   void store_mixed(const std::string& id, Datum&& d, const std::vector<int32_t>& idx,
-                   const std::vector<float>& val, uint64_t v) {
+                   const std::vector<float>& val, uint64_t v, bool forward) {
     store(id, std::move(d), idx, val, false);
     version_[id] = v;
+    if (forward) {
+      dirty_.insert(id);
+      removed_.erase(id);
+    }
   }
-  void remove_mixed(const std::string& id, uint64_t v) {
+  void remove_mixed(const std::string& id, uint64_t v, bool forward) {
     remove(id, false);
     version_[id] = v;
+    if (forward) {
+      removed_.insert(id);
+      dirty_.erase(id);
+    }
   }
   bool weight_diff(int64_t* docs, int64_t* len, std::vector<int64_t>* idx, std::vector<int64_t>* cnt) const {
     if (!conv.uses_weights()) { *docs = *len = 0; return false; }

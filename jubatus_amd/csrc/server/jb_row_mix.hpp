@@ -86,8 +86,10 @@ inline void write_datum(MsgpackWriter& w, const Datum& d) {
 //                 const std::vector<float>**) const
 //   int32_t slot_id(const std::string&) const        (-1: none)
 //   void store_mixed(const std::string&, Datum&&, const std::vector<int32_t>&,
-//                    const std::vector<float>&, uint64_t version)
-//   void remove_mixed(const std::string&, uint64_t version)
+//                    const std::vector<float>&, uint64_t version, bool forward)
+//   void remove_mixed(const std::string&, uint64_t version, bool forward)
+//     (forward: a push MIX passes the row on in its later rounds - it stays
+//      in the written / removed sets until the MIX ends)
 //   bool weight_diff(int64_t*, int64_t*, std::vector<int64_t>*, std::vector<int64_t>*) const
 //   void put_weight_diff(int64_t, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&)
 //   void mix_done()                                   forget the written / removed sets
@@ -154,9 +156,12 @@ inline const std::string& diff_bin(const Value* b) {
 
 // fold every rank's diff (rank order) and apply what this store does not
 // hold yet; -> rows written (their slots appended to *changed, with the
-// slots of removed rows)
+// slots of removed rows). forward: one round of a push MIX (what was applied
+// is shipped again in the MIX's later rounds; the caller forgets the diff
+// when the MIX ends)
 template <class S>
-size_t apply_row_diffs(S& st, const std::vector<Value>& parts, std::vector<int32_t>* changed) {
+size_t apply_row_diffs(S& st, const std::vector<Value>& parts, std::vector<int32_t>* changed,
+                       bool forward = false) {
   struct Win {
     uint64_t v;
     size_t p, i;
@@ -217,7 +222,7 @@ size_t apply_row_diffs(S& st, const std::vector<Value>& parts, std::vector<int32
       }
       Datum dd;
       parse_datum(dat->a[w.i], &dd);
-      st.store_mixed(id, std::move(dd), idx, val, w.v);
+      st.store_mixed(id, std::move(dd), idx, val, w.v, forward);
       if (changed) changed->push_back(st.slot_id(id));
       ++written;
     }
@@ -227,7 +232,7 @@ size_t apply_row_diffs(S& st, const std::vector<Value>& parts, std::vector<int32
     if (!st.version_of(g.first, &have) || have <= g.second) {
       const int32_t s = st.slot_id(g.first);
       if (s >= 0 && changed) changed->push_back(s);
-      st.remove_mixed(g.first, g.second);
+      st.remove_mixed(g.first, g.second, forward);
     }
   }
   int64_t docs = 0, len = 0;
@@ -257,7 +262,7 @@ size_t apply_row_diffs(S& st, const std::vector<Value>& parts, std::vector<int32
     }
     st.put_weight_diff(docs, len, ks, cs);
   }
-  st.mix_done();
+  if (!forward) st.mix_done();
   return written;
 }
 

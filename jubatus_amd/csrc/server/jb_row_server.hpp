@@ -201,6 +201,35 @@ class Model : public jb::mix::Mixable {
     for (const auto& r : raw) bytes += r.size();
     return bytes;
   }
+  // push mixers: the pair folds its two row diffs, lower rank first
+  uint64_t pair_mix(jb::mix::Group& g, int peer) override {
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    std::string mine;
+    if (peer >= 0) {
+      MsgpackWriter w;
+      eng_->pack_diff(w);
+      mine = std::move(w.out);
+    }
+    const std::string theirs = g.plane().exchange_bytes(g.star(), peer, mine, g.deadline());
+    if (peer < 0) return 0;
+    Value a = MsgpackReader((const uint8_t*)mine.data(), mine.size()).read();
+    Value b = MsgpackReader((const uint8_t*)theirs.data(), theirs.size()).read();
+    std::vector<Value> parts;
+    if (g.rank() < peer) { parts.push_back(std::move(a)); parts.push_back(std::move(b)); }
+    else { parts.push_back(std::move(b)); parts.push_back(std::move(a)); }
+    std::vector<int32_t> changed;
+    const size_t n = eng_->apply_diffs(parts, &changed, /*forward=*/true);
+    if (kind_ == Kind::kAnomaly && n > 0) lof_.reset();
+    HIPCHK(hipStreamSynchronize(stream_));
+    last_mix_rows_ = n;
+    return mine.size();
+  }
+  bool push_mixable() const override { return true; }
+  void push_end() override {
+    std::unique_lock<std::shared_mutex> lk(mu_);
+    eng_->mix_done();
+  }
+
   // obsolete protocol: rank src's whole model replaces an obsolete member's
   void hand_over(jb::mix::Group& g, int src, bool apply) override {
     std::string mine;
@@ -721,6 +750,7 @@ class Server {
       node_->register_actor(a_.eth, a_.port);
       node_->register_cht(a_.eth, a_.port);
       jb::mix::MixerArgs ma;
+      ma.kind = a_.mixer;
       ma.type = type();
       ma.name = a_.name;
       ma.eth = a_.eth;
@@ -733,7 +763,7 @@ class Server {
         return m->make_plane(g.star(), dl);
       }));
       mixer_->start();
-      logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
+      logf_("INFO", "registered group membership as %s (native %s)", ident().c_str(), a_.mixer.c_str());
     }
     logf_("INFO", "%s RPC server startup (native)", prog_name());
     wait_for_term();
@@ -980,7 +1010,7 @@ inline int row_main(int argc, char** argv, Kind kind) {
   Config cfg;
   const int rc = startup(argc, argv, &a, &text, [&cfg, kind](const std::string& t, std::string* why) {
     return parse_config(kind, t, &cfg, why);
-  }, true, /*native_dist=*/true);
+  }, true, /*native_dist=*/true, /*native_push=*/true);
   if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
   try {

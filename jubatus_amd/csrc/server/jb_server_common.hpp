@@ -582,7 +582,7 @@ inline bool config_from_coordinator(const Args& a, std::string* text, std::strin
 // handed to the Python server
 template <class Check>
 int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool needs_gpu = true,
-            bool native_dist = false) {
+            bool native_dist = false, bool native_push = false) {
   int rc = parse_args(argc, argv, a);
   if (rc == -1) return 0;
   if (rc) return rc;
@@ -595,7 +595,9 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool
   const bool dist = !a->zookeeper.empty();
   if (!a->native_check) {
     if (dist && !native_dist) exec_python(argc, argv, "distributed mode");
-    if (dist && a->mixer != "linear_mixer") exec_python(argc, argv, "distributed mode with a push mixer");
+    const bool push = a->mixer == "random_mixer" || a->mixer == "broadcast_mixer" || a->mixer == "skip_mixer";
+    if (dist && a->mixer != "linear_mixer" && !(push && native_push))
+      exec_python(argc, argv, "distributed mode with a push mixer");
     if (needs_gpu && (a->cpu || getenv("JUBATUS_FORCE_CPU")))
       exec_python(argc, argv, "host backend requested");
     if (needs_gpu && access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");

@@ -841,7 +841,7 @@ int main(int argc, char** argv) {
   std::string text;
   const int rc = startup(argc, argv, &a, &text,
                          [](const std::string& t, std::string* why) { return check_config(t, why, nullptr); },
-                         /*needs_gpu=*/true, /*native_dist=*/true);
+                         /*needs_gpu=*/true, /*native_dist=*/true, /*native_push=*/true);
   if (rc >= 0) return rc;
   try {
     const int device = device_and_signals(a);

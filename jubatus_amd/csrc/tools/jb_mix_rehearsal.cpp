@@ -314,6 +314,27 @@ class HostRowModel : public jb::mix::Mixable {
     for (const auto& r : raw) bytes += r.size();
     return bytes;
   }
+  // push mixers: the pair folds its two diffs, lower rank first
+  uint64_t pair_mix(Group& grp, int peer) override {
+    std::lock_guard<std::mutex> g(mu_);
+    jb::val::MsgpackWriter w;
+    if (peer >= 0) jb::row::pack_row_diff(*this, w);
+    const std::string theirs = grp.plane().exchange_bytes(grp.star(), peer, w.out, grp.deadline());
+    if (peer < 0) return 0;
+    jb::val::Value a = jb::val::MsgpackReader((const uint8_t*)w.out.data(), w.out.size()).read();
+    jb::val::Value b = jb::val::MsgpackReader((const uint8_t*)theirs.data(), theirs.size()).read();
+    std::vector<jb::val::Value> parts;
+    if (grp.rank() < peer) { parts.push_back(a); parts.push_back(b); }
+    else { parts.push_back(b); parts.push_back(a); }
+    last_applied_ = jb::row::apply_row_diffs(*this, parts, nullptr, /*forward=*/true);
+    return w.out.size();
+  }
+  bool push_mixable() const override { return true; }
+  void push_end() override {
+    std::lock_guard<std::mutex> g(mu_);
+    mix_done();
+  }
+
   // obsolete protocol: rank src's whole store (every row as written) replaces mine
   void hand_over(Group& grp, int src, bool apply) override {
     std::lock_guard<std::mutex> g(mu_);
@@ -375,17 +396,19 @@ class HostRowModel : public jb::mix::Mixable {
     return it == rows_.end() ? -1 : it->second.slot;
   }
   void store_mixed(const std::string& id, jb::row::Datum&& d, const std::vector<int32_t>& idx,
-                   const std::vector<float>& val, uint64_t v) {
+                   const std::vector<float>& val, uint64_t v, bool forward) {
     Row r;
     r.d = std::move(d);
     r.idx = idx;
     r.val = val;
     write(id, std::move(r));
     version_[id] = v;
+    if (forward) { dirty_.insert(id); removed_.erase(id); }
   }
-  void remove_mixed(const std::string& id, uint64_t v) {
+  void remove_mixed(const std::string& id, uint64_t v, bool forward) {
     rows_.erase(id);
     version_[id] = v;
+    if (forward) { removed_.insert(id); dirty_.erase(id); }
   }
   bool weight_diff(int64_t* docs, int64_t* len, std::vector<int64_t>*, std::vector<int64_t>*) const {
     *docs = *len = 0;
@@ -418,10 +441,12 @@ int main(int argc, char** argv) {
   std::string zk, name;
   int port = 0, H = 1024, ic = 10, icount = 0, isec = 0, zkt = 10;
   bool rows_mode = false;
+  std::string kind = "linear_mixer";
   int c;
-  while ((c = getopt(argc, argv, "z:n:p:H:I:i:s:Z:R")) != -1) {
+  while ((c = getopt(argc, argv, "z:n:p:H:I:i:s:Z:Rx:")) != -1) {
     switch (c) {
       case 'R': rows_mode = true; break;
+      case 'x': kind = optarg; break;
       case 'z': zk = optarg; break;
       case 'n': name = optarg; break;
       case 'p': port = atoi(optarg); break;
@@ -499,6 +524,7 @@ int main(int argc, char** argv) {
   }
   node.register_actor("127.0.0.1", port);
   jb::mix::MixerArgs ma;
+  ma.kind = kind;
   ma.type = type;
   ma.name = name;
   ma.eth = "127.0.0.1";

@@ -41,11 +41,12 @@ def coord():
 
 
 class RowRank:
-    def __init__(self, zport, name, ic=5):
+    def __init__(self, zport, name, ic=5, mixer="linear_mixer"):
         self.port = free_port()
+        self.mixer = mixer
         log = open(os.path.join(tempfile.gettempdir(), f"rowmix_{name}_{self.port}.log"), "wb")
-        self.proc = subprocess.Popen([BIN, "-R", "-z", f"127.0.0.1:{zport}", "-n", name, "-p", str(self.port),
-                                      "-I", str(ic), "-i", "0", "-s", "0", "-Z", "3"],
+        self.proc = subprocess.Popen([BIN, "-R", "-x", mixer, "-z", f"127.0.0.1:{zport}", "-n", name, "-p",
+                                      str(self.port), "-I", str(ic), "-i", "0", "-s", "0", "-Z", "3"],
                                      stdout=subprocess.DEVNULL, stderr=log)
         assert wait_server("127.0.0.1", self.port, 30)
         self.c = RpcClient("127.0.0.1", self.port, 60.0)
@@ -74,10 +75,10 @@ class RowRank:
 
 def wait_group(ranks, n, timeout=60):
     deadline = time.time() + timeout
+    k = ranks[0].mixer
     while time.time() < deadline:
         sts = [r.status() for r in ranks]
-        if all(s.get("linear_mixer.group_size") == str(n) and s.get("linear_mixer.is_obsolete") == "0"
-               for s in sts):
+        if all(s.get(f"{k}.group_size") == str(n) and s.get(f"{k}.is_obsolete") == "0" for s in sts):
             return True
         time.sleep(0.2)
     return False
@@ -162,6 +163,53 @@ def test_late_row_rank_receives_the_store(coord):
         ranks.append(RowRank(coord.port, "late"))
         assert wait_group(ranks, 3)
         assert ranks[2].rows() == ranks[0].rows()
+    finally:
+        for r in ranks:
+            r.stop()
+
+
+@pytest.mark.parametrize("mixer", ["skip_mixer", "broadcast_mixer"])
+def test_push_mixers_reach_the_union(coord, mixer):
+    """push mixers (push_mixer.cpp:335-408): skip_mixer's butterfly rounds
+    (strides N/2, N/4, ..., 1) and broadcast_mixer's tournament both bring
+    every rank the union within one MIX - a round forwards what earlier
+    rounds delivered"""
+    ranks = [RowRank(coord.port, f"push_{mixer}", mixer=mixer) for _ in range(4)]
+    try:
+        assert wait_group(ranks, 4)
+        for i, r in enumerate(ranks):
+            r.call("put", 500 + i, 20, 1000)
+        want = set()
+        for r in ranks:
+            want |= set(r.rows())
+        assert ranks[0].call("do_mix") is True
+        deadline = time.time() + 20
+        while time.time() < deadline and any(set(r.rows()) != want for r in ranks):
+            time.sleep(0.1)
+        for r in ranks:
+            assert set(r.rows()) == want
+            assert int(r.status()[f"{mixer}.mix_count"]) >= 1
+    finally:
+        for r in ranks:
+            r.stop()
+
+
+def test_random_mixer_pairs_up(coord):
+    """random_mixer: one random perfect matching per MIX; each rank ends with
+    its own rows and its partner's"""
+    ranks = [RowRank(coord.port, "push_random", mixer="random_mixer") for _ in range(4)]
+    try:
+        assert wait_group(ranks, 4)
+        for i, r in enumerate(ranks):
+            r.call("put", 900 + i, 10, 1000)
+        before = [set(r.rows()) for r in ranks]
+        assert ranks[0].call("do_mix") is True
+        time.sleep(1.0)
+        after = [set(r.rows()) for r in ranks]
+        for i in range(4):
+            got = after[i] - before[i]
+            partners = [j for j in range(4) if j != i and before[j] <= after[i]]
+            assert len(partners) == 1 and got == before[partners[0]] - before[i], (i, partners)
     finally:
         for r in ranks:
             r.stop()
