@@ -116,6 +116,13 @@ class HostFvWide {
     return 0;
   }
 
+  // one datum at the cursor (HostFvHasher::hash_datum contract: 0 ok,
+  // 1 malformed, 2 out of slots); update: count it into the statistics
+  int hash_datum(Cursor& c, int32_t* idx, float* val, int64_t max_slots, int64_t* slots, bool update) {
+    if (global_ && (!df_ || !counts_)) return 1;
+    return datum(c, idx, val, max_slots, slots, update);
+  }
+
  private:
   bool match_key(const HostRule& r, const uint8_t* k, uint32_t kn) const {
     if (r.match_kind == 0) return true;

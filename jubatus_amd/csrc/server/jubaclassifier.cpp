@@ -46,6 +46,7 @@
 
 #include "jb_hash.hpp"
 #include "jb_hostfv.hpp"
+#include "jb_linear_conv.hpp"
 #include "jb_mix_device.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_pack.hpp"
@@ -105,6 +106,8 @@ struct Config {
   int method = -1;
   float C = 1.f;
   Rules rules;
+  bool wide = false;     // the wide rule set on the host (no GPU request scan)
+  WideRules wrules;
 };
 
 bool parse_config(const std::string& text, Config* c, std::string* why) {
@@ -131,7 +134,7 @@ bool parse_config(const std::string& text, Config* c, std::string* why) {
   Value empty;
   empty.kind = Value::MAP;
   c->rules.H = device_hash_max_size();   // unless the converter names hash_max_size
-  if (!build_rules(conv ? *conv : empty, &c->rules, why)) return false;
+  if (!build_linear_rules(conv ? *conv : empty, &c->rules, &c->wide, &c->wrules, why)) return false;
   c->text = text;
   return true;
 }
@@ -200,9 +203,7 @@ class Classifier : public jb::mix::Mixable {
     use_s_ = mid_ >= kMethodCW;
     H_ = cfg.rules.H;
     const Rules& r = cfg.rules;
-    hasher_.reset(new jb::HostFvHasher((const uint8_t*)r.s.data(), (int)r.s.size(),
-                                       (const uint8_t*)r.n.data(), (int)r.n.size(),
-                                       (const uint8_t*)r.blob.data(), r.blob.size(), H_));
+    conv_.configure(r, cfg.wide, cfg.wrules);
     const size_t rs = sizeof(jb::HostRule);
     for (void** p : {&d_srules_, &d_nrules_, (void**)&d_blob_})
       if (*p) { HIPCHK(hipFree(*p)); *p = nullptr; }
@@ -230,7 +231,7 @@ class Classifier : public jb::mix::Mixable {
     train_batches += 1;
     update_count += R;
     std::vector<int64_t> counts(R);
-    bool gpu_ok = R > 0;
+    bool gpu_ok = R > 0 && !conv_.wide();   // the wide rule set hashes on the host
     uint64_t used = 0;
     for (size_t k = 0; k < R && gpu_ok; ++k) {
       counts[k] = body_count(arena + reqs[k].off, reqs[k].len);
@@ -314,7 +315,7 @@ class Classifier : public jb::mix::Mixable {
       first[k] = n;
       const int64_t n0 = n, s0 = slots;
       while (true) {
-        int rc = hasher_->hash_body(bodies[k].first, bodies[k].second, cidx_.p, cval_.p, row_.p,
+        int rc = conv_.hash_body(bodies[k].first, bodies[k].second, cidx_.p, cval_.p, row_.p,
                                     (int64_t)row_.cap - 1, (int64_t)cidx_.cap, &n, &slots);
         if (rc == 2) {   // grow and re-hash this body
           n = n0;
@@ -403,6 +404,7 @@ class Classifier : public jb::mix::Mixable {
     HIPCHK(hipDeviceSynchronize());
     count_base_.clear();
     labels_.clear();
+    conv_.clear();
     alloc_locked(kLabelCaps[0], true);
   }
 
@@ -452,8 +454,8 @@ class Classifier : public jb::mix::Mixable {
     u.str("rows"); u.bin(rows.data(), rows.size() * 8);
     u.str("W"); u.bin(Wr.data(), Wr.size() * 4);
     u.str("P"); u.bin(Sr.data(), Sr.size() * 4);
-    u.str("weights"); u.arr(3); u.uint(0); u.uint(0);
-    u.map(2); u.str("idx"); u.arr(0); u.str("df"); u.arr(0);
+    u.str("weights");
+    conv_.pack(u);
     return std::move(u.out);
   }
 
@@ -502,6 +504,7 @@ class Classifier : public jb::mix::Mixable {
       }
       HIPCHK(hipMemcpy(S_, S.data(), S.size() * 4, hipMemcpyHostToDevice));
     }
+    conv_.unpack(obj.get("weights"));
   }
 
   // ------------------------------------------------------------ MIX
@@ -642,6 +645,19 @@ class Classifier : public jb::mix::Mixable {
         count_base_[canon[c]] = nb;
       }
       HIPCHK(hipStreamSynchronize(compute_));
+    }
+    // 6. the document statistics of idf / bm25 converters (the reference
+    //    mixes the weight manager with the model)
+    if (conv_.global()) {
+      std::string dm;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        dm = conv_.get_diff();
+      }
+      const auto parts = pl.allgather_bytes(star, dm, grp.deadline());
+      std::lock_guard<std::mutex> g(mu_);
+      conv_.put_diffs(parts);
+      bytes += dm.size();
     }
     last_applied_ = applied;
     return bytes;
@@ -1012,33 +1028,43 @@ class Classifier : public jb::mix::Mixable {
     int64_t slots = 0;
     HostBuf<int64_t>& row = hrow_;
     row.get((size_t)cnt + 1)[0] = 0;
+    // the document statistics this request counts are undone if it fails
+    // (the wide converter's idf / bm25); out of slots: grow, hash it again
+    const jb::Cursor start = c;
+    conv_.begin();
     for (uint32_t k = 0; k < cnt; ++k) {
       uint32_t two;
       const uint8_t* ls;
       uint32_t ln;
-      if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { *res = -1; return; }
+      if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { conv_.rollback(); *res = -1; return; }
       labs.emplace_back(ls, ln);
-      while (true) {
-        jb::Cursor save = c;
-        const int64_t s0 = slots;
-        const int64_t cap = (int64_t)std::max<size_t>(hidx_.cap, 256);
-        int rc = hasher_->hash_datum(c, hidx_.get(cap), hval_.get(cap), cap, &slots);
-        if (rc == 2) { c = save; slots = s0; hidx_.get(2 * cap); hval_.get(2 * cap); continue; }
-        if (rc != 0) { *res = -1; return; }
-        break;
+      const int64_t cap = (int64_t)std::max<size_t>(hidx_.cap, 256);
+      int rc = conv_.hash_datum(c, hidx_.get(cap), hval_.get(cap), cap, &slots, true);
+      if (rc == 2) {
+        conv_.rollback();
+        hidx_.get(2 * cap);
+        hval_.get(2 * cap);
+        c = start;
+        labs.clear();
+        slots = 0;
+        k = (uint32_t)-1;   // restart the request
+        conv_.begin();
+        continue;
       }
+      if (rc != 0) { conv_.rollback(); *res = -1; return; }
       row.p[k + 1] = slots;
     }
-    if (c.p != c.end) { *res = -1; return; }
+    if (c.p != c.end) { conv_.rollback(); *res = -1; return; }
     int32_t* lab = hlab_.get(std::max<uint32_t>(cnt, 1));
     for (uint32_t k = 0; k < cnt; ++k) {
       const int id = labels_.get_or_add((const char*)labs[k].first, labs[k].second);
-      if (id < 0) { *res = -2; *msg = "label table full"; return; }
+      if (id < 0) { conv_.rollback(); *res = -2; *msg = "label table full"; return; }
       lab[k] = id;
     }
     try {
       sync_labels_locked();
     } catch (const std::exception& e) {
+      conv_.rollback();
       *res = -2;
       *msg = e.what();
       return;
@@ -1112,7 +1138,7 @@ class Classifier : public jb::mix::Mixable {
   DevBuf<int32_t> lt_meta_;
   DevBuf<uint8_t> lt_blob_;
   int64_t lt_cap_ = 16, lt_blob_len_ = 1;
-  std::unique_ptr<jb::HostFvHasher> hasher_;
+  LinearConv conv_;
   void* d_srules_ = nullptr;
   void* d_nrules_ = nullptr;
   uint8_t* d_blob_ = nullptr;

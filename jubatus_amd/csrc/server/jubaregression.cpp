@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "jb_hostfv.hpp"
+#include "jb_linear_conv.hpp"
 #include "jb_mix_device.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_rpc.hpp"
@@ -58,6 +59,8 @@ struct Config {
   std::string text;
   float eps = 0.1f, C = 3.40282e+38f;
   Rules rules;
+  bool wide = false;     // the wide rule set on the host (bigram / combinations)
+  WideRules wrules;
 };
 
 // models/regression.py PARegression.__init__ + the fixed-slot converter check
@@ -86,7 +89,7 @@ bool parse_config(const std::string& text, Config* c, std::string* why) {
   Value empty;
   empty.kind = Value::MAP;
   c->rules.H = device_hash_max_size();   // unless the converter names hash_max_size
-  if (!build_rules(conv ? *conv : empty, &c->rules, why)) return false;
+  if (!build_linear_rules(conv ? *conv : empty, &c->rules, &c->wide, &c->wrules, why)) return false;
   c->text = text;
   return true;
 }
@@ -122,9 +125,7 @@ class Regression : public jb::mix::Mixable {
     ++gen_;
     cfg_ = cfg;
     const Rules& r = cfg.rules;
-    hasher_.reset(new jb::HostFvHasher((const uint8_t*)r.s.data(), (int)r.s.size(),
-                                       (const uint8_t*)r.n.data(), (int)r.n.size(),
-                                       (const uint8_t*)r.blob.data(), r.blob.size(), r.H));
+    conv_.configure(r, cfg.wide, cfg.wrules);
     if (w_) HIPCHK(hipFree(w_));
     if (stats_) HIPCHK(hipFree(stats_));
     HIPCHK(hipMalloc((void**)&w_, r.H * 4));
@@ -183,7 +184,7 @@ class Regression : public jb::mix::Mixable {
       first[k] = n;
       const int64_t n0 = n, s0 = slots;
       while (true) {
-        int rc = hasher_->hash_body(bodies[k].first, bodies[k].second, idx_.p, val_.p, row_.p,
+        int rc = conv_.hash_body(bodies[k].first, bodies[k].second, idx_.p, val_.p, row_.p,
                                     (int64_t)row_.cap - 1, (int64_t)idx_.cap, &n, &slots);
         if (rc == 2) {
           n = n0;
@@ -267,9 +268,21 @@ class Regression : public jb::mix::Mixable {
     }
     star.allreduce_max(hh, 3, grp.deadline());
     if (hh[0] != -hh[1]) throw std::runtime_error("mix: members disagree on hash_max_size");
+    uint64_t wbytes = 0;
+    if (conv_.global()) {   // the document statistics of idf / bm25 converters
+      std::string dm;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        dm = conv_.get_diff();
+      }
+      const auto parts = pl.allgather_bytes(star, dm, grp.deadline());
+      std::lock_guard<std::mutex> g(mu_);
+      conv_.put_diffs(parts);
+      wbytes = dm.size();
+    }
     if (hh[2] != 0) {
       last_applied_ = false;
-      return 24;
+      return 24 + wbytes;
     }
     pl.allreduce_sum(red_.p, H + 3, grp.deadline());
     std::lock_guard<std::mutex> g(mu_);
@@ -344,8 +357,8 @@ class Regression : public jb::mix::Mixable {
     u.str("w"); u.bin(vals.data(), vals.size() * 4);
     u.str("stats"); u.arr(3);
     for (float x : st) u.dbl((double)x);
-    u.str("weights"); u.arr(3); u.uint(0); u.uint(0);
-    u.map(2); u.str("idx"); u.arr(0); u.str("df"); u.arr(0);
+    u.str("weights");
+    conv_.pack(u);
     return std::move(u.out);
   }
 
@@ -372,6 +385,7 @@ class Regression : public jb::mix::Mixable {
     HIPCHK(hipStreamSynchronize(stream_));
     HIPCHK(hipMemcpy(w_, w.data(), Hn * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(stats_, st, sizeof st, hipMemcpyHostToDevice));
+    conv_.unpack(obj.get("weights"));
   }
 
   void status(std::vector<std::pair<std::string, std::string>>* st) {
@@ -394,6 +408,7 @@ class Regression : public jb::mix::Mixable {
 
  private:
   void clear_locked() {
+    conv_.clear();
     HIPCHK(hipMemsetAsync(w_, 0, cfg_.rules.H * 4, stream_));
     HIPCHK(hipMemsetAsync(stats_, 0, 3 * 4, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
@@ -401,33 +416,45 @@ class Regression : public jb::mix::Mixable {
 
   // one list<[score, datum]> body appended to the host CSR (validated as a
   // whole: false leaves nothing behind)
+  // (the wide converter's document statistics of a body that fails are undone)
   bool parse_scored(const uint8_t* b, size_t len, int64_t* n, int64_t* slots) {
+    conv_.begin();
+    const int64_t n0 = *n, s0 = *slots;
+    for (;;) {
+      const int rc = parse_scored_once(b, len, n, slots);
+      if (rc == 0) return true;
+      conv_.rollback();
+      *n = n0;
+      *slots = s0;
+      if (rc != 2) return false;
+      const size_t cap = std::max<size_t>(idx_.cap, 256);   // out of slots: grow, hash the body again
+      idx_.get(2 * cap);
+      val_.get(2 * cap);
+      conv_.begin();
+    }
+  }
+  // -> 0 ok, 1 malformed, 2 out of slots
+  int parse_scored_once(const uint8_t* b, size_t len, int64_t* n, int64_t* slots) {
     jb::Cursor c{b, b + len};
     uint32_t cnt;
-    if (!c.array(&cnt) || cnt > len) return false;
+    if (!c.array(&cnt) || cnt > len) return 1;
     row_.get((size_t)*n + cnt + 1);
     tgt_.get((size_t)*n + cnt + 1);
     for (uint32_t k = 0; k < cnt; ++k) {
       uint32_t two;
       double y;
-      if (!c.array(&two) || two != 2) return false;
-      if (c.p < c.end && (*c.p == 0xc2 || *c.p == 0xc3)) return false;   // bool is not a score
-      if (!c.number(&y)) return false;
-      while (true) {
-        jb::Cursor save = c;
-        const int64_t s0 = *slots;
-        const int64_t cap = (int64_t)std::max<size_t>(idx_.cap, 256);
-        idx_.get(cap);
-        val_.get(cap);
-        int rc = hasher_->hash_datum(c, idx_.p, val_.p, cap, slots);
-        if (rc == 2) { c = save; *slots = s0; idx_.get(2 * cap); val_.get(2 * cap); continue; }
-        if (rc != 0) return false;
-        break;
-      }
+      if (!c.array(&two) || two != 2) return 1;
+      if (c.p < c.end && (*c.p == 0xc2 || *c.p == 0xc3)) return 1;   // bool is not a score
+      if (!c.number(&y)) return 1;
+      const int64_t cap = (int64_t)std::max<size_t>(idx_.cap, 256);
+      idx_.get(cap);
+      val_.get(cap);
+      const int rc = conv_.hash_datum(c, idx_.p, val_.p, cap, slots, true);
+      if (rc != 0) return rc;
       tgt_.p[*n] = (float)y;
       row_.p[++*n] = *slots;
     }
-    return c.p == c.end;
+    return c.p == c.end ? 0 : 1;
   }
 
   void upload(int64_t n, int64_t slots) {
@@ -452,7 +479,7 @@ class Regression : public jb::mix::Mixable {
   float* w_ = nullptr;
   float* stats_ = nullptr;
   uint64_t samples_ = 0;
-  std::unique_ptr<jb::HostFvHasher> hasher_;
+  LinearConv conv_;
   HostVec<int32_t> idx_;
   HostVec<float> val_, tgt_;
   HostVec<int64_t> row_;

@@ -306,3 +306,53 @@ def test_native_regression_matches_oracle_and_files(tmp_path):
             p.wait(timeout=30)
         except subprocess.TimeoutExpired:
             p.kill()
+
+
+@pytest.mark.parametrize("cfg_name", ["classifier/default.json", "classifier/arow_combinational_feature.json"])
+def test_native_wide_converter_configs_match_oracle(cfg_name, tmp_path):
+    """the reference's default classifier config (bigram tokens, tf / idf
+    weights) and the mul-combination config run natively: host wide
+    converter (jb_hostfv_wide.hpp) with the document statistics, exact
+    single-stream updates; the model equals the host oracle's, the weights
+    travel in the model file"""
+    from jubatus_amd.framework import save_load
+    cfg_file = config_path(cfg_name)
+    port, p = _start(cfg_file, tmp_path)
+    try:
+        c = Classifier("127.0.0.1", port, "", timeout=60)
+        ora = _oracle(cfg_file)
+        rng = random.Random(13)
+        words = ["alpha beta", "gamma", "beta gamma delta", "epsilon", "zeta eta"]
+        for _ in range(4):
+            chunk = []
+            for _ in range(30):
+                y = rng.randrange(3)
+                chunk.append((f"L{y}", Datum({"text": words[(y + rng.randrange(2)) % 5] + f" w{y}",
+                                              "x": float(y) + rng.random()})))
+            assert c.train(chunk) == 30
+            ora.train([(l, d) for l, d in chunk])
+        test = [Datum({"text": words[i % 5] + f" w{i % 3}", "x": float(i % 3)}) for i in range(15)]
+        got = _scores(c.classify(test))
+        want = [dict(r) for r in ora.classify(test)]
+        for g, w in zip(got, want):
+            assert set(g) == set(w)
+            for k in w:
+                assert abs(g[k] - w[k]) <= 1e-3 * max(1.0, abs(w[k])), (k, g[k], w[k])
+        _, st = _status(c)
+        assert st["server_runtime"] == "native"
+        (_, path), = c.save("wide").items()
+        with open(path, "rb") as f:
+            _, pack = save_load.load_server(f, "classifier", open(cfg_file).read(), 1, False)
+        ora2 = _oracle(cfg_file)
+        ora2.unpack(pack)
+        want2 = [dict(r) for r in ora2.classify(test)]
+        for g, w in zip(got, want2):
+            for k in w:
+                assert abs(g[k] - w[k]) <= 1e-3 * max(1.0, abs(w[k])), (k, g[k], w[k])
+        c.close()
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
