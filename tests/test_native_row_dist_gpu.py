@@ -95,7 +95,10 @@ def _point(rng):
 
 
 def test_native_anomaly_distributed_add_mix_equals_one_node(coord):
-    cfg_path = os.path.join(ROOT, "config/anomaly/lof.json")
+    # inverted_index_euclid: exact distances (an LSH backend's quantized
+    # distances tie, and ties break by slot order, which differs between a
+    # server that was sent rows by a MIX and one that added them itself)
+    cfg_path = os.path.join(ROOT, "config/anomaly/default.json")
     ls, ports, procs, (a, b) = _cluster(coord, "anomaly", "adist", cfg_path)
     solo_port = free_port()
     solo = spawn("jubaanomaly", ["-f", cfg_path, "-p", str(solo_port), "-b", "127.0.0.1"], f"solo_{solo_port}")

@@ -56,12 +56,13 @@ def main():
             upd.append((st1["updated"] - st0["updated"]) / max(1, st1["trained"] - st0["trained"]))
             if mode == "exact":
                 d = clf._serial.last_batch()
+                keys = ("segments", "wasted_steps", "refreshes", "committer_updates", "last_segment_rows", "rounds")
                 diag.append((d["exact_steps"], (d["end"] - d["tail_start"]) / max(1, d["end"]),
-                             {k: v for k, v in d.items() if k.startswith("commit")}))
+                             {k: v for k, v in d.items() if k.startswith("commit") or k in keys}))
             if b % 10 == 9:
                 print(f"{mode} batch {b + 1}: {times[-1]:.2f} ms, update fraction {upd[-1]:.4f}"
-                      + (f", exact steps {diag[-1][0]}, sequential tail {diag[-1][1]:.3f}" if diag else ""),
-                      file=sys.stderr, flush=True)
+                      + (f", exact steps {diag[-1][0]}, sequential tail {diag[-1][1]:.3f}, {diag[-1][2]}"
+                         if diag else ""), file=sys.stderr, flush=True)
         edges = [0, 5, 20] + list(range(40, len(times) + 1, max(20, len(times) // 10)))
         for lo, hi in zip(edges, edges[1:] + [len(times)]):
             if lo >= len(times) or hi <= lo:
