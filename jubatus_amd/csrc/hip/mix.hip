@@ -61,6 +61,26 @@ __global__ __launch_bounds__(256) void mix_take_kernel(uint8_t* __restrict__ tou
   touched[i] = 0;
 }
 
+// push mixers' pair round: p += q (float tables) / p = max(p, q) (bitmaps),
+// q being what the peer sent (16 B per lane)
+__global__ __launch_bounds__(256) void mix_pair_sum_kernel(float* __restrict__ p, const float* __restrict__ q,
+                                                           int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (4 * i + 3 < n) {
+    float4 a = reinterpret_cast<float4*>(p)[i];
+    const float4 b = reinterpret_cast<const float4*>(q)[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    reinterpret_cast<float4*>(p)[i] = a;
+  } else {
+    for (int64_t j = 4 * i; j < n; ++j) p[j] += q[j];
+  }
+}
+__global__ __launch_bounds__(256) void mix_pair_max_kernel(uint8_t* __restrict__ p, const uint8_t* __restrict__ q,
+                                                           int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = p[i] > q[i] ? p[i] : q[i];
+}
+
 }  // namespace jb
 
 namespace {
@@ -108,5 +128,19 @@ extern "C" int jb_mix_fold(float* W, float* S, int LC, const int64_t* rows, int6
   if (n <= 0 || Lc <= 0) return 0;
   hipLaunchKernelGGL(jb::mix_fold_kernel, dim3(blocks_for(n * (S ? 2 : 1) * Lc)), dim3(256), 0, st, W, S, LC,
                      rows, n, map, Lc, snap, red, inv_n);
+  return (int)hipGetLastError();
+}
+
+// p += q over n floats (p, q device memory, 16-byte aligned)
+extern "C" int jb_mix_pair_sum(float* p, const float* q, int64_t n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(jb::mix_pair_sum_kernel, dim3(blocks_for((n + 3) / 4)), dim3(256), 0, st, p, q, n);
+  return (int)hipGetLastError();
+}
+
+// p = max(p, q) over n bytes
+extern "C" int jb_mix_pair_max(uint8_t* p, const uint8_t* q, int64_t n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(jb::mix_pair_max_kernel, dim3(blocks_for(n)), dim3(256), 0, st, p, q, n);
   return (int)hipGetLastError();
 }

@@ -393,6 +393,23 @@ class Plane {
   virtual std::string exchange_bytes(Star& s, int peer, const std::string& mine, double dl) {
     return s.permute(peer, mine, dl);
   }
+  // one round of a pairwise schedule over tables in the plane's memory:
+  // p += the peer's p / p = max(p, the peer's p). Every rank calls it once
+  // per round (peer -1, n 0: sits the round out). The default moves host
+  // memory over the control plane; the device plane sends point-to-point
+  virtual void pair_sum(Star& s, float* p, size_t n, int peer, double dl) {
+    const std::string theirs = s.permute(peer, std::string((const char*)p, peer >= 0 ? n * 4 : 0), dl);
+    if (peer < 0) return;
+    if (theirs.size() != n * 4) throw std::runtime_error("pair MIX: the peer's table differs in size");
+    const float* q = (const float*)theirs.data();
+    for (size_t i = 0; i < n; ++i) p[i] += q[i];
+  }
+  virtual void pair_max(Star& s, uint8_t* p, size_t n, int peer, double dl) {
+    const std::string theirs = s.permute(peer, std::string((const char*)p, peer >= 0 ? n : 0), dl);
+    if (peer < 0) return;
+    if (theirs.size() != n) throw std::runtime_error("pair MIX: the peer's bitmap differs in size");
+    for (size_t i = 0; i < n; ++i) p[i] = std::max(p[i], (uint8_t)theirs[i]);
+  }
 };
 
 // host memory over the star (CPU servers, rehearsals)

@@ -19,6 +19,10 @@
 
 #include "jb_mix_group.hpp"
 
+// csrc/hip/mix.hip
+extern "C" int jb_mix_pair_sum(float* p, const float* q, int64_t n, hipStream_t st);
+extern "C" int jb_mix_pair_max(uint8_t* p, const uint8_t* q, int64_t n, hipStream_t st);
+
 namespace jb {
 namespace mix {
 
@@ -108,6 +112,23 @@ class RcclPlane : public Plane {
     return out;
   }
 
+  // pair rounds: send / receive with the peer only (RCCL point-to-point over
+  // xGMI), then fold what arrived; a rank without a peer does nothing
+  void pair_sum(Star&, float* p, size_t n, int peer, double dl) override {
+    if (peer < 0 || n == 0) return;
+    float* q = (float*)dev_bytes(n * 4);
+    pair_xfer(p, q, n * 4, peer, dl);
+    hipchk((hipError_t)jb_mix_pair_sum(p, q, (int64_t)n, st_), "jb_mix_pair_sum");
+    wait_stream(st_, dl);
+  }
+  void pair_max(Star&, uint8_t* p, size_t n, int peer, double dl) override {
+    if (peer < 0 || n == 0) return;
+    uint8_t* q = dev_bytes(n);
+    pair_xfer(p, q, n, peer, dl);
+    hipchk((hipError_t)jb_mix_pair_max(p, q, (int64_t)n, st_), "jb_mix_pair_max");
+    wait_stream(st_, dl);
+  }
+
   void abort() override {
     if (comm_ && !aborted_) {
       aborted_ = true;
@@ -130,6 +151,13 @@ class RcclPlane : public Plane {
   void check(ncclResult_t r, double dl, const char* what) {
     if (r == ncclInProgress) { settle(dl, what); return; }
     if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+  }
+
+  void pair_xfer(const void* send, void* recv, size_t bytes, int peer, double dl) {
+    check(ncclGroupStart(), dl, "ncclGroupStart");
+    check(ncclSend(send, bytes, ncclUint8, peer, comm_, st_), dl, "ncclSend");
+    check(ncclRecv(recv, bytes, ncclUint8, peer, comm_, st_), dl, "ncclRecv");
+    check(ncclGroupEnd(), dl, "ncclGroupEnd");
   }
 
   uint8_t* dev_bytes(size_t n) {
@@ -171,6 +199,16 @@ class StagedPlane : public Plane {
     void* h = stage(p, bytes, dl);
     host_.bcast(h, bytes, root, dl);
     unstage(p, bytes, dl);
+  }
+  void pair_sum(Star& s, float* p, size_t n, int peer, double dl) override {
+    float* h = peer >= 0 ? (float*)stage(p, n * 4, dl) : nullptr;
+    host_.pair_sum(s, h, peer >= 0 ? n : 0, peer, dl);
+    if (peer >= 0) unstage(p, n * 4, dl);
+  }
+  void pair_max(Star& s, uint8_t* p, size_t n, int peer, double dl) override {
+    uint8_t* h = peer >= 0 ? (uint8_t*)stage(p, n, dl) : nullptr;
+    host_.pair_max(s, h, peer >= 0 ? n : 0, peer, dl);
+    if (peer >= 0) unstage(p, n, dl);
   }
 
  private:

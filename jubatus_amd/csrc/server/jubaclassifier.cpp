@@ -5,13 +5,13 @@
 // framework/server_base.cpp (save / load / status) and server_helper.hpp
 // (startup). SURVEY section 7.1: server binaries must not need Python.
 //
-// Scope: standalone servers of the linear methods (perceptron, PA, PA1, PA2,
-// CW, AROW, NHERD) whose converter runs on the fixed-slot GPU path
-// (fv_converter/gpu_path.py fast_eligible: str rules with bin global
-// weights, num / log rules, no filters / combinations / plug-ins). Every
-// other configuration - and distributed mode (-z), --cpu, a host without
-// /dev/kfd - is handed to the Python server (jubatus_amd.cmd.server) by exec
-// BEFORE anything touches the GPU.
+// Scope: the linear methods (perceptron, PA, PA1, PA2, CW, AROW, NHERD),
+// standalone or distributed (linear and push mixers over the native MIX
+// plane, csrc/native/jb_mix_group.hpp), with converters on the fixed-slot GPU
+// path (fv_converter/gpu_path.py fast_eligible) or the host wide rule set
+// (bigram / combination / idf, jb_linear_conv.hpp). The NN methods, --cpu
+// and a host without /dev/kfd are handed to the Python server
+// (jubatus_amd.cmd.server) by exec BEFORE anything touches the GPU.
 //
 // Data path (the same kernels as the Python server, csrc/hip):
 //   train    the transport copies request bodies into pinned arena slots
@@ -663,6 +663,140 @@ class Classifier : public jb::mix::Mixable {
     return bytes;
   }
 
+  // ------------------------------------------------------------ push MIX
+  // random / broadcast / skip mixers (push_mixer.cpp:335-408): a round
+  // exchanges with one peer and both keep the pairwise mean over the rows
+  // either of them touched since this MIX began; rows a round brought in go
+  // on to the next round's peer. Python twin: models/classifier.py pair_mix
+  // (whole tables). Label counts stay per server, as there.
+  bool push_mixable() const override { return true; }
+  void push_begin() override {
+    std::lock_guard<std::mutex> g(mu_);
+    mark_.get(H_);
+    if (jb_mix_take(touched_, mark_.p, (int64_t)H_, compute_) != 0) throw std::runtime_error("jb_mix_take failed");
+    HIPCHK(hipStreamSynchronize(compute_));
+    push_dirty_ = false;
+  }
+  void push_end() override {
+    if (!push_dirty_) return;
+    std::lock_guard<std::mutex> g(mu_);   // a round that could not fold: the next MIX is dense
+    HIPCHK(hipMemsetAsync(touched_, 1, H_, compute_));
+  }
+
+  uint64_t pair_mix(jb::mix::Group& grp, int peer) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    const double dl = grp.deadline();
+    std::string mine;
+    if (peer >= 0) {
+      std::lock_guard<std::mutex> g(mu_);
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      for (size_t c = 0; c < nm.size(); ++c)
+        if (al[c]) put_name(&mine, nm[c]);
+    }
+    // every call below is one of the round's collectives: a rank without a
+    // peer makes them too, with nothing
+    const std::string theirs = pl.exchange_bytes(star, peer, mine, dl);
+    if (peer < 0) {
+      pl.pair_max(star, nullptr, 0, -1, dl);
+      pl.exchange_bytes(star, -1, std::string(), dl);
+      pl.pair_sum(star, nullptr, 0, -1, dl);
+      if (conv_.global()) pl.exchange_bytes(star, -1, std::string(), dl);
+      return 0;
+    }
+    // 1. label agreement: the lower rank's labels, then the other's new ones
+    std::vector<std::string> canon;
+    {
+      std::set<std::string> seen;
+      const std::string& first = grp.rank() < peer ? mine : theirs;
+      const std::string& second = grp.rank() < peer ? theirs : mine;
+      for (const std::string* p : {&first, &second})
+        for (auto& n : get_names(*p))
+          if (seen.insert(n).second) canon.push_back(n);
+    }
+    const int Lc = (int)canon.size();
+    std::vector<int32_t> map((size_t)std::max(Lc, 1), 0);
+    uint64_t gen;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& n : canon)
+        if (labels_.lookup(n) < 0 && labels_.get_or_add(n.data(), n.size()) < 0)
+          throw std::runtime_error("label table full");
+      sync_labels_locked();
+      for (int c = 0; c < Lc; ++c) map[c] = labels_.lookup(canon[c]);
+      gen = gen_;
+    }
+    // 2. the pair's row union (it stays marked for the MIX's later rounds)
+    pl.pair_max(star, mark_.p, H_, peer, dl);
+    uint64_t bytes = H_;
+    const int64_t tb = jb_mix_compact_temp_bytes((int64_t)H_);
+    if (tb < 0) throw std::runtime_error("jb_mix_compact_temp_bytes failed");
+    rows_.get(H_);
+    count_dev_.get(1);
+    temp_.get((size_t)std::max<int64_t>(tb, 1));
+    if (jb_mix_compact(mark_.p, (int64_t)H_, rows_.p, count_dev_.p, temp_.p, tb, mixs_) != 0)
+      throw std::runtime_error("jb_mix_compact failed");
+    HIPCHK(hipMemcpyAsync(count_host_, count_dev_.p, 8, hipMemcpyDeviceToHost, mixs_));
+    jb::mix::wait_stream(mixs_, dl);
+    const int64_t nu = *(volatile int64_t*)count_host_;
+    const bool dense = (uint64_t)nu * 2 > H_;
+    const int64_t* rows = dense ? nullptr : rows_.p;
+    const int64_t n = dense ? (int64_t)H_ : nu;
+    last_rows_ = (uint64_t)n;
+    last_dense_ = dense;
+    const size_t width = (size_t)(use_s_ ? 2 : 1) * Lc;
+    const size_t elems = (size_t)std::max<int64_t>(n, 0) * width;
+    // 3. snapshot of the union rows behind the queued training
+    bool applied = gen == gen_;
+    if (applied && elems > 0) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (gen != gen_) {
+        applied = false;
+      } else {
+        HIPCHK(hipMemcpyAsync(map_dev_.get((size_t)Lc), map.data(), 4 * (size_t)Lc, hipMemcpyHostToDevice, compute_));
+        if (jb_mix_gather(W_, S_, LC_, rows, n, map_dev_.p, Lc, snap_.get(elems), compute_) != 0)
+          throw std::runtime_error("jb_mix_gather failed");
+        HIPCHK(hipMemcpyAsync(red_.get(elems), snap_.p, elems * 4, hipMemcpyDeviceToDevice, compute_));
+        HIPCHK(hipEventRecord(mix_ev_, compute_));
+        HIPCHK(hipStreamWaitEvent(mixs_, mix_ev_, 0));
+      }
+    }
+    // 4. both sides fold, or neither
+    const std::string ok = pl.exchange_bytes(star, peer, applied ? "1" : "0", dl);
+    const bool both = applied && ok == "1";
+    pl.pair_sum(star, both ? red_.p : nullptr, both ? elems : 0, both ? peer : -1, dl);
+    if (both && elems > 0) {
+      bytes += elems * 4;
+      // 5. fold: T += (mine + theirs) / 2 - snapshot (updates made meanwhile stay)
+      std::lock_guard<std::mutex> g(mu_);
+      HIPCHK(hipEventRecord(mix_ev_, mixs_));
+      HIPCHK(hipStreamWaitEvent(compute_, mix_ev_, 0));
+      if (gen == gen_) {
+        if (jb_mix_fold(W_, S_, LC_, rows, n, map_dev_.p, Lc, snap_.p, red_.p, 0.5f, compute_) != 0)
+          throw std::runtime_error("jb_mix_fold failed");
+      } else {
+        applied = false;
+      }
+      HIPCHK(hipStreamSynchronize(compute_));
+    }
+    if (!both) push_dirty_ = true;
+    // 6. the document statistics of idf / bm25 converters
+    if (conv_.global()) {
+      std::string dm;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        dm = conv_.get_diff();
+      }
+      const std::string td = pl.exchange_bytes(star, peer, dm, dl);
+      std::lock_guard<std::mutex> g(mu_);
+      conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm});
+      bytes += dm.size();
+    }
+    last_applied_ = applied && both;
+    return bytes;
+  }
+
   // obsolete protocol: rank src sends its tables and labels; apply = take them
   void hand_over(jb::mix::Group& grp, int src, bool apply) override {
     jb::mix::Star& star = grp.star();
@@ -1190,6 +1324,7 @@ class Classifier : public jb::mix::Mixable {
   std::map<std::string, uint64_t> count_base_;
   uint64_t last_rows_ = 0;
   bool last_dense_ = false, last_applied_ = true;
+  bool push_dirty_ = false;   // a pair round of this push MIX did not fold
 
   static void put_name(std::string* o, const std::string& n) {
     const uint32_t k = (uint32_t)n.size();
@@ -1536,7 +1671,7 @@ int main(int argc, char** argv) {
   Config cfg;
   const int rc = startup(argc, argv, &a, &text, [&cfg](const std::string& t, std::string* why) {
     return parse_config(t, &cfg, why);
-  }, true, true);
+  }, true, /*native_dist=*/true, /*native_push=*/true);
   if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
   try {

@@ -5,10 +5,11 @@
 // jubatus_core's PA regression; the update rule and its oracle are in
 // models/regression.py, the kernels in csrc/hip/regression.hip.
 //
-// Scope: standalone servers whose converter runs on the fixed-slot GPU path
-// (the classifier server's rule check, csrc/server/jb_server_common.hpp);
-// other configurations, distributed mode, --cpu and hosts without a GPU go
-// to the Python server (exec before any GPU call).
+// Scope: standalone and distributed servers (linear and push mixers over the
+// native MIX plane, csrc/native/jb_mix_group.hpp), fixed-slot converters and
+// the wide rule set (bigram / combination, idf with MIXed document
+// statistics); --cpu and hosts without a GPU go to the Python server (exec
+// before any GPU call).
 //
 // Data path: the batch of queued train RPCs is validated and hashed on the
 // host (jb_hostfv.hpp, bit-identical to fv_hash.hip), one request per
@@ -305,6 +306,78 @@ class Regression : public jb::mix::Mixable {
     last_applied_ = true;
     ++mixes_;
     return (H + 3) * 4;
+  }
+
+  // push mixers (random / broadcast / skip, push_mixer.cpp:335-408): one
+  // round = the pairwise mean of [w | stats] with the peer (point-to-point),
+  // folded like mix() so training meanwhile is kept. Python twin:
+  // models/regression.py through parallel/mixable.py pair_exchange.
+  bool push_mixable() const override { return true; }
+  uint64_t pair_mix(jb::mix::Group& grp, int peer) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    const double dl = grp.deadline();
+    uint64_t gen = 0, H = 0;
+    if (peer >= 0) {
+      std::lock_guard<std::mutex> g(mu_);
+      gen = gen_;
+      H = cfg_.rules.H;
+      if (jb_mix_gather(w_, nullptr, 1, nullptr, (int64_t)H, map_.p, 1, snap_.get(H + 3), stream_) != 0)
+        throw std::runtime_error("jb_mix_gather failed");
+      HIPCHK(hipMemcpyAsync(snap_.p + H, stats_, 12, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(red_.get(H + 3), snap_.p, (H + 3) * 4, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipEventRecord(mix_ev_, stream_));
+      HIPCHK(hipStreamWaitEvent(mixs_, mix_ev_, 0));
+    }
+    // the pair checks the layout and whether both can fold; every call below
+    // is one of the round's collectives (a rank without a peer sends nothing)
+    std::string me;
+    if (peer >= 0) me = std::to_string(H) + (gen != gen_ ? " 1" : " 0");
+    const std::string th = pl.exchange_bytes(star, peer, me, dl);
+    bool fold = peer >= 0 && gen == gen_;
+    if (peer >= 0) {
+      if (th.substr(0, th.find(' ')) != std::to_string(H))
+        throw std::runtime_error("mix: members disagree on hash_max_size");
+      fold = fold && th.size() > 2 && th.back() == '0';
+    }
+    uint64_t wbytes = 0;
+    if (conv_.global()) {
+      std::string dm;
+      if (peer >= 0) {
+        std::lock_guard<std::mutex> g(mu_);
+        dm = conv_.get_diff();
+      }
+      const std::string td = pl.exchange_bytes(star, peer, dm, dl);
+      if (peer >= 0) {
+        std::lock_guard<std::mutex> g(mu_);
+        conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm});
+        wbytes = dm.size();
+      }
+    }
+    pl.pair_sum(star, fold ? red_.p : nullptr, fold ? H + 3 : 0, fold ? peer : -1, dl);
+    if (!fold) {
+      if (peer >= 0) last_applied_ = false;
+      return wbytes;
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    HIPCHK(hipEventRecord(mix_ev_, mixs_));
+    HIPCHK(hipStreamWaitEvent(stream_, mix_ev_, 0));
+    if (gen != gen_) {
+      last_applied_ = false;
+      return (H + 3) * 4 + wbytes;
+    }
+    if (jb_mix_fold(w_, nullptr, 1, nullptr, (int64_t)H, map_.p, 1, snap_.p, red_.p, 0.5f, stream_) != 0)
+      throw std::runtime_error("jb_mix_fold failed");
+    float sn[3], rd[3], cur[3];
+    HIPCHK(hipMemcpyAsync(sn, snap_.p + H, 12, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipMemcpyAsync(rd, red_.p + H, 12, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipMemcpyAsync(cur, stats_, 12, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    for (int i = 0; i < 3; ++i) cur[i] += rd[i] * 0.5f - sn[i];
+    HIPCHK(hipMemcpy(stats_, cur, 12, hipMemcpyHostToDevice));
+    last_applied_ = true;
+    ++mixes_;
+    return (H + 3) * 4 + wbytes;
   }
 
   // obsolete protocol: rank src sends w and stats; apply = take them
@@ -732,7 +805,7 @@ int main(int argc, char** argv) {
   Config cfg;
   const int rc = startup(argc, argv, &a, &text, [&cfg](const std::string& t, std::string* why) {
     return parse_config(t, &cfg, why);
-  }, true, true);
+  }, true, /*native_dist=*/true, /*native_push=*/true);
   if (rc >= 0) return rc;
   // below this line the process owns the GPU: no exec
   try {

@@ -169,6 +169,73 @@ class HostModel : public jb::mix::Mixable {
     return bytes;
   }
 
+  // --------------------------------------------- the classifier's push MIX, on the host
+  // (jubaclassifier.cpp pair_mix: label agreement with the peer, the pair's
+  // row union - kept for the MIX's later rounds - and the pairwise mean)
+  bool push_mixable() const override { return true; }
+  void push_begin() override {
+    std::lock_guard<std::mutex> g(mu_);
+    pmark_.swap(touched_);
+    touched_.assign((size_t)H_, 0);
+  }
+  uint64_t pair_mix(Group& grp, int peer) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    const double dl = grp.deadline();
+    std::string mine;
+    if (peer >= 0) {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& n : names_) put_name(&mine, n);
+    }
+    const std::string theirs = pl.exchange_bytes(star, peer, mine, dl);
+    if (peer < 0) {
+      pl.pair_max(star, nullptr, 0, -1, dl);
+      pl.exchange_bytes(star, -1, std::string(), dl);
+      pl.pair_sum(star, nullptr, 0, -1, dl);
+      return 0;
+    }
+    std::vector<std::string> canon;
+    std::set<std::string> seen;
+    for (const std::string* p : {grp.rank() < peer ? &mine : &theirs, grp.rank() < peer ? &theirs : &mine})
+      for (auto& n : get_names(*p))
+        if (seen.insert(n).second) canon.push_back(n);
+    const int Lc = (int)canon.size();
+    std::vector<int> map(Lc);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (int c = 0; c < Lc; ++c) {
+        map[c] = column(canon[c]);
+        if (map[c] < 0) throw std::runtime_error("label table full");
+      }
+    }
+    pl.pair_max(star, pmark_.data(), pmark_.size(), peer, dl);
+    std::vector<int64_t> rows;
+    for (int64_t r = 0; r < H_; ++r)
+      if (pmark_[(size_t)r]) rows.push_back(r);
+    const size_t width = 2 * (size_t)Lc;
+    std::vector<float> snap(rows.size() * width);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t i = 0; i < rows.size(); ++i)
+        for (int c = 0; c < Lc; ++c) {
+          snap[i * width + c] = W_[(size_t)rows[i] * LC + map[c]];
+          snap[i * width + Lc + c] = S_[(size_t)rows[i] * LC + map[c]];
+        }
+    }
+    const std::string ok = pl.exchange_bytes(star, peer, "1", dl);
+    std::vector<float> red = snap;
+    pl.pair_sum(star, red.data(), red.size(), ok == "1" ? peer : -1, dl);
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < rows.size(); ++i)
+      for (int c = 0; c < Lc; ++c) {
+        W_[(size_t)rows[i] * LC + map[c]] += red[i * width + c] * 0.5f - snap[i * width + c];
+        S_[(size_t)rows[i] * LC + map[c]] += red[i * width + Lc + c] * 0.5f - snap[i * width + Lc + c];
+      }
+    last_rows_ = rows.size();
+    last_dense_ = false;
+    return (uint64_t)H_ + red.size() * 4;
+  }
+
   void hand_over(Group& grp, int src, bool apply) override {
     std::string meta;
     std::vector<float> w, s;
@@ -246,7 +313,7 @@ class HostModel : public jb::mix::Mixable {
   std::mutex mu_;
   int64_t H_;
   std::vector<float> W_, S_;
-  std::vector<uint8_t> touched_;
+  std::vector<uint8_t> touched_, pmark_;   // pmark_: rows of the push MIX under way
   std::vector<std::string> names_;
   std::vector<uint64_t> counts_ = std::vector<uint64_t>(LC, 0);
   std::map<std::string, uint64_t> base_;

@@ -42,10 +42,10 @@ def coord():
 
 
 class Rank:
-    def __init__(self, zport, name, ic=3, env=None, H=512):
+    def __init__(self, zport, name, ic=3, env=None, H=512, mixer="linear_mixer"):
         self.port = free_port()
         log = open(os.path.join(tempfile.gettempdir(), f"mixreh_{name}_{self.port}.log"), "wb")
-        self.proc = subprocess.Popen([BIN, "-z", f"127.0.0.1:{zport}", "-n", name, "-p", str(self.port),
+        self.proc = subprocess.Popen([BIN, "-x", mixer, "-z", f"127.0.0.1:{zport}", "-n", name, "-p", str(self.port),
                                       "-H", str(H), "-I", str(ic), "-i", "0", "-s", "0", "-Z", "3"],
                                      stdout=subprocess.DEVNULL, stderr=log,
                                      env=dict(os.environ, **(env or {})))
@@ -77,11 +77,11 @@ class Rank:
                 self.proc.kill()
 
 
-def wait_group(ranks, n, timeout=60):
+def wait_group(ranks, n, timeout=60, mixer="linear_mixer"):
     deadline = time.time() + timeout
     while time.time() < deadline:
         sts = [r.status() for r in ranks]
-        if all(s.get("linear_mixer.group_size") == str(n) and s.get("linear_mixer.is_obsolete") == "0"
+        if all(s.get(f"{mixer}.group_size") == str(n) and s.get(f"{mixer}.is_obsolete") == "0"
                for s in sts):
             return True
         time.sleep(0.2)
@@ -139,6 +139,70 @@ def test_four_ranks_mix_to_the_mean(coord):
         cnts = [{lab: v[0] for lab, v in m.items()} for m in after]
         assert all(c == cnts[0] for c in cnts)
         assert sum(cnts[0].values()) == sum(base.values()) + 4 * 20
+    finally:
+        for r in ranks:
+            r.stop()
+
+
+def _models_equal(a, b):
+    assert sorted(a) == sorted(b)
+    for lab in a:
+        np.testing.assert_allclose(a[lab][1], b[lab][1], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(a[lab][2], b[lab][2], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("mixer,n", [("skip_mixer", 4), ("random_mixer", 2)])
+def test_push_mixers_reach_the_mean(coord, mixer, n):
+    """the classifier's native pair MIX (label agreement with the peer, the
+    pair's row union, pairwise mean): the skip mixer's butterfly over 4 ranks
+    and the random mixer's one pair both end at the cluster mean"""
+    ranks = [Rank(coord.port, f"push{n}", mixer=mixer) for _ in range(n)]
+    try:
+        assert wait_group(ranks, n, mixer=mixer)
+        for i, r in enumerate(ranks):
+            r.call("train", 300 + i, 200, 2 + i)
+        before = [r.model() for r in ranks]
+        assert ranks[0].call("do_mix") is True
+        want = mean_models(before)
+        for r in ranks:
+            m = r.model()
+            assert sorted(m) == sorted(want)
+            for lab, (w, s) in want.items():
+                np.testing.assert_allclose(m[lab][1], w, rtol=1e-5, atol=1e-6)
+                np.testing.assert_allclose(m[lab][2], s, rtol=1e-5, atol=1e-6)
+        st = ranks[-1].status()
+        assert st[f"{mixer}.runtime"] == "native" and int(st[f"{mixer}.mix_count"]) >= 1
+        # a second MIX moves only the rows trained since (sparse union)
+        ranks[0].call("train", 999, 10, 2)
+        assert ranks[1].call("do_mix") is True
+        assert 0 < int(ranks[1].status()["mix.last_rows"]) <= 10 * (2 if mixer == "random_mixer" else 4)
+        ms = [r.model() for r in ranks]
+        if mixer == "random_mixer":
+            _models_equal(ms[0], ms[1])
+    finally:
+        for r in ranks:
+            r.stop()
+
+
+def test_broadcast_mixer_spreads_labels(coord):
+    """broadcast (round-robin tournament) over 3 ranks: every rank ends with
+    every label, and models move toward each other"""
+    ranks = [Rank(coord.port, "bcast3", mixer="broadcast_mixer") for _ in range(3)]
+    try:
+        assert wait_group(ranks, 3, mixer="broadcast_mixer")
+        for i, r in enumerate(ranks):
+            r.call("train", 500 + i, 150, 1 + 2 * i)
+        before = [r.model() for r in ranks]
+        assert ranks[2].call("do_mix") is True
+        after = [r.model() for r in ranks]
+        labels = sorted(set().union(*[m.keys() for m in before]))
+        want = mean_models(before)
+        for b, a in zip(before, after):
+            assert sorted(a) == labels
+            for lab in labels:   # closer to the mean than before
+                if lab in b:
+                    assert (np.abs(a[lab][1] - want[lab][0]).sum()
+                            <= np.abs(b[lab][1] - want[lab][0]).sum() + 1e-4)
     finally:
         for r in ranks:
             r.stop()
