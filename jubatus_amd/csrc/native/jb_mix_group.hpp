@@ -1102,6 +1102,19 @@ class ClusterNode {
     }
     return out;
   }
+  // the whole ring, sorted by vnode hash: (md5 hex, "ip_port") - for engines
+  // that place many keys at once (burst's processed keywords)
+  std::vector<std::pair<std::string, std::string>> cht_ring() {
+    const std::string dir = actor_path(type_, name_) + "/cht";
+    std::vector<std::string> h = coord_->list(dir);
+    std::sort(h.begin(), h.end());
+    std::vector<std::pair<std::string, std::string>> out;
+    for (const auto& x : h) {
+      std::string loc;
+      if (coord_->read(dir + "/" + x, &loc)) out.emplace_back(x, loc);
+    }
+    return out;
+  }
   // global_id_generator_zk: the data version of <actor>/id_generator
   uint64_t create_id() {
     const std::string path = actor_path(type_, name_) + "/id_generator";

@@ -1,5 +1,5 @@
 // RPC shell of the native host-engine servers (jubastat, jubabandit,
-// jubaburst, jubagraph): the
+// jubaburst, jubagraph, jubaweight): the
 // engines whose state is small per-key bookkeeping and stays on the host
 // (SURVEY K14), served without Python. Reference: the generated
 // <engine>_impl.cpp RPC tables and framework/server_base.cpp (save / load /
@@ -62,6 +62,14 @@ class HostEngine {
   virtual std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& s, double dl) {
     (void)dl;
     return std::unique_ptr<jb::mix::Plane>(new jb::mix::HostPlane(&s));
+  }
+  // distributed mode: the cluster this server joined (its CHT, its
+  // server-to-server peers) and its own address; called before serving and
+  // again when a loaded model file replaces the engine
+  virtual void attach(jb::mix::ClusterNode* node, const std::string& eth, int port) {
+    (void)node;
+    (void)eth;
+    (void)port;
   }
 };
 
@@ -145,6 +153,10 @@ class HostServer : public jb::mix::Mixable {
       return 1;
     }
     a_.port = port;
+    if (node_) {
+      std::unique_lock<std::shared_mutex> g(model_mu_);
+      eng_->attach(node_.get(), a_.eth, a_.port);
+    }
     logf_("INFO", "start listening at port %d", port);
     cs_.start_time = time(nullptr);
     rpc_->start();
@@ -328,6 +340,7 @@ class HostServer : public jb::mix::Mixable {
       config_ = mf.config;
       table_.clear();
       for (auto& m : eng_->methods()) table_.push_back(m);
+      if (node_) eng_->attach(node_.get(), a_.eth, a_.port);
     }
     eng_->unpack(mf.user);
     std::lock_guard<std::mutex> s(st_mu_);

@@ -11,11 +11,16 @@
 // 1 - 1e-9), emission -ln(C(d,r) p^r (1-p)^(d-r)), entering the burst state
 // costs gamma ln(n); bursting batches report cost(p0) - cost(p1), cut below
 // a positive costcut_threshold; result_window_rotate_size past windows kept.
-// Standalone: every keyword is processed here. Model files are shared with
-// the Python server (Burst.pack()).
+// Standalone: every keyword is processed here. Distributed (-z): a keyword
+// is processed by its two CHT owners (replication 2, burst_serv.cpp:200-246;
+// the processed set is re-derived when the ring changes) and the others get
+// its result windows through MIX (keywords and the processed keywords'
+// windows, models/burst.py get_diff / mix_diff / put_diff). Model files are
+// shared with the Python server (Burst.pack()).
 #include <math.h>
 
 #include <algorithm>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -128,6 +133,7 @@ class Burst : public HostEngine {
     return {
         {"add_documents", 2, true, [this](const std::vector<Value>& a, MsgpackWriter* w) {
            if (a[0].kind != Value::ARR) throw std::invalid_argument("list expected");
+           rehash();
            int64_t n = 0;
            for (const Value& doc : a[0].a) {
              if (doc.kind != Value::ARR || doc.a.size() < 2) throw std::invalid_argument("document");
@@ -170,6 +176,7 @@ class Burst : public HostEngine {
            order_.erase(std::find(order_.begin(), order_.end(), k));
            r_.erase(k);
            results_.erase(k);
+           proc_.erase(k);
            w->boolean(true);
          }},
         {"remove_all_keywords", 1, true, [this](const std::vector<Value>&, MsgpackWriter* w) {
@@ -177,6 +184,7 @@ class Burst : public HostEngine {
            order_.clear();
            r_.clear();
            results_.clear();
+           proc_.clear();
            w->boolean(true);
          }},
         {"clear", 1, true, [this](const std::vector<Value>&, MsgpackWriter* w) {
@@ -203,8 +211,7 @@ class Burst : public HostEngine {
     u.map(6);
     u.str("keywords"); u.map(order_.size());
     for (const auto& k : order_) { u.str(k); u.arr(2); u.dbl(kw_.at(k).first); u.dbl(kw_.at(k).second); }
-    std::vector<std::string> proc(order_);
-    std::sort(proc.begin(), proc.end());
+    std::vector<std::string> proc(proc_.begin(), proc_.end());   // sorted
     u.str("processed"); u.arr(proc.size());
     for (const auto& k : proc) u.str(k);
     u.str("start");
@@ -247,9 +254,15 @@ class Burst : public HostEngine {
     order_.clear();
     r_.clear();
     results_.clear();
+    proc_.clear();
     for (const auto& k : kv->o) {
       kw_[k.first] = {k.second.a.at(0).num(), k.second.a.at(1).num()};
       order_.push_back(k.first);
+    }
+    if (const Value* pv = obj.get("processed")) {
+      if (pv->kind == Value::ARR)
+        for (const Value& k : pv->a)
+          if (k.is_str() && kw_.count(k.s)) proc_.insert(k.s);
     }
     has_start_ = st && st->is_num();
     start_ = has_start_ ? st->num() : 0.0;
@@ -278,7 +291,7 @@ class Burst : public HostEngine {
   void status(std::vector<std::pair<std::string, std::string>>* st) override {
     char b[64];
     st->emplace_back("num_keywords", std::to_string(kw_.size()));
-    st->emplace_back("processed_keywords", std::to_string(kw_.size()));
+    st->emplace_back("processed_keywords", std::to_string(proc_.size()));
     if (has_start_) { snprintf(b, sizeof b, "%.17g", start_); st->emplace_back("window_start", b); }
     else st->emplace_back("window_start", "None");
     st->emplace_back("window_batch_size", std::to_string(p_.window));
@@ -286,13 +299,103 @@ class Burst : public HostEngine {
     st->emplace_back("batch_interval", b);
   }
 
+  // ---- distributed mode
+  bool mixable() const override { return true; }
+  bool uses_cht() const override { return true; }
+  void attach(jb::mix::ClusterNode* node, const std::string& eth, int port) override {
+    node_ = node;
+    loc_ = eth + "_" + std::to_string(port);
+    ring_.clear();
+  }
+  // {"keywords": {k: [scaling, gamma]}, "results": {processed k: windows}}
+  std::string get_diff() override {
+    MsgpackWriter u;
+    u.map(2);
+    u.str("keywords");
+    u.map(order_.size());
+    for (const auto& k : order_) { u.str(k); u.arr(2); u.dbl(kw_.at(k).first); u.dbl(kw_.at(k).second); }
+    u.str("results");
+    size_t n = 0;
+    for (const auto& k : order_) n += proc_.count(k) && results_.count(k);
+    u.map(n);
+    for (const auto& k : order_) {
+      if (!proc_.count(k) || !results_.count(k)) continue;
+      u.str(k);
+      write_hist(&u, results_.at(k));
+    }
+    return std::move(u.out);
+  }
+  // mix_diff folded in rank order (a later member's entry wins), then
+  // put_diff: new keywords join, windows of keywords not processed here
+  // are taken
+  void put_diffs(const std::vector<Value>& parts) override {
+    std::vector<std::string> korder;
+    std::unordered_map<std::string, std::pair<double, double>> kws;
+    std::vector<std::string> rorder;
+    std::unordered_map<std::string, const Value*> res;
+    for (const Value& d : parts) {
+      const Value* kv = d.get("keywords");
+      const Value* rv = d.get("results");
+      if (!kv || kv->kind != Value::MAP || !rv || rv->kind != Value::MAP)
+        throw std::runtime_error("mix: malformed burst diff");
+      for (const auto& k : kv->o) {
+        if (!kws.count(k.first)) korder.push_back(k.first);
+        kws[k.first] = {k.second.a.at(0).num(), k.second.a.at(1).num()};
+      }
+      for (const auto& k : rv->o) {
+        if (!res.count(k.first)) rorder.push_back(k.first);
+        res[k.first] = &k.second;
+      }
+    }
+    for (const auto& k : korder)
+      if (!kw_.count(k)) {
+        kw_[k] = kws[k];
+        order_.push_back(k);
+        r_[k].assign((size_t)p_.window, 0);
+      }
+    for (const auto& k : rorder) {
+      if (!kw_.count(k) || proc_.count(k)) continue;
+      std::vector<Window> hist;
+      for (const Value& win : res[k]->a) {
+        Window wd{win.a.at(0).num(), {}};
+        for (const Value& b : win.a.at(1).a)
+          wd.batches.push_back({(int64_t)b.a.at(0).num(), (int64_t)b.a.at(1).num(), b.a.at(2).num()});
+        hist.push_back(std::move(wd));
+      }
+      results_[k] = std::move(hist);
+    }
+  }
+
  private:
+  // is this server one of the keyword's 2 CHT owners (standalone: always)
+  bool will_process(const std::string& k) const {
+    if (!node_ || ring_.empty()) return true;
+    const std::string h = jb::Md5::hex(k);
+    size_t i = (size_t)(std::lower_bound(ring_.begin(), ring_.end(), std::make_pair(h, std::string())) -
+                        ring_.begin()) % ring_.size();
+    for (int n = 0; n < 2; ++n, i = (i + 1) % ring_.size())
+      if (ring_[i].second == loc_) return true;
+    return false;
+  }
+  // the ring changed (a member joined / left): derive the processed set again
+  void rehash() {
+    if (!node_) return;
+    auto ring = node_->cht_ring();
+    if (ring == ring_) return;
+    ring_ = std::move(ring);
+    proc_.clear();
+    for (const auto& k : order_)
+      if (will_process(k)) proc_.insert(k);
+  }
+
   bool add_keyword(const std::string& k, double scaling, double gamma) {
     if (kw_.count(k)) return false;
     if (!(scaling > 1.0) || !(gamma > 0.0)) throw EngineError("scaling_param must be > 1 and gamma > 0");
+    rehash();
     kw_[k] = {scaling, gamma};
     order_.push_back(k);
     r_[k].assign((size_t)p_.window, 0);
+    if (will_process(k)) proc_.insert(k);
     return true;
   }
 
@@ -328,6 +431,7 @@ class Burst : public HostEngine {
   void calculate() {
     if (!has_start_) return;
     for (const auto& k : order_) {
+      if (!proc_.count(k)) continue;
       const auto& sg = kw_.at(k);
       const auto& rr = r_.at(k);
       const std::vector<double> w = detect(d_, rr, sg.first, sg.second, p_.costcut);
@@ -375,6 +479,16 @@ class Burst : public HostEngine {
     }
   }
 
+  static void write_hist(MsgpackWriter* u, const std::vector<Window>& hist) {
+    u->arr(hist.size());
+    for (const Window& win : hist) {
+      u->arr(2);
+      u->dbl(win.start);
+      u->arr(win.batches.size());
+      for (const Batch& b : win.batches) { u->arr(3); u->sint(b.d); u->sint(b.r); u->dbl(b.w); }
+    }
+  }
+
   static void write_window(MsgpackWriter* w, const Window& win) {
     w->arr(2);
     w->dbl(win.start);
@@ -388,6 +502,10 @@ class Burst : public HostEngine {
   }
 
   Params p_;
+  jb::mix::ClusterNode* node_ = nullptr;
+  std::string loc_;                                            // "ip_port" of this server
+  std::vector<std::pair<std::string, std::string>> ring_;      // CHT vnodes seen last
+  std::set<std::string> proc_;                                 // keywords processed here
   bool has_start_ = false;
   double start_ = 0;
   std::vector<int64_t> d_;
@@ -411,5 +529,6 @@ int main(int argc, char** argv) {
         std::string why;
         if (!parse_params(text, &p, &why)) throw std::runtime_error(why);
         return std::unique_ptr<HostEngine>(new Burst(p));
-      });
+      },
+      /*native_dist=*/true);
 }

@@ -176,3 +176,51 @@ def test_native_weight_distributed_idf(coord):
             solo.terminate()
             solo.wait(timeout=15)
         cl.close()
+
+
+def test_native_burst_distributed_keywords(coord):
+    """three jubaburst servers: the proxy broadcasts keywords and documents,
+    each keyword is processed by its 2 CHT owners, and after a MIX every
+    server answers get_result for every keyword as one standalone server
+    does (reference burst_serv.cpp:200-246, models/burst.py MIX)."""
+    cfg = json.load(open(os.path.join(ROOT, "config/burst/default.json")))
+    cl = Cluster(coord, "burst", "budist", cfg, n=3)
+    solo_port = free_port()
+    cfg_path = os.path.join(tempfile.gettempdir(), f"busolo_{solo_port}.json")
+    json.dump(cfg, open(cfg_path, "w"))
+    solo = subprocess.Popen([os.path.join(NB, "jubaburst"), "-f", cfg_path, "-p", str(solo_port), "-b", "127.0.0.1"],
+                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        assert wait_server("127.0.0.1", solo_port, 60)
+        s = Client("127.0.0.1", solo_port, "", timeout=30.0)
+        kws = [f"kw{i}" for i in range(12)]
+        for k in kws:
+            for c in cl.c + [s]:
+                assert c.call("add_keyword", [k, 2.0, 1.0]) is True
+        import random
+        rng = random.Random(3)
+        docs = []
+        for t in range(400):
+            words = [rng.choice(kws) for _ in range(rng.randint(0, 2))]
+            if t > 300 and rng.random() < 0.6:
+                words.append("kw3")          # a burst late in the stream
+            docs.append([float(t) * 0.25, " ".join(words) or "nothing"])
+        for i in range(0, len(docs), 50):
+            for c in cl.c + [s]:
+                assert c.call("add_documents", docs[i:i + 50]) == 50
+        procs = [int(status(c)["processed_keywords"]) for c in cl.c]
+        # 2 consecutive vnodes per keyword (a server may own both: cht.cpp:107-143)
+        assert len(kws) <= sum(procs) <= 2 * len(kws) and min(procs) < len(kws), procs
+        cl.mix()
+        for k in kws:
+            want = s.call("get_result", k)
+            for c in cl.c:
+                got = c.call("get_result", k)
+                assert got == want, (k, got, want)
+        assert s.call("get_all_bursted_results") == cl.c[0].call("get_all_bursted_results")
+        s.close()
+    finally:
+        if solo.poll() is None:
+            solo.terminate()
+            solo.wait(timeout=15)
+        cl.close()
