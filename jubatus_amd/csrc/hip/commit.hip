@@ -8,31 +8,37 @@
 //
 //   1. delta_s0_kernel (whole GPU, one wave per sample): every sample's LC
 //      label scores against the model at the segment start M0 (the global
-//      W / P tables, which nothing writes while the segment runs).
-//   2. delta_commit_kernel (ONE 1024-thread workgroup, 16 waves = 64 groups
-//      of 16 lanes; a group is a DPP row): walks the batch in order, 128
-//      samples per round, each group owning 2 consecutive samples with
-//      feature u / label u on lane u of the row. Everything the batch writes
-//      lives in LDS until the segment ends:
+//      W / P tables, which nothing writes while the segment runs), its best
+//      wrong label at M0 and, per feature, the precisions P0(row, y) and
+//      P0(row, that label) - the step of a sample reads them from its
+//      registers instead of a dependent global load.
+//   2. delta_commit_kernel (ONE 512-thread workgroup, 8 waves = 32 groups of
+//      16 lanes; a group is a DPP row): walks the batch in order, 64 samples
+//      per round, each group owning 2 consecutive samples with feature u /
+//      label u on lane u of the row. Everything the segment writes lives in
+//      LDS until it ends:
 //        dW[slot][LC], dP[slot][LC]  the summed increments since M0 of every
-//                                    row the segment wrote (hash -> slot),
-//      so the live model is M0 (global, never written, prefetchable) + the LDS
-//      deltas. Each sample's scores are kept EXACT (not bounded): at round
-//      start a lane adds x_u * dW[row_u][:] of the rows already written, and
-//      after every update the stepping group publishes its per-row increments
-//      (a small LDS step table) and every later sample of the round adds
-//      x * dW_step to its scores of the two labels the update touched (one
-//      probe per lane, two row sums). The first sample of the round whose
-//      exact margin says it updates takes the exact step - its 16 lanes read
-//      P0 + dP of (feature, y / best wrong), compute the method's
-//      coefficients and add the increments into LDS - and the round
-//      continues after it. A sample that does not update costs no table
-//      access at all; an update costs two workgroup barriers and LDS work.
+//                                    row the segment wrote (row -> slot hash),
+//      so the live model is M0 + the LDS deltas. Scores are kept EXACT:
+//        - round start: lane u reads the dW row of its feature (4 x b128) and
+//          a 16 x 16 transpose-reduce over the row (mirror / half-mirror /
+//          quad DPP adds, no LDS round trip) gives lane l the correction of
+//          label l; the exact margin gives the sample's slack to its update
+//          threshold;
+//        - the first sample whose slack is not positive takes the exact step
+//          (its group reads P0 + dP, computes the method's coefficients and
+//          adds the increments into LDS), stamping the rows it wrote with the
+//          step id and their increments of the two labels it moved;
+//        - every later sample of the round adds x * increment of its stamped
+//          rows to those two label scores (one LDS probe per feature, two row
+//          sums) and lowers its slack by the correction's size; only a sample
+//          whose slack runs out recomputes its exact margin.
+//      A sample that does not update costs no table access beyond these.
 //   3. When the LDS row store is full the segment ends: the deltas are added
-//      to W / P (one coalesced pass), and the next segment re-scores the rest
-//      of the batch against the new tables. A sample wider than 64 features
-//      ends the committer; the rest of the batch runs the single-stream exact
-//      kernel (linear.hip kExact), as in serial.hip.
+//      to W / P (one coalesced pass over the row hash), and the next segment
+//      re-scores the rest of the batch against the new tables. A sample wider
+//      than 32 features ends the committer; the rest of the batch runs the
+//      single-stream exact kernel (linear.hip kExact), as in serial.hip.
 //
 // Rounding: scores are S0 + incremental corrections, summed in another order
 // than a fresh recomputation; a sample whose margin lies within a relative
@@ -48,16 +54,20 @@ namespace dc {
 
 constexpr int kT = 512;               // committer threads (8 waves)
 constexpr int kNG = kT / 16;          // groups (DPP rows) of 16 lanes
-constexpr int kR = 4;                 // samples per group per round
+constexpr int kR = 2;                 // samples per group per round
 constexpr int kNS = kNG * kR;         // samples per round
 constexpr int kFC = 2;                // feature chunks of 16 held in registers
 constexpr int kNFMax = 16 * kFC;      // widest sample the committer takes
-constexpr int kSHS = 128;             // step-table hash slots (<= 32 rows per step)
 constexpr float kGuard = 1e-4f;       // relative guard band of a decision
 constexpr int kInf = 0x7fffffff;
+constexpr uint64_t kEmpty = ~0ull;    // free row-hash entry
 // stop reasons (tail[kTailReason]); the values are serial.hip's
 constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2;
 constexpr int kTailReason = 20;
+// phase timing (tail[4..19]): shader cycles of wave 0 per phase, the wall
+// clock of the kernel and every wave's own round-start work
+constexpr bool kProf = true;
+__device__ __forceinline__ uint64_t cyc() { return kProf ? __builtin_amdgcn_s_memtime() : 0; }
 
 constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
 
@@ -65,19 +75,13 @@ template <int LC>
 struct Geo {
   static constexpr int K = (LC + 15) / 16;                 // labels per lane
   static constexpr int NSLOT = 16384 / (LC > 16 ? LC : 16); // rows the LDS store holds
-  static constexpr int HS = 2 * NSLOT;                      // row hash slots (load <= 1/2)
+  static constexpr int HS = 2 * NSLOT;                      // row hash entries (load <= 1/2)
   static constexpr int HB = ilog2(HS);
 };
 
 __device__ __forceinline__ uint32_t hmix(int32_t r) { return (uint32_t)r * 0x9E3779B1u; }
-
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int CTRL>
-__device__ __forceinline__ int dppi(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+__device__ __forceinline__ uint64_t hpack(int32_t row, int slot) {
+  return (uint64_t)(uint32_t)row | ((uint64_t)(uint32_t)slot << 32);
 }
 
 // best wrong label over a row of 16 lanes (lowest label on ties); the DPP
@@ -85,8 +89,8 @@ __device__ __forceinline__ int dppi(int v) {
 __device__ __forceinline__ void row16_argmax(float& b, int& bl) {
 #define JB_ARGSTEP(C)                                                              \
   {                                                                                \
-    const float ob = dppf<C>(b);                                                   \
-    const int ol = dppi<C>(bl);                                                    \
+    const float ob = dpp_f<C>(b);                                                  \
+    const int ol = dpp_i<C>(bl);                                                   \
     if (ol >= 0 && (bl < 0 || ob > b || (ob == b && ol < bl))) { b = ob; bl = ol; } \
   }
   JB_ARGSTEP(kDppXor1)
@@ -96,21 +100,18 @@ __device__ __forceinline__ void row16_argmax(float& b, int& bl) {
 #undef JB_ARGSTEP
 }
 
-// value of lane (row base + u)
-__device__ __forceinline__ float rowb_f(float v, int base, int u) { return __shfl(v, base + u, 64); }
-__device__ __forceinline__ int rowb_i(int v, int base, int u) { return __shfl(v, base + u, 64); }
-
-// margin of a sample held by a group: score(y) - best active wrong label
+// exact margin of a sample held by a group: score(y) - best active wrong
+// label (every lane of the row gets the same values)
 template <int LC>
 __device__ __forceinline__ float group_margin(const float (&s)[Geo<LC>::K], int y,
-                                              const bool (&act)[Geo<LC>::K], int sub, int base,
+                                              const bool (&act)[Geo<LC>::K], int sub,
                                               int* lstar, float* sy_out, float* best_out) {
   constexpr int K = Geo<LC>::K;
-  float sv = s[0];
+  float v = 0.f;
 #pragma unroll
-  for (int k = 1; k < K; ++k)
-    if (k == (y >> 4)) sv = s[k];
-  const float sy = rowb_f(sv, base, y & 15);
+  for (int k = 0; k < K; ++k)
+    if (k == (y >> 4) && sub == (y & 15)) v = s[k];
+  const float sy = row16_sum(v);   // one non-zero term: exact
   float b = -INFINITY;
   int bl = -1;
 #pragma unroll
@@ -125,81 +126,101 @@ __device__ __forceinline__ float group_margin(const float (&s)[Geo<LC>::K], int 
   return sy - (bl >= 0 ? b : 0.f);
 }
 
-// may the sample update under its (exact up to rounding) margin? NaN: yes
-// (the exact step decides). CW's threshold phi * var is bounded by
-// phi * (1 or 2) * |x|^2: every precision is >= 1.
-__device__ __forceinline__ bool may_update(int method, float m, float nrm, bool has_l, float C,
-                                           float sy, float best) {
+// distance of a margin to the update threshold of the method, less the guard
+// band: a sample updates only if this is not positive (NaN: it may). CW's
+// threshold phi * var is bounded by phi * (1 or 2) * |x|^2 (precisions >= 1).
+__device__ __forceinline__ float slack_of(int method, float m, float nrm, bool has_l, float C,
+                                          float sy, float best) {
   const float g = kGuard * (1.f + fabsf(sy) + fabsf(best));
   switch (method) {
-    case PERCEPTRON: return !(m > g);
-    case PA: case PA1: case PA2: return nrm > 0.f && !(m >= 1.f + g);
-    case CW: return nrm > 0.f && !(m >= C * (has_l ? 2.f : 1.f) * nrm + g);
-    default: return !(m >= 1.f + g);
+    case PERCEPTRON: return m - g;
+    case PA: case PA1: case PA2: return nrm > 0.f ? m - 1.f - g : INFINITY;
+    case CW: return nrm > 0.f ? m - C * (has_l ? 2.f : 1.f) * nrm - g : INFINITY;
+    default: return m - 1.f - g;
   }
 }
 
-// LDS row store: open-addressed row -> slot hash over HS entries
+// LDS row store: open-addressed row -> slot hash of packed (row, slot) words
 template <int LC>
-__device__ __forceinline__ int cache_find(const int32_t* hkey, const int16_t* hslot, int32_t row) {
+__device__ __forceinline__ int cache_find(const uint64_t* hent, int32_t row) {
   using Gm = Geo<LC>;
   if (row < 0) return -1;
   uint32_t h = hmix(row) >> (32 - Gm::HB);
   for (int p = 0; p < Gm::HS; ++p) {
-    const int32_t k = hkey[h];
-    if (k == row) return hslot[h];
-    if (k < 0) return -1;
+    const uint64_t e = hent[h];
+    const int32_t r = (int32_t)(uint32_t)e;
+    if (r == row) return (int)(e >> 32);
+    if (r == -1) return -1;
     h = (h + 1) & (Gm::HS - 1);
   }
   return -1;
 }
 
-// insert (the stepping group only; the caller checked the capacity); returns
-// the hash position - the slot is read from it once the group's inserts are
-// done (a lane that found its row claimed by another lane of the same
-// instruction reads the slot that lane stores)
+// round-start correction: s[k] (label sub + 16k) += sum over the row's lanes
+// of x_c * dW[slot_c][label]. Lane i reads the quads of its row in the order
+// q ^ (i >> 2); the mirror (lane 15 - i) and half-mirror (lane i ^ 7) DPP
+// adds then leave lane i the quad of labels 4 (i >> 2) .. + 3 summed over 4
+// lanes, and two quad-permute steps hand each lane its own label.
 template <int LC>
-__device__ __forceinline__ uint32_t cache_insert(int32_t* hkey, int16_t* hslot, int32_t* ckey, int* cn,
-                                                 int32_t row) {
-  using Gm = Geo<LC>;
-  uint32_t h = hmix(row) >> (32 - Gm::HB);
-  for (int p = 0; p < Gm::HS; ++p) {
-    const int32_t old = atomicCAS(&hkey[h], -1, row);
-    if (old == -1) {
-      const int s = atomicAdd(cn, 1);
-      hslot[h] = (int16_t)s;
-      ckey[s] = row;
-      return h;
+__device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[kFC],
+                                            const float (&x)[kFC], int sub,
+                                            float (&s)[Geo<LC>::K]) {
+  constexpr int K = Geo<LC>::K;
+  const int qs = sub >> 2;
+#pragma unroll
+  for (int b = 0; b < K; ++b) {
+    float4 v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int c = 0; c < kFC; ++c) {
+      if (slot[c] < 0) continue;
+      const float xc = x[c];
+      const float* rowp = dw + slot[c] * LC + 16 * b;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int qq = q ^ qs;
+        if (16 * b + 4 * qq < LC) {
+          const float4 w = *reinterpret_cast<const float4*>(rowp + 4 * qq);
+          v[q].x += xc * w.x; v[q].y += xc * w.y; v[q].z += xc * w.z; v[q].w += xc * w.w;
+        }
+      }
     }
-    if (old == row) return h;
-    h = (h + 1) & (Gm::HS - 1);
+#define JB_DADD(D, S, C) \
+  D.x += dpp_f<C>(S.x); D.y += dpp_f<C>(S.y); D.z += dpp_f<C>(S.z); D.w += dpp_f<C>(S.w);
+    JB_DADD(v[0], v[3], kDppMirror)
+    JB_DADD(v[1], v[2], kDppMirror)
+    JB_DADD(v[0], v[1], kDppHalfMirror)
+#undef JB_DADD
+    const bool h2 = (sub & 2) != 0;
+    float k0 = h2 ? v[0].z : v[0].x;
+    float k1 = h2 ? v[0].w : v[0].y;
+    const float s0 = h2 ? v[0].x : v[0].z;
+    const float s1 = h2 ? v[0].y : v[0].w;
+    k0 += dpp_f<kDppXor2>(s0);
+    k1 += dpp_f<kDppXor2>(s1);
+    const bool h1 = (sub & 1) != 0;
+    float kk = h1 ? k1 : k0;
+    kk += dpp_f<kDppXor1>(h1 ? k0 : k1);
+    s[b] += kk;
   }
-  return 0;   // unreachable: the table is at most half full
-}
-
-__device__ __forceinline__ int step_find(const int32_t* skey, int32_t row) {
-  if (row < 0) return -1;
-  uint32_t h = hmix(row) >> (32 - ilog2(kSHS));
-  for (int p = 0; p < kSHS; ++p) {
-    const int32_t k = skey[h];
-    if (k == row) return (int)h;
-    if (k < 0) return -1;
-    h = (h + 1) & (kSHS - 1);
-  }
-  return -1;
 }
 
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
-__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ------------------------------------------------------------ S0 scores
+// S0[i * LC + l]: score of label l of sample beg + i at the segment start;
+// LS0[i]: its best active wrong label there (-1: none); PP0[i * 32 + f]:
+// (P0(row_f, y), P0(row_f, LS0[i])) of its first 32 features (P != nullptr)
 template <int LC>
 __global__ __launch_bounds__(256) void delta_s0_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
-    const float* __restrict__ fval, const int64_t* __restrict__ stream_ptr, int nstreams,
-    const float* __restrict__ W, float* __restrict__ S0, const int64_t* __restrict__ reason) {
+    const float* __restrict__ fval, const int32_t* __restrict__ labels,
+    const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
+    const float* __restrict__ P, const int32_t* __restrict__ active, float* __restrict__ S0,
+    int32_t* __restrict__ LS0, float2* __restrict__ PP0, const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   static_assert(LC <= 64, "delta committer: LC <= 64");
   if (reason != nullptr && (*reason == kStopDense || *reason == kStopDone)) return;
@@ -209,6 +230,7 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int g = lane / L::LW;
   const int l0 = lane % L::LW;
+  const bool la = l0 < LC && active[l0] != 0;
   for (int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wid < cnt; wid += nwaves) {
     const int64_t s = beg + wid;
     const int64_t fb = row_ptr[s];
@@ -221,10 +243,31 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
 #pragma unroll
     for (int off = L::LW; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
     if (lane < LC) S0[wid * LC + lane] = acc;
+    if (P == nullptr) continue;
+    const int y = labels[s];
+    if (y < 0 || y >= LC) continue;
+    float b = (la && l0 != y) ? acc : -INFINITY;
+    int bl = (la && l0 != y) ? l0 : -1;
+#pragma unroll
+    for (int off = 1; off < L::LW; off <<= 1) {
+      const float ob = __shfl_xor(b, off, 64);
+      const int ol = __shfl_xor(bl, off, 64);
+      if (ol >= 0 && (bl < 0 || ob > b || (ob == b && ol < bl))) { b = ob; bl = ol; }
+    }
+    if (lane == 0) LS0[wid] = bl;
+    if (lane < kNFMax && lane < n) {
+      const int32_t idx = fidx[fb + lane];
+      float2 pp = make_float2(1.f, 1.f);
+      if (idx >= 0) {
+        pp.x = P[(int64_t)idx * LC + y];
+        if (bl >= 0) pp.y = P[(int64_t)idx * LC + bl];
+      }
+      PP0[wid * kNFMax + lane] = pp;
+    }
   }
 }
 
-// one sample's round data (group layout: lane u holds features u, u+16, ...)
+// one sample's round data (group layout: lane u holds features u, u + 16)
 struct Desc {
   int64_t fb;
   int nf;
@@ -235,7 +278,10 @@ template <int LC>
 struct Samp {
   int32_t fi[kFC];
   float fx[kFC];
+  float py[kFC];   // P0(row, y), P0(row, ls0)
+  float pl[kFC];
   float s[Geo<LC>::K];
+  int ls0;
 };
 
 // ------------------------------------------------------------ committer
@@ -245,8 +291,9 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* __restrict__ W,
     float* __restrict__ P, const int32_t* __restrict__ active, int method, float C,
-    const float* __restrict__ S0, unsigned long long* __restrict__ stats,
-    uint8_t* __restrict__ touched, int64_t* __restrict__ tail, int seg) {
+    const float* __restrict__ S0, const int32_t* __restrict__ LS0, const float2* __restrict__ PP0,
+    unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
+    int64_t* __restrict__ tail, int seg) {
   using Gm = Geo<LC>;
   constexpr int K = Gm::K;
   constexpr int NSLOT = Gm::NSLOT;
@@ -254,33 +301,34 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   if (seg > 0 && (tail[kTailReason] == kStopDense || tail[kTailReason] == kStopDone)) return;
   __shared__ float s_dw[NSLOT * LC];
   __shared__ float s_dp[NSLOT * LC];
-  __shared__ int32_t s_hkey[HS];
-  __shared__ int16_t s_hslot[HS];
-  __shared__ int32_t s_ckey[NSLOT];
-  __shared__ int32_t s_skey[kSHS];
-  __shared__ float s_sdy[kSHS];
-  __shared__ float s_sdl[kSHS];
-  __shared__ int32_t s_spos[kNFMax];
-  __shared__ int s_sn, s_cn, s_stop, s_upd, s_yk, s_lk;
+  __shared__ uint64_t s_hent[HS];
+  __shared__ int32_t s_sst[NSLOT];    // id of the last step that wrote the slot
+  __shared__ float s_sdy[NSLOT];      // that step's increment of labels y / l
+  __shared__ float s_sdl[NSLOT];
+  __shared__ int s_cn, s_stop, s_upd, s_yk, s_lk, s_nins;
   __shared__ int s_first[2];
   __shared__ unsigned s_nupd, s_waste, s_refresh;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int sub = lane & 15;
-  const int base = lane & 48;
   const int G = tid >> 4;
+  const int wv = tid >> 6;
   const bool use_s = method >= CW;
+  const uint64_t t_k0 = cyc();
+  const uint64_t w_k0 = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};   // start, barrier A, step, corrections, flush, init
+  uint64_t wwork = 0;
 
   {
     float4* dw4 = reinterpret_cast<float4*>(s_dw);
     float4* dp4 = reinterpret_cast<float4*>(s_dp);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = tid; i < NSLOT * LC / 4; i += kT) { dw4[i] = z; dp4[i] = z; }
-    for (int i = tid; i < HS; i += kT) s_hkey[i] = -1;
-    for (int i = tid; i < kSHS; i += kT) { s_skey[i] = -1; s_sdy[i] = 0.f; s_sdl[i] = 0.f; }
+    for (int i = tid; i < NSLOT * LC / 4; i += kT) { dw4[i] = z; if (use_s) dp4[i] = z; }
+    for (int i = tid; i < HS; i += kT) s_hent[i] = kEmpty;
+    for (int i = tid; i < NSLOT; i += kT) s_sst[i] = -1;
     if (tid == 0) {
-      s_sn = 0; s_cn = 0; s_stop = -1; s_upd = 0; s_yk = -1; s_lk = -1;
+      s_cn = 0; s_stop = -1; s_upd = 0; s_yk = -1; s_lk = -1; s_nins = 0;
       s_first[0] = s_first[1] = kInf;
       s_nupd = 0; s_waste = 0; s_refresh = 0;
     }
@@ -315,16 +363,22 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       const bool ok = j < end && d[r].y >= 0 && d[r].y < LC;
       const int32_t* fp = fidx + d[r].fb + sub;
       const float* vp = fval + d[r].fb + sub;
+      const float2* pp = PP0 + (j - beg) * kNFMax + sub;
 #pragma unroll
       for (int c = 0; c < kFC; ++c) {
         const bool v = ok && c * 16 + sub < d[r].nf;
         sm[r].fi[c] = v ? fp[c * 16] : -1;
         sm[r].fx[c] = v ? vp[c * 16] : 0.f;
+        float2 q = make_float2(1.f, 1.f);
+        if (use_s && v) q = pp[c * 16];
+        sm[r].py[c] = q.x;
+        sm[r].pl[c] = q.y;
       }
       const float* s0p = S0 + (j - beg) * LC + sub;
 #pragma unroll
       for (int k = 0; k < K; ++k)
         sm[r].s[k] = (ok && sub + 16 * k < LC) ? s0p[16 * k] : 0.f;
+      sm[r].ls0 = (use_s && ok) ? LS0[j - beg] : -1;
     }
   };
 
@@ -334,64 +388,60 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   load_samp(beg, dn, sn);
   load_desc(beg + kNS, dnn);
   __syncthreads();
+  ph[5] = cyc() - t_k0;
 
   int64_t stop = end;
   int64_t why = kStopDone;
   unsigned n_valid = 0;
   int iter = 0;
-  int64_t n_steps = 0, n_rounds = 0;
+  int n_steps = 0;
+  int64_t n_rounds = 0;
 
   for (int64_t p = beg; p < end; p += kNS) {
+    uint64_t tt = cyc();
 #pragma unroll
     for (int r = 0; r < kR; ++r) { dc[r] = dn[r]; sc[r] = sn[r]; dn[r] = dnn[r]; }
     if (p + kNS < end) load_samp(p + kNS, dn, sn);
     if (p + 2 * kNS < end) load_desc(p + 2 * kNS, dnn);
 
-    // ---- round start: deltas of the rows the segment wrote, margins
+    // ---- round start: slots, deltas of the rows the segment wrote, slacks
     bool alive[kR], unsafe[kR];
-    float nrm[kR];
-    int nch[kR];
+    float nrm[kR], slack[kR];
+    int slot[kR][kFC];
+    bool any = false;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int64_t j = p + G * kR + r;
-      const int y = dc[r].y;
-      alive[r] = j < end && y >= 0 && y < LC;
-      nch[r] = (dc[r].nf + 15) >> 4;
-      unsafe[r] = false;
-      nrm[r] = 0.f;
-      if (!alive[r]) continue;
-      if (dc[r].nf > kNFMax) { unsafe[r] = true; continue; }   // ends the committer when reached
-      float q = 0.f;
+      alive[r] = j < end && dc[r].y >= 0 && dc[r].y < LC;
 #pragma unroll
       for (int c = 0; c < kFC; ++c) {
-        if (c >= nch[r]) break;
-        const int32_t row = sc[r].fi[c];
-        const float x = sc[r].fx[c];
-        if (row >= 0) q += x * x;
-        const int slot = cache_find<LC>(s_hkey, s_hslot, row);
-        // rows with a delta, over the whole wave: skip features no row of it has
-        const uint64_t any = __builtin_amdgcn_ballot_w64(slot >= 0);
-        if (any == 0) continue;
-        for (int u = 0; u < 16; ++u) {
-          // lanes u of the four rows
-          if (((any >> u) | (any >> (16 + u)) | (any >> (32 + u)) | (any >> (48 + u))) & 1ull) {
-            const int su = rowb_i(slot, base, u);
-            const float xu = rowb_f(x, base, u);
-            if (su >= 0) {
-#pragma unroll
-              for (int k = 0; k < K; ++k) {
-                const int lab = sub + 16 * k;
-                if (lab < LC) sc[r].s[k] += xu * s_dw[su * LC + lab];
-              }
-            }
-          }
-        }
+        slot[r][c] = -1;
+        if (alive[r] && dc[r].nf <= kNFMax) slot[r][c] = cache_find<LC>(s_hent, sc[r].fi[c]);
+        any |= slot[r][c] >= 0;
       }
+    }
+    // rows with a delta anywhere in the wave: the transposed correction
+    if (__builtin_amdgcn_ballot_w64(any) != 0) {
+#pragma unroll
+      for (int r = 0; r < kR; ++r) row_correct<LC>(s_dw, slot[r], sc[r].fx, sub, sc[r].s);
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < kFC; ++c) q += sc[r].fx[c] * sc[r].fx[c];
       nrm[r] = row16_sum(q);
       int ls;
       float sy, best;
-      const float m = group_margin<LC>(sc[r].s, y, act, sub, base, &ls, &sy, &best);
-      unsafe[r] = may_update(method, m, nrm[r], ls >= 0, C, sy, best);
+      const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
+      slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
+      unsafe[r] = alive[r] && (dc[r].nf > kNFMax || !(slack[r] > 0.f));
+    }
+    {
+      const uint64_t t2 = cyc();
+      ph[0] += t2 - tt;
+      wwork += t2 - tt;
+      tt = t2;
     }
 
     int lim = -1;               // round positions <= lim are settled
@@ -401,52 +451,60 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 #pragma unroll
       for (int r = kR - 1; r >= 0; --r) {
         const int pos = G * kR + r;
-        if (alive[r] && unsafe[r] && pos > lim) myfirst = pos;
+        if (unsafe[r] && pos > lim) myfirst = pos;
       }
       myfirst = min(myfirst, partner16_i(myfirst, lane));
       myfirst = min(myfirst, partner32_i(myfirst, lane));
       if (lane == 0 && myfirst != kInf) atomicMin(&s_first[iter & 1], myfirst);
       lds_barrier();            // A: the first sample of the round that may update
+      {
+        const uint64_t t2 = cyc();
+        ph[1] += t2 - tt;
+        tt = t2;
+      }
       const int k = s_first[iter & 1];
       if (tid == 0) s_first[(iter + 1) & 1] = kInf;
       ++iter;
       if (k == kInf) break;
+      const int sid = n_steps;
       if (G == k / kR) {
         // ---------------- the exact step of sample k (this group's 16 lanes)
         const int rk = k % kR;
         Samp<LC> t = sc[0];
         Desc dd = dc[0];
         float tn = nrm[0];
+        int sl[kFC];
+#pragma unroll
+        for (int c = 0; c < kFC; ++c) sl[c] = slot[0][c];
 #pragma unroll
         for (int r = 1; r < kR; ++r)
-          if (r == rk) { t = sc[r]; dd = dc[r]; tn = nrm[r]; }
-        const int y = dd.y;
-        // the previous step's table is no longer read (barrier A)
-        for (int i = sub; i < s_sn; i += 16) {
-          const int h = s_spos[i];
-          s_skey[h] = -1; s_sdy[h] = 0.f; s_sdl[h] = 0.f;
-        }
-        int nvalid = 0;
+          if (r == rk) {
+            t = sc[r]; dd = dc[r]; tn = nrm[r];
 #pragma unroll
-        for (int c = 0; c < kFC; ++c) nvalid += t.fi[c] >= 0 ? 1 : 0;
-        nvalid = (int)row16_sum((float)nvalid);
-        lds_wait();
-        if (sub == 0) s_sn = 0;
+            for (int c = 0; c < kFC; ++c) sl[c] = slot[r][c];
+          }
+        const int y = dd.y;
+        // rows the step would add to the store
+        uint64_t nb[kFC];
+        int nnew = 0;
+#pragma unroll
+        for (int c = 0; c < kFC; ++c) {
+          nb[c] = __builtin_amdgcn_ballot_w64(t.fi[c] >= 0 && sl[c] < 0);
+          nnew += __popcll(nb[c]);
+        }
+        const int base = s_cn;
+        if (sub == 0) { s_nins = 0; s_upd = 0; }
         if (dd.nf > kNFMax) {
           if (sub == 0) s_stop = (int)kStopDense;
-        } else if (s_cn + nvalid > NSLOT) {
+        } else if (base + nnew > NSLOT) {
           if (sub == 0) s_stop = (int)kStopSaturated;
         } else {
-          int slot[kFC];
-          const int nc = (dd.nf + 15) >> 4;
-#pragma unroll
-          for (int c = 0; c < kFC; ++c) slot[c] = c < nc ? cache_find<LC>(s_hkey, s_hslot, t.fi[c]) : -1;
-          float py[kFC], pl[kFC];
           int ls = -1;
           float m = 0.f, sy = 0.f, best = 0.f, var = 0.f;
+          float py[kFC], pl[kFC];
           bool refreshed = false;
           for (;;) {
-            m = group_margin<LC>(t.s, y, act, sub, base, &ls, &sy, &best);
+            m = group_margin<LC>(t.s, y, act, sub, &ls, &sy, &best);
             float v = 0.f;
 #pragma unroll
             for (int c = 0; c < kFC; ++c) {
@@ -454,9 +512,12 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
               pl[c] = 1.f;
               const int32_t row = t.fi[c];
               if (!use_s || row < 0) continue;
-              const int64_t rb = (int64_t)row * LC;
-              py[c] = P[rb + y] + (slot[c] >= 0 ? s_dp[slot[c] * LC + y] : 0.f);
-              if (ls >= 0) pl[c] = P[rb + ls] + (slot[c] >= 0 ? s_dp[slot[c] * LC + ls] : 0.f);
+              const float* dpr = s_dp + (sl[c] >= 0 ? sl[c] : 0) * LC;
+              py[c] = t.py[c] + (sl[c] >= 0 ? dpr[y] : 0.f);
+              if (ls >= 0) {
+                const float p0 = ls == t.ls0 ? t.pl[c] : P[(int64_t)row * LC + ls];
+                pl[c] = p0 + (sl[c] >= 0 ? dpr[ls] : 0.f);
+              }
               const float x2 = t.fx[c] * t.fx[c];
               v += x2 * (1.f / py[c] + (ls >= 0 ? 1.f / pl[c] : 0.f));
             }
@@ -473,11 +534,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
             for (int kk = 0; kk < K; ++kk) ns[kk] = 0.f;
 #pragma unroll
             for (int c = 0; c < kFC; ++c) {
-              if (c >= nc) break;
+#pragma unroll 1
               for (int u = 0; u < 16; ++u) {
-                const int32_t ru = rowb_i(t.fi[c], base, u);
-                const float xu = rowb_f(t.fx[c], base, u);
-                const int su = rowb_i(slot[c], base, u);
+                const int32_t ru = __shfl(t.fi[c], (lane & 48) + u, 64);
+                const float xu = __shfl(t.fx[c], (lane & 48) + u, 64);
+                const int su = __shfl(sl[c], (lane & 48) + u, 64);
                 if (ru < 0) continue;
 #pragma unroll
                 for (int kk = 0; kk < K; ++kk) {
@@ -493,45 +554,51 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           float tau = 0.f, beta = 0.f;
           const bool up = step_coeffs(method, m, var, tn, ls >= 0, C, &tau, &beta);
           if (up) {
-            uint32_t hp[kFC];
-#pragma unroll
-            for (int c = 0; c < kFC; ++c)
-              hp[c] = (t.fi[c] >= 0 && slot[c] < 0)
-                          ? cache_insert<LC>(s_hkey, s_hslot, s_ckey, &s_cn, t.fi[c]) : 0u;
-            lds_wait();
-#pragma unroll
-            for (int c = 0; c < kFC; ++c)
-              if (t.fi[c] >= 0 && slot[c] < 0) slot[c] = s_hslot[hp[c]];
+            // new rows: slots base + rank among the row's new features (a row
+            // another lane inserted first keeps that lane's slot)
+            const uint64_t below = (1ull << lane) - 1ull;
+            int off = 0;
 #pragma unroll
             for (int c = 0; c < kFC; ++c) {
-              const int32_t row = t.fi[c];
-              if (row < 0) continue;
+              if (t.fi[c] >= 0 && sl[c] < 0) {
+                const int ns = base + off + __popcll(nb[c] & below);
+                uint32_t h = hmix(t.fi[c]) >> (32 - Gm::HB);
+                for (int q = 0; q < HS; ++q) {
+                  const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(&s_hent[h]),
+                                                 (unsigned long long)kEmpty,
+                                                 (unsigned long long)hpack(t.fi[c], ns));
+                  if (old == kEmpty) { sl[c] = ns; break; }
+                  if ((int32_t)(uint32_t)old == t.fi[c]) { sl[c] = (int)(old >> 32); break; }
+                  h = (h + 1) & (HS - 1);
+                }
+              }
+              off += __popcll(nb[c]);
+            }
+#pragma unroll
+            for (int c = 0; c < kFC; ++c)
+              if (t.fi[c] >= 0) { s_sst[sl[c]] = sid; s_sdy[sl[c]] = 0.f; s_sdl[sl[c]] = 0.f; }
+#pragma unroll
+            for (int c = 0; c < kFC; ++c) {
+              if (t.fi[c] < 0) continue;
               const float x = t.fx[c];
               const float a = use_s ? 1.f / py[c] : 1.f;
               const float b = (use_s && ls >= 0) ? 1.f / pl[c] : 1.f;
               const float dwy = tau * a * x;
               const float dwl = ls >= 0 ? -tau * b * x : 0.f;
-              float* dwr = s_dw + slot[c] * LC;
+              float* dwr = s_dw + sl[c] * LC;
               atomicAdd(dwr + y, dwy);
               if (ls >= 0) atomicAdd(dwr + ls, dwl);
               if (use_s) {
-                float* dpr = s_dp + slot[c] * LC;
+                float* dpr = s_dp + sl[c] * LC;
                 atomicAdd(dpr + y, dprec(method, beta, x, a));
                 if (ls >= 0) atomicAdd(dpr + ls, dprec(method, beta, x, b));
               }
-              // the step table: this update's increments per row
-              uint32_t h = hmix(row) >> (32 - ilog2(kSHS));
-              for (int q = 0; q < kSHS; ++q) {
-                const int32_t old = atomicCAS(&s_skey[h], -1, row);
-                if (old == -1) { s_spos[atomicAdd(&s_sn, 1)] = (int)h; break; }
-                if (old == row) break;
-                h = (h + 1) & (kSHS - 1);
-              }
-              atomicAdd(&s_sdy[h], dwy);
-              atomicAdd(&s_sdl[h], dwl);
+              atomicAdd(&s_sdy[sl[c]], dwy);
+              atomicAdd(&s_sdl[sl[c]], dwl);
             }
           }
           if (sub == 0) {
+            if (up) { s_cn = base + nnew; s_nins = nnew; }
             s_upd = up ? 1 : 0;
             s_yk = y;
             s_lk = ls;
@@ -540,6 +607,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         }
       }
       lds_barrier();            // B: the step (or the stop) is visible
+      {
+        const uint64_t t2 = cyc();
+        ph[2] += t2 - tt;
+        tt = t2;
+      }
       ++n_steps;
       const int sc_stop = s_stop;
       if (sc_stop >= 0) {
@@ -548,8 +620,9 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         stop = p + k;
         break;
       }
-      if (s_upd) {
-        const int yk = s_yk, lk = s_lk;
+      // samples after k: the step's increments of their stamped rows
+      if (s_upd && (wv + 1) * 4 * kR - 1 > k) {
+        const int yk = s_yk, lk = s_lk, nins = s_nins;
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
           const int pos = G * kR + r;
@@ -557,11 +630,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           float cy = 0.f, cl = 0.f;
 #pragma unroll
           for (int c = 0; c < kFC; ++c) {
-            if (c >= nch[r]) break;
-            const int h = step_find(s_skey, sc[r].fi[c]);
-            if (h >= 0) {
-              cy += sc[r].fx[c] * s_sdy[h];
-              cl += sc[r].fx[c] * s_sdl[h];
+            if (slot[r][c] < 0 && nins > 0) slot[r][c] = cache_find<LC>(s_hent, sc[r].fi[c]);
+            const int s = slot[r][c];
+            if (s >= 0 && s_sst[s] == sid) {
+              cy += sc[r].fx[c] * s_sdy[s];
+              cl += sc[r].fx[c] * s_sdl[s];
             }
           }
           cy = row16_sum(cy);
@@ -572,13 +645,23 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
             if (lab == yk) sc[r].s[kk] += cy;
             if (lab == lk) sc[r].s[kk] += cl;
           }
-          int ls;
-          float sy, best;
-          const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, base, &ls, &sy, &best);
-          unsafe[r] = may_update(method, m, nrm[r], ls >= 0, C, sy, best);
+          // the margin moves by at most |cy| + |cl| (the guard band by 1e-4 of it)
+          slack[r] -= (fabsf(cy) + fabsf(cl)) * (1.f + 4.f * kGuard);
+          if (!(slack[r] > 0.f)) {
+            int ls;
+            float sy, best;
+            const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
+            slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
+            unsafe[r] = !(slack[r] > 0.f);
+          }
         }
       }
       lim = k;
+      {
+        const uint64_t t2 = cyc();
+        ph[3] += t2 - tt;
+        tt = t2;
+      }
     }
     ++n_rounds;
     if (sub == 0) {
@@ -589,27 +672,45 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     if (stop != end) break;
   }
   __syncthreads();
+  const uint64_t t_f0 = cyc();
   // ---- segment end: the deltas into the tables (the committer is their only writer)
   {
-    const int n = s_cn;
-    for (int i = tid; i < n * LC; i += kT) {
-      const int sl = i / LC;
-      const int l = i % LC;
-      const int64_t row = s_ckey[sl];
-      W[row * LC + l] += s_dw[i];
-      if (use_s) P[row * LC + l] += s_dp[i];
-      if (l == 0 && touched != nullptr) touched[row] = 1;
+    constexpr int Q = LC / 4;
+    for (int i = tid; i < HS * Q; i += kT) {
+      const uint64_t e = s_hent[i / Q];
+      const int32_t row = (int32_t)(uint32_t)e;
+      if (row < 0) continue;
+      const int q = i % Q;
+      const int sl = (int)(e >> 32);
+      float4* w4 = reinterpret_cast<float4*>(W + (int64_t)row * LC) + q;
+      const float4 d = reinterpret_cast<const float4*>(s_dw + sl * LC)[q];
+      float4 w = *w4;
+      w.x += d.x; w.y += d.y; w.z += d.z; w.w += d.w;
+      *w4 = w;
+      if (use_s) {
+        float4* p4 = reinterpret_cast<float4*>(P + (int64_t)row * LC) + q;
+        const float4 dp = reinterpret_cast<const float4*>(s_dp + sl * LC)[q];
+        float4 pv = *p4;
+        pv.x += dp.x; pv.y += dp.y; pv.z += dp.z; pv.w += dp.w;
+        *p4 = pv;
+      }
+      if (q == 0 && touched != nullptr) touched[row] = 1;
     }
   }
   if (n_valid > 0 && stats != nullptr) atomicAdd(stats + 1, (unsigned long long)n_valid);
+  auto put = [&](int i, int64_t v) { tail[i] = seg == 0 ? v : tail[i] + v; };
+  if (kProf && lane == 0 && tid > 0) put(12 + wv, (int64_t)wwork);
   if (tid == 0) {
-    auto put = [&](int i, int64_t v) { tail[i] = seg == 0 ? v : tail[i] + v; };
     tail[0] = stop;
     tail[1] = end;
     tail[kTailReason] = why;
     put(2, n_steps);
     put(3, n_rounds);
-    for (int i = 4; i < 20; ++i) put(i, 0);
+    ph[4] = cyc() - t_f0;
+    for (int i = 0; i < 6; ++i) put(4 + i, (int64_t)ph[i]);
+    put(10, kProf ? (int64_t)(__builtin_amdgcn_s_memrealtime() - w_k0) : 0);
+    put(11, (int64_t)(cyc() - t_k0));
+    put(12, (int64_t)wwork);
     put(21, 1);
     put(22, (int64_t)s_waste);
     put(23, (int64_t)s_refresh);
@@ -622,9 +723,13 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 }  // namespace dc
 }  // namespace jb
 
+// bytes of the delta committer's scratch per sample: S0 (<= 64 floats),
+// PP0 (32 float2), LS0 (one int, padded)
+extern "C" int64_t jb_delta_scratch_per_sample() { return 256 + 256 + 8; }
+
 // Steps 1-2 of a kSerial batch for LC <= 64 (see the header); the caller
 // runs the exact single-stream kernel over [tail[0], tail[1]) afterwards.
-// scratch: [tail int64 x 32][S0: n_max x LC floats].
+// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2][LS0: n_max ints].
 extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
@@ -633,6 +738,9 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
   if (LC > 64) return -1;
   int64_t* tail = (int64_t*)scratch;
   float* s0 = (float*)((uint8_t*)scratch + 256);
+  float2* pp0 = (float2*)((uint8_t*)scratch + 256 + 256 * n_max);
+  int32_t* ls0 = (int32_t*)((uint8_t*)scratch + 256 + 512 * n_max);
+  float* Pp = method >= jb::CW ? S : nullptr;
   const int64_t blocks = std::min<int64_t>((n_max * 64 + 255) / 256, 2048);
   for (int seg = 0; seg < nseg; ++seg) {
     const int64_t* sp = seg == 0 ? stream_ptr : tail;
@@ -640,10 +748,10 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
     const int64_t* why = seg == 0 ? nullptr : tail + jb::dc::kTailReason;
 #define JB_DELTA(L)                                                                                \
   hipLaunchKernelGGL((jb::dc::delta_s0_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream,  \
-                     row_ptr, fidx, fval, sp, ns, W, s0, why);                                    \
+                     row_ptr, fidx, fval, labels, sp, ns, W, Pp, active, s0, ls0, pp0, why);      \
   hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L>), dim3(1), dim3(jb::dc::kT), 0, stream,       \
-                     row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, s0, stats,      \
-                     touched, tail, seg);
+                     row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, s0, ls0, pp0,  \
+                     stats, touched, tail, seg);
     switch (LC) {
       case 8: JB_DELTA(8); break;
       case 16: JB_DELTA(16); break;

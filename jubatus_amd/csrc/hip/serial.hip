@@ -35,6 +35,9 @@
 #include "jb_linear.hpp"
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 namespace jb {
 
@@ -63,6 +66,8 @@ constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2, kStopRescor
 constexpr int kSerialSegments = 4;       // segments of a small batch
 constexpr int kSerialSegmentsBig = 48;   // of a batch of >= kSerialBigBatch samples
 constexpr int64_t kSerialBigBatch = 16384;
+constexpr int kDeltaSegmentsMin = 8;     // delta committer segments of a big batch
+constexpr int kDeltaSegmentsMax = 128;
 constexpr int kRescoreWaste = 16;        // wasted exact steps that end a segment
 constexpr int kScoreMaxBlocks = 8192;    // serial_score_kernel grid cap (grid-stride)
 // committer phase timings (tail[4..19]): shader-clock reads in the step loop
@@ -764,12 +769,16 @@ __global__ __launch_bounds__(kCommitThreads) void serial_commit_kernel(
 
 }  // namespace jb
 
+// commit.hip: per-sample scratch bytes of the delta committer
+extern "C" int64_t jb_delta_scratch_per_sample();
+
 // bytes of the kSerial scratch for batches of up to n_max samples:
-// [tail int64 x 32 = 256 B][per sample: the delta committer's S0 scores
-// (commit.hip, LC <= 64 floats) or this file's slack + |x|_1 (LC > 64)];
-// n_max bounds the batch's sample count stream_ptr[nstreams] - stream_ptr[0]
+// [tail int64 x 32 = 256 B][per sample: the delta committer's S0 scores,
+// precisions and best wrong label (commit.hip, LC <= 64) or this file's
+// slack + |x|_1 (LC > 64)]; n_max bounds the batch's sample count
+// stream_ptr[nstreams] - stream_ptr[0]
 extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max) {
-  return 256 + 256 * (n_max > 0 ? n_max : 1);
+  return 256 + jb_delta_scratch_per_sample() * (n_max > 0 ? n_max : 1);
 }
 
 // commit.hip: the delta committer (label capacities <= 64)
@@ -778,6 +787,20 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
                                 int method, float C, unsigned long long* stats, uint8_t* touched,
                                 void* scratch, int nseg, hipStream_t stream);
+
+// pinned host word per scratch buffer: segments the last delta batch used
+static int64_t* delta_segments_seen(void* scratch) {
+  static std::mutex mu;
+  static std::unordered_map<void*, int64_t*> seen;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = seen.find(scratch);
+  if (it != seen.end()) return it->second;
+  int64_t* p = nullptr;
+  if (hipHostMalloc((void**)&p, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
+  *p = 0;
+  seen[scratch] = p;
+  return p;
+}
 
 // committer of LC <= 64: 1 = delta (commit.hip, default), 0 = this file's
 // bound committer (JB_SERIAL_COMMITTER=bound, for A/B runs)
@@ -803,10 +826,22 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   if (scratch == nullptr || scratch_bytes < jb_serial_scratch_bytes(n_max)) return -3;
   if (method >= jb::CW && S == nullptr) return -4;
   if (LC <= 64 && serial_committer() == 1) {
-    // delta committer: segments end only when the LDS row store fills
-    const int nseg = n_max >= jb::kSerialBigBatch ? 24 : jb::kSerialSegments;
-    return jb_delta_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W, S, active,
-                            LC, method, C, stats, touched, scratch, nseg, stream);
+    // delta committer: segments end only when the LDS row store fills. A
+    // segment that finds the batch done costs two empty launches (~4 us), a
+    // batch that runs out of segments hands its rest to the sequential kernel:
+    // the count follows the segments the previous batch on this scratch used
+    // (read back asynchronously into pinned memory, one batch late at worst)
+    int nseg = jb::kSerialSegments;
+    int64_t* seen = delta_segments_seen(scratch);
+    if (n_max >= jb::kSerialBigBatch) {
+      const int64_t prev = seen != nullptr ? *(volatile int64_t*)seen : 0;
+      nseg = (int)std::min<int64_t>(jb::kDeltaSegmentsMax, std::max<int64_t>(jb::kDeltaSegmentsMin, 2 * prev + 4));
+    }
+    const int rc = jb_delta_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W, S, active,
+                                    LC, method, C, stats, touched, scratch, nseg, stream);
+    if (rc == 0 && seen != nullptr)
+      (void)hipMemcpyAsync(seen, (int64_t*)scratch + 21, sizeof(int64_t), hipMemcpyDeviceToHost, stream);
+    return rc;
   }
   int64_t* tail = (int64_t*)scratch;
   float* slack = (float*)((uint8_t*)scratch + 256);

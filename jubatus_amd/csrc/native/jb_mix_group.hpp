@@ -1102,6 +1102,15 @@ class ClusterNode {
     }
     return out;
   }
+  // every registered actor ("ip_port" children of <actor>/nodes, membership.py get_all_nodes)
+  std::vector<std::pair<std::string, int>> actors() {
+    std::vector<std::pair<std::string, int>> out;
+    for (const auto& loc : coord_->list(actor_path(type_, name_) + "/nodes")) {
+      const size_t u = loc.rfind('_');
+      if (u != std::string::npos) out.emplace_back(loc.substr(0, u), atoi(loc.c_str() + u + 1));
+    }
+    return out;
+  }
   // the whole ring, sorted by vnode hash: (md5 hex, "ip_port") - for engines
   // that place many keys at once (burst's processed keywords)
   std::vector<std::pair<std::string, std::string>> cht_ring() {

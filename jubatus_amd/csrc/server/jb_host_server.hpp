@@ -44,6 +44,10 @@ struct HostMethod {
   // optional zero-decode handler: the raw msgpack params array (arity
   // checked), for bulk payloads the engine reads in place (clustering push)
   std::function<void(const std::string&, MsgpackWriter*)> raw = nullptr;
+  // the handler takes the model lock itself (HostEngine::set_lock): methods
+  // that call other servers must not hold it meanwhile (graph_serv.cpp:
+  // create_node / remove_node / create_edge)
+  bool self_lock = false;
 };
 
 class HostEngine {
@@ -66,11 +70,12 @@ class HostEngine {
   // distributed mode: the cluster this server joined (its CHT, its
   // server-to-server peers) and its own address; called before serving and
   // again when a loaded model file replaces the engine
-  virtual void attach(jb::mix::ClusterNode* node, const std::string& eth, int port) {
+  virtual void attach(jb::mix::ClusterNode* node, const Args& a) {
     (void)node;
-    (void)eth;
-    (void)port;
+    (void)a;
   }
+  // the server's model lock, for self_lock methods
+  virtual void set_lock(std::shared_mutex* mu) { (void)mu; }
 };
 
 // a method error reported to the client as the message string
@@ -86,6 +91,7 @@ class HostServer : public jb::mix::Mixable {
   HostServer(const Args& a, const std::string& config, Factory make)
       : a_(a), config_(config), make_(std::move(make)) {
     eng_ = make_(config_);
+    eng_->set_lock(&model_mu_);
     for (auto& m : eng_->methods()) table_.push_back(m);
   }
 
@@ -155,7 +161,7 @@ class HostServer : public jb::mix::Mixable {
     a_.port = port;
     if (node_) {
       std::unique_lock<std::shared_mutex> g(model_mu_);
-      eng_->attach(node_.get(), a_.eth, a_.port);
+      eng_->attach(node_.get(), a_);
     }
     logf_("INFO", "start listening at port %d", port);
     cs_.start_time = time(nullptr);
@@ -258,7 +264,13 @@ class HostServer : public jb::mix::Mixable {
         if (args.a.size() != hm->arity)
           return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
         std::vector<Value> rest(args.a.begin() + 1, args.a.end());
-        if (hm->update) {
+        if (hm->self_lock) {
+          if (hm->update) {
+            if (mixer_) mixer_->updated(1);
+            update_count_ += 1;
+          }
+          hm->fn(rest, &w);
+        } else if (hm->update) {
           if (mixer_) mixer_->updated(1);
           std::unique_lock<std::shared_mutex> g(model_mu_);
           update_count_ += 1;
@@ -337,10 +349,11 @@ class HostServer : public jb::mix::Mixable {
     std::unique_lock<std::shared_mutex> g(model_mu_);
     if (overwrite_config && !jb::val::same_config(mf.config, config_)) {
       eng_ = make_(mf.config);
+      eng_->set_lock(&model_mu_);
       config_ = mf.config;
       table_.clear();
       for (auto& m : eng_->methods()) table_.push_back(m);
-      if (node_) eng_->attach(node_.get(), a_.eth, a_.port);
+      if (node_) eng_->attach(node_.get(), a_);
     }
     eng_->unpack(mf.user);
     std::lock_guard<std::mutex> s(st_mu_);

@@ -302,9 +302,9 @@ class Burst : public HostEngine {
   // ---- distributed mode
   bool mixable() const override { return true; }
   bool uses_cht() const override { return true; }
-  void attach(jb::mix::ClusterNode* node, const std::string& eth, int port) override {
+  void attach(jb::mix::ClusterNode* node, const Args& a) override {
     node_ = node;
-    loc_ = eth + "_" + std::to_string(port);
+    loc_ = a.eth + "_" + std::to_string(a.port);
     ring_.clear();
   }
   // {"keywords": {k: [scaling, gamma]}, "results": {processed k: windows}}

@@ -9,14 +9,23 @@
 // index of the last update_index; centrality 0 = damped PageRank fixed point
 // s = (1 - d) + d A^T (s / outdeg) on the query's subgraph; shortest path =
 // hop-limited BFS over the indexed subgraph (edges in insertion order).
-// Standalone only: distributed mode (CHT-replicated writes, MIX) is the
-// Python server's. Model files are shared with it (Graph.pack()).
+// Distributed (-z, graph_serv.cpp:150-330): node and edge ids come from the
+// coordinator's id generator; create_node creates the node on its two CHT
+// owners (create_node_here, server to server; the primary must succeed),
+// remove_node tells every member (remove_global_node) after releasing the
+// model lock, create_edge stores the edge here and replicates it to the
+// source node's other owner (create_edge_here); the indices are built at MIX
+// over the local graph plus every member's nodes and edges (models/graph.py
+// get_diff / mix_diff / put_diff). Model files are shared with the Python
+// server (Graph.pack()).
 #include <math.h>
 
 #include <algorithm>
 #include <deque>
 #include <map>
+#include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -135,28 +144,112 @@ class Graph : public HostEngine {
 
   std::vector<HostMethod> methods() override {
     using A = const std::vector<Value>&;
+    HostMethod cn{"create_node", 1, true, [this](A, MsgpackWriter* w) {
+      if (!node_) {
+        std::unique_lock<std::shared_mutex> g(*mu_);
+        const uint64_t id = next_id_++;
+        create_node_here(id, true);
+        w->raw(std::to_string(id));
+        return;
+      }
+      const std::string sid = std::to_string(node_->create_id());
+      const auto owners = node_->cht_find(sid, 2);
+      selective_create(owners[0], sid);   // the primary must succeed
+      for (size_t i = 1; i < owners.size(); ++i) {
+        try {
+          selective_create(owners[i], sid);
+        } catch (const std::exception& e) {
+          if (!strstr(e.what(), "exists"))
+            logf_("WARN", "cannot create replica of node %s (%s): %s:%d", sid.c_str(), e.what(),
+                  owners[i].first.c_str(), owners[i].second);
+        }
+      }
+      w->raw(sid);
+    }};
+    cn.self_lock = true;
+    HostMethod rn{"remove_node", 2, true, [this](A a, MsgpackWriter* w) {
+      const uint64_t id = node_id(a[0]);
+      {
+        std::unique_lock<std::shared_mutex> g(*mu_);
+        Node& n = node(id);
+        if (!n.in.empty() || !n.out.empty())
+          throw EngineError("cannot remove node " + std::to_string(id) + ": it has edges");
+        nodes_.erase(id);
+        node_order_.erase(std::find(node_order_.begin(), node_order_.end(), id));
+        global_.erase(id);
+      }
+      if (node_) {   // every other member forgets it (no result awaited: rpc_no_result)
+        for (const auto& m : node_->actors()) {
+          if (is_me(m)) continue;
+          try {
+            MsgpackWriter p;
+            p.arr(2);
+            p.raw(name_);
+            p.raw(std::to_string(id));
+            peer_call(m, "remove_global_node", p.out);
+          } catch (const std::exception& e) {
+            logf_("INFO", "remove_global_node: %s", e.what());
+          }
+        }
+      }
+      w->boolean(true);
+    }};
+    rn.self_lock = true;
+    HostMethod ce{"create_edge", 3, true, [this](A a, MsgpackWriter* w) {
+      const Value& e = a[1];
+      if (e.kind != Value::ARR || e.a.size() != 3) throw std::invalid_argument("edge expected");
+      const uint64_t src = node_id(e.a[1]), tgt = node_id(e.a[2]);
+      Props pr = props_of(e.a[0]);
+      if (!node_) {
+        std::unique_lock<std::shared_mutex> g(*mu_);
+        const uint64_t eid = next_id_++;   // taken before the checks (graph_serv.cpp create_edge)
+        if (!nodes_.count(src)) throw EngineError("unknown_id: source node " + std::to_string(src));
+        if (!nodes_.count(tgt) && !global_.count(tgt))
+          throw EngineError("unknown_id: target node " + std::to_string(tgt));
+        put_edge(eid, src, tgt, std::move(pr));
+        w->uint(eid);
+        return;
+      }
+      const uint64_t eid = node_->create_id();
+      const auto owners = node_->cht_find(std::to_string(src), 2);
+      MsgpackWriter p;   // create_edge_here(name, eid, [prop, src, tgt])
+      p.arr(3);
+      p.raw(name_);
+      p.uint(eid);
+      p.arr(3);
+      p.map(pr.size());
+      for (const auto& kv : pr) { p.raw(kv.first); p.raw(kv.second); }
+      p.raw(std::to_string(src));
+      p.raw(std::to_string(tgt));
+      {
+        std::unique_lock<std::shared_mutex> g(*mu_);
+        edge_here(eid, src, tgt, std::move(pr));
+      }
+      for (size_t i = 1; i < owners.size(); ++i) {
+        if (is_me(owners[i])) continue;
+        try {
+          peer_call(owners[i], "create_edge_here", p.out);
+        } catch (const std::exception& ex) {
+          logf_("WARN", "cannot create replica of edge %llu (%s): %s:%d", (unsigned long long)eid, ex.what(),
+                owners[i].first.c_str(), owners[i].second);
+        }
+      }
+      w->uint(eid);
+    }};
+    ce.self_lock = true;
     return {
-        {"create_node", 1, true, [this](A, MsgpackWriter* w) {
-           const uint64_t id = next_id_++;
-           create_node_here(id, true);
-           w->raw(std::to_string(id));
-         }},
+        cn,
+        rn,
+        ce,
         {"create_node_here", 2, true, [this](A a, MsgpackWriter* w) {
            create_node_here(node_id(a[0]), false);
            w->boolean(true);
          }},
-        {"remove_node", 2, true, [this](A a, MsgpackWriter* w) {
-           const uint64_t id = node_id(a[0]);
-           Node& n = node(id);
-           if (!n.in.empty() || !n.out.empty())
-             throw EngineError("cannot remove node " + std::to_string(id) + ": it has edges");
-           nodes_.erase(id);
-           node_order_.erase(std::find(node_order_.begin(), node_order_.end(), id));
-           global_.erase(id);
-           w->boolean(true);
-         }},
         {"remove_global_node", 2, true, [this](A a, MsgpackWriter* w) {
-           global_.erase(node_id(a[0]));
+           const uint64_t id = node_id(a[0]);
+           global_.erase(id);
+           if (remote_nodes_.erase(id))
+             remote_order_.erase(std::find(remote_order_.begin(), remote_order_.end(), id));
            w->boolean(true);
          }},
         {"update_node", 3, true, [this](A a, MsgpackWriter* w) {
@@ -173,25 +266,11 @@ class Graph : public HostEngine {
            w->arr(n.out.size());
            for (uint64_t e : n.out) w->uint(e);
          }},
-        {"create_edge", 3, true, [this](A a, MsgpackWriter* w) {
-           const Value& e = a[1];
-           if (e.kind != Value::ARR || e.a.size() != 3) throw std::invalid_argument("edge expected");
-           const uint64_t src = node_id(e.a[1]), tgt = node_id(e.a[2]);
-           Props pr = props_of(e.a[0]);
-           const uint64_t eid = next_id_++;   // taken before the checks (graph_serv.cpp create_edge)
-           if (!nodes_.count(src)) throw EngineError("unknown_id: source node " + std::to_string(src));
-           if (!nodes_.count(tgt) && !global_.count(tgt))
-             throw EngineError("unknown_id: target node " + std::to_string(tgt));
-           put_edge(eid, src, tgt, std::move(pr));
-           w->uint(eid);
-         }},
         {"create_edge_here", 3, true, [this](A a, MsgpackWriter* w) {
            const uint64_t eid = edge_id(a[0]);
            const Value& e = a[1];
            if (e.kind != Value::ARR || e.a.size() != 3) throw std::invalid_argument("edge expected");
-           const uint64_t src = node_id(e.a[1]), tgt = node_id(e.a[2]);
-           if (!nodes_.count(src)) { nodes_[src] = Node{}; node_order_.push_back(src); }
-           put_edge(eid, src, tgt, props_of(e.a[0]));
+           edge_here(eid, node_id(e.a[1]), node_id(e.a[2]), props_of(e.a[0]));
            w->boolean(true);
          }},
         {"update_edge", 4, true, [this](A a, MsgpackWriter* w) {
@@ -219,13 +298,17 @@ class Graph : public HostEngine {
          }},
         {"get_edge", 3, false, [this](A a, MsgpackWriter* w) {
            const uint64_t eid = edge_id(a[1]);
+           const Edge* e = nullptr;
            auto it = edges_.find(eid);
-           if (it == edges_.end()) throw EngineError("unknown_id: edge " + std::to_string(eid));
+           if (it != edges_.end()) e = &it->second;
+           auto rt = remote_edges_.find(eid);
+           if (!e && rt != remote_edges_.end()) e = &rt->second;
+           if (!e) throw EngineError("unknown_id: edge " + std::to_string(eid));
            w->arr(3);
-           w->map(it->second.p.size());
-           for (const auto& kv : it->second.p) { w->raw(kv.first); w->raw(kv.second); }
-           w->raw(std::to_string(it->second.s));
-           w->raw(std::to_string(it->second.t));
+           w->map(e->p.size());
+           for (const auto& kv : e->p) { w->raw(kv.first); w->raw(kv.second); }
+           w->raw(std::to_string(e->s));
+           w->raw(std::to_string(e->t));
          }},
         {"add_centrality_query", 2, true, [this](A a, MsgpackWriter* w) {
            cq_.insert(qkey(a[0]));
@@ -248,6 +331,7 @@ class Graph : public HostEngine {
            w->boolean(true);
          }},
         {"update_index", 1, true, [this](A, MsgpackWriter* w) {
+           if (node_) throw EngineError("manual mix is available only in standalone mode.");
            update_index();
            w->boolean(true);
          }},
@@ -262,7 +346,7 @@ class Graph : public HostEngine {
              auto it = sc->second.find(id);
              if (it != sc->second.end()) { w->dbl(it->second); return; }
            }
-           if (nodes_.count(id)) { w->dbl(0.0); return; }
+           if (nodes_.count(id) || remote_nodes_.count(id)) { w->dbl(0.0); return; }   // not indexed yet
            throw EngineError("unknown_id: node " + std::to_string(id));
          }},
         {"get_shortest_path", 2, false, [this](A a, MsgpackWriter* w) {
@@ -284,6 +368,10 @@ class Graph : public HostEngine {
     node_order_.clear();
     edges_.clear();
     edge_order_.clear();
+    remote_nodes_.clear();
+    remote_order_.clear();
+    remote_edges_.clear();
+    remote_edge_order_.clear();
     global_.clear();
     cq_.clear();
     sq_.clear();
@@ -300,28 +388,9 @@ class Graph : public HostEngine {
     u.str("nodes"); u.map(node_order_.size());
     for (uint64_t id : node_order_) write_props(&u, std::to_string(id), nodes_.at(id).p);
     u.str("edges"); u.map(edge_order_.size());
-    for (uint64_t eid : edge_order_) {
-      const Edge& e = edges_.at(eid);
-      u.str(std::to_string(eid));
-      u.arr(3);
-      u.uint(e.s);
-      u.uint(e.t);
-      u.map(e.p.size());
-      for (const auto& kv : e.p) { u.str(kv.first); u.str(kv.second); }
-    }
-    auto queries = [&](const char* name, const std::set<QKey>& qs) {
-      u.str(name);
-      u.arr(qs.size());
-      for (const QKey& k : qs) {
-        u.arr(2);
-        for (const Cond* c : {&k.first, &k.second}) {
-          u.arr(c->size());
-          for (const auto& kv : *c) { u.arr(2); u.str(kv.first); u.str(kv.second); }
-        }
-      }
-    };
-    queries("cq", cq_);
-    queries("sq", sq_);
+    for (uint64_t eid : edge_order_) write_edge(&u, eid, edges_.at(eid));
+    write_queries(&u, "cq", cq_);
+    write_queries(&u, "sq", sq_);
     std::vector<uint64_t> g(global_.begin(), global_.end());
     std::sort(g.begin(), g.end());
     u.str("global"); u.arr(g.size());
@@ -376,6 +445,74 @@ class Graph : public HostEngine {
     update_index();
   }
 
+  // ---- distributed mode
+  void set_lock(std::shared_mutex* mu) override { mu_ = mu; }
+  void attach(jb::mix::ClusterNode* node, const Args& a) override {
+    node_ = node;
+    eth_ = a.eth;
+    port_ = a.port;
+    name_ = a.name;
+    ic_timeout_ = std::max(1, a.ic_timeout);
+  }
+  bool mixable() const override { return true; }
+  bool uses_cht() const override { return true; }
+  // models/graph.py get_diff: the local nodes (properties), edges and queries
+  std::string get_diff() override {
+    MsgpackWriter u;
+    u.map(4);
+    u.str("nodes"); u.map(node_order_.size());
+    for (uint64_t id : node_order_) write_props(&u, std::to_string(id), nodes_.at(id).p);
+    u.str("edges"); u.map(edge_order_.size());
+    for (uint64_t eid : edge_order_) write_edge(&u, eid, edges_.at(eid));
+    write_queries(&u, "cq", cq_);
+    write_queries(&u, "sq", sq_);
+    return std::move(u.out);
+  }
+  // mix_diff in rank order (a later member's entry wins), then put_diff: the
+  // others' nodes and edges become the remote part, queries join, and the
+  // indices are rebuilt over local + remote
+  void put_diffs(const std::vector<Value>& parts) override {
+    std::vector<uint64_t> norder, eorder;
+    std::unordered_map<uint64_t, Props> nodes;
+    std::unordered_map<uint64_t, Edge> edges;
+    for (const Value& d : parts) {
+      const Value* nv = d.get("nodes");
+      const Value* ev = d.get("edges");
+      const Value* cv = d.get("cq");
+      const Value* sv = d.get("sq");
+      if (!nv || !ev || !cv || !sv) throw std::runtime_error("mix: malformed graph diff");
+      for (const auto& kv : nv->o) {
+        const uint64_t id = strtoull(kv.first.c_str(), nullptr, 10);
+        if (!nodes.count(id)) norder.push_back(id);
+        nodes[id] = props_of(kv.second);
+      }
+      for (const auto& kv : ev->o) {
+        const uint64_t eid = strtoull(kv.first.c_str(), nullptr, 10);
+        if (!edges.count(eid)) eorder.push_back(eid);
+        edges[eid] = Edge{(uint64_t)kv.second.a.at(0).num(), (uint64_t)kv.second.a.at(1).num(),
+                          props_of(kv.second.a.at(2))};
+      }
+      for (const Value& q : cv->a) cq_.insert(qkey(q));
+      for (const Value& q : sv->a) sq_.insert(qkey(q));
+    }
+    remote_nodes_.clear();
+    remote_order_.clear();
+    for (uint64_t id : norder)
+      if (!nodes_.count(id)) {
+        remote_nodes_[id] = std::move(nodes[id]);
+        remote_order_.push_back(id);
+        global_.insert(id);
+      }
+    remote_edges_.clear();
+    remote_edge_order_.clear();
+    for (uint64_t eid : eorder)
+      if (!edges_.count(eid)) {
+        remote_edges_[eid] = std::move(edges[eid]);
+        remote_edge_order_.push_back(eid);
+      }
+    update_index();
+  }
+
   void status(std::vector<std::pair<std::string, std::string>>* st) override {
     st->emplace_back("local_node_num", std::to_string(nodes_.size()));
     st->emplace_back("global_node_num", std::to_string(global_.size()));
@@ -389,6 +526,61 @@ class Graph : public HostEngine {
     u->str(key);
     u->map(p.size());
     for (const auto& kv : p) { u->str(kv.first); u->str(kv.second); }
+  }
+  static void write_edge(MsgpackWriter* u, uint64_t eid, const Edge& e) {
+    u->str(std::to_string(eid));
+    u->arr(3);
+    u->uint(e.s);
+    u->uint(e.t);
+    u->map(e.p.size());
+    for (const auto& kv : e.p) { u->str(kv.first); u->str(kv.second); }
+  }
+  static void write_queries(MsgpackWriter* u, const char* name, const std::set<QKey>& qs) {
+    u->str(name);
+    u->arr(qs.size());
+    for (const QKey& k : qs) {
+      u->arr(2);
+      for (const Cond* c : {&k.first, &k.second}) {
+        u->arr(c->size());
+        for (const auto& kv : *c) { u->arr(2); u->str(kv.first); u->str(kv.second); }
+      }
+    }
+  }
+
+  bool is_me(const std::pair<std::string, int>& hp) const { return hp.first == eth_ && hp.second == port_; }
+
+  // a server-to-server call (interconnect timeout); throws on any error
+  void peer_call(const std::pair<std::string, int>& hp, const char* method, const std::string& params) {
+    jb::cc::Conn c(hp.first, hp.second, ic_timeout_);
+    const double dl = jb::cc::now_s() + ic_timeout_;
+    const uint32_t mid = c.send_request(method, params, dl);
+    jb::cc::CallResult res;
+    c.recv_response(mid, dl, &res);
+    if (!res.transport_ok) throw std::runtime_error(res.transport_error);
+    if (!res.err.empty()) {
+      const Value e = MsgpackReader((const uint8_t*)res.err.data(), res.err.size()).read();
+      throw std::runtime_error(e.is_str() ? e.s : std::string("remote error"));
+    }
+  }
+
+  // create_node_here on one owner (this server under the model lock, else by RPC)
+  void selective_create(const std::pair<std::string, int>& owner, const std::string& sid) {
+    if (is_me(owner)) {
+      std::unique_lock<std::shared_mutex> g(*mu_);
+      create_node_here(strtoull(sid.c_str(), nullptr, 10), false);
+      return;
+    }
+    MsgpackWriter p;
+    p.arr(2);
+    p.raw(name_);
+    p.raw(sid);
+    peer_call(owner, "create_node_here", p.out);
+  }
+
+  // replica path: the source node is created when missing, no target check
+  void edge_here(uint64_t eid, uint64_t src, uint64_t tgt, Props pr) {
+    if (!nodes_.count(src)) { nodes_[src] = Node{}; node_order_.push_back(src); }
+    put_edge(eid, src, tgt, std::move(pr));
   }
 
   Node& node(uint64_t id) {
@@ -417,14 +609,21 @@ class Graph : public HostEngine {
   }
 
   // nodes of the query (sorted) and its edges in insertion order
+  // (models/graph.py _all: the remote part from the last MIX, then the local
+  // graph over it)
   void subgraph(const QKey& k, std::vector<uint64_t>* ids, std::vector<std::pair<uint64_t, uint64_t>>* es) const {
     std::unordered_set<uint64_t> keep;
     for (const auto& kv : nodes_)
       if (match(kv.second.p, k.second)) { keep.insert(kv.first); ids->push_back(kv.first); }
+    for (const auto& kv : remote_nodes_)
+      if (match(kv.second, k.second)) { keep.insert(kv.first); ids->push_back(kv.first); }
     std::sort(ids->begin(), ids->end());
-    for (uint64_t eid : edge_order_) {
-      const Edge& e = edges_.at(eid);
-      if (keep.count(e.s) && keep.count(e.t) && match(e.p, k.first)) es->emplace_back(e.s, e.t);
+    for (const auto* order : {&remote_edge_order_, &edge_order_}) {
+      const auto& tab = order == &edge_order_ ? edges_ : remote_edges_;
+      for (uint64_t eid : *order) {
+        const Edge& e = tab.at(eid);
+        if (keep.count(e.s) && keep.count(e.t) && match(e.p, k.first)) es->emplace_back(e.s, e.t);
+      }
     }
   }
 
@@ -499,12 +698,21 @@ class Graph : public HostEngine {
   }
 
   GraphParams p_;
+  std::shared_mutex* mu_ = nullptr;          // the server's model lock (self_lock methods)
+  jb::mix::ClusterNode* node_ = nullptr;     // distributed mode
+  std::string eth_, name_;
+  int port_ = 0;
+  double ic_timeout_ = 10;
   uint64_t next_id_ = 0;
   std::unordered_map<uint64_t, Node> nodes_;
   std::vector<uint64_t> node_order_;
   std::unordered_map<uint64_t, Edge> edges_;
   std::vector<uint64_t> edge_order_;
   std::unordered_set<uint64_t> global_;
+  std::unordered_map<uint64_t, Props> remote_nodes_;   // the other members' (last MIX)
+  std::vector<uint64_t> remote_order_;
+  std::unordered_map<uint64_t, Edge> remote_edges_;
+  std::vector<uint64_t> remote_edge_order_;
   std::set<QKey> cq_, sq_;
   std::map<QKey, std::unordered_map<uint64_t, double>> scores_;
   std::map<QKey, std::unordered_map<uint64_t, std::vector<uint64_t>>> sp_;
@@ -524,5 +732,6 @@ int main(int argc, char** argv) {
         std::string why;
         if (!parse_params(text, &p, &why)) throw std::runtime_error(why);
         return std::unique_ptr<HostEngine>(new Graph(p));
-      });
+      },
+      /*native_dist=*/true);
 }

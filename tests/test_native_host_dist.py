@@ -224,3 +224,70 @@ def test_native_burst_distributed_keywords(coord):
             solo.terminate()
             solo.wait(timeout=15)
         cl.close()
+
+
+def test_native_graph_distributed_replicated_writes(coord):
+    """three jubagraph servers: create_node lands on the node's two CHT
+    owners (server-to-server create_node_here), create_edge is replicated to
+    the source's other owner, and after a MIX every server answers
+    centrality and shortest path over the whole graph as one standalone
+    server does (graph_serv.cpp:150-330, models/graph.py MIX)."""
+    from jubatus_amd.common.cht import CHT
+    cfg = json.load(open(os.path.join(ROOT, "config/graph/default.json")))
+    cl = Cluster(coord, "graph", "gdist", cfg, n=3)
+    solo_port = free_port()
+    cfg_path = os.path.join(tempfile.gettempdir(), f"gsolo_{solo_port}.json")
+    json.dump(cfg, open(cfg_path, "w"))
+    solo = subprocess.Popen([os.path.join(NB, "jubagraph"), "-f", cfg_path, "-p", str(solo_port), "-b", "127.0.0.1"],
+                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    dec = lambda x: x.decode() if isinstance(x, bytes) else x
+    try:
+        assert wait_server("127.0.0.1", solo_port, 60)
+        s = Client("127.0.0.1", solo_port, "", timeout=30.0)
+        by_port = dict(zip(cl.ports, cl.c))
+        cht = CHT(cl.ls, "graph", "gdist")
+        ids, sids = [], []
+        for i in range(8):
+            nid = dec(cl.c[i % 3].call("create_node"))
+            ids.append(nid)
+            sids.append(dec(s.call("create_node")))
+            owners = {int(p) for _, p in cht.find(nid, 2)}
+            for p in owners:                      # the node is on each of its owners
+                assert by_port[p].call("get_node", nid) is not None
+        assert len(set(ids)) == len(ids)
+        edges = [(i, (i + 1) % 8) for i in range(8)] + [(0, 4), (2, 6), (5, 1)]
+        for a, b in edges:
+            src_owner = int(cht.find(ids[a], 2)[0][1])   # the proxy routes by the source node
+            eid = by_port[src_owner].call("create_edge", ids[a], [{}, ids[a], ids[b]])
+            s.call("create_edge", sids[a], [{}, sids[a], sids[b]])
+            for _, p in cht.find(ids[a], 2):   # stored on both owners of the source
+                assert by_port[int(p)].call("get_edge", ids[a], eid) is not None
+        q = [[], []]
+        for c in cl.c + [s]:
+            assert c.call("add_centrality_query", q) is True
+            assert c.call("add_shortest_path_query", q) is True
+        with pytest.raises(Exception):
+            cl.c[0].call("update_index")
+        assert s.call("update_index") is True
+        cl.mix()
+        for i in range(8):
+            want = s.call("get_centrality", sids[i], 0, q)
+            for c in cl.c:
+                assert abs(c.call("get_centrality", ids[i], 0, q) - want) < 1e-9
+        want = [sids.index(dec(x)) for x in s.call("get_shortest_path", [sids[0], sids[6], 10, q])]
+        for c in cl.c:
+            got = [ids.index(dec(x)) for x in c.call("get_shortest_path", [ids[0], ids[6], 10, q])]
+            assert got == want, (got, want)
+        # remove_node reaches every member's global node set
+        lone = dec(cl.c[1].call("create_node"))
+        before = [int(status(c)["global_node_num"]) for c in cl.c]
+        owner = int(cht.find(lone, 2)[0][1])
+        assert by_port[owner].call("remove_node", lone) is True
+        after = [int(status(c)["global_node_num"]) for c in cl.c]
+        assert all(a <= b for a, b in zip(after, before)) and after[cl.ports.index(owner)] < before[cl.ports.index(owner)]
+        s.close()
+    finally:
+        if solo.poll() is None:
+            solo.terminate()
+            solo.wait(timeout=15)
+        cl.close()
