@@ -1,6 +1,8 @@
 // The RPC server of the native row engines: jubarecommender,
 // jubanearest_neighbor and jubaanomaly (one binary each, csrc/server/
-// juba{recommender,nearest_neighbor,anomaly}.cpp), no Python in the process.
+// juba{recommender,nearest_neighbor,anomaly}.cpp), and jubaclassifier's
+// nearest-neighbor methods (NN over lsh / euclid_lsh / minhash, cosine,
+// euclidean: models/nn_classifier.py), no Python in the process.
 //
 // Reference: jubatus/server/server/recommender_serv.cpp:126-224,
 // recommender_impl.cpp (RPC table), nearest_neighbor_serv.cpp:121-178,
@@ -16,8 +18,9 @@
 // when members share a device), newest version wins (parallel/row_mix.py's
 // protocol); CHT registration, and anomaly's add over the coordinator's id
 // generator + CHT owners with server-to-server update (anomaly_serv.cpp:
-// 178-211,275-297). Push mixers, other configurations, --cpu and hosts
-// without a GPU go to the Python server (exec before any GPU call).
+// 178-211,275-297), push mixers (pairwise row diffs). Other configurations,
+// --cpu and hosts without a GPU go to the Python server (exec before any GPU
+// call).
 //
 // Concurrency (the reference: nearest_neighbor analysis lock-free,
 // ChangeLog.rst:102, nearest_neighbor_serv.cpp:138-172 NOLOCK; recommender
@@ -31,8 +34,12 @@
 #pragma once
 #include <time.h>
 
+#include <math.h>
+
 #include <atomic>
 #include <condition_variable>
+#include <random>
+#include <set>
 #include <deque>
 #include <exception>
 #include <map>
@@ -41,6 +48,7 @@
 #include <shared_mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "jb_lof_state.hpp"
@@ -63,10 +71,12 @@ using jb::row::RowEngine;
 
 constexpr int kCompleteK = 10;   // models/recommender.py COMPLETE_K
 
-enum class Kind { kRecommender, kNearestNeighbor, kAnomaly };
+enum class Kind { kRecommender, kNearestNeighbor, kAnomaly, kClassifier };
 
 inline const char* kind_name(Kind k) {
-  return k == Kind::kRecommender ? "recommender" : k == Kind::kNearestNeighbor ? "nearest_neighbor" : "anomaly";
+  return k == Kind::kRecommender ? "recommender"
+         : k == Kind::kNearestNeighbor ? "nearest_neighbor"
+         : k == Kind::kAnomaly ? "anomaly" : "classifier";
 }
 
 struct Config {
@@ -78,7 +88,16 @@ struct Config {
   // anomaly (models/anomaly.py LOF)
   int k = 10, rnn = 30;
   bool ignore_kth_same = false;
+  // classifier (models/nn_classifier.py): k nearest rows, label score
+  // sum exp(-alpha d) (NN, euclidean) or summed similarity (cosine)
+  int nn_k = 128;
+  double alpha = 1.0;
+  bool similar = false;
 };
+
+inline bool is_nn_classifier(const std::string& m) {
+  return m == "NN" || m == "nearest_neighbor" || m == "cosine" || m == "euclidean";
+}
 
 inline bool is_lsh(const std::string& m) { return m == "lsh" || m == "euclid_lsh" || m == "minhash"; }
 
@@ -101,6 +120,30 @@ inline bool parse_config(Kind kind, const std::string& text, Config* c, std::str
   c->inner = c->outer;
   if (kind == Kind::kNearestNeighbor) {
     if (!is_lsh(c->outer)) { *why = "nearest_neighbor method " + c->outer; return false; }
+  } else if (kind == Kind::kClassifier) {
+    if (!is_nn_classifier(c->outer)) { *why = "classifier method " + c->outer + " is not a nearest-neighbor one"; return false; }
+    auto num = [&](const char* key, double d) {
+      const Value* x = c->param.get(key);
+      return x && x->is_num() ? x->num() : d;
+    };
+    c->nn_k = (int)num("nearest_neighbor_num", 128);
+    c->alpha = num("local_sensitivity", 1.0);
+    if (c->nn_k <= 0 || c->alpha < 0) { *why = "nearest_neighbor_num must be positive, local_sensitivity >= 0"; return false; }
+    Value inner = empty;
+    if (c->outer == "cosine") {
+      c->inner = "inverted_index";
+      c->similar = true;
+    } else if (c->outer == "euclidean") {
+      c->inner = "inverted_index_euclid";
+    } else {
+      c->inner = c->param.str_or("method", "lsh");
+      if (!is_lsh(c->inner)) { *why = "unknown nearest neighbor method: " + c->inner; return false; }
+      if (const Value* ip = c->param.get("parameter"))
+        if (ip->kind == Value::MAP) inner = *ip;
+    }
+    for (const char* key : {"unlearner", "unlearner_parameter"})
+      if (const Value* x = c->param.get(key)) inner.o.emplace_back(key, *x);
+    c->param = inner;
   } else if (kind == Kind::kAnomaly) {
     // lof: any recommender backend; light_lof: the nearest_neighbor (LSH) ones
     if (c->outer != "lof" && c->outer != "light_lof") { *why = "anomaly method " + c->outer; return false; }
@@ -185,13 +228,12 @@ class Model : public jb::mix::Mixable {
   uint64_t mix(jb::mix::Group& g) override {
     std::unique_lock<std::shared_mutex> lk(mu_);
     MsgpackWriter w;
-    eng_->pack_diff(w);
+    pack_mix(w);
     const auto raw = g.plane().allgather_bytes(g.star(), w.out, g.deadline());
     std::vector<Value> parts;
     parts.reserve(raw.size());
     for (const auto& r : raw) parts.push_back(MsgpackReader((const uint8_t*)r.data(), r.size()).read());
-    std::vector<int32_t> changed;
-    const size_t n = eng_->apply_diffs(parts, &changed);
+    const size_t n = apply_mix(parts, false);
     // LOF: the neighbour lists are caches of the row set; rows written by the
     // MIX invalidate them (rebuilt on demand against the mixed rows)
     if (kind_ == Kind::kAnomaly && n > 0) lof_.reset();
@@ -207,7 +249,7 @@ class Model : public jb::mix::Mixable {
     std::string mine;
     if (peer >= 0) {
       MsgpackWriter w;
-      eng_->pack_diff(w);
+      pack_mix(w);
       mine = std::move(w.out);
     }
     const std::string theirs = g.plane().exchange_bytes(g.star(), peer, mine, g.deadline());
@@ -217,8 +259,7 @@ class Model : public jb::mix::Mixable {
     std::vector<Value> parts;
     if (g.rank() < peer) { parts.push_back(std::move(a)); parts.push_back(std::move(b)); }
     else { parts.push_back(std::move(b)); parts.push_back(std::move(a)); }
-    std::vector<int32_t> changed;
-    const size_t n = eng_->apply_diffs(parts, &changed, /*forward=*/true);
+    const size_t n = apply_mix(parts, true);
     if (kind_ == Kind::kAnomaly && n > 0) lof_.reset();
     HIPCHK(hipStreamSynchronize(stream_));
     last_mix_rows_ = n;
@@ -263,6 +304,100 @@ class Model : public jb::mix::Mixable {
     cfg_ = cfg;
     if (kind_ == Kind::kAnomaly)   // LOF._remove: a removed row's dependants go stale
       eng_->on_remove = [this](int32_t s) { if (lof_) lof_->moved({s}); };
+    if (kind_ == Kind::kClassifier) {   // an evicted / removed row loses its label (NNClassifier._gc)
+      eng_->on_remove = [this](int32_t s) { row_label_.erase(eng_->at(s).id); };
+      row_label_.clear();
+      labels_.clear();
+      label_order_.clear();
+      seq_ = 0;
+      if (prefix_.empty()) {
+        std::random_device rd;
+        char b[16];
+        snprintf(b, sizeof b, "%08x", (unsigned)rd());
+        prefix_ = b;
+      }
+    }
+  }
+
+  // ------------------------------------------------------------ classifier
+  // models/nn_classifier.py train: each example a row "<prefix>-<seq>"
+  // tagged with its label
+  int64_t nn_train(const Value& data) {
+    std::vector<std::pair<std::string, Datum>> ex;
+    for (const Value& x : data.a) {
+      if (x.kind != Value::ARR || x.a.size() != 2 || !x.a[0].is_str()) throw ArgError("labeled_datum expected");
+      Datum d;
+      jb::row::parse_datum(x.a[1], &d);
+      ex.emplace_back(x.a[0].s, std::move(d));
+    }
+    std::unique_lock<std::shared_mutex> g(mu_);
+    ++update_count;
+    for (auto& e : ex) {
+      const std::string rid = prefix_ + "-" + std::to_string(seq_++);
+      eng_->set(rid, std::move(e.second));
+      if (eng_->slot(rid) >= 0) row_label_[rid] = e.first;
+      add_label(e.first, 1);
+    }
+    return (int64_t)ex.size();
+  }
+  // every known label, scored over the query's k nearest rows
+  std::vector<std::vector<std::pair<std::string, double>>> nn_classify(const Value& data) {
+    const size_t n = data.a.size();
+    std::vector<QReq> rs(n);
+    for (size_t i = 0; i < n; ++i) {
+      Datum chk;
+      jb::row::parse_datum(data.a[i], &chk);
+      MsgpackWriter w;
+      write_value(w, data.a[i]);
+      rs[i].kind = QReq::kDatum;
+      rs[i].datum = std::move(w.out);
+      rs[i].k = cfg_.nn_k;
+      rs[i].similar = cfg_.similar;
+    }
+    std::vector<QReq*> ps;
+    for (auto& r : rs) ps.push_back(&r);
+    submit_many(ps);
+    std::shared_lock<std::shared_mutex> g(mu_);
+    std::vector<std::vector<std::pair<std::string, double>>> out(n);
+    for (size_t i = 0; i < n; ++i) {
+      std::unordered_map<std::string, double> sc;
+      for (const auto& lab : label_order_) sc[lab] = 0.0;
+      std::vector<std::string> extra;
+      for (const auto& hv : rs[i].res) {
+        auto it = row_label_.find(hv.first);
+        if (it == row_label_.end()) continue;
+        if (!sc.count(it->second)) extra.push_back(it->second);
+        sc[it->second] += cfg_.similar ? hv.second : exp(-cfg_.alpha * hv.second);
+      }
+      for (const auto& lab : label_order_) out[i].emplace_back(lab, sc[lab]);
+      for (const auto& lab : extra) out[i].emplace_back(lab, sc[lab]);
+    }
+    return out;
+  }
+  std::vector<std::pair<std::string, uint64_t>> nn_labels() {
+    std::shared_lock<std::shared_mutex> g(mu_);
+    std::vector<std::pair<std::string, uint64_t>> out;
+    for (const auto& lab : label_order_) out.emplace_back(lab, labels_.at(lab));
+    return out;
+  }
+  bool nn_set_label(const std::string& lab) {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    ++update_count;
+    if (labels_.count(lab)) return false;
+    add_label(lab, 0);
+    return true;
+  }
+  bool nn_delete_label(const std::string& lab) {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    ++update_count;
+    if (!labels_.count(lab)) return false;
+    std::vector<std::string> drop;
+    for (const auto& kv : row_label_)
+      if (kv.second == lab) drop.push_back(kv.first);
+    for (const auto& rid : drop) eng_->remove(rid);   // on_remove drops the tag
+    labels_.erase(lab);
+    label_order_.erase(std::find(label_order_.begin(), label_order_.end(), lab));
+    return true;
   }
   const std::string& config_text() const { return cfg_.text; }
 
@@ -306,6 +441,10 @@ class Model : public jb::mix::Mixable {
     eng_->clear();
     lof_.reset();
     next_id_ = 0;
+    row_label_.clear();
+    labels_.clear();
+    label_order_.clear();
+    seq_ = 0;
   }
 
   // ------------------------------------------------------------- anomaly
@@ -433,12 +572,40 @@ class Model : public jb::mix::Mixable {
     MsgpackWriter u;
     u.arr(2);
     u.uint(1);
+    if (kind_ == Kind::kClassifier) {   // NNClassifier.pack()
+      u.map(5);
+      u.str("method"); u.str(cfg_.outer);
+      u.str("engine"); eng_->pack(u, eng_->method());
+      u.str("row_label"); u.map(row_label_.size());
+      for (const auto& kv : row_label_) { u.str(kv.first); u.str(kv.second); }
+      u.str("labels"); u.map(label_order_.size());
+      for (const auto& lab : label_order_) { u.str(lab); u.uint(labels_.at(lab)); }
+      u.str("seq"); u.uint(seq_);
+      return std::move(u.out);
+    }
     eng_->pack(u, eng_->method());
     return std::move(u.out);
   }
   void unpack(const Value& obj) {
     std::unique_lock<std::shared_mutex> g(mu_);
     lof_.reset();                  // LOF.unpack: lists rebuilt on demand
+    if (kind_ == Kind::kClassifier) {
+      const Value* ev = obj.get("engine");
+      const Value* rl = obj.get("row_label");
+      const Value* lv = obj.get("labels");
+      const Value* sq = obj.get("seq");
+      if (!ev || !rl || rl->kind != Value::MAP || !lv || lv->kind != Value::MAP)
+        throw std::runtime_error("broken model data: nn classifier");
+      eng_->unpack(*ev);
+      row_label_.clear();
+      for (const auto& kv : rl->o) row_label_[kv.first] = kv.second.s;
+      labels_.clear();
+      label_order_.clear();
+      for (const auto& kv : lv->o) add_label(kv.first, (uint64_t)kv.second.num());
+      seq_ = sq && sq->is_num() ? (uint64_t)sq->num() : 0;
+      HIPCHK(hipStreamSynchronize(stream_));
+      return;
+    }
     eng_->unpack(obj);
     lof_.reset();
     HIPCHK(hipStreamSynchronize(stream_));
@@ -458,6 +625,14 @@ class Model : public jb::mix::Mixable {
     std::shared_lock<std::shared_mutex> g(mu_);
     auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
     add("method", kind_ == Kind::kNearestNeighbor ? eng_->method() : cfg_.outer);
+    if (kind_ == Kind::kClassifier) {
+      add("num_labels", std::to_string(labels_.size()));
+      add("nearest_neighbor_num", std::to_string(cfg_.nn_k));
+      char b[40];
+      snprintf(b, sizeof b, "%.17g", cfg_.alpha);
+      add("local_sensitivity", b);
+      add("nn.method", eng_->method());
+    }
     if (kind_ == Kind::kAnomaly) add("backend", eng_->method());
     add("num_rows", std::to_string(eng_->size()));
     add("storage", "hbm");
@@ -476,6 +651,66 @@ class Model : public jb::mix::Mixable {
 
  private:
   int clamp_k(int64_t k) const { return (int)std::min<int64_t>(k, 1 << 30); }
+
+  void add_label(const std::string& lab, uint64_t n) {   // mu_ held
+    auto it = labels_.find(lab);
+    if (it == labels_.end()) {
+      labels_[lab] = n;
+      label_order_.push_back(lab);
+    } else {
+      it->second += n;
+    }
+  }
+
+  // the MIX payload: the row diff (jb_row_mix.hpp); the classifier adds the
+  // labels of the rows in it and its label counts (NNClassifier.get_diff)
+  void pack_mix(MsgpackWriter& w) {
+    if (kind_ != Kind::kClassifier) {
+      eng_->pack_diff(w);
+      return;
+    }
+    w.arr(3);
+    eng_->pack_diff(w);
+    const std::vector<std::string> ids = eng_->mix_ids();
+    size_t nt = 0;
+    for (const auto& id : ids) nt += row_label_.count(id);
+    w.map(nt);
+    for (const auto& id : ids) {
+      auto it = row_label_.find(id);
+      if (it != row_label_.end()) { w.str(id); w.str(it->second); }
+    }
+    w.map(label_order_.size());
+    for (const auto& lab : label_order_) { w.str(lab); w.uint(labels_.at(lab)); }
+  }
+  // mix_diff folded in rank order + put_diff; -> rows applied
+  size_t apply_mix(const std::vector<Value>& parts, bool forward) {
+    std::vector<int32_t> changed;
+    if (kind_ != Kind::kClassifier) return eng_->apply_diffs(parts, &changed, forward);
+    std::vector<Value> rows;
+    std::vector<std::pair<std::string, std::string>> tags;
+    std::vector<std::string> lorder;
+    std::set<std::string> lseen;
+    for (const Value& p : parts) {
+      if (p.kind != Value::ARR || p.a.size() != 3 || p.a[1].kind != Value::MAP || p.a[2].kind != Value::MAP)
+        throw std::runtime_error("mix: malformed nn classifier diff");
+      rows.push_back(p.a[0]);
+      for (const auto& kv : p.a[1].o) tags.emplace_back(kv.first, kv.second.s);
+      for (const auto& kv : p.a[2].o)
+        if (lseen.insert(kv.first).second) lorder.push_back(kv.first);
+    }
+    const size_t n = eng_->apply_diffs(rows, &changed, forward);
+    for (const auto& t : tags)
+      if (eng_->slot(t.first) >= 0) row_label_[t.first] = t.second;
+    // counts: the labels of the rows held now (put_diff), every label known
+    std::vector<std::string> order = lorder;
+    for (const auto& lab : label_order_)
+      if (!lseen.count(lab)) order.push_back(lab);
+    labels_.clear();
+    label_order_.clear();
+    for (const auto& lab : order) add_label(lab, 0);
+    for (const auto& kv : row_label_) add_label(kv.second, 1);
+    return n;
+  }
 
   void fv_of(const Value& dv, std::vector<int32_t>* idx, std::vector<float>* val) {
     Datum chk;
@@ -553,6 +788,20 @@ class Model : public jb::mix::Mixable {
     qcv_.notify_one();
     dcv_.wait(lk, [&] { return r->done; });
     if (r->err) std::rethrow_exception(r->err);
+  }
+  // several queries of one call: queued together, so they share a pass
+  void submit_many(const std::vector<QReq*>& rs) {
+    if (rs.empty()) return;
+    std::unique_lock<std::mutex> lk(qmu_);
+    for (QReq* r : rs) q_.push_back(r);
+    qcv_.notify_one();
+    dcv_.wait(lk, [&] {
+      for (QReq* r : rs)
+        if (!r->done) return false;
+      return true;
+    });
+    for (QReq* r : rs)
+      if (r->err) std::rethrow_exception(r->err);
   }
 
   void batch_loop() {
@@ -706,6 +955,12 @@ class Model : public jb::mix::Mixable {
   std::unique_ptr<RowEngine> eng_;
   std::unique_ptr<jb::row::LofState> lof_;
   int64_t next_id_ = 0;
+  // classifier: row -> label, label counts in first-seen order, row sequence
+  std::unordered_map<std::string, std::string> row_label_;
+  std::unordered_map<std::string, uint64_t> labels_;
+  std::vector<std::string> label_order_;
+  uint64_t seq_ = 0;
+  std::string prefix_;
 };
 
 inline void write_pairs(MsgpackWriter& w, const std::vector<std::pair<std::string, double>>& r) {
@@ -807,7 +1062,13 @@ class Server {
         {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
         {"clear_row", "s"}, {"add", "d"}, {"update", "sd"}, {"overwrite", "sd"}, {"calc_score", "d"},
         {"get_all_rows", ""}, {"do_mix", ""}};
-    const auto& table = kind_ == Kind::kRecommender ? rec : kind_ == Kind::kNearestNeighbor ? nn : an;
+    static const std::vector<std::pair<std::string, std::string>> cl = {
+        {"get_config", ""}, {"save", "s"}, {"load", "s"}, {"get_status", ""}, {"clear", ""},
+        {"train", "l"}, {"classify", "l"}, {"get_labels", ""}, {"set_label", "s"}, {"delete_label", "s"},
+        {"do_mix", ""}};
+    const auto& table = kind_ == Kind::kRecommender ? rec
+                        : kind_ == Kind::kNearestNeighbor ? nn
+                        : kind_ == Kind::kAnomaly ? an : cl;
     const std::string* sig = nullptr;
     for (const auto& x : table)
       if (x.first == m) sig = &x.second;
@@ -816,7 +1077,7 @@ class Server {
     for (size_t k = 0; ok && k < sig->size(); ++k) {
       const Value& x = args.a[k + 1];
       const char c = (*sig)[k];
-      ok = c == 's' ? x.is_str() : c == 'k' ? (x.kind == Value::INT || x.kind == Value::UINT) : x.kind == Value::ARR;
+      ok = c == 's' ? x.is_str() : c == 'k' ? (x.kind == Value::INT || x.kind == Value::UINT) : x.kind == Value::ARR;   // d, l: arrays
     }
     if (!ok) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
     auto size_arg = [&](size_t i) -> int64_t {
@@ -826,7 +1087,7 @@ class Server {
     MsgpackWriter w;
     // update calls drive the MIX trigger (event_model_updated)
     static const char* const kUpdates[] = {"clear", "clear_row", "update_row", "set_row", "add", "update",
-                                           "overwrite", "load"};
+                                           "overwrite", "load", "train", "set_label", "delete_label"};
     if (mixer_)
       for (const char* u : kUpdates)
         if (m == u && !(m == "add" && node_)) { mixer_->updated(1); break; }
@@ -867,6 +1128,20 @@ class Server {
         jb::row::write_datum(w, model_->complete_row_from_datum(args.a[1]));
       } else if (m == "decode_row") {
         jb::row::write_datum(w, model_->decode_row(args.a[1].s));
+      } else if (m == "train") {
+        w.sint(model_->nn_train(args.a[1]));
+      } else if (m == "classify") {
+        const auto res = model_->nn_classify(args.a[1]);
+        w.arr(res.size());
+        for (const auto& r : res) write_pairs(w, r);
+      } else if (m == "get_labels") {
+        const auto ls = model_->nn_labels();
+        w.map(ls.size());
+        for (const auto& kv : ls) { w.raw(kv.first); w.uint(kv.second); }
+      } else if (m == "set_label") {
+        w.boolean(model_->nn_set_label(args.a[1].s));
+      } else if (m == "delete_label") {
+        w.boolean(model_->nn_delete_label(args.a[1].s));
       } else if (m == "get_all_rows") {
         const auto ids = model_->get_all_rows();
         w.arr(ids.size());
@@ -1003,16 +1278,8 @@ class Server {
   CommonStatus cs_;
 };
 
-inline int row_main(int argc, char** argv, Kind kind) {
-  set_engine(kind_name(kind));
-  Args a;
-  std::string text;
-  Config cfg;
-  const int rc = startup(argc, argv, &a, &text, [&cfg, kind](const std::string& t, std::string* why) {
-    return parse_config(kind, t, &cfg, why);
-  }, true, /*native_dist=*/true, /*native_push=*/true);
-  if (rc >= 0) return rc;
-  // below this line the process owns the GPU: no exec
+// after startup(): serve (the process owns the GPU from here: no exec)
+inline int row_serve(Kind kind, Args& a, const Config& cfg) {
   try {
     const int device = device_and_signals(a);
     logf_("INFO", "starting %s %s RPC server at %s:%d (native, device %d)", prog_name(), kVersion,
@@ -1027,6 +1294,18 @@ inline int row_main(int argc, char** argv, Kind kind) {
     logf_("FATAL", "failed to start %s: %s", engine_name(), e.what());
     return 1;
   }
+}
+
+inline int row_main(int argc, char** argv, Kind kind) {
+  set_engine(kind_name(kind));
+  Args a;
+  std::string text;
+  Config cfg;
+  const int rc = startup(argc, argv, &a, &text, [&cfg, kind](const std::string& t, std::string* why) {
+    return parse_config(kind, t, &cfg, why);
+  }, true, /*native_dist=*/true, /*native_push=*/true);
+  if (rc >= 0) return rc;
+  return row_serve(kind, a, cfg);
 }
 
 }  // namespace rowsrv

@@ -9,9 +9,11 @@
 // standalone or distributed (linear and push mixers over the native MIX
 // plane, csrc/native/jb_mix_group.hpp), with converters on the fixed-slot GPU
 // path (fv_converter/gpu_path.py fast_eligible) or the host wide rule set
-// (bigram / combination / idf, jb_linear_conv.hpp). The NN methods, --cpu
+// (bigram / combination / idf, jb_linear_conv.hpp). --cpu
 // and a host without /dev/kfd are handed to the Python server
-// (jubatus_amd.cmd.server) by exec BEFORE anything touches the GPU.
+// (jubatus_amd.cmd.server) by exec BEFORE anything touches the GPU. The
+// nearest-neighbor methods (NN, cosine, euclidean) run on the native row
+// server (jb_row_server.hpp Kind::kClassifier: rows in HBM, batched k-NN).
 //
 // Data path (the same kernels as the Python server, csrc/hip):
 //   train    the transport copies request bodies into pinned arena slots
@@ -48,6 +50,7 @@
 #include "jb_hostfv.hpp"
 #include "jb_linear_conv.hpp"
 #include "jb_mix_device.hpp"
+#include "jb_row_server.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_pack.hpp"
 #include "jb_rpc.hpp"
@@ -1669,10 +1672,21 @@ int main(int argc, char** argv) {
   Args a;
   std::string text;
   Config cfg;
-  const int rc = startup(argc, argv, &a, &text, [&cfg](const std::string& t, std::string* why) {
-    return parse_config(t, &cfg, why);
+  jb::rowsrv::Config ncfg;   // NN / cosine / euclidean: the row server (jb_row_server.hpp)
+  bool nn = false;
+  const int rc = startup(argc, argv, &a, &text, [&](const std::string& t, std::string* why) {
+    std::string wn;
+    if (jb::rowsrv::parse_config(jb::rowsrv::Kind::kClassifier, t, &ncfg, &wn)) {
+      nn = true;
+      return true;
+    }
+    nn = false;
+    if (parse_config(t, &cfg, why)) return true;
+    if (jb::rowsrv::is_nn_classifier(ncfg.outer)) *why = wn;
+    return false;
   }, true, /*native_dist=*/true, /*native_push=*/true);
   if (rc >= 0) return rc;
+  if (nn) return jb::rowsrv::row_serve(jb::rowsrv::Kind::kClassifier, a, ncfg);
   // below this line the process owns the GPU: no exec
   try {
     const int device = device_and_signals(a);

@@ -15,10 +15,11 @@ from jubatus_amd.common.mprpc import RpcClient, RpcIOError, RpcTimeoutError
 BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaclassifier")
 REG_BIN = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaregression")
 
-NATIVE = ["arow.json", "cw.json", "nherd.json", "pa.json", "pa1.json", "pa2.json", "perceptron.json"]
-PYTHON = {"arow_combinational_feature.json": "combination_rules", "cosine.json": "not a linear method",
-          "default.json": "string type", "nn.json": "not a linear method",
-          "euclidean.json": "not a linear method"}
+# every reference classifier config: linear methods on the fixed-slot GPU
+# hasher or the host wide rule set (bigram, combinations, idf), the
+# nearest-neighbor methods on the native row server
+NATIVE = ["arow.json", "cw.json", "nherd.json", "pa.json", "pa1.json", "pa2.json", "perceptron.json",
+          "arow_combinational_feature.json", "default.json", "cosine.json", "nn.json", "euclidean.json"]
 
 
 def _check(cfg_file, binary=BIN):
@@ -33,18 +34,20 @@ def test_linear_configs_are_native(name):
     assert _check(config_path(f"classifier/{name}")) == "native"
 
 
-@pytest.mark.parametrize("name,why", sorted(PYTHON.items()))
-def test_other_configs_go_to_python(name, why):
-    out = _check(config_path(f"classifier/{name}"))
-    assert out.startswith("python: ") and why in out, out
+def test_unknown_methods_go_to_python(tmp_path):
+    import json
+    p = tmp_path / "c.json"
+    p.write_text(json.dumps({"method": "SVM", "converter": {}, "parameter": {}}))
+    out = _check(str(p))
+    assert out.startswith("python: "), out
+    p.write_text(json.dumps({"method": "NN", "converter": {},
+                             "parameter": {"method": "bogus", "nearest_neighbor_num": 4}}))
+    assert "unknown nearest neighbor method" in _check(str(p))
 
 
 @pytest.mark.parametrize("cfg,why", [
     ({"method": "AROW", "converter": {"num_rules": [{"key": "/x.*/", "type": "num"}]},
       "parameter": {"regularization_weight": 1.0}}, "regex"),
-    ({"method": "AROW", "converter": {"string_rules": [
-        {"key": "*", "type": "str", "sample_weight": "tf", "global_weight": "idf"}]},
-      "parameter": {"regularization_weight": 1.0}}, "global_weight idf"),
     ({"method": "CW", "converter": {}, "parameter": {}}, "regularization_weight"),
     ({"method": "PA", "converter": {"string_rules": [{"key": "*", "type": "str"}],
                                     "num_types": {"num": {"method": "add", "value": 1}},
@@ -58,8 +61,8 @@ def test_config_details(tmp_path, cfg, why):
     assert why in out, out
 
 
-@pytest.mark.parametrize("name,want", [("pa.json", "native"), ("default.json", "python: string type"),
-                                       ("pa_combinational_feature.json", "python: combination_rules")])
+@pytest.mark.parametrize("name,want", [("pa.json", "native"), ("default.json", "native"),
+                                       ("pa_combinational_feature.json", "native")])
 def test_regression_configs(name, want):
     assert _check(config_path(f"regression/{name}"), REG_BIN).startswith(want)
 

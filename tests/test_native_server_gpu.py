@@ -356,3 +356,58 @@ def test_native_wide_converter_configs_match_oracle(cfg_name, tmp_path):
             p.wait(timeout=30)
         except subprocess.TimeoutExpired:
             p.kill()
+
+
+@pytest.mark.parametrize("cfg_name", ["classifier/cosine.json", "classifier/euclidean.json", "classifier/nn.json"])
+def test_native_nn_classifier_matches_python_driver(cfg_name, tmp_path):
+    """the nearest-neighbor classifier methods run natively on the row
+    server (jb_row_server.hpp Kind::kClassifier: rows in HBM, batched k-NN
+    scans): labels, scores and model files agree with the Python driver
+    (models/nn_classifier.py over the same GPU row kernels)"""
+    import torch
+    from jubatus_amd.framework import save_load
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.models.nn_classifier import NNClassifier
+    cfg_file = config_path(cfg_name)
+    cfg = json.load(open(cfg_file))
+    port, p = _start(cfg_file, tmp_path)
+    try:
+        c = Classifier("127.0.0.1", port, "", timeout=60)
+        ora = NNClassifier(cfg["method"], cfg.get("parameter"), DatumToFvConverter(cfg["converter"]),
+                           device=torch.device("cuda", 0))
+        rng = random.Random(21)
+        for _ in range(3):
+            chunk = _data(rng, 40)
+            assert c.train(chunk) == 40
+            ora.train([(l, d) for l, d in chunk])
+        assert c.set_label("spare") is True and ora.set_label("spare") is True
+        test = [d for _, d in _data(random.Random(5), 12)]
+        got = _scores(c.classify(test))
+        want = [dict(r) for r in ora.classify(test)]
+        for g, w in zip(got, want):
+            assert set(g) == set(w), (g, w)
+            for k in w:
+                assert abs(g[k] - w[k]) <= 1e-4 * max(1.0, abs(w[k])), (k, g[k], w[k])
+        labels = {(k.decode() if isinstance(k, bytes) else k): v for k, v in c.get_labels().items()}
+        assert labels == ora.get_labels()
+        _, st = _status(c)
+        assert st["server_runtime"] == "native" and st["method"] == cfg["method"]
+        # the model file loads into the Python driver and answers the same
+        (_, path), = c.save("nn").items()
+        with open(path, "rb") as f:
+            _, pack = save_load.load_server(f, "classifier", open(cfg_file).read(), 1, False)
+        ora2 = NNClassifier(cfg["method"], cfg.get("parameter"), DatumToFvConverter(cfg["converter"]),
+                            device=torch.device("cuda", 0))
+        ora2.unpack(pack)
+        for g, w in zip(got, [dict(r) for r in ora2.classify(test)]):
+            for k in w:
+                assert abs(g[k] - w[k]) <= 1e-4 * max(1.0, abs(w[k])), (k, g[k], w[k])
+        assert c.delete_label("L0") is True
+        assert "L0" not in {(k.decode() if isinstance(k, bytes) else k) for k in c.get_labels()}
+        c.close()
+    finally:
+        p.terminate()
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
