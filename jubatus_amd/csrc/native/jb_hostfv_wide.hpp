@@ -75,6 +75,10 @@ class HostFvWide {
     df_ = df; diff_ = diff; counts_ = counts;
   }
   bool needs_weights() const { return global_; }
+  // the table height of the document statistics when it differs from the
+  // feature index's (clustering keys features over 2^31 - 1 while the
+  // weight manager counts them in the converter's hash_max_size rows)
+  void set_df_height(uint64_t H) { Hdf_ = H; }
 
   // Optional sinks of hash_body: the name of every emitted slot (appended to
   // *names, end offsets in *name_end) and the byte span of every datum in the
@@ -274,7 +278,7 @@ class HostFvWide {
   void weigh(bool update) {
     gidx_.clear();
     for (const auto& f : feats_)
-      if (f.gw != kGwBin) gidx_.push_back(f.idx);
+      if (f.gw != kGwBin) gidx_.push_back(dfi(f));
     const int64_t dl = (int64_t)gidx_.size();
     if (update) {
       counts_[0] += 1; counts_[2] += 1;
@@ -292,7 +296,7 @@ class HostFvWide {
     const double avg = nd ? (double)counts_[1] / (double)nd : 1.0;
     for (auto& f : feats_) {
       if (f.gw == kGwBin) continue;
-      const int64_t df = df_[f.idx];
+      const int64_t df = df_[dfi(f)];
       const double idf = (df > 0 && nd > 0) ? log((double)nd / (double)df) : 0.0;
       if (f.gw == kGwIdf) {
         f.w *= idf;
@@ -302,6 +306,8 @@ class HostFvWide {
       }
     }
   }
+
+  int32_t dfi(const WideFeat& f) const { return Hdf_ ? (int32_t)hash_to_index(f.h, Hdf_) : f.idx; }
 
   void put_name(const WideName& nm, bool end = true) {
     for (int i = 0; i < nm.k; ++i) names_->append((const char*)nm.p[i], nm.n[i]);
@@ -317,6 +323,7 @@ class HostFvWide {
   std::vector<HostRule> s_, n_, c_;
   std::vector<uint8_t> blob_;
   uint64_t H_;
+  uint64_t Hdf_ = 0;     // 0: the document statistics use H_
   bool global_ = false;
   int64_t *df_ = nullptr, *diff_ = nullptr, *counts_ = nullptr;
   std::vector<WideFeat> feats_;

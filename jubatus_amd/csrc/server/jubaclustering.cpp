@@ -13,8 +13,10 @@
 // launches. The random stream is CPython's (csrc/native/jb_pyrandom.hpp), so
 // the native and the Python server draw the same seeds. Model files are
 // shared with the Python server (Clustering.pack(): pending / buckets /
-// others as [weight, {feature: value}, datum]). Converters outside the wide
-// converter, or with idf / bm25 global weights, go to the Python server.
+// others as [weight, {feature: value}, datum]). idf / bm25 global weights
+// count documents in the converter's hash_max_size rows (DocStats, MIXed
+// with the coresets and kept in the model file under "weights"); converters
+// outside the wide rule set go to the Python server.
 #include <hip/hip_runtime_api.h>
 #include <math.h>
 #include <string.h>
@@ -28,6 +30,7 @@
 #include <vector>
 
 #include "jb_host_server.hpp"
+#include "jb_linear_conv.hpp"
 #include "jb_mix_device.hpp"
 #include "jb_msgpack.hpp"
 #include "jb_pyrandom.hpp"
@@ -104,7 +107,6 @@ bool check_config(const std::string& text, std::string* why, Params* out) {
   empty.kind = Value::MAP;
   if (!jb::row::build_wide_rules(conv ? *conv : empty, &p.s, &p.n, &p.c, &p.blob, &p.H, &p.global, why))
     return false;
-  if (p.global) { *why = "idf / bm25 global weights need the Python converter"; return false; }
   if (out) *out = std::move(p);
   return true;
 }
@@ -183,6 +185,11 @@ class Clustering : public HostEngine {
     hw_.reset(new jb::HostFvWide((const uint8_t*)p_.s.data(), (int)p_.s.size(), (const uint8_t*)p_.n.data(),
                                  (int)p_.n.size(), (const uint8_t*)p_.c.data(), (int)p_.c.size() / 2,
                                  (const uint8_t*)p_.blob.data(), p_.blob.size(), kKeySpace));
+    if (p_.global) {   // document statistics over the converter's table height
+      stats_.reset(p_.H);
+      stats_.attach(hw_.get());
+      hw_->set_df_height(p_.H);
+    }
     HIPCHK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&mix_st_, hipStreamNonBlocking));
     HIPCHK(hipGetDevice(&device_));
@@ -209,18 +216,22 @@ class Clustering : public HostEngine {
     PointSet all;
     for (const auto& b : buckets_) all.append(b);
     MsgpackWriter u;
-    u.arr(3);
+    u.arr(4);
     u.str(token_);
     wire(u, all);
     u.uint(revision_);
+    if (p_.global) u.out += stats_.get_diff();   // the weight manager's diff (encoded)
+    else u.nil();
     return std::move(u.out);
   }
   void put_diffs(const std::vector<Value>& parts) override {
     PointSet before, after, others;
     bool mine = false;
     uint64_t rev = revision_;
+    std::vector<Value> wd;
     for (const Value& d : parts) {
-      if (d.kind != Value::ARR || d.a.size() != 3) throw std::runtime_error("mix: malformed clustering diff");
+      if (d.kind != Value::ARR || d.a.size() < 3) throw std::runtime_error("mix: malformed clustering diff");
+      if (d.a.size() > 3 && d.a[3].kind == Value::ARR) wd.push_back(d.a[3]);
       rev = std::max<uint64_t>(rev, (uint64_t)d.a[2].num());
       if (d.a[0].s == token_) { mine = true; continue; }
       PointSet ps = unwire(d.a[1]);
@@ -229,6 +240,7 @@ class Clustering : public HostEngine {
     }
     others_ = std::move(others);
     revision_ = rev;
+    if (p_.global && !wd.empty()) stats_.put_diffs(wd);
     if (!buckets_.empty() || others_.size()) recluster(&before, &after);
   }
 
@@ -264,6 +276,7 @@ class Clustering : public HostEngine {
     dim_keys_.clear();
     assign_.clear();
     rng_ = jb::PyRandom(p_.seed);
+    stats_.clear();
   }
 
   // ---------------------------------------------------------- persist
@@ -271,13 +284,14 @@ class Clustering : public HostEngine {
     MsgpackWriter u;
     u.arr(2);
     u.uint(1);
-    u.map(5);
+    u.map(p_.global ? 6 : 5);
     u.str("method"); u.str(p_.method);
     u.str("revision"); u.uint(revision_);
     u.str("pending"); wire(u, pending_);
     u.str("buckets"); u.arr(buckets_.size());
     for (const auto& b : buckets_) wire(u, b);
     u.str("others"); wire(u, others_);
+    if (p_.global) { u.str("weights"); stats_.pack(u); }
     return std::move(u.out);
   }
 
@@ -291,6 +305,7 @@ class Clustering : public HostEngine {
     pending_ = unwire(*pv);
     for (const Value& b : bv->a) buckets_.push_back(unwire(b));
     others_ = unwire(*ov);
+    if (p_.global) stats_.unpack(obj.get("weights"));
     const uint64_t rev = (uint64_t)rv->num();
     if (!buckets_.empty() || others_.size()) recluster();
     revision_ = rev;
@@ -326,9 +341,11 @@ class Clustering : public HostEngine {
       spans.clear();
       rp_[0] = 0;
       hw_->set_sinks(&names, &name_end, &spans);
+      if (p_.global) hw_->begin();
       rc = hw_->hash_body(body, len, idx_.data(), fv_.data(), rp_.data(), (int64_t)rp_.size() - 1,
                           (int64_t)idx_.size(), &n, &slots, update);
       hw_->set_sinks(nullptr, nullptr, nullptr);
+      if (rc != 0 && p_.global) hw_->rollback();   // a retry / a malformed body counts nothing
       if (rc != 2) break;
       idx_.resize(idx_.size() * 4);
       fv_.resize(idx_.size());
@@ -812,6 +829,7 @@ class Clustering : public HostEngine {
   Params p_;
   jb::PyRandom rng_;
   std::unique_ptr<jb::HostFvWide> hw_;
+  DocStats stats_;   // idf / bm25 document statistics (p_.global)
   hipStream_t st_ = nullptr;
   hipStream_t mix_st_ = nullptr;   // the RCCL plane of the MIX
   int device_ = 0;
