@@ -443,6 +443,175 @@ def _loadgen(exe: str, port: int, method: str, pfile: str, conns: int, depth: in
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
+DIST_ENGINE_CASES = (
+    # name, engine, config, update RPC, query RPC
+    ("lof", "anomaly", "config/anomaly/lof.json", "add", "calc_score"),
+    ("kmeans", "clustering", "config/clustering/kmeans.json", "push", "get_nearest_center"),
+    ("gmm", "clustering", "config/clustering/gmm.json", "push", "get_nearest_center"),
+)
+
+
+def dist_engine_records(args, rank: int, world: int, local: int, device, group) -> dict:
+    """BASELINE #4 / #5 on N ranks: one engine server per rank (the native
+    binary; on --device cpu it hands over to the Python server) joins one
+    cluster through a coordinator rank 0 starts; every rank fills its own
+    server (anomaly add: cluster-wide ids, CHT owners, server-to-server
+    update; clustering push), rank 0 forces one MIX (do_mix: the row diffs /
+    coresets over the group's plane, RCCL between GPUs) and every rank then
+    queries its server. Per engine: observed world size, fill rate, MIX
+    latency / bytes / plane, query rate (sum over ranks) and whether the
+    members answer alike after the MIX."""
+    import threading
+    import torch.distributed as dist
+    from jubatus_amd.common.mprpc import RpcClient
+    out: dict = {}
+    coord = None
+    ls = None
+    if rank == 0:
+        from jubatus_amd.common.coordinator import NativeCoordinator
+        from jubatus_amd.common.lock_service import CoordinatorClient
+        coord = NativeCoordinator(0, "127.0.0.1")
+        ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=10.0)
+    box = [coord.port if coord else 0]
+    dist.broadcast_object_list(box, src=0, group=group)
+    zk = f"127.0.0.1:{box[0]}"
+    # the servers are not ranks of this job: no torch.distributed environment
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                        "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME")
+           and not k.startswith("TORCHELASTIC_")}
+    if device is None:
+        env["JUBATUS_FORCE_CPU"] = "1"     # no GPU: the native binary execs the Python server
+    rows = _row_datums(args.dist_engine_rows + 64, 101 + rank)
+    queries, rows = rows[-64:], rows[:-64]
+    def status_of(port, cname):
+        with RpcClient("127.0.0.1", port, 60.0) as c:
+            (_, raw), = c.call("get_status", cname).items()
+        return {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
+                for k, v in raw.items()}
+
+    def gather(x):
+        xs = [None] * world
+        dist.all_gather_object(xs, x, group=group)
+        return xs
+
+    try:
+        for name, engine, cfg, upd, qry in DIST_ENGINE_CASES:
+            if args.dist_engines != "all" and name not in args.dist_engines.split(","):
+                continue
+            # every rank makes the same collective calls in the same order;
+            # a local failure only empties its contribution
+            cname = f"bench_{name}"
+            if rank == 0:
+                from jubatus_amd.common import config as zkconfig
+                zkconfig.config_tozk(ls, engine, cname, open(os.path.join(ROOT, cfg)).read())
+            dist.barrier(group=group)
+            port = _free_port()
+            srv = subprocess.Popen([os.path.join(ROOT, "jubatus_amd", "native_bin", f"juba{engine}"),
+                                    "-z", zk, "-n", cname, "-p", str(port), "-b", "127.0.0.1", "-s", "0",
+                                    "-i", "0", "-I", "30", "-Z", "10", "-c", "8", "--gpu", str(local)],
+                                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
+            rec: dict = {"config": cfg, "world_size_observed": world}
+            err = None
+            st: dict = {}
+            try:
+                deadline = time.time() + 180
+                while time.time() < deadline:
+                    try:
+                        st = status_of(port, cname)
+                        if st.get("linear_mixer.group_size") == str(world):
+                            break
+                    except Exception:  # noqa: BLE001 - not up yet
+                        if srv.poll() is not None:
+                            raise RuntimeError(f"juba{engine} exited ({srv.returncode})")
+                    time.sleep(0.3)
+                else:
+                    raise RuntimeError("the group did not form")
+            except Exception as e:  # noqa: BLE001
+                err = repr(e)[:300]
+            up = gather(err is None)
+            rec["server_runtime"] = st.get("server_runtime", "python")
+            rate = None
+            if all(up):
+                errs = []
+
+                def fill(part):
+                    try:
+                        with RpcClient("127.0.0.1", port, 120.0) as c:
+                            if upd == "add":
+                                for d in part:
+                                    c.call("add", cname, msgpack.unpackb(d, raw=False))
+                            else:
+                                for i in range(0, len(part), 100):
+                                    c.call("push", cname, [msgpack.unpackb(d, raw=False) for d in part[i:i + 100]])
+                    except Exception as e:  # noqa: BLE001
+                        errs.append(repr(e)[:300])
+                # clustering: enough points for the coresets to be clustered (bucket_size)
+                part = rows if upd == "add" else (rows * (1 + 2500 // max(1, len(rows))))[:max(len(rows), 2500)]
+                t0 = time.perf_counter()
+                ths = [threading.Thread(target=fill, args=(part[i::4],)) for i in range(4)]
+                for t in ths:
+                    t.start()
+                for t in ths:
+                    t.join()
+                rate = len(part) / (time.perf_counter() - t0)
+                if errs:
+                    err, rate = errs[0], None
+            rates = gather(rate)
+            if all(r is not None for r in rates):
+                rec["rows_per_rank"] = len(rows) if upd == "add" else max(len(rows), 2500)
+                rec[f"{upd}_per_s_total"] = round(sum(rates), 1)
+                if rank == 0:
+                    try:
+                        with RpcClient("127.0.0.1", port, 300.0) as c:
+                            t0 = time.perf_counter()
+                            rec["do_mix"] = bool(c.call("do_mix", cname))
+                            rec["mix_latency_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+                    except Exception as e:  # noqa: BLE001
+                        err = repr(e)[:300]
+            dist.barrier(group=group)
+            mine = None
+            if all(r is not None for r in rates):
+                try:
+                    st = status_of(port, cname)
+                    with RpcClient("127.0.0.1", port, 60.0) as c:
+                        first = c.call(qry, cname, msgpack.unpackb(queries[0], raw=False))
+                        n, t0 = 0, time.perf_counter()
+                        while time.perf_counter() - t0 < args.dist_engine_seconds:
+                            c.call(qry, cname, msgpack.unpackb(queries[n % len(queries)], raw=False))
+                            n += 1
+                        qps = n / (time.perf_counter() - t0)
+                    mine = {"mix_count": st.get("linear_mixer.mix_count"),
+                            "bytes": int(st.get("linear_mixer.last_mix_bytes") or 0),
+                            "sec": float(st.get("linear_mixer.last_mix_sec") or 0),
+                            "plane": st.get("linear_mixer.backend"), "qps": qps, "first": repr(first)}
+                except Exception as e:  # noqa: BLE001
+                    err = repr(e)[:300]
+            stats = gather(mine)
+            errors = gather(err)
+            if all(x is not None for x in stats):
+                rec["mix_count_per_rank"] = [x["mix_count"] for x in stats]
+                rec["mix_bytes_per_rank"] = [x["bytes"] for x in stats]
+                rec["mix_seconds_per_rank"] = [x["sec"] for x in stats]
+                rec["mix_plane"] = stats[0]["plane"]
+                rec[f"{qry}_per_s_total"] = round(sum(x["qps"] for x in stats), 1)
+                rec["members_agree_after_mix"] = len({x["first"] for x in stats}) == 1
+            if any(errors):
+                rec["errors"] = [e for e in errors if e][:2]
+            srv.terminate()
+            try:
+                srv.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                srv.kill()
+            dist.barrier(group=group)
+            out[name] = rec
+    finally:
+        if coord is not None:
+            ls.close()
+            coord.stop()
+    return out
+
+
 def engine_records(args, local: int) -> dict:
     """Per BASELINE secondary config: fill N distinct rows through the
     engine's update RPC (rate over the whole fill), then over-RPC latency of
@@ -725,6 +894,12 @@ def main() -> None:
     ap.add_argument("--lof-rows", type=int, default=100_000,
                     help="rows added to the LOF server before its queries")
     ap.add_argument("--engine-seconds", type=float, default=3.0)
+    ap.add_argument("--dist-engines", default="lof,kmeans",
+                    help="N > 1: distributed engine records (lof,kmeans,gmm / all / none): one server per "
+                         "rank in one cluster, a forced MIX, queries on every member")
+    ap.add_argument("--dist-engine-rows", type=int, default=0,
+                    help="rows / points each rank fills in (0: 4000 on GPUs, 200 with --device cpu)")
+    ap.add_argument("--dist-engine-seconds", type=float, default=1.5)
     ap.add_argument("--cluster-points", type=int, default=200_000,
                     help="points pushed into each clustering server (kmeans.json, gmm.json)")
     ap.add_argument("--no-rpc", action="store_true",
@@ -1019,6 +1194,14 @@ def main() -> None:
     engines = None
     if world == 1 and device is not None and args.engines != "none":
         engines = engine_records(args, local)
+    engines_dist = None
+    if world > 1 and args.dist_engines != "none":
+        if args.dist_engine_rows <= 0:
+            args.dist_engine_rows = 4000 if device is not None else 200
+        try:
+            engines_dist = dist_engine_records(args, rank, world, local, device, meta)
+        except Exception as e:  # noqa: BLE001 - the headline stands without it
+            engines_dist = {"error": repr(e)[:300]}
 
     total = samples_per_step * args.steps * world
     value = total / elapsed
@@ -1080,6 +1263,7 @@ def main() -> None:
             "served": served,
             "served_native": served_native,
             "engines": engines,
+            "engines_dist": engines_dist,
             "classify_latency_us_p50": round(p50, 1),
             "classify_latency_us_p99": round(p99, 1),
             "heldout_accuracy": round(acc, 4),

@@ -26,7 +26,7 @@ def test_bench_two_ranks_cpu(mode):
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--requests", "8",
            "--per-request", "16", "--hash-bits", "12", "--latency-iters", "5", "--mix-mode", mode,
-           "--batches-per-step", "2"]
+           "--batches-per-step", "2", "--dist-engines", "none"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -47,7 +47,7 @@ def test_bench_spawns_ranks_without_torchrun():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
            "--warmup", "1", "--device", "cpu", "--requests", "4", "--per-request", "8",
-           "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "1"]
+           "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "1", "--dist-engines", "none"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])

@@ -75,8 +75,9 @@ def test_bench_eight_ranks_cpu():
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(WORLD), "--steps", "2",
            "--warmup", "1", "--device", "cpu", "--requests", "4", "--per-request", "8",
-           "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "2", "--engines", "none"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd="/tmp", env=env)
+           "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "2", "--engines", "none",
+           "--dist-engines", "lof,kmeans", "--dist-engine-rows", "120", "--dist-engine-seconds", "0.5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert out["n_gpus"] == WORLD and out["config"]["world_size_observed"] == WORLD
@@ -88,6 +89,14 @@ def test_bench_eight_ranks_cpu():
     assert mt["count"] >= 1 and mt["world"] == WORLD and mt["bytes_per_rank_mean"] > 0
     assert mt["latency_ms_p50"] is not None and mt["latency_ms_p50"] >= 0
     assert out["config"]["world_size_observed"] == WORLD
+    # BASELINE #4 / #5 on 8 ranks: one server per rank in one cluster, a MIX
+    # every member took part in, queries after it (CPU: the Python servers)
+    for name, qry in (("lof", "calc_score"), ("kmeans", "get_nearest_center")):
+        rec = out["engines_dist"][name]
+        assert "errors" not in rec, rec
+        assert rec["world_size_observed"] == WORLD and rec["do_mix"] is True
+        assert rec["mix_count_per_rank"] == ["1"] * WORLD and min(rec["mix_bytes_per_rank"]) > 0
+        assert rec["mix_latency_ms"] > 0 and rec[f"{qry}_per_s_total"] > 0
 
 
 def test_bench_pinned_budget_eight_ranks():
