@@ -267,11 +267,14 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
   }
 }
 
-// one sample's round data (group layout: lane u holds features u, u + 16)
+// one sample's round data (group layout: lane u holds features u, u + 16).
+// The feature count is taken from the two row offsets when the descriptor is
+// used (a round after its loads), never right after they are issued: that
+// would wait out the global-load latency in the round start.
 struct Desc {
-  int64_t fb;
-  int nf;
+  int64_t fb, fe;
   int y;
+  __device__ __forceinline__ int nf() const { return (int)(fe - fb); }
 };
 
 template <int LC>
@@ -350,9 +353,9 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       if (j < end) {
         d[r].y = labels[j];
         d[r].fb = row_ptr[j];
-        d[r].nf = (int)(row_ptr[j + 1] - d[r].fb);
+        d[r].fe = row_ptr[j + 1];
       } else {
-        d[r].y = -1; d[r].fb = 0; d[r].nf = 0;
+        d[r].y = -1; d[r].fb = 0; d[r].fe = 0;
       }
     }
   };
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       const float2* pp = PP0 + (j - beg) * kNFMax + sub;
 #pragma unroll
       for (int c = 0; c < kFC; ++c) {
-        const bool v = ok && c * 16 + sub < d[r].nf;
+        const bool v = ok && c * 16 + sub < d[r].nf();
         sm[r].fi[c] = v ? fp[c * 16] : -1;
         sm[r].fx[c] = v ? vp[c * 16] : 0.f;
         float2 q = make_float2(1.f, 1.f);
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 #pragma unroll
       for (int c = 0; c < kFC; ++c) {
         slot[r][c] = -1;
-        if (alive[r] && dc[r].nf <= kNFMax) slot[r][c] = cache_find<LC>(s_hent, sc[r].fi[c]);
+        if (alive[r] && dc[r].nf() <= kNFMax) slot[r][c] = cache_find<LC>(s_hent, sc[r].fi[c]);
         any |= slot[r][c] >= 0;
       }
     }
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       float sy, best;
       const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
       slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
-      unsafe[r] = alive[r] && (dc[r].nf > kNFMax || !(slack[r] > 0.f));
+      unsafe[r] = alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f));
     }
     {
       const uint64_t t2 = cyc();
@@ -494,7 +497,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         }
         const int base = s_cn;
         if (sub == 0) { s_nins = 0; s_upd = 0; }
-        if (dd.nf > kNFMax) {
+        if (dd.nf() > kNFMax) {
           if (sub == 0) s_stop = (int)kStopDense;
         } else if (base + nnew > NSLOT) {
           if (sub == 0) s_stop = (int)kStopSaturated;
@@ -626,7 +629,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
           const int pos = G * kR + r;
-          if (!alive[r] || pos <= k || dc[r].nf > kNFMax) continue;
+          if (!alive[r] || pos <= k || dc[r].nf() > kNFMax) continue;
           float cy = 0.f, cl = 0.f;
 #pragma unroll
           for (int c = 0; c < kFC; ++c) {

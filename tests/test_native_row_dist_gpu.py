@@ -125,6 +125,11 @@ def test_native_anomaly_distributed_add_mix_equals_one_node(coord):
         rows = [sorted(x.decode() if isinstance(x, bytes) else x for x in c.call("get_all_rows"))
                 for c in (a, b, s)]
         assert rows[0] == rows[1] == rows[2] == sorted(ids)
+        # the LOF tables (kdist / lrd) of a server that inserted rows one by
+        # one are incremental; a MIX re-derives them from the mixed rows, as a
+        # model load does: the oracle reloads its own model first
+        (_, path), = s.save("lof_oracle").items()
+        assert s.load("lof_oracle") is True
         q = random.Random(9)
         for _ in range(20):
             d = _point(q)
