@@ -329,12 +329,23 @@ def test_native_jubavisor_jubactl_cluster(coord, tmp_path, monkeypatch):
     assert rc == 0, (tmp_path / "visor.err").read_text()[-2000:]
 
 
-def test_native_jubavisor_rpc_errors_and_shutdown(coord, tmp_path, monkeypatch):
-    """bad names / arity, pool exhaustion, and SIGTERM stopping the children"""
+@pytest.mark.parametrize("impl", ["native", "python"])
+def test_jubavisor_twins_rpc_errors_and_shutdown(coord, tmp_path, monkeypatch, impl):
+    """the native supervisor and its Python twin (cmd/jubavisor.py) answer
+    the same: bad names / arity, pool exhaustion, a start that registers the
+    child, and shutdown (SIGTERM / close) stopping the children"""
     monkeypatch.setenv("JUBATUS_FORCE_CPU", "1")
     zk = f"127.0.0.1:{coord.port}"
     vport = free_port_block(1)
-    proc, err = _native_visor(zk, vport, tmp_path, maxc=1)
+    if impl == "native":
+        proc, err = _native_visor(zk, vport, tmp_path, maxc=1)
+    else:
+        visor = Jubavisor(zk, vport, max_children=1, listen_addr="127.0.0.1")
+        rpc = RpcServer(2)
+        rpc.add("start", visor.start, arity=3)
+        rpc.add("stop", visor.stop, arity=2)
+        rpc.listen(vport, "127.0.0.1")
+        rpc.start()
     ls = CoordinatorClient(zk, timeout=5.0)
     argv = argv_to_wire({"threadnum": 2, "timeout": 10, "interval_sec": 0, "interval_count": 0,
                          "datadir": str(tmp_path), "mixer": "linear_mixer"})
@@ -358,9 +369,14 @@ def test_native_jubavisor_rpc_errors_and_shutdown(coord, tmp_path, monkeypatch):
             time.sleep(0.3)
         assert ls.list(nodes_path) == [f"127.0.0.1_{vport + 1}"]
     finally:
-        proc.terminate()          # the supervisor takes its children down with it
-        rc = proc.wait(30)
-        err.close()
+        if impl == "native":
+            proc.terminate()          # the supervisor takes its children down with it
+            rc = proc.wait(30)
+            err.close()
+        else:
+            rpc.stop()
+            visor.close()
+            rc = 0
     deadline = time.time() + 30
     while ls.list(nodes_path) and time.time() < deadline:
         time.sleep(0.3)
