@@ -943,7 +943,11 @@ def main() -> None:
                     help="overlap: the RCCL all-reduce of batch k runs during batch k+1 and its "
                          "mean is folded in afterwards (updates made meanwhile are kept); "
                          "sync: blocking MIX at the end of every batch")
+    ap.add_argument("--mix-dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="bf16: the MIX all-reduce moves bf16 values (half the bytes; the snapshot and "
+                         "the fold stay fp32, the mean is rounded once per MIX)")
     args = ap.parse_args()
+    os.environ["JUBATUS_MIX_DTYPE"] = args.mix_dtype     # parallel/table_mix.py (read at import)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one rank per GPU: launch them before this process touches the GPU
@@ -1238,7 +1242,8 @@ def main() -> None:
                         f"chunked dense past half the table), {args.mix_mode}, "
                         + (f"every {args.mix_every} batch(es)" if args.mix_every > 0 else
                            "back to back (a new MIX as soon as the previous one finished)")
-                        + f"; {mixes[0]} MIXes in the timed steps") if world > 1 else "standalone",
+                        + f"; {mixes[0]} MIXes in the timed steps; {args.mix_dtype} on the wire")
+                       if world > 1 else "standalone",
                 "concurrent_update": args.update_mode,
                 "hot_rows": clf.hot_rows,
                 "numa_node": numa.get("node"),

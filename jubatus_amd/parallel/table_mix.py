@@ -22,6 +22,12 @@ Rows nobody touched since the last MIX are equal on every rank (the last MIX
 made them so), so leaving them out is exact. The bytes moved scale with the
 touched rows, and the extra memory is 2 x the union's rows.
 
+``wire_dtype`` (``JUBATUS_MIX_DTYPE``): ``fp32`` (default) or
+``bf16`` - the SUM all-reduce then moves bf16 values (half the bytes over
+xGMI); the snapshot and the fold stay fp32, so each MIX rounds the mean to
+bf16 once (relative error <= 2^-8 per MIX, not accumulated: the next MIX
+replaces it) while updates made during the collective are kept exactly.
+
 When the union exceeds ``dense_frac`` of the table (or no touched map
 exists: host backend, after a model load or a label re-layout), the MIX is
 dense but chunked: at most two chunks of ``chunk_bytes`` are snapshotted and
@@ -40,6 +46,7 @@ import torch.distributed as dist
 
 DEFAULT_CHUNK_BYTES = int(os.environ.get("JUBATUS_MIX_CHUNK_BYTES", 256 << 20))
 DEFAULT_DENSE_FRAC = float(os.environ.get("JUBATUS_MIX_DENSE_FRAC", "0.5"))
+DEFAULT_WIRE_DTYPE = os.environ.get("JUBATUS_MIX_DTYPE", "fp32")
 
 
 def _world(group) -> int:
@@ -50,9 +57,13 @@ class TableMix:
     """One MIX of ``tables`` (each [H, C], same H, same device)."""
 
     def __init__(self, tables: Sequence[torch.Tensor], touched: torch.Tensor | None, group=None,
-                 dense_frac: float = DEFAULT_DENSE_FRAC, chunk_bytes: int = DEFAULT_CHUNK_BYTES):
+                 dense_frac: float = DEFAULT_DENSE_FRAC, chunk_bytes: int = DEFAULT_CHUNK_BYTES,
+                 wire_dtype: str = DEFAULT_WIRE_DTYPE):
         if not tables:
             raise ValueError("nothing to mix")
+        if wire_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"mix wire dtype must be fp32 or bf16, not {wire_dtype}")
+        self.wire = torch.bfloat16 if wire_dtype == "bf16" else torch.float32
         self.tables = list(tables)
         self.H = self.tables[0].shape[0]
         if any(t.shape[0] != self.H or not t.is_contiguous() for t in self.tables):
@@ -158,7 +169,7 @@ class TableMix:
         # collective adds fp32, the fold rounds once)
         snap = torch.cat([t.index_select(0, rows).reshape(self.rows, -1).float() for t in self.tables],
                          dim=1)
-        red = snap.clone()
+        red = snap.to(self.wire, copy=True)   # never an alias of snap
         self.nbytes += red.numel() * red.element_size()
         work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._sparse = (rows, snap, red, work)
@@ -167,7 +178,7 @@ class TableMix:
     # ------------------------------------------------------------ dense
     def _launch(self, r0: int, r1: int) -> None:
         snap = torch.cat([t[r0:r1].reshape(r1 - r0, -1).float() for t in self.tables], dim=1)
-        red = snap.clone()
+        red = snap.to(self.wire, copy=True)   # never an alias of snap
         self.nbytes += red.numel() * red.element_size()
         work = dist.all_reduce(red, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight.append((r0, r1, snap, red, work))
@@ -181,7 +192,7 @@ class TableMix:
     def _fold(self, r0: int, r1: int, snap: torch.Tensor, red: torch.Tensor) -> None:
         if self.abandoned:
             return
-        upd = red.mul_(1.0 / self.n).sub_(snap)
+        upd = red.float().mul_(1.0 / self.n).sub_(snap)
         c0 = 0
         for t in self.tables:
             w = t[0].numel()
@@ -247,7 +258,7 @@ class TableMix:
             rows, snap, red, work = self._sparse
             work.wait()
             if not self.abandoned:
-                upd = red.mul_(1.0 / self.n).sub_(snap)
+                upd = red.float().mul_(1.0 / self.n).sub_(snap)
                 c0 = 0
                 for t in self.tables:
                     w = t[0].numel()
@@ -265,4 +276,5 @@ class TableMix:
 
     def stats(self) -> dict:
         return {"mode": self.mode, "rows": self.rows, "bytes": self.nbytes,
-                "abandoned": self.abandoned, "latency_ms": self.latency_ms, "world": self.n}
+                "abandoned": self.abandoned, "latency_ms": self.latency_ms, "world": self.n,
+                "wire": "bf16" if self.wire == torch.bfloat16 else "fp32"}

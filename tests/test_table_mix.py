@@ -54,14 +54,14 @@ def _worker(rank, world, port, mode, q):
             q.put((rank, job.stats(), nbytes, float((W - ref_w).abs().max()),
                    float((P - ref_p).abs().max()), int(touched.sum())))
             return
-        if mode == "sparse":
-            job = TableMix([W, P], touched, None).begin()
+        if mode in ("sparse", "sparse_bf16"):
+            job = TableMix([W, P], touched, None, wire_dtype="bf16" if mode == "sparse_bf16" else "fp32").begin()
         else:      # dense, chunked into 16 KiB pieces
             job = TableMix([W, P], None, None, chunk_bytes=16 << 10).begin()
             assert job.chunk_rows < H
         # an update made while the collective is in flight survives the MIX
         # (dense: in the first chunk, whose snapshot begin() took)
-        late = (3000 if mode == "sparse" else 5) + rank
+        late = (3000 if mode.startswith("sparse") else 5) + rank
         W[late, 0] += 100.0
         while not job.ready():
             pass
@@ -74,7 +74,7 @@ def _worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense", "full_union"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "full_union", "sparse_bf16"])
 def test_table_mix_equals_dense_mean(mode):
     world = 2
     ctx = mp.get_context("spawn")
@@ -88,6 +88,12 @@ def test_table_mix_equals_dense_mean(mode):
         p.join(60)
         assert p.exitcode == 0
     for rank, st, nbytes, ew, ep, left in res:
+        if mode == "sparse_bf16":
+            # bf16 on the wire: the mean is rounded once (|values| < ~8 here:
+            # 2^-8 relative -> < 0.05), half the bytes; the late update stays exact
+            assert ew < 0.05 and ep < 0.05, (rank, ew, ep)
+            assert st["wire"] == "bf16" and nbytes == st["rows"] * 2 * C * 2 + H
+            continue
         assert ew < 1e-5 and ep < 1e-5, (rank, ew, ep)
         if mode == "sparse":
             assert st["mode"] == "sparse"
