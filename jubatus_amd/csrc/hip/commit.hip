@@ -60,7 +60,6 @@ constexpr int kFC = 2;                // feature chunks of 16 held in registers
 constexpr int kNFMax = 16 * kFC;      // widest sample the committer takes
 constexpr float kGuard = 1e-4f;       // relative guard band of a decision
 constexpr int kInf = 0x7fffffff;
-constexpr uint64_t kEmpty = ~0ull;    // free row-hash entry
 // stop reasons (tail[kTailReason]); the values are serial.hip's
 constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2;
 constexpr int kTailReason = 20;
@@ -75,14 +74,10 @@ template <int LC>
 struct Geo {
   static constexpr int K = (LC + 15) / 16;                 // labels per lane
   static constexpr int NSLOT = 16384 / (LC > 16 ? LC : 16); // rows the LDS store holds
-  static constexpr int HS = 2 * NSLOT;                      // row hash entries (load <= 1/2)
-  static constexpr int HB = ilog2(HS);
+  static constexpr int NB = NSLOT / 4;                      // 4-way buckets of row keys
+  static constexpr int BB = ilog2(NB);
+  static constexpr int PAD = LC + 16;   // a zero row (slot NSLOT) + read overrun of LC = 8
 };
-
-__device__ __forceinline__ uint32_t hmix(int32_t r) { return (uint32_t)r * 0x9E3779B1u; }
-__device__ __forceinline__ uint64_t hpack(int32_t row, int slot) {
-  return (uint64_t)(uint32_t)row | ((uint64_t)(uint32_t)slot << 32);
-}
 
 // best wrong label over a row of 16 lanes (lowest label on ties); the DPP
 // pairings xor 1, xor 2, xor 7 (half mirror), xor 8 (rotate 8) span the row
@@ -140,18 +135,64 @@ __device__ __forceinline__ float slack_of(int method, float m, float nrm, bool h
   }
 }
 
-// LDS row store: open-addressed row -> slot hash of packed (row, slot) words
+// LDS row store: row keys in 2-choice 4-way buckets; a row's slot is its
+// position in the key array (its dW / dP rows live at that index), so a
+// lookup is two 16-byte LDS reads and eight compares, no probe loop
 template <int LC>
-__device__ __forceinline__ int cache_find(const uint64_t* hent, int32_t row) {
+__device__ __forceinline__ void buckets_of(int32_t row, int* b1, int* b2) {
   using Gm = Geo<LC>;
-  if (row < 0) return -1;
-  uint32_t h = hmix(row) >> (32 - Gm::HB);
-  for (int p = 0; p < Gm::HS; ++p) {
-    const uint64_t e = hent[h];
-    const int32_t r = (int32_t)(uint32_t)e;
-    if (r == row) return (int)(e >> 32);
-    if (r == -1) return -1;
-    h = (h + 1) & (Gm::HS - 1);
+  const int x = (int)(((uint32_t)row * 0x9E3779B1u) >> (32 - Gm::BB));
+  const int y = (int)((((uint32_t)row ^ 0x5BD1E995u) * 0x85EBCA77u) >> (32 - Gm::BB));
+  *b1 = x;
+  *b2 = y == x ? (y ^ 1) : y;
+}
+
+template <int LC>
+__device__ __forceinline__ int cache_find(const int32_t* key, int32_t row) {
+  int b1, b2;
+  buckets_of<LC>(row, &b1, &b2);
+  const int4 k1 = reinterpret_cast<const int4*>(key)[b1];
+  const int4 k2 = reinterpret_cast<const int4*>(key)[b2];
+  const int32_t r = row < 0 ? -2 : row;     // no key is -2 (free entries are -1)
+  int s = -1;
+  s = k1.x == r ? 4 * b1 : s;
+  s = k1.y == r ? 4 * b1 + 1 : s;
+  s = k1.z == r ? 4 * b1 + 2 : s;
+  s = k1.w == r ? 4 * b1 + 3 : s;
+  s = k2.x == r ? 4 * b2 : s;
+  s = k2.y == r ? 4 * b2 + 1 : s;
+  s = k2.z == r ? 4 * b2 + 2 : s;
+  s = k2.w == r ? 4 * b2 + 3 : s;
+  return s;
+}
+
+// the stepping group's lanes add their new rows (the emptier bucket first;
+// keys are only added during a segment, so a bucket fills in order); a lane
+// whose row another lane of the same instruction added takes that slot.
+// -1: both buckets are full (the segment ends)
+template <int LC>
+__device__ __forceinline__ int cache_insert(int32_t* key, int32_t row) {
+  int b1, b2;
+  buckets_of<LC>(row, &b1, &b2);
+  const int4 k1 = reinterpret_cast<const int4*>(key)[b1];
+  const int4 k2 = reinterpret_cast<const int4*>(key)[b2];
+  // added meanwhile (an earlier feature chunk of the same sample)
+  if (k1.x == row) return 4 * b1;
+  if (k1.y == row) return 4 * b1 + 1;
+  if (k1.z == row) return 4 * b1 + 2;
+  if (k1.w == row) return 4 * b1 + 3;
+  if (k2.x == row) return 4 * b2;
+  if (k2.y == row) return 4 * b2 + 1;
+  if (k2.z == row) return 4 * b2 + 2;
+  if (k2.w == row) return 4 * b2 + 3;
+  const int n1 = (k1.x >= 0) + (k1.y >= 0) + (k1.z >= 0) + (k1.w >= 0);
+  const int n2 = (k2.x >= 0) + (k2.y >= 0) + (k2.z >= 0) + (k2.w >= 0);
+  const int first = n2 < n1 ? b2 : b1;
+  const int second = first == b1 ? b2 : b1;
+  for (int t = first == b1 ? n1 : n2; t < 8; ++t) {
+    const int pos = t < 4 ? 4 * first + t : 4 * second + (t - 4);
+    const int old = atomicCAS(&key[pos], -1, row);
+    if (old == -1 || old == row) return pos;
   }
   return -1;
 }
@@ -161,9 +202,12 @@ __device__ __forceinline__ int cache_find(const uint64_t* hent, int32_t row) {
 // q ^ (i >> 2); the mirror (lane 15 - i) and half-mirror (lane i ^ 7) DPP
 // adds then leave lane i the quad of labels 4 (i >> 2) .. + 3 summed over 4
 // lanes, and two quad-permute steps hand each lane its own label.
+// Branch-free: a lane without a row reads the zero row (slot NSLOT); with
+// LC = 8 the quads past the labels read padding / the next row, which only
+// ever sums into labels >= LC (lanes 8..15), never read.
 template <int LC>
 __device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[kFC],
-                                            const float (&x)[kFC], int sub,
+                                            const float (&x)[kFC], int sub, bool two,
                                             float (&s)[Geo<LC>::K]) {
   constexpr int K = Geo<LC>::K;
   const int qs = sub >> 2;
@@ -174,16 +218,13 @@ __device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[k
     for (int q = 0; q < 4; ++q) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int c = 0; c < kFC; ++c) {
-      if (slot[c] < 0) continue;
+      if (c > 0 && !two) break;              // wave-uniform
       const float xc = x[c];
-      const float* rowp = dw + slot[c] * LC + 16 * b;
+      const float* rowp = dw + (slot[c] >= 0 ? slot[c] : Geo<LC>::NSLOT) * LC + 16 * b;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int qq = q ^ qs;
-        if (16 * b + 4 * qq < LC) {
-          const float4 w = *reinterpret_cast<const float4*>(rowp + 4 * qq);
-          v[q].x += xc * w.x; v[q].y += xc * w.y; v[q].z += xc * w.z; v[q].w += xc * w.w;
-        }
+        const float4 w = *reinterpret_cast<const float4*>(rowp + 4 * (q ^ qs));
+        v[q].x += xc * w.x; v[q].y += xc * w.y; v[q].z += xc * w.z; v[q].w += xc * w.w;
       }
     }
 #define JB_DADD(D, S, C) \
@@ -300,11 +341,10 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   using Gm = Geo<LC>;
   constexpr int K = Gm::K;
   constexpr int NSLOT = Gm::NSLOT;
-  constexpr int HS = Gm::HS;
   if (seg > 0 && (tail[kTailReason] == kStopDense || tail[kTailReason] == kStopDone)) return;
-  __shared__ float s_dw[NSLOT * LC];
-  __shared__ float s_dp[NSLOT * LC];
-  __shared__ uint64_t s_hent[HS];
+  __shared__ __attribute__((aligned(16))) float s_dw[NSLOT * LC + Gm::PAD];
+  __shared__ __attribute__((aligned(16))) float s_dp[NSLOT * LC + Gm::PAD];
+  __shared__ __attribute__((aligned(16))) int32_t s_key[NSLOT];   // row of each slot (-1: free)
   __shared__ int32_t s_sst[NSLOT];    // id of the last step that wrote the slot
   __shared__ float s_sdy[NSLOT];      // that step's increment of labels y / l
   __shared__ float s_sdl[NSLOT];
@@ -327,8 +367,8 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     float4* dw4 = reinterpret_cast<float4*>(s_dw);
     float4* dp4 = reinterpret_cast<float4*>(s_dp);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = tid; i < NSLOT * LC / 4; i += kT) { dw4[i] = z; if (use_s) dp4[i] = z; }
-    for (int i = tid; i < HS; i += kT) s_hent[i] = kEmpty;
+    for (int i = tid; i < (NSLOT * LC + Gm::PAD) / 4; i += kT) { dw4[i] = z; if (use_s) dp4[i] = z; }
+    for (int i = tid; i < NSLOT; i += kT) s_key[i] = -1;
     for (int i = tid; i < NSLOT; i += kT) s_sst[i] = -1;
     if (tid == 0) {
       s_cn = 0; s_stop = -1; s_upd = 0; s_yk = -1; s_lk = -1; s_nins = 0;
@@ -411,22 +451,27 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     bool alive[kR], unsafe[kR];
     float nrm[kR], slack[kR];
     int slot[kR][kFC];
-    bool any = false;
+    bool any = false, wide = false;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int64_t j = p + G * kR + r;
       alive[r] = j < end && dc[r].y >= 0 && dc[r].y < LC;
+      wide |= alive[r] && dc[r].nf() > 16;
+    }
+    // the second feature chunk only when a sample of the wave has one
+    const bool two = __builtin_amdgcn_ballot_w64(wide) != 0;
 #pragma unroll
-      for (int c = 0; c < kFC; ++c) {
-        slot[r][c] = -1;
-        if (alive[r] && dc[r].nf() <= kNFMax) slot[r][c] = cache_find<LC>(s_hent, sc[r].fi[c]);
-        any |= slot[r][c] >= 0;
-      }
+    for (int r = 0; r < kR; ++r) {
+      const bool ok = alive[r] && dc[r].nf() <= kNFMax;
+      slot[r][0] = ok ? cache_find<LC>(s_key, sc[r].fi[0]) : -1;
+      slot[r][1] = -1;
+      if (two) slot[r][1] = ok ? cache_find<LC>(s_key, sc[r].fi[1]) : -1;
+      any |= slot[r][0] >= 0 || slot[r][1] >= 0;
     }
     // rows with a delta anywhere in the wave: the transposed correction
     if (__builtin_amdgcn_ballot_w64(any) != 0) {
 #pragma unroll
-      for (int r = 0; r < kR; ++r) row_correct<LC>(s_dw, slot[r], sc[r].fx, sub, sc[r].s);
+      for (int r = 0; r < kR; ++r) row_correct<LC>(s_dw, slot[r], sc[r].fx, sub, two, sc[r].s);
     }
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
@@ -487,19 +532,27 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
             for (int c = 0; c < kFC; ++c) sl[c] = slot[r][c];
           }
         const int y = dd.y;
-        // rows the step would add to the store
-        uint64_t nb[kFC];
-        int nnew = 0;
-#pragma unroll
-        for (int c = 0; c < kFC; ++c) {
-          nb[c] = __builtin_amdgcn_ballot_w64(t.fi[c] >= 0 && sl[c] < 0);
-          nnew += __popcll(nb[c]);
-        }
-        const int base = s_cn;
         if (sub == 0) { s_nins = 0; s_upd = 0; }
+        // the sample's rows not in the store yet are added first (a step
+        // that then does not update leaves them with zero deltas); a full
+        // bucket pair ends the segment before anything is applied
+        int nnew = 0;
+        bool full = false;
+        if (dd.nf() <= kNFMax) {
+#pragma unroll
+          for (int c = 0; c < kFC; ++c) {
+            const bool need = t.fi[c] >= 0 && sl[c] < 0;
+            nnew += __popcll(__builtin_amdgcn_ballot_w64(need));
+            if (need) {
+              sl[c] = cache_insert<LC>(s_key, t.fi[c]);
+              full |= sl[c] < 0;
+            }
+          }
+          full = __builtin_amdgcn_ballot_w64(full) != 0;
+        }
         if (dd.nf() > kNFMax) {
           if (sub == 0) s_stop = (int)kStopDense;
-        } else if (base + nnew > NSLOT) {
+        } else if (full) {
           if (sub == 0) s_stop = (int)kStopSaturated;
         } else {
           int ls = -1;
@@ -515,11 +568,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
               pl[c] = 1.f;
               const int32_t row = t.fi[c];
               if (!use_s || row < 0) continue;
-              const float* dpr = s_dp + (sl[c] >= 0 ? sl[c] : 0) * LC;
-              py[c] = t.py[c] + (sl[c] >= 0 ? dpr[y] : 0.f);
+              const float* dpr = s_dp + sl[c] * LC;    // every row of the sample has a slot now
+              py[c] = t.py[c] + dpr[y];
               if (ls >= 0) {
                 const float p0 = ls == t.ls0 ? t.pl[c] : P[(int64_t)row * LC + ls];
-                pl[c] = p0 + (sl[c] >= 0 ? dpr[ls] : 0.f);
+                pl[c] = p0 + dpr[ls];
               }
               const float x2 = t.fx[c] * t.fx[c];
               v += x2 * (1.f / py[c] + (ls >= 0 ? 1.f / pl[c] : 0.f));
@@ -546,8 +599,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 #pragma unroll
                 for (int kk = 0; kk < K; ++kk) {
                   const int lab = sub + 16 * kk;
-                  if (lab < LC)
-                    ns[kk] += xu * (W[(int64_t)ru * LC + lab] + (su >= 0 ? s_dw[su * LC + lab] : 0.f));
+                  if (lab < LC) ns[kk] += xu * (W[(int64_t)ru * LC + lab] + s_dw[su * LC + lab]);
                 }
               }
             }
@@ -557,26 +609,6 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           float tau = 0.f, beta = 0.f;
           const bool up = step_coeffs(method, m, var, tn, ls >= 0, C, &tau, &beta);
           if (up) {
-            // new rows: slots base + rank among the row's new features (a row
-            // another lane inserted first keeps that lane's slot)
-            const uint64_t below = (1ull << lane) - 1ull;
-            int off = 0;
-#pragma unroll
-            for (int c = 0; c < kFC; ++c) {
-              if (t.fi[c] >= 0 && sl[c] < 0) {
-                const int ns = base + off + __popcll(nb[c] & below);
-                uint32_t h = hmix(t.fi[c]) >> (32 - Gm::HB);
-                for (int q = 0; q < HS; ++q) {
-                  const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long*>(&s_hent[h]),
-                                                 (unsigned long long)kEmpty,
-                                                 (unsigned long long)hpack(t.fi[c], ns));
-                  if (old == kEmpty) { sl[c] = ns; break; }
-                  if ((int32_t)(uint32_t)old == t.fi[c]) { sl[c] = (int)(old >> 32); break; }
-                  h = (h + 1) & (HS - 1);
-                }
-              }
-              off += __popcll(nb[c]);
-            }
 #pragma unroll
             for (int c = 0; c < kFC; ++c)
               if (t.fi[c] >= 0) { s_sst[sl[c]] = sid; s_sdy[sl[c]] = 0.f; s_sdl[sl[c]] = 0.f; }
@@ -601,7 +633,8 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
             }
           }
           if (sub == 0) {
-            if (up) { s_cn = base + nnew; s_nins = nnew; }
+            s_cn += nnew;
+            s_nins = nnew;
             s_upd = up ? 1 : 0;
             s_yk = y;
             s_lk = ls;
@@ -623,9 +656,21 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         stop = p + k;
         break;
       }
-      // samples after k: the step's increments of their stamped rows
+      // samples after k: the slots of rows the step added (also when it did
+      // not update: a later step may write them), then the step's
+      // increments of their stamped rows
+      const int nins = s_nins;
+      if (nins > 0 && (wv + 1) * 4 * kR - 1 > k) {
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+          if (G * kR + r <= k) continue;
+#pragma unroll
+          for (int c = 0; c < kFC; ++c)
+            if (slot[r][c] < 0 && sc[r].fi[c] >= 0) slot[r][c] = cache_find<LC>(s_key, sc[r].fi[c]);
+        }
+      }
       if (s_upd && (wv + 1) * 4 * kR - 1 > k) {
-        const int yk = s_yk, lk = s_lk, nins = s_nins;
+        const int yk = s_yk, lk = s_lk;
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
           const int pos = G * kR + r;
@@ -633,7 +678,6 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           float cy = 0.f, cl = 0.f;
 #pragma unroll
           for (int c = 0; c < kFC; ++c) {
-            if (slot[r][c] < 0 && nins > 0) slot[r][c] = cache_find<LC>(s_hent, sc[r].fi[c]);
             const int s = slot[r][c];
             if (s >= 0 && s_sst[s] == sid) {
               cy += sc[r].fx[c] * s_sdy[s];
@@ -679,12 +723,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   // ---- segment end: the deltas into the tables (the committer is their only writer)
   {
     constexpr int Q = LC / 4;
-    for (int i = tid; i < HS * Q; i += kT) {
-      const uint64_t e = s_hent[i / Q];
-      const int32_t row = (int32_t)(uint32_t)e;
+    for (int i = tid; i < NSLOT * Q; i += kT) {
+      const int sl = i / Q;
+      const int32_t row = s_key[sl];
       if (row < 0) continue;
       const int q = i % Q;
-      const int sl = (int)(e >> 32);
       float4* w4 = reinterpret_cast<float4*>(W + (int64_t)row * LC) + q;
       const float4 d = reinterpret_cast<const float4*>(s_dw + sl * LC)[q];
       float4 w = *w4;
