@@ -79,27 +79,31 @@ struct Geo {
   static constexpr int PAD = LC + 16;   // a zero row (slot NSLOT) + read overrun of LC = 8
 };
 
-// best wrong label over a row of 16 lanes (lowest label on ties); the DPP
-// pairings xor 1, xor 2, xor 7 (half mirror), xor 8 (rotate 8) span the row
+// best wrong label over a row of 16 lanes (lowest label on ties): the row's
+// maximum (4 DPP max steps over the pairings xor 1, xor 2, xor 7 - half
+// mirror - and xor 8 - rotate 8 - which span the row), then the lowest label
+// holding it (4 DPP min steps). b: the lane's best candidate (-inf: none),
+// bl its label; every lane gets the row's (b, bl), bl = -1 when no lane has one.
 __device__ __forceinline__ void row16_argmax(float& b, int& bl) {
-#define JB_ARGSTEP(C)                                                              \
-  {                                                                                \
-    const float ob = dpp_f<C>(b);                                                  \
-    const int ol = dpp_i<C>(bl);                                                   \
-    if (ol >= 0 && (bl < 0 || ob > b || (ob == b && ol < bl))) { b = ob; bl = ol; } \
-  }
-  JB_ARGSTEP(kDppXor1)
-  JB_ARGSTEP(kDppXor2)
-  JB_ARGSTEP(kDppHalfMirror)
-  JB_ARGSTEP(kDppRowRor8)
-#undef JB_ARGSTEP
+  float m = b;
+  m = fmaxf(m, dpp_f<kDppXor1>(m));
+  m = fmaxf(m, dpp_f<kDppXor2>(m));
+  m = fmaxf(m, dpp_f<kDppHalfMirror>(m));
+  m = fmaxf(m, dpp_f<kDppRowRor8>(m));
+  int c = (bl >= 0 && b == m) ? bl : 0x7fff;
+  c = min(c, dpp_i<kDppXor1>(c));
+  c = min(c, dpp_i<kDppXor2>(c));
+  c = min(c, dpp_i<kDppHalfMirror>(c));
+  c = min(c, dpp_i<kDppRowRor8>(c));
+  bl = c == 0x7fff ? -1 : c;
+  b = m;
 }
 
 // exact margin of a sample held by a group: score(y) - best active wrong
 // label (every lane of the row gets the same values)
 template <int LC>
 __device__ __forceinline__ float group_margin(const float (&s)[Geo<LC>::K], int y,
-                                              const bool (&act)[Geo<LC>::K], int sub,
+                                              const int (&act)[Geo<LC>::K], int sub,
                                               int* lstar, float* sy_out, float* best_out) {
   constexpr int K = Geo<LC>::K;
   float v = 0.f;
@@ -112,7 +116,7 @@ __device__ __forceinline__ float group_margin(const float (&s)[Geo<LC>::K], int 
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int lab = sub + 16 * k;
-    if (lab < LC && act[k] && lab != y && s[k] > b) { b = s[k]; bl = lab; }
+    if (lab < LC && act[k] != 0 && lab != y && s[k] > b) { b = s[k]; bl = lab; }
   }
   row16_argmax(b, bl);
   *lstar = bl;
@@ -247,21 +251,34 @@ __device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[k
   }
 }
 
+// a wave-uniform value moved into a VGPR: the committer holds more loop
+// invariants than the SGPR file (a spilled SGPR costs a v_readlane at every
+// use); the prefetch's base pointers and bounds live in VGPRs instead
+__device__ __forceinline__ uint64_t in_vgpr(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32), vl, vh;
+  asm("v_mov_b32 %0, %1" : "=v"(vl) : "s"(lo));
+  asm("v_mov_b32 %0, %1" : "=v"(vh) : "s"(hi));
+  return (uint64_t)vl | ((uint64_t)vh << 32);
+}
+template <class T>
+__device__ __forceinline__ T* in_vgpr(T* p) { return (T*)in_vgpr((uint64_t)p); }
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ------------------------------------------------------------ S0 scores
 // S0[i * LC + l]: score of label l of sample beg + i at the segment start;
-// LS0[i]: its best active wrong label there (-1: none); PP0[i * 32 + f]:
-// (P0(row_f, y), P0(row_f, LS0[i])) of its first 32 features (P != nullptr)
+// AUX[i] = (its best active wrong label there - -1: none, |x|^2 as float
+// bits); PP0[i * 32 + f]: (P0(row_f, y), P0(row_f, that label)) of its first
+// 32 features (P != nullptr)
 template <int LC>
 __global__ __launch_bounds__(256) void delta_s0_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
     const float* __restrict__ P, const int32_t* __restrict__ active, float* __restrict__ S0,
-    int32_t* __restrict__ LS0, float2* __restrict__ PP0, const int64_t* __restrict__ reason) {
+    int2* __restrict__ AUX, float2* __restrict__ PP0, const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   static_assert(LC <= 64, "delta committer: LC <= 64");
   if (reason != nullptr && (*reason == kStopDense || *reason == kStopDone)) return;
@@ -284,9 +301,20 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
 #pragma unroll
     for (int off = L::LW; off < 64; off <<= 1) acc += __shfl_xor(acc, off, 64);
     if (lane < LC) S0[wid * LC + lane] = acc;
-    if (P == nullptr) continue;
+    // |x|^2 over the sample's features (hashed-out slots count too, as in
+    // the sequential kernel's norm)
+    float q = 0.f;
+    for (int j = lane; j < n; j += 64) {
+      const float x = fval[fb + j];
+      q += x * x;
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) q += __shfl_xor(q, off, 64);
     const int y = labels[s];
-    if (y < 0 || y >= LC) continue;
+    if (P == nullptr || y < 0 || y >= LC) {
+      if (lane == 0) AUX[wid] = make_int2(-1, __float_as_int(q));
+      continue;
+    }
     float b = (la && l0 != y) ? acc : -INFINITY;
     int bl = (la && l0 != y) ? l0 : -1;
 #pragma unroll
@@ -295,7 +323,7 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
       const int ol = __shfl_xor(bl, off, 64);
       if (ol >= 0 && (bl < 0 || ob > b || (ob == b && ol < bl))) { b = ob; bl = ol; }
     }
-    if (lane == 0) LS0[wid] = bl;
+    if (lane == 0) AUX[wid] = make_int2(bl, __float_as_int(q));
     if (lane < kNFMax && lane < n) {
       const int32_t idx = fidx[fb + lane];
       float2 pp = make_float2(1.f, 1.f);
@@ -326,16 +354,20 @@ struct Samp {
   float pl[kFC];
   float s[Geo<LC>::K];
   int ls0;
+  float nrm;       // |x|^2
 };
 
 // ------------------------------------------------------------ committer
-template <int LC>
+// MT: the method, a template argument - the step's coefficient code, the
+// precision path (CW / AROW / NHERD) and the slack thresholds fold away for
+// the other methods
+template <int LC, int MT>
 __global__ __launch_bounds__(kT) void delta_commit_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
-    const float* __restrict__ fval, const int32_t* __restrict__ labels,
+    const int64_t* __restrict__ row_ptr_k, const int32_t* __restrict__ fidx_k,
+    const float* __restrict__ fval_k, const int32_t* __restrict__ labels_k,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* __restrict__ W,
-    float* __restrict__ P, const int32_t* __restrict__ active, int method, float C,
-    const float* __restrict__ S0, const int32_t* __restrict__ LS0, const float2* __restrict__ PP0,
+    float* __restrict__ P, const int32_t* __restrict__ active, float C,
+    const float* __restrict__ S0_k, const int2* __restrict__ AUX_k, const float2* __restrict__ PP0_k,
     unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
     int64_t* __restrict__ tail, int seg) {
   using Gm = Geo<LC>;
@@ -357,7 +389,8 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   const int sub = lane & 15;
   const int G = tid >> 4;
   const int wv = tid >> 6;
-  const bool use_s = method >= CW;
+  constexpr int method = MT;
+  constexpr bool use_s = MT >= CW;
   const uint64_t t_k0 = cyc();
   const uint64_t w_k0 = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};   // start, barrier A, step, corrections, flush, init
@@ -376,14 +409,21 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       s_nupd = 0; s_waste = 0; s_refresh = 0;
     }
   }
-  bool act[K];
+  int act[K];   // ints, not lane masks: every bool array held across the loop is an SGPR pair
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int lab = sub + 16 * k;
-    act[k] = lab < LC && active[lab] != 0;
+    act[k] = (lab < LC && active[lab] != 0) ? 1 : 0;
   }
-  const int64_t beg = stream_ptr[0];
-  const int64_t end = stream_ptr[nstreams];
+  const int64_t* __restrict__ row_ptr = in_vgpr(row_ptr_k);
+  const int32_t* __restrict__ fidx = in_vgpr(fidx_k);
+  const float* __restrict__ fval = in_vgpr(fval_k);
+  const int32_t* __restrict__ labels = in_vgpr(labels_k);
+  const float* __restrict__ S0 = in_vgpr(S0_k);
+  const int2* __restrict__ AUX = in_vgpr(AUX_k);
+  const float2* __restrict__ PP0 = in_vgpr(PP0_k);
+  const int64_t beg = (int64_t)in_vgpr((uint64_t)stream_ptr[0]);
+  const int64_t end = (int64_t)in_vgpr((uint64_t)stream_ptr[nstreams]);
 
   // two-deep prefetch: descriptors two rounds ahead, features / S0 one round ahead
   auto load_desc = [&](int64_t p, Desc (&d)[kR]) {
@@ -399,29 +439,53 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       }
     }
   };
+  // Loads without branches: every address is clamped into the batch (the
+  // features [F0, F1], the samples [beg, end)) and a lane that has nothing
+  // there selects its neutral value instead; the second feature chunk is
+  // loaded only when a sample of the wave has one (wave-uniform).
+  const int64_t F0 = (int64_t)in_vgpr((uint64_t)row_ptr_k[stream_ptr[0]]);
+  const int64_t F1 = (int64_t)in_vgpr((uint64_t)row_ptr_k[stream_ptr[nstreams]]) - 1;
+  const bool has_feat = F1 >= F0;
   auto load_samp = [&](int64_t p, const Desc (&d)[kR], Samp<LC> (&sm)[kR]) {
+    bool wide2 = false;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) wide2 |= d[r].nf() > 16;
+    const bool two2 = __builtin_amdgcn_ballot_w64(wide2) != 0;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int64_t j = p + G * kR + r;
+      const int64_t jc = (j < end ? j : end - 1) - beg;
       const bool ok = j < end && d[r].y >= 0 && d[r].y < LC;
-      const int32_t* fp = fidx + d[r].fb + sub;
-      const float* vp = fval + d[r].fb + sub;
-      const float2* pp = PP0 + (j - beg) * kNFMax + sub;
 #pragma unroll
       for (int c = 0; c < kFC; ++c) {
+        sm[r].fi[c] = -1;
+        sm[r].fx[c] = 0.f;
+        sm[r].py[c] = 1.f;
+        sm[r].pl[c] = 1.f;
+        if ((c > 0 && !two2) || !has_feat) continue;      // wave-uniform
         const bool v = ok && c * 16 + sub < d[r].nf();
-        sm[r].fi[c] = v ? fp[c * 16] : -1;
-        sm[r].fx[c] = v ? vp[c * 16] : 0.f;
-        float2 q = make_float2(1.f, 1.f);
-        if (use_s && v) q = pp[c * 16];
-        sm[r].py[c] = q.x;
-        sm[r].pl[c] = q.y;
+        int64_t fi = d[r].fb + c * 16 + sub;
+        fi = fi < F0 ? F0 : (fi > F1 ? F1 : fi);
+        const int32_t ix = fidx[fi];
+        const float xv = fval[fi];
+        sm[r].fi[c] = v ? ix : -1;
+        sm[r].fx[c] = v ? xv : 0.f;
+        if (use_s) {
+          const float2 q = PP0[jc * kNFMax + c * 16 + sub];
+          sm[r].py[c] = v ? q.x : 1.f;
+          sm[r].pl[c] = v ? q.y : 1.f;
+        }
       }
-      const float* s0p = S0 + (j - beg) * LC + sub;
+      const float* s0p = S0 + jc * LC;
 #pragma unroll
-      for (int k = 0; k < K; ++k)
-        sm[r].s[k] = (ok && sub + 16 * k < LC) ? s0p[16 * k] : 0.f;
-      sm[r].ls0 = (use_s && ok) ? LS0[j - beg] : -1;
+      for (int k = 0; k < K; ++k) {
+        const int lab = sub + 16 * k;
+        const float sv = s0p[lab < LC ? lab : LC - 1];
+        sm[r].s[k] = (ok && lab < LC) ? sv : 0.f;
+      }
+      const int2 aux = AUX[jc];
+      sm[r].ls0 = (use_s && ok) ? aux.x : -1;
+      sm[r].nrm = ok ? __int_as_float(aux.y) : 0.f;
     }
   };
 
@@ -448,14 +512,14 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     if (p + 2 * kNS < end) load_desc(p + 2 * kNS, dnn);
 
     // ---- round start: slots, deltas of the rows the segment wrote, slacks
-    bool alive[kR], unsafe[kR];
+    int alive[kR], unsafe[kR];
     float nrm[kR], slack[kR];
     int slot[kR][kFC];
     bool any = false, wide = false;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int64_t j = p + G * kR + r;
-      alive[r] = j < end && dc[r].y >= 0 && dc[r].y < LC;
+      alive[r] = (j < end && dc[r].y >= 0 && dc[r].y < LC) ? 1 : 0;
       wide |= alive[r] && dc[r].nf() > 16;
     }
     // the second feature chunk only when a sample of the wave has one
@@ -475,15 +539,12 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     }
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      float q = 0.f;
-#pragma unroll
-      for (int c = 0; c < kFC; ++c) q += sc[r].fx[c] * sc[r].fx[c];
-      nrm[r] = row16_sum(q);
+      nrm[r] = sc[r].nrm;
       int ls;
       float sy, best;
       const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
       slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
-      unsafe[r] = alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f));
+      unsafe[r] = (alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f))) ? 1 : 0;
     }
     {
       const uint64_t t2 = cyc();
@@ -699,7 +760,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
             float sy, best;
             const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
             slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
-            unsafe[r] = !(slack[r] > 0.f);
+            unsafe[r] = (slack[r] > 0.f) ? 0 : 1;
           }
         }
       }
@@ -769,13 +830,40 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 }  // namespace dc
 }  // namespace jb
 
+// one segment: the S0 pass, then the committer of the method
+template <int L>
+static int launch_delta(int64_t blocks, int method, const int64_t* row_ptr, const int32_t* fidx,
+                        const float* fval, const int32_t* labels, const int64_t* sp, int ns, float* W,
+                        float* S, float* Pp, const int32_t* active, float C, float* s0, int2* aux,
+                        float2* pp0, unsigned long long* stats, uint8_t* touched, int64_t* tail, int seg,
+                        const int64_t* why, hipStream_t stream) {
+  hipLaunchKernelGGL((jb::dc::delta_s0_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream, row_ptr, fidx,
+                     fval, labels, sp, ns, W, Pp, active, s0, aux, pp0, why);
+#define JB_DELTA_M(M)                                                                                  \
+  hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M>), dim3(1), dim3(jb::dc::kT), 0, stream, row_ptr, \
+                     fidx, fval, labels, sp, ns, W, S, active, C, s0, aux, pp0, stats, touched, tail, seg); \
+  break;
+  switch (method) {
+    case jb::PERCEPTRON: JB_DELTA_M(jb::PERCEPTRON)
+    case jb::PA: JB_DELTA_M(jb::PA)
+    case jb::PA1: JB_DELTA_M(jb::PA1)
+    case jb::PA2: JB_DELTA_M(jb::PA2)
+    case jb::CW: JB_DELTA_M(jb::CW)
+    case jb::AROW: JB_DELTA_M(jb::AROW)
+    case jb::NHERD: JB_DELTA_M(jb::NHERD)
+    default: return -1;
+  }
+#undef JB_DELTA_M
+  return 0;
+}
+
 // bytes of the delta committer's scratch per sample: S0 (<= 64 floats),
-// PP0 (32 float2), LS0 (one int, padded)
+// PP0 (32 float2), AUX (int2: best wrong label at M0, |x|^2)
 extern "C" int64_t jb_delta_scratch_per_sample() { return 256 + 256 + 8; }
 
 // Steps 1-2 of a kSerial batch for LC <= 64 (see the header); the caller
 // runs the exact single-stream kernel over [tail[0], tail[1]) afterwards.
-// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2][LS0: n_max ints].
+// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2][AUX: n_max int2].
 extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
@@ -785,27 +873,26 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
   int64_t* tail = (int64_t*)scratch;
   float* s0 = (float*)((uint8_t*)scratch + 256);
   float2* pp0 = (float2*)((uint8_t*)scratch + 256 + 256 * n_max);
-  int32_t* ls0 = (int32_t*)((uint8_t*)scratch + 256 + 512 * n_max);
+  int2* aux = (int2*)((uint8_t*)scratch + 256 + 512 * n_max);
   float* Pp = method >= jb::CW ? S : nullptr;
   const int64_t blocks = std::min<int64_t>((n_max * 64 + 255) / 256, 2048);
   for (int seg = 0; seg < nseg; ++seg) {
     const int64_t* sp = seg == 0 ? stream_ptr : tail;
     const int ns = seg == 0 ? nstreams : 1;
     const int64_t* why = seg == 0 ? nullptr : tail + jb::dc::kTailReason;
-#define JB_DELTA(L)                                                                                \
-  hipLaunchKernelGGL((jb::dc::delta_s0_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream,  \
-                     row_ptr, fidx, fval, labels, sp, ns, W, Pp, active, s0, ls0, pp0, why);      \
-  hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L>), dim3(1), dim3(jb::dc::kT), 0, stream,       \
-                     row_ptr, fidx, fval, labels, sp, ns, W, S, active, method, C, s0, ls0, pp0,  \
-                     stats, touched, tail, seg);
+    int rc = 0;
     switch (LC) {
-      case 8: JB_DELTA(8); break;
-      case 16: JB_DELTA(16); break;
-      case 32: JB_DELTA(32); break;
-      case 64: JB_DELTA(64); break;
+      case 8: rc = launch_delta<8>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
+                                   aux, pp0, stats, touched, tail, seg, why, stream); break;
+      case 16: rc = launch_delta<16>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
+                                     aux, pp0, stats, touched, tail, seg, why, stream); break;
+      case 32: rc = launch_delta<32>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
+                                     aux, pp0, stats, touched, tail, seg, why, stream); break;
+      case 64: rc = launch_delta<64>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
+                                     aux, pp0, stats, touched, tail, seg, why, stream); break;
       default: return -1;
     }
-#undef JB_DELTA
+    if (rc) return rc;
   }
   return (int)hipGetLastError();
 }
