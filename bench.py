@@ -1190,6 +1190,13 @@ def main() -> None:
         hot = exact_record(args, cfg, device, warm, ws, wb, samples_per_batch, sync,
                            mode=args.update_mode, steps=args.worst_steps, hot_rows=True)
         worst["hot_rows_replica"] = {k: hot[k] for k in ("value", "ms_per_step", "update_fraction")}
+        if exact is not None:
+            # the servers' default (serial-equivalent) mode on the same stream
+            ew = exact_record(args, cfg, device, warm, ws, wb, samples_per_batch, sync,
+                              mode="exact", steps=min(2, args.worst_steps))
+            ew["data"] = worst["data"]
+            ew["batches_per_step"] = wb
+            exact["worst_case"] = ew
         del ws
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:
@@ -1262,6 +1269,9 @@ def main() -> None:
                               if args.batches_per_step <= 0 else {"batches_per_step_flag": bps}),
             "samples_replayed_batches": replayed,
             "data_gen_s": round(t_gen, 1),
+            "headline_update_mode": args.update_mode,
+            "servers_default_update_mode": "exact",
+            "exact_mode_value": exact["value"] if exact else (round(value, 1) if args.update_mode == "exact" else None),
             "exact_mode": exact,
             "bf16_weights": bf16,
             "worst_case": worst,

@@ -269,16 +269,18 @@ __device__ __forceinline__ void lds_barrier() {
 
 // ------------------------------------------------------------ S0 scores
 // S0[i * LC + l]: score of label l of sample beg + i at the segment start;
-// AUX[i] = (its best active wrong label there - -1: none, |x|^2 as float
-// bits); PP0[i * 32 + f]: (P0(row_f, y), P0(row_f, that label)) of its first
-// 32 features (P != nullptr)
+// AUX[i] = (its best active wrong label there - -1: none, |x|^2, its slack
+// to the method's update threshold there - both as float bits, 0);
+// PP0[i * 32 + f]: (P0(row_f, y), P0(row_f, that label)) of its first 32
+// features (P != nullptr)
 template <int LC>
 __global__ __launch_bounds__(256) void delta_s0_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
-    const float* __restrict__ P, const int32_t* __restrict__ active, float* __restrict__ S0,
-    int2* __restrict__ AUX, float2* __restrict__ PP0, const int64_t* __restrict__ reason) {
+    const float* __restrict__ P, const int32_t* __restrict__ active, int method, float C,
+    float* __restrict__ S0, int4* __restrict__ AUX, float2* __restrict__ PP0,
+    const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   static_assert(LC <= 64, "delta committer: LC <= 64");
   if (reason != nullptr && (*reason == kStopDense || *reason == kStopDone)) return;
@@ -311,8 +313,8 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) q += __shfl_xor(q, off, 64);
     const int y = labels[s];
-    if (P == nullptr || y < 0 || y >= LC) {
-      if (lane == 0) AUX[wid] = make_int2(-1, __float_as_int(q));
+    if (y < 0 || y >= LC) {
+      if (lane == 0) AUX[wid] = make_int4(-1, __float_as_int(q), 0, 0);
       continue;
     }
     float b = (la && l0 != y) ? acc : -INFINITY;
@@ -323,7 +325,12 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
       const int ol = __shfl_xor(bl, off, 64);
       if (ol >= 0 && (bl < 0 || ob > b || (ob == b && ol < bl))) { b = ob; bl = ol; }
     }
-    if (lane == 0) AUX[wid] = make_int2(bl, __float_as_int(q));
+    // the margin at M0 and its slack (group_margin / slack_of of the committer)
+    const float sy = __shfl(acc, y, 64);
+    const float best = bl >= 0 ? b : 0.f;
+    const float sl0 = slack_of(method, sy - best, q, bl >= 0, C, sy, best);
+    if (lane == 0) AUX[wid] = make_int4(bl, __float_as_int(q), __float_as_int(sl0), 0);
+    if (P == nullptr) continue;
     if (lane < kNFMax && lane < n) {
       const int32_t idx = fidx[fb + lane];
       float2 pp = make_float2(1.f, 1.f);
@@ -355,6 +362,7 @@ struct Samp {
   float s[Geo<LC>::K];
   int ls0;
   float nrm;       // |x|^2
+  float slack0;    // slack at M0 (the segment start)
 };
 
 // ------------------------------------------------------------ committer
@@ -367,7 +375,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     const float* __restrict__ fval_k, const int32_t* __restrict__ labels_k,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* __restrict__ W,
     float* __restrict__ P, const int32_t* __restrict__ active, float C,
-    const float* __restrict__ S0_k, const int2* __restrict__ AUX_k, const float2* __restrict__ PP0_k,
+    const float* __restrict__ S0_k, const int4* __restrict__ AUX_k, const float2* __restrict__ PP0_k,
     unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
     int64_t* __restrict__ tail, int seg) {
   using Gm = Geo<LC>;
@@ -380,6 +388,8 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   __shared__ int32_t s_sst[NSLOT];    // id of the last step that wrote the slot
   __shared__ float s_sdy[NSLOT];      // that step's increment of labels y / l
   __shared__ float s_sdl[NSLOT];
+  __shared__ float s_rmax[NSLOT];     // a bound on max_l |dW[slot][l]| (sum of the |increments|)
+  __shared__ unsigned s_nexact, s_nalive;
   __shared__ int s_cn, s_stop, s_upd, s_yk, s_lk, s_nins;
   __shared__ int s_first[2];
   __shared__ unsigned s_nupd, s_waste, s_refresh;
@@ -403,10 +413,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     for (int i = tid; i < (NSLOT * LC + Gm::PAD) / 4; i += kT) { dw4[i] = z; if (use_s) dp4[i] = z; }
     for (int i = tid; i < NSLOT; i += kT) s_key[i] = -1;
     for (int i = tid; i < NSLOT; i += kT) s_sst[i] = -1;
+    for (int i = tid; i < NSLOT; i += kT) s_rmax[i] = 0.f;
     if (tid == 0) {
       s_cn = 0; s_stop = -1; s_upd = 0; s_yk = -1; s_lk = -1; s_nins = 0;
       s_first[0] = s_first[1] = kInf;
-      s_nupd = 0; s_waste = 0; s_refresh = 0;
+      s_nupd = 0; s_waste = 0; s_refresh = 0; s_nexact = 0; s_nalive = 0;
     }
   }
   int act[K];   // ints, not lane masks: every bool array held across the loop is an SGPR pair
@@ -420,7 +431,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   const float* __restrict__ fval = in_vgpr(fval_k);
   const int32_t* __restrict__ labels = in_vgpr(labels_k);
   const float* __restrict__ S0 = in_vgpr(S0_k);
-  const int2* __restrict__ AUX = in_vgpr(AUX_k);
+  const int4* __restrict__ AUX = in_vgpr(AUX_k);
   const float2* __restrict__ PP0 = in_vgpr(PP0_k);
   const int64_t beg = (int64_t)in_vgpr((uint64_t)stream_ptr[0]);
   const int64_t end = (int64_t)in_vgpr((uint64_t)stream_ptr[nstreams]);
@@ -483,9 +494,10 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         const float sv = s0p[lab < LC ? lab : LC - 1];
         sm[r].s[k] = (ok && lab < LC) ? sv : 0.f;
       }
-      const int2 aux = AUX[jc];
+      const int4 aux = AUX[jc];
       sm[r].ls0 = (use_s && ok) ? aux.x : -1;
       sm[r].nrm = ok ? __int_as_float(aux.y) : 0.f;
+      sm[r].slack0 = ok ? __int_as_float(aux.z) : 1.f;
     }
   };
 
@@ -512,10 +524,10 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     if (p + 2 * kNS < end) load_desc(p + 2 * kNS, dnn);
 
     // ---- round start: slots, deltas of the rows the segment wrote, slacks
-    int alive[kR], unsafe[kR];
+    int alive[kR], unsafe[kR], exact[kR];
     float nrm[kR], slack[kR];
     int slot[kR][kFC];
-    bool any = false, wide = false;
+    bool wide = false;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int64_t j = p + G * kR + r;
@@ -530,21 +542,57 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       slot[r][0] = ok ? cache_find<LC>(s_key, sc[r].fi[0]) : -1;
       slot[r][1] = -1;
       if (two) slot[r][1] = ok ? cache_find<LC>(s_key, sc[r].fi[1]) : -1;
-      any |= slot[r][0] >= 0 || slot[r][1] >= 0;
     }
-    // rows with a delta anywhere in the wave: the transposed correction
-    if (__builtin_amdgcn_ballot_w64(any) != 0) {
+    // samples of this wave whose slack ran out (positions > after) and are
+    // still on S0 scores: exact scores S0 + x . dW (the live deltas), exact
+    // margin and slack. Wave-uniform call; most waves have none.
+    auto make_exact = [&](int after) {
+      bool need[kR];
+      bool anyneed = false;
 #pragma unroll
-      for (int r = 0; r < kR; ++r) row_correct<LC>(s_dw, slot[r], sc[r].fx, sub, two, sc[r].s);
-    }
+      for (int r = 0; r < kR; ++r) {
+        need[r] = alive[r] && !exact[r] && dc[r].nf() <= kNFMax && G * kR + r > after && !(slack[r] > 0.f);
+        anyneed |= need[r];
+      }
+      if (__builtin_amdgcn_ballot_w64(anyneed) == 0) return;
+#pragma unroll
+      for (int r = 0; r < kR; ++r) {
+        float t[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) t[k] = sc[r].s[k];
+        row_correct<LC>(s_dw, slot[r], sc[r].fx, sub, two, t);
+        int ls;
+        float sy, best;
+        const float m = group_margin<LC>(t, dc[r].y, act, sub, &ls, &sy, &best);
+        const float sl = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
+        if (need[r]) {
+#pragma unroll
+          for (int k = 0; k < K; ++k) sc[r].s[k] = t[k];
+          slack[r] = sl;
+          exact[r] = 1;
+          if (kProf && sub == 0) atomicAdd(&s_nexact, 1u);
+        }
+      }
+    };
+    // slack at round start: the slack at M0 less a bound on what the
+    // segment's deltas moved the margin (2 sum_f |x_f| max_l |dW_f[l]|; the
+    // guard band moves by 1e-4 of it). Scores stay S0 until a sample's slack
+    // runs out; then (make_exact) it is scored exactly against M0 + dW.
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
+      float bsum = 0.f;
+#pragma unroll
+      for (int c = 0; c < kFC; ++c)
+        bsum += slot[r][c] >= 0 ? fabsf(sc[r].fx[c]) * s_rmax[slot[r][c]] : 0.f;
       nrm[r] = sc[r].nrm;
-      int ls;
-      float sy, best;
-      const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
-      slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
+      slack[r] = sc[r].slack0 - 2.f * (1.f + 4.f * kGuard) * row16_sum(bsum);
+      exact[r] = 0;
+    }
+    make_exact(-1);
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
       unsafe[r] = (alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f))) ? 1 : 0;
+      if (kProf && sub == 0 && alive[r] && dc[r].nf() <= kNFMax) atomicAdd(&s_nalive, 1u);
     }
     {
       const uint64_t t2 = cyc();
@@ -691,6 +739,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
               }
               atomicAdd(&s_sdy[sl[c]], dwy);
               atomicAdd(&s_sdl[sl[c]], dwl);
+              atomicAdd(&s_rmax[sl[c]], fmaxf(fabsf(dwy), fabsf(dwl)));
             }
           }
           if (sub == 0) {
@@ -747,22 +796,28 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           }
           cy = row16_sum(cy);
           cl = row16_sum(cl);
+          if (exact[r]) {
 #pragma unroll
-          for (int kk = 0; kk < K; ++kk) {
-            const int lab = sub + 16 * kk;
-            if (lab == yk) sc[r].s[kk] += cy;
-            if (lab == lk) sc[r].s[kk] += cl;
+            for (int kk = 0; kk < K; ++kk) {
+              const int lab = sub + 16 * kk;
+              if (lab == yk) sc[r].s[kk] += cy;
+              if (lab == lk) sc[r].s[kk] += cl;
+            }
           }
           // the margin moves by at most |cy| + |cl| (the guard band by 1e-4 of it)
           slack[r] -= (fabsf(cy) + fabsf(cl)) * (1.f + 4.f * kGuard);
-          if (!(slack[r] > 0.f)) {
+          if (exact[r] && !(slack[r] > 0.f)) {
             int ls;
             float sy, best;
             const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
             slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
-            unsafe[r] = (slack[r] > 0.f) ? 0 : 1;
           }
         }
+        // samples still on S0 scores whose bounded slack ran out
+        make_exact(k);
+#pragma unroll
+        for (int r = 0; r < kR; ++r)
+          if (G * kR + r > k) unsafe[r] = (alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f))) ? 1 : 0;
       }
       lim = k;
       {
@@ -823,6 +878,8 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     put(23, (int64_t)s_refresh);
     put(24, (int64_t)s_nupd);
     put(25, (int64_t)s_cn);
+    put(26, (int64_t)s_nexact);
+    put(27, (int64_t)s_nalive);
     if (stats != nullptr && s_nupd > 0) atomicAdd(stats, (unsigned long long)s_nupd);
   }
 }
@@ -834,11 +891,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 template <int L>
 static int launch_delta(int64_t blocks, int method, const int64_t* row_ptr, const int32_t* fidx,
                         const float* fval, const int32_t* labels, const int64_t* sp, int ns, float* W,
-                        float* S, float* Pp, const int32_t* active, float C, float* s0, int2* aux,
+                        float* S, float* Pp, const int32_t* active, float C, float* s0, int4* aux,
                         float2* pp0, unsigned long long* stats, uint8_t* touched, int64_t* tail, int seg,
                         const int64_t* why, hipStream_t stream) {
   hipLaunchKernelGGL((jb::dc::delta_s0_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream, row_ptr, fidx,
-                     fval, labels, sp, ns, W, Pp, active, s0, aux, pp0, why);
+                     fval, labels, sp, ns, W, Pp, active, method, C, s0, aux, pp0, why);
 #define JB_DELTA_M(M)                                                                                  \
   hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M>), dim3(1), dim3(jb::dc::kT), 0, stream, row_ptr, \
                      fidx, fval, labels, sp, ns, W, S, active, C, s0, aux, pp0, stats, touched, tail, seg); \
@@ -858,12 +915,12 @@ static int launch_delta(int64_t blocks, int method, const int64_t* row_ptr, cons
 }
 
 // bytes of the delta committer's scratch per sample: S0 (<= 64 floats),
-// PP0 (32 float2), AUX (int2: best wrong label at M0, |x|^2)
-extern "C" int64_t jb_delta_scratch_per_sample() { return 256 + 256 + 8; }
+// PP0 (32 float2), AUX (int4: best wrong label at M0, |x|^2, slack at M0)
+extern "C" int64_t jb_delta_scratch_per_sample() { return 256 + 256 + 16; }
 
 // Steps 1-2 of a kSerial batch for LC <= 64 (see the header); the caller
 // runs the exact single-stream kernel over [tail[0], tail[1]) afterwards.
-// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2][AUX: n_max int2].
+// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2][AUX: n_max int4].
 extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
@@ -873,7 +930,7 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
   int64_t* tail = (int64_t*)scratch;
   float* s0 = (float*)((uint8_t*)scratch + 256);
   float2* pp0 = (float2*)((uint8_t*)scratch + 256 + 256 * n_max);
-  int2* aux = (int2*)((uint8_t*)scratch + 256 + 512 * n_max);
+  int4* aux = (int4*)((uint8_t*)scratch + 256 + 512 * n_max);
   float* Pp = method >= jb::CW ? S : nullptr;
   const int64_t blocks = std::min<int64_t>((n_max * 64 + 255) / 256, 2048);
   for (int seg = 0; seg < nseg; ++seg) {

@@ -695,7 +695,10 @@ inline std::vector<std::vector<int>> push_schedule(const std::string& kind, int 
       std::swap(order[(size_t)i], order[(size_t)(x % (uint64_t)(i + 1))]);
     }
     std::vector<int> m((size_t)n, -1);
-    for (int i = 0; i + 1 < n; i += 2) { m[(size_t)order[(size_t)i]] = order[(size_t)i + 1]; m[(size_t)order[(size_t)i + 1]] = order[(size_t)i]; }
+    for (int i = 0; i + 1 < n; i += 2) {
+      m[(size_t)order[(size_t)i]] = order[(size_t)i + 1];
+      m[(size_t)order[(size_t)i + 1]] = order[(size_t)i];
+    }
     rounds.push_back(m);
   } else if (kind == "broadcast_mixer") {
     tournament(n);                     // every pair once

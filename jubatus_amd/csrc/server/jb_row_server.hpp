@@ -121,14 +121,20 @@ inline bool parse_config(Kind kind, const std::string& text, Config* c, std::str
   if (kind == Kind::kNearestNeighbor) {
     if (!is_lsh(c->outer)) { *why = "nearest_neighbor method " + c->outer; return false; }
   } else if (kind == Kind::kClassifier) {
-    if (!is_nn_classifier(c->outer)) { *why = "classifier method " + c->outer + " is not a nearest-neighbor one"; return false; }
+    if (!is_nn_classifier(c->outer)) {
+      *why = "classifier method " + c->outer + " is not a nearest-neighbor one";
+      return false;
+    }
     auto num = [&](const char* key, double d) {
       const Value* x = c->param.get(key);
       return x && x->is_num() ? x->num() : d;
     };
     c->nn_k = (int)num("nearest_neighbor_num", 128);
     c->alpha = num("local_sensitivity", 1.0);
-    if (c->nn_k <= 0 || c->alpha < 0) { *why = "nearest_neighbor_num must be positive, local_sensitivity >= 0"; return false; }
+    if (c->nn_k <= 0 || c->alpha < 0) {
+      *why = "nearest_neighbor_num must be positive, local_sensitivity >= 0";
+      return false;
+    }
     Value inner = empty;
     if (c->outer == "cosine") {
       c->inner = "inverted_index";
@@ -1072,12 +1078,14 @@ class Server {
     const std::string* sig = nullptr;
     for (const auto& x : table)
       if (x.first == m) sig = &x.second;
-    if (!sig || (m == "do_mix" && !mixer_)) return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
+    if (!sig || (m == "do_mix" && !mixer_))
+      return r.notify ? std::string() : jb::val::response_code(r.msgid, kNoMethodError);
     bool ok = args.a.size() == sig->size() + 1 && args.a[0].is_str();
     for (size_t k = 0; ok && k < sig->size(); ++k) {
       const Value& x = args.a[k + 1];
       const char c = (*sig)[k];
-      ok = c == 's' ? x.is_str() : c == 'k' ? (x.kind == Value::INT || x.kind == Value::UINT) : x.kind == Value::ARR;   // d, l: arrays
+      // s: string, k: size, d / l: arrays
+      ok = c == 's' ? x.is_str() : c == 'k' ? (x.kind == Value::INT || x.kind == Value::UINT) : x.kind == Value::ARR;
     }
     if (!ok) return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
     auto size_arg = [&](size_t i) -> int64_t {

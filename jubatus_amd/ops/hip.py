@@ -677,13 +677,15 @@ class SerialScratch:
             # delta committer (csrc/hip/commit.hip): steps that did not update,
             # guard-band re-scores, updates, rows in the LDS store at the end
             out.update(wasted_steps=v[22], refreshes=v[23], committer_updates=v[24],
-                       last_segment_rows=v[25])
+                       last_segment_rows=v[25], bound_settled=v[26], committed_samples=v[27])
         # committer phases in shader cycles, scaled to us by the wall clock
         wall_us = v[10] / 100.0
         if v[11] > 0:
             us = wall_us / v[11]
             out["commit_us"] = round(wall_us, 1)
-            for i, nm in enumerate(("bound", "barrier_a", "stage_b1", "step", "barrier_b2", "round")):
+            names = (("start", "barrier_a", "step", "corr", "flush", "init") if "committer_updates" in out
+                     else ("bound", "barrier_a", "stage_b1", "step", "barrier_b2", "round"))
+            for i, nm in enumerate(names):
                 out[f"commit_{nm}_us"] = round(v[4 + i] * us, 1)
             for w in range(8):     # per wave: round-start bounds + post-step work
                 out[f"commit_wave{w}_work_us"] = round(v[12 + w] * us, 1)

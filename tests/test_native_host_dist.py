@@ -136,13 +136,15 @@ def test_native_bandit_distributed_arm_info(coord):
         cl.mix()
         want = {"x": [4, 3.5], "y": [1, 2.0]}
         for c in cl.c:
-            info = {(k.decode() if isinstance(k, bytes) else k): list(v) for k, v in c.call("get_arm_info", "p").items()}
+            info = {(k.decode() if isinstance(k, bytes) else k): list(v)
+                    for k, v in c.call("get_arm_info", "p").items()}
             assert info == want, info
         # increments after the MIX are shipped once, not again
         a.call("register_reward", "p", "y", 1.0)
         cl.mix()
         for c in cl.c:
-            info = {(k.decode() if isinstance(k, bytes) else k): list(v) for k, v in c.call("get_arm_info", "p").items()}
+            info = {(k.decode() if isinstance(k, bytes) else k): list(v)
+                    for k, v in c.call("get_arm_info", "p").items()}
             assert info["y"] == [2, 3.0] and info["x"] == [4, 3.5], info
     finally:
         cl.close()
@@ -284,7 +286,8 @@ def test_native_graph_distributed_replicated_writes(coord):
         owner = int(cht.find(lone, 2)[0][1])
         assert by_port[owner].call("remove_node", lone) is True
         after = [int(status(c)["global_node_num"]) for c in cl.c]
-        assert all(a <= b for a, b in zip(after, before)) and after[cl.ports.index(owner)] < before[cl.ports.index(owner)]
+        oi = cl.ports.index(owner)
+        assert all(a <= b for a, b in zip(after, before)) and after[oi] < before[oi]
         s.close()
     finally:
         if solo.poll() is None:
