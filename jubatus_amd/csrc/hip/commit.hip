@@ -61,8 +61,19 @@ constexpr int kNFMax = 16 * kFC;      // widest sample the committer takes
 constexpr float kGuard = 1e-4f;       // relative guard band of a decision
 constexpr int kInf = 0x7fffffff;
 // stop reasons (tail[kTailReason]); the values are serial.hip's
-constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2;
+constexpr int64_t kStopDone = 0, kStopSaturated = 1, kStopDense = 2, kStopWindow = 3;
 constexpr int kTailReason = 20;
+// A segment scores and commits a window of the batch, not its whole rest:
+// twice the samples the previous segment took, at least kWinMin (the S0
+// pass of a segment that saturates early would otherwise re-score the whole
+// rest of the batch every time). tail[kTailWin]: samples the last segment took.
+constexpr int kTailWin = 29;
+constexpr int64_t kWinMin = 8192;
+__device__ __forceinline__ int64_t window_end(int64_t beg, int64_t end, const int64_t* tail) {
+  int64_t w = tail[kTailWin];   // the previous batch's last segment for a batch's first one
+  w = (w <= 0 || w > ((int64_t)1 << 30)) ? kWinMin : (2 * w > kWinMin ? 2 * w : kWinMin);
+  return beg + w < end ? beg + w : end;
+}
 // phase timing (tail[4..19]): shader cycles of wave 0 per phase, the wall
 // clock of the kernel and every wave's own round-start work
 constexpr bool kProf = true;
@@ -209,9 +220,9 @@ __device__ __forceinline__ int cache_insert(int32_t* key, int32_t row) {
 // Branch-free: a lane without a row reads the zero row (slot NSLOT); with
 // LC = 8 the quads past the labels read padding / the next row, which only
 // ever sums into labels >= LC (lanes 8..15), never read.
-template <int LC>
-__device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[kFC],
-                                            const float (&x)[kFC], int sub, bool two,
+template <int LC, int FC>
+__device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[FC],
+                                            const float (&x)[FC], int sub, bool two,
                                             float (&s)[Geo<LC>::K]) {
   constexpr int K = Geo<LC>::K;
   const int qs = sub >> 2;
@@ -221,7 +232,7 @@ __device__ __forceinline__ void row_correct(const float* dw, const int (&slot)[k
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int c = 0; c < kFC; ++c) {
+    for (int c = 0; c < FC; ++c) {
       if (c > 0 && !two) break;              // wave-uniform
       const float xc = x[c];
       const float* rowp = dw + (slot[c] >= 0 ? slot[c] : Geo<LC>::NSLOT) * LC + 16 * b;
@@ -263,30 +274,64 @@ __device__ __forceinline__ uint64_t in_vgpr(uint64_t x) {
 template <class T>
 __device__ __forceinline__ T* in_vgpr(T* p) { return (T*)in_vgpr((uint64_t)p); }
 
+// a load through the global address space: a pointer that went through
+// in_vgpr is generic to the compiler, and a flat load counts on lgkmcnt too,
+// so every LDS wait would also wait for the prefetches in flight
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+// HIP's vector structs copy through generic references: load native vectors
+typedef float jb_f2v __attribute__((ext_vector_type(2)));
+typedef int jb_i4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float2 gld(const float2* p) {
+  const jb_f2v v = *(const __attribute__((address_space(1))) jb_f2v*)p;
+  return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ int4 gld(const int4* p) {
+  const jb_i4v v = *(const __attribute__((address_space(1))) jb_i4v*)p;
+  return make_int4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ------------------------------------------------------------ S0 scores
-// S0[i * LC + l]: score of label l of sample beg + i at the segment start;
-// AUX[i] = (its best active wrong label there - -1: none, |x|^2, its slack
-// to the method's update threshold there - both as float bits, 0);
-// PP0[i * 32 + f]: (P0(row_f, y), P0(row_f, that label)) of its first 32
-// features (P != nullptr)
+// Per sample i of the segment (sample beg + i), everything the committer
+// reads of it, at addresses that depend on i alone (no descriptor load
+// before the feature loads, so the committer prefetches two rounds ahead):
+//   S0[i * LC + l]   score of label l at the segment start
+//   AUX[i]           (label y | best active wrong label there << 8 | feature
+//                    count << 16 - labels as int8, -1: none / invalid y;
+//                    |x|^2, the slack to the method's update threshold
+//                    there - both as float bits; 0)
+//   FI / FX[i * 32 + f]  row and value of feature f < 32 (-1 / 0 past the end)
+//   PP0[i * 32 + f]  (P0(row_f, y), P0(row_f, that label)) (P != nullptr)
+// *wide: set when a sample has more than 16 features (the committer with
+// two feature chunks per lane takes the segment)
+__device__ __forceinline__ int aux_pack(int y, int ls, int n) {
+  return (y & 0xff) | ((ls & 0xff) << 8) | ((n < 0xffff ? n : 0xffff) << 16);
+}
+__device__ __forceinline__ int aux_y(int v) { return (int)(int8_t)(v & 0xff); }
+__device__ __forceinline__ int aux_ls(int v) { return (int)(int8_t)((v >> 8) & 0xff); }
+__device__ __forceinline__ int aux_nf(int v) { return (int)((unsigned)v >> 16); }
+
 template <int LC>
 __global__ __launch_bounds__(256) void delta_s0_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels,
     const int64_t* __restrict__ stream_ptr, int nstreams, const float* __restrict__ W,
     const float* __restrict__ P, const int32_t* __restrict__ active, int method, float C,
-    float* __restrict__ S0, int4* __restrict__ AUX, float2* __restrict__ PP0,
+    float* __restrict__ S0, int4* __restrict__ AUX, float2* __restrict__ PP0, int32_t* __restrict__ FI,
+    float* __restrict__ FX, unsigned long long* __restrict__ wide, const int64_t* __restrict__ tail,
     const int64_t* __restrict__ reason) {
   using L = Lanes<LC>;
   static_assert(LC <= 64, "delta committer: LC <= 64");
   if (reason != nullptr && (*reason == kStopDense || *reason == kStopDone)) return;
   const int lane = threadIdx.x & 63;
   const int64_t beg = stream_ptr[0];
-  const int64_t cnt = stream_ptr[nstreams] - beg;
+  const int64_t cnt = window_end(beg, stream_ptr[nstreams], tail) - beg;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int g = lane / L::LW;
   const int l0 = lane % L::LW;
@@ -295,6 +340,12 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
     const int64_t s = beg + wid;
     const int64_t fb = row_ptr[s];
     const int n = (int)(row_ptr[s + 1] - fb);
+    if (lane < kNFMax) {
+      const bool in = lane < n;
+      FI[wid * kNFMax + lane] = in ? fidx[fb + lane] : -1;
+      FX[wid * kNFMax + lane] = in ? fval[fb + lane] : 0.f;
+    }
+    if (lane == 0 && n > 16) atomicOr(wide, 1ull);
     float acc = 0.f;
     for (int j = g; j < n; j += L::G) {
       const int32_t idx = fidx[fb + j];
@@ -314,7 +365,7 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
     for (int off = 1; off < 64; off <<= 1) q += __shfl_xor(q, off, 64);
     const int y = labels[s];
     if (y < 0 || y >= LC) {
-      if (lane == 0) AUX[wid] = make_int4(-1, __float_as_int(q), 0, 0);
+      if (lane == 0) AUX[wid] = make_int4(aux_pack(-1, -1, n), __float_as_int(q), 0, 0);
       continue;
     }
     float b = (la && l0 != y) ? acc : -INFINITY;
@@ -329,38 +380,47 @@ __global__ __launch_bounds__(256) void delta_s0_kernel(
     const float sy = __shfl(acc, y, 64);
     const float best = bl >= 0 ? b : 0.f;
     const float sl0 = slack_of(method, sy - best, q, bl >= 0, C, sy, best);
-    if (lane == 0) AUX[wid] = make_int4(bl, __float_as_int(q), __float_as_int(sl0), 0);
+    if (lane == 0) AUX[wid] = make_int4(aux_pack(y, bl, n), __float_as_int(q), __float_as_int(sl0), 0);
     if (P == nullptr) continue;
-    if (lane < kNFMax && lane < n) {
-      const int32_t idx = fidx[fb + lane];
+    if (lane < kNFMax) {
       float2 pp = make_float2(1.f, 1.f);
-      if (idx >= 0) {
-        pp.x = P[(int64_t)idx * LC + y];
-        if (bl >= 0) pp.y = P[(int64_t)idx * LC + bl];
+      if (lane < n) {
+        const int32_t idx = fidx[fb + lane];
+        if (idx >= 0) {
+          pp.x = P[(int64_t)idx * LC + y];
+          if (bl >= 0) pp.y = P[(int64_t)idx * LC + bl];
+        }
       }
       PP0[wid * kNFMax + lane] = pp;
     }
   }
 }
 
-// one sample's round data (group layout: lane u holds features u, u + 16).
-// The feature count is taken from the two row offsets when the descriptor is
-// used (a round after its loads), never right after they are issued: that
-// would wait out the global-load latency in the round start.
-struct Desc {
-  int64_t fb, fe;
-  int y;
-  __device__ __forceinline__ int nf() const { return (int)(fe - fb); }
+// one sample's record as loaded (group layout: lane u holds features u,
+// u + 16); nothing reads it until the round it belongs to, so its loads stay
+// in flight for PD rounds
+template <int LC, int FC>
+struct Raw {
+  int32_t fi[FC];
+  float fx[FC];
+  float2 pp[FC];
+  float s[Geo<LC>::K];
+  int aux;       // AUX .x (labels, feature count)
+  float nrm;     // AUX .y (read only by the methods that use |x|^2)
+  float slack0;  // AUX .z
 };
 
-template <int LC>
+// one sample's round data
+template <int LC, int FC>
 struct Samp {
-  int32_t fi[kFC];
-  float fx[kFC];
-  float py[kFC];   // P0(row, y), P0(row, ls0)
-  float pl[kFC];
+  int32_t fi[FC];
+  float fx[FC];
+  float py[FC];    // P0(row, y), P0(row, ls0)
+  float pl[FC];
   float s[Geo<LC>::K];
+  int y;           // -1: no sample / label out of range
   int ls0;
+  int nf;
   float nrm;       // |x|^2
   float slack0;    // slack at M0 (the segment start)
 };
@@ -368,20 +428,24 @@ struct Samp {
 // ------------------------------------------------------------ committer
 // MT: the method, a template argument - the step's coefficient code, the
 // precision path (CW / AROW / NHERD) and the slack thresholds fold away for
-// the other methods
-template <int LC, int MT>
+// the other methods. FC: feature chunks of 16 a lane holds (1: samples of at
+// most 16 features, the registers it frees buy a deeper prefetch; 2: up to
+// 32). Both are launched per segment; *wide (the S0 pass) picks one.
+template <int LC, int MT, int FC>
 __global__ __launch_bounds__(kT) void delta_commit_kernel(
-    const int64_t* __restrict__ row_ptr_k, const int32_t* __restrict__ fidx_k,
-    const float* __restrict__ fval_k, const int32_t* __restrict__ labels_k,
     const int64_t* __restrict__ stream_ptr, int nstreams, float* __restrict__ W,
     float* __restrict__ P, const int32_t* __restrict__ active, float C,
     const float* __restrict__ S0_k, const int4* __restrict__ AUX_k, const float2* __restrict__ PP0_k,
-    unsigned long long* __restrict__ stats, uint8_t* __restrict__ touched,
-    int64_t* __restrict__ tail, int seg) {
+    const int32_t* __restrict__ FI_k, const float* __restrict__ FX_k,
+    unsigned long long* __restrict__ wide, unsigned long long* __restrict__ stats,
+    uint8_t* __restrict__ touched, int64_t* __restrict__ tail, int seg) {
   using Gm = Geo<LC>;
+  using S = Samp<LC, FC>;
   constexpr int K = Gm::K;
   constexpr int NSLOT = Gm::NSLOT;
+  constexpr int NFM = 16 * FC;        // widest sample this variant takes
   if (seg > 0 && (tail[kTailReason] == kStopDense || tail[kTailReason] == kStopDone)) return;
+  if ((*wide != 0) != (FC == 2)) return;
   __shared__ __attribute__((aligned(16))) float s_dw[NSLOT * LC + Gm::PAD];
   __shared__ __attribute__((aligned(16))) float s_dp[NSLOT * LC + Gm::PAD];
   __shared__ __attribute__((aligned(16))) int32_t s_key[NSLOT];   // row of each slot (-1: free)
@@ -401,6 +465,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   const int wv = tid >> 6;
   constexpr int method = MT;
   constexpr bool use_s = MT >= CW;
+  constexpr bool use_nrm = MT == PA || MT == PA1 || MT == PA2 || MT == CW;   // |x|^2 (slack_of, step_coeffs)
   const uint64_t t_k0 = cyc();
   const uint64_t w_k0 = kProf ? __builtin_amdgcn_s_memrealtime() : 0;
   uint64_t ph[6] = {0, 0, 0, 0, 0, 0};   // start, barrier A, step, corrections, flush, init
@@ -426,86 +491,74 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     const int lab = sub + 16 * k;
     act[k] = (lab < LC && active[lab] != 0) ? 1 : 0;
   }
-  const int64_t* __restrict__ row_ptr = in_vgpr(row_ptr_k);
-  const int32_t* __restrict__ fidx = in_vgpr(fidx_k);
-  const float* __restrict__ fval = in_vgpr(fval_k);
-  const int32_t* __restrict__ labels = in_vgpr(labels_k);
   const float* __restrict__ S0 = in_vgpr(S0_k);
   const int4* __restrict__ AUX = in_vgpr(AUX_k);
   const float2* __restrict__ PP0 = in_vgpr(PP0_k);
+  const int32_t* __restrict__ FI = in_vgpr(FI_k);
+  const float* __restrict__ FX = in_vgpr(FX_k);
+  // [beg, end): this segment's window; bend: the batch end
+  const int64_t bend = stream_ptr[nstreams];
   const int64_t beg = (int64_t)in_vgpr((uint64_t)stream_ptr[0]);
-  const int64_t end = (int64_t)in_vgpr((uint64_t)stream_ptr[nstreams]);
+  const int64_t end = (int64_t)in_vgpr((uint64_t)window_end(stream_ptr[0], bend, tail));
 
-  // two-deep prefetch: descriptors two rounds ahead, features / S0 one round ahead
-  auto load_desc = [&](int64_t p, Desc (&d)[kR]) {
+  // sample loads PD rounds ahead, at addresses of the sample index alone;
+  // no branches: a position past the batch reads the last sample's record
+  // (the round that uses it selects the neutral values)
+  using R = Raw<LC, FC>;
+  auto load_raw = [&](int64_t p, R (&rw)[kR]) {
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const int64_t j = p + G * kR + r;
-      if (j < end) {
-        d[r].y = labels[j];
-        d[r].fb = row_ptr[j];
-        d[r].fe = row_ptr[j + 1];
-      } else {
-        d[r].y = -1; d[r].fb = 0; d[r].fe = 0;
+      int64_t jc = (j < end ? j : end - 1) - beg;
+      jc = jc < 0 ? 0 : jc;             // an empty range reads record 0 (the scratch holds >= 1)
+#pragma unroll
+      for (int c = 0; c < FC; ++c) {
+        const int64_t o = jc * kNFMax + c * 16 + sub;
+        rw[r].fi[c] = gld(FI + o);
+        rw[r].fx[c] = gld(FX + o);
+        if (use_s) rw[r].pp[c] = gld(PP0 + o);
       }
-    }
-  };
-  // Loads without branches: every address is clamped into the batch (the
-  // features [F0, F1], the samples [beg, end)) and a lane that has nothing
-  // there selects its neutral value instead; the second feature chunk is
-  // loaded only when a sample of the wave has one (wave-uniform).
-  const int64_t F0 = (int64_t)in_vgpr((uint64_t)row_ptr_k[stream_ptr[0]]);
-  const int64_t F1 = (int64_t)in_vgpr((uint64_t)row_ptr_k[stream_ptr[nstreams]]) - 1;
-  const bool has_feat = F1 >= F0;
-  auto load_samp = [&](int64_t p, const Desc (&d)[kR], Samp<LC> (&sm)[kR]) {
-    bool wide2 = false;
-#pragma unroll
-    for (int r = 0; r < kR; ++r) wide2 |= d[r].nf() > 16;
-    const bool two2 = __builtin_amdgcn_ballot_w64(wide2) != 0;
-#pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      const int64_t j = p + G * kR + r;
-      const int64_t jc = (j < end ? j : end - 1) - beg;
-      const bool ok = j < end && d[r].y >= 0 && d[r].y < LC;
-#pragma unroll
-      for (int c = 0; c < kFC; ++c) {
-        sm[r].fi[c] = -1;
-        sm[r].fx[c] = 0.f;
-        sm[r].py[c] = 1.f;
-        sm[r].pl[c] = 1.f;
-        if ((c > 0 && !two2) || !has_feat) continue;      // wave-uniform
-        const bool v = ok && c * 16 + sub < d[r].nf();
-        int64_t fi = d[r].fb + c * 16 + sub;
-        fi = fi < F0 ? F0 : (fi > F1 ? F1 : fi);
-        const int32_t ix = fidx[fi];
-        const float xv = fval[fi];
-        sm[r].fi[c] = v ? ix : -1;
-        sm[r].fx[c] = v ? xv : 0.f;
-        if (use_s) {
-          const float2 q = PP0[jc * kNFMax + c * 16 + sub];
-          sm[r].py[c] = v ? q.x : 1.f;
-          sm[r].pl[c] = v ? q.y : 1.f;
-        }
-      }
-      const float* s0p = S0 + jc * LC;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
         const int lab = sub + 16 * k;
-        const float sv = s0p[lab < LC ? lab : LC - 1];
-        sm[r].s[k] = (ok && lab < LC) ? sv : 0.f;
+        rw[r].s[k] = gld(S0 + jc * LC + (lab < LC ? lab : LC - 1));
       }
-      const int4 aux = AUX[jc];
-      sm[r].ls0 = (use_s && ok) ? aux.x : -1;
-      sm[r].nrm = ok ? __int_as_float(aux.y) : 0.f;
-      sm[r].slack0 = ok ? __int_as_float(aux.z) : 1.f;
+      // only the words the method reads: a loaded register nothing reads
+      // is reused at once, and that write waits for the load (vmcnt(0))
+      const int* a = reinterpret_cast<const int*>(AUX + jc);
+      rw[r].aux = gld(a);
+      rw[r].slack0 = __int_as_float(gld(a + 2));
+      if (use_nrm) rw[r].nrm = __int_as_float(gld(a + 1));
+    }
+  };
+  auto unpack = [&](int64_t p, const R (&rw)[kR], S (&sm)[kR]) {
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const bool ok = p + G * kR + r < end;
+#pragma unroll
+      for (int c = 0; c < FC; ++c) {
+        sm[r].fi[c] = ok ? rw[r].fi[c] : -1;
+        sm[r].fx[c] = ok ? rw[r].fx[c] : 0.f;
+        sm[r].py[c] = (use_s && ok) ? rw[r].pp[c].x : 1.f;
+        sm[r].pl[c] = (use_s && ok) ? rw[r].pp[c].y : 1.f;
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) sm[r].s[k] = (ok && sub + 16 * k < LC) ? rw[r].s[k] : 0.f;
+      const int aux = rw[r].aux;
+      sm[r].y = ok ? aux_y(aux) : -1;
+      sm[r].ls0 = (use_s && ok) ? aux_ls(aux) : -1;
+      sm[r].nf = ok ? aux_nf(aux) : 0;
+      sm[r].nrm = (use_nrm && ok) ? rw[r].nrm : 0.f;
+      sm[r].slack0 = ok ? rw[r].slack0 : 1.f;
     }
   };
 
-  Desc dc[kR], dn[kR], dnn[kR];
-  Samp<LC> sc[kR], sn[kR];
-  load_desc(beg, dn);
-  load_samp(beg, dn, sn);
-  load_desc(beg + kNS, dnn);
+  // pf[i]: the records of round p + i kNS (prefetch depth PD)
+  constexpr int PD = FC == 1 ? 3 : 2;
+  S sc[kR];
+  R pf[PD][kR];
+#pragma unroll
+  for (int i = 0; i < PD; ++i) load_raw(beg + i * kNS, pf[i]);
   __syncthreads();
   ph[5] = cyc() - t_k0;
 
@@ -516,32 +569,29 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   int n_steps = 0;
   int64_t n_rounds = 0;
 
-  for (int64_t p = beg; p < end; p += kNS) {
-    uint64_t tt = cyc();
-#pragma unroll
-    for (int r = 0; r < kR; ++r) { dc[r] = dn[r]; sc[r] = sn[r]; dn[r] = dnn[r]; }
-    if (p + kNS < end) load_samp(p + kNS, dn, sn);
-    if (p + 2 * kNS < end) load_desc(p + 2 * kNS, dnn);
+  // one round at p (the samples p .. p + kNS - 1, already in sc)
+  auto round = [&](int64_t p, uint64_t tt) __attribute__((always_inline)) {
 
     // ---- round start: slots, deltas of the rows the segment wrote, slacks
     int alive[kR], unsafe[kR], exact[kR];
-    float nrm[kR], slack[kR];
-    int slot[kR][kFC];
-    bool wide = false;
+    float slack[kR];
+    int slot[kR][FC];
+    bool widew = false;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      const int64_t j = p + G * kR + r;
-      alive[r] = (j < end && dc[r].y >= 0 && dc[r].y < LC) ? 1 : 0;
-      wide |= alive[r] && dc[r].nf() > 16;
+      alive[r] = (sc[r].y >= 0 && sc[r].y < LC) ? 1 : 0;
+      widew |= alive[r] && sc[r].nf > 16;
     }
     // the second feature chunk only when a sample of the wave has one
-    const bool two = __builtin_amdgcn_ballot_w64(wide) != 0;
+    const bool two = FC == 2 && __builtin_amdgcn_ballot_w64(widew) != 0;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      const bool ok = alive[r] && dc[r].nf() <= kNFMax;
+      const bool ok = alive[r] && sc[r].nf <= NFM;
       slot[r][0] = ok ? cache_find<LC>(s_key, sc[r].fi[0]) : -1;
-      slot[r][1] = -1;
-      if (two) slot[r][1] = ok ? cache_find<LC>(s_key, sc[r].fi[1]) : -1;
+      if (FC == 2) {
+        slot[r][FC - 1] = -1;
+        if (two) slot[r][FC - 1] = ok ? cache_find<LC>(s_key, sc[r].fi[FC - 1]) : -1;
+      }
     }
     // samples of this wave whose slack ran out (positions > after) and are
     // still on S0 scores: exact scores S0 + x . dW (the live deltas), exact
@@ -551,7 +601,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       bool anyneed = false;
 #pragma unroll
       for (int r = 0; r < kR; ++r) {
-        need[r] = alive[r] && !exact[r] && dc[r].nf() <= kNFMax && G * kR + r > after && !(slack[r] > 0.f);
+        need[r] = alive[r] && !exact[r] && sc[r].nf <= NFM && G * kR + r > after && !(slack[r] > 0.f);
         anyneed |= need[r];
       }
       if (__builtin_amdgcn_ballot_w64(anyneed) == 0) return;
@@ -560,11 +610,11 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         float t[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) t[k] = sc[r].s[k];
-        row_correct<LC>(s_dw, slot[r], sc[r].fx, sub, two, t);
+        row_correct<LC, FC>(s_dw, slot[r], sc[r].fx, sub, two, t);
         int ls;
         float sy, best;
-        const float m = group_margin<LC>(t, dc[r].y, act, sub, &ls, &sy, &best);
-        const float sl = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
+        const float m = group_margin<LC>(t, sc[r].y, act, sub, &ls, &sy, &best);
+        const float sl = slack_of(method, m, sc[r].nrm, ls >= 0, C, sy, best);
         if (need[r]) {
 #pragma unroll
           for (int k = 0; k < K; ++k) sc[r].s[k] = t[k];
@@ -582,17 +632,16 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     for (int r = 0; r < kR; ++r) {
       float bsum = 0.f;
 #pragma unroll
-      for (int c = 0; c < kFC; ++c)
+      for (int c = 0; c < FC; ++c)
         bsum += slot[r][c] >= 0 ? fabsf(sc[r].fx[c]) * s_rmax[slot[r][c]] : 0.f;
-      nrm[r] = sc[r].nrm;
       slack[r] = sc[r].slack0 - 2.f * (1.f + 4.f * kGuard) * row16_sum(bsum);
       exact[r] = 0;
     }
     make_exact(-1);
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-      unsafe[r] = (alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f))) ? 1 : 0;
-      if (kProf && sub == 0 && alive[r] && dc[r].nf() <= kNFMax) atomicAdd(&s_nalive, 1u);
+      unsafe[r] = (alive[r] && (sc[r].nf > NFM || !(slack[r] > 0.f))) ? 1 : 0;
+      if (kProf && sub == 0 && alive[r] && sc[r].nf <= NFM) atomicAdd(&s_nalive, 1u);
     }
     {
       const uint64_t t2 = cyc();
@@ -627,29 +676,27 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       if (G == k / kR) {
         // ---------------- the exact step of sample k (this group's 16 lanes)
         const int rk = k % kR;
-        Samp<LC> t = sc[0];
-        Desc dd = dc[0];
-        float tn = nrm[0];
-        int sl[kFC];
+        S t = sc[0];
+        int sl[FC];
 #pragma unroll
-        for (int c = 0; c < kFC; ++c) sl[c] = slot[0][c];
+        for (int c = 0; c < FC; ++c) sl[c] = slot[0][c];
 #pragma unroll
         for (int r = 1; r < kR; ++r)
           if (r == rk) {
-            t = sc[r]; dd = dc[r]; tn = nrm[r];
+            t = sc[r];
 #pragma unroll
-            for (int c = 0; c < kFC; ++c) sl[c] = slot[r][c];
+            for (int c = 0; c < FC; ++c) sl[c] = slot[r][c];
           }
-        const int y = dd.y;
+        const int y = t.y;
         if (sub == 0) { s_nins = 0; s_upd = 0; }
         // the sample's rows not in the store yet are added first (a step
         // that then does not update leaves them with zero deltas); a full
         // bucket pair ends the segment before anything is applied
         int nnew = 0;
         bool full = false;
-        if (dd.nf() <= kNFMax) {
+        if (t.nf <= NFM) {
 #pragma unroll
-          for (int c = 0; c < kFC; ++c) {
+          for (int c = 0; c < FC; ++c) {
             const bool need = t.fi[c] >= 0 && sl[c] < 0;
             nnew += __popcll(__builtin_amdgcn_ballot_w64(need));
             if (need) {
@@ -659,20 +706,20 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           }
           full = __builtin_amdgcn_ballot_w64(full) != 0;
         }
-        if (dd.nf() > kNFMax) {
+        if (t.nf > NFM) {
           if (sub == 0) s_stop = (int)kStopDense;
         } else if (full) {
           if (sub == 0) s_stop = (int)kStopSaturated;
         } else {
           int ls = -1;
           float m = 0.f, sy = 0.f, best = 0.f, var = 0.f;
-          float py[kFC], pl[kFC];
+          float py[FC], pl[FC];
           bool refreshed = false;
           for (;;) {
             m = group_margin<LC>(t.s, y, act, sub, &ls, &sy, &best);
             float v = 0.f;
 #pragma unroll
-            for (int c = 0; c < kFC; ++c) {
+            for (int c = 0; c < FC; ++c) {
               py[c] = 1.f;
               pl[c] = 1.f;
               const int32_t row = t.fi[c];
@@ -698,7 +745,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 #pragma unroll
             for (int kk = 0; kk < K; ++kk) ns[kk] = 0.f;
 #pragma unroll
-            for (int c = 0; c < kFC; ++c) {
+            for (int c = 0; c < FC; ++c) {
 #pragma unroll 1
               for (int u = 0; u < 16; ++u) {
                 const int32_t ru = __shfl(t.fi[c], (lane & 48) + u, 64);
@@ -716,13 +763,13 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
             for (int kk = 0; kk < K; ++kk) t.s[kk] = ns[kk];
           }
           float tau = 0.f, beta = 0.f;
-          const bool up = step_coeffs(method, m, var, tn, ls >= 0, C, &tau, &beta);
+          const bool up = step_coeffs(method, m, var, t.nrm, ls >= 0, C, &tau, &beta);
           if (up) {
 #pragma unroll
-            for (int c = 0; c < kFC; ++c)
+            for (int c = 0; c < FC; ++c)
               if (t.fi[c] >= 0) { s_sst[sl[c]] = sid; s_sdy[sl[c]] = 0.f; s_sdl[sl[c]] = 0.f; }
 #pragma unroll
-            for (int c = 0; c < kFC; ++c) {
+            for (int c = 0; c < FC; ++c) {
               if (t.fi[c] < 0) continue;
               const float x = t.fx[c];
               const float a = use_s ? 1.f / py[c] : 1.f;
@@ -775,7 +822,7 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
         for (int r = 0; r < kR; ++r) {
           if (G * kR + r <= k) continue;
 #pragma unroll
-          for (int c = 0; c < kFC; ++c)
+          for (int c = 0; c < FC; ++c)
             if (slot[r][c] < 0 && sc[r].fi[c] >= 0) slot[r][c] = cache_find<LC>(s_key, sc[r].fi[c]);
         }
       }
@@ -784,10 +831,10 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
           const int pos = G * kR + r;
-          if (!alive[r] || pos <= k || dc[r].nf() > kNFMax) continue;
+          if (!alive[r] || pos <= k || sc[r].nf > NFM) continue;
           float cy = 0.f, cl = 0.f;
 #pragma unroll
-          for (int c = 0; c < kFC; ++c) {
+          for (int c = 0; c < FC; ++c) {
             const int s = slot[r][c];
             if (s >= 0 && s_sst[s] == sid) {
               cy += sc[r].fx[c] * s_sdy[s];
@@ -809,15 +856,15 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
           if (exact[r] && !(slack[r] > 0.f)) {
             int ls;
             float sy, best;
-            const float m = group_margin<LC>(sc[r].s, dc[r].y, act, sub, &ls, &sy, &best);
-            slack[r] = slack_of(method, m, nrm[r], ls >= 0, C, sy, best);
+            const float m = group_margin<LC>(sc[r].s, sc[r].y, act, sub, &ls, &sy, &best);
+            slack[r] = slack_of(method, m, sc[r].nrm, ls >= 0, C, sy, best);
           }
         }
         // samples still on S0 scores whose bounded slack ran out
         make_exact(k);
 #pragma unroll
         for (int r = 0; r < kR; ++r)
-          if (G * kR + r > k) unsafe[r] = (alive[r] && (dc[r].nf() > kNFMax || !(slack[r] > 0.f))) ? 1 : 0;
+          if (G * kR + r > k) unsafe[r] = (alive[r] && (sc[r].nf > NFM || !(slack[r] > 0.f))) ? 1 : 0;
       }
       lim = k;
       {
@@ -832,7 +879,23 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
       for (int r = 0; r < kR; ++r)
         if (alive[r] && G * kR + r < rstop) ++n_valid;
     }
-    if (stop != end) break;
+  };
+  // the round loop unrolled PD times: round u of an iteration reads prefetch
+  // slot u and refills it PD rounds ahead, so no slot is ever copied (a copy
+  // of a register a load is still writing waits for that load)
+  for (int64_t p0 = beg; p0 < end && stop == end; p0 += PD * kNS) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      // the refill is issued whether or not the round runs: the loads then
+      // leave in the same order on every path, so each round waits only for
+      // its own slot (a path that skipped a refill would make the compiler
+      // drain every load in flight)
+      const int64_t p = p0 + u * kNS;
+      const uint64_t tt = cyc();
+      unpack(p, pf[u], sc);
+      load_raw(p + PD * kNS, pf[u]);     // clamped: past the end it re-reads the last record
+      if (p < end && stop == end) round(p, tt);
+    }
   }
   __syncthreads();
   const uint64_t t_f0 = cyc();
@@ -863,9 +926,12 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
   auto put = [&](int i, int64_t v) { tail[i] = seg == 0 ? v : tail[i] + v; };
   if (kProf && lane == 0 && tid > 0) put(12 + wv, (int64_t)wwork);
   if (tid == 0) {
+    if (stop == end && end < bend) why = kStopWindow;   // the next segment takes the next window
     tail[0] = stop;
-    tail[1] = end;
+    tail[1] = bend;
     tail[kTailReason] = why;
+    tail[kTailWin] = stop - beg;
+    *wide = 0;                // the next segment's S0 pass sets it again
     put(2, n_steps);
     put(3, n_rounds);
     ph[4] = cyc() - t_f0;
@@ -887,18 +953,22 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
 }  // namespace dc
 }  // namespace jb
 
-// one segment: the S0 pass, then the committer of the method
+// one segment: the S0 pass, then the committers of the method (one chunk /
+// two chunks per lane; the S0 pass's wide flag lets one of them run)
 template <int L>
 static int launch_delta(int64_t blocks, int method, const int64_t* row_ptr, const int32_t* fidx,
                         const float* fval, const int32_t* labels, const int64_t* sp, int ns, float* W,
                         float* S, float* Pp, const int32_t* active, float C, float* s0, int4* aux,
-                        float2* pp0, unsigned long long* stats, uint8_t* touched, int64_t* tail, int seg,
+                        float2* pp0, int32_t* fi, float* fx, unsigned long long* wide,
+                        unsigned long long* stats, uint8_t* touched, int64_t* tail, int seg,
                         const int64_t* why, hipStream_t stream) {
   hipLaunchKernelGGL((jb::dc::delta_s0_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream, row_ptr, fidx,
-                     fval, labels, sp, ns, W, Pp, active, method, C, s0, aux, pp0, why);
-#define JB_DELTA_M(M)                                                                                  \
-  hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M>), dim3(1), dim3(jb::dc::kT), 0, stream, row_ptr, \
-                     fidx, fval, labels, sp, ns, W, S, active, C, s0, aux, pp0, stats, touched, tail, seg); \
+                     fval, labels, sp, ns, W, Pp, active, method, C, s0, aux, pp0, fi, fx, wide, tail, why);
+#define JB_DELTA_M(M)                                                                                     \
+  hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M, 1>), dim3(1), dim3(jb::dc::kT), 0, stream, sp, ns, \
+                     W, S, active, C, s0, aux, pp0, fi, fx, wide, stats, touched, tail, seg);              \
+  hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M, 2>), dim3(1), dim3(jb::dc::kT), 0, stream, sp, ns, \
+                     W, S, active, C, s0, aux, pp0, fi, fx, wide, stats, touched, tail, seg);              \
   break;
   switch (method) {
     case jb::PERCEPTRON: JB_DELTA_M(jb::PERCEPTRON)
@@ -915,12 +985,13 @@ static int launch_delta(int64_t blocks, int method, const int64_t* row_ptr, cons
 }
 
 // bytes of the delta committer's scratch per sample: S0 (<= 64 floats),
-// PP0 (32 float2), AUX (int4: best wrong label at M0, |x|^2, slack at M0)
-extern "C" int64_t jb_delta_scratch_per_sample() { return 256 + 256 + 16; }
+// PP0 (32 float2), FI / FX (32 ints / floats), AUX (int4)
+extern "C" int64_t jb_delta_scratch_per_sample() { return 256 + 256 + 128 + 128 + 16; }
 
 // Steps 1-2 of a kSerial batch for LC <= 64 (see the header); the caller
 // runs the exact single-stream kernel over [tail[0], tail[1]) afterwards.
-// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2][AUX: n_max int4].
+// scratch: [tail int64 x 32][S0: n_max x 64 floats][PP0: n_max x 32 float2]
+// [FI: n_max x 32][FX: n_max x 32][AUX: n_max int4]; tail[28] is the wide flag.
 extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
                                 int64_t n_max, float* W, float* S, const int32_t* active, int LC,
@@ -928,9 +999,14 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
                                 void* scratch, int nseg, hipStream_t stream) {
   if (LC > 64) return -1;
   int64_t* tail = (int64_t*)scratch;
-  float* s0 = (float*)((uint8_t*)scratch + 256);
-  float2* pp0 = (float2*)((uint8_t*)scratch + 256 + 256 * n_max);
-  int4* aux = (int4*)((uint8_t*)scratch + 256 + 512 * n_max);
+  uint8_t* base = (uint8_t*)scratch + 256;
+  float* s0 = (float*)base;
+  float2* pp0 = (float2*)(base + 256 * n_max);
+  int32_t* fi = (int32_t*)(base + 512 * n_max);
+  float* fx = (float*)(base + 640 * n_max);
+  int4* aux = (int4*)(base + 768 * n_max);
+  unsigned long long* wide = (unsigned long long*)(tail + 28);
+  if (hipMemsetAsync(wide, 0, sizeof(*wide), stream) != hipSuccess) return -2;
   float* Pp = method >= jb::CW ? S : nullptr;
   const int64_t blocks = std::min<int64_t>((n_max * 64 + 255) / 256, 2048);
   for (int seg = 0; seg < nseg; ++seg) {
@@ -938,17 +1014,18 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
     const int ns = seg == 0 ? nstreams : 1;
     const int64_t* why = seg == 0 ? nullptr : tail + jb::dc::kTailReason;
     int rc = 0;
+#define JB_DELTA_L(L)                                                                                      \
+  rc = launch_delta<L>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0, aux, \
+                       pp0, fi, fx, wide, stats, touched, tail, seg, why, stream);                        \
+  break;
     switch (LC) {
-      case 8: rc = launch_delta<8>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
-                                   aux, pp0, stats, touched, tail, seg, why, stream); break;
-      case 16: rc = launch_delta<16>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
-                                     aux, pp0, stats, touched, tail, seg, why, stream); break;
-      case 32: rc = launch_delta<32>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
-                                     aux, pp0, stats, touched, tail, seg, why, stream); break;
-      case 64: rc = launch_delta<64>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0,
-                                     aux, pp0, stats, touched, tail, seg, why, stream); break;
+      case 8: JB_DELTA_L(8)
+      case 16: JB_DELTA_L(16)
+      case 32: JB_DELTA_L(32)
+      case 64: JB_DELTA_L(64)
       default: return -1;
     }
+#undef JB_DELTA_L
     if (rc) return rc;
   }
   return (int)hipGetLastError();
