@@ -495,6 +495,63 @@ class Model : public jb::mix::Mixable {
   }
 
   // ------------------------------------------------------------- queries
+  // Analysis calls handed over by the RPC batch thread (every queued
+  // similar_row_* / neighbor_row_* / calc_score of one method): validated
+  // here, then run as ONE batch on this thread - no RPC worker blocks on a
+  // query, so the batch size follows the requests in flight, not the -c
+  // worker count.
+  enum CallKind { kCallDatum = 0, kCallId = 1, kCallScore = 2 };
+  struct Call {
+    CallKind what = kCallDatum;
+    const Value* dv = nullptr;   // kCallDatum, kCallScore
+    std::string id;              // kCallId
+    int64_t k = 0;
+    bool similar = true;
+    std::vector<std::pair<std::string, double>> res;
+    double score = 0.0;
+    std::exception_ptr err;
+  };
+  void run_calls(std::vector<Call>& cs) {
+    std::vector<QReq> reqs(cs.size());
+    std::vector<QReq*> ptrs;
+    for (size_t i = 0; i < cs.size(); ++i) {
+      Call& c = cs[i];
+      QReq& r = reqs[i];
+      try {
+        if (c.what == kCallId) {
+          r.kind = QReq::kId;
+          r.id = c.id;
+          r.k = c.k <= 0 ? 0 : clamp_k(c.k);
+          r.neg_k = c.k <= 0;
+          r.similar = c.similar;
+        } else {
+          Datum chk;
+          jb::row::parse_datum(*c.dv, &chk);           // validate first (ARGUMENT_ERROR)
+          if (c.what == kCallDatum && c.k <= 0) continue;
+          MsgpackWriter w;
+          write_value(w, *c.dv);
+          r.datum = std::move(w.out);
+          r.kind = c.what == kCallScore ? (int)QReq::kScore : (int)QReq::kDatum;
+          r.k = c.what == kCallScore ? cfg_.k : clamp_k(c.k);
+          r.similar = c.similar;
+        }
+        ptrs.push_back(&r);
+      } catch (...) {
+        c.err = std::current_exception();
+      }
+    }
+    if (!ptrs.empty()) {
+      std::lock_guard<std::mutex> g(run_mu_);
+      run_batch(ptrs);
+    }
+    for (size_t i = 0; i < cs.size(); ++i) {
+      if (cs[i].err) continue;
+      cs[i].err = reqs[i].err;
+      cs[i].res = std::move(reqs[i].res);
+      cs[i].score = reqs[i].score;
+    }
+  }
+
   std::vector<std::pair<std::string, double>> query_id(const std::string& id, int64_t k, bool similar) {
     QReq r;
     r.kind = QReq::kId;
@@ -820,7 +877,10 @@ class Model : public jb::mix::Mixable {
         take.assign(q_.begin(), q_.end());
         q_.clear();
       }
-      run_batch(take);
+      {
+        std::lock_guard<std::mutex> g(run_mu_);
+        run_batch(take);
+      }
       {
         std::lock_guard<std::mutex> lk(qmu_);
         for (QReq* r : take) r->done = true;
@@ -952,6 +1012,7 @@ class Model : public jb::mix::Mixable {
   std::shared_mutex mu_;      // the model: updates exclusive, analysis shared
   std::mutex hash_mu_;        // the converter's hashers (scratch state) under a shared lock
   std::mutex qmu_;            // the batcher's queue
+  std::mutex run_mu_;         // one run_batch at a time (the engine's query buffers, the stream)
   std::condition_variable qcv_, dcv_;
   std::deque<QReq*> q_;
   bool stop_ = false;
@@ -996,6 +1057,19 @@ class Server {
   int run() {
     rpc_.reset(new jb::RpcServer([this](const jb::RpcRequest& r) { return dispatch(r); }, a_.threads, 0.0));
     rpc_->set_io_threads(std::max(1, a_.threads / 4));
+    // analysis RPCs bypass the workers: the batch thread serves everything
+    // queued of one method with one device pass (Model::run_calls)
+    std::vector<std::string> qm;
+    if (kind_ == Kind::kRecommender || kind_ == Kind::kNearestNeighbor)
+      qm = {"similar_row_from_datum", "similar_row_from_id"};
+    if (kind_ == Kind::kNearestNeighbor) {
+      qm.push_back("neighbor_row_from_datum");
+      qm.push_back("neighbor_row_from_id");
+    }
+    if (kind_ == Kind::kAnomaly) qm = {"calc_score"};
+    if (!qm.empty())
+      rpc_->set_batch(qm, [this](const std::string& m, std::vector<jb::RpcRequest>& rs) { return query_batch(m, rs); },
+                      1024);
     int port;
     try {
       port = rpc_->listen(a_.bind, a_.port);
@@ -1041,6 +1115,60 @@ class Server {
  private:
   std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
   const char* type() const { return kind_name(kind_); }
+
+  // one batch of analysis requests of method m (see run()): malformed ones
+  // answer as dispatch() would, the rest run as one Model::run_calls
+  std::vector<std::string> query_batch(const std::string& m, std::vector<jb::RpcRequest>& rs) {
+    std::vector<std::string> out(rs.size());
+    std::vector<Value> args(rs.size());
+    std::vector<Model::Call> calls;
+    std::vector<size_t> at;
+    const bool score = m == "calc_score";
+    const bool by_id = m == "similar_row_from_id" || m == "neighbor_row_from_id";
+    for (size_t i = 0; i < rs.size(); ++i) {
+      const jb::RpcRequest& r = rs[i];
+      bool ok = true;
+      try {
+        args[i] = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
+      } catch (const std::exception&) {
+        ok = false;
+      }
+      const Value& a = args[i];
+      ok = ok && a.kind == Value::ARR && a.a.size() == (score ? 2u : 3u) && a.a[0].is_str() &&
+           (by_id ? a.a[1].is_str() : a.a[1].kind == Value::ARR) &&
+           (score || a.a[2].kind == Value::INT || a.a[2].kind == Value::UINT);
+      if (!ok) {
+        out[i] = r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+        continue;
+      }
+      Model::Call c;
+      c.what = score ? Model::kCallScore : by_id ? Model::kCallId : Model::kCallDatum;
+      if (by_id) c.id = a.a[1].s; else c.dv = &a.a[1];
+      if (!score) {
+        const Value& x = a.a[2];
+        c.k = x.kind == Value::UINT ? (int64_t)std::min<uint64_t>(x.u, (uint64_t)INT64_MAX) : x.i;
+      }
+      c.similar = m.compare(0, 7, "similar") == 0;
+      calls.push_back(std::move(c));
+      at.push_back(i);
+    }
+    model_->run_calls(calls);
+    for (size_t j = 0; j < calls.size(); ++j) {
+      const jb::RpcRequest& r = rs[at[j]];
+      if (r.notify) continue;
+      try {
+        if (calls[j].err) std::rethrow_exception(calls[j].err);
+        MsgpackWriter w;
+        if (score) w.dbl(calls[j].score); else write_pairs(w, calls[j].res);
+        out[at[j]] = jb::val::response_ok(r.msgid, w.out);
+      } catch (const ArgError&) {
+        out[at[j]] = jb::val::response_code(r.msgid, kArgumentError);
+      } catch (const std::exception& e) {
+        out[at[j]] = jb::val::response_msg(r.msgid, e.what());
+      }
+    }
+    return out;
+  }
 
   std::string dispatch(const jb::RpcRequest& r) {
     Value args;

@@ -593,23 +593,31 @@ class Clustering : public HostEngine {
     HIPCHK(hipMemcpyAsync(dw, w.data(), 4 * n, hipMemcpyHostToDevice, st_));
     HIPCHK(hipMemcpyAsync(dc, C.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
     int rc = jb_lloyd(dx, (int)n, (int)D, dw, dc, (int)kk, 100, 1e-6f, 1e-5f, da, nullptr, dd, st_);
+    const bool gmm = p_.method == "gmm";
+    const bool lloyd_dev = rc != -2;    // Lloyd's centers are in dc
     if (rc == -2) {
       host_lloyd(X, w, n, D, kk, &C, &assign);   // k x dims beyond the kernel's LDS
     } else {
       if (rc) throw std::runtime_error("jb_lloyd failed");
-      HIPCHK(hipMemcpyAsync(C.data(), dc, 4 * kk * D, hipMemcpyDeviceToHost, st_));
-      HIPCHK(hipMemcpyAsync(assign.data(), da, 4 * n, hipMemcpyDeviceToHost, st_));
-      HIPCHK(hipStreamSynchronize(st_));
+      if (!gmm) {   // GMM's EM starts from Lloyd's centers where they are (no round trip)
+        HIPCHK(hipMemcpyAsync(C.data(), dc, 4 * kk * D, hipMemcpyDeviceToHost, st_));
+        HIPCHK(hipMemcpyAsync(assign.data(), da, 4 * n, hipMemcpyDeviceToHost, st_));
+        HIPCHK(hipStreamSynchronize(st_));
+      }
     }
-    if (p_.method == "gmm") {
+    if (gmm) {
       std::vector<float> var(kk * D, 1.f), pi(kk, 1.f / (float)kk);
       float* dv = dV_.get(kk * D);
       float* dp = dP_.get(kk);
-      HIPCHK(hipMemcpyAsync(dc, C.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
+      if (rc == -2) HIPCHK(hipMemcpyAsync(dc, C.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
       HIPCHK(hipMemcpyAsync(dv, var.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
       HIPCHK(hipMemcpyAsync(dp, pi.data(), 4 * kk, hipMemcpyHostToDevice, st_));
       rc = jb_gmm_em(dx, (int)n, (int)D, dw, dc, dv, dp, (int)kk, 50, da, st_);
       if (rc == -2) {
+        if (lloyd_dev) {
+          HIPCHK(hipMemcpyAsync(C.data(), dc, 4 * kk * D, hipMemcpyDeviceToHost, st_));
+          HIPCHK(hipStreamSynchronize(st_));
+        }
         host_em(X, w, n, D, kk, &C, &var, &pi, &assign);
       } else {
         if (rc) throw std::runtime_error("jb_gmm_em failed");
@@ -742,9 +750,19 @@ class Clustering : public HostEngine {
       return best;
     }
     if (D == 0) return 0;
-    const auto dd = sqdist(x, 1, centers_, ncenters_, D);   // the matrix-core distances Python uses
-    for (size_t j = 1; j < ncenters_; ++j)
-      if (dd[j] < dd[best]) best = j;
+    // one query against k centers is k x D host flops: a device launch (and
+    // its two copies) would cost more than the whole RPC. Double precision,
+    // as the reference's host distance (the batched paths use the matrix cores).
+    double bd = INFINITY;
+    for (size_t j = 0; j < ncenters_; ++j) {
+      double d = 0.0;
+      const float* c = &centers_[j * D];
+      for (size_t t = 0; t < D; ++t) {
+        const double e = (double)x[t] - (double)c[t];
+        d += e * e;
+      }
+      if (d < bd) { bd = d; best = j; }
+    }
     return best;
   }
 
