@@ -67,7 +67,7 @@ constexpr int kSerialSegments = 4;       // segments of a small batch
 constexpr int kSerialSegmentsBig = 48;   // of a batch of >= kSerialBigBatch samples
 constexpr int64_t kSerialBigBatch = 16384;
 constexpr int kDeltaSegmentsMin = 8;     // delta committer segments of a big batch
-constexpr int kDeltaSegmentsMax = 128;
+constexpr int kDeltaSegmentsMax = 512;     // a segment costs ~20 us; a sequential tail ~2 us per sample
 constexpr int kRescoreWaste = 16;        // wasted exact steps that end a segment
 constexpr int kScoreMaxBlocks = 8192;    // serial_score_kernel grid cap (grid-stride)
 // committer phase timings (tail[4..19]): shader-clock reads in the step loop
@@ -788,7 +788,8 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
                                 int method, float C, unsigned long long* stats, uint8_t* touched,
                                 void* scratch, int nseg, hipStream_t stream);
 
-// pinned host word per scratch buffer: segments the last delta batch used
+// pinned host words per scratch buffer: the last delta batch's final stop
+// reason and segment count (tail[20], tail[21])
 static int64_t* delta_segments_seen(void* scratch) {
   static std::mutex mu;
   static std::unordered_map<void*, int64_t*> seen;
@@ -796,8 +797,8 @@ static int64_t* delta_segments_seen(void* scratch) {
   auto it = seen.find(scratch);
   if (it != seen.end()) return it->second;
   int64_t* p = nullptr;
-  if (hipHostMalloc((void**)&p, sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
-  *p = 0;
+  if (hipHostMalloc((void**)&p, 2 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
+  p[0] = p[1] = 0;
   seen[scratch] = p;
   return p;
 }
@@ -831,16 +832,23 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
     // batch that runs out of segments hands its rest to the sequential kernel:
     // the count follows the segments the previous batch on this scratch used
     // (read back asynchronously into pinned memory, one batch late at worst)
+    // A batch that ran out of segments (its last stop reason is not done /
+    // dense: the rest went to the sequential kernel, ~100x slower per
+    // sample) or the first batch on this scratch gets every segment.
     int nseg = jb::kSerialSegments;
     int64_t* seen = delta_segments_seen(scratch);
     if (n_max >= jb::kSerialBigBatch) {
-      const int64_t prev = seen != nullptr ? *(volatile int64_t*)seen : 0;
-      nseg = (int)std::min<int64_t>(jb::kDeltaSegmentsMax, std::max<int64_t>(jb::kDeltaSegmentsMin, 2 * prev + 4));
+      const int64_t why = seen != nullptr ? ((volatile int64_t*)seen)[0] : 0;
+      const int64_t prev = seen != nullptr ? ((volatile int64_t*)seen)[1] : 0;
+      const bool short_of = prev == 0 || (why != jb::kStopDone && why != jb::kStopDense);
+      nseg = short_of ? jb::kDeltaSegmentsMax
+                      : (int)std::min<int64_t>(jb::kDeltaSegmentsMax,
+                                               std::max<int64_t>(jb::kDeltaSegmentsMin, 2 * prev + 4));
     }
     const int rc = jb_delta_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W, S, active,
                                     LC, method, C, stats, touched, scratch, nseg, stream);
     if (rc == 0 && seen != nullptr)
-      (void)hipMemcpyAsync(seen, (int64_t*)scratch + 21, sizeof(int64_t), hipMemcpyDeviceToHost, stream);
+      (void)hipMemcpyAsync(seen, (int64_t*)scratch + 20, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, stream);
     return rc;
   }
   int64_t* tail = (int64_t*)scratch;
