@@ -448,6 +448,10 @@ DIST_ENGINE_CASES = (
     ("lof", "anomaly", "config/anomaly/lof.json", "add", "calc_score"),
     ("kmeans", "clustering", "config/clustering/kmeans.json", "push", "get_nearest_center"),
     ("gmm", "clustering", "config/clustering/gmm.json", "push", "get_nearest_center"),
+    # the headline engine through the native servers' linear mixer (touched-row
+    # diff all-reduce on the RCCL plane), next to the Python TableMix path of
+    # the headline's own N-GPU run
+    ("arow", "classifier", "config/classifier/arow.json", "train", "classify"),
 )
 
 
@@ -541,13 +545,18 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                             if upd == "add":
                                 for d in part:
                                     c.call("add", cname, msgpack.unpackb(d, raw=False))
+                            elif upd == "train":
+                                for i in range(0, len(part), 100):
+                                    c.call("train", cname, [[f"l{(i + j) % 4}", msgpack.unpackb(d, raw=False)]
+                                                            for j, d in enumerate(part[i:i + 100])])
                             else:
                                 for i in range(0, len(part), 100):
                                     c.call("push", cname, [msgpack.unpackb(d, raw=False) for d in part[i:i + 100]])
                     except Exception as e:  # noqa: BLE001
                         errs.append(repr(e)[:300])
                 # clustering: enough points for the coresets to be clustered (bucket_size)
-                part = rows if upd == "add" else (rows * (1 + 2500 // max(1, len(rows))))[:max(len(rows), 2500)]
+                part = rows if upd in ("add", "train") else \
+                    (rows * (1 + 2500 // max(1, len(rows))))[:max(len(rows), 2500)]
                 t0 = time.perf_counter()
                 ths = [threading.Thread(target=fill, args=(part[i::4],)) for i in range(4)]
                 for t in ths:
@@ -559,7 +568,7 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                     err, rate = errs[0], None
             rates = gather(rate)
             if all(r is not None for r in rates):
-                rec["rows_per_rank"] = len(rows) if upd == "add" else max(len(rows), 2500)
+                rec["rows_per_rank"] = len(rows) if upd in ("add", "train") else max(len(rows), 2500)
                 rec[f"{upd}_per_s_total"] = round(sum(rates), 1)
                 if rank == 0:
                     try:
@@ -575,10 +584,13 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                 try:
                     st = status_of(port, cname)
                     with RpcClient("127.0.0.1", port, 60.0) as c:
-                        first = c.call(qry, cname, msgpack.unpackb(queries[0], raw=False))
+                        def qargs(d):
+                            x = msgpack.unpackb(d, raw=False)
+                            return [x] if qry == "classify" else x
+                        first = c.call(qry, cname, qargs(queries[0]))
                         n, t0 = 0, time.perf_counter()
                         while time.perf_counter() - t0 < args.dist_engine_seconds:
-                            c.call(qry, cname, msgpack.unpackb(queries[n % len(queries)], raw=False))
+                            c.call(qry, cname, qargs(queries[n % len(queries)]))
                             n += 1
                         qps = n / (time.perf_counter() - t0)
                     mine = {"mix_count": st.get("linear_mixer.mix_count"),
@@ -894,8 +906,8 @@ def main() -> None:
     ap.add_argument("--lof-rows", type=int, default=100_000,
                     help="rows added to the LOF server before its queries")
     ap.add_argument("--engine-seconds", type=float, default=3.0)
-    ap.add_argument("--dist-engines", default="lof,kmeans",
-                    help="N > 1: distributed engine records (lof,kmeans,gmm / all / none): one server per "
+    ap.add_argument("--dist-engines", default="lof,kmeans,arow",
+                    help="N > 1: distributed engine records (lof,kmeans,gmm,arow / all / none): one server per "
                          "rank in one cluster, a forced MIX, queries on every member")
     ap.add_argument("--dist-engine-rows", type=int, default=0,
                     help="rows / points each rank fills in (0: 4000 on GPUs, 200 with --device cpu)")

@@ -76,7 +76,7 @@ def test_bench_eight_ranks_cpu():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(WORLD), "--steps", "2",
            "--warmup", "1", "--device", "cpu", "--requests", "4", "--per-request", "8",
            "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "2", "--engines", "none",
-           "--dist-engines", "lof,kmeans", "--dist-engine-rows", "120", "--dist-engine-seconds", "0.5"]
+           "--dist-engines", "lof,kmeans,arow", "--dist-engine-rows", "120", "--dist-engine-seconds", "0.5"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
@@ -91,7 +91,8 @@ def test_bench_eight_ranks_cpu():
     assert out["config"]["world_size_observed"] == WORLD
     # BASELINE #4 / #5 on 8 ranks: one server per rank in one cluster, a MIX
     # every member took part in, queries after it (CPU: the Python servers)
-    for name, qry in (("lof", "calc_score"), ("kmeans", "get_nearest_center")):
+    # and the headline engine through the servers' linear mixer
+    for name, qry in (("lof", "calc_score"), ("kmeans", "get_nearest_center"), ("arow", "classify")):
         rec = out["engines_dist"][name]
         assert "errors" not in rec, rec
         assert rec["world_size_observed"] == WORLD and rec["do_mix"] is True
