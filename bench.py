@@ -808,7 +808,8 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
                  mode: str = "exact", weight_dtype: str = "fp32", steps: int | None = None,
                  hot_rows: bool = False) -> dict:
     """The headline protocol in another configuration: a fresh model, the
-    same warmup, then timed steps over the first fresh batches. Default: the
+    same warmup (the exact mode: over fresh batches past the timed ones),
+    then timed steps over the first fresh batches. Default: the
     serial-equivalent update mode (``--exact-steps`` steps), whose result
     equals applying the batch's requests one after the other
     (csrc/hip/serial.hip), the reference's semantics. With weight_dtype
@@ -824,15 +825,21 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
     def run(arena):
         clf.train_arena(arena, np.asarray(arena.offs, np.int64), np.asarray(arena.lens, np.int64))
 
+    steps = min(args.exact_steps if steps is None else steps, args.steps)
+    # the serial-equivalent committer's cost follows how many rows a batch
+    # brings that the model has not seen: it warms up on fresh batches it
+    # will not time (the cycled warm pool would leave the model young to the
+    # timed stream), the other modes on the warm pool
+    spare = fresh.batches[steps * bps:] if mode == "exact" else []
+    src = spare if len(spare) >= bps else warm.batches
     for i in range(args.warmup):
         for j in range(bps):
-            run(warm.batches[(i * bps + j) % len(warm.batches)])
+            run(src[(i * bps + j) % len(src)])
         sync()
         _progress(f"{mode}/{weight_dtype}: warmup step {i + 1}/{args.warmup} done")
     st0 = clf.train_stats()
     sync()
     t0 = time.perf_counter()
-    steps = min(args.exact_steps if steps is None else steps, args.steps)
     for i in range(steps):
         for j in range(bps):
             run(fresh.batches[i * bps + j])

@@ -798,7 +798,11 @@ static int64_t* delta_segments_seen(void* scratch) {
   if (it != seen.end()) return it->second;
   int64_t* p = nullptr;
   if (hipHostMalloc((void**)&p, 2 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
-  p[0] = p[1] = 0;
+  // until the first batch reports: done in 16 segments (a host running
+  // batches ahead of the device must not read "unknown" as "short": every
+  // batch would get all segments and pay ~12 us per empty one)
+  p[0] = jb::kStopDone;
+  p[1] = 16;
   seen[scratch] = p;
   return p;
 }
@@ -832,15 +836,15 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
     // batch that runs out of segments hands its rest to the sequential kernel:
     // the count follows the segments the previous batch on this scratch used
     // (read back asynchronously into pinned memory, one batch late at worst)
-    // A batch that ran out of segments (its last stop reason is not done /
-    // dense: the rest went to the sequential kernel, ~100x slower per
-    // sample) or the first batch on this scratch gets every segment.
+    // A batch after one that ran out of segments (its last stop reason is
+    // not done / dense: the rest went to the sequential kernel, ~100x slower
+    // per sample) gets every segment.
     int nseg = jb::kSerialSegments;
     int64_t* seen = delta_segments_seen(scratch);
     if (n_max >= jb::kSerialBigBatch) {
       const int64_t why = seen != nullptr ? ((volatile int64_t*)seen)[0] : 0;
       const int64_t prev = seen != nullptr ? ((volatile int64_t*)seen)[1] : 0;
-      const bool short_of = prev == 0 || (why != jb::kStopDone && why != jb::kStopDense);
+      const bool short_of = why != jb::kStopDone && why != jb::kStopDense;
       nseg = short_of ? jb::kDeltaSegmentsMax
                       : (int)std::min<int64_t>(jb::kDeltaSegmentsMax,
                                                std::max<int64_t>(jb::kDeltaSegmentsMin, 2 * prev + 4));
