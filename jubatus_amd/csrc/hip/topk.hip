@@ -343,14 +343,18 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
     __syncthreads();
   }
   const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
+  if (done != nullptr) {   // latency path: results to pinned host memory, then the flag
+    for (int j = t; j < k; j += T) {
+      sys_store(out_d + o + j, j < cc ? s_cbd[cur][j] : INFINITY);
+      sys_store(out_i + o + j, j < cc ? s_cbi[cur][j] : (int32_t)INT_MAX);
+    }
+    sys_stores_block_done();
+    if (t == 0) sys_store(const_cast<uint32_t*>(done) + q, seq);
+    return;
+  }
   for (int j = t; j < k; j += T) {
     out_d[o + j] = j < cc ? s_cbd[cur][j] : INFINITY;
     out_i[o + j] = j < cc ? s_cbi[cur][j] : INT_MAX;
-  }
-  if (done != nullptr) {   // latency path: results went to pinned host memory
-    __threadfence_system();
-    __syncthreads();
-    if (t == 0) done[q] = seq;
   }
 }
 
@@ -647,12 +651,13 @@ __global__ __launch_bounds__(NW * 64) void topk_lists_kernel(const TopkSrc s, in
   }
   __syncthreads();
   const int64_t o = ((int64_t)q * gridDim.x + blockIdx.x) * k;
-  for (int j = t; j < k; j += T) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
-  if (done != nullptr) {
-    __threadfence_system();
-    __syncthreads();
-    if (t == 0) done[q] = seq;
+  if (done != nullptr) {   // pinned host memory, then the flag (sys_store)
+    for (int j = t; j < k; j += T) { sys_store(out_d + o + j, s_cd[j]); sys_store(out_i + o + j, s_ci[j]); }
+    sys_stores_block_done();
+    if (t == 0) sys_store(const_cast<uint32_t*>(done) + q, seq);
+    return;
   }
+  for (int j = t; j < k; j += T) { out_d[o + j] = s_cd[j]; out_i[o + j] = s_ci[j]; }
 }
 
 // ---------------------------------------------------------------------------
@@ -898,12 +903,81 @@ inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int
                        nrows, per_block, k, out_d, out_i, nullptr, 0u);
 }
 
+// Final merge of the scan's per-block lists (each sorted, k entries) for
+// k <= kListK and <= kMergeLists blocks: ONE wave per query. The lists go to
+// LDS; lane l owns lists l, l + 64, ... and keeps their heads in registers;
+// each of k rounds takes the wave's arg-min head (DPP / permlane) and its
+// owner advances that list. The per-thread insertion lists of
+// topk_lists_kernel cost ~20 us here (16 waves of VALU pops on a handful of
+// real candidates); this is k rounds of a dozen register steps.
+constexpr int kMergeLists = 256;
+__global__ __launch_bounds__(64) void topk_merge_sorted_kernel(const float* __restrict__ cd,
+                                                               const int32_t* __restrict__ ci, int nb, int k,
+                                                               float* __restrict__ out_d,
+                                                               int32_t* __restrict__ out_i,
+                                                               volatile uint32_t* done, uint32_t seq) {
+  constexpr int L = kMergeLists / 64;
+  __shared__ float s_d[kMergeLists * kListK];
+  __shared__ int s_i[kMergeLists * kListK];
+  __shared__ float s_rd[kListK];
+  __shared__ int s_ri[kListK];
+  const int q = blockIdx.x, lane = threadIdx.x;
+  const int n = nb * k;
+  const float* src_d = cd + (int64_t)q * n;
+  const int32_t* src_i = ci + (int64_t)q * n;
+  for (int e = lane; e < n; e += 64) { s_d[e] = src_d[e]; s_i[e] = src_i[e]; }
+  __syncthreads();
+  int pos[L];
+  float hd[L];
+  int hi[L];
+#pragma unroll
+  for (int u = 0; u < L; ++u) {
+    const int list = lane + 64 * u;
+    pos[u] = 0;
+    hd[u] = list < nb ? s_d[list * k] : INFINITY;
+    hi[u] = list < nb ? s_i[list * k] : INT_MAX;
+  }
+  for (int r = 0; r < k; ++r) {
+    float v = hd[0];
+    int id = hi[0], bu = 0;
+#pragma unroll
+    for (int u = 1; u < L; ++u)
+      if (lt_pair(hd[u], hi[u], v, id)) { v = hd[u]; id = hi[u]; bu = u; }
+    float wv = v;
+    int wid = id;
+    wave_argmin(wv, wid, lane);
+    if (lane == 0) { s_rd[r] = wv; s_ri[r] = wid; }
+    if (v == wv && id == wid) {          // the owner (padding entries may match on several lanes: harmless)
+#pragma unroll
+      for (int u = 0; u < L; ++u) {
+        if (u != bu) continue;
+        const int list = lane + 64 * u;
+        const int p = ++pos[u];
+        hd[u] = p < k ? s_d[list * k + p] : INFINITY;
+        hi[u] = p < k ? s_i[list * k + p] : INT_MAX;
+      }
+    }
+  }
+  __syncthreads();
+  const int64_t o = (int64_t)q * k;
+  if (done != nullptr) {
+    for (int j = lane; j < k; j += 64) { sys_store(out_d + o + j, s_rd[j]); sys_store(out_i + o + j, s_ri[j]); }
+    sys_stores_block_done();
+    if (lane == 0) sys_store(const_cast<uint32_t*>(done) + q, seq);
+    return;
+  }
+  for (int j = lane; j < k; j += 64) { out_d[o + j] = s_rd[j]; out_i[o + j] = s_ri[j]; }
+}
+
 // the final merge: one block per query; 16 waves when the (17 k) candidates
 // of the merge stage fit (k <= 37), else 4
 inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out_d,
                          int32_t* out_i, volatile uint32_t* done, uint32_t seq,
                          hipStream_t stream) {
-  if (k <= kListK) {
+  if (k <= kListK && nc % k == 0 && nc / k <= kMergeLists) {
+    hipLaunchKernelGGL(topk_merge_sorted_kernel, dim3(nq), dim3(64), 0, stream, m.src_d, m.src_i, (int)(nc / k), k,
+                       out_d, out_i, done, seq);
+  } else if (k <= kListK) {
     hipLaunchKernelGGL((topk_lists_kernel<2, kListK, 16>), dim3(1, nq), dim3(16 * 64), 0, stream,
                        m, nc, nc, k, out_d, out_i, done, seq);
   } else if (k <= 37) {
