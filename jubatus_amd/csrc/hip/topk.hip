@@ -910,15 +910,16 @@ inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int
 // owner advances that list. The per-thread insertion lists of
 // topk_lists_kernel cost ~20 us here (16 waves of VALU pops on a handful of
 // real candidates); this is k rounds of a dozen register steps.
-constexpr int kMergeLists = 256;
+constexpr int kMergeLists = 512;
 __global__ __launch_bounds__(64) void topk_merge_sorted_kernel(const float* __restrict__ cd,
                                                                const int32_t* __restrict__ ci, int nb, int k,
                                                                float* __restrict__ out_d,
                                                                int32_t* __restrict__ out_i,
                                                                volatile uint32_t* done, uint32_t seq) {
   constexpr int L = kMergeLists / 64;
-  __shared__ float s_d[kMergeLists * kListK];
-  __shared__ int s_i[kMergeLists * kListK];
+  extern __shared__ float s_mg[];    // [nb k] distances, then [nb k] rows
+  float* s_d = s_mg;
+  int* s_i = reinterpret_cast<int*>(s_mg + nb * k);
   __shared__ float s_rd[kListK];
   __shared__ int s_ri[kListK];
   const int q = blockIdx.x, lane = threadIdx.x;
@@ -975,8 +976,8 @@ inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out
                          int32_t* out_i, volatile uint32_t* done, uint32_t seq,
                          hipStream_t stream) {
   if (k <= kListK && nc % k == 0 && nc / k <= kMergeLists) {
-    hipLaunchKernelGGL(topk_merge_sorted_kernel, dim3(nq), dim3(64), 0, stream, m.src_d, m.src_i, (int)(nc / k), k,
-                       out_d, out_i, done, seq);
+    hipLaunchKernelGGL(topk_merge_sorted_kernel, dim3(nq), dim3(64), (size_t)nc * 8, stream, m.src_d, m.src_i,
+                       (int)(nc / k), k, out_d, out_i, done, seq);
   } else if (k <= kListK) {
     hipLaunchKernelGGL((topk_lists_kernel<2, kListK, 16>), dim3(1, nq), dim3(16 * 64), 0, stream,
                        m, nc, nc, k, out_d, out_i, done, seq);
@@ -1004,7 +1005,9 @@ extern "C" int jb_topk_blocks(int64_t nrows, int k) {
   // bound the candidates K2 merges; one block per CU is enough to stream
   // the table (the scan is a few bytes per row)
   // (256: more blocks measured slower for batched queries,
-  // profiles/r02_lsh_block_cap.jsonl)
+  // profiles/r02_lsh_block_cap.jsonl; again with the one-wave merge: 512
+  // blocks took one query at 1M rows 44 -> 42 us but four 48 -> 65 us and one
+  // at 10M rows 102 -> 121 us, profiles/r4_topk_lsh_blocks512.jsonl)
   constexpr int64_t cap = 256;
   int64_t max_blocks = 8192 / k < cap ? 8192 / k : cap;
   if (max_blocks < 1) max_blocks = 1;
