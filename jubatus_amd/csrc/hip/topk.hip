@@ -176,7 +176,7 @@ __device__ __forceinline__ void load_item(const TopkSrc& s, int q, int64_t n, in
 template <int MODE, int R>
 __device__ __forceinline__ void load_rows(const TopkSrc& s, int q, const int64_t (&nn)[R],
                                           const int64_t (&r)[R], const uint64_t* qb, float qn,
-                                          float (&d)[R], int (&id)[R]) {
+                                          float (&d)[R], int (&id)[R], const float* ctab = nullptr) {
   if (MODE != 0) {
 #pragma unroll
     for (int u = 0; u < R; ++u) load_item<MODE>(s, q, nn[u], r[u], qb, qn, d[u], id[u]);
@@ -207,10 +207,13 @@ __device__ __forceinline__ void load_rows(const TopkSrc& s, int q, const int64_t
   for (int u = 0; u < R; ++u) {
     const float frac = (float)ham[u] / (float)s.hash_num;
     float v;
-    if (s.metric == 1)
-      v = sqrtf(fmaxf(0.f, qn * qn + braw[u] * braw[u] - 2.f * qn * braw[u] * __cosf(3.14159265f * frac)));
-    else
+    if (s.metric == 1) {
+      // ctab[h] = the same cos expression per hamming distance (bit-identical)
+      const float c = ctab != nullptr ? ctab[ham[u]] : __cosf(3.14159265f * frac);
+      v = sqrtf(fmaxf(0.f, qn * qn + braw[u] * braw[u] - 2.f * qn * braw[u] * c));
+    } else {
       v = frac;
+    }
     const bool in = r[u] < nn[u];
     d[u] = (in && ok[u]) ? v : INFINITY;
     id[u] = in ? (int)r[u] : INT_MAX;
@@ -278,13 +281,19 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
   __shared__ int s_cbi[2][kTopMaxK];
   __shared__ float s_thr;
   __shared__ uint64_t s_q[kTopMaxWords];
+  __shared__ float s_cos[MODE == 0 ? kTopMaxWords * 64 + 1 : 1];   // euclid_lsh: cos(pi h / hash_num)
   const int q = blockIdx.y;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   int cur = 0, cc = 0;                     // carry buffer / real entries (block-uniform)
   float qn = 0.f;
+  const float* ctab = nullptr;
   if (MODE == 0) {
     for (int w = t; w < s.words; w += T) s_q[w] = s.qbits[(int64_t)q * s.words + w];
     qn = s.qnorm[q];
+    if (s.metric == 1 && s.hash_num <= kTopMaxWords * 64) {
+      for (int h = t; h <= s.hash_num; h += T) s_cos[h] = __cosf(3.14159265f * ((float)h / (float)s.hash_num));
+      ctab = s_cos;
+    }
   }
   if (t == 0) s_thr = INFINITY;
   __syncthreads();
@@ -307,7 +316,7 @@ __global__ __launch_bounds__(NW * 64) void topk_kernel(const TopkSrc s, int64_t 
         rows[r] = base + (int64_t)r * T + t;
         nn[r] = rows[r] < b1 ? n : 0;
       }
-      load_rows<MODE, kTopR>(s, q, nn, rows, qb, qn, d, ix);
+      load_rows<MODE, kTopR>(s, q, nn, rows, qb, qn, d, ix, ctab);
     }
 #pragma unroll
     for (int r = 0; r < kTopR; ++r) {
