@@ -76,15 +76,31 @@ __device__ int cl_draw(const float* __restrict__ wt, int n, double u, double* pa
   const int i0 = t * per, i1 = min(n, i0 + per);
   double s = 0.0;
   for (int i = i0; i < i1; ++i) s += (double)wt[i];
-  part[t] = s;
-  __syncthreads();
-  for (int o = 1; o < kClBlock; o <<= 1) {       // inclusive scan of the chunk sums
-    const double x = t >= o ? part[t - o] : 0.0;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
+  // inclusive scan of the chunk sums: within each wave by shuffles, then the
+  // wave totals (a Hillis-Steele pass over all 1024 took ~20 barriers a draw)
+  const int lane = t & 63, wv = t >> 6;
+  constexpr int NWV = kClBlock / 64;
+  double incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double x = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += x;
   }
-  const double total = part[kClBlock - 1];
+  if (lane == 63) part[kClBlock + wv] = incl;    // wave totals
+  __syncthreads();
+  if (t == 0) {
+    double run = 0.0;
+    for (int w = 0; w < NWV; ++w) {
+      const double x = part[kClBlock + w];
+      part[kClBlock + w] = run;                  // exclusive prefix of the wave
+      run += x;
+    }
+    part[kClBlock + NWV] = run;
+  }
+  __syncthreads();
+  incl += part[kClBlock + wv];
+  part[t] = incl;
+  const double total = part[kClBlock + NWV];
   if (t == 0) *pick = -1;
   __syncthreads();
   if (total > 0.0) {
@@ -115,7 +131,7 @@ __global__ __launch_bounds__(kClBlock) void kmeanspp_kernel(const float* __restr
                                                             float* __restrict__ prob,
                                                             int32_t* __restrict__ out,
                                                             int32_t* __restrict__ status) {
-  __shared__ double part[kClBlock];
+  __shared__ double part[kClBlock + kClBlock / 64 + 1];   // chunk prefixes, wave prefixes, total
   __shared__ int pick;
   const int t = threadIdx.x;
   int c = cl_draw(w, n, u[0], part, &pick);
