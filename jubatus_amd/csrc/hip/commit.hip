@@ -47,6 +47,8 @@
 // pass. Semantics per update (a repeated row counts every time, each
 // occurrence against the pre-sample state) are those of linear.hip's direct
 // path; the oracle is jubatus_amd/models/linear_oracle.py.
+#include <stdlib.h>
+
 #include "jb_linear.hpp"
 
 namespace jb {
@@ -76,8 +78,8 @@ __device__ __forceinline__ int64_t window_end(int64_t beg, int64_t end, const in
 }
 // phase timing (tail[4..19]): shader cycles of wave 0 per phase, the wall
 // clock of the kernel and every wave's own round-start work
-constexpr bool kProf = true;
-__device__ __forceinline__ uint64_t cyc() { return kProf ? __builtin_amdgcn_s_memtime() : 0; }
+// (a kernel argument: JB_COMMIT_PROF=1 turns them on; they cost ~6 % of a
+// steady batch, so the default run leaves them off)
 
 constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
 
@@ -438,7 +440,9 @@ __global__ __launch_bounds__(kT) void delta_commit_kernel(
     const float* __restrict__ S0_k, const int4* __restrict__ AUX_k, const float2* __restrict__ PP0_k,
     const int32_t* __restrict__ FI_k, const float* __restrict__ FX_k,
     unsigned long long* __restrict__ wide, unsigned long long* __restrict__ stats,
-    uint8_t* __restrict__ touched, int64_t* __restrict__ tail, int seg) {
+    uint8_t* __restrict__ touched, int64_t* __restrict__ tail, int seg, int prof) {
+  const bool kProf = prof != 0;      // uniform: scalar branches
+  auto cyc = [&]() -> uint64_t { return kProf ? __builtin_amdgcn_s_memtime() : 0; };
   using Gm = Geo<LC>;
   using S = Samp<LC, FC>;
   constexpr int K = Gm::K;
@@ -961,14 +965,14 @@ static int launch_delta(int64_t blocks, int method, const int64_t* row_ptr, cons
                         float* S, float* Pp, const int32_t* active, float C, float* s0, int4* aux,
                         float2* pp0, int32_t* fi, float* fx, unsigned long long* wide,
                         unsigned long long* stats, uint8_t* touched, int64_t* tail, int seg,
-                        const int64_t* why, hipStream_t stream) {
+                        const int64_t* why, int prof, hipStream_t stream) {
   hipLaunchKernelGGL((jb::dc::delta_s0_kernel<L>), dim3((unsigned)blocks), dim3(256), 0, stream, row_ptr, fidx,
                      fval, labels, sp, ns, W, Pp, active, method, C, s0, aux, pp0, fi, fx, wide, tail, why);
 #define JB_DELTA_M(M)                                                                                     \
   hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M, 1>), dim3(1), dim3(jb::dc::kT), 0, stream, sp, ns, \
-                     W, S, active, C, s0, aux, pp0, fi, fx, wide, stats, touched, tail, seg);              \
+                     W, S, active, C, s0, aux, pp0, fi, fx, wide, stats, touched, tail, seg, prof);        \
   hipLaunchKernelGGL((jb::dc::delta_commit_kernel<L, M, 2>), dim3(1), dim3(jb::dc::kT), 0, stream, sp, ns, \
-                     W, S, active, C, s0, aux, pp0, fi, fx, wide, stats, touched, tail, seg);              \
+                     W, S, active, C, s0, aux, pp0, fi, fx, wide, stats, touched, tail, seg, prof);        \
   break;
   switch (method) {
     case jb::PERCEPTRON: JB_DELTA_M(jb::PERCEPTRON)
@@ -998,6 +1002,10 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
                                 int method, float C, unsigned long long* stats, uint8_t* touched,
                                 void* scratch, int nseg, hipStream_t stream) {
   if (LC > 64) return -1;
+  static const int prof = [] {
+    const char* e = getenv("JB_COMMIT_PROF");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
   int64_t* tail = (int64_t*)scratch;
   uint8_t* base = (uint8_t*)scratch + 256;
   float* s0 = (float*)base;
@@ -1016,7 +1024,7 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
     int rc = 0;
 #define JB_DELTA_L(L)                                                                                      \
   rc = launch_delta<L>(blocks, method, row_ptr, fidx, fval, labels, sp, ns, W, S, Pp, active, C, s0, aux, \
-                       pp0, fi, fx, wide, stats, touched, tail, seg, why, stream);                        \
+                       pp0, fi, fx, wide, stats, touched, tail, seg, why, prof, stream);                  \
   break;
     switch (LC) {
       case 8: JB_DELTA_L(8)

@@ -798,11 +798,14 @@ static int64_t* delta_segments_seen(void* scratch) {
   if (it != seen.end()) return it->second;
   int64_t* p = nullptr;
   if (hipHostMalloc((void**)&p, 2 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
-  // until the first batch reports: done in 16 segments (a host running
+  // until the first batch reports: done in 128 segments (a host running
   // batches ahead of the device must not read "unknown" as "short": every
-  // batch would get all segments and pay ~12 us per empty one)
+  // batch would get all 512 and pay ~12 us per empty one; a young model's
+  // first batches need ~100-300, so 2 x 128 + 4 keeps them whole - with 2 x
+  // 64 + 4 the first ones handed a sequential tail on: 86 vs 45 ms for
+  // batches 0-5, profiles/serial_exact_r4_prof_switch.jsonl)
   p[0] = jb::kStopDone;
-  p[1] = 16;
+  p[1] = 128;
   seen[scratch] = p;
   return p;
 }
