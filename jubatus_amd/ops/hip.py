@@ -677,7 +677,9 @@ class SerialScratch:
             # delta committer (csrc/hip/commit.hip): steps that did not update,
             # guard-band re-scores, updates, rows in the LDS store at the end
             out.update(wasted_steps=v[22], refreshes=v[23], committer_updates=v[24],
-                       last_segment_rows=v[25], exact_rescored=v[26], committed_samples=v[27])
+                       last_segment_rows=v[25])
+            if v[27] > 0:     # counted with the phase stamps only (JB_COMMIT_PROF=1)
+                out.update(exact_rescored=v[26], committed_samples=v[27])
         # committer phases in shader cycles, scaled to us by the wall clock
         wall_us = v[10] / 100.0
         if v[11] > 0:
