@@ -221,11 +221,11 @@ __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict
 // C_j, var_j) + log pi_j); nk = max(sum_i r_ij, 1e-9); C = S1 / nk;
 // var = max(S2 / nk - C^2, 1e-6); pi = nk / sum nk. LDS: C, var, S1, S2
 // [k][d], nk / logdet / log pi [k].
-__global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restrict__ X, int n, int d,
+__global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restrict__ Xg, int n, int d,
                                                           const float* __restrict__ w, float* __restrict__ C,
                                                           float* __restrict__ var, float* __restrict__ pi,
                                                           int k, int iters, int32_t* __restrict__ assign,
-                                                          bool staged) {
+                                                          bool staged, bool xlds) {
   extern __shared__ float s_em[];
   float* sC = s_em;
   float* sV = sC + k * d;
@@ -234,8 +234,14 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
   float* nk = s2 + k * d;          // [k]
   float* lc = nk + k;              // [k] log pi_j - 0.5 sum_q log(2 pi var_jq)
   float* sR = lc + k;              // [n][k] responsibilities (staged)
+  float* sIV = sR + (staged ? (size_t)n * k : 0);   // [k][d] 1 / var (staged)
+  float* sX = sIV + (staged ? (size_t)k * d : 0);   // [n][d] the points (xlds)
   __shared__ float s_tot;
   const int t = threadIdx.x;
+  // the points in LDS when they fit: every E- and M-step pass reads them
+  if (xlds)
+    for (int i = t; i < n * d; i += kClBlock) sX[i] = Xg[i];
+  const float* __restrict__ X = xlds ? sX : Xg;
   const float kLog2Pi = 1.8378770664093453f;
   for (int i = t; i < k * d; i += kClBlock) { sC[i] = C[i]; sV[i] = var[i]; }
   for (int j = t; j < k; j += kClBlock) nk[j] = pi[j];   // (pi until the first M-step)
@@ -252,20 +258,28 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
     __syncthreads();
     (void)kLog2Pi;
     if (staged) {
-      // E-step: each point's responsibilities into LDS (one distance pass)
-      for (int i = t; i < n; i += kClBlock) {
+      // E-step: one thread per (point, component) - the d-long distance
+      // multiplies by 1 / var (one divide per (j, q) an iteration, not one
+      // per point) - then one thread per point normalizes its k entries
+      for (int i = t; i < k * d; i += kClBlock) sIV[i] = 1.f / sV[i];
+      __syncthreads();
+      for (int e = t; e < n * k; e += kClBlock) {
+        const int i = e / k, j = e - i * k;
         const float* x = X + (int64_t)i * d;
+        const float* c = sC + j * d;
+        const float* iv = sIV + j * d;
+        float q2 = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float df = x[q] - c[q];
+          q2 += df * df * iv[q];
+        }
+        sR[e] = lc[j] - 0.5f * q2;
+      }
+      __syncthreads();
+      for (int i = t; i < n; i += kClBlock) {
         float* r = sR + (size_t)i * k;
         float mx = -INFINITY;
-        for (int j = 0; j < k; ++j) {
-          float q2 = 0.f;
-          for (int q = 0; q < d; ++q) {
-            const float df = x[q] - sC[j * d + q];
-            q2 += df * df / sV[j * d + q];
-          }
-          r[j] = lc[j] - 0.5f * q2;
-          mx = fmaxf(mx, r[j]);
-        }
+        for (int j = 0; j < k; ++j) mx = fmaxf(mx, r[j]);
         float den = 0.f;
         for (int j = 0; j < k; ++j) den += expf(r[j] - mx);
         const float wi = w[i] / den;
@@ -387,11 +401,14 @@ extern "C" int jb_gmm_em(const float* X, int n, int d, const float* w, float* C,
   if (lds > 64 * 1024) return -2;
   // responsibilities staged in LDS when they fit: the M-step then reduces
   // per (cluster, column) instead of contending on LDS float atomics
-  const size_t staged = lds + sizeof(float) * (size_t)n * k;
+  const size_t staged = lds + sizeof(float) * ((size_t)n * k + (size_t)k * d);   // + 1 / var
   const bool stage = staged <= 64 * 1024;
   if (stage) lds = staged;
+  const size_t withx = lds + sizeof(float) * (size_t)n * d;
+  const bool xlds = stage && withx <= 64 * 1024;
+  if (xlds) lds = withx;
   hipLaunchKernelGGL(jb::gmm_em_kernel, dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var, pi, k,
-                     iters, assign, stage);
+                     iters, assign, stage, xlds);
   return (int)hipGetLastError();
 }
 

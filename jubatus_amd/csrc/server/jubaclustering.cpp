@@ -430,14 +430,14 @@ class Clustering : public HostEngine {
     float* dxn = dXn_.get(n);
     float* dcn = dCn_.get(m);
     float* dout = dOut_.get(n * m);
-    HIPCHK(hipMemcpyAsync(dx, X.data(), 4 * n * D, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(dc, C.data(), 4 * m * D, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(dxn, xn.data(), 4 * n, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(dcn, cn.data(), 4 * m, hipMemcpyHostToDevice, st_));
+    h2d(dx, X.data(), 4 * n * D);
+    h2d(dc, C.data(), 4 * m * D);
+    h2d(dxn, xn.data(), 4 * n);
+    h2d(dcn, cn.data(), 4 * m);
     if (jb_sqdist_mfma(dx, (int64_t)n, dc, (int)m, (int)D, dxn, dcn, dout, st_) != 0)
       throw std::runtime_error("jb_sqdist_mfma failed");
-    HIPCHK(hipMemcpyAsync(out.data(), dout, 4 * n * m, hipMemcpyDeviceToHost, st_));
-    HIPCHK(hipStreamSynchronize(st_));
+    d2h(out.data(), dout, 4 * n * m);
+    sync();
     return out;
   }
 
@@ -453,14 +453,14 @@ class Clustering : public HostEngine {
     double* du = dU_.get((size_t)m);
     float* scr = dScr_.get(2 * n);
     int32_t* dout = dI_.get((size_t)m + 1);
-    HIPCHK(hipMemcpyAsync(dx, X.data(), 4 * n * D, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(dw, w.data(), 4 * n, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(du, u.data(), 8 * (size_t)m, hipMemcpyHostToDevice, st_));
+    h2d(dx, X.data(), 4 * n * D);
+    h2d(dw, w.data(), 4 * n);
+    h2d(du, u.data(), 8 * (size_t)m);
     if (jb_kmeanspp(dx, (int)n, (int)D, dw, du, (int)m, scr, scr + n, dout, dout + m, st_) != 0)
       throw std::runtime_error("jb_kmeanspp failed");
     std::vector<int32_t> o((size_t)m + 1);
-    HIPCHK(hipMemcpyAsync(o.data(), dout, 4 * ((size_t)m + 1), hipMemcpyDeviceToHost, st_));
-    HIPCHK(hipStreamSynchronize(st_));
+    d2h(o.data(), dout, 4 * ((size_t)m + 1));
+    sync();
     const int status = o[(size_t)m];
     std::vector<int64_t> chosen;
     if (status == 0) {
@@ -589,9 +589,9 @@ class Clustering : public HostEngine {
     float* dc = dC_.get(kk * D);
     int32_t* da = dA_.get(n);
     int32_t* dd = dI_.get(1);
-    HIPCHK(hipMemcpyAsync(dx, X.data(), 4 * n * D, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(dw, w.data(), 4 * n, hipMemcpyHostToDevice, st_));
-    HIPCHK(hipMemcpyAsync(dc, C.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
+    h2d(dx, X.data(), 4 * n * D);
+    h2d(dw, w.data(), 4 * n);
+    h2d(dc, C.data(), 4 * kk * D);
     int rc = jb_lloyd(dx, (int)n, (int)D, dw, dc, (int)kk, 100, 1e-6f, 1e-5f, da, nullptr, dd, st_);
     const bool gmm = p_.method == "gmm";
     const bool lloyd_dev = rc != -2;    // Lloyd's centers are in dc
@@ -600,32 +600,32 @@ class Clustering : public HostEngine {
     } else {
       if (rc) throw std::runtime_error("jb_lloyd failed");
       if (!gmm) {   // GMM's EM starts from Lloyd's centers where they are (no round trip)
-        HIPCHK(hipMemcpyAsync(C.data(), dc, 4 * kk * D, hipMemcpyDeviceToHost, st_));
-        HIPCHK(hipMemcpyAsync(assign.data(), da, 4 * n, hipMemcpyDeviceToHost, st_));
-        HIPCHK(hipStreamSynchronize(st_));
+        d2h(C.data(), dc, 4 * kk * D);
+        d2h(assign.data(), da, 4 * n);
+        sync();
       }
     }
     if (gmm) {
       std::vector<float> var(kk * D, 1.f), pi(kk, 1.f / (float)kk);
       float* dv = dV_.get(kk * D);
       float* dp = dP_.get(kk);
-      if (rc == -2) HIPCHK(hipMemcpyAsync(dc, C.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
-      HIPCHK(hipMemcpyAsync(dv, var.data(), 4 * kk * D, hipMemcpyHostToDevice, st_));
-      HIPCHK(hipMemcpyAsync(dp, pi.data(), 4 * kk, hipMemcpyHostToDevice, st_));
+      if (rc == -2) h2d(dc, C.data(), 4 * kk * D);
+      h2d(dv, var.data(), 4 * kk * D);
+      h2d(dp, pi.data(), 4 * kk);
       rc = jb_gmm_em(dx, (int)n, (int)D, dw, dc, dv, dp, (int)kk, 50, da, st_);
       if (rc == -2) {
         if (lloyd_dev) {
-          HIPCHK(hipMemcpyAsync(C.data(), dc, 4 * kk * D, hipMemcpyDeviceToHost, st_));
-          HIPCHK(hipStreamSynchronize(st_));
+          d2h(C.data(), dc, 4 * kk * D);
+          sync();
         }
         host_em(X, w, n, D, kk, &C, &var, &pi, &assign);
       } else {
         if (rc) throw std::runtime_error("jb_gmm_em failed");
-        HIPCHK(hipMemcpyAsync(C.data(), dc, 4 * kk * D, hipMemcpyDeviceToHost, st_));
-        HIPCHK(hipMemcpyAsync(var.data(), dv, 4 * kk * D, hipMemcpyDeviceToHost, st_));
-        HIPCHK(hipMemcpyAsync(pi.data(), dp, 4 * kk, hipMemcpyDeviceToHost, st_));
-        HIPCHK(hipMemcpyAsync(assign.data(), da, 4 * n, hipMemcpyDeviceToHost, st_));
-        HIPCHK(hipStreamSynchronize(st_));
+        d2h(C.data(), dc, 4 * kk * D);
+        d2h(var.data(), dv, 4 * kk * D);
+        d2h(pi.data(), dp, 4 * kk);
+        d2h(assign.data(), da, 4 * n);
+        sync();
       }
       var_ = var;
       pi_ = pi;
@@ -867,6 +867,43 @@ class Clustering : public HostEngine {
   Dev<float> dX_, dW_, dC_, dXn_, dCn_, dOut_, dScr_, dV_, dP_;
   Dev<double> dU_;
   Dev<int32_t> dI_, dA_;
+
+  // Copies through page-locked staging: from pageable memory the runtime
+  // stages each copy through a buffer of its own and waits for it (27 such
+  // copies per 1000-point push). Offsets grow until sync(), which waits for
+  // the stream, hands the device-to-host results to their vectors and
+  // resets the staging.
+  PinBuf<uint8_t> pin_;
+  size_t pin_off_ = 0;
+  struct Pending { void* dst; const uint8_t* src; size_t n; };
+  std::vector<Pending> back_;
+  uint8_t* stage(size_t n) {
+    const size_t a = (pin_off_ + 255) & ~(size_t)255;
+    if (pin_.p == nullptr || a + n > pin_.cap) {
+      sync();                       // everything staged so far is done with
+      pin_.get(std::max<size_t>(2 * pin_.cap, n + 4096));
+      pin_off_ = n;
+      return pin_.p;
+    }
+    pin_off_ = a + n;
+    return pin_.p + a;
+  }
+  void h2d(void* dst, const void* src, size_t n) {
+    uint8_t* b = stage(n);
+    memcpy(b, src, n);
+    HIPCHK(hipMemcpyAsync(dst, b, n, hipMemcpyHostToDevice, st_));
+  }
+  void d2h(void* dst, const void* src, size_t n) {
+    uint8_t* b = stage(n);
+    HIPCHK(hipMemcpyAsync(b, src, n, hipMemcpyDeviceToHost, st_));
+    back_.push_back({dst, b, n});
+  }
+  void sync() {
+    HIPCHK(hipStreamSynchronize(st_));
+    for (const Pending& q : back_) memcpy(q.dst, q.src, q.n);
+    back_.clear();
+    pin_off_ = 0;
+  }
 };
 
 }  // namespace
