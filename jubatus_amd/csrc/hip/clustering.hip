@@ -124,16 +124,37 @@ __device__ int cl_draw(const float* __restrict__ wt, int n, double u, double* pa
 // k-means++ seeding: m draws (u: host-drawn uniforms, one per draw, as the
 // host path consumes its RNG). out[j] = chosen row, or status = 1 when every
 // remaining weight is zero (the host continues with its uniform fallback).
-__global__ __launch_bounds__(kClBlock) void kmeanspp_kernel(const float* __restrict__ X, int n,
-                                                            int d, const float* __restrict__ w,
+__global__ __launch_bounds__(kClBlock) void kmeanspp_kernel(const float* __restrict__ Xg, int n,
+                                                            int d, const float* __restrict__ wg,
                                                             const double* __restrict__ u, int m,
-                                                            float* __restrict__ d2,
-                                                            float* __restrict__ prob,
+                                                            float* __restrict__ d2g,
+                                                            float* __restrict__ probg,
                                                             int32_t* __restrict__ out,
-                                                            int32_t* __restrict__ status) {
+                                                            int32_t* __restrict__ status, int lds_mode) {
   __shared__ double part[kClBlock + kClBlock / 64 + 1];   // chunk prefixes, wave prefixes, total
   __shared__ int pick;
   const int t = threadIdx.x;
+  // lds_mode 1: weights, d2 and draw weights in LDS (every draw reads and
+  // writes them; through global memory each was an L2 round trip); 2: the
+  // points too
+  extern __shared__ float s_pp[];
+  const float* w = wg;
+  float* d2 = d2g;
+  float* prob = probg;
+  const float* X = Xg;
+  if (lds_mode > 0) {
+    float* sw = s_pp;
+    d2 = sw + n;
+    prob = d2 + n;
+    for (int i = t; i < n; i += kClBlock) sw[i] = wg[i];
+    w = sw;
+    if (lds_mode > 1) {
+      float* sx = prob + n;
+      for (int i = t; i < n * d; i += kClBlock) sx[i] = Xg[i];
+      X = sx;
+    }
+    __syncthreads();
+  }
   int c = cl_draw(w, n, u[0], part, &pick);
   if (t == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
   if (c < 0) return;
@@ -424,8 +445,11 @@ extern "C" int jb_kmeanspp(const float* X, int n, int d, const float* w, const d
                            float* d2, float* prob, int32_t* out, int32_t* status,
                            hipStream_t stream) {
   if (n <= 0 || m <= 0) return 0;
-  hipLaunchKernelGGL(jb::kmeanspp_kernel, dim3(1), dim3(jb::kClBlock), 0, stream, X, n, d, w, u, m,
-                     d2, prob, out, status);
+  const size_t base = sizeof(float) * 3 * (size_t)n;
+  const size_t withx = base + sizeof(float) * (size_t)n * d;
+  const int mode = withx <= 64 * 1024 ? 2 : (base <= 64 * 1024 ? 1 : 0);
+  hipLaunchKernelGGL(jb::kmeanspp_kernel, dim3(1), dim3(jb::kClBlock), mode == 2 ? withx : (mode == 1 ? base : 0),
+                     stream, X, n, d, w, u, m, d2, prob, out, status, mode);
   return (int)hipGetLastError();
 }
 
