@@ -24,6 +24,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "jb_device.hpp"
 #include "jb_host_wait.hpp"
 
 namespace jb {
@@ -214,7 +215,7 @@ __device__ __forceinline__ float lof_lrd(const int32_t* s, const float* d, int k
 // LOF of one point from its neighbours (ts, td: nt entries, ascending):
 // refreshes the stale lrd of those neighbours, writes to pinned host memory
 // out = [status, score bits, lrd(q) bits, nmissing, missing slots...]:
-// (status published last, after a system-scope fence) status 1 = done,
+// (status published last, by system-scope stores) status 1 = done,
 // 2 = rows without a valid list (missing) - the host
 // installs their lists and runs the kernel again. One block.
 __device__ __forceinline__ void lof_score_body(
@@ -228,7 +229,7 @@ __device__ __forceinline__ void lof_score_body(
   const int t = threadIdx.x;
   auto miss = [&](int32_t s) {
     const int w = atomicAdd(&nmiss, 1);
-    if (w < max_missing) out[4 + w] = (uint32_t)s;
+    if (w < max_missing) sys_store(out + 4 + w, (uint32_t)s);
   };
   if (t < nt) {
     const int32_t o = ts[t];
@@ -248,12 +249,15 @@ __device__ __forceinline__ void lof_score_body(
       }
     }
   }
-  __syncthreads();
+  // the host reads out[] once out[0] is set: every thread's system-scope
+  // stores are acknowledged before the barrier, the status goes last (a
+  // system-scope release fence would write back the whole L2 instead)
+  sys_stores_block_done();
   if (t != 0) return;
   if (nmiss > 0) {
-    out[3] = (uint32_t)(nmiss < max_missing ? nmiss : max_missing);
-    __threadfence_system();
-    *(volatile uint32_t*)&out[0] = 2u;
+    sys_store(out + 3, (uint32_t)(nmiss < max_missing ? nmiss : max_missing));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sys_store(out, 2u);
     return;
   }
   // lrd of the query point itself (its own neighbours' k-distances)
@@ -275,11 +279,11 @@ __device__ __forceinline__ void lof_score_body(
     else score = mean_lo / lp;
   }
   if (store_slot >= 0) { lrd[store_slot] = lp; lrd_ok[store_slot] = 1; }
-  out[1] = __float_as_uint(score);
-  out[2] = __float_as_uint(lp);
-  out[3] = 0;
-  __threadfence_system();
-  *(volatile uint32_t*)&out[0] = 1u;
+  sys_store(out + 1, __float_as_uint(score));
+  sys_store(out + 2, __float_as_uint(lp));
+  sys_store(out + 3, 0u);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sys_store(out, 1u);
 }
 
 __global__ __launch_bounds__(64) void lof_score_kernel(
