@@ -513,9 +513,12 @@ __global__ __launch_bounds__(64) void scan_fixup_kernel(
   const int lane = threadIdx.x;
   if (k >= R) return;
   if (k == 0) {   // the batch's check, straight into coherent host memory
-    for (int i = lane; i < nhist; i += 64) host_out[1 + i] = (int32_t)hist[i];
-    if (lane == 0) host_out[0] = *err;
-    __threadfence_system();
+    // system-scope stores (past the L2), the error word after the counts
+    // are acknowledged; the host reads the record after the batch's event.
+    // (A system-scope fence here wrote back the whole L2 every batch.)
+    for (int i = lane; i < nhist; i += 64) sys_store(host_out + 1 + i, (int32_t)hist[i]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) sys_store(host_out, *err);
   }
   const int64_t s0 = sample_base[k], s1 = sample_base[k + 1];
   if (*err) {   // the batch goes to the host path: every sample becomes a no-op
