@@ -862,12 +862,16 @@ __global__ __launch_bounds__(1024) void topk_final_kernel(const float* __restric
     }
     __syncthreads();
   }
-  for (int x = t; x < k; x += T) { out_d[(int64_t)q * k + x] = s_cd[x]; out_i[(int64_t)q * k + x] = s_ci[x]; }
-  __threadfence_system();
-  __syncthreads();
+  // pinned host memory by system-scope stores, the flag after every
+  // thread's stores are acknowledged (no L2 write-back fence)
+  for (int x = t; x < k; x += T) {
+    sys_store(out_d + (int64_t)q * k + x, s_cd[x]);
+    sys_store(out_i + (int64_t)q * k + x, (int32_t)s_ci[x]);
+  }
+  sys_stores_block_done();
   // too few candidates is only a failure when T cut rows off (T < +inf)
   const bool retry = c_all > cap || (c_all < k && thr[q] < INFINITY);
-  if (t == 0) done[q] = retry ? (seq | kTopRetry) : seq;
+  if (t == 0) sys_store(const_cast<uint32_t*>(done) + q, retry ? (seq | kTopRetry) : seq);
 }
 
 constexpr int kListK = 16;   // k up to this uses topk_lists_kernel
@@ -1420,15 +1424,14 @@ __global__ __launch_bounds__(1024) void topk_rank_final_kernel(
         if ((x & 63) == 63 && rank >= k) break;    // already out of the top k
       }
       if (rank < k) {
-        out_d[(int64_t)q * k + rank] = d;
-        out_i[(int64_t)q * k + rank] = id;
+        sys_store(out_d + (int64_t)q * k + rank, d);
+        sys_store(out_i + (int64_t)q * k + rank, (int32_t)id);
       }
     }
   }
-  __threadfence_system();
-  __syncthreads();
+  sys_stores_block_done();
   const bool retry = over || (c_all < k && thr[q] < INFINITY);
-  if (t == 0) done[q] = retry ? (seq | kTopRetry) : seq;
+  if (t == 0) sys_store(const_cast<uint32_t*>(done) + q, retry ? (seq | kTopRetry) : seq);
 }
 
 }  // namespace jb
