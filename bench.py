@@ -582,7 +582,13 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
             mine = None
             if all(r is not None for r in rates):
                 try:
+                    # a member applies the MIX's fold after the round returns
+                    # on rank 0: wait (bounded) until its count shows it
                     st = status_of(port, cname)
+                    t_w = time.time() + 15
+                    while st.get("linear_mixer.mix_count") in (None, "0") and time.time() < t_w:
+                        time.sleep(0.1)
+                        st = status_of(port, cname)
                     with RpcClient("127.0.0.1", port, 60.0) as c:
                         def qargs(d):
                             x = msgpack.unpackb(d, raw=False)
