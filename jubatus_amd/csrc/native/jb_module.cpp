@@ -413,9 +413,11 @@ int64_t frame(py::buffer b) {
 }  // namespace
 
 void register_synth(py::module_& m);   // jb_synth.cpp
+void register_cpu_serial(py::module_& m);   // jb_cpu_serial.cpp
 
 PYBIND11_MODULE(_jubatus_native, m) {
   register_synth(m);
+  register_cpu_serial(m);
   m.def("csr_normalize", &csr_normalize, "sort / merge / drop-negative a CSR per row, with norms");
   m.doc() = "jubatus_amd host-native runtime: request scanning, hashing, CRC32, MD5";
   py::class_<jb::LabelTable>(m, "LabelTable")
