@@ -868,6 +868,65 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
     return out
 
 
+def cpu_baseline_record(args, cfg, nat, warm_batches, timed_batches, worst_batches) -> dict:
+    """The in-house CPU baseline (the reference publishes no
+    numbers; its semantics trained on this host are the bar): the servers'
+    default serial semantics on the host in native C++
+    (csrc/native/jb_cpu_serial.cpp: the same msgpack parse, hasher and update
+    rules as the GPU path; one sample after another, as the reference's
+    classifier_serv.cpp:138-144), over the same fresh request batches the
+    exact-mode record times. ``threads_1``: parse + hash + train on one core;
+    ``threads_all``: parse + hash on all cores, the train (sequential by
+    definition) on one. The model warms up on ``warm_batches`` first."""
+    from jubatus_amd.fv_converter.converter import DatumToFvConverter
+    from jubatus_amd.fv_converter.gpu_path import GpuRuleTable
+    H = int(cfg["converter"]["hash_max_size"])
+    rt = GpuRuleTable(DatumToFvConverter(cfg["converter"]))
+    hasher = nat.HostFvHasher(rt.srules, rt.n_srules, rt.nrules, rt.n_nrules, rt.blob, H)
+    LC = 1
+    while LC < args.labels:
+        LC *= 2
+    LC = max(LC, 8)
+    ncpu = max(1, min(16, os.cpu_count() or 1))
+
+    def model():
+        table = nat.LabelTable()
+        for y in range(args.labels):
+            table.get_or_add(f"label{y}")
+        return table, np.zeros((H, LC), np.float32), np.ones((H, LC), np.float32)
+
+    active = np.zeros(LC, np.uint8)
+    active[:args.labels] = 1
+
+    def run(batches, table, W, P, threads):
+        n = u = 0
+        sec = 0.0
+        for a in batches:
+            k, up, dt = nat.cpu_train_arena(hasher, a.np.ctypes.data, np.asarray(a.offs, np.int64),
+                                            np.asarray(a.lens, np.int64), table, 5, 1.0, LC,
+                                            W.ctypes.data, P.ctypes.data, active, threads)
+            n, u, sec = n + k, u + up, sec + dt
+        return n, u, sec
+
+    out = {"semantics": "serial (one sample after another), AROW, fp32, native C++ on the host",
+           "host_cpus_used_all": ncpu, "warm_batches": len(warm_batches)}
+    table, W, P = model()
+    run(warm_batches, table, W, P, ncpu)
+    W0, P0 = W.copy(), P.copy()
+    for name, threads in (("threads_1", 1), ("threads_all", ncpu)):
+        W[:], P[:] = W0, P0
+        n, u, sec = run(timed_batches, table, W, P, threads)
+        out[name] = {"value": round(n / sec, 1), "unit": "samples/s", "batches": len(timed_batches),
+                     "update_fraction": round(u / max(1, n), 5), "threads": threads}
+    if worst_batches:
+        table, W, P = model()
+        n, u, sec = run(worst_batches, table, W, P, ncpu)
+        out["worst_case"] = {"value": round(n / sec, 1), "unit": "samples/s", "batches": len(worst_batches),
+                             "update_fraction": round(u / max(1, n), 5), "threads": ncpu,
+                             "data": "worst case: noise string values (every sample updates), fresh model"}
+    return out
+
+
 def _mix_summary(log: list) -> dict:
     """per-MIX bytes per rank and host-observed latency (begin -> done) of
     the MIXes completed in the timed steps"""
@@ -953,6 +1012,8 @@ def main() -> None:
                     help="1 GPU: also time this many steps (16 batches each) of the headline's update "
                          "mode on the worst-case stream (noise string values: every sample updates) "
                          "and report them under worst_case")
+    ap.add_argument("--cpu-baseline", type=int, default=1,
+                    help="1: the in-house CPU baseline record (serial semantics on the host) beside exact_mode")
     ap.add_argument("--weight-dtype", choices=("fp32", "bf16"), default="fp32",
                     help="storage of the headline model's W table (P and arithmetic stay fp32)")
     ap.add_argument("--bf16-steps", type=int, default=5,
@@ -1222,6 +1283,16 @@ def main() -> None:
             ew["data"] = worst["data"]
             ew["batches_per_step"] = wb
             exact["worst_case"] = ew
+        if args.cpu_baseline and exact is not None:
+            _progress("cpu baseline (host serial trainer)")
+            spare = fresh.batches[min(args.exact_steps, args.steps) * bps:]
+            tb = fresh.batches[:min(len(fresh.batches), 8)]
+            exact["cpu_baseline"] = cpu_baseline_record(args, cfg, nat, spare[:96], tb, ws.batches[:4])
+            for k in ("threads_1", "threads_all"):
+                exact["cpu_baseline"][f"gpu_exact_vs_{k}"] = round(
+                    exact["value"] / max(1.0, exact["cpu_baseline"][k]["value"]), 2)
+            exact["cpu_baseline"]["gpu_exact_worst_vs_cpu_worst"] = round(
+                exact["worst_case"]["value"] / max(1.0, exact["cpu_baseline"]["worst_case"]["value"]), 2)
         del ws
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:

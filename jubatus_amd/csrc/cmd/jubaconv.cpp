@@ -226,6 +226,7 @@ struct Wide {
   uint64_t H = 1ull << 20;
   bool global = false;
 };
+std::shared_ptr<jb::WideExt> ext;   // plug-ins, filters, binary rules of the converter
 
 [[noreturn]] void run_python(char** argv) {
   std::string here(256, '\0');
@@ -280,11 +281,12 @@ int main(int argc, char** argv) {
     empty.kind = Value::MAP;
     std::string why;
     if (!jb::row::build_wide_rules(conv && conv->kind == Value::MAP ? *conv : empty, &w.s, &w.n, &w.c, &w.blob,
-                                   &w.H, &w.global, &why))
+                                   &w.H, &w.global, &why, &ext))
       run_python(argv);
     hw.reset(new jb::HostFvWide((const uint8_t*)w.s.data(), (int)w.s.size(), (const uint8_t*)w.n.data(),
                                 (int)w.n.size(), (const uint8_t*)w.c.data(), (int)w.c.size() / 2,
                                 (const uint8_t*)w.blob.data(), w.blob.size(), w.H));
+    hw->set_ext(ext);
   }
   std::stringstream ss;
   ss << std::cin.rdbuf();

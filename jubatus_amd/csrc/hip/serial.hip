@@ -67,7 +67,8 @@ constexpr int kSerialSegments = 4;       // segments of a small batch
 constexpr int kSerialSegmentsBig = 48;   // of a batch of >= kSerialBigBatch samples
 constexpr int64_t kSerialBigBatch = 16384;
 constexpr int kDeltaSegmentsMin = 8;     // delta committer segments of a big batch
-constexpr int kDeltaSegmentsMax = 512;     // a segment costs ~20 us; a sequential tail ~2 us per sample
+constexpr int kDeltaSegmentsMax = 512;
+constexpr int kVerifiedSegmentsMax = 2048;  // verified committer windows of a big batch (vcommit.hip)     // a segment costs ~20 us; a sequential tail ~2 us per sample
 constexpr int kRescoreWaste = 16;        // wasted exact steps that end a segment
 constexpr int kScoreMaxBlocks = 8192;    // serial_score_kernel grid cap (grid-stride)
 // committer phase timings (tail[4..19]): shader-clock reads in the step loop
@@ -777,8 +778,12 @@ extern "C" int64_t jb_delta_scratch_per_sample();
 // precisions and best wrong label (commit.hip, LC <= 64) or this file's
 // slack + |x|_1 (LC > 64)]; n_max bounds the batch's sample count
 // stream_ptr[nstreams] - stream_ptr[0]
+extern "C" int64_t jb_vcommit_fixed_bytes();
 extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max) {
-  return 256 + jb_delta_scratch_per_sample() * (n_max > 0 ? n_max : 1);
+  const int64_t n = n_max > 0 ? n_max : 1;
+  // vcommit.hip: the slack of every sample (4 B) after the records, then its
+  // 256-aligned fixed region (state, candidate bits, staged store)
+  return 256 + ((jb_delta_scratch_per_sample() + 4) * n + 255) / 256 * 256 + jb_vcommit_fixed_bytes();
 }
 
 // commit.hip: the delta committer (label capacities <= 64)
@@ -810,12 +815,22 @@ static int64_t* delta_segments_seen(void* scratch) {
   return p;
 }
 
-// committer of LC <= 64: 1 = delta (commit.hip, default), 0 = this file's
-// bound committer (JB_SERIAL_COMMITTER=bound, for A/B runs)
+// vcommit.hip: the verified committer (label capacities <= 64)
+extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                  const int32_t* labels, const int64_t* stream_ptr, int nstreams, int64_t n_max,
+                                  float* W, float* S, const int32_t* active, int LC, int method, float C,
+                                  unsigned long long* stats, uint8_t* touched, void* scratch, int nseg,
+                                  hipStream_t stream);
+
+// committer of LC <= 64: 2 = verified (vcommit.hip, default), 1 = delta
+// (commit.hip, JB_SERIAL_COMMITTER=delta), 0 = this file's bound committer
+// (JB_SERIAL_COMMITTER=bound); the last two for A/B runs
 static int serial_committer() {
   static const int v = [] {
     const char* e = getenv("JB_SERIAL_COMMITTER");
-    return (e != nullptr && strcmp(e, "bound") == 0) ? 0 : 1;
+    if (e != nullptr && strcmp(e, "bound") == 0) return 0;
+    if (e != nullptr && strcmp(e, "delta") == 0) return 1;
+    return 2;
   }();
   return v;
 }
@@ -833,6 +848,30 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
   if (nstreams <= 0 || n_max <= 0) return 0;
   if (scratch == nullptr || scratch_bytes < jb_serial_scratch_bytes(n_max)) return -3;
   if (method >= jb::CW && S == nullptr) return -4;
+  if (LC <= 64 && serial_committer() == 2) {
+    // verified committer: a segment is one window (score, gather, commit,
+    // verify); a window that fails verification runs again. The count follows
+    // the segments the previous batch on this scratch used (pinned readback,
+    // one batch late at worst); the rest of a batch that runs out of them goes
+    // to the sequential kernel.
+    int nseg = jb::kSerialSegments;
+    int64_t* seen = delta_segments_seen(scratch);
+    if (n_max >= jb::kSerialBigBatch) {
+      const int64_t why = seen != nullptr ? ((volatile int64_t*)seen)[0] : 0;
+      const int64_t prev = seen != nullptr ? ((volatile int64_t*)seen)[1] : 0;
+      const bool short_of = why != jb::kStopDone && why != jb::kStopDense;
+      nseg = short_of ? jb::kVerifiedSegmentsMax
+                      : (int)std::min<int64_t>(jb::kVerifiedSegmentsMax,
+                                               std::max<int64_t>(jb::kDeltaSegmentsMin, prev + prev / 2 + 8));
+    } else {
+      nseg = 8;
+    }
+    const int rc = jb_vcommit_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W, S, active,
+                                      LC, method, C, stats, touched, scratch, nseg, stream);
+    if (rc == 0 && seen != nullptr)
+      (void)hipMemcpyAsync(seen, (int64_t*)scratch + 20, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, stream);
+    return rc;
+  }
   if (LC <= 64 && serial_committer() == 1) {
     // delta committer: segments end only when the LDS row store fills. A
     // segment that finds the batch done costs two empty launches (~4 us), a

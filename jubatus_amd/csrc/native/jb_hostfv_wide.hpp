@@ -15,6 +15,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -23,11 +25,58 @@
 #include "jb_hash.hpp"
 #include "jb_hostfv.hpp"
 #include "jb_msgpack.hpp"
+#include "jb_plugin_host.hpp"
 
 namespace jb {
 
-// string rule value_kind bit fields (fv_converter/gpu_path.py)
-constexpr int kSplitStr = 0, kSplitNgram = 1, kSplitSpace = 2;
+// string rule value_kind bit fields (fv_converter/gpu_path.py); kSplitPlugin:
+// a "dynamic" splitter (pad: its plug-in in WideExt)
+constexpr int kSplitStr = 0, kSplitNgram = 1, kSplitSpace = 2, kSplitPlugin = 3;
+// num rule value_kind: num, log, a "dynamic" num_feature plug-in (pad: its
+// index), add (pad: the value's index in WideExt::addv), str
+constexpr int kNumNum = 0, kNumLog = 1, kNumPlugin = 2, kNumAdd = 3, kNumStr = 4;
+// combination rule value_kind: add, mul, a "dynamic" plug-in (pad: its index)
+constexpr int kCombAdd = 0, kCombMul = 1, kCombPlugin = 2;
+
+// What the rule tables cannot carry: the plug-ins of "dynamic" types
+// (jb_plugin_host.hpp), the filter rules, the binary rules and the values of
+// "add" num types. Output order and names are those of the Python converter
+// (fv_converter/converter.py _filtered / _convert).
+struct WideExt {
+  std::vector<std::unique_ptr<plug::Plugin>> plugins;
+  // num filter kinds
+  enum { kAdd = 0, kLinear = 1, kGauss = 2, kSigmoid = 3, kPlug = 4 };
+  struct Filter {
+    HostRule m;            // key matcher (its argument in blob)
+    std::string suffix;
+    int kind = kPlug;      // string filters: plug-ins only
+    double a = 0, b = 0;
+    bool trunc = true;
+    int plug = -1;
+  };
+  std::vector<Filter> sf, nf;
+  struct BinRule {
+    HostRule m;
+    std::string type;      // "@<type>"
+    int plug;
+  };
+  std::vector<BinRule> br;
+  std::vector<double> addv;
+  std::string blob;
+  int add_plugin(std::unique_ptr<plug::Plugin> p) {
+    plugins.push_back(std::move(p));
+    return (int)plugins.size() - 1;
+  }
+  bool needed() const { return !plugins.empty() || !sf.empty() || !nf.empty() || !br.empty() || !addv.empty(); }
+};
+
+// %.17g of a value, an integer without a fraction (converter.py _num_str)
+inline std::string num_str(double x) {
+  char b[64];
+  if (x == (double)(long long)x && fabs(x) < 1e16) snprintf(b, sizeof(b), "%lld", (long long)x);
+  else snprintf(b, sizeof(b), "%.17g", x);
+  return b;
+}
 constexpr int kSwBin = 0, kSwTf = 1, kSwLogTf = 2;
 constexpr int kGwBin = 0, kGwIdf = 1, kGwBm25 = 2;
 
@@ -75,6 +124,9 @@ class HostFvWide {
     df_ = df; diff_ = diff; counts_ = counts;
   }
   bool needs_weights() const { return global_; }
+  // plug-ins, filters, binary rules (shared: every converter built from one
+  // config may hold it)
+  void set_ext(std::shared_ptr<WideExt> e) { ext_ = std::move(e); }
   // the table height of the document statistics when it differs from the
   // feature index's (clustering keys features over 2^31 - 1 while the
   // weight manager counts them in the converter's hash_max_size rows)
@@ -173,19 +225,114 @@ class HostFvWide {
     }
   }
 
+  bool match_ext(const HostRule& r, const uint8_t* k, uint32_t kn) const {
+    if (r.match_kind == 0) return true;
+    const uint8_t* m = (const uint8_t*)ext_->blob.data() + r.match_off;
+    const uint32_t mn = (uint32_t)r.match_len;
+    if (r.match_kind == 3 && kn != mn) return false;
+    if (kn < mn) return false;
+    const uint8_t* base = (r.match_kind == 2) ? (k + kn - mn) : k;
+    return memcmp(base, m, mn) == 0;
+  }
+  // bytes that must live until the datum's features are out (filtered keys
+  // and values, plug-in tokens and names): a deque never moves its strings
+  const std::string& keep(std::string s) {
+    store_.push_back(std::move(s));
+    return store_.back();
+  }
+  static const uint8_t* u8(const std::string& s) { return (const uint8_t*)s.data(); }
+
+  void add_feat(const WideName& nm, double w, int gw) {
+    WideFeat f;
+    f.h = nm.fnv(kFnvOffset);
+    f.idx = (int32_t)hash_to_index(f.h, H_);
+    f.w = w;
+    f.gw = gw;
+    f.name = nm;
+    feats_.push_back(f);
+  }
+
   int datum(Cursor& c, int32_t* idx, float* val, int64_t max_slots, int64_t* slots, bool update) {
     uint32_t top, ns, nn;
     if (!c.array(&top) || top < 2) return 1;
     feats_.clear();
+    store_.clear();
+    sv_.clear();
+    nv_.clear();
     if (!c.array(&ns)) return 1;
     for (uint32_t i = 0; i < ns; ++i) {
       uint32_t two; const uint8_t *k, *v; uint32_t kn, vn;
       if (!c.array(&two) || two != 2 || !c.raw(&k, &kn) || !c.raw(&v, &vn)) return 1;
+      sv_.push_back({k, kn, v, vn});
+    }
+    if (!c.array(&nn)) return 1;
+    for (uint32_t i = 0; i < nn; ++i) {
+      uint32_t two; const uint8_t* k; uint32_t kn; double x;
+      if (!c.array(&two) || two != 2 || !c.raw(&k, &kn) || !c.number(&x)) return 1;
+      nv_.push_back({k, kn, x});
+    }
+    // filters (converter.py _filtered): every filter sees the values the
+    // earlier ones appended
+    if (ext_) {
+      for (const WideExt::Filter& f : ext_->sf) {
+        const size_t n0 = sv_.size();
+        for (size_t i = 0; i < n0; ++i) {
+          const SV e = sv_[i];
+          if (!match_ext(f.m, e.k, e.kn)) continue;
+          const std::string& nk = keep(std::string((const char*)e.k, e.kn) + f.suffix);
+          const std::string& nvl = keep(ext_->plugins[(size_t)f.plug]->filter_string((const char*)e.v, e.vn));
+          sv_.push_back({u8(nk), (uint32_t)nk.size(), u8(nvl), (uint32_t)nvl.size()});
+        }
+      }
+      for (const WideExt::Filter& f : ext_->nf) {
+        const size_t n0 = nv_.size();
+        for (size_t i = 0; i < n0; ++i) {
+          const NV e = nv_[i];
+          if (!match_ext(f.m, e.k, e.kn)) continue;
+          double y;
+          switch (f.kind) {
+            case WideExt::kAdd: y = e.x + f.a; break;
+            case WideExt::kLinear:
+              y = (e.x - f.a) / (f.b - f.a);
+              if (f.trunc) y = std::min(1.0, std::max(0.0, y));
+              break;
+            case WideExt::kGauss: y = (e.x - f.a) / f.b; break;
+            case WideExt::kSigmoid: y = 1.0 / (1.0 + exp(-f.a * (e.x - f.b))); break;
+            default: y = ext_->plugins[(size_t)f.plug]->filter_num(e.x); break;
+          }
+          const std::string& nk = keep(std::string((const char*)e.k, e.kn) + f.suffix);
+          nv_.push_back({u8(nk), (uint32_t)nk.size(), y});
+        }
+      }
+    }
+    for (const SV& e : sv_) {
+      const uint8_t *k = e.k, *v = e.v;
+      const uint32_t kn = e.kn, vn = e.vn;
       uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
       hk = fnv_bytes(hk, (const uint8_t*)"$", 1);
       for (const HostRule& r : s_) {
         if (!match_key(r, k, kn)) continue;
         const int sp = r.value_kind & 15, sw = r.value_kind >> 4 & 15, gw = r.value_kind >> 8 & 15;
+        const uint8_t* suf = blob_.data() + r.suffix_off;
+        if (sp == kSplitPlugin) {
+          // a plug-in splitter: its tokens' bytes, counted in first-occurrence order
+          ext_->plugins[(size_t)r.pad]->split((const char*)v, vn, &ptok_);
+          uniqs_.clear();
+          for (const std::string& t : ptok_) {
+            bool found = false;
+            for (auto& u : uniqs_)
+              if (u.first == t) { ++u.second; found = true; break; }
+            if (!found) uniqs_.emplace_back(t, 1);
+          }
+          for (const auto& u : uniqs_) {
+            const std::string& tok = keep(u.first);
+            const double w = sw == kSwBin ? 1.0 : sw == kSwTf ? (double)u.second : log(1.0 + (double)u.second);
+            add_feat(WideName{{k, (const uint8_t*)"$", u8(tok), suf}, {kn, 1, (uint32_t)tok.size(),
+                                                                         (uint32_t)r.suffix_len}, 4},
+                     w, gw);
+          }
+          continue;
+        }
         split(sp, r.pad, v, vn);
         // distinct tokens in first-occurrence order with their counts
         uniq_.clear();
@@ -205,7 +352,6 @@ class HostFvWide {
             else ++uniq_[it.first->second].cnt;
           }
         }
-        const uint8_t* suf = blob_.data() + r.suffix_off;
         for (const auto& u : uniq_) {
           WideFeat f;
           f.h = fnv_bytes(fnv_bytes(hk, v + u.off, u.len), suf, (size_t)r.suffix_len);
@@ -218,24 +364,60 @@ class HostFvWide {
       }
     }
     if (global_) weigh(update);
-    if (!c.array(&nn)) return 1;
-    for (uint32_t i = 0; i < nn; ++i) {
-      uint32_t two; const uint8_t* k; uint32_t kn; double x;
-      if (!c.array(&two) || two != 2 || !c.raw(&k, &kn) || !c.number(&x)) return 1;
+    for (const NV& e : nv_) {
+      const uint8_t* k = e.k;
+      const uint32_t kn = e.kn;
+      const double x = e.x;
       const uint64_t hk = fnv_bytes(kFnvOffset, k, kn);
       for (const HostRule& r : n_) {
         if (!match_key(r, k, kn)) continue;
         const uint8_t* suf = blob_.data() + r.suffix_off;
+        if (r.value_kind == kNumPlugin) {
+          ext_->plugins[(size_t)r.pad]->num_feature(std::string((const char*)k, kn), x, &pnamed_);
+          for (const auto& nv : pnamed_) {
+            const std::string& nm = keep(nv.first);
+            add_feat(WideName{{u8(nm), nullptr, nullptr, nullptr}, {(uint32_t)nm.size(), 0, 0, 0}, 1}, nv.second,
+                     kGwBin);
+          }
+          continue;
+        }
+        if (r.value_kind == kNumStr) {      // <key>$<value>@<type>, weight 1
+          const std::string& vs = keep(num_str(x));
+          add_feat(WideName{{k, (const uint8_t*)"$", u8(vs), suf}, {kn, 1, (uint32_t)vs.size(),
+                                                                    (uint32_t)r.suffix_len}, 4},
+                   1.0, kGwBin);
+          continue;
+        }
         WideFeat f;
         f.h = fnv_bytes(hk, suf, (size_t)r.suffix_len);
         f.idx = (int32_t)hash_to_index(f.h, H_);
-        f.w = r.value_kind == 1 ? log(x > 1.0 ? x : 1.0) : x;
+        f.w = r.value_kind == kNumLog ? log(x > 1.0 ? x : 1.0)
+              : r.value_kind == kNumAdd ? x + ext_->addv[(size_t)r.pad] : x;
         f.gw = kGwBin;
         f.name = WideName{{k, suf, nullptr, nullptr}, {kn, (uint32_t)r.suffix_len, 0, 0}, 2};
         feats_.push_back(f);
       }
     }
-    for (uint32_t i = 2; i < top; ++i)   // binary values carry no feature on this path
+    // binary values: plug-in features <key>$<token>@<type> (others carry none)
+    if (top >= 3 && ext_ && !ext_->br.empty()) {
+      uint32_t nb;
+      if (!c.array(&nb)) return 1;
+      for (uint32_t i = 0; i < nb; ++i) {
+        uint32_t two; const uint8_t *k, *v; uint32_t kn, vn;
+        if (!c.array(&two) || two != 2 || !c.raw(&k, &kn) || !c.raw(&v, &vn)) return 1;
+        for (const WideExt::BinRule& r : ext_->br) {
+          if (!match_ext(r.m, k, kn)) continue;
+          ext_->plugins[(size_t)r.plug]->binary_feature(std::string((const char*)k, kn), (const char*)v, vn, &pnamed_);
+          for (const auto& tv : pnamed_) {
+            const std::string& tok = keep(tv.first);
+            add_feat(WideName{{k, (const uint8_t*)"$", u8(tok), u8(r.type)},
+                              {kn, 1, (uint32_t)tok.size(), (uint32_t)r.type.size()}, 4},
+                     tv.second, kGwBin);
+          }
+        }
+      }
+    }
+    for (uint32_t i = (top >= 3 && ext_ && !ext_->br.empty()) ? 3 : 2; i < top; ++i)   // the rest carries no feature
       if (!c.skip()) return 1;
     const size_t nb = feats_.size();
     for (size_t i = 0; i < nb; ++i) {
@@ -258,7 +440,9 @@ class HostFvWide {
           const uint64_t h = fnv_bytes(feats_[j].name.fnv(hi), suf, (size_t)L.suffix_len);
           idx[*slots] = (int32_t)hash_to_index(h, H_);
           const double a = feats_[i].w, b = feats_[j].w;
-          val[*slots] = (float)(L.value_kind == 1 ? a * b : a + b);
+          val[*slots] = (float)(L.value_kind == kCombMul ? a * b
+                                : L.value_kind == kCombPlugin ? ext_->plugins[(size_t)L.pad]->combine(a, b)
+                                                              : a + b);
           ++*slots;
           if (names_) {     // left & right + the rule's suffix (the hashed bytes)
             put_name(feats_[i].name, false);
@@ -334,6 +518,16 @@ class HostFvWide {
   std::vector<int32_t> gidx_;
   std::vector<int32_t> journal_;
   int64_t jdocs_ = 0, jlen_ = 0;
+  // one datum's values (spans into the body or into store_) and extension state
+  struct SV { const uint8_t* k; uint32_t kn; const uint8_t* v; uint32_t vn; };
+  struct NV { const uint8_t* k; uint32_t kn; double x; };
+  std::vector<SV> sv_;
+  std::vector<NV> nv_;
+  std::deque<std::string> store_;
+  std::shared_ptr<WideExt> ext_;
+  std::vector<std::string> ptok_;
+  std::vector<std::pair<std::string, int>> uniqs_;
+  std::vector<std::pair<std::string, double>> pnamed_;
 };
 
 }  // namespace jb

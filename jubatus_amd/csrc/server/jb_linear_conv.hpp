@@ -25,6 +25,7 @@ struct WideRules {
   std::vector<HostRule> s, n, c;
   std::string blob;
   bool global = false;
+  std::shared_ptr<WideExt> ext;   // plug-ins ("dynamic" types), filters, binary rules
 };
 
 // the converter section: fast rules, else wide rules (why: the reason neither fits)
@@ -34,7 +35,7 @@ inline bool build_linear_rules(const Value& conv, Rules* fast, bool* wide, WideR
   if (build_rules(conv, fast, &why_fast)) return true;
   uint64_t H = fast->H;
   std::string why_wide;
-  if (!jb::row::build_wide_rules(conv, &w->s, &w->n, &w->c, &w->blob, &H, &w->global, &why_wide)) {
+  if (!jb::row::build_wide_rules(conv, &w->s, &w->n, &w->c, &w->blob, &H, &w->global, &why_wide, &w->ext)) {
     *why = why_fast + "; " + why_wide;
     return false;
   }
@@ -154,6 +155,7 @@ class LinearConv {
     wide_.reset(new HostFvWide((const uint8_t*)w.s.data(), (int)w.s.size(), (const uint8_t*)w.n.data(),
                                (int)w.n.size(), (const uint8_t*)w.c.data(), (int)w.c.size() / 2,
                                (const uint8_t*)w.blob.data(), w.blob.size(), H_));
+    wide_->set_ext(w.ext);
     if (wide_->needs_weights()) {
       st_.reset(H_);
       st_.attach(wide_.get());

@@ -116,11 +116,13 @@ class Converter {
     std::vector<HostRule> s, n, c;
     std::string blob;
     uint64_t H = 1ull << 20;
-    if (!build_wide_rules(conv, &s, &n, &c, &blob, &H, &global_, why)) return false;
+    std::shared_ptr<WideExt> ext;
+    if (!build_wide_rules(conv, &s, &n, &c, &blob, &H, &global_, why, &ext)) return false;
     H_ = H;
     wide_.reset(new HostFvWide((const uint8_t*)s.data(), (int)s.size(), (const uint8_t*)n.data(),
                                (int)n.size(), (const uint8_t*)c.data(), (int)c.size() / 2,
                                (const uint8_t*)blob.data(), blob.size(), H));
+    wide_->set_ext(ext);
     if (wide_->needs_weights()) {
       df_.assign(H, 0);
       diff_.assign(H, 0);

@@ -62,6 +62,7 @@ struct Params {
   std::string blob;
   uint64_t H = 1ull << 20;
   bool global = false;
+  std::shared_ptr<jb::WideExt> ext;   // plug-ins, filters, binary rules
 };
 
 double num_or(const Value* p, const char* k, double d) {
@@ -105,7 +106,7 @@ bool check_config(const std::string& text, std::string* why, Params* out) {
   const Value* conv = v.get("converter");
   Value empty;
   empty.kind = Value::MAP;
-  if (!jb::row::build_wide_rules(conv ? *conv : empty, &p.s, &p.n, &p.c, &p.blob, &p.H, &p.global, why))
+  if (!jb::row::build_wide_rules(conv ? *conv : empty, &p.s, &p.n, &p.c, &p.blob, &p.H, &p.global, why, &p.ext))
     return false;
   if (out) *out = std::move(p);
   return true;
@@ -185,6 +186,7 @@ class Clustering : public HostEngine {
     hw_.reset(new jb::HostFvWide((const uint8_t*)p_.s.data(), (int)p_.s.size(), (const uint8_t*)p_.n.data(),
                                  (int)p_.n.size(), (const uint8_t*)p_.c.data(), (int)p_.c.size() / 2,
                                  (const uint8_t*)p_.blob.data(), p_.blob.size(), kKeySpace));
+    hw_->set_ext(p_.ext);
     if (p_.global) {   // document statistics over the converter's table height
       stats_.reset(p_.H);
       stats_.attach(hw_.get());

@@ -29,6 +29,7 @@ struct WideConfig {
   std::string blob;
   uint64_t H = 1ull << 20;      // fv_converter/converter.py DEFAULT_HASH_MAX_SIZE
   bool global = false;
+  std::shared_ptr<jb::WideExt> ext;   // plug-ins, filters, binary rules
 };
 
 bool check_config(const std::string& text, std::string* why, WideConfig* out) {
@@ -42,7 +43,7 @@ bool check_config(const std::string& text, std::string* why, WideConfig* out) {
   const Value* conv = v.get("converter");
   if (!conv) { *why = "weight config requires converter"; return false; }
   WideConfig w;
-  if (!jb::row::build_wide_rules(*conv, &w.s, &w.n, &w.c, &w.blob, &w.H, &w.global, why)) return false;
+  if (!jb::row::build_wide_rules(*conv, &w.s, &w.n, &w.c, &w.blob, &w.H, &w.global, why, &w.ext)) return false;
   if (out) *out = std::move(w);
   return true;
 }
@@ -75,6 +76,7 @@ class Weight : public HostEngine {
                                  (const uint8_t*)cfg_.n.data(), (int)cfg_.n.size(),
                                  (const uint8_t*)cfg_.c.data(), (int)cfg_.c.size() / 2,
                                  (const uint8_t*)cfg_.blob.data(), cfg_.blob.size(), cfg_.H));
+    hw_->set_ext(cfg_.ext);
     if (hw_->needs_weights()) {
       df_.assign(cfg_.H, 0);
       diff_.assign(cfg_.H, 0);

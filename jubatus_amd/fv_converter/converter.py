@@ -406,8 +406,12 @@ class DatumToFvConverter:
             elif m == "dynamic":
                 plug = self._plugin("num_feature", _params(p))
                 nt[name] = (lambda plug: lambda k, x: list(plug(k, x)))(plug)
-            elif m in ("num", "log", "str"):
-                nt[name] = nt[m]
+            elif m == "num":       # a user type is named after itself (key@<type>), as the GPU rules
+                nt[name] = (lambda n: lambda k, x: [(f"{k}@{n}", x)])(name)
+            elif m == "log":
+                nt[name] = (lambda n: lambda k, x: [(f"{k}@{n}", math.log(max(1.0, x)))])(name)
+            elif m == "str":
+                nt[name] = (lambda n: lambda k, x: [(f"{k}${_num_str(x)}@{n}", 1.0)])(name)
             else:
                 raise ConverterError(f"unknown num type method: {m}")
             num_meta[name] = m

@@ -673,6 +673,17 @@ class SerialScratch:
         reasons = ("done", "saturated", "dense", "rescore")
         out = {"tail_start": v[0], "end": v[1], "exact_steps": v[2], "rounds": v[3],
                "segments": v[21], "stop_reason": reasons[v[20]] if 0 <= v[20] < 4 else v[20]}
+        if v[31] == 1:
+            # verified committer (csrc/hip/vcommit.hip): windows, verification
+            # retries, candidates the committer walked, non-candidates cleared
+            # by the bound, the window length / threshold T it ends with
+            import struct
+            out.update(verified=True, windows=v[21] - v[28], retries=v[28], saturated_windows=v[29],
+                       candidates=v[27], non_candidates_verified=v[7], committer_updates=v[24],
+                       wasted_steps=v[22], refreshes=v[23], exact_rescored=v[26], last_segment_rows=v[25],
+                       window_len=v[8], T=round(struct.unpack("f", struct.pack("I", v[9] & 0xffffffff))[0], 4),
+                       commit_kernel_us=round(v[30] / 100.0, 1))
+            return out
         if v[24] > 0 or v[22] > 0:
             # delta committer (csrc/hip/commit.hip): steps that did not update,
             # guard-band re-scores, updates, rows in the LDS store at the end

@@ -506,6 +506,62 @@ def test_serial_mode_big_batch_rescores(method):
                                    atol=2e-3 * float(c.P.max()))
 
 
+def _bench_like(n, nlabels=8, seed=51, p_corr=0.6, vocab=3000):
+    """the headline bench's datum shape (label-correlated tokens, shared
+    numeric keys), small vocabulary so windows fill the committer's store"""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        y = rng.randrange(nlabels)
+        sv = [[f"s{j}", f"t{y * 131 + rng.randrange(16) if rng.random() < p_corr else rng.randrange(vocab)}"]
+              for j in range(6)]
+        nv = [[f"n{j}", (y - nlabels / 2) * 0.05 + rng.gauss(0.0, 1.0)] for j in range(4)]
+        out.append((f"L{y}", [sv, nv, []]))
+    return out
+
+
+@pytest.mark.parametrize("method,t_force", [("AROW", None), ("PA1", None), ("AROW", "0.001"), ("CW", "0.001")])
+def test_serial_mode_verified_windows(method, t_force, monkeypatch):
+    """the verified committer (csrc/hip/vcommit.hip) over big batches: several
+    windows per batch (the store fills), candidates walked by the one-wave
+    committer, the rest cleared by the bound. t_force: a candidate threshold
+    so small that verification fails and windows run again (the retry path).
+    The result must be the requests applied one after the other."""
+    from jubatus_amd.models.classifier import LinearClassifier
+
+    if t_force is not None:
+        monkeypatch.setenv("JB_VERIFIED_T", t_force)
+    param = {"regularization_weight": 0.5}
+    data = _bench_like(128 * 160 * 2, seed=53 + len(method))
+    reqs = [data[i:i + 160] for i in range(0, len(data), 160)]
+    g = LinearClassifier(method, param, DatumToFvConverter(CONV), device=_device())
+    for r in reqs[:2]:
+        g.train(r)
+    diags = []
+    half = 2 + (len(reqs) - 2) // 2
+    for lo, hi in ((2, half), (half, len(reqs))):      # two big batches (>= 16384 samples each)
+        g.train_requests([msgpack.packb([[l, d] for l, d in r], use_bin_type=False) for r in reqs[lo:hi]])
+        g.synchronize()
+        diags.append(g._serial.last_batch())
+    c = _oracle_serial(method, param, CONV, reqs)
+    g.pipe.check_errors()
+    print(diags)
+    for d in diags:
+        assert d.get("verified"), d
+        assert d["tail_start"] == d["end"], d          # no sequential tail
+    assert max(d["windows"] for d in diags) > 1, diags
+    if t_force is not None:
+        assert sum(d["retries"] for d in diags) > 0, diags
+    st = g.train_stats()
+    assert st["trained"] == len(data)
+    assert st["updated"] == c.train_stats()["updated"], (st, c.train_stats())
+    scale = float(np.abs(c.W).max()) or 1.0
+    np.testing.assert_allclose(g.W.cpu().numpy()[:, :c.LC], c.W, rtol=2e-3, atol=2e-3 * scale)
+    if c.P is not None:
+        np.testing.assert_allclose(g.P.cpu().numpy()[:, :c.LC], c.P, rtol=2e-3,
+                                   atol=2e-3 * float(c.P.max()))
+
+
 @pytest.mark.parametrize("nlabels", [6, 100])
 def test_serial_mode_every_sample_updates(nlabels):
     """noise labels: (almost) every sample updates, so the committer hands

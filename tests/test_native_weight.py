@@ -19,7 +19,23 @@ from jubatus_amd.common.mprpc import RpcClient, RpcIOError, RpcTimeoutError
 
 NATIVE = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaweight")
 
+PLUG = "libjubatus_sample_plugins.so"
 CONFIGS = {
+    # plug-ins loaded by the native server (dlopen, jb_plugin_host.hpp): splitter,
+    # string / num filters, num feature, combination; idf over the plug-in tokens
+    "plugin": {"string_filter_types": {"up": {"method": "dynamic", "path": PLUG, "function": "create_upper_filter"}},
+               "string_filter_rules": [{"key": "s", "type": "up", "suffix": "-up"}],
+               "num_filter_types": {"aff": {"method": "dynamic", "path": PLUG, "function": "create_affine_filter",
+                                            "scale": "2", "shift": "1"}},
+               "num_filter_rules": [{"key": "*", "type": "aff", "suffix": "-aff"}],
+               "string_types": {"sp": {"method": "dynamic", "path": PLUG, "function": "create_splitter",
+                                       "delimiter": " ", "min_length": "2"}},
+               "string_rules": [{"key": "*", "type": "sp", "sample_weight": "tf", "global_weight": "idf"}],
+               "num_types": {"bk": {"method": "dynamic", "path": PLUG, "function": "create_bucket_feature",
+                                    "width": "10"}},
+               "num_rules": [{"key": "*", "type": "bk"}, {"key": "*", "type": "num"}],
+               "combination_types": {"mx": {"method": "dynamic", "path": PLUG, "function": "create_max_combination"}},
+               "combination_rules": [{"key_left": "*@num", "key_right": "*-aff@num", "type": "mx"}]},
     "bin": {"string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
             "num_rules": [{"key": "*", "type": "num"}]},
     "idf": {"string_types": {"bigram": {"method": "ngram", "char_num": "2"}},

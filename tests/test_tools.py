@@ -96,7 +96,35 @@ JUBACONV_INPUTS = [
                       {"key": "*", "type": "space", "sample_weight": "log_tf", "global_weight": "bin"}],
      "num_rules": [{"key": "*", "type": "log"}],
      "combination_rules": [{"key_left": "*", "key_right": "*", "type": "add"}]},
-    # outside the wide set (a filter): the native tool hands it to the Python twin
+    # plug-ins ("dynamic": splitter, string / num filters, num feature,
+    # combination) and the built-in num filters / types: loaded natively (dlopen)
+    {"string_filter_types": {"up": {"method": "dynamic", "path": "libjubatus_sample_plugins.so",
+                                    "function": "create_upper_filter"}},
+     "string_filter_rules": [{"key": "/t*", "type": "up", "suffix": "-up"}],
+     "num_filter_types": {"aff": {"method": "dynamic", "path": "libjubatus_sample_plugins.so",
+                                  "function": "create_affine_filter", "scale": "2", "shift": "1"},
+                          "lin": {"method": "linear_normalization", "min": "0", "max": "100"},
+                          "gs": {"method": "gaussian_normalization", "average": 1, "standard_deviation": 2.5},
+                          "sg": {"method": "sigmoid_normalization", "gain": 0.5, "bias": 1.0},
+                          "ad": {"method": "add", "value": 3}},
+     "num_filter_rules": [{"key": "/n*", "type": "aff", "suffix": "-aff"},
+                          {"key": "*", "type": "lin", "suffix": "-lin"},
+                          {"key": "/w", "type": "gs", "suffix": "-gs"},
+                          {"key": "/w", "type": "sg", "suffix": "-sg"},
+                          {"key": "/user/age", "type": "ad", "suffix": "-ad"}],
+     "string_types": {"sp": {"method": "dynamic", "path": "libjubatus_sample_plugins.so",
+                             "function": "create_splitter", "delimiter": " ", "min_length": "2"}},
+     "string_rules": [{"key": "*", "type": "sp", "sample_weight": "tf", "global_weight": "bin"},
+                      {"key": "/user/name", "type": "str", "sample_weight": "bin", "global_weight": "bin"}],
+     "num_types": {"bk": {"method": "dynamic", "path": "libjubatus_sample_plugins.so",
+                          "function": "create_bucket_feature", "width": "10"},
+                   "plus": {"method": "add", "value": "0.5"}, "s": {"method": "str"}},
+     "num_rules": [{"key": "*", "type": "bk"}, {"key": "/w*", "type": "plus"}, {"key": "/user/age", "type": "s"},
+                   {"key": "*", "type": "num"}],
+     "combination_types": {"mx": {"method": "dynamic", "path": "libjubatus_sample_plugins.so",
+                                  "function": "create_max_combination"}},
+     "combination_rules": [{"key_left": "/w@num", "key_right": "*", "type": "mx"}]},
+    # outside the native set (a regexp filter): the native tool hands it to the Python twin
     {"string_filter_types": {"dl": {"method": "regexp", "pattern": "o", "replace": ""}},
      "string_filter_rules": [{"key": "/text", "type": "dl", "suffix": "-x"}],
      "string_rules": [{"key": "*", "type": "str", "sample_weight": "bin", "global_weight": "bin"}]},
@@ -113,8 +141,10 @@ def test_native_jubaconv_matches_python(tmp_path, conf):
             args = ["-i", i, "-o", o] + (["-c", str(cfg)] if o == "fv" else [])
             py = io.StringIO()
             prc = jubaconv.main(args, stdin=io.StringIO(js), out=py)
-            r = subprocess.run([exe, *args], input=js, capture_output=True, text=True, timeout=60,
-                               env=dict(os.environ, PYTHONPATH=ROOT))
+            env = dict(os.environ, PYTHONPATH=ROOT)
+            if '"dynamic"' in json.dumps(conf):
+                env["PATH"] = "/nonexistent"     # plug-in configs: no Python fallback to hide behind
+            r = subprocess.run([exe, *args], input=js, capture_output=True, text=True, timeout=60, env=env)
             assert (r.returncode, r.stdout) == (prc & 0xff, py.getvalue()), (i, o, js, r.stderr)
             if o == "datum":    # the datum output read back as input
                 d = r.stdout
