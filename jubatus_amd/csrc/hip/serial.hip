@@ -795,10 +795,17 @@ extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, con
 
 // pinned host words per scratch buffer: the last delta batch's final stop
 // reason and segment count (tail[20], tail[21])
-static int64_t* delta_segments_seen(void* scratch) {
+static std::mutex& delta_seen_mu() {
   static std::mutex mu;
+  return mu;
+}
+static std::unordered_map<void*, int64_t*>& delta_seen_map() {
   static std::unordered_map<void*, int64_t*> seen;
-  std::lock_guard<std::mutex> g(mu);
+  return seen;
+}
+static int64_t* delta_segments_seen(void* scratch) {
+  std::lock_guard<std::mutex> g(delta_seen_mu());
+  auto& seen = delta_seen_map();
   auto it = seen.find(scratch);
   if (it != seen.end()) return it->second;
   int64_t* p = nullptr;
@@ -821,6 +828,18 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
                                   float* W, float* S, const int32_t* active, int LC, int method, float C,
                                   unsigned long long* stats, uint8_t* touched, void* scratch, int nseg,
                                   hipStream_t stream);
+
+// a scratch buffer's owner (re)allocated it: the pinned words of a freed
+// buffer that had the same address must not carry its segment history over
+extern "C" int jb_serial_scratch_forget(void* scratch) {
+  std::lock_guard<std::mutex> g(delta_seen_mu());
+  auto& seen = delta_seen_map();
+  auto it = seen.find(scratch);
+  if (it == seen.end()) return 0;
+  (void)hipHostFree(it->second);
+  seen.erase(it);
+  return 1;
+}
 
 // committer of LC <= 64: 2 = verified (vcommit.hip, default), 1 = delta
 // (commit.hip, JB_SERIAL_COMMITTER=delta), 0 = this file's bound committer

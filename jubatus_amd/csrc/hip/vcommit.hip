@@ -53,17 +53,25 @@
 // Device state (int64 words, 256 B) lives in the kSerial scratch; every kernel
 // reads the status first, so a batch's segments are queued without a host round
 // trip and the finished ones cost an empty launch each.
+#include <type_traits>
+
 #include "jb_commit.hpp"
 
 namespace jb {
 namespace vc {
 
 using dc::Geo;
-constexpr int kR = 4;                   // samples per 16-lane group per round
+#ifndef JB_VC_R
+#define JB_VC_R 2
+#endif
+constexpr int kR = JB_VC_R;             // samples per 16-lane group per round
 constexpr int kNS = 4 * kR;             // candidates per round (one wave)
 constexpr int kFC = 2;                  // feature chunks of 16 per lane
 constexpr int kNFM = 16 * kFC;          // widest sample the committer takes
-constexpr int kPD = 2;                  // rounds of records in flight
+#ifndef JB_VC_PD
+#define JB_VC_PD 2
+#endif
+constexpr int kPD = JB_VC_PD;           // rounds of records in flight
 constexpr int64_t kLwMin = 2048, kLwMax = 65536, kLwInit = 8192;
 constexpr int kBitWords = (int)(kLwMax / 64);
 constexpr float kTInit = 0.5f, kTMin = 0.125f, kTMax = 64.f;
@@ -526,191 +534,218 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
       }
       if (k == dc::kInf) break;
       const int Gk = k / kR, rk = k % kR;
+      (void)rk;
       const bool mine = G == Gk;
-      S t = sc[0];
-      int sl[kFC];
+      // the step of sample k, with its round slot a compile-time index (a
+      // runtime one puts the samples in scratch memory: a load that drains
+      // every prefetch in flight)
+      auto step_of = [&](auto RKc) __attribute__((always_inline)) -> int {
+        constexpr int rk = decltype(RKc)::value;
+        S t = sc[rk];
+        int sl[kFC];
 #pragma unroll
-      for (int c = 0; c < kFC; ++c) sl[c] = slot[0][c];
-#pragma unroll
-      for (int r = 1; r < kR; ++r)
-        if (r == rk) {
-          t = sc[r];
-#pragma unroll
-          for (int c = 0; c < kFC; ++c) sl[c] = slot[r][c];
-        }
-      const int kpos = __builtin_amdgcn_readlane(t.pos, Gk * 16);
-      const int knf = __builtin_amdgcn_readlane(t.nf, Gk * 16);
-      if (knf > kNFM) {
-        stopped = 1;
-        why = kWhyDense;
-        pend = wb + kpos;
-        break;
-      }
-      const int y = t.y;
-      int ls = -1;
-      float m = 0.f, sy = 0.f, best = 0.f, var = 0.f;
-      float py[kFC], pl[kFC];
-      bool refreshed = false;
-      for (;;) {
-        m = dc::group_margin<LC>(t.s, y, act, sub, &ls, &sy, &best);
-        float v = 0.f;
-#pragma unroll
-        for (int c = 0; c < kFC; ++c) {
-          py[c] = 1.f;
-          pl[c] = 1.f;
-          const int32_t row = t.fi[c];
-          if (!use_s || row < 0) continue;
-          const float* dpr = s_dp + (sl[c] >= 0 ? sl[c] : NSLOT) * LC;
-          py[c] = t.py[c] + dpr[y];
-          if (ls >= 0) {
-            const float p0 = ls == t.ls0 ? t.pl[c] : P[(int64_t)row * LC + ls];
-            pl[c] = p0 + dpr[ls];
-          }
-          const float x2 = t.fx[c] * t.fx[c];
-          v += x2 * (1.f / py[c] + (ls >= 0 ? 1.f / pl[c] : 0.f));
-        }
-        var = use_s ? row16_sum(v) : 0.f;
-        if (refreshed) break;
-        const float thr = method == PERCEPTRON ? 0.f : method == CW ? C * var : 1.f;
-        const float g = kG * (1.f + fabsf(sy) + fabsf(best));
-        if (__builtin_amdgcn_ballot_w64(mine && fabsf(m - thr) < g) == 0) break;
-        // near the threshold: re-score from the live model (M0 + dW)
-        refreshed = true;
-        ++n_refresh;
-        float ns[K];
-#pragma unroll
-        for (int kk = 0; kk < K; ++kk) ns[kk] = 0.f;
-#pragma unroll
-        for (int c = 0; c < kFC; ++c) {
-#pragma unroll 1
-          for (int u = 0; u < 16; ++u) {
-            const int32_t ru = __shfl(t.fi[c], (lane & 48) + u, 64);
-            const float xu = __shfl(t.fx[c], (lane & 48) + u, 64);
-            const int su0 = __shfl(sl[c], (lane & 48) + u, 64);
-            const int su = su0 >= 0 ? su0 : NSLOT;
-            if (ru < 0) continue;
-#pragma unroll
-            for (int kk = 0; kk < K; ++kk) {
-              const int lab = sub + 16 * kk;
-              if (lab < LC) ns[kk] += xu * (W[(int64_t)ru * LC + lab] + s_dw[su * LC + lab]);
-            }
-          }
-        }
-#pragma unroll
-        for (int kk = 0; kk < K; ++kk) t.s[kk] = ns[kk];
-      }
-      float tau = 0.f, beta = 0.f;
-      const bool up_l = step_coeffs(method, m, var, t.nrm, ls >= 0, C, &tau, &beta);
-      const bool up = __builtin_amdgcn_ballot_w64(mine && up_l) != 0;
-      const int sid = n_steps++;
-      if (!up) {
-        ++n_waste;
-      } else {
-        // the sample's rows not in the store yet; a full bucket pair ends the
-        // window before this candidate (nothing of its step is applied)
-        bool full = false;
-        bool any_new = false;
-#pragma unroll
-        for (int c = 0; c < kFC; ++c) {
-          const bool need = mine && t.fi[c] >= 0 && sl[c] < 0;
-          any_new |= need;
-          if (need) {
-            sl[c] = dc::cache_insert<LC>(s_key, t.fi[c]);
-            full |= sl[c] < 0;
-          }
-        }
-        if (__builtin_amdgcn_ballot_w64(full) != 0) {
+        for (int c = 0; c < kFC; ++c) sl[c] = slot[rk][c];
+        const int kpos = __builtin_amdgcn_readlane(t.pos, Gk * 16);
+        const int knf = __builtin_amdgcn_readlane(t.nf, Gk * 16);
+        if (knf > kNFM) {
           stopped = 1;
-          why = kWhySat;
+          why = kWhyDense;
           pend = wb + kpos;
-          break;
+          return 1;
         }
-        const bool nins = __builtin_amdgcn_ballot_w64(any_new) != 0;
-        ++n_upd;
-        if (mine) {
+        const int y = t.y;
+        int ls = -1;
+        float m = 0.f, sy = 0.f, best = 0.f, var = 0.f;
+        float py[kFC], pl[kFC];
+        bool refreshed = false;
+        for (;;) {
+          m = dc::group_margin<LC>(t.s, y, act, sub, &ls, &sy, &best);
+          // P0 of the best wrong label: prefetched for the one at M0; another
+          // one is read from the table behind a wave-uniform branch (a
+          // conditional load the compiler joins waits for every load in flight)
+          float p0l[kFC];
 #pragma unroll
-          for (int c = 0; c < kFC; ++c)
-            if (t.fi[c] >= 0) {
-              float* sg = reinterpret_cast<float*>(&s_sg[sl[c]]);
-              sg[0] = __int_as_float(sid);
-              sg[1] = 0.f;
-              sg[2] = 0.f;
-            }
+          for (int c = 0; c < kFC; ++c) p0l[c] = t.pl[c];
+          if (use_s && __builtin_amdgcn_ballot_w64(mine && ls >= 0 && ls != t.ls0) != 0) {
+            // scalar loads at the group's (uniform) rows: they count on
+            // lgkmcnt, so waiting for them does not wait for the prefetches
+            const int lsu = __builtin_amdgcn_readlane(ls, Gk * 16);
 #pragma unroll
-          for (int c = 0; c < kFC; ++c) {
-            if (t.fi[c] < 0) continue;
-            const float x = t.fx[c];
-            const float a = use_s ? 1.f / py[c] : 1.f;
-            const float b = (use_s && ls >= 0) ? 1.f / pl[c] : 1.f;
-            const float dwy = tau * a * x;
-            const float dwl = ls >= 0 ? -tau * b * x : 0.f;
-            float* dwr = s_dw + sl[c] * LC;
-            atomicAdd(dwr + y, dwy);
-            if (ls >= 0) atomicAdd(dwr + ls, dwl);
-            if (use_s) {
-              float* dpr = s_dp + sl[c] * LC;
-              atomicAdd(dpr + y, dprec(method, beta, x, a));
-              if (ls >= 0) atomicAdd(dpr + ls, dprec(method, beta, x, b));
-            }
-            float* sg = reinterpret_cast<float*>(&s_sg[sl[c]]);
-            atomicAdd(sg + 1, dwy);
-            atomicAdd(sg + 2, dwl);
-            atomicAdd(sg + 3, fmaxf(fabsf(dwy), fabsf(dwl)));
-          }
-        }
-        // the later samples of the round: slots of the rows the step added,
-        // then the step's increments of their stamped rows
-        const int yk = __builtin_amdgcn_readlane(y, Gk * 16);
-        const int lk = __builtin_amdgcn_readlane(ls, Gk * 16);
-        if (nins) {
-#pragma unroll
-          for (int r = 0; r < kR; ++r) {
-            if (G * kR + r <= k || !alive[r]) continue;
-#pragma unroll
-            for (int c = 0; c < kFC; ++c)
-              if ((c == 0 || two) && slot[r][c] < 0 && sc[r].fi[c] >= 0)
-                slot[r][c] = dc::cache_find<LC>(s_key, sc[r].fi[c]);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < kR; ++r) {
-          const int pos = G * kR + r;
-          if (!alive[r] || pos <= k || sc[r].nf > kNFM) continue;
-          float cy = 0.f, cl = 0.f;
-#pragma unroll
-          for (int c = 0; c < kFC; ++c) {
-            const int s = slot[r][c];
-            if (s >= 0) {
-              const Stamp sg = s_sg[s];
-              if (__float_as_int(sg.sid) == sid) {
-                cy += sc[r].fx[c] * sg.dy;
-                cl += sc[r].fx[c] * sg.dl;
+            for (int c = 0; c < kFC; ++c) {
+              if (c > 0 && !two) break;
+              for (int u = 0; u < 16; ++u) {
+                const int ru = __builtin_amdgcn_readlane(t.fi[c], Gk * 16 + u);
+                if (ru < 0) continue;
+                const float pv = P[(int64_t)ru * LC + lsu];
+                p0l[c] = sub == u ? pv : p0l[c];
               }
             }
           }
-          cy = row16_sum(cy);
-          cl = row16_sum(cl);
-          if (exact[r]) {
+          float v = 0.f;
 #pragma unroll
-            for (int kk = 0; kk < K; ++kk) {
-              const int lab = sub + 16 * kk;
-              if (lab == yk) sc[r].s[kk] += cy;
-              if (lab == lk) sc[r].s[kk] += cl;
+          for (int c = 0; c < kFC; ++c) {
+            py[c] = 1.f;
+            pl[c] = 1.f;
+            const int32_t row = t.fi[c];
+            if (!use_s || row < 0) continue;
+            const float* dpr = s_dp + (sl[c] >= 0 ? sl[c] : NSLOT) * LC;
+            py[c] = t.py[c] + dpr[y];
+            if (ls >= 0) pl[c] = p0l[c] + dpr[ls];
+            const float x2 = t.fx[c] * t.fx[c];
+            v += x2 * (1.f / py[c] + (ls >= 0 ? 1.f / pl[c] : 0.f));
+          }
+          var = use_s ? row16_sum(v) : 0.f;
+          if (refreshed) break;
+          const float thr = method == PERCEPTRON ? 0.f : method == CW ? C * var : 1.f;
+          const float g = kG * (1.f + fabsf(sy) + fabsf(best));
+          if (__builtin_amdgcn_ballot_w64(mine && fabsf(m - thr) < g) == 0) break;
+          // near the threshold: re-score from the live model (M0 + dW)
+          refreshed = true;
+          ++n_refresh;
+          float ns[K];
+#pragma unroll
+          for (int kk = 0; kk < K; ++kk) ns[kk] = 0.f;
+#pragma unroll
+          for (int c = 0; c < kFC; ++c) {
+#pragma unroll 1
+            for (int u = 0; u < 16; ++u) {
+              const int32_t ru = __shfl(t.fi[c], (lane & 48) + u, 64);
+              const float xu = __shfl(t.fx[c], (lane & 48) + u, 64);
+              const int su0 = __shfl(sl[c], (lane & 48) + u, 64);
+              const int su = su0 >= 0 ? su0 : NSLOT;
+              if (ru < 0) continue;
+#pragma unroll
+              for (int kk = 0; kk < K; ++kk) {
+                const int lab = sub + 16 * kk;
+                if (lab < LC) ns[kk] += xu * (W[(int64_t)ru * LC + lab] + s_dw[su * LC + lab]);
+              }
             }
           }
-          slack[r] -= (fabsf(cy) + fabsf(cl)) * (1.f + 4.f * kG);
-          if (exact[r] && !(slack[r] > 0.f)) {
-            int ls2;
-            float sy2, best2;
-            const float m2 = dc::group_margin<LC>(sc[r].s, sc[r].y, act, sub, &ls2, &sy2, &best2);
-            slack[r] = dc::slack_of(method, m2, sc[r].nrm, ls2 >= 0, C, sy2, best2);
-          }
-        }
-        make_exact(k);
 #pragma unroll
-        for (int r = 0; r < kR; ++r)
-          if (G * kR + r > k) unsafe[r] = (alive[r] && (sc[r].nf > kNFM || !(slack[r] > 0.f))) ? 1 : 0;
+          for (int kk = 0; kk < K; ++kk) t.s[kk] = ns[kk];
+        }
+        float tau = 0.f, beta = 0.f;
+        const bool up_l = step_coeffs(method, m, var, t.nrm, ls >= 0, C, &tau, &beta);
+        const bool up = __builtin_amdgcn_ballot_w64(mine && up_l) != 0;
+        const int sid = n_steps++;
+        if (!up) {
+          ++n_waste;
+        } else {
+          // the sample's rows not in the store yet; a full bucket pair ends the
+          // window before this candidate (nothing of its step is applied)
+          bool full = false;
+          bool any_new = false;
+#pragma unroll
+          for (int c = 0; c < kFC; ++c) {
+            const bool need = mine && t.fi[c] >= 0 && sl[c] < 0;
+            any_new |= need;
+            if (need) {
+              sl[c] = dc::cache_insert<LC>(s_key, t.fi[c]);
+              full |= sl[c] < 0;
+            }
+          }
+          if (__builtin_amdgcn_ballot_w64(full) != 0) {
+            stopped = 1;
+            why = kWhySat;
+            pend = wb + kpos;
+            return 1;
+          }
+          const bool nins = __builtin_amdgcn_ballot_w64(any_new) != 0;
+          ++n_upd;
+          if (mine) {
+#pragma unroll
+            for (int c = 0; c < kFC; ++c)
+              if (t.fi[c] >= 0) {
+                float* sg = reinterpret_cast<float*>(&s_sg[sl[c]]);
+                sg[0] = __int_as_float(sid);
+                sg[1] = 0.f;
+                sg[2] = 0.f;
+              }
+#pragma unroll
+            for (int c = 0; c < kFC; ++c) {
+              if (t.fi[c] < 0) continue;
+              const float x = t.fx[c];
+              const float a = use_s ? 1.f / py[c] : 1.f;
+              const float b = (use_s && ls >= 0) ? 1.f / pl[c] : 1.f;
+              const float dwy = tau * a * x;
+              const float dwl = ls >= 0 ? -tau * b * x : 0.f;
+              float* dwr = s_dw + sl[c] * LC;
+              atomicAdd(dwr + y, dwy);
+              if (ls >= 0) atomicAdd(dwr + ls, dwl);
+              if (use_s) {
+                float* dpr = s_dp + sl[c] * LC;
+                atomicAdd(dpr + y, dprec(method, beta, x, a));
+                if (ls >= 0) atomicAdd(dpr + ls, dprec(method, beta, x, b));
+              }
+              float* sg = reinterpret_cast<float*>(&s_sg[sl[c]]);
+              atomicAdd(sg + 1, dwy);
+              atomicAdd(sg + 2, dwl);
+              atomicAdd(sg + 3, fmaxf(fabsf(dwy), fabsf(dwl)));
+            }
+          }
+          // the later samples of the round: slots of the rows the step added,
+          // then the step's increments of their stamped rows
+          const int yk = __builtin_amdgcn_readlane(y, Gk * 16);
+          const int lk = __builtin_amdgcn_readlane(ls, Gk * 16);
+          if (nins) {
+#pragma unroll
+            for (int r = 0; r < kR; ++r) {
+              if (G * kR + r <= k || !alive[r]) continue;
+#pragma unroll
+              for (int c = 0; c < kFC; ++c)
+                if ((c == 0 || two) && slot[r][c] < 0 && sc[r].fi[c] >= 0)
+                  slot[r][c] = dc::cache_find<LC>(s_key, sc[r].fi[c]);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < kR; ++r) {
+            const int pos = G * kR + r;
+            if (!alive[r] || pos <= k || sc[r].nf > kNFM) continue;
+            float cy = 0.f, cl = 0.f;
+#pragma unroll
+            for (int c = 0; c < kFC; ++c) {
+              const int s = slot[r][c];
+              if (s >= 0) {
+                const Stamp sg = s_sg[s];
+                if (__float_as_int(sg.sid) == sid) {
+                  cy += sc[r].fx[c] * sg.dy;
+                  cl += sc[r].fx[c] * sg.dl;
+                }
+              }
+            }
+            cy = row16_sum(cy);
+            cl = row16_sum(cl);
+            if (exact[r]) {
+#pragma unroll
+              for (int kk = 0; kk < K; ++kk) {
+                const int lab = sub + 16 * kk;
+                if (lab == yk) sc[r].s[kk] += cy;
+                if (lab == lk) sc[r].s[kk] += cl;
+              }
+            }
+            slack[r] -= (fabsf(cy) + fabsf(cl)) * (1.f + 4.f * kG);
+            if (exact[r] && !(slack[r] > 0.f)) {
+              int ls2;
+              float sy2, best2;
+              const float m2 = dc::group_margin<LC>(sc[r].s, sc[r].y, act, sub, &ls2, &sy2, &best2);
+              slack[r] = dc::slack_of(method, m2, sc[r].nrm, ls2 >= 0, C, sy2, best2);
+            }
+          }
+          make_exact(k);
+#pragma unroll
+          for (int r = 0; r < kR; ++r)
+            if (G * kR + r > k) unsafe[r] = (alive[r] && (sc[r].nf > kNFM || !(slack[r] > 0.f))) ? 1 : 0;
+        }
+        return 0;
+      };
+      int stop_code = 0;
+      switch (rk) {
+        case 0: stop_code = step_of(std::integral_constant<int, 0>{}); break;
+        case 1: if constexpr (kR > 1) stop_code = step_of(std::integral_constant<int, (kR > 1 ? 1 : 0)>{}); break;
+        case 2: if constexpr (kR > 2) stop_code = step_of(std::integral_constant<int, (kR > 2 ? 2 : 0)>{}); break;
+        default: if constexpr (kR > 3) stop_code = step_of(std::integral_constant<int, (kR > 3 ? 3 : 0)>{}); break;
       }
+      if (stop_code) break;
       lim = k;
     }
     ++n_rounds;

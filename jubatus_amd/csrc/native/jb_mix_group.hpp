@@ -917,15 +917,20 @@ class LinearMixer {
       faults_.on_mix("handover");
       hand_over();
     }
-    int64_t flags[4];
+    // [wants a MIX, forced, protocol version, -version, MIX count]: the count is
+    // agreed too - the push mixers derive the pairing of a round from it, and
+    // members' own counts differ (solo ticks, a member that joined late, a
+    // MIX that failed on one side); every member mixes round max(counts)
+    int64_t flags[5];
     {
       std::lock_guard<std::mutex> l(mu_);
       flags[0] = want_locked() ? 1 : 0;
       flags[1] = force_ ? 1 : 0;
+      flags[4] = (int64_t)mix_count_;
     }
     flags[2] = a_.protocol_version;
     flags[3] = -a_.protocol_version;
-    g.star().allreduce_max(flags, 4, g.deadline());
+    g.star().allreduce_max(flags, 5, g.deadline());
     if (flags[2] != -flags[3]) {
       log("FATAL", "mix protocol version mismatch in the cluster: shutting down");
       kill(getpid(), SIGTERM);
@@ -939,11 +944,8 @@ class LinearMixer {
       bytes = model_->mix(g);
     } else {
       // push mixers: the rounds of the pairwise schedule (push_mixer.cpp:335-408)
-      uint64_t round_no;
-      {
-        std::lock_guard<std::mutex> l(mu_);
-        round_no = mix_count_;
-      }
+      // of the agreed round number
+      const uint64_t round_no = (uint64_t)flags[4];
       model_->push_begin();
       for (const auto& m : push_schedule(a_.kind, g.world(), g.epoch(), round_no)) {
         faults_.on_mix("pair");
@@ -953,6 +955,7 @@ class LinearMixer {
     }
     const double sec = now_s() - t0;
     std::lock_guard<std::mutex> l(mu_);
+    mix_count_ = (uint64_t)flags[4];      // every member leaves this MIX at the same count
     mixed_locked(bytes, sec);
     char b[160];
     snprintf(b, sizeof b, "mixed with %d servers in %.6f secs, %llu bytes", g.world(), sec,

@@ -63,6 +63,11 @@ class HostEngine {
   virtual bool uses_cht() const { return false; }
   virtual std::string get_diff() { return std::string(); }            // msgpack
   virtual void put_diffs(const std::vector<Value>& parts) { (void)parts; }  // every rank's, rank order
+  // one round of a push MIX ([own, partner] in rank order): engines whose
+  // diffs are plain counts keep their own diff for the MIX's later partners
+  // and drop it in push_done(); the default folds the pair like a linear MIX
+  virtual void put_diffs_push(const std::vector<Value>& parts) { put_diffs(parts); }
+  virtual void push_done() {}
   virtual std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& s, double dl) {
     (void)dl;
     return std::unique_ptr<jb::mix::Plane>(new jb::mix::HostPlane(&s));
@@ -129,10 +134,14 @@ class HostServer : public jb::mix::Mixable {
     std::vector<Value> parts;
     if (g.rank() < peer) { parts.push_back(std::move(a)); parts.push_back(std::move(b)); }
     else { parts.push_back(std::move(b)); parts.push_back(std::move(a)); }
-    eng_->put_diffs(parts);
+    eng_->put_diffs_push(parts);
     return mine.size();
   }
   bool push_mixable() const override { return true; }
+  void push_end() override {
+    std::unique_lock<std::shared_mutex> lk(model_mu_);
+    eng_->push_done();
+  }
 
   void hand_over(jb::mix::Group& g, int src, bool apply) override {
     std::string mine;

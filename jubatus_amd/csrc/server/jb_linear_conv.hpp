@@ -76,7 +76,9 @@ struct DocStats {
     u.bin(cn.data(), cn.size() * 8);
     return std::move(u.out);
   }
-  void put_diffs(const std::vector<Value>& parts) {
+  // keep_own: one round of a push MIX (the own diff goes to the later
+  // partners too; clear_diff() when the MIX ends) - see jb_row_engine.hpp put_diff
+  void put_diffs(const std::vector<Value>& parts, bool keep_own = false) {
     if (df.empty()) return;
     int64_t docs = 0, len = 0;
     std::vector<int64_t> acc(df.size(), 0);
@@ -95,13 +97,17 @@ struct DocStats {
     counts[0] += docs - counts[2];
     counts[1] += len - counts[3];
     for (size_t i = 0; i < df.size(); ++i) df[i] = std::max<int64_t>(0, df[i] - diff[i] + acc[i]);
+    if (keep_own) return;
+    clear_diff();
+  }
+  void clear_diff() {
     std::fill(diff.begin(), diff.end(), 0);
     counts[2] = counts[3] = 0;
   }
-  void put_diffs(const std::vector<std::string>& raw) {
+  void put_diffs(const std::vector<std::string>& raw, bool keep_own = false) {
     std::vector<Value> parts;
     for (const auto& r : raw) parts.push_back(MsgpackReader((const uint8_t*)r.data(), r.size()).read());
-    put_diffs(parts);
+    put_diffs(parts, keep_own);
   }
   // WeightManager.pack(): [doc_count, total_len, {"idx": [...], "df": [...]}]
   void pack(MsgpackWriter& u) const {
@@ -186,8 +192,11 @@ class LinearConv {
   void pack(MsgpackWriter& u) const { st_.pack(u); }
   void unpack(const Value* w) { st_.unpack(w); }
   std::string get_diff() const { return st_.get_diff(); }
-  void put_diffs(const std::vector<std::string>& parts) {
-    if (!st_.df.empty()) st_.put_diffs(parts);
+  void put_diffs(const std::vector<std::string>& parts, bool keep_own = false) {
+    if (!st_.df.empty()) st_.put_diffs(parts, keep_own);
+  }
+  void clear_diff() {
+    if (!st_.df.empty()) st_.clear_diff();
   }
   int64_t docs() const { return st_.counts[0]; }
 

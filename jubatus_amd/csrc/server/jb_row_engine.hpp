@@ -177,7 +177,15 @@ class Converter {
     for (size_t i = 0; i < diff_.size(); ++i)
       if (diff_[i] != 0) { idx->push_back((int64_t)i); cnt->push_back(diff_[i]); }
   }
-  void put_diff(int64_t docs, int64_t len, const std::vector<int64_t>& idx, const std::vector<int64_t>& cnt) {
+  // the sum of the members' diffs (this member's included) replaces its own
+  // contribution. keep_own: one round of a push MIX - the own diff stays, so
+  // the MIX's later partners get it too (each round adds just the partner's
+  // counts; clear_diff() when the MIX ends). Under broadcast_mixer (every pair
+  // once per MIX) every member ends with every member's counts exactly once;
+  // random / skip mixers reach the MIX's partners only (the statistics carry
+  // no versions to forward them without double counting).
+  void put_diff(int64_t docs, int64_t len, const std::vector<int64_t>& idx, const std::vector<int64_t>& cnt,
+                bool keep_own = false) {
     if (df_.empty()) return;
     counts_[0] += docs - counts_[2];
     counts_[1] += len - counts_[3];
@@ -185,6 +193,12 @@ class Converter {
     for (size_t k = 0; k < idx.size() && k < cnt.size(); ++k)
       if (idx[k] >= 0 && (uint64_t)idx[k] < H_) df_[(size_t)idx[k]] += cnt[k];
     for (auto& x : df_) x = std::max<int64_t>(x, 0);
+    if (keep_own) return;
+    std::fill(diff_.begin(), diff_.end(), 0);
+    counts_[2] = counts_[3] = 0;
+  }
+  void clear_diff() {
+    if (df_.empty()) return;
     std::fill(diff_.begin(), diff_.end(), 0);
     counts_[2] = counts_[3] = 0;
   }
@@ -1121,12 +1135,14 @@ class RowEngine {
     conv.get_diff(docs, len, idx, cnt);
     return true;
   }
-  void put_weight_diff(int64_t docs, int64_t len, const std::vector<int64_t>& idx, const std::vector<int64_t>& cnt) {
-    conv.put_diff(docs, len, idx, cnt);
+  void put_weight_diff(int64_t docs, int64_t len, const std::vector<int64_t>& idx, const std::vector<int64_t>& cnt,
+                       bool keep_own = false) {
+    conv.put_diff(docs, len, idx, cnt, keep_own);
   }
   void mix_done() {
     dirty_.clear();
     removed_.clear();
+    conv.clear_diff();
   }
 
   // RowEngine.pack(): {"method", "rows": {id: [version, [sv, nv, bv]]}, "weights"}

@@ -91,7 +91,7 @@ inline void write_datum(MsgpackWriter& w, const Datum& d) {
 //     (forward: a push MIX passes the row on in its later rounds - it stays
 //      in the written / removed sets until the MIX ends)
 //   bool weight_diff(int64_t*, int64_t*, std::vector<int64_t>*, std::vector<int64_t>*) const
-//   void put_weight_diff(int64_t, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&)
+//   void put_weight_diff(int64_t, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&, bool keep_own)
 //   void mix_done()                                   forget the written / removed sets
 template <class S>
 void pack_row_diff(const S& st, MsgpackWriter& w) {
@@ -260,7 +260,7 @@ size_t apply_row_diffs(S& st, const std::vector<Value>& parts, std::vector<int32
       ks.push_back(kv.first);
       cs.push_back(kv.second);
     }
-    st.put_weight_diff(docs, len, ks, cs);
+    st.put_weight_diff(docs, len, ks, cs, forward);
   }
   if (!forward) st.mix_done();
   return written;

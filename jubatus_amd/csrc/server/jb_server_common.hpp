@@ -509,6 +509,20 @@ struct CommonStatus {
   std::string last_saved_path, last_loaded_path;
 };
 
+// the engines whose requests route by consistent hashing (the reference's
+// server_helper<...>(a, true): anomaly, bandit, burst, graph,
+// nearest_neighbor, recommender and stat *_impl.cpp:20)
+inline bool engine_uses_cht() {
+  static const char* const kCht[] = {"jubaanomaly", "jubabandit", "jubaburst", "jubagraph",
+                                     "jubanearest_neighbor", "jubarecommender", "jubastat"};
+  std::string n = prog_name();
+  const size_t s = n.rfind('/');
+  if (s != std::string::npos) n = n.substr(s + 1);
+  for (const char* k : kCht)
+    if (n == k) return true;
+  return false;
+}
+
 inline void common_status(const Args& a, const CommonStatus& cs, uint64_t update_count,
                           std::vector<std::pair<std::string, std::string>>* st) {
   const time_t now = time(nullptr);
@@ -552,7 +566,7 @@ inline void common_status(const Args& a, const CommonStatus& cs, uint64_t update
     add("zookeeper_timeout", std::to_string(a.zk_timeout));
     add("interconnect_timeout", std::to_string(a.ic_timeout));
     add("connected_zookeeper", a.connected_zookeeper);
-    add("use_cht", "0");
+    add("use_cht", engine_uses_cht() ? "1" : "0");
     add("mixer", a.mixer);
   }
 }

@@ -66,6 +66,7 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
                                unsigned long long* stats, uint8_t* touched, int64_t n_max,
                                void* scratch, int64_t scratch_bytes, hipStream_t stream);
 extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max);
+extern "C" int jb_serial_scratch_forget(void* scratch);
 extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                   int n_samples, const float* W, int LC, float* out,
                                   hipStream_t stream);
@@ -681,6 +682,10 @@ class Classifier : public jb::mix::Mixable {
     push_dirty_ = false;
   }
   void push_end() override {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      conv_.clear_diff();              // the own statistics went to every partner of this MIX
+    }
     if (!push_dirty_) return;
     std::lock_guard<std::mutex> g(mu_);   // a round that could not fold: the next MIX is dense
     HIPCHK(hipMemsetAsync(touched_, 1, H_, compute_));
@@ -793,7 +798,8 @@ class Classifier : public jb::mix::Mixable {
       }
       const std::string td = pl.exchange_bytes(star, peer, dm, dl);
       std::lock_guard<std::mutex> g(mu_);
-      conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm});
+      conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm},
+                      true);
       bytes += dm.size();
     }
     last_applied_ = applied && both;
@@ -902,6 +908,7 @@ class Classifier : public jb::mix::Mixable {
     DevBuf<float> val;
     DevBuf<uint32_t> hist;
     DevBuf<uint8_t> serial;        // kSerial scratch (tail range + slack per sample)
+    void* serial_seen = nullptr;   // the buffer jb_serial_scratch_forget last saw
     PinBuf<int64_t> meta_host;
     int32_t* host_out = nullptr;   // fine-grained: [err | hist nhist]
     int64_t nhist = 0, host_cap = 0;
@@ -1119,6 +1126,10 @@ class Classifier : public jb::mix::Mixable {
       const int64_t sb = jb_serial_scratch_bytes(std::max<int64_t>(n, 1));
       a.serial_scratch = s.serial.get((size_t)sb);
       a.serial_bytes = sb;
+      if (a.serial_scratch != s.serial_seen) {     // a new buffer: no inherited segment history
+        jb_serial_scratch_forget(a.serial_scratch);
+        s.serial_seen = a.serial_scratch;
+      }
     }
     a.merge_every = 1;
     a.hot_waves = kHotWaves;

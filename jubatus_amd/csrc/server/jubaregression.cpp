@@ -313,6 +313,10 @@ class Regression : public jb::mix::Mixable {
   // folded like mix() so training meanwhile is kept. Python twin:
   // models/regression.py through parallel/mixable.py pair_exchange.
   bool push_mixable() const override { return true; }
+  void push_end() override {
+    std::lock_guard<std::mutex> g(mu_);
+    conv_.clear_diff();              // the own statistics went to every partner of this MIX
+  }
   uint64_t pair_mix(jb::mix::Group& grp, int peer) override {
     jb::mix::Star& star = grp.star();
     jb::mix::Plane& pl = grp.plane();
@@ -350,7 +354,8 @@ class Regression : public jb::mix::Mixable {
       const std::string td = pl.exchange_bytes(star, peer, dm, dl);
       if (peer >= 0) {
         std::lock_guard<std::mutex> g(mu_);
-        conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm});
+        conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm},
+                      true);
         wbytes = dm.size();
       }
     }

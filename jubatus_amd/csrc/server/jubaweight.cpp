@@ -214,7 +214,15 @@ class Weight : public HostEngine {
     u.bin(cn.data(), cn.size() * 8);
     return std::move(u.out);
   }
-  void put_diffs(const std::vector<Value>& parts) override {
+  void put_diffs(const std::vector<Value>& parts) override { fold(parts, false); }
+  // push MIX: the own counts go to every partner of the MIX (broadcast_mixer:
+  // every member's exactly once), dropped when it ends
+  void put_diffs_push(const std::vector<Value>& parts) override { fold(parts, true); }
+  void push_done() override {
+    std::fill(diff_.begin(), diff_.end(), 0);
+    counts_[2] = counts_[3] = 0;
+  }
+  void fold(const std::vector<Value>& parts, bool keep_own) {
     int64_t docs = 0, len = 0;
     std::vector<int64_t> acc(df_.size(), 0);
     for (const Value& d : parts) {
@@ -234,6 +242,7 @@ class Weight : public HostEngine {
     counts_[0] += docs - counts_[2];
     counts_[1] += len - counts_[3];
     for (size_t i = 0; i < df_.size(); ++i) df_[i] = std::max<int64_t>(0, df_[i] - diff_[i] + acc[i]);
+    if (keep_own) return;
     std::fill(diff_.begin(), diff_.end(), 0);
     counts_[2] = counts_[3] = 0;
   }

@@ -481,7 +481,7 @@ class HostRowModel : public jb::mix::Mixable {
     *docs = *len = 0;
     return false;
   }
-  void put_weight_diff(int64_t, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&) {}
+  void put_weight_diff(int64_t, int64_t, const std::vector<int64_t>&, const std::vector<int64_t>&, bool) {}
   void mix_done() {
     dirty_.clear();
     removed_.clear();

@@ -49,6 +49,7 @@ _SIGS = {
     "jb_df_weigh": [_c_void_p, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
                     _i64, _i32, _c_void_p, _i64, _c_void_p, _c_void_p],
     "jb_serial_scratch_bytes": [_i64],
+    "jb_serial_scratch_forget": [_c_void_p],
     "jb_hot_detect": [_c_void_p, _i32, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                       _i32, _c_void_p, _c_void_p, _c_void_p],
     "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
@@ -711,6 +712,9 @@ class SerialScratch:
                 torch.cuda.synchronize(self.device)
             self.nbytes = max(need, 2 * self.nbytes)
             self.buf = torch.empty(self.nbytes, dtype=torch.uint8, device=self.device)
+            # a new buffer starts without the segment history of whatever
+            # buffer had its address before (csrc/hip/serial.hip)
+            _fn("jb_serial_scratch_forget")(self.buf.data_ptr())
         return self.buf.data_ptr()
 
 

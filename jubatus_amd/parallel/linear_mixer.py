@@ -190,14 +190,20 @@ class CollectiveMixer(Mixer):
         with self._lock:
             want = 1 if self._want() else 0
             force = 1 if self._force else 0
-        flags = g.allreduce_max_ints([want, force, self.protocol_version, -self.protocol_version])
+            count = self.mix_count
+        # the MIX count is agreed too (the push mixers' pairing of a round
+        # follows it; members' own counts differ after solo ticks, a late join
+        # or a MIX that failed on one side): every member mixes round max(counts)
+        flags = g.allreduce_max_ints([want, force, self.protocol_version, -self.protocol_version, count])
         if flags[2] != -flags[3]:
             log.critical("mix protocol version mismatch in the cluster: shutting down")
             mb.shutdown_server()
             return
         if flags[0] or flags[1]:
+            self.round_no = int(flags[4])
             st = self.mix_once()
             with self._lock:
+                self.mix_count = self.round_no      # every member leaves at the same count
                 self._mixed(st)
             log.info("mixed with %d servers in %.6f secs, %d bytes", g.world, st["seconds"],
                      st["bytes"])

@@ -101,7 +101,7 @@ class PushMixer(CollectiveMixer):
         import time
         t0 = time.perf_counter()
         g = self.group
-        for peer in self.schedule(g.rank, g.world, self.mix_count):
+        for peer in self.schedule(g.rank, g.world, getattr(self, "round_no", self.mix_count)):
             fault.on_mix("pair")
             with trace.span("mix.pair"):
                 pair_exchange(self.driver, peer)

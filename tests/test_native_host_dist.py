@@ -53,36 +53,44 @@ def status(c):
 
 
 class Cluster:
-    def __init__(self, coord, engine, name, cfg, n=2, extra=()):
+    def __init__(self, coord, engine, name, cfg, n=2, extra=(), mixer="linear_mixer", start=True):
         self.ls = CoordinatorClient(f"127.0.0.1:{coord.port}", timeout=5.0)
         zkconfig.config_tozk(self.ls, engine, name, json.dumps(cfg))
-        self.engine, self.name = engine, name
-        self.ports = [free_port() for _ in range(n)]
-        self.procs = []
-        for p in self.ports:
-            log = open(os.path.join(tempfile.gettempdir(), f"hostdist_{name}_{p}.log"), "wb")
-            self.procs.append(subprocess.Popen(
-                [os.path.join(NB, f"juba{engine}"), "-z", f"127.0.0.1:{coord.port}", "-n", name, "-p", str(p),
-                 "-b", "127.0.0.1", "-s", "0", "-i", "0", "-I", "5", "-Z", "5", *extra],
-                stdout=subprocess.DEVNULL, stderr=log))
-        for p in self.ports:
-            assert wait_server("127.0.0.1", p, 60)
-        self.c = [Client("127.0.0.1", p, name, timeout=30.0) for p in self.ports]
+        self.engine, self.name, self.coord, self.mixer = engine, name, coord, mixer
+        self.extra = tuple(extra) + (("-x", mixer) if mixer != "linear_mixer" else ())
+        self.ports, self.procs, self.c = [], [], []
+        for _ in range(n if start else 0):
+            self.add()
+        if start:
+            self.wait_group(n)
+
+    def add(self):
+        p = free_port()
+        log = open(os.path.join(tempfile.gettempdir(), f"hostdist_{self.name}_{p}.log"), "wb")
+        self.procs.append(subprocess.Popen(
+            [os.path.join(NB, f"juba{self.engine}"), "-z", f"127.0.0.1:{self.coord.port}", "-n", self.name,
+             "-p", str(p), "-b", "127.0.0.1", "-s", "0", "-i", "0", "-I", "5", "-Z", "5", *self.extra],
+            stdout=subprocess.DEVNULL, stderr=log))
+        assert wait_server("127.0.0.1", p, 60)
+        self.ports.append(p)
+        self.c.append(Client("127.0.0.1", p, self.name, timeout=30.0))
+        return self.c[-1]
+
+    def wait_group(self, n):
+        k = self.mixer
         deadline = time.time() + 60
         while time.time() < deadline:
             sts = [status(c) for c in self.c]
-            if all(s.get("linear_mixer.group_size") == str(n) and s.get("linear_mixer.is_obsolete") == "0"
-                   for s in sts):
-                break
+            if all(s.get(f"{k}.group_size") == str(n) and s.get(f"{k}.is_obsolete") == "0" for s in sts):
+                return
             time.sleep(0.2)
-        else:
-            raise AssertionError("group did not form")
+        raise AssertionError("group did not form")
 
-    def mix(self):
+    def mix(self, at_least=1):
         assert self.c[0].do_mix() is True
         deadline = time.time() + 20
         while time.time() < deadline:
-            if all(int(status(c).get("linear_mixer.mix_count", "0")) >= 1 for c in self.c):
+            if all(int(status(c).get(f"{self.mixer}.mix_count", "0")) >= at_least for c in self.c):
                 return
             time.sleep(0.1)
 
@@ -105,6 +113,7 @@ def test_native_stat_distributed_entropy(coord):
         st = status(cl.c[0])
         assert st["server_runtime"] == "native" and st["linear_mixer.runtime"] == "native"
         assert st["is_standalone"] == "0"
+        assert st["use_cht"] == "1"      # server_helper<stat_serv>(a, true) (stat_impl.cpp:20)
         # CHT-routed engine: 8 vnodes per server
         assert len(cl.ls.list(mb.build_actor_path("stat", "sdist") + "/cht")) == 16
         keys = {}
@@ -293,4 +302,76 @@ def test_native_graph_distributed_replicated_writes(coord):
         if solo.poll() is None:
             solo.terminate()
             solo.wait(timeout=15)
+        cl.close()
+
+
+def test_native_weight_broadcast_mixer_idf_three_members(coord):
+    """push MIX of the document statistics: with broadcast_mixer
+    every pair meets once per MIX and each member's own counts go to every
+    partner, so three members end with the statistics of all documents -
+    calc_weight equals a server that saw every document"""
+    cfg = json.load(open(os.path.join(ROOT, "config/weight/default.json")))
+    cl = Cluster(coord, "weight", "wbc", cfg, n=3, mixer="broadcast_mixer")
+    solo_port = free_port()
+    cfg_path = os.path.join(tempfile.gettempdir(), f"wbsolo_{solo_port}.json")
+    json.dump(cfg, open(cfg_path, "w"))
+    solo = subprocess.Popen([os.path.join(NB, "jubaweight"), "-f", cfg_path, "-p", str(solo_port), "-b", "127.0.0.1"],
+                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        assert wait_server("127.0.0.1", solo_port, 60)
+        s = Client("127.0.0.1", solo_port, "", timeout=30.0)
+        docs = [Datum({"text": t}) for t in ("the quick brown fox", "the lazy dog", "quick quick fox",
+                                             "a dog and a fox", "brown dog", "the end")]
+        for i, d in enumerate(docs):
+            cl.c[i % 3].call("update", d)
+            s.call("update", d)
+        cl.mix()
+        q = Datum({"text": "quick dog the fox"})
+        want = sorted((k, round(v, 5)) for k, v in s.call("calc_weight", q))
+        for c in cl.c:
+            got = sorted((k, round(v, 5)) for k, v in c.call("calc_weight", q))
+            assert got == want, (got, want)
+        # a second MIX with nothing new changes nothing (no double counting)
+        cl.mix(at_least=2)
+        for c in cl.c:
+            assert sorted((k, round(v, 5)) for k, v in c.call("calc_weight", q)) == want
+        s.close()
+    finally:
+        if solo.poll() is None:
+            solo.terminate()
+            solo.wait(timeout=15)
+        cl.close()
+
+
+def test_native_random_mixer_late_members_agree_round(coord):
+    """push mixers pair members by the MIX round number; a member
+    that mixed alone before the others joined has a higher count. The count
+    is agreed in the MIX trigger, so three members with different counts
+    still pair up and every MIX completes"""
+    cfg = json.load(open(os.path.join(ROOT, "config/weight/default.json")))
+    cl = Cluster(coord, "weight", "wrm", cfg, n=0, mixer="random_mixer", start=False)
+    try:
+        a = cl.add()
+        cl.wait_group(1)
+        for _ in range(3):                      # solo MIXes: a's count moves ahead
+            assert a.do_mix() is True
+        assert int(status(a)["random_mixer.mix_count"]) >= 3
+        cl.add()
+        cl.add()
+        cl.wait_group(3)
+        for d in ("alpha beta", "beta gamma", "gamma delta"):
+            for c in cl.c:
+                c.call("update", Datum({"text": d}))
+        counts = [int(status(c)["random_mixer.mix_count"]) for c in cl.c]
+        for _ in range(3):
+            assert cl.c[1].do_mix() is True
+        deadline = time.time() + 20
+        while True:
+            after = [int(status(c)["random_mixer.mix_count"]) for c in cl.c]
+            if len(set(after)) == 1 or time.time() > deadline:
+                break
+            time.sleep(0.1)
+        assert len(set(after)) == 1 and after[0] >= max(counts) + 3, (counts, after)
+        assert all(status(c)["random_mixer.watchdog_aborts"] == "0" for c in cl.c)
+    finally:
         cl.close()
