@@ -260,6 +260,7 @@ def served_train(args, local: int, nat) -> dict:
                 "requests_per_s": lg["requests_per_s"], "samples_per_request": args.per_request,
                 "connections": lg["connections"], "depth": lg["depth"],
                 "distinct_requests": lg["distinct_requests"], "fresh_values": lg.get("fresh_values"),
+                "noise_per_mille": lg.get("noise_per_mille", 0),
                 "rpc_p50_us": lg["p50_us"],
                 "rpc_p99_us": lg["p99_us"], "seconds": lg["seconds"],
                 "samples_trained_in_window": tr,
@@ -292,10 +293,14 @@ def _proc_cpu(pid: int) -> float:
     return (int(fields[11]) + int(fields[12])) / tck
 
 
-def served_train_native(args, local: int, nat) -> dict:
+def served_train_native(args, local: int, nat, mode: str | None = None, noise_pm: int = 0,
+                        classify: bool = True) -> dict:
     """The served train path of the native server binary
     (csrc/server/jubaclassifier.cpp: no Python in the server process): the
-    same load generator, request set and configuration as served_train."""
+    same load generator, request set and configuration as served_train.
+    mode: the server's update mode (default: the headline's); noise_pm: per
+    mille of the samples sent with every string token redrawn (jubaloadgen
+    -u: unseen features, the model keeps updating - a learning stream)."""
     import socket
     import tempfile
     from jubatus_amd.common.mprpc import RpcClient
@@ -316,7 +321,7 @@ def served_train_native(args, local: int, nat) -> dict:
     p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
                           "-c", str(args.rpc_threads), "--gpu", str(local)],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                         env=dict(os.environ, JUBATUS_UPDATE_MODE=args.update_mode))
+                         env=dict(os.environ, JUBATUS_UPDATE_MODE=mode or args.update_mode))
 
     def status():
         with RpcClient("127.0.0.1", port, 30.0) as c:
@@ -350,6 +355,8 @@ def served_train_native(args, local: int, nat) -> dict:
                 f.write(b"\x92\xa0" + buf[o:o + n].tobytes())
         base = [exe, "-p", str(port), "-m", "train", "-f", pfile, "-c", str(args.rpc_conns),
                 "-d", str(args.rpc_depth)] + _fresh_flag(args)
+        if noise_pm > 0 and args.rpc_fresh:
+            base += ["-u", str(noise_pm)]
         subprocess.run(base + ["-t", "1.5"], capture_output=True, text=True, timeout=120)  # warmup
         st0 = status()
         cpu0 = _proc_cpu(p.pid)
@@ -363,11 +370,13 @@ def served_train_native(args, local: int, nat) -> dict:
         tr = int(st1["train.samples_trained"]) - int(st0["train.samples_trained"])
         up = int(st1["train.samples_updated"]) - int(st0["train.samples_updated"])
         # classify over RPC: one datum per request, one connection, one in flight
-        one = msgpack.unpackb(buf[offs[0]:offs[0] + lens[0]].tobytes(), raw=False)[0][1]
-        cfile = os.path.join(tmp, "classify_params.bin")
-        with open(cfile, "wb") as f:
-            f.write(msgpack.packb(["", [one]], use_bin_type=False))
-        cl = _loadgen(exe, port, "classify", cfile, 1, 1, secs=2.0, timeout=120)
+        cl = {"p50_us": None, "p99_us": None}
+        if classify:
+            one = msgpack.unpackb(buf[offs[0]:offs[0] + lens[0]].tobytes(), raw=False)[0][1]
+            cfile = os.path.join(tmp, "classify_params.bin")
+            with open(cfile, "wb") as f:
+                f.write(msgpack.packb(["", [one]], use_bin_type=False))
+            cl = _loadgen(exe, port, "classify", cfile, 1, 1, secs=2.0, timeout=120)
         return {"served_train_samples_per_sec": round(lg["requests_per_s"] * args.per_request, 1),
                 "requests_per_s": lg["requests_per_s"], "samples_per_request": args.per_request,
                 "connections": lg["connections"], "depth": lg["depth"],
@@ -1298,6 +1307,14 @@ def main() -> None:
     if world == 1 and device is not None and not args.no_rpc:
         served = served_train(args, local, nat)
         served_native = served_train_native(args, local, nat)
+        if isinstance(served_native, dict) and "error" not in served_native:
+            # the servers' default (serial-equivalent) mode over RPC, and a
+            # stream that keeps learning (2 % of the samples all-new tokens)
+            served_native["exact_mode"] = served_train_native(args, local, nat, mode="exact", classify=False)
+            served_native["learning_stream"] = served_train_native(args, local, nat, noise_pm=20,
+                                                                   classify=False)
+            served_native["learning_stream_exact"] = served_train_native(args, local, nat, mode="exact",
+                                                                         noise_pm=20, classify=False)
     engines = None
     if world == 1 and device is not None and args.engines != "none":
         engines = engine_records(args, local)

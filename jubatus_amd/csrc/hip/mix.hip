@@ -19,6 +19,35 @@
 
 namespace jb {
 
+// bf16 wire (JUBATUS_MIX_DTYPE=bf16): the W columns of a [n][w] snapshot
+// (w = 2 Lc: W then S columns; Lc without S) to bf16 with round-to-nearest-
+// even, the S columns (precisions) stay fp32 - and back after the SUM
+__global__ __launch_bounds__(256) void mix_pack_bf16_kernel(const float* __restrict__ snap, int64_t n, int Lc,
+                                                            int has_s, uint16_t* __restrict__ wb,
+                                                            float* __restrict__ sb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * Lc) return;
+  const int64_t r = i / Lc;
+  const int c = (int)(i - r * Lc);
+  const int64_t w = (has_s ? 2 : 1) * (int64_t)Lc;
+  const uint32_t u = __float_as_uint(snap[r * w + c]);
+  // RNE; NaN stays NaN
+  wb[i] = (u & 0x7fffffffu) > 0x7f800000u ? (uint16_t)((u >> 16) | 0x40u)
+                                            : (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  if (has_s) sb[i] = snap[r * w + Lc + c];
+}
+__global__ __launch_bounds__(256) void mix_unpack_bf16_kernel(const uint16_t* __restrict__ wb,
+                                                              const float* __restrict__ sb, int64_t n, int Lc,
+                                                              int has_s, float* __restrict__ red) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * Lc) return;
+  const int64_t r = i / Lc;
+  const int c = (int)(i - r * Lc);
+  const int64_t w = (has_s ? 2 : 1) * (int64_t)Lc;
+  red[r * w + c] = __uint_as_float((uint32_t)wb[i] << 16);
+  if (has_s) red[r * w + Lc + c] = sb[i];
+}
+
 // rows == nullptr: row r is r (dense MIX)
 __global__ __launch_bounds__(256) void mix_gather_kernel(const float* __restrict__ W, const float* __restrict__ S,
                                                          int LC, const int64_t* __restrict__ rows, int64_t n,
@@ -142,5 +171,21 @@ extern "C" int jb_mix_pair_sum(float* p, const float* q, int64_t n, hipStream_t 
 extern "C" int jb_mix_pair_max(uint8_t* p, const uint8_t* q, int64_t n, hipStream_t st) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(jb::mix_pair_max_kernel, dim3(blocks_for(n)), dim3(256), 0, st, p, q, n);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jb_mix_pack_bf16(const float* snap, int64_t n, int Lc, int has_s, uint16_t* wb, float* sb,
+                                hipStream_t st) {
+  if (n <= 0 || Lc <= 0) return 0;
+  hipLaunchKernelGGL(jb::mix_pack_bf16_kernel, dim3(blocks_for(n * Lc)), dim3(256), 0, st, snap, n, Lc, has_s,
+                     wb, sb);
+  return (int)hipGetLastError();
+}
+
+extern "C" int jb_mix_unpack_bf16(const uint16_t* wb, const float* sb, int64_t n, int Lc, int has_s, float* red,
+                                  hipStream_t st) {
+  if (n <= 0 || Lc <= 0) return 0;
+  hipLaunchKernelGGL(jb::mix_unpack_bf16_kernel, dim3(blocks_for(n * Lc)), dim3(256), 0, st, wb, sb, n, Lc,
+                     has_s, red);
   return (int)hipGetLastError();
 }

@@ -53,6 +53,8 @@
 // Device state (int64 words, 256 B) lives in the kSerial scratch; every kernel
 // reads the status first, so a batch's segments are queued without a host round
 // trip and the finished ones cost an empty launch each.
+#include <string.h>
+
 #include <type_traits>
 
 #include "jb_commit.hpp"
@@ -61,17 +63,8 @@ namespace jb {
 namespace vc {
 
 using dc::Geo;
-#ifndef JB_VC_R
-#define JB_VC_R 2
-#endif
-constexpr int kR = JB_VC_R;             // samples per 16-lane group per round
-constexpr int kNS = 4 * kR;             // candidates per round (one wave)
 constexpr int kFC = 2;                  // feature chunks of 16 per lane
 constexpr int kNFM = 16 * kFC;          // widest sample the committer takes
-#ifndef JB_VC_PD
-#define JB_VC_PD 2
-#endif
-constexpr int kPD = JB_VC_PD;           // rounds of records in flight
 constexpr int64_t kLwMin = 2048, kLwMax = 65536, kLwInit = 8192;
 constexpr int kBitWords = (int)(kLwMax / 64);
 constexpr float kTInit = 0.5f, kTMin = 0.125f, kTMax = 64.f;
@@ -345,7 +338,7 @@ struct Samp {
 // max_l |dW[row][l]| (the summed step magnitudes)
 struct __attribute__((aligned(16))) Stamp { float sid, dy, dl, rmax; };
 
-template <int LC, int MT>
+template <int LC, int MT, int R_, int PD_>
 __global__ __launch_bounds__(64) void vc_commit_kernel(
     int64_t* __restrict__ st, const float* __restrict__ W, const float* __restrict__ P,
     const int32_t* __restrict__ active, float C, const float* __restrict__ S0_k,
@@ -355,6 +348,11 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
   using Gm = Geo<LC>;
   using Rw = Raw<LC>;
   using S = Samp<LC>;
+  // R_ samples per group and round, PD_ rounds of records in flight: the code
+  // of a round is instantiated R_ x PD_ times (the instruction cache decides)
+  constexpr int kR = R_;
+  constexpr int kNS = 4 * R_;
+  constexpr int kPD = PD_;
   constexpr int K = Gm::K;
   constexpr int NSLOT = Gm::NSLOT;
   constexpr int method = MT;
@@ -970,15 +968,32 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
                      float* fx, int32_t* gk, float* gr, float* gdw, float* gdp, uint8_t* touched,
                      unsigned long long* stats, int64_t* tail, int nseg, hipStream_t stream) {
   using namespace jb::vc;
+  // committer shape (samples per group x rounds in flight), for A/B runs:
+  // JB_VC_SHAPE = r2pd2 | r2pd1 | r1pd1 | r1pd3; default r1pd2
+  static const int shape = [] {
+    const char* e = getenv("JB_VC_SHAPE");
+    if (e == nullptr) return 0;
+    if (strcmp(e, "r2pd2") == 0) return 1;
+    if (strcmp(e, "r2pd1") == 0) return 2;
+    if (strcmp(e, "r1pd1") == 0) return 3;
+    if (strcmp(e, "r1pd3") == 0) return 4;
+    return 0;
+  }();
   float* Pp = method >= jb::CW ? S : nullptr;
   for (int seg = 0; seg < nseg; ++seg) {
     hipLaunchKernelGGL((vc_score_kernel<L>), dim3(1024), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        W, active, method, C, sl, bits);
     hipLaunchKernelGGL((vc_gather_kernel<L>), dim3(512), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx);
-#define JB_VC_M(M)                                                                                      \
-  hipLaunchKernelGGL((vc_commit_kernel<L, M>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, aux, \
-                     pp0, fi, fx, gk, gr, gdw, gdp);                                                    \
+#define JB_VC_S(M, R, PD)                                                                                    \
+  hipLaunchKernelGGL((vc_commit_kernel<L, M, R, PD>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, \
+                     aux, pp0, fi, fx, gk, gr, gdw, gdp);
+#define JB_VC_M(M)                               \
+  if (shape == 1) { JB_VC_S(M, 2, 2) }           \
+  else if (shape == 2) { JB_VC_S(M, 2, 1) }      \
+  else if (shape == 3) { JB_VC_S(M, 1, 1) }      \
+  else if (shape == 4) { JB_VC_S(M, 1, 3) }      \
+  else { JB_VC_S(M, 1, 2) }                      \
   break;
     switch (method) {
       case jb::PERCEPTRON: JB_VC_M(jb::PERCEPTRON)
@@ -991,6 +1006,7 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
       default: return -1;
     }
 #undef JB_VC_M
+#undef JB_VC_S
     hipLaunchKernelGGL((vc_verify_kernel<L>), dim3(256), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        sl, bits, gk, gr, gdw, gdp, W, Pp, touched, stats, tail);
   }

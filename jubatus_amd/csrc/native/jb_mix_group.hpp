@@ -376,6 +376,12 @@ class Plane {
   virtual const char* name() const = 0;
   virtual void allreduce_sum(float* p, size_t n, double dl) = 0;
   virtual void allreduce_max(uint8_t* p, size_t n, double dl) = 0;
+  // bf16 SUM (the bit patterns in uint16): only the device plane has it
+  // (false: not supported, the caller sends fp32)
+  virtual bool allreduce_sum_bf16(uint16_t* p, size_t n, double dl) {
+    (void)p; (void)n; (void)dl;
+    return false;
+  }
   virtual void bcast(void* p, size_t bytes, int root, double dl) = 0;
   virtual void abort() {}
   // variable-size host byte strings (row diffs, whole models): every rank's

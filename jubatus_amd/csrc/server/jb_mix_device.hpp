@@ -76,6 +76,12 @@ class RcclPlane : public Plane {
     check(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm_, st_), dl, "ncclAllReduce");
     wait_stream(st_, dl);
   }
+  bool allreduce_sum_bf16(uint16_t* p, size_t n, double dl) override {
+    if (!n) return true;
+    check(ncclAllReduce(p, p, n, ncclBfloat16, ncclSum, comm_, st_), dl, "ncclAllReduce");
+    wait_stream(st_, dl);
+    return true;
+  }
   void bcast(void* p, size_t bytes, int root, double dl) override {
     if (!bytes) return;
     check(ncclBroadcast(p, p, bytes, ncclUint8, root, comm_, st_), dl, "ncclBroadcast");

@@ -74,6 +74,10 @@ extern "C" int jb_classify_direct(const int32_t* idx, const float* val, const in
                                   int n, const float* W, int LC, float* out_host,
                                   uint32_t* done_host, hipStream_t stream);
 extern "C" int jb_mix_take(uint8_t* touched, uint8_t* mark, int64_t H, hipStream_t st);
+extern "C" int jb_mix_pack_bf16(const float* snap, int64_t n, int Lc, int has_s, uint16_t* wb, float* sb,
+                                hipStream_t st);
+extern "C" int jb_mix_unpack_bf16(const uint16_t* wb, const float* sb, int64_t n, int Lc, int has_s, float* red,
+                                  hipStream_t st);
 extern "C" int64_t jb_mix_compact_temp_bytes(int64_t H);
 extern "C" int jb_mix_compact(const uint8_t* mark, int64_t H, int64_t* rows, int64_t* count, void* temp,
                               int64_t temp_bytes, hipStream_t st);
@@ -619,8 +623,26 @@ class Classifier : public jb::mix::Mixable {
       int64_t ok[1] = {applied ? 0 : 1};
       star.allreduce_max(ok, 1, grp.deadline());   // a rank whose tables changed: nobody folds
       if (ok[0] == 0) {
-        pl.allreduce_sum(red_.p, elems, grp.deadline());
-        bytes += elems * 4;
+        // JUBATUS_MIX_DTYPE=bf16: the weight columns travel as bf16 (half the
+        // bytes; each hop of the ring SUM rounds to bf16, ~2^-9 relative), the
+        // precisions fp32; members agree on the wire over the control plane
+        int64_t wire[1] = {mix_bf16() && std::string(pl.name()) == "rccl" ? 0 : 1};
+        star.allreduce_max(wire, 1, grp.deadline());
+        last_wire_bf16_ = wire[0] == 0;
+        if (last_wire_bf16_) {
+          const int has_s = use_s_ ? 1 : 0;
+          const size_t nl = (size_t)n * (size_t)Lc;
+          uint16_t* wb = (uint16_t*)wire_.get(nl * 2 + (has_s ? nl * 4 : 0) + 16);
+          float* sb = (float*)((uint8_t*)wb + ((nl * 2 + 15) & ~(size_t)15));
+          if (jb_mix_pack_bf16(snap_.p, n, Lc, has_s, wb, sb, mixs_) != 0) throw std::runtime_error("jb_mix_pack_bf16");
+          pl.allreduce_sum_bf16(wb, nl, grp.deadline());
+          if (has_s) pl.allreduce_sum(sb, nl, grp.deadline());
+          if (jb_mix_unpack_bf16(wb, sb, n, Lc, has_s, red_.p, mixs_) != 0) throw std::runtime_error("jb_mix_unpack_bf16");
+          bytes += nl * 2 + (has_s ? nl * 4 : 0);
+        } else {
+          pl.allreduce_sum(red_.p, elems, grp.deadline());
+          bytes += elems * 4;
+        }
         // 5. fold: T += mean(snapshot) - snapshot (updates made meanwhile stay)
         std::lock_guard<std::mutex> g(mu_);
         HIPCHK(hipEventRecord(mix_ev_, mixs_));
@@ -897,6 +919,7 @@ class Classifier : public jb::mix::Mixable {
       add("mix.last_rows", std::to_string(last_rows_));
       add("mix.last_mode", last_dense_ ? "dense" : "sparse");
       add("mix.last_applied", last_applied_ ? "1" : "0");
+      add("mix.wire_dtype", last_wire_bf16_ ? "bf16" : "fp32");
     }
   }
 
@@ -1334,6 +1357,15 @@ class Classifier : public jb::mix::Mixable {
   DevBuf<int64_t> rows_, count_dev_;
   DevBuf<int32_t> map_dev_;
   DevBuf<float> snap_, red_, hw_, hs_;
+  DevBuf<uint8_t> wire_;          // bf16 weight columns + fp32 precisions of a bf16-wire MIX
+  bool last_wire_bf16_ = false;
+  static bool mix_bf16() {
+    static const bool v = [] {
+      const char* e = getenv("JUBATUS_MIX_DTYPE");
+      return e != nullptr && strcmp(e, "bf16") == 0;
+    }();
+    return v;
+  }
   int64_t* count_host_ = nullptr;
   std::map<std::string, uint64_t> count_base_;
   uint64_t last_rows_ = 0;

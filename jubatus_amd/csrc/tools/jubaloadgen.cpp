@@ -24,8 +24,12 @@
 // keeps meeting data it has not seen, as in the in-process bench's
 // non-repeating stream - at the cost of a few draws per sample, no copy.
 //
+// -u N (with -r): N per mille of the samples sent get new digits in every
+// string value instead (all their tokens unseen: the model updates on them) -
+// a stream that keeps learning.
+//
 // Usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH] [-t SECONDS]
-//                    [-o 1] [-r SEED]
+//                    [-o 1] [-r SEED [-u N]]
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/tcp.h>
@@ -117,6 +121,9 @@ int connect_to(const std::string& host, int port) {
 struct FreshSlots {
   std::vector<uint32_t> f64;                          // payload offsets
   std::vector<std::pair<uint32_t, uint32_t>> digits;  // (offset, length) runs
+  // -u: the digit runs of every string value, per sample [all_begin[i], all_begin[i + 1])
+  std::vector<std::pair<uint32_t, uint32_t>> all;
+  std::vector<uint32_t> all_begin{0};
   bool empty() const { return f64.empty(); }
 };
 
@@ -134,14 +141,16 @@ FreshSlots fresh_slots(const std::string& prm) {
     for (uint32_t j = 0; j < sn; ++j) {
       uint32_t kv;
       if (!c.array(&kv) || kv != 2 || !c.raw(&s, &n) || !c.raw(&s, &n)) return {};
-      if (j + 1 == sn) {                              // the last value's digits
-        uint32_t k = 0;
-        while (k < n && !(s[k] >= '0' && s[k] <= '9')) ++k;
-        uint32_t e = k;
-        while (e < n && s[e] >= '0' && s[e] <= '9') ++e;
-        if (e > k) out.digits.emplace_back((uint32_t)(s + k - b), e - k);
+      uint32_t k = 0;
+      while (k < n && !(s[k] >= '0' && s[k] <= '9')) ++k;
+      uint32_t e = k;
+      while (e < n && s[e] >= '0' && s[e] <= '9') ++e;
+      if (e > k) {
+        out.all.emplace_back((uint32_t)(s + k - b), e - k);
+        if (j + 1 == sn) out.digits.emplace_back((uint32_t)(s + k - b), e - k);   // the last value's digits
       }
     }
+    out.all_begin.push_back((uint32_t)out.all.size());
     if (!c.array(&nn)) return {};
     for (uint32_t j = 0; j < nn; ++j) {
       uint32_t kv;
@@ -195,8 +204,19 @@ struct FreshReq {
     base.clear();
     for (const uint32_t o : sl->f64) base.push_back(get_f64((const uint8_t*)src.data() + o));
   }
-  void refresh(Fresh* rng) {
+  // noise_pm: per mille of the samples whose every string value gets new
+  // digits (tokens the model has not seen: the sample updates the model)
+  void refresh(Fresh* rng, int noise_pm) {
     uint8_t* b = (uint8_t*)&buf[0];
+    if (noise_pm > 0)
+      for (size_t i = 0; i + 1 < slots->all_begin.size(); ++i) {
+        if ((int)(rng->next() % 1000) >= noise_pm) continue;
+        for (uint32_t q = slots->all_begin[i]; q < slots->all_begin[i + 1]; ++q) {
+          const auto& d = slots->all[q];
+          uint64_t r = rng->next();
+          for (uint32_t k = 0; k < d.second; ++k, r /= 10) b[d.first + k] = (uint8_t)('0' + r % 10);
+        }
+      }
     for (size_t i = 0; i < slots->f64.size(); ++i) {
       const double v = base[i] + rng->half_gauss();
       uint64_t u;
@@ -219,7 +239,8 @@ struct Result {
 
 void run_conn(const std::string& host, int port, const std::string& method,
               const std::vector<std::string>* params, const std::vector<FreshSlots>* fresh,
-              uint64_t seed, size_t first, size_t last, bool once, int depth, double secs, Result* r) {
+              uint64_t seed, size_t first, size_t last, bool once, int depth, double secs, int noise_pm,
+              Result* r) {
   const int fd = connect_to(host, port);
   if (fd < 0) { r->error = "connect failed"; return; }
   std::vector<Clock::time_point> sent(1 << 16);
@@ -251,7 +272,7 @@ void run_conn(const std::string& host, int port, const std::string& method,
       heads.push_back(request_head(next, method));
       if (fresh) {
         FreshReq& f = priv[heads.size() - 1];
-        f.refresh(&rng);
+        f.refresh(&rng, noise_pm);
         bodies.push_back(&f.buf);
       } else {
         bodies.push_back(&(*params)[which]);
@@ -301,6 +322,7 @@ int main(int argc, char** argv) {
   bool once = false;
   double secs = 3.0;
   long long fresh_seed = -1;
+  int noise_pm = 0;
   for (int i = 1; i + 1 < argc; i += 2) {
     const std::string a = argv[i], v = argv[i + 1];
     if (a == "-H") host = v;
@@ -312,12 +334,13 @@ int main(int argc, char** argv) {
     else if (a == "-t") secs = atof(v.c_str());
     else if (a == "-o") once = atoi(v.c_str()) != 0;
     else if (a == "-r") fresh_seed = atoll(v.c_str());
+    else if (a == "-u") noise_pm = atoi(v.c_str());
     else { fprintf(stderr, "unknown option %s\n", a.c_str()); return 1; }
   }
   if (!port || method.empty() || file.empty() || conns < 1 || depth < 1) {
     fprintf(stderr,
             "usage: jubaloadgen -p PORT -m METHOD -f PARAMS.bin [-H HOST] [-c CONNS] [-d DEPTH]"
-            " [-t SECONDS] [-o 1] [-r SEED]\n");
+            " [-t SECONDS] [-o 1] [-r SEED [-u NOISE_PER_MILLE]]\n");
     return 1;
   }
   std::ifstream ifs(file, std::ios::binary);
@@ -347,7 +370,7 @@ int main(int argc, char** argv) {
     ts.emplace_back(run_conn, host, port, method, &params, fresh_seed >= 0 ? &slots : nullptr,
                     (uint64_t)(fresh_seed >= 0 ? fresh_seed : 0),
                     (size_t)i * params.size() / (size_t)conns,
-                    (size_t)(i + 1) * params.size() / (size_t)conns, once, depth, secs, &res[i]);
+                    (size_t)(i + 1) * params.size() / (size_t)conns, once, depth, secs, noise_pm, &res[i]);
   for (auto& t : ts) t.join();
   const double dt = std::chrono::duration<double>(Clock::now() - t0).count();
   uint64_t done = 0;
@@ -360,9 +383,9 @@ int main(int argc, char** argv) {
   std::sort(lat.begin(), lat.end());
   auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[(size_t)(q * (lat.size() - 1))]; };
   printf("{\"requests\": %llu, \"seconds\": %.3f, \"requests_per_s\": %.1f, \"connections\": %d, "
-         "\"depth\": %d, \"distinct_requests\": %zu, \"fresh_values\": %s, \"p50_us\": %.1f, "
-         "\"p99_us\": %.1f}\n",
+         "\"depth\": %d, \"distinct_requests\": %zu, \"fresh_values\": %s, \"noise_per_mille\": %d, "
+         "\"p50_us\": %.1f, \"p99_us\": %.1f}\n",
          (unsigned long long)done, dt, done / dt, conns, depth, params.size(),
-         fresh_seed >= 0 ? "true" : "false", pct(0.5), pct(0.99));
+         fresh_seed >= 0 ? "true" : "false", noise_pm, pct(0.5), pct(0.99));
   return 0;
 }
