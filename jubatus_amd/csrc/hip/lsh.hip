@@ -121,6 +121,23 @@ __global__ __launch_bounds__(64) void signature_query_kernel(const QueryArgs a, 
   if (valid != nullptr && threadIdx.x == 0) valid[row] = 1;
 }
 
+// a batch of table rows from a device CSR (the row server's batched writes):
+// one wave per row, row q of the CSR into table slot slots[q]
+__global__ __launch_bounds__(64) void signature_rows_kernel(const int64_t* __restrict__ rp,
+                                                            const int64_t* __restrict__ slots,
+                                                            const int32_t* __restrict__ idx,
+                                                            const float* __restrict__ val, int n, int hash_num,
+                                                            uint64_t seed, int mode, uint64_t* __restrict__ bits,
+                                                            float* __restrict__ norms, uint8_t* __restrict__ valid) {
+  const int q = blockIdx.x;
+  if (q >= n) return;
+  const int words = (hash_num + 63) / 64;
+  const int64_t row = slots[q];
+  signature_one(idx, val, rp[q], (int)(rp[q + 1] - rp[q]), hash_num, seed, mode, bits + row * words, norms + row,
+                threadIdx.x);
+  if (threadIdx.x == 0) valid[row] = 1;
+}
+
 namespace {
 int fill_query_args(QueryArgs* a, const int32_t* idx, const float* val, const int64_t* row_ptr,
                     int n, const int64_t* dst) {
@@ -284,5 +301,16 @@ extern "C" int jb_lsh_set_rows_direct(const int32_t* idx, const float* val, cons
   if (jb::fill_query_args(&a, idx, val, row_ptr, n, slots)) return 1;
   hipLaunchKernelGGL(jb::signature_query_kernel, dim3(n), dim3(64), 0, stream, a, hash_num, seed,
                      mode, tbits, tnorm, valid);
+  return (int)hipGetLastError();
+}
+
+// n table rows at once from a device CSR ([rp: n + 1][slots: n] int64, idx /
+// val of rp[n] entries), each into its slot (distinct slots)
+extern "C" int jb_lsh_set_rows_staged(const int64_t* rp, const int64_t* slots, const int32_t* idx, const float* val,
+                                      int n, int hash_num, uint64_t seed, int mode, uint64_t* tbits, float* tnorm,
+                                      uint8_t* valid, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(jb::signature_rows_kernel, dim3(n), dim3(64), 0, stream, rp, slots, idx, val, n, hash_num,
+                     seed, mode, tbits, tnorm, valid);
   return (int)hipGetLastError();
 }

@@ -50,7 +50,7 @@
 // fills. Decisions follow commit.hip's guard band (a margin within 1e-4 of its
 // threshold is re-scored from the live model M0 + dW before the decision).
 //
-// Device state (int64 words, 256 B) lives in the kSerial scratch; every kernel
+// Device state (int64 words, 512 B) lives in the kSerial scratch; every kernel
 // reads the status first, so a batch's segments are queued without a host round
 // trip and the finished ones cost an empty launch each.
 #include <string.h>
@@ -63,8 +63,8 @@ namespace jb {
 namespace vc {
 
 using dc::Geo;
-constexpr int kFC = 2;                  // feature chunks of 16 per lane
-constexpr int kNFM = 16 * kFC;          // widest sample the committer takes
+constexpr int kFCMax = 2;               // feature chunks of 16 per lane (a sample of <= 32 features)
+constexpr int kRec = 16 * kFCMax;       // feature slots of a candidate record
 constexpr int64_t kLwMin = 2048, kLwMax = 65536, kLwInit = 8192;
 constexpr int kBitWords = (int)(kLwMax / 64);
 constexpr float kTInit = 0.5f, kTMin = 0.125f, kTMax = 64.f;
@@ -77,7 +77,7 @@ enum : int {
   S_DONEB, S_NVALID, S_RETRYW, S_WEND,
   // batch counters
   S_WINDOWS, S_RETRIES, S_STEPS, S_ROUNDS, S_WASTED, S_REFRESH, S_EXACT, S_CAND, S_UPD, S_SAT, S_TICKS,
-  S_NONC, S_NWORDS = 32
+  S_NONC, S_PH0, S_PH1, S_PH2, S_PH3, S_PH4, S_PHW, S_WIDE, S_NWORDS = 64
 };
 // committer stop reasons (S_WHY)
 enum : int { kWhyEnd = 0, kWhySat = 1, kWhyDense = 2 };
@@ -87,6 +87,58 @@ __device__ __forceinline__ int64_t ld_st(const int64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ bool live(int status) { return status == kNew || status == kRetry; }
+
+// The committer's arithmetic with hardware reciprocals (v_rcp_f32, 1 ulp)
+// instead of IEEE divisions (a ten-instruction sequence each): a one-wave
+// step is instruction-bound (4 cycles per wave64 VALU op). Same formulas as
+// jb_linear.hpp step_coeffs / dprec; the guard band (1e-4 relative) absorbs
+// the ulp, and the oracle comparisons hold at rtol 2e-3.
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ bool step_coeffs_fast(int method, float margin, float var, float nrm, bool has_l, float C,
+                                                 float* tau, float* beta) {
+  switch (method) {
+    case PERCEPTRON:
+      if (margin <= 0.f) { *tau = 1.f; *beta = 0.f; return true; }
+      return false;
+    case PA: case PA1: case PA2: {
+      const float loss = 1.f - margin;
+      if (!(loss > 0.f && nrm > 0.f)) return false;
+      const float sq = (has_l ? 2.f : 1.f) * nrm;
+      if (method == PA) *tau = loss * frcp(sq);
+      else if (method == PA1) *tau = fminf(C, loss * frcp(sq));
+      else *tau = loss * frcp(sq + 0.5f * frcp(C));
+      *beta = 0.f;
+      return true;
+    }
+    case CW: {
+      if (!(var > 0.f)) return false;
+      const float phi = C;
+      const float b = 1.f + 2.f * phi * margin;
+      const float disc = b * b - 8.f * phi * (margin - phi * var);
+      const float gamma = (-b + sqrtf(fmaxf(disc, 0.f))) * frcp(4.f * phi * var);
+      if (!(gamma > 0.f)) return false;
+      *tau = gamma; *beta = 2.f * gamma * phi;
+      return true;
+    }
+    case AROW:
+      if (!(margin < 1.f)) return false;
+      *beta = frcp(var + frcp(C));
+      *tau = (1.f - margin) * *beta;
+      return true;
+    case NHERD: {
+      if (!(margin < 1.f)) return false;
+      *tau = (1.f - margin) * frcp(var + frcp(C));
+      const float cv = 1.f + C * var;
+      *beta = (C * C * var + 2.f * C) * frcp(cv * cv);
+      return true;
+    }
+    default: return false;
+  }
+}
+__device__ __forceinline__ float dprec_fast(int method, float beta, float x, float s) {
+  const float bx2 = beta * x * x;
+  return method == CW ? bx2 : bx2 * frcp(1.f - bx2 * s);
+}
 
 // ------------------------------------------------------------ init
 // per batch: the range, the status, zero candidate bits; the window length and
@@ -275,11 +327,12 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
     float acc, q;
     wave_score<LC>(row_ptr, fidx, fval, W, s, lane, la, &n, &acc, &q);
     const int64_t fb = row_ptr[s];
-    if (lane < kNFM) {
+    if (lane < kRec) {
       const bool in = lane < n;
-      FI[k * kNFM + lane] = in ? fidx[fb + lane] : -1;
-      FX[k * kNFM + lane] = in ? fval[fb + lane] : 0.f;
+      FI[k * kRec + lane] = in ? fidx[fb + lane] : -1;
+      FX[k * kRec + lane] = in ? fval[fb + lane] : 0.f;
     }
+    if (lane == 0 && n > 16) atomicOr((unsigned long long*)&st[S_WIDE], 1ull);
     if (lane < LC) S0[k * LC + lane] = acc;
     (void)g;
     const int y = labels[s];
@@ -291,7 +344,7 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
     const float sl0 = wave_slack<LC>(acc, y, la, lane, method, C, q, &bl);
     if (lane == 0) AUX[k] = make_int4(dc::aux_pack(y, bl, n), __float_as_int(q), __float_as_int(sl0), pos);
     if (P == nullptr) continue;
-    if (lane < kNFM) {
+    if (lane < kRec) {
       float2 pp = make_float2(1.f, 1.f);
       if (lane < n) {
         const int32_t idx = fidx[fb + lane];
@@ -300,17 +353,17 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
           if (bl >= 0) pp.y = P[(int64_t)idx * LC + bl];
         }
       }
-      PP0[k * kNFM + lane] = pp;
+      PP0[k * kRec + lane] = pp;
     }
   }
 }
 
 // ------------------------------------------------------------ C: the committer
-template <int LC>
+template <int LC, int FC>
 struct Raw {
-  int32_t fi[kFC];
-  float fx[kFC];
-  float2 pp[kFC];
+  int32_t fi[FC];
+  float fx[FC];
+  float2 pp[FC];
   float s[Geo<LC>::K];
   int aux;
   float nrm;
@@ -318,12 +371,12 @@ struct Raw {
   int pos;
 };
 
-template <int LC>
+template <int LC, int FC>
 struct Samp {
-  int32_t fi[kFC];
-  float fx[kFC];
-  float py[kFC];   // P0(row, y), P0(row, best wrong label at M0)
-  float pl[kFC];
+  int32_t fi[FC];
+  float fx[FC];
+  float py[FC];    // P0(row, y), P0(row, best wrong label at M0)
+  float pl[FC];
   float s[Geo<LC>::K];
   int y;           // -1: no candidate / label out of range
   int ls0;
@@ -338,16 +391,20 @@ struct Samp {
 // max_l |dW[row][l]| (the summed step magnitudes)
 struct __attribute__((aligned(16))) Stamp { float sid, dy, dl, rmax; };
 
-template <int LC, int MT, int R_, int PD_>
+template <int LC, int MT, int R_, int PD_, int FC_>
 __global__ __launch_bounds__(64) void vc_commit_kernel(
     int64_t* __restrict__ st, const float* __restrict__ W, const float* __restrict__ P,
     const int32_t* __restrict__ active, float C, const float* __restrict__ S0_k,
     const int4* __restrict__ AUX_k, const float2* __restrict__ PP0_k, const int32_t* __restrict__ FI_k,
     const float* __restrict__ FX_k, int32_t* __restrict__ g_key, float* __restrict__ g_rmax,
-    float* __restrict__ g_dw, float* __restrict__ g_dp) {
+    float* __restrict__ g_dw, float* __restrict__ g_dp, int prof) {
   using Gm = Geo<LC>;
-  using Rw = Raw<LC>;
-  using S = Samp<LC>;
+  using Rw = Raw<LC, FC_>;
+  using S = Samp<LC, FC_>;
+  // FC_ feature chunks of 16 per lane: 1 when no candidate of the window has
+  // more than 16 features (kernel B's wide flag), else 2
+  constexpr int kFC = FC_;
+  constexpr int kNFM = 16 * FC_;
   // R_ samples per group and round, PD_ rounds of records in flight: the code
   // of a round is instantiated R_ x PD_ times (the instruction cache decides)
   constexpr int kR = R_;
@@ -360,6 +417,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
   constexpr bool use_nrm = MT == PA || MT == PA1 || MT == PA2 || MT == CW;
   constexpr float kG = dc::kGuard;
   if (!live((int)st[S_STATUS])) return;
+  if ((st[S_WIDE] != 0) != (FC_ == 2)) return;
   __shared__ __attribute__((aligned(16))) float s_dw[NSLOT * LC + Gm::PAD];
   __shared__ __attribute__((aligned(16))) float s_dp[use_s ? NSLOT * LC + Gm::PAD : 4];
   __shared__ __attribute__((aligned(16))) int32_t s_key[NSLOT];
@@ -369,6 +427,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
   const int sub = lane & 15;
   const int G = lane >> 4;
   const uint64_t t_k0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t t_c0 = __builtin_amdgcn_s_memtime();
   {
     float4* dw4 = reinterpret_cast<float4*>(s_dw);
     float4* dp4 = reinterpret_cast<float4*>(s_dp);
@@ -386,9 +445,9 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
     const int lab = sub + 16 * k;
     act[k] = (lab < LC && active[lab] != 0) ? 1 : 0;
   }
-  const int64_t ncand = st[S_NCAND];
-  const int64_t wb = st[S_BEG];
-  const int64_t we = st[S_WEND];
+  const int64_t ncand = (int64_t)dc::in_vgpr((uint64_t)st[S_NCAND]);
+  const int64_t wb = (int64_t)dc::in_vgpr((uint64_t)st[S_BEG]);
+  const int64_t we = (int64_t)dc::in_vgpr((uint64_t)st[S_WEND]);
   const float* __restrict__ S0 = dc::in_vgpr(S0_k);
   const int4* __restrict__ AUX = dc::in_vgpr(AUX_k);
   const float2* __restrict__ PP0 = dc::in_vgpr(PP0_k);
@@ -405,7 +464,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
       j = j < 0 ? 0 : j;
 #pragma unroll
       for (int c = 0; c < kFC; ++c) {
-        const int64_t o = j * kNFM + c * 16 + sub;
+        const int64_t o = j * kRec + c * 16 + sub;
         rw[r].fi[c] = dc::gld(FI + o);
         rw[r].fx[c] = dc::gld(FX + o);
         if (use_s) rw[r].pp[c] = dc::gld(PP0 + o);
@@ -453,10 +512,31 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
   int stopped = 0;            // wave-uniform
   int64_t pend = we;
   int why = kWhyEnd;
-  int n_steps = 0, n_upd = 0, n_waste = 0, n_refresh = 0, n_exact = 0;
-  int64_t n_rounds = 0;
+  // the step id stays in a register; the other counters live in LDS (lane 0
+  // adds), which keeps them out of the SGPR file (a spilled SGPR costs a
+  // v_writelane / v_readlane pair at every use)
+  int n_steps = 0, n_exact = 0;
+  __shared__ int s_cnt[4];                 // updates, wasted steps, refreshes, rounds
+  __shared__ unsigned long long s_ph[5];   // phase cycles (prof)
+  if (lane < 4) s_cnt[lane] = 0;
+  if (lane < 5) s_ph[lane] = 0;
+  auto bump = [&](int i) __attribute__((always_inline)) {
+    if (lane == 0) s_cnt[i] += 1;
+  };
   const uint64_t kLead = 0x0001000100010001ull;   // lane 0 of each DPP row
 
+  // phase stamps (prof, JB_COMMIT_PROF=1: shader cycles summed per phase -
+  // round start, step selection, decision, apply, corrections; each stamp
+  // waits for the LDS operations in flight, so they cost a little)
+  const bool kProf = prof != 0;
+
+  uint64_t tp = kProf ? __builtin_amdgcn_s_memtime() : 0;
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    if (!kProf) return;
+    const uint64_t t = __builtin_amdgcn_s_memtime();
+    if (lane == 0) s_ph[i] += t - tp;
+    tp = t;
+  };
   auto round = [&](int64_t k0) __attribute__((always_inline)) {
     int alive[kR], unsafe[kR], exact[kR];
     float slack[kR];
@@ -467,12 +547,12 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
       alive[r] = (sc[r].y >= 0 && sc[r].y < LC) ? 1 : 0;
       widew |= alive[r] && sc[r].nf > 16;
     }
-    const bool two = __builtin_amdgcn_ballot_w64(widew) != 0;
+    const bool two = kFC == 2 && __builtin_amdgcn_ballot_w64(widew) != 0;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
       const bool ok = alive[r] && sc[r].nf <= kNFM;
       slot[r][0] = ok ? dc::cache_find<LC>(s_key, sc[r].fi[0]) : -1;
-      slot[r][1] = (two && ok) ? dc::cache_find<LC>(s_key, sc[r].fi[1]) : -1;
+      if (kFC == 2) slot[r][kFC - 1] = (two && ok) ? dc::cache_find<LC>(s_key, sc[r].fi[kFC - 1]) : -1;
     }
     // samples of the round whose slack ran out (positions > after): exact
     // scores S0 + x . dW against the live store, exact margin and slack
@@ -515,6 +595,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
       exact[r] = 0;
     }
     make_exact(-1);
+    stamp(0);
 #pragma unroll
     for (int r = 0; r < kR; ++r) unsafe[r] = (alive[r] && (sc[r].nf > kNFM || !(slack[r] > 0.f))) ? 1 : 0;
 
@@ -530,6 +611,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
           k = min(k, gk * kR + r);
         }
       }
+      stamp(1);
       if (k == dc::kInf) break;
       const int Gk = k / kR, rk = k % kR;
       (void)rk;
@@ -590,7 +672,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
             py[c] = t.py[c] + dpr[y];
             if (ls >= 0) pl[c] = p0l[c] + dpr[ls];
             const float x2 = t.fx[c] * t.fx[c];
-            v += x2 * (1.f / py[c] + (ls >= 0 ? 1.f / pl[c] : 0.f));
+            v += x2 * (frcp(py[c]) + (ls >= 0 ? frcp(pl[c]) : 0.f));
           }
           var = use_s ? row16_sum(v) : 0.f;
           if (refreshed) break;
@@ -599,7 +681,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
           if (__builtin_amdgcn_ballot_w64(mine && fabsf(m - thr) < g) == 0) break;
           // near the threshold: re-score from the live model (M0 + dW)
           refreshed = true;
-          ++n_refresh;
+          bump(2);
           float ns[K];
 #pragma unroll
           for (int kk = 0; kk < K; ++kk) ns[kk] = 0.f;
@@ -623,11 +705,12 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
           for (int kk = 0; kk < K; ++kk) t.s[kk] = ns[kk];
         }
         float tau = 0.f, beta = 0.f;
-        const bool up_l = step_coeffs(method, m, var, t.nrm, ls >= 0, C, &tau, &beta);
+        const bool up_l = step_coeffs_fast(method, m, var, t.nrm, ls >= 0, C, &tau, &beta);
         const bool up = __builtin_amdgcn_ballot_w64(mine && up_l) != 0;
+        stamp(2);
         const int sid = n_steps++;
         if (!up) {
-          ++n_waste;
+          bump(1);
         } else {
           // the sample's rows not in the store yet; a full bucket pair ends the
           // window before this candidate (nothing of its step is applied)
@@ -649,7 +732,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
             return 1;
           }
           const bool nins = __builtin_amdgcn_ballot_w64(any_new) != 0;
-          ++n_upd;
+          bump(0);
           if (mine) {
 #pragma unroll
             for (int c = 0; c < kFC; ++c)
@@ -663,8 +746,8 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
             for (int c = 0; c < kFC; ++c) {
               if (t.fi[c] < 0) continue;
               const float x = t.fx[c];
-              const float a = use_s ? 1.f / py[c] : 1.f;
-              const float b = (use_s && ls >= 0) ? 1.f / pl[c] : 1.f;
+              const float a = use_s ? frcp(py[c]) : 1.f;
+              const float b = (use_s && ls >= 0) ? frcp(pl[c]) : 1.f;
               const float dwy = tau * a * x;
               const float dwl = ls >= 0 ? -tau * b * x : 0.f;
               float* dwr = s_dw + sl[c] * LC;
@@ -672,8 +755,8 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
               if (ls >= 0) atomicAdd(dwr + ls, dwl);
               if (use_s) {
                 float* dpr = s_dp + sl[c] * LC;
-                atomicAdd(dpr + y, dprec(method, beta, x, a));
-                if (ls >= 0) atomicAdd(dpr + ls, dprec(method, beta, x, b));
+                atomicAdd(dpr + y, dprec_fast(method, beta, x, a));
+                if (ls >= 0) atomicAdd(dpr + ls, dprec_fast(method, beta, x, b));
               }
               float* sg = reinterpret_cast<float*>(&s_sg[sl[c]]);
               atomicAdd(sg + 1, dwy);
@@ -683,6 +766,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
           }
           // the later samples of the round: slots of the rows the step added,
           // then the step's increments of their stamped rows
+          stamp(3);
           const int yk = __builtin_amdgcn_readlane(y, Gk * 16);
           const int lk = __builtin_amdgcn_readlane(ls, Gk * 16);
           if (nins) {
@@ -743,10 +827,11 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
         case 2: if constexpr (kR > 2) stop_code = step_of(std::integral_constant<int, (kR > 2 ? 2 : 0)>{}); break;
         default: if constexpr (kR > 3) stop_code = step_of(std::integral_constant<int, (kR > 3 ? 3 : 0)>{}); break;
       }
+      stamp(4);
       if (stop_code) break;
       lim = k;
     }
-    ++n_rounds;
+    bump(3);
   };
   // the round loop unrolled kPD times (each round reads its own prefetch slot
   // and refills it kPD rounds ahead: no register copies of loads in flight)
@@ -780,15 +865,19 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
   if (lane == 0) {
     st[S_PEND] = pend;
     st[S_WHY] = why;
-    st[S_NUPD] = n_upd;
+    st[S_NUPD] = s_cnt[0];
     st[S_NSLOTS] = nslots;
     st[S_STEPS] += n_steps;
-    st[S_ROUNDS] += n_rounds;
-    st[S_WASTED] += n_waste;
-    st[S_REFRESH] += n_refresh;
+    st[S_ROUNDS] += s_cnt[3];
+    st[S_WASTED] += s_cnt[1];
+    st[S_REFRESH] += s_cnt[2];
     st[S_EXACT] += n_exact;
     st[S_CAND] += ncand;
     st[S_TICKS] += (int64_t)(__builtin_amdgcn_s_memrealtime() - t_k0);
+    if (kProf) {
+      for (int i = 0; i < 5; ++i) st[S_PH0 + i] += (int64_t)s_ph[i];
+      st[S_PHW] += (int64_t)(__builtin_amdgcn_s_memtime() - t_c0);
+    }
   }
 }
 
@@ -931,6 +1020,7 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
     st[S_NVALID] = 0;
     st[S_VIOL] = 0;
     const int s2 = (int)st[S_STATUS];
+    if (s2 != kRetry) st[S_WIDE] = 0;   // a retry keeps the window's candidates (and width)
     tail[0] = s2 == kDone ? st[S_BEND] : st[S_BEG];
     tail[1] = st[S_BEND];
     tail[2] = st[S_STEPS];
@@ -947,6 +1037,8 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
     tail[28] = st[S_RETRIES];
     tail[29] = st[S_SAT];
     tail[30] = st[S_TICKS];
+    for (int i = 0; i < 5; ++i) tail[10 + i] = st[S_PH0 + i];
+    tail[15] = st[S_PHW];
     tail[8] = st[S_LW];
     tail[9] = st[S_T];
     tail[7] = st[S_NONC];
@@ -957,8 +1049,8 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
 }  // namespace jb
 
 // bytes of the verified committer's fixed region (after the per-sample arrays):
-// state (256 B), candidate bits, the staged store (keys, rmax, dW, dP)
-static constexpr int64_t kVcFixed = 256 + 8 * jb::vc::kBitWords + 4 * 1024 + 4 * 1024 + 2 * 4 * 16384;
+// state (512 B), candidate bits, the staged store (keys, rmax, dW, dP)
+static constexpr int64_t kVcFixed = 512 + 8 * jb::vc::kBitWords + 4 * 1024 + 4 * 1024 + 2 * 4 * 16384;
 extern "C" int64_t jb_vcommit_fixed_bytes() { return kVcFixed; }
 
 template <int L>
@@ -968,8 +1060,13 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
                      float* fx, int32_t* gk, float* gr, float* gdw, float* gdp, uint8_t* touched,
                      unsigned long long* stats, int64_t* tail, int nseg, hipStream_t stream) {
   using namespace jb::vc;
+  static const int prof = [] {
+    const char* e = getenv("JB_COMMIT_PROF");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
   // committer shape (samples per group x rounds in flight), for A/B runs:
-  // JB_VC_SHAPE = r2pd2 | r2pd1 | r1pd1 | r1pd3; default r1pd2
+  // JB_VC_SHAPE = r1pd1; default r1pd2 (measured: r1pd2 7.19, r1pd1 7.27,
+  // r1pd3 7.25, r2pd1 8.47, r2pd2 8.45 ms per steady 131 K batch)
   static const int shape = [] {
     const char* e = getenv("JB_VC_SHAPE");
     if (e == nullptr) return 0;
@@ -985,14 +1082,13 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
                        W, active, method, C, sl, bits);
     hipLaunchKernelGGL((vc_gather_kernel<L>), dim3(512), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx);
-#define JB_VC_S(M, R, PD)                                                                                    \
-  hipLaunchKernelGGL((vc_commit_kernel<L, M, R, PD>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, \
-                     aux, pp0, fi, fx, gk, gr, gdw, gdp);
+#define JB_VC_S(M, R, PD)                                                                                       \
+  hipLaunchKernelGGL((vc_commit_kernel<L, M, R, PD, 1>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, \
+                     aux, pp0, fi, fx, gk, gr, gdw, gdp, prof);                                                  \
+  hipLaunchKernelGGL((vc_commit_kernel<L, M, R, PD, 2>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, \
+                     aux, pp0, fi, fx, gk, gr, gdw, gdp, prof);
 #define JB_VC_M(M)                               \
-  if (shape == 1) { JB_VC_S(M, 2, 2) }           \
-  else if (shape == 2) { JB_VC_S(M, 2, 1) }      \
-  else if (shape == 3) { JB_VC_S(M, 1, 1) }      \
-  else if (shape == 4) { JB_VC_S(M, 1, 3) }      \
+  if (shape == 3) { JB_VC_S(M, 1, 1) }           \
   else { JB_VC_S(M, 1, 2) }                      \
   break;
     switch (method) {
@@ -1034,8 +1130,8 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
   float* sl = (float*)(base + 784 * n_max);
   uint8_t* fixed = base + ((788 * n_max + 255) & ~(int64_t)255);
   int64_t* st = (int64_t*)fixed;
-  unsigned long long* bits = (unsigned long long*)(fixed + 256);
-  int32_t* gk = (int32_t*)(fixed + 256 + 8 * jb::vc::kBitWords);
+  unsigned long long* bits = (unsigned long long*)(fixed + 512);
+  int32_t* gk = (int32_t*)(fixed + 512 + 8 * jb::vc::kBitWords);
   float* gr = (float*)((uint8_t*)gk + 4 * 1024);
   float* gdw = (float*)((uint8_t*)gr + 4 * 1024);
   float* gdp = gdw + 16384;

@@ -57,6 +57,9 @@ int jb_lsh_query_direct(const int32_t* idx, const float* val, const int64_t* row
 int jb_lsh_set_rows_direct(const int32_t* idx, const float* val, const int64_t* row_ptr, int n,
                            const int64_t* slots, int hash_num, uint64_t seed, int mode,
                            uint64_t* tbits, float* tnorm, uint8_t* valid, hipStream_t stream);
+int jb_lsh_set_rows_staged(const int64_t* rp, const int64_t* slots, const int32_t* idx, const float* val, int n,
+                           int hash_num, uint64_t seed, int mode, uint64_t* tbits, float* tnorm, uint8_t* valid,
+                           hipStream_t stream);
 int jb_topk_direct_query(const uint64_t* qbits, const float* qnorm, int nq, const uint64_t* tbits,
                          const float* tnorm, const uint8_t* valid, int64_t nrows, int words,
                          int hash_num, int metric, int k, float* scratch_d, int32_t* scratch_i,
@@ -91,6 +94,7 @@ using jb::val::MsgpackReader;
 using jb::val::MsgpackWriter;
 using jb::val::Value;
 using jb::srv::DevBuf;
+using jb::srv::PinBuf;
 
 constexpr int kTopMaxK = 128;        // csrc/hip/topk.hip kTopMaxK
 constexpr int kQueryMax = 8;         // lsh.hip kQueryMax
@@ -330,13 +334,76 @@ class LshIndex {
   int metric() const { return metric_; }
 
   void clear() {
+    pend_slot_.clear();
+    pend_rp_.assign(1, 0);
+    pend_idx_.clear();
+    pend_val_.clear();
     cap_ = 0;
     bits_.p = nullptr; bits_.cap = 0;
     alloc(1024);
   }
 
+  // batched writes (the row server's write batches): rows set while deferred
+  // are kept on the host and written by one staged launch in flush(); every
+  // other access flushes first, so nothing observes the deferral
+  void set_defer(bool on) {
+    if (!on) flush();
+    defer_ = on;
+  }
+  void flush() {
+    if (pend_slot_.empty()) return;
+    // the last write of a slot wins (rows of one launch must be distinct)
+    std::unordered_map<int32_t, size_t> last;
+    for (size_t i = 0; i < pend_slot_.size(); ++i) last[pend_slot_[i]] = i;
+    std::vector<size_t> keep;
+    for (size_t i = 0; i < pend_slot_.size(); ++i)
+      if (last[pend_slot_[i]] == i) keep.push_back(i);
+    const size_t n = keep.size();
+    size_t nnz = 0;
+    for (size_t i : keep) nnz += pend_rp_[i + 1] - pend_rp_[i];
+    const size_t bytes = 8 * (2 * n + 1) + 8 * nnz + 16;
+    uint8_t* h = stage_host_.get(bytes);
+    int64_t* rp = (int64_t*)h;
+    int64_t* sl = rp + n + 1;
+    int32_t* ix = (int32_t*)(sl + n);
+    float* vx = (float*)(ix + nnz);
+    rp[0] = 0;
+    size_t o = 0;
+    for (size_t q = 0; q < n; ++q) {
+      const size_t i = keep[q];
+      const size_t b = pend_rp_[i], e = pend_rp_[i + 1];
+      memcpy(ix + o, pend_idx_.data() + b, 4 * (e - b));
+      memcpy(vx + o, pend_val_.data() + b, 4 * (e - b));
+      o += e - b;
+      rp[q + 1] = (int64_t)o;
+      sl[q] = pend_slot_[i];
+    }
+    uint8_t* d = stage_dev_.get(bytes);
+    HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream_));
+    const int64_t* drp = (const int64_t*)d;
+    const int rc = jb_lsh_set_rows_staged(drp, drp + n + 1, (const int32_t*)(drp + 2 * n + 1),
+                                          (const float*)((const int32_t*)(drp + 2 * n + 1) + nnz), (int)n, hash_num_,
+                                          seed_, mode_, (uint64_t*)bits_.p, norms_.p, valid_.p, stream_);
+    if (rc != 0) throw std::runtime_error("lsh staged set failed: " + std::to_string(rc));
+    HIPCHK(hipStreamSynchronize(stream_));   // the pinned staging is reused by the next batch
+    pend_slot_.clear();
+    pend_rp_.assign(1, 0);
+    pend_idx_.clear();
+    pend_val_.clear();
+    ++flushes_;
+  }
+  uint64_t flushes() const { return flushes_; }
+
   void set(int32_t slot, const std::vector<int32_t>& idx, const std::vector<float>& val) {
     grow(slot + 1);
+    if (defer_) {
+      pend_slot_.push_back(slot);
+      pend_idx_.insert(pend_idx_.end(), idx.begin(), idx.end());
+      pend_val_.insert(pend_val_.end(), val.begin(), val.end());
+      pend_rp_.push_back(pend_idx_.size());
+      if (pend_slot_.size() >= 4096) flush();
+      return;
+    }
     const int64_t rp[2] = {0, (int64_t)idx.size()};
     const int64_t sl = slot;
     int rc = jb_lsh_set_rows_direct(idx.data(), val.data(), rp, 1, &sl, hash_num_, seed_, mode_,
@@ -352,12 +419,14 @@ class LshIndex {
   }
 
   void remove(int32_t slot) {
+    flush();
     if (slot < cap_) HIPCHK(hipMemsetAsync(valid_.p + slot, 0, 1, stream_));
   }
 
   // k nearest rows of a hashed feature vector (ascending distance)
   std::vector<Hit> query_fv(const std::vector<int32_t>& idx, const std::vector<float>& val,
                             int64_t nrows, int k) {
+    flush();
     if (nrows <= 0 || k <= 0) return {};
     if (k <= kTopMaxK) {
       bufs_.scratch(nrows, k, 1);
@@ -383,6 +452,7 @@ class LshIndex {
   bool query_fv_many(const std::vector<const std::vector<int32_t>*>& idx,
                      const std::vector<const std::vector<float>*>& val, int64_t nrows, int k,
                      std::vector<std::vector<Hit>>* out) {
+    flush();
     const int nq = (int)idx.size();
     if (nq <= 0 || nq > kQueryMax || nrows <= 0 || k <= 0 || k > kTopMaxK) return false;
     std::vector<int64_t> rp(1, 0);
@@ -406,6 +476,7 @@ class LshIndex {
   }
 
   std::vector<Hit> query_slot(int32_t slot, int64_t nrows, int k) {
+    flush();
     if (nrows <= 0 || k <= 0) return {};
     return query_sig((const uint64_t*)bits_.p + (size_t)slot * words_, norms_.p + slot, nrows, k);
   }
@@ -552,6 +623,15 @@ class LshIndex {
   DevBuf<int32_t> d_idx_;
   DevBuf<float> d_val_;
   QueryBufs bufs_;
+  // deferred writes (set_defer)
+  bool defer_ = false;
+  std::vector<int32_t> pend_slot_;
+  std::vector<size_t> pend_rp_{0};
+  std::vector<int32_t> pend_idx_;
+  std::vector<float> pend_val_;
+  PinBuf<uint8_t> stage_host_;
+  DevBuf<uint8_t> stage_dev_;
+  uint64_t flushes_ = 0;
 };
 
 // ------------------------------------------------------- inverted index
@@ -948,6 +1028,12 @@ class RowEngine {
         remove(victim);
       }
     }
+  }
+
+  // batched writes (Model::write_many): the LSH index keeps the rows set
+  // meanwhile on the host and writes them in one launch when it ends
+  void defer_writes(bool on) {
+    if (lsh_) lsh_->set_defer(on);
   }
 
   // called with the slot of every removed row (the LOF state's moved())

@@ -298,6 +298,7 @@ class Model : public jb::mix::Mixable {
     if (batcher_.joinable()) batcher_.join();
   }
   uint64_t batches() const { return n_batches_.load(); }
+  uint64_t n_write_batches_ = 0, n_write_rows_ = 0;   // (under mu_)
   uint64_t batched_queries() const { return n_batched_.load(); }
 
   void configure(const Config& cfg) {
@@ -419,6 +420,10 @@ class Model : public jb::mix::Mixable {
     Datum nd;
     jb::row::parse_datum(dv, &nd);
     std::unique_lock<std::shared_mutex> g(mu_);
+    update_row_locked(id, std::move(nd));
+    return true;
+  }
+  void update_row_locked(const std::string& id, Datum&& nd) {
     ++update_count;
     ++update_row_cnt;
     if (const jb::row::Row* r = eng_->find(id)) {
@@ -429,8 +434,58 @@ class Model : public jb::mix::Mixable {
       nd = std::move(m);
     }
     eng_->set(id, std::move(nd));
-    return true;
   }
+
+  // A batch of queued writes of one method (the RPC batch thread, see
+  // Server::run): the datums parse outside the model lock, the writes apply
+  // in arrival order under ONE exclusive section, and the LSH signatures of
+  // the whole batch go to the device in one staged launch (LshIndex
+  // set_defer) instead of one launch per row. kind: 0 update_row, 1
+  // set_row, 2 clear_row. -> per write: 1 / 0 (clear_row of an unknown id),
+  // or the exception it raised
+  struct Write {
+    const std::string* id;
+    const Value* dv;
+    int result = 0;
+    std::exception_ptr err;
+  };
+  void write_many(int kind, std::vector<Write>& ws) {
+    std::vector<Datum> ds(ws.size());
+    for (size_t i = 0; i < ws.size(); ++i) {
+      if (kind == 2) continue;
+      try {
+        jb::row::parse_datum(*ws[i].dv, &ds[i]);
+      } catch (...) {
+        ws[i].err = std::current_exception();
+      }
+    }
+    std::unique_lock<std::shared_mutex> g(mu_);
+    eng_->defer_writes(true);
+    for (size_t i = 0; i < ws.size(); ++i) {
+      if (ws[i].err) continue;
+      try {
+        if (kind == 0) {
+          update_row_locked(*ws[i].id, std::move(ds[i]));
+          ws[i].result = 1;
+        } else if (kind == 1) {
+          ++update_count;
+          eng_->set(*ws[i].id, std::move(ds[i]));
+          ws[i].result = 1;
+        } else {
+          ++update_count;
+          ++clear_row_cnt;
+          ws[i].result = eng_->remove(*ws[i].id) ? 1 : 0;
+        }
+      } catch (...) {
+        ws[i].err = std::current_exception();
+      }
+    }
+    eng_->defer_writes(false);
+    ++n_write_batches_;
+    n_write_rows_ += ws.size();
+  }
+  uint64_t write_batches() const { return n_write_batches_; }
+  uint64_t write_rows() const { return n_write_rows_; }
   // nearest_neighbor set_row: replace
   bool set_row(const std::string& id, const Value& dv) {
     Datum nd;
@@ -688,6 +743,8 @@ class Model : public jb::mix::Mixable {
     std::shared_lock<std::shared_mutex> g(mu_);
     auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
     add("method", kind_ == Kind::kNearestNeighbor ? eng_->method() : cfg_.outer);
+    add("write_batches", std::to_string(n_write_batches_));   // Model::write_many
+    add("write_batch_rows", std::to_string(n_write_rows_));
     if (kind_ == Kind::kClassifier) {
       add("num_labels", std::to_string(labels_.size()));
       add("nearest_neighbor_num", std::to_string(cfg_.nn_k));
@@ -1067,9 +1124,18 @@ class Server {
       qm.push_back("neighbor_row_from_id");
     }
     if (kind_ == Kind::kAnomaly) qm = {"calc_score"};
+    // writes of the similarity engines: one exclusive section and one device
+    // launch per batch of queued writes (Model::write_many)
+    if (kind_ == Kind::kRecommender) {
+      qm.push_back("update_row");
+      qm.push_back("clear_row");
+    }
+    if (kind_ == Kind::kNearestNeighbor) qm.push_back("set_row");
     if (!qm.empty())
-      rpc_->set_batch(qm, [this](const std::string& m, std::vector<jb::RpcRequest>& rs) { return query_batch(m, rs); },
-                      1024);
+      rpc_->set_batch(qm, [this](const std::string& m, std::vector<jb::RpcRequest>& rs) {
+        if (m == "update_row" || m == "set_row" || m == "clear_row") return write_batch(m, rs);
+        return query_batch(m, rs);
+      }, 1024);
     int port;
     try {
       port = rpc_->listen(a_.bind, a_.port);
@@ -1115,6 +1181,55 @@ class Server {
  private:
   std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
   const char* type() const { return kind_name(kind_); }
+
+  // one batch of writes of method m (see run()): malformed ones answer as
+  // dispatch() would, the rest apply as one Model::write_many
+  std::vector<std::string> write_batch(const std::string& m, std::vector<jb::RpcRequest>& rs) {
+    std::vector<std::string> out(rs.size());
+    std::vector<Value> args(rs.size());
+    std::vector<Model::Write> ws;
+    std::vector<size_t> at;
+    const bool clr = m == "clear_row";
+    for (size_t i = 0; i < rs.size(); ++i) {
+      const jb::RpcRequest& r = rs[i];
+      bool ok = true;
+      try {
+        args[i] = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
+      } catch (const std::exception&) {
+        ok = false;
+      }
+      const Value& a = args[i];
+      ok = ok && a.kind == Value::ARR && a.a.size() == (clr ? 2u : 3u) && a.a[0].is_str() && a.a[1].is_str() &&
+           (clr || a.a[2].kind == Value::ARR);
+      if (!ok) {
+        out[i] = r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+        continue;
+      }
+      Model::Write w;
+      w.id = &a.a[1].s;
+      w.dv = clr ? nullptr : &a.a[2];
+      ws.push_back(w);
+      at.push_back(i);
+    }
+    if (ws.empty()) return out;
+    if (mixer_) mixer_->updated(ws.size());   // event_model_updated, once per write
+    model_->write_many(m == "update_row" ? 0 : m == "set_row" ? 1 : 2, ws);
+    for (size_t j = 0; j < ws.size(); ++j) {
+      const jb::RpcRequest& r = rs[at[j]];
+      if (r.notify) continue;
+      try {
+        if (ws[j].err) std::rethrow_exception(ws[j].err);
+        MsgpackWriter w;
+        w.boolean(ws[j].result != 0);
+        out[at[j]] = jb::val::response_ok(r.msgid, w.out);
+      } catch (const ArgError&) {
+        out[at[j]] = jb::val::response_code(r.msgid, kArgumentError);
+      } catch (const std::exception& e) {
+        out[at[j]] = jb::val::response_msg(r.msgid, e.what());
+      }
+    }
+    return out;
+  }
 
   // one batch of analysis requests of method m (see run()): malformed ones
   // answer as dispatch() would, the rest run as one Model::run_calls

@@ -684,6 +684,10 @@ class SerialScratch:
                        wasted_steps=v[22], refreshes=v[23], exact_rescored=v[26], last_segment_rows=v[25],
                        window_len=v[8], T=round(struct.unpack("f", struct.pack("I", v[9] & 0xffffffff))[0], 4),
                        commit_kernel_us=round(v[30] / 100.0, 1))
+            if v[15] > 0:      # JB_COMMIT_PROF=1: committer phases (shader cycles -> us by the wall clock)
+                us = (v[30] / 100.0) / v[15]
+                for i, nm in enumerate(("round_start", "select", "decide", "apply", "correct")):
+                    out[f"commit_{nm}_us"] = round(v[10 + i] * us, 1)
             return out
         if v[24] > 0 or v[22] > 0:
             # delta committer (csrc/hip/commit.hip): steps that did not update,

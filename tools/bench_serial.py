@@ -57,7 +57,8 @@ def main():
             if mode == "exact":
                 d = clf._serial.last_batch()
                 keys = ("segments", "wasted_steps", "refreshes", "committer_updates", "last_segment_rows", "rounds",
-                        "exact_rescored", "committed_samples")
+                        "exact_rescored", "committed_samples", "windows", "retries", "candidates", "T",
+                        "window_len", "saturated_windows", "non_candidates_verified")
                 diag.append((d["exact_steps"], (d["end"] - d["tail_start"]) / max(1, d["end"]),
                              {k: v for k, v in d.items() if k.startswith("commit") or k in keys}))
             if b % 10 == 9:

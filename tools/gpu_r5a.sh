@@ -1,9 +1,11 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for sh in r1pd2 r1pd1 r1pd3 r2pd1 r2pd2; do
-  JB_VC_SHAPE=$sh timeout -k 10 200 python tools/bench_serial.py --batches 30 --modes exact > gpurun_out/serial_$sh.log 2>&1
-  echo "$sh rc=$?"; tail -1 gpurun_out/serial_$sh.log | cut -c1-200
-done
-JB_VC_SHAPE=r1pd2 timeout -k 10 300 python tools/bench_serial.py --batches 6 --modes exact --worst-case > gpurun_out/serial_vw.log 2>&1
-echo "worst rc=$?"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_linear.py -m gpu -x -q --timeout 300 --timeout-method thread -k "serial" > gpurun_out/t_serial.log 2>&1
+echo "pytest rc=$?"; tail -3 gpurun_out/t_serial.log
+JB_COMMIT_PROF=1 timeout -k 10 200 python tools/bench_serial.py --batches 30 --modes exact > gpurun_out/serial_prof.log 2>&1
+echo "prof rc=$?"
+timeout -k 10 200 python tools/bench_serial.py --batches 40 --modes exact > gpurun_out/serial_v.log 2>&1
+echo "v rc=$?"
+JB_COMMIT_PROF=1 timeout -k 10 200 python tools/bench_serial.py --batches 4 --modes exact --worst-case > gpurun_out/serial_profw.log 2>&1
+echo "profw rc=$?"
