@@ -67,8 +67,13 @@ constexpr int kFCMax = 2;               // feature chunks of 16 per lane (a samp
 constexpr int kRec = 16 * kFCMax;       // feature slots of a candidate record
 constexpr int64_t kLwMin = 2048, kLwMax = 65536, kLwInit = 8192;
 constexpr int kBitWords = (int)(kLwMax / 64);
-constexpr float kTInit = 0.5f, kTMin = 0.125f, kTMax = 64.f;
-constexpr int64_t kMagic = 0x56434f4d4d495432LL;
+// candidate rule (kernel A): slack0 <= max(kTFloor, T x the sample's bound
+// under the PREVIOUS window's per-row step magnitudes) - the bound the
+// verification will apply, predicted from the window before (the hot rows -
+// shared numeric keys, frequent tokens - are written in every window alike).
+// T adapts: x1.5 on a verification failure, x0.97 per committed window.
+constexpr float kTInit = 2.f, kTMin = 1.25f, kTMax = 64.f, kTFloor = 0.02f;
+constexpr int64_t kMagic = 0x56434f4d4d495433LL;
 constexpr int kRetryForce = 3;          // retries of one window before all its samples are candidates
 enum : int { kNew = 0, kRetry = 1, kDone = 2, kDense = 3 };
 // state words
@@ -145,10 +150,15 @@ __device__ __forceinline__ float dprec_fast(int method, float beta, float x, flo
 // T persist across batches on the same scratch (a model's stream)
 __global__ __launch_bounds__(256) void vc_init_kernel(int64_t* __restrict__ st, const int64_t* __restrict__ sp,
                                                       int nstreams, unsigned long long* __restrict__ bits,
-                                                      int64_t* __restrict__ tail, float t_force) {
+                                                      int64_t* __restrict__ tail, float t_force,
+                                                      int32_t* __restrict__ g_key, float* __restrict__ g_rmax) {
   for (int i = threadIdx.x; i < kBitWords; i += blockDim.x) bits[i] = 0ull;
+  const bool fresh = st[S_MAGIC] != kMagic;
+  if (fresh)      // no previous window: the candidate rule's row bounds are empty
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) { g_key[i] = -1; g_rmax[i] = 0.f; }
+  __syncthreads();
   if (threadIdx.x != 0) return;
-  if (st[S_MAGIC] != kMagic) {
+  if (fresh) {
     for (int i = 0; i < S_NWORDS; ++i) st[i] = 0;
     st[S_MAGIC] = kMagic;
     st[S_LW] = kLwInit;
@@ -226,10 +236,19 @@ __global__ __launch_bounds__(256) void vc_score_kernel(
     const int64_t* __restrict__ st, const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ fidx,
     const float* __restrict__ fval, const int32_t* __restrict__ labels, const float* __restrict__ W,
     const int32_t* __restrict__ active, int method, float C, float* __restrict__ SL,
-    unsigned long long* __restrict__ bits) {
+    unsigned long long* __restrict__ bits, const int32_t* __restrict__ g_key, const float* __restrict__ g_rmax) {
   using L = Lanes<LC>;
+  using Gm = Geo<LC>;
   static_assert(LC <= 64, "verified committer: LC <= 64");
   if (st[S_STATUS] != kNew) return;
+  // the previous window's rows and their step magnitudes (its staged store)
+  __shared__ __attribute__((aligned(16))) int32_t s_key[Gm::NSLOT];
+  __shared__ float s_rmax[Gm::NSLOT];
+  for (int i = threadIdx.x; i < Gm::NSLOT; i += blockDim.x) {
+    s_key[i] = g_key[i];
+    s_rmax[i] = g_rmax[i];
+  }
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t beg = st[S_BEG], bend = st[S_BEND];
   const int64_t lw = st[S_LW];
@@ -250,9 +269,25 @@ __global__ __launch_bounds__(256) void vc_score_kernel(
     }
     int bl;
     const float sl0 = wave_slack<LC>(acc, y, la, lane, method, C, q, &bl);
+    // the predicted bound: sum_f |x_f| rmax_prev(row_f) (feature groups of the
+    // score loop, then across the groups)
+    float pb = 0.f;
+    {
+      const int g = lane / L::LW;
+      const int64_t fb = row_ptr[s];
+      for (int j = g; j < n; j += L::G) {
+        const int32_t row = fidx[fb + j];
+        if (row < 0) continue;
+        const int sl = dc::cache_find<LC>(s_key, row);
+        if (sl >= 0) pb += fabsf(fval[fb + j]) * s_rmax[sl];
+      }
+#pragma unroll
+      for (int off = L::LW; off < 64; off <<= 1) pb += __shfl_xor(pb, off, 64);
+    }
+    const float thr = fmaxf(kTFloor, T * 2.f * (1.f + 4.f * dc::kGuard) * pb);
     if (lane == 0) {
       SL[wid] = sl0;
-      if (!(sl0 > T)) atomicOr(bits + (wid >> 6), 1ull << (wid & 63));
+      if (!(sl0 > thr)) atomicOr(bits + (wid >> 6), 1ull << (wid & 63));
     }
   }
 }
@@ -1079,7 +1114,7 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
   float* Pp = method >= jb::CW ? S : nullptr;
   for (int seg = 0; seg < nseg; ++seg) {
     hipLaunchKernelGGL((vc_score_kernel<L>), dim3(1024), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
-                       W, active, method, C, sl, bits);
+                       W, active, method, C, sl, bits, gk, gr);
     hipLaunchKernelGGL((vc_gather_kernel<L>), dim3(512), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx);
 #define JB_VC_S(M, R, PD)                                                                                       \
@@ -1140,7 +1175,7 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
   const char* te = getenv("JB_VERIFIED_T");
   const float t_force = te != nullptr ? (float)atof(te) : 0.f;
   hipLaunchKernelGGL(jb::vc::vc_init_kernel, dim3(1), dim3(256), 0, stream, st, stream_ptr, nstreams, bits, tail,
-                     t_force);
+                     t_force, gk, gr);
   int rc = 0;
 #define JB_VC_L(L)                                                                                            \
   rc = launch_vc<L>(method, row_ptr, fidx, fval, labels, W, S, active, C, st, sl, bits, s0, aux, pp0, fi, fx, \

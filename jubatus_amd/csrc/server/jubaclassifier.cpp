@@ -810,7 +810,10 @@ class Classifier : public jb::mix::Mixable {
       }
       HIPCHK(hipStreamSynchronize(compute_));
     }
-    if (!both) push_dirty_ = true;
+    // a side that could not fold after the exchange (its labels re-laid out
+    // meanwhile) differs from a peer that did: its next MIX is dense, which
+    // re-marks every row (both sides fold, or the rows return)
+    if (!both || !applied) push_dirty_ = true;
     // 6. the document statistics of idf / bm25 converters
     if (conv_.global()) {
       std::string dm;

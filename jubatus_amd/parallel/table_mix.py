@@ -24,9 +24,15 @@ touched rows, and the extra memory is 2 x the union's rows.
 
 ``wire_dtype`` (``JUBATUS_MIX_DTYPE``): ``fp32`` (default) or
 ``bf16`` - the SUM all-reduce then moves bf16 values (half the bytes over
-xGMI); the snapshot and the fold stay fp32, so each MIX rounds the mean to
-bf16 once (relative error <= 2^-8 per MIX, not accumulated: the next MIX
-replaces it) while updates made during the collective are kept exactly.
+xGMI). The snapshot and the fold stay fp32, so updates made during the
+collective are kept exactly, but the wire's rounding is not: the all-reduce
+itself adds in bf16, so a ring rounds at every hop (relative error of the
+sum ~ world x 2^-9, growing with the world size, not a fixed 2^-8), and the
+fold writes ``mean_bf16 - snapshot`` into the tables, so that error becomes
+part of the model (a later MIX does not undo it; it averages on from there).
+The native mixer (csrc/server/jubaclassifier.cpp) keeps the precision
+tables (S / P of CW, AROW, NHERD) in fp32 on the wire and sends only the
+weights in bf16.
 
 When the union exceeds ``dense_frac`` of the table (or no touched map
 exists: host backend, after a model load or a label re-layout), the MIX is

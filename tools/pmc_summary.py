@@ -85,6 +85,21 @@ def main() -> int:
     for r in rows:
         lines.append(f"| `{r[0]}` | {r[1]} | {f(r[2])} | {f(r[3], 0)} | {f(r[4], 0)} | {f(r[5], 0)} | "
                      f"{f(r[6])} | {f(r[7])} | {f(r[8])} | {f(r[9])} | {f(r[10])} | {f(r[11])} |")
+    # every counter collected, mean per dispatch (the SQ ones per wave too)
+    names = sorted({n for c in vals.values() for n in c})
+    lines += ["", "## all counters (mean per dispatch; SQ_* / SQ_WAVES in parentheses)", "",
+              "| kernel | " + " | ".join(names) + " |", "|---|" + "---:|" * len(names)]
+    for r in rows:
+        c = vals[r[0]]
+        waves = mean(c.get("SQ_WAVES", []))
+        cells = []
+        for n in names:
+            v = mean(c.get(n, []))
+            cell = f(v, 0)
+            if n.startswith("SQ_") and n != "SQ_WAVES" and waves == waves and waves and v == v:
+                cell += f" ({v / waves:,.0f})"
+            cells.append(cell)
+        lines.append(f"| `{r[0]}` | " + " | ".join(cells) + " |")
     with open(out, "w") as fh:
         fh.write("\n".join(lines) + "\n")
     print("\n".join(lines[:14]))
