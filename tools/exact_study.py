@@ -83,6 +83,39 @@ def main():
         updated[np.unique(seg[mag > 0])] = True
         rec = {"batch": b, "updates": int(upd), "update_frac": round(upd / n, 4),
                "train_s": round(sec, 3), "samples_per_s": round(n / sec)}
+        # candidate rules on window [8192, 16384) with [0, 8192) as the previous
+        # window: absolute T, the bound predicted from the previous window's
+        # row steps (kappa x 2 sum |x| R_prev, floor f), and the oracle (the
+        # window's own final bound) - candidates and not-cleared non-candidates
+        def rbound(lo, hi):
+            sl_ = slice(rp[lo], rp[hi])
+            Rw = np.zeros(H, np.float32)
+            m_ = mag[sl_] > 0
+            np.add.at(Rw, idx[sl_][m_], mag[sl_][m_])
+            return Rw
+        lo, hi = 8192, 16384
+        if n >= hi:
+            Rp, Rc = rbound(0, lo), rbound(lo, hi)
+            sl_ = slice(rp[lo], rp[hi])
+            ax = np.abs(val[sl_])
+            ok_ = idx[sl_] >= 0
+            def bsum(R):
+                return 2 * (1 + 4 * g) * np.add.reduceat(ax * np.where(ok_, R[np.maximum(idx[sl_], 0)], 0),
+                                                         rp[lo:hi] - rp[lo])
+            b_prev, b_true = bsum(Rp), bsum(Rc)
+            s_ = slack0[lo:hi]
+            rules = {}
+            for T in (0.05, 0.125, 0.25):
+                c_ = s_ <= T
+                rules[f"abs{T}"] = (int(c_.sum()), int(((~c_) & (s_ <= b_true)).sum()))
+            for kap in (1.0, 2.0, 4.0):
+                for fl in (0.02, 0.05, 0.125):
+                    c_ = s_ <= np.maximum(fl, kap * b_prev)
+                    rules[f"prev_k{kap}_f{fl}"] = (int(c_.sum()), int(((~c_) & (s_ <= b_true)).sum()))
+            c_ = s_ <= b_true
+            rules["oracle"] = (int(c_.sum()), 0)
+            rules["updates"] = int(updated[lo:hi].sum())
+            rec["rules_w8192"] = rules
         for w in wins:
             # windows of w samples from the batch start: R over the window's updates
             lo, hi = 0, min(n, w)

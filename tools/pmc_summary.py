@@ -30,7 +30,8 @@ def load(dirs: list[str]):
     vals: dict[str, dict[str, list[float]]] = defaultdict(lambda: defaultdict(list))
     dur: dict[str, list[float]] = defaultdict(list)
     for d in dirs:
-        for path in glob.glob(os.path.join(d, "*counter_collection.csv")):
+        # rocprofv3 nests its files (<dir>/<host>/<pid>_...) depending on -o
+        for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(path) as f:
                 for r in csv.DictReader(f):
                     k = _short(r["Kernel_Name"])
