@@ -1169,7 +1169,16 @@ class RowEngine {
   size_t dirty_rows() const { return dirty_.size() + removed_.size(); }
   void pack_diff(MsgpackWriter& w) const { pack_row_diff(*this, w); }
   size_t apply_diffs(const std::vector<Value>& parts, std::vector<int32_t>* changed, bool forward = false) {
-    return apply_row_diffs(*this, parts, changed, forward);
+    // the LSH signatures of the applied rows: one staged launch at the end
+    defer_writes(true);
+    try {
+      const size_t n = apply_row_diffs(*this, parts, changed, forward);
+      defer_writes(false);
+      return n;
+    } catch (...) {
+      defer_writes(false);
+      throw;
+    }
   }
   // store interface of pack_row_diff / apply_row_diffs
   std::vector<std::string> mix_ids() const {

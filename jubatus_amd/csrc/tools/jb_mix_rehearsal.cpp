@@ -27,6 +27,8 @@
 
 #include <map>
 #include <set>
+#include <unordered_map>
+#include <unordered_set>
 
 #include "jb_mix_group.hpp"
 #include "jb_msgpack.hpp"
@@ -494,9 +496,9 @@ class HostRowModel : public jb::mix::Mixable {
     rows_[id] = std::move(r);
   }
   std::mutex mu_;
-  std::map<std::string, Row> rows_;
-  std::map<std::string, uint64_t> version_;
-  std::set<std::string> dirty_, removed_;
+  std::unordered_map<std::string, Row> rows_;
+  std::unordered_map<std::string, uint64_t> version_;
+  std::unordered_set<std::string> dirty_, removed_;   // (sorted when packed)
   int32_t next_slot_ = 0;
   bool full_ = false;
   size_t last_applied_ = 0;

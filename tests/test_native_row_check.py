@@ -28,7 +28,7 @@ def test_host_converter_configs_go_to_python(tmp_path):
     base = json.load(open(os.path.join(ROOT, "config", "recommender", "euclid_lsh.json")))
     for conv_extra, why in (({"string_filter_rules": [{"key": "*", "type": "x", "suffix": "_f"}],
                               "string_filter_types": {"x": {"method": "regexp", "pattern": "a"}}},
-                             "string_filter_rules"),
+                             "regexp"),   # (the other filter methods convert natively)
                             ({"string_rules": [{"key": "/re/", "type": "str"}]}, "regex")):
         cfg = dict(base)
         cfg["converter"] = {**base["converter"], **conv_extra}

@@ -49,9 +49,11 @@ def test_unknown_methods_go_to_python(tmp_path):
     ({"method": "AROW", "converter": {"num_rules": [{"key": "/x.*/", "type": "num"}]},
       "parameter": {"regularization_weight": 1.0}}, "regex"),
     ({"method": "CW", "converter": {}, "parameter": {}}, "regularization_weight"),
+    # (a user num type shadowing a builtin name converts natively now, as in Python)
     ({"method": "PA", "converter": {"string_rules": [{"key": "*", "type": "str"}],
-                                    "num_types": {"num": {"method": "add", "value": 1}},
-                                    "num_rules": [{"key": "*", "type": "num"}]}}, "num type num"),
+                                    "string_filter_types": {"x": {"method": "regexp", "pattern": "a"}},
+                                    "string_filter_rules": [{"key": "*", "type": "x", "suffix": "_f"}]}},
+     "regexp"),
 ])
 def test_config_details(tmp_path, cfg, why):
     import json
