@@ -12,6 +12,8 @@
 //   A: lane l holds A[l & 15][k = l >> 4]     (X rows)
 //   B: lane l holds B[k = l >> 4][l & 15]     (C^T, i.e. C[l & 15][k])
 //   D: lane l, reg r -> row (l >> 4) * 4 + r, col l & 15
+#include <stdlib.h>
+
 #include "jb_device.hpp"
 
 namespace jb {
@@ -174,6 +176,121 @@ __global__ __launch_bounds__(kClBlock) void kmeanspp_kernel(const float* __restr
   }
 }
 
+// inclusive prefix sum of a double over the wave, in registers: DPP row
+// shifts within each row of 16 lanes, then the row broadcasts of lanes 15 /
+// 31 into the later rows (gfx9 DPP; a __shfl_up per step is an LDS round trip)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, ROWS, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, ROWS, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_incl_scan_d(double x) {
+  x += dpp_d<0x111, 0xF>(x);   // row_shr:1
+  x += dpp_d<0x112, 0xF>(x);   // row_shr:2
+  x += dpp_d<0x114, 0xF>(x);   // row_shr:4
+  x += dpp_d<0x118, 0xF>(x);   // row_shr:8
+  x += dpp_d<0x142, 0xA>(x);   // row_bcast:15 into rows 1, 3
+  x += dpp_d<0x143, 0xC>(x);   // row_bcast:31 into rows 2, 3
+  return x;
+}
+
+// k-means++ seeding on ONE wave (n <= 64 P points): lane l owns rows
+// [l P, l P + P) - a contiguous chunk, as cl_draw's threads - with their
+// weights and distances in registers and the points in LDS, column-major
+// (dimension j of the lane's P rows is P / 4 b128 reads). A draw is a wave
+// prefix sum of the lanes' chunk sums in double (DPP, no barrier), a ballot
+// for the lane holding u * total and that lane's walk over its chunk: the same
+// bisect_right pick as cl_draw without its 4 block barriers per draw.
+template <int P>
+__global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restrict__ Xg, int n, int d,
+                                                           const float* __restrict__ wg,
+                                                           const double* __restrict__ u, int m,
+                                                           int32_t* __restrict__ out,
+                                                           int32_t* __restrict__ status) {
+  static_assert(P % 4 == 0, "b128 column reads");
+  extern __shared__ float s_x[];                   // [d][64 P]
+  constexpr int NP = 64 * P;
+  const int lane = threadIdx.x;
+  for (int e = lane; e < NP * d; e += 64) {
+    const int j = e / NP, i = e - j * NP;
+    s_x[e] = i < n ? Xg[(int64_t)i * d + j] : 0.f;
+  }
+  const int i0 = lane * P;
+  float w[P], d2[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    w[p] = i0 + p < n ? wg[i0 + p] : 0.f;
+    d2[p] = INFINITY;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // the row of draw j over weights wt (-1: total 0)
+  auto draw = [&](const float (&wt)[P], double uj) -> int {
+    double sum = 0.0;
+#pragma unroll
+    for (int p = 0; p < P; ++p) sum += (double)wt[p];
+    const double incl = wave_incl_scan_d(sum);
+    const double total = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(incl), 63),
+                                          __builtin_amdgcn_readlane(__double2loint(incl), 63));
+    if (!(total > 0.0)) return -1;
+    const double target = uj * total;
+    double run = incl - sum;                       // before my chunk
+    const bool mine = run <= target && target < incl;
+    int r = i0 + P - 1;
+    if (mine) {
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        run += (double)wt[p];
+        if (run > target) { r = i0 + p; break; }
+      }
+    }
+    const uint64_t b = __ballot(mine);
+    if (b == 0) return n - 1;                      // u * total rounded onto the end
+    return __builtin_amdgcn_readlane(r, __ffsll((long long)b) - 1);
+  };
+  auto relax = [&](int c) {
+    float acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] = 0.f;
+#pragma unroll 2
+    for (int j = 0; j < d; ++j) {
+      const float* col = s_x + (int64_t)j * NP;
+      const float xc = col[c];
+      float v[P];
+#pragma unroll
+      for (int q = 0; q < P / 4; ++q) {
+        const float4 f = reinterpret_cast<const float4*>(col + i0)[q];
+        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const float t = v[p] - xc;
+        acc[p] = fmaf(t, t, acc[p]);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+      if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
+  };
+  int c = draw(w, u[0]);
+  if (lane == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
+  if (c < 0) return;
+  relax(c);
+  for (int j = 1; j < m; ++j) {
+    float pr[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) pr[p] = d2[p] < INFINITY ? d2[p] * w[p] : 0.f;
+    c = draw(pr, u[j]);
+    if (c < 0) {
+      if (lane == 0) { out[j] = -1; *status = 1 + j; }
+      return;
+    }
+    if (lane == 0) out[j] = c;
+    relax(c);
+  }
+}
+
 // Weighted Lloyd iterations to convergence (|C' - C| <= atol + rtol |C|, as
 // torch.allclose) or `iters`, then the final assignment. C [k, d] in/out.
 __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict__ X, int n, int d,
@@ -242,8 +359,9 @@ __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict
 // C_j, var_j) + log pi_j); nk = max(sum_i r_ij, 1e-9); C = S1 / nk;
 // var = max(S2 / nk - C^2, 1e-6); pi = nk / sum nk. LDS: C, var, S1, S2
 // [k][d], nk / logdet / log pi [k].
-__global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restrict__ Xg, int n, int d,
-                                                          const float* __restrict__ w, float* __restrict__ C,
+template <int T>
+__global__ __launch_bounds__(T) void gmm_em_kernel(const float* __restrict__ Xg, int n, int d,
+                                                          const float* __restrict__ wg, float* __restrict__ C,
                                                           float* __restrict__ var, float* __restrict__ pi,
                                                           int k, int iters, int32_t* __restrict__ assign,
                                                           bool staged, bool xlds) {
@@ -254,37 +372,114 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
   float* s2 = s1 + k * d;
   float* nk = s2 + k * d;          // [k]
   float* lc = nk + k;              // [k] log pi_j - 0.5 sum_q log(2 pi var_jq)
-  float* sR = lc + k;              // [n][k] responsibilities (staged)
+  float* spi = lc + k;             // [k] pi (staged loop)
+  float* sR = spi + k;             // [n][k] responsibilities (staged)
   float* sIV = sR + (staged ? (size_t)n * k : 0);   // [k][d] 1 / var (staged)
   float* sX = sIV + (staged ? (size_t)k * d : 0);   // [n][d] the points (xlds)
+  float* sW = sX + (xlds ? (size_t)n * d : 0);       // [n] the weights (xlds): read every iteration
   __shared__ float s_tot;
   const int t = threadIdx.x;
   // the points in LDS when they fit: every E- and M-step pass reads them
   if (xlds)
-    for (int i = t; i < n * d; i += kClBlock) sX[i] = Xg[i];
+    for (int i = t; i < n * d; i += T) sX[i] = Xg[i];
   const float* __restrict__ X = xlds ? sX : Xg;
+  if (xlds)
+    for (int i = t; i < n; i += T) sW[i] = wg[i];
+  const float* __restrict__ w = xlds ? sW : wg;
   const float kLog2Pi = 1.8378770664093453f;
-  for (int i = t; i < k * d; i += kClBlock) { sC[i] = C[i]; sV[i] = var[i]; }
-  for (int j = t; j < k; j += kClBlock) nk[j] = pi[j];   // (pi until the first M-step)
+  for (int i = t; i < k * d; i += T) { sC[i] = C[i]; sV[i] = var[i]; }
+  for (int j = t; j < k; j += T) { nk[j] = pi[j]; spi[j] = pi[j]; }   // (nk: pi until the first M-step)
   __syncthreads();
-  for (int it = 0; it < iters; ++it) {
-    for (int j = t; j < k; j += kClBlock) {
+  // staged: four barriers an iteration - (lc, 1 / var) | E-step | normalize |
+  // M-step sums (nk floored where it is summed) | C, var, pi - the reads of
+  // each phase follow the writes of the one before it
+  for (int it = 0; staged && it < iters; ++it) {
+    for (int j = t; j < k; j += T) {
+      float ld = 0.f;
+      for (int q = 0; q < d; ++q) ld += logf(6.283185307179586f * sV[j * d + q]);
+      lc[j] = logf(fmaxf(spi[j], 1e-12f)) - 0.5f * ld;
+    }
+    for (int i = t; i < k * d; i += T) sIV[i] = 1.f / sV[i];
+    __syncthreads();
+    for (int e = t; e < n * k; e += T) {
+      const int i = e / k, j = e - i * k;
+      const float* x = X + (int64_t)i * d;
+      const float* c = sC + j * d;
+      const float* iv = sIV + j * d;
+      float q2 = 0.f;
+      for (int q = 0; q < d; ++q) {
+        const float df = x[q] - c[q];
+        q2 += df * df * iv[q];
+      }
+      sR[e] = lc[j] - 0.5f * q2;
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += T) {
+      float* r = sR + (size_t)i * k;
+      float mx = -INFINITY;
+      for (int j = 0; j < k; ++j) mx = fmaxf(mx, r[j]);
+      float den = 0.f;
+      for (int j = 0; j < k; ++j) den += expf(r[j] - mx);
+      const float wi = w[i] / den;
+      for (int j = 0; j < k; ++j) r[j] = wi * expf(r[j] - mx);
+    }
+    __syncthreads();
+    {
+      const int lane = t & 63, wave = t >> 6, cols = 2 * d + 1;
+      for (int pr = wave; pr < k * cols; pr += T / 64) {
+        const int j = pr / cols, col = pr - j * cols;
+        float acc = 0.f;
+        for (int i = lane; i < n; i += 64) {
+          const float r = sR[(size_t)i * k + j];
+          if (col == 2 * d) {
+            acc += r;
+          } else {
+            const float xv = X[(int64_t)i * d + (col < d ? col : col - d)];
+            acc += col < d ? r * xv : r * xv * xv;
+          }
+        }
+        for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (lane == 0) {
+          if (col == 2 * d) nk[j] = fmaxf(acc, 1e-9f);
+          else if (col < d) s1[j * d + col] = acc;
+          else s2[j * d + col - d] = acc;
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = t; i < k * d; i += T) {
+      const float m = nk[i / d];
+      const float c = s1[i] / m;
+      sC[i] = c;
+      sV[i] = fmaxf(s2[i] / m - c * c, 1e-6f);
+    }
+    if (t < k) {
+      float tot = 0.f;
+      for (int j = 0; j < k; ++j) tot += nk[j];
+      spi[t] = nk[t] / tot;                      // pi of the next E-step
+    }
+    __syncthreads();
+  }
+  if (staged)
+    for (int j = t; j < k; j += T) nk[j] = spi[j];
+  for (int it = 0; !staged && it < iters; ++it) {
+    for (int j = t; j < k; j += T) {
       float ld = 0.f;
       for (int q = 0; q < d; ++q) ld += logf(6.283185307179586f * sV[j * d + q]);
       lc[j] = logf(fmaxf(nk[j], 1e-12f)) - 0.5f * ld;
     }
-    for (int i = t; i < k * d; i += kClBlock) { s1[i] = 0.f; s2[i] = 0.f; }
+    for (int i = t; i < k * d; i += T) { s1[i] = 0.f; s2[i] = 0.f; }
     __syncthreads();
-    for (int j = t; j < k; j += kClBlock) nk[j] = 0.f;
+    for (int j = t; j < k; j += T) nk[j] = 0.f;
     __syncthreads();
     (void)kLog2Pi;
     if (staged) {
       // E-step: one thread per (point, component) - the d-long distance
       // multiplies by 1 / var (one divide per (j, q) an iteration, not one
       // per point) - then one thread per point normalizes its k entries
-      for (int i = t; i < k * d; i += kClBlock) sIV[i] = 1.f / sV[i];
+      for (int i = t; i < k * d; i += T) sIV[i] = 1.f / sV[i];
       __syncthreads();
-      for (int e = t; e < n * k; e += kClBlock) {
+      for (int e = t; e < n * k; e += T) {
         const int i = e / k, j = e - i * k;
         const float* x = X + (int64_t)i * d;
         const float* c = sC + j * d;
@@ -297,7 +492,7 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
         sR[e] = lc[j] - 0.5f * q2;
       }
       __syncthreads();
-      for (int i = t; i < n; i += kClBlock) {
+      for (int i = t; i < n; i += T) {
         float* r = sR + (size_t)i * k;
         float mx = -INFINITY;
         for (int j = 0; j < k; ++j) mx = fmaxf(mx, r[j]);
@@ -310,7 +505,7 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
       // M-step sums: one wave per (cluster, column) pair, lanes over the
       // points, a shuffle reduction and one plain store (no LDS atomics)
       const int lane = t & 63, wave = t >> 6, cols = 2 * d + 1;
-      for (int pr = wave; pr < k * cols; pr += kClBlock / 64) {
+      for (int pr = wave; pr < k * cols; pr += T / 64) {
         const int j = pr / cols, col = pr - j * cols;
         float acc = 0.f;
         for (int i = lane; i < n; i += 64) {
@@ -330,7 +525,7 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
         }
       }
     }
-    for (int i = staged ? n : t; i < n; i += kClBlock) {
+    for (int i = staged ? n : t; i < n; i += T) {
       const float* x = X + (int64_t)i * d;
       // log-sum-exp over the clusters (k is small: two passes over d)
       float mx = -INFINITY;
@@ -368,9 +563,9 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
       }
     }
     __syncthreads();
-    for (int j = t; j < k; j += kClBlock) nk[j] = fmaxf(nk[j], 1e-9f);
+    for (int j = t; j < k; j += T) nk[j] = fmaxf(nk[j], 1e-9f);
     __syncthreads();
-    for (int i = t; i < k * d; i += kClBlock) {
+    for (int i = t; i < k * d; i += T) {
       const float m = nk[i / d];
       const float c = s1[i] / m;
       sC[i] = c;
@@ -382,21 +577,21 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
       s_tot = tot;
     }
     __syncthreads();
-    for (int j = t; j < k; j += kClBlock) nk[j] = nk[j] / s_tot;   // pi of the next E-step
+    for (int j = t; j < k; j += T) nk[j] = nk[j] / s_tot;   // pi of the next E-step
     __syncthreads();
   }
-  for (int i = t; i < k * d; i += kClBlock) { C[i] = sC[i]; var[i] = sV[i]; }
-  for (int j = t; j < k; j += kClBlock) pi[j] = nk[j];
+  for (int i = t; i < k * d; i += T) { C[i] = sC[i]; var[i] = sV[i]; }
+  for (int j = t; j < k; j += T) pi[j] = nk[j];
   if (assign == nullptr) return;
   // the most likely component of every point under the final parameters
   // (models/clustering.py _assign: argmax of the log responsibilities)
-  for (int j = t; j < k; j += kClBlock) {
+  for (int j = t; j < k; j += T) {
     float ld = 0.f;
     for (int q = 0; q < d; ++q) ld += logf(6.283185307179586f * sV[j * d + q]);
     lc[j] = logf(fmaxf(nk[j], 1e-12f)) - 0.5f * ld;
   }
   __syncthreads();
-  for (int i = t; i < n; i += kClBlock) {
+  for (int i = t; i < n; i += T) {
     const float* x = X + (int64_t)i * d;
     int best = 0;
     float bv = -INFINITY;
@@ -418,18 +613,47 @@ __global__ __launch_bounds__(kClBlock) void gmm_em_kernel(const float* __restric
 extern "C" int jb_gmm_em(const float* X, int n, int d, const float* w, float* C, float* var, float* pi, int k,
                          int iters, int32_t* assign, hipStream_t stream) {
   if (n <= 0 || k <= 0 || d <= 0) return 0;
-  size_t lds = sizeof(float) * (4 * (size_t)k * d + 2 * (size_t)k);
+  size_t lds = sizeof(float) * (4 * (size_t)k * d + 3 * (size_t)k);
   if (lds > 64 * 1024) return -2;
   // responsibilities staged in LDS when they fit: the M-step then reduces
   // per (cluster, column) instead of contending on LDS float atomics
   const size_t staged = lds + sizeof(float) * ((size_t)n * k + (size_t)k * d);   // + 1 / var
   const bool stage = staged <= 64 * 1024;
   if (stage) lds = staged;
-  const size_t withx = lds + sizeof(float) * (size_t)n * d;
+  const size_t withx = lds + sizeof(float) * (size_t)n * (d + 1);   // the points and their weights
   const bool xlds = stage && withx <= 64 * 1024;
   if (xlds) lds = withx;
-  hipLaunchKernelGGL(jb::gmm_em_kernel, dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var, pi, k,
-                     iters, assign, stage, xlds);
+  // (measured: 256 threads ran the bench's 300-point coresets in 784 us for
+  // 50 iterations, 1024 threads in 341 us - the per-thread work, not the
+  // barriers, sets the iteration's time)
+  hipLaunchKernelGGL((jb::gmm_em_kernel<jb::kClBlock>), dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var,
+                     pi, k, iters, assign, stage, xlds);
+  return (int)hipGetLastError();
+}
+
+namespace jb {
+// the first nearest column of every row of D [n][k] (strict <, as the
+// host's argmin loop and torch.argmin): the compress step's assignment
+// without copying the n x k distances to the host
+__global__ __launch_bounds__(256) void argmin_rows_kernel(const float* __restrict__ D, int64_t n, int k,
+                                                          int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* r = D + i * k;
+  int a = 0;
+  float best = r[0];
+  for (int j = 1; j < k; ++j) {
+    const float v = r[j];
+    if (v < best) { best = v; a = j; }
+  }
+  out[i] = a;
+}
+}  // namespace jb
+
+extern "C" int jb_argmin_rows(const float* D, int64_t n, int k, int32_t* out, hipStream_t stream) {
+  if (n <= 0 || k <= 0) return 0;
+  hipLaunchKernelGGL(jb::argmin_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, D, n, k,
+                     out);
   return (int)hipGetLastError();
 }
 
@@ -445,6 +669,23 @@ extern "C" int jb_kmeanspp(const float* X, int n, int d, const float* w, const d
                            float* d2, float* prob, int32_t* out, int32_t* status,
                            hipStream_t stream) {
   if (n <= 0 || m <= 0) return 0;
+  // one wave when the points fit its registers / LDS (JB_KMEANSPP_BLOCK=1: the block kernel)
+  static const bool block_only = [] {
+    const char* e = getenv("JB_KMEANSPP_BLOCK");
+    return e != nullptr && e[0] == '1';
+  }();
+  const int P = n <= 64 * 4 ? 4 : n <= 64 * 8 ? 8 : n <= 64 * 16 ? 16 : 32;
+  const size_t xb = sizeof(float) * (size_t)(64 * P) * d;   // column-major, padded to 64 P rows
+  if (!block_only && n <= 64 * 32 && xb <= 64 * 1024) {
+#define JB_KPP(P)                                                                                             \
+  hipLaunchKernelGGL((jb::kmeanspp_wave_kernel<P>), dim3(1), dim3(64), xb, stream, X, n, d, w, u, m, out, status); \
+  return (int)hipGetLastError();
+    if (n <= 64 * 4) { JB_KPP(4) }
+    if (n <= 64 * 8) { JB_KPP(8) }
+    if (n <= 64 * 16) { JB_KPP(16) }
+    JB_KPP(32)
+#undef JB_KPP
+  }
   const size_t base = sizeof(float) * 3 * (size_t)n;
   const size_t withx = base + sizeof(float) * (size_t)n * d;
   const int mode = withx <= 64 * 1024 ? 2 : (base <= 64 * 1024 ? 1 : 0);

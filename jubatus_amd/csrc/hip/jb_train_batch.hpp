@@ -68,7 +68,7 @@ struct JbTrainBatch {
   int64_t mode, merge_every, hot_waves;
   unsigned long long* stats;
   uint8_t* touched;
-  // mode kSerial: scratch of jb_serial_scratch_bytes(n) bytes (serial.hip)
+  // mode kSerial: scratch of jb_serial_scratch_bytes_lc(n, LC) bytes (serial.hip)
   void* serial_scratch;
   int64_t serial_bytes;
   // 1: W is a bf16 table (uint16 bit patterns; jb_linear_train_bf16)

@@ -884,7 +884,7 @@ __global__ void mix_apply_kernel(float* __restrict__ w, const float* __restrict_
 // 2 x u64, nullable): += samples that updated, samples with a valid label.
 // touched (device, H bytes, nullable): set to 1 for every row an update wrote.
 // mode kSerial (several streams, serial-equivalent result, serial.hip) needs
-// n_max >= the batch's sample count and scratch of jb_serial_scratch_bytes(n_max).
+// n_max >= the batch's sample count and scratch of jb_serial_scratch_bytes_lc(n_max, LC).
 extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max);
 extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                  const int32_t* labels, const int64_t* stream_ptr, int nstreams,

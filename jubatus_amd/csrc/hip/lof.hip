@@ -117,7 +117,8 @@ __global__ __launch_bounds__(64) void lof_add_kernel(
     const LofArgs a, int p, int k, int ignore_same, int32_t* __restrict__ nb_slot,
     float* __restrict__ nb_dist, float* __restrict__ kdist, uint8_t* __restrict__ ok,
     uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged,
-    int first) {
+    int first, const int32_t* __restrict__ abort_flag = nullptr) {
+  if (abort_flag != nullptr && *abort_flag != 0) return;   // an earlier add of the batch stopped it
   __shared__ int32_t cs[kLofArgMax];
   __shared__ float cd[kLofArgMax];
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
@@ -133,7 +134,9 @@ __global__ __launch_bounds__(256) void lof_mark_kernel(int64_t nrows, int k,
                                                        const int32_t* __restrict__ changed,
                                                        const int32_t* __restrict__ nchanged,
                                                        int clear_ok, uint8_t* __restrict__ ok,
-                                                       uint8_t* __restrict__ lrd_ok) {
+                                                       uint8_t* __restrict__ lrd_ok,
+                                                       const int32_t* __restrict__ abort_flag = nullptr) {
+  if (abort_flag != nullptr && *abort_flag != 0) return;
   __shared__ int32_t tab[2 * kLofMaxChanged];
   const int nch = *nchanged;
   for (int i = threadIdx.x; i < 2 * kLofMaxChanged; i += blockDim.x) tab[i] = -1;
@@ -222,7 +225,8 @@ __device__ __forceinline__ void lof_score_body(
     const int32_t* __restrict__ ts, const float* __restrict__ td, int nt, int k,
     const int32_t* __restrict__ nb_slot, const float* __restrict__ nb_dist,
     const float* __restrict__ kdist, const uint8_t* __restrict__ ok, float* __restrict__ lrd,
-    uint8_t* __restrict__ lrd_ok, int store_slot, uint32_t* __restrict__ out, int max_missing) {
+    uint8_t* __restrict__ lrd_ok, int store_slot, uint32_t* __restrict__ out, int max_missing,
+    int32_t* __restrict__ abort_flag = nullptr) {
   __shared__ int nmiss;
   if (threadIdx.x == 0) nmiss = 0;
   __syncthreads();
@@ -255,6 +259,9 @@ __device__ __forceinline__ void lof_score_body(
   sys_stores_block_done();
   if (t != 0) return;
   if (nmiss > 0) {
+    // a batch of adds stops here: the host installs the missing lists and
+    // scores this add again before the later ones run (sequential order)
+    if (abort_flag != nullptr) *abort_flag = 1;
     sys_store(out + 3, (uint32_t)(nmiss < max_missing ? nmiss : max_missing));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sys_store(out, 2u);
@@ -290,14 +297,19 @@ __global__ __launch_bounds__(64) void lof_score_kernel(
     const LofArgs a, int k, const int32_t* __restrict__ nb_slot,
     const float* __restrict__ nb_dist, const float* __restrict__ kdist,
     const uint8_t* __restrict__ ok, float* __restrict__ lrd, uint8_t* __restrict__ lrd_ok,
-    int store_slot, uint32_t* __restrict__ out, int max_missing) {
+    int store_slot, uint32_t* __restrict__ out, int max_missing,
+    int32_t* __restrict__ abort_flag = nullptr) {
+  if (abort_flag != nullptr && *abort_flag != 0) {   // skipped: an earlier add stopped the batch
+    if (threadIdx.x == 0) sys_store(out, 3u);
+    return;
+  }
   __shared__ int32_t ts[kLofMaxK];
   __shared__ float td[kLofMaxK];
   const int nt = a.n < kLofMaxK ? a.n : kLofMaxK;
   if ((int)threadIdx.x < nt) { ts[threadIdx.x] = a.s[threadIdx.x]; td[threadIdx.x] = a.d[threadIdx.x]; }
   __syncthreads();
   lof_score_body(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, store_slot, out,
-                 max_missing);
+                 max_missing, abort_flag);
 }
 
 }  // namespace jb
@@ -371,6 +383,42 @@ extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host, stream);
+}
+
+// A batch of adds in arrival order, one wait: add i's kernels (insert,
+// mark, score into out_host + i * out_stride) are enqueued behind add i - 1's
+// without a host round trip. An add whose score finds rows without a valid
+// list sets *abort_dev; every later kernel of the batch then exits (status 3)
+// and the host finishes that add (missing lists installed, scored again)
+// before it resubmits the rest - the order of the sequential adds.
+// cs / cd: [nadd][stride] candidates (ascending, p excluded), nc[i] of them.
+extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd,
+                               const int32_t* nc, int stride, int k, int ignore_same, int64_t nrows,
+                               int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok, float* lrd,
+                               uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged, uint32_t* out_host,
+                               int out_stride, int max_missing, int32_t* abort_dev, hipStream_t stream) {
+  if (nadd <= 0) return 0;
+  if (k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax) return -2;
+  hipError_t e = hipMemsetAsync(abort_dev, 0, sizeof(int32_t), stream);
+  if (e != hipSuccess) return (int)e;
+  const unsigned blocks = (unsigned)((nrows + 255) / 256);
+  for (int i = 0; i < nadd; ++i) out_host[(int64_t)i * out_stride] = 0;
+  jb::LofArgs a;
+  for (int i = 0; i < nadd; ++i) {
+    const int n = nc[i];
+    int rc = fill_args(&a, cs + (int64_t)i * stride, cd + (int64_t)i * stride, n < 0 ? 0 : n);
+    if (rc) return rc;
+    hipLaunchKernelGGL(jb::lof_add_kernel, dim3(1), dim3(64), 0, stream, a, ps[i], k, ignore_same, nb_slot,
+                       nb_dist, kdist, ok, lrd_ok, changed, nchanged, 1, (const int32_t*)abort_dev);
+    hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(blocks), dim3(256), 0, stream, nrows, k, nb_slot, changed,
+                       nchanged, 0, ok, lrd_ok, (const int32_t*)abort_dev);
+    a.n = n < k ? n : k;
+    hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist, kdist, ok,
+                       lrd, lrd_ok, ps[i], out_host + (int64_t)i * out_stride, max_missing, abort_dev);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return jb::wait_nonzero(out_host + (int64_t)(nadd - 1) * out_stride, stream);
 }
 
 // LOF of a point from its nt (<= 64) nearest (host arrays), lrd of the

@@ -68,7 +68,9 @@ constexpr int kSerialSegmentsBig = 48;   // of a batch of >= kSerialBigBatch sam
 constexpr int64_t kSerialBigBatch = 16384;
 constexpr int kDeltaSegmentsMin = 8;     // delta committer segments of a big batch
 constexpr int kDeltaSegmentsMax = 512;
-constexpr int kVerifiedSegmentsMax = 2048;  // verified committer windows of a big batch (vcommit.hip)     // a segment costs ~20 us; a sequential tail ~2 us per sample
+// verified committer windows of a big batch (vcommit.hip); a segment costs
+// ~20 us, a sequential tail ~2 us per sample
+constexpr int kVerifiedSegmentsMax = 2048;
 constexpr int kRescoreWaste = 16;        // wasted exact steps that end a segment
 constexpr int kScoreMaxBlocks = 8192;    // serial_score_kernel grid cap (grid-stride)
 // committer phase timings (tail[4..19]): shader-clock reads in the step loop
@@ -786,6 +788,14 @@ extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max) {
   return 256 + ((jb_delta_scratch_per_sample() + 4) * n + 255) / 256 * 256 + jb_vcommit_fixed_bytes();
 }
 
+// the scratch a label capacity needs: past 64 labels only the bound
+// committer runs (tail words, slack and |x|_1 per sample: 8 B a sample)
+extern "C" int64_t jb_serial_scratch_bytes_lc(int64_t n_max, int LC) {
+  const int64_t n = n_max > 0 ? n_max : 1;
+  if (LC > 64) return 256 + (8 * n + 255) / 256 * 256;
+  return jb_serial_scratch_bytes(n_max);
+}
+
 // commit.hip: the delta committer (label capacities <= 64)
 extern "C" int jb_delta_prepare(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                 const int32_t* labels, const int64_t* stream_ptr, int nstreams,
@@ -865,7 +875,7 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
                                  void* scratch, int64_t scratch_bytes, int bail_after,
                                  hipStream_t stream) {
   if (nstreams <= 0 || n_max <= 0) return 0;
-  if (scratch == nullptr || scratch_bytes < jb_serial_scratch_bytes(n_max)) return -3;
+  if (scratch == nullptr || scratch_bytes < jb_serial_scratch_bytes_lc(n_max, LC)) return -3;
   if (method >= jb::CW && S == nullptr) return -4;
   if (LC <= 64 && serial_committer() == 2) {
     // verified committer: a segment is one window (score, gather, commit,

@@ -23,6 +23,8 @@
 // Distances: metric 0 lsh (hamming / hash_num), 2 minhash (mismatch
 // fraction), 1 euclid_lsh (law of cosines on the norms). Invalid rows: +inf.
 #include <limits.h>
+
+#include <atomic>
 #include <stdlib.h>
 
 #include "jb_device.hpp"
@@ -578,6 +580,421 @@ __global__ __launch_bounds__(kWqT) void topk_wq_kernel(const TopkSrc s, int nq, 
   }
 }
 
+// Multi-query scan with the queries in scalar registers (MODE 0, W <= 2
+// signature words, k <= kMqMaxK, up to kMqMaxQ queries a launch), two launches:
+//   M1  topk_mq_sample_kernel, one block per query: the distances of a sample
+//       of the table (32 contiguous segments of 1024 rows, spread over it) into
+//       an LDS histogram - hamming distance (lsh / minhash) or the top 11 bits
+//       of the float (euclid_lsh) - and the bin where the count reaches k. The
+//       sample's rows are table rows, so k of them lie at or below that bin:
+//       its upper edge bounds the k-th distance of the whole table (exact
+//       pruning, no retry).
+//   M2  topk_mq_kernel: every wave streams its own contiguous row range from
+//       HBM once - a lane holds 8 consecutive rows of a 512-row chunk (vector
+//       loads) while the next chunk is in flight - and tests every row against
+//       every query: xor + popcount against the query's bits (SGPRs) and one
+//       compare with the query's bound. Only rows under the bound leave that
+//       loop; they go through the wave's exact selection (compaction + rank, or
+//       the register pop) into its per-query carry.
+// Every bound is a key limit "survive iff key < lim" (key: the hamming
+// distance, or the bits of the non-negative float distance): the sample's bin
+// edge, the wave's own k-th key (a wave visits its chunks in index order, so a
+// tie with its k-th loses) and the block's best k-th key + 1 over its waves
+// (an LDS atomicMin; another wave's rows may precede in index order, so a tie
+// survives). euclid_lsh prefilters on the squared distance against the limit
+// squared (with a relative margin) and computes the exact distance (load_item's
+// expression) for the rows that pass. A first chunk with more than 64 rows
+// under the limit is cut to those at or below the k-th smallest of the lanes'
+// minima (a radix select over ballots): k rows of the chunk lie at or below it.
+// Replaces topk_wq_kernel's LDS tile + waves per query for k <= kMqMaxK: that
+// kernel re-read each staged row from LDS per query and spent 10.3 K VALU per
+// wave, 481 GB/s on 10M rows x 8 queries (profiles/r4_pmc_roofline.md:9).
+// Measured dead ends (profiles/r5_topk_mq_ab.md): a grid-wide bound in one
+// global word per query (the waves' k-th, atomicMax) - every wave polls and
+// updates the same few addresses, which serialize at the memory channel, and
+// the minimum of the waves' k-ths stays far above the k-th of the rows seen.
+constexpr int kMqWaves = 8;
+constexpr int kMqT = kMqWaves * 64;
+constexpr int kMqR = 8;                        // consecutive rows per lane per chunk
+constexpr int kMqChunk = 64 * kMqR;            // 512
+constexpr int kMqMaxK = 32;
+constexpr int kMqMaxQ = 8;
+constexpr int64_t kMqMinRows = (int64_t)2 << 20;
+constexpr int kMqSampT = 1024;                 // sample: threads = rows per segment
+constexpr int kMqSampSegMax = 32;              // sample: segments (16 a round of loads in flight)
+constexpr int kMqBins = 2048;                  // euclid: float bits >> 20
+
+// counters of the scan (JB_TOPK_MQ_STATS; global atomics, slow): survivor passes, chunks, cuts, insertions
+__device__ unsigned long long g_mq_stats[4];
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// the k-th smallest of the wave's 64 keys (k <= 64), MSB-first radix select
+// over ballots; the top bits above NB are assumed equal
+template <int NB>
+__device__ __forceinline__ uint32_t wave_kth_key(uint32_t key, int k) {
+  uint32_t res = 0;
+#pragma unroll
+  for (int b = NB - 1; b >= 0; --b) {
+    const uint32_t trial = res | (1u << b);
+    if (__popcll(__ballot(key < trial)) < k) res = trial;
+  }
+  return res;
+}
+
+// the distance key of a row for one query (hamming distance, or the bits of
+// the exact euclid_lsh distance - load_item's expression)
+template <int W, bool EUC>
+__device__ __forceinline__ uint32_t mq_key(const uint64_t (&qw)[W], float qq, const uint64_t* bits, float b,
+                                           const float* lut, float* dist, float hn) {
+  int ham = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) ham += __popcll(qw[w] ^ bits[w]);
+  if (EUC) {
+    const float v = sqrtf(fmaxf(0.f, qq * qq + b * b - 2.f * qq * b * lut[ham]));
+    *dist = v;
+    return __float_as_uint(v);
+  }
+  *dist = (float)ham / hn;
+  return (uint32_t)ham;
+}
+
+template <int W, bool EUC>
+__global__ __launch_bounds__(kMqSampT) void topk_mq_sample_kernel(const TopkSrc s, int q0, int64_t n, int k,
+                                                                  int nseg, uint32_t* __restrict__ lim_out) {
+  constexpr int NB = EUC ? kMqBins : 64 * W + 1;
+  constexpr int U = 16;                            // sampled rows in flight per thread
+  __shared__ int hist[NB];
+  __shared__ float s_lut[EUC ? 64 * W + 1 : 1];
+  __shared__ int s_part[kMqSampT / 64 + 1];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int q = q0 + blockIdx.x;
+  const float hn = (float)s.hash_num;
+  for (int b = t; b < NB; b += kMqSampT) hist[b] = 0;
+  if (EUC)
+    for (int h = t; h <= s.hash_num && h <= 64 * W; h += kMqSampT) s_lut[h] = __cosf(3.14159265f * ((float)h / hn));
+  uint64_t qw[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) qw[w] = s.qbits[(int64_t)q * s.words + w];
+  const float qq = EUC ? s.qnorm[q] : 0.f;
+  __syncthreads();
+  // every thread: the minimum key of its sampled rows (one per segment);
+  // k distinct threads hold a row at or below their minimum, so the k-th
+  // smallest minimum bounds the table's k-th distance
+  const int64_t S = (int64_t)nseg * kMqSampT;
+  uint32_t mn = 0xffffffffu;
+  for (int j0 = 0; j0 < nseg; j0 += U) {
+    uint64_t bits[U][W];
+    float nrm[U];
+    uint32_t ok[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {                  // loads first, all in flight
+      const int64_t row = n <= S ? (int64_t)(j0 + u) * kMqSampT + t : (n / nseg) * (j0 + u) + t;
+      const int64_t rc = row < n ? row : n - 1;
+#pragma unroll
+      for (int w = 0; w < W; ++w) bits[u][w] = s.tbits[rc * W + w];
+      nrm[u] = EUC ? s.tnorm[rc] : 0.f;
+      ok[u] = row < n ? (uint32_t)s.valid[rc] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float d;
+      const uint32_t key = mq_key<W, EUC>(qw, qq, bits[u], nrm[u], s_lut, &d, hn);
+      mn = (ok[u] != 0 && key < mn) ? key : mn;
+    }
+  }
+  if (mn != 0xffffffffu) atomicAdd(&hist[EUC ? (int)(mn >> 20) : (int)mn], 1);
+  __syncthreads();
+  // the first bin where the running count reaches k
+  constexpr int PER = (NB + kMqSampT - 1) / kMqSampT;
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) c += t * PER + i < NB ? hist[t * PER + i] : 0;
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += x;
+  }
+  if (lane == 63) s_part[wv] = incl;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int w = 0; w < kMqSampT / 64; ++w) {
+      const int x = s_part[w];
+      s_part[w] = run;
+      run += x;
+    }
+    s_part[kMqSampT / 64] = run;
+  }
+  __syncthreads();
+  incl += s_part[wv];
+  if (t == 0 && s_part[kMqSampT / 64] < k) lim_out[q] = 0xffffffffu;   // fewer than k sampled: no bound
+  int run = incl - c;
+  if (run < k && incl >= k) {
+    int b = t * PER;
+    for (int i = 0; i < PER; ++i, ++b) {
+      run += hist[b];
+      if (run >= k) break;
+    }
+    lim_out[q] = EUC ? (uint32_t)(b + 1) << 20 : (uint32_t)(b + 1);
+  }
+}
+
+// lane j (< k) of (cd, ci) holds the wave's j-th best of one query so far;
+// inserts (v, id) when it beats the k-th (one readlane pair, a ballot for
+// its rank and a one-lane shift of the lanes behind it)
+__device__ __forceinline__ void carry_insert(float& cd, int& ci, float v, int id, int k, int lane) {
+  const float kd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cd), k - 1));
+  const int ki = __builtin_amdgcn_readlane(ci, k - 1);
+  if (!lt_pair(v, id, kd, ki)) return;             // wave-uniform
+  const int p = __popcll(__ballot(lane < k && lt_pair(cd, ci, v, id)));
+  float ud;
+  int ui;
+  if (k <= 16) {                                   // the carry sits in DPP row 0: row_shr:1
+    ud = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(cd), __float_as_int(cd), 0x111, 0xF, 0xF, false));
+    ui = __builtin_amdgcn_update_dpp(ci, ci, 0x111, 0xF, 0xF, false);
+  } else {
+    ud = __shfl_up(cd, 1, 64);
+    ui = __shfl_up(ci, 1, 64);
+  }
+  if (lane > p && lane < k) {
+    cd = ud;
+    ci = ui;
+  }
+  if (lane == p) {
+    cd = v;
+    ci = id;
+  }
+}
+
+template <int W, int NQ, bool EUC>
+__global__ __launch_bounds__(kMqT) void topk_mq_kernel(const TopkSrc s, int nq, int q0, int64_t n,
+                                                       int64_t per_block, int k,
+                                                       const uint32_t* __restrict__ lim_in, int stats,
+                                                       float* __restrict__ out_d,
+                                                       int32_t* __restrict__ out_i) {
+  static_assert(NQ <= kMqWaves, "one wave per query merges the block's carries");
+  __shared__ float s_cd[kMqWaves][NQ][kMqMaxK];      // the waves' carries, for the block merge
+  __shared__ int s_ci[kMqWaves][NQ][kMqMaxK];
+  __shared__ float s_md[kMqWaves][2][kMqMaxK];       // merge buffers
+  __shared__ int s_mi[kMqWaves][2][kMqMaxK];
+  __shared__ int s_cc[kMqWaves][NQ];
+  __shared__ uint32_t s_blk[NQ];             // the sample's limit, then min over waves of k-th key + 1
+  __shared__ float s_lut[EUC ? 64 * W + 1 : 1];
+  __shared__ uint64_t s_qb[NQ][W];
+  __shared__ float s_qn[NQ];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const float hn = (float)s.hash_num;
+  if (EUC)
+    for (int h = t; h <= s.hash_num && h <= 64 * W; h += kMqT) s_lut[h] = __cosf(3.14159265f * ((float)h / hn));
+  if (t < NQ) s_blk[t] = t < nq ? lim_in[q0 + t] : 0u;
+  if (t < NQ * W) {
+    const int q = t / W, w = t % W;
+    s_qb[q][w] = q < nq ? s.qbits[(int64_t)(q0 + q) * s.words + w] : 0ull;
+  }
+  if (t < NQ) s_qn[t] = (EUC && t < nq) ? s.qnorm[q0 + t] : 0.f;
+  __syncthreads();
+  uint64_t qb[NQ][W];
+  float qn[NQ];
+  float cd[NQ];                                      // the wave's carries (lane j < k: j-th best)
+  int ci[NQ];
+  uint32_t own[NQ];                                  // survive: key < own (a tie with the k-th loses)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) qb[q][w] = uniform64(s_qb[q][w]);
+    qn[q] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s_qn[q])));
+    cd[q] = INFINITY;
+    ci[q] = INT_MAX;
+    own[q] = 0xffffffffu;
+  }
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  const int64_t pw = ((per_block / kMqWaves) + kMqChunk - 1) / kMqChunk * kMqChunk;
+  const int64_t w0 = b0 + (int64_t)wv * pw;
+  const int64_t w1 = w0 + pw < b1 ? w0 + pw : b1;
+
+  // the next chunk in flight: raw loads only - nothing reads them before the
+  // next iteration (a value used inside this one would make the compiler wait
+  // for every load in flight, vmcnt counting in order)
+  uint64_t pb[kMqR][W];
+  float pn[kMqR];
+  uint32_t pv[kMqR];                 // valid bytes: packed (pv[0..1], whole chunks) or one per row
+  bool packed = false;
+  auto fetch = [&](int64_t base) {
+    const int64_t r0 = base + (int64_t)lane * kMqR;
+    packed = base + kMqChunk <= w1;
+    if (packed) {                    // a whole chunk: vector loads of the lane's 8 rows
+      const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(s.tbits + r0 * W);
+#pragma unroll
+      for (int j = 0; j < kMqR * W / 2; ++j) {
+        const ulonglong2 v = bp[j];
+        pb[(2 * j) / W][(2 * j) % W] = v.x;
+        pb[(2 * j + 1) / W][(2 * j + 1) % W] = v.y;
+      }
+      const uint2 vv = *reinterpret_cast<const uint2*>(s.valid + r0);
+      pv[0] = vv.x;
+      pv[1] = vv.y;
+#pragma unroll
+      for (int i = 2; i < kMqR; ++i) pv[i] = 0u;   // constants: no copy of an older load's register
+      if (EUC) {
+        const float4* np = reinterpret_cast<const float4*>(s.tnorm + r0);
+        const float4 a = np[0], b = np[1];
+        pn[0] = a.x; pn[1] = a.y; pn[2] = a.z; pn[3] = a.w;
+        pn[4] = b.x; pn[5] = b.y; pn[6] = b.z; pn[7] = b.w;
+      }
+    } else {                         // the table's last chunk: clamped rows
+#pragma unroll
+      for (int i = 0; i < kMqR; ++i) {
+        const int64_t row = r0 + i;
+        const int64_t rc = row < w1 ? row : w1 - 1;
+#pragma unroll
+        for (int w = 0; w < W; ++w) pb[i][w] = s.tbits[rc * W + w];
+        pv[i] = s.valid[rc];
+        if (EUC) pn[i] = s.tnorm[rc];
+      }
+    }
+    if (!EUC) {
+#pragma unroll
+      for (int i = 0; i < kMqR; ++i) pn[i] = 0.f;
+    }
+  };
+
+  int st_surv = 0, st_chunks = 0, st_cut = 0, st_ins = 0;
+  if (w0 < w1) fetch(w0);
+  for (int64_t base = w0; base < w1; base += kMqChunk) {
+    ++st_chunks;
+    uint64_t bb[kMqR][W];
+    float bn[kMqR];
+    uint32_t okl = 0;                                // the lane's valid rows (bit i: row i)
+#pragma unroll
+    for (int i = 0; i < kMqR; ++i) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) bb[i][w] = pb[i][w];
+      bn[i] = pn[i];
+      const uint32_t vb = packed ? (pv[i >> 2] >> (8 * (i & 3))) & 0xffu : pv[i];
+      okl |= (base + (int64_t)lane * kMqR + i < w1 && vb != 0) ? (1u << i) : 0u;
+    }
+    if (base + kMqChunk < w1) fetch(base + kMqChunk);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q >= nq) break;
+      const uint32_t blk = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&s_blk[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      const uint32_t lim = own[q] < blk ? own[q] : blk;
+      // the prefilter: xor + popcount and one compare per row
+      bool any = false;
+      if (EUC) {
+        const float f = __uint_as_float(lim);          // 0xffffffff: NaN -> no bound
+        const float t2 = f < INFINITY ? f * f * 1.0001f + 1e-30f : INFINITY;
+        const float q2 = qn[q] * qn[q], tqn = 2.f * qn[q];
+#pragma unroll
+        for (int i = 0; i < kMqR; ++i) {
+          int ham = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) ham += __popcll(qb[q][w] ^ bb[i][w]);
+          const float b = bn[i];
+          const float x = q2 + b * b - tqn * b * s_lut[ham];
+          any |= ((okl >> i) & 1u) && x <= t2;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < kMqR; ++i) {
+          int ham = 0;
+#pragma unroll
+          for (int w = 0; w < W; ++w) ham += __popcll(qb[q][w] ^ bb[i][w]);
+          any |= ((okl >> i) & 1u) && (uint32_t)ham < lim;
+        }
+      }
+      if (__ballot(any) == 0) continue;              // the common case: nothing of the chunk passes
+      // the exact keys of the chunk's rows under the limit, into the carry
+      ++st_surv;
+      uint32_t key[kMqR];
+      float d[kMqR];
+      uint32_t kmin = 0xffffffffu;
+#pragma unroll
+      for (int i = 0; i < kMqR; ++i) {
+        key[i] = mq_key<W, EUC>(qb[q], qn[q], bb[i], bn[i], s_lut, &d[i], hn);
+        if (!((okl >> i) & 1u) || !(key[i] < lim)) key[i] = 0xffffffffu;
+        kmin = key[i] < kmin ? key[i] : kmin;
+      }
+      int total = 0;
+#pragma unroll
+      for (int i = 0; i < kMqR; ++i) total += __popcll(__ballot(key[i] != 0xffffffffu));
+      if (total > 2 * k) {
+        ++st_cut;
+        // at least k rows of the chunk lie at or below the k-th smallest lane
+        // minimum (k distinct lanes): the rest cannot enter the carry
+        const uint32_t kb = EUC ? wave_kth_key<32>(kmin, k) : wave_kth_key<8>(kmin, k);
+#pragma unroll
+        for (int i = 0; i < kMqR; ++i)
+          if (key[i] > kb) key[i] = 0xffffffffu;
+      }
+#pragma unroll
+      for (int i = 0; i < kMqR; ++i) {
+        uint64_t m = __ballot(key[i] != 0xffffffffu);
+        while (m != 0) {                             // wave-uniform
+          const int l = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[i]), l));
+          carry_insert(cd[q], ci[q], v, (int)(base + (int64_t)l * kMqR + i), k, lane);
+          ++st_ins;
+        }
+      }
+      const float kd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cd[q]), k - 1));
+      if (kd < INFINITY) {
+        const uint32_t kk = EUC ? __float_as_uint(kd) : (uint32_t)(int)rintf(kd * hn);
+        own[q] = kk;
+        if (lane == 0 && kk + 1u < blk) atomicMin(&s_blk[q], kk + 1u);
+      }
+    }
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&g_mq_stats[0], (unsigned long long)st_surv);
+    atomicAdd(&g_mq_stats[1], (unsigned long long)st_chunks);
+    atomicAdd(&g_mq_stats[2], (unsigned long long)st_cut);
+    atomicAdd(&g_mq_stats[3], (unsigned long long)st_ins);
+  }
+  // the carries to LDS, then query q's wave merges the block's lists
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    if (q >= nq) break;
+    if (lane < k) {
+      s_cd[wv][q][lane] = cd[q];
+      s_ci[wv][q][lane] = ci[q];
+    }
+    const int cc = __popcll(__ballot(lane < k && ci[q] != INT_MAX));
+    if (lane == 0) s_cc[wv][q] = cc;
+  }
+  __syncthreads();
+  if (wv >= nq) return;
+  const int q = wv;
+  const float* ad = s_cd[wv][q];
+  const int* ai = s_ci[wv][q];
+  int cc = s_cc[wv][q], cur = 0;
+  for (int ow = 0; ow < kMqWaves; ++ow) {
+    if (ow == wv) continue;
+    const int oc = s_cc[ow][q];
+    if (oc == 0) continue;
+    cc = wave_merge(ad, ai, cc, s_cd[ow][q], s_ci[ow][q], oc, k, s_md[wv][cur], s_mi[wv][cur], lane);
+    wave_sync();
+    ad = s_md[wv][cur];
+    ai = s_mi[wv][cur];
+    cur ^= 1;
+  }
+  const int64_t o = ((int64_t)(q0 + q) * gridDim.x + blockIdx.x) * k;
+  for (int j = lane; j < k; j += 64) {
+    out_d[o + j] = j < cc ? ad[j] : INFINITY;
+    out_i[o + j] = j < cc ? ai[j] : INT_MAX;
+  }
+}
+
 // Small k (<= KL): every thread keeps its own sorted top-KL of the items it
 // reads (strided across the block's range) in registers and the block merges
 // once at the end (per-wave pops, then wave 0). Used for the final merge of
@@ -895,9 +1312,87 @@ inline int scan_waves(int k, int nq, int64_t nrows) {
 // register lists (measured ~3 us faster than the tile kernel's rank merge,
 // profiles/r02_lsh_merge_ab.jsonl)
 
+// JB_TOPK_MQ=0 turns the register multi-query scan off (A/B runs)
+inline bool mq_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("JB_TOPK_MQ");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
+inline int mq_stats_on() {
+  static const int on = [] {
+    const char* e = getenv("JB_TOPK_MQ_STATS");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
+  return on;
+}
+
+// sample size: one round of loads for few queries (its latency is the
+// whole cost), two for many (each survivor of the looser bound costs every
+// query's wave a pass; measured profiles/r5_topk_mq_ab.md)
+inline int mq_sample_segments(int nq) { return nq >= 4 ? kMqSampSegMax : kMqSampSegMax / 2; }
+
+template <int W, int NQ>
+inline void launch_mq_nq(const TopkSrc& s, int blocks, int nq, int q0, int64_t nrows, int64_t per_block, int k,
+                         uint32_t* lim, float* out_d, int32_t* out_i, hipStream_t stream) {
+  if (s.metric == 1) {
+    hipLaunchKernelGGL((topk_mq_sample_kernel<W, true>), dim3(nq), dim3(kMqSampT), 0, stream, s, q0, nrows, k,
+                       mq_sample_segments(nq), lim);
+    hipLaunchKernelGGL((topk_mq_kernel<W, NQ, true>), dim3(blocks), dim3(kMqT), 0, stream, s, nq, q0, nrows,
+                       per_block, k, lim, mq_stats_on(), out_d, out_i);
+  } else {
+    hipLaunchKernelGGL((topk_mq_sample_kernel<W, false>), dim3(nq), dim3(kMqSampT), 0, stream, s, q0, nrows, k,
+                       mq_sample_segments(nq), lim);
+    hipLaunchKernelGGL((topk_mq_kernel<W, NQ, false>), dim3(blocks), dim3(kMqT), 0, stream, s, nq, q0, nrows,
+                       per_block, k, lim, mq_stats_on(), out_d, out_i);
+  }
+}
+
+template <int W>
+inline void launch_mq_w(const TopkSrc& s, int blocks, int nq, int q0, int64_t nrows, int64_t per_block, int k,
+                        uint32_t* lim, float* out_d, int32_t* out_i, hipStream_t stream) {
+  if (nq <= 1) launch_mq_nq<W, 1>(s, blocks, nq, q0, nrows, per_block, k, lim, out_d, out_i, stream);
+  else if (nq <= 2) launch_mq_nq<W, 2>(s, blocks, nq, q0, nrows, per_block, k, lim, out_d, out_i, stream);
+  else if (nq <= 4) launch_mq_nq<W, 4>(s, blocks, nq, q0, nrows, per_block, k, lim, out_d, out_i, stream);
+  else launch_mq_nq<W, 8>(s, blocks, nq, q0, nrows, per_block, k, lim, out_d, out_i, stream);
+}
+
+// Launches the scan stage; returns the number of blocks (= candidate lists
+// per query, each of k entries, at out + (q * blocks + b) * k), <= blocks.
 template <int MODE>
-inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
-                        int k, float* out_d, int32_t* out_i, hipStream_t stream) {
+inline int launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
+                       int k, float* out_d, int32_t* out_i, hipStream_t stream) {
+  // (measured against topk_wq / topk_kernel, profiles/r5_topk_mq_ab.md: ahead
+  // up to 8 queries for lsh / minhash, up to 4 for euclid_lsh, whose
+  // prefilter costs a table lookup and a few FMAs per row and query)
+  // Tables under ~2M rows keep the tile kernels: the sample launch and the
+  // block merge cost more there than the scan saves (measured through the
+  // servers: 1M-row euclid_lsh similar_row 53 -> 63 us p50, 100 K-row LOF
+  // calc_score 54 -> 74 us)
+  if (MODE == 0 && mq_enabled() && blocks > 1 && nrows >= kMqMinRows && k <= kMqMaxK &&
+      (s.words == 1 || s.words == 2) && s.hash_num <= 64 * s.words && nq <= (s.metric == 1 ? 4 : kMqMaxQ)) {
+    // the sampled bound, then the table streamed once per launch of up to
+    // kMqMaxQ queries (topk_mq_kernel); at least 4 chunks a wave so its carry
+    // prunes, fewer blocks than the caller sized the candidate scratch for
+    // (the sample's limits live past the candidates, at out_i + nq mb k)
+    constexpr int64_t kPer = (int64_t)kMqWaves * kMqChunk;
+    int64_t mb = (nrows + 4 * kPer - 1) / (4 * kPer);
+    mb = mb < 1 ? 1 : (mb > blocks - 1 ? blocks - 1 : mb);
+    int64_t pb = (nrows + mb - 1) / mb;
+    pb = (pb + kPer - 1) / kPer * kPer;
+    mb = (nrows + pb - 1) / pb;
+    uint32_t* lim = reinterpret_cast<uint32_t*>(out_i + (int64_t)nq * mb * k);
+    for (int q0 = 0; q0 < nq; q0 += kMqMaxQ) {
+      const int nqi = nq - q0 < kMqMaxQ ? nq - q0 : kMqMaxQ;
+      if (s.words == 1)
+        launch_mq_w<1>(s, (int)mb, nqi, q0, nrows, pb, k, lim, out_d, out_i, stream);
+      else
+        launch_mq_w<2>(s, (int)mb, nqi, q0, nrows, pb, k, lim, out_d, out_i, stream);
+    }
+    return (int)mb;
+  }
   if (MODE == 0 && nq > 1 && nq <= kWqWaves && s.words <= 2 && s.hash_num <= 64 * s.words) {
     // several queries per table pass, one wave per query (topk_wq_kernel)
     if (s.words == 1)
@@ -906,7 +1401,7 @@ inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int
     else
       hipLaunchKernelGGL((topk_wq_kernel<2>), dim3(blocks), dim3(kWqT), 0, stream, s, nq, nrows,
                          per_block, k, out_d, out_i);
-    return;
+    return blocks;
   }
   if (scan_waves(k, nq, nrows) == 16)
     hipLaunchKernelGGL((topk_kernel<MODE, 16>), dim3(blocks, nq), dim3(16 * 64), 0, stream, s,
@@ -914,6 +1409,7 @@ inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int
   else
     hipLaunchKernelGGL((topk_kernel<MODE, 4>), dim3(blocks, nq), dim3(4 * 64), 0, stream, s,
                        nrows, per_block, k, out_d, out_i, nullptr, 0u);
+  return blocks;
 }
 
 // Final merge of the scan's per-block lists (each sorted, k entries) for
@@ -924,7 +1420,8 @@ inline void launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int
 // topk_lists_kernel cost ~20 us here (16 waves of VALU pops on a handful of
 // real candidates); this is k rounds of a dozen register steps.
 constexpr int kMergeLists = 512;
-__global__ __launch_bounds__(64) void topk_merge_sorted_kernel(const float* __restrict__ cd,
+constexpr int kMergeStageT = 256;   // threads staging the lists into LDS (wave 0 merges)
+__global__ __launch_bounds__(kMergeStageT) void topk_merge_sorted_kernel(const float* __restrict__ cd,
                                                                const int32_t* __restrict__ ci, int nb, int k,
                                                                float* __restrict__ out_d,
                                                                int32_t* __restrict__ out_i,
@@ -939,8 +1436,9 @@ __global__ __launch_bounds__(64) void topk_merge_sorted_kernel(const float* __re
   const int n = nb * k;
   const float* src_d = cd + (int64_t)q * n;
   const int32_t* src_i = ci + (int64_t)q * n;
-  for (int e = lane; e < n; e += 64) { s_d[e] = src_d[e]; s_i[e] = src_i[e]; }
+  for (int e = threadIdx.x; e < n; e += kMergeStageT) { s_d[e] = src_d[e]; s_i[e] = src_i[e]; }
   __syncthreads();
+  if (threadIdx.x >= 64) return;                  // the merge is one wave's
   int pos[L];
   float hd[L];
   int hi[L];
@@ -972,11 +1470,11 @@ __global__ __launch_bounds__(64) void topk_merge_sorted_kernel(const float* __re
       }
     }
   }
-  __syncthreads();
+  wave_sync();                          // (waves 1..3 have left: wave-level ordering only)
   const int64_t o = (int64_t)q * k;
   if (done != nullptr) {
     for (int j = lane; j < k; j += 64) { sys_store(out_d + o + j, s_rd[j]); sys_store(out_i + o + j, s_ri[j]); }
-    sys_stores_block_done();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's stores acknowledged, then the flag
     if (lane == 0) sys_store(const_cast<uint32_t*>(done) + q, seq);
     return;
   }
@@ -989,7 +1487,7 @@ inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out
                          int32_t* out_i, volatile uint32_t* done, uint32_t seq,
                          hipStream_t stream) {
   if (k <= kListK && nc % k == 0 && nc / k <= kMergeLists) {
-    hipLaunchKernelGGL(topk_merge_sorted_kernel, dim3(nq), dim3(64), (size_t)nc * 8, stream, m.src_d, m.src_i,
+    hipLaunchKernelGGL(topk_merge_sorted_kernel, dim3(nq), dim3(kMergeStageT), (size_t)nc * 8, stream, m.src_d, m.src_i,
                        (int)(nc / k), k, out_d, out_i, done, seq);
   } else if (k <= kListK) {
     hipLaunchKernelGGL((topk_lists_kernel<2, kListK, 16>), dim3(1, nq), dim3(16 * 64), 0, stream,
@@ -1039,13 +1537,11 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
-  if (mode == 0)
-    jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
-  else
-    jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+  const int used = mode == 0 ? jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream)
+                              : jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const int64_t nc = (int64_t)blocks * k;   // candidates per query
+  const int64_t nc = (int64_t)used * k;   // candidates per query
   jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
   jb::launch_merge(m, nq, nc, k, out_d, out_i, nullptr, 0u, stream);
   return (int)hipGetLastError();
@@ -1064,10 +1560,10 @@ static int topk_to_host_tile(const uint64_t* qbits, const float* qnorm, int nq,
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
-  jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+  const int used = jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  const int64_t nc = (int64_t)blocks * k;
+  const int64_t nc = (int64_t)used * k;
   jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
   jb::launch_merge(m, nq, nc, k, out_d_host, out_i_host, (volatile uint32_t*)done_host, seq,
                    stream);
@@ -1944,10 +2440,10 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
     const int blocks = jb_topk_blocks(nrows, k);
     const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
     const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
-    jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+    const int used = jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
-    const int64_t nc = (int64_t)blocks * k;
+    const int64_t nc = (int64_t)used * k;
     jb::TopkSrc m{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, scratch_d, scratch_i, 0};
     jb::launch_merge(m, nq, nc, k, out_d_host, out_i_host, (volatile uint32_t*)done_host, seq,
                      stream);
@@ -2019,4 +2515,13 @@ extern "C" int jb_topk_scores_direct(const float* src_d, int flip, int nq, int64
                                      hipStream_t stream) {
   return jb_topk_scores_direct_path(src_d, flip, nq, nrows, k, scratch_d, scratch_i, out_d_host,
                                     out_i_host, done_host, -1, stream);
+}
+
+// the scan counters since the last call (JB_TOPK_MQ_STATS=1; synchronizes the device)
+extern "C" int jb_topk_mq_stats(unsigned long long* out4) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(out4, HIP_SYMBOL(jb::g_mq_stats), 4 * sizeof(unsigned long long));
+  unsigned long long z[4] = {0, 0, 0, 0};
+  if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(jb::g_mq_stats), z, sizeof(z));
+  return (int)e;
 }

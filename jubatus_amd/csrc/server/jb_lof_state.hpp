@@ -27,6 +27,10 @@ int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int k, int ign
                int64_t nrows, int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok,
                float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
                uint32_t* out_host, int max_missing, hipStream_t stream);
+int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd, const int32_t* nc,
+                    int stride, int k, int ignore_same, int64_t nrows, int32_t* nb_slot, float* nb_dist,
+                    float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
+                    uint32_t* out_host, int out_stride, int max_missing, int32_t* abort_dev, hipStream_t stream);
 int jb_lof_score(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
                  const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd,
                  uint8_t* lrd_ok, int store_slot, uint32_t* out_host, int max_missing,
@@ -46,6 +50,7 @@ constexpr int kLofMaxK = 64;          // lof.hip kLofMaxK
 constexpr int kLofMaxChanged = 1024;  // kLofMaxChanged
 constexpr int kLofMaxMissing = 1024;
 constexpr int kLofArgMax = 128;       // candidates in the kernel arguments
+constexpr int kLofBatchMax = 64;      // adds of one jb_lof_add_many
 
 class LofState {
  public:
@@ -54,14 +59,18 @@ class LofState {
     if (!out_) throw std::runtime_error("hipHostMalloc failed");
     changed_.get(kLofMaxChanged);
     nchanged_.get(1);
+    abort_.get(1);
+    out_many_ = (uint32_t*)jb_host_alloc(4 * (size_t)kOutStride * kLofBatchMax);
+    if (!out_many_) throw std::runtime_error("hipHostMalloc failed");
   }
 
   ~LofState() {
     for (void* q : {(void*)nb_slot_.p, (void*)nb_dist_.p, (void*)kdist_.p, (void*)lrd_.p, (void*)ok_.p,
                     (void*)lrd_ok_.p, (void*)changed_.p, (void*)nchanged_.p, (void*)up_[0].p, (void*)up_[1].p,
-                    (void*)up_[2].p})
+                    (void*)up_[2].p, (void*)abort_.p})
       if (q) (void)hipFree(q);
     if (out_) jb_host_free(out_);
+    if (out_many_) jb_host_free(out_many_);
   }
   LofState(const LofState&) = delete;
   LofState& operator=(const LofState&) = delete;
@@ -90,6 +99,53 @@ class LofState {
                               out_, kLofMaxMissing, stream_);
     if (rc != 0) throw std::runtime_error("lof add failed: " + std::to_string(rc));
     return result(score, missing);
+  }
+
+  // a batch of adds in order with one wait (<= kLofBatchMax, candidates <= kLofArgMax each):
+  // -> the number completed (their scores in *scores); when short of all,
+  // add [return] stopped on rows without a valid list (*missing) - its
+  // insert is applied, its score is not (the caller scores it, as after a
+  // false add()), and the later adds did not run
+  size_t add_many(const std::vector<int32_t>& ps, const std::vector<std::vector<int32_t>>& cs,
+                  const std::vector<std::vector<float>>& cd, std::vector<float>* scores,
+                  std::vector<int32_t>* missing) {
+    const size_t n = ps.size();
+    if (n == 0) return 0;
+    if (n > (size_t)kLofBatchMax) throw std::runtime_error("lof add_many: batch too large");
+    int stride = 1;
+    for (const auto& c : cs) stride = std::max(stride, (int)c.size());
+    if (stride > kLofArgMax) throw std::runtime_error("lof add_many: too many candidates");
+    std::vector<int32_t> fcs(n * (size_t)stride, -1), nc(n);
+    std::vector<float> fcd(n * (size_t)stride, INFINITY);
+    for (size_t i = 0; i < n; ++i) {
+      nc[i] = (int32_t)cs[i].size();
+      std::copy(cs[i].begin(), cs[i].end(), fcs.begin() + (int64_t)i * stride);
+      std::copy(cd[i].begin(), cd[i].end(), fcd.begin() + (int64_t)i * stride);
+    }
+    const int rc = jb_lof_add_many((int)n, ps.data(), fcs.data(), fcd.data(), nc.data(), stride, k_, ignore_ ? 1 : 0,
+                                   cap_, nb_slot_.p, nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p,
+                                   nchanged_.p, out_many_, kOutStride, kLofMaxMissing, abort_.p, stream_);
+    if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
+    scores->clear();
+    for (size_t i = 0; i < n; ++i) {
+      const uint32_t* o = out_many_ + i * kOutStride;
+      const uint32_t st = ((volatile const uint32_t*)o)[0];
+      if (st == 1) {
+        float sc;
+        memcpy(&sc, &o[1], 4);
+        scores->push_back(sc);
+        continue;
+      }
+      if (st != 2) throw std::runtime_error("lof add_many: kernel did not complete");
+      missing->clear();
+      const uint32_t nm = std::min<uint32_t>(o[3], kLofMaxMissing);
+      for (uint32_t j = 0; j < nm; ++j) {
+        const int32_t s = (int32_t)o[4 + j];
+        if (std::find(missing->begin(), missing->end(), s) == missing->end()) missing->push_back(s);
+      }
+      return i;
+    }
+    return n;
   }
 
   bool score(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store, float* sc,
@@ -199,7 +255,10 @@ class LofState {
   DevBuf<uint8_t> ok_, lrd_ok_;
   DevBuf<int32_t> changed_, nchanged_;
   DevBuf<int32_t> up_[3];
+  DevBuf<int32_t> abort_;
   uint32_t* out_ = nullptr;
+  static constexpr int kOutStride = 4 + kLofMaxMissing;
+  uint32_t* out_many_ = nullptr;   // [kLofBatchMax][kOutStride] pinned
   int32_t nh_ = 0;
 };
 

@@ -518,6 +518,43 @@ class Model : public jb::mix::Mixable {
     const std::string id = std::to_string(next_id_++);
     return {id, (double)insert(id, std::move(d))};
   }
+  // A batch of anomaly adds (Server::add_batch; anomaly_serv.cpp:157-176 per
+  // add): the rows are set with one staged signature launch, their
+  // neighbours come from multi-query passes over the table holding the whole
+  // batch (k = rnn + batch, then each add drops itself and the rows added
+  // after it - exactly its sequential candidate list), and the LOF inserts
+  // run as one enqueue (LofState::add_many). Ids, candidates and scores are
+  // those of the adds one by one, in arrival order.
+  struct AddReq {
+    const Value* dv = nullptr;
+    std::string id;
+    double score = 0;
+    std::exception_ptr err;
+  };
+  void add_many(std::vector<AddReq>& rs) {
+    std::vector<Datum> ds(rs.size());
+    for (size_t i = 0; i < rs.size(); ++i) {
+      try {
+        jb::row::parse_datum(*rs[i].dv, &ds[i]);
+      } catch (...) {
+        rs[i].err = std::current_exception();
+      }
+    }
+    std::unique_lock<std::shared_mutex> g(mu_);
+    const size_t chunk = (size_t)std::max(1, std::min(jb::row::kLofBatchMax, 128 - cfg_.rnn));
+    std::vector<size_t> todo;
+    for (size_t i = 0; i < rs.size(); ++i)
+      if (!rs[i].err) todo.push_back(i);
+    for (size_t c0 = 0; c0 < todo.size(); c0 += chunk) {
+      const size_t c1 = std::min(todo.size(), c0 + chunk);
+      try {
+        add_chunk(rs, ds, std::vector<size_t>(todo.begin() + c0, todo.begin() + c1));
+      } catch (...) {
+        for (size_t j = c0; j < c1; ++j)
+          if (!rs[todo[j]].err && rs[todo[j]].id.empty()) rs[todo[j]].err = std::current_exception();
+      }
+    }
+  }
   // update merges into the stored datum, overwrite replaces it
   double update(const std::string& id, const Value& dv, bool merge) {
     Datum nd;
@@ -1014,28 +1051,101 @@ class Model : public jb::mix::Mixable {
     return *lof_;
   }
 
-  // row_engine.query_slot_lists: each row's nearest (itself included), live rows
-  std::vector<std::vector<std::pair<int32_t, float>>> slot_lists(const std::vector<int32_t>& slots, int k) {
+  // row_engine.query_slot_lists: each row's nearest (itself included), live
+  // rows; absent: rows a batch of adds set but has not added yet
+  std::vector<std::vector<std::pair<int32_t, float>>> slot_lists(const std::vector<int32_t>& slots, int k,
+                                                                 const std::unordered_set<int32_t>* absent = nullptr) {
     std::vector<std::vector<std::pair<int32_t, float>>> out;
+    const int kq = k + (absent ? (int)absent->size() : 0);
     for (int32_t s : slots) {
       std::vector<std::pair<int32_t, float>> l;
-      for (const Hit& h : eng_->query_slot(s, k))
-        if (live(h.slot)) l.push_back({h.slot, h.dist});
+      for (const Hit& h : eng_->query_slot(s, std::min(kq, 128))) {
+        if (!live(h.slot) || (absent && absent->count(h.slot))) continue;
+        if ((int)l.size() >= k) break;
+        l.push_back({h.slot, h.dist});
+      }
       out.push_back(std::move(l));
     }
     return out;
   }
 
   // LOF._score_from: refresh missing neighbour lists until the score resolves
-  float score_from(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store) {
+  float score_from(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store,
+                   const std::unordered_set<int32_t>* absent = nullptr) {
     jb::row::LofState& st = state();
     std::vector<int32_t> missing;
     for (int it = 0; it < 1 + 2 * cfg_.k; ++it) {
       float sc;
       if (st.score(ts, td, store, &sc, &missing)) return sc;
-      st.set_lists(missing, slot_lists(missing, cfg_.k + 1));
+      st.set_lists(missing, slot_lists(missing, cfg_.k + 1, absent));
     }
     throw std::runtime_error("lof: neighbour lists did not converge");
+  }
+
+  // one chunk of add_many (mu_ held exclusively; idx: positions in rs)
+  void add_chunk(std::vector<AddReq>& rs, std::vector<Datum>& ds, const std::vector<size_t>& idx) {
+    const size_t B = idx.size();
+    // fresh ids only (an id a client set with update / overwrite takes the sequential path)
+    bool fresh = true;
+    for (size_t j = 0; j < B && fresh; ++j) fresh = eng_->slot(std::to_string(next_id_ + (int64_t)j)) < 0;
+    if (!fresh || B == 1 || eng_->lru()) {
+      for (size_t i : idx) {
+        ++update_count;
+        rs[i].id = std::to_string(next_id_++);
+        rs[i].score = (double)insert(rs[i].id, std::move(ds[i]));
+      }
+      return;
+    }
+    std::vector<int32_t> slots(B);
+    eng_->defer_writes(true);
+    for (size_t j = 0; j < B; ++j) {
+      const size_t i = idx[j];
+      ++update_count;
+      rs[i].id = std::to_string(next_id_++);
+      eng_->set(rs[i].id, std::move(ds[i]));
+      slots[j] = eng_->slot(rs[i].id);
+    }
+    eng_->defer_writes(false);
+    std::unordered_map<int32_t, size_t> order;
+    for (size_t j = 0; j < B; ++j) order[slots[j]] = j;
+    std::vector<const std::vector<int32_t>*> qi;
+    std::vector<const std::vector<float>*> qv;
+    for (int32_t s : slots) {
+      qi.push_back(&eng_->at(s).idx);
+      qv.push_back(&eng_->at(s).val);
+    }
+    const auto hits = eng_->query_fv_many(qi, qv, cfg_.rnn + (int)B);
+    std::vector<std::vector<int32_t>> cs(B);
+    std::vector<std::vector<float>> cd(B);
+    for (size_t j = 0; j < B; ++j)
+      for (const Hit& h : hits[j]) {
+        if (!live(h.slot) || h.slot == slots[j]) continue;
+        auto it = order.find(h.slot);
+        if (it != order.end() && it->second > j) continue;   // added after j
+        if ((int)cs[j].size() >= cfg_.rnn) break;
+        cs[j].push_back(h.slot);
+        cd[j].push_back(h.dist);
+      }
+    jb::row::LofState& st = state();
+    size_t j = 0;
+    while (j < B) {
+      std::vector<int32_t> ps(slots.begin() + j, slots.end());
+      std::vector<std::vector<int32_t>> c(cs.begin() + j, cs.end());
+      std::vector<std::vector<float>> d(cd.begin() + j, cd.end());
+      std::vector<float> sc;
+      std::vector<int32_t> missing;
+      const size_t m = st.add_many(ps, c, d, &sc, &missing);
+      for (size_t q = 0; q < m; ++q) rs[idx[j + q]].score = (double)sc[q];
+      j += m;
+      if (j < B) {   // add j stopped on lists to install: finish it as insert() does
+        std::unordered_set<int32_t> absent(slots.begin() + j + 1, slots.end());
+        const size_t kk = std::min<size_t>(cs[j].size(), (size_t)cfg_.k);
+        rs[idx[j]].score = (double)score_from(std::vector<int32_t>(cs[j].begin(), cs[j].begin() + kk),
+                                              std::vector<float>(cd[j].begin(), cd[j].begin() + kk), slots[j],
+                                              &absent);
+        ++j;
+      }
+    }
   }
 
   // LOF._insert
@@ -1124,6 +1234,9 @@ class Server {
       qm.push_back("neighbor_row_from_id");
     }
     if (kind_ == Kind::kAnomaly) qm = {"calc_score"};
+    // standalone anomaly adds: one LOF pass per queued batch (Model::add_many);
+    // in a cluster an add goes to its CHT owners one by one (add_zk)
+    if (kind_ == Kind::kAnomaly && !node_) qm.push_back("add");
     // writes of the similarity engines: one exclusive section and one device
     // launch per batch of queued writes (Model::write_many)
     if (kind_ == Kind::kRecommender) {
@@ -1134,6 +1247,7 @@ class Server {
     if (!qm.empty())
       rpc_->set_batch(qm, [this](const std::string& m, std::vector<jb::RpcRequest>& rs) {
         if (m == "update_row" || m == "set_row" || m == "clear_row") return write_batch(m, rs);
+        if (m == "add") return add_batch(rs);
         return query_batch(m, rs);
       }, 1024);
     int port;
@@ -1221,6 +1335,54 @@ class Server {
         if (ws[j].err) std::rethrow_exception(ws[j].err);
         MsgpackWriter w;
         w.boolean(ws[j].result != 0);
+        out[at[j]] = jb::val::response_ok(r.msgid, w.out);
+      } catch (const ArgError&) {
+        out[at[j]] = jb::val::response_code(r.msgid, kArgumentError);
+      } catch (const std::exception& e) {
+        out[at[j]] = jb::val::response_msg(r.msgid, e.what());
+      }
+    }
+    return out;
+  }
+
+  // one batch of anomaly adds (see run()): malformed ones answer as
+  // dispatch() would, the rest run as one Model::add_many in arrival order
+  std::vector<std::string> add_batch(std::vector<jb::RpcRequest>& rs) {
+    std::vector<std::string> out(rs.size());
+    std::vector<Value> args(rs.size());
+    std::vector<Model::AddReq> reqs;
+    std::vector<size_t> at;
+    for (size_t i = 0; i < rs.size(); ++i) {
+      const jb::RpcRequest& r = rs[i];
+      bool ok = true;
+      try {
+        args[i] = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
+      } catch (const std::exception&) {
+        ok = false;
+      }
+      const Value& a = args[i];
+      ok = ok && a.kind == Value::ARR && a.a.size() == 2 && a.a[0].is_str() && a.a[1].kind == Value::ARR;
+      if (!ok) {
+        out[i] = r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
+        continue;
+      }
+      Model::AddReq q;
+      q.dv = &a.a[1];
+      reqs.push_back(q);
+      at.push_back(i);
+    }
+    if (reqs.empty()) return out;
+    if (mixer_) mixer_->updated(reqs.size());   // event_model_updated, once per add
+    model_->add_many(reqs);
+    for (size_t j = 0; j < reqs.size(); ++j) {
+      const jb::RpcRequest& r = rs[at[j]];
+      if (r.notify) continue;
+      try {
+        if (reqs[j].err) std::rethrow_exception(reqs[j].err);
+        MsgpackWriter w;
+        w.arr(2);
+        w.raw(reqs[j].id);
+        w.dbl(reqs[j].score);
         out[at[j]] = jb::val::response_ok(r.msgid, w.out);
       } catch (const ArgError&) {
         out[at[j]] = jb::val::response_code(r.msgid, kArgumentError);

@@ -65,7 +65,7 @@ extern "C" int jb_linear_train(const int64_t* row_ptr, const int32_t* fidx, cons
                                float* hot_rep, int merge_every, int hot_waves,
                                unsigned long long* stats, uint8_t* touched, int64_t n_max,
                                void* scratch, int64_t scratch_bytes, hipStream_t stream);
-extern "C" int64_t jb_serial_scratch_bytes(int64_t n_max);
+extern "C" int64_t jb_serial_scratch_bytes_lc(int64_t n_max, int LC);
 extern "C" int jb_serial_scratch_forget(void* scratch);
 extern "C" int jb_linear_classify(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                                   int n_samples, const float* W, int LC, float* out,
@@ -637,7 +637,8 @@ class Classifier : public jb::mix::Mixable {
           if (jb_mix_pack_bf16(snap_.p, n, Lc, has_s, wb, sb, mixs_) != 0) throw std::runtime_error("jb_mix_pack_bf16");
           pl.allreduce_sum_bf16(wb, nl, grp.deadline());
           if (has_s) pl.allreduce_sum(sb, nl, grp.deadline());
-          if (jb_mix_unpack_bf16(wb, sb, n, Lc, has_s, red_.p, mixs_) != 0) throw std::runtime_error("jb_mix_unpack_bf16");
+          if (jb_mix_unpack_bf16(wb, sb, n, Lc, has_s, red_.p, mixs_) != 0)
+            throw std::runtime_error("jb_mix_unpack_bf16");
           bytes += nl * 2 + (has_s ? nl * 4 : 0);
         } else {
           pl.allreduce_sum(red_.p, elems, grp.deadline());
@@ -1149,7 +1150,7 @@ class Classifier : public jb::mix::Mixable {
     a.C = C_;
     a.mode = R > 1 ? update_mode_ : kUpdateExact;
     if (a.mode == kUpdateSerial) {
-      const int64_t sb = jb_serial_scratch_bytes(std::max<int64_t>(n, 1));
+      const int64_t sb = jb_serial_scratch_bytes_lc(std::max<int64_t>(n, 1), LC_);
       a.serial_scratch = s.serial.get((size_t)sb);
       a.serial_bytes = sb;
       if (a.serial_scratch != s.serial_seen) {     // a new buffer: no inherited segment history

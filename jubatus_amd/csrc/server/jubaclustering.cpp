@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <numeric>
@@ -36,6 +37,7 @@
 #include "jb_pyrandom.hpp"
 #include "jb_wide_rules.hpp"
 
+extern "C" int jb_argmin_rows(const float* D, int64_t n, int k, int32_t* out, hipStream_t stream);
 extern "C" int jb_sqdist_mfma(const float* X, int64_t n, const float* C, int k, int d, const float* xn2,
                               const float* cn2, float* out, hipStream_t stream);
 extern "C" int jb_kmeanspp(const float* X, int n, int d, const float* w, const double* u, int m, float* d2,
@@ -443,6 +445,36 @@ class Clustering : public HostEngine {
     return out;
   }
 
+  // nearest row of C [m][D] for every row of X (the sqdist values and the
+  // first-minimum rule of sqdist + argmin), computed and reduced on the
+  // device: n indices come back instead of n x m distances. x_dev: X is in
+  // dX_ already (the k-means++ call just uploaded it)
+  std::vector<int32_t> nearest(const std::vector<float>& X, size_t n, const std::vector<float>& C, size_t m,
+                               size_t D, bool x_dev) {
+    std::vector<float> xn(n, 0.f), cn(m, 0.f);
+    for (size_t i = 0; i < n; ++i)
+      for (size_t q = 0; q < D; ++q) xn[i] += X[i * D + q] * X[i * D + q];
+    for (size_t j = 0; j < m; ++j)
+      for (size_t q = 0; q < D; ++q) cn[j] += C[j * D + q] * C[j * D + q];
+    float* dx = dX_.get(n * D);
+    float* dc = dC_.get(m * D);
+    float* dxn = dXn_.get(n);
+    float* dcn = dCn_.get(m);
+    float* dout = dOut_.get(n * m);
+    int32_t* da = dA_.get(n);
+    if (!x_dev) h2d(dx, X.data(), 4 * n * D);
+    h2d(dc, C.data(), 4 * m * D);
+    h2d(dxn, xn.data(), 4 * n);
+    h2d(dcn, cn.data(), 4 * m);
+    if (jb_sqdist_mfma(dx, (int64_t)n, dc, (int)m, (int)D, dxn, dcn, dout, st_) != 0 ||
+        jb_argmin_rows(dout, (int64_t)n, (int)m, da, st_) != 0)
+      throw std::runtime_error("jb_sqdist_mfma failed");
+    std::vector<int32_t> a(n);
+    d2h(a.data(), da, 4 * n);
+    sync();
+    return a;
+  }
+
   // k-means++ over rows of X (models/clustering.py _kmeanspp: one uniform per
   // draw for the device kernel, the host draws after a zero-mass stop)
   std::vector<int64_t> kmeanspp(const std::vector<float>& X, const std::vector<float>& w, size_t n, size_t D,
@@ -522,14 +554,11 @@ class Clustering : public HostEngine {
     const auto reps = kmeanspp(X, w, n, D, m, rng_);
     std::vector<float> C;
     for (int64_t r : reps) C.insert(C.end(), X.begin() + r * (int64_t)D, X.begin() + (r + 1) * (int64_t)D);
-    const auto dd = sqdist(X, n, C, reps.size(), D);
+    // (X is in dX_ from the k-means++ call: its kernel path uploaded it, and
+    // its host fallback's sqdist calls upload the same rows)
+    const auto asg = nearest(X, n, C, reps.size(), D, true);
     std::vector<float> ws(reps.size(), 0.f);
-    for (size_t i = 0; i < n; ++i) {
-      size_t a = 0;
-      for (size_t j = 1; j < reps.size(); ++j)
-        if (dd[i * reps.size() + j] < dd[i * reps.size() + a]) a = j;
-      ws[a] += w[i];
-    }
+    for (size_t i = 0; i < n; ++i) ws[(size_t)asg[i]] += w[i];
     std::vector<int64_t> keep;
     std::vector<double> nw;
     for (size_t j = 0; j < reps.size(); ++j)
@@ -537,8 +566,27 @@ class Clustering : public HostEngine {
     return ps.take(keep, &nw);
   }
 
+  // JB_CLUSTER_PROF=1: wall time per phase of a closed bucket, logged every
+  // 50 buckets (compress, merge-compress, k-means++, Lloyd, EM)
+  struct Prof {
+    bool on = false;
+    double us[5] = {0, 0, 0, 0, 0};
+    int64_t buckets = 0;
+  } prof_;
+  using Clock = std::chrono::steady_clock;
+  static double since_us(Clock::time_point t0) {
+    return std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+  }
+
   void close_bucket(const PointSet& full) {
+    static const bool prof_on = [] {
+      const char* e = getenv("JB_CLUSTER_PROF");
+      return e != nullptr && e[0] == '1';
+    }();
+    prof_.on = prof_on;
+    auto t0 = Clock::now();
     PointSet core = compress(full, p_.compressed);
+    if (prof_.on) prof_.us[0] += since_us(t0);
     if (p_.forgetting_factor > 0) {
       const double f = exp(-p_.forgetting_factor);
       std::vector<PointSet> out;
@@ -554,6 +602,7 @@ class Clustering : public HostEngine {
       buckets_.swap(out);
     }
     buckets_.push_back(std::move(core));
+    t0 = Clock::now();
     while ((int64_t)buckets_.size() > p_.bucket_length) {
       PointSet both = buckets_[0];
       both.append(buckets_[1]);
@@ -561,7 +610,14 @@ class Clustering : public HostEngine {
       buckets_.erase(buckets_.begin(), buckets_.begin() + 2);
       buckets_.insert(buckets_.begin(), std::move(merged));
     }
+    if (prof_.on) prof_.us[1] += since_us(t0);
     recluster();
+    if (prof_.on && ++prof_.buckets % 50 == 0)
+      fprintf(stderr,
+              "cluster prof: %lld buckets, us per bucket: compress %.1f merge %.1f kmeans++ %.1f lloyd %.1f "
+              "em %.1f\n",
+              (long long)prof_.buckets, prof_.us[0] / prof_.buckets, prof_.us[1] / prof_.buckets,
+              prof_.us[2] / prof_.buckets, prof_.us[3] / prof_.buckets, prof_.us[4] / prof_.buckets);
   }
 
   // ---------------------------------------------------------- cluster
@@ -580,7 +636,10 @@ class Clustering : public HostEngine {
     const auto X = dense(pts, keys);
     std::vector<float> w(pts.w.begin(), pts.w.end());
     jb::PyRandom rng(p_.seed + (int64_t)revision_);
+    auto t0 = Clock::now();
     const auto seeds = kmeanspp(X, w, n, D, (int64_t)k, rng);
+    if (prof_.on) prof_.us[2] += since_us(t0);
+    t0 = Clock::now();
     std::vector<float> C;
     for (int64_t r : seeds) C.insert(C.end(), X.begin() + r * (int64_t)D, X.begin() + (r + 1) * (int64_t)D);
     const size_t kk = seeds.size();
@@ -597,6 +656,11 @@ class Clustering : public HostEngine {
     int rc = jb_lloyd(dx, (int)n, (int)D, dw, dc, (int)kk, 100, 1e-6f, 1e-5f, da, nullptr, dd, st_);
     const bool gmm = p_.method == "gmm";
     const bool lloyd_dev = rc != -2;    // Lloyd's centers are in dc
+    if (prof_.on && gmm) {   // (kmeans: the Lloyd time includes the read-back below)
+      sync();
+      prof_.us[3] += since_us(t0);
+      t0 = Clock::now();
+    }
     if (rc == -2) {
       host_lloyd(X, w, n, D, kk, &C, &assign);   // k x dims beyond the kernel's LDS
     } else {
@@ -631,6 +695,9 @@ class Clustering : public HostEngine {
       }
       var_ = var;
       pi_ = pi;
+      if (prof_.on) prof_.us[4] += since_us(t0);
+    } else if (prof_.on) {
+      prof_.us[3] += since_us(t0);
     }
     centers_ = C;
     ncenters_ = kk;

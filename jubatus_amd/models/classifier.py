@@ -298,7 +298,7 @@ class LinearClassifier:
         # exact with several streams runs as serial-equivalent (linear.hip),
         # which needs the scratch as much as an explicit serial mode does
         if a.mode == hip.UPDATE_SERIAL or (a.mode == hip.UPDATE_EXACT and R > 1):
-            a.serial_scratch = self._serial.ptr(max(1, n))
+            a.serial_scratch = self._serial.ptr(max(1, n), self.LC)
             a.serial_bytes = self._serial.nbytes
         a.merge_every = self.hot_merge
         a.hot_waves = hip.HOT_WAVES

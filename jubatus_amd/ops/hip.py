@@ -49,6 +49,7 @@ _SIGS = {
     "jb_df_weigh": [_c_void_p, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64,
                     _i64, _i32, _c_void_p, _i64, _c_void_p, _c_void_p],
     "jb_serial_scratch_bytes": [_i64],
+    "jb_serial_scratch_bytes_lc": [_i64, _i32],
     "jb_serial_scratch_forget": [_c_void_p],
     "jb_hot_detect": [_c_void_p, _i32, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                       _i32, _c_void_p, _c_void_p, _c_void_p],
@@ -71,6 +72,7 @@ _SIGS = {
     "jb_topk": [_i32, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32,
                 _i32, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p],
     "jb_topk_blocks": [_i64, _i32],
+    "jb_topk_mq_stats": [_c_void_p],
     "jb_topk_direct_scratch": [_i32],
     "jb_topk_scratch_init": [_c_void_p, _c_void_p],
     "jb_topk_set_prof": [_c_void_p],
@@ -361,6 +363,14 @@ def topk_scores(scores, nq: int, nrows: int, k: int, flip: bool):
                  scores.device)
 
 
+def topk_mq_stats() -> list:
+    """counters of the multi-query scan since the last call (JB_TOPK_MQ_STATS=1):
+    survivor passes, chunks, first-chunk cuts, register pops"""
+    out = (ctypes.c_ulonglong * 4)()
+    _check(_fn("jb_topk_mq_stats")(ctypes.addressof(out)), "jb_topk_mq_stats")
+    return list(out)
+
+
 def _topk(mode, qbits, qnorm, nq, tbits, tnorm, valid, nrows, words, hash_num, metric, src, flip,
           k, device):
     blocks = _fn("jb_topk_blocks")(nrows, k)
@@ -638,7 +648,7 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
         rc = _fn("jb_linear_train_bf16")(
             _p(row_ptr), _p(fidx), _p(fval), _p(labels), _p(stream_ptr), nstreams, _p(W),
             _p(S) if S is not None else None, _p(active), LC, method, float(C), int(mode),
-            _p(stats), _p(touched), scratch.ptr(max(n_max, 1)) if scratch is not None else None,
+            _p(stats), _p(touched), scratch.ptr(max(n_max, 1), LC) if scratch is not None else None,
             scratch.nbytes if scratch is not None else 0, _stream())
         _check(rc, "jb_linear_train_bf16")
         return
@@ -650,7 +660,7 @@ def linear_train(row_ptr: torch.Tensor, fidx: torch.Tensor, fval: torch.Tensor,
                                 _p(hot.rep) if hot is not None else None, int(merge_every),
                                 HOT_WAVES,
                                 _p(stats), _p(touched), int(n_max),
-                                scratch.ptr(n_max) if scratch is not None else None,
+                                scratch.ptr(n_max, LC) if scratch is not None else None,
                                 scratch.nbytes if scratch is not None else 0, _stream())
     _check(rc, "jb_linear_train")
 
@@ -709,8 +719,10 @@ class SerialScratch:
                 out[f"commit_wave{w}_work_us"] = round(v[12 + w] * us, 1)
         return out
 
-    def ptr(self, n_max: int) -> int:
-        need = int(_fn("jb_serial_scratch_bytes")(int(n_max)))
+    def ptr(self, n_max: int, lc: int = 0) -> int:
+        """lc: the model's label capacity (0: the largest need, any capacity)"""
+        need = int(_fn("jb_serial_scratch_bytes_lc")(int(n_max), int(lc)) if lc > 0
+                   else _fn("jb_serial_scratch_bytes")(int(n_max)))
         if need > self.nbytes:
             if self.buf is not None:
                 torch.cuda.synchronize(self.device)

@@ -150,6 +150,34 @@ def test_clustering_on_gpu_matches_cpu(gpu_min_elems):
     assert cs == sorted([(0, 0), (8, 8), (-8, 8)])
 
 
+@pytest.mark.parametrize("n,d,m", [(50, 3, 10), (200, 10, 100), (1000, 10, 100), (1500, 7, 40), (3000, 4, 20)])
+def test_kmeanspp_matches_host_draws(n, d, m):
+    """csrc/hip/clustering.hip k-means++ (one wave up to 2048 points, the
+    workgroup kernel past that) == the host's draws: bisect_right over the
+    double running sum of weight x min squared distance, the same uniforms"""
+    import bisect
+
+    import numpy as np
+    import torch
+    from jubatus_amd.ops import hip
+    rng = np.random.default_rng(n + d)
+    X = (rng.standard_normal((n, d)) * 3).astype(np.float32)
+    w = (rng.random(n) + 0.25).astype(np.float32)
+    u = rng.random(m)
+    got, status = hip.kmeanspp(torch.from_numpy(X).to(dev()), torch.from_numpy(w).to(dev()), list(u), m)
+    assert status == 0
+    want, d2 = [], np.full(n, np.inf, np.float32)
+    wt = w.astype(np.float64)
+    for j in range(m):
+        cum = np.cumsum(wt)
+        c = min(bisect.bisect_right(cum.tolist(), u[j] * cum[-1]), n - 1)
+        want.append(c)
+        t = X - X[c]
+        d2 = np.minimum(d2, np.einsum("ij,ij->i", t, t).astype(np.float32))
+        wt = (d2 * w).astype(np.float64)
+    assert got == want
+
+
 @pytest.mark.parametrize("n,k,d", [(300, 3, 4), (1000, 5, 17), (64, 1, 2)])
 def test_gmm_em_kernel_matches_fp32_torch(n, k, d):
     """csrc/hip/clustering.hip gmm_em_kernel (one launch for all iterations)
@@ -204,12 +232,19 @@ def test_default_clustering_config_runs_on_device(method):
                                                     (2, 1, 5000, 4, 64), (1, 128, 70_000, 2, 64),
                                                     (0, 37, 3000, 5, 64), (1, 100, 50, 1, 64),
                                                     (0, 10, 400_000, 8, 64), (1, 31, 300_000, 8, 100),
-                                                    (2, 100, 200_000, 7, 128)])
+                                                    (2, 100, 200_000, 7, 128),
+                                                    # topk_mq_kernel (tables of 2M+ rows): one query, 8
+                                                    # queries, euclid_lsh with 2 words, a partial last chunk
+                                                    (0, 10, 2_200_000, 1, 64), (0, 10, 2_300_000, 8, 64),
+                                                    (1, 16, 2_500_000, 3, 128), (2, 5, 2_100_007, 2, 64),
+                                                    (1, 16, 500_000, 12, 128), (2, 32, 300_000, 16, 64)])
 def test_topk_hamming_matches_full_sort(metric, k, nrows, nq, bits):
     """csrc/hip/topk.hip (fused scan + exact top-k) == full distance matrix
     + stable argsort, including ties (lsh/minhash distances are multiples of
-    1/hash_num) and invalid rows. 2..8 queries with <= 128 bits take the
-    one-wave-per-query kernel (topk_wq_kernel)."""
+    1/hash_num) and invalid rows. Tables of 2M+ rows with k <= 32, <= 128
+    bits and <= 8 queries (4 for euclid_lsh) take the sampled bound + register
+    multi-query scan (topk_mq_sample_kernel, topk_mq_kernel); smaller tables
+    or more queries the tile kernels (topk_wq_kernel / topk_kernel)."""
     import torch
     from jubatus_amd.ops import hip
     g = torch.Generator().manual_seed(nrows + k)
