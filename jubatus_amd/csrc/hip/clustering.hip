@@ -438,7 +438,7 @@ __global__ __launch_bounds__(T) void gmm_em_kernel(const float* __restrict__ Xg,
             acc += col < d ? r * xv : r * xv * xv;
           }
         }
-        for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        acc = wave_sum_fast(acc, lane);              // DPP / permlane: no LDS round trips
         if (lane == 0) {
           if (col == 2 * d) nk[j] = fmaxf(acc, 1e-9f);
           else if (col < d) s1[j * d + col] = acc;

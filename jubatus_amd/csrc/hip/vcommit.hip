@@ -959,26 +959,52 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
   const int64_t viol = ld_st(&st[S_VIOL]);
   const int64_t wend = st[S_WEND];
   if (viol == 0) {
-    // commit the window: the staged deltas into W / P (this block is their only writer)
+    // commit the window: the staged deltas into W / P (this block is their
+    // only writer). The used slots first (a window writes a few hundred of
+    // NSLOT), then kU read-modify-writes per thread in flight at once: one
+    // item per loop trip waited a whole HBM round trip per item
+    __shared__ int s_used[NSLOT];
+    __shared__ int s_nused;
+    if (tid == 0) s_nused = 0;
+    __syncthreads();
+    for (int i = tid; i < NSLOT; i += blockDim.x)
+      if (s_key[i] >= 0) s_used[atomicAdd(&s_nused, 1)] = i;
+    __syncthreads();
     constexpr int Q = LC / 4;
-    for (int i = tid; i < NSLOT * Q; i += blockDim.x) {
-      const int sl = i / Q;
-      const int32_t row = s_key[sl];
-      if (row < 0) continue;
-      const int q = i % Q;
-      float4* w4 = reinterpret_cast<float4*>(W + (int64_t)row * LC) + q;
-      const float4 d = reinterpret_cast<const float4*>(g_dw)[i];
-      float4 w = *w4;
-      w.x += d.x; w.y += d.y; w.z += d.z; w.w += d.w;
-      *w4 = w;
-      if (P != nullptr) {
-        float4* p4 = reinterpret_cast<float4*>(P + (int64_t)row * LC) + q;
-        const float4 dp = reinterpret_cast<const float4*>(g_dp)[i];
-        float4 pv = *p4;
-        pv.x += dp.x; pv.y += dp.y; pv.z += dp.z; pv.w += dp.w;
-        *p4 = pv;
+    constexpr int kU = 4;
+    const int items = s_nused * Q;
+    for (int b0 = 0; b0 < items; b0 += kU * (int)blockDim.x) {
+      float4 w[kU], d[kU], pv[kU], dp[kU];
+      int64_t off[kU];
+      bool on[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int it = b0 + u * (int)blockDim.x + tid;
+        on[u] = it < items;
+        const int sl = s_used[on[u] ? it / Q : 0];
+        const int q = it % Q;
+        off[u] = (int64_t)s_key[sl] * Q + q;
+        const int gi = sl * Q + q;
+        if (on[u]) {
+          w[u] = reinterpret_cast<const float4*>(W)[off[u]];
+          d[u] = reinterpret_cast<const float4*>(g_dw)[gi];
+          if (P != nullptr) {
+            pv[u] = reinterpret_cast<const float4*>(P)[off[u]];
+            dp[u] = reinterpret_cast<const float4*>(g_dp)[gi];
+          }
+        }
       }
-      if (q == 0 && touched != nullptr) touched[row] = 1;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (!on[u]) continue;
+        w[u].x += d[u].x; w[u].y += d[u].y; w[u].z += d[u].z; w[u].w += d[u].w;
+        reinterpret_cast<float4*>(W)[off[u]] = w[u];
+        if (P != nullptr) {
+          pv[u].x += dp[u].x; pv[u].y += dp[u].y; pv[u].z += dp[u].z; pv[u].w += dp[u].w;
+          reinterpret_cast<float4*>(P)[off[u]] = pv[u];
+        }
+        if (off[u] % Q == 0 && touched != nullptr) touched[off[u] / Q] = 1;
+      }
     }
     for (int i = tid; i < kBitWords; i += blockDim.x) bits[i] = 0ull;
     if (tid == 0) {
