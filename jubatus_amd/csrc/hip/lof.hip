@@ -50,67 +50,111 @@ struct LofArgs {
   float d[kLofArgMax];
 };
 
+// LDS of the insert and score bodies (one block of 64 threads; a kernel
+// running both shares one copy): per candidate / target row its list, the
+// distances, its rows' k-distances and list flags; +1 per row so that the
+// 64 threads' rows start on different banks
+struct LofLds {
+  int32_t s[64][kLofMaxK + 1];
+  float d[64][kLofMaxK + 1];
+  float kd[64][kLofMaxK + 1];
+  uint8_t okb[64][kLofMaxK + 1];
+  uint8_t ok1[64], stale[64];
+  float kd1[64], lrd1[64];
+  uint32_t lst[64];
+  int n_ch, nmiss;
+};
+
+// Staleness stamps (optional, kstamp / lstamp non-null): kstamp[x] = the add
+// epoch that last changed x's list / k-distance, lstamp[o] = the epoch lrd[o]
+// was computed at; lrd[o] is current only while lrd_ok[o] and every row x it
+// lists has kstamp[x] <= lstamp[o]. With stamps an add needs no mark pass over
+// every list (lof_add_score_kernel: insert and score in one launch).
 // p's list from its candidates; candidates o take p in. One block of 64
-// threads; each thread's working copy of a list sits in LDS.
+// threads. The candidates' lists are fetched cooperatively first (every
+// (candidate, entry) load of a round of 64 candidates in flight at once, one
+// memory latency instead of k dependent ones per thread), then each thread
+// edits its candidate's copy in LDS and writes it back.
 __device__ __forceinline__ void lof_insert_body(
     int p, const int32_t* __restrict__ cs, const float* __restrict__ cd, int nc, int k,
     int ignore_same, int32_t* __restrict__ nb_slot, float* __restrict__ nb_dist,
     float* __restrict__ kdist, uint8_t* __restrict__ ok, uint8_t* __restrict__ lrd_ok,
-    int32_t* __restrict__ changed, int32_t* __restrict__ nchanged, bool first = true) {
-  __shared__ int n_ch;
-  __shared__ int32_t l_s[64][kLofMaxK];
-  __shared__ float l_d[64][kLofMaxK];
-  if (threadIdx.x == 0 && !first) n_ch = *nchanged;   // a later chunk of candidates: reverse inserts only
-  if (threadIdx.x == 0 && first) {
-    n_ch = 0;
+    int32_t* __restrict__ changed, int32_t* __restrict__ nchanged, bool first, LofLds& L,
+    uint32_t* __restrict__ kstamp = nullptr, uint32_t epoch = 0) {
+  int& n_ch = L.n_ch;
+  auto& l_s = L.s;
+  auto& l_d = L.d;
+  uint8_t* l_ok = L.ok1;
+  const int t = threadIdx.x;
+  if (t == 0 && !first) n_ch = *nchanged;   // a later chunk of candidates: reverse inserts only
+  if (t == 0 && first) {
     int32_t* ps = nb_slot + (int64_t)p * k;
     float* pd = nb_dist + (int64_t)p * k;
     for (int j = 0; j < k; ++j) {
       ps[j] = j < nc ? cs[j] : -1;
       pd[j] = j < nc ? cd[j] : INFINITY;
     }
-    kdist[p] = lof_kth(ps, pd, k, ignore_same);
+    kdist[p] = lof_kth(cs, cd, nc < k ? nc : k, ignore_same);
     ok[p] = 1;
     lrd_ok[p] = 0;
+    if (kstamp != nullptr) kstamp[p] = epoch;
     changed[0] = p;
     n_ch = 1;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < nc; i += blockDim.x) {
-    const int32_t o = cs[i];
-    const float d = cd[i];
-    if (o < 0 || o == p || !ok[o]) continue;
-    int32_t* os = nb_slot + (int64_t)o * k;
-    float* od = nb_dist + (int64_t)o * k;
-    int32_t* ts = l_s[threadIdx.x];
-    float* td = l_d[threadIdx.x];
-    int n = 0;
-    bool had = false;
-    for (int j = 0; j < k; ++j) {            // o's list without p
-      if (os[j] < 0) break;
-      if (os[j] == p) { had = true; continue; }
-      ts[n] = os[j];
-      td[n] = od[j];
-      ++n;
+  for (int c0 = 0; c0 < nc; c0 += 64) {
+    const int cn = nc - c0 < 64 ? nc - c0 : 64;
+    for (int e = t; e < cn * k; e += 64) {
+      const int c = e / k, j = e - c * k;
+      const int32_t o = cs[c0 + c];
+      if (o >= 0 && o != p) {
+        l_s[c][j] = nb_slot[(int64_t)o * k + j];
+        l_d[c][j] = nb_dist[(int64_t)o * k + j];
+      }
     }
-    const bool full = n == k;
-    if (!had && full && !(d < td[k - 1] || (d == td[k - 1] && p < ts[k - 1]))) continue;
-    int at = n;                               // insert (d, p) in (distance, slot) order
-    while (at > 0 && (td[at - 1] > d || (td[at - 1] == d && ts[at - 1] > p))) --at;
-    for (int j = (n < k ? n : k - 1); j > at; --j) { ts[j] = ts[j - 1]; td[j] = td[j - 1]; }
-    if (at < k) { ts[at] = p; td[at] = d; }
-    const int m = n < k ? n + 1 : k;
-    for (int j = 0; j < k; ++j) {
-      os[j] = j < m ? ts[j] : -1;
-      od[j] = j < m ? td[j] : INFINITY;
+    if (t < cn) {
+      const int32_t o = cs[c0 + t];
+      l_ok[t] = (o >= 0 && o != p) ? ok[o] : 0;
     }
-    kdist[o] = lof_kth(os, od, k, ignore_same);
-    lrd_ok[o] = 0;
-    const int w = atomicAdd(&n_ch, 1);
-    if (w < kLofMaxChanged) changed[w] = o;
+    __syncthreads();
+    if (t < cn && l_ok[t]) {
+      const int32_t o = cs[c0 + t];
+      const float d = cd[c0 + t];
+      int32_t* ts = l_s[t];
+      float* td = l_d[t];
+      int n = 0;
+      bool had = false;
+      for (int j = 0; j < k; ++j) {          // o's list without p (compacted in place)
+        const int32_t x = ts[j];
+        if (x < 0) break;
+        if (x == p) { had = true; continue; }
+        ts[n] = x;
+        td[n] = td[j];
+        ++n;
+      }
+      const bool full = n == k;
+      if (had || !full || d < td[k - 1] || (d == td[k - 1] && p < ts[k - 1])) {
+        int at = n;                             // insert (d, p) in (distance, slot) order
+        while (at > 0 && (td[at - 1] > d || (td[at - 1] == d && ts[at - 1] > p))) --at;
+        for (int j = (n < k ? n : k - 1); j > at; --j) { ts[j] = ts[j - 1]; td[j] = td[j - 1]; }
+        if (at < k) { ts[at] = p; td[at] = d; }
+        const int m = n < k ? n + 1 : k;
+        int32_t* os = nb_slot + (int64_t)o * k;
+        float* od = nb_dist + (int64_t)o * k;
+        for (int j = 0; j < k; ++j) {
+          if (j >= m) { ts[j] = -1; td[j] = INFINITY; }
+          os[j] = ts[j];
+          od[j] = td[j];
+        }
+        kdist[o] = lof_kth(ts, td, k, ignore_same);
+        lrd_ok[o] = 0;
+        if (kstamp != nullptr) kstamp[o] = epoch;
+        const int w = atomicAdd(&n_ch, 1);
+        if (w < kLofMaxChanged) changed[w] = o;
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x == 0) *nchanged = n_ch < kLofMaxChanged ? n_ch : kLofMaxChanged;
+  if (t == 0) *nchanged = n_ch < kLofMaxChanged ? n_ch : kLofMaxChanged;
 }
 
 __global__ __launch_bounds__(64) void lof_add_kernel(
@@ -123,12 +167,18 @@ __global__ __launch_bounds__(64) void lof_add_kernel(
   __shared__ float cd[kLofArgMax];
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
   __syncthreads();
+  __shared__ LofLds L;
   lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
-                  nchanged, first != 0);
+                  nchanged, first != 0, L);
 }
 
 // Every row listing a changed row: lrd_ok = 0 (and, clear_ok: ok = 0 -
 // its list must be recomputed, e.g. the listed row moved or was removed).
+// The lists are read as one flat array, 8 entries a thread (two 16-byte
+// loads, coalesced); the changed rows sit in an LDS hash table sized to
+// their count. Rows without a valid list may be marked too: harmless, their
+// lrd is not used before their list is installed (which resets both flags).
+constexpr int kMarkPer = 8;
 __global__ __launch_bounds__(256) void lof_mark_kernel(int64_t nrows, int k,
                                                        const int32_t* __restrict__ nb_slot,
                                                        const int32_t* __restrict__ changed,
@@ -139,36 +189,49 @@ __global__ __launch_bounds__(256) void lof_mark_kernel(int64_t nrows, int k,
   if (abort_flag != nullptr && *abort_flag != 0) return;
   __shared__ int32_t tab[2 * kLofMaxChanged];
   const int nch = *nchanged;
-  for (int i = threadIdx.x; i < 2 * kLofMaxChanged; i += blockDim.x) tab[i] = -1;
+  int bits = 6;
+  while ((1 << bits) < 2 * nch) ++bits;
+  const uint32_t mask = (1u << bits) - 1u;
+  for (int i = threadIdx.x; i <= (int)mask; i += blockDim.x) tab[i] = -1;
   __syncthreads();
   for (int i = threadIdx.x; i < nch; i += blockDim.x) {
     const int32_t c = changed[i];
-    uint32_t h = ((uint32_t)c * 0x9E3779B1u) >> 21;
+    uint32_t h = ((uint32_t)c * 0x9E3779B1u) >> (32 - bits);
     while (true) {
       const int32_t old = atomicCAS(&tab[h], -1, c);
       if (old == -1 || old == c) break;
-      h = (h + 1) & (2 * kLofMaxChanged - 1);
+      h = (h + 1) & mask;
     }
   }
   __syncthreads();
-  const int64_t y = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (y >= nrows || !ok[y]) return;
-  const int32_t* ys = nb_slot + y * k;
-  for (int j = 0; j < k; ++j) {
-    const int32_t x = ys[j];
-    if (x < 0) break;
-    uint32_t h = ((uint32_t)x * 0x9E3779B1u) >> 21;
+  const int64_t total = nrows * k;
+  const int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * kMarkPer;
+  if (e0 >= total) return;
+  int32_t x[kMarkPer];
+  if (e0 + kMarkPer <= total) {
+    const int4 v0 = *reinterpret_cast<const int4*>(nb_slot + e0);
+    const int4 v1 = *reinterpret_cast<const int4*>(nb_slot + e0 + 4);
+    x[0] = v0.x; x[1] = v0.y; x[2] = v0.z; x[3] = v0.w;
+    x[4] = v1.x; x[5] = v1.y; x[6] = v1.z; x[7] = v1.w;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kMarkPer; ++u) x[u] = e0 + u < total ? nb_slot[e0 + u] : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < kMarkPer; ++u) {
+    if (x[u] < 0) continue;
+    uint32_t h = ((uint32_t)x[u] * 0x9E3779B1u) >> (32 - bits);
     bool hit = false;
     while (true) {
-      const int32_t t = tab[h];
-      if (t == x) { hit = true; break; }
-      if (t == -1) break;
-      h = (h + 1) & (2 * kLofMaxChanged - 1);
+      const int32_t tv = tab[h];
+      if (tv == x[u]) { hit = true; break; }
+      if (tv == -1) break;
+      h = (h + 1) & mask;
     }
     if (hit) {
+      const int64_t y = (e0 + u) / k;
       lrd_ok[y] = 0;
       if (clear_ok) ok[y] = 0;
-      return;
     }
   }
 }
@@ -201,20 +264,6 @@ __global__ __launch_bounds__(256) void lof_set_lists_kernel(
   if (i < kLofMaxChanged) changed[i] = s;
 }
 
-__device__ __forceinline__ float lof_lrd(const int32_t* s, const float* d, int k,
-                                         const float* __restrict__ kdist) {
-  float sum = 0.f;
-  int n = 0;
-  for (int j = 0; j < k; ++j) {
-    if (s[j] < 0) break;
-    sum += fmaxf(kdist[s[j]], d[j]);
-    ++n;
-  }
-  if (n == 0) return 0.f;
-  const float mean = sum / n;
-  return mean <= 0.f ? INFINITY : 1.f / mean;
-}
-
 // LOF of one point from its neighbours (ts, td: nt entries, ascending):
 // refreshes the stale lrd of those neighbours, writes to pinned host memory
 // out = [status, score bits, lrd(q) bits, nmissing, missing slots...]:
@@ -226,32 +275,78 @@ __device__ __forceinline__ void lof_score_body(
     const int32_t* __restrict__ nb_slot, const float* __restrict__ nb_dist,
     const float* __restrict__ kdist, const uint8_t* __restrict__ ok, float* __restrict__ lrd,
     uint8_t* __restrict__ lrd_ok, int store_slot, uint32_t* __restrict__ out, int max_missing,
-    int32_t* __restrict__ abort_flag = nullptr) {
-  __shared__ int nmiss;
-  if (threadIdx.x == 0) nmiss = 0;
-  __syncthreads();
+    int32_t* __restrict__ abort_flag, LofLds& L, const uint32_t* __restrict__ kstamp = nullptr,
+    uint32_t* __restrict__ lstamp = nullptr, uint32_t epoch = 0) {
+  // the targets' lists and their rows' flags / k-distances (and stamps) are
+  // fetched in two cooperative rounds (every load of a round in flight at
+  // once), then each target's thread works from LDS
+  int& nmiss = L.nmiss;
+  auto& l_s = L.s;
+  auto& l_d = L.d;
+  auto& l_kd = L.kd;
+  auto& l_ok = L.okb;
+  uint8_t* s_ok = L.ok1;
+  float* s_kd = L.kd1;
+  float* s_lrd = L.lrd1;
   const int t = threadIdx.x;
+  if (t == 0) nmiss = 0;
+  uint8_t lok = 0;
+  float lr = 0.f;
+  if (t < nt) {
+    const int32_t o = ts[t];
+    s_ok[t] = ok[o];
+    lok = lrd_ok[o];
+    lr = lrd[o];
+    s_kd[t] = kdist[o];
+    L.stale[t] = 0;
+    if (kstamp != nullptr) L.lst[t] = lstamp[o];
+  }
+  for (int e = t; e < nt * k; e += blockDim.x) {
+    const int c = e / k, j = e - c * k;
+    const int64_t at = (int64_t)ts[c] * k + j;
+    l_s[c][j] = nb_slot[at];
+    l_d[c][j] = nb_dist[at];
+  }
+  __syncthreads();
+  for (int e = t; e < nt * k; e += blockDim.x) {
+    const int c = e / k, j = e - c * k;
+    const int32_t x = l_s[c][j];
+    if (s_ok[c] && x >= 0) {     // a list is valid (in range) only while its row is ok
+      l_ok[c][j] = ok[x];
+      l_kd[c][j] = kdist[x];
+      if (kstamp != nullptr && kstamp[x] > L.lst[c]) L.stale[c] = 1;
+    }
+  }
+  __syncthreads();
   auto miss = [&](int32_t s) {
     const int w = atomicAdd(&nmiss, 1);
     if (w < max_missing) sys_store(out + 4 + w, (uint32_t)s);
   };
   if (t < nt) {
     const int32_t o = ts[t];
-    if (!ok[o]) {
+    if (!s_ok[t]) {
       miss(o);
     } else {
       // lrd[o] is current only while every row o lists has a valid list
-      const int32_t* os = nb_slot + (int64_t)o * k;
       bool good = true;
+      int n = 0;
+      float sum = 0.f;
       for (int j = 0; j < k; ++j) {
-        if (os[j] < 0) break;
-        if (!ok[os[j]]) { miss(os[j]); good = false; }
+        const int32_t x = l_s[t][j];
+        if (x < 0) break;
+        if (!l_ok[t][j]) { miss(x); good = false; }
+        sum += fmaxf(l_kd[t][j], l_d[t][j]);
+        ++n;
       }
-      if (good && !lrd_ok[o]) {
-        lrd[o] = lof_lrd(os, nb_dist + (int64_t)o * k, k, kdist);
+      if (good && (!lok || L.stale[t])) {
+        const float mean = n > 0 ? sum / n : 0.f;
+        lr = n == 0 ? 0.f : (mean <= 0.f ? INFINITY : 1.f / mean);
+        lrd[o] = lr;
         lrd_ok[o] = 1;
+        if (lstamp != nullptr) lstamp[o] = epoch;
       }
     }
+    s_lrd[t] = lr;
   }
   // the host reads out[] once out[0] is set: every thread's system-scope
   // stores are acknowledged before the barrier, the status goes last (a
@@ -271,8 +366,8 @@ __device__ __forceinline__ void lof_score_body(
   float sum = 0.f, lsum = 0.f;
   bool linf = false;
   for (int j = 0; j < nt; ++j) {
-    sum += fmaxf(kdist[ts[j]], td[j]);
-    const float l = lrd[ts[j]];
+    sum += fmaxf(s_kd[j], td[j]);
+    const float l = s_lrd[j];
     if (isinf(l)) linf = true; else lsum += l;
   }
   float score = 1.f, lp = 0.f;
@@ -285,7 +380,11 @@ __device__ __forceinline__ void lof_score_body(
     else if (isinf(mean_lo)) score = INFINITY;
     else score = mean_lo / lp;
   }
-  if (store_slot >= 0) { lrd[store_slot] = lp; lrd_ok[store_slot] = 1; }
+  if (store_slot >= 0) {
+    lrd[store_slot] = lp;
+    lrd_ok[store_slot] = 1;
+    if (lstamp != nullptr) lstamp[store_slot] = epoch;
+  }
   sys_store(out + 1, __float_as_uint(score));
   sys_store(out + 2, __float_as_uint(lp));
   sys_store(out + 3, 0u);
@@ -298,29 +397,62 @@ __global__ __launch_bounds__(64) void lof_score_kernel(
     const float* __restrict__ nb_dist, const float* __restrict__ kdist,
     const uint8_t* __restrict__ ok, float* __restrict__ lrd, uint8_t* __restrict__ lrd_ok,
     int store_slot, uint32_t* __restrict__ out, int max_missing,
-    int32_t* __restrict__ abort_flag = nullptr) {
+    int32_t* __restrict__ abort_flag = nullptr, const uint32_t* __restrict__ kstamp = nullptr,
+    uint32_t* __restrict__ lstamp = nullptr, uint32_t epoch = 0) {
   if (abort_flag != nullptr && *abort_flag != 0) {   // skipped: an earlier add stopped the batch
     if (threadIdx.x == 0) sys_store(out, 3u);
     return;
   }
   __shared__ int32_t ts[kLofMaxK];
   __shared__ float td[kLofMaxK];
+  __shared__ LofLds L;
   const int nt = a.n < kLofMaxK ? a.n : kLofMaxK;
   if ((int)threadIdx.x < nt) { ts[threadIdx.x] = a.s[threadIdx.x]; td[threadIdx.x] = a.d[threadIdx.x]; }
   __syncthreads();
   lof_score_body(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, store_slot, out,
-                 max_missing, abort_flag);
+                 max_missing, abort_flag, L, kstamp, lstamp, epoch);
+}
+
+// One add in one launch (stamps, no mark pass): p's insert (candidates in
+// the arguments, all <= kLofArgMax of them), then its score from the k
+// nearest, lrd[p] stored; out as lof_score_kernel
+__global__ __launch_bounds__(64) void lof_add_score_kernel(
+    const LofArgs a, int p, int k, int ignore_same, int32_t* __restrict__ nb_slot,
+    float* __restrict__ nb_dist, float* __restrict__ kdist, uint8_t* __restrict__ ok,
+    float* __restrict__ lrd, uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed,
+    int32_t* __restrict__ nchanged, uint32_t* __restrict__ kstamp, uint32_t* __restrict__ lstamp,
+    uint32_t epoch, uint32_t* __restrict__ out, int max_missing, int32_t* __restrict__ abort_flag) {
+  if (abort_flag != nullptr && *abort_flag != 0) {   // skipped: an earlier add stopped the batch
+    if (threadIdx.x == 0) sys_store(out, 3u);
+    return;
+  }
+  __shared__ int32_t cs[kLofArgMax];
+  __shared__ float cd[kLofArgMax];
+  __shared__ LofLds L;
+  for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
+  __syncthreads();
+  lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
+                  nchanged, true, L, kstamp, epoch);
+  // the insert's global stores are visible to the block after the barrier
+  __syncthreads();
+  const int nt = a.n < k ? a.n : k;
+  lof_score_body(cs, cd, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, p, out, max_missing,
+                 abort_flag, L, kstamp, lstamp, epoch);
 }
 
 }  // namespace jb
+
+static unsigned mark_blocks(int64_t nrows, int k) {
+  const int64_t per_block = 256 * jb::kMarkPer;
+  return (unsigned)((nrows * k + per_block - 1) / per_block);
+}
 
 extern "C" int jb_lof_mark(int64_t nrows, int k, const int32_t* nb_slot, const int32_t* changed,
                            const int32_t* nchanged, int clear_ok, uint8_t* ok, uint8_t* lrd_ok,
                            hipStream_t stream) {
   if (nrows <= 0) return 0;
-  const unsigned blocks = (unsigned)((nrows + 255) / 256);
-  hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(blocks), dim3(256), 0, stream, nrows, k, nb_slot,
-                     changed, nchanged, clear_ok, ok, lrd_ok);
+  hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(mark_blocks(nrows, k)), dim3(256), 0, stream, nrows, k,
+                     nb_slot, changed, nchanged, clear_ok, ok, lrd_ok);
   return (int)hipGetLastError();
 }
 
@@ -350,20 +482,33 @@ int fill_args(jb::LofArgs* a, const int32_t* sl, const float* d, int n) {
 // p, ascending, p excluded; host arrays) go in the kernel arguments; p's
 // list is written and p enters its candidates' lists (lof_add_kernel), the
 // rows depending on a changed list are marked (lof_mark_kernel), then p is
-// scored from its k nearest (lof_score_kernel, lrd[p] stored). Waits for
-// the score; out_host = [status, score, lrd, nmissing, missing...].
-extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int k,
-                          int ignore_same, int64_t nrows, int32_t* nb_slot, float* nb_dist,
-                          float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
-                          int32_t* changed, int32_t* nchanged, uint32_t* out_host,
-                          int max_missing, hipStream_t stream) {
+// scored from its k nearest (lof_score_kernel, lrd[p] stored). With stamps
+// (kstamp / lstamp non-null, epoch = this add's, above every earlier one) and
+// nc <= kLofArgMax the add is one launch instead (lof_add_score_kernel).
+// Waits for the score; out_host = [status, score, lrd, nmissing, missing...].
+extern "C" int jb_lof_add_st(int p, const int32_t* cs, const float* cd, int nc, int k,
+                             int ignore_same, int64_t nrows, int32_t* nb_slot, float* nb_dist,
+                             float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
+                             int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp,
+                             uint32_t epoch, uint32_t* out_host, int max_missing, hipStream_t stream) {
   if (k <= 0 || k > jb::kLofMaxK || nc < 0) return -2;
+  jb::LofArgs a;
+  out_host[0] = 0;
+  if (kstamp != nullptr && lstamp != nullptr && nc <= jb::kLofArgMax) {
+    int rc = fill_args(&a, cs, cd, nc);
+    if (rc) return rc;
+    hipLaunchKernelGGL(jb::lof_add_score_kernel, dim3(1), dim3(64), 0, stream, a, p, k, ignore_same, nb_slot,
+                       nb_dist, kdist, ok, lrd, lrd_ok, changed, nchanged, kstamp, lstamp, epoch, out_host,
+                       max_missing, (int32_t*)nullptr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    return jb::wait_nonzero(out_host, stream);
+  }
   // the candidates travel in the kernel arguments, kLofArgMax per launch: the
   // first launch sets p's own list (its k nearest are the head of the first
   // chunk) and the reverse inserts of that chunk, later ones (a
   // reverse_nearest_neighbor_num above the argument budget) only insert p
   // into their candidates' lists
-  jb::LofArgs a;
   for (int c0 = 0; c0 == 0 || c0 < nc; c0 += jb::kLofArgMax) {
     const int cn = nc - c0 < jb::kLofArgMax ? nc - c0 : jb::kLofArgMax;
     int rc = fill_args(&a, cs + c0, cd + c0, cn < 0 ? 0 : cn);
@@ -373,48 +518,54 @@ extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int
   }
   int rc = fill_args(&a, cs, cd, nc < jb::kLofArgMax ? nc : jb::kLofArgMax);
   if (rc) return rc;
-  const unsigned blocks = (unsigned)((nrows + 255) / 256);
-  hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(blocks), dim3(256), 0, stream, nrows, k, nb_slot,
-                     changed, nchanged, 0, ok, lrd_ok);
+  hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(mark_blocks(nrows, k)), dim3(256), 0, stream, nrows, k,
+                     nb_slot, changed, nchanged, 0, ok, lrd_ok);
   a.n = nc < k ? nc : k;               // score from the k nearest
-  out_host[0] = 0;
   hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist,
-                     kdist, ok, lrd, lrd_ok, p, out_host, max_missing);
+                     kdist, ok, lrd, lrd_ok, p, out_host, max_missing, (int32_t*)nullptr,
+                     (const uint32_t*)kstamp, lstamp, epoch);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host, stream);
 }
 
-// A batch of adds in arrival order, one wait: add i's kernels (insert,
-// mark, score into out_host + i * out_stride) are enqueued behind add i - 1's
-// without a host round trip. An add whose score finds rows without a valid
-// list sets *abort_dev; every later kernel of the batch then exits (status 3)
-// and the host finishes that add (missing lists installed, scored again)
-// before it resubmits the rest - the order of the sequential adds.
-// cs / cd: [nadd][stride] candidates (ascending, p excluded), nc[i] of them.
+extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int k,
+                          int ignore_same, int64_t nrows, int32_t* nb_slot, float* nb_dist,
+                          float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
+                          int32_t* changed, int32_t* nchanged, uint32_t* out_host,
+                          int max_missing, hipStream_t stream) {
+  return jb_lof_add_st(p, cs, cd, nc, k, ignore_same, nrows, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok,
+                       changed, nchanged, nullptr, nullptr, 0, out_host, max_missing, stream);
+}
+
+// A batch of adds in arrival order, one wait: add i (epoch epoch0 + i; one
+// lof_add_score_kernel, score into out_host + i * out_stride) is enqueued
+// behind add i - 1's without a host round trip. An add whose score finds
+// rows without a valid list sets *abort_dev; every later kernel of the batch
+// then exits (status 3) and the host finishes that add (missing lists
+// installed, scored again) before it resubmits the rest - the order of the
+// sequential adds. cs / cd: [nadd][stride] candidates (ascending, p
+// excluded), nc[i] of them.
 extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd,
-                               const int32_t* nc, int stride, int k, int ignore_same, int64_t nrows,
-                               int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok, float* lrd,
-                               uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged, uint32_t* out_host,
-                               int out_stride, int max_missing, int32_t* abort_dev, hipStream_t stream) {
+                               const int32_t* nc, int stride, int k, int ignore_same, int32_t* nb_slot,
+                               float* nb_dist, float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
+                               int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp,
+                               uint32_t epoch0, uint32_t* out_host, int out_stride, int max_missing,
+                               int32_t* abort_dev, hipStream_t stream) {
   if (nadd <= 0) return 0;
-  if (k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax) return -2;
+  if (k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax || kstamp == nullptr || lstamp == nullptr)
+    return -2;
   hipError_t e = hipMemsetAsync(abort_dev, 0, sizeof(int32_t), stream);
   if (e != hipSuccess) return (int)e;
-  const unsigned blocks = (unsigned)((nrows + 255) / 256);
   for (int i = 0; i < nadd; ++i) out_host[(int64_t)i * out_stride] = 0;
   jb::LofArgs a;
   for (int i = 0; i < nadd; ++i) {
     const int n = nc[i];
     int rc = fill_args(&a, cs + (int64_t)i * stride, cd + (int64_t)i * stride, n < 0 ? 0 : n);
     if (rc) return rc;
-    hipLaunchKernelGGL(jb::lof_add_kernel, dim3(1), dim3(64), 0, stream, a, ps[i], k, ignore_same, nb_slot,
-                       nb_dist, kdist, ok, lrd_ok, changed, nchanged, 1, (const int32_t*)abort_dev);
-    hipLaunchKernelGGL(jb::lof_mark_kernel, dim3(blocks), dim3(256), 0, stream, nrows, k, nb_slot, changed,
-                       nchanged, 0, ok, lrd_ok, (const int32_t*)abort_dev);
-    a.n = n < k ? n : k;
-    hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist, kdist, ok,
-                       lrd, lrd_ok, ps[i], out_host + (int64_t)i * out_stride, max_missing, abort_dev);
+    hipLaunchKernelGGL(jb::lof_add_score_kernel, dim3(1), dim3(64), 0, stream, a, ps[i], k, ignore_same,
+                       nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, changed, nchanged, kstamp, lstamp,
+                       epoch0 + (uint32_t)i, out_host + (int64_t)i * out_stride, max_missing, abort_dev);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
@@ -422,21 +573,32 @@ extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, c
 }
 
 // LOF of a point from its nt (<= 64) nearest (host arrays), lrd of the
-// targets refreshed; waits; same out_host layout
-extern "C" int jb_lof_score(const int32_t* ts, const float* td, int nt, int k,
-                            const int32_t* nb_slot, const float* nb_dist, const float* kdist,
-                            const uint8_t* ok, float* lrd, uint8_t* lrd_ok, int store_slot,
-                            uint32_t* out_host, int max_missing, hipStream_t stream) {
+// targets refreshed (stamped with epoch when kstamp / lstamp are given);
+// waits; same out_host layout
+extern "C" int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k,
+                               const int32_t* nb_slot, const float* nb_dist, const float* kdist,
+                               const uint8_t* ok, float* lrd, uint8_t* lrd_ok, int store_slot,
+                               const uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch,
+                               uint32_t* out_host, int max_missing, hipStream_t stream) {
   if (nt > 64 || k > jb::kLofMaxK) return -2;
   jb::LofArgs a;
   int rc = fill_args(&a, ts, td, nt);
   if (rc) return rc;
   out_host[0] = 0;
   hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist,
-                     kdist, ok, lrd, lrd_ok, store_slot, out_host, max_missing);
+                     kdist, ok, lrd, lrd_ok, store_slot, out_host, max_missing, (int32_t*)nullptr,
+                     kstamp, lstamp, epoch);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host, stream);
+}
+
+extern "C" int jb_lof_score(const int32_t* ts, const float* td, int nt, int k,
+                            const int32_t* nb_slot, const float* nb_dist, const float* kdist,
+                            const uint8_t* ok, float* lrd, uint8_t* lrd_ok, int store_slot,
+                            uint32_t* out_host, int max_missing, hipStream_t stream) {
+  return jb_lof_score_st(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, store_slot, nullptr,
+                         nullptr, 0, out_host, max_missing, stream);
 }
 
 namespace jb {

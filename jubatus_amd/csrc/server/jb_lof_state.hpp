@@ -1,7 +1,8 @@
 // Incremental LOF state in HBM for the native jubaanomaly: the C++ twin of
 // models/lof_state.py DeviceLofState over csrc/hip/lof.hip (per-slot k
-// nearest neighbour lists, k-distance, lrd, validity flags; insert + mark +
-// score of an add in one host call; staleness marks over all lists).
+// nearest neighbour lists, k-distance, lrd, validity flags and stamps;
+// insert + score of an add in one launch; staleness marks over all lists
+// for moved rows and installed lists).
 //
 // Reference: anomaly_serv.cpp:157-244 over jubatus_core's lof_storage
 // (EXTERNAL); the algorithm (Breunig et al. 2000) and its host oracle are
@@ -27,14 +28,19 @@ int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int k, int ign
                int64_t nrows, int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok,
                float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
                uint32_t* out_host, int max_missing, hipStream_t stream);
+int jb_lof_add_st(int p, const int32_t* cs, const float* cd, int nc, int k, int ignore_same, int64_t nrows,
+                  int32_t* nb_slot, float* nb_dist, float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
+                  int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch,
+                  uint32_t* out_host, int max_missing, hipStream_t stream);
 int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd, const int32_t* nc,
-                    int stride, int k, int ignore_same, int64_t nrows, int32_t* nb_slot, float* nb_dist,
-                    float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
-                    uint32_t* out_host, int out_stride, int max_missing, int32_t* abort_dev, hipStream_t stream);
-int jb_lof_score(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
-                 const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd,
-                 uint8_t* lrd_ok, int store_slot, uint32_t* out_host, int max_missing,
-                 hipStream_t stream);
+                    int stride, int k, int ignore_same, int32_t* nb_slot, float* nb_dist, float* kdist,
+                    uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
+                    uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch0, uint32_t* out_host, int out_stride,
+                    int max_missing, int32_t* abort_dev, hipStream_t stream);
+int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
+                    const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd, uint8_t* lrd_ok,
+                    int store_slot, const uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch,
+                    uint32_t* out_host, int max_missing, hipStream_t stream);
 int jb_lof_invalidate(const int32_t* slots, int n, int64_t nrows, uint8_t* ok, uint8_t* lrd_ok,
                       hipStream_t stream);
 void* jb_host_alloc(int64_t nbytes);
@@ -66,7 +72,7 @@ class LofState {
 
   ~LofState() {
     for (void* q : {(void*)nb_slot_.p, (void*)nb_dist_.p, (void*)kdist_.p, (void*)lrd_.p, (void*)ok_.p,
-                    (void*)lrd_ok_.p, (void*)changed_.p, (void*)nchanged_.p, (void*)up_[0].p, (void*)up_[1].p,
+                    (void*)lrd_ok_.p, (void*)kstamp_.p, (void*)lstamp_.p, (void*)changed_.p, (void*)nchanged_.p, (void*)up_[0].p, (void*)up_[1].p,
                     (void*)up_[2].p, (void*)abort_.p})
       if (q) (void)hipFree(q);
     if (out_) jb_host_free(out_);
@@ -86,6 +92,8 @@ class LofState {
     regrow(lrd_, cap_, cap, 0);
     regrow(ok_, cap_, cap, 0);
     regrow(lrd_ok_, cap_, cap, 0);
+    regrow(kstamp_, cap_, cap, 0);
+    regrow(lstamp_, cap_, cap, 0);
     cap_ = cap;
   }
 
@@ -94,9 +102,9 @@ class LofState {
   bool add(int32_t p, const std::vector<int32_t>& cs, const std::vector<float>& cd, float* score,
            std::vector<int32_t>* missing) {
     const int nc = (int)cs.size();     // (kLofArgMax candidates per launch inside)
-    const int rc = jb_lof_add(p, cs.data(), cd.data(), nc, k_, ignore_ ? 1 : 0, cap_, nb_slot_.p,
-                              nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p,
-                              out_, kLofMaxMissing, stream_);
+    const int rc = jb_lof_add_st(p, cs.data(), cd.data(), nc, k_, ignore_ ? 1 : 0, cap_, nb_slot_.p,
+                                 nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p,
+                                 kstamp_.p, lstamp_.p, ++epoch_, out_, kLofMaxMissing, stream_);
     if (rc != 0) throw std::runtime_error("lof add failed: " + std::to_string(rc));
     return result(score, missing);
   }
@@ -122,9 +130,12 @@ class LofState {
       std::copy(cs[i].begin(), cs[i].end(), fcs.begin() + (int64_t)i * stride);
       std::copy(cd[i].begin(), cd[i].end(), fcd.begin() + (int64_t)i * stride);
     }
+    const uint32_t epoch0 = epoch_ + 1;
+    epoch_ += (uint32_t)n;            // (adds after a stop leave gaps: stamps only need to grow)
     const int rc = jb_lof_add_many((int)n, ps.data(), fcs.data(), fcd.data(), nc.data(), stride, k_, ignore_ ? 1 : 0,
-                                   cap_, nb_slot_.p, nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p,
-                                   nchanged_.p, out_many_, kOutStride, kLofMaxMissing, abort_.p, stream_);
+                                   nb_slot_.p, nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p,
+                                   nchanged_.p, kstamp_.p, lstamp_.p, epoch0, out_many_, kOutStride, kLofMaxMissing,
+                                   abort_.p, stream_);
     if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
     scores->clear();
     for (size_t i = 0; i < n; ++i) {
@@ -151,8 +162,9 @@ class LofState {
   bool score(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store, float* sc,
              std::vector<int32_t>* missing) {
     if (ts.empty()) { *sc = 1.f; return true; }
-    const int rc = jb_lof_score(ts.data(), td.data(), (int)ts.size(), k_, nb_slot_.p, nb_dist_.p, kdist_.p,
-                                ok_.p, lrd_.p, lrd_ok_.p, store, out_, kLofMaxMissing, stream_);
+    const int rc = jb_lof_score_st(ts.data(), td.data(), (int)ts.size(), k_, nb_slot_.p, nb_dist_.p, kdist_.p,
+                                   ok_.p, lrd_.p, lrd_ok_.p, store, kstamp_.p, lstamp_.p, epoch_, out_,
+                                   kLofMaxMissing, stream_);
     if (rc != 0) throw std::runtime_error("lof score failed: " + std::to_string(rc));
     return result(sc, missing);
   }
@@ -253,6 +265,11 @@ class LofState {
   DevBuf<int32_t> nb_slot_;
   DevBuf<float> nb_dist_, kdist_, lrd_;
   DevBuf<uint8_t> ok_, lrd_ok_;
+  // staleness stamps (lof.hip): the add epoch that last changed a row's list
+  // (kstamp) and the epoch its lrd was computed at (lstamp); adds stamp
+  // instead of marking every list that names a changed row
+  DevBuf<uint32_t> kstamp_, lstamp_;
+  uint32_t epoch_ = 0;
   DevBuf<int32_t> changed_, nchanged_;
   DevBuf<int32_t> up_[3];
   DevBuf<int32_t> abort_;
