@@ -1619,7 +1619,23 @@ static int topk_onepass_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int 
                                int32_t* scratch_i, float* out_d_host, int32_t* out_i_host,
                                uint32_t* done_host, uint32_t seq, hipStream_t stream);
 
-// path: -1 default, 0 tile, 2 one launch (grid barriers), 3 one pass. Default (measured at 1M rows,
+template <int MODE>
+static int topk_select_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, float* scratch_d,
+                              int32_t* scratch_i, float* out_d_host, int32_t* out_i_host,
+                              uint32_t* done_host, uint32_t seq, hipStream_t stream);
+
+// the LDS-select launch by default (tools/bench_topk_lsh.py, 100 K and 1M
+// rows): for k past kListK while rows x k stays moderate (1M rows: k 31 67 us
+// vs 80, 4 queries k 40 81 vs 131; k 100 106 vs 91 one launch), and for
+// several queries on small tables (100 K rows, 4 x k 10: 38 vs 44 us; at 1M
+// the tile path's multi-query scan wins, 49 vs 92)
+static bool select_default(int64_t nrows, int k, int nq) {
+  if (nrows < 16384) return false;
+  if (k > jb::kListK) return nrows * k <= ((int64_t)64 << 20);
+  return nq > 1 && nrows <= 256 * 1024;
+}
+
+// path: -1 default, 0 tile, 2 one launch (grid barriers), 3 one pass, 4 LDS select. Default (measured at 1M rows,
 // profiles/r03_topk_paths_ab.jsonl): the tile path up to k = kListK (k 10:
 // 58 us vs 86 us one launch, whose two grid barriers cost more than the
 // tile path's second launch), one launch past it (k 100: 94 us vs 224 us,
@@ -1636,6 +1652,11 @@ static int topk_to_host_any(const uint64_t* qbits, const float* qnorm, int nq,
     jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
     return topk_onepass_launch<0>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
                                   done_host, seq, stream);
+  }
+  if (path == 4 || (path < 0 && j == 0 && select_default(nrows, k, nq))) {
+    jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
+    return topk_select_launch<0>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host, done_host,
+                                 seq, stream);
   }
   if (path == 2 || (path < 0 && j == 0 && nrows >= 16384 && k > jb::kListK)) {
     jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
@@ -2361,6 +2382,297 @@ __global__ __launch_bounds__(256) void topk_onepass_kernel(const TopkSrc s, int6
   stamp(6);
 }
 
+// ---------------------------------------------------------------------------
+// Tables up to ~1M rows, k up to kTopMaxK, one launch without a grid barrier
+// (the one-launch kernel above waits twice for every block): B blocks per
+// query stream contiguous ranges in chunks of kSelChunk rows. The rows of a
+// chunk that beat the block's running k-th (all of them until it has k) are
+// appended to LDS after the running top-k, in row order, and an exact select
+// keeps the k smallest (distance key, row) pairs: a radix select over the
+// key's 8-bit digits, stopping at the first digit whose bin holds exactly the
+// pairs still needed; pairs tied on the whole key go by row (the LDS order),
+// so the result stays in row order for the next chunk. The block publishes its
+// k (write-through stores, one counter add); the last block of the query
+// selects the k of the B x k the same way (candidates in block order are in
+// row order), ranks them and writes the results to pinned host memory. A
+// block short of k rows pads with keys above +inf.
+constexpr int kSelThreads = 256;
+constexpr int kSelChunk = 4096;                       // rows per chunk (16 per thread)
+constexpr int kSelRounds = kSelChunk / kSelThreads;   // 16
+constexpr int kSelCap = kSelChunk + kTopMaxK;         // LDS pairs; the last block: B x k <= kSelChunk
+constexpr uint32_t kSelPadKey = 0xffffffffu;          // above dist_key(+inf)
+
+struct SelLds {
+  uint32_t key[kSelCap];
+  uint32_t id[kSelCap];
+  uint32_t tk[kTopMaxK], ti[kTopMaxK];                // the selected pairs
+  uint32_t hist[256];
+  uint32_t cnt[kSelRounds * 4];                       // survivors per (round, wave), then offsets
+  uint32_t wsum[4];
+  uint64_t wmax[4];
+  uint32_t st[4];                                     // digit, count before it, count in it
+};
+
+__device__ __forceinline__ uint64_t sel_comp(uint32_t key, uint32_t id) { return ((uint64_t)key << 32) | id; }
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(v, o, 64);
+    if (lane >= o) v += x;
+  }
+  return v;
+}
+
+// exclusive block scan of v over the 256 threads
+__device__ __forceinline__ uint32_t block_excl_scan(SelLds& L, uint32_t v) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t incl = wave_incl_scan_u32(v, lane);
+  if (lane == 63) L.wsum[w] = incl;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int j = 0; j < w; ++j) off += L.wsum[j];
+  __syncthreads();
+  return off + incl - v;
+}
+
+// the k smallest (key, id) of L[0, n) (n > k, ids increasing with the index
+// among equal keys) -> L[0, k) in index order; returns the largest of them
+// (want_max; else 0)
+__device__ uint64_t block_select(SelLds& L, int n, int k, bool want_max) {
+  const int t = threadIdx.x, lane = t & 63;
+  uint32_t prefix = 0;
+  int need = k, shift = 24;
+  for (;; shift -= 8) {
+    L.hist[t] = 0;
+    __syncthreads();
+    const uint32_t hi = shift == 24 ? 0u : prefix >> (shift + 8);
+    for (int i = t; i < n; i += kSelThreads) {
+      const uint32_t c = L.key[i];
+      if (shift == 24 || (c >> (shift + 8)) == hi) atomicAdd(&L.hist[(c >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {
+      const uint32_t h0 = L.hist[4 * lane], h1 = L.hist[4 * lane + 1];
+      const uint32_t h2 = L.hist[4 * lane + 2], h3 = L.hist[4 * lane + 3];
+      const uint32_t sum = h0 + h1 + h2 + h3;
+      uint32_t run = wave_incl_scan_u32(sum, lane) - sum;
+      const uint32_t hv[4] = {h0, h1, h2, h3};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (run < (uint32_t)need && run + hv[j] >= (uint32_t)need) {
+          L.st[0] = 4 * lane + j;
+          L.st[1] = run;
+          L.st[2] = hv[j];
+        }
+        run += hv[j];
+      }
+    }
+    __syncthreads();
+    const uint32_t digit = L.st[0], before = L.st[1], inbin = L.st[2];
+    prefix |= digit << shift;
+    need -= (int)before;
+    if ((int)inbin == need || shift == 0) break;
+    __syncthreads();                                  // st / hist reused by the next digit
+  }
+  // taken: key digits (down to `shift`) below the prefix, and the first
+  // `need` of those equal to it in index order (all of them when the bin
+  // held exactly `need`). Thread t owns a contiguous index range.
+  const uint32_t lim = prefix >> shift;
+  const int per = (n + kSelThreads - 1) / kSelThreads;
+  const int i0 = t * per, i1 = min(n, i0 + per);
+  uint32_t cs = 0, ct = 0;
+  for (int i = i0; i < i1; ++i) {
+    const uint32_t d = L.key[i] >> shift;
+    cs += d < lim;
+    ct += d == lim;
+  }
+  const uint32_t ex = block_excl_scan(L, cs | (ct << 16));
+  uint32_t sb = ex & 0xffffu, tb = ex >> 16;
+  uint64_t mx = 0;
+  for (int i = i0; i < i1; ++i) {
+    const uint32_t key = L.key[i], d = key >> shift;
+    int pos = -1;
+    if (d < lim) {
+      pos = (int)(sb + min(tb, (uint32_t)need));
+      ++sb;
+    } else if (d == lim) {
+      if (tb < (uint32_t)need) pos = (int)(sb + tb);
+      ++tb;
+    }
+    if (pos >= 0) {
+      L.tk[pos] = key;
+      L.ti[pos] = L.id[i];
+      mx = max(mx, sel_comp(key, L.id[i]));
+    }
+  }
+  if (want_max) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t x = ((uint64_t)(uint32_t)__shfl_xor((int)(mx >> 32), o, 64) << 32) |
+                         (uint32_t)__shfl_xor((int)(uint32_t)mx, o, 64);
+      mx = max(mx, x);
+    }
+    if (lane == 0) L.wmax[t >> 6] = mx;
+  }
+  __syncthreads();
+  for (int i = t; i < k; i += kSelThreads) { L.key[i] = L.tk[i]; L.id[i] = L.ti[i]; }
+  const uint64_t m = want_max ? max(max(L.wmax[0], L.wmax[1]), max(L.wmax[2], L.wmax[3])) : 0ull;
+  __syncthreads();
+  return m;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kSelThreads) void topk_select_kernel(
+    const TopkSrc s, int64_t n, int64_t per_block, int k, float* __restrict__ cand_d,
+    int32_t* __restrict__ cand_i, int cap, uint32_t* __restrict__ counter, float* __restrict__ out_d,
+    int32_t* __restrict__ out_i, volatile uint32_t* done, uint32_t seq) {
+  __shared__ SelLds L;
+  __shared__ uint64_t s_q[kTopMaxWords];
+  __shared__ int s_last;
+  const int q = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  float qn = 0.f;
+  if (MODE == 0) {
+    for (int w = t; w < s.words; w += kSelThreads) s_q[w] = s.qbits[(int64_t)q * s.words + w];
+    qn = s.qnorm[q];
+  }
+  __syncthreads();
+  uint64_t qb[kTopMaxWords];
+#pragma unroll
+  for (int w = 0; w < kTopMaxWords; ++w) qb[w] = (MODE == 0 && w < s.words) ? s_q[w] : 0ull;
+  const int64_t b0 = (int64_t)blockIdx.x * per_block;
+  const int64_t b1 = b0 + per_block < n ? b0 + per_block : n;
+  int have = 0;                                       // the running top-k: L[0, have), row order
+  uint64_t tau = ~0ull;                               // its largest pair once have == k
+  for (int64_t base = b0; base < b1; base += kSelChunk) {
+    const int rows = (int)(b1 - base < kSelChunk ? b1 - base : kSelChunk);
+    int m;
+    if (tau == ~0ull) {
+      // every row goes in (the running set is not full yet): at its own index
+#pragma unroll
+      for (int h = 0; h < kSelRounds / 8; ++h) {
+        constexpr int R = 8;
+        int64_t rr[R], nn[R];
+        float d[R];
+        int ix[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const int j = (h * R + u) * kSelThreads + t;
+          rr[u] = base + j;
+          nn[u] = j < rows ? n : 0;
+        }
+        load_rows<MODE, R>(s, q, nn, rr, qb, qn, d, ix);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const int j = (h * R + u) * kSelThreads + t;
+          if (j < rows) { L.key[have + j] = dist_key(d[u]); L.id[have + j] = (uint32_t)(base + j); }
+        }
+      }
+      m = have + rows;
+      __syncthreads();
+    } else {
+      // only rows below the running k-th, appended in row order
+      uint32_t key[kSelRounds];
+      uint64_t bits = 0;                              // survivor flags per round
+#pragma unroll
+      for (int h = 0; h < kSelRounds / 8; ++h) {
+        constexpr int R = 8;
+        int64_t rr[R], nn[R];
+        float d[R];
+        int ix[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const int j = (h * R + u) * kSelThreads + t;
+          rr[u] = base + j;
+          nn[u] = j < rows ? n : 0;
+        }
+        load_rows<MODE, R>(s, q, nn, rr, qb, qn, d, ix);
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const int r = h * R + u;
+          const int j = r * kSelThreads + t;
+          key[r] = dist_key(d[u]);
+          const bool sv = j < rows && sel_comp(key[r], (uint32_t)(base + j)) < tau;
+          const uint64_t bm = __ballot(sv);
+          if (lane == 0) L.cnt[r * 4 + wv] = (uint32_t)__popcll(bm);
+          if (sv) bits |= 1ull << r;
+        }
+      }
+      __syncthreads();
+      if (t < 64) {                                   // offsets of (round, wave) in row order
+        const uint32_t c = L.cnt[lane];
+        const uint32_t inc = wave_incl_scan_u32(c, lane);
+        L.cnt[lane] = inc - c;
+        if (lane == 63) L.st[3] = inc;                // the chunk's survivors
+      }
+      __syncthreads();
+      m = have + (int)L.st[3];
+#pragma unroll
+      for (int r = 0; r < kSelRounds; ++r) {
+        const bool sv = (bits >> r) & 1ull;
+        const uint64_t bm = __ballot(sv);
+        if (sv) {
+          const int pos = have + (int)L.cnt[r * 4 + wv] + __popcll(bm & ((1ull << lane) - 1ull));
+          L.key[pos] = key[r];
+          L.id[pos] = (uint32_t)(base + r * kSelThreads + t);
+        }
+      }
+      __syncthreads();
+    }
+    if (m > k) {
+      tau = block_select(L, m, k, base + kSelChunk < b1);
+      have = k;
+    } else {
+      have = m;
+    }
+  }
+  __syncthreads();
+  // publish the block's k (pads above +inf with distinct ids when short)
+  float* cd = cand_d + (int64_t)q * cap;
+  int32_t* ci = cand_i + (int64_t)q * cap;
+  for (int j = t; j < k; j += kSelThreads) {
+    const uint32_t key = j < have ? L.key[j] : kSelPadKey;
+    const uint32_t id = j < have ? L.id[j] : (0x80000000u | (uint32_t)(blockIdx.x * kTopMaxK + j));
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(cd) + (int64_t)blockIdx.x * k + j, key, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(ci) + (int64_t)blockIdx.x * k + j, id, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  uint32_t* qc = counter + (int64_t)q * kFuseSync;
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(qc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  // the last block: the k of the B x k candidates, ranked
+  const int nc = (int)gridDim.x * k;
+  for (int j = t; j < nc; j += kSelThreads) {
+    L.key[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(cd) + j, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    L.id[j] = __hip_atomic_load(reinterpret_cast<const uint32_t*>(ci) + j, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (nc > k) block_select(L, nc, k, false);
+  float* od = out_d + (int64_t)q * k;
+  int32_t* oi = out_i + (int64_t)q * k;
+  for (int i = t; i < k; i += kSelThreads) {
+    const uint64_t c = sel_comp(L.key[i], L.id[i]);
+    int rank = 0;
+    for (int j = 0; j < k; ++j) rank += sel_comp(L.key[j], L.id[j]) < c;
+    const uint32_t key = L.key[i];
+    const bool fin = key < dist_key(INFINITY);
+    od[rank] = fin ? key_dist(key) : INFINITY;
+    oi[rank] = fin ? (int32_t)L.id[i] : INT_MAX;
+  }
+  if (t == 0) __hip_atomic_store(qc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) done[q] = seq;
+}
+
 }  // namespace jb
 
 // blocks of one fused launch that are resident at once (all queries): the
@@ -2388,7 +2700,12 @@ static int topk_fused_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k,
                              int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
                              hipStream_t stream) {
   uint32_t* st = (uint32_t*)(scratch_i + kFuseStateOff);
-  int64_t B = (nrows + 1023) / 1024;
+  static const int64_t rows_per_block = [] {
+    const char* e = getenv("JB_FUSE_ROWS");                // diagnostics: rows per block
+    const long v = e != nullptr ? atol(e) : 0;
+    return (int64_t)(v >= 256 ? v : 1024);
+  }();
+  int64_t B = (nrows + rows_per_block - 1) / rows_per_block;
   const int64_t bmax = fused_resident_blocks() / nq;
   if (B > bmax) B = bmax;
   if (B < 1) B = 1;
@@ -2424,8 +2741,30 @@ static int topk_onepass_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int 
   return (int)hipGetLastError();
 }
 
+// one-launch select path (k <= kTopMaxK): ~2048 rows a block, B x k
+// candidates at most kSelChunk (the last block's LDS); counter as the one-pass
+// launch's (each leaves it zero)
+template <int MODE>
+static int topk_select_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, float* scratch_d,
+                              int32_t* scratch_i, float* out_d_host, int32_t* out_i_host,
+                              uint32_t* done_host, uint32_t seq, hipStream_t stream) {
+  if (k > jb::kTopMaxK || nq > 8) return -2;
+  uint32_t* counter = (uint32_t*)(scratch_i + kFuseStateOff) + 16 * kRadixBins + 3;
+  int64_t B = (nrows + 2047) / 2048;
+  const int64_t bmax = jb::kSelChunk / k;
+  if (B > bmax) B = bmax;
+  if (B > 256) B = 256;
+  if (B < 1) B = 1;
+  const int64_t per_block = (nrows + B - 1) / B;
+  B = (nrows + per_block - 1) / per_block;
+  hipLaunchKernelGGL(jb::topk_select_kernel<MODE>, dim3((unsigned)B, nq), dim3(jb::kSelThreads), 0, stream, s,
+                     nrows, per_block, k, scratch_d + 64, scratch_i + 64, kCandCap, counter, out_d_host,
+                     out_i_host, (volatile uint32_t*)done_host, seq);
+  return (int)hipGetLastError();
+}
+
 // path: 0 tile scan + merge, 1 radix chain (6 launches + memset), 2 one launch
-// (grid barriers), 3 one pass (k <= kListK)
+// (grid barriers), 3 one pass (k <= kListK), 4 one launch, LDS select
 static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k, int path,
                               float* scratch_d, int32_t* scratch_i, float* out_d_host,
                               int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
@@ -2436,6 +2775,9 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
   if (path == 3)
     return topk_onepass_launch<1>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
                                   done_host, seq, stream);
+  if (path == 4)
+    return topk_select_launch<1>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
+                                 done_host, seq, stream);
   if (path == 0) {
     const int blocks = jb_topk_blocks(nrows, k);
     const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
@@ -2494,7 +2836,11 @@ extern "C" int jb_topk_scores_direct_path(const float* src_d, int flip, int nq, 
   if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
   if (k > jb::kTopMaxK || nq > 8) return -2;
   jb::TopkSrc s{nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, src_d, nullptr, flip};
-  const int path = nrows >= 16384 ? (path_sel < 0 ? 1 : path_sel) : 0;
+  // default: one query on the LDS select (tools/bench_topk_scores.py, 1M rows:
+  // k 10 44-56 us vs 47-101 on the radix chain, which degrades on quantized
+  // scores - k 100 with 64 score levels: 105 vs 631 us); several queries on
+  // the chain (4 x k 10: 55-66 vs 71-78 us without ties)
+  const int path = nrows >= 16384 ? (path_sel < 0 ? (nq == 1 ? 4 : 1) : path_sel) : 0;
   uint32_t seq = jb::next_seq();
   int rc = topk_scores_launch(s, nq, nrows, k, path, scratch_d, scratch_i, out_d_host,
                               out_i_host, done_host, seq, stream);

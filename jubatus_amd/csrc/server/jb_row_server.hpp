@@ -1020,18 +1020,46 @@ class Model : public jb::mix::Mixable {
         for (size_t i : kv.second) rs[i]->err = std::current_exception();
       }
     }
+    // the batch's calc_score queries: one LOF launch each, one wait; a query
+    // that meets rows without a valid list is finished alone below
+    std::vector<size_t> sq;
+    std::vector<std::vector<int32_t>> sts;
+    std::vector<std::vector<float>> std_;
+    std::vector<float> ssc;
+    std::vector<char> sdone;
     for (size_t i = 0; i < n; ++i) {
       QReq* r = rs[i];
+      if (r->err || r->kind != QReq::kScore) continue;
+      sq.push_back(i);
+      sts.emplace_back();
+      std_.emplace_back();
+      for (const Hit& hh : hits[i])
+        if (live(hh.slot)) { sts.back().push_back(hh.slot); std_.back().push_back(hh.dist); }
+    }
+    if (sq.size() > 1) {
+      try {
+        state().score_many(sts, std_, &ssc, &sdone);
+      } catch (...) {
+        for (size_t i : sq) rs[i]->err = std::current_exception();
+      }
+    }
+    for (size_t j = 0; j < sq.size(); ++j) {
+      QReq* r = rs[sq[j]];
       if (r->err) continue;
+      try {
+        if (sq.size() > 1 && sdone[j]) r->score = (double)ssc[j];
+        else if (sts[j].empty()) r->score = 1.0;
+        else r->score = (double)score_from(sts[j], std_[j], -1);
+      } catch (...) {
+        r->err = std::current_exception();
+      }
+    }
+    for (size_t i = 0; i < n; ++i) {
+      QReq* r = rs[i];
+      if (r->err || r->kind == QReq::kScore) continue;
       try {
         if (r->kind == QReq::kDatum) {
           r->res = eng_->results(hits[i], r->similar);
-        } else if (r->kind == QReq::kScore) {
-          std::vector<int32_t> ts;
-          std::vector<float> td;
-          for (const Hit& hh : hits[i])
-            if (live(hh.slot)) { ts.push_back(hh.slot); td.push_back(hh.dist); }
-          r->score = (double)score_from(ts, td, -1);
         } else {
           const int32_t s = eng_->slot(r->id);
           if (s < 0) throw std::runtime_error("'row not found: " + r->id + "'");   // str(KeyError)

@@ -487,14 +487,15 @@ def test_topk_16_wave_path_matches_full_sort(k):
                                               ("random", 10, 3, 0), ("ties", 10, 2, 1),
                                               ("ties", 100, 1, 1), ("sparse_valid", 20, 2, 1),
                                               ("levels", 10, 4, 0), ("levels", 31, 2, 2)])
-@pytest.mark.parametrize("path", [-1, 2, 3])
+@pytest.mark.parametrize("path", [-1, 2, 3, 4])
 def test_direct_topk_one_launch_path(case, k, nq, metric, path):
     """latency top-k below the sampled path's 2M rows: ONE launch
     (csrc/hip/topk.hip topk_fused_kernel: distances cached in LDS, two radix
     levels across grid barriers, last-block selection) == full distance
     matrix + stable sort; also the default choice (-1) and the one-pass
     kernel (3, topk_onepass_kernel: register lists, last-block merge; k <= 16
-    only). "ties" (every row at one distance: the candidates
+    only) and the LDS radix-select kernel (4, topk_select_kernel: per-block
+    exact top-k over (distance, row) composites, last-block select). "ties" (every row at one distance: the candidates
     overflow the LDS ranking and k > 16 retries on the tile path, k <= 16
     selects from L2), "levels" (8 distinct signatures: ~125k rows per
     distance level) and "sparse_valid" (fewer valid rows than k)"""

@@ -20,7 +20,7 @@ def _oracle(sc, k, flip):
 
 @pytest.mark.parametrize("frac,levels", [(0.01, 0), (0.2, 0), (0.2, 64), (0.00001, 0)])
 @pytest.mark.parametrize("nq", [1, 3])
-@pytest.mark.parametrize("path", [-1, 1, 2, 3])
+@pytest.mark.parametrize("path", [-1, 1, 2, 3, 4])
 def test_scores_topk_matches_oracle(frac, levels, nq, path):
     from jubatus_amd.ops import hip
     dev = torch.device("cuda", 0)
@@ -57,7 +57,7 @@ def test_scores_topk_repeated_calls_reset_counters():
         np.testing.assert_array_equal(idx[0], ri)
 
 
-@pytest.mark.parametrize("k,path", [(16, -1), (20, -1), (16, 2), (20, 2), (16, 3)])
+@pytest.mark.parametrize("k,path", [(16, -1), (20, -1), (16, 2), (20, 2), (16, 3), (20, 4), (100, 4)])
 def test_scores_topk_ties_list_and_rank_paths(k, path):
     """~1000 rows tied at the threshold: k <= 16 merges register lists, larger
     k ranks the candidates (early exit once a candidate is out of the top k)"""

@@ -31,7 +31,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--cases", default="1:10,4:10,1:100", help="nq:k pairs")
+    ap.add_argument("--paths", default="tile,fused,onepass,select,default")
+    ap.add_argument("--metrics", default="1,0")
     a = ap.parse_args()
+    cases = [tuple(int(x) for x in c.split(":")) for c in a.cases.split(",")]
+    paths = [p for p in (("tile", 0), ("fused", 2), ("onepass", 3), ("select", 4), ("default", -1))
+             if p[0] in a.paths.split(",")]
     d = torch.device("cuda", 0)
     n = a.rows
     g = torch.Generator().manual_seed(0)
@@ -39,13 +45,13 @@ def main():
     tn = torch.rand(n, generator=g)
     valid = torch.ones(n, dtype=torch.uint8)
     bufs = hip.DirectQueryBuffers(d, 1)
-    for metric in (1, 0):
-        for nq, k in ((1, 10), (4, 10), (1, 100)):
+    for metric in (int(m) for m in a.metrics.split(",")):
+        for nq, k in cases:
             qb = torch.randint(-2**62, 2**62, (nq, 1), generator=g, dtype=torch.int64)
             qn = torch.rand(nq, generator=g)
             t = tuple(x.to(d) for x in (qb, qn, tb, tn, valid))
             ref = None
-            for name, path in (("tile", 0), ("fused", 2), ("onepass", 3), ("default", -1)):
+            for name, path in paths:
                 if path == 3 and k > 16:
                     continue
                 lat = []
@@ -57,6 +63,7 @@ def main():
                 if ref is None:
                     ref = idx
                 print(json.dumps({"rows": n, "metric": metric, "nq": nq, "k": k, "path": name,
+                                  "fuse_rows": os.environ.get("JB_FUSE_ROWS", ""),
                                   "p50_us": round(float(np.median(lat)), 1),
                                   "p90_us": round(float(np.percentile(lat, 90)), 1),
                                   "same_rows_as_tile": bool(np.array_equal(idx, ref)),

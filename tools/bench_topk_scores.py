@@ -17,7 +17,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from jubatus_amd.ops import hip  # noqa: E402
 
-PATHS = {"tile": 0, "chain": 1, "fused": 2, "onepass": 3, "default": -1}
+PATHS = {"tile": 0, "chain": 1, "fused": 2, "onepass": 3, "select": 4, "default": -1}
 
 
 def run(sc, nq, rows, k, path, bufs):
