@@ -31,6 +31,7 @@ namespace jb {
 
 constexpr int kLofMaxK = 64;
 constexpr int kLofMaxChanged = 1024;
+constexpr int kLofU = 8;                // cooperative loads in flight per thread
 
 __device__ __forceinline__ float lof_kth(const int32_t* s, const float* d, int k, int ignore_same) {
   float kd = 0.f;
@@ -59,8 +60,8 @@ struct LofLds {
   float d[64][kLofMaxK + 1];
   float kd[64][kLofMaxK + 1];
   uint8_t okb[64][kLofMaxK + 1];
-  uint8_t ok1[64], stale[64];
-  float kd1[64], lrd1[64];
+  uint8_t ok1[64], stale[64], lok1[64], chg[64];
+  float kd1[64], lrd1[64], lr1[64];
   uint32_t lst[64];
   int n_ch, nmiss;
 };
@@ -80,7 +81,13 @@ __device__ __forceinline__ void lof_insert_body(
     int ignore_same, int32_t* __restrict__ nb_slot, float* __restrict__ nb_dist,
     float* __restrict__ kdist, uint8_t* __restrict__ ok, uint8_t* __restrict__ lrd_ok,
     int32_t* __restrict__ changed, int32_t* __restrict__ nchanged, bool first, LofLds& L,
-    uint32_t* __restrict__ kstamp = nullptr, uint32_t epoch = 0) {
+    uint32_t* __restrict__ kstamp = nullptr, uint32_t epoch = 0, const float* __restrict__ lrd = nullptr,
+    const uint32_t* __restrict__ lstamp = nullptr) {
+  // fused (lrd non-null, nc <= 64): candidate c's fields the score needs -
+  // ok, lrd_ok, lrd, kdist, lstamp, as they stand after this insert - are
+  // left in L (ok1, lok1, lr1, kd1, lst) and its list in L.s / L.d[c]: the
+  // score of p (its targets are the head of the candidates) reads them there
+  const bool fused = lrd != nullptr;
   int& n_ch = L.n_ch;
   auto& l_s = L.s;
   auto& l_d = L.d;
@@ -103,17 +110,50 @@ __device__ __forceinline__ void lof_insert_body(
   }
   for (int c0 = 0; c0 < nc; c0 += 64) {
     const int cn = nc - c0 < 64 ? nc - c0 : 64;
-    for (int e = t; e < cn * k; e += 64) {
-      const int c = e / k, j = e - c * k;
-      const int32_t o = cs[c0 + c];
-      if (o >= 0 && o != p) {
-        l_s[c][j] = nb_slot[(int64_t)o * k + j];
-        l_d[c][j] = nb_dist[(int64_t)o * k + j];
+    // the candidate's own flags first (issued with the list loads below)
+    uint8_t f_ok = 0, f_lok = 0;
+    float f_lr = 0.f, f_kd = 0.f;
+    uint32_t f_lst = 0;
+    if (t < cn) {
+      const int32_t o = cs[c0 + t];
+      const int32_t oc = o >= 0 ? o : p;
+      f_ok = ok[oc];
+      if (fused) {
+        f_lok = lrd_ok[oc];
+        f_lr = lrd[oc];
+        f_kd = kdist[oc];
+        f_lst = lstamp != nullptr ? lstamp[oc] : 0u;
+      }
+      if (o < 0 || o == p) f_ok = 0;
+    }
+    // kLofU loads of each array in flight per thread before the first LDS
+    // store (a load -> store loop waits one memory latency per entry)
+    for (int e0 = t; e0 < cn * k; e0 += 64 * kLofU) {
+      int32_t vs[kLofU];
+      float vd[kLofU];
+#pragma unroll
+      for (int u = 0; u < kLofU; ++u) {
+        const int e = e0 + 64 * u;
+        const int c = e < cn * k ? e / k : 0, j = e - c * k;
+        const int32_t o = cs[c0 + c];
+        const int64_t at = (int64_t)(o >= 0 ? o : p) * k + (e < cn * k ? j : 0);
+        vs[u] = nb_slot[at];
+        vd[u] = nb_dist[at];
+      }
+#pragma unroll
+      for (int u = 0; u < kLofU; ++u) {
+        const int e = e0 + 64 * u;
+        if (e < cn * k) {
+          const int c = e / k, j = e - c * k;
+          l_s[c][j] = vs[u];
+          l_d[c][j] = vd[u];
+        }
       }
     }
     if (t < cn) {
-      const int32_t o = cs[c0 + t];
-      l_ok[t] = (o >= 0 && o != p) ? ok[o] : 0;
+      L.chg[t] = 0;
+      l_ok[t] = f_ok;
+      if (fused) { L.lok1[t] = f_lok; L.lr1[t] = f_lr; L.kd1[t] = f_kd; L.lst[t] = f_lst; }
     }
     __syncthreads();
     if (t < cn && l_ok[t]) {
@@ -138,18 +178,26 @@ __device__ __forceinline__ void lof_insert_body(
         for (int j = (n < k ? n : k - 1); j > at; --j) { ts[j] = ts[j - 1]; td[j] = td[j - 1]; }
         if (at < k) { ts[at] = p; td[at] = d; }
         const int m = n < k ? n + 1 : k;
-        int32_t* os = nb_slot + (int64_t)o * k;
-        float* od = nb_dist + (int64_t)o * k;
-        for (int j = 0; j < k; ++j) {
-          if (j >= m) { ts[j] = -1; td[j] = INFINITY; }
-          os[j] = ts[j];
-          od[j] = td[j];
-        }
-        kdist[o] = lof_kth(ts, td, k, ignore_same);
+        for (int j = m; j < k; ++j) { ts[j] = -1; td[j] = INFINITY; }
+        L.chg[t] = 1;                           // written back below, row by row
+        const float kd = lof_kth(ts, td, k, ignore_same);
+        kdist[o] = kd;
         lrd_ok[o] = 0;
         if (kstamp != nullptr) kstamp[o] = epoch;
+        if (fused) { L.kd1[t] = kd; L.lok1[t] = 0; }
         const int w = atomicAdd(&n_ch, 1);
         if (w < kLofMaxChanged) changed[w] = o;
+      }
+    }
+    __syncthreads();
+    // the changed lists back to HBM, consecutive lanes on consecutive entries
+    // of a row (a lane per row would touch 64 rows per store instruction)
+    for (int e = t; e < cn * k; e += 64) {
+      const int c = e / k, j = e - c * k;
+      if (L.chg[c]) {
+        const int64_t at = (int64_t)cs[c0 + c] * k + j;
+        nb_slot[at] = l_s[c][j];
+        nb_dist[at] = l_d[c][j];
       }
     }
     __syncthreads();
@@ -276,7 +324,15 @@ __device__ __forceinline__ void lof_score_body(
     const float* __restrict__ kdist, const uint8_t* __restrict__ ok, float* __restrict__ lrd,
     uint8_t* __restrict__ lrd_ok, int store_slot, uint32_t* __restrict__ out, int max_missing,
     int32_t* __restrict__ abort_flag, LofLds& L, const uint32_t* __restrict__ kstamp = nullptr,
-    uint32_t* __restrict__ lstamp = nullptr, uint32_t epoch = 0) {
+    uint32_t* __restrict__ lstamp = nullptr, uint32_t epoch = 0, bool defer = false, bool have_lists = false) {
+  // have_lists: the targets' lists and fields are in L already (the fused
+  // insert left them there; targets = its candidates' head)
+  // defer: out is device scratch the caller copies to the host later - plain
+  // stores, no waits for acknowledgements (a batch of adds in one launch)
+  auto put = [&](uint32_t* at, uint32_t v) {
+    if (defer) *at = v;
+    else sys_store(at, v);
+  };
   // the targets' lists and their rows' flags / k-distances (and stamps) are
   // fetched in two cooperative rounds (every load of a round in flight at
   // once), then each target's thread works from LDS
@@ -292,7 +348,13 @@ __device__ __forceinline__ void lof_score_body(
   if (t == 0) nmiss = 0;
   uint8_t lok = 0;
   float lr = 0.f;
-  if (t < nt) {
+  if (have_lists) {
+    if (t < nt) {
+      lok = L.lok1[t];
+      lr = L.lr1[t];
+      L.stale[t] = 0;
+    }
+  } else if (t < nt) {
     const int32_t o = ts[t];
     s_ok[t] = ok[o];
     lok = lrd_ok[o];
@@ -301,26 +363,61 @@ __device__ __forceinline__ void lof_score_body(
     L.stale[t] = 0;
     if (kstamp != nullptr) L.lst[t] = lstamp[o];
   }
-  for (int e = t; e < nt * k; e += blockDim.x) {
-    const int c = e / k, j = e - c * k;
-    const int64_t at = (int64_t)ts[c] * k + j;
-    l_s[c][j] = nb_slot[at];
-    l_d[c][j] = nb_dist[at];
+  for (int e0 = t; e0 < (have_lists ? 0 : nt * k); e0 += 64 * kLofU) {
+    int32_t vs[kLofU];
+    float vd[kLofU];
+#pragma unroll
+    for (int u = 0; u < kLofU; ++u) {
+      const int e = e0 + 64 * u < nt * k ? e0 + 64 * u : 0;
+      const int c = e / k, j = e - c * k;
+      const int64_t at = (int64_t)ts[c] * k + j;
+      vs[u] = nb_slot[at];
+      vd[u] = nb_dist[at];
+    }
+#pragma unroll
+    for (int u = 0; u < kLofU; ++u) {
+      const int e = e0 + 64 * u;
+      if (e < nt * k) {
+        const int c = e / k, j = e - c * k;
+        l_s[c][j] = vs[u];
+        l_d[c][j] = vd[u];
+      }
+    }
   }
   __syncthreads();
-  for (int e = t; e < nt * k; e += blockDim.x) {
-    const int c = e / k, j = e - c * k;
-    const int32_t x = l_s[c][j];
-    if (s_ok[c] && x >= 0) {     // a list is valid (in range) only while its row is ok
-      l_ok[c][j] = ok[x];
-      l_kd[c][j] = kdist[x];
-      if (kstamp != nullptr && kstamp[x] > L.lst[c]) L.stale[c] = 1;
+  for (int e0 = t; e0 < nt * k; e0 += 64 * kLofU) {
+    uint8_t vo[kLofU];
+    float vk[kLofU];
+    uint32_t vt[kLofU];
+#pragma unroll
+    for (int u = 0; u < kLofU; ++u) {
+      const int e = e0 + 64 * u;
+      const int c = e < nt * k ? e / k : 0, j = e - c * k;
+      const int32_t x = e < nt * k ? l_s[c][j] : -1;
+      // a list is valid (in range) only while its row is ok
+      const int32_t xr = (s_ok[c] && x >= 0) ? x : 0;
+      vo[u] = ok[xr];
+      vk[u] = kdist[xr];
+      vt[u] = kstamp != nullptr ? kstamp[xr] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kLofU; ++u) {
+      const int e = e0 + 64 * u;
+      if (e < nt * k) {
+        const int c = e / k, j = e - c * k;
+        const int32_t x = l_s[c][j];
+        if (s_ok[c] && x >= 0) {
+          l_ok[c][j] = vo[u];
+          l_kd[c][j] = vk[u];
+          if (kstamp != nullptr && vt[u] > L.lst[c]) L.stale[c] = 1;
+        }
+      }
     }
   }
   __syncthreads();
   auto miss = [&](int32_t s) {
     const int w = atomicAdd(&nmiss, 1);
-    if (w < max_missing) sys_store(out + 4 + w, (uint32_t)s);
+    if (w < max_missing) put(out + 4 + w, (uint32_t)s);
   };
   if (t < nt) {
     const int32_t o = ts[t];
@@ -351,15 +448,16 @@ __device__ __forceinline__ void lof_score_body(
   // the host reads out[] once out[0] is set: every thread's system-scope
   // stores are acknowledged before the barrier, the status goes last (a
   // system-scope release fence would write back the whole L2 instead)
-  sys_stores_block_done();
+  if (defer) __syncthreads();
+  else sys_stores_block_done();
   if (t != 0) return;
   if (nmiss > 0) {
     // a batch of adds stops here: the host installs the missing lists and
     // scores this add again before the later ones run (sequential order)
     if (abort_flag != nullptr) *abort_flag = 1;
-    sys_store(out + 3, (uint32_t)(nmiss < max_missing ? nmiss : max_missing));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    sys_store(out, 2u);
+    put(out + 3, (uint32_t)(nmiss < max_missing ? nmiss : max_missing));
+    if (!defer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    put(out, 2u);
     return;
   }
   // lrd of the query point itself (its own neighbours' k-distances)
@@ -385,11 +483,11 @@ __device__ __forceinline__ void lof_score_body(
     lrd_ok[store_slot] = 1;
     if (lstamp != nullptr) lstamp[store_slot] = epoch;
   }
-  sys_store(out + 1, __float_as_uint(score));
-  sys_store(out + 2, __float_as_uint(lp));
-  sys_store(out + 3, 0u);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  sys_store(out, 1u);
+  put(out + 1, __float_as_uint(score));
+  put(out + 2, __float_as_uint(lp));
+  put(out + 3, 0u);
+  if (!defer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  put(out, 1u);
 }
 
 __global__ __launch_bounds__(64) void lof_score_kernel(
@@ -431,13 +529,80 @@ __global__ __launch_bounds__(64) void lof_add_score_kernel(
   __shared__ LofLds L;
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
   __syncthreads();
+  const bool fz = a.n <= 64;                         // targets' lists stay in LDS
   lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
-                  nchanged, true, L, kstamp, epoch);
+                  nchanged, true, L, kstamp, epoch, fz ? lrd : nullptr, lstamp);
   // the insert's global stores are visible to the block after the barrier
   __syncthreads();
   const int nt = a.n < k ? a.n : k;
   lof_score_body(cs, cd, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, p, out, max_missing,
-                 abort_flag, L, kstamp, lstamp, epoch);
+                 abort_flag, L, kstamp, lstamp, epoch, false, fz);
+}
+
+// A batch of adds in one launch, in order (one block loops over them: no
+// launch or inter-kernel gap per add): add i (epoch epoch0 + i) inserts p =
+// ps[i] with its nc[i] candidates, then scores it into out + i * out_stride.
+// The candidates are read from pinned host memory once, into cand (device
+// scratch, [nadd][stride] slots then distances). An add that meets rows
+// without a valid list stops the batch there (status 2); the later ones get
+// status 3 (not run) and the host resubmits them after finishing it.
+__global__ __launch_bounds__(64) void lof_add_batch_kernel(
+    int nadd, const int32_t* __restrict__ ps, const int32_t* __restrict__ nc, const int32_t* __restrict__ cs_h,
+    const float* __restrict__ cd_h, int stride, int k, int ignore_same, int32_t* __restrict__ nb_slot,
+    float* __restrict__ nb_dist, float* __restrict__ kdist, uint8_t* __restrict__ ok, float* __restrict__ lrd,
+    uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged,
+    uint32_t* __restrict__ kstamp, uint32_t* __restrict__ lstamp, uint32_t epoch0, int32_t* __restrict__ cand,
+    uint32_t* __restrict__ res, uint32_t* __restrict__ out, int out_stride, int max_missing) {
+  __shared__ int32_t cs[kLofArgMax];
+  __shared__ float cd[kLofArgMax];
+  __shared__ int32_t s_p[64], s_n[64];
+  __shared__ LofLds L;
+  const int t = threadIdx.x;
+  const int tot = nadd * stride;
+  float* cand_d = reinterpret_cast<float*>(cand + tot);
+  for (int e0 = t; e0 < tot; e0 += 64 * kLofU) {  // one pass over host memory, kLofU loads in flight
+    int32_t vs[kLofU];
+    float vd[kLofU];
+#pragma unroll
+    for (int u = 0; u < kLofU; ++u) {
+      const int e = e0 + 64 * u < tot ? e0 + 64 * u : 0;
+      vs[u] = cs_h[e];
+      vd[u] = cd_h[e];
+    }
+#pragma unroll
+    for (int u = 0; u < kLofU; ++u)
+      if (e0 + 64 * u < tot) { cand[e0 + 64 * u] = vs[u]; cand_d[e0 + 64 * u] = vd[u]; }
+  }
+  if (t < nadd) { s_p[t] = ps[t]; s_n[t] = nc[t]; }
+  __syncthreads();
+  int ran = nadd;
+  for (int i = 0; i < nadd; ++i) {
+    const int n = s_n[i], p = s_p[i];
+    for (int e = t; e < n; e += blockDim.x) { cs[e] = cand[i * stride + e]; cd[e] = cand_d[i * stride + e]; }
+    __syncthreads();
+    const bool fz = n <= 64;                         // targets' lists stay in LDS
+    lof_insert_body(p, cs, cd, n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed, nchanged, true,
+                    L, kstamp, epoch0 + (uint32_t)i, fz ? lrd : nullptr, lstamp);
+    __syncthreads();
+    lof_score_body(cs, cd, n < k ? n : k, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, p,
+                   res + (int64_t)i * out_stride, max_missing, nullptr, L, kstamp, lstamp, epoch0 + (uint32_t)i,
+                   true, fz);
+    __syncthreads();
+    if (L.nmiss > 0) { ran = i + 1; break; }      // stopped: the later adds did not run
+  }
+  // results to the host: every word but the statuses, acknowledged, then the
+  // statuses (the last add's last: the host waits for it)
+  const int nm = L.nmiss > 0 ? (L.nmiss < max_missing ? L.nmiss : max_missing) : 0;
+  for (int i = t; i < ran; i += blockDim.x)
+    for (int w = 1; w < 4; ++w) sys_store(out + (int64_t)i * out_stride + w, res[(int64_t)i * out_stride + w]);
+  for (int w = t; w < nm; w += blockDim.x)
+    sys_store(out + (int64_t)(ran - 1) * out_stride + 4 + w, res[(int64_t)(ran - 1) * out_stride + 4 + w]);
+  sys_stores_block_done();
+  for (int i = t; i < nadd - 1; i += blockDim.x)
+    sys_store(out + (int64_t)i * out_stride, i < ran ? res[(int64_t)i * out_stride] : 3u);
+  sys_stores_block_done();
+  const int64_t last = (int64_t)(nadd - 1) * out_stride;
+  if (t == 0) sys_store(out + last, nadd - 1 < ran ? res[last] : 3u);
 }
 
 }  // namespace jb
@@ -538,36 +703,31 @@ extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int
                        changed, nchanged, nullptr, nullptr, 0, out_host, max_missing, stream);
 }
 
-// A batch of adds in arrival order, one wait: add i (epoch epoch0 + i; one
-// lof_add_score_kernel, score into out_host + i * out_stride) is enqueued
-// behind add i - 1's without a host round trip. An add whose score finds
-// rows without a valid list sets *abort_dev; every later kernel of the batch
-// then exits (status 3) and the host finishes that add (missing lists
-// installed, scored again) before it resubmits the rest - the order of the
-// sequential adds. cs / cd: [nadd][stride] candidates (ascending, p
-// excluded), nc[i] of them.
+// A batch of adds in arrival order, one launch and one wait
+// (lof_add_batch_kernel). ps / nc / cs / cd: pinned host memory the kernel
+// reads ([nadd][stride] candidates, ascending, p excluded); cand: device
+// scratch of 2 x nadd x stride words, res: of nadd x out_stride (the results
+// before they go to the host); out_host[i * out_stride] = status 1
+// done, 2 stopped on rows without a valid list (its insert is applied, its
+// score is not), 3 not run.
 extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd,
                                const int32_t* nc, int stride, int k, int ignore_same, int32_t* nb_slot,
                                float* nb_dist, float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                                int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp,
-                               uint32_t epoch0, uint32_t* out_host, int out_stride, int max_missing,
-                               int32_t* abort_dev, hipStream_t stream) {
+                               uint32_t epoch0, int32_t* cand, uint32_t* res, uint32_t* out_host, int out_stride,
+                               int max_missing, hipStream_t stream) {
   if (nadd <= 0) return 0;
-  if (k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax || kstamp == nullptr || lstamp == nullptr)
+  if (nadd > 64 || k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax || kstamp == nullptr ||
+      lstamp == nullptr)
     return -2;
-  hipError_t e = hipMemsetAsync(abort_dev, 0, sizeof(int32_t), stream);
-  if (e != hipSuccess) return (int)e;
-  for (int i = 0; i < nadd; ++i) out_host[(int64_t)i * out_stride] = 0;
-  jb::LofArgs a;
   for (int i = 0; i < nadd; ++i) {
-    const int n = nc[i];
-    int rc = fill_args(&a, cs + (int64_t)i * stride, cd + (int64_t)i * stride, n < 0 ? 0 : n);
-    if (rc) return rc;
-    hipLaunchKernelGGL(jb::lof_add_score_kernel, dim3(1), dim3(64), 0, stream, a, ps[i], k, ignore_same,
-                       nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, changed, nchanged, kstamp, lstamp,
-                       epoch0 + (uint32_t)i, out_host + (int64_t)i * out_stride, max_missing, abort_dev);
+    if (nc[i] < 0 || nc[i] > stride) return -2;
+    out_host[(int64_t)i * out_stride] = 0;
   }
-  e = hipGetLastError();
+  hipLaunchKernelGGL(jb::lof_add_batch_kernel, dim3(1), dim3(64), 0, stream, nadd, ps, nc, cs, cd, stride, k,
+                     ignore_same, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, changed, nchanged, kstamp, lstamp,
+                     epoch0, cand, res, out_host, out_stride, max_missing);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host + (int64_t)(nadd - 1) * out_stride, stream);
 }
@@ -591,6 +751,32 @@ extern "C" int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host, stream);
+}
+
+// Several independent scores (calc_score of a batch of queries), one wait:
+// query i's targets are ts / td [i * stride, + nt[i]), its status and score
+// go to out_host + i * out_stride. The kernels only refresh cached lrd values
+// (the same values in any order); a query that finds rows without a valid
+// list reports them (status 2) and the host finishes it alone.
+extern "C" int jb_lof_score_many(int nq, const int32_t* ts, const float* td, const int32_t* nt, int stride,
+                                 int k, const int32_t* nb_slot, const float* nb_dist, const float* kdist,
+                                 const uint8_t* ok, float* lrd, uint8_t* lrd_ok, const uint32_t* kstamp,
+                                 uint32_t* lstamp, uint32_t epoch, uint32_t* out_host, int out_stride,
+                                 int max_missing, hipStream_t stream) {
+  if (nq <= 0) return 0;
+  if (k > jb::kLofMaxK || stride > 64) return -2;
+  for (int i = 0; i < nq; ++i) out_host[(int64_t)i * out_stride] = 0;
+  jb::LofArgs a;
+  for (int i = 0; i < nq; ++i) {
+    int rc = fill_args(&a, ts + (int64_t)i * stride, td + (int64_t)i * stride, nt[i]);
+    if (rc) return rc;
+    hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist, kdist, ok,
+                       lrd, lrd_ok, -1, out_host + (int64_t)i * out_stride, max_missing, (int32_t*)nullptr,
+                       kstamp, lstamp, epoch);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return jb::wait_nonzero(out_host + (int64_t)(nq - 1) * out_stride, stream);
 }
 
 extern "C" int jb_lof_score(const int32_t* ts, const float* td, int nt, int k,

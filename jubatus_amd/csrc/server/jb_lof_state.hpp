@@ -35,12 +35,16 @@ int jb_lof_add_st(int p, const int32_t* cs, const float* cd, int nc, int k, int 
 int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd, const int32_t* nc,
                     int stride, int k, int ignore_same, int32_t* nb_slot, float* nb_dist, float* kdist,
                     uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
-                    uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch0, uint32_t* out_host, int out_stride,
-                    int max_missing, int32_t* abort_dev, hipStream_t stream);
+                    uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch0, int32_t* cand, uint32_t* res,
+                    uint32_t* out_host, int out_stride, int max_missing, hipStream_t stream);
 int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
                     const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                     int store_slot, const uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch,
                     uint32_t* out_host, int max_missing, hipStream_t stream);
+int jb_lof_score_many(int nq, const int32_t* ts, const float* td, const int32_t* nt, int stride, int k,
+                      const int32_t* nb_slot, const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd,
+                      uint8_t* lrd_ok, const uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch, uint32_t* out_host,
+                      int out_stride, int max_missing, hipStream_t stream);
 int jb_lof_invalidate(const int32_t* slots, int n, int64_t nrows, uint8_t* ok, uint8_t* lrd_ok,
                       hipStream_t stream);
 void* jb_host_alloc(int64_t nbytes);
@@ -65,18 +69,22 @@ class LofState {
     if (!out_) throw std::runtime_error("hipHostMalloc failed");
     changed_.get(kLofMaxChanged);
     nchanged_.get(1);
-    abort_.get(1);
+    cand_.get(2 * (size_t)kLofBatchMax * kLofArgMax);
+    res_.get((size_t)kLofBatchMax * kOutStride);
+    stage_ = (int32_t*)jb_host_alloc(4 * (2 * (size_t)kLofBatchMax + 2 * (size_t)kLofBatchMax * kLofArgMax));
+    if (!stage_) throw std::runtime_error("hipHostMalloc failed");
     out_many_ = (uint32_t*)jb_host_alloc(4 * (size_t)kOutStride * kLofBatchMax);
     if (!out_many_) throw std::runtime_error("hipHostMalloc failed");
   }
 
   ~LofState() {
     for (void* q : {(void*)nb_slot_.p, (void*)nb_dist_.p, (void*)kdist_.p, (void*)lrd_.p, (void*)ok_.p,
-                    (void*)lrd_ok_.p, (void*)kstamp_.p, (void*)lstamp_.p, (void*)changed_.p, (void*)nchanged_.p, (void*)up_[0].p, (void*)up_[1].p,
-                    (void*)up_[2].p, (void*)abort_.p})
+                    (void*)lrd_ok_.p, (void*)kstamp_.p, (void*)lstamp_.p, (void*)changed_.p, (void*)nchanged_.p,
+                    (void*)up_[0].p, (void*)up_[1].p, (void*)up_[2].p, (void*)cand_.p, (void*)res_.p})
       if (q) (void)hipFree(q);
     if (out_) jb_host_free(out_);
     if (out_many_) jb_host_free(out_many_);
+    if (stage_) jb_host_free(stage_);
   }
   LofState(const LofState&) = delete;
   LofState& operator=(const LofState&) = delete;
@@ -123,19 +131,26 @@ class LofState {
     int stride = 1;
     for (const auto& c : cs) stride = std::max(stride, (int)c.size());
     if (stride > kLofArgMax) throw std::runtime_error("lof add_many: too many candidates");
-    std::vector<int32_t> fcs(n * (size_t)stride, -1), nc(n);
-    std::vector<float> fcd(n * (size_t)stride, INFINITY);
+    // pinned staging the kernel reads: ps [64], nc [64], cs [n][stride], cd [n][stride]
+    int32_t* hps = stage_;
+    int32_t* hnc = stage_ + kLofBatchMax;
+    int32_t* hcs = stage_ + 2 * kLofBatchMax;
+    float* hcd = reinterpret_cast<float*>(hcs + n * (size_t)stride);
     for (size_t i = 0; i < n; ++i) {
-      nc[i] = (int32_t)cs[i].size();
-      std::copy(cs[i].begin(), cs[i].end(), fcs.begin() + (int64_t)i * stride);
-      std::copy(cd[i].begin(), cd[i].end(), fcd.begin() + (int64_t)i * stride);
+      hps[i] = ps[i];
+      hnc[i] = (int32_t)cs[i].size();
+      int32_t* c = hcs + (int64_t)i * stride;
+      float* d = hcd + (int64_t)i * stride;
+      std::copy(cs[i].begin(), cs[i].end(), c);
+      std::copy(cd[i].begin(), cd[i].end(), d);
+      std::fill(c + cs[i].size(), c + stride, -1);
+      std::fill(d + cd[i].size(), d + stride, INFINITY);
     }
     const uint32_t epoch0 = epoch_ + 1;
     epoch_ += (uint32_t)n;            // (adds after a stop leave gaps: stamps only need to grow)
-    const int rc = jb_lof_add_many((int)n, ps.data(), fcs.data(), fcd.data(), nc.data(), stride, k_, ignore_ ? 1 : 0,
-                                   nb_slot_.p, nb_dist_.p, kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p,
-                                   nchanged_.p, kstamp_.p, lstamp_.p, epoch0, out_many_, kOutStride, kLofMaxMissing,
-                                   abort_.p, stream_);
+    const int rc = jb_lof_add_many((int)n, hps, hcs, hcd, hnc, stride, k_, ignore_ ? 1 : 0, nb_slot_.p, nb_dist_.p,
+                                   kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p, kstamp_.p, lstamp_.p,
+                                   epoch0, cand_.p, res_.p, out_many_, kOutStride, kLofMaxMissing, stream_);
     if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
     scores->clear();
     for (size_t i = 0; i < n; ++i) {
@@ -167,6 +182,40 @@ class LofState {
                                    kLofMaxMissing, stream_);
     if (rc != 0) throw std::runtime_error("lof score failed: " + std::to_string(rc));
     return result(sc, missing);
+  }
+
+  // independent scores (no store), one wait: (*done)[i] = 1 and (*scores)[i]
+  // for the queries that resolved; the others found rows without a valid
+  // list and are left to score() (the caller installs the lists)
+  void score_many(const std::vector<std::vector<int32_t>>& ts, const std::vector<std::vector<float>>& td,
+                  std::vector<float>* scores, std::vector<char>* done) {
+    const size_t n = ts.size();
+    scores->assign(n, 1.f);
+    done->assign(n, 0);
+    for (size_t b = 0; b < n; b += kLofBatchMax) {
+      const size_t m = std::min<size_t>(kLofBatchMax, n - b);
+      int stride = 1;
+      for (size_t i = 0; i < m; ++i) stride = std::max(stride, (int)ts[b + i].size());
+      if (stride > 64) return;         // (the caller scores them one by one)
+      std::vector<int32_t> fts(m * (size_t)stride, 0), nt(m);
+      std::vector<float> ftd(m * (size_t)stride, 0.f);
+      for (size_t i = 0; i < m; ++i) {
+        nt[i] = (int32_t)ts[b + i].size();
+        std::copy(ts[b + i].begin(), ts[b + i].end(), fts.begin() + (int64_t)i * stride);
+        std::copy(td[b + i].begin(), td[b + i].end(), ftd.begin() + (int64_t)i * stride);
+      }
+      const int rc = jb_lof_score_many((int)m, fts.data(), ftd.data(), nt.data(), stride, k_, nb_slot_.p, nb_dist_.p,
+                                       kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, kstamp_.p, lstamp_.p, epoch_, out_many_,
+                                       kOutStride, kLofMaxMissing, stream_);
+      if (rc != 0) throw std::runtime_error("lof score_many failed: " + std::to_string(rc));
+      for (size_t i = 0; i < m; ++i) {
+        const uint32_t* o = out_many_ + i * kOutStride;
+        if (((volatile const uint32_t*)o)[0] == 1) {
+          memcpy(&(*scores)[b + i], &o[1], 4);
+          (*done)[b + i] = 1;
+        }
+      }
+    }
   }
 
   // rows changed or removed: their lists and every list naming them invalid
@@ -272,7 +321,9 @@ class LofState {
   uint32_t epoch_ = 0;
   DevBuf<int32_t> changed_, nchanged_;
   DevBuf<int32_t> up_[3];
-  DevBuf<int32_t> abort_;
+  DevBuf<int32_t> cand_;          // add_many's candidates on the device
+  DevBuf<uint32_t> res_;          // add_many's results before they go to the host
+  int32_t* stage_ = nullptr;       // add_many's pinned staging (the kernel reads it)
   uint32_t* out_ = nullptr;
   static constexpr int kOutStride = 4 + kLofMaxMissing;
   uint32_t* out_many_ = nullptr;   // [kLofBatchMax][kOutStride] pinned
