@@ -828,6 +828,12 @@ class PoolIndex {
 
   // similarity.py DevicePool.lanes_per_row
   int lanes_per_row(int nq) const {
+    static const int forced = [] {         // diagnostics: JB_POOL_LPR = 1 / 4 / 16
+      const char* e = getenv("JB_POOL_LPR");
+      const int v = e != nullptr ? atoi(e) : 0;
+      return (v == 1 || v == 4 || v == 16) ? v : 0;
+    }();
+    if (forced) return forced;
     const int64_t rows = std::max<int64_t>(1, nlive_);
     const double mean = (double)live_ / (double)rows;
     if (nq >= 4 && mean <= 24) return 1;
