@@ -2,7 +2,8 @@
 # One GPU-box session: build, GPU tests, smoke, bench, rocprofv3 stats.
 # Stops at the first step that faults / aborts / times out (exit 124, 134,
 # 137, 139 or signal); plain test failures (exit 1) do not stop the session.
-# Usage: tools/gpu_session.sh [steps...]   steps: build tests alltests smoke serial serialworst serialprof kbench scan engines bench prof
+# Usage: tools/gpu_session.sh [steps...]   steps: build tests alltests smoke serial serialworst serialprof kbench scan
+#        engines bench prof lof topk gaps pmc_train pmc_topk
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -46,6 +47,36 @@ for s in $STEPS; do
       (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
          python "$ROOT/bench.py" --steps 5 --warmup 2 --latency-iters 20)
       find "$OUT/prof" -name "*stats*" | head -20 ;;
+    lof)   # LOF engine record (native server over RPC) + its kernel stats
+      run lof 300 python tools/bench_engine_records.py --engines anomaly_lof
+      rm -rf /tmp/lofprof
+      (cd /tmp && run lofprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/lofprof -o run -- \
+         python3 "$ROOT/tools/bench_engine_records.py" --engines anomaly_lof) || exit $?
+      cp /tmp/lofprof/run_kernel_stats.csv "$OUT/lof_kernel_stats.csv" ;;
+    topk)  # signature / score top-k paths below 2M rows (select vs the previous default)
+      run topk_100k 300 python tools/bench_topk_lsh.py --rows 100000 --iters 200 \
+        --cases 1:10,4:10,1:31,4:40,1:94 --paths fused,select,default --metrics 1,0
+      run topk_1m 300 python tools/bench_topk_lsh.py --rows 1000000 --iters 100 \
+        --cases 1:10,4:10,1:31,4:40,1:100 --paths fused,select,default --metrics 1
+      run topk_scores 300 python tools/bench_topk_scores.py --rows 1000000 --iters 100 --paths chain,fused,select,default ;;
+    gaps)  # kernel-trace gaps of the exact-mode committer
+      rm -rf /tmp/ktv
+      (cd /tmp && run gaps_trace 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/ktv -o run -- \
+         python3 "$ROOT/tools/bench_serial.py" --batches 30 --modes exact) || exit $?
+      python3 tools/trace_gaps.py /tmp/ktv "$OUT/gaps_steady.md" --last 1500 > /dev/null
+      python3 tools/trace_gaps.py /tmp/ktv "$OUT/gaps_all.md" > /dev/null ;;
+    pmc_train|pmc_topk)   # counter passes, one rocprofv3 run each (block limits per pass)
+      if [ "$s" = pmc_train ]; then B="python3 $ROOT/tools/bench_serial.py --batches 6 --modes exact,atomic"; M="";
+      else B="python3 $ROOT/tools/bench_topk_mq.py --quick --iters 3"; M="--match topk"; fi
+      P=0
+      for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" \
+               "SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH" \
+               "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+        P=$((P + 1)); rm -rf /tmp/pmc$P
+        (cd /tmp && run ${s}_$P 240 rocprofv3 --pmc $c --kernel-trace --output-format csv -d /tmp/pmc$P -o run -- $B) \
+          || exit $?
+      done
+      python3 tools/pmc_summary.py "$OUT/$s.md" /tmp/pmc1 /tmp/pmc2 /tmp/pmc3 /tmp/pmc4 /tmp/pmc5 $M ;;
     *) echo "unknown step $s" ;;
   esac
 done
