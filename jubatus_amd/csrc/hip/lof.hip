@@ -32,6 +32,7 @@ namespace jb {
 constexpr int kLofMaxK = 64;
 constexpr int kLofMaxChanged = 1024;
 constexpr int kLofU = 8;                // cooperative loads in flight per thread
+constexpr int kLofKR = 16;              // k up to this: list edits and scores in registers
 
 __device__ __forceinline__ float lof_kth(const int32_t* s, const float* d, int k, int ignore_same) {
   float kd = 0.f;
@@ -64,7 +65,30 @@ struct LofLds {
   float kd1[64], lrd1[64], lr1[64];
   uint32_t lst[64];
   int n_ch, nmiss;
+  bool prof;                      // phase stamps on (lof_add_batch_kernel, prof != nullptr)
+  unsigned long long ph[8], tlast;
 };
+
+// The insert / score bodies run in one-wave blocks (every launch is 64
+// threads): lanes exchange LDS data after their LDS operations complete -
+// no barrier, and no wait for the global stores in flight (a __syncthreads
+// fence waits for every store's acknowledgement, ~1-2 us after scattered
+// row writes). __syncthreads stays where a later global load depends on
+// another lane's global store.
+__device__ __forceinline__ void lof_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// phase stamp i (shader cycles since the previous stamp), lane 0, when on
+__device__ __forceinline__ void lof_stamp(LofLds& L, int i) {
+  if (!L.prof) return;
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) {
+    L.ph[i] += t - L.tlast;
+    L.tlast = t;
+  }
+}
 
 // Staleness stamps (optional, kstamp / lstamp non-null): kstamp[x] = the add
 // epoch that last changed x's list / k-distance, lstamp[o] = the epoch lrd[o]
@@ -155,32 +179,87 @@ __device__ __forceinline__ void lof_insert_body(
       l_ok[t] = f_ok;
       if (fused) { L.lok1[t] = f_lok; L.lr1[t] = f_lr; L.kd1[t] = f_kd; L.lst[t] = f_lst; }
     }
-    __syncthreads();
+    lof_lds_sync();
+    lof_stamp(L, 1);
     if (t < cn && l_ok[t]) {
       const int32_t o = cs[c0 + t];
       const float d = cd[c0 + t];
       int32_t* ts = l_s[t];
       float* td = l_d[t];
-      int n = 0;
-      bool had = false;
-      for (int j = 0; j < k; ++j) {          // o's list without p (compacted in place)
-        const int32_t x = ts[j];
-        if (x < 0) break;
-        if (x == p) { had = true; continue; }
-        ts[n] = x;
-        td[n] = td[j];
-        ++n;
+      bool upd = false;
+      float kd = 0.f;
+      if (k <= kLofKR) {
+        // in registers (static indices throughout): a list edit of dependent
+        // LDS round trips costs ~10 K cycles per add, this ~a few hundred
+        int32_t rs[kLofKR];
+        float rd[kLofKR];
+#pragma unroll
+        for (int j = 0; j < kLofKR; ++j) {      // unconditional reads (rows hold kLofMaxK + 1), then masks
+          const int32_t vs = ts[j];
+          const float vd = td[j];
+          rs[j] = j < k ? vs : -1;
+          rd[j] = j < k ? vd : INFINITY;
+        }
+        // o's list without p (lists are sorted, -1 padded at the end)
+        bool had = false;
+#pragma unroll
+        for (int j = 0; j < kLofKR; ++j) {
+          had |= rs[j] == p;
+          rs[j] = had ? (j + 1 < kLofKR ? rs[j + 1] : -1) : rs[j];
+          rd[j] = had ? (j + 1 < kLofKR ? rd[j + 1] : INFINITY) : rd[j];
+        }
+        int n = 0, at = 0;
+        int32_t ls = -1;
+        float ld = INFINITY;
+#pragma unroll
+        for (int j = 0; j < kLofKR; ++j) {
+          const bool v = j < k && rs[j] >= 0;
+          n += v;
+          at += v && (rd[j] < d || (rd[j] == d && rs[j] < p));
+          if (j == k - 1) { ls = rs[j]; ld = rd[j]; }
+        }
+        upd = had || n < k || d < ld || (d == ld && p < ls);
+        if (upd) {
+          const int m = n < k ? n + 1 : k;
+#pragma unroll
+          for (int j = kLofKR - 1; j >= 0; --j) {
+            // insert (d, p) at `at`: later entries move up one
+            const int32_t sj = j < at ? rs[j] : (j == at ? p : (j > 0 ? rs[j - 1] : -1));
+            const float dj = j < at ? rd[j] : (j == at ? d : (j > 0 ? rd[j - 1] : INFINITY));
+            rs[j] = j < m ? sj : -1;
+            rd[j] = j < m ? dj : INFINITY;
+          }
+#pragma unroll
+          for (int j = 0; j < kLofKR; ++j) {
+            if (j < k) { ts[j] = rs[j]; td[j] = rd[j]; }
+            if (j < k && rs[j] >= 0 && (!ignore_same || rd[j] > 0.f)) kd = rd[j];
+          }
+        }
+      } else {
+        int n = 0;
+        bool had = false;
+        for (int j = 0; j < k; ++j) {          // o's list without p (compacted in place)
+          const int32_t x = ts[j];
+          if (x < 0) break;
+          if (x == p) { had = true; continue; }
+          ts[n] = x;
+          td[n] = td[j];
+          ++n;
+        }
+        const bool full = n == k;
+        upd = had || !full || d < td[k - 1] || (d == td[k - 1] && p < ts[k - 1]);
+        if (upd) {
+          int at = n;                             // insert (d, p) in (distance, slot) order
+          while (at > 0 && (td[at - 1] > d || (td[at - 1] == d && ts[at - 1] > p))) --at;
+          for (int j = (n < k ? n : k - 1); j > at; --j) { ts[j] = ts[j - 1]; td[j] = td[j - 1]; }
+          if (at < k) { ts[at] = p; td[at] = d; }
+          const int m = n < k ? n + 1 : k;
+          for (int j = m; j < k; ++j) { ts[j] = -1; td[j] = INFINITY; }
+          kd = lof_kth(ts, td, k, ignore_same);
+        }
       }
-      const bool full = n == k;
-      if (had || !full || d < td[k - 1] || (d == td[k - 1] && p < ts[k - 1])) {
-        int at = n;                             // insert (d, p) in (distance, slot) order
-        while (at > 0 && (td[at - 1] > d || (td[at - 1] == d && ts[at - 1] > p))) --at;
-        for (int j = (n < k ? n : k - 1); j > at; --j) { ts[j] = ts[j - 1]; td[j] = td[j - 1]; }
-        if (at < k) { ts[at] = p; td[at] = d; }
-        const int m = n < k ? n + 1 : k;
-        for (int j = m; j < k; ++j) { ts[j] = -1; td[j] = INFINITY; }
+      if (upd) {
         L.chg[t] = 1;                           // written back below, row by row
-        const float kd = lof_kth(ts, td, k, ignore_same);
         kdist[o] = kd;
         lrd_ok[o] = 0;
         if (kstamp != nullptr) kstamp[o] = epoch;
@@ -189,7 +268,8 @@ __device__ __forceinline__ void lof_insert_body(
         if (w < kLofMaxChanged) changed[w] = o;
       }
     }
-    __syncthreads();
+    lof_lds_sync();
+    lof_stamp(L, 2);
     // the changed lists back to HBM, consecutive lanes on consecutive entries
     // of a row (a lane per row would touch 64 rows per store instruction)
     for (int e = t; e < cn * k; e += 64) {
@@ -201,6 +281,7 @@ __device__ __forceinline__ void lof_insert_body(
       }
     }
     __syncthreads();
+    lof_stamp(L, 3);
   }
   if (t == 0) *nchanged = n_ch < kLofMaxChanged ? n_ch : kLofMaxChanged;
 }
@@ -214,7 +295,7 @@ __global__ __launch_bounds__(64) void lof_add_kernel(
   __shared__ int32_t cs[kLofArgMax];
   __shared__ float cd[kLofArgMax];
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
-  __syncthreads();
+  lof_lds_sync();
   __shared__ LofLds L;
   lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
                   nchanged, first != 0, L);
@@ -384,7 +465,7 @@ __device__ __forceinline__ void lof_score_body(
       }
     }
   }
-  __syncthreads();
+  lof_lds_sync();
   for (int e0 = t; e0 < nt * k; e0 += 64 * kLofU) {
     uint8_t vo[kLofU];
     float vk[kLofU];
@@ -414,7 +495,8 @@ __device__ __forceinline__ void lof_score_body(
       }
     }
   }
-  __syncthreads();
+  lof_lds_sync();
+  lof_stamp(L, 5);
   auto miss = [&](int32_t s) {
     const int w = atomicAdd(&nmiss, 1);
     if (w < max_missing) put(out + 4 + w, (uint32_t)s);
@@ -428,12 +510,35 @@ __device__ __forceinline__ void lof_score_body(
       bool good = true;
       int n = 0;
       float sum = 0.f;
-      for (int j = 0; j < k; ++j) {
-        const int32_t x = l_s[t][j];
-        if (x < 0) break;
-        if (!l_ok[t][j]) { miss(x); good = false; }
-        sum += fmaxf(l_kd[t][j], l_d[t][j]);
-        ++n;
+      if (k <= kLofKR) {
+        // all of the list's LDS reads issued together, then the sum in order
+        int32_t xs[kLofKR];
+        uint8_t xo[kLofKR];
+        float xm[kLofKR];
+#pragma unroll
+        for (int j = 0; j < kLofKR; ++j) {
+          const int32_t vs = l_s[t][j];
+          const uint8_t vo = l_ok[t][j];
+          const float vm = fmaxf(l_kd[t][j], l_d[t][j]);
+          xs[j] = j < k ? vs : -1;
+          xo[j] = j < k ? vo : 1;
+          xm[j] = j < k ? vm : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < kLofKR; ++j) {
+          if (xs[j] < 0) continue;              // (-1 entries are a suffix)
+          if (!xo[j]) { miss(xs[j]); good = false; }
+          sum += xm[j];
+          ++n;
+        }
+      } else {
+        for (int j = 0; j < k; ++j) {
+          const int32_t x = l_s[t][j];
+          if (x < 0) break;
+          if (!l_ok[t][j]) { miss(x); good = false; }
+          sum += fmaxf(l_kd[t][j], l_d[t][j]);
+          ++n;
+        }
       }
       if (good && (!lok || L.stale[t])) {
         const float mean = n > 0 ? sum / n : 0.f;
@@ -448,7 +553,7 @@ __device__ __forceinline__ void lof_score_body(
   // the host reads out[] once out[0] is set: every thread's system-scope
   // stores are acknowledged before the barrier, the status goes last (a
   // system-scope release fence would write back the whole L2 instead)
-  if (defer) __syncthreads();
+  if (defer) lof_lds_sync();
   else sys_stores_block_done();
   if (t != 0) return;
   if (nmiss > 0) {
@@ -463,10 +568,22 @@ __device__ __forceinline__ void lof_score_body(
   // lrd of the query point itself (its own neighbours' k-distances)
   float sum = 0.f, lsum = 0.f;
   bool linf = false;
-  for (int j = 0; j < nt; ++j) {
-    sum += fmaxf(s_kd[j], td[j]);
-    const float l = s_lrd[j];
-    if (isinf(l)) linf = true; else lsum += l;
+  for (int j0 = 0; j0 < nt; j0 += 16) {         // 16 LDS reads of each array in flight
+    float a[16], l[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {               // (the arrays hold 64: reads in bounds)
+      const int jj = (j0 + u) & 63;
+      const float va = fmaxf(s_kd[jj], td[jj]);
+      const float vl = s_lrd[jj];
+      a[u] = j0 + u < nt ? va : 0.f;
+      l[u] = j0 + u < nt ? vl : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (j0 + u >= nt) break;
+      sum += a[u];
+      if (isinf(l[u])) linf = true; else lsum += l[u];
+    }
   }
   float score = 1.f, lp = 0.f;
   if (nt > 0) {
@@ -506,7 +623,7 @@ __global__ __launch_bounds__(64) void lof_score_kernel(
   __shared__ LofLds L;
   const int nt = a.n < kLofMaxK ? a.n : kLofMaxK;
   if ((int)threadIdx.x < nt) { ts[threadIdx.x] = a.s[threadIdx.x]; td[threadIdx.x] = a.d[threadIdx.x]; }
-  __syncthreads();
+  lof_lds_sync();
   lof_score_body(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, store_slot, out,
                  max_missing, abort_flag, L, kstamp, lstamp, epoch);
 }
@@ -528,12 +645,12 @@ __global__ __launch_bounds__(64) void lof_add_score_kernel(
   __shared__ float cd[kLofArgMax];
   __shared__ LofLds L;
   for (int i = threadIdx.x; i < a.n; i += blockDim.x) { cs[i] = a.s[i]; cd[i] = a.d[i]; }
-  __syncthreads();
+  lof_lds_sync();
   const bool fz = a.n <= 64;                         // targets' lists stay in LDS
   lof_insert_body(p, cs, cd, a.n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed,
                   nchanged, true, L, kstamp, epoch, fz ? lrd : nullptr, lstamp);
   // the insert's global stores are visible to the block after the barrier
-  __syncthreads();
+  lof_lds_sync();
   const int nt = a.n < k ? a.n : k;
   lof_score_body(cs, cd, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, p, out, max_missing,
                  abort_flag, L, kstamp, lstamp, epoch, false, fz);
@@ -552,7 +669,8 @@ __global__ __launch_bounds__(64) void lof_add_batch_kernel(
     float* __restrict__ nb_dist, float* __restrict__ kdist, uint8_t* __restrict__ ok, float* __restrict__ lrd,
     uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged,
     uint32_t* __restrict__ kstamp, uint32_t* __restrict__ lstamp, uint32_t epoch0, int32_t* __restrict__ cand,
-    uint32_t* __restrict__ res, uint32_t* __restrict__ out, int out_stride, int max_missing) {
+    uint32_t* __restrict__ res, uint32_t* __restrict__ out, int out_stride, int max_missing,
+    unsigned long long* __restrict__ prof) {
   __shared__ int32_t cs[kLofArgMax];
   __shared__ float cd[kLofArgMax];
   __shared__ int32_t s_p[64], s_n[64];
@@ -574,20 +692,28 @@ __global__ __launch_bounds__(64) void lof_add_batch_kernel(
       if (e0 + 64 * u < tot) { cand[e0 + 64 * u] = vs[u]; cand_d[e0 + 64 * u] = vd[u]; }
   }
   if (t < nadd) { s_p[t] = ps[t]; s_n[t] = nc[t]; }
+  if (t < 8) L.ph[t] = 0;
+  if (t == 0) {
+    L.prof = prof != nullptr;
+    L.tlast = __builtin_amdgcn_s_memtime();
+  }
   __syncthreads();
+  lof_stamp(L, 7);                                // the candidates' copy from the host
   int ran = nadd;
   for (int i = 0; i < nadd; ++i) {
     const int n = s_n[i], p = s_p[i];
     for (int e = t; e < n; e += blockDim.x) { cs[e] = cand[i * stride + e]; cd[e] = cand_d[i * stride + e]; }
-    __syncthreads();
+    lof_lds_sync();
+    lof_stamp(L, 0);
     const bool fz = n <= 64;                         // targets' lists stay in LDS
     lof_insert_body(p, cs, cd, n, k, ignore_same, nb_slot, nb_dist, kdist, ok, lrd_ok, changed, nchanged, true,
                     L, kstamp, epoch0 + (uint32_t)i, fz ? lrd : nullptr, lstamp);
-    __syncthreads();
+    lof_lds_sync();
     lof_score_body(cs, cd, n < k ? n : k, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, p,
                    res + (int64_t)i * out_stride, max_missing, nullptr, L, kstamp, lstamp, epoch0 + (uint32_t)i,
                    true, fz);
     __syncthreads();
+    lof_stamp(L, 6);
     if (L.nmiss > 0) { ran = i + 1; break; }      // stopped: the later adds did not run
   }
   // results to the host: every word but the statuses, acknowledged, then the
@@ -603,6 +729,12 @@ __global__ __launch_bounds__(64) void lof_add_batch_kernel(
   sys_stores_block_done();
   const int64_t last = (int64_t)(nadd - 1) * out_stride;
   if (t == 0) sys_store(out + last, nadd - 1 < ran ? res[last] : 3u);
+  // phases (cycles): 0 candidates to LDS, 1 list loads, 2 edits, 3 write-back,
+  // 4 (unused), 5 score loads, 6 score, 7 host copy; prof[8] adds
+  if (prof != nullptr && t == 0) {
+    for (int i = 0; i < 8; ++i) atomicAdd(prof + i, L.ph[i]);
+    atomicAdd(prof + 8, (unsigned long long)ran);
+  }
 }
 
 }  // namespace jb
@@ -715,7 +847,7 @@ extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, c
                                float* nb_dist, float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                                int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp,
                                uint32_t epoch0, int32_t* cand, uint32_t* res, uint32_t* out_host, int out_stride,
-                               int max_missing, hipStream_t stream) {
+                               int max_missing, unsigned long long* prof, hipStream_t stream) {
   if (nadd <= 0) return 0;
   if (nadd > 64 || k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax || kstamp == nullptr ||
       lstamp == nullptr)
@@ -726,7 +858,7 @@ extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, c
   }
   hipLaunchKernelGGL(jb::lof_add_batch_kernel, dim3(1), dim3(64), 0, stream, nadd, ps, nc, cs, cd, stride, k,
                      ignore_same, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, changed, nchanged, kstamp, lstamp,
-                     epoch0, cand, res, out_host, out_stride, max_missing);
+                     epoch0, cand, res, out_host, out_stride, max_missing, prof);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return jb::wait_nonzero(out_host + (int64_t)(nadd - 1) * out_stride, stream);

@@ -36,7 +36,8 @@ int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float*
                     int stride, int k, int ignore_same, int32_t* nb_slot, float* nb_dist, float* kdist,
                     uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
                     uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch0, int32_t* cand, uint32_t* res,
-                    uint32_t* out_host, int out_stride, int max_missing, hipStream_t stream);
+                    uint32_t* out_host, int out_stride, int max_missing, unsigned long long* prof,
+                    hipStream_t stream);
 int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
                     const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                     int store_slot, const uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch,
@@ -150,7 +151,7 @@ class LofState {
     epoch_ += (uint32_t)n;            // (adds after a stop leave gaps: stamps only need to grow)
     const int rc = jb_lof_add_many((int)n, hps, hcs, hcd, hnc, stride, k_, ignore_ ? 1 : 0, nb_slot_.p, nb_dist_.p,
                                    kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p, kstamp_.p, lstamp_.p,
-                                   epoch0, cand_.p, res_.p, out_many_, kOutStride, kLofMaxMissing, stream_);
+                                   epoch0, cand_.p, res_.p, out_many_, kOutStride, kLofMaxMissing, nullptr, stream_);
     if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
     scores->clear();
     for (size_t i = 0; i < n; ++i) {
