@@ -3,7 +3,7 @@
 # Stops at the first step that faults / aborts / times out (exit 124, 134,
 # 137, 139 or signal); plain test failures (exit 1) do not stop the session.
 # Usage: tools/gpu_session.sh [steps...]   steps: build tests alltests smoke serial serialworst serialprof kbench scan
-#        engines bench prof lof topk gaps pmc_train pmc_topk
+#        engines bench prof lof topk gaps pmc_train pmc_topk pmc_select pmc_lof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -65,9 +65,14 @@ for s in $STEPS; do
          python3 "$ROOT/tools/bench_serial.py" --batches 30 --modes exact) || exit $?
       python3 tools/trace_gaps.py /tmp/ktv "$OUT/gaps_steady.md" --last 1500 > /dev/null
       python3 tools/trace_gaps.py /tmp/ktv "$OUT/gaps_all.md" > /dev/null ;;
-    pmc_train|pmc_topk)   # counter passes, one rocprofv3 run each (block limits per pass)
-      if [ "$s" = pmc_train ]; then B="python3 $ROOT/tools/bench_serial.py --batches 6 --modes exact,atomic"; M="";
-      else B="python3 $ROOT/tools/bench_topk_mq.py --quick --iters 3"; M="--match topk"; fi
+    pmc_train|pmc_topk|pmc_select|pmc_lof)   # counter passes, one rocprofv3 run each (block limits per pass)
+      case $s in
+        pmc_train) B="python3 $ROOT/tools/bench_serial.py --batches 6 --modes exact,atomic"; M="" ;;
+        pmc_topk) B="python3 $ROOT/tools/bench_topk_mq.py --quick --iters 3"; M="--match topk" ;;
+        pmc_select) B="python3 $ROOT/tools/bench_topk_lsh.py --rows 1000000 --iters 20 --cases 1:31,4:40 --paths select --metrics 1"
+                    M="--match select" ;;
+        *) B="python3 $ROOT/tools/bench_lof_kernel.py --batches 40"; M="--match lof" ;;
+      esac
       P=0
       for c in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES" \
                "SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH" \
