@@ -80,6 +80,12 @@ __device__ __forceinline__ void lof_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// e / k for the flattened (row, entry) indices of a round (e < 2^16, k <= 64):
+// one multiply-high by ceil(2^32 / k) instead of an integer division's ~25
+// instructions (exact while e * k < 2^32)
+__device__ __forceinline__ uint32_t lof_kinv(int k) { return (uint32_t)((0x100000000ull + k - 1) / k); }
+__device__ __forceinline__ int lof_div(int e, uint32_t kinv) { return (int)__umulhi((uint32_t)e, kinv); }
+
 // phase stamp i (shader cycles since the previous stamp), lane 0, when on
 __device__ __forceinline__ void lof_stamp(LofLds& L, int i) {
   if (!L.prof) return;
@@ -117,6 +123,7 @@ __device__ __forceinline__ void lof_insert_body(
   auto& l_d = L.d;
   uint8_t* l_ok = L.ok1;
   const int t = threadIdx.x;
+  const uint32_t kinv = lof_kinv(k);
   if (t == 0 && !first) n_ch = *nchanged;   // a later chunk of candidates: reverse inserts only
   if (t == 0 && first) {
     int32_t* ps = nb_slot + (int64_t)p * k;
@@ -158,7 +165,7 @@ __device__ __forceinline__ void lof_insert_body(
 #pragma unroll
       for (int u = 0; u < kLofU; ++u) {
         const int e = e0 + 64 * u;
-        const int c = e < cn * k ? e / k : 0, j = e - c * k;
+        const int c = e < cn * k ? lof_div(e, kinv) : 0, j = e - c * k;
         const int32_t o = cs[c0 + c];
         const int64_t at = (int64_t)(o >= 0 ? o : p) * k + (e < cn * k ? j : 0);
         vs[u] = nb_slot[at];
@@ -168,7 +175,7 @@ __device__ __forceinline__ void lof_insert_body(
       for (int u = 0; u < kLofU; ++u) {
         const int e = e0 + 64 * u;
         if (e < cn * k) {
-          const int c = e / k, j = e - c * k;
+          const int c = lof_div(e, kinv), j = e - c * k;
           l_s[c][j] = vs[u];
           l_d[c][j] = vd[u];
         }
@@ -273,7 +280,7 @@ __device__ __forceinline__ void lof_insert_body(
     // the changed lists back to HBM, consecutive lanes on consecutive entries
     // of a row (a lane per row would touch 64 rows per store instruction)
     for (int e = t; e < cn * k; e += 64) {
-      const int c = e / k, j = e - c * k;
+      const int c = lof_div(e, kinv), j = e - c * k;
       if (L.chg[c]) {
         const int64_t at = (int64_t)cs[c0 + c] * k + j;
         nb_slot[at] = l_s[c][j];
@@ -426,6 +433,7 @@ __device__ __forceinline__ void lof_score_body(
   float* s_kd = L.kd1;
   float* s_lrd = L.lrd1;
   const int t = threadIdx.x;
+  const uint32_t kinv = lof_kinv(k);
   if (t == 0) nmiss = 0;
   uint8_t lok = 0;
   float lr = 0.f;
@@ -450,7 +458,7 @@ __device__ __forceinline__ void lof_score_body(
 #pragma unroll
     for (int u = 0; u < kLofU; ++u) {
       const int e = e0 + 64 * u < nt * k ? e0 + 64 * u : 0;
-      const int c = e / k, j = e - c * k;
+      const int c = lof_div(e, kinv), j = e - c * k;
       const int64_t at = (int64_t)ts[c] * k + j;
       vs[u] = nb_slot[at];
       vd[u] = nb_dist[at];
@@ -459,7 +467,7 @@ __device__ __forceinline__ void lof_score_body(
     for (int u = 0; u < kLofU; ++u) {
       const int e = e0 + 64 * u;
       if (e < nt * k) {
-        const int c = e / k, j = e - c * k;
+        const int c = lof_div(e, kinv), j = e - c * k;
         l_s[c][j] = vs[u];
         l_d[c][j] = vd[u];
       }
@@ -473,7 +481,7 @@ __device__ __forceinline__ void lof_score_body(
 #pragma unroll
     for (int u = 0; u < kLofU; ++u) {
       const int e = e0 + 64 * u;
-      const int c = e < nt * k ? e / k : 0, j = e - c * k;
+      const int c = e < nt * k ? lof_div(e, kinv) : 0, j = e - c * k;
       const int32_t x = e < nt * k ? l_s[c][j] : -1;
       // a list is valid (in range) only while its row is ok
       const int32_t xr = (s_ok[c] && x >= 0) ? x : 0;
@@ -485,7 +493,7 @@ __device__ __forceinline__ void lof_score_body(
     for (int u = 0; u < kLofU; ++u) {
       const int e = e0 + 64 * u;
       if (e < nt * k) {
-        const int c = e / k, j = e - c * k;
+        const int c = lof_div(e, kinv), j = e - c * k;
         const int32_t x = l_s[c][j];
         if (s_ok[c] && x >= 0) {
           l_ok[c][j] = vo[u];
