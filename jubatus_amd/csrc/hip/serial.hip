@@ -889,9 +889,18 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
       const int64_t why = seen != nullptr ? ((volatile int64_t*)seen)[0] : 0;
       const int64_t prev = seen != nullptr ? ((volatile int64_t*)seen)[1] : 0;
       const bool short_of = why != jb::kStopDone && why != jb::kStopDense;
+      // slack over the previous batch's count: prev / 2 + 8 by default
+      // (JB_VC_SEG_SLACK = d,c: prev / d + c, an A/B knob)
+      static const std::pair<int, int> slack = [] {
+        const char* e = getenv("JB_VC_SEG_SLACK");
+        int d = 2, c = 8;
+        if (e != nullptr && sscanf(e, "%d,%d", &d, &c) != 2) { d = 2; c = 8; }
+        return std::make_pair(d > 0 ? d : 2, c >= 0 ? c : 8);
+      }();
       nseg = short_of ? jb::kVerifiedSegmentsMax
                       : (int)std::min<int64_t>(jb::kVerifiedSegmentsMax,
-                                               std::max<int64_t>(jb::kDeltaSegmentsMin, prev + prev / 2 + 8));
+                                               std::max<int64_t>(jb::kDeltaSegmentsMin,
+                                                                 prev + prev / slack.first + slack.second));
     } else {
       nseg = 8;
     }
