@@ -35,7 +35,7 @@ for s in $STEPS; do
     serialworst) run serialworst 400 python tools/bench_serial.py --batches 8 --modes exact --worst-case ;;
     serialprof)
       rm -rf "$OUT/sprof"
-      (cd /tmp && run serialprof 400 rocprofv3 --kernel-trace --stats -d "$OUT/sprof" -o run -- \
+      (cd /tmp && run serialprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sprof" -o run -- \
          python "$ROOT/tools/bench_serial.py" --batches 30 --modes exact)
       find "$OUT/sprof" -name "*stats*" | head -20 ;;
     kbench) run kbench 300 python tools/bench_train_kernel.py ;;
@@ -44,7 +44,7 @@ for s in $STEPS; do
     bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
     prof)
       rm -rf "$OUT/prof"
-      (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+      (cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
          python "$ROOT/bench.py" --steps 5 --warmup 2 --latency-iters 20)
       find "$OUT/prof" -name "*stats*" | head -20 ;;
     lof)   # LOF engine record (native server over RPC) + its kernel stats
