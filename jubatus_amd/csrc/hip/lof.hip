@@ -412,7 +412,10 @@ __device__ __forceinline__ void lof_score_body(
     const float* __restrict__ kdist, const uint8_t* __restrict__ ok, float* __restrict__ lrd,
     uint8_t* __restrict__ lrd_ok, int store_slot, uint32_t* __restrict__ out, int max_missing,
     int32_t* __restrict__ abort_flag, LofLds& L, const uint32_t* __restrict__ kstamp = nullptr,
-    uint32_t* __restrict__ lstamp = nullptr, uint32_t epoch = 0, bool defer = false, bool have_lists = false) {
+    uint32_t* __restrict__ lstamp = nullptr, uint32_t epoch = 0, bool defer = false, bool have_lists = false,
+    bool no_cache = false) {
+  // no_cache: recomputed lrd values are used, not stored (several blocks
+  // scoring at once could otherwise see one block's lrd_ok before its lrd)
   // have_lists: the targets' lists and fields are in L already (the fused
   // insert left them there; targets = its candidates' head)
   // defer: out is device scratch the caller copies to the host later - plain
@@ -551,9 +554,11 @@ __device__ __forceinline__ void lof_score_body(
       if (good && (!lok || L.stale[t])) {
         const float mean = n > 0 ? sum / n : 0.f;
         lr = n == 0 ? 0.f : (mean <= 0.f ? INFINITY : 1.f / mean);
-        lrd[o] = lr;
-        lrd_ok[o] = 1;
-        if (lstamp != nullptr) lstamp[o] = epoch;
+        if (!no_cache) {
+          lrd[o] = lr;
+          lrd_ok[o] = 1;
+          if (lstamp != nullptr) lstamp[o] = epoch;
+        }
       }
     }
     s_lrd[t] = lr;
@@ -634,6 +639,32 @@ __global__ __launch_bounds__(64) void lof_score_kernel(
   lof_lds_sync();
   lof_score_body(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, store_slot, out,
                  max_missing, abort_flag, L, kstamp, lstamp, epoch);
+}
+
+// Independent scores in one launch, a block each (calc_score of a batch):
+// query q's targets ts_h / td_h [q * stride, + nt_h[q]) in pinned host
+// memory, its status and score into out + q * out_stride. Reads only: the
+// lrd values a block recomputes are not cached.
+__global__ __launch_bounds__(64) void lof_score_many_kernel(
+    const int32_t* __restrict__ ts_h, const float* __restrict__ td_h, const int32_t* __restrict__ nt_h, int stride,
+    int k, const int32_t* __restrict__ nb_slot, const float* __restrict__ nb_dist, const float* __restrict__ kdist,
+    const uint8_t* __restrict__ ok, float* __restrict__ lrd, uint8_t* __restrict__ lrd_ok,
+    const uint32_t* __restrict__ kstamp, uint32_t* __restrict__ lstamp, uint32_t* __restrict__ out, int out_stride,
+    int max_missing) {
+  __shared__ int32_t ts[kLofMaxK];
+  __shared__ float td[kLofMaxK];
+  __shared__ LofLds L;
+  const int q = blockIdx.x;
+  const int nt0 = nt_h[q];
+  const int nt = nt0 < kLofMaxK ? nt0 : kLofMaxK;
+  if ((int)threadIdx.x < nt) {
+    ts[threadIdx.x] = ts_h[(int64_t)q * stride + threadIdx.x];
+    td[threadIdx.x] = td_h[(int64_t)q * stride + threadIdx.x];
+  }
+  if (threadIdx.x == 0) L.prof = false;
+  lof_lds_sync();
+  lof_score_body(ts, td, nt, k, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, -1, out + (int64_t)q * out_stride,
+                 max_missing, nullptr, L, kstamp, lstamp, 0u, false, false, true);
 }
 
 // One add in one launch (stamps, no mark pass): p's insert (candidates in
@@ -893,30 +924,32 @@ extern "C" int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k
   return jb::wait_nonzero(out_host, stream);
 }
 
-// Several independent scores (calc_score of a batch of queries), one wait:
-// query i's targets are ts / td [i * stride, + nt[i]), its status and score
-// go to out_host + i * out_stride. The kernels only refresh cached lrd values
-// (the same values in any order); a query that finds rows without a valid
-// list reports them (status 2) and the host finishes it alone.
+// Several independent scores (calc_score of a batch of queries), one launch
+// (lof_score_many_kernel, a block per query): ts / td / nt in pinned host
+// memory (query i's targets [i * stride, + nt[i])), its status and score go to
+// out_host + i * out_stride. A query that finds rows without a valid list
+// reports them (status 2) and the host finishes it alone.
 extern "C" int jb_lof_score_many(int nq, const int32_t* ts, const float* td, const int32_t* nt, int stride,
                                  int k, const int32_t* nb_slot, const float* nb_dist, const float* kdist,
                                  const uint8_t* ok, float* lrd, uint8_t* lrd_ok, const uint32_t* kstamp,
                                  uint32_t* lstamp, uint32_t epoch, uint32_t* out_host, int out_stride,
                                  int max_missing, hipStream_t stream) {
+  (void)epoch;
   if (nq <= 0) return 0;
   if (k > jb::kLofMaxK || stride > 64) return -2;
-  for (int i = 0; i < nq; ++i) out_host[(int64_t)i * out_stride] = 0;
-  jb::LofArgs a;
   for (int i = 0; i < nq; ++i) {
-    int rc = fill_args(&a, ts + (int64_t)i * stride, td + (int64_t)i * stride, nt[i]);
-    if (rc) return rc;
-    hipLaunchKernelGGL(jb::lof_score_kernel, dim3(1), dim3(64), 0, stream, a, k, nb_slot, nb_dist, kdist, ok,
-                       lrd, lrd_ok, -1, out_host + (int64_t)i * out_stride, max_missing, (int32_t*)nullptr,
-                       kstamp, lstamp, epoch);
+    if (nt[i] < 0 || nt[i] > stride) return -2;
+    out_host[(int64_t)i * out_stride] = 0;
   }
+  hipLaunchKernelGGL(jb::lof_score_many_kernel, dim3((unsigned)nq), dim3(64), 0, stream, ts, td, nt, stride, k,
+                     nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, kstamp, lstamp, out_host, out_stride, max_missing);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
-  return jb::wait_nonzero(out_host + (int64_t)(nq - 1) * out_stride, stream);
+  for (int i = 0; i < nq; ++i) {          // the blocks finish in any order
+    const int rc = jb::wait_nonzero(out_host + (int64_t)i * out_stride, stream);
+    if (rc != 0) return rc;
+  }
+  return 0;
 }
 
 extern "C" int jb_lof_score(const int32_t* ts, const float* td, int nt, int k,

@@ -198,16 +198,19 @@ class LofState {
       int stride = 1;
       for (size_t i = 0; i < m; ++i) stride = std::max(stride, (int)ts[b + i].size());
       if (stride > 64) return;         // (the caller scores them one by one)
-      std::vector<int32_t> fts(m * (size_t)stride, 0), nt(m);
-      std::vector<float> ftd(m * (size_t)stride, 0.f);
+      // pinned staging the kernel reads (the add path's; never in use at once):
+      // ts [m][stride], td [m][stride], nt [m]
+      int32_t* fts = stage_;
+      float* ftd = reinterpret_cast<float*>(stage_ + m * (size_t)stride);
+      int32_t* nt = stage_ + 2 * m * (size_t)stride;
       for (size_t i = 0; i < m; ++i) {
         nt[i] = (int32_t)ts[b + i].size();
-        std::copy(ts[b + i].begin(), ts[b + i].end(), fts.begin() + (int64_t)i * stride);
-        std::copy(td[b + i].begin(), td[b + i].end(), ftd.begin() + (int64_t)i * stride);
+        std::copy(ts[b + i].begin(), ts[b + i].end(), fts + (int64_t)i * stride);
+        std::copy(td[b + i].begin(), td[b + i].end(), ftd + (int64_t)i * stride);
       }
-      const int rc = jb_lof_score_many((int)m, fts.data(), ftd.data(), nt.data(), stride, k_, nb_slot_.p, nb_dist_.p,
-                                       kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, kstamp_.p, lstamp_.p, epoch_, out_many_,
-                                       kOutStride, kLofMaxMissing, stream_);
+      const int rc = jb_lof_score_many((int)m, fts, ftd, nt, stride, k_, nb_slot_.p, nb_dist_.p, kdist_.p, ok_.p,
+                                       lrd_.p, lrd_ok_.p, kstamp_.p, lstamp_.p, epoch_, out_many_, kOutStride,
+                                       kLofMaxMissing, stream_);
       if (rc != 0) throw std::runtime_error("lof score_many failed: " + std::to_string(rc));
       for (size_t i = 0; i < m; ++i) {
         const uint32_t* o = out_many_ + i * kOutStride;
