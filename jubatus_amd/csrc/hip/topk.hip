@@ -2642,6 +2642,13 @@ __global__ __launch_bounds__(kSelThreads) void topk_select_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   uint32_t* qc = counter + (int64_t)q * kFuseSync;
+  // The hand-off is the guide's fence-free valid form (MI355X_MICROARCH.md,
+  // inter-workgroup visibility, Consumer bullet conditions 1-4): every byte
+  // is stored sc1 (agent atomic store) and read back sc1 (agent atomic load),
+  // every storing wave drains (vmcnt(0)) before the barrier, one lane adds
+  // behind it. No agent release / acquire fence is needed for sc1 traffic; a
+  // fence per block is an L2 write-back (~1.7-3.5 us, measured +25 us per call
+  // on the round-3 merge), which this kernel exists to avoid.
   if (t == 0)
     s_last = __hip_atomic_fetch_add(qc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
   __syncthreads();

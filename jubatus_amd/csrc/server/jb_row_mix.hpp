@@ -23,6 +23,7 @@
 // A receiver parses the datum of a row only when that row wins the fold and
 // is not held already.
 #pragma once
+#include <cmath>
 #include <string.h>
 
 #include <algorithm>
@@ -203,7 +204,11 @@ inline DiffView diff_view(const Value& d) {
   DiffView v;
   const Value* n = d.get("n");
   if (!n || !n->is_num()) throw std::runtime_error("mix: malformed row diff");
-  v.n = (size_t)n->num();
+  // n is a peer's double: reject negative / non-integral / NaN values before
+  // the cast, and compare sizes by division so no product can wrap
+  const double nd = n->num();
+  if (!(nd >= 0) || nd != std::floor(nd) || nd > 9.0e15) throw std::runtime_error("mix: malformed row diff");
+  v.n = (size_t)nd;
   v.ids = &diff_bin(d.get("ids"));
   v.ido = &diff_bin(d.get("ido"));
   v.ver = &diff_bin(d.get("ver"));
@@ -212,8 +217,11 @@ inline DiffView diff_view(const Value& d) {
   v.rp = &diff_bin(d.get("rp"));
   v.idx = &diff_bin(d.get("idx"));
   v.val = &diff_bin(d.get("val"));
-  if (v.ido->size() != 4 * (v.n + 1) || v.dato->size() != 4 * (v.n + 1) || v.ver->size() != 8 * v.n ||
-      v.rp->size() != 8 * (v.n + 1))
+  auto count_is = [](const std::string* b, size_t width, size_t want) {
+    return b->size() % width == 0 && b->size() / width == want;
+  };
+  if (!count_is(v.ver, 8, v.n) || !count_is(v.ido, 4, v.n + 1) || !count_is(v.dato, 4, v.n + 1) ||
+      !count_is(v.rp, 8, v.n + 1))
     throw std::runtime_error("mix: malformed row diff");
   for (size_t i = 0; i < v.n; ++i)
     if (v.off(*v.ido, i) > v.off(*v.ido, i + 1) || v.off(*v.dato, i) > v.off(*v.dato, i + 1))

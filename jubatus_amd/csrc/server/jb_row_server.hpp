@@ -529,6 +529,7 @@ class Model : public jb::mix::Mixable {
     const Value* dv = nullptr;
     std::string id;
     double score = 0;
+    bool scored = false;   // the add finished (a chunk that throws fails the rest)
     std::exception_ptr err;
   };
   void add_many(std::vector<AddReq>& rs) {
@@ -551,7 +552,7 @@ class Model : public jb::mix::Mixable {
         add_chunk(rs, ds, std::vector<size_t>(todo.begin() + c0, todo.begin() + c1));
       } catch (...) {
         for (size_t j = c0; j < c1; ++j)
-          if (!rs[todo[j]].err && rs[todo[j]].id.empty()) rs[todo[j]].err = std::current_exception();
+          if (!rs[todo[j]].err && !rs[todo[j]].scored) rs[todo[j]].err = std::current_exception();
       }
     }
   }
@@ -1121,19 +1122,27 @@ class Model : public jb::mix::Mixable {
         ++update_count;
         rs[i].id = std::to_string(next_id_++);
         rs[i].score = (double)insert(rs[i].id, std::move(ds[i]));
+        rs[i].scored = true;
       }
       return;
     }
     std::vector<int32_t> slots(B);
-    eng_->defer_writes(true);
-    for (size_t j = 0; j < B; ++j) {
-      const size_t i = idx[j];
-      ++update_count;
-      rs[i].id = std::to_string(next_id_++);
-      eng_->set(rs[i].id, std::move(ds[i]));
-      slots[j] = eng_->slot(rs[i].id);
+    // deferral always ends (a failed set must not leave the index deferred)
+    struct DeferGuard {
+      RowEngine* e;
+      ~DeferGuard() { e->defer_writes(false); }
+    };
+    {
+      eng_->defer_writes(true);
+      DeferGuard guard{eng_.get()};
+      for (size_t j = 0; j < B; ++j) {
+        const size_t i = idx[j];
+        ++update_count;
+        rs[i].id = std::to_string(next_id_++);
+        eng_->set(rs[i].id, std::move(ds[i]));
+        slots[j] = eng_->slot(rs[i].id);
+      }
     }
-    eng_->defer_writes(false);
     std::unordered_map<int32_t, size_t> order;
     for (size_t j = 0; j < B; ++j) order[slots[j]] = j;
     std::vector<const std::vector<int32_t>*> qi;
@@ -1163,7 +1172,10 @@ class Model : public jb::mix::Mixable {
       std::vector<float> sc;
       std::vector<int32_t> missing;
       const size_t m = st.add_many(ps, c, d, &sc, &missing);
-      for (size_t q = 0; q < m; ++q) rs[idx[j + q]].score = (double)sc[q];
+      for (size_t q = 0; q < m; ++q) {
+        rs[idx[j + q]].score = (double)sc[q];
+        rs[idx[j + q]].scored = true;
+      }
       j += m;
       if (j < B) {   // add j stopped on lists to install: finish it as insert() does
         std::unordered_set<int32_t> absent(slots.begin() + j + 1, slots.end());
@@ -1171,6 +1183,7 @@ class Model : public jb::mix::Mixable {
         rs[idx[j]].score = (double)score_from(std::vector<int32_t>(cs[j].begin(), cs[j].begin() + kk),
                                               std::vector<float>(cd[j].begin(), cd[j].begin() + kk), slots[j],
                                               &absent);
+        rs[idx[j]].scored = true;
         ++j;
       }
     }

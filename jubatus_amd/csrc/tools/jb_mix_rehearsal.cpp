@@ -19,6 +19,7 @@
 //   put(name, seed, n, keys) -> n       n rows written (ids from a keyspace)
 //   remove(name, id) -> bool
 //   rows(name) -> {id: [version, x]}    the store (x: the row's "x" value)
+//   apply_raw(name, bytes) -> n         apply one msgpack row diff as a MIX would
 //
 // usage: jb_mix_rehearsal -z host:port -n name -p port [-H rows] [-I ic_timeout]
 //                         [-i interval_count] [-s interval_sec] [-Z zk_timeout] [-R]
@@ -383,6 +384,12 @@ class HostRowModel : public jb::mix::Mixable {
     for (const auto& r : raw) bytes += r.size();
     return bytes;
   }
+  // one peer diff applied as a MIX would (tests feed malformed diffs here)
+  size_t apply_raw(const std::string& raw) {
+    std::lock_guard<std::mutex> g(mu_);
+    return jb::row::apply_row_diffs(*this, {jb::val::MsgpackReader((const uint8_t*)raw.data(), raw.size()).read()},
+                                    nullptr);
+  }
   // push mixers: the pair folds its two diffs, lower rank first
   uint64_t pair_mix(Group& grp, int peer) override {
     std::lock_guard<std::mutex> g(mu_);
@@ -567,6 +574,10 @@ int main(int argc, char** argv) {
             return resp_ok(r.msgid, Value::boolean(ok));
           }
           if (r.method == "rows") return resp_ok(r.msgid, rmodel.rows());
+          if (r.method == "apply_raw" && a.size() == 2) {   // a peer's diff bytes, as a MIX receives them
+            const std::string raw = a[1].as_str();
+            return resp_ok(r.msgid, Value::integer((int64_t)rmodel.apply_raw(raw)));
+          }
           if (r.method == "do_mix") return resp_ok(r.msgid, Value::boolean(mixer && mixer->do_mix()));
           if (r.method == "get_status") {
             std::vector<std::pair<std::string, std::string>> st;

@@ -213,3 +213,29 @@ def test_random_mixer_pairs_up(coord):
     finally:
         for r in ranks:
             r.stop()
+
+
+@pytest.mark.parametrize("n", [2 ** 62, 2 ** 61 + 1, -1, 1.5, float("nan"), 3])
+def test_malformed_row_diff_is_rejected(coord, n):
+    """a peer's row count must not pass the size checks by
+    wrapping (n = 2^62 with 4-byte offsets) nor be negative / fractional /
+    NaN; a diff whose arrays do not hold n rows is rejected whole and the
+    store is untouched"""
+    import msgpack
+    import struct
+    r = RowRank(coord.port, f"bad{abs(hash(str(n))) % 1000}")
+    try:
+        r.call("put", 3, 5, 100)
+        before = r.rows()
+        diff = {"n": n, "ids": b"abcd", "ido": struct.pack("<I", 0), "ver": b"",
+                "dat": b"", "dato": struct.pack("<I", 0), "rp": struct.pack("<q", 0),
+                "idx": b"", "val": b"", "removed": [], "w": [0, 0, b"", b""]}
+        raw = msgpack.packb(diff, use_bin_type=True)
+        with pytest.raises(Exception, match="malformed row diff"):
+            r.call("apply_raw", raw)
+        assert r.rows() == before
+        # the same arrays with the count they do hold (0 rows) apply cleanly
+        diff["n"] = 0
+        assert r.call("apply_raw", msgpack.packb(diff, use_bin_type=True)) == 0
+    finally:
+        r.stop()
