@@ -173,6 +173,99 @@ __device__ __forceinline__ void argmax_wrong(float& best, int& bl) {
   }
 }
 
+// apply the update of one feature (lane-per-feature form)
+template <int LC, int MODE, typename WT>
+__device__ __forceinline__ void apply_feature(WT* W, float* P, int32_t idx, float x, int y,
+                                              int lstar, bool use_s, int method, float tau,
+                                              float beta, float a, float b, float wy, float wl,
+                                              uint32_t rnd) {
+  const int64_t row = (int64_t)idx * LC;
+  const float dwy = use_s ? tau * a * x : tau * x;
+  const float dwl = use_s ? -tau * b * x : -tau * x;
+  if (MODE == kAtomic) {
+    addw(W + row + y, dwy, jb_mix32((uint32_t)(row + y), rnd));
+    if (lstar >= 0) addw(W + row + lstar, dwl, jb_mix32((uint32_t)(row + lstar), rnd));
+    if (use_s) {
+      atomicAdd(P + row + y, dprec(method, beta, x, a));
+      if (lstar >= 0) atomicAdd(P + row + lstar, dprec(method, beta, x, b));
+    }
+  } else {
+    stw(W + row + y, wy + dwy, jb_mix32((uint32_t)(row + y), rnd));
+    if (lstar >= 0) stw(W + row + lstar, wl + dwl, jb_mix32((uint32_t)(row + lstar), rnd));
+    if (use_s) {
+      P[row + y] = 1.f / a + dprec(method, beta, x, a);
+      if (lstar >= 0) P[row + lstar] = 1.f / b + dprec(method, beta, x, b);
+    }
+  }
+}
+
+// One sample on the direct path: gathers straight from W / P (any feature
+// count, any label capacity) and applies the update. Used for samples wider
+// than the pipelined window and for label capacities above 64. Returns
+// whether the sample updated. The increments are applied with float atomics
+// in every mode: a row repeated inside the sample then counts every time
+// (as in the reference's per-feature loop), and in exact mode (one stream)
+// nothing else touches the table, so the result is the same as plain stores.
+template <int LC, int MODE, typename WT>
+__device__ __forceinline__ bool general_sample(const int32_t* __restrict__ fidx,
+                                               const float* __restrict__ fval, int64_t beg, int n,
+                                               int y, WT* W, float* P, const bool (&act)[Lanes<LC>::K],
+                                               int lane, int method, float C,
+                                               uint8_t* __restrict__ touched) {
+  using L = Lanes<LC>;
+  const int l0 = lane % L::LW;
+  const bool use_s = method >= CW;
+  float acc[L::K];
+  sample_scores<LC>(fidx, fval, beg, n, W, lane, acc);
+  float sy = 0.f, best = -INFINITY;
+  int bl = -1;
+#pragma unroll
+  for (int k = 0; k < L::K; ++k) {
+    const int l = l0 + 64 * k;
+    if (l == y) sy = acc[k];
+    if (act[k] && l != y && acc[k] > best) { best = acc[k]; bl = l; }
+  }
+  sy = __shfl(sy, y % L::LW, 64);
+  argmax_wrong<L::LW>(best, bl);
+  const int lstar = bl;
+  const float margin = sy - (lstar >= 0 ? best : 0.f);
+  float var = 0.f, nrm = 0.f;
+  for (int base = 0; base < n; base += 64) {
+    const int j = base + lane;
+    if (j < n) {
+      const int32_t idx = fidx[beg + j];
+      const float x = fval[beg + j];
+      if (idx >= 0) {
+        const int64_t row = (int64_t)idx * LC;
+        nrm += x * x;
+        if (use_s) {
+          const float a = 1.f / ld_agent(P + row + y);
+          const float b = lstar >= 0 ? 1.f / ld_agent(P + row + lstar) : 0.f;
+          var += x * x * (a + b);
+        }
+      }
+    }
+  }
+  var = wave_sum(var);
+  nrm = wave_sum(nrm);
+  float tau = 0.f, beta = 0.f;
+  if (!step_coeffs(method, margin, var, nrm, lstar >= 0, C, &tau, &beta)) return false;
+  for (int base = 0; base < n; base += 64) {
+    const int j = base + lane;
+    if (j >= n) continue;
+    const int32_t idx = fidx[beg + j];
+    if (idx < 0) continue;
+    const float x = fval[beg + j];
+    const int64_t row = (int64_t)idx * LC;
+    const float a = use_s ? 1.f / ld_agent(P + row + y) : 1.f;
+    const float b = (use_s && lstar >= 0) ? 1.f / ld_agent(P + row + lstar) : 1.f;
+    apply_feature<LC, kAtomic>(W, P, idx, x, y, lstar, use_s, method, tau, beta, a, b, 0.f, 0.f,
+                               (uint32_t)beg);
+    if (touched != nullptr) touched[idx] = 1;
+  }
+  return true;
+}
+
 }  // namespace jb
 
 // label-capacity template dispatch (LC is a power of two, 8..1024)

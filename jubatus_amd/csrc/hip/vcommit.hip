@@ -84,7 +84,7 @@ enum : int {
   S_DONEB, S_NVALID, S_RETRYW, S_WEND,
   // batch counters
   S_WINDOWS, S_RETRIES, S_STEPS, S_ROUNDS, S_WASTED, S_REFRESH, S_EXACT, S_CAND, S_UPD, S_SAT, S_TICKS,
-  S_NONC, S_PH0, S_PH1, S_PH2, S_PH3, S_PH4, S_PHW, S_WIDE, S_NWORDS = 64
+  S_NONC, S_PH0, S_PH1, S_PH2, S_PH3, S_PH4, S_PHW, S_WIDE, S_DENSE_PM, S_NWORDS = 64
 };
 // committer stop reasons (S_WHY)
 enum : int { kWhyEnd = 0, kWhySat = 1, kWhyDense = 2 };
@@ -153,7 +153,8 @@ __device__ __forceinline__ float dprec_fast(int method, float beta, float x, flo
 __global__ __launch_bounds__(256) void vc_init_kernel(int64_t* __restrict__ st, const int64_t* __restrict__ sp,
                                                       int nstreams, unsigned long long* __restrict__ bits,
                                                       int64_t* __restrict__ tail, float t_force,
-                                                      int32_t* __restrict__ g_key, float* __restrict__ g_rmax) {
+                                                      int32_t* __restrict__ g_key, float* __restrict__ g_rmax,
+                                                      int dense_pm) {
   for (int i = threadIdx.x; i < kBitWords; i += blockDim.x) bits[i] = 0ull;
   const bool fresh = st[S_MAGIC] != kMagic;
   if (fresh)      // no previous window: the candidate rule's row bounds are empty
@@ -174,6 +175,7 @@ __global__ __launch_bounds__(256) void vc_init_kernel(int64_t* __restrict__ st, 
   st[S_STATUS] = beg < bend ? kNew : kDone;
   for (int i = S_NCAND; i <= S_RETRYW; ++i) st[i] = 0;
   for (int i = S_WINDOWS; i < S_NWORDS; ++i) st[i] = 0;
+  st[S_DENSE_PM] = dense_pm;
   for (int i = 0; i < 32; ++i) tail[i] = 0;
   tail[0] = beg < bend ? beg : bend;
   tail[1] = bend;
@@ -1020,7 +1022,13 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
       st[S_WINDOWS] += 1;
       st[S_UPD] += nupd;
       if (why == kWhySat) st[S_SAT] += 1;
-      st[S_STATUS] = why == kWhyDense ? kDense : (pe >= bend ? kDone : kNew);
+      // an update-dense window (more than dense_pm per mille of its samples
+      // updated): the rest of the batch goes to the sequential stepper
+      // (stepper.hip, ~0.2 us a sample whatever updates), which beats this
+      // committer's ~2.2 us a step once updates are that frequent
+      const int64_t dpm = st[S_DENSE_PM];
+      const bool dense = dpm > 0 && pe < bend && nupd * 1000 > dpm * (pe - wb);
+      st[S_STATUS] = (why == kWhyDense || dense) ? kDense : (pe >= bend ? kDone : kNew);
       // the window length follows where the store fills; T relaxes slowly
       int64_t lw = st[S_LW];
       if (why == kWhySat) {
@@ -1179,8 +1187,12 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
   // verification failures with a tiny one); unset: T adapts across batches
   const char* te = getenv("JB_VERIFIED_T");
   const float t_force = te != nullptr ? (float)atof(te) : 0.f;
+  // JB_VC_DENSE_PM: updates per mille of a committed window past which the
+  // rest of the batch goes to the stepper (0: never; default 100)
+  const char* de = getenv("JB_VC_DENSE_PM");
+  const int dense_pm = de != nullptr ? atoi(de) : 100;
   hipLaunchKernelGGL(jb::vc::vc_init_kernel, dim3(1), dim3(256), 0, stream, st, stream_ptr, nstreams, bits, tail,
-                     t_force, gk, gr);
+                     t_force, gk, gr, dense_pm);
   int rc = 0;
 #define JB_VC_L(L)                                                                                            \
   rc = launch_vc<L>(method, row_ptr, fidx, fval, labels, W, S, active, C, st, sl, bits, s0, aux, pp0, fi, fx, \

@@ -594,9 +594,11 @@ inline bool config_from_coordinator(const Args& a, std::string* text, std::strin
 // native_dist: the engine serves distributed mode (-z) natively with the
 // linear mixer (csrc/native/jb_mix_group.hpp); other mixers and engines are
 // handed to the Python server
+// host_ok: the engine serves on a GPU-less host natively (its host backend);
+// otherwise --cpu / no /dev/kfd hand the configuration to the Python server
 template <class Check>
 int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool needs_gpu = true,
-            bool native_dist = false, bool native_push = false) {
+            bool native_dist = false, bool native_push = false, bool host_ok = false) {
   int rc = parse_args(argc, argv, a);
   if (rc == -1) return 0;
   if (rc) return rc;
@@ -612,9 +614,9 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool
     const bool push = a->mixer == "random_mixer" || a->mixer == "broadcast_mixer" || a->mixer == "skip_mixer";
     if (dist && a->mixer != "linear_mixer" && !(push && native_push))
       exec_python(argc, argv, "distributed mode with a push mixer");
-    if (needs_gpu && (a->cpu || getenv("JUBATUS_FORCE_CPU")))
+    if (needs_gpu && !host_ok && (a->cpu || getenv("JUBATUS_FORCE_CPU")))
       exec_python(argc, argv, "host backend requested");
-    if (needs_gpu && access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
+    if (needs_gpu && !host_ok && access("/dev/kfd", R_OK | W_OK) != 0) exec_python(argc, argv, "no GPU (/dev/kfd)");
   }
   if (dist && a->name.empty()) {
     fprintf(stderr, "can't start multinode mode without name specified\n");
@@ -684,13 +686,24 @@ int startup(int argc, char** argv, Args* a, std::string* text, Check check, bool
       return 1;
     }
   } else if (!a->model_file.empty()) {
+    // the reference rejects what it cannot load and exits
+    // (server_helper.hpp:81-113: load_file throws; save_load.cpp:169-285)
     std::string bytes;
     ModelFile mf;
-    if (!read_file(a->model_file, &bytes)) exec_python(argc, argv, "unreadable model file");
-    if (!read_model_file(bytes, &mf).empty()) exec_python(argc, argv, "model file check");
+    if (!read_file(a->model_file, &bytes)) {
+      fprintf(stderr, "%s: cannot open input file: %s: %s\n", prog_name(), a->model_file.c_str(), strerror(errno));
+      return 1;
+    }
+    const std::string err = read_model_file(bytes, &mf);
+    if (!err.empty()) {
+      fprintf(stderr, "%s: %s: %s\n", prog_name(), a->model_file.c_str(), err.c_str());
+      return 1;
+    }
     *text = mf.config;
   } else if (!read_file(a->configpath, text)) {
-    exec_python(argc, argv, "unreadable config file");
+    // config.cpp:39-48 config_fromlocal: "can't read <path> ."
+    fprintf(stderr, "%s: can't read %s .\n", prog_name(), a->configpath.c_str());
+    return 1;
   }
   std::string why;
   if (a->native_check) {   // the config check alone (tests, operators): no GPU, no exec

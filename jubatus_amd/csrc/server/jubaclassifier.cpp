@@ -44,9 +44,11 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "jb_hash.hpp"
+#include "jb_host_linear.hpp"
 #include "jb_hostfv.hpp"
 #include "jb_linear_conv.hpp"
 #include "jb_mix_device.hpp"
@@ -226,6 +228,13 @@ class Classifier : public jb::mix::Mixable {
   }
 
   const std::string& config_text() const { return cfg_.text; }
+
+  // pinned receive slots of the transport (H2D straight from them)
+  static uint8_t* alloc_arena(size_t bytes) {
+    uint8_t* p = nullptr;
+    HIPCHK(hipHostMalloc((void**)&p, bytes, hipHostMallocDefault));
+    return p;
+  }
 
   // --------------------------------------------------------------- train
   // served train batch over an arena slot: -> per request sample count, -1
@@ -1399,13 +1408,709 @@ class Classifier : public jb::mix::Mixable {
   }
 };
 
+
+// ------------------------------------------------------------ host backend
+// GPU-less hosts (no /dev/kfd), --cpu and JUBATUS_FORCE_CPU: the same RPC
+// surface, model files and MIX protocol with the tables in host memory, so a
+// classifier server never needs Python (BASELINE config
+// #1: pa.json standalone on the CPU). Training is the reference's loop, one
+// sample after another under the model lock (classifier_serv.cpp:138-144),
+// with the update rules of jb_host_linear.hpp (the host serial trainer of the
+// CPU baseline); classify scores on the host; MIX runs the device tables'
+// protocol over the host plane (HostPlane: the coordinator star carries the
+// bytes). No HIP call is made in this mode.
+class HostClassifier : public jb::mix::Mixable {
+ public:
+  std::atomic<uint64_t> update_count{0};
+  std::atomic<uint64_t> train_calls{0}, train_batches{0};
+
+  explicit HostClassifier(const Config& cfg) { configure(cfg); }
+
+  static uint8_t* alloc_arena(size_t bytes) {
+    void* p = nullptr;
+    if (posix_memalign(&p, 4096, bytes) != 0) throw std::bad_alloc();
+    return (uint8_t*)p;
+  }
+
+  void configure(const Config& cfg) {
+    std::lock_guard<std::mutex> g(mu_);
+    cfg_ = cfg;
+    mid_ = cfg.method;
+    C_ = cfg.C;
+    use_s_ = mid_ >= kMethodCW;
+    H_ = cfg.rules.H;
+    conv_.configure(cfg.rules, cfg.wide, cfg.wrules);
+    labels_.clear();
+    count_base_.clear();
+    alloc_locked(kLabelCaps[0], true);
+    if (mixing_) touched_.assign(H_, 1);
+  }
+
+  const std::string& config_text() const { return cfg_.text; }
+
+  void train_arena(const uint8_t* arena, const std::vector<jb::ArenaReq>& reqs, std::vector<int64_t>* res,
+                   std::vector<std::string>* msgs) {
+    const size_t R = reqs.size();
+    res->assign(R, -1);
+    msgs->assign(R, std::string());
+    train_calls += R;
+    train_batches += 1;
+    update_count += R;
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t k = 0; k < R; ++k) train_locked(arena + reqs[k].off, reqs[k].len, &(*res)[k], &(*msgs)[k]);
+  }
+
+  void train_body(const uint8_t* b, size_t n, int64_t* res, std::string* msg) {
+    train_calls += 1;
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    train_locked(b, n, res, msg);
+  }
+
+  std::vector<std::string> classify(const std::vector<std::pair<const uint8_t*, size_t>>& bodies,
+                                    const std::vector<uint32_t>& msgids) {
+    const size_t R = bodies.size();
+    std::vector<std::string> out(R);
+    std::vector<int32_t> idx(1024);
+    std::vector<float> val(1024);
+    std::vector<int64_t> row(1024);
+    std::vector<float> sc;
+    std::lock_guard<std::mutex> g(mu_);
+    sync_labels_locked();
+    auto nm = labels_.names();
+    auto al = labels_.alive();
+    std::vector<int> cols;
+    for (size_t c = 0; c < nm.size(); ++c)
+      if (al[c]) cols.push_back((int)c);
+    for (size_t k = 0; k < R; ++k) {
+      int64_t n = 0, slots = 0;
+      row[0] = 0;
+      int rc;
+      while ((rc = conv_.hash_body(bodies[k].first, bodies[k].second, idx.data(), val.data(), row.data(),
+                                   (int64_t)row.size() - 1, (int64_t)idx.size(), &n, &slots)) == 2) {
+        n = slots = 0;
+        idx.resize(2 * idx.size());
+        val.resize(idx.size());
+        row.resize(2 * row.size());
+      }
+      if (rc != 0) { out[k] = jb::val::response_code(msgids[k], kArgumentError); continue; }
+      MsgpackWriter w;
+      w.arr((size_t)n);
+      sc.resize((size_t)LC_);
+      for (int64_t i = 0; i < n; ++i) {
+        jb::hl::scores(W_.data(), LC_, idx.data() + row[i], val.data() + row[i], (int)(row[i + 1] - row[i]),
+                       sc.data());
+        w.arr(cols.size());
+        for (int c : cols) {
+          w.arr(2);
+          w.raw(nm[c]);
+          w.dbl((double)sc[(size_t)c]);
+        }
+      }
+      out[k] = jb::val::response_ok(msgids[k], w.out);
+    }
+    return out;
+  }
+
+  std::vector<std::pair<std::string, uint64_t>> get_labels() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<std::pair<std::string, uint64_t>> out;
+    auto nm = labels_.names();
+    auto al = labels_.alive();
+    for (size_t c = 0; c < nm.size(); ++c)
+      if (al[c]) out.emplace_back(nm[c], labels_.count((int)c));
+    return out;
+  }
+
+  bool set_label(const std::string& l) {
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    if (labels_.lookup(l) >= 0) return false;
+    if (labels_.get_or_add(l.data(), l.size()) < 0) throw std::runtime_error("label table full");
+    sync_labels_locked();
+    return true;
+  }
+
+  bool delete_label(const std::string& l) {
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    const int i = labels_.lookup(l);
+    if (i < 0) return false;
+    labels_.remove(l);
+    for (uint64_t h = 0; h < H_; ++h) {
+      W_[h * LC_ + i] = 0.f;
+      if (use_s_) S_[h * LC_ + i] = 1.f;
+    }
+    sync_labels_locked();
+    return true;
+  }
+
+  void clear() {
+    update_count += 1;
+    std::lock_guard<std::mutex> g(mu_);
+    count_base_.clear();
+    labels_.clear();
+    conv_.clear();
+    alloc_locked(kLabelCaps[0], true);
+    if (mixing_) touched_.assign(H_, 1);
+  }
+
+  // the same user data as the device tables (models/classifier.py pack())
+  std::string pack_user_data() {
+    std::lock_guard<std::mutex> g(mu_);
+    auto nm = labels_.names();
+    auto al = labels_.alive();
+    std::vector<int> cols;
+    for (size_t c = 0; c < nm.size(); ++c)
+      if (al[c]) cols.push_back((int)c);
+    std::vector<int64_t> rows;
+    std::vector<float> Wr, Sr;
+    for (uint64_t h = 0; h < H_; ++h) {
+      const float* w = W_.data() + h * LC_;
+      bool t = false;
+      for (int c : cols) t |= w[c] != 0.f;
+      if (use_s_) {
+        const float* s = S_.data() + h * LC_;
+        for (int c : cols) t |= s[c] != 1.f;
+      }
+      if (!t) continue;
+      rows.push_back((int64_t)h);
+      for (int c : cols) Wr.push_back(w[c]);
+      if (use_s_)
+        for (int c : cols) Sr.push_back(S_[h * LC_ + c]);
+    }
+    MsgpackWriter u;
+    u.arr(2);
+    u.uint(1);
+    u.map(8);
+    u.str("method"); u.str(kMethods[mid_]);
+    u.str("H"); u.uint(H_);
+    u.str("labels"); u.arr(cols.size());
+    for (int c : cols) u.str(nm[c]);
+    u.str("counts"); u.arr(cols.size());
+    for (int c : cols) u.uint(labels_.count(c));
+    u.str("rows"); u.bin(rows.data(), rows.size() * 8);
+    u.str("W"); u.bin(Wr.data(), Wr.size() * 4);
+    u.str("P"); u.bin(Sr.data(), Sr.size() * 4);
+    u.str("weights");
+    conv_.pack(u);
+    return std::move(u.out);
+  }
+
+  void unpack(const Value& obj) {
+    if (obj.kind != Value::MAP) throw std::runtime_error("broken model data: driver pack");
+    const Value* H = obj.get("H");
+    if (!H || !H->is_num() || (uint64_t)H->num() != H_)
+      throw std::runtime_error("model hash_max_size differs from the configuration");
+    const Value* lv = obj.get("labels");
+    const Value* cv = obj.get("counts");
+    const Value* rv = obj.get("rows");
+    const Value* wv = obj.get("W");
+    const Value* pv = obj.get("P");
+    if (!lv || lv->kind != Value::ARR || !cv || cv->kind != Value::ARR || !rv || !wv)
+      throw std::runtime_error("broken model data: classifier tables");
+    const size_t L = lv->a.size();
+    const size_t nr = rv->s.size() / 8;
+    if (wv->s.size() != nr * L * 4) throw std::runtime_error("broken model data: W rows");
+    std::lock_guard<std::mutex> g(mu_);
+    labels_.clear();
+    int cap = -1;
+    for (int c : kLabelCaps)
+      if ((size_t)c >= std::max<size_t>(1, L)) { cap = c; break; }
+    if (cap < 0) throw std::runtime_error("at most 1024 labels are supported");
+    alloc_locked(cap, true);
+    for (size_t k = 0; k < L; ++k) {
+      labels_.get_or_add(lv->a[k].s.data(), lv->a[k].s.size());
+      labels_.set_count((int)k, k < cv->a.size() ? (uint64_t)cv->a[k].num() : 0);
+    }
+    sync_labels_locked();
+    const int64_t* rows = (const int64_t*)rv->s.data();
+    const float* wr = (const float*)wv->s.data();
+    const bool has_p = use_s_ && pv && pv->s.size() == nr * L * 4;
+    for (size_t k = 0; k < nr; ++k) {
+      if (rows[k] < 0 || (uint64_t)rows[k] >= H_) throw std::runtime_error("broken model data: row index");
+      memcpy(&W_[(size_t)rows[k] * LC_], wr + k * L, L * 4);
+      if (has_p) memcpy(&S_[(size_t)rows[k] * LC_], (const float*)pv->s.data() + k * L, L * 4);
+    }
+    conv_.unpack(obj.get("weights"));
+    if (mixing_) touched_.assign(H_, 1);
+  }
+
+  void status(std::vector<std::pair<std::string, std::string>>* st) {
+    std::lock_guard<std::mutex> g(mu_);
+    int live = 0;
+    for (bool a : labels_.alive()) live += a;
+    auto add = [&](const char* k, const std::string& v) { st->emplace_back(k, v); };
+    add("num_classes", std::to_string(live));
+    add("num_features", std::to_string(H_));
+    add("label_capacity", std::to_string(LC_));
+    add("method", kMethods[mid_]);
+    add("storage", "host");
+    add("fv_path", "host");
+    add("server_runtime", "native");
+    add("backend", "host");
+    add("train.samples_updated", std::to_string(n_upd_));
+    add("train.samples_trained", std::to_string(n_valid_));
+    add("train.update_mode", "exact");
+    add("batching.train.calls", std::to_string(train_calls.load()));
+    add("batching.train.launches", std::to_string(train_batches.load()));
+    add("host_model_bytes", std::to_string((W_.size() + S_.size()) * 4));
+    if (mixing_) {
+      add("mix.last_rows", std::to_string(last_rows_));
+      add("mix.last_mode", last_dense_ ? "dense" : "sparse");
+      add("mix.last_applied", last_applied_ ? "1" : "0");
+      add("mix.wire_dtype", "fp32");
+    }
+  }
+
+  // ------------------------------------------------------------ MIX (host)
+  void enable_mix() {
+    std::lock_guard<std::mutex> g(mu_);
+    mixing_ = true;
+    touched_.assign(H_, 1);   // the first MIX is dense
+  }
+  std::unique_ptr<jb::mix::Plane> make_plane(jb::mix::Star& star, double) {
+    return std::unique_ptr<jb::mix::Plane>(new jb::mix::HostPlane(&star));
+  }
+
+  uint64_t mix(jb::mix::Group& grp) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    std::string mine;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      for (size_t c = 0; c < nm.size(); ++c)
+        if (al[c]) put_name(&mine, nm[c]);
+    }
+    const auto parts = star.allgather(mine, grp.deadline());
+    std::vector<std::string> canon;
+    {
+      std::set<std::string> seen;
+      for (const auto& p : parts)
+        for (auto& n : get_names(p))
+          if (seen.insert(n).second) canon.push_back(n);
+    }
+    const int Lc = (int)canon.size();
+    std::vector<int32_t> map((size_t)std::max(Lc, 1), 0);
+    std::vector<int64_t> delta((size_t)std::max(Lc, 1), 0);
+    std::vector<uint64_t> cur_at((size_t)std::max(Lc, 1), 0);
+    std::vector<uint8_t> mark;
+    uint64_t gen;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& n : canon)
+        if (labels_.lookup(n) < 0 && labels_.get_or_add(n.data(), n.size()) < 0)
+          throw std::runtime_error("label table full");
+      sync_labels_locked();
+      for (int c = 0; c < Lc; ++c) {
+        const int col = labels_.lookup(canon[c]);
+        map[c] = col;
+        cur_at[c] = labels_.count(col);
+        delta[c] = (int64_t)cur_at[c] - (int64_t)count_base_[canon[c]];
+      }
+      mark.swap(touched_);
+      touched_.assign(H_, 0);
+      gen = gen_;
+    }
+    star.allreduce_sum(delta.data(), (size_t)Lc, grp.deadline());
+    uint64_t bytes = 8ull * Lc;
+    pl.allreduce_max(mark.data(), H_, grp.deadline());
+    bytes += H_;
+    std::vector<int64_t> rows;
+    for (uint64_t h = 0; h < H_; ++h)
+      if (mark[h]) rows.push_back((int64_t)h);
+    const bool dense = rows.size() * 2 > H_;
+    if (dense) {
+      rows.resize(H_);
+      for (uint64_t h = 0; h < H_; ++h) rows[h] = (int64_t)h;
+    }
+    last_rows_ = rows.size();
+    last_dense_ = dense;
+    bool applied = true;
+    if (!rows.empty() && Lc > 0) {
+      const size_t width = (size_t)(use_s_ ? 2 : 1) * Lc;
+      std::vector<float> snap(rows.size() * width), red;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (gen != gen_) applied = false;
+        else gather_locked(rows, map, Lc, snap.data());
+      }
+      int64_t ok[1] = {applied ? 0 : 1};
+      star.allreduce_max(ok, 1, grp.deadline());
+      if (ok[0] == 0) {
+        int64_t wire[1] = {1};   // fp32 on the wire (the device tables' agreement call)
+        star.allreduce_max(wire, 1, grp.deadline());
+        red = snap;
+        pl.allreduce_sum(red.data(), red.size(), grp.deadline());
+        bytes += red.size() * 4;
+        std::lock_guard<std::mutex> g(mu_);
+        if (gen == gen_) fold_locked(rows, map, Lc, snap.data(), red.data(), 1.f / (float)grp.world());
+        else applied = false;
+      } else {
+        applied = false;
+      }
+      if (!applied) {
+        std::lock_guard<std::mutex> g(mu_);
+        touched_.assign(H_, 1);
+      }
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (int c = 0; c < Lc; ++c) {
+        const uint64_t nb = (uint64_t)((int64_t)count_base_[canon[c]] + delta[c]);
+        const int col = labels_.lookup(canon[c]);
+        if (col >= 0) labels_.set_count(col, nb + (labels_.count(col) - cur_at[c]));
+        count_base_[canon[c]] = nb;
+      }
+    }
+    if (conv_.global()) {
+      std::string dm;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        dm = conv_.get_diff();
+      }
+      const auto dparts = pl.allgather_bytes(star, dm, grp.deadline());
+      std::lock_guard<std::mutex> g(mu_);
+      conv_.put_diffs(dparts);
+      bytes += dm.size();
+    }
+    last_applied_ = applied;
+    return bytes;
+  }
+
+  bool push_mixable() const override { return true; }
+  void push_begin() override {
+    std::lock_guard<std::mutex> g(mu_);
+    pmark_.swap(touched_);
+    touched_.assign(H_, 0);
+    push_dirty_ = false;
+  }
+  void push_end() override {
+    std::lock_guard<std::mutex> g(mu_);
+    conv_.clear_diff();
+    if (push_dirty_) touched_.assign(H_, 1);
+  }
+
+  uint64_t pair_mix(jb::mix::Group& grp, int peer) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    const double dl = grp.deadline();
+    std::string mine;
+    if (peer >= 0) {
+      std::lock_guard<std::mutex> g(mu_);
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      for (size_t c = 0; c < nm.size(); ++c)
+        if (al[c]) put_name(&mine, nm[c]);
+    }
+    const std::string theirs = pl.exchange_bytes(star, peer, mine, dl);
+    if (peer < 0) {
+      pl.pair_max(star, nullptr, 0, -1, dl);
+      pl.exchange_bytes(star, -1, std::string(), dl);
+      pl.pair_sum(star, nullptr, 0, -1, dl);
+      if (conv_.global()) pl.exchange_bytes(star, -1, std::string(), dl);
+      return 0;
+    }
+    std::vector<std::string> canon;
+    {
+      std::set<std::string> seen;
+      const std::string& first = grp.rank() < peer ? mine : theirs;
+      const std::string& second = grp.rank() < peer ? theirs : mine;
+      for (const std::string* p : {&first, &second})
+        for (auto& n : get_names(*p))
+          if (seen.insert(n).second) canon.push_back(n);
+    }
+    const int Lc = (int)canon.size();
+    std::vector<int32_t> map((size_t)std::max(Lc, 1), 0);
+    uint64_t gen;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (const auto& n : canon)
+        if (labels_.lookup(n) < 0 && labels_.get_or_add(n.data(), n.size()) < 0)
+          throw std::runtime_error("label table full");
+      sync_labels_locked();
+      for (int c = 0; c < Lc; ++c) map[c] = labels_.lookup(canon[c]);
+      gen = gen_;
+    }
+    if (pmark_.size() != H_) pmark_.assign(H_, 1);
+    pl.pair_max(star, pmark_.data(), H_, peer, dl);
+    uint64_t bytes = H_;
+    std::vector<int64_t> rows;
+    for (uint64_t h = 0; h < H_; ++h)
+      if (pmark_[h]) rows.push_back((int64_t)h);
+    last_rows_ = rows.size();
+    last_dense_ = rows.size() * 2 > H_;
+    const size_t width = (size_t)(use_s_ ? 2 : 1) * Lc;
+    const size_t elems = rows.size() * width;
+    std::vector<float> snap(elems), red;
+    bool applied = gen == gen_;
+    if (applied && elems > 0) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (gen != gen_) applied = false;
+      else gather_locked(rows, map, Lc, snap.data());
+    }
+    const std::string ok = pl.exchange_bytes(star, peer, applied ? "1" : "0", dl);
+    const bool both = applied && ok == "1";
+    red = snap;
+    pl.pair_sum(star, both ? red.data() : nullptr, both ? elems : 0, both ? peer : -1, dl);
+    if (both && elems > 0) {
+      bytes += elems * 4;
+      std::lock_guard<std::mutex> g(mu_);
+      if (gen == gen_) fold_locked(rows, map, Lc, snap.data(), red.data(), 0.5f);
+      else applied = false;
+    }
+    if (!both || !applied) push_dirty_ = true;
+    if (conv_.global()) {
+      std::string dm;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        dm = conv_.get_diff();
+      }
+      const std::string td = pl.exchange_bytes(star, peer, dm, dl);
+      std::lock_guard<std::mutex> g(mu_);
+      conv_.put_diffs(grp.rank() < peer ? std::vector<std::string>{dm, td} : std::vector<std::string>{td, dm},
+                      true);
+      bytes += dm.size();
+    }
+    last_applied_ = applied && both;
+    return bytes;
+  }
+
+  void hand_over(jb::mix::Group& grp, int src, bool apply) override {
+    jb::mix::Star& star = grp.star();
+    jb::mix::Plane& pl = grp.plane();
+    std::string meta;
+    int LC = 0;
+    std::vector<float> hw, hs;
+    if (grp.rank() == src) {
+      std::lock_guard<std::mutex> g(mu_);
+      LC = LC_;
+      auto nm = labels_.names();
+      auto al = labels_.alive();
+      meta.append((const char*)&LC, 4);
+      for (size_t c = 0; c < nm.size(); ++c) {
+        put_name(&meta, nm[c]);
+        const uint64_t cnt = labels_.count((int)c);
+        meta.append((const char*)&cnt, 8);
+        meta.push_back(al[c] ? 1 : 0);
+      }
+      hw = W_;
+      hs = S_;
+    }
+    meta = star.bcast_str(src, meta, grp.deadline());
+    if (meta.size() < 4) throw std::runtime_error("hand-over: broken label table");
+    memcpy(&LC, meta.data(), 4);
+    const size_t tb = H_ * (size_t)LC;
+    hw.resize(tb);
+    pl.bcast(hw.data(), tb * 4, src, grp.deadline());
+    if (use_s_) {
+      hs.resize(tb);
+      pl.bcast(hs.data(), tb * 4, src, grp.deadline());
+    }
+    if (!apply || grp.rank() == src) return;
+    std::lock_guard<std::mutex> g(mu_);
+    labels_.clear();
+    alloc_locked(LC, true);
+    size_t o = 4;
+    count_base_.clear();
+    while (o < meta.size()) {
+      std::string nm = take_name(meta, &o);
+      uint64_t cnt;
+      if (o + 9 > meta.size()) throw std::runtime_error("hand-over: broken label table");
+      memcpy(&cnt, meta.data() + o, 8);
+      const bool alive = meta[o + 8] != 0;
+      o += 9;
+      const int id = labels_.get_or_add(nm.data(), nm.size());
+      labels_.set_count(id, cnt);
+      count_base_[nm] = cnt;
+      if (!alive) labels_.remove(nm);
+    }
+    W_ = std::move(hw);
+    if (use_s_) S_ = std::move(hs);
+    sync_labels_locked();
+  }
+
+ private:
+  // one request body on the host: validate it whole, commit labels and
+  // counts, hash, then its samples one after another
+  void train_locked(const uint8_t* b, size_t len, int64_t* res, std::string* msg) {
+    jb::Cursor c{b, b + len};
+    uint32_t cnt;
+    if (!c.array(&cnt) || cnt > len) { *res = -1; return; }
+    std::vector<std::pair<const uint8_t*, uint32_t>> labs;
+    labs.reserve(cnt);
+    int64_t slots = 0;
+    row_.assign((size_t)cnt + 1, 0);
+    const jb::Cursor start = c;
+    conv_.begin();
+    for (uint32_t k = 0; k < cnt; ++k) {
+      uint32_t two;
+      const uint8_t* ls;
+      uint32_t ln;
+      if (!c.array(&two) || two != 2 || !c.raw(&ls, &ln)) { conv_.rollback(); *res = -1; return; }
+      labs.emplace_back(ls, ln);
+      if (idx_.size() < 256) { idx_.resize(256); val_.resize(256); }
+      const int rc = conv_.hash_datum(c, idx_.data(), val_.data(), (int64_t)idx_.size(), &slots, true);
+      if (rc == 2) {   // out of slots: grow and hash the request again
+        conv_.rollback();
+        idx_.resize(2 * idx_.size());
+        val_.resize(idx_.size());
+        c = start;
+        labs.clear();
+        slots = 0;
+        k = (uint32_t)-1;
+        conv_.begin();
+        continue;
+      }
+      if (rc != 0) { conv_.rollback(); *res = -1; return; }
+      row_[k + 1] = slots;
+    }
+    if (c.p != c.end) { conv_.rollback(); *res = -1; return; }
+    std::vector<int32_t> lab(cnt);
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const int id = labels_.get_or_add((const char*)labs[k].first, labs[k].second);
+      if (id < 0) { conv_.rollback(); *res = -2; *msg = "label table full"; return; }
+      lab[k] = id;
+    }
+    try {
+      sync_labels_locked();
+    } catch (const std::exception& e) {
+      conv_.rollback();
+      *res = -2;
+      *msg = e.what();
+      return;
+    }
+    for (uint32_t k = 0; k < cnt; ++k) labels_.add_count(lab[k], 1);
+    *res = cnt;
+    jb::hl::Trainer tr(mid_, C_, LC_, active_.data(), W_.data(), use_s_ ? S_.data() : nullptr);
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const int y = lab[k];
+      if (y < 0 || y >= LC_) continue;
+      ++n_valid_;
+      const int32_t* ix = idx_.data() + row_[k];
+      const int n = (int)(row_[k + 1] - row_[k]);
+      if (k + 1 < cnt) tr.prefetch(idx_.data() + row_[k + 1], (int)(row_[k + 2] - row_[k + 1]));
+      if (tr.step(ix, val_.data() + row_[k], n, y, nullptr)) {
+        ++n_upd_;
+        if (mixing_)
+          for (int f = 0; f < n; ++f)
+            if (ix[f] >= 0) touched_[(size_t)ix[f]] = 1;
+      }
+    }
+  }
+
+  void alloc_locked(int LC, bool fresh) {
+    std::vector<float> W((size_t)H_ * LC, 0.f), S;
+    if (use_s_) S.assign((size_t)H_ * LC, 1.f);
+    if (!fresh && LC_ > 0 && !W_.empty())
+      for (uint64_t h = 0; h < H_; ++h) {
+        memcpy(&W[h * LC], &W_[h * LC_], (size_t)LC_ * 4);
+        if (use_s_) memcpy(&S[h * LC], &S_[h * LC_], (size_t)LC_ * 4);
+      }
+    W_.swap(W);
+    S_.swap(S);
+    LC_ = LC;
+    active_.assign((size_t)LC, 0);
+    label_version_ = ~0ull;
+    ++gen_;
+  }
+
+  void sync_labels_locked() {
+    const uint64_t v = labels_.version();
+    if (v == label_version_) return;
+    const int n = labels_.size();
+    if (n > LC_) {
+      int cap = -1;
+      for (int c : kLabelCaps)
+        if (c >= n) { cap = c; break; }
+      if (cap < 0) throw std::runtime_error("at most 1024 labels are supported");
+      alloc_locked(cap, false);
+    }
+    auto alive = labels_.alive();
+    active_.assign((size_t)LC_, 0);
+    for (size_t i = 0; i < alive.size() && i < (size_t)LC_; ++i) active_[i] = alive[i] ? 1 : 0;
+    label_version_ = v;
+  }
+
+  // [W columns | S columns] of the union rows, in canonical label order
+  void gather_locked(const std::vector<int64_t>& rows, const std::vector<int32_t>& map, int Lc, float* snap) {
+    const size_t width = (size_t)(use_s_ ? 2 : 1) * Lc;
+    for (size_t i = 0; i < rows.size(); ++i) {
+      const float* w = W_.data() + (size_t)rows[i] * LC_;
+      for (int c = 0; c < Lc; ++c) snap[i * width + c] = w[map[c]];
+      if (use_s_) {
+        const float* s = S_.data() + (size_t)rows[i] * LC_;
+        for (int c = 0; c < Lc; ++c) snap[i * width + Lc + c] = s[map[c]];
+      }
+    }
+  }
+  // T += sum * scale - snapshot (updates made during the MIX stay)
+  void fold_locked(const std::vector<int64_t>& rows, const std::vector<int32_t>& map, int Lc, const float* snap,
+                   const float* red, float scale) {
+    const size_t width = (size_t)(use_s_ ? 2 : 1) * Lc;
+    for (size_t i = 0; i < rows.size(); ++i) {
+      float* w = W_.data() + (size_t)rows[i] * LC_;
+      for (int c = 0; c < Lc; ++c) w[map[c]] += red[i * width + c] * scale - snap[i * width + c];
+      if (use_s_) {
+        float* s = S_.data() + (size_t)rows[i] * LC_;
+        for (int c = 0; c < Lc; ++c) s[map[c]] += red[i * width + Lc + c] * scale - snap[i * width + Lc + c];
+      }
+    }
+  }
+
+  static void put_name(std::string* o, const std::string& n) {
+    const uint32_t k = (uint32_t)n.size();
+    o->append((const char*)&k, 4);
+    *o += n;
+  }
+  static std::string take_name(const std::string& b, size_t* o) {
+    if (*o + 4 > b.size()) throw std::runtime_error("MIX: broken label list");
+    uint32_t k;
+    memcpy(&k, b.data() + *o, 4);
+    *o += 4;
+    if (*o + k > b.size()) throw std::runtime_error("MIX: broken label list");
+    std::string n = b.substr(*o, k);
+    *o += k;
+    return n;
+  }
+  static std::vector<std::string> get_names(const std::string& b) {
+    std::vector<std::string> out;
+    size_t o = 0;
+    while (o < b.size()) out.push_back(take_name(b, &o));
+    return out;
+  }
+
+  std::mutex mu_;
+  Config cfg_;
+  int mid_ = 0, LC_ = 0;
+  float C_ = 1.f;
+  bool use_s_ = false;
+  uint64_t H_ = 0;
+  std::vector<float> W_, S_;
+  std::vector<uint8_t> active_;
+  jb::LabelTable labels_;
+  uint64_t label_version_ = ~0ull, gen_ = 0;
+  LinearConv conv_;
+  std::vector<int32_t> idx_;
+  std::vector<float> val_;
+  std::vector<int64_t> row_;
+  uint64_t n_upd_ = 0, n_valid_ = 0;
+  // distributed mode
+  bool mixing_ = false;
+  std::vector<uint8_t> touched_, pmark_;
+  std::map<std::string, uint64_t> count_base_;
+  uint64_t last_rows_ = 0;
+  bool last_dense_ = false, last_applied_ = true, push_dirty_ = false;
+};
+
 // ----------------------------------------------------------------- server
+// M: Classifier (device tables) or HostClassifier (host tables)
+template <class M>
 class Server {
  public:
-  Server(const Args& a, const Config& cfg, int device) : a_(a) {
-    clf_.reset(new Classifier(cfg, device));
-    cs_.start_time = time(nullptr);
-  }
+  Server(const Args& a, std::unique_ptr<M> clf) : a_(a), clf_(std::move(clf)) { cs_.start_time = time(nullptr); }
 
   void load_file(const std::string& path) { load_impl(path, true); }
 
@@ -1421,11 +2126,7 @@ class Server {
     const char* mb = getenv("JUBATUS_TRAIN_ARENA_MB");
     const size_t slot_bytes = (size_t)atoll(mb ? mb : "32") << 20;
     const int nbatch = atoi(getenv("JUBATUS_ARENA_THREADS") ? getenv("JUBATUS_ARENA_THREADS") : "2");
-    for (int k = 0; k < std::max(1, nbatch) + 2; ++k) {
-      uint8_t* p = nullptr;
-      HIPCHK(hipHostMalloc((void**)&p, slot_bytes, hipHostMallocDefault));
-      slots_.push_back(p);
-    }
+    for (int k = 0; k < std::max(1, nbatch) + 2; ++k) slots_.push_back(M::alloc_arena(slot_bytes));
     rpc_->set_arena_batch("train", slots_, slot_bytes,
                           [this](int slot, const std::vector<jb::ArenaReq>& reqs) {
                             return arena(slot, reqs);
@@ -1452,14 +2153,14 @@ class Server {
       ma.interval_sec = a_.interval_sec;
       ma.interval_count = a_.interval_count;
       ma.interconnect_timeout = a_.ic_timeout;
-      Classifier* c = clf_.get();
+      M* c = clf_.get();
       mixer_.reset(new jb::mix::LinearMixer(node_->coord(), ma, c, [c](jb::mix::Group& g, double dl) {
         return c->make_plane(g.star(), dl);
       }));
       mixer_->start();
       logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
     }
-    logf_("INFO", "jubaclassifier RPC server startup (native)");
+    logf_("INFO", "jubaclassifier RPC server startup (native%s)", std::is_same<M, HostClassifier>::value ? ", host" : "");
     wait_for_term();
     if (mixer_) {
       logf_("INFO", "stopping mixer thread");
@@ -1703,7 +2404,7 @@ class Server {
   }
 
   Args a_;
-  std::unique_ptr<Classifier> clf_;
+  std::unique_ptr<M> clf_;
   std::unique_ptr<jb::mix::ClusterNode> node_;
   std::unique_ptr<jb::mix::LinearMixer> mixer_;
   std::unique_ptr<jb::RpcServer> rpc_;
@@ -1731,15 +2432,38 @@ int main(int argc, char** argv) {
     if (parse_config(t, &cfg, why)) return true;
     if (jb::rowsrv::is_nn_classifier(ncfg.outer)) *why = wn;
     return false;
-  }, true, /*native_dist=*/true, /*native_push=*/true);
+  }, true, /*native_dist=*/true, /*native_push=*/true, /*host_ok=*/true);
   if (rc >= 0) return rc;
+  // a GPU-less host (or --cpu / JUBATUS_FORCE_CPU): the linear methods run on
+  // the native host backend; the nearest-neighbor methods need the device
+  const bool host = a.cpu || getenv("JUBATUS_FORCE_CPU") != nullptr || access("/dev/kfd", R_OK | W_OK) != 0;
+  if (nn && host) exec_python(argc, argv, "nearest-neighbor classifier without a GPU");
   if (nn) return jb::rowsrv::row_serve(jb::rowsrv::Kind::kClassifier, a, ncfg);
+  if (host) {
+    try {
+      block_signals();
+      logf_("INFO", "starting jubaclassifier %s RPC server at %s:%d (native, host backend)", kVersion,
+            a.eth.c_str(), a.port);
+      Server<HostClassifier> srv(a, std::unique_ptr<HostClassifier>(new HostClassifier(cfg)));
+      if (!a.zookeeper.empty()) {
+        srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
+            new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), "classifier", a.name)));
+      } else if (!a.model_file.empty()) {
+        srv.load_file(a.model_file);
+      }
+      logf_("INFO", "config loaded: %s", kMethods[cfg.method]);
+      return srv.run();
+    } catch (const std::exception& e) {
+      logf_("FATAL", "failed to start classifier: %s", e.what());
+      return 1;
+    }
+  }
   // below this line the process owns the GPU: no exec
   try {
     const int device = device_and_signals(a);
     logf_("INFO", "starting jubaclassifier %s RPC server at %s:%d (native, device %d)", kVersion,
           a.eth.c_str(), a.port, device);
-    Server srv(a, cfg, device);
+    Server<Classifier> srv(a, std::unique_ptr<Classifier>(new Classifier(cfg, device)));
     if (!a.zookeeper.empty()) {
       srv.join_cluster(std::unique_ptr<jb::mix::ClusterNode>(
           new jb::mix::ClusterNode(a.zookeeper, std::max(1, a.zk_timeout), "classifier", a.name)));

@@ -51,6 +51,8 @@ _SIGS = {
     "jb_serial_scratch_bytes": [_i64],
     "jb_serial_scratch_bytes_lc": [_i64, _i32],
     "jb_serial_scratch_forget": [_c_void_p],
+    "jb_stepper_error": [],
+    "jb_stepper_prof": [_c_void_p],
     "jb_hot_detect": [_c_void_p, _i32, _c_void_p, _i64, _i32, _i32, _i32, _c_void_p, _c_void_p,
                       _i32, _c_void_p, _c_void_p, _c_void_p],
     "jb_linear_classify": [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p,
@@ -510,6 +512,27 @@ UPDATE_MODES = {"exact": UPDATE_SERIAL, "atomic": UPDATE_ATOMIC, "hogwild": UPDA
 METHODS = {"perceptron": 0, "PA": 1, "PA1": 2, "PA2": 3, "CW": 4, "AROW": 5, "NHERD": 6}
 
 
+def stepper_error() -> int:
+    """abort reason of a sequential-stepper launch since the last call (0:
+    none; csrc/hip/stepper.hip waits time out instead of hanging)"""
+    return int(_fn("jb_stepper_error")())
+
+
+STEPPER_PROF_KEYS = ("step_total", "step_wait", "load_idle", "fetch_retire", "load_stuck", "meta_room",
+                     "samples", "stages", "misses", "direct", "load_lookup", "fetch_issue", "load_total",
+                     "meta_total", "fetch_total")
+
+
+def stepper_prof() -> dict:
+    """JB_STEPPER_PROF=1: shader cycles per stepper wave phase (and sample /
+    stage / miss counts) since the last call"""
+    import numpy as np
+    out = np.zeros(16, np.uint64)
+    if _fn("jb_stepper_prof")(out.ctypes.data) != 0:
+        return {}
+    return {k: int(v) for k, v in zip(STEPPER_PROF_KEYS, out.tolist())}
+
+
 def _fn(name: str):
     f = _fns.get(name)
     if f is None:
@@ -693,7 +716,10 @@ class SerialScratch:
                        candidates=v[27], non_candidates_verified=v[7], committer_updates=v[24],
                        wasted_steps=v[22], refreshes=v[23], exact_rescored=v[26], last_segment_rows=v[25],
                        window_len=v[8], T=round(struct.unpack("f", struct.pack("I", v[9] & 0xffffffff))[0], 4),
-                       commit_kernel_us=round(v[30] / 100.0, 1))
+                       commit_kernel_us=round(v[30] / 100.0, 1),
+                       # the rest after an update-dense window (stop_reason
+                       # "dense") ran on the sequential stepper (csrc/hip/stepper.hip)
+                       stepper_samples=v[1] - v[0])
             if v[15] > 0:      # JB_COMMIT_PROF=1: committer phases (shader cycles -> us by the wall clock)
                 us = (v[30] / 100.0) / v[15]
                 for i, nm in enumerate(("round_start", "select", "decide", "apply", "correct")):

@@ -45,6 +45,7 @@ def main():
         for y in range(16):
             clf.set_label(f"label{y}")
         times, upd, diag = [], [], []
+        sprof = {}
         for b, arena in enumerate(data.batches):
             st0 = clf.train_stats()
             torch.cuda.synchronize()
@@ -61,6 +62,12 @@ def main():
                         "window_len", "saturated_windows", "non_candidates_verified")
                 diag.append((d["exact_steps"], (d["end"] - d["tail_start"]) / max(1, d["end"]),
                              {k: v for k, v in d.items() if k.startswith("commit") or k in keys}))
+            if os.environ.get("JB_STEPPER_PROF") == "1" and mode == "exact":
+                from jubatus_amd.ops import hip as _hip
+                sp = _hip.stepper_prof()
+                if b >= 2:
+                    for k, v in sp.items():
+                        sprof[k] = sprof.get(k, 0) + v
             if b % 10 == 9:
                 print(f"{mode} batch {b + 1}: {times[-1]:.2f} ms, update fraction {upd[-1]:.4f}"
                       + (f", exact steps {diag[-1][0]}, sequential tail {diag[-1][1]:.3f}, {diag[-1][2]}"
@@ -79,6 +86,13 @@ def main():
                 for key in diag[lo][2]:
                     rec[key] = round(float(np.mean([x[2].get(key, 0) for x in diag[lo:hi]])), 1)
             print(json.dumps(rec), flush=True)
+        if sprof:
+            # stepper wave phases over batches 2+ (shader cycles; per sample)
+            ns = max(1, sprof.get("samples", 1))
+            print(json.dumps({"mode": mode, "stepper_prof": sprof,
+                              "cycles_per_sample": {k: round(v / ns, 1) for k, v in sprof.items()
+                                                    if k not in ("samples", "stages", "misses", "direct")}}),
+                  flush=True)
         del clf
         torch.cuda.empty_cache()
 
