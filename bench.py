@@ -38,6 +38,7 @@ Usage: python bench.py --gpus N --steps K --warmup W
 from __future__ import annotations
 
 import argparse
+import io
 import json
 import os
 import random
@@ -457,26 +458,91 @@ DIST_ENGINE_CASES = (
     ("lof", "anomaly", "config/anomaly/lof.json", "add", "calc_score"),
     ("kmeans", "clustering", "config/clustering/kmeans.json", "push", "get_nearest_center"),
     ("gmm", "clustering", "config/clustering/gmm.json", "push", "get_nearest_center"),
-    # the headline engine through the native servers' linear mixer (touched-row
-    # diff all-reduce on the RCCL plane), next to the Python TableMix path of
-    # the headline's own N-GPU run
+    # the headline engine served natively on every rank: jubaclassifier with
+    # the linear mixer (touched-row diff all-reduce on the RCCL plane) under a
+    # timed train load, MIXes running inside the window
     ("arow", "classifier", "config/classifier/arow.json", "train", "classify"),
 )
 
 
+def _dist_files(args, nat, name: str, upd: str, qry: str, cname: str, rank: int, tmp: str):
+    """per-rank jubaloadgen parameter files of a distributed engine case:
+    (fill file, query file, units the fill carries). LOF: one distinct row per
+    add; clustering: 1000-point pushes (three blobs); AROW: 128-sample train
+    requests of the headline's label-correlated stream"""
+    cn = msgpack.packb(cname)
+    fill = os.path.join(tmp, f"{name}_{rank}_fill.bin")
+    qf = os.path.join(tmp, f"{name}_{rank}_query.bin")
+    if upd == "add":
+        rows = _row_datums(args.dist_engine_rows + 512, 101 + rank)
+        queries, rows = rows[-512:], rows[:-512]
+        with open(fill, "wb") as f:
+            for d in rows:
+                f.write(b"\x92" + cn + d)
+        with open(qf, "wb") as f:
+            for d in queries:
+                f.write(b"\x92" + cn + d)
+        return fill, qf, len(rows)
+    if upd == "push":
+        rng = np.random.default_rng(7 + rank)
+        centers = np.array([[0.0, 0.0, 0.0], [10.0, 10.0, 0.0], [-10.0, 10.0, 5.0]])
+        npts, per = args.dist_cluster_points, 1000
+
+        def point(i):
+            c = centers[i % 3] + rng.normal(0, 0.5, 3)
+            return [[["tag", f"t{i % 7}"]], [["a", float(c[0])], ["b", float(c[1])], ["c", float(c[2])]], []]
+        with open(fill, "wb") as f:
+            for b0 in range(0, npts, per):
+                f.write(b"\x92" + cn + msgpack.packb([point(b0 + i) for i in range(per)], use_bin_type=False))
+        with open(qf, "wb") as f:
+            for i in range(512):
+                f.write(b"\x92" + cn + msgpack.packb(point(i), use_bin_type=False))
+        return fill, qf, (npts + per - 1) // per * per
+    # train: the headline's request shape and stream (fresh values per send)
+    K = max(16, min(args.rpc_distinct, 256))
+    cap = K * args.per_request * 400 + (1 << 20)
+    buf = np.zeros(cap, np.uint8)
+    offs = np.zeros(K, np.int64)
+    lens = np.zeros(K, np.int64)
+    used = nat.synth_requests(buf.ctypes.data, cap, offs.ctypes.data, lens.ctypes.data, 4242 + rank, 0,
+                              K, args.per_request, args.labels, args.str_features, args.num_features,
+                              args.vocab, 16, 0.6, 8)
+    assert used > 0
+    with open(fill, "wb") as f:
+        for o, n in zip(offs, lens):
+            f.write(b"\x92" + cn + buf[o:o + n].tobytes())
+    one = msgpack.unpackb(buf[offs[0]:offs[0] + lens[0]].tobytes(), raw=False)
+    with open(qf, "wb") as f:
+        for _, d in one[:64]:
+            f.write(b"\x92" + cn + msgpack.packb([d], use_bin_type=False))
+    return fill, qf, args.per_request
+
+
 def dist_engine_records(args, rank: int, world: int, local: int, device, group) -> dict:
-    """BASELINE #4 / #5 on N ranks: one engine server per rank (the native
-    binary; on --device cpu it hands over to the Python server) joins one
-    cluster through a coordinator rank 0 starts; every rank fills its own
-    server (anomaly add: cluster-wide ids, CHT owners, server-to-server
-    update; clustering push), rank 0 forces one MIX (do_mix: the row diffs /
-    coresets over the group's plane, RCCL between GPUs) and every rank then
-    queries its server. Per engine: observed world size, fill rate, MIX
-    latency / bytes / plane, query rate (sum over ranks) and whether the
-    members answer alike after the MIX."""
-    import threading
+    """BASELINE #4 / #5 (and the headline engine) on N ranks through the
+    native servers: one engine server per rank joins one cluster through a
+    coordinator rank 0 starts; every rank fills its own server with the
+    native load generator (csrc/tools/jubaloadgen.cpp) at BASELINE scale -
+    LOF 100 K rows per rank (anomaly add: cluster-wide ids, CHT owners,
+    server-to-server update; anomaly_serv.cpp:178-211), k-means / GMM 200 K
+    points per rank (1000-point pushes), AROW train requests at full rate for
+    a timed window with a MIX every second inside it. Then rank 0 forces a
+    MIX and times it (do_mix: row diffs / coresets / touched W-P rows over the
+    group's plane, RCCL between GPUs), every rank reports the reference's MIX
+    line (linear_mixer.cpp:538-543: bytes and seconds of its last MIX) and
+    queries its server (1 connection x 1 in flight for p50, 8 x 4 for the
+    rate). Per engine: observed world size, fill rate (sum over ranks), MIX
+    latency / bytes / plane per rank, query p50 and rate, and whether the
+    members answer alike after the MIX. --device cpu rehearses the same calls
+    (the row / clustering binaries hand over to the Python servers there; the
+    classifier serves on its native host backend)."""
+    import shutil
+    import tempfile
     import torch.distributed as dist
+    from jubatus_amd._native import native
     from jubatus_amd.common.mprpc import RpcClient
+    exe = os.path.join(ROOT, "jubatus_amd", "native_bin", "jubaloadgen")
+    nat = native()
     out: dict = {}
     coord = None
     ls = None
@@ -494,9 +560,9 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                         "GROUP_RANK", "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME")
            and not k.startswith("TORCHELASTIC_")}
     if device is None:
-        env["JUBATUS_FORCE_CPU"] = "1"     # no GPU: the native binary execs the Python server
-    rows = _row_datums(args.dist_engine_rows + 64, 101 + rank)
-    queries, rows = rows[-64:], rows[:-64]
+        env["JUBATUS_FORCE_CPU"] = "1"     # no GPU: host backends / Python servers
+    tmp = tempfile.mkdtemp(prefix=f"jb_dist_{rank}_")
+
     def status_of(port, cname):
         with RpcClient("127.0.0.1", port, 60.0) as c:
             (_, raw), = c.call("get_status", cname).items()
@@ -512,6 +578,7 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
         for name, engine, cfg, upd, qry in DIST_ENGINE_CASES:
             if args.dist_engines != "all" and name not in args.dist_engines.split(","):
                 continue
+            _progress(f"dist engine {name}: start")
             # every rank makes the same collective calls in the same order;
             # a local failure only empties its contribution
             cname = f"bench_{name}"
@@ -519,10 +586,15 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                 from jubatus_amd.common import config as zkconfig
                 zkconfig.config_tozk(ls, engine, cname, open(os.path.join(ROOT, cfg)).read())
             dist.barrier(group=group)
+            fill, qf, units = _dist_files(args, nat, name, upd, qry, cname, rank, tmp)
             port = _free_port()
+            # MIX trigger: forced only (-s 0 -i 0), except the served train
+            # window, which MIXes every second as the reference's time trigger
+            # does every 16 s (server_util.cpp:184-189)
+            interval = "1" if upd == "train" else "0"
             srv = subprocess.Popen([os.path.join(ROOT, "jubatus_amd", "native_bin", f"juba{engine}"),
-                                    "-z", zk, "-n", cname, "-p", str(port), "-b", "127.0.0.1", "-s", "0",
-                                    "-i", "0", "-I", "30", "-Z", "10", "-c", "8", "--gpu", str(local)],
+                                    "-z", zk, "-n", cname, "-p", str(port), "-b", "127.0.0.1", "-s", interval,
+                                    "-i", "0", "-I", "60", "-Z", "10", "-c", "16", "--gpu", str(local)],
                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
             rec: dict = {"config": cfg, "world_size_observed": world}
             err = None
@@ -544,83 +616,101 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                 err = repr(e)[:300]
             up = gather(err is None)
             rec["server_runtime"] = st.get("server_runtime", "python")
+            if st.get("storage"):
+                rec["storage"] = st.get("storage")     # hbm (device tables) / host (host backend)
             rate = None
+            fill_info = None
             if all(up):
-                errs = []
-
-                def fill(part):
-                    try:
-                        with RpcClient("127.0.0.1", port, 120.0) as c:
-                            if upd == "add":
-                                for d in part:
-                                    c.call("add", cname, msgpack.unpackb(d, raw=False))
-                            elif upd == "train":
-                                for i in range(0, len(part), 100):
-                                    c.call("train", cname, [[f"l{(i + j) % 4}", msgpack.unpackb(d, raw=False)]
-                                                            for j, d in enumerate(part[i:i + 100])])
-                            else:
-                                for i in range(0, len(part), 100):
-                                    c.call("push", cname, [msgpack.unpackb(d, raw=False) for d in part[i:i + 100]])
-                    except Exception as e:  # noqa: BLE001
-                        errs.append(repr(e)[:300])
-                # clustering: enough points for the coresets to be clustered (bucket_size)
-                part = rows if upd in ("add", "train") else \
-                    (rows * (1 + 2500 // max(1, len(rows))))[:max(len(rows), 2500)]
-                t0 = time.perf_counter()
-                ths = [threading.Thread(target=fill, args=(part[i::4],)) for i in range(4)]
-                for t in ths:
-                    t.start()
-                for t in ths:
-                    t.join()
-                rate = len(part) / (time.perf_counter() - t0)
-                if errs:
-                    err, rate = errs[0], None
+                dist.barrier(group=group)      # the ranks' loads start together
+                try:
+                    t0 = time.perf_counter()
+                    if upd == "train":
+                        secs = args.dist_train_seconds
+                        r = subprocess.run([exe, "-p", str(port), "-m", "train", "-f", fill, "-c", "16", "-d", "8",
+                                            "-t", str(secs)] + _fresh_flag(args),
+                                           capture_output=True, text=True, timeout=secs + 300)
+                        if r.returncode != 0:
+                            raise RuntimeError(f"jubaloadgen train: {(r.stderr or r.stdout)[-300:]}")
+                        lg = json.loads(r.stdout.strip().splitlines()[-1])
+                        rate = lg["requests_per_s"] * units
+                        fill_info = {"rpc_p50_us": lg["p50_us"], "rpc_p99_us": lg["p99_us"], "seconds": lg["seconds"]}
+                    else:
+                        # a distributed add blocks its RPC worker on the CHT owners' updates
+                        # (anomaly_serv.cpp:178-211): fewer adds in flight than workers, so
+                        # the peers' update calls always find one free
+                        conns, depth = (8, 1) if upd == "add" else (4, 2)
+                        r = _loadgen(exe, port, upd, fill, conns, depth, once=True)
+                        dt = time.perf_counter() - t0
+                        rate = units / dt
+                        fill_info = {"seconds": round(dt, 2), "rpc_p50_us": r["p50_us"]}
+                except Exception as e:  # noqa: BLE001
+                    err, rate = repr(e)[:300], None
             rates = gather(rate)
+            infos = gather(fill_info)
             if all(r is not None for r in rates):
-                rec["rows_per_rank"] = len(rows) if upd in ("add", "train") else max(len(rows), 2500)
-                rec[f"{upd}_per_s_total"] = round(sum(rates), 1)
+                rec["units_per_rank"] = units if upd != "train" else None
+                key = {"add": "add_rows", "push": "push_points", "train": "train_samples"}[upd]
+                rec[f"{key}_per_s_total"] = round(sum(rates), 1)
+                rec[f"{key}_per_s_per_rank"] = [round(r, 1) for r in rates]
+                rec["fill_per_rank"] = infos
+                if upd == "train":
+                    rec["load"] = (f"jubaloadgen per rank: 16 connections x 8 in flight, {args.per_request}-sample "
+                                   f"requests, {args.dist_train_seconds} s, fresh values; MIX every 1 s")
                 if rank == 0:
                     try:
-                        with RpcClient("127.0.0.1", port, 300.0) as c:
+                        with RpcClient("127.0.0.1", port, 600.0) as c:
                             t0 = time.perf_counter()
                             rec["do_mix"] = bool(c.call("do_mix", cname))
                             rec["mix_latency_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
                     except Exception as e:  # noqa: BLE001
                         err = repr(e)[:300]
-            dist.barrier(group=group)
+            # the forced MIX's count on rank 0: every member waits until its own
+            # count shows it (a member finishes its fold after rank 0's round returns)
+            target = [0]
+            if rank == 0 and rec.get("do_mix"):
+                try:
+                    target = [int(status_of(port, cname).get("linear_mixer.mix_count") or 0)]
+                except Exception:  # noqa: BLE001
+                    target = [0]
+            dist.broadcast_object_list(target, src=0, group=group)
             mine = None
             if all(r is not None for r in rates):
                 try:
-                    # a member applies the MIX's fold after the round returns
-                    # on rank 0: wait (bounded) until its count shows it
                     st = status_of(port, cname)
-                    t_w = time.time() + 15
-                    while st.get("linear_mixer.mix_count") in (None, "0") and time.time() < t_w:
+                    t_w = time.time() + 30
+                    while int(st.get("linear_mixer.mix_count") or 0) < max(1, target[0]) and time.time() < t_w:
                         time.sleep(0.1)
                         st = status_of(port, cname)
+                    lat = _loadgen(exe, port, qry, qf, 1, 1, secs=args.dist_engine_seconds)
+                    thr = _loadgen(exe, port, qry, qf, 8, 4, secs=args.dist_engine_seconds)
+                    # the members' answer to the same query (rank 0's first query)
+                    q0 = gather(open(qf, "rb").read(4096))[0]
+                    qargs = next(msgpack.Unpacker(io.BytesIO(q0), raw=False))
                     with RpcClient("127.0.0.1", port, 60.0) as c:
-                        def qargs(d):
-                            x = msgpack.unpackb(d, raw=False)
-                            return [x] if qry == "classify" else x
-                        first = c.call(qry, cname, qargs(queries[0]))
-                        n, t0 = 0, time.perf_counter()
-                        while time.perf_counter() - t0 < args.dist_engine_seconds:
-                            c.call(qry, cname, qargs(queries[n % len(queries)]))
-                            n += 1
-                        qps = n / (time.perf_counter() - t0)
+                        first = c.call(qry, cname, *qargs[1:])
+                    if qry == "classify":   # label columns are in each member's own order
+                        first = [sorted(((l.decode() if isinstance(l, bytes) else l), round(float(v), 4))
+                                        for l, v in r) for r in first]
+                    elif isinstance(first, float):
+                        first = round(first, 4)
                     mine = {"mix_count": st.get("linear_mixer.mix_count"),
                             "bytes": int(st.get("linear_mixer.last_mix_bytes") or 0),
                             "sec": float(st.get("linear_mixer.last_mix_sec") or 0),
-                            "plane": st.get("linear_mixer.backend"), "qps": qps, "first": repr(first)}
+                            "plane": st.get("linear_mixer.backend"), "p50": lat["p50_us"],
+                            "qps": thr["requests_per_s"], "first": repr(first)}
                 except Exception as e:  # noqa: BLE001
                     err = repr(e)[:300]
             stats = gather(mine)
             errors = gather(err)
             if all(x is not None for x in stats):
                 rec["mix_count_per_rank"] = [x["mix_count"] for x in stats]
+                # linear_mixer.cpp:538-543: "mixed with N servers in T secs, S bytes"
+                rec["mix_line_per_rank"] = [f"mixed with {world} servers in {x['sec']:.6f} secs, {x['bytes']} bytes"
+                                            for x in stats]
                 rec["mix_bytes_per_rank"] = [x["bytes"] for x in stats]
                 rec["mix_seconds_per_rank"] = [x["sec"] for x in stats]
                 rec["mix_plane"] = stats[0]["plane"]
+                rec[f"{qry}_p50_us_per_rank"] = [x["p50"] for x in stats]
                 rec[f"{qry}_per_s_total"] = round(sum(x["qps"] for x in stats), 1)
                 rec["members_agree_after_mix"] = len({x["first"] for x in stats}) == 1
             if any(errors):
@@ -632,7 +722,9 @@ def dist_engine_records(args, rank: int, world: int, local: int, device, group) 
                 srv.kill()
             dist.barrier(group=group)
             out[name] = rec
+            _progress(f"dist engine {name}: done")
     finally:
+        shutil.rmtree(tmp, ignore_errors=True)
         if coord is not None:
             ls.close()
             coord.stop()
@@ -928,12 +1020,59 @@ def cpu_baseline_record(args, cfg, nat, warm_batches, timed_batches, worst_batch
         out[name] = {"value": round(n / sec, 1), "unit": "samples/s", "batches": len(timed_batches),
                      "update_fraction": round(u / max(1, n), 5), "threads": threads}
     if worst_batches:
-        table, W, P = model()
-        n, u, sec = run(worst_batches, table, W, P, ncpu)
-        out["worst_case"] = {"value": round(n / sec, 1), "unit": "samples/s", "batches": len(worst_batches),
-                             "update_fraction": round(u / max(1, n), 5), "threads": ncpu,
-                             "data": "worst case: noise string values (every sample updates), fresh model"}
+        # the worst case on one core and with the parse pool (the train itself
+        # is sequential either way)
+        for name, threads in (("worst_case_threads_1", 1), ("worst_case", ncpu)):
+            table, W, P = model()
+            n, u, sec = run(worst_batches, table, W, P, threads)
+            out[name] = {"value": round(n / sec, 1), "unit": "samples/s", "batches": len(worst_batches),
+                         "update_fraction": round(u / max(1, n), 5), "threads": threads,
+                         "data": "worst case: noise string values (every sample updates), fresh model"}
     return out
+
+
+def _summary(out: dict) -> dict:
+    """the records a reader looks for first, flat (the end of the JSON line)"""
+    def g(d, *ks):
+        for k in ks:
+            if not isinstance(d, dict):
+                return None
+            d = d.get(k)
+        return d
+    ex = out.get("exact_mode") or {}
+    sm = {"headline_samples_per_s": out.get("value"), "headline_update_mode": out.get("headline_update_mode"),
+          "exact_mode_samples_per_s": g(ex, "value"), "exact_mode_update_fraction": g(ex, "update_fraction"),
+          "exact_worst_case_samples_per_s": g(ex, "worst_case", "value"),
+          "exact_worst_case_stepper_samples": g(ex, "worst_case", "last_batch", "stepper_samples"),
+          "cpu_threads_1": g(ex, "cpu_baseline", "threads_1", "value"),
+          "cpu_threads_all": g(ex, "cpu_baseline", "threads_all", "value"),
+          "cpu_worst_threads_1": g(ex, "cpu_baseline", "worst_case_threads_1", "value"),
+          "cpu_worst_threads_all": g(ex, "cpu_baseline", "worst_case", "value"),
+          "gpu_exact_worst_vs_cpu_worst_threads_1": g(ex, "cpu_baseline", "gpu_exact_worst_vs_cpu_worst_threads_1"),
+          "bf16_weights_samples_per_s": g(out, "bf16_weights", "value"),
+          "atomic_worst_case_samples_per_s": g(out, "worst_case", "value"),
+          "served_native_samples_per_s": g(out, "served_native", "served_train_samples_per_sec"),
+          "served_native_cpus": g(out, "served_native", "server_cpus"),
+          "served_native_exact_samples_per_s": g(out, "served_native", "exact_mode", "served_train_samples_per_sec"),
+          "served_native_learning_exact_samples_per_s": g(out, "served_native", "learning_stream_exact",
+                                                          "served_train_samples_per_sec"),
+          "served_native_learning_exact_p99_us": g(out, "served_native", "learning_stream_exact", "rpc_p99_us"),
+          "classify_rpc_p50_us": g(out, "served_native", "classify_rpc_p50_us"),
+          "classify_latency_us_p50": out.get("classify_latency_us_p50")}
+    eng = out.get("engines") or {}
+    for name, rec in eng.items():
+        if isinstance(rec, dict):
+            for k, v in rec.items():
+                if k.endswith(("_per_s_fill", "_p50_us", "_per_s", "_points_per_s")) and isinstance(v, (int, float)):
+                    sm[f"{name}.{k}"] = v
+    for name, rec in (out.get("engines_dist") or {}).items():
+        if isinstance(rec, dict):
+            for k, v in rec.items():
+                if k.endswith("_per_s_total") or k in ("mix_latency_ms", "members_agree_after_mix", "server_runtime"):
+                    sm[f"dist.{name}.{k}"] = v
+            if rec.get("mix_line_per_rank"):
+                sm[f"dist.{name}.mix_line_rank0"] = rec["mix_line_per_rank"][0]
+    return {k: v for k, v in sm.items() if v is not None}
 
 
 def _mix_summary(log: list) -> dict:
@@ -987,11 +1126,15 @@ def main() -> None:
     ap.add_argument("--lof-rows", type=int, default=100_000,
                     help="rows added to the LOF server before its queries")
     ap.add_argument("--engine-seconds", type=float, default=3.0)
-    ap.add_argument("--dist-engines", default="lof,kmeans,arow",
+    ap.add_argument("--dist-engines", default="lof,kmeans,gmm,arow",
                     help="N > 1: distributed engine records (lof,kmeans,gmm,arow / all / none): one server per "
                          "rank in one cluster, a forced MIX, queries on every member")
     ap.add_argument("--dist-engine-rows", type=int, default=0,
-                    help="rows / points each rank fills in (0: 4000 on GPUs, 200 with --device cpu)")
+                    help="LOF rows each rank adds (0: 100000 on GPUs, 300 with --device cpu)")
+    ap.add_argument("--dist-cluster-points", type=int, default=0,
+                    help="points each rank pushes into its clustering server (0: 200000 on GPUs, 3000 on cpu)")
+    ap.add_argument("--dist-train-seconds", type=float, default=3.0,
+                    help="N > 1: length of the served AROW train window per rank (MIX every second)")
     ap.add_argument("--dist-engine-seconds", type=float, default=1.5)
     ap.add_argument("--cluster-points", type=int, default=200_000,
                     help="points pushed into each clustering server (kmeans.json, gmm.json)")
@@ -1302,6 +1445,8 @@ def main() -> None:
                     exact["value"] / max(1.0, exact["cpu_baseline"][k]["value"]), 2)
             exact["cpu_baseline"]["gpu_exact_worst_vs_cpu_worst"] = round(
                 exact["worst_case"]["value"] / max(1.0, exact["cpu_baseline"]["worst_case"]["value"]), 2)
+            exact["cpu_baseline"]["gpu_exact_worst_vs_cpu_worst_threads_1"] = round(
+                exact["worst_case"]["value"] / max(1.0, exact["cpu_baseline"]["worst_case_threads_1"]["value"]), 2)
         del ws
     served = served_native = None
     if world == 1 and device is not None and not args.no_rpc:
@@ -1321,7 +1466,9 @@ def main() -> None:
     engines_dist = None
     if world > 1 and args.dist_engines != "none":
         if args.dist_engine_rows <= 0:
-            args.dist_engine_rows = 4000 if device is not None else 200
+            args.dist_engine_rows = 100_000 if device is not None else 300
+        if args.dist_cluster_points <= 0:
+            args.dist_cluster_points = 200_000 if device is not None else 3000
         try:
             engines_dist = dist_engine_records(args, rank, world, local, device, meta)
         except Exception as e:  # noqa: BLE001 - the headline stands without it
@@ -1397,6 +1544,8 @@ def main() -> None:
             "heldout_accuracy": round(acc, 4),
             "baseline_note": "reference publishes no numbers (BASELINE.md)",
         }
+        # the key records again, last: the driver keeps the tail of the line
+        out["summary"] = _summary(out)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -835,14 +835,16 @@ class LinearMixer {
   }
 
   // force a MIX at the next tick and wait for it (RPC do_mix)
+  // a MIX that begins after this call (a MIX already under way snapshotted
+  // the model before it: its end does not count)
   bool do_mix() {
     std::unique_lock<std::mutex> g(mu_);
-    const uint64_t target = mix_count_ + 1;
+    const uint64_t want = begun_ + 1;
     force_ = true;
     cv_.notify_all();
     const double dl = now_s() + std::max(30.0, 4 * a_.interconnect_timeout);
-    while (mix_count_ < target && !stop_ && now_s() < dl) cv_.wait_for(g, std::chrono::milliseconds(100));
-    return mix_count_ >= target;
+    while (ended_ < want && !stop_ && now_s() < dl) cv_.wait_for(g, std::chrono::milliseconds(100));
+    return ended_ >= want;
   }
 
   void status(std::vector<std::pair<std::string, std::string>>* st) {
@@ -872,12 +874,18 @@ class LinearMixer {
     return a_.interval_sec > 0 && now_s() - ticktime_ > a_.interval_sec;
   }
 
-  void mixed_locked(uint64_t bytes, double sec) {
+  // a MIX begins: the force it answers is consumed (a do_mix after this
+  // point waits for the next one) -> its sequence number
+  uint64_t begin_locked() {
+    force_ = false;
+    return ++begun_;
+  }
+  void mixed_locked(uint64_t seq, uint64_t bytes, double sec) {
     counter_ = 0;
     ticktime_ = now_s();
     ticktime_wall_ = (double)time(nullptr);
     ++mix_count_;
-    force_ = false;
+    if (seq > ended_) ended_ = seq;
     last_bytes_ = bytes;
     last_sec_ = sec;
     cv_.notify_all();
@@ -916,7 +924,7 @@ class LinearMixer {
         register_active();
       }
       std::lock_guard<std::mutex> l(mu_);
-      if (force_ || want_locked()) mixed_locked(0, 0.0);
+      if (force_ || want_locked()) mixed_locked(begin_locked(), 0, 0.0);
       return;
     }
     if (formed) {
@@ -943,6 +951,11 @@ class LinearMixer {
       return;
     }
     if (!(flags[0] || flags[1])) return;
+    uint64_t seq;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      seq = begin_locked();
+    }
     faults_.on_mix("allreduce");
     const double t0 = now_s();
     uint64_t bytes = 0;
@@ -962,7 +975,7 @@ class LinearMixer {
     const double sec = now_s() - t0;
     std::lock_guard<std::mutex> l(mu_);
     mix_count_ = (uint64_t)flags[4];      // every member leaves this MIX at the same count
-    mixed_locked(bytes, sec);
+    mixed_locked(seq, bytes, sec);
     char b[160];
     snprintf(b, sizeof b, "mixed with %d servers in %.6f secs, %llu bytes", g.world(), sec,
              (unsigned long long)bytes);
@@ -996,6 +1009,7 @@ class LinearMixer {
   bool stop_ = false, force_ = false, obsolete_ = true;
   std::atomic<bool> running_{false};
   uint64_t counter_ = 0, mix_count_ = 0, last_bytes_ = 0;
+  uint64_t begun_ = 0, ended_ = 0;   // MIXes this member began / finished (do_mix)
   double ticktime_ = 0, ticktime_wall_ = (double)time(nullptr), last_sec_ = 0;
 };
 

@@ -76,7 +76,8 @@ def test_bench_eight_ranks_cpu():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(WORLD), "--steps", "2",
            "--warmup", "1", "--device", "cpu", "--requests", "4", "--per-request", "8",
            "--hash-bits", "10", "--latency-iters", "2", "--batches-per-step", "2", "--engines", "none",
-           "--dist-engines", "lof,kmeans,arow", "--dist-engine-rows", "120", "--dist-engine-seconds", "0.5"]
+           "--dist-engines", "lof,kmeans,arow", "--dist-engine-rows", "120", "--dist-engine-seconds", "0.5",
+           "--dist-cluster-points", "3000", "--dist-train-seconds", "1.5"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
@@ -89,15 +90,24 @@ def test_bench_eight_ranks_cpu():
     assert mt["count"] >= 1 and mt["world"] == WORLD and mt["bytes_per_rank_mean"] > 0
     assert mt["latency_ms_p50"] is not None and mt["latency_ms_p50"] >= 0
     assert out["config"]["world_size_observed"] == WORLD
-    # BASELINE #4 / #5 on 8 ranks: one server per rank in one cluster, a MIX
-    # every member took part in, queries after it (CPU: the Python servers)
-    # and the headline engine through the servers' linear mixer
-    for name, qry in (("lof", "calc_score"), ("kmeans", "get_nearest_center"), ("arow", "classify")):
+    # BASELINE #4 / #5 on 8 ranks: one server per rank in one cluster filled
+    # by the native load generator, a MIX every member took part in, queries
+    # after it (CPU: the Python row / clustering servers), and the headline
+    # engine served natively (host backend here) under a timed train load
+    # with MIXes inside the window
+    for name, qry, key in (("lof", "calc_score", "add_rows"), ("kmeans", "get_nearest_center", "push_points"),
+                           ("arow", "classify", "train_samples")):
         rec = out["engines_dist"][name]
         assert "errors" not in rec, rec
         assert rec["world_size_observed"] == WORLD and rec["do_mix"] is True
-        assert rec["mix_count_per_rank"] == ["1"] * WORLD and min(rec["mix_bytes_per_rank"]) > 0
+        assert rec[f"{key}_per_s_total"] > 0 and len(rec[f"{key}_per_s_per_rank"]) == WORLD
+        counts = [int(c) for c in rec["mix_count_per_rank"]]
+        assert min(counts) >= 1 and min(rec["mix_bytes_per_rank"]) > 0
+        assert all(l.startswith(f"mixed with {WORLD} servers in ") for l in rec["mix_line_per_rank"])
         assert rec["mix_latency_ms"] > 0 and rec[f"{qry}_per_s_total"] > 0
+        if name == "arow":    # the averaged linear model (LOF / k-means re-derive lists / centers per member)
+            assert rec["members_agree_after_mix"] is True, rec
+    assert out["engines_dist"]["arow"]["server_runtime"] == "native"
 
 
 def test_bench_pinned_budget_eight_ranks():
