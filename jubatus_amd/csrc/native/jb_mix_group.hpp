@@ -53,6 +53,7 @@
 #include <vector>
 
 #include "jb_coord_client.hpp"
+#include "jb_roctx.hpp"
 #include "jb_hash.hpp"
 
 namespace jb {
@@ -960,6 +961,7 @@ class LinearMixer {
     const double t0 = now_s();
     uint64_t bytes = 0;
     if (a_.kind == "linear_mixer") {
+      jb::tx::Range tr("mix.linear");
       bytes = model_->mix(g);
     } else {
       // push mixers: the rounds of the pairwise schedule (push_mixer.cpp:335-408)
@@ -968,6 +970,7 @@ class LinearMixer {
       model_->push_begin();
       for (const auto& m : push_schedule(a_.kind, g.world(), g.epoch(), round_no)) {
         faults_.on_mix("pair");
+        jb::tx::Range tr("mix.push_round");
         bytes += model_->pair_mix(g, m[(size_t)g.rank()]);
       }
       model_->push_end();

@@ -20,6 +20,7 @@
 #include <stdexcept>
 
 #include "jb_msgpack.hpp"
+#include "jb_roctx.hpp"
 
 namespace jb {
 
@@ -397,7 +398,13 @@ void RpcServer::batch_loop(int idx) {
         }
       continue;
     }
-    std::vector<std::string> resp = batch_handler_(batch[0].method, batch);
+    std::vector<std::string> resp;
+    {
+      // JUBATUS_ROCTX=1: one range per handed-over batch (rocprofv3 --marker-trace)
+      const std::string tag = "rpc.batch." + batch[0].method;
+      jb::tx::Range tr(tag.c_str());
+      resp = batch_handler_(batch[0].method, batch);
+    }
     batches_.fetch_add(1);
     served_.fetch_add(batch.size());
     std::vector<uint64_t> ids(batch.size());
@@ -762,7 +769,11 @@ bool RpcServer::arena_batch_once() {
     reqs.swap(s.reqs);
   }
   const auto t0 = std::chrono::steady_clock::now();
-  std::vector<std::string> resp = arena_handler_(k, reqs);
+  std::vector<std::string> resp;
+  {
+    jb::tx::Range tr("rpc.arena_batch");
+    resp = arena_handler_(k, reqs);
+  }
   const auto t1 = std::chrono::steady_clock::now();
   batches_.fetch_add(1);
   served_.fetch_add(reqs.size());
@@ -861,7 +872,14 @@ void RpcServer::worker_loop() {
       qlen_.store(queue_.size(), std::memory_order_relaxed);
     }
     busy = true;
-    std::string resp = handler_(req);
+    std::string resp;
+    if (jb::tx::enabled()) {
+      const std::string tag = "rpc." + req.method;
+      jb::tx::Range tr(tag.c_str());
+      resp = handler_(req);
+    } else {
+      resp = handler_(req);
+    }
     served_.fetch_add(1);
     if (!req.notify && !resp.empty()) send_response(req.conn_id, resp);
   }

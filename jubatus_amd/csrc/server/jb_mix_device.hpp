@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "jb_mix_group.hpp"
+#include "jb_roctx.hpp"
 
 // csrc/hip/mix.hip
 extern "C" int jb_mix_pair_sum(float* p, const float* q, int64_t n, hipStream_t st);
@@ -68,22 +69,26 @@ class RcclPlane : public Plane {
 
   void allreduce_sum(float* p, size_t n, double dl) override {
     if (!n) return;
+    jb::tx::Range tr("rccl.allreduce_sum_f32");
     check(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, comm_, st_), dl, "ncclAllReduce");
     wait_stream(st_, dl);
   }
   void allreduce_max(uint8_t* p, size_t n, double dl) override {
     if (!n) return;
+    jb::tx::Range tr("rccl.allreduce_max_u8");
     check(ncclAllReduce(p, p, n, ncclUint8, ncclMax, comm_, st_), dl, "ncclAllReduce");
     wait_stream(st_, dl);
   }
   bool allreduce_sum_bf16(uint16_t* p, size_t n, double dl) override {
     if (!n) return true;
+    jb::tx::Range tr("rccl.allreduce_sum_bf16");
     check(ncclAllReduce(p, p, n, ncclBfloat16, ncclSum, comm_, st_), dl, "ncclAllReduce");
     wait_stream(st_, dl);
     return true;
   }
   void bcast(void* p, size_t bytes, int root, double dl) override {
     if (!bytes) return;
+    jb::tx::Range tr("rccl.broadcast");
     check(ncclBroadcast(p, p, bytes, ncclUint8, root, comm_, st_), dl, "ncclBroadcast");
     wait_stream(st_, dl);
   }
@@ -97,6 +102,7 @@ class RcclPlane : public Plane {
     uint8_t* d = dev_bytes(mx * (size_t)(w + 1));
     hipchk(hipMemsetAsync(d, 0, mx, st_), "MIX memset");
     if (!mine.empty()) hipchk(hipMemcpyAsync(d, mine.data(), mine.size(), hipMemcpyHostToDevice, st_), "MIX H2D");
+    jb::tx::Range tr("rccl.allgather_bytes");
     check(ncclAllGather(d, d + mx, mx, ncclUint8, comm_, st_), dl, "ncclAllGather");
     std::string all(mx * (size_t)w, '\0');
     hipchk(hipMemcpyAsync(&all[0], d + mx, all.size(), hipMemcpyDeviceToHost, st_), "MIX D2H");

@@ -52,6 +52,7 @@
 #include <vector>
 
 #include "jb_lof_state.hpp"
+#include "jb_roctx.hpp"
 #include "jb_mix_device.hpp"
 #include "jb_mix_group.hpp"
 #include "jb_msgpack.hpp"
@@ -605,6 +606,7 @@ class Model : public jb::mix::Mixable {
     std::exception_ptr err;
   };
   void run_calls(std::vector<Call>& cs) {
+    jb::tx::Range tr("rows.query_batch");
     std::vector<QReq> reqs(cs.size());
     std::vector<QReq*> ptrs;
     for (size_t i = 0; i < cs.size(); ++i) {
@@ -1389,6 +1391,7 @@ class Server {
   // one batch of anomaly adds (see run()): malformed ones answer as
   // dispatch() would, the rest run as one Model::add_many in arrival order
   std::vector<std::string> add_batch(std::vector<jb::RpcRequest>& rs) {
+    jb::tx::Range tr("rows.lof_add_batch");
     std::vector<std::string> out(rs.size());
     std::vector<Value> args(rs.size());
     std::vector<Model::AddReq> reqs;

@@ -48,6 +48,7 @@
 #include <vector>
 
 #include "jb_hash.hpp"
+#include "jb_roctx.hpp"
 #include "jb_host_linear.hpp"
 #include "jb_hostfv.hpp"
 #include "jb_linear_conv.hpp"
@@ -271,6 +272,7 @@ class Classifier : public jb::mix::Mixable {
         if (labels_.size() > 0) si = submit_scan_locked(arena, reqs, counts, used);
       }
       if (si >= 0) {
+        jb::tx::Range tr("train.scan_check_wait");
         Set& s = sets_[si];
         const auto t1 = std::chrono::steady_clock::now();
         const hipError_t we = hipEventSynchronize(s.check_done);
@@ -1073,6 +1075,7 @@ class Classifier : public jb::mix::Mixable {
   // one GPU-scan batch (feature_pipeline.scan_batch_args + classifier._submit_scan)
   int submit_scan_locked(const uint8_t* arena, const std::vector<jb::ArenaReq>& reqs,
                          const std::vector<int64_t>& counts, uint64_t used) {
+    jb::tx::Range tr("train.submit_h2d_scan_hash_train");
     sync_labels_locked();
     const int64_t R = (int64_t)reqs.size();
     int64_t n = 0;
@@ -1204,6 +1207,7 @@ class Classifier : public jb::mix::Mixable {
   // host path of one request: validate the whole body, then commit labels
   // and counts, hash, one exact single-stream train launch
   void host_train_locked(const uint8_t* b, size_t len, int64_t* res, std::string* msg) {
+    jb::tx::Range tr("train.host_path");
     jb::Cursor c{b, b + len};
     uint32_t cnt;
     if (!c.array(&cnt) || cnt > len) { *res = -1; return; }
@@ -1274,6 +1278,7 @@ class Classifier : public jb::mix::Mixable {
 
   // scores of the hashed classify batch (cidx_/cval_/row_) into out[n * LC]
   void score_locked(int64_t n, int64_t slots, float* out) {
+    jb::tx::Range tr("classify.score");
     const int64_t* row = row_.p;
     if (n <= kDirectMaxSamples && row[n] - row[0] <= kDirectMaxSlots) {
       hipStream_t st = hipStreamQuery(compute_) == hipSuccess ? prio_ : compute_;

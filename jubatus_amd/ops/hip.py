@@ -8,6 +8,7 @@ order naturally with torch ops and RCCL collectives.
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 
 import torch
@@ -533,6 +534,29 @@ def stepper_prof() -> dict:
     return {k: int(v) for k, v in zip(STEPPER_PROF_KEYS, out.tolist())}
 
 
+_ROCTX: list = []
+
+
+def _roctx():
+    """the ROCm marker library when JUBATUS_ROCTX=1 (csrc/native/jb_roctx.hpp
+    is the native twin), else None"""
+    if not _ROCTX:
+        lib = None
+        if os.environ.get("JUBATUS_ROCTX") == "1":
+            for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                         "libroctx64.so.4"):
+                try:
+                    lib = ctypes.CDLL(name, mode=ctypes.RTLD_GLOBAL)
+                    lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                    lib.roctxRangePushA.restype = ctypes.c_int
+                    lib.roctxRangePop.restype = ctypes.c_int
+                    break
+                except (OSError, AttributeError):
+                    lib = None
+        _ROCTX.append(lib)
+    return _ROCTX[0]
+
+
 def _fn(name: str):
     f = _fns.get(name)
     if f is None:
@@ -542,11 +566,26 @@ def _fn(name: str):
         raw.restype = ctypes.c_int64 if name.endswith(("_bytes", "_create")) else ctypes.c_int
         tag = "hip." + name[3:]
 
-        def f(*args, _raw=raw, _tag=tag):
-            t0 = time.perf_counter_ns()
-            rc = _raw(*args)
-            trace.record(_tag, time.perf_counter_ns() - t0)
-            return rc
+        tx = _roctx()
+        if tx is not None:
+            # JUBATUS_ROCTX=1: a roctx range per kernel-group call (rocprofv3 --marker-trace)
+            label = tag.encode()
+
+            def f(*args, _raw=raw, _tag=tag, _label=label, _tx=tx):
+                t0 = time.perf_counter_ns()
+                _tx.roctxRangePushA(_label)
+                try:
+                    rc = _raw(*args)
+                finally:
+                    _tx.roctxRangePop()
+                trace.record(_tag, time.perf_counter_ns() - t0)
+                return rc
+        else:
+            def f(*args, _raw=raw, _tag=tag):
+                t0 = time.perf_counter_ns()
+                rc = _raw(*args)
+                trace.record(_tag, time.perf_counter_ns() - t0)
+                return rc
         _fns[name] = f
     return f
 
