@@ -72,11 +72,13 @@ struct Geo {
   static constexpr int QC = 16 / G;                                   // features per lane of a 16-feature sample
   // LDS carve (bytes, every offset a multiple of 16)
   static constexpr int oW = 0;
-  static constexpr int oP = oW + NSLOT * LC * 4;
-  static constexpr int oKey = oP + NSLOT * LC * 4;
-  static constexpr int oUse = oKey + NSLOT * 4;
-  static constexpr int oDirty = oUse + NSLOT * 4;
-  static constexpr int oHdr = oDirty + NSLOT * 4;                      // int4 [kSR]: meta_seq, ready_seq, y|n, off
+  // W / P rows of NSLOT cache slots + one dummy slot (index NSLOT) that
+  // absent features of a sample point at (zero x, adds of zero)
+  static constexpr int oP = oW + (NSLOT + 1) * LC * 4;
+  static constexpr int oKey = oP + (NSLOT + 1) * LC * 4;
+  static constexpr int oUse = oKey + (NSLOT + 4) * 4;
+  static constexpr int oDirty = oUse + (NSLOT + 4) * 4;
+  static constexpr int oHdr = oDirty + (NSLOT + 4) * 4;                      // int4 [kSR]: meta_seq, ready_seq, y|n, off
   static constexpr int oFend = oHdr + kSR * 16;                        // int [kSR]
   static constexpr int oFR = oFend + kSR * 4;                          // int2 [kFR]: row (then slot), x
   static constexpr int oStage = oFR + kFR * 8;                         // [kK][W 1 KB | P 1 KB]
@@ -101,7 +103,8 @@ __device__ int g_err;                                            // first abort 
 // jb_stepper_prof() (accumulated by lane 0 of each wave)
 enum : int {
   P_STEP_TOTAL = 0, P_STEP_WAIT, P_LOAD_IDLE, P_LOAD_RETIRE, P_LOAD_STUCK, P_META_ROOM, P_SAMPLES, P_STAGES,
-  P_MISSES, P_DIRECT, P_LOAD_LOOKUP, P_LOAD_ISSUE, P_LOAD_TOTAL, P_META_TOTAL, P_FETCH_TOTAL, P_NWORDS = 16
+  P_MISSES, P_DIRECT, P_LOAD_LOOKUP, P_LOAD_ISSUE, P_LOAD_TOTAL, P_META_TOTAL, P_FETCH_TOTAL, P_LK_ITERS,
+  P_LK_KEYS, P_LK_CAS, P_ST_READ, P_ST_REDUCE, P_ST_COEF, P_ST_APPLY, P_NWORDS = 24
 };
 __device__ unsigned long long g_prof[P_NWORDS];
 
@@ -226,6 +229,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                                                      unsigned long long* __restrict__ prof) {
   using Gm = Geo<LC>;
   constexpr bool use_s = MT >= CW;
+  constexpr bool use_nrm = MT == PA || MT == PA1 || MT == PA2;
   constexpr int NSLOT = Gm::NSLOT, NB = Gm::NB, G = Gm::G, RPS = Gm::RPS, LPR = Gm::LPR;
   constexpr int QC = Gm::QC;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -254,12 +258,12 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   const int N = (int)(end - beg);
 
   // ---- init (all waves)
-  for (int i = tid; i < NSLOT; i += kT) {
+  for (int i = tid; i < NSLOT + 4; i += kT) {
     key[i] = -1;
     use[i] = -1;
     dirty[i] = 0;
   }
-  for (int i = tid; i < NSLOT * LC; i += kT) {   // empty slots hold the initial model
+  for (int i = tid; i < (NSLOT + 1) * LC; i += kT) {   // empty slots hold the initial model
     Wc[i] = 0.f;
     Pc[i] = 1.f;
   }
@@ -331,13 +335,15 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       float xv[QC], inv[QC];
 #pragma unroll
       for (int u = 0; u < QC; ++u) {
-        sl[u] = u * G + g < n ? e[u].x : -1;
-        xv[u] = sl[u] >= 0 ? __int_as_float(e[u].y) : 0.f;
+        const bool ok = u * G + g < n && e[u].x >= 0;
+        sl[u] = ok ? e[u].x : NSLOT;
+        xv[u] = ok ? __int_as_float(e[u].y) : 0.f;
       }
       // the next sample's header and entries (stale if it is not published yet)
       const int tn = t + 1;
       hd = lds_ld(&hdr[tn & (kSR - 1)]);
       entries(hd.w);
+      uint64_t s3 = 0;
       if (y >= 0) {
         ++n_valid;
         if (n < 0) {
@@ -353,23 +359,27 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         } else {
           // scores, |x|^2 and x^2 / P of this lane's label over its features
           // (lanes: label l x feature group g); all reads before any add
+          // (absent features: the dummy slot, x 0 - no selects, no branches)
           float s = 0.f, vq = 0.f, nq = 0.f;
           const bool one = n <= QC * G;
+          const uint64_t s0 = clk();
           auto chunk = [&]() __attribute__((always_inline)) {
             float w[QC], p[QC];
 #pragma unroll
             for (int u = 0; u < QC; ++u) {
-              const int si = sl[u] >= 0 ? sl[u] : 0;
-              w[u] = Wc[si * LC + l];
-              p[u] = use_s ? Pc[si * LC + l] : 1.f;
+              w[u] = Wc[sl[u] * LC + l];
+              p[u] = use_s ? Pc[sl[u] * LC + l] : 1.f;
             }
 #pragma unroll
             for (int u = 0; u < QC; ++u) {
-              const bool ok = sl[u] >= 0;
-              s += ok ? xv[u] * w[u] : 0.f;
-              nq += xv[u] * xv[u];
-              inv[u] = (use_s && ok) ? rcp_nr(p[u]) : 1.f;
-              vq += ok ? xv[u] * xv[u] * inv[u] : 0.f;
+              s = fmaf(xv[u], w[u], s);
+              if (use_nrm) nq = fmaf(xv[u], xv[u], nq);
+              if (use_s) {
+                inv[u] = rcp_nr(p[u]);
+                vq = fmaf(xv[u] * xv[u], inv[u], vq);
+              } else {
+                inv[u] = 1.f;
+              }
             }
           };
           chunk();
@@ -378,13 +388,16 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
             for (int u = 0; u < QC; ++u) {
               const int j = (q0 + u) * G + g;
               const int2 ej = fring[(off + j) & (kFR - 1)];
-              sl[u] = j < n ? ej.x : -1;
-              xv[u] = sl[u] >= 0 ? __int_as_float(ej.y) : 0.f;
+              const bool ok = j < n && ej.x >= 0;
+              sl[u] = ok ? ej.x : NSLOT;
+              xv[u] = ok ? __int_as_float(ej.y) : 0.f;
             }
             chunk();
           }
+          const uint64_t s1 = clk();
+          pc[P_ST_READ] += s1 - s0;
           s = group_sum<LC>(s, lane);
-          nq = group_sum<LC>(nq, lane);
+          if (use_nrm) nq = group_sum<LC>(nq, lane);
           if (use_s) vq = group_sum<LC>(vq, lane);
           const float v = (act && l != y) ? s : -INFINITY;
           const float m = group_max<LC>(v, lane);
@@ -393,18 +406,22 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           const float sy = readlane_f(s, y);
           const float best = bl >= 0 ? readlane_f(s, bl) : 0.f;
           const float var = use_s ? readlane_f(vq, y) + (bl >= 0 ? readlane_f(vq, bl) : 0.f) : 0.f;
-          const float nrm = readlane_f(nq, 0);
+          const float nrm = use_nrm ? readlane_f(nq, 0) : 0.f;
           float tau = 0.f, beta = 0.f;
-          if (step_coeffs(MT, sy - best, var, nrm, bl >= 0, C, &tau, &beta)) {
+          const uint64_t s2 = clk();
+          pc[P_ST_REDUCE] += s2 - s1;
+          const bool upd = step_coeffs(MT, sy - best, var, nrm, bl >= 0, C, &tau, &beta);
+          s3 = clk();
+          pc[P_ST_COEF] += s3 - s2;
+          if (upd) {
             ++n_upd;
             const bool isy = l == y, isl = l == bl;
             if (isy || isl) {
               const float sg = isy ? tau : -tau;
               if (one) {
 #pragma unroll
-                for (int u = 0; u < QC; ++u) {
-                  if (sl[u] < 0) continue;
-                  atomicAdd(&Wc[sl[u] * LC + l], sg * (use_s ? inv[u] : 1.f) * xv[u]);
+                for (int u = 0; u < QC; ++u) {   // (absent features add 0 to the dummy slot)
+                  atomicAdd(&Wc[sl[u] * LC + l], sg * inv[u] * xv[u]);
                   if (use_s) atomicAdd(&Pc[sl[u] * LC + l], dprec_nr(MT, beta, xv[u], inv[u]));
                   if (isy) dirty[sl[u]] = 1;
                 }
@@ -443,6 +460,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         }
       }
       if (lane == 0) lds_st(&ctl[C_PROGRESS], t + 1);
+      if (s3 != 0) pc[P_ST_APPLY] += clk() - s3;
     }
     if (lane == 0 && stats != nullptr) {
       if (n_upd) atomicAdd(stats, (unsigned long long)n_upd);
@@ -534,6 +552,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
     // earlier sample stepped, its cached rows (and the previous rows of the
     // ways its partial lookup took) written back and dropped, then it is
     // handed on as direct; the lookup waits until the stepper is past it
+    // (y < 0: a sample without a label whose group overflowed - only the
+    // partial lookup is undone, the sample is handed on as it was)
     auto go_direct = [&](int t, int y, int jpos0) __attribute__((always_inline)) {
       if (!wait_progress(t, kErrTimeoutLoad)) { dead = true; return; }
       auto drop = [&](int sl, int wrow) {
@@ -561,7 +581,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       jhead = jpos0;
       const int64_t s = beg + t;
       const int64_t rb = row_ptr[s];
-      const int n = (int)(row_ptr[s + 1] - rb);
+      const int n = y >= 0 ? (int)(row_ptr[s + 1] - rb) : 0;
       for (int j0 = 0; j0 < n; j0 += 64) {
         const int j = j0 + lane;
         const int row = j < n ? fidx[rb + j] : -1;
@@ -583,7 +603,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) {
-        lds_st(reinterpret_cast<int*>(&hdr[t & (kSR - 1)]) + 2, (y + 1) << 16);   // n = -1: direct
+        if (y >= 0) lds_st(reinterpret_cast<int*>(&hdr[t & (kSR - 1)]) + 2, (y + 1) << 16);   // n = -1: direct
         int* lp = reinterpret_cast<int*>(&lk[t & (kSR - 1)]);
         lds_st(&lp[1], jhead);
         lds_st(&lp[2], -1);
@@ -600,47 +620,66 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       }
     };
 
-    for (int t = 0; t < N && !dead; ++t) {
-      // the sample's header from the meta wave
-      int4 hd = lds_ld(&hdr[t & (kSR - 1)]);
-      if (hd.x != t) {
+    // Samples of at most 16 features are looked up four at a time (lanes
+    // 16 k + j: feature j of sample t + k), wider ones alone in 64-lane
+    // chunks. A group's fetch jobs all count for its first sample, which is
+    // then published last of them landing - the later ones of the group
+    // carry no jobs, and the fetch wave publishes in order.
+    int jdone_c = 0;   // the fetch wave's consumed-job count, as last read
+    for (int t = 0; t < N && !dead;) {
+      int4 h0 = lds_ld(&hdr[t & (kSR - 1)]);
+      if (h0.x != t) {
         const uint64_t w0 = clk();
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while ((hd = lds_ld(&hdr[t & (kSR - 1)])).x != t) {
+        while ((h0 = lds_ld(&hdr[t & (kSR - 1)])).x != t) {
           if (lds_ld(&ctl[C_ABORT]) != 0 || timed_out(t0)) { abort_with(kErrTimeoutLoad); dead = true; break; }
           __builtin_amdgcn_s_sleep(1);
         }
         pc[P_LOAD_IDLE] += clk() - w0;
         if (dead) break;
       }
-      const int y = (hd.z >> 16) - 1;
-      const int n = (hd.z & 0xffff) - 1;
-      const int off = hd.w;
-      if (y < 0 || n == 0) {
-        lk_done(t, jhead, 0);
-        continue;
-      }
-      if (n < 0) {
+      const int y0 = (h0.z >> 16) - 1;
+      const int n0 = (h0.z & 0xffff) - 1;
+      if (y0 >= 0 && n0 < 0) {
         pc[P_DIRECT] += 1;
-        go_direct(t, y, jhead);
+        go_direct(t, y0, jhead);
+        ++t;
         continue;
       }
+      // the group: sample t and the next ready ones of <= 16 features
+      const int gk = lane >> 4, gj = lane & 15;
+      const int4 hk = gk == 0 ? h0 : lds_ld(&hdr[(t + gk) & (kSR - 1)]);
+      const int yk = (hk.z >> 16) - 1, nk = (hk.z & 0xffff) - 1;
+      const bool small_k = hk.x == t + gk && t + gk < N && (yk < 0 || (nk >= 0 && nk <= 16));
+      const uint64_t okm = __ballot(gj == 0 && small_k) & 0x0001000100010001ull;
+      // consecutive ready groups from k = 0 (the bit of group k is lane 16 k)
+      int K = 0;
+      while (K < 4 && ((okm >> (16 * K)) & 1ull)) ++K;
+      const bool single = K == 0;   // sample t is wider than 16 features
+      if (single) K = 1;
+      const int n_lanes = single ? n0 : 16;
       const uint64_t l0 = clk();
       const int jpos0 = jhead;
+      int prog = lds_ld(&ctl[C_PROGRESS]);
       bool overflow = false;
-      for (int c0 = 0; c0 < n && !overflow && !dead; c0 += 64) {
-        // room in the job ring for this chunk's misses
-        if (jhead + 64 - lds_ld(&ctl[C_JDONE]) > kJR) {
+      for (int c0 = 0; c0 < n_lanes && !overflow && !dead; c0 += 64) {
+        // room in the job ring for this pass's misses
+        if (jhead + 64 - jdone_c > kJR) {
           const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-          while (jhead + 64 - lds_ld(&ctl[C_JDONE]) > kJR) {
+          while (jhead + 64 - (jdone_c = lds_ld(&ctl[C_JDONE])) > kJR) {
             if (lds_ld(&ctl[C_ABORT]) != 0 || timed_out(t0)) { abort_with(kErrTimeoutLoad); dead = true; break; }
             __builtin_amdgcn_s_sleep(1);
           }
           if (dead) break;
         }
-        const int j = c0 + lane;
-        int2* fe = &fring[(off + j) & (kFR - 1)];
-        const int row = j < n ? lds_ld(&fe->x) : -1;
+        const int kk = single ? 0 : gk;
+        const int j = single ? c0 + lane : gj;
+        const int tk = t + kk;
+        const int4 hh = single ? h0 : hk;
+        const int yh = (hh.z >> 16) - 1, nh = (hh.z & 0xffff) - 1;
+        const bool in = kk < K && yh >= 0 && j < nh;
+        int2* fe = &fring[(hh.w + j) & (kFR - 1)];
+        const int row = in ? lds_ld(&fe->x) : -1;
         int b1 = 0, b2 = 0;
         if (row >= 0) buckets(row, NB, &b1, &b2);
         int4 k1 = make_int4(-1, -1, -1, -1), k2 = k1;
@@ -661,13 +700,16 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           return s;
         };
         int sl = row >= 0 ? match() : -1;
-        // hits are marked before any lane of the sample picks a victim
-        if (sl >= 0) use[sl] = t;
+        const uint64_t lk1 = clk();
+        pc[P_LK_KEYS] += lk1 - l0;
+        // hits are marked (the latest sample of the group that holds the
+        // row) before any lane reads the ways' last uses - LDS keeps this
+        // wave's order - so no lane evicts a row the group holds
+        if (sl >= 0) atomicMax(&use[sl], tk);
         bool need = row >= 0 && sl < 0;
         bool first = true;
         uint64_t ts = 0;
         while (__ballot(need) != 0ull) {
-          const int prog = lds_ld(&ctl[C_PROGRESS]);
           bool mine = false, stuck = false;
           int vk = -1;
           if (need) {
@@ -675,7 +717,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
               k1 = lds_ld(reinterpret_cast<const int4*>(key + 4 * b1));
               k2 = lds_ld(reinterpret_cast<const int4*>(key + 4 * b2));
               sl = match();
-              if (sl >= 0) { use[sl] = t; need = false; }
+              if (sl >= 0) { atomicMax(&use[sl], tk); need = false; }
             }
             if (need) {
               const int4 u1 = lds_ld(reinterpret_cast<const int4*>(use + 4 * b1));
@@ -695,7 +737,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
               cand(4 * b2 + 3, k2.w, u2.w);
               if (v >= 0) {
                 if (atomicCAS(&key[v], vk, row) == vk) {
-                  use[v] = t;
+                  atomicMax(&use[v], tk);
                   sl = v;
                   need = false;
                   mine = true;
@@ -706,6 +748,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
             }
           }
           first = false;
+          pc[P_LK_ITERS] += 1;
           const uint64_t mb = __ballot(mine);
           if (mine) {
             const int pos = jhead + __popcll(mb & ((1ull << lane) - 1ull));
@@ -715,8 +758,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           const uint64_t nb = __ballot(need);
           if (nb != 0ull && nb == __ballot(stuck)) {
             // every open lane lacks a free way: wait for the stepper; once it
-            // has passed every earlier sample, the sample itself holds the
-            // ways (overflow)
+            // has passed every earlier sample, the group itself holds the ways
+            // (overflow: sample t goes direct, the rest of the group again)
             const uint64_t w0 = clk();
             if (prog >= t) {
               overflow = true;
@@ -724,22 +767,32 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
               if (ts == 0) ts = __builtin_amdgcn_s_memrealtime();
               if (lds_ld(&ctl[C_ABORT]) != 0 || timed_out(ts)) { abort_with(kErrTimeoutLoad); dead = true; break; }
               __builtin_amdgcn_s_sleep(1);
+              prog = lds_ld(&ctl[C_PROGRESS]);
             }
             pc[P_LOAD_STUCK] += clk() - w0;
             if (overflow) break;
           }
         }
-        if (!overflow && j < n) lds_st(&fe->x, sl);
+        pc[P_LK_CAS] += clk() - lk1;
+        if (!overflow && in) lds_st(&fe->x, sl);
       }
       pc[P_LOAD_LOOKUP] += clk() - l0;
       if (dead) break;
       if (overflow) {
         pc[P_DIRECT] += 1;
-        go_direct(t, y, jpos0);
+        go_direct(t, y0, jpos0);
+        ++t;
         continue;
       }
       pc[P_MISSES] += (unsigned long long)(jhead - jpos0);
-      lk_done(t, jpos0, jhead - jpos0);
+      // the group's lookup records (its jobs on the first sample), in order
+      if (gj == 0 && gk < K) {
+        int* lp = reinterpret_cast<int*>(&lk[(t + gk) & (kSR - 1)]);
+        lds_st(&lp[1], gk == 0 ? jpos0 : jhead);
+        lds_st(&lp[2], gk == 0 ? jhead - jpos0 : 0);
+        lds_st(&lp[0], t + gk);
+      }
+      t += K;
     }
     if (dead) abort_with(kErrTimeoutLoad);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -521,14 +521,15 @@ def stepper_error() -> int:
 
 STEPPER_PROF_KEYS = ("step_total", "step_wait", "load_idle", "fetch_retire", "load_stuck", "meta_room",
                      "samples", "stages", "misses", "direct", "load_lookup", "fetch_issue", "load_total",
-                     "meta_total", "fetch_total")
+                     "meta_total", "fetch_total", "lk_iters", "lk_keys", "lk_cas", "st_read", "st_reduce",
+                     "st_coef", "st_apply")
 
 
 def stepper_prof() -> dict:
     """JB_STEPPER_PROF=1: shader cycles per stepper wave phase (and sample /
     stage / miss counts) since the last call"""
     import numpy as np
-    out = np.zeros(16, np.uint64)
+    out = np.zeros(32, np.uint64)
     if _fn("jb_stepper_prof")(out.ctypes.data) != 0:
         return {}
     return {k: int(v) for k, v in zip(STEPPER_PROF_KEYS, out.tolist())}

@@ -91,7 +91,7 @@ def main():
             ns = max(1, sprof.get("samples", 1))
             print(json.dumps({"mode": mode, "stepper_prof": sprof,
                               "cycles_per_sample": {k: round(v / ns, 1) for k, v in sprof.items()
-                                                    if k not in ("samples", "stages", "misses", "direct")}}),
+                                                    if k not in ("samples", "stages", "misses", "direct", "lk_iters")}}),
                   flush=True)
         del clf
         torch.cuda.empty_cache()
