@@ -32,8 +32,9 @@
 //                     label (lanes = label x feature group), best wrong label
 //                     by DPP max + ballot, the variance, the method's step
 //                     (jb_linear.hpp step_coeffs, IEEE divisions; per-feature
-//                     inverse precisions by rcp + one Newton step) and LDS
-//                     float adds into the cached rows. The next sample's
+//                     inverse precisions by rcp + one Newton step) and the
+//                     updated values stored into the cached rows (LDS float
+//                     adds when the meta wave saw a row twice in the sample). The next sample's
 //                     header and entries are read while a sample computes, so
 //                     a step is one LDS round trip (its rows) plus VALU work,
 //                     no HBM.
@@ -54,6 +55,8 @@ constexpr int kT = 256;
 constexpr int kSR = 256;            // sample header ring (power of two)
 constexpr int kFR = 1024;           // feature ring entries (power of two)
 constexpr int kFMax = 256;          // features of a cached sample (<= kFR / 2)
+constexpr int kNMask = 0x3fff;      // header word z: (y + 1) << 16 | dup bit | (n + 1)
+constexpr int kDupBit = 0x8000;
 constexpr int kK = 8;               // fetch stages in flight
 constexpr int kC = 5;               // VMEM instructions per stage (see issue_stage)
 constexpr int kSlotBytes = 98304;   // the W / P row cache
@@ -181,26 +184,54 @@ __device__ __forceinline__ bool timed_out(uint64_t t0) {
   return (int64_t)(__builtin_amdgcn_s_memrealtime() - t0) > kTimeout;
 }
 
-// sums over the G feature groups (lanes l + LC g) / max over the LC labels of a group
-template <int LC>
-__device__ __forceinline__ float group_sum(float v, int lane) {
-  if constexpr (LC == 8) v += dpp_f<kDppRowRor8>(v);
-  if constexpr (LC <= 16) v += partner16_f(v, lane);
-  if constexpr (LC <= 32) v += partner32_f(v, lane);
-  return v;
+// floats as ints of the same order (non-NaN): negative values flip their
+// magnitude bits
+__device__ __forceinline__ int ord_i(float f) {
+  const int b = __float_as_int(f);
+  return b ^ ((b >> 31) & 0x7fffffff);
 }
+// max over the LC labels of a group (lanes [k LC, (k + 1) LC))
 template <int LC>
-__device__ __forceinline__ float group_max(float v, int lane) {
-  v = fmaxf(v, dpp_f<kDppXor1>(v));
-  v = fmaxf(v, dpp_f<kDppXor2>(v));
-  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
-  if constexpr (LC >= 16) v = fmaxf(v, dpp_f<kDppMirror>(v));
-  if constexpr (LC >= 32) v = fmaxf(v, partner16_f(v, lane));
-  if constexpr (LC >= 64) v = fmaxf(v, partner32_f(v, lane));
+__device__ __forceinline__ int group_max_i(int v, int lane) {
+  v = max(v, dpp_i<kDppXor1>(v));
+  v = max(v, dpp_i<kDppXor2>(v));
+  v = max(v, dpp_i<kDppHalfMirror>(v));
+  if constexpr (LC >= 16) v = max(v, dpp_i<kDppMirror>(v));
+  if constexpr (LC >= 32) v = max(v, partner16_i(v, lane));
+  if constexpr (LC >= 64) v = max(v, partner32_i(v, lane));
   return v;
 }
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// s and a second per-lane sum q reduced over the G feature groups together:
+// one permlane swap exchanges s's odd rows with q's even rows, so one add
+// sums both (s's totals land in lanes [0, LC), q's at kQOff + [0, LC);
+// LC 64 has one group - nothing to reduce, q stays in its own register)
+template <int LC>
+struct PairLanes {
+  static constexpr int kQOff = LC <= 16 ? 16 : 32;
+};
+template <int LC>
+__device__ __forceinline__ float pair_sum(float s, float q) {
+  if constexpr (LC == 64) {
+    return s;
+  } else if constexpr (LC == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(q), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);   // [s_lo + s_hi | q_lo + q_hi]
+  } else {
+    if constexpr (LC == 8) {
+      s += dpp_f<kDppRowRor8>(s);
+      q += dpp_f<kDppRowRor8>(q);
+    }
+    // rows [s0 s1 s2 s3] [q0 q1 q2 q3] -> [s0 q0 s2 q2] + [s1 q1 s3 q3]
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(q), false, false);
+    const float t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    // -> [S Q S Q]
+    const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+    return __uint_as_float(h[0]) + __uint_as_float(h[1]);
+  }
 }
 
 // 1 / p to within ~1 ulp: the hardware reciprocal and one Newton step (three
@@ -217,7 +248,7 @@ __device__ __forceinline__ float dprec_nr(int method, float beta, float x, float
   return method == CW ? bx2 : bx2 * rcp_nr(1.f - bx2 * s);
 }
 
-template <int LC, int MT>
+template <int LC, int MT, bool PROF>
 __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__ row_ptr,
                                                      const int32_t* __restrict__ fidx,
                                                      const float* __restrict__ fval,
@@ -277,10 +308,11 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   unsigned long long pc[P_NWORDS];
 #pragma unroll
   for (int i = 0; i < P_NWORDS; ++i) pc[i] = 0;
-  const uint64_t c_start = __builtin_amdgcn_s_memtime();
   auto clk = [&]() __attribute__((always_inline)) -> uint64_t {
-    return prof != nullptr ? __builtin_amdgcn_s_memtime() : 0;
+    if constexpr (PROF) return __builtin_amdgcn_s_memtime();
+    return 0;
   };
+  const uint64_t c_start = clk();
   auto abort_with = [&](int why) __attribute__((always_inline)) {
     if (lane == 0) {
       lds_st(&ctl[C_ABORT], 1);
@@ -329,7 +361,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         entries(hd.w);
       }
       const int y = __builtin_amdgcn_readfirstlane((hd.z >> 16) - 1);
-      const int n = __builtin_amdgcn_readfirstlane((hd.z & 0xffff) - 1);
+      const int n = __builtin_amdgcn_readfirstlane((hd.z & kNMask) - 1);
+      const bool dup = __builtin_amdgcn_readfirstlane(hd.z & kDupBit) != 0;
       const int off = __builtin_amdgcn_readfirstlane(hd.w);
       int sl[QC];
       float xv[QC], inv[QC];
@@ -363,8 +396,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           float s = 0.f, vq = 0.f, nq = 0.f;
           const bool one = n <= QC * G;
           const uint64_t s0 = clk();
+          float w[QC], p[QC];
           auto chunk = [&]() __attribute__((always_inline)) {
-            float w[QC], p[QC];
 #pragma unroll
             for (int u = 0; u < QC; ++u) {
               w[u] = Wc[sl[u] * LC + l];
@@ -396,17 +429,25 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           }
           const uint64_t s1 = clk();
           pc[P_ST_READ] += s1 - s0;
-          s = group_sum<LC>(s, lane);
-          if (use_nrm) nq = group_sum<LC>(nq, lane);
-          if (use_s) vq = group_sum<LC>(vq, lane);
-          const float v = (act && l != y) ? s : -INFINITY;
-          const float m = group_max<LC>(v, lane);
-          const uint64_t bal = __ballot(lane < LC && act && l != y && v == m && v > -INFINITY);
+          // s and the method's second sum (x^2 / P or |x|^2) reduced together
+          const float q = use_s ? vq : nq;
+          const float r = pair_sum<LC>(s, q);
+          // best wrong label: max over the labels as order-preserving ints
+          // (one fused DPP max per step, no float canonicalisation)
+          const int v = (act && l != y) ? ord_i(r) : ord_i(-INFINITY);
+          const int m = group_max_i<LC>(v, lane);
+          const uint64_t bal = __ballot(lane < LC && act && l != y && v == m && v > ord_i(-INFINITY));
           const int bl = bal != 0ull ? (int)__ffsll((long long)bal) - 1 : -1;
-          const float sy = readlane_f(s, y);
-          const float best = bl >= 0 ? readlane_f(s, bl) : 0.f;
-          const float var = use_s ? readlane_f(vq, y) + (bl >= 0 ? readlane_f(vq, bl) : 0.f) : 0.f;
-          const float nrm = use_nrm ? readlane_f(nq, 0) : 0.f;
+          const int blr = bl >= 0 ? bl : y;   // a lane to read without a branch (discarded if bl < 0)
+          auto rq = [&](int i) __attribute__((always_inline)) {
+            return LC == 64 ? readlane_f(q, i) : readlane_f(r, PairLanes<LC>::kQOff + i);
+          };
+          const float sy = readlane_f(r, y);
+          const float sb = readlane_f(r, blr);
+          const float best = bl >= 0 ? sb : 0.f;
+          const float qb = rq(blr);
+          const float var = use_s ? rq(y) + (bl >= 0 ? qb : 0.f) : 0.f;
+          const float nrm = use_nrm ? rq(0) : 0.f;
           float tau = 0.f, beta = 0.f;
           const uint64_t s2 = clk();
           pc[P_ST_REDUCE] += s2 - s1;
@@ -418,12 +459,19 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
             const bool isy = l == y, isl = l == bl;
             if (isy || isl) {
               const float sg = isy ? tau : -tau;
-              if (one) {
+              if (one && !dup) {
+                // distinct slots: the values read above plus the deltas
+                // (absent features store the dummy slot's value back)
+#pragma unroll
+                for (int u = 0; u < QC; ++u) {
+                  Wc[sl[u] * LC + l] = fmaf(sg * inv[u], xv[u], w[u]);
+                  if (use_s) Pc[sl[u] * LC + l] = p[u] + dprec_nr(MT, beta, xv[u], inv[u]);
+                }
+              } else if (one) {
 #pragma unroll
                 for (int u = 0; u < QC; ++u) {   // (absent features add 0 to the dummy slot)
                   atomicAdd(&Wc[sl[u] * LC + l], sg * inv[u] * xv[u]);
                   if (use_s) atomicAdd(&Pc[sl[u] * LC + l], dprec_nr(MT, beta, xv[u], inv[u]));
-                  if (isy) dirty[sl[u]] = 1;
                 }
               } else {
                 // wide sample: the entries again, chunk by chunk. Every
@@ -441,7 +489,6 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                     const float iv = use_s ? rcp_nr(Pc[sj * LC + l]) : 1.f;
                     atomicAdd(&Wc[sj * LC + l], sg * iv * x);
                     if (use_s) dps[2 * j + (isy ? 0 : 1)] = dprec_nr(MT, beta, x, iv);
-                    if (isy) dirty[sj] = 1;
                   }
                 }
                 if (use_s) {
@@ -515,23 +562,46 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
       const int base = head + ex;
-      for (int f0 = 0; f0 < mx; f0 += 8) {
-        int id[8];
-        float xv[8];
+      // dup: two features of the sample share a row (so a slot) - the stepper
+      // then applies with LDS atomics; else with plain stores. Decided for
+      // samples of <= 16 features (the stepper's one-pass case)
+      int dup = 0;
+      if (mx <= 16) {
+        int id[16];
+        float xv[16];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const bool on = take && f0 + i < ns;
-          id[i] = on ? fidx[rp0 + f0 + i] : -1;
-          xv[i] = on ? fval[rp0 + f0 + i] : 0.f;
+        for (int i = 0; i < 16; ++i) {
+          const bool on = take && i < ns;
+          id[i] = on ? fidx[rp0 + i] : -1 - i;
+          xv[i] = on ? fval[rp0 + i] : 0.f;
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (take && f0 + i < ns) fring[(base + f0 + i) & (kFR - 1)] = make_int2(id[i], __float_as_int(xv[i]));
+        for (int i = 1; i < 16; ++i)
+#pragma unroll
+          for (int k = 0; k < i; ++k) dup |= id[i] == id[k] ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (take && i < ns) fring[(base + i) & (kFR - 1)] = make_int2(id[i], __float_as_int(xv[i]));
+      } else {
+        for (int f0 = 0; f0 < mx; f0 += 8) {
+          int id[8];
+          float xv[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const bool on = take && f0 + i < ns;
+            id[i] = on ? fidx[rp0 + f0 + i] : -1;
+            xv[i] = on ? fval[rp0 + f0 + i] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (take && f0 + i < ns) fring[(base + f0 + i) & (kFR - 1)] = make_int2(id[i], __float_as_int(xv[i]));
+        }
+        dup = 1;
       }
       if (take) {
         const int hh = t & (kSR - 1);
         int* hp = reinterpret_cast<int*>(&hdr[hh]);
-        lds_st(&hp[2], ((vy ? y : -1) + 1) << 16 | ((hn + 1) & 0xffff));
+        lds_st(&hp[2], ((vy ? y : -1) + 1) << 16 | (dup ? kDupBit : 0) | ((hn + 1) & kNMask));
         lds_st(&hp[3], base);
         lds_st(&fend[hh], base + ns);
         lds_st(&hp[0], t);   // meta_seq last
@@ -639,7 +709,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         if (dead) break;
       }
       const int y0 = (h0.z >> 16) - 1;
-      const int n0 = (h0.z & 0xffff) - 1;
+      const int n0 = (h0.z & kNMask) - 1;
       if (y0 >= 0 && n0 < 0) {
         pc[P_DIRECT] += 1;
         go_direct(t, y0, jhead);
@@ -649,7 +719,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       // the group: sample t and the next ready ones of <= 16 features
       const int gk = lane >> 4, gj = lane & 15;
       const int4 hk = gk == 0 ? h0 : lds_ld(&hdr[(t + gk) & (kSR - 1)]);
-      const int yk = (hk.z >> 16) - 1, nk = (hk.z & 0xffff) - 1;
+      const int yk = (hk.z >> 16) - 1, nk = (hk.z & kNMask) - 1;
       const bool small_k = hk.x == t + gk && t + gk < N && (yk < 0 || (nk >= 0 && nk <= 16));
       const uint64_t okm = __ballot(gj == 0 && small_k) & 0x0001000100010001ull;
       // consecutive ready groups from k = 0 (the bit of group k is lane 16 k)
@@ -676,7 +746,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         const int j = single ? c0 + lane : gj;
         const int tk = t + kk;
         const int4 hh = single ? h0 : hk;
-        const int yh = (hh.z >> 16) - 1, nh = (hh.z & 0xffff) - 1;
+        const int yh = (hh.z >> 16) - 1, nh = (hh.z & kNMask) - 1;
         const bool in = kk < K && yh >= 0 && j < nh;
         int2* fe = &fring[(hh.w + j) & (kFR - 1)];
         const int row = in ? lds_ld(&fe->x) : -1;
@@ -858,7 +928,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       *reinterpret_cast<float4*>(dw) = ow;
       *reinterpret_cast<float4*>(dp) = op;
       *dt = 1;
-      if (on && part == 0) dirty[sl] = 0;
+      if (on && part == 0) dirty[sl] = 1;   // every cached row goes back when evicted
       const float* sw = on ? W + (int64_t)row * LC + 4 * part : dummy;
       const float* sp = (on && use_s) ? P + (int64_t)row * LC + 4 * part : dummy;
       const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(stage + b * 2048));
@@ -915,7 +985,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
     if (c == 0 && touched != nullptr) touched[k] = 1;
   }
   if (tid == 0 && ctl[C_ABORT] != 0 && err != nullptr) atomicMax(err, ctl[C_WHY] != 0 ? ctl[C_WHY] : 9);
-  if (prof != nullptr && lane == 0) {
+  if (PROF && prof != nullptr && lane == 0) {
 #pragma unroll
     for (int i = 0; i < P_NWORDS; ++i)
       if (pc[i] != 0) atomicAdd(prof + i, pc[i]);
@@ -941,7 +1011,8 @@ extern "C" int jb_stepper_error() {
 }
 
 // JB_STEPPER_PROF=1: the launches accumulate per-wave phase cycles into
-// g_prof; jb_stepper_prof copies them out (uint64 [16]) and resets them
+// g_prof (label capacities 8 and 16; the others run unprofiled);
+// jb_stepper_prof copies them out (uint64 [P_NWORDS]) and resets them
 static bool stepper_prof_on() {
   static const bool on = [] {
     const char* e = getenv("JB_STEPPER_PROF");
@@ -990,16 +1061,24 @@ extern "C" int jb_stepper_train(const int64_t* row_ptr, const int32_t* fidx, con
     }();
     prof = gp;
   }
-#define JB_SP_LAUNCH(L, M)                                                                                    \
+#define JB_SP_LAUNCH_P(L, M, PR)                                                                              \
   {                                                                                                           \
     static bool attr = [] {                                                                                   \
-      return hipFuncSetAttribute((const void*)jb::sp::stepper_kernel<L, M>,                                  \
+      return hipFuncSetAttribute((const void*)jb::sp::stepper_kernel<L, M, PR>,                              \
                                  hipFuncAttributeMaxDynamicSharedMemorySize, jb::sp::Geo<L>::kBytes) ==      \
              hipSuccess;                                                                                      \
     }();                                                                                                      \
     (void)attr;                                                                                               \
-    hipLaunchKernelGGL((jb::sp::stepper_kernel<L, M>), dim3(1), dim3(jb::sp::kT), jb::sp::Geo<L>::kBytes,   \
+    hipLaunchKernelGGL((jb::sp::stepper_kernel<L, M, PR>), dim3(1), dim3(jb::sp::kT), jb::sp::Geo<L>::kBytes, \
                        stream, row_ptr, fidx, fval, labels, range, W, P, active, C, stats, touched, err, prof);    \
+  }
+  // the phase counters are compiled into the label-capacity 8 and 16 kernels only
+#define JB_SP_LAUNCH(L, M)                                   \
+  if constexpr (L <= 16) {                                   \
+    if (prof != nullptr) JB_SP_LAUNCH_P(L, M, true)          \
+    else JB_SP_LAUNCH_P(L, M, false)                         \
+  } else {                                                   \
+    JB_SP_LAUNCH_P(L, M, false)                              \
   }
 #define JB_SP_M(L)                                          \
   switch (method) {                                         \
@@ -1021,5 +1100,6 @@ extern "C" int jb_stepper_train(const int64_t* row_ptr, const int32_t* fidx, con
   }
 #undef JB_SP_M
 #undef JB_SP_LAUNCH
+#undef JB_SP_LAUNCH_P
   return (int)hipGetLastError();
 }
