@@ -1,0 +1,50 @@
+// The verified committer's device state words (vcommit.hip), shared with the
+// sequential stepper (stepper.hip): after an update-dense committed window
+// (status kDense) the stepper applies the next chunk of the batch in order
+// from the window's end, then hands the batch back to the committer
+// (status kNew at the chunk's end, kDone at the batch end).
+#pragma once
+#include <stdint.h>
+
+namespace jb {
+namespace vc {
+
+enum : int { kNew = 0, kRetry = 1, kDone = 2, kDense = 3 };
+// state words (int64 each, 512 B)
+enum : int {
+  S_MAGIC = 0, S_BEG, S_BEND, S_STATUS, S_LW, S_T, S_NCAND, S_PEND, S_WHY, S_NUPD, S_NSLOTS, S_VIOL,
+  S_DONEB, S_NVALID, S_RETRYW, S_WEND,
+  // batch counters
+  S_WINDOWS, S_RETRIES, S_STEPS, S_ROUNDS, S_WASTED, S_REFRESH, S_EXACT, S_CAND, S_UPD, S_SAT, S_TICKS,
+  S_NONC, S_PH0, S_PH1, S_PH2, S_PH3, S_PH4, S_PHW, S_WIDE, S_DENSE_PM,
+  S_DCHUNK,    // samples of the next stepper chunk (doubles while windows stay dense)
+  S_STEPPED,   // samples the stepper chunks applied in this batch
+  S_NCHUNK,    // stepper chunks in this batch
+  S_BBEG,      // the batch's first sample
+  S_NWORDS = 64
+};
+// committer stop reasons (S_WHY)
+enum : int { kWhyEnd = 0, kWhySat = 1, kWhyDense = 2 };
+// first stepper chunk after a dense window; chunks double up to kDenseChunkMax
+constexpr int64_t kDenseChunk0 = 8192, kDenseChunkMax = 1 << 20;
+// tail words (the batch's int64 x 32 diagnostics, jb_commit.hpp) the stepper
+// chunks report through
+constexpr int kTailStepped = 16, kTailChunks = 17, kTailSegEst = 18;
+// tail[kTailReasonW]: the batch's stop reason (jb_commit.hpp dc::kTailReason / kStop*)
+constexpr int kTailReasonW = 20;
+constexpr int64_t kReasonDone = 0, kReasonSaturated = 1;
+
+// segments the batch would have used without stepper chunks (its windows and
+// retries, plus the chunks' samples at the batch's mean committed window) -
+// the next batch's segment budget (serial.hip): a batch that is sparse again
+// after a dense one must not run out of segments
+__device__ inline int64_t seg_estimate(const int64_t* st) {
+  const int64_t wins = st[S_WINDOWS], stepped = st[S_STEPPED];
+  const int64_t committed = st[S_BEG] - st[S_BBEG] - stepped;
+  int64_t per = committed > 0 && wins > 0 ? committed / wins : 2048;
+  per = per < 64 ? 64 : per;
+  return wins + st[S_RETRIES] + (stepped + per - 1) / per;
+}
+
+}  // namespace vc
+}  // namespace jb

@@ -819,7 +819,7 @@ static int64_t* delta_segments_seen(void* scratch) {
   auto it = seen.find(scratch);
   if (it != seen.end()) return it->second;
   int64_t* p = nullptr;
-  if (hipHostMalloc((void**)&p, 2 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
+  if (hipHostMalloc((void**)&p, 4 * sizeof(int64_t), hipHostMallocDefault) != hipSuccess) return nullptr;
   // until the first batch reports: done in 128 segments (a host running
   // batches ahead of the device must not read "unknown" as "short": every
   // batch would get all 512 and pay ~12 us per empty one; a young model's
@@ -828,6 +828,7 @@ static int64_t* delta_segments_seen(void* scratch) {
   // batches 0-5, profiles/serial_exact_r4_prof_switch.jsonl)
   p[0] = jb::kStopDone;
   p[1] = 128;
+  p[2] = 0;   // (verified committer) segment estimate with its stepper chunks
   seen[scratch] = p;
   return p;
 }
@@ -887,7 +888,11 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
     int64_t* seen = delta_segments_seen(scratch);
     if (n_max >= jb::kSerialBigBatch) {
       const int64_t why = seen != nullptr ? ((volatile int64_t*)seen)[0] : 0;
-      const int64_t prev = seen != nullptr ? ((volatile int64_t*)seen)[1] : 0;
+      // (with the windows the previous batch's stepper chunks stood in for -
+      // vcommit.hip seg_estimate: a batch that is sparse again after a dense
+      // one must not run out of segments)
+      const int64_t est = seen != nullptr ? ((volatile int64_t*)seen)[2] : 0;
+      const int64_t prev = std::max<int64_t>(seen != nullptr ? ((volatile int64_t*)seen)[1] : 0, est);
       const bool short_of = why != jb::kStopDone && why != jb::kStopDense;
       // slack over the previous batch's count: prev / 2 + 8 by default
       // (JB_VC_SEG_SLACK = d,c: prev / d + c, an A/B knob)
@@ -906,8 +911,10 @@ extern "C" int jb_serial_prepare(const int64_t* row_ptr, const int32_t* fidx, co
     }
     const int rc = jb_vcommit_prepare(row_ptr, fidx, fval, labels, stream_ptr, nstreams, n_max, W, S, active,
                                       LC, method, C, stats, touched, scratch, nseg, stream);
-    if (rc == 0 && seen != nullptr)
+    if (rc == 0 && seen != nullptr) {
       (void)hipMemcpyAsync(seen, (int64_t*)scratch + 20, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, stream);
+      (void)hipMemcpyAsync(seen + 2, (int64_t*)scratch + 18, sizeof(int64_t), hipMemcpyDeviceToHost, stream);
+    }
     return rc;
   }
   if (LC <= 64 && serial_committer() == 1) {

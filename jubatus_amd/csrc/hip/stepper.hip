@@ -47,6 +47,7 @@
 #include <string.h>
 
 #include "jb_linear.hpp"
+#include "jb_vc_state.hpp"
 
 namespace jb {
 namespace sp {
@@ -81,7 +82,7 @@ struct Geo {
   static constexpr int oKey = oP + (NSLOT + 1) * LC * 4;
   static constexpr int oUse = oKey + (NSLOT + 4) * 4;
   static constexpr int oDirty = oUse + (NSLOT + 4) * 4;
-  static constexpr int oHdr = oDirty + (NSLOT + 4) * 4;                      // int4 [kSR]: meta_seq, ready_seq, y|n, off
+  static constexpr int oHdr = oDirty + (NSLOT + 4) * 4;  // int4 [kSR]: meta/ready seq, y|n, off
   static constexpr int oFend = oHdr + kSR * 16;                        // int [kSR]
   static constexpr int oFR = oFend + kSR * 4;                          // int2 [kFR]: row (then slot), x
   static constexpr int oStage = oFR + kFR * 8;                         // [kK][W 1 KB | P 1 KB]
@@ -118,7 +119,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // sc1: past the CU's L1 (a row written back by this CU earlier is read from L2)
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(lds_dst)
                : "memory");
@@ -257,7 +259,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                                                      const int32_t* __restrict__ active, float C,
                                                      unsigned long long* __restrict__ stats,
                                                      uint8_t* __restrict__ touched, int* __restrict__ err,
-                                                     unsigned long long* __restrict__ prof) {
+                                                     unsigned long long* __restrict__ prof, int64_t* vst,
+                                                     int64_t* vtail) {
   using Gm = Geo<LC>;
   constexpr bool use_s = MT >= CW;
   constexpr bool use_nrm = MT == PA || MT == PA1 || MT == PA2;
@@ -283,10 +286,19 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int64_t beg = range[0];
-  const int64_t end = range[1];
-  if (end <= beg) return;
-  const int N = (int)(end - beg);
+  // vst (a verified committer's state, vcommit.hip): a chunk after an
+  // update-dense window - nothing to do unless the committer stopped dense
+  int64_t beg, end;
+  if (vst != nullptr) {
+    if (vst[vc::S_STATUS] != vc::kDense) return;
+    beg = vst[vc::S_BEG];
+    end = min(vst[vc::S_BEND], beg + vst[vc::S_DCHUNK]);
+  } else {
+    beg = range[0];
+    end = range[1];
+  }
+  if (end <= beg && vst == nullptr) return;
+  const int N = (int)(end > beg ? end - beg : 0);
 
   // ---- init (all waves)
   for (int i = tid; i < NSLOT + 4; i += kT) {
@@ -631,7 +643,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           for (int c = 0; c < LC; c += 4) {
             *reinterpret_cast<float4*>(W + (int64_t)wrow * LC + c) = *reinterpret_cast<const float4*>(Wc + sl * LC + c);
             if (use_s)
-              *reinterpret_cast<float4*>(P + (int64_t)wrow * LC + c) = *reinterpret_cast<const float4*>(Pc + sl * LC + c);
+              *reinterpret_cast<float4*>(P + (int64_t)wrow * LC + c) =
+                  *reinterpret_cast<const float4*>(Pc + sl * LC + c);
           }
           if (touched != nullptr) touched[wrow] = 1;
         }
@@ -985,6 +998,22 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
     if (c == 0 && touched != nullptr) touched[k] = 1;
   }
   if (tid == 0 && ctl[C_ABORT] != 0 && err != nullptr) atomicMax(err, ctl[C_WHY] != 0 ? ctl[C_WHY] : 9);
+  if (tid == 0 && vst != nullptr) {
+    // the batch back to the committer from the chunk's end
+    const int64_t bend = vst[vc::S_BEND];
+    const bool done = end >= bend;
+    vst[vc::S_BEG] = end;
+    vst[vc::S_STATUS] = done ? vc::kDone : vc::kNew;
+    vst[vc::S_STEPPED] += end - beg;
+    vst[vc::S_NCHUNK] += 1;
+    vst[vc::S_DCHUNK] = min(2 * vst[vc::S_DCHUNK], vc::kDenseChunkMax);
+    vtail[0] = done ? bend : end;
+    vtail[1] = bend;
+    vtail[vc::kTailReasonW] = done ? vc::kReasonDone : vc::kReasonSaturated;
+    vtail[vc::kTailStepped] = vst[vc::S_STEPPED];
+    vtail[vc::kTailChunks] = vst[vc::S_NCHUNK];
+    vtail[vc::kTailSegEst] = vc::seg_estimate(vst);
+  }
   if (PROF && prof != nullptr && lane == 0) {
 #pragma unroll
     for (int i = 0; i < P_NWORDS; ++i)
@@ -1002,7 +1031,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
 // stepper abort reason since the last call (0: none); resets it
 extern "C" int jb_stepper_error() {
   int v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(jb::sp::g_err), sizeof(int), 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(jb::sp::g_err), sizeof(int), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
   if (v != 0) {
     const int z = 0;
     (void)hipMemcpyToSymbol(HIP_SYMBOL(jb::sp::g_err), &z, sizeof(int), 0, hipMemcpyHostToDevice);
@@ -1040,10 +1070,10 @@ extern "C" int jb_stepper_enabled() {
   return on;
 }
 
-extern "C" int jb_stepper_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
-                                const int32_t* labels, const int64_t* range, float* W, float* P,
-                                const int32_t* active, int LC, int method, float C, unsigned long long* stats,
-                                uint8_t* touched, int* err, hipStream_t stream) {
+static int stepper_launch(const int64_t* row_ptr, const int32_t* fidx, const float* fval, const int32_t* labels,
+                          const int64_t* range, float* W, float* P, const int32_t* active, int LC, int method,
+                          float C, unsigned long long* stats, uint8_t* touched, int* err, int64_t* vst,
+                          int64_t* vtail, hipStream_t stream) {
   if (LC < 8 || LC > 64) return -1;
   if (method >= jb::CW && P == nullptr) return -4;
   if (err == nullptr) {
@@ -1070,7 +1100,8 @@ extern "C" int jb_stepper_train(const int64_t* row_ptr, const int32_t* fidx, con
     }();                                                                                                      \
     (void)attr;                                                                                               \
     hipLaunchKernelGGL((jb::sp::stepper_kernel<L, M, PR>), dim3(1), dim3(jb::sp::kT), jb::sp::Geo<L>::kBytes, \
-                       stream, row_ptr, fidx, fval, labels, range, W, P, active, C, stats, touched, err, prof);    \
+                       stream, row_ptr, fidx, fval, labels, range, W, P, active, C, stats, touched, err, prof,     \
+                       vst, vtail);                                                                          \
   }
   // the phase counters are compiled into the label-capacity 8 and 16 kernels only
 #define JB_SP_LAUNCH(L, M)                                   \
@@ -1102,4 +1133,26 @@ extern "C" int jb_stepper_train(const int64_t* row_ptr, const int32_t* fidx, con
 #undef JB_SP_LAUNCH
 #undef JB_SP_LAUNCH_P
   return (int)hipGetLastError();
+}
+
+extern "C" int jb_stepper_train(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                                const int32_t* labels, const int64_t* range, float* W, float* P,
+                                const int32_t* active, int LC, int method, float C, unsigned long long* stats,
+                                uint8_t* touched, int* err, hipStream_t stream) {
+  return stepper_launch(row_ptr, fidx, fval, labels, range, W, P, active, LC, method, C, stats, touched, err, nullptr,
+                        nullptr, stream);
+}
+
+// One chunk of a verified-committer batch after an update-dense window
+// (vcommit.hip launches it after every segment): [S_BEG, S_BEG + S_DCHUNK)
+// of the batch when vst's status is kDense, then the status is kNew (kDone at
+// the batch end) and the next segment continues from the chunk's end; an
+// empty launch otherwise.
+extern "C" int jb_stepper_chunk(const int64_t* row_ptr, const int32_t* fidx, const float* fval, const int32_t* labels,
+                                float* W, float* P, const int32_t* active, int LC, int method, float C,
+                                unsigned long long* stats, uint8_t* touched, int64_t* vst, int64_t* vtail,
+                                hipStream_t stream) {
+  if (vst == nullptr || vtail == nullptr) return -2;
+  return stepper_launch(row_ptr, fidx, fval, labels, nullptr, W, P, active, LC, method, C, stats, touched, nullptr,
+                        vst, vtail, stream);
 }

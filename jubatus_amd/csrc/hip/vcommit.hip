@@ -45,8 +45,11 @@
 //
 // The window ends where the committer stops: at its end, when the LDS store is
 // full (the next window re-scores from there), or at a candidate wider than 32
-// features (the rest of the batch goes to the single-stream exact kernel, as
-// with the other committers). Windows adapt their length to where the store
+// features. Such a window, and one whose updates were dense (JB_VC_DENSE_PM),
+// hands the next chunk of the batch to the sequential stepper (stepper.hip,
+// launched after every segment, empty unless the status says kDense); the
+// next segment continues after the chunk. Chunks double while the windows
+// between them stay dense. Windows adapt their length to where the store
 // fills. Decisions follow commit.hip's guard band (a margin within 1e-4 of its
 // threshold is re-scored from the live model M0 + dW before the decision).
 //
@@ -58,6 +61,7 @@
 #include <type_traits>
 
 #include "jb_commit.hpp"
+#include "jb_vc_state.hpp"
 
 namespace jb {
 namespace vc {
@@ -77,17 +81,10 @@ constexpr int kBitWords = (int)(kLwMax / 64);
 constexpr float kTInit = 0.5f, kTMin = 0.125f, kTMax = 64.f;
 constexpr int64_t kMagic = 0x56434f4d4d495433LL;
 constexpr int kRetryForce = 3;          // retries of one window before all its samples are candidates
-enum : int { kNew = 0, kRetry = 1, kDone = 2, kDense = 3 };
-// state words
-enum : int {
-  S_MAGIC = 0, S_BEG, S_BEND, S_STATUS, S_LW, S_T, S_NCAND, S_PEND, S_WHY, S_NUPD, S_NSLOTS, S_VIOL,
-  S_DONEB, S_NVALID, S_RETRYW, S_WEND,
-  // batch counters
-  S_WINDOWS, S_RETRIES, S_STEPS, S_ROUNDS, S_WASTED, S_REFRESH, S_EXACT, S_CAND, S_UPD, S_SAT, S_TICKS,
-  S_NONC, S_PH0, S_PH1, S_PH2, S_PH3, S_PH4, S_PHW, S_WIDE, S_DENSE_PM, S_NWORDS = 64
-};
-// committer stop reasons (S_WHY)
-enum : int { kWhyEnd = 0, kWhySat = 1, kWhyDense = 2 };
+// (status, state words and stop reasons: jb_vc_state.hpp, shared with the stepper)
+static_assert(kTailReasonW == dc::kTailReason && kReasonDone == dc::kStopDone &&
+                  kReasonSaturated == dc::kStopSaturated,
+              "jb_vc_state.hpp mirrors jb_commit.hpp's tail words");
 
 __device__ __forceinline__ float st_T(const int64_t* st) { return __int_as_float((int)st[S_T]); }
 __device__ __forceinline__ int64_t ld_st(const int64_t* p) {
@@ -176,6 +173,8 @@ __global__ __launch_bounds__(256) void vc_init_kernel(int64_t* __restrict__ st, 
   for (int i = S_NCAND; i <= S_RETRYW; ++i) st[i] = 0;
   for (int i = S_WINDOWS; i < S_NWORDS; ++i) st[i] = 0;
   st[S_DENSE_PM] = dense_pm;
+  st[S_DCHUNK] = kDenseChunk0;
+  st[S_BBEG] = beg;
   for (int i = 0; i < 32; ++i) tail[i] = 0;
   tail[0] = beg < bend ? beg : bend;
   tail[1] = bend;
@@ -1023,12 +1022,14 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
       st[S_UPD] += nupd;
       if (why == kWhySat) st[S_SAT] += 1;
       // an update-dense window (more than dense_pm per mille of its samples
-      // updated): the rest of the batch goes to the sequential stepper
-      // (stepper.hip, ~0.2 us a sample whatever updates), which beats this
-      // committer's ~2.2 us a step once updates are that frequent
+      // updated): the next chunk of the batch goes to the sequential stepper
+      // (stepper.hip, ~0.8 us a sample whatever updates), which beats this
+      // committer's ~2.2 us a step once updates are that frequent; the
+      // segment after it continues from the chunk's end
       const int64_t dpm = st[S_DENSE_PM];
       const bool dense = dpm > 0 && pe < bend && nupd * 1000 > dpm * (pe - wb);
       st[S_STATUS] = (why == kWhyDense || dense) ? kDense : (pe >= bend ? kDone : kNew);
+      if (!(why == kWhyDense || dense)) st[S_DCHUNK] = kDenseChunk0;   // sparse again: chunks start small
       // the window length follows where the store fills; T relaxes slowly
       int64_t lw = st[S_LW];
       if (why == kWhySat) {
@@ -1076,6 +1077,9 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
     // stop reason: done / saturated (segments ran out) / dense
     tail[dc::kTailReason] = s2 == kDone ? dc::kStopDone : s2 == kDense ? dc::kStopDense : dc::kStopSaturated;
     tail[21] = st[S_WINDOWS] + st[S_RETRIES];   // segments used
+    tail[kTailStepped] = st[S_STEPPED];
+    tail[kTailChunks] = st[S_NCHUNK];
+    tail[kTailSegEst] = seg_estimate(st);
     tail[22] = st[S_WASTED];
     tail[23] = st[S_REFRESH];
     tail[24] = st[S_UPD];
@@ -1101,12 +1105,19 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
 static constexpr int64_t kVcFixed = 512 + 8 * jb::vc::kBitWords + 4 * 1024 + 4 * 1024 + 2 * 4 * 16384;
 extern "C" int64_t jb_vcommit_fixed_bytes() { return kVcFixed; }
 
+// stepper.hip
+extern "C" int jb_stepper_enabled();
+extern "C" int jb_stepper_chunk(const int64_t* row_ptr, const int32_t* fidx, const float* fval, const int32_t* labels,
+                                float* W, float* P, const int32_t* active, int LC, int method, float C,
+                                unsigned long long* stats, uint8_t* touched, int64_t* vst, int64_t* vtail,
+                                hipStream_t stream);
+
 template <int L>
 static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                      const int32_t* labels, float* W, float* S, const int32_t* active, float C, int64_t* st,
                      float* sl, unsigned long long* bits, float* s0, int4* aux, float2* pp0, int32_t* fi,
                      float* fx, int32_t* gk, float* gr, float* gdw, float* gdp, uint8_t* touched,
-                     unsigned long long* stats, int64_t* tail, int nseg, hipStream_t stream) {
+                     unsigned long long* stats, int64_t* tail, int nseg, bool chunks, hipStream_t stream) {
   using namespace jb::vc;
   static const int prof = [] {
     const char* e = getenv("JB_COMMIT_PROF");
@@ -1153,6 +1164,13 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
 #undef JB_VC_S
     hipLaunchKernelGGL((vc_verify_kernel<L>), dim3(256), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        sl, bits, gk, gr, gdw, gdp, W, Pp, touched, stats, tail);
+    // after an update-dense window: the stepper's chunk (an empty launch
+    // otherwise), then the next segment continues from its end
+    if (chunks) {
+      const int rc = jb_stepper_chunk(row_ptr, fidx, fval, labels, W, Pp, active, L, method, C, stats, touched, st,
+                                      tail, stream);
+      if (rc != 0) return rc;
+    }
   }
   return 0;
 }
@@ -1188,15 +1206,20 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
   const char* te = getenv("JB_VERIFIED_T");
   const float t_force = te != nullptr ? (float)atof(te) : 0.f;
   // JB_VC_DENSE_PM: updates per mille of a committed window past which the
-  // rest of the batch goes to the stepper (0: never; default 100)
+  // next chunk of the batch goes to the stepper (0: never; default 300 - the
+  // committer costs ~2.2 us an update, the stepper ~0.8 us a sample)
   const char* de = getenv("JB_VC_DENSE_PM");
-  const int dense_pm = de != nullptr ? atoi(de) : 100;
+  const int dense_pm = de != nullptr ? atoi(de) : 300;
   hipLaunchKernelGGL(jb::vc::vc_init_kernel, dim3(1), dim3(256), 0, stream, st, stream_ptr, nstreams, bits, tail,
                      t_force, gk, gr, dense_pm);
+  // fp32 tables with the stepper on: dense windows hand the next chunk to it
+  // inside the segment sequence (else the batch's rest goes to the caller's
+  // single-stream kernel at the end)
+  const bool chunks = dense_pm > 0 && jb_stepper_enabled();
   int rc = 0;
 #define JB_VC_L(L)                                                                                            \
   rc = launch_vc<L>(method, row_ptr, fidx, fval, labels, W, S, active, C, st, sl, bits, s0, aux, pp0, fi, fx, \
-                    gk, gr, gdw, gdp, touched, stats, tail, nseg, stream);                                     \
+                    gk, gr, gdw, gdp, touched, stats, tail, nseg, chunks, stream);                             \
   break;
   switch (LC) {
     case 8: JB_VC_L(8)

@@ -2165,7 +2165,8 @@ class Server {
       mixer_->start();
       logf_("INFO", "registered group membership as %s (native linear_mixer)", ident().c_str());
     }
-    logf_("INFO", "jubaclassifier RPC server startup (native%s)", std::is_same<M, HostClassifier>::value ? ", host" : "");
+    logf_("INFO", "jubaclassifier RPC server startup (native%s)",
+          std::is_same<M, HostClassifier>::value ? ", host" : "");
     wait_for_term();
     if (mixer_) {
       logf_("INFO", "stopping mixer thread");

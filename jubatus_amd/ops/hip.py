@@ -757,9 +757,10 @@ class SerialScratch:
                        wasted_steps=v[22], refreshes=v[23], exact_rescored=v[26], last_segment_rows=v[25],
                        window_len=v[8], T=round(struct.unpack("f", struct.pack("I", v[9] & 0xffffffff))[0], 4),
                        commit_kernel_us=round(v[30] / 100.0, 1),
-                       # the rest after an update-dense window (stop_reason
-                       # "dense") ran on the sequential stepper (csrc/hip/stepper.hip)
-                       stepper_samples=v[1] - v[0])
+                       # samples the sequential stepper (csrc/hip/stepper.hip)
+                       # applied: chunks after update-dense windows, and the
+                       # rest the segments left (stop_reason "dense")
+                       stepper_samples=v[16] + v[1] - v[0], stepper_chunks=v[17])
             if v[15] > 0:      # JB_COMMIT_PROF=1: committer phases (shader cycles -> us by the wall clock)
                 us = (v[30] / 100.0) / v[15]
                 for i, nm in enumerate(("round_start", "select", "decide", "apply", "correct")):

@@ -54,8 +54,11 @@ def test_signatures_match_host(method):
     cb, cn = c._signatures(rs)
     gb = gb.cpu().numpy().view(np.uint64)
     agree = np.mean([bin(int(a) ^ int(b)).count("1") == 0 for a, b in zip(gb.ravel(), cb.ravel())])
-    # bits of projections within fp32 rounding of 0 may flip; nearly all words agree
-    assert agree > 0.97, agree
+    # only a projection within fp32 rounding of 0 may flip a bit (the host
+    # sums in another order): at most one word in a thousand differs
+    assert agree >= 0.999, agree
+    bit_diff = np.mean([bin(int(a) ^ int(b)).count("1") for a, b in zip(gb.ravel(), cb.ravel())]) / 64
+    assert bit_diff <= 1e-4, bit_diff
     np.testing.assert_allclose(gn.cpu().numpy(), cn, rtol=1e-5)
 
 

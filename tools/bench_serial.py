@@ -89,9 +89,10 @@ def main():
         if sprof:
             # stepper wave phases over batches 2+ (shader cycles; per sample)
             ns = max(1, sprof.get("samples", 1))
+            counts = ("samples", "stages", "misses", "direct", "lk_iters")
             print(json.dumps({"mode": mode, "stepper_prof": sprof,
                               "cycles_per_sample": {k: round(v / ns, 1) for k, v in sprof.items()
-                                                    if k not in ("samples", "stages", "misses", "direct", "lk_iters")}}),
+                                                    if k not in counts}}),
                   flush=True)
         del clf
         torch.cuda.empty_cache()
