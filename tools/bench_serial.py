@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--requests", type=int, default=1024)
     ap.add_argument("--per-request", type=int, default=128)
     ap.add_argument("--worst-case", action="store_true")
+    ap.add_argument("--warm", type=int, default=0,
+                    help="label-correlated batches trained first (as bench.py's exact records do)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -44,6 +46,12 @@ def main():
                                device=dev, concurrent_update=mode)
         for y in range(16):
             clf.set_label(f"label{y}")
+        if a.warm:
+            wd = bench.FreshStream(native(), torch, True, args, 777, a.warm, 16, 0.6, 100000)
+            for arena in wd.batches:
+                clf.train_arena(arena, np.asarray(arena.offs, np.int64), np.asarray(arena.lens, np.int64))
+            clf.synchronize()
+            del wd
         times, upd, diag = [], [], []
         sprof = {}
         for b, arena in enumerate(data.batches):
