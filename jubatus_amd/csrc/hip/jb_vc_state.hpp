@@ -41,8 +41,10 @@ constexpr int64_t kReasonDone = 0, kReasonSaturated = 1;
 __device__ inline int64_t seg_estimate(const int64_t* st) {
   const int64_t wins = st[S_WINDOWS], stepped = st[S_STEPPED];
   const int64_t committed = st[S_BEG] - st[S_BBEG] - stepped;
+  // (a dense batch's windows commit few samples each: at least 1024 a window,
+  // or a worst-case batch would queue ~1500 empty segments for the next one)
   int64_t per = committed > 0 && wins > 0 ? committed / wins : 2048;
-  per = per < 64 ? 64 : per;
+  per = per < 1024 ? 1024 : per;
   return wins + st[S_RETRIES] + (stepped + per - 1) / per;
 }
 

