@@ -91,7 +91,8 @@ struct Geo {
   static constexpr int oLk = oStPub + 64;                              // int4 [kSR]: lk_seq, job pos, misses
   static constexpr int oJobs = oLk + kSR * 16;                         // int4 [kJR]: row, slot, previous row
   static constexpr int oDps = oJobs + kJR * 16;                        // float [kFMax][2]: a wide sample's dP
-  static constexpr int oCtl = oDps + 2 * kFMax * 4;                    // control words
+  static constexpr int oDps2 = oDps + 2 * kFMax * 4;                   // float [kFMax][2]: its P / sigma values
+  static constexpr int oCtl = oDps2 + 2 * kFMax * 4;                   // control words
   static constexpr int kBytes = oCtl + 64;
   static_assert(kBytes <= 160 * 1024, "stepper LDS");
 };
@@ -244,6 +245,9 @@ __device__ __forceinline__ float rcp_nr(float p) {
   const float r = __builtin_amdgcn_rcpf(p);
   return fmaf(r, fmaf(-p, r, 1.f), r);
 }
+__device__ __forceinline__ float4 rcp4(float4 v) {
+  return make_float4(rcp_nr(v.x), rcp_nr(v.y), rcp_nr(v.z), rcp_nr(v.w));
+}
 // jb_linear.hpp dprec with rcp_nr for the division
 __device__ __forceinline__ float dprec_nr(int method, float beta, float x, float s) {
   const float bx2 = beta * x * x;
@@ -263,6 +267,11 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                                                      int64_t* vtail) {
   using Gm = Geo<LC>;
   constexpr bool use_s = MT >= CW;
+  // AROW / NHERD: the cache holds sigma = 1 / P (converted when a row lands
+  // and when it goes back): P += b x^2 / (1 - b x^2 sigma) is then
+  // sigma -= b x^2 sigma^2 - no reciprocal in a step (CW's P += b x^2 keeps P)
+  constexpr bool kSig = MT == AROW || MT == NHERD;
+  auto to_hbm = [](float4 v) __attribute__((always_inline)) { return kSig ? rcp4(v) : v; };
   constexpr bool use_nrm = MT == PA || MT == PA1 || MT == PA2;
   constexpr int NSLOT = Gm::NSLOT, NB = Gm::NB, G = Gm::G, RPS = Gm::RPS, LPR = Gm::LPR;
   constexpr int QC = Gm::QC;
@@ -281,6 +290,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   int4* lk = reinterpret_cast<int4*>(smem + Gm::oLk);
   int4* jobs = reinterpret_cast<int4*>(smem + Gm::oJobs);
   float* dps = reinterpret_cast<float*>(smem + Gm::oDps);
+  float* dps2 = reinterpret_cast<float*>(smem + Gm::oDps2);
   int* ctl = reinterpret_cast<int*>(smem + Gm::oCtl);
 
   const int tid = threadIdx.x;
@@ -420,7 +430,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
               s = fmaf(xv[u], w[u], s);
               if (use_nrm) nq = fmaf(xv[u], xv[u], nq);
               if (use_s) {
-                inv[u] = rcp_nr(p[u]);
+                inv[u] = kSig ? p[u] : rcp_nr(p[u]);
                 vq = fmaf(xv[u] * xv[u], inv[u], vq);
               } else {
                 inv[u] = 1.f;
@@ -477,9 +487,14 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
 #pragma unroll
                 for (int u = 0; u < QC; ++u) {
                   Wc[sl[u] * LC + l] = fmaf(sg * inv[u], xv[u], w[u]);
-                  if (use_s) Pc[sl[u] * LC + l] = p[u] + dprec_nr(MT, beta, xv[u], inv[u]);
+                  if (kSig) {
+                    const float bx = beta * xv[u] * xv[u] * p[u];
+                    Pc[sl[u] * LC + l] = fmaf(-bx, p[u], p[u]);   // sigma - b x^2 sigma^2
+                  } else if (use_s) {
+                    Pc[sl[u] * LC + l] = p[u] + dprec_nr(MT, beta, xv[u], inv[u]);
+                  }
                 }
-              } else if (one) {
+              } else if (one && !kSig) {
 #pragma unroll
                 for (int u = 0; u < QC; ++u) {   // (absent features add 0 to the dummy slot)
                   atomicAdd(&Wc[sl[u] * LC + l], sg * inv[u] * xv[u]);
@@ -498,12 +513,32 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                     const int sj = j < n ? ej.x : -1;
                     if (sj < 0) continue;
                     const float x = __int_as_float(ej.y);
-                    const float iv = use_s ? rcp_nr(Pc[sj * LC + l]) : 1.f;
+                    const float pv = use_s ? Pc[sj * LC + l] : 1.f;
+                    const float iv = kSig ? pv : (use_s ? rcp_nr(pv) : 1.f);
                     atomicAdd(&Wc[sj * LC + l], sg * iv * x);
                     if (use_s) dps[2 * j + (isy ? 0 : 1)] = dprec_nr(MT, beta, x, iv);
+                    if (kSig) dps2[2 * j + (isy ? 0 : 1)] = pv;
                   }
                 }
-                if (use_s) {
+                // sigma cache, a row repeated in the sample (or wide): the
+                // precisions back as P, the increments added, sigma again -
+                // each pass reads everything before it writes
+                auto each = [&](auto&& fn) __attribute__((always_inline)) {
+                  for (int q0 = 0; q0 * G < n; q0 += QC) {
+#pragma unroll
+                    for (int u = 0; u < QC; ++u) {
+                      const int j = (q0 + u) * G + g;
+                      const int sj = j < n ? fring[(off + j) & (kFR - 1)].x : -1;
+                      if (sj >= 0) fn(sj, 2 * j + (isy ? 0 : 1));
+                    }
+                  }
+                };
+                if (kSig) {
+                  each([&](int sj, int d) { Pc[sj * LC + l] = rcp_nr(dps2[d]); });
+                  each([&](int sj, int d) { atomicAdd(&Pc[sj * LC + l], dps[d]); });
+                  each([&](int sj, int d) { dps2[d] = Pc[sj * LC + l]; });
+                  each([&](int sj, int d) { Pc[sj * LC + l] = rcp_nr(dps2[d]); });
+                } else if (use_s) {
                   for (int q0 = 0; q0 * G < n; q0 += QC) {
 #pragma unroll
                     for (int u = 0; u < QC; ++u) {
@@ -644,7 +679,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
             *reinterpret_cast<float4*>(W + (int64_t)wrow * LC + c) = *reinterpret_cast<const float4*>(Wc + sl * LC + c);
             if (use_s)
               *reinterpret_cast<float4*>(P + (int64_t)wrow * LC + c) =
-                  *reinterpret_cast<const float4*>(Pc + sl * LC + c);
+                  to_hbm(*reinterpret_cast<const float4*>(Pc + sl * LC + c));
           }
           if (touched != nullptr) touched[wrow] = 1;
         }
@@ -913,7 +948,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       if (use_s) p = lds_ld(reinterpret_cast<const float4*>(stage + b * 2048 + 1024 + 16 * lane));
       if (sl >= 0) {
         *reinterpret_cast<float4*>(Wc + sl * LC + 4 * part) = w;
-        if (use_s) *reinterpret_cast<float4*>(Pc + sl * LC + 4 * part) = p;
+        if (use_s) *reinterpret_cast<float4*>(Pc + sl * LC + 4 * part) = kSig ? rcp4(p) : p;
       }
       if (pub >= 0) publish_to(pub);
       --pend;
@@ -933,7 +968,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       const int dv = dirty[sl];
       const float4 ow = lds_ld(reinterpret_cast<const float4*>(Wc + sl * LC + 4 * part));
       float4 op = ow;
-      if (use_s) op = lds_ld(reinterpret_cast<const float4*>(Pc + sl * LC + 4 * part));
+      if (use_s) op = to_hbm(lds_ld(reinterpret_cast<const float4*>(Pc + sl * LC + 4 * part)));
       const bool dirt = on && old >= 0 && dv != 0;
       float* dw = dirt ? W + (int64_t)old * LC + 4 * part : dummy;
       float* dp = (dirt && use_s) ? P + (int64_t)old * LC + 4 * part : dummy;
@@ -994,7 +1029,8 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
     if (k < 0 || dirty[sl] == 0) continue;
     const int c = (i % Q) * 4;
     *reinterpret_cast<float4*>(W + (int64_t)k * LC + c) = *reinterpret_cast<const float4*>(Wc + sl * LC + c);
-    if (use_s) *reinterpret_cast<float4*>(P + (int64_t)k * LC + c) = *reinterpret_cast<const float4*>(Pc + sl * LC + c);
+    if (use_s)
+      *reinterpret_cast<float4*>(P + (int64_t)k * LC + c) = to_hbm(*reinterpret_cast<const float4*>(Pc + sl * LC + c));
     if (c == 0 && touched != nullptr) touched[k] = 1;
   }
   if (tid == 0 && ctl[C_ABORT] != 0 && err != nullptr) atomicMax(err, ctl[C_WHY] != 0 ? ctl[C_WHY] : 9);
