@@ -40,6 +40,7 @@ from __future__ import annotations
 import argparse
 import io
 import json
+import shlex
 import os
 import random
 import shutil
@@ -319,8 +320,12 @@ def served_train_native(args, local: int, nat, mode: str | None = None, noise_pm
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
-                          "-c", str(args.rpc_threads), "--gpu", str(local)],
+    # JB_SERVED_WRAP: a command prefix for the server process (profiling:
+    # "rocprofv3 --marker-trace --kernel-trace -d DIR -o srv --" with
+    # JUBATUS_ROCTX=1 records the server's roctx ranges)
+    wrap = shlex.split(os.environ.get("JB_SERVED_WRAP", ""))
+    p = subprocess.Popen(wrap + [srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg_path, "-d", tmp,
+                                 "-c", str(args.rpc_threads), "--gpu", str(local)],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
                          env=dict(os.environ, JUBATUS_UPDATE_MODE=mode or args.update_mode))
 
@@ -397,7 +402,7 @@ def served_train_native(args, local: int, nat, mode: str | None = None, noise_pm
     finally:
         p.terminate()
         try:
-            p.wait(timeout=30)
+            p.wait(timeout=90 if wrap else 30)
         except subprocess.TimeoutExpired:
             p.kill()
 
