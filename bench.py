@@ -918,7 +918,7 @@ def fresh_budget(fresh_gb: float, local_ranks: int) -> float:
 
 def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: int, sync,
                  mode: str = "exact", weight_dtype: str = "fp32", steps: int | None = None,
-                 hot_rows: bool = False) -> dict:
+                 hot_rows: bool = False, warmup: int | None = None) -> dict:
     """The headline protocol in another configuration: a fresh model, the
     same warmup (the exact mode: over fresh batches past the timed ones),
     then timed steps over the first fresh batches. Default: the
@@ -944,11 +944,12 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
     # timed stream), the other modes on the warm pool
     spare = fresh.batches[steps * bps:] if mode == "exact" else []
     src = spare if len(spare) >= bps else warm.batches
-    for i in range(args.warmup):
+    nwarm = args.warmup if warmup is None else warmup
+    for i in range(nwarm):
         for j in range(bps):
             run(src[(i * bps + j) % len(src)])
         sync()
-        _progress(f"{mode}/{weight_dtype}: warmup step {i + 1}/{args.warmup} done")
+        _progress(f"{mode}/{weight_dtype}: warmup step {i + 1}/{nwarm} done")
     st0 = clf.train_stats()
     sync()
     t0 = time.perf_counter()
@@ -971,6 +972,30 @@ def exact_record(args, cfg, device, warm, fresh, bps: int, samples_per_batch: in
         out["last_batch"] = clf._serial.last_batch() if getattr(clf, "_serial", None) is not None else None
     else:
         out["w_bytes"] = int(clf.W.numel() * clf.W.element_size())
+    return out
+
+
+def exact_shape_records(args, cfg, device, nat, torch, pinned, gen_threads, sync) -> dict:
+    """The serial-equivalent mode on other stream shapes: a text-like stream
+    (120 string + 8 numeric features a sample: the committer takes samples of
+    up to 32 features, wider candidates hand chunks to the stepper) and 64 /
+    256 labels (above 64 the batch runs on the single-stream kernel). Label-
+    correlated streams; 2 batches a step, one warmup step over batches the
+    timed step does not see, one timed step."""
+    out = {}
+    shapes = (("wide_128_features", {"str_features": 120, "num_features": 8, "requests": 256}),
+              ("labels_64", {"labels": 64}),
+              ("labels_256", {"labels": 256}))
+    for i, (name, over) in enumerate(shapes):
+        a = argparse.Namespace(**dict(vars(args), **over))
+        _progress(f"exact mode, {name}")
+        fs = FreshStream(nat, torch, pinned, a, 9090 + i, 4, gen_threads, 0.6, args.vocab)
+        rec = exact_record(a, cfg, device, None, fs, 2, a.requests * a.per_request, sync, mode="exact", steps=1,
+                           warmup=1)
+        rec["stream"] = {k: v for k, v in over.items() if k != "requests"}
+        rec["samples_per_batch"] = a.requests * a.per_request
+        out[name] = rec
+        del fs
     return out
 
 
@@ -1049,6 +1074,10 @@ def _summary(out: dict) -> dict:
           "exact_mode_samples_per_s": g(ex, "value"), "exact_mode_update_fraction": g(ex, "update_fraction"),
           "exact_worst_case_samples_per_s": g(ex, "worst_case", "value"),
           "exact_worst_case_stepper_samples": g(ex, "worst_case", "last_batch", "stepper_samples"),
+          "exact_wide_samples_per_s": g(ex, "shapes", "wide_128_features", "value"),
+          "exact_wide_update_fraction": g(ex, "shapes", "wide_128_features", "update_fraction"),
+          "exact_labels_64_samples_per_s": g(ex, "shapes", "labels_64", "value"),
+          "exact_labels_256_samples_per_s": g(ex, "shapes", "labels_256", "value"),
           "cpu_threads_1": g(ex, "cpu_baseline", "threads_1", "value"),
           "cpu_threads_all": g(ex, "cpu_baseline", "threads_all", "value"),
           "cpu_worst_threads_1": g(ex, "cpu_baseline", "worst_case_threads_1", "value"),
@@ -1169,6 +1198,8 @@ def main() -> None:
                     help="1 GPU: also time this many steps (16 batches each) of the headline's update "
                          "mode on the worst-case stream (noise string values: every sample updates) "
                          "and report them under worst_case")
+    ap.add_argument("--exact-shapes", type=int, default=1,
+                    help="1: exact-mode records on a text-like stream and on 64 / 256 labels")
     ap.add_argument("--cpu-baseline", type=int, default=1,
                     help="1: the in-house CPU baseline record (serial semantics on the host) beside exact_mode")
     ap.add_argument("--weight-dtype", choices=("fp32", "bf16"), default="fp32",
@@ -1440,6 +1471,8 @@ def main() -> None:
             ew["data"] = worst["data"]
             ew["batches_per_step"] = wb
             exact["worst_case"] = ew
+        if args.exact_shapes and exact is not None:
+            exact["shapes"] = exact_shape_records(args, cfg, device, nat, torch, pinned, gen_threads, sync)
         if args.cpu_baseline and exact is not None:
             _progress("cpu baseline (host serial trainer)")
             spare = fresh.batches[min(args.exact_steps, args.steps) * bps:]
