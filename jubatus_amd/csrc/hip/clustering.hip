@@ -195,6 +195,8 @@ __device__ __forceinline__ double wave_incl_scan_d(double x) {
   return x;
 }
 
+constexpr int kKppMaxM = 1024;   // draws whose uniforms the wave kernel stages in LDS
+
 // k-means++ seeding on ONE wave (n <= 64 P points): lane l owns rows
 // [l P, l P + P) - a contiguous chunk, as cl_draw's threads - with their
 // weights and distances in registers and the points in LDS, column-major
@@ -210,12 +212,17 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
                                                            int32_t* __restrict__ status) {
   static_assert(P % 4 == 0, "b128 column reads");
   extern __shared__ float s_x[];                   // [d][64 P]
+  __shared__ double s_u[kKppMaxM];                 // the draws' uniforms (a global read per draw
+                                                   // was a memory round trip on the chain)
   constexpr int NP = 64 * P;
   const int lane = threadIdx.x;
   for (int e = lane; e < NP * d; e += 64) {
     const int j = e / NP, i = e - j * NP;
     s_x[e] = i < n ? Xg[(int64_t)i * d + j] : 0.f;
   }
+  const bool u_lds = m <= kKppMaxM;
+  if (u_lds)
+    for (int j = lane; j < m; j += 64) s_u[j] = u[j];
   const int i0 = lane * P;
   float w[P], d2[P];
 #pragma unroll
@@ -273,7 +280,8 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
     for (int p = 0; p < P; ++p)
       if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
   };
-  int c = draw(w, u[0]);
+  auto uj = [&](int j) -> double { return u_lds ? s_u[j] : u[j]; };
+  int c = draw(w, uj(0));
   if (lane == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
   if (c < 0) return;
   relax(c);
@@ -281,7 +289,7 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
     float pr[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) pr[p] = d2[p] < INFINITY ? d2[p] * w[p] : 0.f;
-    c = draw(pr, u[j]);
+    c = draw(pr, uj(j));
     if (c < 0) {
       if (lane == 0) { out[j] = -1; *status = 1 + j; }
       return;

@@ -381,25 +381,49 @@ class Clustering : public HostEngine {
     uint32_t nn;
     if (!c.array(&two) || two != 2 || !c.raw(&nm, &nn)) throw std::invalid_argument("push");
     PointSet ps;
+    auto t0 = Clock::now();
     if (!convert(c.p, (size_t)(c.end - c.p), true, &ps)) throw std::invalid_argument("push: malformed points");
-    pending_.append(ps);
+    if (prof_.on) prof_.us[5] += since_us(t0);
+    t0 = Clock::now();
+    if (pending_.size() == 0) pending_ = std::move(ps);
+    else pending_.append(ps);
     while ((int64_t)pending_.size() >= p_.bucket_size) {
-      std::vector<int64_t> head((size_t)p_.bucket_size), tail(pending_.size() - (size_t)p_.bucket_size);
-      std::iota(head.begin(), head.end(), 0);
-      std::iota(tail.begin(), tail.end(), p_.bucket_size);
-      PointSet full = pending_.take(head);
-      pending_ = pending_.take(tail);
+      PointSet full;
+      if ((int64_t)pending_.size() == p_.bucket_size) {   // the common case: a whole bucket, no copies
+        full = std::move(pending_);
+        pending_ = PointSet();
+      } else {
+        std::vector<int64_t> head((size_t)p_.bucket_size), tail(pending_.size() - (size_t)p_.bucket_size);
+        std::iota(head.begin(), head.end(), 0);
+        std::iota(tail.begin(), tail.end(), p_.bucket_size);
+        full = pending_.take(head);
+        pending_ = pending_.take(tail);
+      }
+      if (prof_.on) prof_.us[6] += since_us(t0);
       close_bucket(full);
+      t0 = Clock::now();
     }
+    if (prof_.on) prof_.us[6] += since_us(t0);
     w->boolean(true);
   }
 
   // ---------------------------------------------------------- dense
   // feature keys of a set ordered by name, and those names
   void columns(const PointSet& ps, std::vector<int64_t>* keys, std::vector<std::string>* dims) {
-    std::vector<int64_t> k(ps.key);
-    std::sort(k.begin(), k.end());
-    k.erase(std::unique(k.begin(), k.end()), k.end());
+    // distinct keys: a linear scan while there are few (a bucket's points
+    // share a handful of columns), a sort past that
+    std::vector<int64_t> k;
+    bool few = true;
+    for (int64_t x : ps.key) {
+      if (std::find(k.begin(), k.end(), x) != k.end()) continue;
+      k.push_back(x);
+      if (k.size() > 32) { few = false; break; }
+    }
+    if (!few) {
+      k = ps.key;
+      std::sort(k.begin(), k.end());
+      k.erase(std::unique(k.begin(), k.end()), k.end());
+    }
     std::vector<size_t> order(k.size());
     std::iota(order.begin(), order.end(), 0);
     std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return names_[k[a]] < names_[k[b]]; });
@@ -411,6 +435,15 @@ class Clustering : public HostEngine {
   std::vector<float> dense(const PointSet& ps, const std::vector<int64_t>& keys) {
     const size_t m = ps.size(), D = keys.size();
     std::vector<float> X(m * D, 0.f);
+    if (D <= 32) {   // few columns: a linear scan beats hashing
+      for (size_t r = 0; r < m; ++r)
+        for (int64_t s = ps.rp[r]; s < ps.rp[r + 1]; ++s) {
+          const int64_t kk = ps.key[(size_t)s];
+          for (size_t j = 0; j < D; ++j)
+            if (keys[j] == kk) { X[r * D + j] += ps.val[(size_t)s]; break; }
+        }
+      return X;
+    }
     std::unordered_map<int64_t, size_t> col;
     for (size_t j = 0; j < D; ++j) col[keys[j]] = j;
     for (size_t r = 0; r < m; ++r)
@@ -551,12 +584,16 @@ class Clustering : public HostEngine {
     const size_t n = ps.size(), D = keys.size();
     const auto X = dense(ps, keys);
     std::vector<float> w(ps.w.begin(), ps.w.end());
+    auto t0 = Clock::now();
     const auto reps = kmeanspp(X, w, n, D, m, rng_);
+    if (prof_.on) prof_.us[7] += since_us(t0);
+    t0 = Clock::now();
     std::vector<float> C;
     for (int64_t r : reps) C.insert(C.end(), X.begin() + r * (int64_t)D, X.begin() + (r + 1) * (int64_t)D);
     // (X is in dX_ from the k-means++ call: its kernel path uploaded it, and
     // its host fallback's sqdist calls upload the same rows)
     const auto asg = nearest(X, n, C, reps.size(), D, true);
+    if (prof_.on) prof_.us[8] += since_us(t0);
     std::vector<float> ws(reps.size(), 0.f);
     for (size_t i = 0; i < n; ++i) ws[(size_t)asg[i]] += w[i];
     std::vector<int64_t> keep;
@@ -570,7 +607,9 @@ class Clustering : public HostEngine {
   // 50 buckets (compress, merge-compress, k-means++, Lloyd, EM)
   struct Prof {
     bool on = false;
-    double us[5] = {0, 0, 0, 0, 0};
+    // compress, merge, k-means++, Lloyd, EM; push conversion, the bucket
+    // hand-over, compress's k-means++ and nearest calls
+    double us[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     int64_t buckets = 0;
   } prof_;
   using Clock = std::chrono::steady_clock;
@@ -615,9 +654,11 @@ class Clustering : public HostEngine {
     if (prof_.on && ++prof_.buckets % 50 == 0)
       fprintf(stderr,
               "cluster prof: %lld buckets, us per bucket: compress %.1f merge %.1f kmeans++ %.1f lloyd %.1f "
-              "em %.1f\n",
+              "em %.1f convert %.1f hand-over %.1f compress.kmeans++ %.1f compress.nearest %.1f\n",
               (long long)prof_.buckets, prof_.us[0] / prof_.buckets, prof_.us[1] / prof_.buckets,
-              prof_.us[2] / prof_.buckets, prof_.us[3] / prof_.buckets, prof_.us[4] / prof_.buckets);
+              prof_.us[2] / prof_.buckets, prof_.us[3] / prof_.buckets, prof_.us[4] / prof_.buckets,
+              prof_.us[5] / prof_.buckets, prof_.us[6] / prof_.buckets, prof_.us[7] / prof_.buckets,
+              prof_.us[8] / prof_.buckets);
   }
 
   // ---------------------------------------------------------- cluster

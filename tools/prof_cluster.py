@@ -9,6 +9,7 @@ Usage: python tools/prof_cluster.py [--method gmm] [--points 200000] [--out LOG]
 import argparse
 import json
 import os
+import shlex
 import subprocess
 import sys
 import tempfile
@@ -48,7 +49,9 @@ def main():
     log = a.out or os.path.join(tmp, "server.log")
     env = dict(os.environ, JB_CLUSTER_PROF="1")
     with open(log, "w") as lf:
-        p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg, "-d", tmp, "-c", "4"],
+        # JB_SERVED_WRAP: a command prefix for the server (e.g. rocprofv3 ... --)
+        wrap = shlex.split(os.environ.get("JB_SERVED_WRAP", ""))
+        p = subprocess.Popen(wrap + [srv, "-p", str(port), "-b", "127.0.0.1", "-f", cfg, "-d", tmp, "-c", "4"],
                              stdout=lf, stderr=lf, env=env)
         try:
             deadline = time.time() + 60
@@ -68,7 +71,7 @@ def main():
                               "push_rpc_p50_us": r["p50_us"]}), flush=True)
         finally:
             p.terminate()
-            p.wait(timeout=30)
+            p.wait(timeout=90)
     with open(log) as lf:
         lines = [ln.strip() for ln in lf if "cluster prof" in ln]
     if lines:
