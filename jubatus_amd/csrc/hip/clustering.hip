@@ -299,6 +299,119 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
   }
 }
 
+// k-means++ seeding on NW waves (256 < n <= 64 NW P points): the wave
+// kernel's draw with a quarter of its rows a lane. Each draw: the lanes'
+// chunk sums scanned in double per wave (DPP), the wave totals through LDS
+// (one barrier), every thread's interval [lo, hi) of the running sum from the
+// same sequential sums (lane i's hi is lane i + 1's lo bit for bit, so at
+// most one lane holds u * total), that lane's walk over its chunk, the pick
+// through LDS (a second barrier), then every thread relaxes its rows. The
+// wave kernel's relax (P rows x d dims a lane) was ~70 % of a draw at P 16.
+template <int P, int NW>
+__global__ __launch_bounds__(NW * 64) void kmeanspp_blk_kernel(const float* __restrict__ Xg, int n, int d,
+                                                               const float* __restrict__ wg,
+                                                               const double* __restrict__ u, int m,
+                                                               int32_t* __restrict__ out,
+                                                               int32_t* __restrict__ status) {
+  static_assert(P % 4 == 0, "b128 column reads");
+  extern __shared__ float s_x[];                   // [d][NT P]
+  __shared__ double s_u[kKppMaxM];
+  __shared__ double s_tot[2][NW];
+  __shared__ int s_pick[2];
+  constexpr int NT = NW * 64, NP = NT * P;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int e = t; e < NP * d; e += NT) {
+    const int j = e / NP, i = e - j * NP;
+    s_x[e] = i < n ? Xg[(int64_t)i * d + j] : 0.f;
+  }
+  const bool u_lds = m <= kKppMaxM;
+  if (u_lds)
+    for (int j = t; j < m; j += NT) s_u[j] = u[j];
+  if (t == 0) { s_pick[0] = n - 1; s_pick[1] = n - 1; }
+  const int i0 = t * P;
+  float w[P], d2[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    w[p] = i0 + p < n ? wg[i0 + p] : 0.f;
+    d2[p] = INFINITY;
+  }
+  __syncthreads();
+  auto draw = [&](const float (&wt)[P], double uj, int j) -> int {
+    const int b = j & 1;
+    double sum = 0.0;
+#pragma unroll
+    for (int p = 0; p < P; ++p) sum += (double)wt[p];
+    const double incl = wave_incl_scan_d(sum);
+    const int phi = __shfl_up(__double2hiint(incl), 1, 64), plo = __shfl_up(__double2loint(incl), 1, 64);
+    const double excl = lane == 0 ? 0.0 : __hiloint2double(phi, plo);
+    if (lane == 63) s_tot[b][wv] = incl;
+    __syncthreads();
+    // the next draw's default (every thread has read the previous draw's pick)
+    if (t == 0) s_pick[b ^ 1] = n - 1;
+    double off = 0.0, total = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      if (q == wv) off = total;
+      total += s_tot[b][q];
+    }
+    if (!(total > 0.0)) return -1;                 // (block-uniform)
+    const double target = uj * total;
+    const double lo = off + excl, hi = off + incl;
+    if (lo <= target && target < hi) {
+      double run = lo;
+      int r = i0 + P - 1;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        run += (double)wt[p];
+        if (run > target) { r = i0 + p; break; }
+      }
+      s_pick[b] = r;
+    }
+    __syncthreads();
+    return s_pick[b];
+  };
+  auto relax = [&](int c) {
+    float acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] = 0.f;
+    for (int j = 0; j < d; ++j) {
+      const float* col = s_x + (int64_t)j * NP;
+      const float xc = col[c];
+      float v[P];
+#pragma unroll
+      for (int q = 0; q < P / 4; ++q) {
+        const float4 f = reinterpret_cast<const float4*>(col + i0)[q];
+        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+      }
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const float tt = v[p] - xc;
+        acc[p] = fmaf(tt, tt, acc[p]);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p)
+      if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
+  };
+  auto uj = [&](int j) -> double { return u_lds ? s_u[j] : u[j]; };
+  int c = draw(w, uj(0), 0);
+  if (t == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
+  if (c < 0) return;
+  relax(c);
+  for (int j = 1; j < m; ++j) {
+    float pr[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) pr[p] = d2[p] < INFINITY ? d2[p] * w[p] : 0.f;
+    c = draw(pr, uj(j), j);
+    if (c < 0) {
+      if (t == 0) { out[j] = -1; *status = 1 + j; }
+      return;
+    }
+    if (t == 0) out[j] = c;
+    relax(c);
+  }
+}
+
 // Weighted Lloyd iterations to convergence (|C' - C| <= atol + rtol |C|, as
 // torch.allclose) or `iters`, then the final assignment. C [k, d] in/out.
 __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict__ X, int n, int d,
@@ -401,6 +514,11 @@ __global__ __launch_bounds__(T) void gmm_em_kernel(const float* __restrict__ Xg,
   // staged: four barriers an iteration - (lc, 1 / var) | E-step | normalize |
   // M-step sums (nk floored where it is summed) | C, var, pi - the reads of
   // each phase follow the writes of the one before it
+  // an iteration that leaves C, var and pi bit for bit as they were is a
+  // fixed point: every later one would too (the staged loop is deterministic:
+  // no atomics), so the loop stops there with the result of all `iters`
+  __shared__ int s_moved;
+  if (t == 0) s_moved = 0;
   for (int it = 0; staged && it < iters; ++it) {
     for (int j = t; j < k; j += T) {
       float ld = 0.f;
@@ -409,6 +527,7 @@ __global__ __launch_bounds__(T) void gmm_em_kernel(const float* __restrict__ Xg,
     }
     for (int i = t; i < k * d; i += T) sIV[i] = 1.f / sV[i];
     __syncthreads();
+    if (t == 0) s_moved = 0;   // (every thread read the last iteration's flag before the barrier above)
     for (int e = t; e < n * k; e += T) {
       const int i = e / k, j = e - i * k;
       const float* x = X + (int64_t)i * d;
@@ -455,18 +574,25 @@ __global__ __launch_bounds__(T) void gmm_em_kernel(const float* __restrict__ Xg,
       }
     }
     __syncthreads();
+    bool moved = false;
     for (int i = t; i < k * d; i += T) {
       const float m = nk[i / d];
       const float c = s1[i] / m;
+      const float v = fmaxf(s2[i] / m - c * c, 1e-6f);
+      moved |= __float_as_uint(c) != __float_as_uint(sC[i]) || __float_as_uint(v) != __float_as_uint(sV[i]);
       sC[i] = c;
-      sV[i] = fmaxf(s2[i] / m - c * c, 1e-6f);
+      sV[i] = v;
     }
     if (t < k) {
       float tot = 0.f;
       for (int j = 0; j < k; ++j) tot += nk[j];
-      spi[t] = nk[t] / tot;                      // pi of the next E-step
+      const float pn = nk[t] / tot;               // pi of the next E-step
+      moved |= __float_as_uint(pn) != __float_as_uint(spi[t]);
+      spi[t] = pn;
     }
+    if (moved) s_moved = 1;
     __syncthreads();
+    if (s_moved == 0) break;                      // (block-uniform)
   }
   if (staged)
     for (int j = t; j < k; j += T) nk[j] = spi[j];
@@ -682,6 +808,25 @@ extern "C" int jb_kmeanspp(const float* X, int n, int d, const float* w, const d
     const char* e = getenv("JB_KMEANSPP_BLOCK");
     return e != nullptr && e[0] == '1';
   }();
+  // past 256 points: four waves, 4 or 8 rows a lane (JB_KMEANSPP_WAVE=1:
+  // the one-wave kernel there too, for A/B runs)
+  static const bool wave_only = [] {
+    const char* e = getenv("JB_KMEANSPP_WAVE");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (!block_only && !wave_only && n > 64 * 4 && n <= 256 * 8) {
+    const int P4 = n <= 256 * 4 ? 4 : 8;
+    const size_t xb4 = sizeof(float) * (size_t)(256 * P4) * d;
+    if (xb4 <= 64 * 1024) {
+      if (P4 == 4)
+        hipLaunchKernelGGL((jb::kmeanspp_blk_kernel<4, 4>), dim3(1), dim3(256), xb4, stream, X, n, d, w, u, m, out,
+                           status);
+      else
+        hipLaunchKernelGGL((jb::kmeanspp_blk_kernel<8, 4>), dim3(1), dim3(256), xb4, stream, X, n, d, w, u, m, out,
+                           status);
+      return (int)hipGetLastError();
+    }
+  }
   const int P = n <= 64 * 4 ? 4 : n <= 64 * 8 ? 8 : n <= 64 * 16 ? 16 : 32;
   const size_t xb = sizeof(float) * (size_t)(64 * P) * d;   // column-major, padded to 64 P rows
   if (!block_only && n <= 64 * 32 && xb <= 64 * 1024) {
