@@ -195,6 +195,31 @@ __device__ __forceinline__ double wave_incl_scan_d(double x) {
   return x;
 }
 
+// X [n][d] (row-major, global) into LDS column-major [d][np]: coalesced
+// reads, eight in flight per thread (a load-then-store loop waited a memory
+// round trip per element - ~160 of them a lane for 1000 x 10 points on one
+// wave, the bulk of a k-means++ launch)
+__device__ __forceinline__ void stage_cols(float* __restrict__ s_x, const float* __restrict__ Xg, int n, int d, int np,
+                                           int tid, int nth) {
+  const int tot = n * d;
+  for (int e0 = tid; e0 < tot; e0 += 8 * nth) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * nth;
+      v[u] = e < tot ? Xg[e] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * nth;
+      if (e < tot) {
+        const int i = e / d, j = e - i * d;
+        s_x[j * np + i] = v[u];
+      }
+    }
+  }
+}
+
 constexpr int kKppMaxM = 1024;   // draws whose uniforms the wave kernel stages in LDS
 
 // k-means++ seeding on ONE wave (n <= 64 P points): lane l owns rows
@@ -216,13 +241,17 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
                                                    // was a memory round trip on the chain)
   constexpr int NP = 64 * P;
   const int lane = threadIdx.x;
-  for (int e = lane; e < NP * d; e += 64) {
-    const int j = e / NP, i = e - j * NP;
-    s_x[e] = i < n ? Xg[(int64_t)i * d + j] : 0.f;
-  }
-  const bool u_lds = m <= kKppMaxM;
-  if (u_lds)
-    for (int j = lane; j < m; j += 64) s_u[j] = u[j];
+  stage_cols(s_x, Xg, n, d, NP, lane, 64);   // (rows past n stay unread: their d2 stays INFINITY)
+  // the draws' uniforms in LDS, kKppMaxM at a time (an LDS read per draw; a
+  // pointer select between LDS and global memory compiled to a flat load
+  // that waited on the vector memory path every draw)
+  auto stage_u = [&](int j0) {
+    __builtin_amdgcn_wave_barrier();
+    for (int j = j0 + lane; j < m && j < j0 + kKppMaxM; j += 64) s_u[j - j0] = u[j];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  };
+  stage_u(0);
   const int i0 = lane * P;
   float w[P], d2[P];
 #pragma unroll
@@ -280,7 +309,10 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
     for (int p = 0; p < P; ++p)
       if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
   };
-  auto uj = [&](int j) -> double { return u_lds ? s_u[j] : u[j]; };
+  auto uj = [&](int j) -> double {
+    if (j % kKppMaxM == 0 && j > 0) stage_u(j);
+    return s_u[j % kKppMaxM];
+  };
   int c = draw(w, uj(0));
   if (lane == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
   if (c < 0) return;
@@ -320,13 +352,8 @@ __global__ __launch_bounds__(NW * 64) void kmeanspp_blk_kernel(const float* __re
   __shared__ int s_pick[2];
   constexpr int NT = NW * 64, NP = NT * P;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int e = t; e < NP * d; e += NT) {
-    const int j = e / NP, i = e - j * NP;
-    s_x[e] = i < n ? Xg[(int64_t)i * d + j] : 0.f;
-  }
-  const bool u_lds = m <= kKppMaxM;
-  if (u_lds)
-    for (int j = t; j < m; j += NT) s_u[j] = u[j];
+  stage_cols(s_x, Xg, n, d, NP, t, NT);
+  for (int j = t; j < m && j < kKppMaxM; j += NT) s_u[j] = u[j];   // (past kKppMaxM: restaged below)
   if (t == 0) { s_pick[0] = n - 1; s_pick[1] = n - 1; }
   const int i0 = t * P;
   float w[P], d2[P];
@@ -393,7 +420,14 @@ __global__ __launch_bounds__(NW * 64) void kmeanspp_blk_kernel(const float* __re
     for (int p = 0; p < P; ++p)
       if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
   };
-  auto uj = [&](int j) -> double { return u_lds ? s_u[j] : u[j]; };
+  auto uj = [&](int j) -> double {
+    if (j % kKppMaxM == 0 && j > 0) {   // (block-uniform)
+      __syncthreads();
+      for (int i = j + t; i < m && i < j + kKppMaxM; i += NT) s_u[i - j] = u[i];
+      __syncthreads();
+    }
+    return s_u[j % kKppMaxM];
+  };
   int c = draw(w, uj(0), 0);
   if (t == 0) { out[0] = c; *status = c < 0 ? 1 : 0; }
   if (c < 0) return;
@@ -480,12 +514,16 @@ __global__ __launch_bounds__(kClBlock) void lloyd_kernel(const float* __restrict
 // C_j, var_j) + log pi_j); nk = max(sum_i r_ij, 1e-9); C = S1 / nk;
 // var = max(S2 / nk - C^2, 1e-6); pi = nk / sum nk. LDS: C, var, S1, S2
 // [k][d], nk / logdet / log pi [k].
-template <int T>
+// XL: the points and weights are staged in LDS (a compile-time choice: a
+// runtime select between LDS and global pointers compiles to flat loads,
+// which wait on the vector memory path)
+template <int T, bool XL>
 __global__ __launch_bounds__(T) void gmm_em_kernel(const float* __restrict__ Xg, int n, int d,
                                                           const float* __restrict__ wg, float* __restrict__ C,
                                                           float* __restrict__ var, float* __restrict__ pi,
                                                           int k, int iters, int32_t* __restrict__ assign,
-                                                          bool staged, bool xlds) {
+                                                          bool staged) {
+  constexpr bool xlds = XL;
   extern __shared__ float s_em[];
   float* sC = s_em;
   float* sV = sC + k * d;
@@ -760,8 +798,12 @@ extern "C" int jb_gmm_em(const float* X, int n, int d, const float* w, float* C,
   // (measured: 256 threads ran the bench's 300-point coresets in 784 us for
   // 50 iterations, 1024 threads in 341 us - the per-thread work, not the
   // barriers, sets the iteration's time)
-  hipLaunchKernelGGL((jb::gmm_em_kernel<jb::kClBlock>), dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w, C, var,
-                     pi, k, iters, assign, stage, xlds);
+  if (xlds)
+    hipLaunchKernelGGL((jb::gmm_em_kernel<jb::kClBlock, true>), dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d, w,
+                       C, var, pi, k, iters, assign, stage);
+  else
+    hipLaunchKernelGGL((jb::gmm_em_kernel<jb::kClBlock, false>), dim3(1), dim3(jb::kClBlock), lds, stream, X, n, d,
+                       w, C, var, pi, k, iters, assign, stage);
   return (int)hipGetLastError();
 }
 
@@ -782,10 +824,41 @@ __global__ __launch_bounds__(256) void argmin_rows_kernel(const float* __restric
   }
   out[i] = a;
 }
+// the same for rows of 32+ columns: one wave a row, coalesced reads, lane
+// minima (first index on ties) merged by shuffles - the first minimum of
+// the row, as the loop above (a thread a row read its k columns strided by k)
+__global__ __launch_bounds__(256) void argmin_rows_wave_kernel(const float* __restrict__ D, int64_t n, int k,
+                                                               int32_t* __restrict__ out) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const float* r = D + i * k;
+  float best = INFINITY;
+  int a = INT_MAX;
+  for (int j = lane; j < k; j += 64) {
+    const float v = r[j];
+    if (v < best || (a == INT_MAX && !(v > best))) { best = v; a = j; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oa = __shfl_xor(a, o, 64);
+    if (ob < best || (ob == best && oa < a) || (a == INT_MAX && oa != INT_MAX && !(ob > best))) {
+      best = ob;
+      a = oa;
+    }
+  }
+  if (lane == 0) out[i] = a == INT_MAX ? 0 : a;
+}
 }  // namespace jb
 
 extern "C" int jb_argmin_rows(const float* D, int64_t n, int k, int32_t* out, hipStream_t stream) {
   if (n <= 0 || k <= 0) return 0;
+  if (k >= 32) {
+    hipLaunchKernelGGL(jb::argmin_rows_wave_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, stream, D,
+                       n, k, out);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(jb::argmin_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, D, n, k,
                      out);
   return (int)hipGetLastError();
