@@ -620,6 +620,7 @@ constexpr int kMqChunk = 64 * kMqR;            // 512
 constexpr int kMqMaxK = 32;
 constexpr int kMqMaxQ = 8;
 constexpr int64_t kMqMinRows = (int64_t)2 << 20;
+constexpr int kMqBlocksMax = 511;                 // the scan's blocks (<= kMergeLists - 1 lists)
 constexpr int kMqSampT = 1024;                 // sample: threads = rows per segment
 constexpr int kMqSampSegMax = 32;              // sample: segments (16 a round of loads in flight)
 constexpr int kMqBins = 2048;                  // euclid: float bits >> 20
@@ -1361,9 +1362,19 @@ inline void launch_mq_w(const TopkSrc& s, int blocks, int nq, int q0, int64_t nr
 
 // Launches the scan stage; returns the number of blocks (= candidate lists
 // per query, each of k entries, at out + (q * blocks + b) * k), <= blocks.
+// JB_TOPK_MQ_BLOCKS: fewer scan blocks than kMqBlocksMax (A/B runs)
+inline int mq_blocks_cap() {
+  static const int v = [] {
+    const char* e = getenv("JB_TOPK_MQ_BLOCKS");
+    const int x = e != nullptr ? atoi(e) : kMqBlocksMax;
+    return x < 1 ? 1 : (x > kMqBlocksMax ? kMqBlocksMax : x);
+  }();
+  return v;
+}
+
 template <int MODE>
 inline int launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int64_t per_block,
-                       int k, float* out_d, int32_t* out_i, hipStream_t stream) {
+                       int k, float* out_d, int32_t* out_i, hipStream_t stream, int mq_lists = 0) {
   // (measured against topk_wq / topk_kernel, profiles/r5_topk_mq_ab.md: ahead
   // up to 8 queries for lsh / minhash, up to 4 for euclid_lsh, whose
   // prefilter costs a table lookup and a few FMAs per row and query)
@@ -1378,8 +1389,12 @@ inline int launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int6
     // prunes, fewer blocks than the caller sized the candidate scratch for
     // (the sample's limits live past the candidates, at out_i + nq mb k)
     constexpr int64_t kPer = (int64_t)kMqWaves * kMqChunk;
+    // (mq_lists: the candidate lists the caller's scratch holds - the mb
+    // lists plus the sample's limits must fit)
+    const int64_t room = (mq_lists > 1 ? mq_lists : blocks) - 1;
+    const int64_t cap = room < mq_blocks_cap() ? room : mq_blocks_cap();
     int64_t mb = (nrows + 4 * kPer - 1) / (4 * kPer);
-    mb = mb < 1 ? 1 : (mb > blocks - 1 ? blocks - 1 : mb);
+    mb = mb < 1 ? 1 : (mb > cap ? cap : mb);
     int64_t pb = (nrows + mb - 1) / mb;
     pb = (pb + kPer - 1) / kPer * kPer;
     mb = (nrows + pb - 1) / pb;
@@ -1510,7 +1525,7 @@ inline void launch_merge(const TopkSrc& m, int nq, int64_t nc, int k, float* out
 //   mode 1: score vector src_d [nq][nrows] (flip: distance = 1 - score)
 // out_d / out_i: [nq][k] (+inf / INT_MAX padding). scratch_d / scratch_i:
 // >= nq * jb_topk_blocks(nrows, k) * k entries each. k <= 128.
-extern "C" int jb_topk_blocks(int64_t nrows, int k) {
+static int topk_tile_blocks(int64_t nrows, int k) {
   if (k <= 0 || nrows <= 0) return 0;
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   // bound the candidates K2 merges; one block per CU is enough to stream
@@ -1526,6 +1541,16 @@ extern "C" int jb_topk_blocks(int64_t nrows, int k) {
   return (int)((tiles + tiles_per_block - 1) / tiles_per_block);
 }
 
+// candidate lists the scratch must hold per query: the tile kernels' grid,
+// or the multi-query scan's (up to jb::kMqBlocksMax blocks on tables of
+// kMqMinRows and more: two blocks a CU keep more rows in flight than one)
+extern "C" int jb_topk_blocks(int64_t nrows, int k) {
+  const int tb = topk_tile_blocks(nrows, k);
+  if (tb > 0 && nrows >= jb::kMqMinRows && k <= jb::kMqMaxK)
+    return tb > jb::kMqBlocksMax + 1 ? tb : jb::kMqBlocksMax + 1;
+  return tb;
+}
+
 extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int nq,
                        const uint64_t* tbits, const float* tnorm, const uint8_t* valid,
                        int64_t nrows, int words, int hash_num, int metric, const float* src_d,
@@ -1533,12 +1558,15 @@ extern "C" int jb_topk(int mode, const uint64_t* qbits, const float* qnorm, int 
                        int32_t* out_i, hipStream_t stream) {
   if (nq <= 0 || nrows <= 0 || k <= 0) return 0;
   if (k > jb::kTopMaxK || words > jb::kTopMaxWords || (mode != 0 && mode != 1)) return -2;
-  const int blocks = jb_topk_blocks(nrows, k);
+  const int blocks = topk_tile_blocks(nrows, k);
+  const int lists = jb_topk_blocks(nrows, k);
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, src_d, nullptr, flip};
-  const int used = mode == 0 ? jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream)
-                              : jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+  const int used = mode == 0 ? jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream,
+                                                  lists)
+                              : jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream,
+                                                  lists);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)used * k;   // candidates per query
@@ -1556,11 +1584,12 @@ static int topk_to_host_tile(const uint64_t* qbits, const float* qnorm, int nq,
                              float* scratch_d, int32_t* scratch_i, float* out_d_host,
                              int32_t* out_i_host, uint32_t* done_host, uint32_t seq,
                              hipStream_t stream) {
-  const int blocks = jb_topk_blocks(nrows, k);
+  const int blocks = topk_tile_blocks(nrows, k);
   const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
   const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
   jb::TopkSrc s{qbits, qnorm, tbits, tnorm, valid, words, hash_num, metric, nullptr, nullptr, 0};
-  const int used = jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+  const int used = jb::launch_scan<0>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream,
+                                      jb_topk_blocks(nrows, k));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   const int64_t nc = (int64_t)used * k;
@@ -2786,10 +2815,11 @@ static int topk_scores_launch(const jb::TopkSrc& s, int nq, int64_t nrows, int k
     return topk_select_launch<1>(s, nq, nrows, k, scratch_d, scratch_i, out_d_host, out_i_host,
                                  done_host, seq, stream);
   if (path == 0) {
-    const int blocks = jb_topk_blocks(nrows, k);
+    const int blocks = topk_tile_blocks(nrows, k);
     const int64_t tiles = (nrows + jb::kTopTile - 1) / jb::kTopTile;
     const int64_t per_block = ((tiles + blocks - 1) / blocks) * jb::kTopTile;
-    const int used = jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream);
+    const int used = jb::launch_scan<1>(s, blocks, nq, nrows, per_block, k, scratch_d, scratch_i, stream,
+                                        jb_topk_blocks(nrows, k));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     const int64_t nc = (int64_t)used * k;

@@ -138,7 +138,19 @@ _SIGS = {
                  _c_void_p, _c_void_p, _c_void_p],
     "jb_sqdist_mfma": [_c_void_p, _i64, _c_void_p, _i32, _i32, _c_void_p, _c_void_p, _c_void_p,
                        _c_void_p],
+    "jb_argmin_rows": [_c_void_p, _i64, _i32, _c_void_p, _c_void_p],
 }
+
+
+def argmin_rows(D: torch.Tensor) -> torch.Tensor:
+    """first minimum column of every row of D [n, k] (int32 [n]); the
+    nearest-representative step of the clustering coresets"""
+    _dev(D, torch.float32, "D")
+    n, k = D.shape
+    out = torch.empty(n, dtype=torch.int32, device=D.device)
+    rc = _fn("jb_argmin_rows")(_p(D), n, k, _p(out), _stream())
+    _check(rc, "jb_argmin_rows")
+    return out
 
 
 def sqdist(X: torch.Tensor, C: torch.Tensor) -> torch.Tensor:

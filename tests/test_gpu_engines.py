@@ -538,3 +538,16 @@ def test_direct_topk_one_launch_path(case, k, nq, metric, path):
             np.testing.assert_array_equal(oi[q][:fin.sum()], order[fin])
             np.testing.assert_allclose(od[q][:fin.sum()], ref[fin], rtol=1e-6)
             assert np.all(np.isinf(od[q][fin.sum():]))
+
+
+@pytest.mark.parametrize("n,k", [(1000, 100), (300, 7), (50, 64), (2000, 33)])
+def test_argmin_rows_first_minimum(n, k):
+    """csrc/hip/clustering.hip argmin (a thread a row below 32 columns, a
+    wave a row past that) == numpy's first minimum, ties included"""
+    import numpy as np
+    import torch
+    from jubatus_amd.ops import hip
+    rng = np.random.default_rng(n + k)
+    D = rng.integers(0, 6, size=(n, k)).astype(np.float32)   # many ties
+    got = hip.argmin_rows(torch.from_numpy(D).to(dev())).cpu().numpy()
+    assert (got == D.argmin(1)).all()
