@@ -168,6 +168,7 @@ def _thread_cpu() -> dict:
         name = st[st.index("(") + 1:st.rindex(")")]
         fields = st[st.rindex(")") + 2:].split()
         out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tck
+        out[name + ":sys"] = out.get(name + ":sys", 0.0) + int(fields[12]) / tck   # (kernel time: the TCP stack)
     return out
 
 
@@ -295,6 +296,27 @@ def _proc_cpu(pid: int) -> float:
     return (int(fields[11]) + int(fields[12])) / tck
 
 
+def _proc_thread_cpu(pid: int) -> dict:
+    """CPU seconds of a process's threads, summed by thread name (and the
+    kernel-mode part of them under "<name>:sys")"""
+    tck = os.sysconf("SC_CLK_TCK")
+    out: dict = {}
+    try:
+        tids = os.listdir(f"/proc/{pid}/task")
+    except OSError:
+        return out
+    for tid in tids:
+        try:
+            with open(f"/proc/{pid}/task/{tid}/stat") as f:
+                st = f.read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        fields = st[st.rindex(")") + 2:].split()
+        out[name] = out.get(name, 0.0) + (int(fields[11]) + int(fields[12])) / tck
+    return out
+
+
 def served_train_native(args, local: int, nat, mode: str | None = None, noise_pm: int = 0,
                         classify: bool = True) -> dict:
     """The served train path of the native server binary
@@ -366,9 +388,11 @@ def served_train_native(args, local: int, nat, mode: str | None = None, noise_pm
         subprocess.run(base + ["-t", "1.5"], capture_output=True, text=True, timeout=120)  # warmup
         st0 = status()
         cpu0 = _proc_cpu(p.pid)
+        th0 = _proc_thread_cpu(p.pid)
         r = subprocess.run(base + ["-t", str(args.rpc_seconds)], capture_output=True, text=True,
                            timeout=args.rpc_seconds + 120)
         cpu1 = _proc_cpu(p.pid)
+        th1 = _proc_thread_cpu(p.pid)
         if r.returncode != 0:
             return {"error": (r.stderr or r.stdout)[-400:]}
         lg = json.loads(r.stdout.strip().splitlines()[-1])
@@ -392,6 +416,8 @@ def served_train_native(args, local: int, nat, mode: str | None = None, noise_pm
                 "update_fraction": round(up / tr, 4) if tr else None,
                 "server_threads": args.rpc_threads,
                 "server_cpus": round((cpu1 - cpu0) / lg["seconds"], 2),
+                "server_cpus_by_thread": {k: round((v - th0.get(k, 0.0)) / lg["seconds"], 2)
+                                          for k, v in sorted(th1.items()) if v - th0.get(k, 0.0) > 0.005},
                 "classify_rpc_p50_us": cl["p50_us"], "classify_rpc_p99_us": cl["p99_us"],
                 "classify_rpc": "one datum per request, 1 connection x 1 in flight, loopback TCP",
                 "train_scan": {k[len("train_scan."):]: int(v) for k, v in st1.items()

@@ -2190,10 +2190,26 @@ class Server {
   std::string ident() const { return a_.eth + "_" + std::to_string(a_.port); }
 
   std::vector<std::string> arena(int slot, const std::vector<jb::ArenaReq>& reqs) {
+    // JB_RPC_NULL_TRAIN=1 (measurement only): answer every train request of
+    // the batch without training - the RPC layer's own ceiling (loopback TCP,
+    // framing, the copies into the arena) at the same load (tools/rpc_ceiling.py)
+    static const bool null_train = [] {
+      const char* e = getenv("JB_RPC_NULL_TRAIN");
+      return e != nullptr && e[0] == '1';
+    }();
+    std::vector<std::string> out(reqs.size());
+    if (null_train) {
+      rpc_->release_slot(slot);
+      for (size_t k = 0; k < reqs.size(); ++k) {
+        MsgpackWriter w;
+        w.uint(0);
+        out[k] = jb::val::response_ok(reqs[k].msgid, w.out);
+      }
+      return out;
+    }
     if (mixer_) mixer_->updated(reqs.size());
     std::vector<int64_t> res;
     std::vector<std::string> msgs;
-    std::vector<std::string> out(reqs.size());
     try {
       clf_->train_arena(slots_[slot], reqs, &res, &msgs);
     } catch (const std::exception& e) {
