@@ -60,7 +60,7 @@ constexpr int kNMask = 0x3fff;      // header word z: (y + 1) << 16 | dup bit | 
 constexpr int kDupBit = 0x8000;
 constexpr int kK = 8;               // fetch stages in flight
 constexpr int kC = 5;               // VMEM instructions per stage (see issue_stage)
-constexpr int kSlotBytes = 98304;   // the W / P row cache
+constexpr int kSlotBytes = vc::kSpSlotBytes;   // the W / P row cache
 constexpr int kJR = 512;            // fetch job ring (power of two, >= kFMax + 64)
 constexpr int64_t kTimeout = 200000000;   // 2 s of s_memrealtime (100 MHz)
 
@@ -68,8 +68,7 @@ template <int LC>
 struct Geo {
   static_assert(LC >= 8 && LC <= 64, "stepper: 8 <= LC <= 64");
   static constexpr int G = 64 / LC;                                    // feature groups of a step
-  static constexpr int NSLOT0 = kSlotBytes / (8 * LC);
-  static constexpr int NSLOT = NSLOT0 > 1024 ? 1024 : NSLOT0;
+  static constexpr int NSLOT = vc::sp_nslot(LC);
   static constexpr int NB = NSLOT / 4;                                 // 4-way buckets
   static constexpr int RPS = 256 / LC;                                 // rows per fetch stage
   static constexpr int LPR = 64 / RPS;                                 // lanes per row (16 B of W, 16 B of P)
@@ -92,13 +91,19 @@ struct Geo {
   static constexpr int oJobs = oLk + kSR * 16;                         // int4 [kJR]: row, slot, previous row
   static constexpr int oDps = oJobs + kJR * 16;                        // float [kFMax][2]: a wide sample's dP
   static constexpr int oDps2 = oDps + 2 * kFMax * 4;                   // float [kFMax][2]: its P / sigma values
-  static constexpr int oCtl = oDps2 + 2 * kFMax * 4;                   // control words
+  static constexpr int oRmx = oDps2 + 2 * kFMax * 4;                   // float [NSLOT + 4]: rows' step bounds (CS)
+  static constexpr int oCtl = oRmx + (NSLOT + 4) * 4;                  // control words
   static constexpr int kBytes = oCtl + 64;
   static_assert(kBytes <= 160 * 1024, "stepper LDS");
 };
 
 // control words (int [16] at oCtl)
-enum : int { C_PROGRESS = 0, C_ABORT = 1, C_WHY = 2, C_JDONE = 3 };
+// C_STOP: the first sample not taken (candidate mode: the cache cannot pin
+// another updated row - the window ends there)
+enum : int { C_PROGRESS = 0, C_ABORT = 1, C_WHY = 2, C_JDONE = 3, C_STOP = 4, C_NUPD = 5 };
+// launch modes: a range (single stream), a chunk after a dense window, the
+// candidates of a verified-committer window (vcommit.hip, kernel C's place)
+enum : int { kModeRange = 0, kModeChunk = 1, kModeCand = 2 };
 // abort reasons (stats[2] when non-zero)
 enum : int { kErrTimeoutStep = 1, kErrTimeoutLoad = 2, kErrTimeoutMeta = 3, kErrTimeoutFetch = 4 };
 
@@ -158,16 +163,7 @@ __device__ __forceinline__ void lds_st(T* p, T v) {
   asm volatile("" ::: "memory");
 }
 
-__device__ __forceinline__ void buckets(int row, int NB, int* b1, int* b2) {
-  const uint32_t h1 = (uint32_t)row * 0x9E3779B1u;
-  uint32_t h2 = ((uint32_t)row ^ 0x5bd1e995u) * 0x85EBCA77u;
-  h2 ^= h2 >> 13;
-  h2 *= 0xC2B2AE35u;
-  *b1 = (int)__umulhi(h1, (uint32_t)NB);
-  int c = (int)__umulhi(h2, (uint32_t)NB);
-  if (c == *b1) c = c + 1 == NB ? 0 : c + 1;
-  *b2 = c;
-}
+__device__ __forceinline__ void buckets(int row, int NB, int* b1, int* b2) { vc::sp_buckets(row, NB, b1, b2); }
 __device__ __forceinline__ int find_in(const int* key, int b1, int b2, int row) {
   const int4 k1 = lds_ld(reinterpret_cast<const int4*>(key + 4 * b1));
   const int4 k2 = lds_ld(reinterpret_cast<const int4*>(key + 4 * b2));
@@ -264,7 +260,9 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                                                      unsigned long long* __restrict__ stats,
                                                      uint8_t* __restrict__ touched, int* __restrict__ err,
                                                      unsigned long long* __restrict__ prof, int64_t* vst,
-                                                     int64_t* vtail) {
+                                                     int64_t* vtail, int mode, const int4* __restrict__ aux,
+                                                     int32_t* __restrict__ g_key, float* __restrict__ g_rmax,
+                                                     float* __restrict__ g_dw, float* __restrict__ g_dp) {
   using Gm = Geo<LC>;
   constexpr bool use_s = MT >= CW;
   // AROW / NHERD: the cache holds sigma = 1 / P (converted when a row lands
@@ -291,6 +289,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   int4* jobs = reinterpret_cast<int4*>(smem + Gm::oJobs);
   float* dps = reinterpret_cast<float*>(smem + Gm::oDps);
   float* dps2 = reinterpret_cast<float*>(smem + Gm::oDps2);
+  float* rmx = reinterpret_cast<float*>(smem + Gm::oRmx);
   int* ctl = reinterpret_cast<int*>(smem + Gm::oCtl);
 
   const int tid = threadIdx.x;
@@ -298,8 +297,16 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   const int wave = tid >> 6;
   // vst (a verified committer's state, vcommit.hip): a chunk after an
   // update-dense window - nothing to do unless the committer stopped dense
+  // kModeCand: the window's candidates (kernel B's records, in order) from
+  // the model at the window's start; nothing is written to W / P
+  const bool cs = mode == kModeCand;
   int64_t beg, end;
-  if (vst != nullptr) {
+  if (cs) {
+    const int stv = (int)vst[vc::S_STATUS];
+    if (!(stv == vc::kNew || stv == vc::kRetry) || vst[vc::S_CSMODE] != 1) return;
+    beg = vst[vc::S_BEG];
+    end = beg + vst[vc::S_NCAND];    // (N candidates; sample t is beg + aux[t].w)
+  } else if (vst != nullptr) {
     if (vst[vc::S_STATUS] != vc::kDense) return;
     beg = vst[vc::S_BEG];
     end = min(vst[vc::S_BEND], beg + vst[vc::S_DCHUNK]);
@@ -309,12 +316,14 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   }
   if (end <= beg && vst == nullptr) return;
   const int N = (int)(end > beg ? end - beg : 0);
+  auto sidx = [&](int t) __attribute__((always_inline)) -> int64_t { return cs ? beg + aux[t].w : beg + t; };
 
   // ---- init (all waves)
   for (int i = tid; i < NSLOT + 4; i += kT) {
     key[i] = -1;
     use[i] = -1;
     dirty[i] = 0;
+    rmx[i] = 0.f;
   }
   for (int i = tid; i < (NSLOT + 1) * LC; i += kT) {   // empty slots hold the initial model
     Wc[i] = 0.f;
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
     hdr[i] = make_int4(-1, -1, 0, 0);
     lk[i] = make_int4(-1, 0, 0, 0);
   }
-  if (tid < 16) ctl[tid] = 0;
+  if (tid < 16) ctl[tid] = tid == C_STOP ? N : 0;
   __syncthreads();
   // phase cycles of this wave (prof != nullptr only)
   unsigned long long pc[P_NWORDS];
@@ -376,6 +385,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           __builtin_amdgcn_s_sleep(1);
           hd = lds_ld(&hdr[t & (kSR - 1)]);
           if (hd.y == t) break;
+          if (cs && lds_ld(&ctl[C_STOP]) <= t) { dead = true; break; }   // the window ends before t
           if (lds_ld(&ctl[C_ABORT]) != 0 || timed_out(t0)) { abort_with(kErrTimeoutStep); dead = true; break; }
         }
         pc[P_STEP_WAIT] += clk() - w0;
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         if (n < 0) {
           // a sample the cache does not hold: on HBM (the loader wrote back
           // and dropped its rows), drained before the progress word moves
-          const int64_t s = beg + t;
+          const int64_t s = sidx(t);
           const int64_t rb = row_ptr[s];
           const bool ak[1] = {act};
           if (general_sample<LC, kAtomic, float>(fidx, fval, rb, (int)(row_ptr[s + 1] - rb), y, W, P, ak, lane, MT,
@@ -478,6 +488,23 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
           pc[P_ST_COEF] += s3 - s2;
           if (upd) {
             ++n_upd;
+            if (cs && one && !(kSig && dup)) {   // (kSig repeats: the wide loops below)
+              // candidate mode: the step's bound on every row it writes (for
+              // kernel D) - the larger |dW| of its two labels, the best wrong
+              // label's from its lane by a permute - added to the row's rmax;
+              // the row stays pinned in the cache until the window is staged
+              const float sgl = l == y ? tau : -tau;
+              const int src = g * LC + (bl >= 0 ? bl : y);
+#pragma unroll
+              for (int u = 0; u < QC; ++u) {
+                const float a = fabsf(sgl * inv[u] * xv[u]);
+                const float b = __shfl(a, src, 64);
+                if (l == y) {
+                  atomicAdd(&rmx[sl[u]], bl >= 0 ? fmaxf(a, b) : a);
+                  dirty[sl[u]] = 1;
+                }
+              }
+            }
             const bool isy = l == y, isl = l == bl;
             if (isy || isl) {
               const float sg = isy ? tau : -tau;
@@ -518,6 +545,10 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
                     atomicAdd(&Wc[sj * LC + l], sg * iv * x);
                     if (use_s) dps[2 * j + (isy ? 0 : 1)] = dprec_nr(MT, beta, x, iv);
                     if (kSig) dps2[2 * j + (isy ? 0 : 1)] = pv;
+                    if (cs) {   // (wide: both labels' |dW| summed - an upper bound of their max)
+                      atomicAdd(&rmx[sj], fabsf(sg * iv * x));
+                      if (isy) dirty[sj] = 1;
+                    }
                   }
                 }
                 // sigma cache, a row repeated in the sample (or wide): the
@@ -556,7 +587,9 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       if (lane == 0) lds_st(&ctl[C_PROGRESS], t + 1);
       if (s3 != 0) pc[P_ST_APPLY] += clk() - s3;
     }
-    if (lane == 0 && stats != nullptr) {
+    if (cs) {
+      if (lane == 0) lds_st(&ctl[C_NUPD], (int)n_upd);   // (kernel D counts a committed window's updates)
+    } else if (lane == 0 && stats != nullptr) {
       if (n_upd) atomicAdd(stats, (unsigned long long)n_upd);
       if (n_valid) atomicAdd(stats + 1, (unsigned long long)n_valid);
     }
@@ -572,9 +605,10 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       int64_t rp0 = 0, rp1 = 0;
       int y = -1;
       if (in) {
-        rp0 = row_ptr[beg + t];
-        rp1 = row_ptr[beg + t + 1];
-        y = labels[beg + t];
+        const int64_t si = sidx(t);
+        rp0 = row_ptr[si];
+        rp1 = row_ptr[si + 1];
+        y = labels[si];
       }
       const int n = (int)(rp1 - rp0);
       const bool vy = in && y >= 0 && y < LC;
@@ -600,6 +634,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         const int prog = lds_ld(&ctl[C_PROGRESS]);
         const int cons = prog > 0 ? lds_ld(&fend[(prog - 1) & (kSR - 1)]) : 0;
         if (t0 + cnt < prog + kSR && head + total - cons <= kFR) break;
+        if (cs && lds_ld(&ctl[C_STOP]) < N) { dead = true; break; }   // the window ended: no more headers
         if (lds_ld(&ctl[C_ABORT]) != 0 || timed_out(tw)) { abort_with(kErrTimeoutMeta); dead = true; break; }
         __builtin_amdgcn_s_sleep(2);
       }
@@ -697,7 +732,7 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
         drop(jb.y, jb.z);
       }
       jhead = jpos0;
-      const int64_t s = beg + t;
+      const int64_t s = sidx(t);
       const int64_t rb = row_ptr[s];
       const int n = y >= 0 ? (int)(row_ptr[s + 1] - rb) : 0;
       for (int j0 = 0; j0 < n; j0 += 64) {
@@ -759,6 +794,10 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       const int y0 = (h0.z >> 16) - 1;
       const int n0 = (h0.z & kNMask) - 1;
       if (y0 >= 0 && n0 < 0) {
+        if (cs) {   // (candidate mode writes no HBM rows: the window ends before t)
+          if (lane == 0) lds_st(&ctl[C_STOP], t);
+          break;
+        }
         pc[P_DIRECT] += 1;
         go_direct(t, y0, jhead);
         ++t;
@@ -840,19 +879,25 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
             if (need) {
               const int4 u1 = lds_ld(reinterpret_cast<const int4*>(use + 4 * b1));
               const int4 u2 = lds_ld(reinterpret_cast<const int4*>(use + 4 * b2));
+              // (candidate mode: a way holding an updated row stays pinned)
+              int4 d1 = make_int4(0, 0, 0, 0), d2 = d1;
+              if (cs) {
+                d1 = lds_ld(reinterpret_cast<const int4*>(dirty + 4 * b1));
+                d2 = lds_ld(reinterpret_cast<const int4*>(dirty + 4 * b2));
+              }
               int v = -1, vu = 0x7fffffff;
-              auto cand = [&](int s, int k, int u) {
+              auto cand = [&](int s, int k, int u, int dv) {
                 const int score = k < 0 ? -2 : u;   // an empty way first, else the least recently used
-                if ((k < 0 || u < prog) && score < vu) { v = s; vu = score; vk = k; }
+                if ((k < 0 || (u < prog && dv == 0)) && score < vu) { v = s; vu = score; vk = k; }
               };
-              cand(4 * b1, k1.x, u1.x);
-              cand(4 * b1 + 1, k1.y, u1.y);
-              cand(4 * b1 + 2, k1.z, u1.z);
-              cand(4 * b1 + 3, k1.w, u1.w);
-              cand(4 * b2, k2.x, u2.x);
-              cand(4 * b2 + 1, k2.y, u2.y);
-              cand(4 * b2 + 2, k2.z, u2.z);
-              cand(4 * b2 + 3, k2.w, u2.w);
+              cand(4 * b1, k1.x, u1.x, d1.x);
+              cand(4 * b1 + 1, k1.y, u1.y, d1.y);
+              cand(4 * b1 + 2, k1.z, u1.z, d1.z);
+              cand(4 * b1 + 3, k1.w, u1.w, d1.w);
+              cand(4 * b2, k2.x, u2.x, d2.x);
+              cand(4 * b2 + 1, k2.y, u2.y, d2.y);
+              cand(4 * b2 + 2, k2.z, u2.z, d2.z);
+              cand(4 * b2 + 3, k2.w, u2.w, d2.w);
               if (v >= 0) {
                 if (atomicCAS(&key[v], vk, row) == vk) {
                   atomicMax(&use[v], tk);
@@ -897,6 +942,10 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       pc[P_LOAD_LOOKUP] += clk() - l0;
       if (dead) break;
       if (overflow) {
+        if (cs) {   // the cache cannot pin another updated row: the window ends before t
+          if (lane == 0) lds_st(&ctl[C_STOP], t);
+          break;
+        }
         pc[P_DIRECT] += 1;
         go_direct(t, y0, jpos0);
         ++t;
@@ -976,7 +1025,12 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
       *reinterpret_cast<float4*>(dw) = ow;
       *reinterpret_cast<float4*>(dp) = op;
       *dt = 1;
-      if (on && part == 0) dirty[sl] = 1;   // every cached row goes back when evicted
+      // every cached row goes back when evicted; candidate mode: only rows the
+      // stepper updated count (and those are never evicted), with their bound
+      if (on && part == 0) {
+        dirty[sl] = cs ? 0 : 1;
+        if (cs) rmx[sl] = 0.f;
+      }
       const float* sw = on ? W + (int64_t)row * LC + 4 * part : dummy;
       const float* sp = (on && use_s) ? P + (int64_t)row * LC + 4 * part : dummy;
       const uint32_t lb = __builtin_amdgcn_readfirstlane(lds_addr(stage + b * 2048));
@@ -990,10 +1044,12 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
 
     int t = 0;
     uint64_t tw = __builtin_amdgcn_s_memrealtime();
-    while ((t < N || pend > 0) && !dead) {
+    while (!dead) {
+      const int Ne = cs ? min(N, lds_ld(&ctl[C_STOP])) : N;   // (candidate mode: up to the window's end)
+      if (!(t < Ne || pend > 0)) break;
       int4 lkv = make_int4(-1, 0, 0, 0);
-      if (t < N) lkv = lds_ld(&lk[t & (kSR - 1)]);
-      if (t >= N || lkv.x != t) {
+      if (t < Ne) lkv = lds_ld(&lk[t & (kSR - 1)]);
+      if (t >= Ne || lkv.x != t) {
         if (pend > 0) {
           retire();
         } else {
@@ -1023,18 +1079,61 @@ __global__ __launch_bounds__(kT) void stepper_kernel(const int64_t* __restrict__
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   constexpr int Q = LC / 4;
-  for (int i = tid; i < NSLOT * Q; i += kT) {
-    const int sl = i / Q;
-    const int k = key[sl];
-    if (k < 0 || dirty[sl] == 0) continue;
-    const int c = (i % Q) * 4;
-    *reinterpret_cast<float4*>(W + (int64_t)k * LC + c) = *reinterpret_cast<const float4*>(Wc + sl * LC + c);
-    if (use_s)
-      *reinterpret_cast<float4*>(P + (int64_t)k * LC + c) = to_hbm(*reinterpret_cast<const float4*>(Pc + sl * LC + c));
-    if (c == 0 && touched != nullptr) touched[k] = 1;
+  if (cs) {
+    // candidate mode: the window's updated rows staged as kernel C stages its
+    // store - keys and rmax in this cache's slot layout (kernel D looks rows
+    // up with vc::sp_find), the deltas to the model at the window's start
+    constexpr int NSD = 16384 / (LC > 16 ? LC : 16);   // kernel D's table (jb_commit.hpp dc::Geo NSLOT)
+    static_assert(NSLOT <= NSD, "the staged table holds the cache");
+    for (int i = tid; i < NSD; i += kT) {
+      const bool on = i < NSLOT && key[i] >= 0 && dirty[i] != 0;
+      g_key[i] = on ? key[i] : -1;
+      g_rmax[i] = on ? rmx[i] : 0.f;
+    }
+    for (int i = tid; i < NSLOT * Q; i += kT) {
+      const int sl = i / Q;
+      const int k = key[sl];
+      if (k < 0 || dirty[sl] == 0) continue;
+      const int c = (i % Q) * 4;
+      const float4 w0 = *reinterpret_cast<const float4*>(W + (int64_t)k * LC + c);
+      const float4 wn = *reinterpret_cast<const float4*>(Wc + sl * LC + c);
+      *reinterpret_cast<float4*>(g_dw + sl * LC + c) =
+          make_float4(wn.x - w0.x, wn.y - w0.y, wn.z - w0.z, wn.w - w0.w);
+      if (use_s) {
+        const float4 p0 = *reinterpret_cast<const float4*>(P + (int64_t)k * LC + c);
+        const float4 pn = to_hbm(*reinterpret_cast<const float4*>(Pc + sl * LC + c));
+        *reinterpret_cast<float4*>(g_dp + sl * LC + c) =
+            make_float4(pn.x - p0.x, pn.y - p0.y, pn.z - p0.z, pn.w - p0.w);
+      }
+    }
+    if (tid == 0) {
+      const int stop = ctl[C_STOP];
+      const bool stopped = stop < N;
+      int nsl = 0;
+      for (int i = 0; i < NSLOT; ++i) nsl += (key[i] >= 0 && dirty[i] != 0) ? 1 : 0;
+      vst[vc::S_PEND] = stopped ? beg + aux[stop].w : vst[vc::S_WEND];
+      vst[vc::S_WHY] = stopped ? vc::kWhySat : vc::kWhyEnd;
+      vst[vc::S_NUPD] = ctl[C_NUPD];
+      vst[vc::S_NSLOTS] = nsl;
+      vst[vc::S_STEPS] += stopped ? stop : N;
+      vst[vc::S_CAND] += N;
+      vst[vc::S_CSN] += 1;
+    }
+  } else {
+    for (int i = tid; i < NSLOT * Q; i += kT) {
+      const int sl = i / Q;
+      const int k = key[sl];
+      if (k < 0 || dirty[sl] == 0) continue;
+      const int c = (i % Q) * 4;
+      *reinterpret_cast<float4*>(W + (int64_t)k * LC + c) = *reinterpret_cast<const float4*>(Wc + sl * LC + c);
+      if (use_s)
+        *reinterpret_cast<float4*>(P + (int64_t)k * LC + c) =
+            to_hbm(*reinterpret_cast<const float4*>(Pc + sl * LC + c));
+      if (c == 0 && touched != nullptr) touched[k] = 1;
+    }
   }
   if (tid == 0 && ctl[C_ABORT] != 0 && err != nullptr) atomicMax(err, ctl[C_WHY] != 0 ? ctl[C_WHY] : 9);
-  if (tid == 0 && vst != nullptr) {
+  if (tid == 0 && mode == kModeChunk) {
     // the batch back to the committer from the chunk's end
     const int64_t bend = vst[vc::S_BEND];
     const bool done = end >= bend;
@@ -1109,7 +1208,9 @@ extern "C" int jb_stepper_enabled() {
 static int stepper_launch(const int64_t* row_ptr, const int32_t* fidx, const float* fval, const int32_t* labels,
                           const int64_t* range, float* W, float* P, const int32_t* active, int LC, int method,
                           float C, unsigned long long* stats, uint8_t* touched, int* err, int64_t* vst,
-                          int64_t* vtail, hipStream_t stream) {
+                          int64_t* vtail, hipStream_t stream, int mode = jb::sp::kModeRange,
+                          const int4* aux = nullptr, int32_t* g_key = nullptr, float* g_rmax = nullptr,
+                          float* g_dw = nullptr, float* g_dp = nullptr) {
   if (LC < 8 || LC > 64) return -1;
   if (method >= jb::CW && P == nullptr) return -4;
   if (err == nullptr) {
@@ -1137,7 +1238,7 @@ static int stepper_launch(const int64_t* row_ptr, const int32_t* fidx, const flo
     (void)attr;                                                                                               \
     hipLaunchKernelGGL((jb::sp::stepper_kernel<L, M, PR>), dim3(1), dim3(jb::sp::kT), jb::sp::Geo<L>::kBytes, \
                        stream, row_ptr, fidx, fval, labels, range, W, P, active, C, stats, touched, err, prof,     \
-                       vst, vtail);                                                                          \
+                       vst, vtail, mode, aux, g_key, g_rmax, g_dw, g_dp);                                    \
   }
   // the phase counters are compiled into the label-capacity 8 and 16 kernels only
 #define JB_SP_LAUNCH(L, M)                                   \
@@ -1190,5 +1291,20 @@ extern "C" int jb_stepper_chunk(const int64_t* row_ptr, const int32_t* fidx, con
                                 hipStream_t stream) {
   if (vst == nullptr || vtail == nullptr) return -2;
   return stepper_launch(row_ptr, fidx, fval, labels, nullptr, W, P, active, LC, method, C, stats, touched, nullptr,
-                        vst, vtail, stream);
+                        vst, vtail, stream, jb::sp::kModeChunk);
+}
+
+// The candidates of a verified-committer window (vcommit.hip, in kernel C's
+// place when kernel B set S_CSMODE): [0, S_NCAND) in order, sample
+// S_BEG + aux[k].w, from the model at the window's start; the updated rows
+// staged into (g_key, g_rmax, g_dw, g_dp) as kernel C stages its store, the
+// stop position / updates into the state words; W / P untouched. An empty
+// launch unless the window is live and in candidate mode.
+extern "C" int jb_stepper_cand(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                               const int32_t* labels, float* W, float* P, const int32_t* active, int LC, int method,
+                               float C, int64_t* vst, const int4* aux, int32_t* g_key, float* g_rmax, float* g_dw,
+                               float* g_dp, hipStream_t stream) {
+  if (vst == nullptr || aux == nullptr || g_key == nullptr) return -2;
+  return stepper_launch(row_ptr, fidx, fval, labels, nullptr, W, P, active, LC, method, C, nullptr, nullptr, nullptr,
+                        vst, nullptr, stream, jb::sp::kModeCand, aux, g_key, g_rmax, g_dw, g_dp);
 }

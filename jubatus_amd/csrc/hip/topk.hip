@@ -1451,7 +1451,23 @@ __global__ __launch_bounds__(kMergeStageT) void topk_merge_sorted_kernel(const f
   const int n = nb * k;
   const float* src_d = cd + (int64_t)q * n;
   const int32_t* src_i = ci + (int64_t)q * n;
-  for (int e = threadIdx.x; e < n; e += kMergeStageT) { s_d[e] = src_d[e]; s_i[e] = src_i[e]; }
+  // (eight loads a thread in flight: one load-then-store a trip waited a
+  // memory round trip each, most of this kernel's time)
+  for (int e0 = threadIdx.x; e0 < n; e0 += 8 * kMergeStageT) {
+    float vd[8];
+    int vi[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * kMergeStageT;
+      vd[u] = e < n ? src_d[e] : 0.f;
+      vi[u] = e < n ? src_i[e] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * kMergeStageT;
+      if (e < n) { s_d[e] = vd[u]; s_i[e] = vi[u]; }
+    }
+  }
   __syncthreads();
   if (threadIdx.x >= 64) return;                  // the merge is one wave's
   int pos[L];

@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
     const float* __restrict__ fval, const int32_t* __restrict__ labels, const float* __restrict__ W,
     const float* __restrict__ P, const int32_t* __restrict__ active, int method, float C,
     const unsigned long long* __restrict__ bits, float* __restrict__ S0, int4* __restrict__ AUX,
-    float2* __restrict__ PP0, int32_t* __restrict__ FI, float* __restrict__ FX) {
+    float2* __restrict__ PP0, int32_t* __restrict__ FI, float* __restrict__ FX, int cs_min) {
   using L = Lanes<LC>;
   if (!live((int)st[S_STATUS])) return;
   __shared__ int s_pref[kBitWords + 1];
@@ -322,6 +322,8 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
   if (blockIdx.x == 0 && tid == 0) {
     st[S_NCAND] = ncand;
     st[S_WEND] = we;
+    // enough candidates: the stepper walks them (stepper.hip, candidate mode)
+    st[S_CSMODE] = (cs_min > 0 && ncand >= cs_min) ? 1 : 0;
   }
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int g = lane / L::LW;
@@ -432,6 +434,7 @@ __global__ __launch_bounds__(64) void vc_commit_kernel(
   constexpr bool use_nrm = MT == PA || MT == PA1 || MT == PA2 || MT == CW;
   constexpr float kG = dc::kGuard;
   if (!live((int)st[S_STATUS])) return;
+  if (st[S_CSMODE] == 1) return;   // (the stepper walks this window's candidates)
   if ((st[S_WIDE] != 0) != (FC_ == 2)) return;
   __shared__ __attribute__((aligned(16))) float s_dw[NSLOT * LC + Gm::PAD];
   __shared__ __attribute__((aligned(16))) float s_dp[use_s ? NSLOT * LC + Gm::PAD : 4];
@@ -922,6 +925,7 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
   if (tid == 0) { s_valid = 0; s_viol = 0; }
   __syncthreads();
   const int64_t wb = st[S_BEG], pe = st[S_PEND];
+  const bool cs_mode = st[S_CSMODE] == 1;
   unsigned nvalid = 0, nviol = 0, nnonc = 0;
   for (int64_t i = wb + (int64_t)blockIdx.x * blockDim.x + tid; i < pe; i += (int64_t)gridDim.x * blockDim.x) {
     const int y = labels[i];
@@ -935,7 +939,8 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
     for (int64_t j = row_ptr[i]; j < row_ptr[i + 1]; ++j) {
       const int32_t row = fidx[j];
       if (row < 0) continue;
-      const int s = dc::cache_find<LC>(s_key, row);
+      // (the store's layout: kernel C's, or the stepper cache's in candidate mode)
+      const int s = cs_mode ? sp_find(s_key, sp_nslot(LC) / 4, row) : dc::cache_find<LC>(s_key, row);
       if (s >= 0) bound += fabsf(fval[j]) * s_rmax[s];
     }
     bound *= 2.f * (1.f + 4.f * kG);
@@ -1080,6 +1085,7 @@ __global__ __launch_bounds__(256) void vc_verify_kernel(
     tail[kTailStepped] = st[S_STEPPED];
     tail[kTailChunks] = st[S_NCHUNK];
     tail[kTailSegEst] = seg_estimate(st);
+    tail[kTailCsWindows] = st[S_CSN];
     tail[22] = st[S_WASTED];
     tail[23] = st[S_REFRESH];
     tail[24] = st[S_UPD];
@@ -1111,13 +1117,18 @@ extern "C" int jb_stepper_chunk(const int64_t* row_ptr, const int32_t* fidx, con
                                 float* W, float* P, const int32_t* active, int LC, int method, float C,
                                 unsigned long long* stats, uint8_t* touched, int64_t* vst, int64_t* vtail,
                                 hipStream_t stream);
+extern "C" int jb_stepper_cand(const int64_t* row_ptr, const int32_t* fidx, const float* fval,
+                               const int32_t* labels, float* W, float* P, const int32_t* active, int LC, int method,
+                               float C, int64_t* vst, const int4* aux, int32_t* g_key, float* g_rmax, float* g_dw,
+                               float* g_dp, hipStream_t stream);
 
 template <int L>
 static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, const float* fval,
                      const int32_t* labels, float* W, float* S, const int32_t* active, float C, int64_t* st,
                      float* sl, unsigned long long* bits, float* s0, int4* aux, float2* pp0, int32_t* fi,
                      float* fx, int32_t* gk, float* gr, float* gdw, float* gdp, uint8_t* touched,
-                     unsigned long long* stats, int64_t* tail, int nseg, bool chunks, hipStream_t stream) {
+                     unsigned long long* stats, int64_t* tail, int nseg, bool chunks, int cs_min,
+                     hipStream_t stream) {
   using namespace jb::vc;
   static const int prof = [] {
     const char* e = getenv("JB_COMMIT_PROF");
@@ -1140,7 +1151,7 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
     hipLaunchKernelGGL((vc_score_kernel<L>), dim3(1024), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        W, active, method, C, sl, bits, gk, gr);
     hipLaunchKernelGGL((vc_gather_kernel<L>), dim3(512), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
-                       W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx);
+                       W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx, cs_min);
 #define JB_VC_S(M, R, PD)                                                                                       \
   hipLaunchKernelGGL((vc_commit_kernel<L, M, R, PD, 1>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, \
                      aux, pp0, fi, fx, gk, gr, gdw, gdp, prof);                                                  \
@@ -1162,6 +1173,12 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
     }
 #undef JB_VC_M
 #undef JB_VC_S
+    // candidate mode (kernel B's choice): the stepper walks the candidates
+    if (cs_min > 0) {
+      const int rc = jb_stepper_cand(row_ptr, fidx, fval, labels, W, Pp, active, L, method, C, st, aux, gk, gr, gdw,
+                                     gdp, stream);
+      if (rc != 0) return rc;
+    }
     hipLaunchKernelGGL((vc_verify_kernel<L>), dim3(256), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        sl, bits, gk, gr, gdw, gdp, W, Pp, touched, stats, tail);
     // after an update-dense window: the stepper's chunk (an empty launch
@@ -1216,10 +1233,18 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
   // inside the segment sequence (else the batch's rest goes to the caller's
   // single-stream kernel at the end)
   const bool chunks = dense_pm > 0 && jb_stepper_enabled();
+  // JB_VC_CS=n: windows of at least n candidates are walked by the stepper
+  // (candidate mode; unset / 0: kernel C for all). Off by default: measured
+  // on the bench stream (tools/bench_serial.py, batches 20-30) 11.3 ms a
+  // batch against kernel C's 6.8 - the stepper pins a window's updated rows
+  // in its 768-slot cache and stops at ~400 of them (C's store: ~650), so a
+  // batch takes twice the windows, each with its own score / gather / verify
+  const char* cs_e = getenv("JB_VC_CS");
+  const int cs_min = (cs_e != nullptr && jb_stepper_enabled()) ? atoi(cs_e) : 0;
   int rc = 0;
 #define JB_VC_L(L)                                                                                            \
   rc = launch_vc<L>(method, row_ptr, fidx, fval, labels, W, S, active, C, st, sl, bits, s0, aux, pp0, fi, fx, \
-                    gk, gr, gdw, gdp, touched, stats, tail, nseg, chunks, stream);                             \
+                    gk, gr, gdw, gdp, touched, stats, tail, nseg, chunks, cs_min, stream);                     \
   break;
   switch (LC) {
     case 8: JB_VC_L(8)

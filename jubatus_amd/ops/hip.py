@@ -772,7 +772,9 @@ class SerialScratch:
                        # samples the sequential stepper (csrc/hip/stepper.hip)
                        # applied: chunks after update-dense windows, and the
                        # rest the segments left (stop_reason "dense")
-                       stepper_samples=v[16] + v[1] - v[0], stepper_chunks=v[17])
+                       stepper_samples=v[16] + v[1] - v[0], stepper_chunks=v[17],
+                       # windows whose candidates the stepper walked (kernel C's place)
+                       stepper_windows=v[19])
             if v[15] > 0:      # JB_COMMIT_PROF=1: committer phases (shader cycles -> us by the wall clock)
                 us = (v[30] / 100.0) / v[15]
                 for i, nm in enumerate(("round_start", "select", "decide", "apply", "correct")):

@@ -150,3 +150,41 @@ def test_stepper_chunks_between_sparse_windows():
     assert d["tail_start"] == d["end"], d
     assert d["stepper_chunks"] >= 1 and d["stepper_samples"] < 0.8 * d["end"], d
     _close(g, c)
+
+
+def test_stepper_candidate_windows_match_oracle(monkeypatch):
+    """JB_VC_CS: verified-committer windows whose candidates the stepper walks
+    in kernel C's place (no W / P writes; its updated rows staged for kernel
+    D, which verifies the rest of the window and commits)"""
+    from jubatus_amd.models.classifier import LinearClassifier
+    from jubatus_amd.ops import hip
+
+    monkeypatch.setenv("JB_VC_CS", "16")
+    rng = random.Random(21)
+    data = []
+    for _ in range(40 * 512):
+        y = rng.randrange(6)
+        sv = [[f"s{j}", f"t{y * 131 + rng.randrange(16) if rng.random() < 0.6 else rng.randrange(4000)}"]
+              for j in range(6)]
+        nv = [[f"n{j}", (y - 3) * 0.05 + rng.gauss(0.0, 1.0)] for j in range(4)]
+        data.append((f"L{y}", [sv, nv, []]))
+    param = {"regularization_weight": 1.0}
+    reqs = [data[i:i + 128] for i in range(0, len(data), 128)]
+    g = LinearClassifier("AROW", param, DatumToFvConverter(CONV), device=_device())
+    c = LinearClassifier("AROW", param, DatumToFvConverter(CONV))
+    for y in range(6):
+        g.set_label(f"L{y}")
+        c.set_label(f"L{y}")
+    hip.stepper_error()
+    half = len(reqs) // 2
+    wins = 0
+    for part in (reqs[:half], reqs[half:]):
+        g.train_requests([msgpack.packb([[l, d] for l, d in r], use_bin_type=False) for r in part])
+        g.synchronize()
+        wins += g._serial.last_batch().get("stepper_windows", 0)
+    for r in reqs:
+        c.train(r)
+    g.pipe.check_errors()
+    assert hip.stepper_error() == 0
+    assert wins > 0
+    _close(g, c)
