@@ -36,8 +36,8 @@ constexpr int kTailStepped = 16, kTailChunks = 17, kTailSegEst = 18, kTailCsWind
 constexpr int kTailReasonW = 20;
 constexpr int64_t kReasonDone = 0, kReasonSaturated = 1;
 
-// Candidates on the stepper (JB_VC_CS=n, off by default - see vcommit.hip):
-// a window of at least n candidates is walked by the sequential stepper instead of the
+// Candidates on the stepper (JB_VC_CS / JB_VC_CS_PM, see vcommit.hip): an
+// update-heavy window's candidates are walked by the sequential stepper instead of the
 // one-wave committer C - in candidate order, from the model at the window's
 // start, without writing W / P: its updated rows stay pinned in its LDS
 // cache and are staged like C's store (keys, rmax, dW, dP) in the stepper's

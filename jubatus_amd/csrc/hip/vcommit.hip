@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
     const float* __restrict__ fval, const int32_t* __restrict__ labels, const float* __restrict__ W,
     const float* __restrict__ P, const int32_t* __restrict__ active, int method, float C,
     const unsigned long long* __restrict__ bits, float* __restrict__ S0, int4* __restrict__ AUX,
-    float2* __restrict__ PP0, int32_t* __restrict__ FI, float* __restrict__ FX, int cs_min) {
+    float2* __restrict__ PP0, int32_t* __restrict__ FI, float* __restrict__ FX, int cs_min, int cs_pm) {
   using L = Lanes<LC>;
   if (!live((int)st[S_STATUS])) return;
   __shared__ int s_pref[kBitWords + 1];
@@ -320,10 +320,14 @@ __global__ __launch_bounds__(256) void vc_gather_kernel(
   __syncthreads();
   const int ncand = s_pref[kBitWords];
   if (blockIdx.x == 0 && tid == 0) {
+    // the stepper walks the candidates (stepper.hip, candidate mode) when
+    // there are enough and the last window updated on more than cs_pm per
+    // mille of its candidates: kernel C pays ~2.3 us an update and little for
+    // the rest, the stepper ~0.8 us a candidate either way
+    const int64_t pn = st[S_NCAND], pu = st[S_NUPD];
+    st[S_CSMODE] = (cs_min > 0 && ncand >= cs_min && pu * 1000 >= (int64_t)cs_pm * (pn > 0 ? pn : 1)) ? 1 : 0;
     st[S_NCAND] = ncand;
     st[S_WEND] = we;
-    // enough candidates: the stepper walks them (stepper.hip, candidate mode)
-    st[S_CSMODE] = (cs_min > 0 && ncand >= cs_min) ? 1 : 0;
   }
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   const int g = lane / L::LW;
@@ -1127,7 +1131,7 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
                      const int32_t* labels, float* W, float* S, const int32_t* active, float C, int64_t* st,
                      float* sl, unsigned long long* bits, float* s0, int4* aux, float2* pp0, int32_t* fi,
                      float* fx, int32_t* gk, float* gr, float* gdw, float* gdp, uint8_t* touched,
-                     unsigned long long* stats, int64_t* tail, int nseg, bool chunks, int cs_min,
+                     unsigned long long* stats, int64_t* tail, int nseg, bool chunks, int cs_min, int cs_pm,
                      hipStream_t stream) {
   using namespace jb::vc;
   static const int prof = [] {
@@ -1151,7 +1155,7 @@ static int launch_vc(int method, const int64_t* row_ptr, const int32_t* fidx, co
     hipLaunchKernelGGL((vc_score_kernel<L>), dim3(1024), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
                        W, active, method, C, sl, bits, gk, gr);
     hipLaunchKernelGGL((vc_gather_kernel<L>), dim3(512), dim3(256), 0, stream, st, row_ptr, fidx, fval, labels,
-                       W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx, cs_min);
+                       W, Pp, active, method, C, bits, s0, aux, pp0, fi, fx, cs_min, cs_pm);
 #define JB_VC_S(M, R, PD)                                                                                       \
   hipLaunchKernelGGL((vc_commit_kernel<L, M, R, PD, 1>), dim3(1), dim3(64), 0, stream, st, W, Pp, active, C, s0, \
                      aux, pp0, fi, fx, gk, gr, gdw, gdp, prof);                                                  \
@@ -1233,18 +1237,22 @@ extern "C" int jb_vcommit_prepare(const int64_t* row_ptr, const int32_t* fidx, c
   // inside the segment sequence (else the batch's rest goes to the caller's
   // single-stream kernel at the end)
   const bool chunks = dense_pm > 0 && jb_stepper_enabled();
-  // JB_VC_CS=n: windows of at least n candidates are walked by the stepper
-  // (candidate mode; unset / 0: kernel C for all). Off by default: measured
-  // on the bench stream (tools/bench_serial.py, batches 20-30) 11.3 ms a
-  // batch against kernel C's 6.8 - the stepper pins a window's updated rows
-  // in its 768-slot cache and stops at ~400 of them (C's store: ~650), so a
-  // batch takes twice the windows, each with its own score / gather / verify
+  // JB_VC_CS=n (0 / unset: off): windows of at least n candidates go to the
+  // stepper when the last window updated on more than JB_VC_CS_PM per mille
+  // of its candidates (default 350). Off by default: measured on the bench
+  // stream (tools/bench_serial.py, batches 20-30: ~22 % of candidates update)
+  // with every window on the stepper 11.3 ms a batch against kernel C's 6.8
+  // (the stepper costs ~0.8 us a candidate, C ~2.3 us an update and little
+  // else, and the stepper's windows end at fewer pinned rows), and on the
+  // served learning stream (18 % updates) 1.61 M samples/s against 1.65 M
   const char* cs_e = getenv("JB_VC_CS");
-  const int cs_min = (cs_e != nullptr && jb_stepper_enabled()) ? atoi(cs_e) : 0;
+  const char* cs_p = getenv("JB_VC_CS_PM");
+  const int cs_min = (jb_stepper_enabled() && cs_e != nullptr) ? atoi(cs_e) : 0;
+  const int cs_pm = cs_p != nullptr ? atoi(cs_p) : 350;
   int rc = 0;
 #define JB_VC_L(L)                                                                                            \
   rc = launch_vc<L>(method, row_ptr, fidx, fval, labels, W, S, active, C, st, sl, bits, s0, aux, pp0, fi, fx, \
-                    gk, gr, gdw, gdp, touched, stats, tail, nseg, chunks, cs_min, stream);                     \
+                    gk, gr, gdw, gdp, touched, stats, tail, nseg, chunks, cs_min, cs_pm, stream);              \
   break;
   switch (LC) {
     case 8: JB_VC_L(8)

@@ -160,6 +160,7 @@ def test_stepper_candidate_windows_match_oracle(monkeypatch):
     from jubatus_amd.ops import hip
 
     monkeypatch.setenv("JB_VC_CS", "16")
+    monkeypatch.setenv("JB_VC_CS_PM", "0")   # every window of 16+ candidates
     rng = random.Random(21)
     data = []
     for _ in range(40 * 512):
