@@ -28,7 +28,10 @@ def test_two_ranks_one_gpu_gloo():
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "4", "--warmup", "2", "--dist-backend", "gloo",
            "--requests", "64", "--per-request", "32", "--hash-bits", "16", "--latency-iters", "5",
-           "--batches-per-step", "3"]
+           "--batches-per-step", "3",
+           # the distributed engine records at a rehearsal size (the BASELINE-scale
+           # fills are the driver's 8-GPU run; tests/test_eight_ranks.py covers them on CPU)
+           "--dist-engines", "arow", "--dist-train-seconds", "1", "--dist-engine-rows", "2000"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
