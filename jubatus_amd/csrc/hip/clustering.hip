@@ -220,6 +220,49 @@ __device__ __forceinline__ void stage_cols(float* __restrict__ s_x, const float*
   }
 }
 
+// acc[p] += sum_j (x[i0 + p][j] - x[c][j])^2 over the d columns of a
+// column-major LDS table [d][NP], in column order (the host's order), four
+// columns' loads issued before their arithmetic: one LDS round trip per four
+// columns instead of one per column - the relax step of a k-means++ draw
+template <int P, int NP>
+__device__ __forceinline__ void relax_cols(const float* __restrict__ s_x, int d, int c, int i0, float (&acc)[P]) {
+  int j = 0;
+  for (; j + 4 <= d; j += 4) {
+    float xc[4], v[4][P];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float* col = s_x + (int64_t)(j + q) * NP;
+      xc[q] = col[c];
+#pragma unroll
+      for (int r = 0; r < P / 4; ++r) {
+        const float4 f = reinterpret_cast<const float4*>(col + i0)[r];
+        v[q][4 * r] = f.x; v[q][4 * r + 1] = f.y; v[q][4 * r + 2] = f.z; v[q][4 * r + 3] = f.w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const float tt = v[q][p] - xc[q];
+        acc[p] = fmaf(tt, tt, acc[p]);
+      }
+  }
+  for (; j < d; ++j) {
+    const float* col = s_x + (int64_t)j * NP;
+    const float xc = col[c];
+#pragma unroll
+    for (int r = 0; r < P / 4; ++r) {
+      const float4 f = reinterpret_cast<const float4*>(col + i0)[r];
+      const float vv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float tt = vv[e] - xc;
+        acc[4 * r + e] = fmaf(tt, tt, acc[4 * r + e]);
+      }
+    }
+  }
+}
+
 constexpr int kKppMaxM = 1024;   // draws whose uniforms the wave kernel stages in LDS
 
 // k-means++ seeding on ONE wave (n <= 64 P points): lane l owns rows
@@ -289,22 +332,7 @@ __global__ __launch_bounds__(64) void kmeanspp_wave_kernel(const float* __restri
     float acc[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) acc[p] = 0.f;
-#pragma unroll 2
-    for (int j = 0; j < d; ++j) {
-      const float* col = s_x + (int64_t)j * NP;
-      const float xc = col[c];
-      float v[P];
-#pragma unroll
-      for (int q = 0; q < P / 4; ++q) {
-        const float4 f = reinterpret_cast<const float4*>(col + i0)[q];
-        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
-      }
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const float t = v[p] - xc;
-        acc[p] = fmaf(t, t, acc[p]);
-      }
-    }
+    relax_cols<P, NP>(s_x, d, c, i0, acc);
 #pragma unroll
     for (int p = 0; p < P; ++p)
       if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
@@ -401,21 +429,7 @@ __global__ __launch_bounds__(NW * 64) void kmeanspp_blk_kernel(const float* __re
     float acc[P];
 #pragma unroll
     for (int p = 0; p < P; ++p) acc[p] = 0.f;
-    for (int j = 0; j < d; ++j) {
-      const float* col = s_x + (int64_t)j * NP;
-      const float xc = col[c];
-      float v[P];
-#pragma unroll
-      for (int q = 0; q < P / 4; ++q) {
-        const float4 f = reinterpret_cast<const float4*>(col + i0)[q];
-        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
-      }
-#pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const float tt = v[p] - xc;
-        acc[p] = fmaf(tt, tt, acc[p]);
-      }
-    }
+    relax_cols<P, NP>(s_x, d, c, i0, acc);
 #pragma unroll
     for (int p = 0; p < P; ++p)
       if (i0 + p < n) d2[p] = fminf(d2[p], acc[p]);
