@@ -330,7 +330,14 @@ class LshIndex {
     words_ = (hash_num + 63) / 64;
     bufs_.init();
     alloc(1024);
+    for (auto& e : stage_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
+  ~LshIndex() {
+    for (auto& e : stage_ev_)
+      if (e != nullptr) (void)hipEventDestroy(e);
+  }
+  LshIndex(const LshIndex&) = delete;
+  LshIndex& operator=(const LshIndex&) = delete;
   int metric() const { return metric_; }
 
   void clear() {
@@ -362,7 +369,13 @@ class LshIndex {
     size_t nnz = 0;
     for (size_t i : keep) nnz += pend_rp_[i + 1] - pend_rp_[i];
     const size_t bytes = 8 * (2 * n + 1) + 8 * nnz + 16;
-    uint8_t* h = stage_host_.get(bytes);
+    // a ring of staging buffers: a batch's launch runs while the RPC answers
+    // go out and the next batch stages (a stream sync per batch waited for
+    // each launch on the write path); a buffer is reused once its launch ended
+    const int k = stage_next_;
+    stage_next_ = (stage_next_ + 1) % kStageRing;
+    if (stage_used_[k]) HIPCHK(hipEventSynchronize(stage_ev_[k]));
+    uint8_t* h = stage_host_[k].get(bytes);
     int64_t* rp = (int64_t*)h;
     int64_t* sl = rp + n + 1;
     int32_t* ix = (int32_t*)(sl + n);
@@ -378,14 +391,15 @@ class LshIndex {
       rp[q + 1] = (int64_t)o;
       sl[q] = pend_slot_[i];
     }
-    uint8_t* d = stage_dev_.get(bytes);
+    uint8_t* d = stage_dev_[k].get(bytes);
     HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, stream_));
     const int64_t* drp = (const int64_t*)d;
     const int rc = jb_lsh_set_rows_staged(drp, drp + n + 1, (const int32_t*)(drp + 2 * n + 1),
                                           (const float*)((const int32_t*)(drp + 2 * n + 1) + nnz), (int)n, hash_num_,
                                           seed_, mode_, (uint64_t*)bits_.p, norms_.p, valid_.p, stream_);
     if (rc != 0) throw std::runtime_error("lsh staged set failed: " + std::to_string(rc));
-    HIPCHK(hipStreamSynchronize(stream_));   // the pinned staging is reused by the next batch
+    HIPCHK(hipEventRecord(stage_ev_[k], stream_));   // (later work on stream_ sees the rows)
+    stage_used_[k] = true;
     pend_slot_.clear();
     pend_rp_.assign(1, 0);
     pend_idx_.clear();
@@ -629,8 +643,12 @@ class LshIndex {
   std::vector<size_t> pend_rp_{0};
   std::vector<int32_t> pend_idx_;
   std::vector<float> pend_val_;
-  PinBuf<uint8_t> stage_host_;
-  DevBuf<uint8_t> stage_dev_;
+  static constexpr int kStageRing = 4;
+  PinBuf<uint8_t> stage_host_[kStageRing];
+  DevBuf<uint8_t> stage_dev_[kStageRing];
+  hipEvent_t stage_ev_[kStageRing] = {};
+  bool stage_used_[kStageRing] = {};
+  int stage_next_ = 0;
   uint64_t flushes_ = 0;
 };
 
