@@ -817,9 +817,15 @@ def engine_records(args, local: int) -> dict:
                     f.write((b"\x93" + nil + d + b"\x0a") if query_m.startswith("similar") else
                             (b"\x92" + nil + d))
             t0 = time.perf_counter()
+            th0 = _proc_thread_cpu(p.pid)
             r = _loadgen(exe, port, fill_m, fill, 16, 8, once=True)
+            th1 = _proc_thread_cpu(p.pid)
             rec["fill_s"] = round(time.perf_counter() - t0, 2)
             rec[f"{fill_m}_per_s_fill"] = r["requests_per_s"]
+            # where the fill's server time goes (CPUs per thread name)
+            rec["fill_server_cpus_by_thread"] = {k: round((v - th0.get(k, 0.0)) / max(1e-9, rec["fill_s"]), 2)
+                                                 for k, v in sorted(th1.items())
+                                                 if v - th0.get(k, 0.0) > 0.01 * rec["fill_s"]}
             with RpcClient("127.0.0.1", port, 60.0) as c:
                 (_, st), = c.call("get_status", "").items()
             st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
