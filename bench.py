@@ -786,8 +786,9 @@ def engine_records(args, local: int) -> dict:
         rec: dict = {"config": cfg, "rows": nrows, "server": f"native juba{engine} (no Python)"}
         _progress(f"engine {name}: fill {nrows} rows")
         port = _free_port()
-        p = subprocess.Popen([srv, "-p", str(port), "-b", "127.0.0.1", "-f", os.path.join(ROOT, cfg),
-                              "-d", tmp, "-c", "4", "--gpu", str(local)],
+        wrap = shlex.split(os.environ.get("JB_SERVED_WRAP", ""))   # (profiling prefix)
+        p = subprocess.Popen(wrap + [srv, "-p", str(port), "-b", "127.0.0.1", "-f", os.path.join(ROOT, cfg),
+                                     "-d", tmp, "-c", "4", "--gpu", str(local)],
                              stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
         try:
             deadline = time.time() + 60
@@ -831,6 +832,9 @@ def engine_records(args, local: int) -> dict:
             st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
                   for k, v in st.items()}
             rec["rows_stored"] = int(st.get("num_rows", -1))
+            if "write_batch_us" in st:   # the fill's write batches: count, rows, phase times
+                rec["fill_write_batches"] = {k: st.get(k) for k in ("write_batches", "write_batch_rows",
+                                                                    "write_batch_us")}
             _progress(f"engine {name}: filled in {rec['fill_s']} s; queries")
             lat = _loadgen(exe, port, query_m, q, 1, 1, secs=args.engine_seconds)
             rec[f"{query_m}_p50_us"] = lat["p50_us"]

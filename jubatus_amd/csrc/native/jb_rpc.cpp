@@ -346,6 +346,7 @@ void RpcServer::set_batch(const std::vector<std::string>& methods, BatchHandler 
 void RpcServer::enqueue(RpcRequest&& req) {
   for (const auto& m : batch_methods_)
     if (m == req.method) {
+      if (prep_) prep_(req);
       std::lock_guard<std::mutex> g(bmu_);
       bqueue_.push_back(std::move(req));
       bcv_.notify_all();  // the generic-queue thread must see it
@@ -378,11 +379,16 @@ void RpcServer::batch_loop(int idx) {
       if (!running_.load()) return;
       if (!generic || bqueue_.empty()) continue;
       const std::string method = bqueue_.front().method;
+      auto ordered = [this](const std::string& m) {
+        return std::find(ordered_.begin(), ordered_.end(), m) != ordered_.end();
+      };
+      const bool keep_order = ordered(method);
       for (auto it = bqueue_.begin(); it != bqueue_.end() && batch.size() < max_batch_;) {
         if (it->method == method) {
           batch.push_back(std::move(*it));
           it = bqueue_.erase(it);
         } else {
+          if (keep_order || ordered(it->method)) break;
           ++it;
         }
       }

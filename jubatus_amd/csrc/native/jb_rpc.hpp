@@ -35,6 +35,7 @@ struct RpcRequest {
   bool notify;
   std::string method;
   std::string params;  // msgpack array bytes
+  std::shared_ptr<void> prep;   // the prep hook's result (set_prep), or null
 };
 
 // A request of the arena-batched method: its body (params[1]) sits at
@@ -112,6 +113,16 @@ class RpcServer {
   // drains everything queued for a method and calls `h` once for all of it
   // (concurrent train / classify RPCs become one GPU launch). Call before start().
   void set_batch(const std::vector<std::string>& methods, BatchHandler h, size_t max_batch);
+  // Batched methods that write: a batch keeps arrival order around them
+  // (it never takes a request past one of another method when either is
+  // an ordered method), so pipelined writes of different methods - an
+  // update_row, then a clear_row of the row - apply in the order sent.
+  // Reads of different methods still batch past each other.
+  void set_ordered(const std::vector<std::string>& methods) { ordered_ = methods; }
+  // Called on the IO thread for every request of a batched method before it
+  // is queued (e.g. decode and hash a write's datum there, so the batch
+  // thread - the serial part - only applies it). Call before start().
+  void set_prep(std::function<void(RpcRequest&)> h) { prep_ = std::move(h); }
 
   // arena handler(slot, requests) -> one encoded response per request
   using ArenaHandler = std::function<std::vector<std::string>(int, const std::vector<ArenaReq>&)>;
@@ -199,6 +210,8 @@ class RpcServer {
   std::atomic<size_t> qlen_{0};   // queue_.size(), readable without qmu_
   // batched methods
   std::vector<std::string> batch_methods_;
+  std::vector<std::string> ordered_;
+  std::function<void(RpcRequest&)> prep_;
   BatchHandler batch_handler_;
   size_t max_batch_ = 4096;
   std::mutex bmu_;

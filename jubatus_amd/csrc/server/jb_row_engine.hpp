@@ -169,6 +169,30 @@ class Converter {
     }
   }
 
+  // the fixed-slot hasher, which keeps no document statistics (null: this
+  // converter keeps statistics). Immutable and shared: the RPC IO threads
+  // hash write datums with it outside the model lock (Model::prep_write)
+  std::shared_ptr<const HostFvHasher> stateless() const { return fast_; }
+  // one datum's msgpack bytes -> (idx, val) with such a hasher
+  static void hash_with(const HostFvHasher& h, const uint8_t* d, size_t n, std::vector<int32_t>* idx,
+                        std::vector<float>* val) {
+    std::string body(1, (char)0x91);
+    body.append((const char*)d, n);
+    size_t cap = std::max<size_t>(256, n / 2 + 64);
+    for (;;) {
+      idx->resize(cap);
+      val->resize(cap);
+      int64_t rp[2] = {0, 0}, nn = 0, slots = 0;
+      const int rc = h.hash_body((const uint8_t*)body.data(), body.size(), idx->data(), val->data(), rp, 1,
+                                 (int64_t)cap, &nn, &slots);
+      if (rc == 2) { cap *= 4; continue; }
+      if (rc != 0 || nn != 1) throw ArgError("malformed datum");
+      idx->resize((size_t)rp[1]);
+      val->resize((size_t)rp[1]);
+      return;
+    }
+  }
+
   // document statistics of the MIX (WeightManager.get_diff / put_diff):
   // this server's contribution since the last MIX, then the cluster's sum
   // replaces it
@@ -251,7 +275,7 @@ class Converter {
   }
 
  private:
-  std::unique_ptr<HostFvHasher> fast_;
+  std::shared_ptr<HostFvHasher> fast_;
   std::unique_ptr<HostFvWide> wide_;
   std::vector<int64_t> df_, diff_;
   int64_t counts_[4] = {0, 0, 0, 0};
@@ -664,7 +688,40 @@ class PoolIndex {
   }
   int metric() const { return euclid_ ? 1 : 0; }
 
-  void clear() { reset(); }
+  void clear() {
+    pend_meta_.clear();
+    pend_idx_.clear();
+    pend_val_.clear();
+    reset();
+  }
+
+  // batched writes (the row server's write batches): the runs of rows set
+  // while deferred are appended on the host (their pool offsets are taken at
+  // once) and go to the device in one staged jb_pool_append in flush(); every
+  // read of the pool flushes first
+  void set_defer(bool on) {
+    if (!on) flush();
+    defer_ = on;
+  }
+  void flush() {
+    if (pend_meta_.empty()) return;
+    // the last write of a slot wins (one launch writes each slot's row once);
+    // the runs of earlier writes stay in the pool as dead entries
+    const size_t nw = pend_meta_.size() / 4;
+    std::unordered_map<int64_t, size_t> last;
+    for (size_t i = 0; i < nw; ++i) last[pend_meta_[4 * i]] = i;
+    std::vector<int64_t> meta;
+    meta.reserve(4 * last.size());
+    for (size_t i = 0; i < nw; ++i)
+      if (last[pend_meta_[4 * i]] == i)
+        meta.insert(meta.end(), pend_meta_.begin() + 4 * i, pend_meta_.begin() + 4 * i + 4);
+    const int n = (int)(meta.size() / 4);
+    const int64_t nnz = (int64_t)pend_idx_.size();
+    stage_append(meta.data(), n, pend_idx_.data(), pend_val_.data(), nnz, pend_base_);
+    pend_meta_.clear();
+    pend_idx_.clear();
+    pend_val_.clear();
+  }
 
   // csr_normalize of one row + jb_pool_append (latency path: pinned staging)
   void set(int32_t slot, const std::vector<int32_t>& idx, const std::vector<float>& val) {
@@ -688,36 +745,33 @@ class PoolIndex {
     }
     const int64_t nnz = (int64_t)ni.size();
     grow_rows(slot + 1);
-    if (end_ + nnz > cap_entries_ && end_ - live_ > live_) compact();
+    if (end_ + nnz > cap_entries_ && end_ - live_ > live_) {
+      flush();   // the compaction reads the pool back
+      compact();
+    }
     grow_entries(end_ + nnz);
-    // pack: [slot, len, n2 bits, run] int64 | idx int32 | val f32
-    const size_t bytes = 32 + 8 * (size_t)nnz;
-    Stage& s = stage_[turn_];
-    turn_ = (turn_ + 1) % kStages;
-    if (s.used) HIPCHK(hipEventSynchronize(s.ev));
-    uint8_t* p = s.host.get(bytes);
+    // meta: [slot, len, n2 bits, run offset from the launch's base]
     int64_t meta[4] = {slot, nnz, 0, 0};
     memcpy(&meta[2], &sq, 8);
-    memcpy(p, meta, 32);
-    if (nnz) {
-      memcpy(p + 32, ni.data(), 4 * (size_t)nnz);
-      memcpy(p + 32 + 4 * (size_t)nnz, nv.data(), 4 * (size_t)nnz);
+    if (defer_) {
+      if (pend_meta_.empty()) pend_base_ = end_;
+      meta[3] = end_ - pend_base_;
+      pend_meta_.insert(pend_meta_.end(), meta, meta + 4);
+      pend_idx_.insert(pend_idx_.end(), ni.begin(), ni.end());
+      pend_val_.insert(pend_val_.end(), nv.begin(), nv.end());
+    } else {
+      stage_append(meta, 1, ni.data(), nv.data(), nnz, end_);
     }
-    uint8_t* d = s.dev.get(bytes);
-    HIPCHK(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, stream_));
-    const int rc = jb_pool_append(d, 1, nnz, end_, r_off_.p, r_len_.p, r_n2_.p, valid_.p, p_idx_.p, p_val_.p,
-                                  stream_);
-    if (rc != 0) throw std::runtime_error("pool append failed: " + std::to_string(rc));
-    HIPCHK(hipEventRecord(s.ev, stream_));
-    s.used = true;
     live_ += nnz - len_h_[slot];
     if (!has_h_[slot]) { ++nlive_; has_h_[slot] = 1; }
     off_h_[slot] = end_;
     len_h_[slot] = nnz;
     end_ += nnz;
+    if (defer_ && pend_meta_.size() >= 4 * 4096) flush();
   }
 
   void remove(int32_t slot) {
+    flush();
     if (slot < 0 || slot >= cap_rows_) return;
     live_ -= len_h_[slot];
     if (has_h_[slot]) { --nlive_; has_h_[slot] = 0; }
@@ -727,6 +781,7 @@ class PoolIndex {
 
   std::vector<Hit> query_fv(const std::vector<int32_t>& idx, const std::vector<float>& val,
                             int64_t nrows, int k) {
+    flush();
     if (nrows <= 0 || k <= 0) return {};
     if (k <= kTopMaxK) {
       bufs_.scratch(nrows, k, 1);
@@ -778,6 +833,7 @@ class PoolIndex {
   bool query_fv_many(const std::vector<const std::vector<int32_t>*>& idx,
                      const std::vector<const std::vector<float>*>& val, int64_t nrows, int k,
                      std::vector<std::vector<Hit>>* out) {
+    flush();
     const int nq = (int)idx.size();
     if (nq <= 0 || nq > kPoolMaxQ || nrows <= 0 || k <= 0 || k > kTopMaxK) return false;
     std::vector<int64_t> rp(1, 0);
@@ -801,6 +857,7 @@ class PoolIndex {
   }
 
   std::vector<Hit> query_slot(int32_t slot, int64_t nrows, int k) {
+    flush();
     if (nrows <= 0 || k <= 0) return {};
     if (k <= kTopMaxK && len_h_[slot] <= kPoolMaxQEntries) {
       bufs_.scratch(nrows, k, 1);
@@ -833,6 +890,29 @@ class PoolIndex {
     hipEvent_t ev;
     bool used = false;
   };
+
+  // n rows' meta + their runs (nnz entries from pool offset base) through
+  // a pinned staging buffer of the ring, one jb_pool_append launch
+  void stage_append(const int64_t* meta, int n, const int32_t* ni, const float* nv, int64_t nnz, int64_t base) {
+    // pack: [slot, len, n2 bits, run] int64 x n | idx int32 | val f32
+    const size_t bytes = 32 * (size_t)n + 8 * (size_t)nnz;
+    Stage& s = stage_[turn_];
+    turn_ = (turn_ + 1) % kStages;
+    if (s.used) HIPCHK(hipEventSynchronize(s.ev));
+    uint8_t* p = s.host.get(bytes);
+    memcpy(p, meta, 32 * (size_t)n);
+    if (nnz) {
+      memcpy(p + 32 * (size_t)n, ni, 4 * (size_t)nnz);
+      memcpy(p + 32 * (size_t)n + 4 * (size_t)nnz, nv, 4 * (size_t)nnz);
+    }
+    uint8_t* d = s.dev.get(bytes);
+    HIPCHK(hipMemcpyAsync(d, p, bytes, hipMemcpyHostToDevice, stream_));
+    const int rc = jb_pool_append(d, n, nnz, base, r_off_.p, r_len_.p, r_n2_.p, valid_.p, p_idx_.p, p_val_.p,
+                                  stream_);
+    if (rc != 0) throw std::runtime_error("pool append failed: " + std::to_string(rc));
+    HIPCHK(hipEventRecord(s.ev, stream_));
+    s.used = true;
+  }
 
   // scores (cosine similarity / euclidean distance) -> k smallest distances
   std::vector<Hit> scores_topk(const float* scores, int64_t nrows, int k) {
@@ -956,6 +1036,12 @@ class PoolIndex {
   Stage stage_[kStages];
   int turn_ = 0;
   QueryBufs bufs_;
+  // deferred writes (set_defer)
+  bool defer_ = false;
+  int64_t pend_base_ = 0;
+  std::vector<int64_t> pend_meta_;
+  std::vector<int32_t> pend_idx_;
+  std::vector<float> pend_val_;
 };
 
 // ------------------------------------------------------------- row store
@@ -1058,6 +1144,7 @@ class RowEngine {
   // meanwhile on the host and writes them in one launch when it ends
   void defer_writes(bool on) {
     if (lsh_) lsh_->set_defer(on);
+    else pool_->set_defer(on);
   }
 
   // called with the slot of every removed row (the LOF state's moved())

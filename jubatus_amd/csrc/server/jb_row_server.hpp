@@ -37,6 +37,7 @@
 #include <math.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <random>
 #include <set>
@@ -300,6 +301,13 @@ class Model : public jb::mix::Mixable {
   }
   uint64_t batches() const { return n_batches_.load(); }
   uint64_t n_write_batches_ = 0, n_write_rows_ = 0;   // (under mu_)
+  // wall microseconds of the write batches (under mu_): parse / hash outside
+  // the lock, the locked apply, the device flush; the RPC side adds the
+  // argument decoding (status key write_batch_us)
+  double wb_us_[4] = {0, 0, 0, 0};
+  // the stateless hasher of the current converter (prep_write; atomic
+  // shared_ptr access: the IO threads read it without the model lock)
+  std::shared_ptr<const jb::HostFvHasher> prep_h_;
   uint64_t batched_queries() const { return n_batched_.load(); }
 
   void configure(const Config& cfg) {
@@ -309,6 +317,7 @@ class Model : public jb::mix::Mixable {
     eng_.reset(new RowEngine(cfg.inner, &cfg.param, stream_));
     std::string why;
     if (!eng_->conv.configure(cfg.conv, &why)) throw std::runtime_error("converter: " + why);
+    std::atomic_store(&prep_h_, eng_->conv.stateless());
     cfg_ = cfg;
     if (kind_ == Kind::kAnomaly)   // LOF._remove: a removed row's dependants go stale
       eng_->on_remove = [this](int32_t s) { if (lof_) lof_->moved({s}); };
@@ -444,33 +453,96 @@ class Model : public jb::mix::Mixable {
   // set_defer) instead of one launch per row. kind: 0 update_row, 1
   // set_row, 2 clear_row. -> per write: 1 / 0 (clear_row of an unknown id),
   // or the exception it raised
+  // a write decoded and hashed on the RPC IO thread (prep_write)
+  struct PrepWrite {
+    std::shared_ptr<const jb::HostFvHasher> h;   // the hasher it used
+    std::string id;
+    Datum d;
+    std::vector<int32_t> idx;
+    std::vector<float> val;
+  };
   struct Write {
     const std::string* id;
-    const Value* dv;
+    const Value* dv;          // or:
+    PrepWrite* pre = nullptr;
     int result = 0;
     std::exception_ptr err;
   };
+  // IO thread, no model lock (the hasher is an immutable snapshot): decode
+  // an update_row / set_row and hash its datum as a row of its own; null
+  // when the converter keeps statistics or the request is not well formed
+  // (the batch path decodes it again and answers the error)
+  std::shared_ptr<PrepWrite> prep_write(const std::string& params) const {
+    std::shared_ptr<const jb::HostFvHasher> h = std::atomic_load(&prep_h_);
+    if (!h) return nullptr;
+    try {
+      Value a = MsgpackReader((const uint8_t*)params.data(), params.size()).read();
+      if (a.kind != Value::ARR || a.a.size() != 3 || !a.a[0].is_str() || !a.a[1].is_str() ||
+          a.a[2].kind != Value::ARR)
+        return nullptr;
+      auto p = std::make_shared<PrepWrite>();
+      jb::row::parse_datum(a.a[2], &p->d);
+      MsgpackWriter w;
+      jb::row::write_datum(w, p->d);
+      jb::row::Converter::hash_with(*h, (const uint8_t*)w.out.data(), w.out.size(), &p->idx, &p->val);
+      p->id = std::move(a.a[1].s);
+      p->h = std::move(h);
+      return p;
+    } catch (...) {
+      return nullptr;
+    }
+  }
   void write_many(int kind, std::vector<Write>& ws) {
+    // parse each datum, and with a stateless converter hash it as a row of
+    // its own (a write whose id turns out to be stored merges and hashes
+    // again under the lock); the IO threads did both for most writes
     std::vector<Datum> ds(ws.size());
-    for (size_t i = 0; i < ws.size(); ++i) {
-      if (kind == 2) continue;
-      try {
-        jb::row::parse_datum(*ws[i].dv, &ds[i]);
-      } catch (...) {
-        ws[i].err = std::current_exception();
+    std::vector<std::vector<int32_t>> hi(ws.size());
+    std::vector<std::vector<float>> hv(ws.size());
+    std::vector<uint8_t> pre(ws.size(), 0);
+    using Clk = std::chrono::steady_clock;
+    const auto t0 = Clk::now();
+    if (kind != 2) {
+      std::shared_lock<std::shared_mutex> rd(mu_);   // (the converter stays as it is)
+      const std::shared_ptr<const jb::HostFvHasher> h = eng_->conv.stateless();
+      for (size_t i = 0; i < ws.size(); ++i) {
+        try {
+          if (PrepWrite* p = ws[i].pre) {
+            ds[i] = std::move(p->d);
+            if (p->h == h) {
+              hi[i] = std::move(p->idx);
+              hv[i] = std::move(p->val);
+              pre[i] = 1;
+              continue;
+            }
+          } else {
+            jb::row::parse_datum(*ws[i].dv, &ds[i]);
+          }
+          if (h) {
+            MsgpackWriter w;
+            jb::row::write_datum(w, ds[i]);
+            jb::row::Converter::hash_with(*h, (const uint8_t*)w.out.data(), w.out.size(), &hi[i], &hv[i]);
+            pre[i] = 1;
+          }
+        } catch (...) {
+          ws[i].err = std::current_exception();
+        }
       }
     }
+    const auto t1 = Clk::now();
     std::unique_lock<std::shared_mutex> g(mu_);
     eng_->defer_writes(true);
     for (size_t i = 0; i < ws.size(); ++i) {
       if (ws[i].err) continue;
       try {
-        if (kind == 0) {
+        if (kind == 0 && (!pre[i] || eng_->find(*ws[i].id) != nullptr)) {
           update_row_locked(*ws[i].id, std::move(ds[i]));
           ws[i].result = 1;
-        } else if (kind == 1) {
+        } else if (kind != 2) {
           ++update_count;
-          eng_->set(*ws[i].id, std::move(ds[i]));
+          if (kind == 0) ++update_row_cnt;
+          if (pre[i]) eng_->store(*ws[i].id, std::move(ds[i]), hi[i], hv[i], true);
+          else eng_->set(*ws[i].id, std::move(ds[i]));
           ws[i].result = 1;
         } else {
           ++update_count;
@@ -481,11 +553,20 @@ class Model : public jb::mix::Mixable {
         ws[i].err = std::current_exception();
       }
     }
+    const auto t2 = Clk::now();
     eng_->defer_writes(false);
+    const auto t3 = Clk::now();
+    wb_us_[0] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    wb_us_[1] += std::chrono::duration<double, std::micro>(t2 - t1).count();
+    wb_us_[2] += std::chrono::duration<double, std::micro>(t3 - t2).count();
     ++n_write_batches_;
     n_write_rows_ += ws.size();
   }
   uint64_t write_batches() const { return n_write_batches_; }
+  void add_decode_us(double us) {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    wb_us_[3] += us;
+  }
   uint64_t write_rows() const { return n_write_rows_; }
   // nearest_neighbor set_row: replace
   bool set_row(const std::string& id, const Value& dv) {
@@ -785,6 +866,12 @@ class Model : public jb::mix::Mixable {
     add("method", kind_ == Kind::kNearestNeighbor ? eng_->method() : cfg_.outer);
     add("write_batches", std::to_string(n_write_batches_));   // Model::write_many
     add("write_batch_rows", std::to_string(n_write_rows_));
+    {   // decode (RPC args), prep (parse / hash), apply (locked), flush (device)
+      char b[160];
+      snprintf(b, sizeof b, "decode %.0f prep %.0f apply %.0f flush %.0f", wb_us_[3], wb_us_[0], wb_us_[1],
+               wb_us_[2]);
+      add("write_batch_us", b);
+    }
     if (kind_ == Kind::kClassifier) {
       add("num_labels", std::to_string(labels_.size()));
       add("nearest_neighbor_num", std::to_string(cfg_.nn_k));
@@ -1287,6 +1374,12 @@ class Server {
       qm.push_back("clear_row");
     }
     if (kind_ == Kind::kNearestNeighbor) qm.push_back("set_row");
+    rpc_->set_ordered({"update_row", "clear_row", "set_row", "add"});
+    if (kind_ == Kind::kRecommender || kind_ == Kind::kNearestNeighbor)
+      rpc_->set_prep([this](jb::RpcRequest& r) {
+        if (r.method == (kind_ == Kind::kRecommender ? "update_row" : "set_row"))
+          r.prep = model_->prep_write(r.params);
+      });
     if (!qm.empty())
       rpc_->set_batch(qm, [this](const std::string& m, std::vector<jb::RpcRequest>& rs) {
         if (m == "update_row" || m == "set_row" || m == "clear_row") return write_batch(m, rs);
@@ -1343,12 +1436,22 @@ class Server {
   // dispatch() would, the rest apply as one Model::write_many
   std::vector<std::string> write_batch(const std::string& m, std::vector<jb::RpcRequest>& rs) {
     std::vector<std::string> out(rs.size());
+    const auto td = std::chrono::steady_clock::now();
     std::vector<Value> args(rs.size());
     std::vector<Model::Write> ws;
     std::vector<size_t> at;
     const bool clr = m == "clear_row";
     for (size_t i = 0; i < rs.size(); ++i) {
       const jb::RpcRequest& r = rs[i];
+      if (r.prep) {   // decoded and hashed on the IO thread
+        Model::Write w;
+        w.pre = static_cast<Model::PrepWrite*>(r.prep.get());
+        w.id = &w.pre->id;
+        w.dv = nullptr;
+        ws.push_back(w);
+        at.push_back(i);
+        continue;
+      }
       bool ok = true;
       try {
         args[i] = MsgpackReader((const uint8_t*)r.params.data(), r.params.size()).read();
@@ -1368,6 +1471,7 @@ class Server {
       ws.push_back(w);
       at.push_back(i);
     }
+    model_->add_decode_us(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - td).count());
     if (ws.empty()) return out;
     if (mixer_) mixer_->updated(ws.size());   // event_model_updated, once per write
     model_->write_many(m == "update_row" ? 0 : m == "set_row" ? 1 : 2, ws);
