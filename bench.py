@@ -832,9 +832,11 @@ def engine_records(args, local: int) -> dict:
             st = {(k.decode() if isinstance(k, bytes) else k): (v.decode() if isinstance(v, bytes) else v)
                   for k, v in st.items()}
             rec["rows_stored"] = int(st.get("num_rows", -1))
-            if "write_batch_us" in st:   # the fill's write batches: count, rows, phase times
+            if int(st.get("write_batches", 0) or 0):   # the fill's write batches: count, rows, phases
                 rec["fill_write_batches"] = {k: st.get(k) for k in ("write_batches", "write_batch_rows",
                                                                     "write_batch_us")}
+            if "add_batch_us" in st:   # batched anomaly adds: LOF chunks, phase times
+                rec["fill_add_batches"] = st["add_batch_us"]
             _progress(f"engine {name}: filled in {rec['fill_s']} s; queries")
             lat = _loadgen(exe, port, query_m, q, 1, 1, secs=args.engine_seconds)
             rec[f"{query_m}_p50_us"] = lat["p50_us"]

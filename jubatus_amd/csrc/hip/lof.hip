@@ -880,13 +880,14 @@ extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int
 // scratch of 2 x nadd x stride words, res: of nadd x out_stride (the results
 // before they go to the host); out_host[i * out_stride] = status 1
 // done, 2 stopped on rows without a valid list (its insert is applied, its
-// score is not), 3 not run.
+// score is not), 3 not run. wait = 0: return once launched (the caller
+// overlaps other work, then jb_lof_add_many_wait).
 extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd,
                                const int32_t* nc, int stride, int k, int ignore_same, int32_t* nb_slot,
                                float* nb_dist, float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                                int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp,
                                uint32_t epoch0, int32_t* cand, uint32_t* res, uint32_t* out_host, int out_stride,
-                               int max_missing, unsigned long long* prof, hipStream_t stream) {
+                               int max_missing, unsigned long long* prof, hipStream_t stream, int wait) {
   if (nadd <= 0) return 0;
   if (nadd > 64 || k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax || kstamp == nullptr ||
       lstamp == nullptr)
@@ -900,6 +901,12 @@ extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, c
                      epoch0, cand, res, out_host, out_stride, max_missing, prof);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
+  return wait ? jb::wait_nonzero(out_host + (int64_t)(nadd - 1) * out_stride, stream) : 0;
+}
+
+// the wait of a jb_lof_add_many launched with wait = 0 (its last add's status)
+extern "C" int jb_lof_add_many_wait(int nadd, uint32_t* out_host, int out_stride, hipStream_t stream) {
+  if (nadd <= 0) return 0;
   return jb::wait_nonzero(out_host + (int64_t)(nadd - 1) * out_stride, stream);
 }
 

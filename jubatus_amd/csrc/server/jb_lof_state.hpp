@@ -37,7 +37,8 @@ int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float*
                     uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
                     uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch0, int32_t* cand, uint32_t* res,
                     uint32_t* out_host, int out_stride, int max_missing, unsigned long long* prof,
-                    hipStream_t stream);
+                    hipStream_t stream, int wait);
+int jb_lof_add_many_wait(int nadd, uint32_t* out_host, int out_stride, hipStream_t stream);
 int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
                     const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                     int store_slot, const uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch,
@@ -126,8 +127,19 @@ class LofState {
   size_t add_many(const std::vector<int32_t>& ps, const std::vector<std::vector<int32_t>>& cs,
                   const std::vector<std::vector<float>>& cd, std::vector<float>* scores,
                   std::vector<int32_t>* missing) {
+    launch_many(ps, cs, cd);
+    return finish_many(scores, missing);
+  }
+
+  // add_many in two halves: the launch returns at once (the host stages the
+  // next batch meanwhile - the batch's kernel is one wave), finish_many waits
+  // for it and reads the results. The staging the kernel reads is rewritten
+  // only by the next launch, after the finish.
+  void launch_many(const std::vector<int32_t>& ps, const std::vector<std::vector<int32_t>>& cs,
+                   const std::vector<std::vector<float>>& cd) {
     const size_t n = ps.size();
-    if (n == 0) return 0;
+    if (launched_ != 0) throw std::logic_error("lof launch_many: the previous batch is not finished");
+    if (n == 0) return;
     if (n > (size_t)kLofBatchMax) throw std::runtime_error("lof add_many: batch too large");
     int stride = 1;
     for (const auto& c : cs) stride = std::max(stride, (int)c.size());
@@ -151,9 +163,19 @@ class LofState {
     epoch_ += (uint32_t)n;            // (adds after a stop leave gaps: stamps only need to grow)
     const int rc = jb_lof_add_many((int)n, hps, hcs, hcd, hnc, stride, k_, ignore_ ? 1 : 0, nb_slot_.p, nb_dist_.p,
                                    kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p, kstamp_.p, lstamp_.p,
-                                   epoch0, cand_.p, res_.p, out_many_, kOutStride, kLofMaxMissing, nullptr, stream_);
+                                   epoch0, cand_.p, res_.p, out_many_, kOutStride, kLofMaxMissing, nullptr, stream_,
+                                   0);
     if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
+    launched_ = n;
+  }
+  bool in_flight() const { return launched_ != 0; }
+  size_t finish_many(std::vector<float>* scores, std::vector<int32_t>* missing) {
+    const size_t n = launched_;
+    launched_ = 0;
     scores->clear();
+    if (n == 0) return 0;
+    const int rc = jb_lof_add_many_wait((int)n, out_many_, kOutStride, stream_);
+    if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
     for (size_t i = 0; i < n; ++i) {
       const uint32_t* o = out_many_ + i * kOutStride;
       const uint32_t st = ((volatile const uint32_t*)o)[0];
@@ -315,6 +337,7 @@ class LofState {
   bool ignore_;
   hipStream_t stream_;
   int64_t cap_ = 0;
+  size_t launched_ = 0;   // adds of the launch_many in flight
   DevBuf<int32_t> nb_slot_;
   DevBuf<float> nb_dist_, kdist_, lrd_;
   DevBuf<uint8_t> ok_, lrd_ok_;
