@@ -231,7 +231,14 @@ class HostServer : public jb::mix::Mixable {
         return r.notify ? std::string() : jb::val::response_code(r.msgid, kArgumentError);
       MsgpackWriter w;
       try {
-        if (x.update) {
+        if (x.self_lock) {   // the handler takes model_mu_ itself (after its lock-free part)
+          if (x.update) {
+            if (mixer_) mixer_->updated(1);
+            update_count_ += 1;
+          }
+          std::shared_lock<std::shared_mutex> life(life_mu_);   // (the engine is not replaced meanwhile)
+          x.raw(r.params, &w);
+        } else if (x.update) {
           if (mixer_) mixer_->updated(1);
           std::unique_lock<std::shared_mutex> g(model_mu_);
           update_count_ += 1;
@@ -355,6 +362,7 @@ class HostServer : public jb::mix::Mixable {
     if (mf.user_version != 1)
       throw std::runtime_error("user data version mismatched: " + std::to_string(mf.user_version) +
                                ", current version: 1");
+    std::unique_lock<std::shared_mutex> life(life_mu_);   // (no self-locking handler runs)
     std::unique_lock<std::shared_mutex> g(model_mu_);
     if (overwrite_config && !jb::val::same_config(mf.config, config_)) {
       eng_ = make_(mf.config);
@@ -380,6 +388,7 @@ class HostServer : public jb::mix::Mixable {
   std::unique_ptr<jb::mix::LinearMixer> mixer_;
   std::unique_ptr<jb::RpcServer> rpc_;
   std::shared_mutex model_mu_;
+  std::shared_mutex life_mu_;   // shared: a self-locking raw handler runs; exclusive: the engine is replaced
   std::mutex st_mu_;
   CommonStatus cs_;
   std::atomic<uint64_t> update_count_{0};

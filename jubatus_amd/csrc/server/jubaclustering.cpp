@@ -248,9 +248,12 @@ class Clustering : public HostEngine {
     if (!buckets_.empty() || others_.size()) recluster(&before, &after);
   }
 
+  void set_lock(std::shared_mutex* mu) override { mu_ = mu; }
+
   std::vector<HostMethod> methods() override {
     std::vector<HostMethod> m = {
-        {"push", 2, true, nullptr, [this](const std::string& params, MsgpackWriter* w) { push_raw(params, w); }},
+        {"push", 2, true, nullptr, [this](const std::string& params, MsgpackWriter* w) { push_raw(params, w); },
+         true},
         {"get_revision", 1, false, [this](const std::vector<Value>&, MsgpackWriter* w) { w->uint(revision_); }},
         {"get_core_members", 1, false,
          [this](const std::vector<Value>&, MsgpackWriter* w) { core_members(w); }},
@@ -329,13 +332,24 @@ class Clustering : public HostEngine {
 
  private:
   // ---------------------------------------------------------- convert
-  // one msgpack list<datum> body -> points (weight 1); false: malformed
-  bool convert(const uint8_t* body, size_t len, bool update, PointSet* out) {
+  // hashing scratch of one converter
+  struct Conv {
+    jb::HostFvWide* h = nullptr;
+    std::unique_ptr<jb::HostFvWide> own;   // a pooled converter's hasher
+    std::vector<int32_t> idx;
+    std::vector<float> fv;
+    std::vector<int64_t> rp;
+  };
+  // one msgpack list<datum> body -> points (weight 1); false: malformed.
+  // names: the (key, name) of each distinct feature key the body holds
+  bool convert(Conv& cv, const uint8_t* body, size_t len, bool update, PointSet* out,
+               std::vector<std::pair<int64_t, std::string>>* names_out) {
     std::string names;
     std::vector<int64_t> name_end, spans;
-    idx_.resize(std::max<size_t>(idx_.size(), 4096));
-    fv_.resize(idx_.size());
-    rp_.resize(std::max<size_t>(rp_.size(), 1025));
+    cv.idx.resize(std::max<size_t>(cv.idx.size(), 4096));
+    cv.fv.resize(cv.idx.size());
+    cv.rp.resize(std::max<size_t>(cv.rp.size(), 1025));
+    jb::HostFvWide& h = *cv.h;
     int rc;
     int64_t n = 0, slots = 0;
     for (;;) {
@@ -343,37 +357,75 @@ class Clustering : public HostEngine {
       names.clear();
       name_end.clear();
       spans.clear();
-      rp_[0] = 0;
-      hw_->set_sinks(&names, &name_end, &spans);
-      if (p_.global) hw_->begin();
-      rc = hw_->hash_body(body, len, idx_.data(), fv_.data(), rp_.data(), (int64_t)rp_.size() - 1,
-                          (int64_t)idx_.size(), &n, &slots, update);
-      hw_->set_sinks(nullptr, nullptr, nullptr);
-      if (rc != 0 && p_.global) hw_->rollback();   // a retry / a malformed body counts nothing
+      cv.rp[0] = 0;
+      h.set_sinks(&names, &name_end, &spans);
+      if (p_.global) h.begin();
+      rc = h.hash_body(body, len, cv.idx.data(), cv.fv.data(), cv.rp.data(), (int64_t)cv.rp.size() - 1,
+                       (int64_t)cv.idx.size(), &n, &slots, update);
+      h.set_sinks(nullptr, nullptr, nullptr);
+      if (rc != 0 && p_.global) h.rollback();   // a retry / a malformed body counts nothing
       if (rc != 2) break;
-      idx_.resize(idx_.size() * 4);
-      fv_.resize(idx_.size());
-      rp_.resize(rp_.size() * 4);
+      cv.idx.resize(cv.idx.size() * 4);
+      cv.fv.resize(cv.idx.size());
+      cv.rp.resize(cv.rp.size() * 4);
     }
     if (rc) return false;
     int64_t st = 0;
     for (int64_t s = 0; s < slots; ++s) {
-      const int64_t k = idx_[(size_t)s];
-      if (!names_.count(k)) names_[k] = names.substr((size_t)st, (size_t)(name_end[(size_t)s] - st));
+      const int64_t k = cv.idx[(size_t)s];
+      bool seen = false;   // (a body holds a handful of distinct keys)
+      for (const auto& kv : *names_out)
+        if (kv.first == k) { seen = true; break; }
+      if (!seen) names_out->emplace_back(k, names.substr((size_t)st, (size_t)(name_end[(size_t)s] - st)));
       st = name_end[(size_t)s];
       out->key.push_back(k);
-      out->val.push_back(fv_[(size_t)s]);
+      out->val.push_back(cv.fv[(size_t)s]);
     }
     const int64_t off = out->rp.back();
     for (int64_t i = 0; i < n; ++i) {
-      out->rp.push_back(off + rp_[(size_t)i + 1]);
+      out->rp.push_back(off + cv.rp[(size_t)i + 1]);
       out->w.push_back(1.0);
       out->raw.emplace_back((const char*)body + spans[2 * (size_t)i],
                             (size_t)(spans[2 * (size_t)i + 1] - spans[2 * (size_t)i]));
     }
     return true;
   }
+  // the engine's own converter (hw_: the document statistics hang off it)
+  bool convert(const uint8_t* body, size_t len, bool update, PointSet* out) {
+    main_.h = hw_.get();
+    std::vector<std::pair<int64_t, std::string>> nm;
+    if (!convert(main_, body, len, update, out, &nm)) return false;
+    for (auto& kv : nm)
+      if (!names_.count(kv.first)) names_[kv.first] = std::move(kv.second);
+    return true;
+  }
+  // converters for pushes hashed outside the model lock (no document
+  // statistics: p_.global is false), one per push in flight
+  std::unique_ptr<Conv> take_conv() {
+    {
+      std::lock_guard<std::mutex> g(conv_mu_);
+      if (!conv_pool_.empty()) {
+        std::unique_ptr<Conv> c = std::move(conv_pool_.back());
+        conv_pool_.pop_back();
+        return c;
+      }
+    }
+    std::unique_ptr<Conv> c(new Conv);
+    c->own.reset(new jb::HostFvWide((const uint8_t*)p_.s.data(), (int)p_.s.size(), (const uint8_t*)p_.n.data(),
+                                    (int)p_.n.size(), (const uint8_t*)p_.c.data(), (int)p_.c.size() / 2,
+                                    (const uint8_t*)p_.blob.data(), p_.blob.size(), kKeySpace));
+    c->own->set_ext(p_.ext);
+    c->h = c->own.get();
+    return c;
+  }
+  void give_conv(std::unique_ptr<Conv> c) {
+    std::lock_guard<std::mutex> g(conv_mu_);
+    conv_pool_.push_back(std::move(c));
+  }
 
+  // push: HostMethod::self_lock - without document statistics the points
+  // are hashed before the model lock (pushes in flight hash in parallel on
+  // the RPC workers while one closes a bucket), then appended under it
   void push_raw(const std::string& params, MsgpackWriter* w) {
     jb::Cursor c{(const uint8_t*)params.data(), (const uint8_t*)params.data() + params.size()};
     uint32_t two;
@@ -382,9 +434,30 @@ class Clustering : public HostEngine {
     if (!c.array(&two) || two != 2 || !c.raw(&nm, &nn)) throw std::invalid_argument("push");
     PointSet ps;
     auto t0 = Clock::now();
-    if (!convert(c.p, (size_t)(c.end - c.p), true, &ps)) throw std::invalid_argument("push: malformed points");
-    if (prof_.on) prof_.us[5] += since_us(t0);
-    t0 = Clock::now();
+    if (!p_.global && mu_ != nullptr) {
+      std::unique_ptr<Conv> cv = take_conv();
+      std::vector<std::pair<int64_t, std::string>> names;
+      const bool ok = convert(*cv, c.p, (size_t)(c.end - c.p), true, &ps, &names);
+      give_conv(std::move(cv));
+      if (!ok) throw std::invalid_argument("push: malformed points");
+      const double conv_us = since_us(t0);
+      std::unique_lock<std::shared_mutex> g(*mu_);
+      if (prof_.on) prof_.us[5] += conv_us;
+      for (auto& kv : names)
+        if (!names_.count(kv.first)) names_[kv.first] = std::move(kv.second);
+      append_points(std::move(ps));
+    } else {
+      std::unique_lock<std::shared_mutex> g;
+      if (mu_ != nullptr) g = std::unique_lock<std::shared_mutex>(*mu_);
+      if (!convert(c.p, (size_t)(c.end - c.p), true, &ps)) throw std::invalid_argument("push: malformed points");
+      if (prof_.on) prof_.us[5] += since_us(t0);
+      append_points(std::move(ps));
+    }
+    w->boolean(true);
+  }
+  // (model lock held) the points join the pending bucket; full buckets close
+  void append_points(PointSet&& ps) {
+    auto t0 = Clock::now();
     if (pending_.size() == 0) pending_ = std::move(ps);
     else pending_.append(ps);
     while ((int64_t)pending_.size() >= p_.bucket_size) {
@@ -404,7 +477,6 @@ class Clustering : public HostEngine {
       t0 = Clock::now();
     }
     if (prof_.on) prof_.us[6] += since_us(t0);
-    w->boolean(true);
   }
 
   // ---------------------------------------------------------- dense
@@ -971,9 +1043,10 @@ class Clustering : public HostEngine {
   std::vector<std::string> dims_;
   std::vector<int64_t> dim_keys_;
   std::vector<int32_t> assign_;
-  std::vector<int32_t> idx_;
-  std::vector<float> fv_;
-  std::vector<int64_t> rp_;
+  Conv main_;                       // hw_'s scratch (queries, pushes with statistics)
+  std::shared_mutex* mu_ = nullptr;  // the server's model lock (set_lock)
+  std::mutex conv_mu_;
+  std::vector<std::unique_ptr<Conv>> conv_pool_;
   Dev<float> dX_, dW_, dC_, dXn_, dCn_, dOut_, dScr_, dV_, dP_;
   Dev<double> dU_;
   Dev<int32_t> dI_, dA_;

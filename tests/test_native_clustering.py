@@ -170,3 +170,51 @@ def test_native_clustering_matches_python_driver(method, compressor, gw, tmp_pat
             if q is not None:
                 q.terminate()
                 q.wait(timeout=30)
+
+
+@pytest.mark.gpu
+def test_native_clustering_concurrent_pushes(tmp_path):
+    """pushes from several connections at once: each is hashed before the
+    model lock (jubaclustering.cpp push_raw, a pooled converter per push in
+    flight) and appended under it - every point lands once (pending + closed
+    buckets account for all of them) and the feature names stay whole"""
+    cfg = json.load(open(os.path.join(ROOT, "config", "clustering", "kmeans.json")))
+    cfg["parameter"]["bucket_size"] = 500
+    path = tmp_path / "kmeans.json"
+    path.write_text(json.dumps(cfg))
+    p, port = _start(tmp_path, path)
+    try:
+        import threading
+        errs = []
+
+        def worker(seed):
+            rng = random.Random(seed)
+            try:
+                with RpcClient("127.0.0.1", port, 60.0) as c:
+                    for _ in range(15):
+                        assert c.call("push", "", [_datum(rng, rng.randrange(3)) for _ in range(70)]) is True
+            except Exception as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+
+        ts = [threading.Thread(target=worker, args=(s,)) for s in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+        total = 6 * 15 * 70
+        with RpcClient("127.0.0.1", port, 60.0) as c:
+            (_, st), = c.call("get_status", "").items()
+            st = {_s(k): _s(v) for k, v in st.items()}
+            assert int(st["pending"]) == total % 500
+            assert int(st["revision"]) >= 1
+            centers = c.call("get_k_center", "")
+            assert len(centers) == 3
+            for cen in centers:   # whole feature names, finite values
+                names = {_s(k) for k, _ in cen[1]}
+                assert {"x@num", "y@num"} <= names, names
+                assert names <= {"x@num", "y@num"} | {f"tag${t}@str#bin/bin" for t in "abc"}, names
+                assert all(math.isfinite(float(v)) for _, v in cen[1])
+    finally:
+        p.terminate()
+        p.wait(timeout=30)
