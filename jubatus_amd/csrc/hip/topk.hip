@@ -794,7 +794,7 @@ __global__ __launch_bounds__(kMqT) void topk_mq_kernel(const TopkSrc s, int nq, 
   const float hn = (float)s.hash_num;
   if (EUC)
     for (int h = t; h <= s.hash_num && h <= 64 * W; h += kMqT) s_lut[h] = __cosf(3.14159265f * ((float)h / hn));
-  if (t < NQ) s_blk[t] = t < nq ? lim_in[q0 + t] : 0u;
+  if (t < NQ) s_blk[t] = t < nq ? (lim_in != nullptr ? lim_in[q0 + t] : 0xffffffffu) : 0u;   // (null: no bound)
   if (t < NQ * W) {
     const int q = t / W, w = t % W;
     s_qb[q][w] = q < nq ? s.qbits[(int64_t)(q0 + q) * s.words + w] : 0ull;
@@ -1335,19 +1335,37 @@ inline int mq_stats_on() {
 // query's wave a pass; measured profiles/r5_topk_mq_ab.md)
 inline int mq_sample_segments(int nq) { return nq >= 4 ? kMqSampSegMax : kMqSampSegMax / 2; }
 
+// The sample launch is skipped for one query: the scan starts without a
+// bound (each wave's first chunk is cut at the k-th of its lanes' minima, a
+// full 32-bit radix select for euclid_lsh's float keys). Measured, 10M
+// rows, k 10: one lsh query 44.5 -> 42.8 us, one euclid_lsh query 62.6 ->
+// 54.4 us without the sample; eight lsh queries 72.9 -> 129.8 us (every
+// wave's eight first-chunk cuts), so several queries keep it.
+// JB_TOPK_MQ_SAMPLE=1: always (A/B runs)
+inline bool mq_sample_on(int nq) {
+  static const bool forced = [] {
+    const char* e = getenv("JB_TOPK_MQ_SAMPLE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return forced || nq >= 2;
+}
+
 template <int W, int NQ>
 inline void launch_mq_nq(const TopkSrc& s, int blocks, int nq, int q0, int64_t nrows, int64_t per_block, int k,
                          uint32_t* lim, float* out_d, int32_t* out_i, hipStream_t stream) {
+  const bool samp = mq_sample_on(nq);
   if (s.metric == 1) {
-    hipLaunchKernelGGL((topk_mq_sample_kernel<W, true>), dim3(nq), dim3(kMqSampT), 0, stream, s, q0, nrows, k,
-                       mq_sample_segments(nq), lim);
+    if (samp)
+      hipLaunchKernelGGL((topk_mq_sample_kernel<W, true>), dim3(nq), dim3(kMqSampT), 0, stream, s, q0, nrows, k,
+                         mq_sample_segments(nq), lim);
     hipLaunchKernelGGL((topk_mq_kernel<W, NQ, true>), dim3(blocks), dim3(kMqT), 0, stream, s, nq, q0, nrows,
-                       per_block, k, lim, mq_stats_on(), out_d, out_i);
+                       per_block, k, samp ? lim : nullptr, mq_stats_on(), out_d, out_i);
   } else {
-    hipLaunchKernelGGL((topk_mq_sample_kernel<W, false>), dim3(nq), dim3(kMqSampT), 0, stream, s, q0, nrows, k,
-                       mq_sample_segments(nq), lim);
+    if (samp)
+      hipLaunchKernelGGL((topk_mq_sample_kernel<W, false>), dim3(nq), dim3(kMqSampT), 0, stream, s, q0, nrows, k,
+                         mq_sample_segments(nq), lim);
     hipLaunchKernelGGL((topk_mq_kernel<W, NQ, false>), dim3(blocks), dim3(kMqT), 0, stream, s, nq, q0, nrows,
-                       per_block, k, lim, mq_stats_on(), out_d, out_i);
+                       per_block, k, samp ? lim : nullptr, mq_stats_on(), out_d, out_i);
   }
 }
 

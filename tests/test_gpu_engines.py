@@ -240,6 +240,10 @@ def test_default_clustering_config_runs_on_device(method):
                                                     # queries, euclid_lsh with 2 words, a partial last chunk
                                                     (0, 10, 2_200_000, 1, 64), (0, 10, 2_300_000, 8, 64),
                                                     (1, 16, 2_500_000, 3, 128), (2, 5, 2_100_007, 2, 64),
+                                                    # one query: no sample launch (the scan starts
+                                                    # unbounded, first chunks cut in the kernel)
+                                                    (1, 10, 2_400_000, 1, 64), (1, 32, 2_200_000, 1, 128),
+                                                    (2, 10, 2_100_000, 1, 64), (0, 32, 2_300_000, 1, 128),
                                                     (1, 16, 500_000, 12, 128), (2, 32, 300_000, 16, 64)])
 def test_topk_hamming_matches_full_sort(metric, k, nrows, nq, bits):
     """csrc/hip/topk.hip (fused scan + exact top-k) == full distance matrix
@@ -272,9 +276,18 @@ def test_topk_hamming_matches_full_sort(metric, k, nrows, nq, bits):
         order = np.argsort(full[q], kind="stable")[:k]
         ref = full[q][order]
         fin = np.isfinite(ref)
-        np.testing.assert_array_equal(oi[q][:fin.sum()], order[fin])
-        np.testing.assert_allclose(od[q][:fin.sum()], ref[fin], rtol=1e-6)
-        assert np.all(np.isinf(od[q][fin.sum():]))
+        nf = int(fin.sum())
+        if metric == 1:
+            # euclid_lsh distances are float expressions: two kernels may round
+            # a near tie (measured: 2.4e-7 apart at 1.409) either way, so the
+            # rows must carry the k smallest distances, in order, each once
+            got = oi[q][:nf]
+            assert len(set(got.tolist())) == nf
+            np.testing.assert_allclose(full[q][got], ref[fin], rtol=1e-6)
+        else:
+            np.testing.assert_array_equal(oi[q][:nf], order[fin])
+        np.testing.assert_allclose(od[q][:nf], ref[fin], rtol=1e-6)
+        assert np.all(np.isinf(od[q][nf:]))
 
 
 @pytest.mark.parametrize("k", [1, 10, 31, 100])
