@@ -1115,18 +1115,20 @@ class RowEngine {
              bool bump) {
     std::vector<int32_t> fi;
     std::vector<float> fv;
+    fi.reserve(idx.size());
+    fv.reserve(idx.size());
     for (size_t i = 0; i < idx.size(); ++i)
       if (idx[i] >= 0) { fi.push_back(idx[i]); fv.push_back(val[i]); }
     const int32_t s = assign(id);
     Row& r = rows_[(size_t)s];
     r.d = std::move(d);
-    r.idx = fi;
-    r.val = fv;
+    r.idx = std::move(fi);
+    r.val = std::move(fv);
     r.live = true;
     if (bump) {
       version_[id] += 1;
       dirty_.insert(id);
-      removed_.erase(id);
+      if (!removed_.empty()) removed_.erase(id);
     }
     if (lsh_) lsh_->set(s, idx, val);
     else pool_->set(s, idx, val);

@@ -463,7 +463,7 @@ class Model : public jb::mix::Mixable {
   // or the exception it raised
   // a write decoded and hashed on the RPC IO thread (prep_write)
   struct PrepWrite {
-    std::shared_ptr<const jb::HostFvHasher> h;   // the hasher it used
+    std::shared_ptr<const jb::HostFvHasher> h;   // the hasher it used (null: parsed only)
     std::string id;
     Datum d;
     std::vector<int32_t> idx;
@@ -477,12 +477,12 @@ class Model : public jb::mix::Mixable {
     std::exception_ptr err;
   };
   // IO thread, no model lock (the hasher is an immutable snapshot): decode
-  // an update_row / set_row and hash its datum as a row of its own; null
-  // when the converter keeps statistics or the request is not well formed
-  // (the batch path decodes it again and answers the error)
+  // an update_row / set_row and hash its datum as a row of its own - or only
+  // decode it when the converter keeps statistics (they change under the
+  // lock); null when the request is not well formed (the batch path decodes
+  // it again and answers the error)
   std::shared_ptr<PrepWrite> prep_write(const std::string& params) const {
     std::shared_ptr<const jb::HostFvHasher> h = std::atomic_load(&prep_h_);
-    if (!h) return nullptr;
     try {
       Value a = MsgpackReader((const uint8_t*)params.data(), params.size()).read();
       if (a.kind != Value::ARR || a.a.size() != 3 || !a.a[0].is_str() || !a.a[1].is_str() ||
@@ -490,9 +490,11 @@ class Model : public jb::mix::Mixable {
         return nullptr;
       auto p = std::make_shared<PrepWrite>();
       jb::row::parse_datum(a.a[2], &p->d);
-      MsgpackWriter w;
-      jb::row::write_datum(w, p->d);
-      jb::row::Converter::hash_with(*h, (const uint8_t*)w.out.data(), w.out.size(), &p->idx, &p->val);
+      if (h) {
+        MsgpackWriter w;
+        jb::row::write_datum(w, p->d);
+        jb::row::Converter::hash_with(*h, (const uint8_t*)w.out.data(), w.out.size(), &p->idx, &p->val);
+      }
       p->id = std::move(a.a[1].s);
       p->h = std::move(h);
       return p;
@@ -517,7 +519,7 @@ class Model : public jb::mix::Mixable {
         try {
           if (PrepWrite* p = ws[i].pre) {
             ds[i] = std::move(p->d);
-            if (p->h == h) {
+            if (p->h != nullptr && p->h == h) {
               hi[i] = std::move(p->idx);
               hv[i] = std::move(p->val);
               pre[i] = 1;
