@@ -63,12 +63,16 @@ def _pipelined_adds(port, datums):
     return [got[i] for i in range(len(datums))]
 
 
-@pytest.mark.parametrize("name", ["lof.json", "light_lof.json"])
-def test_batched_adds_equal_sequential_adds(name, tmp_path):
+@pytest.mark.parametrize("name,k,rnn", [("lof.json", 5, 12), ("light_lof.json", 5, 12),
+                                        # k > 16 (the LDS list edits), more than 64 candidates
+                                        ("lof.json", 20, 70)])
+def test_batched_adds_equal_sequential_adds(name, k, rnn, tmp_path):
+    """(the batch thread stages each chunk of 8 adds while the previous
+    chunk's kernel runs: Model::add_many's pipeline keeps the arrival order)"""
     cfg = json.load(open(config_path(f"anomaly/{name}")))
     if "nearest_neighbor_num" in cfg.get("parameter", {}):
-        cfg["parameter"]["nearest_neighbor_num"] = 5
-        cfg["parameter"]["reverse_nearest_neighbor_num"] = 12
+        cfg["parameter"]["nearest_neighbor_num"] = k
+        cfg["parameter"]["reverse_nearest_neighbor_num"] = rnn
     path = tmp_path / name
     path.write_text(json.dumps(cfg))
     for sub in ("a", "b"):
