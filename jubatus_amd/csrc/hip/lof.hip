@@ -709,12 +709,21 @@ __global__ __launch_bounds__(64) void lof_add_batch_kernel(
     uint8_t* __restrict__ lrd_ok, int32_t* __restrict__ changed, int32_t* __restrict__ nchanged,
     uint32_t* __restrict__ kstamp, uint32_t* __restrict__ lstamp, uint32_t epoch0, int32_t* __restrict__ cand,
     uint32_t* __restrict__ res, uint32_t* __restrict__ out, int out_stride, int max_missing,
-    unsigned long long* __restrict__ prof) {
+    unsigned long long* __restrict__ prof, uint32_t* __restrict__ chain) {
   __shared__ int32_t cs[kLofArgMax];
   __shared__ float cd[kLofArgMax];
   __shared__ int32_t s_p[64], s_n[64];
   __shared__ LofLds L;
   const int t = threadIdx.x;
+  // chain (optional): set when a batch stops; a batch queued behind a stopped
+  // one does not run (status 3 for every add: the host reruns it after
+  // installing the missing lists and clearing the word)
+  if (chain != nullptr && chain[0] != 0u) {
+    for (int i = t; i < nadd - 1; i += blockDim.x) sys_store(out + (int64_t)i * out_stride, 3u);
+    sys_stores_block_done();
+    if (t == 0) sys_store(out + (int64_t)(nadd - 1) * out_stride, 3u);
+    return;
+  }
   const int tot = nadd * stride;
   float* cand_d = reinterpret_cast<float*>(cand + tot);
   for (int e0 = t; e0 < tot; e0 += 64 * kLofU) {  // one pass over host memory, kLofU loads in flight
@@ -755,6 +764,7 @@ __global__ __launch_bounds__(64) void lof_add_batch_kernel(
     lof_stamp(L, 6);
     if (L.nmiss > 0) { ran = i + 1; break; }      // stopped: the later adds did not run
   }
+  if (chain != nullptr && t == 0 && L.nmiss > 0) chain[0] = 1u;   // (the next batch on the stream sees it)
   // results to the host: every word but the statuses, acknowledged, then the
   // statuses (the last add's last: the host waits for it)
   const int nm = L.nmiss > 0 ? (L.nmiss < max_missing ? L.nmiss : max_missing) : 0;
@@ -881,13 +891,16 @@ extern "C" int jb_lof_add(int p, const int32_t* cs, const float* cd, int nc, int
 // before they go to the host); out_host[i * out_stride] = status 1
 // done, 2 stopped on rows without a valid list (its insert is applied, its
 // score is not), 3 not run. wait = 0: return once launched (the caller
-// overlaps other work, then jb_lof_add_many_wait).
+// overlaps other work, then jb_lof_add_many_wait). chain (optional device
+// word): a batch sets it when it stops, and a batch that finds it set does
+// not run - batches queued back to back keep their order.
 extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float* cd,
                                const int32_t* nc, int stride, int k, int ignore_same, int32_t* nb_slot,
                                float* nb_dist, float* kdist, uint8_t* ok, float* lrd, uint8_t* lrd_ok,
                                int32_t* changed, int32_t* nchanged, uint32_t* kstamp, uint32_t* lstamp,
                                uint32_t epoch0, int32_t* cand, uint32_t* res, uint32_t* out_host, int out_stride,
-                               int max_missing, unsigned long long* prof, hipStream_t stream, int wait) {
+                               int max_missing, unsigned long long* prof, hipStream_t stream, int wait,
+                               uint32_t* chain) {
   if (nadd <= 0) return 0;
   if (nadd > 64 || k <= 0 || k > jb::kLofMaxK || stride > jb::kLofArgMax || kstamp == nullptr ||
       lstamp == nullptr)
@@ -898,7 +911,7 @@ extern "C" int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, c
   }
   hipLaunchKernelGGL(jb::lof_add_batch_kernel, dim3(1), dim3(64), 0, stream, nadd, ps, nc, cs, cd, stride, k,
                      ignore_same, nb_slot, nb_dist, kdist, ok, lrd, lrd_ok, changed, nchanged, kstamp, lstamp,
-                     epoch0, cand, res, out_host, out_stride, max_missing, prof);
+                     epoch0, cand, res, out_host, out_stride, max_missing, prof, chain);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   return wait ? jb::wait_nonzero(out_host + (int64_t)(nadd - 1) * out_stride, stream) : 0;

@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 #include <vector>
 
 #include "jb_server_common.hpp"
@@ -37,7 +38,7 @@ int jb_lof_add_many(int nadd, const int32_t* ps, const int32_t* cs, const float*
                     uint8_t* ok, float* lrd, uint8_t* lrd_ok, int32_t* changed, int32_t* nchanged,
                     uint32_t* kstamp, uint32_t* lstamp, uint32_t epoch0, int32_t* cand, uint32_t* res,
                     uint32_t* out_host, int out_stride, int max_missing, unsigned long long* prof,
-                    hipStream_t stream, int wait);
+                    hipStream_t stream, int wait, uint32_t* chain);
 int jb_lof_add_many_wait(int nadd, uint32_t* out_host, int out_stride, hipStream_t stream);
 int jb_lof_score_st(const int32_t* ts, const float* td, int nt, int k, const int32_t* nb_slot,
                     const float* nb_dist, const float* kdist, const uint8_t* ok, float* lrd, uint8_t* lrd_ok,
@@ -73,16 +74,20 @@ class LofState {
     nchanged_.get(1);
     cand_.get(2 * (size_t)kLofBatchMax * kLofArgMax);
     res_.get((size_t)kLofBatchMax * kOutStride);
-    stage_ = (int32_t*)jb_host_alloc(4 * (2 * (size_t)kLofBatchMax + 2 * (size_t)kLofBatchMax * kLofArgMax));
+    stage_ = (int32_t*)jb_host_alloc(4 * 2 * kStageWords);            // two batches in flight
     if (!stage_) throw std::runtime_error("hipHostMalloc failed");
-    out_many_ = (uint32_t*)jb_host_alloc(4 * (size_t)kOutStride * kLofBatchMax);
+    out_many_ = (uint32_t*)jb_host_alloc(4 * 2 * (size_t)kOutStride * kLofBatchMax);
     if (!out_many_) throw std::runtime_error("hipHostMalloc failed");
+    chain_.get(1);
+    HIPCHK(hipMemsetAsync(chain_.p, 0, 4, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
   }
 
   ~LofState() {
     for (void* q : {(void*)nb_slot_.p, (void*)nb_dist_.p, (void*)kdist_.p, (void*)lrd_.p, (void*)ok_.p,
                     (void*)lrd_ok_.p, (void*)kstamp_.p, (void*)lstamp_.p, (void*)changed_.p, (void*)nchanged_.p,
-                    (void*)up_[0].p, (void*)up_[1].p, (void*)up_[2].p, (void*)cand_.p, (void*)res_.p})
+                    (void*)up_[0].p, (void*)up_[1].p, (void*)up_[2].p, (void*)cand_.p, (void*)res_.p,
+                    (void*)chain_.p})
       if (q) (void)hipFree(q);
     if (out_) jb_host_free(out_);
     if (out_many_) jb_host_free(out_many_);
@@ -131,23 +136,28 @@ class LofState {
     return finish_many(scores, missing);
   }
 
-  // add_many in two halves: the launch returns at once (the host stages the
-  // next batch meanwhile - the batch's kernel is one wave), finish_many waits
-  // for it and reads the results. The staging the kernel reads is rewritten
-  // only by the next launch, after the finish.
+  // add_many in two halves: the launch returns at once, finish_many waits for
+  // the oldest batch in flight and reads its results. Up to two batches in
+  // flight, queued back to back on the stream (the second starts the moment
+  // the first ends, no host round trip between them), each with its own
+  // pinned staging and results. A batch that stops (rows without a valid
+  // list) sets the chain word, so the batch queued behind it does not run:
+  // finish_many then drains it (*dropped = 1: the caller reruns it) and
+  // clears the word.
   void launch_many(const std::vector<int32_t>& ps, const std::vector<std::vector<int32_t>>& cs,
                    const std::vector<std::vector<float>>& cd) {
     const size_t n = ps.size();
-    if (launched_ != 0) throw std::logic_error("lof launch_many: the previous batch is not finished");
+    if (fl_.size() >= 2) throw std::logic_error("lof launch_many: two batches in flight");
     if (n == 0) return;
     if (n > (size_t)kLofBatchMax) throw std::runtime_error("lof add_many: batch too large");
     int stride = 1;
     for (const auto& c : cs) stride = std::max(stride, (int)c.size());
     if (stride > kLofArgMax) throw std::runtime_error("lof add_many: too many candidates");
+    const int buf = fl_.empty() ? 0 : 1 - fl_.front().buf;
     // pinned staging the kernel reads: ps [64], nc [64], cs [n][stride], cd [n][stride]
-    int32_t* hps = stage_;
-    int32_t* hnc = stage_ + kLofBatchMax;
-    int32_t* hcs = stage_ + 2 * kLofBatchMax;
+    int32_t* hps = stage_ + (size_t)buf * kStageWords;
+    int32_t* hnc = hps + kLofBatchMax;
+    int32_t* hcs = hps + 2 * kLofBatchMax;
     float* hcd = reinterpret_cast<float*>(hcs + n * (size_t)stride);
     for (size_t i = 0; i < n; ++i) {
       hps[i] = ps[i];
@@ -161,23 +171,29 @@ class LofState {
     }
     const uint32_t epoch0 = epoch_ + 1;
     epoch_ += (uint32_t)n;            // (adds after a stop leave gaps: stamps only need to grow)
+    uint32_t* out = out_many_ + (size_t)buf * kOutStride * kLofBatchMax;
     const int rc = jb_lof_add_many((int)n, hps, hcs, hcd, hnc, stride, k_, ignore_ ? 1 : 0, nb_slot_.p, nb_dist_.p,
                                    kdist_.p, ok_.p, lrd_.p, lrd_ok_.p, changed_.p, nchanged_.p, kstamp_.p, lstamp_.p,
-                                   epoch0, cand_.p, res_.p, out_many_, kOutStride, kLofMaxMissing, nullptr, stream_,
-                                   0);
+                                   epoch0, cand_.p, res_.p, out, kOutStride, kLofMaxMissing, nullptr, stream_, 0,
+                                   chain_.p);
     if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
-    launched_ = n;
+    fl_.push_back({n, buf});
   }
-  bool in_flight() const { return launched_ != 0; }
-  size_t finish_many(std::vector<float>* scores, std::vector<int32_t>* missing) {
-    const size_t n = launched_;
-    launched_ = 0;
+  bool in_flight() const { return !fl_.empty(); }
+  size_t finish_many(std::vector<float>* scores, std::vector<int32_t>* missing, size_t* dropped = nullptr) {
+    if (dropped) *dropped = 0;
     scores->clear();
-    if (n == 0) return 0;
-    const int rc = jb_lof_add_many_wait((int)n, out_many_, kOutStride, stream_);
-    if (rc != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
-    for (size_t i = 0; i < n; ++i) {
-      const uint32_t* o = out_many_ + i * kOutStride;
+    if (fl_.empty()) return 0;
+    const Flight f = fl_.front();
+    fl_.pop_front();
+    const uint32_t* out = out_many_ + (size_t)f.buf * kOutStride * kLofBatchMax;
+    const int rc = jb_lof_add_many_wait((int)f.n, const_cast<uint32_t*>(out), kOutStride, stream_);
+    if (rc != 0) {
+      fl_.clear();
+      throw std::runtime_error("lof add_many failed: " + std::to_string(rc));
+    }
+    for (size_t i = 0; i < f.n; ++i) {
+      const uint32_t* o = out + i * kOutStride;
       const uint32_t st = ((volatile const uint32_t*)o)[0];
       if (st == 1) {
         float sc;
@@ -192,9 +208,19 @@ class LofState {
         const int32_t s = (int32_t)o[4 + j];
         if (std::find(missing->begin(), missing->end(), s) == missing->end()) missing->push_back(s);
       }
+      // the batches queued behind did not run: wait for them, clear the word
+      while (!fl_.empty()) {
+        const Flight g = fl_.front();
+        fl_.pop_front();
+        const int rw = jb_lof_add_many_wait((int)g.n, out_many_ + (size_t)g.buf * kOutStride * kLofBatchMax,
+                                            kOutStride, stream_);
+        if (rw != 0) throw std::runtime_error("lof add_many failed: " + std::to_string(rw));
+        if (dropped) ++*dropped;
+      }
+      HIPCHK(hipMemsetAsync(chain_.p, 0, 4, stream_));
       return i;
     }
-    return n;
+    return f.n;
   }
 
   bool score(const std::vector<int32_t>& ts, const std::vector<float>& td, int32_t store, float* sc,
@@ -337,7 +363,13 @@ class LofState {
   bool ignore_;
   hipStream_t stream_;
   int64_t cap_ = 0;
-  size_t launched_ = 0;   // adds of the launch_many in flight
+  struct Flight {
+    size_t n;   // adds
+    int buf;    // staging / results buffer
+  };
+  std::deque<Flight> fl_;   // launch_many batches in flight, oldest first
+  static constexpr size_t kStageWords = 2 * (size_t)kLofBatchMax + 2 * (size_t)kLofBatchMax * kLofArgMax;
+  DevBuf<uint32_t> chain_;  // set by a batch that stops (lof_add_batch_kernel)
   DevBuf<int32_t> nb_slot_;
   DevBuf<float> nb_dist_, kdist_, lrd_;
   DevBuf<uint8_t> ok_, lrd_ok_;

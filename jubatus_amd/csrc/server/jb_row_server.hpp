@@ -659,11 +659,11 @@ class Model : public jb::mix::Mixable {
         if (!rs[i].err && !rs[i].scored) rs[i].err = std::current_exception();
     };
     std::unique_ptr<AddChunk> prev;
-    auto finish_prev = [&](const std::vector<int32_t>& later) {
+    auto finish_prev = [&](const std::vector<int32_t>& later, AddChunk* next) {
       if (!prev) return;
       const auto t0 = Clk::now();
       try {
-        finish_chunk(rs, *prev, later);
+        finish_chunk(rs, *prev, later, next);
       } catch (...) {
         fail(prev->idx);
       }
@@ -675,7 +675,7 @@ class Model : public jb::mix::Mixable {
       std::unique_ptr<AddChunk> cur(new AddChunk);
       cur->idx.assign(todo.begin() + c0, todo.begin() + c1);
       if (!batchable(cur->idx.size())) {
-        finish_prev({});
+        finish_prev({}, nullptr);
         try {
           for (size_t i : cur->idx) {
             ++update_count;
@@ -698,17 +698,31 @@ class Model : public jb::mix::Mixable {
       }
       ab_us_[0] += us(t0, Clk::now());
       ++ab_chunks_;
-      finish_prev(ok ? cur->slots : std::vector<int32_t>());
-      if (!ok) continue;
+      if (!ok) {
+        finish_prev({}, nullptr);
+        continue;
+      }
+      // a previous chunk whose batch did not run (queued behind one that
+      // stopped) reruns first, alone: nothing may queue ahead of its adds
+      if (prev && !prev->launched) finish_prev(cur->slots, nullptr);
+      // queued behind the previous chunk's kernel: it starts when that one
+      // ends (or does not run if that one stops - finish_chunk reruns it)
+      std::exception_ptr lerr;
       try {
         state().launch_many(cur->slots, cur->cs, cur->cd);
         cur->launched = true;
-        prev = std::move(cur);
       } catch (...) {
-        fail(cur->idx);
+        lerr = std::current_exception();
       }
+      finish_prev(cur->slots, cur.get());
+      if (lerr) {
+        for (size_t i : cur->idx)
+          if (!rs[i].err && !rs[i].scored) rs[i].err = lerr;
+        continue;
+      }
+      prev = std::move(cur);
     }
-    finish_prev({});
+    finish_prev({}, nullptr);
   }
   // update merges into the stored datum, overwrite replaces it
   double update(const std::string& id, const Value& dv, bool merge) {
@@ -1337,7 +1351,9 @@ class Model : public jb::mix::Mixable {
   }
   // the LOF adds of a prepared chunk (the first launch may be in flight);
   // later: rows set by the next chunk already, not added yet
-  void finish_chunk(std::vector<AddReq>& rs, AddChunk& ch, const std::vector<int32_t>& later) {
+  // next: the chunk queued behind this one (its batch does not run when
+  // this one stops: it is marked for a rerun)
+  void finish_chunk(std::vector<AddReq>& rs, AddChunk& ch, const std::vector<int32_t>& later, AddChunk* next) {
     const size_t B = ch.idx.size();
     jb::row::LofState& st = state();
     size_t j = 0;
@@ -1347,7 +1363,9 @@ class Model : public jb::mix::Mixable {
       size_t m;
       if (ch.launched) {
         ch.launched = false;
-        m = st.finish_many(&sc, &missing);
+        size_t dropped = 0;
+        m = st.finish_many(&sc, &missing, &dropped);
+        if (dropped > 0 && next != nullptr) next->launched = false;
       } else {
         std::vector<int32_t> ps(ch.slots.begin() + j, ch.slots.end());
         std::vector<std::vector<int32_t>> c(ch.cs.begin() + j, ch.cs.end());

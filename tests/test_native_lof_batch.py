@@ -100,3 +100,45 @@ def test_batched_adds_equal_sequential_adds(name, k, rnn, tmp_path):
         for p in (pa, pb):
             p.terminate()
             p.wait(timeout=30)
+
+
+def test_batched_adds_after_removals_equal_sequential_adds(tmp_path):
+    """rows removed between two add streams leave rows without a valid list
+    behind: batched adds then stop on them (status 2) - the chunk queued
+    behind a stopped one does not run and is rerun after the lists are
+    installed (LofState::finish_many, Model::add_many) - and the ids and
+    scores must still be those of the adds one by one"""
+    cfg = json.load(open(config_path("anomaly/lof.json")))
+    cfg["parameter"]["nearest_neighbor_num"] = 5
+    cfg["parameter"]["reverse_nearest_neighbor_num"] = 12
+    path = tmp_path / "lof.json"
+    path.write_text(json.dumps(cfg))
+    for sub in ("a", "b"):
+        (tmp_path / sub).mkdir()
+    rng = random.Random(13)
+
+    def datums(n):
+        return [[[["tag", f"t{rng.randrange(5)}"]],
+                 [["x", round(rng.gauss(0, 1), 4)], ["y", round(rng.gauss(0, 1), 4)]], []] for _ in range(n)]
+
+    first, second = datums(400), datums(400)
+    drop = [str(i) for i in rng.sample(range(400), 60)]
+    (pa, porta), (pb, portb) = _start(str(path), tmp_path / "a"), _start(str(path), tmp_path / "b")
+    try:
+        with RpcClient("127.0.0.1", porta, 60.0) as a, RpcClient("127.0.0.1", portb, 60.0) as b:
+            seq = [a.call("add", "", d) for d in first]
+            bat = _pipelined_adds(portb, first)
+            for rid in drop:
+                assert a.call("clear_row", "", rid) == b.call("clear_row", "", rid)
+            seq += [a.call("add", "", d) for d in second]
+        bat += _pipelined_adds(portb, second)
+        assert len(seq) == len(bat)
+        for (ia, sa), (ib, sb) in zip(seq, bat):
+            ia = ia.decode() if isinstance(ia, bytes) else ia
+            ib = ib.decode() if isinstance(ib, bytes) else ib
+            assert ia == ib
+            assert sa == pytest.approx(sb, rel=1e-5, abs=1e-5) or (sa == sb)
+    finally:
+        for p in (pa, pb):
+            p.terminate()
+            p.wait(timeout=30)

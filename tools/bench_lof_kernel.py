@@ -59,7 +59,7 @@ def main():
     lib = hip.hip_lib()
     f = lib.jb_lof_add_many
     P, I, U = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32
-    f.argtypes = [I, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, U, P, P, P, I, I, P, P]
+    f.argtypes = [I, P, P, P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, U, P, P, P, I, I, P, P, I, P]
     f.restype = I
     rng = np.random.default_rng(1)
     hps = stage.view(np.int32, 64)
@@ -84,7 +84,7 @@ def main():
                nb_slot.data_ptr(), nb_dist.data_ptr(), kdist.data_ptr(), ok.data_ptr(), lrd.data_ptr(),
                lrd_ok.data_ptr(), changed.data_ptr(), nchanged.data_ptr(), kstamp.data_ptr(), lstamp.data_ptr(),
                epoch, cand.data_ptr(), res.data_ptr(), out.ptr, stride_out, 1024,
-               prof.data_ptr() if b >= 5 else None, hip._stream())
+               prof.data_ptr() if b >= 5 else None, hip._stream(), 1, None)
         times.append(time.perf_counter() - t0)
         epoch += B
         if rc != 0:
