@@ -133,6 +133,13 @@ class RpcServer:
         self._batch[name] = fn
         self._srv.set_batch(sorted(self._batch), self._dispatch_batch)
 
+    def set_ordered(self, names: list[str]) -> None:
+        """Batched methods that write: a batch never takes a request past one
+        of another method when either is one of these (pipelined writes of
+        different methods apply in arrival order; reads still batch past
+        reads). Register before start()."""
+        self._srv.set_ordered(sorted(names))
+
     def set_arena(self, name: str, slots: list[int], slot_bytes: int, fn: Callable) -> None:
         """Arena batching (csrc/native/jb_rpc.cpp): the IO threads copy each
         ``name`` request's body (params [cluster name, body]) into one of the

@@ -231,6 +231,7 @@ class PyRpcServer {
   }
   void set_io_threads(int n) { srv_->set_io_threads(n); }
   void set_batch_threads(int n) { srv_->set_batch_threads(n); }
+  void set_ordered(std::vector<std::string> methods) { srv_->set_ordered(methods); }
   int listen(const std::string& addr, int port) { return srv_->listen(addr, port); }
   void start() { srv_->start(); }
   void stop() {
@@ -471,6 +472,7 @@ PYBIND11_MODULE(_jubatus_native, m) {
       .def("set_max_message", &PyRpcServer::set_max_message)
       .def("set_io_threads", &PyRpcServer::set_io_threads)
       .def("set_batch_threads", &PyRpcServer::set_batch_threads)
+      .def("set_ordered", &PyRpcServer::set_ordered, py::arg("methods"))
       .def("arena_ns", &PyRpcServer::arena_ns)
       .def("listen", &PyRpcServer::listen)
       .def("start", &PyRpcServer::start)

@@ -192,6 +192,58 @@ def test_transport_batching_merges_concurrent_requests():
         srv.stop()
 
 
+def test_batches_keep_arrival_order_around_writes():
+    """csrc/native/jb_rpc.cpp set_ordered: pipelined requests of batched
+    methods on one connection - a batch of a write never takes a request
+    past one of another method, no batch takes a request past a write;
+    reads may still batch past other reads"""
+    import time as _t
+
+    from jubatus_amd.common.mprpc import RpcServer
+
+    seen = []
+    lock = threading.Lock()
+
+    def mk(name):
+        def fn(params_list):
+            with lock:
+                seen.extend((name, msgpack.unpackb(p)[0]) for p in params_list)
+            _t.sleep(0.002)          # (requests pile up behind the batch)
+            return [0] * len(params_list)
+        return fn
+
+    srv = RpcServer(nthreads=2)
+    for m in ("w1", "w2", "r1", "r2"):
+        srv.add_batch(m, mk(m))
+    srv.set_ordered(["w1", "w2"])
+    port = srv.listen(0, "127.0.0.1")
+    srv.start()
+    try:
+        rng = __import__("random").Random(3)
+        calls = [(rng.choice(["w1", "w2", "r1", "r2", "w1"]), i) for i in range(400)]
+        s = socket.create_connection(("127.0.0.1", port))
+        s.sendall(b"".join(msgpack.packb([0, i, m, [i]]) for m, i in calls))
+        up = msgpack.Unpacker(raw=False)
+        got = set()
+        while len(got) < len(calls):
+            chunk = s.recv(1 << 16)
+            assert chunk
+            up.feed(chunk)
+            for msg in up:
+                got.add(msg[1])
+        s.close()
+        assert len(seen) == len(calls)
+        pos = {i: n for n, (_, i) in enumerate(seen)}
+        writes = [i for m, i in calls if m.startswith("w")]
+        # every write keeps its place against every other request
+        for _, i in calls:
+            for w in writes:
+                if i != w:
+                    assert (pos[i] < pos[w]) == (i < w), (i, w)
+    finally:
+        srv.stop()
+
+
 @pytest.mark.parametrize("name", ["", "c", "x" * 40, "y" * 300])
 def test_name_and_rest(name):
     from jubatus_amd.common.mprpc import ArgumentError, name_and_rest
