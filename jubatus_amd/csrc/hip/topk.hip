@@ -1314,6 +1314,17 @@ inline int scan_waves(int k, int nq, int64_t nrows) {
 // profiles/r02_lsh_merge_ab.jsonl)
 
 // JB_TOPK_MQ=0 turns the register multi-query scan off (A/B runs)
+// JB_TOPK_MQ_MIN_ROWS: the table size from which the multi-query scan runs
+// (kMqMinRows; A/B runs)
+inline int64_t mq_min_rows() {
+  static const int64_t v = [] {
+    const char* e = getenv("JB_TOPK_MQ_MIN_ROWS");
+    const long long x = e != nullptr ? atoll(e) : 0;
+    return x > 0 ? (int64_t)x : kMqMinRows;
+  }();
+  return v;
+}
+
 inline bool mq_enabled() {
   static const bool on = [] {
     const char* e = getenv("JB_TOPK_MQ");
@@ -1400,7 +1411,7 @@ inline int launch_scan(const TopkSrc& s, int blocks, int nq, int64_t nrows, int6
   // block merge cost more there than the scan saves (measured through the
   // servers: 1M-row euclid_lsh similar_row 53 -> 63 us p50, 100 K-row LOF
   // calc_score 54 -> 74 us)
-  if (MODE == 0 && mq_enabled() && blocks > 1 && nrows >= kMqMinRows && k <= kMqMaxK &&
+  if (MODE == 0 && mq_enabled() && blocks > 1 && nrows >= mq_min_rows() && k <= kMqMaxK &&
       (s.words == 1 || s.words == 2) && s.hash_num <= 64 * s.words && nq <= (s.metric == 1 ? 4 : kMqMaxQ)) {
     // the sampled bound, then the table streamed once per launch of up to
     // kMqMaxQ queries (topk_mq_kernel); at least 4 chunks a wave so its carry
@@ -1580,7 +1591,7 @@ static int topk_tile_blocks(int64_t nrows, int k) {
 // kMqMinRows and more: two blocks a CU keep more rows in flight than one)
 extern "C" int jb_topk_blocks(int64_t nrows, int k) {
   const int tb = topk_tile_blocks(nrows, k);
-  if (tb > 0 && nrows >= jb::kMqMinRows && k <= jb::kMqMaxK)
+  if (tb > 0 && nrows >= jb::mq_min_rows() && k <= jb::kMqMaxK)
     return tb > jb::kMqBlocksMax + 1 ? tb : jb::kMqBlocksMax + 1;
   return tb;
 }
