@@ -24,6 +24,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 #include <functional>
 #include <list>
 #include <map>
@@ -1071,6 +1072,11 @@ class RowEngine {
     } else {
       throw std::runtime_error("unknown similarity method: " + method);
     }
+    // the id tables sized for a million rows up front: growing them rehashes
+    // every node (a cache miss each) at every doubling, on the write path
+    slot_of_.reserve((size_t)1 << 20);
+    version_.reserve((size_t)1 << 20);
+    dirty_.reserve((size_t)1 << 20);
     const Value* unl = param ? param->get("unlearner") : nullptr;
     if (unl && unl->kind != Value::NIL) {
       if (!unl->is_str() || unl->s != "lru") throw std::runtime_error("unknown unlearner");
@@ -1429,7 +1435,7 @@ class RowEngine {
   hipStream_t stream_;
   std::unique_ptr<LshIndex> lsh_;
   std::unique_ptr<PoolIndex> pool_;
-  std::vector<Row> rows_;
+  std::deque<Row> rows_;   // (a deque: growth moves no rows and keeps references)
   std::list<std::string> insertion_;
   std::unordered_map<std::string, std::pair<int32_t, std::list<std::string>::iterator>> slot_of_;
   std::vector<int32_t> free_;
