@@ -184,7 +184,9 @@ def test_push_mixers_reach_the_union(coord, mixer):
             want |= set(r.rows())
         assert ranks[0].call("do_mix") is True
         deadline = time.time() + 20
-        while time.time() < deadline and any(set(r.rows()) != want for r in ranks):
+        # (a rank applies the rows before its MIX round ends and counts it)
+        while time.time() < deadline and (any(set(r.rows()) != want for r in ranks) or
+                                           any(int(r.status()[f"{mixer}.mix_count"]) < 1 for r in ranks)):
             time.sleep(0.1)
         for r in ranks:
             assert set(r.rows()) == want
